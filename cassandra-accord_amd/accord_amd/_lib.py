@@ -1,0 +1,119 @@
+"""ctypes binding of include/accord_amd.h (libaccord_amd.so, built for gfx950).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be loaded this module
+raises, and every op fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libaccord_amd.so")
+
+ACC_OK, ACC_E_ARG, ACC_E_STATE, ACC_E_NOMEM, ACC_E_DEVICE, ACC_E_CAP = 0, -1, -2, -3, -4, -5
+ACC_MEM_HOST, ACC_MEM_DEVICE = 0, 1
+ACC_OPT_TIMING = 1
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+u8p = C.POINTER(C.c_uint8)
+
+# Every symbol declared in include/accord_amd.h (tests check the library exports all of them).
+EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
+           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_merge", "acc_levelise",
+           "acc_timing_count", "acc_timing_get", "acc_timing_reset"]
+
+
+class Opts(C.Structure):
+    _fields_ = [("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class TsCols(C.Structure):
+    _fields_ = [("msb", C.c_void_p), ("lsb", C.c_void_p), ("node", C.c_void_p)]
+
+
+class BatchIn(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32), ("mem", C.c_uint32), ("n_pairs", C.c_uint64),
+                ("txn_id", TsCols), ("execute_at", TsCols),
+                ("status", C.c_void_p), ("key_off", C.c_void_p), ("key_code", C.c_void_p)]
+
+
+class KeydepsView(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32),
+                ("total_arena", C.c_uint64), ("total_keys", C.c_uint64), ("total_deps", C.c_uint64),
+                ("total_edges", C.c_uint64),
+                ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("kd_off", C.c_void_p),
+                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+
+
+class KeydepsOut(C.Structure):
+    _fields_ = [("mem", C.c_uint32),
+                ("cap_arena", C.c_uint64), ("cap_keys", C.c_uint64), ("cap_deps", C.c_uint64),
+                ("need_arena", C.c_uint64), ("need_keys", C.c_uint64), ("need_deps", C.c_uint64),
+                ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("kd_off", C.c_void_p),
+                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+
+
+class MergeIn(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n_groups", C.c_uint32), ("n_replies", C.c_uint64),
+                ("grp_off", C.c_void_p), ("key_off", C.c_void_p), ("key_code", C.c_void_p),
+                ("val_off", C.c_void_p), ("txn_rank", C.c_void_p), ("k2v_off", C.c_void_p),
+                ("k2v", C.c_void_p)]
+
+
+class MergeView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32),
+                ("total_keys", C.c_uint64), ("total_vals", C.c_uint64), ("total_k2v", C.c_uint64),
+                ("total_in_entries", C.c_uint64),
+                ("key_off", C.c_void_p), ("key_code", C.c_void_p),
+                ("val_off", C.c_void_p), ("txn_rank", C.c_void_p),
+                ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class GraphIn(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
+                ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
+
+
+_lib = None
+
+
+def load():
+    """Load libaccord_amd.so; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"accord_amd: HIP library not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    L.acc_create.argtypes = [C.c_int, C.POINTER(Opts), C.POINTER(C.c_void_p)]
+    L.acc_create.restype = C.c_int
+    L.acc_destroy.argtypes = [C.c_void_p]
+    L.acc_destroy.restype = None
+    L.acc_last_error.argtypes = [C.c_void_p]
+    L.acc_last_error.restype = C.c_char_p
+    L.acc_sync.argtypes = [C.c_void_p]
+    L.acc_sync.restype = C.c_int
+    L.acc_stream.argtypes = [C.c_void_p]
+    L.acc_stream.restype = C.c_void_p
+    L.acc_version.argtypes = []
+    L.acc_version.restype = C.c_char_p
+    L.acc_keydeps_batch.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(KeydepsView)]
+    L.acc_keydeps_batch.restype = C.c_int
+    L.acc_keydeps_copy_out.argtypes = [C.c_void_p, C.POINTER(KeydepsOut)]
+    L.acc_keydeps_copy_out.restype = C.c_int
+    L.acc_keydeps_merge.argtypes = [C.c_void_p, C.POINTER(MergeIn), C.POINTER(MergeView)]
+    L.acc_keydeps_merge.restype = C.c_int
+    L.acc_levelise.argtypes = [C.c_void_p, C.POINTER(GraphIn), u32p, u32p, u32p]
+    L.acc_levelise.restype = C.c_int
+    L.acc_timing_count.argtypes = [C.c_void_p]
+    L.acc_timing_count.restype = C.c_int
+    L.acc_timing_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                                 C.POINTER(C.c_uint64)]
+    L.acc_timing_get.restype = C.c_int
+    L.acc_timing_reset.argtypes = [C.c_void_p]
+    L.acc_timing_reset.restype = None
+    _lib = L
+    return L

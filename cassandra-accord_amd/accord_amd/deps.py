@@ -1,0 +1,244 @@
+"""Host-side mirror of the reference deps API over the C ABI (include/accord_amd.h).
+
+Names and error behaviour follow accord-core: ``KeyDeps`` (primitives/KeyDeps.java) with the Java
+three-array layout, ``calculate_partial_deps`` for a whole batch (messages/PreAccept.java:245-265 over
+local/CommandsForKey.java:614-650), ``KeyDeps.merge`` (primitives/KeyDeps.java:115-135). Errors map to
+``IllegalArgumentException`` / ``IllegalStateException`` like utils/Invariants.java:98-205.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+class AccordError(RuntimeError):
+    code = None
+
+
+class IllegalArgumentException(AccordError):
+    code = L.ACC_E_ARG
+
+
+class IllegalStateException(AccordError):
+    code = L.ACC_E_STATE
+
+
+class DeviceError(AccordError):
+    code = L.ACC_E_DEVICE
+
+
+class CapacityError(AccordError):
+    code = L.ACC_E_CAP
+
+
+_ERRORS = {L.ACC_E_ARG: IllegalArgumentException, L.ACC_E_STATE: IllegalStateException,
+           L.ACC_E_DEVICE: DeviceError, L.ACC_E_NOMEM: DeviceError, L.ACC_E_CAP: CapacityError}
+
+
+def _ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One acc_ctx: a HIP stream plus device scratch (one per host thread / CommandStore)."""
+
+    def __init__(self, device: int = 0, timing: bool = False):
+        self._lib = L.load()
+        h = C.c_void_p()
+        opts = L.Opts(L.ACC_OPT_TIMING if timing else 0, 0)
+        rc = self._lib.acc_create(device, C.byref(opts), C.byref(h))
+        if rc != L.ACC_OK:
+            raise _ERRORS.get(rc, AccordError)(f"acc_create failed ({rc})")
+        self._h = h
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.acc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.acc_stream(self._h) or 0)
+
+    def check(self, rc: int):
+        if rc != L.ACC_OK:
+            msg = (self._lib.acc_last_error(self._h) or b"").decode()
+            raise _ERRORS.get(rc, AccordError)(msg)
+
+    def sync(self):
+        self.check(self._lib.acc_sync(self._h))
+
+    # ---- timing
+    def timing(self) -> dict:
+        n = self._lib.acc_timing_count(self._h)
+        out = {}
+        for i in range(max(n, 0)):
+            name = C.c_char_p()
+            ms = C.c_double()
+            cnt = C.c_uint64()
+            self._lib.acc_timing_get(self._h, i, C.byref(name), C.byref(ms), C.byref(cnt))
+            out[name.value.decode()] = (ms.value, cnt.value)
+        return out
+
+    def timing_reset(self):
+        self._lib.acc_timing_reset(self._h)
+
+    # ---- KeyDeps batch
+    def keydeps_batch_raw(self, batch_in: "L.BatchIn") -> "L.KeydepsView":
+        view = L.KeydepsView()
+        self.check(self._lib.acc_keydeps_batch(self._h, C.byref(batch_in), C.byref(view)))
+        return view
+
+    def calculate_partial_deps(self, batch) -> "BatchKeyDeps":
+        """PreAccept.calculatePartialDeps for every txn of `batch` (host numpy arrays in, host out)."""
+        arrs = dict(tm=np.ascontiguousarray(batch.txn_msb, dtype=np.uint64),
+                    tl=np.ascontiguousarray(batch.txn_lsb, dtype=np.uint64),
+                    tn=np.ascontiguousarray(batch.txn_node, dtype=np.int32),
+                    em=np.ascontiguousarray(batch.exe_msb, dtype=np.uint64),
+                    el=np.ascontiguousarray(batch.exe_lsb, dtype=np.uint64),
+                    en=np.ascontiguousarray(batch.exe_node, dtype=np.int32),
+                    st=np.ascontiguousarray(batch.status, dtype=np.uint8),
+                    ko=np.ascontiguousarray(batch.key_off, dtype=np.uint32),
+                    kc=np.ascontiguousarray(batch.key_code, dtype=np.uint64))
+        n = int(arrs["st"].shape[0])
+        bi = L.BatchIn(n, L.ACC_MEM_HOST, int(arrs["ko"][-1]) if n else 0,
+                       L.TsCols(arrs["tm"].ctypes.data, arrs["tl"].ctypes.data, arrs["tn"].ctypes.data),
+                       L.TsCols(arrs["em"].ctypes.data, arrs["el"].ctypes.data, arrs["en"].ctypes.data),
+                       arrs["st"].ctypes.data, arrs["ko"].ctypes.data, arrs["kc"].ctypes.data)
+        view = self.keydeps_batch_raw(bi)
+        return self.copy_out(view, batch)
+
+    def copy_out(self, view: "L.KeydepsView", batch=None) -> "BatchKeyDeps":
+        n = view.n_txn
+        out = L.KeydepsOut()
+        out.mem = L.ACC_MEM_HOST
+        # first call: sizing (ACC_E_CAP with need_* filled)
+        rc = self._lib.acc_keydeps_copy_out(self._h, C.byref(out))
+        if rc not in (L.ACC_OK, L.ACC_E_CAP):
+            self.check(rc)
+        arena_off = np.zeros(n + 1, np.uint64)
+        kd_off = np.zeros(n + 1, np.uint64)
+        u_off = np.zeros(n + 1, np.uint64)
+        arena = np.zeros(max(out.need_arena, 1), np.int32)
+        key_idx = np.zeros(max(out.need_keys, 1), np.uint32)
+        dep_txn = np.zeros(max(out.need_deps, 1), np.uint32)
+        out.cap_arena, out.cap_keys, out.cap_deps = out.need_arena, out.need_keys, out.need_deps
+        out.arena_off, out.kd_off, out.u_off = arena_off.ctypes.data, kd_off.ctypes.data, u_off.ctypes.data
+        out.arena, out.key_idx, out.dep_txn = arena.ctypes.data, key_idx.ctypes.data, dep_txn.ctypes.data
+        self.check(self._lib.acc_keydeps_copy_out(self._h, C.byref(out)))
+        return BatchKeyDeps(arena_off, arena[:out.need_arena], kd_off, key_idx[:out.need_keys], u_off,
+                            dep_txn[:out.need_deps], int(view.total_edges), batch)
+
+
+@dataclass
+class BatchKeyDeps:
+    """Per-txn PartialDeps.keyDeps of a batch in the acc_keydeps_view layout."""
+    arena_off: np.ndarray
+    arena: np.ndarray
+    kd_off: np.ndarray
+    key_idx: np.ndarray
+    u_off: np.ndarray
+    dep_txn: np.ndarray
+    total_edges: int
+    batch: object = None
+
+    def txn(self, t: int):
+        a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
+        k = self.key_idx[self.kd_off[t]:self.kd_off[t + 1]]
+        d = self.dep_txn[self.u_off[t]:self.u_off[t + 1]]
+        return k, d, a
+
+    def key_deps(self, t: int) -> "KeyDeps":
+        """KeyDeps of txn t with real key codes and TxnId tuples (needs the input batch)."""
+        k, d, a = self.txn(t)
+        b = self.batch
+        keys = b.key_code[int(b.key_off[t]) + k.astype(np.int64)]
+        txn_ids = [TxnId(int(b.txn_msb[x]), int(b.txn_lsb[x]), int(b.txn_node[x])) for x in d]
+        return KeyDeps(keys, txn_ids, a)
+
+
+class TxnId(tuple):
+    """(msb, lsb, node) with Timestamp.compareTo/equals semantics (primitives/Timestamp.java:208-249)."""
+
+    def __new__(cls, msb, lsb, node):
+        return super().__new__(cls, (int(msb), int(lsb), int(node)))
+
+    def order_key(self):
+        msb, lsb, node = self
+        return (msb, lsb >> 16, lsb & 0x1E, node)
+
+    @property
+    def epoch(self):
+        return self[0] >> 15
+
+    @property
+    def hlc(self):
+        return ((self[0] & 0x7FFF) << 48) | (self[1] >> 16)
+
+    @property
+    def flags(self):
+        return self[1] & 0xFFFF
+
+    def __str__(self):  # TxnId.toString (TxnId.java:119-122) without the kind/domain short names
+        return f"[{self.epoch},{self.hlc},{self.flags},{self[2]}]"
+
+
+class KeyDeps:
+    """KeyDeps in the reference layout (primitives/KeyDeps.java:150-172): keys (sorted unique codes),
+    txnIds (sorted unique), keysToTxnIds (Java int[]: end offsets from keys.length, then indices)."""
+
+    def __init__(self, keys, txn_ids, keys_to_txn_ids):
+        self.keys = np.asarray(keys, dtype=np.uint64)
+        self.txn_ids = list(txn_ids)
+        self.keys_to_txn_ids = np.asarray(keys_to_txn_ids, dtype=np.int32)
+        nk = len(self.keys)
+        # KeyDeps ctor check (KeyDeps.java:184-185)
+        if nk and int(self.keys_to_txn_ids[nk - 1]) != len(self.keys_to_txn_ids):
+            raise IllegalArgumentException("Last key in keyToTxnId does not point to the end of the array")
+
+    def is_empty(self):
+        return len(self.keys) == 0
+
+    def txn_id_count(self):
+        return len(self.txn_ids)
+
+    def for_each(self, key):
+        """TxnIds depended on for `key` (KeyDeps.forEach(key, ...))."""
+        i = int(np.searchsorted(self.keys, np.uint64(key)))
+        if i >= len(self.keys) or int(self.keys[i]) != int(key):
+            return []
+        start = len(self.keys) if i == 0 else int(self.keys_to_txn_ids[i - 1])
+        end = int(self.keys_to_txn_ids[i])
+        return [self.txn_ids[int(x)] for x in self.keys_to_txn_ids[start:end]]
+
+    def canonical(self):
+        return {int(k): self.for_each(k) for k in self.keys}
+
+    def __eq__(self, other):  # RelationMultiMap.testEquality (:1027-1036)
+        return (isinstance(other, KeyDeps) and np.array_equal(self.keys, other.keys)
+                and self.txn_ids == other.txn_ids
+                and np.array_equal(self.keys_to_txn_ids, other.keys_to_txn_ids))
+
+    def __str__(self):
+        return "{" + ", ".join(f"{k}:[{', '.join(str(t) for t in v)}]" for k, v in self.canonical().items()) + "}"

@@ -1,0 +1,215 @@
+"""Seeded synthetic batches for the dependency-calculation path.
+
+Every stream is counter-based SplitMix64 (``x_i = mix64(seed ^ salt + (i+1)*GAMMA)``), so the same
+(seed, config) gives the same arrays on every host. Layout matches ``acc_batch_in`` (include/accord_amd.h):
+TxnId/executeAt as (msb, lsb, node) columns, InternalStatus ordinals, CSR key offsets and IntKey codes.
+
+TxnId i: epoch=1, hlc=i+1, node=1+(i mod 8), flags = kind<<1 | domain (Timestamp.java:81-89,
+TxnId.java:124-137). Committed-class txns get executeAt bumped to hlc+U[1,1000] with node 1000+(i mod 8)
+for 10% of them, so no executeAt compares equal to any TxnId or other executeAt.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+# InternalStatus ordinals (CommandsForKey.java:194-203)
+TRANSITIVELY_KNOWN, HISTORICAL, PREACCEPTED, ACCEPTED, COMMITTED, STABLE, APPLIED, INVALID_OR_TRUNCATED = range(8)
+# Txn.Kind ordinals (Txn.java:53-113)
+READ, WRITE, EPHEMERAL_READ, SYNC_POINT, EXCLUSIVE_SYNC_POINT, LOCAL_ONLY = range(6)
+
+CONFIG_SEEDS = {
+    "1a": 0xACC00101,
+    "1b": 0xACC00102,
+    "2": 0xACC00002,
+    "3u": 0xACC00003,
+    "3z": 0xACC00004,
+    "4": 0xACC00005,
+    "5": 0xACC00006,
+}
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        z ^= z >> np.uint64(30)
+        z *= M1
+        z ^= z >> np.uint64(27)
+        z *= M2
+        z ^= z >> np.uint64(31)
+    return z
+
+
+def stream(seed: int, salt: int, n: int, offset: int = 0) -> np.ndarray:
+    """n SplitMix64 outputs of stream `salt` starting at counter `offset`."""
+    base = np.uint64((seed ^ (salt * 0x632BE59BD9B4E019)) & 0xFFFFFFFFFFFFFFFF)
+    ctr = np.arange(offset + 1, offset + n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return mix64(base + ctr * GAMMA)
+
+
+def uniform01(seed: int, salt: int, n: int, offset: int = 0) -> np.ndarray:
+    return (stream(seed, salt, n, offset) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
+def int_key_code(keys: np.ndarray) -> np.ndarray:
+    """IntKey order-preserving code: u32(key ^ 0x80000000) as u64."""
+    return (keys.astype(np.int64) + (1 << 31)).astype(np.uint64)
+
+
+def encode_ts(epoch, hlc, flags, node):
+    """Timestamp(epoch, hlc, flags, node) fields (Timestamp.java:81-89)."""
+    epoch = np.asarray(epoch, dtype=np.uint64)
+    hlc = np.asarray(hlc, dtype=np.uint64)
+    flags = np.asarray(flags, dtype=np.uint64)
+    msb = (epoch << np.uint64(15)) | (hlc >> np.uint64(48))
+    with np.errstate(over="ignore"):
+        lsb = (hlc << np.uint64(16)) | flags
+    return msb, lsb, np.asarray(node, dtype=np.int32)
+
+
+@dataclass
+class Batch:
+    """One CommandsForKey snapshot: the acc_batch_in columns."""
+    txn_msb: np.ndarray
+    txn_lsb: np.ndarray
+    txn_node: np.ndarray
+    exe_msb: np.ndarray
+    exe_lsb: np.ndarray
+    exe_node: np.ndarray
+    status: np.ndarray
+    key_off: np.ndarray
+    key_code: np.ndarray
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_txn(self) -> int:
+        return int(self.status.shape[0])
+
+    @property
+    def n_pairs(self) -> int:
+        return int(self.key_off[-1])
+
+    def permuted(self, perm: np.ndarray) -> "Batch":
+        """Same batch with txns reordered: new txn i = old txn perm[i]."""
+        counts = np.diff(self.key_off.astype(np.int64))[perm]
+        off = np.zeros(len(perm) + 1, dtype=np.uint32)
+        np.cumsum(counts, out=off[1:])
+        starts = self.key_off[:-1].astype(np.int64)[perm]
+        idx = np.repeat(starts - off[:-1].astype(np.int64), counts) + np.arange(int(off[-1]), dtype=np.int64)
+        return Batch(self.txn_msb[perm], self.txn_lsb[perm], self.txn_node[perm], self.exe_msb[perm],
+                     self.exe_lsb[perm], self.exe_node[perm], self.status[perm], off, self.key_code[idx],
+                     dict(self.meta, permuted=True))
+
+    def arrays(self):
+        return dict(txn_msb=self.txn_msb, txn_lsb=self.txn_lsb, txn_node=self.txn_node, exe_msb=self.exe_msb,
+                    exe_lsb=self.exe_lsb, exe_node=self.exe_node, status=self.status, key_off=self.key_off,
+                    key_code=self.key_code)
+
+
+def _distinct_keys(seed: int, n_txn: int, k: int, sample) -> np.ndarray:
+    """n_txn rows of k distinct key ids; duplicates are redrawn from fresh counters until none remain."""
+    keys = sample(0, n_txn * k).reshape(n_txn, k)
+    offset = n_txn * k
+    for _ in range(200):
+        keys.sort(axis=1)
+        dup = np.zeros_like(keys, dtype=bool)
+        dup[:, 1:] = keys[:, 1:] == keys[:, :-1]
+        nd = int(dup.sum())
+        if nd == 0:
+            return keys
+        keys[dup] = sample(offset, nd)
+        offset += nd
+    raise RuntimeError("could not draw distinct keys")
+
+
+def zipf_sampler(seed: int, salt: int, n_keys: int, s: float, permute: bool):
+    w = 1.0 / np.power(np.arange(1, n_keys + 1, dtype=np.float64), s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    perm = None
+    if permute:
+        perm = np.argsort(stream(seed, salt + 7, n_keys), kind="stable").astype(np.int64)
+
+    def sample(offset, n):
+        r = np.searchsorted(cdf, uniform01(seed, salt, n, offset), side="right")
+        r = np.minimum(r, n_keys - 1)
+        return perm[r] if perm is not None else r
+    return sample
+
+
+def uniform_sampler(seed: int, salt: int, n_keys: int):
+    def sample(offset, n):
+        return (stream(seed, salt, n, offset) % np.uint64(n_keys)).astype(np.int64)
+    return sample
+
+
+def keydeps_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, dist: str = "uniform",
+                  zipf_s: float = 0.99, status_model: str = "model", window: int = 10_000,
+                  p_write: float = 0.5, p_syncpoint: float = 0.0, permute_keys: bool = True) -> Batch:
+    """Synthetic batch per SURVEY.md §8(d).
+
+    status_model: "preaccepted" (config 1a: every txn PREACCEPTED) or "model" (window W of
+    PREACCEPTED 70%/ACCEPTED 30%, else APPLIED 80%/STABLE 10%/COMMITTED 10%, plus 0.1%
+    INVALID_OR_TRUNCATED and 0.1% TRANSITIVELY_KNOWN).
+    """
+    i = np.arange(n_txn, dtype=np.int64)
+    u_kind = uniform01(seed, 1, n_txn)
+    kind = np.where(u_kind < p_write, WRITE, READ).astype(np.int64)
+    if p_syncpoint > 0:
+        kind = np.where(uniform01(seed, 2, n_txn) < p_syncpoint, SYNC_POINT, kind)
+    flags = (kind << 1) | 0  # domain Key = 0
+    t_msb, t_lsb, t_node = encode_ts(np.ones(n_txn), i + 1, flags, 1 + (i % 8))
+
+    if status_model == "preaccepted":
+        status = np.full(n_txn, PREACCEPTED, dtype=np.uint8)
+    elif status_model == "model":
+        u = uniform01(seed, 3, n_txn)
+        in_window = i >= n_txn - window
+        status = np.where(in_window, np.where(u < 0.7, PREACCEPTED, ACCEPTED),
+                          np.where(u < 0.8, APPLIED, np.where(u < 0.9, STABLE, COMMITTED))).astype(np.uint8)
+        u2 = uniform01(seed, 4, n_txn)
+        status = np.where(u2 < 0.001, INVALID_OR_TRUNCATED,
+                          np.where(u2 < 0.002, TRANSITIVELY_KNOWN, status)).astype(np.uint8)
+    else:
+        raise ValueError(status_model)
+
+    committed = (status >= COMMITTED) & (status <= APPLIED)
+    bump = committed & (uniform01(seed, 5, n_txn) < 0.1)
+    bump_by = 1 + (stream(seed, 6, n_txn) % np.uint64(1000)).astype(np.int64)
+    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + (i % 8))
+    exe_msb = np.where(bump, e_msb, t_msb).astype(np.uint64)
+    exe_lsb = np.where(bump, e_lsb_b, t_lsb).astype(np.uint64)
+    exe_node = np.where(bump, e_node_b, t_node).astype(np.int32)
+
+    if dist == "uniform":
+        sampler = uniform_sampler(seed, 10, n_keys)
+    elif dist == "zipf":
+        sampler = zipf_sampler(seed, 10, n_keys, zipf_s, permute_keys)
+    else:
+        raise ValueError(dist)
+    keys = _distinct_keys(seed, n_txn, keys_per_txn, sampler)
+    key_off = (np.arange(n_txn + 1, dtype=np.int64) * keys_per_txn).astype(np.uint32)
+    key_code = int_key_code(keys.reshape(-1))
+    meta = dict(n_txn=n_txn, keys_per_txn=keys_per_txn, n_keys=n_keys, seed=seed, dist=dist, zipf_s=zipf_s,
+                status_model=status_model, window=window, p_write=p_write)
+    return Batch(t_msb, t_lsb, t_node, exe_msb, exe_lsb, exe_node, status, key_off, key_code, meta)
+
+
+def config(name: str, scale: float = 1.0) -> Batch:
+    """BASELINE.json configs 1a/1b (10k x 4 over 1k keys) and 2 (1M x 8, zipf 0.99 over 1M keys)."""
+    if name == "1a":
+        return keydeps_batch(10_000, 4, 1_000, CONFIG_SEEDS["1a"], "uniform", status_model="preaccepted")
+    if name == "1b":
+        # status model with a 1,000-txn uncommitted window (an absolute W = 10,000 would cover all 10k txns)
+        return keydeps_batch(10_000, 4, 1_000, CONFIG_SEEDS["1b"], "uniform", status_model="model", window=1_000)
+    if name == "2":
+        n = int(1_000_000 * scale)
+        return keydeps_batch(n, 8, max(1000, int(1_000_000 * scale)), CONFIG_SEEDS["2"], "zipf", 0.99,
+                             status_model="model")
+    raise ValueError(name)

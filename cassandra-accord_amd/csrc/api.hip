@@ -1,0 +1,140 @@
+// api.hip — the extern "C" surface of include/accord_amd.h: context lifecycle, error text, result
+// copy-out with two-call sizing, and kernel timing read-out.
+#include "prims.hpp"
+
+namespace acc {
+void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view);
+void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
+void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
+}  // namespace acc
+
+extern "C" {
+
+const char *acc_version(void) { return "accord_amd 0.1 (gfx950)"; }
+
+int acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
+{
+    if (!out_ctx) return ACC_E_ARG;
+    *out_ctx = nullptr;
+    acc_ctx *ctx = new (std::nothrow) acc_ctx();
+    if (!ctx) return ACC_E_NOMEM;
+    int rc = acc_guard(ctx, [&] {
+        int count = 0;
+        ACC_HIP(hipGetDeviceCount(&count));
+        if (device < 0 || device >= count) acc::fail(ACC_E_ARG, "no such HIP device");
+        ACC_HIP(hipSetDevice(device));
+        ctx->device = device;
+        ctx->flags = opts ? opts->flags : 0;
+        ACC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ACC_HIP(hipHostMalloc((void **)&ctx->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault));
+    });
+    if (rc != ACC_OK) {
+        acc_destroy(ctx);
+        return rc;
+    }
+    *out_ctx = ctx;
+    return ACC_OK;
+}
+
+void acc_destroy(acc_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->bufs)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (void *p : ctx->graveyard) (void)hipFree(p);
+    for (auto &p : ctx->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *acc_last_error(const acc_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int acc_sync(acc_ctx *ctx)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] { ctx->sync(); });
+}
+
+void *acc_stream(acc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int acc_keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::keydeps_batch(ctx, in, out_view);
+    });
+}
+
+int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        if (!out) acc::fail(ACC_E_ARG, "null output");
+        if (!ctx->kd_valid) acc::fail(ACC_E_STATE, "no keydeps result on this context");
+        const acc_keydeps_view &v = ctx->kd_view;
+        out->need_arena = v.total_arena;
+        out->need_keys = v.total_keys;
+        out->need_deps = v.total_deps;
+        if (!out->arena_off || !out->kd_off || !out->u_off)   // sizing call
+            acc::fail(ACC_E_CAP, "sizing call (null offset arrays); required sizes written to need_*");
+        if (out->cap_arena < v.total_arena || out->cap_keys < v.total_keys || out->cap_deps < v.total_deps)
+            acc::fail(ACC_E_CAP, "output capacity too small; required sizes written to need_*");
+        hipMemcpyKind kind = out->mem == ACC_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        size_t n1 = (size_t)v.n_txn + 1;
+        ACC_HIP(hipMemcpyAsync(out->arena_off, v.arena_off, n1 * 8, kind, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->kd_off, v.kd_off, n1 * 8, kind, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->u_off, v.u_off, n1 * 8, kind, ctx->stream));
+        if (v.total_arena) ACC_HIP(hipMemcpyAsync(out->arena, v.arena, v.total_arena * 4, kind, ctx->stream));
+        if (v.total_keys) ACC_HIP(hipMemcpyAsync(out->key_idx, v.key_idx, v.total_keys * 4, kind, ctx->stream));
+        if (v.total_deps) ACC_HIP(hipMemcpyAsync(out->dep_txn, v.dep_txn, v.total_deps * 4, kind, ctx->stream));
+        ctx->sync();
+    });
+}
+
+int acc_keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::keydeps_merge(ctx, in, out_view);
+    });
+}
+
+int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::levelise(ctx, in, level, order, n_levels);
+    });
+}
+
+int acc_timing_count(acc_ctx *ctx)
+{
+    if (!ctx) return 0;
+    int rc = acc_guard(ctx, [&] { ctx->sync(); });
+    return rc == ACC_OK ? (int)ctx->slots.size() : rc;
+}
+
+int acc_timing_get(acc_ctx *ctx, int i, const char **name, double *total_ms, uint64_t *launches)
+{
+    if (!ctx || i < 0 || i >= (int)ctx->slots.size()) return ACC_E_ARG;
+    if (name) *name = ctx->slots[i].name.c_str();
+    if (total_ms) *total_ms = ctx->slots[i].total_ms;
+    if (launches) *launches = ctx->slots[i].launches;
+    return ACC_OK;
+}
+
+void acc_timing_reset(acc_ctx *ctx)
+{
+    if (!ctx) return;
+    acc_guard(ctx, [&] { ctx->sync(); });
+    for (auto &s : ctx->slots) { s.total_ms = 0; s.launches = 0; }
+}
+
+}  // extern "C"

@@ -1,0 +1,196 @@
+// ctx.hpp — acc_ctx: one HIP stream, a grow-only device arena keyed by buffer name, per-kernel
+// HIP-event timing, and the exception -> error-code plumbing behind the C ABI (include/accord_amd.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/accord_amd.h"
+
+namespace acc {
+
+// Internal failure: carried to the C boundary and mapped to an ACC_E_* code.
+struct Error {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] inline void fail(int code, const std::string &msg) { throw Error{code, msg}; }
+
+#define ACC_HIP(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            ::acc::fail(e_ == hipErrorOutOfMemory ? ACC_E_NOMEM : ACC_E_DEVICE,                \
+                        std::string(#expr ": ") + hipGetErrorString(e_));                      \
+    } while (0)
+
+struct Buf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct TimingSlot {
+    std::string name;
+    double total_ms = 0;
+    uint64_t launches = 0;
+};
+
+struct PendingEvent {
+    int slot;
+    hipEvent_t start, stop;
+};
+
+}  // namespace acc
+
+struct acc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t flags = 0;
+    std::string last_error;
+    std::unordered_map<std::string, acc::Buf> bufs;
+    // buffers replaced by a larger allocation while kernels may still read them: freed at the next sync
+    std::vector<void *> graveyard;
+    // pinned host staging for small read-backs (sizes, flags)
+    uint64_t *pinned = nullptr;
+    // timing
+    std::vector<acc::TimingSlot> slots;
+    std::unordered_map<std::string, int> slot_index;
+    std::vector<acc::PendingEvent> pending;
+    std::vector<hipEvent_t> event_pool;
+    // last results
+    acc_keydeps_view kd_view{};
+    acc_merge_view merge_view{};
+    bool kd_valid = false;
+
+    // Grow-only named device buffer. Contents are NOT preserved across growth.
+    template <class T>
+    T *get(const char *name, size_t count)
+    {
+        size_t bytes = count * sizeof(T);
+        if (bytes == 0) bytes = 16;
+        acc::Buf &b = bufs[name];
+        if (b.bytes < bytes) {
+            if (b.ptr) graveyard.push_back(b.ptr);
+            b.ptr = nullptr;
+            size_t want = bytes + bytes / 8;  // headroom for the next, slightly larger batch
+            ACC_HIP(hipMalloc(&b.ptr, want));
+            b.bytes = want;
+        }
+        return static_cast<T *>(b.ptr);
+    }
+
+    hipEvent_t take_event()
+    {
+        if (!event_pool.empty()) {
+            hipEvent_t e = event_pool.back();
+            event_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        ACC_HIP(hipEventCreate(&e));
+        return e;
+    }
+
+    int slot(const char *name)
+    {
+        auto it = slot_index.find(name);
+        if (it != slot_index.end()) return it->second;
+        int i = (int)slots.size();
+        slots.push_back({name, 0, 0});
+        slot_index[name] = i;
+        return i;
+    }
+
+    // Resolve recorded kernel intervals (requires the stream to be idle).
+    void resolve_timing()
+    {
+        for (auto &p : pending) {
+            float ms = 0;
+            ACC_HIP(hipEventElapsedTime(&ms, p.start, p.stop));
+            slots[p.slot].total_ms += ms;
+            slots[p.slot].launches += 1;
+            event_pool.push_back(p.start);
+            event_pool.push_back(p.stop);
+        }
+        pending.clear();
+    }
+
+    void sync()
+    {
+        ACC_HIP(hipStreamSynchronize(stream));
+        for (void *p : graveyard) ACC_HIP(hipFree(p));
+        graveyard.clear();
+        if (!pending.empty()) resolve_timing();
+    }
+};
+
+namespace acc {
+
+// Launch a kernel on the context stream; with ACC_OPT_TIMING, bracket it with HIP events recorded on
+// that same stream (so the interval is the kernel's own device time).
+template <class K, class... Args>
+inline void launch(acc_ctx *ctx, const char *name, K kernel, dim3 grid, dim3 block, size_t shmem, Args... args)
+{
+    if (grid.x == 0 || grid.y == 0 || grid.z == 0) return;
+    PendingEvent pe{};
+    bool timed = (ctx->flags & ACC_OPT_TIMING) != 0;
+    if (timed) {
+        pe.slot = ctx->slot(name);
+        pe.start = ctx->take_event();
+        pe.stop = ctx->take_event();
+        ACC_HIP(hipEventRecord(pe.start, ctx->stream));
+    }
+    hipLaunchKernelGGL(kernel, grid, block, shmem, ctx->stream, args...);
+    ACC_HIP(hipGetLastError());
+    if (timed) {
+        ACC_HIP(hipEventRecord(pe.stop, ctx->stream));
+        ctx->pending.push_back(pe);
+    }
+}
+
+inline unsigned grid_for(size_t n, unsigned per_block)
+{
+    size_t g = (n + per_block - 1) / per_block;
+    return (unsigned)(g ? g : 1);
+}
+
+// Copy caller input (host or device) into a device buffer owned by the context.
+template <class T>
+inline const T *stage_in(acc_ctx *ctx, const char *name, const T *src, size_t count, uint32_t mem)
+{
+    if (count == 0) return ctx->get<T>(name, 1);
+    if (!src) fail(ACC_E_ARG, std::string("null input array: ") + name);
+    if (mem == ACC_MEM_DEVICE) return src;
+    T *d = ctx->get<T>(name, count);
+    ACC_HIP(hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+    return d;
+}
+
+}  // namespace acc
+
+// Run `body` and translate failures into the C error model.
+template <class F>
+inline int acc_guard(acc_ctx *ctx, F &&body)
+{
+    try {
+        body();
+        if (ctx) ctx->last_error.clear();
+        return ACC_OK;
+    } catch (const acc::Error &e) {
+        if (ctx) ctx->last_error = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        if (ctx) ctx->last_error = "host allocation failed";
+        return ACC_E_NOMEM;
+    } catch (...) {
+        if (ctx) ctx->last_error = "unknown failure";
+        return ACC_E_STATE;
+    }
+}

@@ -1,0 +1,339 @@
+// prims.hpp — wave64 building blocks for the dependency path: block/device scans (add / max),
+// order-preserving bit compaction (pext over a run plan) and a stable LSD radix sort of
+// (u64 key, u32 value) pairs with 8-bit digits. Integer work only: HBM-bound, no MFMA.
+#pragma once
+
+#include "ctx.hpp"
+
+namespace acc {
+
+constexpr int BLOCK = 256;
+constexpr int WAVES = BLOCK / 64;
+
+// ---------------------------------------------------------------- wave helpers
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+template <class T>
+__device__ __forceinline__ T shfl_up(T v, unsigned d)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u = (uint64_t)v;
+        uint32_t lo = __shfl_up((uint32_t)u, d, 64), hi = __shfl_up((uint32_t)(u >> 32), d, 64);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__shfl_up((uint32_t)v, d, 64);
+    }
+}
+
+template <class T>
+__device__ __forceinline__ T shfl_idx(T v, int src)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u = (uint64_t)v;
+        uint32_t lo = __shfl((uint32_t)u, src, 64), hi = __shfl((uint32_t)(u >> 32), src, 64);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__shfl((uint32_t)v, src, 64);
+    }
+}
+
+template <class T>
+struct OpAdd {
+    __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
+    static __device__ __forceinline__ T identity() { return (T)0; }
+};
+
+// max over unsigned values; identity 0
+template <class T>
+struct OpMax {
+    __device__ __forceinline__ T operator()(T a, T b) const { return a > b ? a : b; }
+    static __device__ __forceinline__ T identity() { return (T)0; }
+};
+
+template <class T, class Op>
+__device__ __forceinline__ T wave_inclusive(T v, Op op)
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (unsigned d = 1; d < 64; d <<= 1) {
+        T u = shfl_up(v, d);
+        if (lane >= d) v = op(u, v);
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of per-thread values; returns the exclusive prefix of this thread and
+// the block total. `lds` holds WAVES elements.
+template <class T, class Op>
+__device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
+{
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    T incl = wave_inclusive(v, op);
+    if (lane == 63) lds[wave] = incl;
+    __syncthreads();
+    T wave_prefix = Op::identity();
+    T tot = Op::identity();
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+        T x = lds[w];
+        if (w < (int)wave) wave_prefix = op(wave_prefix, x);
+        tot = op(tot, x);
+    }
+    __syncthreads();
+    T excl = shfl_up(incl, 1);
+    if (lane == 0) excl = Op::identity();
+    total = tot;
+    return op(wave_prefix, excl);
+}
+
+// ---------------------------------------------------------------- device-wide scan
+
+template <class T, class Op, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_tile_reduce(const T *__restrict__ in, size_t n, T *__restrict__ out)
+{
+    __shared__ T lds[WAVES];
+    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
+    Op op;
+    T acc = Op::identity();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+        if (base + i < n) acc = op(acc, in[base + i]);
+    T total;
+    block_exclusive(acc, op, lds, total);
+    if (threadIdx.x == 0) out[blockIdx.x] = total;
+}
+
+// Scan one tile of BLOCK*ITEMS elements (thread-contiguous chunks), seeded with prefix[blockIdx]
+// (or identity). exclusive: out[i] = op(prefix, in[0..i-1]); else inclusive. If total_out is set,
+// the block holding element n-1 writes the grand total there.
+template <class T, class Op, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_tile_scan(const T *__restrict__ in, T *__restrict__ out, size_t n,
+                                                   const T *__restrict__ prefix, int exclusive,
+                                                   T *__restrict__ total_out)
+{
+    __shared__ T lds[WAVES];
+    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
+    Op op;
+    T v[ITEMS];
+    T acc = Op::identity();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        v[i] = base + i < n ? in[base + i] : Op::identity();
+        acc = op(acc, v[i]);
+    }
+    T total;
+    T run = block_exclusive(acc, op, lds, total);
+    if (prefix) run = op(prefix[blockIdx.x], run);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        T x = v[i];
+        T incl = op(run, x);
+        if (base + i < n) out[base + i] = exclusive ? run : incl;
+        if (total_out && base + i == n - 1) *total_out = incl;
+        run = incl;
+    }
+}
+
+template <class T, class Op>
+void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr, int level = 0)
+{
+    constexpr int ITEMS = sizeof(T) == 8 ? 4 : 8;
+    constexpr size_t TILE = (size_t)BLOCK * ITEMS;
+    if (n == 0) {
+        if (total_out) ACC_HIP(hipMemsetAsync(total_out, 0, sizeof(T), ctx->stream));
+        return;
+    }
+    size_t nb = (n + TILE - 1) / TILE;
+    if (nb == 1) {
+        launch(ctx, "scan", k_tile_scan<T, Op, ITEMS>, dim3(1), dim3(BLOCK), 0, in, out, n, (const T *)nullptr,
+               (int)exclusive, total_out);
+        return;
+    }
+    char name_s[48], name_p[48];
+    snprintf(name_s, sizeof name_s, "scan_sums_%d_%zu", level, sizeof(T));
+    snprintf(name_p, sizeof name_p, "scan_pref_%d_%zu", level, sizeof(T));
+    T *sums = ctx->get<T>(name_s, nb);
+    T *pref = ctx->get<T>(name_p, nb);
+    launch(ctx, "scan", k_tile_reduce<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, n, sums);
+    scan<T, Op>(ctx, sums, pref, nb, true, (T *)nullptr, level + 1);
+    launch(ctx, "scan", k_tile_scan<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, out, n,
+           (const T *)pref, (int)exclusive, total_out);
+}
+
+// ---------------------------------------------------------------- bit compaction plan
+
+// pext(w, mask) as a list of contiguous runs; masks with more than MAX_RUNS runs fall back to the
+// hull [lowest set bit, highest set bit] (a superset: still order preserving, a few more bits).
+struct Runs {
+    static constexpr int MAX_RUNS = 12;
+    int n = 0;
+    int bits = 0;
+    uint8_t lo[MAX_RUNS] = {}, len[MAX_RUNS] = {}, dst[MAX_RUNS] = {};
+};
+
+inline Runs make_runs(uint64_t mask)
+{
+    Runs r;
+    int b = 0;
+    int count = 0;
+    for (int i = 0; i < 64;) {
+        if (!((mask >> i) & 1)) { ++i; continue; }
+        int j = i;
+        while (j < 64 && ((mask >> j) & 1)) ++j;
+        ++count;
+        i = j;
+    }
+    if (count > Runs::MAX_RUNS) {
+        int lo = __builtin_ctzll(mask), hi = 63 - __builtin_clzll(mask);
+        r.n = 1; r.lo[0] = (uint8_t)lo; r.len[0] = (uint8_t)(hi - lo + 1); r.dst[0] = 0; r.bits = hi - lo + 1;
+        return r;
+    }
+    for (int i = 0; i < 64;) {
+        if (!((mask >> i) & 1)) { ++i; continue; }
+        int j = i;
+        while (j < 64 && ((mask >> j) & 1)) ++j;
+        r.lo[r.n] = (uint8_t)i; r.len[r.n] = (uint8_t)(j - i); r.dst[r.n] = (uint8_t)b;
+        b += j - i; ++r.n;
+        i = j;
+    }
+    r.bits = b;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t pext_runs(uint64_t w, const Runs &r)
+{
+    uint64_t o = 0;
+    for (int i = 0; i < r.n; ++i) {
+        uint64_t m = r.len[i] >= 64 ? ~0ull : ((1ull << r.len[i]) - 1);
+        o |= ((w >> r.lo[i]) & m) << r.dst[i];
+    }
+    return o;
+}
+
+// ---------------------------------------------------------------- LSD radix sort
+
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = BLOCK * RS_ITEMS;
+
+static __global__ __launch_bounds__(BLOCK) void k_rs_hist(const uint64_t *__restrict__ keys, size_t n, int shift,
+                                                   uint32_t *__restrict__ hist, uint32_t ntiles)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        size_t e = base + (size_t)k * BLOCK + threadIdx.x;
+        if (e < n) atomicAdd(&h[(keys[e] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter: element order inside a tile is (k, wave, lane); ranks come from 8 ballots per
+// wave (peer mask of equal digits) plus a per-digit running count across waves and k steps.
+static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                      size_t n, int shift, const uint32_t *__restrict__ hist_scanned,
+                                                      uint32_t ntiles, int iota_vals)
+{
+    __shared__ uint32_t cnt[WAVES][256];
+    __shared__ uint32_t wpre[WAVES][256];
+    __shared__ uint32_t run[256];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    run[tid] = hist_scanned[(size_t)tid * ntiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) cnt[w][tid] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        size_t e = base + (size_t)k * BLOCK + tid;
+        bool valid = e < n;
+        uint64_t key = valid ? kin[e] : 0;
+        uint32_t val = valid ? (iota_vals ? (uint32_t)e : vin[e]) : 0;
+        uint32_t d = (uint32_t)(key >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint64_t bal = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bal : ~bal;
+        }
+        uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
+        if (valid && rank == 0) cnt[wave][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        {
+            uint32_t r = run[tid];
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                wpre[w][tid] = r;
+                r += cnt[w][tid];
+                cnt[w][tid] = 0;
+            }
+            run[tid] = r;
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t dst = wpre[wave][d] + rank;
+            kout[dst] = key;
+            vout[dst] = val;
+        }
+    }
+}
+
+static __global__ void k_iota(uint32_t *__restrict__ out, size_t n)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)i;
+}
+
+struct Sorted {
+    uint64_t *keys;
+    uint32_t *vals;
+};
+
+// Stable sort of n (key, value) pairs by the low `bits` bits of key (higher bits must be zero).
+// vals == nullptr sorts with values = index. Results live in context buffers "<tag>_k?/_v?" and stay
+// valid until the next sort with the same tag.
+static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *keys, const uint32_t *vals, size_t n, int bits)
+{
+    char nk0[40], nk1[40], nv0[40], nv1[40], nh[40];
+    snprintf(nk0, sizeof nk0, "%s_k0", tag); snprintf(nk1, sizeof nk1, "%s_k1", tag);
+    snprintf(nv0, sizeof nv0, "%s_v0", tag); snprintf(nv1, sizeof nv1, "%s_v1", tag);
+    snprintf(nh, sizeof nh, "%s_hist", tag);
+    uint64_t *k[2] = { ctx->get<uint64_t>(nk0, n), ctx->get<uint64_t>(nk1, n) };
+    uint32_t *v[2] = { ctx->get<uint32_t>(nv0, n), ctx->get<uint32_t>(nv1, n) };
+    int passes = (bits + 7) / 8;
+    if (n == 0) return { k[0], v[0] };
+    if (passes == 0) {
+        ACC_HIP(hipMemcpyAsync(k[0], keys, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        if (vals) ACC_HIP(hipMemcpyAsync(v[0], vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, ctx->stream));
+        else launch(ctx, "iota", k_iota, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, v[0], n);
+        return { k[0], v[0] };
+    }
+    uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint32_t *hist = ctx->get<uint32_t>(nh, (size_t)256 * ntiles);
+    const uint64_t *kin = keys;
+    const uint32_t *vin = vals;
+    int cur = 0;
+    for (int p = 0; p < passes; ++p) {
+        int shift = 8 * p;
+        launch(ctx, "rs_hist", k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, kin, n, shift, hist, ntiles);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, hist, hist, (size_t)256 * ntiles, true);
+        launch(ctx, "rs_scatter", k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, shift,
+               (const uint32_t *)hist, ntiles, (p == 0 && !vals) ? 1 : 0);
+        kin = k[cur];
+        vin = v[cur];
+        cur ^= 1;
+    }
+    return { (uint64_t *)kin, (uint32_t *)vin };
+}
+
+inline int bits_for(uint64_t max_value)
+{
+    return max_value == 0 ? 0 : 64 - __builtin_clzll(max_value);
+}
+
+}  // namespace acc

@@ -1,0 +1,204 @@
+/*
+ * accord_amd.h — C ABI of the MI355X-native Accord dependency-calculation path.
+ *
+ * This is the drop-in boundary a JVM shim (JNI for Java 11, FFM for Java >= 22) binds; see
+ * INTEGRATION.md for the binding stubs. Plain pointers and sizes only: no C++, no torch types.
+ *
+ * Reference interfaces replaced (paths relative to accord-core/src/main/java/accord/):
+ *
+ *   acc_keydeps_batch      PreAccept.calculatePartialDeps            messages/PreAccept.java:245-265
+ *                          -> SafeCommandStore.mapReduceActive        local/SafeCommandStore.java:279
+ *                          -> InMemorySafeStore.mapReduceActive       impl/InMemoryCommandStore.java:863-870
+ *                          -> CommandsForKey.mapReduceActive          local/CommandsForKey.java:614-650
+ *                          -> KeyDeps.Builder / AbstractBuilder.build utils/RelationMultiMap.java:88-260
+ *                          evaluated for every txn of a batch against one CommandsForKey snapshot
+ *                          (batch semantics: SURVEY.md §8 "Batch semantics").
+ *   acc_keydeps_merge      KeyDeps.merge(List, getter, getter)       primitives/KeyDeps.java:115-135
+ *                          (LinearMerger fold of linearUnion,         utils/RelationMultiMap.java:284-406,561-816)
+ *                          batched over many coordinated txns (Deps.merge primitives/Deps.java:256-260).
+ *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
+ *                          (deterministic wavefront schedule).
+ *
+ * Array-level seams mirrored: KeyDeps.SerializerSupport.create(Keys, TxnId[], int[])
+ * (primitives/KeyDeps.java:55-73): every per-txn result is emitted as the exact Java `keysToTxnIds`
+ * int[] plus the key subset and the TxnId array (as batch indices).
+ *
+ * Error model (utils/Invariants.java:98-205): IllegalArgumentException -> ACC_E_ARG,
+ * IllegalStateException / AssertionError -> ACC_E_STATE. Device failures have their own codes.
+ * acc_last_error(ctx) returns the message of the last failing call on that context.
+ *
+ * Threading (local/SafeCommandStore.java:50-55): one acc_ctx per host thread / CommandStore shard;
+ * calls on one ctx are not re-entrant; distinct contexts run on independent HIP streams.
+ */
+#ifndef ACCORD_AMD_H
+#define ACCORD_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ---- */
+#define ACC_OK          0
+#define ACC_E_ARG      (-1)   /* IllegalArgumentException class */
+#define ACC_E_STATE    (-2)   /* IllegalStateException / invariant violation */
+#define ACC_E_NOMEM    (-3)   /* device allocation failed */
+#define ACC_E_DEVICE   (-4)   /* HIP runtime error */
+#define ACC_E_CAP      (-5)   /* caller buffer too small; required sizes were written */
+
+/* ---- InternalStatus ordinals (local/CommandsForKey.java:194-203) ---- */
+#define ACC_ST_TRANSITIVELY_KNOWN   0
+#define ACC_ST_HISTORICAL           1
+#define ACC_ST_PREACCEPTED          2
+#define ACC_ST_ACCEPTED             3
+#define ACC_ST_COMMITTED            4
+#define ACC_ST_STABLE               5
+#define ACC_ST_APPLIED              6
+#define ACC_ST_INVALID_OR_TRUNCATED 7
+
+/* ---- Txn.Kind ordinals (primitives/Txn.java:53-113); kind = (lsb >> 1) & 7 (TxnId.java:149-152) ---- */
+#define ACC_KIND_READ                 0
+#define ACC_KIND_WRITE                1
+#define ACC_KIND_EPHEMERAL_READ       2
+#define ACC_KIND_SYNC_POINT           3
+#define ACC_KIND_EXCLUSIVE_SYNC_POINT 4
+#define ACC_KIND_LOCAL_ONLY           5
+
+/* ---- memory placement of caller arrays ---- */
+#define ACC_MEM_HOST   0
+#define ACC_MEM_DEVICE 1
+
+/* ---- context options ---- */
+#define ACC_OPT_TIMING 0x1u   /* record per-kernel HIP events (bench / profiling) */
+
+typedef struct acc_ctx acc_ctx;
+
+typedef struct acc_opts {
+    uint32_t flags;           /* ACC_OPT_* */
+    uint32_t reserved;
+} acc_opts;
+
+/* Timestamp / TxnId as three SoA columns: Timestamp.msb, Timestamp.lsb, Node.Id.id
+ * (primitives/Timestamp.java:77-79). Order = Timestamp.compareTo (:208-217), identity = equals (:244-249). */
+typedef struct acc_ts_cols {
+    const uint64_t *msb;
+    const uint64_t *lsb;
+    const int32_t  *node;
+} acc_ts_cols;
+
+/* One batch = one CommandsForKey snapshot of one CommandStore. Every txn of the batch is both an
+ * entry of the CFK of each of its keys and a query T evaluated with startedBefore = T.executeAt and
+ * testKind = T.kind().witnesses(); p1 = (executeAt.equals(txnId) ? null : txnId). */
+typedef struct acc_batch_in {
+    uint32_t    n_txn;        /* N */
+    uint32_t    mem;          /* ACC_MEM_HOST or ACC_MEM_DEVICE for every pointer below */
+    uint64_t    n_pairs;      /* P = key_off[N]; must be < 2^32 */
+    acc_ts_cols txn_id;       /* [N] TxnIds, pairwise distinct under Timestamp.equals */
+    acc_ts_cols execute_at;   /* [N] executeAt (== txnId for PREACCEPTED-style entries) */
+    const uint8_t  *status;   /* [N] InternalStatus ordinal */
+    const uint32_t *key_off;  /* [N+1] CSR offsets into key_code */
+    const uint64_t *key_code; /* [P] order-preserving key codes, sorted unique within each txn (Keys) */
+} acc_batch_in;
+
+/* Result view of the last acc_keydeps_batch on a context. Pointers are DEVICE pointers owned by
+ * the context and valid until the next compute call on it. For txn t:
+ *   arena[arena_off[t] .. arena_off[t+1])  = Java KeyDeps.keysToTxnIds (int[]) of t's PartialDeps
+ *   key_idx[kd_off[t] .. kd_off[t+1])      = KeyDeps.keys as indices into t's input keys
+ *   dep_txn[u_off[t] .. u_off[t+1])        = KeyDeps.txnIds as batch indices, ascending TxnId order */
+typedef struct acc_keydeps_view {
+    uint32_t n_txn;
+    uint64_t total_arena, total_keys, total_deps, total_edges; /* Σ(Kd+E), ΣKd, ΣU, ΣE */
+    const uint64_t *arena_off;
+    const int32_t  *arena;
+    const uint64_t *kd_off;
+    const uint32_t *key_idx;
+    const uint64_t *u_off;
+    const uint32_t *dep_txn;
+} acc_keydeps_view;
+
+/* Caller-owned output buffers (two-call sizing: capacities in elements; a call with null offset
+ * arrays, or with a capacity below the requirement, returns ACC_E_CAP after writing the required
+ * totals to need_*, and touches nothing else). */
+typedef struct acc_keydeps_out {
+    uint32_t  mem;            /* ACC_MEM_HOST or ACC_MEM_DEVICE */
+    uint64_t  cap_arena, cap_keys, cap_deps;
+    uint64_t  need_arena, need_keys, need_deps;  /* written */
+    uint64_t *arena_off;      /* [N+1] */
+    int32_t  *arena;          /* [cap_arena] */
+    uint64_t *kd_off;         /* [N+1] */
+    uint32_t *key_idx;        /* [cap_keys] */
+    uint64_t *u_off;          /* [N+1] */
+    uint32_t *dep_txn;        /* [cap_deps] */
+} acc_keydeps_out;
+
+/* ---- context ---- */
+int         acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx);
+void        acc_destroy(acc_ctx *ctx);
+const char *acc_last_error(const acc_ctx *ctx);
+int         acc_sync(acc_ctx *ctx);
+/* HIP stream (hipStream_t) the context launches on, as an opaque handle. */
+void       *acc_stream(acc_ctx *ctx);
+const char *acc_version(void);
+
+/* ---- KeyDeps batch: CommandsForKey conflict scan + KeyDeps.Builder for all txns of a batch ---- */
+int acc_keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *out_view);
+int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out);
+
+/* ---- Deps.merge over many replies per txn ----
+ * Input: R = n_groups groups (one coordinated txn each); group g owns replies
+ * [grp_off[g], grp_off[g+1]); reply r is a KeyDeps in Java layout over integer ids:
+ *   keys:   key_code[key_off[r] .. key_off[r+1])          (sorted unique)
+ *   txnIds: txn_rank[val_off[r] .. val_off[r+1])          (sorted unique u32 order ranks of TxnIds)
+ *   keysToTxnIds: k2v[k2v_off[r] .. k2v_off[r+1])         (Java int[] verbatim)
+ * Output per group: the KeyDeps.merge result (== canonical union, KeyDepsTest.java:275-283) in the
+ * same three-array layout, device-resident in the context. */
+typedef struct acc_merge_in {
+    uint32_t mem;
+    uint32_t n_groups;
+    uint64_t n_replies;
+    const uint64_t *grp_off;   /* [n_groups+1] into replies */
+    const uint64_t *key_off;   /* [n_replies+1] */
+    const uint64_t *key_code;  /* [key_off[n_replies]] */
+    const uint64_t *val_off;   /* [n_replies+1] */
+    const uint32_t *txn_rank;  /* [val_off[n_replies]] */
+    const uint64_t *k2v_off;   /* [n_replies+1] */
+    const int32_t  *k2v;       /* [k2v_off[n_replies]] */
+} acc_merge_in;
+
+typedef struct acc_merge_view {
+    uint32_t n_groups;
+    uint64_t total_keys, total_vals, total_k2v, total_in_entries;
+    const uint64_t *key_off;  const uint64_t *key_code;
+    const uint64_t *val_off;  const uint32_t *txn_rank;
+    const uint64_t *k2v_off;  const int32_t  *k2v;
+} acc_merge_view;
+
+int acc_keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *out_view);
+
+/* ---- Levelisation of a dependency graph by executeAt ----
+ * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
+ * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).
+ * level[t] = 0 without remaining preds, else 1 + max level(pred); order = txns sorted by
+ * (level, exec_rank, index). Outputs are caller buffers of n elements in `mem`. */
+typedef struct acc_graph_in {
+    uint32_t mem;
+    uint32_t n;
+    const uint64_t *off;       /* [n+1] */
+    const uint32_t *dep;       /* [off[n]] */
+    const uint32_t *exec_rank; /* [n] */
+} acc_graph_in;
+
+int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
+
+/* ---- timing (ACC_OPT_TIMING) ---- */
+/* Per-kernel accumulated device time since the last reset: name[i], total ms, launch count. */
+int  acc_timing_count(acc_ctx *ctx);
+int  acc_timing_get(acc_ctx *ctx, int i, const char **name, double *total_ms, uint64_t *launches);
+void acc_timing_reset(acc_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACCORD_AMD_H */

@@ -1,0 +1,686 @@
+/*
+ * accord_oracle.c — TEST INFRASTRUCTURE ONLY (see accord_oracle.h header for the rules).
+ *
+ * Plain-C restatement of the reference Java, function by function. Paths are relative to
+ * /root/reference/accord-core/src/main/java/accord/. The O(prefix) CommandsForKey scan and the
+ * object-style builder are kept on purpose: this file is also the CPU baseline ("port").
+ */
+#define _GNU_SOURCE
+#include "accord_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ Timestamp / TxnId */
+
+typedef struct ts { uint64_t msb, lsb; int32_t node; } ts;
+
+/* Timestamp.IDENTITY_LSB / IDENTITY_FLAGS (Timestamp.java:41-42) */
+#define IDENTITY_LSB   0xFFFFFFFFFFFF001EULL
+#define IDENTITY_FLAGS 0x001EULL
+
+/* Timestamp.compareTo (Timestamp.java:208-217): unsigned msb, then lowHlc = lsb>>>16 (signed long
+ * compare of a non-negative value), then lsb & IDENTITY_FLAGS, then Node.Id.compareTo (signed int,
+ * local/Node.java:136-139). */
+static inline int ts_cmp(const ts *a, const ts *b)
+{
+    if (a->msb != b->msb) return a->msb < b->msb ? -1 : 1;
+    uint64_t ah = a->lsb >> 16, bh = b->lsb >> 16;
+    if (ah != bh) return ah < bh ? -1 : 1;
+    uint64_t af = a->lsb & IDENTITY_FLAGS, bf = b->lsb & IDENTITY_FLAGS;
+    if (af != bf) return af < bf ? -1 : 1;
+    if (a->node != b->node) return a->node < b->node ? -1 : 1;
+    return 0;
+}
+
+/* Timestamp.equals (Timestamp.java:244-249) */
+static inline int ts_eq(const ts *a, const ts *b)
+{
+    return a->msb == b->msb && ((a->lsb ^ b->lsb) & IDENTITY_LSB) == 0 && a->node == b->node;
+}
+
+int orc_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode)
+{
+    ts a = { amsb, alsb, anode }, b = { bmsb, blsb, bnode };
+    return ts_cmp(&a, &b);
+}
+
+/* TxnId.kind(): rwOrdinal = (flags >> 1) & 7 (TxnId.java:149-152) */
+static inline int ts_kind(const ts *t) { return (int)((t->lsb >> 1) & 7); }
+
+/* Txn.Kind ordinals (Txn.java:53-113) */
+enum { K_READ = 0, K_WRITE = 1, K_EREAD = 2, K_SYNC = 3, K_XSYNC = 4, K_LOCAL = 5, K_COUNT = 6 };
+/* Kinds predicates as bitmasks over Kind ordinals (Txn.java:125-153) */
+#define KINDS_WS           (1u << K_WRITE)
+#define KINDS_RS_OR_WS     ((1u << K_READ) | (1u << K_WRITE))
+#define KINDS_ANY_VISIBLE  ((1u << K_READ) | (1u << K_WRITE) | (1u << K_SYNC) | (1u << K_XSYNC))
+
+/* Kind.witnesses() (Txn.java:221-236). Returns -1 for kinds whose witnesses() throws. */
+static int kind_witnesses(int kind)
+{
+    switch (kind) {
+    case K_EREAD: case K_READ: return (int)KINDS_WS;
+    case K_WRITE: case K_SYNC: return (int)KINDS_RS_OR_WS;
+    case K_XSYNC:              return (int)KINDS_ANY_VISIBLE;
+    default:                   return -1;   /* LocalOnly: AssertionError; >5: ofOrdinal out of range */
+    }
+}
+
+/* CommandsForKey.InternalStatus ordinals (CommandsForKey.java:194-203) */
+enum { ST_TK = 0, ST_HIST = 1, ST_PRE = 2, ST_ACC = 3, ST_COMMITTED = 4, ST_STABLE = 5, ST_APPLIED = 6, ST_INVALID = 7 };
+
+/* ------------------------------------------------------------------ error plumbing */
+
+typedef struct err { int code; char msg[256]; } err;
+static void set_err(err *e, int code, const char *m)
+{
+    if (e->code) return;
+    e->code = code;
+    snprintf(e->msg, sizeof e->msg, "%s", m);
+}
+
+/* ------------------------------------------------------------------ growable buffers */
+
+typedef struct ivec { int64_t *v; size_t n, cap; } ivec;
+static void iv_push(ivec *a, int64_t x)
+{
+    if (a->n == a->cap) { a->cap = a->cap ? a->cap * 2 : 16; a->v = realloc(a->v, a->cap * sizeof *a->v); }
+    a->v[a->n++] = x;
+}
+
+/* ------------------------------------------------------------------ stable merge sort of indices */
+
+typedef int (*icmp_fn)(int64_t a, int64_t b, const void *ctx);
+
+/* Stable (like java.util.Arrays.sort on Objects / TimSort: equal elements keep input order). */
+static void stable_sort(int64_t *a, size_t n, icmp_fn cmp, const void *ctx)
+{
+    if (n < 2) return;
+    int64_t *tmp = malloc(n * sizeof *tmp);
+    for (size_t w = 1; w < n; w *= 2) {
+        for (size_t lo = 0; lo < n; lo += 2 * w) {
+            size_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+            size_t i = lo, j = mid, k = lo;
+            while (i < mid && j < hi) tmp[k++] = cmp(a[j], a[i], ctx) < 0 ? a[j++] : a[i++];
+            while (i < mid) tmp[k++] = a[i++];
+            while (j < hi) tmp[k++] = a[j++];
+        }
+        memcpy(a, tmp, n * sizeof *a);
+    }
+    free(tmp);
+}
+
+/* ------------------------------------------------------------------ batch data */
+
+typedef struct batch {
+    uint32_t n;
+    ts *id, *ex;
+    const uint8_t *status;
+    const uint32_t *key_off;
+    const uint64_t *key_code;
+} batch;
+
+static int cmp_txn_by_id(int64_t a, int64_t b, const void *c)
+{
+    const batch *B = c; return ts_cmp(&B->id[a], &B->id[b]);
+}
+static int cmp_txn_by_exec(int64_t a, int64_t b, const void *c)
+{
+    const batch *B = c; return ts_cmp(&B->ex[a], &B->ex[b]);
+}
+
+/* ------------------------------------------------------------------ CommandsForKey */
+
+/* One key's summary: txns sorted by TxnId (CommandsForKey.java:403-404) and committed[] = entries
+ * with COMMITTED <= status < INVALID_OR_TRUNCATED sorted by executeAt with a stable sort
+ * (ctor, CommandsForKey.java:459-469). Entries are batch txn indices. */
+typedef struct cfk {
+    uint64_t key;
+    int64_t *txns; size_t ntxns;
+    int64_t *committed; size_t ncommitted;
+} cfk;
+
+static void cfk_init(cfk *c, const batch *B)
+{
+    stable_sort(c->txns, c->ntxns, cmp_txn_by_id, B);
+    c->committed = malloc((c->ntxns ? c->ntxns : 1) * sizeof *c->committed);
+    c->ncommitted = 0;
+    for (size_t i = 0; i < c->ntxns; ++i) {
+        int s = B->status[c->txns[i]];
+        if (s >= ST_COMMITTED && s != ST_INVALID) c->committed[c->ncommitted++] = c->txns[i];
+    }
+    stable_sort(c->committed, c->ncommitted, cmp_txn_by_exec, B);
+}
+
+/* SortedArrays.binarySearch(..., FAST) (SortedArrays.java:992-1027) with the comparator
+ * (f, v) -> f.compareTo(v.executeAt) used by CommandsForKey.mapReduceActive (:619). */
+static long bsearch_fast_exec(const cfk *c, const batch *B, const ts *find)
+{
+    long from = 0, to = (long)c->ncommitted;
+    while (from < to) {
+        long i = (long)(((unsigned long)from + (unsigned long)to) >> 1);
+        int cc = ts_cmp(find, &B->ex[c->committed[i]]);
+        if (cc < 0) to = i;
+        else if (cc > 0) from = i + 1;
+        else return i;
+    }
+    return -1 - to;
+}
+
+/* java.util.Arrays.binarySearch(Object[], from, to, key) with Comparable (TxnInfo extends
+ * Timestamp): midVal.compareTo(key); used by CommandsForKey.insertPos (:1698-1703). */
+static long insert_pos(const cfk *c, const batch *B, const ts *key)
+{
+    long low = 0, high = (long)c->ntxns - 1;
+    while (low <= high) {
+        long mid = (long)(((unsigned long)low + (unsigned long)high) >> 1);
+        int cc = ts_cmp(&B->id[c->txns[mid]], key);
+        if (cc < 0) low = mid + 1;
+        else if (cc > 0) high = mid - 1;
+        else return mid;
+    }
+    return low;   /* i < 0 ? -1 - i : i  ==  low */
+}
+
+/* ------------------------------------------------------------------ KeyDeps.Builder */
+
+/* RelationMultiMap.AbstractBuilder<Key, TxnId, KeyDeps> (RelationMultiMap.java:88-260) with keys as
+ * u64 codes (unsigned order = RoutableKey.compareTo via the host's order-preserving encoding) and
+ * values as batch txn indices compared by TxnId (KeyDeps.ADAPTER valueComparator = TxnId::compareTo). */
+typedef struct builder {
+    const batch *B;
+    uint64_t *keys; size_t keys_cap;
+    int64_t *key_limits;
+    int64_t *vals; size_t vals_cap;
+    size_t key_count, key_offset, total_count;
+    int has_ordered_keys, has_ordered_values;
+} builder;
+
+static void b_init(builder *b, const batch *B)
+{
+    memset(b, 0, sizeof *b);
+    b->B = B;
+    b->keys_cap = 16; b->keys = malloc(16 * sizeof *b->keys); b->key_limits = malloc(16 * sizeof *b->key_limits);
+    b->vals_cap = 16; b->vals = malloc(16 * sizeof *b->vals);
+    b->has_ordered_keys = 1; b->has_ordered_values = 1;
+}
+static void b_reset(builder *b)
+{
+    b->key_count = b->key_offset = b->total_count = 0;
+    b->has_ordered_keys = 1; b->has_ordered_values = 1;
+}
+static void b_free(builder *b) { free(b->keys); free(b->key_limits); free(b->vals); }
+
+/* AbstractBuilder.finishKey (:147-171) */
+static void b_finish_key(builder *b)
+{
+    if (b->total_count == b->key_offset && b->key_count > 0) { --b->key_count; return; }
+    if (b->key_count == 0) return;
+    if (!b->has_ordered_values) {
+        stable_sort(b->vals + b->key_offset, b->total_count - b->key_offset, cmp_txn_by_id, b->B);
+        size_t removed = 0;
+        for (size_t i = b->key_offset + 1; i < b->total_count; ++i) {
+            if (ts_eq(&b->B->id[b->vals[i - 1]], &b->B->id[b->vals[i]])) ++removed;
+            else if (removed > 0) b->vals[i - removed] = b->vals[i];
+        }
+        b->total_count -= removed;
+    }
+    b->key_limits[b->key_count - 1] = (int64_t)b->total_count;
+    b->key_offset = b->total_count;
+}
+
+/* AbstractBuilder.nextKey (:125-145) */
+static void b_next_key(builder *b, uint64_t key)
+{
+    if (b->key_count > 0 && b->keys[b->key_count - 1] >= key) b->has_ordered_keys = 0;
+    b_finish_key(b);
+    if (b->key_count == b->keys_cap) {
+        b->keys_cap *= 2;
+        b->keys = realloc(b->keys, b->keys_cap * sizeof *b->keys);
+        b->key_limits = realloc(b->key_limits, b->keys_cap * sizeof *b->key_limits);
+    }
+    b->keys[b->key_count++] = key;
+    b->has_ordered_values = 1;
+}
+
+/* AbstractBuilder.add(V) (:183-199) */
+static void b_add_value(builder *b, int64_t v)
+{
+    if (b->has_ordered_values && b->total_count > b->key_offset
+        && ts_cmp(&b->B->id[b->vals[b->total_count - 1]], &b->B->id[v]) >= 0)
+        b->has_ordered_values = 0;
+    if (b->total_count >= b->vals_cap) { b->vals_cap *= 2; b->vals = realloc(b->vals, b->vals_cap * sizeof *b->vals); }
+    b->vals[b->total_count++] = v;
+}
+
+/* AbstractBuilder.add(K, V) (:173-178) */
+static void b_add(builder *b, uint64_t key, int64_t v)
+{
+    if (b->key_count == 0 || b->keys[b->key_count - 1] != key) b_next_key(b, key);
+    b_add_value(b, v);
+}
+
+/* A built KeyDeps over batch indices: keys (codes), txnIds (batch idx), keysToTxnIds (Java int[]). */
+typedef struct kdeps {
+    uint64_t *keys; size_t nkeys;
+    int64_t  *vals; size_t nvals;
+    int32_t  *k2v;  size_t nk2v;
+} kdeps;
+
+static void kd_free(kdeps *d) { free(d->keys); free(d->vals); free(d->k2v); memset(d, 0, sizeof *d); }
+
+static int cmp_u64(int64_t a, int64_t b, const void *c)
+{
+    const uint64_t *k = c; return k[a] < k[b] ? -1 : k[a] > k[b];
+}
+
+/* SortedArrays.findNextIntersection / foldlIntersection (SortedArrays.java:1148-1173,1271-1292):
+ * indices (into `values`) of the members of the sorted key list, written to out. */
+static size_t fold_intersection(const batch *B, const int64_t *values, size_t nvalues,
+                                const int64_t *list, size_t from, size_t to, int32_t *out)
+{
+    size_t ai = 0, bi = from, n = 0;
+    while (ai < nvalues && bi < to) {
+        int c = ts_cmp(&B->id[values[ai]], &B->id[list[bi]]);
+        if (c == 0) { out[n++] = (int32_t)ai; ++ai; ++bi; }
+        else if (c < 0) ++ai;
+        else ++bi;
+    }
+    return n;
+}
+
+/* AbstractBuilder.build (:201-260). Returns 0 / -1 (IllegalArgumentException: duplicate key). */
+static int b_build(builder *b, kdeps *out, err *e)
+{
+    memset(out, 0, sizeof *out);
+    if (b->total_count == 0) return 0;          /* none() = KeyDeps.NONE */
+    b_finish_key(b);
+
+    size_t total = b->total_count;
+    int64_t *uv = malloc(total * sizeof *uv);
+    memcpy(uv, b->vals, total * sizeof *uv);
+    stable_sort(uv, total, cmp_txn_by_id, b->B);
+    size_t vc = 1;
+    for (size_t i = 1; i < total; ++i)
+        if (!ts_eq(&b->B->id[uv[vc - 1]], &b->B->id[uv[i]])) uv[vc++] = uv[i];
+
+    size_t kc = b->key_count;
+    int64_t *sorted_idx = NULL;          /* sortedKeyIndexes[sorted pos] = original key index */
+    uint64_t *skeys = malloc((kc ? kc : 1) * sizeof *skeys);
+    if (b->has_ordered_keys) {
+        memcpy(skeys, b->keys, kc * sizeof *skeys);
+    } else {
+        int64_t *perm = malloc(kc * sizeof *perm);
+        for (size_t i = 0; i < kc; ++i) perm[i] = (int64_t)i;
+        stable_sort(perm, kc, cmp_u64, b->keys);
+        for (size_t i = 0; i < kc; ++i) skeys[i] = b->keys[perm[i]];
+        for (size_t i = 1; i < kc; ++i)
+            if (skeys[i - 1] == skeys[i]) {
+                free(perm); free(skeys); free(uv);
+                set_err(e, -1, "Key has been visited more than once (AbstractBuilder.build)");
+                return -1;
+            }
+        sorted_idx = perm;
+    }
+
+    int32_t *res = malloc((kc + total) * sizeof *res);
+    size_t offset = kc;
+    for (size_t ki = 0; ki < kc; ++ki) {
+        size_t k = sorted_idx ? (size_t)sorted_idx[ki] : ki;
+        size_t from = k == 0 ? 0 : (size_t)b->key_limits[k - 1];
+        size_t to = (size_t)b->key_limits[k];
+        offset += fold_intersection(b->B, uv, vc, b->vals, from, to, res + offset);
+        res[ki] = (int32_t)offset;
+    }
+    free(sorted_idx);
+    out->keys = skeys; out->nkeys = kc;
+    out->vals = realloc(uv, (vc ? vc : 1) * sizeof *uv); out->nvals = vc;
+    out->k2v = res; out->nk2v = offset;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ linearUnion (KeyDeps.with) */
+
+/* RelationMultiMap.linearUnion (RelationMultiMap.java:561-816), general path. Its fast paths
+ * (:583-730) return an input unchanged only when it already equals the union, so the value result is
+ * always the canonical union (KeyDepsTest.testMergedProperty). Value identity on ties keeps the
+ * LEFT element (SortedArrays.linearUnion :250-255). cmpv compares two value handles. */
+typedef int (*vcmp_fn)(int64_t a, int64_t b, const void *ctx);
+
+static void kd_union(const kdeps *L, const kdeps *R, kdeps *out, vcmp_fn cmpv, const void *ctx)
+{
+    /* SortedArrays.linearUnion of keys and of values (:152-281) */
+    uint64_t *ok = malloc((L->nkeys + R->nkeys + 1) * sizeof *ok); size_t nok = 0;
+    { size_t i = 0, j = 0;
+      while (i < L->nkeys && j < R->nkeys) {
+          if (L->keys[i] < R->keys[j]) ok[nok++] = L->keys[i++];
+          else if (L->keys[i] > R->keys[j]) ok[nok++] = R->keys[j++];
+          else { ok[nok++] = L->keys[i++]; ++j; }
+      }
+      while (i < L->nkeys) ok[nok++] = L->keys[i++];
+      while (j < R->nkeys) ok[nok++] = R->keys[j++]; }
+    int64_t *ov = malloc((L->nvals + R->nvals + 1) * sizeof *ov); size_t nov = 0;
+    int32_t *remapL = malloc((L->nvals + 1) * sizeof *remapL), *remapR = malloc((R->nvals + 1) * sizeof *remapR);
+    { size_t i = 0, j = 0;
+      while (i < L->nvals && j < R->nvals) {
+          int c = cmpv(L->vals[i], R->vals[j], ctx);
+          if (c < 0) { remapL[i] = (int32_t)nov; ov[nov++] = L->vals[i++]; }
+          else if (c > 0) { remapR[j] = (int32_t)nov; ov[nov++] = R->vals[j++]; }
+          else { remapL[i] = remapR[j] = (int32_t)nov; ov[nov++] = L->vals[i++]; ++j; }
+      }
+      while (i < L->nvals) { remapL[i] = (int32_t)nov; ov[nov++] = L->vals[i++]; }
+      while (j < R->nvals) { remapR[j] = (int32_t)nov; ov[nov++] = R->vals[j++]; } }
+
+    int32_t *o = malloc((L->nk2v + R->nk2v + 1) * sizeof *o);
+    size_t lk = 0, rk = 0, okk = 0, l = L->nkeys, r = R->nkeys, olen = nok;
+    while (lk < L->nkeys && rk < R->nkeys) {
+        if (L->keys[lk] < R->keys[rk]) {
+            while (l < (size_t)L->k2v[lk]) o[olen++] = remapL[L->k2v[l++]];
+            o[okk++] = (int32_t)olen; lk++;
+        } else if (L->keys[lk] > R->keys[rk]) {
+            while (r < (size_t)R->k2v[rk]) o[olen++] = remapR[R->k2v[r++]];
+            o[okk++] = (int32_t)olen; rk++;
+        } else {
+            while (l < (size_t)L->k2v[lk] && r < (size_t)R->k2v[rk]) {
+                int32_t nl = remapL[L->k2v[l]], nr = remapR[R->k2v[r]];
+                if (nl <= nr) { o[olen++] = nl; l += 1; r += nl == nr ? 1 : 0; }
+                else { o[olen++] = nr; ++r; }
+            }
+            while (l < (size_t)L->k2v[lk]) o[olen++] = remapL[L->k2v[l++]];
+            while (r < (size_t)R->k2v[rk]) o[olen++] = remapR[R->k2v[r++]];
+            o[okk++] = (int32_t)olen; rk++; lk++;
+        }
+    }
+    while (lk < L->nkeys) { while (l < (size_t)L->k2v[lk]) o[olen++] = remapL[L->k2v[l++]]; o[okk++] = (int32_t)olen; lk++; }
+    while (rk < R->nkeys) { while (r < (size_t)R->k2v[rk]) o[olen++] = remapR[R->k2v[r++]]; o[okk++] = (int32_t)olen; rk++; }
+    free(remapL); free(remapR);
+    out->keys = ok; out->nkeys = nok; out->vals = ov; out->nvals = nov; out->k2v = o; out->nk2v = olen;
+}
+
+static int cmp_vals_by_id(int64_t a, int64_t b, const void *c)
+{
+    const batch *B = c; return ts_cmp(&B->id[a], &B->id[b]);
+}
+
+/* KeyDeps.with (KeyDeps.java:238-253): empty operands short-circuit. */
+static void kd_with(kdeps *acc, const kdeps *that, vcmp_fn cmpv, const void *ctx)
+{
+    if (that->nkeys == 0) return;
+    if (acc->nkeys == 0) {
+        acc->keys = malloc(that->nkeys * sizeof *acc->keys); memcpy(acc->keys, that->keys, that->nkeys * sizeof *acc->keys); acc->nkeys = that->nkeys;
+        acc->vals = malloc((that->nvals + 1) * sizeof *acc->vals); memcpy(acc->vals, that->vals, that->nvals * sizeof *acc->vals); acc->nvals = that->nvals;
+        acc->k2v = malloc(that->nk2v * sizeof *acc->k2v); memcpy(acc->k2v, that->k2v, that->nk2v * sizeof *acc->k2v); acc->nk2v = that->nk2v;
+        return;
+    }
+    kdeps u; kd_union(acc, that, &u, cmpv, ctx);
+    kd_free(acc); *acc = u;
+}
+
+/* ------------------------------------------------------------------ the batch */
+
+static int cmp_pair_key(int64_t a, int64_t b, const void *c)
+{
+    const uint64_t *kc = c; return kc[a] < kc[b] ? -1 : kc[a] > kc[b];
+}
+
+/* CommandsForKey.mapReduceActive (CommandsForKey.java:614-650) feeding the calculatePartialDeps
+ * map function (PreAccept.java:253-259): emits (key, txn) into the builder. */
+static uint64_t cfk_map_reduce_active(const cfk *c, const batch *B, const ts *started_before,
+                                      unsigned test_kinds, long p1, builder *b, err *e)
+{
+    long i = bsearch_fast_exec(c, B, started_before);
+    if (i < 0) i = -2 - i; else --i;
+    while (i >= 0 && ts_kind(&B->id[c->committed[i]]) != K_WRITE) --i;   /* TxnInfo.kind(): kind of the TxnId */
+    const ts *max_committed_before = i < 0 ? NULL : &B->ex[c->committed[i]];
+    long end = insert_pos(c, B, started_before);
+    uint64_t visited = 0;
+    for (long k = 0; k < end; ++k) {
+        int64_t t = c->txns[k];
+        ++visited;
+        int kind = ts_kind(&B->id[t]);
+        if (kind >= K_COUNT) { set_err(e, -1, "Kind.ofOrdinal: invalid kind ordinal"); return visited; }
+        if (!((test_kinds >> kind) & 1u)) continue;
+        switch (B->status[t]) {
+        case ST_COMMITTED: case ST_STABLE: case ST_APPLIED:
+            if (max_committed_before == NULL || ts_cmp(&B->ex[t], max_committed_before) >= 0) break;
+            continue;
+        case ST_TK: case ST_INVALID:
+            continue;
+        default: break;
+        }
+        if (p1 < 0 || !ts_eq(&B->id[t], &B->id[p1])) b_add(b, c->key, t);
+    }
+    return visited;
+}
+
+orc_keydeps_result *orc_keydeps_batch(uint32_t n,
+                                      const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                      const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                      const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi)
+{
+    orc_keydeps_result *R = calloc(1, sizeof *R);
+    err E = { 0, "" };
+    batch B = { n, malloc((n + 1) * sizeof(ts)), malloc((n + 1) * sizeof(ts)), status, key_off, key_code };
+    for (uint32_t i = 0; i < n; ++i) {
+        B.id[i] = (ts){ tmsb[i], tlsb[i], tnode[i] };
+        B.ex[i] = (ts){ emsb[i], elsb[i], enode[i] };
+    }
+    if (n_shards == 0) n_shards = 1;
+    if (query_hi > n) query_hi = n;
+    uint64_t P = key_off[n];
+
+    /* Input validation (what the reference would reject): Keys sorted unique per txn
+     * (Keys.ofSortedUnique), valid kinds/statuses, TxnIds distinct (CFK txns sorted unique). */
+    for (uint32_t t = 0; t < n && !E.code; ++t) {
+        if (status[t] > ST_INVALID) set_err(&E, -1, "invalid InternalStatus ordinal");
+        if (ts_kind(&B.id[t]) >= K_COUNT) set_err(&E, -1, "Kind.ofOrdinal: invalid kind ordinal");
+        for (uint32_t j = key_off[t] + 1; j < key_off[t + 1]; ++j)
+            if (key_code[j - 1] >= key_code[j]) set_err(&E, -1, "keys of a txn must be sorted and unique");
+    }
+
+    /* Group pairs by key -> one CommandsForKey per key (InMemoryCommandStore.commandsForKey). */
+    int64_t *pidx = malloc((P + 1) * sizeof *pidx);
+    for (uint64_t j = 0; j < P; ++j) pidx[j] = (int64_t)j;
+    stable_sort(pidx, P, cmp_pair_key, key_code);
+    int64_t *owner = malloc((P + 1) * sizeof *owner);
+    for (uint32_t t = 0; t < n; ++t) for (uint32_t j = key_off[t]; j < key_off[t + 1]; ++j) owner[j] = t;
+    size_t ncfk = 0;
+    cfk *cfks = calloc(P + 1, sizeof *cfks);
+    for (uint64_t s = 0; s < P; ) {
+        uint64_t e2 = s;
+        while (e2 < P && key_code[pidx[e2]] == key_code[pidx[s]]) ++e2;
+        cfk *c = &cfks[ncfk++];
+        c->key = key_code[pidx[s]];
+        c->ntxns = e2 - s;
+        c->txns = malloc(c->ntxns * sizeof *c->txns);
+        for (uint64_t q = s; q < e2; ++q) c->txns[q - s] = owner[pidx[q]];
+        cfk_init(c, &B);
+        for (size_t q = 1; q < c->ntxns; ++q)
+            if (ts_eq(&B.id[c->txns[q - 1]], &B.id[c->txns[q]]))
+                set_err(&E, -1, "TxnIds of a batch must be distinct (CommandsForKey txns are sorted unique)");
+        s = e2;
+    }
+
+    /* EvenSplit of the observed key-code domain into n_shards contiguous shards
+     * (ShardDistributor.java:106-156). KeyDeps results are invariant to the split. */
+    uint64_t klo = ncfk ? cfks[0].key : 0, khi = ncfk ? cfks[ncfk - 1].key : 0;
+    unsigned __int128 span = (unsigned __int128)(khi - klo) + 1;
+    uint64_t *shard_lo = malloc((n_shards + 1) * sizeof *shard_lo);
+    for (uint32_t s = 0; s < n_shards; ++s) shard_lo[s] = klo + (uint64_t)(span * s / n_shards);
+
+    R->n_txn = n;
+    R->arena_off = calloc(n + 1, sizeof(uint64_t));
+    R->kd_off = calloc(n + 1, sizeof(uint64_t));
+    R->u_off = calloc(n + 1, sizeof(uint64_t));
+    ivec arena = { 0 }, kidx = { 0 }, deps = { 0 };
+    builder b; b_init(&b, &B);
+
+    for (uint32_t t = 0; t < n && !E.code; ++t) {
+        R->arena_off[t] = arena.n; R->kd_off[t] = kidx.n; R->u_off[t] = deps.n;
+        if (t < query_lo || t >= query_hi) continue;
+        int wk = kind_witnesses(ts_kind(&B.id[t]));
+        if (wk < 0) { set_err(&E, -2, "Kind.witnesses(): unhandled kind (AssertionError)"); break; }
+        /* p1 = executeAt.equals(txnId) ? null : txnId (PreAccept.java:259) */
+        long p1 = ts_eq(&B.ex[t], &B.id[t]) ? -1 : (long)t;
+        kdeps acc = { 0 };
+        for (uint32_t sh = 0; sh < n_shards && !E.code; ++sh) {
+            uint64_t lo = shard_lo[sh];
+            int last = sh + 1 == n_shards;
+            uint64_t hi = last ? 0 : shard_lo[sh + 1];
+            b_reset(&b);
+            /* InMemoryCommandStore.mapReduceForKey (:257-272): keys of T in this slice, ascending. */
+            for (uint32_t j = key_off[t]; j < key_off[t + 1]; ++j) {
+                uint64_t k = key_code[j];
+                if (k < lo || (!last && k >= hi)) continue;
+                size_t a = 0, z = ncfk;
+                while (a < z) { size_t m = (a + z) / 2; if (cfks[m].key < k) a = m + 1; else z = m; }
+                R->visited += cfk_map_reduce_active(&cfks[a], &B, &B.ex[t], (unsigned)wk, p1, &b, &E);
+            }
+            kdeps part; if (b_build(&b, &part, &E)) break;
+            /* PreAccept.reduce -> PartialDeps.with -> KeyDeps.with (PreAccept.java:141-156) */
+            kd_with(&acc, &part, cmp_vals_by_id, &B);
+            kd_free(&part);
+        }
+        /* Emit in the ABI layout: key indices into T's keys, deps as batch indices. */
+        for (size_t q = 0; q < acc.nk2v; ++q) iv_push(&arena, acc.k2v[q]);
+        for (size_t q = 0; q < acc.nkeys; ++q) {
+            uint32_t a = key_off[t], z = key_off[t + 1];
+            while (a < z) { uint32_t m = (a + z) / 2; if (key_code[m] < acc.keys[q]) a = m + 1; else z = m; }
+            iv_push(&kidx, (int64_t)(a - key_off[t]));
+        }
+        for (size_t q = 0; q < acc.nvals; ++q) iv_push(&deps, acc.vals[q]);
+        R->total_edges += acc.nk2v - acc.nkeys;
+        kd_free(&acc);
+    }
+    R->arena_off[n] = arena.n; R->kd_off[n] = kidx.n; R->u_off[n] = deps.n;
+    R->arena = malloc((arena.n + 1) * sizeof(int32_t));
+    for (size_t q = 0; q < arena.n; ++q) R->arena[q] = (int32_t)arena.v[q];
+    R->key_idx = malloc((kidx.n + 1) * sizeof(uint32_t));
+    for (size_t q = 0; q < kidx.n; ++q) R->key_idx[q] = (uint32_t)kidx.v[q];
+    R->dep_txn = malloc((deps.n + 1) * sizeof(uint32_t));
+    for (size_t q = 0; q < deps.n; ++q) R->dep_txn[q] = (uint32_t)deps.v[q];
+    R->error = E.code;
+    snprintf(R->message, sizeof R->message, "%s", E.msg);
+
+    b_free(&b);
+    free(arena.v); free(kidx.v); free(deps.v);
+    for (size_t c = 0; c < ncfk; ++c) { free(cfks[c].txns); free(cfks[c].committed); }
+    free(cfks); free(pidx); free(owner); free(shard_lo); free(B.id); free(B.ex);
+    return R;
+}
+
+void orc_keydeps_free(orc_keydeps_result *r)
+{
+    if (!r) return;
+    free(r->arena_off); free(r->arena); free(r->kd_off); free(r->key_idx); free(r->u_off); free(r->dep_txn);
+    free(r);
+}
+
+/* ------------------------------------------------------------------ KeyDeps.merge */
+
+static int cmp_u32_rank(int64_t a, int64_t b, const void *c)
+{
+    (void)c; return a < b ? -1 : a > b;
+}
+
+/* KeyDeps.merge(List, getter, getter) (KeyDeps.java:115-135): skip null/empty, LinearMerger.update
+ * folds linearUnion left to right (RelationMultiMap.java:333-373). Values are u32 TxnId ranks. */
+orc_merge_result *orc_keydeps_merge(uint32_t n_groups, const uint64_t *grp_off,
+                                    const uint64_t *key_off, const uint64_t *key_code,
+                                    const uint64_t *val_off, const uint32_t *txn_rank,
+                                    const uint64_t *k2v_off, const int32_t *k2v)
+{
+    orc_merge_result *R = calloc(1, sizeof *R);
+    R->n_groups = n_groups;
+    R->key_off = calloc(n_groups + 1, sizeof(uint64_t));
+    R->val_off = calloc(n_groups + 1, sizeof(uint64_t));
+    R->k2v_off = calloc(n_groups + 1, sizeof(uint64_t));
+    ivec ok = { 0 }, ov = { 0 }, o = { 0 };
+    for (uint32_t g = 0; g < n_groups; ++g) {
+        kdeps acc = { 0 };
+        for (uint64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) {
+            kdeps in;
+            in.nkeys = key_off[r + 1] - key_off[r];
+            if (in.nkeys == 0) continue;   /* deps.isEmpty() */
+            in.keys = (uint64_t *)(key_code + key_off[r]);
+            in.nvals = val_off[r + 1] - val_off[r];
+            in.vals = malloc((in.nvals + 1) * sizeof *in.vals);
+            for (size_t q = 0; q < in.nvals; ++q) in.vals[q] = txn_rank[val_off[r] + q];
+            in.nk2v = k2v_off[r + 1] - k2v_off[r];
+            in.k2v = (int32_t *)(k2v + k2v_off[r]);
+            /* KeyDeps ctor check (KeyDeps.java:184-185) */
+            if ((uint64_t)in.k2v[in.nkeys - 1] != in.nk2v && !R->error) {
+                R->error = -1; snprintf(R->message, sizeof R->message, "Last key in keyToTxnId does not point to the end of the array");
+            }
+            kd_with(&acc, &in, cmp_u32_rank, NULL);
+            free(in.vals);
+        }
+        R->key_off[g] = ok.n; R->val_off[g] = ov.n; R->k2v_off[g] = o.n;
+        for (size_t q = 0; q < acc.nkeys; ++q) iv_push(&ok, (int64_t)acc.keys[q]);
+        for (size_t q = 0; q < acc.nvals; ++q) iv_push(&ov, acc.vals[q]);
+        for (size_t q = 0; q < acc.nk2v; ++q) iv_push(&o, acc.k2v[q]);
+        kd_free(&acc);
+    }
+    R->key_off[n_groups] = ok.n; R->val_off[n_groups] = ov.n; R->k2v_off[n_groups] = o.n;
+    R->key_code = malloc((ok.n + 1) * sizeof(uint64_t));
+    for (size_t q = 0; q < ok.n; ++q) R->key_code[q] = (uint64_t)ok.v[q];
+    R->txn_rank = malloc((ov.n + 1) * sizeof(uint32_t));
+    for (size_t q = 0; q < ov.n; ++q) R->txn_rank[q] = (uint32_t)ov.v[q];
+    R->k2v = malloc((o.n + 1) * sizeof(int32_t));
+    for (size_t q = 0; q < o.n; ++q) R->k2v[q] = (int32_t)o.v[q];
+    free(ok.v); free(ov.v); free(o.v);
+    return R;
+}
+
+void orc_merge_free(orc_merge_result *r)
+{
+    if (!r) return;
+    free(r->key_off); free(r->key_code); free(r->val_off); free(r->txn_rank); free(r->k2v_off); free(r->k2v);
+    free(r);
+}
+
+/* ------------------------------------------------------------------ levelisation */
+
+static int cmp_exec_rank(int64_t a, int64_t b, const void *c)
+{
+    const uint32_t *er = c; return er[a] < er[b] ? -1 : er[a] > er[b];
+}
+typedef struct lvl_ctx { const uint32_t *level, *exec_rank; } lvl_ctx;
+static int cmp_level_order(int64_t a, int64_t b, const void *c)
+{
+    const lvl_ctx *L = c;
+    if (L->level[a] != L->level[b]) return L->level[a] < L->level[b] ? -1 : 1;
+    if (L->exec_rank[a] != L->exec_rank[b]) return L->exec_rank[a] < L->exec_rank[b] ? -1 : 1;
+    return a < b ? -1 : a > b;
+}
+
+/* A txn waits on each dep whose executeAt is earlier than its own (Commands.updateWaitingOn
+ * drops deps with a later executeAt, Commands.java:804-810). level = 0 without such deps, else
+ * 1 + max(level of dep). Processing in executeAt order makes every dep's level final first. */
+int orc_levelise(uint32_t n, const uint64_t *off, const uint32_t *dep, const uint32_t *exec_rank,
+                 uint32_t *level, uint32_t *order, uint32_t *n_levels)
+{
+    int64_t *idx = malloc((n + 1) * sizeof *idx);
+    for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+    stable_sort(idx, n, cmp_exec_rank, exec_rank);
+    uint32_t maxl = 0;
+    for (uint32_t q = 0; q < n; ++q) {
+        uint32_t t = (uint32_t)idx[q], l = 0;
+        for (uint64_t e = off[t]; e < off[t + 1]; ++e) {
+            uint32_t d = dep[e];
+            if (d >= n) { free(idx); return -1; }
+            if (exec_rank[d] < exec_rank[t] && level[d] + 1 > l) l = level[d] + 1;
+        }
+        level[t] = l;
+        if (l + 1 > maxl) maxl = l + 1;
+    }
+    for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+    lvl_ctx L = { level, exec_rank };
+    stable_sort(idx, n, cmp_level_order, &L);
+    for (uint32_t i = 0; i < n; ++i) order[i] = (uint32_t)idx[i];
+    *n_levels = n ? maxl : 0;
+    free(idx);
+    return 0;
+}

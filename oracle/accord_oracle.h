@@ -1,0 +1,75 @@
+/*
+ * accord_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference (aweisberg/cassandra-accord @ 2025-03-04) algorithms on the
+ * dependency-calculation path. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load this; the product path (libaccord_amd.so) never links or calls it.
+ *
+ * Parity status:
+ *   - KeyDeps.Builder / linearUnion / KeyDeps.merge: pinned by the reference's own property tests
+ *     (KeyDepsTest.testMergedProperty, builder, testSimpleEquality), restated as committed fixtures.
+ *   - CommandsForKey.mapReduceActive: the reference has NO test for it (CommandsForKey.java:126
+ *     "TODO (required): randomised testing"); the Java cannot be built here (no JDK, Gradle needs
+ *     network). Its parity is pinned only by this line-by-line restatement cross-checked against the
+ *     independent Python model in oracle/canonical.py ("parity unpinned" by the reference itself).
+ */
+#ifndef ACCORD_ORACLE_H
+#define ACCORD_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_keydeps_result {
+    uint32_t  n_txn;
+    uint64_t *arena_off;  int32_t  *arena;
+    uint64_t *kd_off;     uint32_t *key_idx;
+    uint64_t *u_off;      uint32_t *dep_txn;
+    uint64_t  total_edges;
+    uint64_t  visited;    /* entries visited by the O(prefix) scans (work counter) */
+    int       error;      /* 0 ok, -1 IllegalArgument, -2 IllegalState */
+    char      message[256];
+} orc_keydeps_result;
+
+/* Batch PreAccept.calculatePartialDeps over one CommandsForKey snapshot (SURVEY.md §8 batch
+ * semantics). n_shards > 1 evaluates it the way CommandStores do: EvenSplit of the key-code domain
+ * into contiguous shards, per-shard calculatePartialDeps, then the PreAccept.reduce fold of
+ * PartialDeps.with in shard order (PreAccept.java:141-156, CommandStores.java:575-592).
+ * query_lo/query_hi restrict which txns are evaluated as queries (all txns stay CFK entries);
+ * results for other txns are empty. */
+orc_keydeps_result *orc_keydeps_batch(uint32_t n,
+                                      const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                      const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                      const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi);
+void orc_keydeps_free(orc_keydeps_result *r);
+
+/* KeyDeps.merge (KeyDeps.java:115-135) over groups of replies in the acc_merge_in layout
+ * (integer key codes, u32 TxnId order ranks). Output arrays are malloc'd; free with orc_merge_free. */
+typedef struct orc_merge_result {
+    uint32_t  n_groups;
+    uint64_t *key_off; uint64_t *key_code;
+    uint64_t *val_off; uint32_t *txn_rank;
+    uint64_t *k2v_off; int32_t  *k2v;
+    int       error;
+    char      message[256];
+} orc_merge_result;
+
+orc_merge_result *orc_keydeps_merge(uint32_t n_groups, const uint64_t *grp_off,
+                                    const uint64_t *key_off, const uint64_t *key_code,
+                                    const uint64_t *val_off, const uint32_t *txn_rank,
+                                    const uint64_t *k2v_off, const int32_t *k2v);
+void orc_merge_free(orc_merge_result *r);
+
+/* Deterministic levelisation restatement. */
+int orc_levelise(uint32_t n, const uint64_t *off, const uint32_t *dep, const uint32_t *exec_rank,
+                 uint32_t *level, uint32_t *order, uint32_t *n_levels);
+
+/* Timestamp.compareTo (Timestamp.java:208-217) — exported for tests. */
+int orc_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

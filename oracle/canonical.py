@@ -1,0 +1,141 @@
+"""Independent canonical model of the batch deps semantics — TEST INFRASTRUCTURE ONLY.
+
+Written from the reference semantics as set definitions (dict of sorted sets), NOT as a port of the
+loops, so it cross-checks the line-by-line C restatement in accord_oracle.c:
+
+  * Timestamp order/identity: tuple (msb, lsb>>>16, lsb & 0x1E, node) (Timestamp.java:208-249).
+  * deps of T on key k (CommandsForKey.mapReduceActive, CommandsForKey.java:614-650):
+        { D on k : D.txnId < S, T.kind.witnesses(D.kind), D.status not in {TRANSITIVELY_KNOWN,
+          INVALID_OR_TRUNCATED}, and (D not committed or M is None or D.executeAt >= M) } minus p1
+    with S = T.executeAt, M = max executeAt of committed Writes on k with executeAt < S.
+    (This set form is exact when committed executeAts on a key are distinct; the FAST-bisection tie
+    quirk is exercised against the C restatement only.)
+  * KeyDeps layout (KeyDeps.java:150-172): keys with >=1 dep, txnIds = sorted union, keysToTxnIds.
+  * KeyDeps.merge == canonical union (KeyDepsTest.java:275-283).
+Pure-Python loops: small inputs only.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+WS = {1}
+RS_OR_WS = {0, 1}
+ANY_VISIBLE = {0, 1, 3, 4}
+WITNESSES = {0: WS, 2: WS, 1: RS_OR_WS, 3: RS_OR_WS, 4: ANY_VISIBLE}  # Txn.java:221-236
+
+
+def ts_key(msb, lsb, node):
+    msb, lsb = int(msb), int(lsb)
+    return (msb, lsb >> 16, lsb & 0x1E, int(node))
+
+
+def kind_of(lsb) -> int:
+    return (int(lsb) >> 1) & 7
+
+
+def keydeps_batch(b, query_lo=0, query_hi=None):
+    """Returns list per txn of (key_idx list, dep_txn list, keysToTxnIds list)."""
+    n = b.n_txn
+    tid = [ts_key(b.txn_msb[i], b.txn_lsb[i], b.txn_node[i]) for i in range(n)]
+    tex = [ts_key(b.exe_msb[i], b.exe_lsb[i], b.exe_node[i]) for i in range(n)]
+    kinds = [kind_of(b.txn_lsb[i]) for i in range(n)]
+    status = [int(s) for s in b.status]
+    by_key: dict[int, list[int]] = {}
+    for t in range(n):
+        for j in range(int(b.key_off[t]), int(b.key_off[t + 1])):
+            by_key.setdefault(int(b.key_code[j]), []).append(t)
+    committed = {4, 5, 6}
+    out = []
+    hi = n if query_hi is None else query_hi
+    for t in range(n):
+        if not (query_lo <= t < hi):
+            out.append(([], [], []))
+            continue
+        S = tex[t]
+        wk = WITNESSES[kinds[t]]
+        p1 = None if tex[t] == tid[t] else t
+        per_key = []
+        keys = [int(x) for x in b.key_code[int(b.key_off[t]):int(b.key_off[t + 1])]]
+        for ki, k in enumerate(keys):
+            entries = by_key[k]
+            cw = [tex[d] for d in entries if status[d] in committed and kinds[d] == 1 and tex[d] < S]
+            M = max(cw) if cw else None
+            deps = sorted((d for d in entries
+                           if tid[d] < S and kinds[d] in wk and status[d] not in (0, 7)
+                           and (status[d] not in committed or M is None or tex[d] >= M)
+                           and d != p1), key=lambda d: tid[d])
+            if deps:
+                per_key.append((ki, deps))
+        union = sorted({d for _, ds in per_key for d in ds}, key=lambda d: tid[d])
+        pos = {d: i for i, d in enumerate(union)}
+        k2v = []
+        end = len(per_key)
+        for _, ds in per_key:
+            end += len(ds)
+            k2v.append(end)
+        for _, ds in per_key:
+            k2v.extend(pos[d] for d in ds)
+        out.append(([ki for ki, _ in per_key], union, k2v))
+    return out
+
+
+def to_canonical_map(keys, txnids, k2v):
+    """KeyDeps arrays -> {key: [txnId...]} (the KeyDepsTest canonical TreeMap form)."""
+    m = {}
+    nk = len(keys)
+    start = nk
+    for i, k in enumerate(keys):
+        end = k2v[i]
+        m[k] = [txnids[x] for x in k2v[start:end]]
+        start = end
+    return m
+
+
+def from_canonical_map(m):
+    """{key: set(txn ranks)} -> (keys, txnIds, keysToTxnIds) in Java layout."""
+    keys = sorted(m)
+    vals = sorted({v for vs in m.values() for v in vs})
+    pos = {v: i for i, v in enumerate(vals)}
+    k2v = []
+    end = len(keys)
+    for k in keys:
+        end += len(m[k])
+        k2v.append(end)
+    for k in keys:
+        k2v.extend(pos[v] for v in sorted(m[k]))
+    return keys, vals, k2v
+
+
+def merge_union(replies):
+    """KeyDeps.merge == canonical union of {key: set(txnIds)} (KeyDepsTest.java:275-283); values of the
+    result are the union of every reply's txnIds array (RelationMultiMap.linearUnion :575-576)."""
+    m: dict = {}
+    allvals = set()
+    for keys, vals, k2v in replies:
+        if not keys:
+            continue
+        allvals.update(vals)
+        for k, ts in to_canonical_map(keys, vals, k2v).items():
+            m.setdefault(k, set()).update(ts)
+    keys = sorted(m)
+    vals = sorted(allvals)
+    pos = {v: i for i, v in enumerate(vals)}
+    k2v = []
+    end = len(keys)
+    for k in keys:
+        end += len(m[k])
+        k2v.append(end)
+    for k in keys:
+        k2v.extend(pos[v] for v in sorted(m[k]))
+    return keys, vals, k2v
+
+
+def levelise(off, dep, exec_rank):
+    n = len(exec_rank)
+    order_by_exec = sorted(range(n), key=lambda t: (exec_rank[t], t))
+    level = [0] * n
+    for t in order_by_exec:
+        preds = [int(d) for d in dep[int(off[t]):int(off[t + 1])] if exec_rank[int(d)] < exec_rank[t]]
+        level[t] = 1 + max(level[d] for d in preds) if preds else 0
+    order = sorted(range(n), key=lambda t: (level[t], exec_rank[t], t))
+    return np.array(level, dtype=np.uint32), np.array(order, dtype=np.uint32)

@@ -1,0 +1,169 @@
+"""ctypes binding of the C restatement (oracle/accord_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module. It is the
+checker, never the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+u8p = C.POINTER(C.c_uint8)
+
+
+class KeydepsResult(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32),
+                ("arena_off", u64p), ("arena", i32p),
+                ("kd_off", u64p), ("key_idx", u32p),
+                ("u_off", u64p), ("dep_txn", u32p),
+                ("total_edges", C.c_uint64), ("visited", C.c_uint64),
+                ("error", C.c_int), ("message", C.c_char * 256)]
+
+
+class MergeResult(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32),
+                ("key_off", u64p), ("key_code", u64p),
+                ("val_off", u64p), ("txn_rank", u32p),
+                ("k2v_off", u64p), ("k2v", i32p),
+                ("error", C.c_int), ("message", C.c_char * 256)]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_keydeps_batch.restype = C.POINTER(KeydepsResult)
+        L.orc_keydeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
+                                        C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_keydeps_free.argtypes = [C.POINTER(KeydepsResult)]
+        L.orc_keydeps_merge.restype = C.POINTER(MergeResult)
+        L.orc_keydeps_merge.argtypes = [C.c_uint32, u64p, u64p, u64p, u64p, u32p, u64p, i32p]
+        L.orc_merge_free.argtypes = [C.POINTER(MergeResult)]
+        L.orc_levelise.restype = C.c_int
+        L.orc_levelise.argtypes = [C.c_uint32, u64p, u32p, u32p, u32p, u32p, u32p]
+        L.orc_ts_compare.restype = C.c_int
+        L.orc_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+@dataclass
+class KeyDepsBatchOut:
+    """Per-txn results in the acc_keydeps_view layout (host numpy arrays)."""
+    arena_off: np.ndarray
+    arena: np.ndarray
+    kd_off: np.ndarray
+    key_idx: np.ndarray
+    u_off: np.ndarray
+    dep_txn: np.ndarray
+    total_edges: int = 0
+    visited: int = 0
+
+    def txn(self, t: int):
+        a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
+        k = self.key_idx[self.kd_off[t]:self.kd_off[t + 1]]
+        d = self.dep_txn[self.u_off[t]:self.u_off[t + 1]]
+        return k, d, a
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__(f"oracle error {code}: {message}")
+        self.code = code
+
+
+def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | None = None) -> KeyDepsBatchOut:
+    L = lib()
+    n = batch.n_txn
+    arrs = [np.ascontiguousarray(x) for x in (batch.txn_msb.astype(np.uint64), batch.txn_lsb.astype(np.uint64),
+                                              batch.txn_node.astype(np.int32), batch.exe_msb.astype(np.uint64),
+                                              batch.exe_lsb.astype(np.uint64), batch.exe_node.astype(np.int32),
+                                              batch.status.astype(np.uint8), batch.key_off.astype(np.uint32),
+                                              batch.key_code.astype(np.uint64))]
+    types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p]
+    r = L.orc_keydeps_batch(n, *[_p(a, t) for a, t in zip(arrs, types)], n_shards, query_lo,
+                            n if query_hi is None else query_hi)
+    try:
+        R = r.contents
+        if R.error:
+            raise OracleError(R.error, R.message.decode())
+        arena_off = np.ctypeslib.as_array(R.arena_off, (n + 1,)).copy()
+        kd_off = np.ctypeslib.as_array(R.kd_off, (n + 1,)).copy()
+        u_off = np.ctypeslib.as_array(R.u_off, (n + 1,)).copy()
+        na, nk, nd = int(arena_off[-1]), int(kd_off[-1]), int(u_off[-1])
+        out = KeyDepsBatchOut(arena_off, np.ctypeslib.as_array(R.arena, (max(na, 1),))[:na].copy(), kd_off,
+                              np.ctypeslib.as_array(R.key_idx, (max(nk, 1),))[:nk].copy(), u_off,
+                              np.ctypeslib.as_array(R.dep_txn, (max(nd, 1),))[:nd].copy(),
+                              int(R.total_edges), int(R.visited))
+    finally:
+        L.orc_keydeps_free(r)
+    return out
+
+
+def keydeps_merge(m: dict) -> dict:
+    """KeyDeps.merge per group over the acc_merge_in layout dict (grp_off, key_off, key_code, val_off,
+    txn_rank, k2v_off, k2v). Returns the same-named merged arrays per group."""
+    L = lib()
+    g = len(m["grp_off"]) - 1
+    a = {k: np.ascontiguousarray(v) for k, v in m.items()}
+    r = L.orc_keydeps_merge(g, _p(a["grp_off"], u64p), _p(a["key_off"], u64p), _p(a["key_code"], u64p),
+                            _p(a["val_off"], u64p), _p(a["txn_rank"], u32p), _p(a["k2v_off"], u64p),
+                            _p(a["k2v"], i32p))
+    try:
+        R = r.contents
+        if R.error:
+            raise OracleError(R.error, R.message.decode())
+        ko = np.ctypeslib.as_array(R.key_off, (g + 1,)).copy()
+        vo = np.ctypeslib.as_array(R.val_off, (g + 1,)).copy()
+        oo = np.ctypeslib.as_array(R.k2v_off, (g + 1,)).copy()
+        out = dict(key_off=ko, val_off=vo, k2v_off=oo,
+                   key_code=np.ctypeslib.as_array(R.key_code, (max(int(ko[-1]), 1),))[:int(ko[-1])].copy(),
+                   txn_rank=np.ctypeslib.as_array(R.txn_rank, (max(int(vo[-1]), 1),))[:int(vo[-1])].copy(),
+                   k2v=np.ctypeslib.as_array(R.k2v, (max(int(oo[-1]), 1),))[:int(oo[-1])].copy())
+    finally:
+        L.orc_merge_free(r)
+    return out
+
+
+def levelise(off: np.ndarray, dep: np.ndarray, exec_rank: np.ndarray):
+    L = lib()
+    n = len(exec_rank)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    dep = np.ascontiguousarray(dep, dtype=np.uint32)
+    er = np.ascontiguousarray(exec_rank, dtype=np.uint32)
+    level = np.zeros(n, dtype=np.uint32)
+    order = np.zeros(n, dtype=np.uint32)
+    nl = np.zeros(1, dtype=np.uint32)
+    rc = L.orc_levelise(n, _p(off, u64p), _p(dep, u32p), _p(er, u32p), _p(level, u32p), _p(order, u32p),
+                        _p(nl, u32p))
+    if rc:
+        raise OracleError(rc, "levelise: dep out of range")
+    return level, order, int(nl[0])
+
+
+def ts_compare(a, b) -> int:
+    return lib().orc_ts_compare(*a, *b)
