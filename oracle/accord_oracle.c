@@ -11,6 +11,14 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
 
 /* ------------------------------------------------------------------ Timestamp / TxnId */
 
@@ -458,9 +466,12 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
                                       const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
                                       const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
-                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi)
+                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
+                                      uint32_t query_stride)
 {
     orc_keydeps_result *R = calloc(1, sizeof *R);
+    double t_start = now_s();
+    if (query_stride == 0) query_stride = 1;
     err E = { 0, "" };
     batch B = { n, malloc((n + 1) * sizeof(ts)), malloc((n + 1) * sizeof(ts)), status, key_off, key_code };
     for (uint32_t i = 0; i < n; ++i) {
@@ -510,6 +521,8 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
     uint64_t *shard_lo = malloc((n_shards + 1) * sizeof *shard_lo);
     for (uint32_t s = 0; s < n_shards; ++s) shard_lo[s] = klo + (uint64_t)(span * s / n_shards);
 
+    R->build_s = now_s() - t_start;
+    double t_query = now_s();
     R->n_txn = n;
     R->arena_off = calloc(n + 1, sizeof(uint64_t));
     R->kd_off = calloc(n + 1, sizeof(uint64_t));
@@ -519,7 +532,8 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
 
     for (uint32_t t = 0; t < n && !E.code; ++t) {
         R->arena_off[t] = arena.n; R->kd_off[t] = kidx.n; R->u_off[t] = deps.n;
-        if (t < query_lo || t >= query_hi) continue;
+        if (t < query_lo || t >= query_hi || (t - query_lo) % query_stride) continue;
+        R->queried_pairs += key_off[t + 1] - key_off[t];
         int wk = kind_witnesses(ts_kind(&B.id[t]));
         if (wk < 0) { set_err(&E, -2, "Kind.witnesses(): unhandled kind (AssertionError)"); break; }
         /* p1 = executeAt.equals(txnId) ? null : txnId (PreAccept.java:259) */
@@ -555,6 +569,7 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
         kd_free(&acc);
     }
     R->arena_off[n] = arena.n; R->kd_off[n] = kidx.n; R->u_off[n] = deps.n;
+    R->query_s = now_s() - t_query;
     R->arena = malloc((arena.n + 1) * sizeof(int32_t));
     for (size_t q = 0; q < arena.n; ++q) R->arena[q] = (int32_t)arena.v[q];
     R->key_idx = malloc((kidx.n + 1) * sizeof(uint32_t));

@@ -28,6 +28,9 @@ typedef struct orc_keydeps_result {
     uint64_t *u_off;      uint32_t *dep_txn;
     uint64_t  total_edges;
     uint64_t  visited;    /* entries visited by the O(prefix) scans (work counter) */
+    uint64_t  queried_pairs; /* (txn, key) pairs evaluated as queries */
+    double    build_s;    /* seconds spent building the CommandsForKey snapshot */
+    double    query_s;    /* seconds spent in the per-txn calculatePartialDeps loop */
     int       error;      /* 0 ok, -1 IllegalArgument, -2 IllegalState */
     char      message[256];
 } orc_keydeps_result;
@@ -36,13 +39,14 @@ typedef struct orc_keydeps_result {
  * semantics). n_shards > 1 evaluates it the way CommandStores do: EvenSplit of the key-code domain
  * into contiguous shards, per-shard calculatePartialDeps, then the PreAccept.reduce fold of
  * PartialDeps.with in shard order (PreAccept.java:141-156, CommandStores.java:575-592).
- * query_lo/query_hi restrict which txns are evaluated as queries (all txns stay CFK entries);
- * results for other txns are empty. */
+ * query_lo/query_hi/query_stride restrict which txns are evaluated as queries (t in [lo, hi) with
+ * (t - lo) % stride == 0); all txns stay CFK entries; results for other txns are empty. */
 orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
                                       const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
                                       const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
-                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi);
+                                      uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
+                                      uint32_t query_stride);
 void orc_keydeps_free(orc_keydeps_result *r);
 
 /* KeyDeps.merge (KeyDeps.java:115-135) over groups of replies in the acc_merge_in layout

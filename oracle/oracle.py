@@ -27,6 +27,7 @@ class KeydepsResult(C.Structure):
                 ("kd_off", u64p), ("key_idx", u32p),
                 ("u_off", u64p), ("dep_txn", u32p),
                 ("total_edges", C.c_uint64), ("visited", C.c_uint64),
+                ("queried_pairs", C.c_uint64), ("build_s", C.c_double), ("query_s", C.c_double),
                 ("error", C.c_int), ("message", C.c_char * 256)]
 
 
@@ -54,7 +55,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         L.orc_keydeps_batch.restype = C.POINTER(KeydepsResult)
         L.orc_keydeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
-                                        C.c_uint32, C.c_uint32, C.c_uint32]
+                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_keydeps_free.argtypes = [C.POINTER(KeydepsResult)]
         L.orc_keydeps_merge.restype = C.POINTER(MergeResult)
         L.orc_keydeps_merge.argtypes = [C.c_uint32, u64p, u64p, u64p, u64p, u32p, u64p, i32p]
@@ -82,6 +83,9 @@ class KeyDepsBatchOut:
     dep_txn: np.ndarray
     total_edges: int = 0
     visited: int = 0
+    queried_pairs: int = 0
+    build_s: float = 0.0
+    query_s: float = 0.0
 
     def txn(self, t: int):
         a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
@@ -96,7 +100,8 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | None = None) -> KeyDepsBatchOut:
+def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | None = None,
+                  query_stride: int = 1) -> KeyDepsBatchOut:
     L = lib()
     n = batch.n_txn
     arrs = [np.ascontiguousarray(x) for x in (batch.txn_msb.astype(np.uint64), batch.txn_lsb.astype(np.uint64),
@@ -106,7 +111,7 @@ def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | N
                                               batch.key_code.astype(np.uint64))]
     types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p]
     r = L.orc_keydeps_batch(n, *[_p(a, t) for a, t in zip(arrs, types)], n_shards, query_lo,
-                            n if query_hi is None else query_hi)
+                            n if query_hi is None else query_hi, query_stride)
     try:
         R = r.contents
         if R.error:
@@ -118,7 +123,8 @@ def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | N
         out = KeyDepsBatchOut(arena_off, np.ctypeslib.as_array(R.arena, (max(na, 1),))[:na].copy(), kd_off,
                               np.ctypeslib.as_array(R.key_idx, (max(nk, 1),))[:nk].copy(), u_off,
                               np.ctypeslib.as_array(R.dep_txn, (max(nd, 1),))[:nd].copy(),
-                              int(R.total_edges), int(R.visited))
+                              int(R.total_edges), int(R.visited), int(R.queried_pairs), float(R.build_s),
+                              float(R.query_s))
     finally:
         L.orc_keydeps_free(r)
     return out
