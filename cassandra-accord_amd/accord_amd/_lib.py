@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "libaccord_amd.so")
 ACC_OK, ACC_E_ARG, ACC_E_STATE, ACC_E_NOMEM, ACC_E_DEVICE, ACC_E_CAP = 0, -1, -2, -3, -4, -5
 ACC_MEM_HOST, ACC_MEM_DEVICE = 0, 1
 ACC_OPT_TIMING = 1
+ACC_OPT_FORCE_REPLAY = 2
 
 u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)

@@ -46,10 +46,10 @@ def _ptr(a: np.ndarray):
 class Context:
     """One acc_ctx: a HIP stream plus device scratch (one per host thread / CommandStore)."""
 
-    def __init__(self, device: int = 0, timing: bool = False):
+    def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False):
         self._lib = L.load()
         h = C.c_void_p()
-        opts = L.Opts(L.ACC_OPT_TIMING if timing else 0, 0)
+        opts = L.Opts((L.ACC_OPT_TIMING if timing else 0) | (L.ACC_OPT_FORCE_REPLAY if force_replay else 0), 0)
         rc = self._lib.acc_create(device, C.byref(opts), C.byref(h))
         if rc != L.ACC_OK:
             raise _ERRORS.get(rc, AccordError)(f"acc_create failed ({rc})")

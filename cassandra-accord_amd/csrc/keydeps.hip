@@ -57,12 +57,27 @@ enum : uint32_t {
     ERR_KEY_OFF = 1u << 5,
 };
 
-// g[0..2] ts word masks, g[3] key mask, g[4] error bits, g[5] batch-not-in-TxnId-order flag
-__device__ __forceinline__ void block_or(uint64_t v, uint64_t *dst)
+// g[0..2] ts word masks, g[3] key mask, g[4] error bits, g[5] batch-not-in-TxnId-order flag.
+// Block-level OR (wave shuffles, then LDS across waves) and ONE atomic per block and word: same-address
+// atomics from every wave serialise at the L2 (1.4 ms for 8M pairs in the first build).
+template <int NW>
+__device__ __forceinline__ void block_or_n(uint64_t (&v)[NW], uint64_t *dst)
 {
+    __shared__ uint64_t part[WAVES][NW];
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v |= shfl_idx(v, (int)(lane_id() ^ d));
-    if (lane_id() == 0 && v) atomicOr((unsigned long long *)dst, (unsigned long long)v);
+    for (int w = 0; w < NW; ++w) {
+        uint64_t x = v[w];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x |= shfl_idx(x, (int)(lane_id() ^ d));
+        if (lane_id() == 0) part[threadIdx.x >> 6][w] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < NW) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int q = 0; q < WAVES; ++q) x |= part[q][threadIdx.x];
+        if (x) atomicOr((unsigned long long *)&dst[threadIdx.x], (unsigned long long)x);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, const uint64_t *__restrict__ tm, const uint64_t *__restrict__ tl,
@@ -93,19 +108,19 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, const uint64_t *
             }
         }
     }
-    block_or(m0, &g[0]);
-    block_or(m1, &g[1]);
-    block_or(m2, &g[2]);
-    block_or(errs, &g[4]);
-    block_or(unsorted, &g[5]);
+    uint64_t v[6] = { m0, m1, m2, 0, errs, unsorted };
+    block_or_n<6>(v, g);
 }
 
+// grid-stride: a few hundred blocks, each ORs many codes before its single atomic
 __global__ __launch_bounds__(BLOCK) void k_prep_keys(size_t P, const uint64_t *__restrict__ key_code, uint64_t *__restrict__ g)
 {
-    size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t ref = key_code[0];
     uint64_t m = 0;
-    if (j < P) m = key_code[j] ^ key_code[0];
-    block_or(m, &g[3]);
+    for (size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x; j < P; j += (size_t)gridDim.x * BLOCK)
+        m |= key_code[j] ^ ref;
+    uint64_t v[1] = { m };
+    block_or_n<1>(v, g + 3);
 }
 
 // ---------------------------------------------------------------- dictionary (order ranks)
@@ -178,7 +193,23 @@ __global__ __launch_bounds__(BLOCK) void k_dup_txn(uint32_t n, const uint32_t *_
     if (t < n) {
         if (atomicAdd(&seen[rank[t]], 1u) != 0) err = ERR_DUP_TXNID;
     }
-    block_or(err, &g[4]);
+    uint64_t v[1] = { err };
+    block_or_n<1>(v, g + 4);
+}
+
+// g[6] != 0: some executeAt compares equal to another txn's TxnId or executeAt. Only then can two
+// committed entries of one key tie on executeAt, where the FAST bisection's pick (CommandsForKey.java:619)
+// is order-dependent; such batches take the exact replay path (v1).
+__global__ __launch_bounds__(BLOCK) void k_exec_ties(uint32_t n, const uint32_t *__restrict__ rank, uint32_t *__restrict__ seen,
+                                                     uint64_t *__restrict__ g)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t tie = 0;
+    if (t < n && rank[n + t] != rank[t]) {
+        if (atomicAdd(&seen[rank[n + t]], 1u) != 0) tie = 1;
+    }
+    uint64_t v[1] = { tie };
+    block_or_n<1>(v, g + 6);
 }
 
 // ---------------------------------------------------------------- CFK build
@@ -517,6 +548,562 @@ __global__ __launch_bounds__(BLOCK) void k_write_keys(size_t P, const uint64_t *
     arena[arena_off[t] + slot] = (int32_t)(kd + (dep_off[j + 1] - dep_off[j0]));
 }
 
+// ---------------------------------------------------------------- v2: run-based conflict scan
+//
+// Without executeAt ties (k_exec_ties), the reference scan of (T, k) equals the union of three kinds of
+// sorted runs over the CFK segment (positions [s0, s1) in TxnId order), with S = T.executeAt,
+// pos = insertPos(S), M = maxCommittedBefore and posM = first position with TxnId >= M:
+//   R1[c]: uncommitted (HISTORICAL/PREACCEPTED/ACCEPTED) entries of kind class c in [s0, pos)
+//   R2[c]: committed entries of kind class c in [posM, pos)   (TxnId >= M  =>  executeAt >= M)
+//   R3   : committed entries before posM with executeAt >= M  (only "bumped" ones, executeAt != TxnId)
+// for every class c witnessed by T.kind, minus T itself (p1). Runs are ranges of per-class position
+// lists, so counts are O(1) prefix differences. M = max(last unbumped committed Write before pos
+// [segmented prefix max], predecessor of S among bumped committed Writes [small sorted list]).
+
+constexpr int NLIST = 6;   // U_R, U_W, U_S, C_R, C_W, C_S
+constexpr int NCNT = 8;    // 6 list counts, bumped-committed count, last-unbumped-committed-write max
+
+// Kind class for the Kinds predicates (Txn.java:140-152): Read 0, Write 1, SyncPoint/ExclusiveSyncPoint 2;
+// EphemeralRead and LocalOnly are witnessed by no predicate (3 = none).
+__device__ __forceinline__ uint32_t kind_class(uint32_t kind)
+{
+    return kind == 0 ? 0u : kind == 1 ? 1u : (kind == 3 || kind == 4) ? 2u : 3u;
+}
+// witness mask over kinds -> mask over classes
+__device__ __forceinline__ uint32_t wk_classes(uint32_t wk)
+{
+    return (wk & 1u) | (((wk >> 1) & 1u) << 1) | (((wk >> 3) & 1u) << 2);
+}
+
+// per-position code: bits 0-2 list id (7 = none), bit 3 bumped committed (class < 3), bit 4 unbumped committed Write
+__device__ __forceinline__ uint32_t v2_code(uint32_t rank, uint32_t exec, uint32_t info)
+{
+    uint32_t st = info & 7u, kind = info >> 3, cls = kind_class(kind);
+    bool u = st >= 1 && st <= 3, c = st >= 4 && st <= 6;
+    uint32_t list = cls < 3 ? (u ? cls : c ? 3 + cls : 7u) : 7u;
+    uint32_t bc = (c && cls < 3 && exec != rank) ? 1u : 0u;
+    uint32_t ucw = (c && kind == 1 && exec == rank) ? 1u : 0u;
+    return list | (bc << 3) | (ucw << 4);
+}
+
+constexpr int V2_ITEMS = 8;
+constexpr int V2_TILE = BLOCK * V2_ITEMS;
+
+__global__ __launch_bounds__(BLOCK) void k_v2_reduce(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
+                                                     const uint8_t *__restrict__ s_info, uint32_t *__restrict__ tile_sums,
+                                                     uint32_t ntiles)
+{
+    __shared__ uint32_t lds[WAVES];
+    const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
+    uint32_t c[NCNT] = {};
+#pragma unroll
+    for (int i = 0; i < V2_ITEMS; ++i) {
+        size_t p = base + i;
+        if (p >= P) break;
+        uint32_t code = v2_code(s_rank[p], s_exec[p], s_info[p]);
+        uint32_t l = code & 7u;
+#pragma unroll
+        for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
+        c[6] += (code >> 3) & 1u;
+        if ((code >> 4) & 1u) c[7] = (uint32_t)p + 1;
+    }
+#pragma unroll
+    for (int q = 0; q < NCNT; ++q) {
+        uint32_t total;
+        if (q < 7) block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
+        else block_exclusive(c[q], OpMax<uint32_t>(), lds, total);
+        if (threadIdx.x == 0) tile_sums[(size_t)q * ntiles + blockIdx.x] = total;
+    }
+}
+
+// list bases: list l occupies [base[l], base[l] + total[l]) of the class-list arrays
+__global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__restrict__ bases)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        uint32_t b = 0;
+        for (int l = 0; l < NLIST; ++l) { bases[l] = b; b += totals[l]; }
+        bases[NLIST] = b;
+    }
+}
+
+struct V2Cols {
+    uint32_t *cnt;        // [NLIST][P+1] exclusive prefix counts per list
+    uint32_t *cbc;        // [P+1] exclusive prefix count of bumped committed
+    uint32_t *lucw;       // [P+1] exclusive prefix max of (pos+1) of unbumped committed Writes
+    uint32_t *list_rank;  // class lists (TxnId ranks), list l at bases[l]
+    uint32_t *bc_rank, *bc_exec;  // bumped committed, position order
+    uint8_t *bc_kind;
+    uint64_t *bc_pm_in;   // (seg << 32) | exec+1, for the segmented prefix max
+    uint64_t *bc_key;     // (seg << rbits) | exec, for the (seg, executeAt) sort
+};
+
+__global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
+                                                    const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ seg_incl,
+                                                    const uint32_t *__restrict__ tile_pref, const uint32_t *__restrict__ bases,
+                                                    uint32_t ntiles, int rbits, V2Cols o)
+{
+    __shared__ uint32_t lds[WAVES];
+    const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
+    uint32_t code[V2_ITEMS];
+    uint32_t c[NCNT] = {};
+#pragma unroll
+    for (int i = 0; i < V2_ITEMS; ++i) {
+        size_t p = base + i;
+        code[i] = p < P ? v2_code(s_rank[p], s_exec[p], s_info[p]) : 7u;
+        uint32_t l = code[i] & 7u;
+#pragma unroll
+        for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
+        c[6] += (code[i] >> 3) & 1u;
+        if ((code[i] >> 4) & 1u) c[7] = (uint32_t)p + 1;
+    }
+    uint32_t run[NCNT];
+#pragma unroll
+    for (int q = 0; q < NCNT; ++q) {
+        uint32_t total;
+        uint32_t pre = tile_pref[(size_t)q * ntiles + blockIdx.x];
+        if (q < 7) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
+        else { uint32_t e = block_exclusive(c[q], OpMax<uint32_t>(), lds, total); run[q] = e > pre ? e : pre; }
+    }
+    uint32_t lb[NLIST];
+#pragma unroll
+    for (int l = 0; l < NLIST; ++l) lb[l] = bases[l];
+#pragma unroll
+    for (int i = 0; i < V2_ITEMS; ++i) {
+        size_t p = base + i;
+        if (p >= P) break;
+#pragma unroll
+        for (int q = 0; q < NLIST; ++q) o.cnt[(size_t)q * (P + 1) + p] = run[q];
+        o.cbc[p] = run[6];
+        o.lucw[p] = run[7];
+        uint32_t l = code[i] & 7u;
+        uint32_t r = s_rank[p];
+        if (l < NLIST) {
+            uint32_t idx = 0;
+#pragma unroll
+            for (int q = 0; q < NLIST; ++q) if ((uint32_t)q == l) idx = lb[q] + run[q];
+            o.list_rank[idx] = r;
+#pragma unroll
+            for (int q = 0; q < NLIST; ++q) run[q] += (uint32_t)q == l;
+        }
+        if ((code[i] >> 3) & 1u) {
+            uint32_t b = run[6]++;
+            uint32_t seg = seg_incl[p] - 1, e = s_exec[p];
+            o.bc_rank[b] = r;
+            o.bc_exec[b] = e;
+            o.bc_kind[b] = (uint8_t)(s_info[p] >> 3);
+            o.bc_pm_in[b] = ((uint64_t)seg << 32) | ((uint64_t)e + 1);
+            o.bc_key[b] = ((uint64_t)seg << rbits) | e;
+        }
+        if ((code[i] >> 4) & 1u) run[7] = (uint32_t)p + 1;
+        if (p == P - 1) {
+#pragma unroll
+            for (int q = 0; q < NLIST; ++q) o.cnt[(size_t)q * (P + 1) + P] = run[q];
+            o.cbc[P] = run[6];
+            o.lucw[P] = run[7];
+        }
+    }
+}
+
+// bumped committed sorted by (segment, executeAt): exec column and nearest-Write index (+1) per entry
+__global__ __launch_bounds__(BLOCK) void k_v2_bcs_cols(uint32_t nbc, const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ svals,
+                                                       const uint8_t *__restrict__ bc_kind, uint64_t rmask,
+                                                       uint32_t *__restrict__ bcs_exec, uint32_t *__restrict__ lastw_in)
+{
+    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nbc) return;
+    bcs_exec[i] = (uint32_t)(skeys[i] & rmask);
+    lastw_in[i] = bc_kind[svals[i]] == 1 ? i + 1 : 0;
+}
+
+struct V2View {
+    const uint32_t *owner, *rank, *pair_pos, *seg_incl, *seg_start, *s_rank;
+    const uint64_t *tl;
+    const uint8_t *status;
+    const uint32_t *cnt, *cbc, *lucw, *list_rank, *bases;
+    const uint32_t *bc_rank, *bc_exec, *bc_pm;
+    const uint8_t *bc_kind;
+    const uint32_t *bcs_exec, *bcs_lastw;
+    uint32_t n;
+    uint64_t P1;  // P + 1 (row stride of cnt)
+};
+
+struct V2Query {
+    uint32_t t, trank, wk, wc, s0, pos, posm, m, b0, bstart, bend;
+    bool bq, has_m;
+};
+
+__device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t j)
+{
+    V2Query q;
+    q.t = v.owner[j];
+    uint32_t p = v.pair_pos[j];
+    uint32_t seg = v.seg_incl[p] - 1;
+    q.s0 = v.seg_start[seg];
+    uint32_t s1 = v.seg_start[seg + 1];
+    q.trank = v.rank[q.t];
+    uint32_t S = v.rank[v.n + q.t];
+    q.wk = witnesses((uint32_t)(v.tl[q.t] >> 1) & 7u);
+    q.wc = wk_classes(q.wk);
+    q.bq = S != q.trank;
+    q.pos = q.bq ? lower_bound_u32(v.s_rank, p + 1, s1, S) : p;
+    // M from the last unbumped committed Write before pos
+    uint32_t lu = v.lucw[q.pos];
+    bool has_mu = lu > q.s0;
+    uint32_t mu = has_mu ? v.s_rank[lu - 1] : 0;
+    // M from bumped committed Writes of this segment: predecessor of S by executeAt, then nearest Write
+    q.b0 = v.cbc[q.s0];
+    uint32_t b1 = v.cbc[s1];
+    bool has_mb = false;
+    uint32_t mb = 0;
+    if (b1 > q.b0) {
+        uint32_t i = lower_bound_u32(v.bcs_exec, q.b0, b1, S);
+        if (i > q.b0) {
+            uint32_t w = v.bcs_lastw[i - 1];
+            if (w > q.b0) { has_mb = true; mb = v.bcs_exec[w - 1]; }
+        }
+    }
+    q.has_m = has_mu || has_mb;
+    q.m = (has_mb && (!has_mu || mb > mu)) ? mb : mu;
+    if (!q.has_m) q.posm = q.s0;
+    else if (has_mu && q.m == mu) q.posm = lu - 1;
+    else q.posm = lower_bound_u32(v.s_rank, q.s0, q.pos, q.m);
+    q.bend = v.cbc[q.posm];
+    q.bstart = q.has_m ? lower_bound_u32(v.bc_pm, q.b0, q.bend, q.m + 1) : q.bend;
+    return q;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out)
+{
+    size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= P) return;
+    V2Query q = v2_query(v, (uint32_t)j);
+    uint64_t e = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        if (!((q.wc >> c) & 1u)) continue;
+        const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
+        e += cu[q.pos] - cu[q.s0];
+        e += cc[q.pos] - cc[q.posm];
+    }
+    for (uint32_t i = q.bstart; i < q.bend; ++i)
+        if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) ++e;
+    if (q.bq) {
+        uint32_t st = v.status[q.t], kind = (uint32_t)(v.tl[q.t] >> 1) & 7u;
+        if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
+    }
+    cnt_out[j] = e;
+}
+
+// ---- write pass: one wave per txn gathers its runs into LDS, sorts (value, key) and emits the Java layout
+
+constexpr int WCAP = 1024;          // entries per wave in LDS
+constexpr int WMAXK = 64;           // keys per txn on the wave path
+constexpr int WPB = WAVES;          // waves (txns) per block
+
+// Append run [a, b) of `src` (values) to the wave buffer, dropping `skip` (T itself) when drop is set.
+__device__ __forceinline__ uint32_t wave_append(uint64_t *buf, uint32_t cursor, const uint32_t *src, uint32_t a, uint32_t b,
+                                                bool drop, uint32_t skip, uint32_t kj)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c = a; c < b; c += 64) {
+        uint32_t i = c + lane;
+        bool in = i < b;
+        uint32_t x = in ? src[i] : 0;
+        bool keep = in && !(drop && x == skip);
+        uint64_t bal = __ballot(keep);
+        if (keep) {
+            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+            if (slot < WCAP) buf[slot] = ((uint64_t)x << 16) | kj;
+        }
+        cursor += (uint32_t)__popcll(bal);
+    }
+    return cursor;
+}
+
+__device__ __forceinline__ uint32_t wave_append_r3(uint64_t *buf, uint32_t cursor, const V2View &v, const V2Query &q, uint32_t kj)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c = q.bstart; c < q.bend; c += 64) {
+        uint32_t i = c + lane;
+        bool keep = false;
+        uint32_t x = 0;
+        if (i < q.bend) {
+            x = v.bc_rank[i];
+            keep = v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u) && !(q.bq && x == q.trank);
+        }
+        uint64_t bal = __ballot(keep);
+        if (keep) {
+            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+            if (slot < WCAP) buf[slot] = ((uint64_t)x << 16) | kj;
+        }
+        cursor += (uint32_t)__popcll(bal);
+    }
+    return cursor;
+}
+
+// Gather all runs of txn t (keys j0..j1) into buf; returns the entry count.
+__device__ uint32_t gather_txn(uint64_t *buf, const V2View &v, uint32_t j0, uint32_t j1, const uint64_t *cnt)
+{
+    uint32_t cursor = 0;
+    for (uint32_t j = j0; j < j1; ++j) {
+        if (cnt[j] == 0) continue;
+        V2Query q = v2_query(v, j);
+        uint32_t kj = j - j0;
+        for (int c = 0; c < 3; ++c) {
+            if (!((q.wc >> c) & 1u)) continue;
+            const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
+            cursor = wave_append(buf, cursor, v.list_rank + v.bases[c], cu[q.s0], cu[q.pos], q.bq, q.trank, kj);
+            cursor = wave_append(buf, cursor, v.list_rank + v.bases[3 + c], cc[q.posm], cc[q.pos], q.bq, q.trank, kj);
+        }
+        if (q.has_m) cursor = wave_append_r3(buf, cursor, v, q, kj);
+    }
+    return cursor;
+}
+
+// in-LDS bitonic sort of n2 (power of two) u64 entries by one wave
+__device__ __forceinline__ void wave_bitonic(uint64_t *buf, uint32_t n2)
+{
+    const uint32_t lane = lane_id();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = lane; i < n2; i += 64) {
+                uint32_t l = i ^ jj;
+                if (l > i) {
+                    uint64_t a = buf[i], b = buf[l];
+                    bool up = (i & k) == 0;
+                    if ((a > b) == up) { buf[i] = b; buf[l] = a; }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
+}
+
+struct V2Out {
+    const uint32_t *key_off;
+    const uint64_t *dep_off, *arena_off;
+    const uint32_t *cnz, *txn_of_rank;
+    int32_t *arena;
+    uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
+    uint64_t *u_cnt;
+    uint32_t *big;           // 1 = txn left for the global path
+    uint64_t *gstat;         // [0] big txns, [1] their entries, [2] internal count mismatches
+};
+
+__global__ __launch_bounds__(BLOCK) void k_v2_write(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ uint64_t sbuf[WPB][WCAP];
+    __shared__ uint32_t skey[WPB][WMAXK];
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t t = blockIdx.x * WPB + wave;
+    if (t >= n) return;
+    uint64_t *buf = sbuf[wave];
+    uint32_t *kc = skey[wave];
+    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
+    const uint64_t e0 = o.dep_off[j0];
+    const uint32_t E = (uint32_t)(o.dep_off[j1] - e0);
+    if (E == 0) { if (lane == 0) { o.u_cnt[t] = 0; o.big[t] = 0; } return; }
+    if (E > WCAP || j1 - j0 > WMAXK) {
+        if (lane == 0) {
+            o.big[t] = 1;
+            atomicAdd((unsigned long long *)&o.gstat[0], 1ull);
+            atomicAdd((unsigned long long *)&o.gstat[1], (unsigned long long)E);
+        }
+        return;
+    }
+    uint32_t got = gather_txn(buf, v, j0, j1, cnt);
+    if (got != E) {   // count and gather disagree: internal invariant violation (reported as ACC_E_STATE)
+        if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
+        return;
+    }
+    uint32_t n2 = 64;
+    while (n2 < E) n2 <<= 1;
+    for (uint32_t i = E + lane; i < n2; i += 64) buf[i] = ~0ull;
+    for (uint32_t i = lane; i < WMAXK; i += 64) kc[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    wave_bitonic(buf, n2);
+    const uint32_t kd = o.cnz[j1] - o.cnz[j0];
+    const uint64_t abase = o.arena_off[t] + kd;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t distinct = 0;
+    for (uint32_t c = 0; c < E; c += 64) {
+        uint32_t i = c + lane;
+        bool in = i < E;
+        uint64_t x = in ? buf[i] : 0;
+        uint32_t val = (uint32_t)(x >> 16), kj = (uint32_t)(x & 0xFFFFu);
+        bool nw = in && (i == 0 || (uint32_t)(buf[i - 1] >> 16) != val);
+        uint64_t bal = __ballot(nw);
+        uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+        distinct += (uint32_t)__popcll(bal);
+        // slot of this entry within its key's list: earlier lanes of this chunk with the same key
+        uint64_t peers = __ballot(in);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            uint64_t bb = __ballot((kj >> b) & 1u);
+            peers &= ((kj >> b) & 1u) ? bb : ~bb;
+        }
+        uint32_t before = (uint32_t)__popcll(peers & lt);
+        if (in) {
+            uint32_t slot = kc[kj] + before;
+            uint64_t kbase = o.dep_off[j0 + kj] - e0;
+            o.arena[abase + kbase + slot] = (int32_t)idx;
+            if (nw) o.dep_scratch[e0 + idx] = o.txn_of_rank[val];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (in && before == 0) kc[kj] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+    if (lane == 0) { o.u_cnt[t] = distinct; o.big[t] = 0; }
+}
+
+// ---- global path for txns beyond the wave path: gather to global, two radix sorts
+
+__global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const uint32_t *__restrict__ big_list,
+                                                         const uint64_t *__restrict__ big_off, V2View v,
+                                                         const uint64_t *__restrict__ cnt, const uint32_t *__restrict__ key_off,
+                                                         int rbits, uint64_t *__restrict__ gkey)
+{
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x * WPB + wave;
+    if (b >= nbig) return;
+    const uint32_t t = big_list[b];
+    uint64_t *out = gkey + big_off[b];
+    // reuse the wave appenders with an unbounded global buffer: WCAP guard off via a large cursor window
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t tb = (uint64_t)b << (rbits + 16);
+    uint32_t cursor = 0;
+    const uint32_t j0 = key_off[t], j1 = key_off[t + 1];
+    for (uint32_t j = j0; j < j1; ++j) {
+        if (cnt[j] == 0) continue;
+        V2Query q = v2_query(v, j);
+        uint32_t kj = j - j0;
+        for (int r = 0; r < 7; ++r) {
+            const uint32_t *src;
+            uint32_t a, e;
+            bool r3 = r == 6;
+            if (r3) {
+                if (!q.has_m) continue;
+                a = q.bstart; e = q.bend; src = v.bc_rank;
+            } else {
+                int c = r >> 1;
+                if (!((q.wc >> c) & 1u)) continue;
+                const uint32_t *cl = v.cnt + (size_t)((r & 1) ? 3 + c : c) * v.P1;
+                a = (r & 1) ? cl[q.posm] : cl[q.s0];
+                e = cl[q.pos];
+                src = v.list_rank + v.bases[(r & 1) ? 3 + c : c];
+            }
+            for (uint32_t c = a; c < e; c += 64) {
+                uint32_t i = c + lane;
+                bool keep = false;
+                uint32_t x = 0;
+                if (i < e) {
+                    x = src[i];
+                    keep = !(q.bq && x == q.trank);
+                    if (r3) keep = keep && v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u);
+                }
+                uint64_t bal = __ballot(keep);
+                if (keep) out[cursor + (uint32_t)__popcll(bal & lt)] = tb | ((uint64_t)x << 16) | kj;
+                cursor += (uint32_t)__popcll(bal);
+            }
+        }
+    }
+}
+
+// sorted by (txn, value, key): dense rank of value within txn; TxnId array for first occurrences
+__global__ __launch_bounds__(BLOCK) void k_v2_big_newflag(uint64_t m, const uint64_t *__restrict__ skey, int rbits,
+                                                          uint32_t *__restrict__ flag)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    flag[i] = i == 0 || (skey[i] >> 16) != (skey[i - 1] >> 16);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_big_rank(uint64_t m, const uint64_t *__restrict__ skey, const uint32_t *__restrict__ incl,
+                                                       const uint32_t *__restrict__ big_list, const uint64_t *__restrict__ big_off,
+                                                       int rbits, const uint32_t *__restrict__ key_off,
+                                                       const uint64_t *__restrict__ dep_off, const uint32_t *__restrict__ txn_of_rank,
+                                                       uint32_t *__restrict__ dep_scratch, uint64_t *__restrict__ u_cnt,
+                                                       uint32_t *__restrict__ idx_by_pos1, uint64_t *__restrict__ key2)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    uint64_t x = skey[i];
+    uint32_t b = (uint32_t)(x >> (rbits + 16));
+    uint32_t val = (uint32_t)((x >> 16) & ((1ull << rbits) - 1));
+    uint32_t kj = (uint32_t)(x & 0xFFFFu);
+    uint64_t start = big_off[b];
+    uint32_t base_incl = start == 0 ? 0 : incl[start - 1];
+    uint32_t idx = incl[i] - base_incl - 1;
+    uint32_t t = big_list[b];
+    bool nw = i == start || (skey[i] >> 16) != (skey[i - 1] >> 16);
+    if (nw) dep_scratch[dep_off[key_off[t]] + idx] = txn_of_rank[val];
+    if (i + 1 == big_off[b + 1]) u_cnt[t] = idx + 1;
+    idx_by_pos1[i] = idx;
+    // arena order of the txn: (key, value); value of the second sort = this position
+    key2[i] = ((uint64_t)b << (16 + rbits)) | ((uint64_t)kj << rbits) | val;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_big_arena(uint64_t m, const uint32_t *__restrict__ sval2, const uint64_t *__restrict__ skey2,
+                                                        const uint32_t *__restrict__ idx_by_pos1, const uint32_t *__restrict__ big_list,
+                                                        const uint64_t *__restrict__ big_off, int rbits,
+                                                        const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ cnz,
+                                                        const uint64_t *__restrict__ arena_off, int32_t *__restrict__ arena)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    uint32_t b = (uint32_t)(skey2[i] >> (16 + rbits));
+    uint32_t t = big_list[b];
+    uint32_t kd = cnz[key_off[t + 1]] - cnz[key_off[t]];
+    arena[arena_off[t] + kd + (i - big_off[b])] = (int32_t)idx_by_pos1[sval2[i]];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_big_list(uint32_t n, const uint32_t *__restrict__ big, const uint32_t *__restrict__ big_idx,
+                                                       const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                       uint32_t *__restrict__ big_list, uint64_t *__restrict__ big_e)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n || !big[t]) return;
+    uint32_t b = big_idx[t];
+    big_list[b] = t;
+    big_e[b] = dep_off[key_off[t + 1]] - dep_off[key_off[t]];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                    const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
+                                                    uint64_t *__restrict__ a_cnt)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    uint32_t j0 = key_off[t], j1 = key_off[t + 1];
+    uint64_t kd = cnz[j1] - cnz[j0];
+    kd_cnt[t] = kd;
+    a_cnt[t] = kd + (dep_off[j1] - dep_off[j0]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_u32_from_u64(size_t n, const uint64_t *__restrict__ in, uint32_t *__restrict__ out)
+{
+    size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)in[i];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_compact(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                      const uint64_t *__restrict__ u_off, const uint32_t *__restrict__ dep_scratch,
+                                                      uint32_t *__restrict__ dep_txn)
+{
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t t = blockIdx.x * WPB + wave;
+    if (t >= n) return;
+    uint64_t src = dep_off[key_off[t]];
+    uint64_t dst = u_off[t], len = u_off[t + 1] - dst;
+    for (uint64_t i = lane; i < len; i += 64) dep_txn[dst + i] = dep_scratch[src + i];
+}
+
 // ---------------------------------------------------------------- host orchestration
 
 static void check_errors(uint64_t errs)
@@ -529,161 +1116,18 @@ static void check_errors(uint64_t errs)
     if (errs & ERR_LOCAL_ONLY) fail(ACC_E_STATE, "Kind.witnesses(): unhandled kind LocalOnly (AssertionError)");
 }
 
-void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+// Exact replay path (v1): committed[] per segment sorted by (executeAt, txn order) and the reference's
+// FAST bisection per query; per-(T,k) lists emitted in order, then the per-T union by binary search.
+// Used when executeAt ties exist (or ACC_OPT_FORCE_REPLAY).
+static void keydeps_v1_tail(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view, uint32_t n, size_t P, int rbits,
+                            const uint8_t *status, const uint64_t *tl, const uint32_t *key_off, const uint32_t *owner,
+                            const uint32_t *rank, const uint32_t *txn_of_rank, uint64_t *g, const uint32_t *seg_incl,
+                            const uint32_t *seg_start, const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info,
+                            const uint32_t *pair_pos, const uint32_t *cflag, const uint32_t *uflag, const uint64_t *pmax_in)
 {
-    if (!in || !view) fail(ACC_E_ARG, "null argument");
-    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
-    const uint32_t n = in->n_txn;
-    const size_t P = (size_t)in->n_pairs;
-    if (P >= 0xFFFFFFFFull) fail(ACC_E_ARG, "n_pairs must be < 2^32");
+    (void)in;
     hipStream_t st = ctx->stream;
-    ctx->kd_valid = false;
-
-    // ---- stage inputs
-    const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
-    if (n == 0 || P == 0) {
-        // no pairs: every txn has KeyDeps.NONE
-        uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
-        uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
-        uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
-        ACC_HIP(hipMemsetAsync(arena_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(kd_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(u_off, 0, ((size_t)n + 1) * 8, st));
-        *view = acc_keydeps_view{ n, 0, 0, 0, 0, arena_off, ctx->get<int32_t>("arena", 1), kd_off,
-                                  ctx->get<uint32_t>("key_idx", 1), u_off, ctx->get<uint32_t>("dep_txn", 1) };
-        ctx->kd_view = *view;
-        ctx->kd_valid = true;
-        ctx->sync();
-        return;
-    }
-    const uint64_t *tm = stage_in(ctx, "in_tm", in->txn_id.msb, n, in->mem);
-    const uint64_t *tl = stage_in(ctx, "in_tl", in->txn_id.lsb, n, in->mem);
-    const int32_t *tn = stage_in(ctx, "in_tn", in->txn_id.node, n, in->mem);
-    const uint64_t *em = stage_in(ctx, "in_em", in->execute_at.msb, n, in->mem);
-    const uint64_t *el = stage_in(ctx, "in_el", in->execute_at.lsb, n, in->mem);
-    const int32_t *en = stage_in(ctx, "in_en", in->execute_at.node, n, in->mem);
-    const uint8_t *status = stage_in(ctx, "in_status", in->status, n, in->mem);
-    const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
-
-    // ---- 1. prep
-    uint64_t *g = ctx->get<uint64_t>("g", 8);
-    uint32_t *owner = ctx->get<uint32_t>("owner", P);
-    ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
-    launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, status,
-           key_off, key_code, owner, g);
-    launch(ctx, "prep_keys", k_prep_keys, dim3(grid_for(P, BLOCK)), dim3(BLOCK), 0, P, key_code, g);
-    // the last key_off entry must equal P
-    {
-        uint32_t last = 0;
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
-        if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
-    }
-    uint64_t hg[8];
-    memcpy(hg, ctx->pinned, sizeof hg);
-    check_errors(hg[4]);
-    const bool batch_sorted = hg[5] == 0;
-
-    // ---- 2. dictionary: order ranks over 2N timestamps
-    TsPlan plan;
-    plan.r0 = make_runs(hg[0]); plan.r1 = make_runs(hg[1]); plan.r2 = make_runs(hg[2]);
-    plan.b0 = plan.r0.bits; plan.b1 = plan.r1.bits; plan.b2 = plan.r2.bits;
-    const size_t m = 2 * (size_t)n;
-    uint32_t *rank = ctx->get<uint32_t>("rank", m);
-    uint32_t *flag = ctx->get<uint32_t>("rank_flag", m);
-    uint32_t *incl = ctx->get<uint32_t>("rank_incl", m);
-    const unsigned gm = grid_for(m, BLOCK);
-    Sorted ts_sorted;
-    if (plan.b0 + plan.b1 + plan.b2 <= 64) {
-        uint64_t *ck = ctx->get<uint64_t>("ts_ckey", m);
-        launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, -1,
-               (const uint32_t *)nullptr, ck);
-        ts_sorted = radix_sort(ctx, "rs_ts", ck, nullptr, m, plan.b0 + plan.b1 + plan.b2);
-        launch(ctx, "rank_flags", k_rank_flags, dim3(gm), dim3(BLOCK), 0, m, (const uint32_t *)ts_sorted.vals,
-               (const uint64_t *)nullptr, (const uint64_t *)nullptr, (const uint64_t *)nullptr,
-               (const uint64_t *)ts_sorted.keys, flag);
-    } else {
-        // multi-word LSD: node word, then lsb word, then msb word (each only over its varying bits)
-        uint64_t *c[3] = { ctx->get<uint64_t>("ts_c0", m), ctx->get<uint64_t>("ts_c1", m), ctx->get<uint64_t>("ts_c2", m) };
-        for (int w = 0; w < 3; ++w)
-            launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, w,
-                   (const uint32_t *)nullptr, c[w]);
-        uint64_t *tmpk = ctx->get<uint64_t>("ts_tmpk", m);
-        uint32_t *permb = ctx->get<uint32_t>("ts_perm", m);
-        const uint32_t *perm = nullptr;
-        const int wbits[3] = { plan.b0, plan.b1, plan.b2 };
-        for (int w = 2; w >= 0; --w) {
-            const uint64_t *keys = c[w];
-            if (perm) {
-                launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, w,
-                       perm, tmpk);
-                keys = tmpk;
-            }
-            Sorted s = radix_sort(ctx, "rs_ts", keys, perm, m, wbits[w]);
-            ACC_HIP(hipMemcpyAsync(permb, s.vals, m * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-            perm = permb;
-        }
-        ts_sorted = { nullptr, permb };
-        launch(ctx, "rank_flags", k_rank_flags, dim3(gm), dim3(BLOCK), 0, m, (const uint32_t *)permb,
-               (const uint64_t *)c[0], (const uint64_t *)c[1], (const uint64_t *)c[2], (const uint64_t *)nullptr, flag);
-    }
-    scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, incl, m, false);
-    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
-    launch(ctx, "rank_scatter", k_rank_scatter, dim3(gm), dim3(BLOCK), 0, m, n, (const uint32_t *)ts_sorted.vals,
-           (const uint32_t *)incl, rank, txn_of_rank);
-    {
-        uint32_t *seen = ctx->get<uint32_t>("dup_seen", m);
-        ACC_HIP(hipMemsetAsync(seen, 0, m * sizeof(uint32_t), st));
-        launch(ctx, "dup_txn", k_dup_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
-    }
-    const int rbits = bits_for(m - 1);
-
-    // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
-    PairPlan pp;
-    pp.rk = make_runs(hg[3]);
-    pp.rbits = rbits;
-    uint64_t *pkey = ctx->get<uint64_t>("pair_key", P);
     const unsigned gP = grid_for(P, BLOCK);
-    Sorted ps;
-    int key_shift = 0;
-    if (batch_sorted) {
-        pp.mode = 0;   // pair index order is already TxnId order within every key: stable sort by key
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
-        ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits);
-    } else if (pp.rk.bits + rbits <= 64) {
-        pp.mode = 1;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
-        ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits + rbits);
-        key_shift = rbits;
-    } else {
-        pp.mode = 2;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 1, pkey);
-        Sorted byrank = radix_sort(ctx, "rs_pair_r", pkey, nullptr, P, rbits);
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
-               (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey);
-        ps = radix_sort(ctx, "rs_pair", pkey, byrank.vals, P, pp.rk.bits);
-    }
-    uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
-    uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P);
-    launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
-    scan<uint32_t, OpAdd<uint32_t>>(ctx, seg_flag, seg_incl, P, false);
-
-    uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
-    uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P);
-    uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P);
-    uint8_t *s_info = ctx->get<uint8_t>("s_info", P);
-    uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
-    uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
-    uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
-    uint64_t *pmax_in = ctx->get<uint64_t>("pmax_in", P);
-    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, n, (const uint32_t *)ps.vals,
-           (const uint32_t *)owner, (const uint32_t *)rank, status, tl, (const uint32_t *)seg_incl,
-           (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
     uint32_t *cum_c = ctx->get<uint32_t>("cum_c", P + 1);
     uint32_t *cum_u = ctx->get<uint32_t>("cum_u", P + 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, cflag, cum_c, P, true, cum_c + P);
@@ -767,6 +1211,308 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
            key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
            (const uint64_t *)arena_off, key_idx, arena);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    *view = acc_keydeps_view{ n, ctx->pinned[0], ctx->pinned[1], ctx->pinned[2], E, arena_off, arena, kd_off,
+                              key_idx, u_off, dep_txn };
+    ctx->kd_view = *view;
+    ctx->kd_valid = true;
+}
+
+void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+{
+    if (!in || !view) fail(ACC_E_ARG, "null argument");
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    const uint32_t n = in->n_txn;
+    const size_t P = (size_t)in->n_pairs;
+    if (P >= 0xFFFFFFFFull) fail(ACC_E_ARG, "n_pairs must be < 2^32");
+    hipStream_t st = ctx->stream;
+    ctx->kd_valid = false;
+
+    // ---- stage inputs
+    const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
+    if (n == 0 || P == 0) {
+        // no pairs: every txn has KeyDeps.NONE
+        uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
+        uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
+        uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
+        ACC_HIP(hipMemsetAsync(arena_off, 0, ((size_t)n + 1) * 8, st));
+        ACC_HIP(hipMemsetAsync(kd_off, 0, ((size_t)n + 1) * 8, st));
+        ACC_HIP(hipMemsetAsync(u_off, 0, ((size_t)n + 1) * 8, st));
+        *view = acc_keydeps_view{ n, 0, 0, 0, 0, arena_off, ctx->get<int32_t>("arena", 1), kd_off,
+                                  ctx->get<uint32_t>("key_idx", 1), u_off, ctx->get<uint32_t>("dep_txn", 1) };
+        ctx->kd_view = *view;
+        ctx->kd_valid = true;
+        ctx->sync();
+        return;
+    }
+    const uint64_t *tm = stage_in(ctx, "in_tm", in->txn_id.msb, n, in->mem);
+    const uint64_t *tl = stage_in(ctx, "in_tl", in->txn_id.lsb, n, in->mem);
+    const int32_t *tn = stage_in(ctx, "in_tn", in->txn_id.node, n, in->mem);
+    const uint64_t *em = stage_in(ctx, "in_em", in->execute_at.msb, n, in->mem);
+    const uint64_t *el = stage_in(ctx, "in_el", in->execute_at.lsb, n, in->mem);
+    const int32_t *en = stage_in(ctx, "in_en", in->execute_at.node, n, in->mem);
+    const uint8_t *status = stage_in(ctx, "in_status", in->status, n, in->mem);
+    const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
+
+    // ---- 1. prep
+    uint64_t *g = ctx->get<uint64_t>("g", 8);
+    uint32_t *owner = ctx->get<uint32_t>("owner", P);
+    ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
+    launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, status,
+           key_off, key_code, owner, g);
+    launch(ctx, "prep_keys", k_prep_keys, dim3(std::min<unsigned>(grid_for(P, BLOCK), 1024u)), dim3(BLOCK), 0, P,
+           key_code, g);
+    // the last key_off entry must equal P
+    {
+        uint32_t last = 0;
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
+        if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
+    }
+    uint64_t hg[8];
+    memcpy(hg, ctx->pinned, sizeof hg);
+    check_errors(hg[4]);
+    const bool batch_sorted = hg[5] == 0;
+
+    // ---- 2. dictionary: order ranks over 2N timestamps
+    TsPlan plan;
+    plan.r0 = make_runs(hg[0]); plan.r1 = make_runs(hg[1]); plan.r2 = make_runs(hg[2]);
+    plan.b0 = plan.r0.bits; plan.b1 = plan.r1.bits; plan.b2 = plan.r2.bits;
+    const size_t m = 2 * (size_t)n;
+    uint32_t *rank = ctx->get<uint32_t>("rank", m);
+    uint32_t *flag = ctx->get<uint32_t>("rank_flag", m);
+    uint32_t *incl = ctx->get<uint32_t>("rank_incl", m);
+    const unsigned gm = grid_for(m, BLOCK);
+    Sorted ts_sorted;
+    if (plan.b0 + plan.b1 + plan.b2 <= 64) {
+        uint64_t *ck = ctx->get<uint64_t>("ts_ckey", m);
+        launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, -1,
+               (const uint32_t *)nullptr, ck);
+        ts_sorted = radix_sort(ctx, "rs_ts", ck, nullptr, m, plan.b0 + plan.b1 + plan.b2);
+        launch(ctx, "rank_flags", k_rank_flags, dim3(gm), dim3(BLOCK), 0, m, (const uint32_t *)ts_sorted.vals,
+               (const uint64_t *)nullptr, (const uint64_t *)nullptr, (const uint64_t *)nullptr,
+               (const uint64_t *)ts_sorted.keys, flag);
+    } else {
+        // multi-word LSD: node word, then lsb word, then msb word (each only over its varying bits)
+        uint64_t *c[3] = { ctx->get<uint64_t>("ts_c0", m), ctx->get<uint64_t>("ts_c1", m), ctx->get<uint64_t>("ts_c2", m) };
+        for (int w = 0; w < 3; ++w)
+            launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, w,
+                   (const uint32_t *)nullptr, c[w]);
+        uint64_t *tmpk = ctx->get<uint64_t>("ts_tmpk", m);
+        uint32_t *permb = ctx->get<uint32_t>("ts_perm", m);
+        const uint32_t *perm = nullptr;
+        const int wbits[3] = { plan.b0, plan.b1, plan.b2 };
+        for (int w = 2; w >= 0; --w) {
+            const uint64_t *keys = c[w];
+            if (perm) {
+                launch(ctx, "ts_compact", k_ts_compact, dim3(gm), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, plan, w,
+                       perm, tmpk);
+                keys = tmpk;
+            }
+            Sorted s = radix_sort(ctx, "rs_ts", keys, perm, m, wbits[w]);
+            ACC_HIP(hipMemcpyAsync(permb, s.vals, m * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+            perm = permb;
+        }
+        ts_sorted = { nullptr, permb };
+        launch(ctx, "rank_flags", k_rank_flags, dim3(gm), dim3(BLOCK), 0, m, (const uint32_t *)permb,
+               (const uint64_t *)c[0], (const uint64_t *)c[1], (const uint64_t *)c[2], (const uint64_t *)nullptr, flag);
+    }
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, incl, m, false);
+    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
+    launch(ctx, "rank_scatter", k_rank_scatter, dim3(gm), dim3(BLOCK), 0, m, n, (const uint32_t *)ts_sorted.vals,
+           (const uint32_t *)incl, rank, txn_of_rank);
+    {
+        uint32_t *seen = ctx->get<uint32_t>("dup_seen", m);
+        ACC_HIP(hipMemsetAsync(seen, 0, m * sizeof(uint32_t), st));
+        launch(ctx, "dup_txn", k_dup_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
+        launch(ctx, "exec_ties", k_exec_ties, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
+    }
+    const int rbits = bits_for(m - 1);
+
+    // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
+    PairPlan pp;
+    pp.rk = make_runs(hg[3]);
+    pp.rbits = rbits;
+    uint64_t *pkey = ctx->get<uint64_t>("pair_key", P);
+    const unsigned gP = grid_for(P, BLOCK);
+    Sorted ps;
+    int key_shift = 0;
+    if (batch_sorted) {
+        pp.mode = 0;   // pair index order is already TxnId order within every key: stable sort by key
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+        ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits);
+    } else if (pp.rk.bits + rbits <= 64) {
+        pp.mode = 1;
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+        ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits + rbits);
+        key_shift = rbits;
+    } else {
+        pp.mode = 2;
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 1, pkey);
+        Sorted byrank = radix_sort(ctx, "rs_pair_r", pkey, nullptr, P, rbits);
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+               (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey);
+        ps = radix_sort(ctx, "rs_pair", pkey, byrank.vals, P, pp.rk.bits);
+    }
+    uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
+    uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P);
+    launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, seg_flag, seg_incl, P, false);
+
+    uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
+    uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P);
+    uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P);
+    uint8_t *s_info = ctx->get<uint8_t>("s_info", P);
+    uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
+    uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
+    uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
+    uint64_t *pmax_in = ctx->get<uint64_t>("pmax_in", P);
+    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, n, (const uint32_t *)ps.vals,
+           (const uint32_t *)owner, (const uint32_t *)rank, status, tl, (const uint32_t *)seg_incl,
+           (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
+    const int segbits = bits_for(P);
+    // ---- v2 structures (class lists, prefix counts, bumped committed list)
+    const uint32_t nt = (uint32_t)((P + V2_TILE - 1) / V2_TILE);
+    uint32_t *tile_sums = ctx->get<uint32_t>("v2_tile_sums", (size_t)NCNT * nt);
+    uint32_t *tile_pref = ctx->get<uint32_t>("v2_tile_pref", (size_t)NCNT * nt);
+    uint32_t *totals = ctx->get<uint32_t>("v2_totals", 16);
+    uint32_t *bases = ctx->get<uint32_t>("v2_bases", 16);
+    launch(ctx, "v2_reduce", k_v2_reduce, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
+           (const uint8_t *)s_info, tile_sums, nt);
+    for (int q = 0; q < 7; ++q)
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, tile_sums + (size_t)q * nt, tile_pref + (size_t)q * nt, nt, true, totals + q);
+    scan<uint32_t, OpMax<uint32_t>>(ctx, tile_sums + (size_t)7 * nt, tile_pref + (size_t)7 * nt, nt, true, totals + 7);
+    launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
+    V2Cols cols;
+    cols.cnt = ctx->get<uint32_t>("v2_cnt", (size_t)NLIST * (P + 1));
+    cols.cbc = ctx->get<uint32_t>("v2_cbc", P + 1);
+    cols.lucw = ctx->get<uint32_t>("v2_lucw", P + 1);
+    cols.list_rank = ctx->get<uint32_t>("v2_list_rank", P);
+    cols.bc_rank = ctx->get<uint32_t>("v2_bc_rank", P);
+    cols.bc_exec = ctx->get<uint32_t>("v2_bc_exec", P);
+    cols.bc_kind = ctx->get<uint8_t>("v2_bc_kind", P);
+    cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
+    cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
+    launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
+           (const uint8_t *)s_info, (const uint32_t *)seg_incl, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
+           rbits, cols);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, g + 4, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    uint32_t htot[8];
+    memcpy(htot, ctx->pinned, sizeof htot);
+    check_errors(ctx->pinned[4]);
+    const bool ties = ctx->pinned[6] != 0;
+    if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
+        keydeps_v1_tail(ctx, in, view, n, P, rbits, status, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
+                        s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
+        return;
+    }
+    const uint32_t nbc = htot[6];
+    if (segbits + rbits > 64) fail(ACC_E_ARG, "batch too large for the (segment, executeAt) composite key");
+    Sorted bcs = radix_sort(ctx, "rs_bc", cols.bc_key, nullptr, nbc, segbits + rbits);
+    uint32_t *bcs_exec = ctx->get<uint32_t>("v2_bcs_exec", nbc);
+    uint32_t *bcs_lw_in = ctx->get<uint32_t>("v2_bcs_lw_in", nbc);
+    uint32_t *bcs_lastw = ctx->get<uint32_t>("v2_bcs_lastw", nbc);
+    launch(ctx, "v2_bcs_cols", k_v2_bcs_cols, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, nbc, (const uint64_t *)bcs.keys,
+           (const uint32_t *)bcs.vals, (const uint8_t *)cols.bc_kind, (uint64_t)((1ull << rbits) - 1), bcs_exec, bcs_lw_in);
+    scan<uint32_t, OpMax<uint32_t>>(ctx, bcs_lw_in, bcs_lastw, nbc, false);
+    uint64_t *bc_pm64 = ctx->get<uint64_t>("v2_bc_pm64", nbc);
+    uint32_t *bc_pm = ctx->get<uint32_t>("v2_bc_pm", nbc);
+    scan<uint64_t, OpMax<uint64_t>>(ctx, cols.bc_pm_in, bc_pm64, nbc, false);
+    launch(ctx, "low32", k_low32, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, (size_t)nbc, (const uint64_t *)bc_pm64, bc_pm);
+
+    V2View vv;
+    vv.owner = owner; vv.rank = rank; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
+    vv.s_rank = s_rank; vv.tl = tl; vv.status = status; vv.cnt = cols.cnt; vv.cbc = cols.cbc; vv.lucw = cols.lucw;
+    vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm;
+    vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw; vv.n = n; vv.P1 = P + 1;
+
+    // ---- count, offsets
+    uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
+    uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt, dep_off, P, true, dep_off + P);
+    uint32_t *nz = ctx->get<uint32_t>("nz", P);
+    uint32_t *cnz = ctx->get<uint32_t>("cnz", P + 1);
+    launch(ctx, "nonempty", k_nonempty, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, nz);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, nz, cnz, P, true, cnz + P);
+    uint64_t *kd_cnt = ctx->get<uint64_t>("kd_cnt", n);
+    uint64_t *a_cnt = ctx->get<uint64_t>("a_cnt", n);
+    launch(ctx, "v2_sizes", k_v2_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
+           (const uint32_t *)cnz, kd_cnt, a_cnt);
+    uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
+    uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, kd_off, n, true, kd_off + n);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, arena_off, n, true, arena_off + n);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, dep_off + P, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t E = ctx->pinned[0];
+    if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
+
+    // ---- write pass
+    int32_t *arena = ctx->get<int32_t>("arena", P + E);
+    uint32_t *key_idx = ctx->get<uint32_t>("key_idx", P);
+    uint32_t *dep_scratch = ctx->get<uint32_t>("v2_dep_scratch", E);
+    uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
+    uint32_t *big = ctx->get<uint32_t>("v2_big", n);
+    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 4);
+    ACC_HIP(hipMemsetAsync(gstat, 0, 4 * sizeof(uint64_t), st));
+    V2Out wo;
+    wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
+    wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.big = big; wo.gstat = gstat;
+    launch(ctx, "v2_write", k_v2_write, dim3((n + WPB - 1) / WPB), dim3(BLOCK), 0, n, vv, (const uint64_t *)cnt, wo);
+    launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
+           key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
+           (const uint64_t *)arena_off, key_idx, arena);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t nbig = ctx->pinned[0], ebig = ctx->pinned[1];
+    if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+    if (nbig) {
+        uint32_t *big_idx = ctx->get<uint32_t>("v2_big_idx", n);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, big, big_idx, n, true);
+        uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", nbig);
+        uint64_t *big_e = ctx->get<uint64_t>("v2_big_e", nbig);
+        uint64_t *big_off = ctx->get<uint64_t>("v2_big_off", nbig + 1);
+        launch(ctx, "v2_big_list", k_v2_big_list, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)big,
+               (const uint32_t *)big_idx, key_off, (const uint64_t *)dep_off, big_list, big_e);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, big_e, big_off, nbig, true, big_off + nbig);
+        const int bbits = bits_for(nbig - 1);
+        if (bbits + rbits + 16 > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
+        uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", ebig);
+        launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nbig + WPB - 1) / WPB)), dim3(BLOCK), 0,
+               (uint32_t)nbig, (const uint32_t *)big_list, (const uint64_t *)big_off, vv, (const uint64_t *)cnt, key_off,
+               rbits, gkey);
+        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, ebig, bbits + rbits + 16);
+        uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", ebig);
+        uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", ebig);
+        launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig,
+               (const uint64_t *)s1.keys, rbits, nflag);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, ebig, false);
+        uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", ebig);
+        uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", ebig);
+        launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig, (const uint64_t *)s1.keys,
+               (const uint32_t *)nincl, (const uint32_t *)big_list, (const uint64_t *)big_off, rbits, key_off,
+               (const uint64_t *)dep_off, (const uint32_t *)txn_of_rank, dep_scratch, u_cnt, idx1, key2);
+        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, ebig, bbits + 16 + rbits);
+        launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig,
+               (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)big_list,
+               (const uint64_t *)big_off, rbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
+    }
+    uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
+    uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
+    launch(ctx, "v2_compact", k_v2_compact, dim3((n + WPB - 1) / WPB), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
+           (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));

@@ -72,6 +72,7 @@ extern "C" {
 
 /* ---- context options ---- */
 #define ACC_OPT_TIMING 0x1u   /* record per-kernel HIP events (bench / profiling) */
+#define ACC_OPT_FORCE_REPLAY 0x2u  /* always take the exact FAST-bisection replay path (testing) */
 
 typedef struct acc_ctx acc_ctx;
 

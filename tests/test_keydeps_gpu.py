@@ -12,10 +12,12 @@ from accord_amd import workload as W
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
+@pytest.fixture(scope="module", params=["runs", "replay"])
+def ctx(request):
+    """Both device paths: the run-based scan (default) and the exact FAST-bisection replay that batches
+    with executeAt ties take (forced here with ACC_OPT_FORCE_REPLAY)."""
     from accord_amd.deps import Context
-    c = Context(0)
+    c = Context(0, force_replay=request.param == "replay")
     yield c
     c.close()
 
