@@ -5,7 +5,7 @@ Every stream is counter-based SplitMix64 (``x_i = mix64(seed ^ salt + (i+1)*GAMM
 TxnId/executeAt as (msb, lsb, node) columns, InternalStatus ordinals, CSR key offsets and IntKey codes.
 
 TxnId i: epoch=1, hlc=i+1, node=1+(i mod 8), flags = kind<<1 | domain (Timestamp.java:81-89,
-TxnId.java:124-137). Committed-class txns get executeAt bumped to hlc+U[1,1000] with node 1000+(i mod 8)
+TxnId.java:124-137). Committed-class txns get executeAt bumped to hlc+U[1,1000] with node 1000+i
 for 10% of them, so no executeAt compares equal to any TxnId or other executeAt.
 """
 from __future__ import annotations
@@ -182,7 +182,7 @@ def keydeps_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, dist: s
     committed = (status >= COMMITTED) & (status <= APPLIED)
     bump = committed & (uniform01(seed, 5, n_txn) < 0.1)
     bump_by = 1 + (stream(seed, 6, n_txn) % np.uint64(1000)).astype(np.int64)
-    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + (i % 8))
+    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + i)  # unique node: no two executeAts tie
     exe_msb = np.where(bump, e_msb, t_msb).astype(np.uint64)
     exe_lsb = np.where(bump, e_lsb_b, t_lsb).astype(np.uint64)
     exe_node = np.where(bump, e_node_b, t_node).astype(np.int32)

@@ -772,11 +772,17 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t j)
     return q;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out)
+// per-pair query record kept for the write pass: (s0, pos, posM, M or NONE), bstart
+constexpr uint32_t NO_M = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out,
+                                                    uint4 *__restrict__ rec, uint32_t *__restrict__ rec_bstart)
 {
     size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (j >= P) return;
     V2Query q = v2_query(v, (uint32_t)j);
+    rec[j] = make_uint4(q.s0, q.pos, q.posm, q.has_m ? q.m : NO_M);
+    rec_bstart[j] = q.bstart;
     uint64_t e = 0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -794,76 +800,36 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
     cnt_out[j] = e;
 }
 
-// ---- write pass: one wave per txn gathers its runs into LDS, sorts (value, key) and emits the Java layout
+// ---- write pass: one wave per txn. Lane k computes the 7 runs of key k from the count pass record
+// (R1/R2 per kind class, R3); all lanes then gather the flattened runs in parallel, drop T itself and
+// non-qualifying R3 entries by ballot compaction into LDS, sort (value << 16 | key) and emit the Java layout.
 
 constexpr int WCAP = 1024;          // entries per wave in LDS
-constexpr int WMAXK = 64;           // keys per txn on the wave path
+constexpr int WMAXK = 64;           // keys per txn on the wave path (one lane per key)
 constexpr int WPB = WAVES;          // waves (txns) per block
+constexpr int NRUN = 7;
 
-// Append run [a, b) of `src` (values) to the wave buffer, dropping `skip` (T itself) when drop is set.
-__device__ __forceinline__ uint32_t wave_append(uint64_t *buf, uint32_t cursor, const uint32_t *src, uint32_t a, uint32_t b,
-                                                bool drop, uint32_t skip, uint32_t kj)
+struct V2Out {
+    const uint32_t *key_off;
+    const uint64_t *dep_off, *arena_off;
+    const uint32_t *cnz, *txn_of_rank;
+    const uint4 *rec;
+    const uint32_t *rec_bstart;
+    int32_t *arena;
+    uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
+    uint64_t *u_cnt;
+    uint32_t *big;           // 1 = txn left for the global path
+    uint64_t *gstat;         // [0] big txns, [1] their entries, [2] internal count mismatches
+};
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
 {
-    const uint32_t lane = lane_id();
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t c = a; c < b; c += 64) {
-        uint32_t i = c + lane;
-        bool in = i < b;
-        uint32_t x = in ? src[i] : 0;
-        bool keep = in && !(drop && x == skip);
-        uint64_t bal = __ballot(keep);
-        if (keep) {
-            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-            if (slot < WCAP) buf[slot] = ((uint64_t)x << 16) | kj;
-        }
-        cursor += (uint32_t)__popcll(bal);
-    }
-    return cursor;
+    uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint32_t wave_append_r3(uint64_t *buf, uint32_t cursor, const V2View &v, const V2Query &q, uint32_t kj)
-{
-    const uint32_t lane = lane_id();
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t c = q.bstart; c < q.bend; c += 64) {
-        uint32_t i = c + lane;
-        bool keep = false;
-        uint32_t x = 0;
-        if (i < q.bend) {
-            x = v.bc_rank[i];
-            keep = v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u) && !(q.bq && x == q.trank);
-        }
-        uint64_t bal = __ballot(keep);
-        if (keep) {
-            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-            if (slot < WCAP) buf[slot] = ((uint64_t)x << 16) | kj;
-        }
-        cursor += (uint32_t)__popcll(bal);
-    }
-    return cursor;
-}
-
-// Gather all runs of txn t (keys j0..j1) into buf; returns the entry count.
-__device__ uint32_t gather_txn(uint64_t *buf, const V2View &v, uint32_t j0, uint32_t j1, const uint64_t *cnt)
-{
-    uint32_t cursor = 0;
-    for (uint32_t j = j0; j < j1; ++j) {
-        if (cnt[j] == 0) continue;
-        V2Query q = v2_query(v, j);
-        uint32_t kj = j - j0;
-        for (int c = 0; c < 3; ++c) {
-            if (!((q.wc >> c) & 1u)) continue;
-            const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
-            cursor = wave_append(buf, cursor, v.list_rank + v.bases[c], cu[q.s0], cu[q.pos], q.bq, q.trank, kj);
-            cursor = wave_append(buf, cursor, v.list_rank + v.bases[3 + c], cc[q.posm], cc[q.pos], q.bq, q.trank, kj);
-        }
-        if (q.has_m) cursor = wave_append_r3(buf, cursor, v, q, kj);
-    }
-    return cursor;
-}
-
-// in-LDS bitonic sort of n2 (power of two) u64 entries by one wave
-__device__ __forceinline__ void wave_bitonic(uint64_t *buf, uint32_t n2)
+// in-LDS bitonic sort of n2 (power of two, >= 128) u64 entries by one wave
+__device__ __forceinline__ void wave_bitonic_lds(uint64_t *buf, uint32_t n2)
 {
     const uint32_t lane = lane_id();
     for (uint32_t k = 2; k <= n2; k <<= 1) {
@@ -882,31 +848,75 @@ __device__ __forceinline__ void wave_bitonic(uint64_t *buf, uint32_t n2)
     }
 }
 
-struct V2Out {
-    const uint32_t *key_off;
-    const uint64_t *dep_off, *arena_off;
-    const uint32_t *cnz, *txn_of_rank;
-    int32_t *arena;
-    uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
-    uint64_t *u_cnt;
-    uint32_t *big;           // 1 = txn left for the global path
-    uint64_t *gstat;         // [0] big txns, [1] their entries, [2] internal count mismatches
+// register bitonic across the 64 lanes (ascending by lane)
+__device__ __forceinline__ uint64_t wave_bitonic_reg(uint64_t x)
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            uint64_t y = shfl_xor64(x, (int)jj);
+            bool up = (lane & k) == 0, lower = (lane & jj) == 0;
+            uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+            x = (lower == up) ? lo : hi;
+        }
+    }
+    return x;
+}
+
+// Emit one chunk of up to 64 sorted entries (lane holds x). Returns the updated distinct count.
+__device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t prev, bool has_prev, uint32_t distinct,
+                                               uint32_t *kc, const V2Out &o, uint32_t j0, uint64_t e0, uint64_t abase)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t val = (uint32_t)(x >> 16), kj = (uint32_t)(x & 0xFFFFu);
+    bool nw = in && (!has_prev || (uint32_t)(prev >> 16) != val);
+    uint64_t bal = __ballot(nw);
+    uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+    uint64_t peers = __ballot(in);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        uint64_t bb = __ballot((kj >> b) & 1u);
+        peers &= ((kj >> b) & 1u) ? bb : ~bb;
+    }
+    uint32_t before = (uint32_t)__popcll(peers & lt);
+    if (in) {
+        uint32_t slot = kc[kj] + before;
+        uint64_t kbase = o.dep_off[j0 + kj] - e0;
+        o.arena[abase + kbase + slot] = (int32_t)idx;
+        if (nw) o.dep_scratch[e0 + idx] = o.txn_of_rank[val];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (in && before == 0) kc[kj] += (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    return distinct + (uint32_t)__popcll(bal);
+}
+
+struct WaveRuns {
+    uint32_t start[WMAXK][NRUN];   // start index in the run's source array
+    uint32_t pre[WMAXK][NRUN + 1]; // local prefix of run lengths within the key
+    uint32_t kbase[WMAXK + 1];     // flattened base of each key
+    uint32_t m[WMAXK];             // M of the key (R3 filter)
+    uint32_t kc[WMAXK];            // per-key emitted count
 };
 
 __global__ __launch_bounds__(BLOCK) void k_v2_write(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ uint64_t sbuf[WPB][WCAP];
-    __shared__ uint32_t skey[WPB][WMAXK];
+    __shared__ WaveRuns sruns[WPB];
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint32_t t = blockIdx.x * WPB + wave;
     if (t >= n) return;
     uint64_t *buf = sbuf[wave];
-    uint32_t *kc = skey[wave];
-    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
+    WaveRuns &R = sruns[wave];
+    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1], nk = j1 - j0;
     const uint64_t e0 = o.dep_off[j0];
     const uint32_t E = (uint32_t)(o.dep_off[j1] - e0);
     if (E == 0) { if (lane == 0) { o.u_cnt[t] = 0; o.big[t] = 0; } return; }
-    if (E > WCAP || j1 - j0 > WMAXK) {
+    if (E > WCAP || nk > WMAXK) {
         if (lane == 0) {
             o.big[t] = 1;
             atomicAdd((unsigned long long *)&o.gstat[0], 1ull);
@@ -914,49 +924,112 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write(uint32_t n, V2View v, const 
         }
         return;
     }
-    uint32_t got = gather_txn(buf, v, j0, j1, cnt);
-    if (got != E) {   // count and gather disagree: internal invariant violation (reported as ACC_E_STATE)
+    const uint32_t trank = v.rank[t];
+    const bool bq = v.rank[v.n + t] != trank;
+    const uint32_t wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u), wc = wk_classes(wk);
+    // ---- lane k: runs of key k
+    uint32_t ktot = 0;
+    if (lane < nk && cnt[j0 + lane] != 0) {
+        const uint32_t j = j0 + lane;
+        uint4 r = o.rec[j];
+        const uint32_t s0 = r.x, pos = r.y, posm = r.z, m = r.w;
+        const bool has_m = m != NO_M;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            uint32_t a0 = 0, l0 = 0, a1 = 0, l1 = 0;
+            if ((wc >> c) & 1u) {
+                const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
+                a0 = v.bases[c] + cu[s0]; l0 = cu[pos] - cu[s0];
+                uint32_t from = has_m ? posm : s0;
+                a1 = v.bases[3 + c] + cc[from]; l1 = cc[pos] - cc[from];
+            }
+            R.start[lane][2 * c] = a0; R.pre[lane][2 * c] = acc; acc += l0;
+            R.start[lane][2 * c + 1] = a1; R.pre[lane][2 * c + 1] = acc; acc += l1;
+        }
+        uint32_t bs = 0, bl = 0;
+        if (has_m) { bs = o.rec_bstart[j]; bl = v.cbc[posm] - bs; }
+        R.start[lane][6] = bs; R.pre[lane][6] = acc; acc += bl;
+        R.pre[lane][7] = acc;
+        R.m[lane] = m;
+        ktot = acc;
+    } else if (lane < nk) {
+        for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
+        R.m[lane] = NO_M;
+    }
+    if (lane < WMAXK) R.kc[lane] = 0;
+    uint32_t ktot_total;
+    {
+        // wave exclusive scan of per-key totals (lanes >= nk contribute 0)
+        uint32_t incl = wave_inclusive(ktot, OpAdd<uint32_t>());
+        uint32_t excl = incl - ktot;
+        if (lane < nk) R.kbase[lane] = excl;
+        ktot_total = shfl_idx(incl, 63);
+        if (lane == 0) R.kbase[nk] = ktot_total;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // ---- flattened gather with filtering, compacted into buf
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t cursor = 0;
+    for (uint32_t c0 = 0; c0 < ktot_total; c0 += 64) {
+        uint32_t e = c0 + lane;
+        bool keep = false;
+        uint64_t item = 0;
+        if (e < ktot_total) {
+            // key: last kbase <= e
+            uint32_t lo = 0, hi = nk;
+            while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
+            uint32_t k = lo, off = e - R.kbase[k];
+            uint32_t r = 0;
+            while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
+            uint32_t idx = R.start[k][r] + (off - R.pre[k][r]);
+            uint32_t x;
+            if (r < 6) {
+                x = v.list_rank[idx];
+                keep = true;
+            } else {
+                x = v.bc_rank[idx];
+                keep = v.bc_exec[idx] >= R.m[k] && ((wk >> v.bc_kind[idx]) & 1u);
+            }
+            keep = keep && !(bq && x == trank);
+            item = ((uint64_t)x << 16) | k;
+        }
+        uint64_t bal = __ballot(keep);
+        if (keep) {
+            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+            if (slot < WCAP) buf[slot] = item;
+        }
+        cursor += (uint32_t)__popcll(bal);
+    }
+    if (cursor != E) {   // count and gather disagree: internal invariant violation (ACC_E_STATE)
         if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
         return;
     }
-    uint32_t n2 = 64;
-    while (n2 < E) n2 <<= 1;
-    for (uint32_t i = E + lane; i < n2; i += 64) buf[i] = ~0ull;
-    for (uint32_t i = lane; i < WMAXK; i += 64) kc[i] = 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    wave_bitonic(buf, n2);
     const uint32_t kd = o.cnz[j1] - o.cnz[j0];
     const uint64_t abase = o.arena_off[t] + kd;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t distinct = 0;
-    for (uint32_t c = 0; c < E; c += 64) {
-        uint32_t i = c + lane;
-        bool in = i < E;
-        uint64_t x = in ? buf[i] : 0;
-        uint32_t val = (uint32_t)(x >> 16), kj = (uint32_t)(x & 0xFFFFu);
-        bool nw = in && (i == 0 || (uint32_t)(buf[i - 1] >> 16) != val);
-        uint64_t bal = __ballot(nw);
-        uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
-        distinct += (uint32_t)__popcll(bal);
-        // slot of this entry within its key's list: earlier lanes of this chunk with the same key
-        uint64_t peers = __ballot(in);
-#pragma unroll
-        for (int b = 0; b < 6; ++b) {
-            uint64_t bb = __ballot((kj >> b) & 1u);
-            peers &= ((kj >> b) & 1u) ? bb : ~bb;
-        }
-        uint32_t before = (uint32_t)__popcll(peers & lt);
-        if (in) {
-            uint32_t slot = kc[kj] + before;
-            uint64_t kbase = o.dep_off[j0 + kj] - e0;
-            o.arena[abase + kbase + slot] = (int32_t)idx;
-            if (nw) o.dep_scratch[e0 + idx] = o.txn_of_rank[val];
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (in && before == 0) kc[kj] += (uint32_t)__popcll(peers);
+    if (E <= 64) {
+        uint64_t x = lane < E ? buf[lane] : ~0ull;
+        x = wave_bitonic_reg(x);
+        uint64_t prev = shfl_up(x, 1);
+        distinct = emit_chunk(x, lane < E, prev, lane > 0, 0, R.kc, o, j0, e0, abase);
+    } else {
+        uint32_t n2 = 128;
+        while (n2 < E) n2 <<= 1;
+        for (uint32_t i = E + lane; i < n2; i += 64) buf[i] = ~0ull;
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        wave_bitonic_lds(buf, n2);
+        for (uint32_t c = 0; c < E; c += 64) {
+            uint32_t i = c + lane;
+            bool in = i < E;
+            uint64_t x = in ? buf[i] : 0;
+            uint64_t prev = i > 0 ? buf[i - 1] : 0;
+            distinct = emit_chunk(x, in, prev, i > 0, distinct, R.kc, o, j0, e0, abase);
+        }
     }
     if (lane == 0) { o.u_cnt[t] = distinct; o.big[t] = 0; }
 }
@@ -1439,7 +1512,9 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     // ---- count, offsets
     uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
     uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
-    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt);
+    uint4 *rec = ctx->get<uint4>("v2_rec", P);
+    uint32_t *rec_bstart = ctx->get<uint32_t>("v2_rec_bstart", P);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt, rec, rec_bstart);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt, dep_off, P, true, dep_off + P);
     uint32_t *nz = ctx->get<uint32_t>("nz", P);
     uint32_t *cnz = ctx->get<uint32_t>("cnz", P + 1);
@@ -1469,6 +1544,7 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     V2Out wo;
     wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.big = big; wo.gstat = gstat;
+    wo.rec = rec; wo.rec_bstart = rec_bstart;
     launch(ctx, "v2_write", k_v2_write, dim3((n + WPB - 1) / WPB), dim3(BLOCK), 0, n, vv, (const uint64_t *)cnt, wo);
     launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
            key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,

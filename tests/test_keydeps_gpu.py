@@ -128,6 +128,24 @@ def test_wide_timestamps_multiword_sort(ctx):
     assert_same(g, o, b.n_txn, "wide")
 
 
+def test_path_selection():
+    """Tie-free batches take the run-based path; executeAt ties switch to the exact replay."""
+    from accord_amd.deps import Context
+    b = W.keydeps_batch(3000, 4, 300, 0x31, "zipf", status_model="model", window=500)
+    with Context(0, timing=True) as c:
+        c.calculate_partial_deps(b)
+        names = set(c.timing())
+    assert "v2_write" in names and "query_emit" not in names
+    com = np.where((b.status >= W.COMMITTED) & (b.status <= W.APPLIED))[0][:2]
+    b.exe_msb[com] = b.exe_msb[com[0]]
+    b.exe_lsb[com] = b.txn_lsb[com].max() + (np.uint64(7) << np.uint64(16))
+    b.exe_node[com] = 77
+    with Context(0, timing=True) as c:
+        c.calculate_partial_deps(b)
+        names = set(c.timing())
+    assert "query_emit" in names
+
+
 def test_edge_cases(ctx):
     import oracle
     # single txn, no deps
