@@ -160,6 +160,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
+    result["path_stats"] = ctx.stats()
     if os.environ.get("ACC_BENCH_KERNELS"):
         result["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in
                                          sorted(timing.items(), key=lambda kv: -kv[1][0])}

@@ -23,8 +23,8 @@ u8p = C.POINTER(C.c_uint8)
 
 # Every symbol declared in include/accord_amd.h (tests check the library exports all of them).
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
-           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_merge", "acc_levelise",
-           "acc_timing_count", "acc_timing_get", "acc_timing_reset"]
+           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
+           "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get"]
 
 
 class Opts(C.Structure):
@@ -73,6 +73,15 @@ class MergeView(C.Structure):
                 ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
 
 
+class MergeOut(C.Structure):
+    _fields_ = [("mem", C.c_uint32),
+                ("cap_keys", C.c_uint64), ("cap_vals", C.c_uint64), ("cap_k2v", C.c_uint64),
+                ("need_keys", C.c_uint64), ("need_vals", C.c_uint64), ("need_k2v", C.c_uint64),
+                ("key_off", C.c_void_p), ("key_code", C.c_void_p),
+                ("val_off", C.c_void_p), ("txn_rank", C.c_void_p),
+                ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -107,6 +116,8 @@ def load():
     L.acc_keydeps_copy_out.restype = C.c_int
     L.acc_keydeps_merge.argtypes = [C.c_void_p, C.POINTER(MergeIn), C.POINTER(MergeView)]
     L.acc_keydeps_merge.restype = C.c_int
+    L.acc_merge_copy_out.argtypes = [C.c_void_p, C.POINTER(MergeOut)]
+    L.acc_merge_copy_out.restype = C.c_int
     L.acc_levelise.argtypes = [C.c_void_p, C.POINTER(GraphIn), u32p, u32p, u32p]
     L.acc_levelise.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]
@@ -116,5 +127,9 @@ def load():
     L.acc_timing_get.restype = C.c_int
     L.acc_timing_reset.argtypes = [C.c_void_p]
     L.acc_timing_reset.restype = None
+    L.acc_stats_count.argtypes = [C.c_void_p]
+    L.acc_stats_count.restype = C.c_int
+    L.acc_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]
+    L.acc_stats_get.restype = C.c_int
     _lib = L
     return L

@@ -101,6 +101,15 @@ class Context:
             out[name.value.decode()] = (ms.value, cnt.value)
         return out
 
+    def stats(self) -> dict:
+        out = {}
+        for i in range(max(self._lib.acc_stats_count(self._h), 0)):
+            name = C.c_char_p()
+            val = C.c_uint64()
+            self._lib.acc_stats_get(self._h, i, C.byref(name), C.byref(val))
+            out[name.value.decode()] = val.value
+        return out
+
     def timing_reset(self):
         self._lib.acc_timing_reset(self._h)
 
@@ -242,3 +251,41 @@ class KeyDeps:
 
     def __str__(self):
         return "{" + ", ".join(f"{k}:[{', '.join(str(t) for t in v)}]" for k, v in self.canonical().items()) + "}"
+
+
+def _merge_in(m: dict, keep: list) -> "L.MergeIn":
+    a = {k: np.ascontiguousarray(v, dtype=dt) for (k, dt), v in
+         zip([("grp_off", np.uint64), ("key_off", np.uint64), ("key_code", np.uint64), ("val_off", np.uint64),
+              ("txn_rank", np.uint32), ("k2v_off", np.uint64), ("k2v", np.int32)],
+             [m["grp_off"], m["key_off"], m["key_code"], m["val_off"], m["txn_rank"], m["k2v_off"], m["k2v"]])}
+    keep.append(a)
+    ng = len(a["grp_off"]) - 1
+    nr = len(a["key_off"]) - 1
+    return L.MergeIn(L.ACC_MEM_HOST, ng, nr, *(a[k].ctypes.data for k in
+                                               ("grp_off", "key_off", "key_code", "val_off", "txn_rank", "k2v_off", "k2v")))
+
+
+def keydeps_merge(ctx: Context, m: dict) -> dict:
+    """KeyDeps.merge for every group of replies (primitives/KeyDeps.java:115-135) on the GPU.
+    `m` uses the acc_merge_in layout (grp_off, key_off, key_code, val_off, txn_rank, k2v_off, k2v)."""
+    keep = []
+    mi = _merge_in(m, keep)
+    view = L.MergeView()
+    ctx.check(ctx._lib.acc_keydeps_merge(ctx.handle, C.byref(mi), C.byref(view)))
+    out = L.MergeOut()
+    out.mem = L.ACC_MEM_HOST
+    rc = ctx._lib.acc_merge_copy_out(ctx.handle, C.byref(out))
+    if rc not in (L.ACC_OK, L.ACC_E_CAP):
+        ctx.check(rc)
+    ng = view.n_groups
+    r = dict(key_off=np.zeros(ng + 1, np.uint64), val_off=np.zeros(ng + 1, np.uint64),
+             k2v_off=np.zeros(ng + 1, np.uint64), key_code=np.zeros(max(out.need_keys, 1), np.uint64),
+             txn_rank=np.zeros(max(out.need_vals, 1), np.uint32), k2v=np.zeros(max(out.need_k2v, 1), np.int32))
+    out.cap_keys, out.cap_vals, out.cap_k2v = out.need_keys, out.need_vals, out.need_k2v
+    for k in r:
+        setattr(out, k, r[k].ctypes.data)
+    ctx.check(ctx._lib.acc_merge_copy_out(ctx.handle, C.byref(out)))
+    r["key_code"] = r["key_code"][:out.need_keys]
+    r["txn_rank"] = r["txn_rank"][:out.need_vals]
+    r["k2v"] = r["k2v"][:out.need_k2v]
+    return r

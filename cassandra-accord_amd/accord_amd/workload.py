@@ -5,7 +5,7 @@ Every stream is counter-based SplitMix64 (``x_i = mix64(seed ^ salt + (i+1)*GAMM
 TxnId/executeAt as (msb, lsb, node) columns, InternalStatus ordinals, CSR key offsets and IntKey codes.
 
 TxnId i: epoch=1, hlc=i+1, node=1+(i mod 8), flags = kind<<1 | domain (Timestamp.java:81-89,
-TxnId.java:124-137). Committed-class txns get executeAt bumped to hlc+U[1,1000] with node 1000+i
+TxnId.java:124-137). Committed-class txns get executeAt bumped to hlc+U[1,1000] with node 1000+(i mod 1024)
 for 10% of them, so no executeAt compares equal to any TxnId or other executeAt.
 """
 from __future__ import annotations
@@ -182,7 +182,7 @@ def keydeps_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, dist: s
     committed = (status >= COMMITTED) & (status <= APPLIED)
     bump = committed & (uniform01(seed, 5, n_txn) < 0.1)
     bump_by = 1 + (stream(seed, 6, n_txn) % np.uint64(1000)).astype(np.int64)
-    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + i)  # unique node: no two executeAts tie
+    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + (i % 1024))  # no ties: |i - i' | < 1024
     exe_msb = np.where(bump, e_msb, t_msb).astype(np.uint64)
     exe_lsb = np.where(bump, e_lsb_b, t_lsb).astype(np.uint64)
     exe_node = np.where(bump, e_node_b, t_node).astype(np.int32)
@@ -213,3 +213,74 @@ def config(name: str, scale: float = 1.0) -> Batch:
         return keydeps_batch(n, 8, max(1000, int(1_000_000 * scale)), CONFIG_SEEDS["2"], "zipf", 0.99,
                              status_model="model")
     raise ValueError(name)
+
+
+def merge_batch(n_txn: int = 16_384, replies: int = 64, seed: int = CONFIG_SEEDS["5"], n_keys: int = 1_000_000,
+                keys_per_txn: int = 8, deps_per_key: int = 4, p_drop: float = 0.1, p_spurious: float = 0.05) -> dict:
+    """Config 5 input in the acc_merge_in layout: group t = coordinated txn t, with `replies` KeyDeps replies.
+
+    Each txn gets a base dependency map (keys_per_txn zipf keys, deps_per_key dep ranks below its own rank),
+    standing in for its config-2-style deps; every reply drops each base entry with p_drop and adds
+    round(p_spurious * base entries) spurious ones on the txn's keys. Replies are built in the Java layout
+    (sorted unique keys / txnId ranks, keysToTxnIds with the end-offset header)."""
+    rng_u = lambda salt, n: uniform01(seed, salt, n)  # noqa: E731
+    keys = _distinct_keys(seed, n_txn, keys_per_txn, zipf_sampler(seed, 40, n_keys, 0.99, True))
+    kc = int_key_code(keys.reshape(-1)).astype(np.int64)
+    t_rank = 2 * np.arange(n_txn, dtype=np.int64) + 2  # ranks of the txns (gaps leave room for other ids)
+    # base entries (t, key, dep)
+    bt = np.repeat(np.arange(n_txn, dtype=np.int64), keys_per_txn * deps_per_key)
+    bk = np.repeat(kc, deps_per_key)
+    bd = (rng_u(41, len(bt)) * t_rank[bt]).astype(np.int64)
+    # replicate per reply, drop, add spurious
+    q_base = np.repeat(bt * replies, replies) + np.tile(np.arange(replies, dtype=np.int64), len(bt))
+    k_base = np.repeat(bk, replies)
+    d_base = np.repeat(bd, replies)
+    keep = rng_u(42, len(q_base)) >= p_drop
+    q, k, d = q_base[keep], k_base[keep], d_base[keep]
+    n_sp = int(round(p_spurious * keys_per_txn * deps_per_key))
+    if n_sp:
+        sq = np.repeat(np.arange(n_txn * replies, dtype=np.int64), n_sp)
+        st = sq // replies
+        sk = kc.reshape(n_txn, keys_per_txn)[st, (rng_u(43, len(sq)) * keys_per_txn).astype(np.int64)]
+        sd = (rng_u(44, len(sq)) * t_rank[st]).astype(np.int64)
+        q, k, d = np.concatenate([q, sq]), np.concatenate([k, sk]), np.concatenate([d, sd])
+    order = np.lexsort((d, k, q))
+    q, k, d = q[order], k[order], d[order]
+    uniq = np.ones(len(q), dtype=bool)
+    uniq[1:] = (q[1:] != q[:-1]) | (k[1:] != k[:-1]) | (d[1:] != d[:-1])
+    q, k, d = q[uniq], k[uniq], d[uniq]
+    nrep = n_txn * replies
+    # keys per reply
+    kfirst = np.ones(len(q), dtype=bool)
+    kfirst[1:] = (q[1:] != q[:-1]) | (k[1:] != k[:-1])
+    key_code = k[kfirst].astype(np.uint64)
+    key_cnt = np.bincount(q[kfirst], minlength=nrep)
+    # values per reply: unique (q, d)
+    comb = np.unique((q << 32) | d)
+    val_cnt = np.bincount(comb >> 32, minlength=nrep)
+    txn_rank = (comb & 0xFFFFFFFF).astype(np.uint32)
+    val_off = np.zeros(nrep + 1, dtype=np.uint64)
+    np.cumsum(val_cnt, out=val_off[1:])
+    key_off = np.zeros(nrep + 1, dtype=np.uint64)
+    np.cumsum(key_cnt, out=key_off[1:])
+    # index of each entry's dep within its reply's txnIds
+    dep_idx = np.searchsorted(comb, (q << 32) | d) - val_off[q].astype(np.int64)
+    ent_cnt = np.bincount(q, minlength=nrep)
+    k2v_len = key_cnt + ent_cnt
+    k2v_off = np.zeros(nrep + 1, dtype=np.uint64)
+    np.cumsum(k2v_len, out=k2v_off[1:])
+    k2v = np.zeros(int(k2v_off[-1]), dtype=np.int32)
+    # entries: after the reply's header
+    ent_start = np.zeros(nrep + 1, dtype=np.int64)
+    np.cumsum(ent_cnt, out=ent_start[1:])
+    pos_in_reply = np.arange(len(q), dtype=np.int64) - ent_start[q]
+    k2v[(k2v_off[q].astype(np.int64) + key_cnt[q] + pos_in_reply)] = dep_idx.astype(np.int32)
+    # header: end offset of each key = nk + entries up to and including that key
+    klast = np.ones(len(q), dtype=bool)
+    klast[:-1] = (q[1:] != q[:-1]) | (k[1:] != k[:-1])
+    kq = q[klast]
+    key_ord = np.arange(len(kq), dtype=np.int64) - key_off[kq].astype(np.int64)
+    k2v[k2v_off[kq].astype(np.int64) + key_ord] = (key_cnt[kq] + pos_in_reply[klast] + 1).astype(np.int32)
+    grp_off = (np.arange(n_txn + 1, dtype=np.uint64) * np.uint64(replies))
+    return dict(grp_off=grp_off, key_off=key_off, key_code=key_code, val_off=val_off, txn_rank=txn_rank,
+                k2v_off=k2v_off, k2v=k2v)

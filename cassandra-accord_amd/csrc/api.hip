@@ -105,6 +105,32 @@ int acc_keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *out_
     });
 }
 
+int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        if (!out) acc::fail(ACC_E_ARG, "null output");
+        if (!ctx->merge_valid) acc::fail(ACC_E_STATE, "no merge result on this context");
+        const acc_merge_view &v = ctx->merge_view;
+        out->need_keys = v.total_keys;
+        out->need_vals = v.total_vals;
+        out->need_k2v = v.total_k2v;
+        if (!out->key_off || !out->val_off || !out->k2v_off)
+            acc::fail(ACC_E_CAP, "sizing call (null offset arrays); required sizes written to need_*");
+        if (out->cap_keys < v.total_keys || out->cap_vals < v.total_vals || out->cap_k2v < v.total_k2v)
+            acc::fail(ACC_E_CAP, "output capacity too small; required sizes written to need_*");
+        hipMemcpyKind kind = out->mem == ACC_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        size_t n1 = (size_t)v.n_groups + 1;
+        ACC_HIP(hipMemcpyAsync(out->key_off, v.key_off, n1 * 8, kind, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->val_off, v.val_off, n1 * 8, kind, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->k2v_off, v.k2v_off, n1 * 8, kind, ctx->stream));
+        if (v.total_keys) ACC_HIP(hipMemcpyAsync(out->key_code, v.key_code, v.total_keys * 8, kind, ctx->stream));
+        if (v.total_vals) ACC_HIP(hipMemcpyAsync(out->txn_rank, v.txn_rank, v.total_vals * 4, kind, ctx->stream));
+        if (v.total_k2v) ACC_HIP(hipMemcpyAsync(out->k2v, v.k2v, v.total_k2v * 4, kind, ctx->stream));
+        ctx->sync();
+    });
+}
+
 int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels)
 {
     if (!ctx) return ACC_E_ARG;
@@ -135,6 +161,16 @@ void acc_timing_reset(acc_ctx *ctx)
     if (!ctx) return;
     acc_guard(ctx, [&] { ctx->sync(); });
     for (auto &s : ctx->slots) { s.total_ms = 0; s.launches = 0; }
+}
+
+int acc_stats_count(acc_ctx *ctx) { return ctx ? (int)ctx->stats.size() : 0; }
+
+int acc_stats_get(acc_ctx *ctx, int i, const char **name, uint64_t *value)
+{
+    if (!ctx || i < 0 || i >= (int)ctx->stats.size()) return ACC_E_ARG;
+    if (name) *name = ctx->stats[i].first.c_str();
+    if (value) *value = ctx->stats[i].second;
+    return ACC_OK;
 }
 
 }  // extern "C"

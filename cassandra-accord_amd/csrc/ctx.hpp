@@ -64,10 +64,19 @@ struct acc_ctx {
     std::unordered_map<std::string, int> slot_index;
     std::vector<acc::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
+    // counters of the last call (name -> value), exposed by acc_stats_*
+    std::vector<std::pair<std::string, uint64_t>> stats;
+    void stat(const char *name, uint64_t value)
+    {
+        for (auto &kv : stats)
+            if (kv.first == name) { kv.second = value; return; }
+        stats.emplace_back(name, value);
+    }
     // last results
     acc_keydeps_view kd_view{};
     acc_merge_view merge_view{};
     bool kd_valid = false;
+    bool merge_valid = false;
 
     // Grow-only named device buffer. Contents are NOT preserved across growth.
     template <class T>

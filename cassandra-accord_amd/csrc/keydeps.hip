@@ -48,6 +48,11 @@ __device__ __forceinline__ uint32_t witnesses(uint32_t kind)
     }
 }
 
+struct TsPlan {
+    Runs r0, r1, r2;
+    int b0, b1, b2;
+};
+
 enum : uint32_t {
     ERR_BAD_STATUS = 1u << 0,
     ERR_BAD_KIND = 1u << 1,
@@ -85,11 +90,16 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, const uint64_t *
                                                     const uint64_t *__restrict__ el, const int32_t *__restrict__ en,
                                                     const uint8_t *__restrict__ status, const uint32_t *__restrict__ key_off,
                                                     const uint64_t *__restrict__ key_code, uint32_t *__restrict__ owner,
-                                                    uint64_t *__restrict__ g)
+                                                    uint32_t *__restrict__ bflag, uint64_t *__restrict__ g)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     uint64_t m0 = 0, m1 = 0, m2 = 0, errs = 0, unsorted = 0;
+    int differs = 0;
     if (t < n) {
+        // executeAt != txnId (Timestamp.equals): these are the only executeAts the sorted-batch
+        // dictionary has to sort
+        differs = tm[t] != em[t] || ts_w1(tl[t]) != ts_w1(el[t]) || tn[t] != en[t];
+        bflag[t] = (uint32_t)differs;
         const uint64_t r0 = tm[0], r1 = ts_w1(tl[0]), r2 = ts_w2(tn[0]);
         m0 = (tm[t] ^ r0) | (em[t] ^ r0);
         m1 = (ts_w1(tl[t]) ^ r1) | (ts_w1(el[t]) ^ r1);
@@ -110,6 +120,74 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, const uint64_t *
     }
     uint64_t v[6] = { m0, m1, m2, 0, errs, unsorted };
     block_or_n<6>(v, g);
+    int nd = __syncthreads_count(differs);
+    if (threadIdx.x == 0 && nd) atomicAdd((unsigned long long *)&g[7], (unsigned long long)nd);
+}
+
+// ---- sorted-batch dictionary: TxnIds are already in order; only the differing executeAts (B) are sorted.
+// rank(txnId_t) = t + |{b in B : b < txnId_t}|, rank(b_k) = k + |{txnIds < b_k}|; exact dense ranks when no
+// executeAt equals another timestamp (checked here; otherwise the general sort recomputes them).
+__global__ __launch_bounds__(BLOCK) void k_b_compact(uint32_t n, const uint32_t *__restrict__ bflag, const uint32_t *__restrict__ bidx,
+                                                     const uint64_t *__restrict__ em, const uint64_t *__restrict__ el,
+                                                     const int32_t *__restrict__ en, const uint64_t *__restrict__ tm,
+                                                     const uint64_t *__restrict__ tl, const int32_t *__restrict__ tn,
+                                                     TsPlan plan, uint64_t *__restrict__ bkey, uint32_t *__restrict__ bsrc,
+                                                     uint64_t *__restrict__ tkey)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    uint64_t c0 = pext_runs(tm[t], plan.r0), c1 = pext_runs(ts_w1(tl[t]), plan.r1), c2 = pext_runs(ts_w2(tn[t]), plan.r2);
+    tkey[t] = (plan.b0 ? (c0 << (plan.b1 + plan.b2)) : 0) | (plan.b1 ? (c1 << plan.b2) : 0) | c2;
+    if (bflag[t]) {
+        c0 = pext_runs(em[t], plan.r0); c1 = pext_runs(ts_w1(el[t]), plan.r1); c2 = pext_runs(ts_w2(en[t]), plan.r2);
+        uint32_t b = bidx[t];
+        bkey[b] = (plan.b0 ? (c0 << (plan.b1 + plan.b2)) : 0) | (plan.b1 ? (c1 << plan.b2) : 0) | c2;
+        bsrc[b] = t;
+    }
+}
+
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v)
+{
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rank_txn_sorted(uint32_t n, uint32_t nb, const uint64_t *__restrict__ tkey,
+                                                           const uint64_t *__restrict__ sb, const uint32_t *__restrict__ bflag,
+                                                           uint32_t *__restrict__ rank, uint32_t *__restrict__ txn_of_rank,
+                                                           uint64_t *__restrict__ g)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t tie = 0;
+    if (t < n) {
+        uint32_t lb = lower_bound_u64(sb, 0, nb, tkey[t]);
+        if (lb < nb && sb[lb] == tkey[t]) tie = 1;
+        uint32_t r = t + lb;
+        rank[t] = r;
+        txn_of_rank[r] = t;
+        if (!bflag[t]) rank[n + t] = r;
+    }
+    uint64_t v[1] = { tie };
+    block_or_n<1>(v, g + 6);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rank_b_sorted(uint32_t n, uint32_t nb, const uint64_t *__restrict__ tkey,
+                                                         const uint64_t *__restrict__ sb, const uint32_t *__restrict__ sperm,
+                                                         const uint32_t *__restrict__ bsrc, uint32_t *__restrict__ rank,
+                                                         uint64_t *__restrict__ g)
+{
+    uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t tie = 0;
+    if (k < nb) {
+        if (k > 0 && sb[k] == sb[k - 1]) tie = 1;
+        uint32_t t = bsrc[sperm[k]];
+        rank[n + t] = k + lower_bound_u64(tkey, 0, n, sb[k]);
+    }
+    uint64_t v[1] = { tie };
+    block_or_n<1>(v, g + 6);
 }
 
 // grid-stride: a few hundred blocks, each ORs many codes before its single atomic
@@ -124,11 +202,6 @@ __global__ __launch_bounds__(BLOCK) void k_prep_keys(size_t P, const uint64_t *_
 }
 
 // ---------------------------------------------------------------- dictionary (order ranks)
-
-struct TsPlan {
-    Runs r0, r1, r2;
-    int b0, b1, b2;
-};
 
 // i < N: TxnId of txn i; i >= N: executeAt of txn i-N. word_sel < 0: whole compacted key (fits 64 bits);
 // else the compaction of that single word.
@@ -800,14 +873,19 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
     cnt_out[j] = e;
 }
 
-// ---- write pass: one wave per txn. Lane k computes the 7 runs of key k from the count pass record
-// (R1/R2 per kind class, R3); all lanes then gather the flattened runs in parallel, drop T itself and
-// non-qualifying R3 entries by ballot compaction into LDS, sort (value << 16 | key) and emit the Java layout.
+// ---- write pass, three tiers by E_T (dependency entries of the txn; 98.7% of config-2 txns have <= 64):
+//   small  (E <= 64,  <= 32 keys): one wave per txn, registers + 512 B of LDS staging, high occupancy
+//   medium (E <= 1024, <= 64 keys): one wave per txn, bitonic sort of (value << 16 | key) in LDS
+//   big    (E <= 8192, <= 64 keys): one block per txn, bitonic sort in 64 KiB of LDS
+//   fallback (otherwise, rare):      global gather + two radix sorts
+// Every tier: lane k derives the 7 runs of key k (R1/R2 per kind class, R3) from the count-pass record,
+// the runs are gathered flattened by all lanes, T itself and non-qualifying R3 entries are dropped.
 
-constexpr int WCAP = 1024;          // entries per wave in LDS
-constexpr int WMAXK = 64;           // keys per txn on the wave path (one lane per key)
-constexpr int WPB = WAVES;          // waves (txns) per block
 constexpr int NRUN = 7;
+constexpr int SMALL_E = 64, SMALL_K = 32;
+constexpr int MED_E = 1024, MED_K = 64;
+constexpr int BIG_K = 64;
+constexpr int BIG_E = 8192;                 // entries per block in LDS (64 KiB)
 
 struct V2Out {
     const uint32_t *key_off;
@@ -818,9 +896,148 @@ struct V2Out {
     int32_t *arena;
     uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
     uint64_t *u_cnt;
-    uint32_t *big;           // 1 = txn left for the global path
-    uint64_t *gstat;         // [0] big txns, [1] their entries, [2] internal count mismatches
+    uint32_t *med_list, *big_list, *fb_list;
+    uint64_t *gstat;         // [0] medium, [1] big, [2] count mismatches, [3] fallback txns, [4] fallback entries
 };
+
+template <int MAXK>
+struct RunsT {
+    uint32_t start[MAXK][NRUN];
+    uint32_t pre[MAXK][NRUN + 1];
+    uint32_t kbase[MAXK + 1];
+    uint32_t m[MAXK];
+    uint32_t kc[MAXK];
+    uint32_t lo, hi;         // value range of all runs (big tier)
+    uint32_t total;
+};
+
+struct TxnCtx {
+    uint32_t t, j0, j1, nk, E, trank, wk, wc;
+    uint64_t e0;
+    bool bq;
+};
+
+__device__ __forceinline__ TxnCtx txn_ctx(const V2View &v, const V2Out &o, uint32_t t)
+{
+    TxnCtx c;
+    c.t = t;
+    c.j0 = o.key_off[t]; c.j1 = o.key_off[t + 1]; c.nk = c.j1 - c.j0;
+    c.e0 = o.dep_off[c.j0];
+    c.E = (uint32_t)(o.dep_off[c.j1] - c.e0);
+    c.trank = v.rank[t];
+    c.bq = v.rank[v.n + t] != c.trank;
+    c.wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u);
+    c.wc = wk_classes(c.wk);
+    return c;
+}
+
+// Called by ONE wave: lane k < nk fills the runs of key k. Returns the flattened raw length.
+template <int MAXK>
+__device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o, const uint64_t *cnt, const TxnCtx &c,
+                                 bool want_range)
+{
+    const uint32_t lane = lane_id();
+    uint32_t ktot = 0, lo = 0xFFFFFFFFu, hi = 0;
+    if (lane < c.nk && cnt[c.j0 + lane] != 0) {
+        const uint32_t j = c.j0 + lane;
+        uint4 r = o.rec[j];
+        const uint32_t s0 = r.x, pos = r.y, posm = r.z, m = r.w;
+        const bool has_m = m != NO_M;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int cl = 0; cl < 3; ++cl) {
+            uint32_t a0 = 0, l0 = 0, a1 = 0, l1 = 0;
+            if ((c.wc >> cl) & 1u) {
+                const uint32_t *cu = v.cnt + (size_t)cl * v.P1, *cc = v.cnt + (size_t)(3 + cl) * v.P1;
+                a0 = v.bases[cl] + cu[s0]; l0 = cu[pos] - cu[s0];
+                uint32_t from = has_m ? posm : s0;
+                a1 = v.bases[3 + cl] + cc[from]; l1 = cc[pos] - cc[from];
+                if (want_range) {
+                    if (l0) { lo = min(lo, v.list_rank[a0]); hi = max(hi, v.list_rank[a0 + l0 - 1]); }
+                    if (l1) { lo = min(lo, v.list_rank[a1]); hi = max(hi, v.list_rank[a1 + l1 - 1]); }
+                }
+            }
+            R.start[lane][2 * cl] = a0; R.pre[lane][2 * cl] = acc; acc += l0;
+            R.start[lane][2 * cl + 1] = a1; R.pre[lane][2 * cl + 1] = acc; acc += l1;
+        }
+        uint32_t bs = 0, bl = 0;
+        if (has_m) {
+            bs = o.rec_bstart[j];
+            bl = v.cbc[posm] - bs;
+            if (want_range && bl) { lo = min(lo, v.bc_rank[bs]); hi = max(hi, v.bc_rank[bs + bl - 1]); }
+        }
+        R.start[lane][6] = bs; R.pre[lane][6] = acc; acc += bl;
+        R.pre[lane][7] = acc;
+        R.m[lane] = m;
+        ktot = acc;
+    } else if (lane < c.nk) {
+        for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
+        R.m[lane] = NO_M;
+    }
+    if (lane < (uint32_t)MAXK) R.kc[lane] = 0;
+    uint32_t incl = wave_inclusive(ktot, OpAdd<uint32_t>());
+    if (lane < c.nk) R.kbase[lane] = incl - ktot;
+    uint32_t total = shfl_idx(incl, 63);
+    if (want_range) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor(lo, d, 64));
+            hi = max(hi, (uint32_t)__shfl_xor(hi, d, 64));
+        }
+    }
+    if (lane == 0) { R.kbase[c.nk] = total; R.lo = lo; R.hi = hi; R.total = total; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    return total;
+}
+
+// Element e of the flattened runs: value x, key k; returns whether it is an entry of the txn's deps.
+template <int MAXK>
+__device__ __forceinline__ bool fetch_elem(const RunsT<MAXK> &R, const V2View &v, const TxnCtx &c, uint32_t e,
+                                           uint32_t &x, uint32_t &k)
+{
+    uint32_t lo = 0, hi = c.nk;
+    while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
+    k = lo;
+    uint32_t off = e - R.kbase[k];
+    uint32_t r = 0;
+    while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
+    uint32_t idx = R.start[k][r] + (off - R.pre[k][r]);
+    bool keep;
+    if (r < 6) {
+        x = v.list_rank[idx];
+        keep = true;
+    } else {
+        x = v.bc_rank[idx];
+        keep = v.bc_exec[idx] >= R.m[k] && ((c.wk >> v.bc_kind[idx]) & 1u);
+    }
+    return keep && !(c.bq && x == c.trank);
+}
+
+// Gather the flattened runs into buf (compacted, at most cap entries). Returns the kept count.
+template <int MAXK>
+__device__ uint32_t gather_to(uint64_t *buf, uint32_t cap, const RunsT<MAXK> &R, const V2View &v, const TxnCtx &c,
+                              uint32_t total)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t cursor = 0;
+    for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+        uint32_t e = c0 + lane;
+        bool keep = false;
+        uint32_t x = 0, k = 0;
+        if (e < total) keep = fetch_elem(R, v, c, e, x, k);
+        uint64_t bal = __ballot(keep);
+        if (keep) {
+            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+            if (slot < cap) buf[slot] = ((uint64_t)x << 16) | k;
+        }
+        cursor += (uint32_t)__popcll(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    return cursor;
+}
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
 {
@@ -867,7 +1084,7 @@ __device__ __forceinline__ uint64_t wave_bitonic_reg(uint64_t x)
 
 // Emit one chunk of up to 64 sorted entries (lane holds x). Returns the updated distinct count.
 __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t prev, bool has_prev, uint32_t distinct,
-                                               uint32_t *kc, const V2Out &o, uint32_t j0, uint64_t e0, uint64_t abase)
+                                               uint32_t *kc, const V2Out &o, const TxnCtx &c, uint64_t abase)
 {
     const uint32_t lane = lane_id();
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -884,9 +1101,9 @@ __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t pre
     uint32_t before = (uint32_t)__popcll(peers & lt);
     if (in) {
         uint32_t slot = kc[kj] + before;
-        uint64_t kbase = o.dep_off[j0 + kj] - e0;
+        uint64_t kbase = o.dep_off[c.j0 + kj] - c.e0;
         o.arena[abase + kbase + slot] = (int32_t)idx;
-        if (nw) o.dep_scratch[e0 + idx] = o.txn_of_rank[val];
+        if (nw) o.dep_scratch[c.e0 + idx] = o.txn_of_rank[val];
     }
     __builtin_amdgcn_wave_barrier();
     if (in && before == 0) kc[kj] += (uint32_t)__popcll(peers);
@@ -895,143 +1112,157 @@ __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t pre
     return distinct + (uint32_t)__popcll(bal);
 }
 
-struct WaveRuns {
-    uint32_t start[WMAXK][NRUN];   // start index in the run's source array
-    uint32_t pre[WMAXK][NRUN + 1]; // local prefix of run lengths within the key
-    uint32_t kbase[WMAXK + 1];     // flattened base of each key
-    uint32_t m[WMAXK];             // M of the key (R3 filter)
-    uint32_t kc[WMAXK];            // per-key emitted count
-};
-
-__global__ __launch_bounds__(BLOCK) void k_v2_write(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+// Tier routing (run once per txn after the count pass) + per-txn sizes.
+__global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                    const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
+                                                    uint64_t *__restrict__ a_cnt, uint32_t *__restrict__ med_list,
+                                                    uint32_t *__restrict__ big_list, uint64_t *__restrict__ gstat)
 {
-    __shared__ uint64_t sbuf[WPB][WCAP];
-    __shared__ WaveRuns sruns[WPB];
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    bool med = false, big = false;
+    if (t < n) {
+        uint32_t j0 = key_off[t], j1 = key_off[t + 1];
+        uint64_t kd = cnz[j1] - cnz[j0];
+        uint64_t E = dep_off[j1] - dep_off[j0];
+        kd_cnt[t] = kd;
+        a_cnt[t] = kd + E;
+        uint32_t nk = j1 - j0;
+        bool small = E <= SMALL_E && nk <= SMALL_K;
+        med = !small && E <= MED_E && nk <= MED_K;
+        big = !small && !med && E > 0;
+    }
+    // wave-aggregated appends (list order is irrelevant: every txn writes only its own outputs)
+    const uint64_t lt = lane_id() == 0 ? 0ull : (~0ull >> (64 - lane_id()));
+    uint64_t bm = __ballot(med), bb = __ballot(big);
+    uint32_t basem = 0, baseb = 0;
+    if (lane_id() == 0) {
+        if (bm) basem = (uint32_t)atomicAdd((unsigned long long *)&gstat[0], (unsigned long long)__popcll(bm));
+        if (bb) baseb = (uint32_t)atomicAdd((unsigned long long *)&gstat[1], (unsigned long long)__popcll(bb));
+    }
+    basem = shfl_idx(basem, 0);
+    baseb = shfl_idx(baseb, 0);
+    if (med) med_list[basem + __popcll(bm & lt)] = t;
+    if (big) big_list[baseb + __popcll(bb & lt)] = t;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_write_small(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ uint64_t sbuf[WAVES][SMALL_E];
+    __shared__ RunsT<SMALL_K> sruns[WAVES];
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t t = blockIdx.x * WPB + wave;
+    const uint32_t t = blockIdx.x * WAVES + wave;
     if (t >= n) return;
+    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
+    const uint64_t E64 = o.dep_off[j1] - o.dep_off[j0];
+    if (E64 == 0) { if (lane == 0) o.u_cnt[t] = 0; return; }
+    if (E64 > SMALL_E || j1 - j0 > SMALL_K) return;
+    TxnCtx c = txn_ctx(v, o, t);
+    RunsT<SMALL_K> &R = sruns[wave];
     uint64_t *buf = sbuf[wave];
-    WaveRuns &R = sruns[wave];
-    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1], nk = j1 - j0;
-    const uint64_t e0 = o.dep_off[j0];
-    const uint32_t E = (uint32_t)(o.dep_off[j1] - e0);
-    if (E == 0) { if (lane == 0) { o.u_cnt[t] = 0; o.big[t] = 0; } return; }
-    if (E > WCAP || nk > WMAXK) {
-        if (lane == 0) {
-            o.big[t] = 1;
-            atomicAdd((unsigned long long *)&o.gstat[0], 1ull);
-            atomicAdd((unsigned long long *)&o.gstat[1], (unsigned long long)E);
-        }
-        return;
-    }
-    const uint32_t trank = v.rank[t];
-    const bool bq = v.rank[v.n + t] != trank;
-    const uint32_t wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u), wc = wk_classes(wk);
-    // ---- lane k: runs of key k
-    uint32_t ktot = 0;
-    if (lane < nk && cnt[j0 + lane] != 0) {
-        const uint32_t j = j0 + lane;
-        uint4 r = o.rec[j];
-        const uint32_t s0 = r.x, pos = r.y, posm = r.z, m = r.w;
-        const bool has_m = m != NO_M;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            uint32_t a0 = 0, l0 = 0, a1 = 0, l1 = 0;
-            if ((wc >> c) & 1u) {
-                const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
-                a0 = v.bases[c] + cu[s0]; l0 = cu[pos] - cu[s0];
-                uint32_t from = has_m ? posm : s0;
-                a1 = v.bases[3 + c] + cc[from]; l1 = cc[pos] - cc[from];
-            }
-            R.start[lane][2 * c] = a0; R.pre[lane][2 * c] = acc; acc += l0;
-            R.start[lane][2 * c + 1] = a1; R.pre[lane][2 * c + 1] = acc; acc += l1;
-        }
-        uint32_t bs = 0, bl = 0;
-        if (has_m) { bs = o.rec_bstart[j]; bl = v.cbc[posm] - bs; }
-        R.start[lane][6] = bs; R.pre[lane][6] = acc; acc += bl;
-        R.pre[lane][7] = acc;
-        R.m[lane] = m;
-        ktot = acc;
-    } else if (lane < nk) {
-        for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
-        R.m[lane] = NO_M;
-    }
-    if (lane < WMAXK) R.kc[lane] = 0;
-    uint32_t ktot_total;
-    {
-        // wave exclusive scan of per-key totals (lanes >= nk contribute 0)
-        uint32_t incl = wave_inclusive(ktot, OpAdd<uint32_t>());
-        uint32_t excl = incl - ktot;
-        if (lane < nk) R.kbase[lane] = excl;
-        ktot_total = shfl_idx(incl, 63);
-        if (lane == 0) R.kbase[nk] = ktot_total;
-    }
+    uint32_t total = compute_runs(R, v, o, cnt, c, false);
+    uint32_t got = gather_to(buf, SMALL_E, R, v, c, total);
+    if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
+    const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+    uint64_t x = lane < c.E ? buf[lane] : ~0ull;
+    x = wave_bitonic_reg(x);
+    uint64_t prev = shfl_up(x, 1);
+    uint32_t distinct = emit_chunk(x, lane < c.E, prev, lane > 0, 0, R.kc, o, c, abase);
+    if (lane == 0) o.u_cnt[t] = distinct;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_write_medium(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
+                                                           const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ uint64_t sbuf[WAVES][MED_E];
+    __shared__ RunsT<MED_K> sruns[WAVES];
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t i = blockIdx.x * WAVES + wave;
+    if (i >= cnt_list) return;
+    const uint32_t t = list[i];
+    TxnCtx c = txn_ctx(v, o, t);
+    RunsT<MED_K> &R = sruns[wave];
+    uint64_t *buf = sbuf[wave];
+    uint32_t total = compute_runs(R, v, o, cnt, c, false);
+    uint32_t got = gather_to(buf, MED_E, R, v, c, total);
+    if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
+    const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+    uint32_t n2 = 128;
+    while (n2 < c.E) n2 <<= 1;
+    for (uint32_t q = c.E + lane; q < n2; q += 64) buf[q] = ~0ull;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // ---- flattened gather with filtering, compacted into buf
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint32_t cursor = 0;
-    for (uint32_t c0 = 0; c0 < ktot_total; c0 += 64) {
-        uint32_t e = c0 + lane;
-        bool keep = false;
-        uint64_t item = 0;
-        if (e < ktot_total) {
-            // key: last kbase <= e
-            uint32_t lo = 0, hi = nk;
-            while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
-            uint32_t k = lo, off = e - R.kbase[k];
-            uint32_t r = 0;
-            while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
-            uint32_t idx = R.start[k][r] + (off - R.pre[k][r]);
-            uint32_t x;
-            if (r < 6) {
-                x = v.list_rank[idx];
-                keep = true;
-            } else {
-                x = v.bc_rank[idx];
-                keep = v.bc_exec[idx] >= R.m[k] && ((wk >> v.bc_kind[idx]) & 1u);
-            }
-            keep = keep && !(bq && x == trank);
-            item = ((uint64_t)x << 16) | k;
-        }
-        uint64_t bal = __ballot(keep);
-        if (keep) {
-            uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-            if (slot < WCAP) buf[slot] = item;
-        }
-        cursor += (uint32_t)__popcll(bal);
-    }
-    if (cursor != E) {   // count and gather disagree: internal invariant violation (ACC_E_STATE)
-        if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
-        return;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const uint32_t kd = o.cnz[j1] - o.cnz[j0];
-    const uint64_t abase = o.arena_off[t] + kd;
+    wave_bitonic_lds(buf, n2);
     uint32_t distinct = 0;
-    if (E <= 64) {
-        uint64_t x = lane < E ? buf[lane] : ~0ull;
-        x = wave_bitonic_reg(x);
-        uint64_t prev = shfl_up(x, 1);
-        distinct = emit_chunk(x, lane < E, prev, lane > 0, 0, R.kc, o, j0, e0, abase);
-    } else {
-        uint32_t n2 = 128;
-        while (n2 < E) n2 <<= 1;
-        for (uint32_t i = E + lane; i < n2; i += 64) buf[i] = ~0ull;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        wave_bitonic_lds(buf, n2);
-        for (uint32_t c = 0; c < E; c += 64) {
-            uint32_t i = c + lane;
-            bool in = i < E;
-            uint64_t x = in ? buf[i] : 0;
-            uint64_t prev = i > 0 ? buf[i - 1] : 0;
-            distinct = emit_chunk(x, in, prev, i > 0, distinct, R.kc, o, j0, e0, abase);
+    for (uint32_t q0 = 0; q0 < c.E; q0 += 64) {
+        uint32_t q = q0 + lane;
+        bool in = q < c.E;
+        uint64_t x = in ? buf[q] : 0;
+        uint64_t prev = q > 0 ? buf[q - 1] : 0;
+        distinct = emit_chunk(x, in, prev, q > 0, distinct, R.kc, o, c, abase);
+    }
+    if (lane == 0) o.u_cnt[t] = distinct;
+}
+
+// Big tier: one block per txn (E <= BIG_E). Wave 0 gathers the runs into LDS, the block bitonic-sorts
+// (value << 16 | key), wave 0 emits with the same per-key running counts as the other tiers.
+__global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
+                                                        const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ uint64_t buf[BIG_E];
+    __shared__ RunsT<BIG_K> R;
+    __shared__ uint32_t got_s;
+    const uint32_t b = blockIdx.x;
+    if (b >= cnt_list) return;
+    const uint32_t t = list[b];
+    TxnCtx c = txn_ctx(v, o, t);
+    if (c.nk > BIG_K || c.E > BIG_E) {
+        if (threadIdx.x == 0) {
+            uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[3], 1ull);
+            atomicAdd((unsigned long long *)&o.gstat[4], (unsigned long long)c.E);
+            o.fb_list[f] = t;
+        }
+        return;
+    }
+    if (threadIdx.x < 64) {
+        uint32_t total = compute_runs(R, v, o, cnt, c, false);
+        uint32_t got = gather_to(buf, BIG_E, R, v, c, total);
+        if (threadIdx.x == 0) got_s = got;
+    }
+    __syncthreads();
+    if (got_s != c.E) {
+        if (threadIdx.x == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
+        return;
+    }
+    uint32_t n2 = 128;
+    while (n2 < c.E) n2 <<= 1;
+    for (uint32_t q = c.E + threadIdx.x; q < n2; q += BLOCK) buf[q] = ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
+                uint32_t l = i ^ jj;
+                if (l > i) {
+                    uint64_t x = buf[i], y = buf[l];
+                    bool up = (i & k) == 0;
+                    if ((x > y) == up) { buf[i] = y; buf[l] = x; }
+                }
+            }
+            __syncthreads();
         }
     }
-    if (lane == 0) { o.u_cnt[t] = distinct; o.big[t] = 0; }
+    if (threadIdx.x < 64) {
+        const uint32_t lane = lane_id();
+        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+        uint32_t distinct = 0;
+        for (uint32_t q0 = 0; q0 < c.E; q0 += 64) {
+            uint32_t q = q0 + lane;
+            bool in = q < c.E;
+            uint64_t x = in ? buf[q] : 0;
+            uint64_t prev = q > 0 ? buf[q - 1] : 0;
+            distinct = emit_chunk(x, in, prev, q > 0, distinct, R.kc, o, c, abase);
+        }
+        if (lane == 0) o.u_cnt[t] = distinct;
+    }
 }
 
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
@@ -1042,7 +1273,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
                                                          int rbits, uint64_t *__restrict__ gkey)
 {
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t b = blockIdx.x * WPB + wave;
+    const uint32_t b = blockIdx.x * WAVES + wave;
     if (b >= nbig) return;
     const uint32_t t = big_list[b];
     uint64_t *out = gkey + big_off[b];
@@ -1136,28 +1367,16 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_arena(uint64_t m, const uint32
     arena[arena_off[t] + kd + (i - big_off[b])] = (int32_t)idx_by_pos1[sval2[i]];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_big_list(uint32_t n, const uint32_t *__restrict__ big, const uint32_t *__restrict__ big_idx,
-                                                       const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                       uint32_t *__restrict__ big_list, uint64_t *__restrict__ big_e)
+__global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t *__restrict__ fb_list,
+                                                    const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                    uint64_t *__restrict__ fb_e)
 {
-    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= n || !big[t]) return;
-    uint32_t b = big_idx[t];
-    big_list[b] = t;
-    big_e[b] = dep_off[key_off[t + 1]] - dep_off[key_off[t]];
+    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nfb) return;
+    uint32_t t = fb_list[i];
+    fb_e[i] = dep_off[key_off[t + 1]] - dep_off[key_off[t]];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                    const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
-                                                    uint64_t *__restrict__ a_cnt)
-{
-    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= n) return;
-    uint32_t j0 = key_off[t], j1 = key_off[t + 1];
-    uint64_t kd = cnz[j1] - cnz[j0];
-    kd_cnt[t] = kd;
-    a_cnt[t] = kd + (dep_off[j1] - dep_off[j0]);
-}
 
 __global__ __launch_bounds__(BLOCK) void k_u32_from_u64(size_t n, const uint64_t *__restrict__ in, uint32_t *__restrict__ out)
 {
@@ -1170,7 +1389,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_compact(uint32_t n, const uint32_t
                                                       uint32_t *__restrict__ dep_txn)
 {
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t t = blockIdx.x * WPB + wave;
+    const uint32_t t = blockIdx.x * WAVES + wave;
     if (t >= n) return;
     uint64_t src = dep_off[key_off[t]];
     uint64_t dst = u_off[t], len = u_off[t + 1] - dst;
@@ -1334,8 +1553,9 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     uint64_t *g = ctx->get<uint64_t>("g", 8);
     uint32_t *owner = ctx->get<uint32_t>("owner", P);
     ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
+    uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
     launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, status,
-           key_off, key_code, owner, g);
+           key_off, key_code, owner, bflag, g);
     launch(ctx, "prep_keys", k_prep_keys, dim3(std::min<unsigned>(grid_for(P, BLOCK), 1024u)), dim3(BLOCK), 0, P,
            key_code, g);
     // the last key_off entry must equal P
@@ -1361,6 +1581,8 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     uint32_t *flag = ctx->get<uint32_t>("rank_flag", m);
     uint32_t *incl = ctx->get<uint32_t>("rank_incl", m);
     const unsigned gm = grid_for(m, BLOCK);
+    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
+    auto general_ranks = [&]() {
     Sorted ts_sorted;
     if (plan.b0 + plan.b1 + plan.b2 <= 64) {
         uint64_t *ck = ctx->get<uint64_t>("ts_ckey", m);
@@ -1396,7 +1618,6 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
                (const uint64_t *)c[0], (const uint64_t *)c[1], (const uint64_t *)c[2], (const uint64_t *)nullptr, flag);
     }
     scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, incl, m, false);
-    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
     launch(ctx, "rank_scatter", k_rank_scatter, dim3(gm), dim3(BLOCK), 0, m, n, (const uint32_t *)ts_sorted.vals,
            (const uint32_t *)incl, rank, txn_of_rank);
     {
@@ -1405,6 +1626,31 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
         launch(ctx, "dup_txn", k_dup_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
         launch(ctx, "exec_ties", k_exec_ties, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
     }
+    };
+    const uint64_t nb = hg[7];
+    bool fast_dict = batch_sorted && plan.b0 + plan.b1 + plan.b2 <= 64 && nb < n;
+    if (fast_dict) {
+        uint32_t *bidx = ctx->get<uint32_t>("bidx", (size_t)n + 1);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, bflag, bidx, n, true, bidx + n);
+        uint64_t *bkey = ctx->get<uint64_t>("bkey", nb);
+        uint32_t *bsrc = ctx->get<uint32_t>("bsrc", nb);
+        uint64_t *tkey = ctx->get<uint64_t>("tkey", n);
+        launch(ctx, "b_compact", k_b_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bflag,
+               (const uint32_t *)bidx, em, el, en, tm, tl, tn, plan, bkey, bsrc, tkey);
+        Sorted sb = radix_sort(ctx, "rs_b", bkey, nullptr, nb, plan.b0 + plan.b1 + plan.b2);
+        launch(ctx, "rank_txn_sorted", k_rank_txn_sorted, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (uint32_t)nb,
+               (const uint64_t *)tkey, (const uint64_t *)sb.keys, (const uint32_t *)bflag, rank, txn_of_rank, g);
+        launch(ctx, "rank_b_sorted", k_rank_b_sorted, dim3(grid_for(nb, BLOCK)), dim3(BLOCK), 0, n, (uint32_t)nb,
+               (const uint64_t *)tkey, (const uint64_t *)sb.keys, (const uint32_t *)sb.vals, (const uint32_t *)bsrc, rank, g);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, g + 6, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        if (ctx->pinned[0]) {   // an executeAt equals another timestamp: dense ranks need the general dictionary
+            ACC_HIP(hipMemsetAsync(g + 6, 0, sizeof(uint64_t), st));
+            fast_dict = false;
+        }
+    }
+    if (!fast_dict) general_ranks();
+    ctx->stat("keydeps.fast_dictionary", fast_dict ? 1 : 0);
     const int rbits = bits_for(m - 1);
 
     // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
@@ -1484,6 +1730,9 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     memcpy(htot, ctx->pinned, sizeof htot);
     check_errors(ctx->pinned[4]);
     const bool ties = ctx->pinned[6] != 0;
+    ctx->stat("keydeps.path_replay", ties || (ctx->flags & ACC_OPT_FORCE_REPLAY) ? 1 : 0);
+    ctx->stat("keydeps.exec_ties", ties ? 1 : 0);
+    ctx->stat("keydeps.batch_sorted", batch_sorted ? 1 : 0);
     if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
         keydeps_v1_tail(ctx, in, view, n, P, rbits, status, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
                         s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
@@ -1522,72 +1771,87 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     scan<uint32_t, OpAdd<uint32_t>>(ctx, nz, cnz, P, true, cnz + P);
     uint64_t *kd_cnt = ctx->get<uint64_t>("kd_cnt", n);
     uint64_t *a_cnt = ctx->get<uint64_t>("a_cnt", n);
+    uint32_t *med_list = ctx->get<uint32_t>("v2_med_list", n);
+    uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", n);
+    uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", n);
+    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 8);
+    ACC_HIP(hipMemsetAsync(gstat, 0, 8 * sizeof(uint64_t), st));
     launch(ctx, "v2_sizes", k_v2_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
-           (const uint32_t *)cnz, kd_cnt, a_cnt);
+           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, gstat);
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, kd_off, n, true, kd_off + n);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, arena_off, n, true, arena_off + n);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, dep_off + P, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gstat, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
+    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2];
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
 
-    // ---- write pass
+    // ---- write pass (three tiers)
     int32_t *arena = ctx->get<int32_t>("arena", P + E);
     uint32_t *key_idx = ctx->get<uint32_t>("key_idx", P);
     uint32_t *dep_scratch = ctx->get<uint32_t>("v2_dep_scratch", E);
     uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
-    uint32_t *big = ctx->get<uint32_t>("v2_big", n);
-    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 4);
-    ACC_HIP(hipMemsetAsync(gstat, 0, 4 * sizeof(uint64_t), st));
     V2Out wo;
     wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
-    wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.big = big; wo.gstat = gstat;
-    wo.rec = rec; wo.rec_bstart = rec_bstart;
-    launch(ctx, "v2_write", k_v2_write, dim3((n + WPB - 1) / WPB), dim3(BLOCK), 0, n, vv, (const uint64_t *)cnt, wo);
+    wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
+    wo.rec = rec; wo.rec_bstart = rec_bstart; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+    launch(ctx, "v2_write_small", k_v2_write_small, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, vv,
+           (const uint64_t *)cnt, wo);
+    if (nmed)
+        launch(ctx, "v2_write_medium", k_v2_write_medium, dim3((unsigned)((nmed + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+               (uint32_t)nmed, (const uint32_t *)med_list, vv, (const uint64_t *)cnt, wo);
+    if (nbig)
+        launch(ctx, "v2_write_big", k_v2_write_big, dim3((unsigned)nbig), dim3(BLOCK), 0, (uint32_t)nbig,
+               (const uint32_t *)big_list, vv, (const uint64_t *)cnt, wo);
     launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
            key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
            (const uint64_t *)arena_off, key_idx, arena);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
-    const uint64_t nbig = ctx->pinned[0], ebig = ctx->pinned[1];
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
-    if (nbig) {
-        uint32_t *big_idx = ctx->get<uint32_t>("v2_big_idx", n);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, big, big_idx, n, true);
-        uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", nbig);
-        uint64_t *big_e = ctx->get<uint64_t>("v2_big_e", nbig);
-        uint64_t *big_off = ctx->get<uint64_t>("v2_big_off", nbig + 1);
-        launch(ctx, "v2_big_list", k_v2_big_list, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)big,
-               (const uint32_t *)big_idx, key_off, (const uint64_t *)dep_off, big_list, big_e);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, big_e, big_off, nbig, true, big_off + nbig);
-        const int bbits = bits_for(nbig - 1);
+    const uint64_t nfb = ctx->pinned[3], efb = ctx->pinned[4];
+    ctx->stat("keydeps.medium_txns", nmed);
+    ctx->stat("keydeps.big_txns", nbig);
+    ctx->stat("keydeps.fallback_txns", nfb);
+    ctx->stat("keydeps.fallback_entries", efb);
+    ctx->stat("keydeps.bumped_committed", nbc);
+    if (nfb) {
+        // txns whose dependency-rank range exceeds the bitmap tier (or > 64 keys): gather to global memory,
+        // sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
+        uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
+        uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
+        launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
+               (const uint32_t *)fb_list, key_off, (const uint64_t *)dep_off, fb_e);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
+        const int bbits = bits_for(nfb - 1);
         if (bbits + rbits + 16 > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
-        uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", ebig);
-        launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nbig + WPB - 1) / WPB)), dim3(BLOCK), 0,
-               (uint32_t)nbig, (const uint32_t *)big_list, (const uint64_t *)big_off, vv, (const uint64_t *)cnt, key_off,
+        uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
+        launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+               (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)cnt, key_off,
                rbits, gkey);
-        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, ebig, bbits + rbits + 16);
-        uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", ebig);
-        uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", ebig);
-        launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig,
+        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + 16);
+        uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
+        uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
+        launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
                (const uint64_t *)s1.keys, rbits, nflag);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, ebig, false);
-        uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", ebig);
-        uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", ebig);
-        launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig, (const uint64_t *)s1.keys,
-               (const uint32_t *)nincl, (const uint32_t *)big_list, (const uint64_t *)big_off, rbits, key_off,
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
+        uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
+        uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
+        launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
+               (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, key_off,
                (const uint64_t *)dep_off, (const uint32_t *)txn_of_rank, dep_scratch, u_cnt, idx1, key2);
-        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, ebig, bbits + 16 + rbits);
-        launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(ebig, BLOCK)), dim3(BLOCK), 0, ebig,
-               (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)big_list,
-               (const uint64_t *)big_off, rbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
+        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + 16 + rbits);
+        launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
+               (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
+               (const uint64_t *)fb_off, rbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
     }
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
     uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
-    launch(ctx, "v2_compact", k_v2_compact, dim3((n + WPB - 1) / WPB), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
+    launch(ctx, "v2_compact", k_v2_compact, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
            (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));

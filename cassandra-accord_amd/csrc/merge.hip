@@ -1,9 +1,364 @@
-// merge.hip — batched KeyDeps.merge (placeholder until the union kernels land).
+// merge.hip — batched KeyDeps.merge (primitives/KeyDeps.java:115-135) for many coordinated txns.
+//
+// The reference folds replies left to right with RelationMultiMap.linearUnion through a LinearMerger
+// (utils/RelationMultiMap.java:284-406, 561-816), skipping empty replies (KeyDeps.isEmpty,
+// KeyDeps.java:292-295: no entries). Its result is the canonical union (KeyDepsTest.testMergedProperty,
+// KeyDepsTest.java:275-283): keys = sorted union of the non-empty replies' key arrays, txnIds = sorted
+// union of their txnId arrays (unreferenced ids included), and per key the sorted union of referenced ids.
+// Here every group (one coordinated txn) is merged at once:
+//   1. expand: (group, key), (group, value) and (group, key, value) records of the non-empty replies,
+//      written at their input offsets (header slots and empty replies become all-ones pads);
+//   2. three stable radix sorts of compacted composite keys;
+//   3. unique + per-group counts (scans) -> per-group CSR in Java layout; each (key, value) entry becomes
+//      the index of the value in the group's txnId array (binary search within the group).
 #include "prims.hpp"
+
 namespace acc {
+
+__device__ __forceinline__ void block_or1(uint64_t v, uint64_t *dst)
+{
+    __shared__ uint64_t part[WAVES];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v |= shfl_idx(v, (int)(lane_id() ^ d));
+    if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t x = 0;
+        for (int q = 0; q < WAVES; ++q) x |= part[q];
+        if (x) atomicOr((unsigned long long *)dst, (unsigned long long)x);
+    }
+}
+
+// per reply: group id, emptiness, input validation (KeyDeps ctor check, KeyDeps.java:184-185)
+__global__ __launch_bounds__(BLOCK) void k_m_replies(uint32_t ng, const uint64_t *__restrict__ grp_off, uint32_t *__restrict__ grp_of)
+{
+    uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= ng) return;
+    for (uint64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) grp_of[r] = g;
+}
+
+// g[0] key-code varying bits, g[1] txn-rank varying bits, g[2] errors
+__global__ __launch_bounds__(BLOCK) void k_m_prep(uint64_t R, const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
+                                                  const uint64_t *__restrict__ val_off, const uint32_t *__restrict__ txn_rank,
+                                                  const uint64_t *__restrict__ k2v_off, const int32_t *__restrict__ k2v,
+                                                  uint64_t *__restrict__ g)
+{
+    uint64_t r = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t km = 0, vm = 0, err = 0;
+    if (r < R) {
+        const uint64_t k0 = key_code[0], v0 = txn_rank[0];
+        uint64_t ka = key_off[r], kb = key_off[r + 1], va = val_off[r], vb = val_off[r + 1];
+        uint64_t oa = k2v_off[r], ob = k2v_off[r + 1];
+        uint64_t nk = kb - ka, nv = vb - va, no = ob - oa;
+        if (kb < ka || vb < va || ob < oa || no < nk) err |= 1;
+        else {
+            for (uint64_t i = ka; i < kb; ++i) {
+                km |= key_code[i] ^ k0;
+                if (i > ka && key_code[i - 1] >= key_code[i]) err |= 2;   // Keys sorted unique
+            }
+            for (uint64_t i = va; i < vb; ++i) {
+                vm |= (uint64_t)txn_rank[i] ^ v0;
+                if (i > va && txn_rank[i - 1] >= txn_rank[i]) err |= 4;   // txnIds sorted unique
+            }
+            if (nk && (uint64_t)(uint32_t)k2v[oa + nk - 1] != no) err |= 8;   // last offset == length
+            uint64_t prev_end = nk;
+            for (uint64_t i = 0; i < nk && !(err & 8); ++i) {
+                uint64_t end = (uint64_t)(uint32_t)k2v[oa + i];
+                if (end < prev_end || end > no) { err |= 8; break; }
+                for (uint64_t q = prev_end; q < end; ++q) {
+                    int32_t x = k2v[oa + q];
+                    if (x < 0 || (uint64_t)x >= nv) { err |= 16; break; }
+                    if (q > prev_end && k2v[oa + q - 1] >= x) err |= 32;     // ascending unique per key
+                }
+                prev_end = end;
+            }
+        }
+    }
+    block_or1(km, &g[0]);
+    block_or1(vm, &g[1]);
+    block_or1(err, &g[2]);
+}
+
+struct MergePlan {
+    Runs rk, rv;
+    uint64_t pad_k, pad_v, pad_kv;       // all ones in each composite's sorted width: sorts after real records
+    int gshift_k, gshift_v, gshift_kv;   // group field position in each composite
+    int vshift_kv;                        // key field position in the (g, key, value) composite
+};
+
+// One thread per reply: expand its records at the input offsets. Empty replies and header slots: pads.
+__global__ __launch_bounds__(BLOCK) void k_m_expand(uint64_t R, const uint32_t *__restrict__ grp_of,
+                                                    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
+                                                    const uint64_t *__restrict__ val_off, const uint32_t *__restrict__ txn_rank,
+                                                    const uint64_t *__restrict__ k2v_off, const int32_t *__restrict__ k2v,
+                                                    MergePlan plan, uint64_t *__restrict__ sk, uint64_t *__restrict__ sv,
+                                                    uint64_t *__restrict__ skv)
+{
+    uint64_t r = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (r >= R) return;
+    const uint64_t g = grp_of[r];
+    uint64_t ka = key_off[r], kb = key_off[r + 1], va = val_off[r], vb = val_off[r + 1];
+    uint64_t oa = k2v_off[r], ob = k2v_off[r + 1];
+    uint64_t nk = kb - ka;
+    const bool empty = (ob - oa) == nk;
+    for (uint64_t i = ka; i < kb; ++i)
+        sk[i] = empty ? plan.pad_k : (g << plan.gshift_k) | pext_runs(key_code[i], plan.rk);
+    for (uint64_t i = va; i < vb; ++i)
+        sv[i] = empty ? plan.pad_v : (g << plan.gshift_v) | pext_runs(txn_rank[i], plan.rv);
+    for (uint64_t i = 0; i < nk; ++i) skv[oa + i] = plan.pad_kv;
+    uint64_t prev_end = nk;
+    for (uint64_t i = 0; i < nk; ++i) {
+        uint64_t end = (uint64_t)(uint32_t)k2v[oa + i];
+        uint64_t kc = pext_runs(key_code[ka + i], plan.rk);
+        for (uint64_t q = prev_end; q < end; ++q) {
+            uint32_t v = txn_rank[va + (uint32_t)k2v[oa + q]];
+            skv[oa + q] = (g << plan.gshift_kv) | (kc << plan.vshift_kv) | pext_runs(v, plan.rv);
+        }
+        prev_end = end;
+    }
+}
+
+// unique flags: first of each distinct composite (pads excluded)
+__global__ __launch_bounds__(BLOCK) void k_m_uniq(uint64_t n, const uint64_t *__restrict__ s, uint64_t pad,
+                                                  uint64_t *__restrict__ flag)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    flag[i] = s[i] != pad && (i == 0 || s[i] != s[i - 1]);
+}
+
+// per-group unique-record counts from the run boundaries of the sorted composites (records of a group are
+// contiguous): the first record of group g stores its unique index, the last one the index past it
+__global__ __launch_bounds__(BLOCK) void k_m_group_bounds(uint64_t n, const uint64_t *__restrict__ s, uint64_t pad,
+                                                          const uint64_t *__restrict__ flag, const uint64_t *__restrict__ idx,
+                                                          int gshift, uint64_t *__restrict__ gfirst, uint64_t *__restrict__ glast)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || s[i] == pad) return;
+    uint64_t g = s[i] >> gshift;
+    if (i == 0 || (s[i - 1] >> gshift) != g) gfirst[g] = idx[i];
+    if (i + 1 == n || s[i + 1] == pad || (s[i + 1] >> gshift) != g) glast[g] = idx[i] + flag[i];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_m_group_counts(uint32_t ng, const uint64_t *__restrict__ gfirst,
+                                                          const uint64_t *__restrict__ glast, uint64_t *__restrict__ cnt)
+{
+    uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g < ng) cnt[g] = glast[g] - gfirst[g];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_m_write_vals(uint64_t n, const uint64_t *__restrict__ flag, const uint64_t *__restrict__ idx,
+                                                        const uint32_t *__restrict__ txn_rank, const uint32_t *__restrict__ src,
+                                                        uint32_t *__restrict__ out_val)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    out_val[idx[i]] = txn_rank[src[i]];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_m_write_keys(uint64_t n, const uint64_t *__restrict__ flag, const uint64_t *__restrict__ idx,
+                                                        const uint64_t *__restrict__ key_code, const uint32_t *__restrict__ src,
+                                                        uint64_t *__restrict__ out_key)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    out_key[idx[i]] = key_code[src[i]];
+}
+
+__device__ __forceinline__ uint64_t lb_u64(const uint64_t *a, uint64_t lo, uint64_t hi, uint64_t v)
+{
+    while (lo < hi) { uint64_t mid = (lo + hi) >> 1; if (a[mid] < v) lo = mid + 1; else hi = mid; }
+    return lo;
+}
+
+// Entry part of keysToTxnIds: the index of the value in its group's txnIds. Header part: the record that
+// closes a (group, key) run (duplicates included) writes that key's end offset and marks the key.
+__global__ __launch_bounds__(BLOCK) void k_m_write_k2v(uint64_t n, const uint64_t *__restrict__ s, MergePlan plan,
+                                                       const uint64_t *__restrict__ flag, const uint64_t *__restrict__ idx,
+                                                       const uint64_t *__restrict__ kv_gstart, const uint64_t *__restrict__ k_gstart,
+                                                       const uint64_t *__restrict__ v_gstart, const uint32_t *__restrict__ out_val,
+                                                       const uint64_t *__restrict__ out_key, const uint32_t *__restrict__ txn_rank,
+                                                       const uint32_t *__restrict__ src, const uint32_t *__restrict__ val_of_slot,
+                                                       const uint32_t *__restrict__ key_of_slot, const uint64_t *__restrict__ key_code,
+                                                       int32_t *__restrict__ out_k2v, uint8_t *__restrict__ has)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t x = s[i];
+    if (x == plan.pad_kv) return;
+    const uint64_t g = x >> plan.gshift_kv;
+    const uint64_t k0 = k_gstart[g], nk = k_gstart[g + 1] - k0;
+    const uint64_t obase = kv_gstart[g] + k0;      // entries + headers of earlier groups
+    if (flag[i]) {
+        const uint32_t v = txn_rank[val_of_slot[src[i]]];
+        uint64_t lo = v_gstart[g], hi = v_gstart[g + 1];
+        while (lo < hi) { uint64_t mid = (lo + hi) >> 1; if (out_val[mid] < v) lo = mid + 1; else hi = mid; }
+        out_k2v[obase + nk + (idx[i] - kv_gstart[g])] = (int32_t)(lo - v_gstart[g]);
+    }
+    const bool last = i + 1 == n || s[i + 1] == plan.pad_kv || (s[i + 1] >> plan.vshift_kv) != (x >> plan.vshift_kv);
+    if (last) {
+        uint64_t a = lb_u64(out_key, k0, k0 + nk, key_code[key_of_slot[src[i]]]);
+        out_k2v[obase + (a - k0)] = (int32_t)(nk + (idx[i] + flag[i] - kv_gstart[g]));
+        has[a] = 1;
+    }
+}
+
+// keys present only in key arrays (no union entries): end offset = previous key's end
+__global__ __launch_bounds__(BLOCK) void k_m_fix_headers(uint32_t ng, const uint64_t *__restrict__ kv_gstart,
+                                                         const uint64_t *__restrict__ k_gstart, int32_t *__restrict__ out_k2v,
+                                                         const uint8_t *__restrict__ has, uint64_t *__restrict__ out_k2v_off)
+{
+    uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g > ng) return;
+    out_k2v_off[g] = kv_gstart[g] + k_gstart[g];
+    if (g == ng) return;
+    const uint64_t k0 = k_gstart[g], nk = k_gstart[g + 1] - k0;
+    const uint64_t obase = kv_gstart[g] + k0;
+    int32_t prev = (int32_t)nk;
+    for (uint64_t q = 0; q < nk; ++q) {
+        if (!has[k0 + q]) out_k2v[obase + q] = prev;
+        prev = out_k2v[obase + q];
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_widen(uint64_t n, const uint32_t *__restrict__ in, uint64_t *__restrict__ out)
+{
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+// key slot (index into key_code) of every k2v entry position, for the (g, key, value) records
+__global__ __launch_bounds__(BLOCK) void k_m_key_of_slot(uint64_t R, const uint64_t *__restrict__ key_off,
+                                                         const uint64_t *__restrict__ val_off,
+                                                         const uint64_t *__restrict__ k2v_off, const int32_t *__restrict__ k2v,
+                                                         uint32_t *__restrict__ key_of_slot, uint32_t *__restrict__ val_of_slot)
+{
+    uint64_t r = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (r >= R) return;
+    uint64_t ka = key_off[r], nk = key_off[r + 1] - ka, oa = k2v_off[r], va = val_off[r];
+    uint64_t prev_end = nk;
+    for (uint64_t i = 0; i < nk; ++i) {
+        uint64_t end = (uint64_t)(uint32_t)k2v[oa + i];
+        for (uint64_t q = prev_end; q < end; ++q) {
+            key_of_slot[oa + q] = (uint32_t)(ka + i);
+            val_of_slot[oa + q] = (uint32_t)(va + (uint32_t)k2v[oa + q]);
+        }
+        prev_end = end;
+    }
+}
+
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
 {
-    (void)ctx; (void)in; (void)view;
-    fail(ACC_E_STATE, "acc_keydeps_merge: not implemented in this build");
+    if (!in || !view) fail(ACC_E_ARG, "null argument");
+    const uint32_t ng = in->n_groups;
+    const uint64_t R = in->n_replies;
+    hipStream_t st = ctx->stream;
+    ctx->merge_valid = false;
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    const uint64_t *grp_off = stage_in(ctx, "m_grp_off", in->grp_off, (size_t)ng + 1, in->mem);
+    const uint64_t *key_off = stage_in(ctx, "m_key_off", in->key_off, R + 1, in->mem);
+    const uint64_t *val_off = stage_in(ctx, "m_val_off", in->val_off, R + 1, in->mem);
+    const uint64_t *k2v_off = stage_in(ctx, "m_k2v_off", in->k2v_off, R + 1, in->mem);
+    // totals (last offsets) are needed on the host to size the arrays
+    uint64_t tot[3] = { 0, 0, 0 };
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, key_off + R, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, val_off + R, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, k2v_off + R, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    memcpy(tot, ctx->pinned, sizeof tot);
+    const uint64_t NK = tot[0], NV = tot[1], NO = tot[2];
+    if (NK >= 0xFFFFFFFFull || NV >= 0xFFFFFFFFull || NO >= 0xFFFFFFFFull) fail(ACC_E_CAP, "merge input too large");
+    const uint64_t *key_code = stage_in(ctx, "m_key_code", in->key_code, NK, in->mem);
+    const uint32_t *txn_rank = stage_in(ctx, "m_txn_rank", in->txn_rank, NV, in->mem);
+    const int32_t *k2v = stage_in(ctx, "m_k2v", in->k2v, NO, in->mem);
+
+    uint32_t *grp_of = ctx->get<uint32_t>("m_grp_of", R);
+    uint64_t *g = ctx->get<uint64_t>("m_g", 4);
+    ACC_HIP(hipMemsetAsync(g, 0, 4 * 8, st));
+    launch(ctx, "m_replies", k_m_replies, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, grp_off, grp_of);
+    launch(ctx, "m_prep", k_m_prep, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, key_off, key_code, val_off, txn_rank,
+           k2v_off, k2v, g);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 3 * 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t kmask = ctx->pinned[0], vmask = ctx->pinned[1], err = ctx->pinned[2];
+    if (err & 1) fail(ACC_E_ARG, "merge offsets must be non-decreasing and k2v hold a header per key");
+    if (err & 2) fail(ACC_E_ARG, "Keys of a KeyDeps must be sorted and unique");
+    if (err & 4) fail(ACC_E_ARG, "txnIds of a KeyDeps must be sorted and unique");
+    if (err & 8) fail(ACC_E_ARG, "Last key in keyToTxnId does not point to the end of the array");
+    if (err & 16) fail(ACC_E_ARG, "keyToTxnId entry out of range of txnIds");
+    if (err & 32) fail(ACC_E_STATE, "Duplicate value found for key (RelationMultiMap.checkValid)");
+
+    MergePlan plan;
+    plan.rk = make_runs(kmask);
+    plan.rv = make_runs(vmask);
+    const int gb = bits_for(ng ? ng - 1 : 0) + 1;   // +1: real records stay below the all-ones pad
+    const int kb = plan.rk.bits, vb = plan.rv.bits;
+    if (gb + kb + vb > 64) fail(ACC_E_CAP, "merge composite key exceeds 64 bits");
+    plan.gshift_k = kb; plan.gshift_v = vb; plan.gshift_kv = kb + vb; plan.vshift_kv = vb;
+    auto ones = [](int b) { return b >= 64 ? ~0ull : ((1ull << b) - 1); };
+    plan.pad_k = ones(gb + kb); plan.pad_v = ones(gb + vb); plan.pad_kv = ones(gb + kb + vb);
+
+    uint64_t *sk = ctx->get<uint64_t>("m_sk", NK);
+    uint64_t *sv = ctx->get<uint64_t>("m_sv", NV);
+    uint64_t *skv = ctx->get<uint64_t>("m_skv", NO);
+    uint32_t *key_of_slot = ctx->get<uint32_t>("m_key_of_slot", NO);
+    uint32_t *val_of_slot = ctx->get<uint32_t>("m_val_of_slot", NO);
+    launch(ctx, "m_expand", k_m_expand, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, (const uint32_t *)grp_of, key_off,
+           key_code, val_off, txn_rank, k2v_off, k2v, plan, sk, sv, skv);
+    launch(ctx, "m_key_of_slot", k_m_key_of_slot, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, key_off, val_off, k2v_off,
+           k2v, key_of_slot, val_of_slot);
+    Sorted ssk = radix_sort(ctx, "m_rs_k", sk, nullptr, NK, gb + kb);
+    Sorted ssv = radix_sort(ctx, "m_rs_v", sv, nullptr, NV, gb + vb);
+    Sorted sskv = radix_sort(ctx, "m_rs_kv", skv, nullptr, NO, gb + kb + vb);
+
+    struct U { uint64_t *flag, *idx, *gstart; };
+    auto uniq = [&](const char *tag, const Sorted &so, uint64_t n, int gshift, uint64_t pad) {
+        char a[48], b2[48], c[48], d[48], e[48], f[48];
+        snprintf(a, sizeof a, "%s_flag", tag); snprintf(b2, sizeof b2, "%s_idx", tag);
+        snprintf(c, sizeof c, "%s_gstart", tag); snprintf(d, sizeof d, "%s_gfirst", tag);
+        snprintf(e, sizeof e, "%s_glast", tag); snprintf(f, sizeof f, "%s_gcnt", tag);
+        U u{ ctx->get<uint64_t>(a, n), ctx->get<uint64_t>(b2, n + 1), ctx->get<uint64_t>(c, (size_t)ng + 1) };
+        uint64_t *gfirst = ctx->get<uint64_t>(d, ng), *glast = ctx->get<uint64_t>(e, ng), *gcnt = ctx->get<uint64_t>(f, ng);
+        launch(ctx, "m_uniq", k_m_uniq, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)so.keys, pad, u.flag);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, u.flag, u.idx, n, true, u.idx + n);
+        ACC_HIP(hipMemsetAsync(gfirst, 0, (size_t)ng * 8, st));
+        ACC_HIP(hipMemsetAsync(glast, 0, (size_t)ng * 8, st));
+        launch(ctx, "m_group_bounds", k_m_group_bounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)so.keys,
+               pad, (const uint64_t *)u.flag, (const uint64_t *)u.idx, gshift, gfirst, glast);
+        launch(ctx, "m_group_counts", k_m_group_counts, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng,
+               (const uint64_t *)gfirst, (const uint64_t *)glast, gcnt);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, gcnt, u.gstart, ng, true, u.gstart + ng);
+        return u;
+    };
+    U uk = uniq("m_k", ssk, NK, plan.gshift_k, plan.pad_k);
+    U uv = uniq("m_v", ssv, NV, plan.gshift_v, plan.pad_v);
+    U ukv = uniq("m_kv", sskv, NO, plan.gshift_kv, plan.pad_kv);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, uk.gstart + ng, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, uv.gstart + ng, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, ukv.gstart + ng, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t TK = ctx->pinned[0], TV = ctx->pinned[1], TKV = ctx->pinned[2];
+
+    uint64_t *out_key = ctx->get<uint64_t>("m_out_key", TK);
+    uint32_t *out_val = ctx->get<uint32_t>("m_out_val", TV);
+    int32_t *out_k2v = ctx->get<int32_t>("m_out_k2v", TK + TKV);
+    uint8_t *has = ctx->get<uint8_t>("m_has", TK);
+    uint64_t *out_k2v_off = ctx->get<uint64_t>("m_out_k2v_off", (size_t)ng + 1);
+    launch(ctx, "m_write_keys", k_m_write_keys, dim3(grid_for(NK, BLOCK)), dim3(BLOCK), 0, NK, (const uint64_t *)uk.flag,
+           (const uint64_t *)uk.idx, key_code, (const uint32_t *)ssk.vals, out_key);
+    launch(ctx, "m_write_vals", k_m_write_vals, dim3(grid_for(NV, BLOCK)), dim3(BLOCK), 0, NV, (const uint64_t *)uv.flag,
+           (const uint64_t *)uv.idx, txn_rank, (const uint32_t *)ssv.vals, out_val);
+    ACC_HIP(hipMemsetAsync(has, 0, TK ? TK : 1, st));
+    launch(ctx, "m_write_k2v", k_m_write_k2v, dim3(grid_for(NO, BLOCK)), dim3(BLOCK), 0, NO, (const uint64_t *)sskv.keys, plan,
+           (const uint64_t *)ukv.flag, (const uint64_t *)ukv.idx, (const uint64_t *)ukv.gstart, (const uint64_t *)uk.gstart,
+           (const uint64_t *)uv.gstart, (const uint32_t *)out_val, (const uint64_t *)out_key, txn_rank,
+           (const uint32_t *)sskv.vals, (const uint32_t *)val_of_slot, (const uint32_t *)key_of_slot, key_code, out_k2v, has);
+    launch(ctx, "m_fix_headers", k_m_fix_headers, dim3(grid_for((size_t)ng + 1, BLOCK)), dim3(BLOCK), 0, ng,
+           (const uint64_t *)ukv.gstart, (const uint64_t *)uk.gstart, out_k2v, (const uint8_t *)has, out_k2v_off);
+    ctx->sync();
+    *view = acc_merge_view{ ng, TK, TV, TK + TKV, NO, uk.gstart, out_key, uv.gstart, out_val, out_k2v_off, out_k2v };
+    ctx->merge_view = *view;
+    ctx->merge_valid = true;
 }
+
 }  // namespace acc

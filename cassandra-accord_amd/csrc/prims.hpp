@@ -299,7 +299,9 @@ struct Sorted {
 // valid until the next sort with the same tag.
 static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *keys, const uint32_t *vals, size_t n, int bits)
 {
-    char nk0[40], nk1[40], nv0[40], nv1[40], nh[40];
+    char nk0[40], nk1[40], nv0[40], nv1[40], nh[40], th[48], ts[48];
+    snprintf(th, sizeof th, "%s.hist", tag);
+    snprintf(ts, sizeof ts, "%s.scatter", tag);
     snprintf(nk0, sizeof nk0, "%s_k0", tag); snprintf(nk1, sizeof nk1, "%s_k1", tag);
     snprintf(nv0, sizeof nv0, "%s_v0", tag); snprintf(nv1, sizeof nv1, "%s_v1", tag);
     snprintf(nh, sizeof nh, "%s_hist", tag);
@@ -320,9 +322,9 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
         int shift = 8 * p;
-        launch(ctx, "rs_hist", k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, kin, n, shift, hist, ntiles);
+        launch(ctx, th, k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, kin, n, shift, hist, ntiles);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, hist, hist, (size_t)256 * ntiles, true);
-        launch(ctx, "rs_scatter", k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, shift,
+        launch(ctx, ts, k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, shift,
                (const uint32_t *)hist, ntiles, (p == 0 && !vals) ? 1 : 0);
         kin = k[cur];
         vin = v[cur];

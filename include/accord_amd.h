@@ -178,6 +178,18 @@ typedef struct acc_merge_view {
 
 int acc_keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *out_view);
 
+/* Caller-owned copy of the last merge result (two-call sizing as acc_keydeps_out). */
+typedef struct acc_merge_out {
+    uint32_t  mem;
+    uint64_t  cap_keys, cap_vals, cap_k2v;
+    uint64_t  need_keys, need_vals, need_k2v;   /* written */
+    uint64_t *key_off;  uint64_t *key_code;     /* [n_groups+1], [cap_keys] */
+    uint64_t *val_off;  uint32_t *txn_rank;     /* [n_groups+1], [cap_vals] */
+    uint64_t *k2v_off;  int32_t  *k2v;          /* [n_groups+1], [cap_k2v] */
+} acc_merge_out;
+
+int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out);
+
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
  * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).
@@ -198,6 +210,10 @@ int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t
 int  acc_timing_count(acc_ctx *ctx);
 int  acc_timing_get(acc_ctx *ctx, int i, const char **name, double *total_ms, uint64_t *launches);
 void acc_timing_reset(acc_ctx *ctx);
+
+/* ---- counters of the last call (e.g. "keydeps.path_replay", "keydeps.big_txns", "keydeps.big_entries") ---- */
+int acc_stats_count(acc_ctx *ctx);
+int acc_stats_get(acc_ctx *ctx, int i, const char **name, uint64_t *value);
 
 #ifdef __cplusplus
 }

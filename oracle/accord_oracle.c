@@ -411,11 +411,15 @@ static int cmp_vals_by_id(int64_t a, int64_t b, const void *c)
     const batch *B = c; return ts_cmp(&B->id[a], &B->id[b]);
 }
 
-/* KeyDeps.with (KeyDeps.java:238-253): empty operands short-circuit. */
+/* KeyDeps.isEmpty (KeyDeps.java:292-295): no entries (keys without values may remain). */
+static int kd_is_empty(const kdeps *d) { return d->nk2v == d->nkeys; }
+
+/* KeyDeps.with (KeyDeps.java:238-253): empty operands short-circuit (isEmpty() ? that : this). */
 static void kd_with(kdeps *acc, const kdeps *that, vcmp_fn cmpv, const void *ctx)
 {
-    if (that->nkeys == 0) return;
-    if (acc->nkeys == 0) {
+    if (!kd_is_empty(acc) && kd_is_empty(that)) return;
+    if (kd_is_empty(acc)) {
+        kd_free(acc);
         acc->keys = malloc(that->nkeys * sizeof *acc->keys); memcpy(acc->keys, that->keys, that->nkeys * sizeof *acc->keys); acc->nkeys = that->nkeys;
         acc->vals = malloc((that->nvals + 1) * sizeof *acc->vals); memcpy(acc->vals, that->vals, that->nvals * sizeof *acc->vals); acc->nvals = that->nvals;
         acc->k2v = malloc(that->nk2v * sizeof *acc->k2v); memcpy(acc->k2v, that->k2v, that->nk2v * sizeof *acc->k2v); acc->nk2v = that->nk2v;
@@ -618,7 +622,7 @@ orc_merge_result *orc_keydeps_merge(uint32_t n_groups, const uint64_t *grp_off,
         for (uint64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) {
             kdeps in;
             in.nkeys = key_off[r + 1] - key_off[r];
-            if (in.nkeys == 0) continue;   /* deps.isEmpty() */
+            if (k2v_off[r + 1] - k2v_off[r] == in.nkeys) continue;   /* deps.isEmpty() (KeyDeps.java:292-295) */
             in.keys = (uint64_t *)(key_code + key_off[r]);
             in.nvals = val_off[r + 1] - val_off[r];
             in.vals = malloc((in.nvals + 1) * sizeof *in.vals);

@@ -112,7 +112,7 @@ def merge_union(replies):
     m: dict = {}
     allvals = set()
     for keys, vals, k2v in replies:
-        if not keys:
+        if len(k2v) == len(keys):  # KeyDeps.isEmpty (KeyDeps.java:292-295)
             continue
         allvals.update(vals)
         for k, ts in to_canonical_map(keys, vals, k2v).items():

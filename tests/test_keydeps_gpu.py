@@ -128,6 +128,32 @@ def test_wide_timestamps_multiword_sort(ctx):
     assert_same(g, o, b.n_txn, "wide")
 
 
+def set_kind(b, idx, kind):
+    b.txn_lsb[idx] = (b.txn_lsb[idx] & ~np.uint64(0xE)) | np.uint64(kind << 1)
+    b.exe_msb[idx], b.exe_lsb[idx], b.exe_node[idx] = b.txn_msb[idx], b.txn_lsb[idx], b.txn_node[idx]
+
+
+@pytest.mark.parametrize("hot_every,tail", [(10, 5), (40, 3)])
+def test_tiers_medium_big_fallback(ctx, hot_every, tail):
+    """One hot key of committed Reads closed by a few PREACCEPTED Writes: those Writes depend on every
+    earlier entry (E up to ~9000), exercising the block tier (E <= 8192) and the global-sort tier."""
+    import oracle
+    b = W.keydeps_batch(90_000, 1, 1_000_000, 0x5EED + hot_every, "uniform", status_model="model", window=0)
+    hot = np.arange(0, b.n_txn, hot_every)
+    b.key_code[hot] = W.int_key_code(np.array([1 << 30]))[0]
+    set_kind(b, hot, W.READ)
+    b.status[hot] = W.APPLIED
+    last = hot[-tail:]
+    set_kind(b, last, W.WRITE)
+    b.status[last] = W.PREACCEPTED
+    g = ctx.calculate_partial_deps(b)
+    o = oracle.keydeps_batch(b)
+    assert_same(g, o, b.n_txn, "tiers")
+    st = ctx.stats()
+    if st.get("keydeps.path_replay") == 0 and hot_every == 10:
+        assert st["keydeps.fallback_txns"] > 0
+
+
 def test_path_selection():
     """Tie-free batches take the run-based path; executeAt ties switch to the exact replay."""
     from accord_amd.deps import Context
@@ -135,7 +161,7 @@ def test_path_selection():
     with Context(0, timing=True) as c:
         c.calculate_partial_deps(b)
         names = set(c.timing())
-    assert "v2_write" in names and "query_emit" not in names
+    assert "v2_write_small" in names and "query_emit" not in names
     com = np.where((b.status >= W.COMMITTED) & (b.status <= W.APPLIED))[0][:2]
     b.exe_msb[com] = b.exe_msb[com[0]]
     b.exe_lsb[com] = b.txn_lsb[com].max() + (np.uint64(7) << np.uint64(16))

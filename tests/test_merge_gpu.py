@@ -1,0 +1,77 @@
+"""GPU parity: acc_keydeps_merge (batched KeyDeps.merge) vs the C restatement of LinearMerger/linearUnion
+and the canonical union (KeyDepsTest.testMergedProperty, KeyDepsTest.java:275-283)."""
+import numpy as np
+import pytest
+
+import canonical
+from test_oracle import gen_keydeps, pack_groups
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from accord_amd.deps import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def check_groups(out, groups):
+    for gi, g in enumerate(groups):
+        keys, vals, k2v = canonical.merge_union(g)
+        a, b = int(out["key_off"][gi]), int(out["key_off"][gi + 1])
+        assert out["key_code"][a:b].tolist() == keys, gi
+        a, b = int(out["val_off"][gi]), int(out["val_off"][gi + 1])
+        assert out["txn_rank"][a:b].tolist() == vals, gi
+        a, b = int(out["k2v_off"][gi]), int(out["k2v_off"][gi + 1])
+        assert out["k2v"][a:b].tolist() == k2v, gi
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_merge_random_groups(ctx, seed):
+    import oracle
+    from accord_amd.deps import keydeps_merge
+    rng = np.random.RandomState(100 + seed)
+    groups = [[gen_keydeps(rng) for _ in range(rng.randint(0, 20))] for _ in range(40)]
+    m = pack_groups(groups)
+    out = keydeps_merge(ctx, m)
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+    check_groups(out, groups)
+
+
+def test_merge_empty_replies_and_keys_without_values(ctx):
+    from accord_amd.deps import keydeps_merge
+    # reply A: keys [5, 9], key 5 has no entries, key 9 -> txn 3 (non-empty: its key 5 is kept)
+    a = ([5, 9], [3, 7], [2, 3, 0])
+    # reply B: empty (keys but no entries) -> skipped entirely, including its txnIds
+    b = ([1, 2], [11], [2, 2])
+    c = ([9, 12], [3, 8], [3, 4, 0, 1])
+    groups = [[a, b, c], [b], [], [b, b], [c, a]]
+    out = keydeps_merge(ctx, pack_groups(groups))
+    check_groups(out, groups)
+    assert out["key_code"][int(out["key_off"][0]):int(out["key_off"][1])].tolist() == [5, 9, 12]
+
+
+def test_merge_rejects_bad_layout(ctx):
+    from accord_amd.deps import IllegalArgumentException, keydeps_merge
+    bad = ([5, 9], [3], [2, 2, 0])   # last offset != length
+    with pytest.raises(IllegalArgumentException):
+        keydeps_merge(ctx, pack_groups([[bad]]))
+    good = ([5, 9], [3], [3, 4, 0, 0])
+    keydeps_merge(ctx, pack_groups([[good]]))
+
+
+def test_merge_config5_shape(ctx):
+    """Config-5 shaped input at reduced size: every txn's true deps replicated over 16 replies with
+    entries dropped (p=0.1) and spurious entries added (5%)."""
+    import oracle
+    from accord_amd import workload as W
+    from accord_amd.deps import keydeps_merge
+    m = W.merge_batch(n_txn=1500, replies=16, seed=0xACC00006, n_keys=2000)
+    out = keydeps_merge(ctx, m)
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
