@@ -289,3 +289,19 @@ def keydeps_merge(ctx: Context, m: dict) -> dict:
     r["txn_rank"] = r["txn_rank"][:out.need_vals]
     r["k2v"] = r["k2v"][:out.need_k2v]
     return r
+
+
+def levelise(ctx: Context, off, dep, exec_rank):
+    """Execution-order levels of a deps graph (restatement of Commands.updateWaitingOn ordering,
+    local/Commands.java:776-830): returns (level[n], order[n], n_levels)."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    dep = np.ascontiguousarray(dep, dtype=np.uint32)
+    er = np.ascontiguousarray(exec_rank, dtype=np.uint32)
+    n = len(er)
+    level = np.zeros(max(n, 1), np.uint32)
+    order = np.zeros(max(n, 1), np.uint32)
+    nl = np.zeros(1, np.uint32)
+    gi = L.GraphIn(L.ACC_MEM_HOST, n, off.ctypes.data, dep.ctypes.data if len(dep) else 0, er.ctypes.data)
+    ctx.check(ctx._lib.acc_levelise(ctx.handle, C.byref(gi), level.ctypes.data_as(L.u32p), order.ctypes.data_as(L.u32p),
+                                    nl.ctypes.data_as(L.u32p)))
+    return level[:n], order[:n], int(nl[0])

@@ -1,0 +1,66 @@
+"""GPU parity: acc_levelise vs the C restatement and the canonical model."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from accord_amd.deps import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def random_graph(rng, n, max_deps, exec_perm=True):
+    exec_rank = (rng.permutation(n) if exec_perm else np.arange(n)).astype(np.uint32)
+    deps = [np.unique(rng.randint(0, n, size=rng.randint(0, max_deps + 1))) for _ in range(n)]
+    off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
+    dep = np.concatenate(deps).astype(np.uint32) if off[-1] else np.zeros(0, np.uint32)
+    return off, dep, exec_rank
+
+
+@pytest.mark.parametrize("n,max_deps", [(1, 0), (100, 5), (5000, 30), (40000, 8)])
+def test_levelise_random(ctx, n, max_deps):
+    import oracle
+    from accord_amd.deps import levelise
+    off, dep, er = random_graph(np.random.RandomState(n), n, max_deps)
+    lv, order, nl = levelise(ctx, off, dep, er)
+    l2, o2, nl2 = oracle.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == nl2
+
+
+def test_levelise_long_chain(ctx):
+    """A hot-key write chain: every txn depends on its predecessor (depth n, crosses many windows)."""
+    import oracle
+    from accord_amd.deps import levelise
+    n = 5000
+    er = np.arange(n, dtype=np.uint32)[::-1].copy()      # executeAt order reversed vs index
+    off = np.concatenate([[0], np.cumsum([1 if t < n - 1 else 0 for t in range(n)])]).astype(np.uint64)
+    dep = np.arange(1, n, dtype=np.uint32)              # t depends on t+1 (earlier executeAt)
+    lv, order, nl = levelise(ctx, off, dep, er)
+    l2, o2, nl2 = oracle.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == n
+
+
+def test_levelise_ignores_later_and_equal_executeAt(ctx):
+    import canonical
+    from accord_amd.deps import levelise
+    er = np.array([5, 5, 1, 9], dtype=np.uint32)
+    off = np.array([0, 1, 3, 4, 6], dtype=np.uint64)
+    dep = np.array([1, 0, 2, 3, 0, 2], dtype=np.uint32)   # equal-executeAt and later-executeAt edges ignored
+    lv, order, nl = levelise(ctx, off, dep, er)
+    l2, o2 = canonical.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+
+
+def test_levelise_rejects_bad_dep(ctx):
+    from accord_amd.deps import IllegalArgumentException, levelise
+    with pytest.raises(IllegalArgumentException):
+        levelise(ctx, np.array([0, 1], np.uint64), np.array([7], np.uint32), np.array([0], np.uint32))
