@@ -1,0 +1,115 @@
+"""Key-range sharding of the deps path across GPUs (one CommandStore per GPU), and the per-node reduce.
+
+Accord splits a node's keyspace into CommandStores (local/ShardDistributor.java:106-156, EvenSplit); each
+store computes `calculatePartialDeps` over its own keys and the per-store results are folded with
+`PartialDeps.with` (PreAccept.reduce, messages/PreAccept.java:141-156). Here:
+
+  1. every rank holds the whole batch's txn table (TxnIds are global) and keeps only the keys of its shard;
+  2. the rank computes its shard's KeyDeps for every txn (acc_keydeps_batch on its GPU);
+  3. per-txn fragments go to the txn's home rank (t mod world) with one all-to-allv (RCCL on GPUs,
+     gloo on CPU) — the only data-path collective;
+  4. the home rank unions its txns' fragments in shard order (acc_keydeps_merge): keys are disjoint across
+     shards, so the union is the concatenation of keys with a union of TxnIds, exactly PartialDeps.with.
+
+Dependency values travel as global batch indices; the batch must be in TxnId order (what a CommandStore
+hands over) so that index order is TxnId order.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .workload import Batch
+
+
+def even_split(key_code: np.ndarray, world: int) -> np.ndarray:
+    """EvenSplit of the observed key-code domain [min, max] into `world` contiguous shards: world+1 bounds
+    (ShardDistributor.EvenSplit.split, local/ShardDistributor.java:106-156, with equal-width pieces)."""
+    lo = int(key_code.min()) if len(key_code) else 0
+    hi = int(key_code.max()) if len(key_code) else 0
+    span = hi - lo + 1
+    b = [lo + (span * s) // world for s in range(world)] + [hi + 1]
+    return np.array(b, dtype=np.uint64)
+
+
+def shard_batch(batch: Batch, bounds: np.ndarray, rank: int) -> Batch:
+    """Same txns (global indices), key lists restricted to [bounds[rank], bounds[rank+1])."""
+    lo, hi = np.uint64(bounds[rank]), np.uint64(bounds[rank + 1])
+    kc = batch.key_code
+    keep = (kc >= lo) & (kc < hi)
+    counts = np.add.reduceat(keep.astype(np.int64), batch.key_off[:-1].astype(np.int64)) if len(kc) else \
+        np.zeros(batch.n_txn, np.int64)
+    # reduceat misbehaves on empty segments: fix them
+    empty = np.diff(batch.key_off.astype(np.int64)) == 0
+    counts[empty] = 0
+    off = np.zeros(batch.n_txn + 1, dtype=np.uint32)
+    np.cumsum(counts, out=off[1:])
+    return Batch(batch.txn_msb, batch.txn_lsb, batch.txn_node, batch.exe_msb, batch.exe_lsb, batch.exe_node,
+                 batch.status, off, kc[keep], dict(batch.meta, shard=rank))
+
+
+def pack_fragments(res, local: Batch, world: int):
+    """Per destination rank, one int64 stream of fragments [t, nk, nv, no, keys..., txnIds..., k2v...] for every
+    txn with a non-empty shard result (KeyDeps.isEmpty fragments carry nothing: PartialDeps.with skips them)."""
+    n = local.n_txn
+    nk = np.diff(res.kd_off.astype(np.int64))
+    na = np.diff(res.arena_off.astype(np.int64))
+    nv = np.diff(res.u_off.astype(np.int64))
+    ts = np.nonzero(na > nk)[0]
+    streams = [[] for _ in range(world)]
+    for t in ts:
+        k0, k1 = int(res.kd_off[t]), int(res.kd_off[t + 1])
+        keys = local.key_code[int(local.key_off[t]) + res.key_idx[k0:k1].astype(np.int64)].astype(np.int64)
+        vals = res.dep_txn[int(res.u_off[t]):int(res.u_off[t + 1])].astype(np.int64)
+        k2v = res.arena[int(res.arena_off[t]):int(res.arena_off[t + 1])].astype(np.int64)
+        streams[int(t) % world].append(np.concatenate([[t, k1 - k0, len(vals), len(k2v)], keys, vals, k2v]))
+    out = [np.concatenate(s) if s else np.zeros(0, np.int64) for s in streams]
+    return out
+
+
+def exchange(send: list, group=None, device=None):
+    """all-to-allv of int64 streams (torch.distributed; nccl = RCCL over xGMI on MI355X, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = device or torch.device("cpu")
+    counts = torch.tensor([len(s) for s in send], dtype=torch.int64, device=dev)
+    recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    send_t = torch.from_numpy(np.concatenate(send) if send else np.zeros(0, np.int64)).to(dev)
+    recv_t = torch.empty(int(recv_counts.sum().item()), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_counts.tolist(),
+                           input_split_sizes=counts.tolist(), group=group)
+    return recv_t.cpu().numpy(), recv_counts.cpu().numpy()
+
+
+def unpack_to_merge(recv: np.ndarray, recv_counts: np.ndarray, home_txns: np.ndarray) -> dict:
+    """Fragments received from every source rank -> acc_merge_in with one group per home txn (ascending),
+    its replies in source-rank (= shard) order, the order of PreAccept.reduce's fold."""
+    frags = {}
+    pos = 0
+    for src, c in enumerate(recv_counts.tolist()):
+        end = pos + c
+        while pos < end:
+            t, nk, nv, no = (int(x) for x in recv[pos:pos + 4])
+            body = recv[pos + 4:pos + 4 + nk + nv + no]
+            frags.setdefault(t, []).append((src, body[:nk], body[nk:nk + nv], body[nk + nv:]))
+            pos += 4 + nk + nv + no
+    grp_off, key_off, val_off, k2v_off = [0], [0], [0], [0]
+    key_code, txn_rank, k2v = [], [], []
+    for t in home_txns.tolist():
+        for _, keys, vals, kv in sorted(frags.get(t, []), key=lambda f: f[0]):
+            key_code.append(keys)
+            txn_rank.append(vals)
+            k2v.append(kv)
+            key_off.append(key_off[-1] + len(keys))
+            val_off.append(val_off[-1] + len(vals))
+            k2v_off.append(k2v_off[-1] + len(kv))
+        grp_off.append(len(key_off) - 1)
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+    return dict(grp_off=np.array(grp_off, np.uint64), key_off=np.array(key_off, np.uint64),
+                key_code=cat(key_code, np.uint64), val_off=np.array(val_off, np.uint64),
+                txn_rank=cat(txn_rank, np.uint32), k2v_off=np.array(k2v_off, np.uint64), k2v=cat(k2v, np.int32))
+
+
+def home_txns(n_txn: int, rank: int, world: int) -> np.ndarray:
+    return np.arange(rank, n_txn, world, dtype=np.int64)
