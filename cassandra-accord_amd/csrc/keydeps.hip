@@ -315,34 +315,48 @@ __global__ __launch_bounds__(BLOCK) void k_seg_flags(size_t P, const uint64_t *_
 }
 
 // Gather per-position CFK columns; fill seg_start; classify committed (C) / uncommitted (U).
-__global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, uint32_t n, const uint32_t *__restrict__ perm,
-                                                      const uint32_t *__restrict__ owner, const uint32_t *__restrict__ rank,
-                                                      const uint8_t *__restrict__ status, const uint64_t *__restrict__ tl,
-                                                      const uint32_t *__restrict__ seg_incl, const uint32_t *__restrict__ seg_flag,
-                                                      uint32_t *__restrict__ seg_start, uint32_t *__restrict__ s_rank,
-                                                      uint32_t *__restrict__ s_exec, uint8_t *__restrict__ s_info,
-                                                      uint32_t *__restrict__ pair_pos, uint32_t *__restrict__ cflag,
-                                                      uint32_t *__restrict__ uflag, uint64_t *__restrict__ pmax_in)
+// per-txn record for the CFK gather: one 16-B random read per pair instead of four
+__global__ __launch_bounds__(BLOCK) void k_txn_info(uint32_t n, const uint32_t *__restrict__ rank, const uint8_t *__restrict__ status,
+                                                    const uint64_t *__restrict__ tl, uint4 *__restrict__ tinfo)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
+    tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), 0u);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, const uint32_t *__restrict__ perm, const uint32_t *__restrict__ owner,
+                                                      const uint4 *__restrict__ tinfo, const uint32_t *__restrict__ seg_incl,
+                                                      const uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ seg_start,
+                                                      uint32_t *__restrict__ s_rank, uint32_t *__restrict__ s_exec,
+                                                      uint8_t *__restrict__ s_info, uint32_t *__restrict__ pair_pos)
 {
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
     uint32_t j = perm[p];
-    uint32_t t = owner[j];
+    uint4 ti = tinfo[owner[j]];
     uint32_t seg = seg_incl[p] - 1;
     if (seg_flag[p]) seg_start[seg] = (uint32_t)p;
     if (p == P - 1) seg_start[seg + 1] = (uint32_t)P;
-    uint32_t st = status[t];
-    uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
-    uint32_t er = rank[n + t];
-    s_rank[p] = rank[t];
-    s_exec[p] = er;
-    s_info[p] = (uint8_t)(st | (kind << 3));
+    s_rank[p] = ti.x;
+    s_exec[p] = ti.y;
+    s_info[p] = (uint8_t)ti.z;
     pair_pos[j] = (uint32_t)p;
+}
+
+// v1 only: committed / uncommitted flags and the segmented prefix-max input
+__global__ __launch_bounds__(BLOCK) void k_v1_flags(size_t P, const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ s_exec,
+                                                    const uint32_t *__restrict__ seg_incl, uint32_t *__restrict__ cflag,
+                                                    uint32_t *__restrict__ uflag, uint64_t *__restrict__ pmax_in)
+{
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= P) return;
+    uint32_t st = s_info[p] & 7u;
     bool c = st >= 4 && st <= 6;
     cflag[p] = c;
     uflag[p] = st >= 1 && st <= 3;
     // segmented prefix-max via a segment-id prefix: max over (seg << 32 | exec+1) never crosses segments
-    pmax_in[p] = ((uint64_t)seg << 32) | (c ? (uint64_t)er + 1 : 0);
+    pmax_in[p] = ((uint64_t)(seg_incl[p] - 1) << 32) | (c ? (uint64_t)s_exec[p] + 1 : 0);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_low32(size_t P, const uint64_t *__restrict__ in, uint32_t *__restrict__ out)
@@ -659,8 +673,22 @@ __device__ __forceinline__ uint32_t v2_code(uint32_t rank, uint32_t exec, uint32
     return list | (bc << 3) | (ucw << 4);
 }
 
-constexpr int V2_ITEMS = 8;
+constexpr int V2_ITEMS = 4;               // consecutive positions per thread: one 16-B load per column
 constexpr int V2_TILE = BLOCK * V2_ITEMS;
+
+// 4 consecutive positions' codes (s_rank / s_exec / s_info are allocated with 4 entries of padding)
+__device__ __forceinline__ void v2_codes4(size_t P, size_t base, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
+                                          const uint8_t *__restrict__ s_info, uint32_t (&code)[V2_ITEMS], uint32_t (&rk)[V2_ITEMS])
+{
+    uint4 r = *reinterpret_cast<const uint4 *>(s_rank + base);
+    uint4 e = *reinterpret_cast<const uint4 *>(s_exec + base);
+    uint32_t inf = *reinterpret_cast<const uint32_t *>(s_info + base);
+    rk[0] = r.x; rk[1] = r.y; rk[2] = r.z; rk[3] = r.w;
+    const uint32_t ex[4] = { e.x, e.y, e.z, e.w };
+#pragma unroll
+    for (int i = 0; i < V2_ITEMS; ++i)
+        code[i] = base + i < P ? v2_code(rk[i], ex[i], (inf >> (8 * i)) & 0xFFu) : 7u;
+}
 
 __global__ __launch_bounds__(BLOCK) void k_v2_reduce(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
                                                      const uint8_t *__restrict__ s_info, uint32_t *__restrict__ tile_sums,
@@ -669,16 +697,17 @@ __global__ __launch_bounds__(BLOCK) void k_v2_reduce(size_t P, const uint32_t *_
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t c[NCNT] = {};
+    if (base < P) {
+        uint32_t code[V2_ITEMS], rk[V2_ITEMS];
+        v2_codes4(P, base, s_rank, s_exec, s_info, code, rk);
 #pragma unroll
-    for (int i = 0; i < V2_ITEMS; ++i) {
-        size_t p = base + i;
-        if (p >= P) break;
-        uint32_t code = v2_code(s_rank[p], s_exec[p], s_info[p]);
-        uint32_t l = code & 7u;
+        for (int i = 0; i < V2_ITEMS; ++i) {
+            uint32_t l = code[i] & 7u;
 #pragma unroll
-        for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
-        c[6] += (code >> 3) & 1u;
-        if ((code >> 4) & 1u) c[7] = (uint32_t)p + 1;
+            for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
+            c[6] += (code[i] >> 3) & 1u;
+            if ((code[i] >> 4) & 1u) c[7] = (uint32_t)(base + i) + 1;
+        }
     }
 #pragma unroll
     for (int q = 0; q < NCNT; ++q) {
@@ -699,10 +728,13 @@ __global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__rest
     }
 }
 
+// Row layout of the per-position prefix columns: row p = 8 u32 (32 B, one sector) =
+//   [0..5] exclusive prefix counts of the 6 class lists, [6] bumped-committed count, [7] last unbumped committed
+//   Write (pos+1, prefix max). A query reads whole rows at s0 / s1 / pos / posM: one line each.
+constexpr int RW_CBC = 6, RW_LUCW = 7;
+
 struct V2Cols {
-    uint32_t *cnt;        // [NLIST][P+1] exclusive prefix counts per list
-    uint32_t *cbc;        // [P+1] exclusive prefix count of bumped committed
-    uint32_t *lucw;       // [P+1] exclusive prefix max of (pos+1) of unbumped committed Writes
+    uint4 *rows;          // [P+1] rows of 8 u32, as 2 x uint4
     uint32_t *list_rank;  // class lists (TxnId ranks), list l at bases[l]
     uint32_t *bc_rank, *bc_exec;  // bumped committed, position order
     uint8_t *bc_kind;
@@ -717,17 +749,18 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
 {
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
-    uint32_t code[V2_ITEMS];
+    uint32_t code[V2_ITEMS] = { 7u, 7u, 7u, 7u }, rk[V2_ITEMS] = {};
     uint32_t c[NCNT] = {};
+    if (base < P) {
+        v2_codes4(P, base, s_rank, s_exec, s_info, code, rk);
 #pragma unroll
-    for (int i = 0; i < V2_ITEMS; ++i) {
-        size_t p = base + i;
-        code[i] = p < P ? v2_code(s_rank[p], s_exec[p], s_info[p]) : 7u;
-        uint32_t l = code[i] & 7u;
+        for (int i = 0; i < V2_ITEMS; ++i) {
+            uint32_t l = code[i] & 7u;
 #pragma unroll
-        for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
-        c[6] += (code[i] >> 3) & 1u;
-        if ((code[i] >> 4) & 1u) c[7] = (uint32_t)p + 1;
+            for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
+            c[6] += (code[i] >> 3) & 1u;
+            if ((code[i] >> 4) & 1u) c[7] = (uint32_t)(base + i) + 1;
+        }
     }
     uint32_t run[NCNT];
 #pragma unroll
@@ -737,6 +770,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         if (q < 7) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
         else { uint32_t e = block_exclusive(c[q], OpMax<uint32_t>(), lds, total); run[q] = e > pre ? e : pre; }
     }
+    if (base >= P) return;
     uint32_t lb[NLIST];
 #pragma unroll
     for (int l = 0; l < NLIST; ++l) lb[l] = bases[l];
@@ -744,12 +778,10 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     for (int i = 0; i < V2_ITEMS; ++i) {
         size_t p = base + i;
         if (p >= P) break;
-#pragma unroll
-        for (int q = 0; q < NLIST; ++q) o.cnt[(size_t)q * (P + 1) + p] = run[q];
-        o.cbc[p] = run[6];
-        o.lucw[p] = run[7];
+        o.rows[2 * p] = make_uint4(run[0], run[1], run[2], run[3]);
+        o.rows[2 * p + 1] = make_uint4(run[4], run[5], run[6], run[7]);
         uint32_t l = code[i] & 7u;
-        uint32_t r = s_rank[p];
+        uint32_t r = rk[i];
         if (l < NLIST) {
             uint32_t idx = 0;
 #pragma unroll
@@ -769,10 +801,8 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         }
         if ((code[i] >> 4) & 1u) run[7] = (uint32_t)p + 1;
         if (p == P - 1) {
-#pragma unroll
-            for (int q = 0; q < NLIST; ++q) o.cnt[(size_t)q * (P + 1) + P] = run[q];
-            o.cbc[P] = run[6];
-            o.lucw[P] = run[7];
+            o.rows[2 * P] = make_uint4(run[0], run[1], run[2], run[3]);
+            o.rows[2 * P + 1] = make_uint4(run[4], run[5], run[6], run[7]);
         }
     }
 }
@@ -789,50 +819,68 @@ __global__ __launch_bounds__(BLOCK) void k_v2_bcs_cols(uint32_t nbc, const uint6
 }
 
 struct V2View {
-    const uint32_t *owner, *rank, *pair_pos, *seg_incl, *seg_start, *s_rank;
-    const uint64_t *tl;
-    const uint8_t *status;
-    const uint32_t *cnt, *cbc, *lucw, *list_rank, *bases;
+    const uint32_t *perm, *pair_pos, *seg_incl, *seg_start, *s_rank, *s_exec;
+    const uint8_t *s_info;
+    const uint4 *rows;
+    const uint32_t *list_rank, *bases;
     const uint32_t *bc_rank, *bc_exec, *bc_pm;
     const uint8_t *bc_kind;
     const uint32_t *bcs_exec, *bcs_lastw;
-    uint32_t n;
-    uint64_t P1;  // P + 1 (row stride of cnt)
+    const uint4 *tinfo;   // per txn: rank, executeAt rank, status | kind << 3
 };
+
+struct Row { uint32_t c[8]; };
+
+__device__ __forceinline__ Row ld_row(const V2View &v, uint32_t p)
+{
+    uint4 a = v.rows[2 * (size_t)p], b = v.rows[2 * (size_t)p + 1];
+    Row r;
+    r.c[0] = a.x; r.c[1] = a.y; r.c[2] = a.z; r.c[3] = a.w;
+    r.c[4] = b.x; r.c[5] = b.y; r.c[6] = b.z; r.c[7] = b.w;
+    return r;
+}
+__device__ __forceinline__ uint32_t ld_cbc(const V2View &v, uint32_t p)
+{
+    return reinterpret_cast<const uint32_t *>(v.rows)[8 * (size_t)p + RW_CBC];
+}
 
 struct V2Query {
-    uint32_t t, trank, wk, wc, s0, pos, posm, m, b0, bstart, bend;
+    uint32_t trank, info, wk, wc, s0, pos, posm, m, bstart, bend;
     bool bq, has_m;
+    Row r0, rp, rm;   // rows at s0, pos, posM
 };
 
-__device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t j)
+// The query of the pair at CFK position p (pair order (key, TxnId)): every per-txn input comes from the
+// position-ordered columns, so neighbouring lanes read neighbouring rows.
+__device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
 {
     V2Query q;
-    q.t = v.owner[j];
-    uint32_t p = v.pair_pos[j];
     uint32_t seg = v.seg_incl[p] - 1;
     q.s0 = v.seg_start[seg];
     uint32_t s1 = v.seg_start[seg + 1];
-    q.trank = v.rank[q.t];
-    uint32_t S = v.rank[v.n + q.t];
-    q.wk = witnesses((uint32_t)(v.tl[q.t] >> 1) & 7u);
+    q.trank = v.s_rank[p];
+    uint32_t S = v.s_exec[p];
+    q.info = v.s_info[p];
+    q.wk = witnesses(q.info >> 3);
     q.wc = wk_classes(q.wk);
     q.bq = S != q.trank;
     q.pos = q.bq ? lower_bound_u32(v.s_rank, p + 1, s1, S) : p;
+    q.rp = ld_row(v, q.pos);
+    q.r0 = ld_row(v, q.s0);
     // M from the last unbumped committed Write before pos
-    uint32_t lu = v.lucw[q.pos];
+    uint32_t lu = q.rp.c[RW_LUCW];
     bool has_mu = lu > q.s0;
     uint32_t mu = has_mu ? v.s_rank[lu - 1] : 0;
     // M from bumped committed Writes of this segment: predecessor of S by executeAt, then nearest Write
-    q.b0 = v.cbc[q.s0];
-    uint32_t b1 = v.cbc[s1];
+    uint32_t b0 = q.r0.c[RW_CBC];
+    uint32_t b1 = ld_cbc(v, s1);
     bool has_mb = false;
     uint32_t mb = 0;
-    if (b1 > q.b0) {
-        uint32_t i = lower_bound_u32(v.bcs_exec, q.b0, b1, S);
-        if (i > q.b0) {
+    if (b1 > b0) {
+        uint32_t i = lower_bound_u32(v.bcs_exec, b0, b1, S);
+        if (i > b0) {
             uint32_t w = v.bcs_lastw[i - 1];
-            if (w > q.b0) { has_mb = true; mb = v.bcs_exec[w - 1]; }
+            if (w > b0) { has_mb = true; mb = v.bcs_exec[w - 1]; }
         }
     }
     q.has_m = has_mu || has_mb;
@@ -840,37 +888,37 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t j)
     if (!q.has_m) q.posm = q.s0;
     else if (has_mu && q.m == mu) q.posm = lu - 1;
     else q.posm = lower_bound_u32(v.s_rank, q.s0, q.pos, q.m);
-    q.bend = v.cbc[q.posm];
-    q.bstart = q.has_m ? lower_bound_u32(v.bc_pm, q.b0, q.bend, q.m + 1) : q.bend;
+    q.rm = q.posm == q.s0 ? q.r0 : ld_row(v, q.posm);
+    q.bend = q.rm.c[RW_CBC];
+    q.bstart = q.has_m ? lower_bound_u32(v.bc_pm, b0, q.bend, q.m + 1) : q.bend;
     return q;
 }
 
-// per-pair query record kept for the write pass: (s0, pos, posM, M or NONE), bstart
+// per-pair query record kept for the write pass, by CFK position: (s0, pos, posM, M or NONE), bstart
 constexpr uint32_t NO_M = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out,
                                                     uint4 *__restrict__ rec, uint32_t *__restrict__ rec_bstart)
 {
-    size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= P) return;
-    V2Query q = v2_query(v, (uint32_t)j);
-    rec[j] = make_uint4(q.s0, q.pos, q.posm, q.has_m ? q.m : NO_M);
-    rec_bstart[j] = q.bstart;
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= P) return;
+    V2Query q = v2_query(v, (uint32_t)p);
+    rec[p] = make_uint4(q.s0, q.pos, q.posm, q.has_m ? q.m : NO_M);
+    rec_bstart[p] = q.bstart;
     uint64_t e = 0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (!((q.wc >> c) & 1u)) continue;
-        const uint32_t *cu = v.cnt + (size_t)c * v.P1, *cc = v.cnt + (size_t)(3 + c) * v.P1;
-        e += cu[q.pos] - cu[q.s0];
-        e += cc[q.pos] - cc[q.posm];
+        e += q.rp.c[c] - q.r0.c[c];
+        e += q.rp.c[3 + c] - q.rm.c[3 + c];
     }
     for (uint32_t i = q.bstart; i < q.bend; ++i)
         if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) ++e;
     if (q.bq) {
-        uint32_t st = v.status[q.t], kind = (uint32_t)(v.tl[q.t] >> 1) & 7u;
+        uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
     }
-    cnt_out[j] = e;
+    cnt_out[v.perm[p]] = e;
 }
 
 // ---- write pass, three tiers by E_T (dependency entries of the txn; 98.7% of config-2 txns have <= 64):
@@ -924,9 +972,10 @@ __device__ __forceinline__ TxnCtx txn_ctx(const V2View &v, const V2Out &o, uint3
     c.j0 = o.key_off[t]; c.j1 = o.key_off[t + 1]; c.nk = c.j1 - c.j0;
     c.e0 = o.dep_off[c.j0];
     c.E = (uint32_t)(o.dep_off[c.j1] - c.e0);
-    c.trank = v.rank[t];
-    c.bq = v.rank[v.n + t] != c.trank;
-    c.wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u);
+    uint4 ti = v.tinfo[t];
+    c.trank = ti.x;
+    c.bq = ti.y != c.trank;
+    c.wk = witnesses(ti.z >> 3);
     c.wc = wk_classes(c.wk);
     return c;
 }
@@ -940,18 +989,19 @@ __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o
     uint32_t ktot = 0, lo = 0xFFFFFFFFu, hi = 0;
     if (lane < c.nk && cnt[c.j0 + lane] != 0) {
         const uint32_t j = c.j0 + lane;
-        uint4 r = o.rec[j];
+        const uint32_t p = v.pair_pos[j];
+        uint4 r = o.rec[p];
         const uint32_t s0 = r.x, pos = r.y, posm = r.z, m = r.w;
         const bool has_m = m != NO_M;
+        const uint32_t from = has_m ? posm : s0;
+        const Row r0 = ld_row(v, s0), rp = ld_row(v, pos), rf = from == s0 ? r0 : ld_row(v, from);
         uint32_t acc = 0;
 #pragma unroll
         for (int cl = 0; cl < 3; ++cl) {
             uint32_t a0 = 0, l0 = 0, a1 = 0, l1 = 0;
             if ((c.wc >> cl) & 1u) {
-                const uint32_t *cu = v.cnt + (size_t)cl * v.P1, *cc = v.cnt + (size_t)(3 + cl) * v.P1;
-                a0 = v.bases[cl] + cu[s0]; l0 = cu[pos] - cu[s0];
-                uint32_t from = has_m ? posm : s0;
-                a1 = v.bases[3 + cl] + cc[from]; l1 = cc[pos] - cc[from];
+                a0 = v.bases[cl] + r0.c[cl]; l0 = rp.c[cl] - r0.c[cl];
+                a1 = v.bases[3 + cl] + rf.c[3 + cl]; l1 = rp.c[3 + cl] - rf.c[3 + cl];
                 if (want_range) {
                     if (l0) { lo = min(lo, v.list_rank[a0]); hi = max(hi, v.list_rank[a0 + l0 - 1]); }
                     if (l1) { lo = min(lo, v.list_rank[a1]); hi = max(hi, v.list_rank[a1 + l1 - 1]); }
@@ -962,8 +1012,8 @@ __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o
         }
         uint32_t bs = 0, bl = 0;
         if (has_m) {
-            bs = o.rec_bstart[j];
-            bl = v.cbc[posm] - bs;
+            bs = o.rec_bstart[p];
+            bl = rf.c[RW_CBC] - bs;
             if (want_range && bl) { lo = min(lo, v.bc_rank[bs]); hi = max(hi, v.bc_rank[bs + bl - 1]); }
         }
         R.start[lane][6] = bs; R.pre[lane][6] = acc; acc += bl;
@@ -1285,7 +1335,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
     const uint32_t j0 = key_off[t], j1 = key_off[t + 1];
     for (uint32_t j = j0; j < j1; ++j) {
         if (cnt[j] == 0) continue;
-        V2Query q = v2_query(v, j);
+        V2Query q = v2_query(v, v.pair_pos[j]);
         uint32_t kj = j - j0;
         for (int r = 0; r < 7; ++r) {
             const uint32_t *src;
@@ -1297,9 +1347,9 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
             } else {
                 int c = r >> 1;
                 if (!((q.wc >> c) & 1u)) continue;
-                const uint32_t *cl = v.cnt + (size_t)((r & 1) ? 3 + c : c) * v.P1;
-                a = (r & 1) ? cl[q.posm] : cl[q.s0];
-                e = cl[q.pos];
+                const int col = (r & 1) ? 3 + c : c;
+                a = (r & 1) ? q.rm.c[col] : q.r0.c[col];
+                e = q.rp.c[col];
                 src = v.list_rank + v.bases[(r & 1) ? 3 + c : c];
             }
             for (uint32_t c = a; c < e; c += 64) {
@@ -1415,11 +1465,15 @@ static void keydeps_v1_tail(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_vi
                             const uint8_t *status, const uint64_t *tl, const uint32_t *key_off, const uint32_t *owner,
                             const uint32_t *rank, const uint32_t *txn_of_rank, uint64_t *g, const uint32_t *seg_incl,
                             const uint32_t *seg_start, const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info,
-                            const uint32_t *pair_pos, const uint32_t *cflag, const uint32_t *uflag, const uint64_t *pmax_in)
+                            const uint32_t *pair_pos)
 {
     (void)in;
     hipStream_t st = ctx->stream;
     const unsigned gP = grid_for(P, BLOCK);
+    uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
+    uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
+    uint64_t *pmax_in = ctx->get<uint64_t>("pmax_in", P);
+    launch(ctx, "v1_flags", k_v1_flags, dim3(gP), dim3(BLOCK), 0, P, s_info, s_exec, seg_incl, cflag, uflag, pmax_in);
     uint32_t *cum_c = ctx->get<uint32_t>("cum_c", P + 1);
     uint32_t *cum_u = ctx->get<uint32_t>("cum_u", P + 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, cflag, cum_c, P, true, cum_c + P);
@@ -1687,16 +1741,15 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     scan<uint32_t, OpAdd<uint32_t>>(ctx, seg_flag, seg_incl, P, false);
 
     uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
-    uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P);
-    uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P);
-    uint8_t *s_info = ctx->get<uint8_t>("s_info", P);
+    uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P + V2_ITEMS);   // padded for the 16-B column loads
+    uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P + V2_ITEMS);
+    uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
-    uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
-    uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
-    uint64_t *pmax_in = ctx->get<uint64_t>("pmax_in", P);
-    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, n, (const uint32_t *)ps.vals,
-           (const uint32_t *)owner, (const uint32_t *)rank, status, tl, (const uint32_t *)seg_incl,
-           (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
+    uint4 *tinfo = ctx->get<uint4>("tinfo", n);
+    launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
+    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals,
+           (const uint32_t *)owner, (const uint4 *)tinfo, (const uint32_t *)seg_incl,
+           (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info, pair_pos);
     const int segbits = bits_for(P);
     // ---- v2 structures (class lists, prefix counts, bumped committed list)
     const uint32_t nt = (uint32_t)((P + V2_TILE - 1) / V2_TILE);
@@ -1711,9 +1764,7 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     scan<uint32_t, OpMax<uint32_t>>(ctx, tile_sums + (size_t)7 * nt, tile_pref + (size_t)7 * nt, nt, true, totals + 7);
     launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
     V2Cols cols;
-    cols.cnt = ctx->get<uint32_t>("v2_cnt", (size_t)NLIST * (P + 1));
-    cols.cbc = ctx->get<uint32_t>("v2_cbc", P + 1);
-    cols.lucw = ctx->get<uint32_t>("v2_lucw", P + 1);
+    cols.rows = ctx->get<uint4>("v2_rows", 2 * (P + 1));
     cols.list_rank = ctx->get<uint32_t>("v2_list_rank", P);
     cols.bc_rank = ctx->get<uint32_t>("v2_bc_rank", P);
     cols.bc_exec = ctx->get<uint32_t>("v2_bc_exec", P);
@@ -1735,7 +1786,7 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     ctx->stat("keydeps.batch_sorted", batch_sorted ? 1 : 0);
     if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
         keydeps_v1_tail(ctx, in, view, n, P, rbits, status, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
-                        s_rank, s_exec, s_info, pair_pos, cflag, uflag, pmax_in);
+                        s_rank, s_exec, s_info, pair_pos);
         return;
     }
     const uint32_t nbc = htot[6];
@@ -1753,10 +1804,10 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     launch(ctx, "low32", k_low32, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, (size_t)nbc, (const uint64_t *)bc_pm64, bc_pm);
 
     V2View vv;
-    vv.owner = owner; vv.rank = rank; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
-    vv.s_rank = s_rank; vv.tl = tl; vv.status = status; vv.cnt = cols.cnt; vv.cbc = cols.cbc; vv.lucw = cols.lucw;
+    vv.perm = ps.vals; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
+    vv.s_rank = s_rank; vv.s_exec = s_exec; vv.s_info = s_info; vv.rows = cols.rows; vv.tinfo = tinfo;
     vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm;
-    vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw; vv.n = n; vv.P1 = P + 1;
+    vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw;
 
     // ---- count, offsets
     uint64_t *cnt = ctx->get<uint64_t>("cnt", P);

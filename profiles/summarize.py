@@ -1,0 +1,74 @@
+"""Summarise a profiles/collect.sh run into a committed per-round file.
+
+    python profiles/summarize.py gpurun_out/prof_r01 profiles/r01 --steps 7
+
+Writes <prefix>_kernel_stats.csv (the rocprofv3 --stats table, accord kernels first), and <prefix>_summary.json:
+per-kernel average duration, per-step device time and per-step HBM traffic from the FETCH_SIZE / WRITE_SIZE
+passes. FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B); both counters are KB.
+`steps` = warmup + timed steps of the profiled bench command (every pipeline kernel of a step runs once per step
+or a fixed number of times, so totals / steps are per-step figures).
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.match(r"(?:acc::)?([A-Za-z0-9_]+)", name)
+    return m.group(1) if m else name
+
+
+def load_counters(path, counter):
+    tot = defaultdict(float)
+    calls = defaultdict(int)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter or not r["Kernel_Name"].startswith("acc::"):
+                continue
+            k = short(r["Kernel_Name"][5:])
+            tot[k] += float(r["Counter_Value"]) * 1024.0
+            calls[k] += 1
+    return tot, calls
+
+
+def main():
+    src, prefix = sys.argv[1], sys.argv[2]
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 7
+    rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    acc = [r for r in rows if r["Name"].startswith("acc::")]
+    with open(prefix + "_kernel_stats.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_ns", "avg_ns", "min_ns", "max_ns", "pct"])
+        for r in acc + [r for r in rows if not r["Name"].startswith("acc::")]:
+            w.writerow([short(r["Name"][5:] if r["Name"].startswith("acc::") else r["Name"]), r["Calls"],
+                        r["TotalDurationNs"], r["AverageNs"], r["MinNs"], r["MaxNs"], r["Percentage"]])
+    fetch, _ = load_counters(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, _ = load_counters(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    kernels = {}
+    for r in acc:
+        k = short(r["Name"][5:])
+        d = kernels.setdefault(k, dict(calls=0, total_ns=0.0))
+        d["calls"] += int(r["Calls"])
+        d["total_ns"] += float(r["TotalDurationNs"])
+    for k, d in kernels.items():
+        d["avg_ns"] = d["total_ns"] / d["calls"]
+        d["ms_per_step"] = d["total_ns"] / steps / 1e6
+        d["hbm_read_bytes_per_step"] = 2.0 * fetch.get(k, 0.0) / steps
+        d["hbm_write_bytes_per_step"] = write.get(k, 0.0) / steps
+    out = dict(
+        source=src, steps_profiled=steps,
+        kernel_ms_per_step=sum(d["ms_per_step"] for d in kernels.values()),
+        hbm_read_bytes_per_step=sum(d["hbm_read_bytes_per_step"] for d in kernels.values()),
+        hbm_write_bytes_per_step=sum(d["hbm_write_bytes_per_step"] for d in kernels.values()),
+        kernels=dict(sorted(kernels.items(), key=lambda kv: -kv[1]["total_ns"])),
+    )
+    out["hbm_bytes_per_step"] = out["hbm_read_bytes_per_step"] + out["hbm_write_bytes_per_step"]
+    json.dump(out, open(prefix + "_summary.json", "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "kernels"}))
+
+
+if __name__ == "__main__":
+    main()
