@@ -894,23 +894,26 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     return q;
 }
 
-// per-pair query record kept for the write pass, by CFK position: (s0, pos, posM, M or NONE), bstart
+// per-pair run record for the write pass, stored by pair index j (the write pass reads a txn's records
+// contiguously): starts a[6] and lengths l[6] of R1/R2 per class (witnessed classes only), R3 = [bs, bs + bl)
+// filtered by executeAt >= M. 64 B = 4 x uint4.
 constexpr uint32_t NO_M = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out,
-                                                    uint4 *__restrict__ rec, uint32_t *__restrict__ rec_bstart)
+__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out, uint4 *__restrict__ rec)
 {
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
     V2Query q = v2_query(v, (uint32_t)p);
-    rec[p] = make_uint4(q.s0, q.pos, q.posm, q.has_m ? q.m : NO_M);
-    rec_bstart[p] = q.bstart;
+    uint32_t a[6] = {}, l[6] = {};
     uint64_t e = 0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (!((q.wc >> c) & 1u)) continue;
-        e += q.rp.c[c] - q.r0.c[c];
-        e += q.rp.c[3 + c] - q.rm.c[3 + c];
+        a[2 * c] = v.bases[c] + q.r0.c[c];
+        l[2 * c] = q.rp.c[c] - q.r0.c[c];
+        a[2 * c + 1] = v.bases[3 + c] + q.rm.c[3 + c];
+        l[2 * c + 1] = q.rp.c[3 + c] - q.rm.c[3 + c];
+        e += l[2 * c] + l[2 * c + 1];
     }
     for (uint32_t i = q.bstart; i < q.bend; ++i)
         if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) ++e;
@@ -918,7 +921,13 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
         uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
     }
-    cnt_out[v.perm[p]] = e;
+    const uint32_t j = v.perm[p];
+    uint4 *r = rec + 4 * (size_t)j;
+    r[0] = make_uint4(a[0], a[1], a[2], a[3]);
+    r[1] = make_uint4(a[4], a[5], l[0], l[1]);
+    r[2] = make_uint4(l[2], l[3], l[4], l[5]);
+    r[3] = make_uint4(q.bstart, q.has_m ? q.bend - q.bstart : 0u, q.has_m ? q.m : NO_M, 0u);
+    cnt_out[j] = e;
 }
 
 // ---- write pass, three tiers by E_T (dependency entries of the txn; 98.7% of config-2 txns have <= 64):
@@ -939,8 +948,7 @@ struct V2Out {
     const uint32_t *key_off;
     const uint64_t *dep_off, *arena_off;
     const uint32_t *cnz, *txn_of_rank;
-    const uint4 *rec;
-    const uint32_t *rec_bstart;
+    const uint4 *rec;        // 4 x uint4 per pair (k_v2_count)
     int32_t *arena;
     uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
     uint64_t *u_cnt;
@@ -955,7 +963,6 @@ struct RunsT {
     uint32_t kbase[MAXK + 1];
     uint32_t m[MAXK];
     uint32_t kc[MAXK];
-    uint32_t lo, hi;         // value range of all runs (big tier)
     uint32_t total;
 };
 
@@ -980,45 +987,23 @@ __device__ __forceinline__ TxnCtx txn_ctx(const V2View &v, const V2Out &o, uint3
     return c;
 }
 
-// Called by ONE wave: lane k < nk fills the runs of key k. Returns the flattened raw length.
+// Called by ONE wave: lane k < nk fills the runs of key k from its 64-B record. Returns the flattened raw length.
 template <int MAXK>
-__device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o, const uint64_t *cnt, const TxnCtx &c,
-                                 bool want_range)
+__device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o, const uint64_t *cnt, const TxnCtx &c)
 {
     const uint32_t lane = lane_id();
-    uint32_t ktot = 0, lo = 0xFFFFFFFFu, hi = 0;
+    uint32_t ktot = 0;
     if (lane < c.nk && cnt[c.j0 + lane] != 0) {
-        const uint32_t j = c.j0 + lane;
-        const uint32_t p = v.pair_pos[j];
-        uint4 r = o.rec[p];
-        const uint32_t s0 = r.x, pos = r.y, posm = r.z, m = r.w;
-        const bool has_m = m != NO_M;
-        const uint32_t from = has_m ? posm : s0;
-        const Row r0 = ld_row(v, s0), rp = ld_row(v, pos), rf = from == s0 ? r0 : ld_row(v, from);
+        const uint4 *r = o.rec + 4 * (size_t)(c.j0 + lane);
+        const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+        const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
+        const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
         uint32_t acc = 0;
 #pragma unroll
-        for (int cl = 0; cl < 3; ++cl) {
-            uint32_t a0 = 0, l0 = 0, a1 = 0, l1 = 0;
-            if ((c.wc >> cl) & 1u) {
-                a0 = v.bases[cl] + r0.c[cl]; l0 = rp.c[cl] - r0.c[cl];
-                a1 = v.bases[3 + cl] + rf.c[3 + cl]; l1 = rp.c[3 + cl] - rf.c[3 + cl];
-                if (want_range) {
-                    if (l0) { lo = min(lo, v.list_rank[a0]); hi = max(hi, v.list_rank[a0 + l0 - 1]); }
-                    if (l1) { lo = min(lo, v.list_rank[a1]); hi = max(hi, v.list_rank[a1 + l1 - 1]); }
-                }
-            }
-            R.start[lane][2 * cl] = a0; R.pre[lane][2 * cl] = acc; acc += l0;
-            R.start[lane][2 * cl + 1] = a1; R.pre[lane][2 * cl + 1] = acc; acc += l1;
-        }
-        uint32_t bs = 0, bl = 0;
-        if (has_m) {
-            bs = o.rec_bstart[p];
-            bl = rf.c[RW_CBC] - bs;
-            if (want_range && bl) { lo = min(lo, v.bc_rank[bs]); hi = max(hi, v.bc_rank[bs + bl - 1]); }
-        }
-        R.start[lane][6] = bs; R.pre[lane][6] = acc; acc += bl;
+        for (int q = 0; q < 6; ++q) { R.start[lane][q] = a[q]; R.pre[lane][q] = acc; acc += l[q]; }
+        R.start[lane][6] = r3.x; R.pre[lane][6] = acc; acc += r3.y;
         R.pre[lane][7] = acc;
-        R.m[lane] = m;
+        R.m[lane] = r3.z;
         ktot = acc;
     } else if (lane < c.nk) {
         for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
@@ -1028,14 +1013,7 @@ __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o
     uint32_t incl = wave_inclusive(ktot, OpAdd<uint32_t>());
     if (lane < c.nk) R.kbase[lane] = incl - ktot;
     uint32_t total = shfl_idx(incl, 63);
-    if (want_range) {
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            lo = min(lo, (uint32_t)__shfl_xor(lo, d, 64));
-            hi = max(hi, (uint32_t)__shfl_xor(hi, d, 64));
-        }
-    }
-    if (lane == 0) { R.kbase[c.nk] = total; R.lo = lo; R.hi = hi; R.total = total; }
+    if (lane == 0) { R.kbase[c.nk] = total; R.total = total; }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     return total;
@@ -1209,7 +1187,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_small(uint32_t n, V2View v, 
     TxnCtx c = txn_ctx(v, o, t);
     RunsT<SMALL_K> &R = sruns[wave];
     uint64_t *buf = sbuf[wave];
-    uint32_t total = compute_runs(R, v, o, cnt, c, false);
+    uint32_t total = compute_runs(R, v, o, cnt, c);
     uint32_t got = gather_to(buf, SMALL_E, R, v, c, total);
     if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
     const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
@@ -1232,7 +1210,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_medium(uint32_t cnt_list, co
     TxnCtx c = txn_ctx(v, o, t);
     RunsT<MED_K> &R = sruns[wave];
     uint64_t *buf = sbuf[wave];
-    uint32_t total = compute_runs(R, v, o, cnt, c, false);
+    uint32_t total = compute_runs(R, v, o, cnt, c);
     uint32_t got = gather_to(buf, MED_E, R, v, c, total);
     if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
     const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
@@ -1253,66 +1231,134 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_medium(uint32_t cnt_list, co
     if (lane == 0) o.u_cnt[t] = distinct;
 }
 
-// Big tier: one block per txn (E <= BIG_E). Wave 0 gathers the runs into LDS, the block bitonic-sorts
-// (value << 16 | key), wave 0 emits with the same per-key running counts as the other tiers.
+// Locate element e of the flattened runs (LDS only): source index, key, R3 flag.
+template <int MAXK>
+__device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, uint32_t e, uint32_t &idx, uint32_t &k, bool &r3)
+{
+    uint32_t lo = 0, hi = nk;
+    while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
+    k = lo;
+    uint32_t off = e - R.kbase[k];
+    uint32_t r = 0;
+    while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
+    idx = R.start[k][r] + (off - R.pre[k][r]);
+    r3 = r == 6;
+}
+
+// Big tier: one block per txn (raw run length <= BIG_E). All four waves gather (dropped entries become
+// all-ones sentinels that sort last), the block bitonic-sorts (value << 16 | key), then each wave emits a
+// quarter of the sorted entries with per-key / distinct-value bases from a per-wave count pass.
+constexpr int BIG_GU = 4;   // independent loads in flight per thread during the gather
+
 __global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
                                                         const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ uint64_t buf[BIG_E];
     __shared__ RunsT<BIG_K> R;
-    __shared__ uint32_t got_s;
+    __shared__ uint32_t s_kept;
+    __shared__ uint32_t wk_cnt[WAVES][BIG_K];
+    __shared__ uint32_t wdist[WAVES];
     const uint32_t b = blockIdx.x;
     if (b >= cnt_list) return;
     const uint32_t t = list[b];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     TxnCtx c = txn_ctx(v, o, t);
-    if (c.nk > BIG_K || c.E > BIG_E) {
-        if (threadIdx.x == 0) {
+    bool oversize = c.nk > BIG_K || c.E > BIG_E;
+    if (!oversize) {
+        if (tid < 64) compute_runs(R, v, o, cnt, c);
+        if (tid < BIG_K) { wk_cnt[0][tid] = 0; wk_cnt[1][tid] = 0; wk_cnt[2][tid] = 0; wk_cnt[3][tid] = 0; }
+        if (tid == 0) s_kept = 0;
+        __syncthreads();
+        oversize = R.total > BIG_E;
+    }
+    if (oversize) {
+        if (tid == 0) {
             uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[3], 1ull);
             atomicAdd((unsigned long long *)&o.gstat[4], (unsigned long long)c.E);
             o.fb_list[f] = t;
         }
         return;
     }
-    if (threadIdx.x < 64) {
-        uint32_t total = compute_runs(R, v, o, cnt, c, false);
-        uint32_t got = gather_to(buf, BIG_E, R, v, c, total);
-        if (threadIdx.x == 0) got_s = got;
+    const uint32_t total = R.total;
+    uint32_t n2 = 128;
+    while (n2 < total) n2 <<= 1;
+    // ---- gather: raw element e -> buf[e] (sentinel when dropped)
+    uint32_t kept = 0;
+    for (uint32_t e0 = tid; e0 < n2; e0 += BIG_GU * BLOCK) {
+        uint32_t idx[BIG_GU], kk[BIG_GU], x[BIG_GU];
+        bool r3[BIG_GU], in[BIG_GU];
+#pragma unroll
+        for (int u = 0; u < BIG_GU; ++u) {
+            const uint32_t e = e0 + u * BLOCK;
+            in[u] = e < total;
+            idx[u] = 0; kk[u] = 0; r3[u] = false;
+            if (in[u]) locate_elem(R, c.nk, e, idx[u], kk[u], r3[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < BIG_GU; ++u) x[u] = in[u] ? (r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
+#pragma unroll
+        for (int u = 0; u < BIG_GU; ++u) {
+            const uint32_t e = e0 + u * BLOCK;
+            bool keep = in[u] && !(c.bq && x[u] == c.trank);
+            if (keep && r3[u]) keep = v.bc_exec[idx[u]] >= R.m[kk[u]] && ((c.wk >> v.bc_kind[idx[u]]) & 1u);
+            kept += keep;
+            if (e < n2) buf[e] = keep ? (((uint64_t)x[u] << 16) | kk[u]) : ~0ull;
+        }
     }
+    kept = wave_inclusive(kept, OpAdd<uint32_t>());
+    if (lane == 63) atomicAdd(&s_kept, kept);
     __syncthreads();
-    if (got_s != c.E) {
-        if (threadIdx.x == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
+    if (s_kept != c.E) {
+        if (tid == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
         return;
     }
-    uint32_t n2 = 128;
-    while (n2 < c.E) n2 <<= 1;
-    for (uint32_t q = c.E + threadIdx.x; q < n2; q += BLOCK) buf[q] = ~0ull;
-    __syncthreads();
+    // ---- bitonic sort over n2 (one compare-exchange per pair index)
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
-                uint32_t l = i ^ jj;
-                if (l > i) {
-                    uint64_t x = buf[i], y = buf[l];
-                    bool up = (i & k) == 0;
-                    if ((x > y) == up) { buf[i] = y; buf[l] = x; }
-                }
+            for (uint32_t pi = tid; pi < (n2 >> 1); pi += BLOCK) {
+                const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
+                const uint32_t l = i | jj;
+                uint64_t xa = buf[i], ya = buf[l];
+                const bool up = (i & k) == 0;
+                if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
             }
             __syncthreads();
         }
     }
-    if (threadIdx.x < 64) {
-        const uint32_t lane = lane_id();
-        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
-        uint32_t distinct = 0;
-        for (uint32_t q0 = 0; q0 < c.E; q0 += 64) {
-            uint32_t q = q0 + lane;
-            bool in = q < c.E;
-            uint64_t x = in ? buf[q] : 0;
-            uint64_t prev = q > 0 ? buf[q - 1] : 0;
-            distinct = emit_chunk(x, in, prev, q > 0, distinct, R.kc, o, c, abase);
-        }
-        if (lane == 0) o.u_cnt[t] = distinct;
+    // ---- emit: wave w owns sorted positions [w*Q, (w+1)*Q), Q a multiple of 64
+    const uint32_t E = c.E;
+    const uint32_t Q = ((E + WAVES * 64 - 1) / (WAVES * 64)) * 64;
+    const uint32_t q_lo = min(E, wave * Q), q_hi = min(E, q_lo + Q);
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t nd = 0;
+    for (uint32_t q0 = q_lo; q0 < q_hi; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool in = q < q_hi;
+        const uint64_t xq = in ? buf[q] : 0;
+        const bool nw = in && (q == 0 || (uint32_t)(buf[q - 1] >> 16) != (uint32_t)(xq >> 16));
+        nd += (uint32_t)__popcll(__ballot(nw));
+        if (in) atomicAdd(&wk_cnt[wave][(uint32_t)(xq & 0xFFFFu)], 1u);
     }
+    if (lane == 0) wdist[wave] = nd;
+    __syncthreads();
+    if (tid < BIG_K) {   // exclusive prefix over waves, per key
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) { uint32_t x = wk_cnt[w][tid]; wk_cnt[w][tid] = run; run += x; }
+    }
+    __syncthreads();
+    uint32_t distinct = 0;
+    for (int w = 0; w < (int)wave; ++w) distinct += wdist[w];
+    const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+    for (uint32_t q0 = q_lo; q0 < q_hi; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool in = q < q_hi;
+        const uint64_t xq = in ? buf[q] : 0;
+        const uint64_t prev = (in && q > 0) ? buf[q - 1] : 0;
+        distinct = emit_chunk(xq, in, prev, q > 0, distinct, wk_cnt[wave], o, c, abase);
+    }
+    if (wave == WAVES - 1 && lane == 0) o.u_cnt[t] = distinct;
+    (void)lt;
 }
 
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
@@ -1812,9 +1858,8 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     // ---- count, offsets
     uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
     uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
-    uint4 *rec = ctx->get<uint4>("v2_rec", P);
-    uint32_t *rec_bstart = ctx->get<uint32_t>("v2_rec_bstart", P);
-    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt, rec, rec_bstart);
+    uint4 *rec = ctx->get<uint4>("v2_rec", 4 * P);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt, rec);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt, dep_off, P, true, dep_off + P);
     uint32_t *nz = ctx->get<uint32_t>("nz", P);
     uint32_t *cnz = ctx->get<uint32_t>("cnz", P + 1);
@@ -1848,7 +1893,7 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     V2Out wo;
     wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
-    wo.rec = rec; wo.rec_bstart = rec_bstart; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+    wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
     launch(ctx, "v2_write_small", k_v2_write_small, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, vv,
            (const uint64_t *)cnt, wo);
     if (nmed)
