@@ -39,6 +39,18 @@ __device__ __forceinline__ T shfl_idx(T v, int src)
 }
 
 template <class T>
+__device__ __forceinline__ T shfl_xor(T v, int m)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u = (uint64_t)v;
+        uint32_t lo = __shfl_xor((uint32_t)u, m, 64), hi = __shfl_xor((uint32_t)(u >> 32), m, 64);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__shfl_xor((uint32_t)v, m, 64);
+    }
+}
+
+template <class T>
 struct OpAdd {
     __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
     static __device__ __forceinline__ T identity() { return (T)0; }
@@ -88,55 +100,111 @@ __device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
 }
 
 // ---------------------------------------------------------------- device-wide scan
+//
+// Single-pass scan with decoupled look-back: tiles take tickets in launch order, publish their aggregate,
+// then the nearest inclusive prefix found looking back over the previous tiles' status words. A status word is
+// one naturally aligned 8-B granule {value | flag << 62} written by ONE agent-scope (sc1) store and polled with
+// agent-scope loads (MI355X_MICROARCH.md, inter-workgroup hand-off: per-XCD L2s are not coherent). Values must
+// stay below 2^62 (every scan here: counts, offsets, (segment << 32 | value) maxima with < 2^30 segments).
+// Loads and stores go through LDS so every global access is coalesced.
 
-template <class T, class Op, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_tile_reduce(const T *__restrict__ in, size_t n, T *__restrict__ out)
+constexpr uint64_t SCAN_AGG = 1ull << 62, SCAN_INC = 2ull << 62, SCAN_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ void scan_status_store(uint64_t *p, uint64_t w)
 {
-    __shared__ T lds[WAVES];
-    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
-    Op op;
-    T acc = Op::identity();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-        if (base + i < n) acc = op(acc, in[base + i]);
-    T total;
-    block_exclusive(acc, op, lds, total);
-    if (threadIdx.x == 0) out[blockIdx.x] = total;
+    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t scan_status_load(const uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Scan one tile of BLOCK*ITEMS elements (thread-contiguous chunks), seeded with prefix[blockIdx]
-// (or identity). exclusive: out[i] = op(prefix, in[0..i-1]); else inclusive. If total_out is set,
-// the block holding element n-1 writes the grand total there.
 template <class T, class Op, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_tile_scan(const T *__restrict__ in, T *__restrict__ out, size_t n,
-                                                   const T *__restrict__ prefix, int exclusive,
-                                                   T *__restrict__ total_out)
+__global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *__restrict__ out, size_t n, int exclusive,
+                                                 T *__restrict__ total_out, uint32_t *__restrict__ ticket,
+                                                 uint64_t *__restrict__ status)
 {
+    constexpr int TILE = BLOCK * ITEMS;
+    __shared__ T tile[TILE + TILE / 32];
     __shared__ T lds[WAVES];
-    const size_t base = (size_t)blockIdx.x * BLOCK * ITEMS + (size_t)threadIdx.x * ITEMS;
+    __shared__ uint32_t s_b;
+    __shared__ T s_prefix;
+    const uint32_t tid = threadIdx.x, lane = lane_id();
+    if (tid == 0) s_b = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t b = s_b;
+    const size_t base = (size_t)b * TILE;
     Op op;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t li = i * BLOCK + tid;
+        const size_t g = base + li;
+        tile[li + li / 32] = g < n ? in[g] : Op::identity();
+    }
+    __syncthreads();
     T v[ITEMS];
     T acc = Op::identity();
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        v[i] = base + i < n ? in[base + i] : Op::identity();
+        const uint32_t li = tid * ITEMS + i;
+        v[i] = tile[li + li / 32];
         acc = op(acc, v[i]);
     }
     T total;
     T run = block_exclusive(acc, op, lds, total);
-    if (prefix) run = op(prefix[blockIdx.x], run);
+    if (b == 0) {
+        if (tid == 0) scan_status_store(&status[0], (uint64_t)total | SCAN_INC);
+    } else {
+        if (tid == 0) scan_status_store(&status[b], (uint64_t)total | SCAN_AGG);
+        if (tid < 64) {
+            T pre = Op::identity();
+            int64_t j = (int64_t)b - 1;
+            while (true) {
+                const int64_t idx = j - (int64_t)lane;
+                uint64_t w = (uint64_t)Op::identity() | SCAN_INC;
+                if (idx >= 0) {
+                    w = scan_status_load(&status[idx]);
+                    while ((w >> 62) == 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        w = scan_status_load(&status[idx]);
+                    }
+                }
+                const uint64_t inc = __ballot((w >> 62) == 2);
+                const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;
+                T x = lane <= stop ? (T)(w & SCAN_VAL) : Op::identity();
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) x = op(x, shfl_xor(x, d));
+                pre = op(pre, x);
+                if (inc) break;
+                j -= 64;
+            }
+            if (tid == 0) {
+                scan_status_store(&status[b], (uint64_t)op(pre, total) | SCAN_INC);
+                s_prefix = pre;
+            }
+        }
+        __syncthreads();
+        run = op(s_prefix, run);
+    }
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        T x = v[i];
-        T incl = op(run, x);
-        if (base + i < n) out[base + i] = exclusive ? run : incl;
-        if (total_out && base + i == n - 1) *total_out = incl;
+        const uint32_t li = tid * ITEMS + i;
+        const T incl = op(run, v[i]);
+        tile[li + li / 32] = exclusive ? run : incl;
+        if (total_out && base + li == n - 1) *total_out = incl;
         run = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t li = i * BLOCK + tid;
+        const size_t g = base + li;
+        if (g < n) out[g] = tile[li + li / 32];
     }
 }
 
 template <class T, class Op>
-void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr, int level = 0)
+void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr)
 {
     constexpr int ITEMS = sizeof(T) == 8 ? 4 : 8;
     constexpr size_t TILE = (size_t)BLOCK * ITEMS;
@@ -144,21 +212,13 @@ void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_
         if (total_out) ACC_HIP(hipMemsetAsync(total_out, 0, sizeof(T), ctx->stream));
         return;
     }
-    size_t nb = (n + TILE - 1) / TILE;
-    if (nb == 1) {
-        launch(ctx, "scan", k_tile_scan<T, Op, ITEMS>, dim3(1), dim3(BLOCK), 0, in, out, n, (const T *)nullptr,
-               (int)exclusive, total_out);
-        return;
-    }
-    char name_s[48], name_p[48];
-    snprintf(name_s, sizeof name_s, "scan_sums_%d_%zu", level, sizeof(T));
-    snprintf(name_p, sizeof name_p, "scan_pref_%d_%zu", level, sizeof(T));
-    T *sums = ctx->get<T>(name_s, nb);
-    T *pref = ctx->get<T>(name_p, nb);
-    launch(ctx, "scan", k_tile_reduce<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, n, sums);
-    scan<T, Op>(ctx, sums, pref, nb, true, (T *)nullptr, level + 1);
-    launch(ctx, "scan", k_tile_scan<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, out, n,
-           (const T *)pref, (int)exclusive, total_out);
+    const size_t nb = (n + TILE - 1) / TILE;
+    if (nb > 0xFFFFFFFFull) fail(ACC_E_CAP, "scan too large");
+    uint64_t *status = ctx->get<uint64_t>("scan_status", nb + 1);
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(status + nb);
+    ACC_HIP(hipMemsetAsync(status, 0, (nb + 1) * sizeof(uint64_t), ctx->stream));
+    launch(ctx, "scan", k_scan_1p<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, out, n, (int)exclusive, total_out,
+           ticket, status);
 }
 
 // ---------------------------------------------------------------- bit compaction plan

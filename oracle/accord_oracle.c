@@ -703,3 +703,177 @@ int orc_levelise(uint32_t n, const uint64_t *off, const uint32_t *dep, const uin
     free(idx);
     return 0;
 }
+
+/* ------------------------------------------------------------------ RangeDeps (range commands) */
+
+/* TxnId.domain(): flags & 1, Key = 0, Range = 1 (TxnId.java:134-157, Routable.Domain ordinals) */
+static inline int ts_is_range(const ts *t) { return (int)(t->lsb & 1); }
+
+typedef struct rng_dict { const uint64_t *s, *e; } rng_dict;
+static int cmp_range(int64_t a, int64_t b, const void *c)
+{
+    /* Range.compare (Range.java:309-317): by start, then end */
+    const rng_dict *D = c;
+    if (D->s[a] != D->s[b]) return D->s[a] < D->s[b] ? -1 : 1;
+    if (D->e[a] != D->e[b]) return D->e[a] < D->e[b] ? -1 : 1;
+    return 0;
+}
+
+/* Range.contains(key) for the two bound types (Range.java:40-138): EndInclusive (s, e], StartInclusive [s, e) */
+static inline int range_contains(uint64_t s, uint64_t e, uint64_t k, int end_inclusive)
+{
+    return end_inclusive ? (s < k && k <= e) : (s <= k && k < e);
+}
+/* Range.compareIntersecting == 0 (Range.java:296-305) */
+static inline int ranges_intersect(uint64_t as, uint64_t ae, uint64_t bs, uint64_t be)
+{
+    return as < be && ae > bs;
+}
+
+typedef struct rd_item { int64_t rid, txn; } rd_item;
+typedef struct rd_ctx { const batch *B; const rd_item *it; } rd_ctx;
+static int cmp_rd_item(int64_t a, int64_t b, const void *c)
+{
+    /* TreeMap<Range, List> by Range::compare, lists in the order range commands are visited (TxnId) */
+    const rd_ctx *X = c;
+    if (X->it[a].rid != X->it[b].rid) return X->it[a].rid < X->it[b].rid ? -1 : 1;
+    return ts_cmp(&X->B->id[X->it[a].txn], &X->B->id[X->it[b].txn]);
+}
+
+orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
+                                          const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                          const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                          const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                          int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride)
+{
+    orc_rangedeps_result *R = calloc(1, sizeof *R);
+    if (query_stride == 0) query_stride = 1;
+    if (query_hi > n) query_hi = n;
+    err E = { 0, "" };
+    batch B = { n, malloc((n + 1) * sizeof(ts)), malloc((n + 1) * sizeof(ts)), status, key_off, key_code };
+    for (uint32_t i = 0; i < n; ++i) {
+        B.id[i] = (ts){ tmsb[i], tlsb[i], tnode[i] };
+        B.ex[i] = (ts){ emsb[i], elsb[i], enode[i] };
+    }
+    /* validation: Keys / Ranges of a txn sorted and deoverlapped (Keys.ofSortedUnique,
+     * Ranges.ofSortedAndDeoverlapped), start < end, a txn's participants match its domain */
+    for (uint32_t t = 0; t < n && !E.code; ++t) {
+        if (status[t] > ST_INVALID) set_err(&E, -1, "invalid InternalStatus ordinal");
+        if (ts_kind(&B.id[t]) >= K_COUNT) set_err(&E, -1, "Kind.ofOrdinal: invalid kind ordinal");
+        int isr = ts_is_range(&B.id[t]);
+        if (isr && key_off[t + 1] != key_off[t]) set_err(&E, -1, "a range txn cannot list keys");
+        if (!isr && rng_off[t + 1] != rng_off[t]) set_err(&E, -1, "a key txn cannot list ranges");
+        for (uint32_t j = key_off[t] + 1; j < key_off[t + 1]; ++j)
+            if (key_code[j - 1] >= key_code[j]) set_err(&E, -1, "keys of a txn must be sorted and unique");
+        for (uint32_t j = rng_off[t]; j < rng_off[t + 1]; ++j) {
+            if (rng_start[j] >= rng_end[j]) set_err(&E, -1, "range start must be below its end");
+            if (j > rng_off[t] && rng_end[j - 1] > rng_start[j]) set_err(&E, -1, "ranges of a txn must be sorted and non-overlapping");
+        }
+    }
+    /* Range commands (InMemoryCommandStore.rangeCommands, a TreeMap by TxnId): range-domain txns whose
+     * saveStatus is below Erased (INVALID here is the erased/invalidated class), in TxnId order. */
+    ivec cmds = { 0 };
+    for (uint32_t t = 0; t < n; ++t)
+        if (ts_is_range(&B.id[t]) && status[t] != ST_INVALID && rng_off[t + 1] > rng_off[t]) iv_push(&cmds, t);
+    stable_sort(cmds.v, cmds.n, cmp_txn_by_id, &B);
+    for (size_t q = 1; q < cmds.n && !E.code; ++q)
+        if (ts_eq(&B.id[cmds.v[q - 1]], &B.id[cmds.v[q]])) set_err(&E, -1, "TxnIds of a batch must be distinct");
+    /* dictionary of the distinct stored ranges in Range::compare order */
+    ivec all = { 0 };
+    for (size_t q = 0; q < cmds.n; ++q)
+        for (uint32_t j = rng_off[cmds.v[q]]; j < rng_off[cmds.v[q] + 1]; ++j) iv_push(&all, j);
+    rng_dict D = { rng_start, rng_end };
+    stable_sort(all.v, all.n, cmp_range, &D);
+    size_t nd = 0;
+    uint64_t *ds = malloc((all.n + 1) * sizeof *ds), *de = malloc((all.n + 1) * sizeof *de);
+    int64_t *rid_of = malloc((rng_off[n] + 1) * sizeof *rid_of);
+    for (size_t q = 0; q < all.n; ++q) {
+        uint64_t s = rng_start[all.v[q]], e = rng_end[all.v[q]];
+        if (nd == 0 || ds[nd - 1] != s || de[nd - 1] != e) { ds[nd] = s; de[nd] = e; ++nd; }
+        rid_of[all.v[q]] = (int64_t)nd - 1;
+    }
+    R->n_txn = n; R->n_ranges = (uint32_t)nd; R->rng_start = ds; R->rng_end = de;
+    R->arena_off = calloc(n + 1, sizeof(uint64_t));
+    R->rd_off = calloc(n + 1, sizeof(uint64_t));
+    R->u_off = calloc(n + 1, sizeof(uint64_t));
+    ivec arena = { 0 }, rids = { 0 }, deps = { 0 };
+    builder b; b_init(&b, &B);
+    rd_item *items = NULL; size_t items_cap = 0;
+    int64_t *order = NULL; size_t order_cap = 0;
+    double t_query = now_s();
+    for (uint32_t t = 0; t < n && !E.code; ++t) {
+        R->arena_off[t] = arena.n; R->rd_off[t] = rids.n; R->u_off[t] = deps.n;
+        if (t < query_lo || t >= query_hi || (t - query_lo) % query_stride) continue;
+        ++R->queried;
+        int wk = kind_witnesses(ts_kind(&B.id[t]));
+        if (wk < 0) { set_err(&E, -2, "Kind.witnesses(): unhandled kind (AssertionError)"); break; }
+        long p1 = ts_eq(&B.ex[t], &B.id[t]) ? -1 : (long)t;   /* PreAccept.java:259 */
+        const int isr = ts_is_range(&B.id[t]);
+        size_t ni = 0;
+        /* commandStore.rangeCommands.forEach (:888-960) */
+        for (size_t q = 0; q < cmds.n; ++q) {
+            int64_t c = cmds.v[q];
+            ++R->visited;
+            if (ts_cmp(&B.id[c], &B.ex[t]) >= 0) continue;                 /* STARTED_BEFORE (:897-898) */
+            if (!(((unsigned)wk >> ts_kind(&B.id[c])) & 1u)) continue;     /* testKind (:926-927) */
+            /* Routables.foldl(rangeCommand.ranges, sliced, ...) (:950-959): each of C's ranges that
+             * intersects T's keys (Range.contains) or T's ranges (compareIntersecting) */
+            for (uint32_t j = rng_off[c]; j < rng_off[c + 1]; ++j) {
+                int hit = 0;
+                if (isr) {
+                    for (uint32_t u = rng_off[t]; u < rng_off[t + 1] && !hit; ++u)
+                        hit = ranges_intersect(rng_start[j], rng_end[j], rng_start[u], rng_end[u]);
+                } else {
+                    for (uint32_t u = key_off[t]; u < key_off[t + 1] && !hit; ++u)
+                        hit = range_contains(rng_start[j], rng_end[j], key_code[u], end_inclusive);
+                }
+                if (!hit) continue;
+                if (ni == items_cap) { items_cap = items_cap ? 2 * items_cap : 64; items = realloc(items, items_cap * sizeof *items); }
+                items[ni++] = (rd_item){ rid_of[j], c };
+            }
+        }
+        /* TreeMap iteration: Range order, then the per-range list in visit (TxnId) order; the list
+         * dedupes consecutive equal TxnIds (:953-955) */
+        if (ni > order_cap) { order_cap = ni; order = realloc(order, order_cap * sizeof *order); }
+        for (size_t q = 0; q < ni; ++q) order[q] = (int64_t)q;
+        rd_ctx X = { &B, items };
+        stable_sort(order, ni, cmp_rd_item, &X);
+        b_reset(&b);
+        for (size_t q = 0; q < ni; ++q) {
+            const rd_item *it = &items[order[q]];
+            if (q > 0 && items[order[q - 1]].rid == it->rid && items[order[q - 1]].txn == it->txn) continue;
+            /* calculatePartialDeps map: skip p1 (PreAccept.java:253-259) -> RangeDeps.Builder.add */
+            if (p1 >= 0 && ts_eq(&B.id[it->txn], &B.id[p1])) continue;
+            b_add(&b, (uint64_t)it->rid, it->txn);
+        }
+        kdeps part; if (b_build(&b, &part, &E)) break;
+        for (size_t q = 0; q < part.nk2v; ++q) iv_push(&arena, part.k2v[q]);
+        for (size_t q = 0; q < part.nkeys; ++q) iv_push(&rids, (int64_t)part.keys[q]);
+        for (size_t q = 0; q < part.nvals; ++q) iv_push(&deps, part.vals[q]);
+        R->total_edges += part.nk2v - part.nkeys;
+        kd_free(&part);
+    }
+    R->arena_off[n] = arena.n; R->rd_off[n] = rids.n; R->u_off[n] = deps.n;
+    R->query_s = now_s() - t_query;
+    R->arena = malloc((arena.n + 1) * sizeof(int32_t));
+    for (size_t q = 0; q < arena.n; ++q) R->arena[q] = (int32_t)arena.v[q];
+    R->range_id = malloc((rids.n + 1) * sizeof(uint32_t));
+    for (size_t q = 0; q < rids.n; ++q) R->range_id[q] = (uint32_t)rids.v[q];
+    R->dep_txn = malloc((deps.n + 1) * sizeof(uint32_t));
+    for (size_t q = 0; q < deps.n; ++q) R->dep_txn[q] = (uint32_t)deps.v[q];
+    R->error = E.code;
+    snprintf(R->message, sizeof R->message, "%s", E.msg);
+    b_free(&b);
+    free(items); free(order); free(arena.v); free(rids.v); free(deps.v); free(cmds.v); free(all.v); free(rid_of);
+    free(B.id); free(B.ex);
+    return R;
+}
+
+void orc_rangedeps_free(orc_rangedeps_result *r)
+{
+    if (!r) return;
+    free(r->rng_start); free(r->rng_end); free(r->arena_off); free(r->arena); free(r->rd_off); free(r->range_id);
+    free(r->u_off); free(r->dep_txn);
+    free(r);
+}

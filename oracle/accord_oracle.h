@@ -70,6 +70,37 @@ void orc_merge_free(orc_merge_result *r);
 int orc_levelise(uint32_t n, const uint64_t *off, const uint32_t *dep, const uint32_t *exec_rank,
                  uint32_t *level, uint32_t *order, uint32_t *n_levels);
 
+/* RangeDeps of a mixed key/range batch (SURVEY.md §8 A8 range part, config 4). Txns whose TxnId domain bit
+ * (lsb & 1, TxnId.java:124-157) is Range are range commands with the ranges [rng_off[t], rng_off[t+1]);
+ * key txns list keys as in orc_keydeps_batch. For every queried txn T, restates
+ * InMemoryCommandStore.mapReduceRangesInternal (InMemoryCommandStore.java:883-1016) as called by
+ * mapReduceActive (:863-870) from PreAccept.calculatePartialDeps (PreAccept.java:245-265): range commands
+ * in TxnId order, TxnId < T.executeAt, kind witnessed by T, status not INVALID (saveStatus < Erased),
+ * each of their ranges intersecting T's keys/ranges collected per Range (Range::compare order), p1
+ * excluded, then RangeDeps.Builder. end_inclusive = 1: Range.EndInclusive (s, e]; 0: StartInclusive [s, e).
+ * Ranges are reported as ids into the dictionary of distinct stored ranges sorted by (start, end). */
+typedef struct orc_rangedeps_result {
+    uint32_t  n_txn;
+    uint32_t  n_ranges;   uint64_t *rng_start; uint64_t *rng_end;   /* dictionary */
+    uint64_t *arena_off;  int32_t  *arena;      /* Java rangesToTxnIds per txn */
+    uint64_t *rd_off;     uint32_t *range_id;   /* per txn: dictionary ids, ascending */
+    uint64_t *u_off;      uint32_t *dep_txn;    /* per txn: batch indices in TxnId order */
+    uint64_t  total_edges;
+    uint64_t  visited;    /* range-command entries examined (work counter) */
+    uint64_t  queried;    /* txns evaluated */
+    double    query_s;
+    int       error;
+    char      message[256];
+} orc_rangedeps_result;
+
+orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
+                                          const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                          const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                          const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                          int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride);
+void orc_rangedeps_free(orc_rangedeps_result *r);
+
 /* Timestamp.compareTo (Timestamp.java:208-217) — exported for tests. */
 int orc_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
 
