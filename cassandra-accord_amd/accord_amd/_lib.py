@@ -23,7 +23,8 @@ u8p = C.POINTER(C.c_uint8)
 
 # Every symbol declared in include/accord_amd.h (tests check the library exports all of them).
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
-           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
+           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
+           "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get"]
 
 
@@ -55,6 +56,33 @@ class KeydepsOut(C.Structure):
                 ("need_arena", C.c_uint64), ("need_keys", C.c_uint64), ("need_deps", C.c_uint64),
                 ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("kd_off", C.c_void_p),
                 ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+
+
+class RangeBatchIn(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32), ("mem", C.c_uint32), ("n_pairs", C.c_uint64), ("n_ranges", C.c_uint64),
+                ("txn_id", TsCols), ("execute_at", TsCols),
+                ("status", C.c_void_p), ("key_off", C.c_void_p), ("key_code", C.c_void_p),
+                ("rng_off", C.c_void_p), ("rng_start", C.c_void_p), ("rng_end", C.c_void_p),
+                ("end_inclusive", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class RangedepsView(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32), ("n_ranges", C.c_uint32),
+                ("total_arena", C.c_uint64), ("total_ranges", C.c_uint64), ("total_deps", C.c_uint64),
+                ("total_edges", C.c_uint64),
+                ("rng_start", C.c_void_p), ("rng_end", C.c_void_p),
+                ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("rd_off", C.c_void_p),
+                ("range_id", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+
+
+class RangedepsOut(C.Structure):
+    _fields_ = [("mem", C.c_uint32),
+                ("cap_arena", C.c_uint64), ("cap_ranges", C.c_uint64), ("cap_deps", C.c_uint64), ("cap_dict", C.c_uint64),
+                ("need_arena", C.c_uint64), ("need_ranges", C.c_uint64), ("need_deps", C.c_uint64),
+                ("need_dict", C.c_uint64),
+                ("rng_start", C.c_void_p), ("rng_end", C.c_void_p),
+                ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("rd_off", C.c_void_p),
+                ("range_id", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
 
 
 class MergeIn(C.Structure):
@@ -114,6 +142,10 @@ def load():
     L.acc_keydeps_batch.restype = C.c_int
     L.acc_keydeps_copy_out.argtypes = [C.c_void_p, C.POINTER(KeydepsOut)]
     L.acc_keydeps_copy_out.restype = C.c_int
+    L.acc_rangedeps_batch.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(RangedepsView)]
+    L.acc_rangedeps_batch.restype = C.c_int
+    L.acc_rangedeps_copy_out.argtypes = [C.c_void_p, C.POINTER(RangedepsOut)]
+    L.acc_rangedeps_copy_out.restype = C.c_int
     L.acc_keydeps_merge.argtypes = [C.c_void_p, C.POINTER(MergeIn), C.POINTER(MergeView)]
     L.acc_keydeps_merge.restype = C.c_int
     L.acc_merge_copy_out.argtypes = [C.c_void_p, C.POINTER(MergeOut)]

@@ -138,6 +138,54 @@ class Context:
         view = self.keydeps_batch_raw(bi)
         return self.copy_out(view, batch)
 
+    # ---- RangeDeps batch
+    def range_batch_in(self, rb, keep: list) -> "L.RangeBatchIn":
+        b = rb.keys
+        a = dict(tm=np.ascontiguousarray(b.txn_msb, dtype=np.uint64), tl=np.ascontiguousarray(b.txn_lsb, dtype=np.uint64),
+                 tn=np.ascontiguousarray(b.txn_node, dtype=np.int32), em=np.ascontiguousarray(b.exe_msb, dtype=np.uint64),
+                 el=np.ascontiguousarray(b.exe_lsb, dtype=np.uint64), en=np.ascontiguousarray(b.exe_node, dtype=np.int32),
+                 st=np.ascontiguousarray(b.status, dtype=np.uint8), ko=np.ascontiguousarray(b.key_off, dtype=np.uint32),
+                 kc=np.ascontiguousarray(b.key_code, dtype=np.uint64), ro=np.ascontiguousarray(rb.rng_off, dtype=np.uint32),
+                 rs=np.ascontiguousarray(rb.rng_start, dtype=np.uint64), re=np.ascontiguousarray(rb.rng_end, dtype=np.uint64))
+        keep.append(a)
+        n = int(a["st"].shape[0])
+        p = lambda k: a[k].ctypes.data  # noqa: E731
+        return L.RangeBatchIn(n, L.ACC_MEM_HOST, int(a["ko"][-1]) if n else 0, int(a["ro"][-1]) if n else 0,
+                              L.TsCols(p("tm"), p("tl"), p("tn")), L.TsCols(p("em"), p("el"), p("en")),
+                              p("st"), p("ko"), p("kc"), p("ro"), p("rs"), p("re"), int(rb.end_inclusive), 0)
+
+    def rangedeps_batch_raw(self, batch_in: "L.RangeBatchIn") -> "L.RangedepsView":
+        view = L.RangedepsView()
+        self.check(self._lib.acc_rangedeps_batch(self._h, C.byref(batch_in), C.byref(view)))
+        return view
+
+    def calculate_partial_range_deps(self, rb) -> "BatchRangeDeps":
+        """PartialDeps.rangeDeps of PreAccept.calculatePartialDeps for every txn of a mixed key/range batch
+        (InMemoryCommandStore.mapReduceRangesInternal, impl/InMemoryCommandStore.java:883-1016)."""
+        keep = []
+        view = self.rangedeps_batch_raw(self.range_batch_in(rb, keep))
+        return self.copy_out_range(view)
+
+    def copy_out_range(self, view: "L.RangedepsView") -> "BatchRangeDeps":
+        n = view.n_txn
+        out = L.RangedepsOut()
+        out.mem = L.ACC_MEM_HOST
+        rc = self._lib.acc_rangedeps_copy_out(self._h, C.byref(out))
+        if rc not in (L.ACC_OK, L.ACC_E_CAP):
+            self.check(rc)
+        r = dict(arena_off=np.zeros(n + 1, np.uint64), rd_off=np.zeros(n + 1, np.uint64), u_off=np.zeros(n + 1, np.uint64),
+                 arena=np.zeros(max(out.need_arena, 1), np.int32), range_id=np.zeros(max(out.need_ranges, 1), np.uint32),
+                 dep_txn=np.zeros(max(out.need_deps, 1), np.uint32), rng_start=np.zeros(max(out.need_dict, 1), np.uint64),
+                 rng_end=np.zeros(max(out.need_dict, 1), np.uint64))
+        out.cap_arena, out.cap_ranges, out.cap_deps, out.cap_dict = (out.need_arena, out.need_ranges, out.need_deps,
+                                                                     out.need_dict)
+        for k, v in r.items():
+            setattr(out, k, v.ctypes.data)
+        self.check(self._lib.acc_rangedeps_copy_out(self._h, C.byref(out)))
+        return BatchRangeDeps(r["rng_start"][:out.need_dict], r["rng_end"][:out.need_dict], r["arena_off"],
+                              r["arena"][:out.need_arena], r["rd_off"], r["range_id"][:out.need_ranges], r["u_off"],
+                              r["dep_txn"][:out.need_deps], int(view.total_edges))
+
     def copy_out(self, view: "L.KeydepsView", batch=None) -> "BatchKeyDeps":
         n = view.n_txn
         out = L.KeydepsOut()
@@ -158,6 +206,37 @@ class Context:
         self.check(self._lib.acc_keydeps_copy_out(self._h, C.byref(out)))
         return BatchKeyDeps(arena_off, arena[:out.need_arena], kd_off, key_idx[:out.need_keys], u_off,
                             dep_txn[:out.need_deps], int(view.total_edges), batch)
+
+
+@dataclass
+class BatchRangeDeps:
+    """Per-txn PartialDeps.rangeDeps of a mixed batch in the acc_rangedeps_view layout: ranges as ids into the
+    dictionary (rng_start, rng_end) of distinct stored ranges sorted by Range::compare."""
+    rng_start: np.ndarray
+    rng_end: np.ndarray
+    arena_off: np.ndarray
+    arena: np.ndarray
+    rd_off: np.ndarray
+    range_id: np.ndarray
+    u_off: np.ndarray
+    dep_txn: np.ndarray
+    total_edges: int
+
+    def txn(self, t: int):
+        a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
+        r = self.range_id[self.rd_off[t]:self.rd_off[t + 1]]
+        d = self.dep_txn[self.u_off[t]:self.u_off[t + 1]]
+        return r, d, a
+
+    def range_deps(self, t: int):
+        """{(start, end): [dep batch index ...]} of txn t (RangeDeps.forEach over its ranges)."""
+        r, d, a = self.txn(t)
+        out, start = {}, len(r)
+        for i, rid in enumerate(r):
+            end = int(a[i])
+            out[(int(self.rng_start[rid]), int(self.rng_end[rid]))] = [int(d[x]) for x in a[start:end]]
+            start = end
+        return out
 
 
 @dataclass

@@ -284,3 +284,103 @@ def merge_batch(n_txn: int = 16_384, replies: int = 64, seed: int = CONFIG_SEEDS
     grp_off = (np.arange(n_txn + 1, dtype=np.uint64) * np.uint64(replies))
     return dict(grp_off=grp_off, key_off=key_off, key_code=key_code, val_off=val_off, txn_rank=txn_rank,
                 k2v_off=k2v_off, k2v=k2v)
+
+
+@dataclass
+class RangeBatch:
+    """A mixed key/range snapshot: `keys` is the acc_batch_in part (key-domain txns
+    list their keys; range-domain txns, TxnId domain bit = 1, list none), plus per-txn Ranges
+    [rng_off[t], rng_off[t+1]) for range-domain txns (sorted, non-overlapping: Ranges.ofSortedAndDeoverlapped)
+    and one Range bound type for the store (end_inclusive: Range.EndInclusive (s, e], else StartInclusive [s, e))."""
+    keys: Batch
+    rng_off: np.ndarray
+    rng_start: np.ndarray
+    rng_end: np.ndarray
+    end_inclusive: int = 1
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_txn(self) -> int:
+        return self.keys.n_txn
+
+    @property
+    def n_ranges(self) -> int:
+        return int(self.rng_off[-1])
+
+    def is_range(self) -> np.ndarray:
+        return (self.keys.txn_lsb & np.uint64(1)).astype(bool)
+
+    def arrays(self):
+        return dict(self.keys.arrays(), rng_off=self.rng_off, rng_start=self.rng_start, rng_end=self.rng_end)
+
+
+def rangedeps_batch(n_txn: int, seed: int, p_range: float = 0.5, keys_per_txn: int = 4, ranges_per_txn: int = 1,
+                    key_bits: int = 32, max_width_log2: int = 16, status_model: str = "model", window: int = 10_000,
+                    p_write: float = 0.5, p_syncpoint: float = 0.0, end_inclusive: int = 1) -> RangeBatch:
+    """Config 4 per SURVEY.md §8(d): txns interleaved in TxnId order, each a range txn with probability p_range
+    (`ranges_per_txn` disjoint ranges, start uniform over the 2^key_bits IntKey code space, width log-uniform
+    in [1, 2^max_width_log2]) or a key txn (`keys_per_txn` distinct uniform keys). Kinds Read/Write (p_write),
+    optional SyncPoint share; statuses and executeAt bumps as keydeps_batch."""
+    i = np.arange(n_txn, dtype=np.int64)
+    is_range = uniform01(seed, 20, n_txn) < p_range
+    kind = np.where(uniform01(seed, 1, n_txn) < p_write, WRITE, READ).astype(np.int64)
+    if p_syncpoint > 0:
+        kind = np.where(uniform01(seed, 2, n_txn) < p_syncpoint, SYNC_POINT, kind)
+    flags = (kind << 1) | is_range.astype(np.int64)
+    t_msb, t_lsb, t_node = encode_ts(np.ones(n_txn), i + 1, flags, 1 + (i % 8))
+    if status_model == "preaccepted":
+        status = np.full(n_txn, PREACCEPTED, dtype=np.uint8)
+    else:
+        u = uniform01(seed, 3, n_txn)
+        in_window = i >= n_txn - window
+        status = np.where(in_window, np.where(u < 0.7, PREACCEPTED, ACCEPTED),
+                          np.where(u < 0.8, APPLIED, np.where(u < 0.9, STABLE, COMMITTED))).astype(np.uint8)
+        u2 = uniform01(seed, 4, n_txn)
+        status = np.where(u2 < 0.001, INVALID_OR_TRUNCATED,
+                          np.where(u2 < 0.002, TRANSITIVELY_KNOWN, status)).astype(np.uint8)
+    committed = (status >= COMMITTED) & (status <= APPLIED)
+    bump = committed & (uniform01(seed, 5, n_txn) < 0.1)
+    bump_by = 1 + (stream(seed, 6, n_txn) % np.uint64(1000)).astype(np.int64)
+    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + (i % 1024))
+    exe_msb = np.where(bump, e_msb, t_msb).astype(np.uint64)
+    exe_lsb = np.where(bump, e_lsb_b, t_lsb).astype(np.uint64)
+    exe_node = np.where(bump, e_node_b, t_node).astype(np.int32)
+
+    space = 1 << key_bits
+    n_key_txn = int((~is_range).sum())
+    keys = _distinct_keys(seed, n_key_txn, keys_per_txn, lambda off, n: (stream(seed, 21, n, off) % np.uint64(space))
+                          .astype(np.int64))
+    counts = np.where(is_range, 0, keys_per_txn)
+    key_off = np.zeros(n_txn + 1, dtype=np.uint32)
+    np.cumsum(counts, out=key_off[1:])
+    key_code = keys.reshape(-1).astype(np.uint64)
+
+    n_rt = int(is_range.sum())
+    m = n_rt * ranges_per_txn
+    width = np.maximum(1, np.floor(np.exp2(uniform01(seed, 22, m) * max_width_log2))).astype(np.int64)
+    start = (stream(seed, 23, m) % np.uint64(max(1, space - (1 << max_width_log2) - 1))).astype(np.int64)
+    # ranges of one txn: sorted and non-overlapping (shift each past its predecessor's end)
+    st = start.reshape(n_rt, ranges_per_txn)
+    wd = width.reshape(n_rt, ranges_per_txn)
+    order = np.argsort(st, axis=1, kind="stable")
+    st = np.take_along_axis(st, order, 1)
+    wd = np.take_along_axis(wd, order, 1)
+    for j in range(1, ranges_per_txn):
+        st[:, j] = np.maximum(st[:, j], st[:, j - 1] + wd[:, j - 1])
+    rs = st.reshape(-1).astype(np.uint64)
+    re = (st + wd).reshape(-1).astype(np.uint64)
+    rcounts = np.where(is_range, ranges_per_txn, 0)
+    rng_off = np.zeros(n_txn + 1, dtype=np.uint32)
+    np.cumsum(rcounts, out=rng_off[1:])
+    kb = Batch(t_msb, t_lsb, t_node, exe_msb, exe_lsb, exe_node, status, key_off, key_code,
+               dict(n_txn=n_txn, seed=seed, p_range=p_range))
+    meta = dict(n_txn=n_txn, seed=seed, p_range=p_range, keys_per_txn=keys_per_txn, ranges_per_txn=ranges_per_txn,
+                key_bits=key_bits, max_width_log2=max_width_log2, status_model=status_model, window=window,
+                p_write=p_write, end_inclusive=end_inclusive)
+    return RangeBatch(kb, rng_off, rs, re, end_inclusive, meta)
+
+
+def config4(scale: float = 1.0, **kw) -> RangeBatch:
+    """BASELINE config 4: 10M range txns (1 EndInclusive range each) interleaved 50/50 with 10M key txns x 4
+    keys over the int32 key space (scale multiplies the txn count)."""
+    return rangedeps_batch(int(20_000_000 * scale), CONFIG_SEEDS["4"], **kw)

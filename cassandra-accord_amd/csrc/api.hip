@@ -6,6 +6,7 @@ namespace acc {
 void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view);
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
 void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
+void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
 }  // namespace acc
 
 extern "C" {
@@ -92,6 +93,46 @@ int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)
         if (v.total_arena) ACC_HIP(hipMemcpyAsync(out->arena, v.arena, v.total_arena * 4, kind, ctx->stream));
         if (v.total_keys) ACC_HIP(hipMemcpyAsync(out->key_idx, v.key_idx, v.total_keys * 4, kind, ctx->stream));
         if (v.total_deps) ACC_HIP(hipMemcpyAsync(out->dep_txn, v.dep_txn, v.total_deps * 4, kind, ctx->stream));
+        ctx->sync();
+    });
+}
+
+int acc_rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::rangedeps_batch(ctx, in, out_view);
+    });
+}
+
+int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        if (!out) acc::fail(ACC_E_ARG, "null argument");
+        if (!ctx->rd_valid) acc::fail(ACC_E_STATE, "no rangedeps result on this context");
+        const acc_rangedeps_view &v = ctx->rd_view;
+        out->need_arena = v.total_arena;
+        out->need_ranges = v.total_ranges;
+        out->need_deps = v.total_deps;
+        out->need_dict = v.n_ranges;
+        if (!out->arena_off || !out->rd_off || !out->u_off || out->cap_arena < v.total_arena ||
+            out->cap_ranges < v.total_ranges || out->cap_deps < v.total_deps || out->cap_dict < v.n_ranges)
+            acc::fail(ACC_E_CAP, "output capacity too small (required sizes written)");
+        if (out->mem != ACC_MEM_HOST && out->mem != ACC_MEM_DEVICE) acc::fail(ACC_E_ARG, "bad mem");
+        const hipMemcpyKind k = out->mem == ACC_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+        const size_t n1 = (size_t)v.n_txn + 1;
+        ACC_HIP(hipMemcpyAsync(out->arena_off, v.arena_off, n1 * 8, k, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->rd_off, v.rd_off, n1 * 8, k, ctx->stream));
+        ACC_HIP(hipMemcpyAsync(out->u_off, v.u_off, n1 * 8, k, ctx->stream));
+        if (v.total_arena) ACC_HIP(hipMemcpyAsync(out->arena, v.arena, v.total_arena * 4, k, ctx->stream));
+        if (v.total_ranges) ACC_HIP(hipMemcpyAsync(out->range_id, v.range_id, v.total_ranges * 4, k, ctx->stream));
+        if (v.total_deps) ACC_HIP(hipMemcpyAsync(out->dep_txn, v.dep_txn, v.total_deps * 4, k, ctx->stream));
+        if (v.n_ranges) {
+            ACC_HIP(hipMemcpyAsync(out->rng_start, v.rng_start, (size_t)v.n_ranges * 8, k, ctx->stream));
+            ACC_HIP(hipMemcpyAsync(out->rng_end, v.rng_end, (size_t)v.n_ranges * 8, k, ctx->stream));
+        }
         ctx->sync();
     });
 }

@@ -75,6 +75,8 @@ struct acc_ctx {
     // last results
     acc_keydeps_view kd_view{};
     acc_merge_view merge_view{};
+    acc_rangedeps_view rd_view{};
+    bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;
 

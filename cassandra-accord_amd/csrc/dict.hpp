@@ -1,0 +1,23 @@
+// dict.hpp — shared front end of the deps paths (keydeps.hip): input validation and the dense order-rank
+// dictionary of every TxnId and executeAt of a batch (Timestamp.compareTo, primitives/Timestamp.java:208-217).
+#pragma once
+
+#include "prims.hpp"
+
+namespace acc {
+
+struct Dictionary {
+    uint32_t *rank = nullptr;         // [2n]: rank[t] = TxnId of t, rank[n + t] = executeAt of t
+    uint32_t *txn_of_rank = nullptr;  // [2n]: txn index of each TxnId rank
+    int rbits = 0;                    // bits of the largest rank
+    bool batch_sorted = false;        // txns given in TxnId order
+    bool fast = false;                // sorted-batch dictionary taken
+    uint64_t hg[8] = {};              // prep words: ts word masks [0..2], key mask [3], errors [4], unsorted [5]
+};
+
+// key_off/key_code: the key-domain part (P pairs); owner[P] receives the txn of every pair; g[8] scratch words.
+void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                     const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
+                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out);
+
+}  // namespace acc

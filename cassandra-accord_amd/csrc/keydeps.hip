@@ -17,7 +17,7 @@
 //                  resolve identically), then only touches [scanStart, insertPos) plus the
 //                  uncommitted entries before scanStart instead of the whole O(prefix).
 //   5. build       per-T union of the per-key lists, indices into it, Java keysToTxnIds layout.
-#include "prims.hpp"
+#include "dict.hpp"
 
 namespace acc {
 
@@ -1613,45 +1613,15 @@ static void keydeps_v1_tail(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_vi
     ctx->kd_valid = true;
 }
 
-void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+// Validation (k_prep_txn: statuses, kinds, key order, TxnId order) and the order-rank dictionary of the 2N
+// timestamps (rank[t] = TxnId of t, rank[n + t] = executeAt of t; equal <=> Timestamp.equals). Shared by the
+// KeyDeps and RangeDeps paths. Throws the first validation error.
+void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                     const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
+                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out)
 {
-    if (!in || !view) fail(ACC_E_ARG, "null argument");
-    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
-    const uint32_t n = in->n_txn;
-    const size_t P = (size_t)in->n_pairs;
-    if (P >= 0xFFFFFFFFull) fail(ACC_E_ARG, "n_pairs must be < 2^32");
     hipStream_t st = ctx->stream;
-    ctx->kd_valid = false;
-
-    // ---- stage inputs
-    const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
-    if (n == 0 || P == 0) {
-        // no pairs: every txn has KeyDeps.NONE
-        uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
-        uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
-        uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
-        ACC_HIP(hipMemsetAsync(arena_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(kd_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(u_off, 0, ((size_t)n + 1) * 8, st));
-        *view = acc_keydeps_view{ n, 0, 0, 0, 0, arena_off, ctx->get<int32_t>("arena", 1), kd_off,
-                                  ctx->get<uint32_t>("key_idx", 1), u_off, ctx->get<uint32_t>("dep_txn", 1) };
-        ctx->kd_view = *view;
-        ctx->kd_valid = true;
-        ctx->sync();
-        return;
-    }
-    const uint64_t *tm = stage_in(ctx, "in_tm", in->txn_id.msb, n, in->mem);
-    const uint64_t *tl = stage_in(ctx, "in_tl", in->txn_id.lsb, n, in->mem);
-    const int32_t *tn = stage_in(ctx, "in_tn", in->txn_id.node, n, in->mem);
-    const uint64_t *em = stage_in(ctx, "in_em", in->execute_at.msb, n, in->mem);
-    const uint64_t *el = stage_in(ctx, "in_el", in->execute_at.lsb, n, in->mem);
-    const int32_t *en = stage_in(ctx, "in_en", in->execute_at.node, n, in->mem);
-    const uint8_t *status = stage_in(ctx, "in_status", in->status, n, in->mem);
-    const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
-
     // ---- 1. prep
-    uint64_t *g = ctx->get<uint64_t>("g", 8);
-    uint32_t *owner = ctx->get<uint32_t>("owner", P);
     ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
     uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
     launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, status,
@@ -1751,7 +1721,60 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     }
     if (!fast_dict) general_ranks();
     ctx->stat("keydeps.fast_dictionary", fast_dict ? 1 : 0);
-    const int rbits = bits_for(m - 1);
+    out.rank = rank;
+    out.txn_of_rank = txn_of_rank;
+    out.rbits = bits_for(m - 1);
+    out.batch_sorted = batch_sorted;
+    out.fast = fast_dict;
+    memcpy(out.hg, hg, sizeof hg);
+}
+
+void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+{
+    if (!in || !view) fail(ACC_E_ARG, "null argument");
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    const uint32_t n = in->n_txn;
+    const size_t P = (size_t)in->n_pairs;
+    if (P >= 0xFFFFFFFFull) fail(ACC_E_ARG, "n_pairs must be < 2^32");
+    hipStream_t st = ctx->stream;
+    ctx->kd_valid = false;
+
+    // ---- stage inputs
+    const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
+    if (n == 0 || P == 0) {
+        // no pairs: every txn has KeyDeps.NONE
+        uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
+        uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
+        uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
+        ACC_HIP(hipMemsetAsync(arena_off, 0, ((size_t)n + 1) * 8, st));
+        ACC_HIP(hipMemsetAsync(kd_off, 0, ((size_t)n + 1) * 8, st));
+        ACC_HIP(hipMemsetAsync(u_off, 0, ((size_t)n + 1) * 8, st));
+        *view = acc_keydeps_view{ n, 0, 0, 0, 0, arena_off, ctx->get<int32_t>("arena", 1), kd_off,
+                                  ctx->get<uint32_t>("key_idx", 1), u_off, ctx->get<uint32_t>("dep_txn", 1) };
+        ctx->kd_view = *view;
+        ctx->kd_valid = true;
+        ctx->sync();
+        return;
+    }
+    const uint64_t *tm = stage_in(ctx, "in_tm", in->txn_id.msb, n, in->mem);
+    const uint64_t *tl = stage_in(ctx, "in_tl", in->txn_id.lsb, n, in->mem);
+    const int32_t *tn = stage_in(ctx, "in_tn", in->txn_id.node, n, in->mem);
+    const uint64_t *em = stage_in(ctx, "in_em", in->execute_at.msb, n, in->mem);
+    const uint64_t *el = stage_in(ctx, "in_el", in->execute_at.lsb, n, in->mem);
+    const int32_t *en = stage_in(ctx, "in_en", in->execute_at.node, n, in->mem);
+    const uint8_t *status = stage_in(ctx, "in_status", in->status, n, in->mem);
+    const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
+
+    // ---- 1-2. prep + dictionary
+    uint64_t *g = ctx->get<uint64_t>("g", 8);
+    uint32_t *owner = ctx->get<uint32_t>("owner", P);
+    Dictionary dict;
+    prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict);
+    uint64_t hg[8];
+    memcpy(hg, dict.hg, sizeof hg);
+    const bool batch_sorted = dict.batch_sorted;
+    uint32_t *rank = dict.rank, *txn_of_rank = dict.txn_of_rank;
+    const int rbits = dict.rbits;
 
     // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
     PairPlan pp;

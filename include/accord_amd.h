@@ -16,6 +16,11 @@
  *   acc_keydeps_merge      KeyDeps.merge(List, getter, getter)       primitives/KeyDeps.java:115-135
  *                          (LinearMerger fold of linearUnion,         utils/RelationMultiMap.java:284-406,561-816)
  *                          batched over many coordinated txns (Deps.merge primitives/Deps.java:256-260).
+ *   acc_rangedeps_batch    the range-command part of InMemorySafeStore.mapReduceActive impl/InMemoryCommandStore.java:863-870
+ *                          -> mapReduceRangesInternal                 impl/InMemoryCommandStore.java:883-1016
+ *                          -> RangeDeps.Builder                       primitives/RangeDeps.java:873-891
+ *                          for every txn of a mixed key/range batch (PreAccept.calculatePartialDeps
+ *                          messages/PreAccept.java:245-265; SearchableRangeList stabbing core/utils/SearchableRangeList.java:89-116).
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -146,6 +151,57 @@ const char *acc_version(void);
 /* ---- KeyDeps batch: CommandsForKey conflict scan + KeyDeps.Builder for all txns of a batch ---- */
 int acc_keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *out_view);
 int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out);
+
+/* ---- RangeDeps batch: range-command stabbing + RangeDeps.Builder for all txns of a mixed batch ----
+ * Txns whose TxnId domain bit (lsb & 1, TxnId.java:124-157) is Range are range commands/queries with Ranges
+ * rng_start/rng_end[rng_off[t] .. rng_off[t+1]) (sorted and deoverlapped, start < end); key-domain txns list keys
+ * in key_off/key_code exactly as acc_batch_in and no ranges. A range txn whose status is INVALID_OR_TRUNCATED is
+ * an erased range command (saveStatus >= Erased, InMemoryCommandStore.java:892-893) and contributes no deps. */
+typedef struct acc_range_batch_in {
+    uint32_t    n_txn;
+    uint32_t    mem;           /* ACC_MEM_HOST or ACC_MEM_DEVICE for every pointer below */
+    uint64_t    n_pairs;       /* P = key_off[N] */
+    uint64_t    n_ranges;      /* R = rng_off[N]; P + R < 2^32 */
+    acc_ts_cols txn_id;
+    acc_ts_cols execute_at;
+    const uint8_t  *status;
+    const uint32_t *key_off;   /* [N+1] */
+    const uint64_t *key_code;  /* [P] */
+    const uint32_t *rng_off;   /* [N+1] */
+    const uint64_t *rng_start; /* [R] order-preserving codes of Range.start() */
+    const uint64_t *rng_end;   /* [R] order-preserving codes of Range.end() */
+    uint32_t    end_inclusive; /* 1: Range.EndInclusive (s, e]; 0: Range.StartInclusive [s, e) (Range.java:40-138) */
+    uint32_t    reserved;
+} acc_range_batch_in;
+
+/* Result of the last acc_rangedeps_batch (device pointers owned by the context). Ranges are ids into the
+ * dictionary of distinct stored ranges (the ranges of non-erased range commands) sorted by Range::compare
+ * (start, then end; Range.java:309-317). For txn t:
+ *   arena[arena_off[t] .. arena_off[t+1])      = Java RangeDeps.rangesToTxnIds (int[])
+ *   range_id[rd_off[t] .. rd_off[t+1])        = RangeDeps.ranges as dictionary ids (ascending)
+ *   dep_txn[u_off[t] .. u_off[t+1])           = RangeDeps.txnIds as batch indices, ascending TxnId order */
+typedef struct acc_rangedeps_view {
+    uint32_t n_txn;
+    uint32_t n_ranges;                  /* dictionary size */
+    uint64_t total_arena, total_ranges, total_deps, total_edges;
+    const uint64_t *rng_start, *rng_end;   /* [n_ranges] dictionary */
+    const uint64_t *arena_off;  const int32_t  *arena;
+    const uint64_t *rd_off;     const uint32_t *range_id;
+    const uint64_t *u_off;      const uint32_t *dep_txn;
+} acc_rangedeps_view;
+
+typedef struct acc_rangedeps_out {
+    uint32_t  mem;
+    uint64_t  cap_arena, cap_ranges, cap_deps, cap_dict;
+    uint64_t  need_arena, need_ranges, need_deps, need_dict;   /* written */
+    uint64_t *rng_start, *rng_end;      /* [cap_dict] */
+    uint64_t *arena_off;  int32_t  *arena;     /* [N+1], [cap_arena] */
+    uint64_t *rd_off;     uint32_t *range_id;  /* [N+1], [cap_ranges] */
+    uint64_t *u_off;      uint32_t *dep_txn;   /* [N+1], [cap_deps] */
+} acc_rangedeps_out;
+
+int acc_rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *out_view);
+int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out);
 
 /* ---- Deps.merge over many replies per txn ----
  * Input: R = n_groups groups (one coordinated txn each); group g owns replies

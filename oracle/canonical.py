@@ -139,3 +139,64 @@ def levelise(off, dep, exec_rank):
         level[t] = 1 + max(level[d] for d in preds) if preds else 0
     order = sorted(range(n), key=lambda t: (level[t], exec_rank[t], t))
     return np.array(level, dtype=np.uint32), np.array(order, dtype=np.uint32)
+
+
+def rangedeps_batch(rb, query_lo=0, query_hi=None):
+    """RangeDeps of a mixed key/range batch as set definitions (InMemoryCommandStore.mapReduceRangesInternal,
+    InMemoryCommandStore.java:883-1016, under PreAccept.calculatePartialDeps, PreAccept.java:245-265):
+
+        deps(T) = { (r, C) : C a range command (range-domain txn, status != INVALID_OR_TRUNCATED),
+                    C.txnId < T.executeAt, T.kind.witnesses(C.kind), r in C.ranges, r intersects T's keys
+                    (Range.contains) or T's ranges (start < that.end && end > that.start) } minus C == p1
+
+    grouped as a RangeDeps map {Range: {TxnId}} in Java layout. Returns (dict_start, dict_end, per txn
+    (range ids, dep txn list, rangesToTxnIds)), range ids indexing the sorted distinct stored ranges."""
+    b = rb.keys
+    n = b.n_txn
+    tid = [ts_key(b.txn_msb[i], b.txn_lsb[i], b.txn_node[i]) for i in range(n)]
+    tex = [ts_key(b.exe_msb[i], b.exe_lsb[i], b.exe_node[i]) for i in range(n)]
+    kinds = [kind_of(b.txn_lsb[i]) for i in range(n)]
+    is_range = [int(b.txn_lsb[i]) & 1 for i in range(n)]
+    status = [int(s) for s in b.status]
+    ranges = [[(int(rb.rng_start[j]), int(rb.rng_end[j])) for j in range(int(rb.rng_off[t]), int(rb.rng_off[t + 1]))]
+              for t in range(n)]
+    keys = [[int(x) for x in b.key_code[int(b.key_off[t]):int(b.key_off[t + 1])]] for t in range(n)]
+    cmds = [c for c in range(n) if is_range[c] and status[c] != 7 and ranges[c]]
+    dictionary = sorted({r for c in cmds for r in ranges[c]})
+    rid = {r: i for i, r in enumerate(dictionary)}
+    ei = int(rb.end_inclusive)
+
+    def contains(r, k):
+        s, e = r
+        return (s < k <= e) if ei else (s <= k < e)
+
+    out = []
+    hi = n if query_hi is None else query_hi
+    for t in range(n):
+        if not (query_lo <= t < hi):
+            out.append(([], [], []))
+            continue
+        wk = WITNESSES[kinds[t]]
+        p1 = None if tex[t] == tid[t] else t
+        m: dict = {}
+        for c in cmds:
+            if not (tid[c] < tex[t]) or kinds[c] not in wk or c == p1:
+                continue
+            for r in ranges[c]:
+                if is_range[t]:
+                    hit = any(r[0] < q[1] and r[1] > q[0] for q in ranges[t])
+                else:
+                    hit = any(contains(r, k) for k in keys[t])
+                if hit:
+                    m.setdefault(rid[r], set()).add(c)
+        rids = sorted(m)
+        union = sorted({c for cs in m.values() for c in cs}, key=lambda d: tid[d])
+        pos = {d: i for i, d in enumerate(union)}
+        k2v, end = [], len(rids)
+        for r in rids:
+            end += len(m[r])
+            k2v.append(end)
+        for r in rids:
+            k2v.extend(pos[d] for d in sorted(m[r], key=lambda d: tid[d]))
+        out.append((rids, union, k2v))
+    return np.array([r[0] for r in dictionary], np.uint64), np.array([r[1] for r in dictionary], np.uint64), out

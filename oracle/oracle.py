@@ -39,6 +39,16 @@ class MergeResult(C.Structure):
                 ("error", C.c_int), ("message", C.c_char * 256)]
 
 
+class RangedepsResult(C.Structure):
+    _fields_ = [("n_txn", C.c_uint32),
+                ("n_ranges", C.c_uint32), ("rng_start", u64p), ("rng_end", u64p),
+                ("arena_off", u64p), ("arena", i32p),
+                ("rd_off", u64p), ("range_id", u32p),
+                ("u_off", u64p), ("dep_txn", u32p),
+                ("total_edges", C.c_uint64), ("visited", C.c_uint64), ("queried", C.c_uint64),
+                ("query_s", C.c_double), ("error", C.c_int), ("message", C.c_char * 256)]
+
+
 _lib = None
 
 
@@ -62,6 +72,10 @@ def lib():
         L.orc_merge_free.argtypes = [C.POINTER(MergeResult)]
         L.orc_levelise.restype = C.c_int
         L.orc_levelise.argtypes = [C.c_uint32, u64p, u32p, u32p, u32p, u32p, u32p]
+        L.orc_rangedeps_batch.restype = C.POINTER(RangedepsResult)
+        L.orc_rangedeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
+                                          u32p, u64p, u64p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_rangedeps_free.argtypes = [C.POINTER(RangedepsResult)]
         L.orc_ts_compare.restype = C.c_int
         L.orc_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
@@ -127,6 +141,64 @@ def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | N
                               float(R.query_s))
     finally:
         L.orc_keydeps_free(r)
+    return out
+
+
+@dataclass
+class RangeDepsBatchOut:
+    """Per-txn RangeDeps in the acc_rangedeps_view layout: ranges as ids into the dictionary of distinct stored
+    ranges (sorted by Range.compare), rangesToTxnIds per txn, txnIds as batch indices."""
+    rng_start: np.ndarray
+    rng_end: np.ndarray
+    arena_off: np.ndarray
+    arena: np.ndarray
+    rd_off: np.ndarray
+    range_id: np.ndarray
+    u_off: np.ndarray
+    dep_txn: np.ndarray
+    total_edges: int = 0
+    visited: int = 0
+    queried: int = 0
+    query_s: float = 0.0
+
+    def txn(self, t: int):
+        a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
+        r = self.range_id[self.rd_off[t]:self.rd_off[t + 1]]
+        d = self.dep_txn[self.u_off[t]:self.u_off[t + 1]]
+        return r, d, a
+
+
+def rangedeps_batch(rb, query_lo: int = 0, query_hi: int | None = None, query_stride: int = 1) -> RangeDepsBatchOut:
+    """RangeDeps of every queried txn of a mixed key/range batch (accord_oracle.c orc_rangedeps_batch)."""
+    L = lib()
+    b = rb.keys
+    n = b.n_txn
+    arrs = [np.ascontiguousarray(x) for x in (b.txn_msb.astype(np.uint64), b.txn_lsb.astype(np.uint64),
+                                              b.txn_node.astype(np.int32), b.exe_msb.astype(np.uint64),
+                                              b.exe_lsb.astype(np.uint64), b.exe_node.astype(np.int32),
+                                              b.status.astype(np.uint8), b.key_off.astype(np.uint32),
+                                              b.key_code.astype(np.uint64), rb.rng_off.astype(np.uint32),
+                                              rb.rng_start.astype(np.uint64), rb.rng_end.astype(np.uint64))]
+    types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u64p, u64p]
+    r = L.orc_rangedeps_batch(n, *[_p(a, t) for a, t in zip(arrs, types)], int(rb.end_inclusive), query_lo,
+                              n if query_hi is None else query_hi, query_stride)
+    try:
+        R = r.contents
+        if R.error:
+            raise OracleError(R.error, R.message.decode())
+        nr = int(R.n_ranges)
+        arena_off = np.ctypeslib.as_array(R.arena_off, (n + 1,)).copy()
+        rd_off = np.ctypeslib.as_array(R.rd_off, (n + 1,)).copy()
+        u_off = np.ctypeslib.as_array(R.u_off, (n + 1,)).copy()
+        na, nk, nd = int(arena_off[-1]), int(rd_off[-1]), int(u_off[-1])
+        out = RangeDepsBatchOut(np.ctypeslib.as_array(R.rng_start, (max(nr, 1),))[:nr].copy(),
+                                np.ctypeslib.as_array(R.rng_end, (max(nr, 1),))[:nr].copy(),
+                                arena_off, np.ctypeslib.as_array(R.arena, (max(na, 1),))[:na].copy(),
+                                rd_off, np.ctypeslib.as_array(R.range_id, (max(nk, 1),))[:nk].copy(),
+                                u_off, np.ctypeslib.as_array(R.dep_txn, (max(nd, 1),))[:nd].copy(),
+                                int(R.total_edges), int(R.visited), int(R.queried), float(R.query_s))
+    finally:
+        L.orc_rangedeps_free(r)
     return out
 
 

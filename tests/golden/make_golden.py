@@ -40,5 +40,28 @@ def main():
         print(path, os.path.getsize(path), "bytes; edges", o.total_edges)
 
 
+def config4s():
+    """BASELINE config 4 scaled by 1/1000 (20k txns) with the key space scaled by 2^-10 so the stab depth (ranges
+    containing a key, ~14) matches the full config: RangeDeps from the C restatement, cross-checked against the
+    canonical set model on three query windows (the set model is O(txns x range commands))."""
+    rb = W.config4(0.001, key_bits=22)
+    o = oracle.rangedeps_batch(rb)
+    for lo in (0, 9_000, 19_700):
+        ds, de, c = canonical.rangedeps_batch(rb, query_lo=lo, query_hi=lo + 300)
+        assert np.array_equal(ds, o.rng_start) and np.array_equal(de, o.rng_end)
+        for t in range(lo, lo + 300):
+            r, d, a = o.txn(t)
+            assert (list(r), list(d), list(a)) == c[t], f"oracle/canonical mismatch at txn {t}"
+    out = {f"out_{f}": getattr(o, f) for f in ("rng_start", "rng_end", "arena_off", "arena", "rd_off", "range_id",
+                                               "u_off", "dep_txn")}
+    path = os.path.join(HERE, "config4s.npz")
+    np.savez_compressed(path, **rb.arrays(), end_inclusive=np.int32(rb.end_inclusive), **out)
+    print(path, os.path.getsize(path), "bytes; edges", o.total_edges)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "4":
+        config4s()
+    else:
+        main()
+        config4s()
