@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
-"""Bench: batched Accord dependency calculation (PreAccept.calculatePartialDeps for every txn of a
-CommandsForKey snapshot) on MI355X through the C ABI.
+"""Bench: batched Accord dependency calculation on MI355X through the C ABI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload = BASELINE.json configs[1]: 1M txns x 8 keys, zipf(0.99) over 1M keys, read/write mix,
-status model of SURVEY.md §8(d). A step = one acc_keydeps_batch over the whole batch with inputs
-already resident in HBM (device pointers) and results left device-resident (acc_keydeps_view).
-Multi-GPU: each rank is one CommandStore shard holding its own 1M-txn snapshot (independent seed), no
-data-path collective: weak scaling. Prints ONE JSON line on rank 0.
+--config 2 (default; BASELINE.json configs[1], the metric's workload): KeyDeps of 1M txns x 8 keys, zipf(0.99) over
+1M keys, read/write mix, status model of SURVEY.md §8(d). A step = one acc_keydeps_batch over the whole batch
+(PreAccept.calculatePartialDeps for every txn of a CommandsForKey snapshot) with inputs already resident in HBM
+(device pointers) and results left device-resident (acc_keydeps_view).
+--config 4 (configs[3]): RangeDeps of 10M range txns (1 EndInclusive range each, log-uniform widths <= 2^16)
+interleaved with 10M key txns x 4 keys over the int32 key space; a step = one acc_rangedeps_batch.
+
+Multi-GPU: each rank is one CommandStore shard holding its own snapshot (independent seed), no data-path
+collective: weak scaling. Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -26,14 +29,67 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
 
 
-def algorithmic_bytes(n_txn, n_pairs, sum_kd, sum_e, sum_u):
-    """compulsory traffic, each input read once and each output written once."""
+def keydeps_bytes(n_txn, n_pairs, sum_kd, sum_e, sum_u):
+    """SURVEY.md §8(d) KeyDeps batch: compulsory traffic, each input read once and each output written once."""
     b_in = 8 * n_pairs + 4 * (n_txn + 1) + 41 * n_txn
     b_out = 4 * (sum_kd + sum_e) + 4 * sum_kd + 4 * sum_u + 8 * (n_txn + 1)
     return b_in, b_out
 
 
-def cpu_baseline(batch, seconds_target):
+def rangedeps_bytes(n_txn, n_pairs, n_ranges, sum_rd, sum_e, sum_u, n_dict):
+    """SURVEY.md §8(d) RangeDeps batch: range bounds + owners + txn columns + keys in; Java arena, range ids, TxnId
+    indices, three offset arrays and the stored-range dictionary out."""
+    b_in = 16 * n_ranges + 8 * (n_txn + 1) + 41 * n_txn + 8 * n_pairs
+    b_out = 4 * (sum_rd + sum_e) + 4 * sum_rd + 4 * sum_u + 24 * (n_txn + 1) + 16 * n_dict
+    return b_in, b_out
+
+
+def profile_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprof summary (profiles/*_summary.json: FETCH_SIZE
+    x 2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get("k_" + kernel) or d.get("kernels", {}).get(kernel)
+        if k and "hbm_read_bytes_per_launch" in k:
+            best = (k["hbm_read_bytes_per_launch"] + k["hbm_write_bytes_per_launch"], os.path.relpath(p, ROOT))
+    return best
+
+
+def roofline(step_bytes, timing, steps):
+    """Contract roofline for the dominant kernel: achieved = algorithmic bytes of the batch one launch processes /
+    that kernel's average launch (HIP events on the context stream). step_* = the same bytes over the device time of
+    every kernel of the step (the whole pipeline as one launch: the stricter figure)."""
+    kernel_ms = sum(v[0] for v in timing.values()) / steps
+    dom_name, (dom_total, dom_launches) = max(timing.items(), key=lambda kv: kv[1][0])
+    dom_avg_ms = dom_total / max(dom_launches, 1)
+    achieved = step_bytes / (dom_avg_ms / 1000.0) / 1e9
+    step_achieved = step_bytes / (kernel_ms / 1000.0) / 1e9
+    tr = profile_traffic(dom_name)
+    return {
+        "bound": "hbm",
+        "kernel": dom_name,
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": int(tr[0]) if tr else None,
+        "traffic_source": tr[1] if tr else None,
+        "algorithmic_bytes_per_launch": int(step_bytes),
+        "kernel_avg_ms": round(dom_avg_ms, 4),
+        "launches_per_step": dom_launches / steps,
+        "share_of_step": round(dom_total / steps / kernel_ms, 3),
+        "step_kernel_ms": round(kernel_ms, 4),
+        "step_achieved": round(step_achieved, 1),
+        "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
+    }
+
+
+def keydeps_cpu_baseline(batch):
     """The C restatement (oracle, kind "port") on a strided sample of query txns, single thread."""
     import oracle
     n = batch.n_txn
@@ -50,55 +106,49 @@ def cpu_baseline(batch, seconds_target):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scale", type=float, default=1.0, help="fraction of config 2 (testing only)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    args = ap.parse_args()
+def rangedeps_cpu_baseline(rb):
+    """The C restatement of mapReduceRangesInternal (a linear walk of every range command per query, as the
+    reference's TreeMap forEach) on a strided sample of query txns, single thread."""
+    import oracle
+    n = rb.n_txn
+    stride = max(1, int(os.environ.get("ACC_CPU_STRIDE_RD", str(max(1, n // 120)))))
+    o = oracle.rangedeps_batch(rb, query_lo=0, query_hi=n, query_stride=stride)
+    kp = np.diff(rb.keys.key_off.astype(np.int64)) + np.diff(rb.rng_off.astype(np.int64))
+    probes = int(kp[::stride].sum())
+    return {
+        "value": round(probes / o.query_s, 1),
+        "unit": "key probes/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"every {stride}th txn of the same config-4 batch ({o.queried} txns, {probes} key/range probes, "
+                   f"{o.query_s:.1f} s of range-command scans + RangeDeps.Builder)"),
+    }
 
+
+def dist_setup(args):
     import torch
     import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+    return world, rank, local, torch.device("cuda", local)
 
-    from accord_amd import _lib as L
-    from accord_amd import workload as W
-    from accord_amd.deps import Context
 
-    # each rank: an independent CommandStore snapshot of config 2 (rank 0 = the canonical seed)
-    seed = W.CONFIG_SEEDS["2"] + 0x1000 * rank
-    n_txn = int(1_000_000 * args.scale)
-    batch = W.keydeps_batch(n_txn, 8, max(1000, n_txn), seed, "zipf", 0.99, status_model="model")
-
-    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in batch.arrays().items()}
-    torch.cuda.synchronize()
-    bi = L.BatchIn(batch.n_txn, L.ACC_MEM_DEVICE, batch.n_pairs,
-                   L.TsCols(t["txn_msb"].data_ptr(), t["txn_lsb"].data_ptr(), t["txn_node"].data_ptr()),
-                   L.TsCols(t["exe_msb"].data_ptr(), t["exe_lsb"].data_ptr(), t["exe_node"].data_ptr()),
-                   t["status"].data_ptr(), t["key_off"].data_ptr(), t["key_code"].data_ptr())
-
-    ctx = Context(local, timing=True)
-    view = None
+def timed_steps(args, world, dev, step):
+    import torch
+    import torch.distributed as dist
     for _ in range(args.warmup):
-        view = ctx.keydeps_batch_raw(bi)
-    ctx.timing_reset()
-
+        step()
+    step.ctx.timing_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        view = ctx.keydeps_batch_raw(bi)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -107,31 +157,42 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    return elapsed
 
-    timing = ctx.timing()  # per kernel name: (total ms over the timed steps, launches)
-    ms_per_step = elapsed * 1000.0 / args.steps
-    kernel_ms = sum(v[0] for v in timing.values()) / args.steps
-    dom_name, (dom_total, dom_launches) = max(timing.items(), key=lambda kv: kv[1][0])
 
-    b_in, b_out = algorithmic_bytes(batch.n_txn, batch.n_pairs, view.total_keys, view.total_edges,
-                                    view.total_deps)
-    step_bytes = b_in + b_out
-    achieved = step_bytes / (kernel_ms / 1000.0) / 1e9
+class Step:
+    def __init__(self, ctx, fn):
+        self.ctx, self.fn, self.view = ctx, fn, None
 
-    pairs_total = batch.n_pairs * world
-    value = pairs_total * args.steps / elapsed
+    def __call__(self):
+        self.view = self.fn()
 
+
+def run_config2(args, world, rank, local, dev):
+    import torch
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import Context
+
+    seed = W.CONFIG_SEEDS["2"] + 0x1000 * rank
+    n_txn = int(1_000_000 * args.scale)
+    batch = W.keydeps_batch(n_txn, 8, max(1000, n_txn), seed, "zipf", 0.99, status_model="model")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in batch.arrays().items()}
+    torch.cuda.synchronize()
+    bi = L.BatchIn(batch.n_txn, L.ACC_MEM_DEVICE, batch.n_pairs,
+                   L.TsCols(t["txn_msb"].data_ptr(), t["txn_lsb"].data_ptr(), t["txn_node"].data_ptr()),
+                   L.TsCols(t["exe_msb"].data_ptr(), t["exe_lsb"].data_ptr(), t["exe_node"].data_ptr()),
+                   t["status"].data_ptr(), t["key_off"].data_ptr(), t["key_code"].data_ptr())
+    ctx = Context(local, timing=True)
+    step = Step(ctx, lambda: ctx.keydeps_batch_raw(bi))
+    elapsed = timed_steps(args, world, dev, step)
+    view = step.view
+    timing = ctx.timing()
+    b_in, b_out = keydeps_bytes(batch.n_txn, batch.n_pairs, view.total_keys, view.total_edges, view.total_deps)
     result = {
         "metric": "txn-key conflict pairs resolved/sec (node)",
-        "value": round(value, 1),
+        "value": round(batch.n_pairs * world * args.steps / elapsed, 1),
         "unit": "txn-key pairs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
         "dtype": "u32/u64 (integer)",
         "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) status model)",
         "config": {
@@ -143,31 +204,94 @@ def main():
             "parallelism": f"keyspace shards x{world} (independent CommandStores)",
         },
         "dep_edges_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
-        "roofline": {
-            "bound": "hbm",
-            "scope": "step: SURVEY §8(d) algorithmic bytes of one batch / device time of all kernels of the step",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "algorithmic_bytes_per_step": int(step_bytes),
-            "kernel_ms_per_step": round(kernel_ms, 4),
-            "dominant_kernel": {"name": dom_name, "avg_ms": round(dom_total / max(dom_launches, 1), 4),
-                                "launches_per_step": dom_launches / args.steps,
-                                "share_of_step": round(dom_total / args.steps / kernel_ms, 3)},
-        },
+        "roofline": roofline(b_in + b_out, timing, args.steps),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
-    result["path_stats"] = ctx.stats()
+        result["cpu_baseline"] = keydeps_cpu_baseline(batch)
+    return ctx, timing, elapsed, result
+
+
+def run_config4(args, world, rank, local, dev):
+    import torch
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import Context
+
+    rb = W.rangedeps_batch(int(20_000_000 * args.scale), W.CONFIG_SEEDS["4"] + 0x1000 * rank)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in rb.arrays().items()}
+    torch.cuda.synchronize()
+    P, R = rb.keys.n_pairs, rb.n_ranges
+    bi = L.RangeBatchIn(rb.n_txn, L.ACC_MEM_DEVICE, P, R,
+                        L.TsCols(t["txn_msb"].data_ptr(), t["txn_lsb"].data_ptr(), t["txn_node"].data_ptr()),
+                        L.TsCols(t["exe_msb"].data_ptr(), t["exe_lsb"].data_ptr(), t["exe_node"].data_ptr()),
+                        t["status"].data_ptr(), t["key_off"].data_ptr(), t["key_code"].data_ptr(),
+                        t["rng_off"].data_ptr(), t["rng_start"].data_ptr(), t["rng_end"].data_ptr(),
+                        int(rb.end_inclusive), 0)
+    ctx = Context(local, timing=True)
+    step = Step(ctx, lambda: ctx.rangedeps_batch_raw(bi))
+    elapsed = timed_steps(args, world, dev, step)
+    view = step.view
+    timing = ctx.timing()
+    b_in, b_out = rangedeps_bytes(rb.n_txn, P, R, view.total_ranges, view.total_edges, view.total_deps, view.n_ranges)
+    probes = P + R
+    result = {
+        "metric": "RangeDeps key probes resolved/sec (node)",
+        "value": round(probes * world * args.steps / elapsed, 1),
+        "unit": "key probes/s",
+        "dtype": "u32/u64 (integer)",
+        "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) config 4)",
+        "config": {
+            "workload": "config4: RangeDeps of a mixed batch, 10M range txns (1 EndInclusive range, width log-uniform "
+                        "in [1, 2^16], start uniform over int32) + 10M key txns x 4 uniform keys, interleaved 50/50",
+            "n_txn_per_gpu": rb.n_txn,
+            "key_probes_per_gpu": probes,
+            "range_commands_per_gpu": R,
+            "dep_entries_per_gpu": int(view.total_edges),
+            "parallelism": f"keyspace shards x{world} (independent CommandStores)",
+        },
+        "dep_entries_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
+        "roofline": roofline(b_in + b_out, timing, args.steps),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = rangedeps_cpu_baseline(rb)
+    return ctx, timing, elapsed, result
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="2", choices=["2", "4"])
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config (testing only)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, dev = dist_setup(args)
+    run = {"2": run_config2, "4": run_config4}[args.config]
+    ctx, timing, elapsed, result = run(args, world, rank, local, dev)
+    out = {
+        "metric": result.pop("metric"),
+        "value": result.pop("value"),
+        "unit": result.pop("unit"),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1000.0 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+    }
+    out.update(result)
+    out["path_stats"] = ctx.stats()
     if os.environ.get("ACC_BENCH_KERNELS"):
-        result["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in
-                                         sorted(timing.items(), key=lambda kv: -kv[1][0])}
+        out["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in
+                                      sorted(timing.items(), key=lambda kv: -kv[1][0])}
     ctx.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

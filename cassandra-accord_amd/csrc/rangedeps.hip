@@ -183,14 +183,20 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint
                                                          uint64_t *__restrict__ dict_e, Runs rs_plan, int s_bits, int cls_only,
                                                          uint64_t *__restrict__ ckey, uint32_t *__restrict__ cls_hist)
 {
+    __shared__ uint32_t h[NCLS];
+    if (threadIdx.x < NCLS) h[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= ne) return;
-    const uint32_t i = perm[p], rid = incl[p] - 1;
-    rid_of[i] = rid;
-    if (flag[p]) { dict_s[rid] = e_s[i]; dict_e[rid] = e_e[i]; }
-    const uint32_t c = width_class(e_s[i], e_e[i]);
-    ckey[i] = cls_only ? (uint64_t)c : (((uint64_t)c << s_bits) | pext_runs(e_s[i], rs_plan));
-    atomicAdd(&cls_hist[c], 1u);
+    if (p < ne) {
+        const uint32_t i = perm[p], rid = incl[p] - 1;
+        rid_of[i] = rid;
+        if (flag[p]) { dict_s[rid] = e_s[i]; dict_e[rid] = e_e[i]; }
+        const uint32_t c = width_class(e_s[i], e_e[i]);
+        ckey[i] = cls_only ? (uint64_t)c : (((uint64_t)c << s_bits) | pext_runs(e_s[i], rs_plan));
+        atomicAdd(&h[c], 1u);   // LDS histogram; one global atomic per class and block (33 hot words otherwise)
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLS && h[threadIdx.x]) atomicAdd(&cls_hist[threadIdx.x], h[threadIdx.x]);
 }
 
 __global__ void k_rd_class_off(const uint32_t *__restrict__ hist, uint32_t *__restrict__ off)
