@@ -24,7 +24,7 @@ u8p = C.POINTER(C.c_uint8)
 # Every symbol declared in include/accord_amd.h (tests check the library exports all of them).
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
            "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
-           "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
+           "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get"]
 
 
@@ -110,6 +110,19 @@ class MergeOut(C.Structure):
                 ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
 
 
+class FragStreams(C.Structure):
+    _fields_ = [("world", C.c_uint32), ("mem", C.c_uint32),
+                ("cap_frag", C.c_uint64), ("cap_keys", C.c_uint64), ("cap_vals", C.c_uint64), ("cap_k2v", C.c_uint64),
+                ("hdr", C.c_void_p), ("keys", C.c_void_p), ("vals", C.c_void_p), ("k2v", C.c_void_p),
+                ("frag_off", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("k2v_off", C.c_void_p)]
+
+
+class FragRecv(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("world", C.c_uint32), ("rank", C.c_uint32), ("n_txn", C.c_uint32),
+                ("n_frag", C.c_void_p), ("n_keys", C.c_void_p), ("n_vals", C.c_void_p), ("n_k2v", C.c_void_p),
+                ("hdr", C.c_void_p), ("keys", C.c_void_p), ("vals", C.c_void_p), ("k2v", C.c_void_p)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -146,6 +159,10 @@ def load():
     L.acc_rangedeps_batch.restype = C.c_int
     L.acc_rangedeps_copy_out.argtypes = [C.c_void_p, C.POINTER(RangedepsOut)]
     L.acc_rangedeps_copy_out.restype = C.c_int
+    L.acc_shard_pack.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(FragStreams)]
+    L.acc_shard_pack.restype = C.c_int
+    L.acc_shard_merge.argtypes = [C.c_void_p, C.POINTER(FragRecv), C.POINTER(MergeView)]
+    L.acc_shard_merge.restype = C.c_int
     L.acc_keydeps_merge.argtypes = [C.c_void_p, C.POINTER(MergeIn), C.POINTER(MergeView)]
     L.acc_keydeps_merge.restype = C.c_int
     L.acc_merge_copy_out.argtypes = [C.c_void_p, C.POINTER(MergeOut)]

@@ -351,6 +351,11 @@ def keydeps_merge(ctx: Context, m: dict) -> dict:
     mi = _merge_in(m, keep)
     view = L.MergeView()
     ctx.check(ctx._lib.acc_keydeps_merge(ctx.handle, C.byref(mi), C.byref(view)))
+    return merge_copy_out(ctx, view)
+
+
+def merge_copy_out(ctx: Context, view) -> dict:
+    """Host copy of the last merge result on ctx (acc_merge_copy_out, two-call sizing)."""
     out = L.MergeOut()
     out.mem = L.ACC_MEM_HOST
     rc = ctx._lib.acc_merge_copy_out(ctx.handle, C.byref(out))

@@ -113,3 +113,106 @@ def unpack_to_merge(recv: np.ndarray, recv_counts: np.ndarray, home_txns: np.nda
 
 def home_txns(n_txn: int, rank: int, world: int) -> np.ndarray:
     return np.arange(rank, n_txn, world, dtype=np.int64)
+
+
+# ---------------------------------------------------------------- device path (acc_shard_pack / acc_shard_merge)
+#
+# The same reduce with every data-path step on the GPU: acc_shard_pack writes the fragment streams (destination-
+# major) straight into torch device buffers, four all_to_all_single calls move them (RCCL over xGMI with the nccl
+# backend; host copies with gloo), acc_shard_merge orders them by txn and runs the batched KeyDeps.merge.
+
+STREAMS = (("hdr", 4, "int32"), ("keys", 1, "int64"), ("vals", 1, "int32"), ("k2v", 1, "int32"))
+
+
+def batch_in_device(batch: Batch, dev):
+    """acc_batch_in over torch device copies of a batch's columns (kept alive in the returned dict)."""
+    import torch
+    from . import _lib as L
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in batch.arrays().items()}
+    bi = L.BatchIn(batch.n_txn, L.ACC_MEM_DEVICE, batch.n_pairs,
+                   L.TsCols(t["txn_msb"].data_ptr(), t["txn_lsb"].data_ptr(), t["txn_node"].data_ptr()),
+                   L.TsCols(t["exe_msb"].data_ptr(), t["exe_lsb"].data_ptr(), t["exe_node"].data_ptr()),
+                   t["status"].data_ptr(), t["key_off"].data_ptr(), t["key_code"].data_ptr())
+    return bi, t
+
+
+def shard_pack(ctx, bi, world: int, dev):
+    """Fragments of the last acc_keydeps_batch on ctx for every home rank: (streams dict of torch tensors on dev,
+    per-destination element counts [4, world] int64 numpy)."""
+    import ctypes as C
+    import torch
+    from . import _lib as L
+    offs = [np.zeros(world + 1, np.uint64) for _ in range(4)]
+    fs = L.FragStreams()
+    fs.world, fs.mem = world, L.ACC_MEM_DEVICE
+    fs.frag_off, fs.key_off, fs.val_off, fs.k2v_off = (o.ctypes.data for o in offs)
+    rc = ctx._lib.acc_shard_pack(ctx.handle, C.byref(bi), C.byref(fs))
+    if rc != L.ACC_E_CAP:
+        ctx.check(rc)
+    need = [int(o[-1]) for o in offs]
+    bufs = {}
+    for (name, mult, dt), cnt in zip(STREAMS, need):
+        bufs[name] = torch.empty(max(cnt * mult, 1), dtype=getattr(torch, dt), device=dev)
+    fs.cap_frag, fs.cap_keys, fs.cap_vals, fs.cap_k2v = need
+    fs.hdr, fs.keys, fs.vals, fs.k2v = (bufs[n].data_ptr() for n, _, _ in STREAMS)
+    ctx.check(ctx._lib.acc_shard_pack(ctx.handle, C.byref(bi), C.byref(fs)))
+    counts = np.stack([np.diff(o.astype(np.int64)) for o in offs])   # [stream, dest]
+    for (name, mult, _), cnt in zip(STREAMS, need):
+        bufs[name] = bufs[name][:cnt * mult]
+    return bufs, counts
+
+
+def exchange_streams(bufs: dict, counts: np.ndarray, group=None):
+    """all-to-all(v) of the four fragment streams: returns (received streams in source order, received counts
+    [4, world]). nccl (RCCL) moves device tensors directly; gloo goes through host copies."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    backend = dist.get_backend(group)
+    dev = bufs["hdr"].device
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    send_c = torch.from_numpy(np.ascontiguousarray(counts.T.reshape(-1))).to(cdev)   # [dest, stream]
+    recv_c = torch.empty_like(send_c)
+    dist.all_to_all_single(recv_c, send_c, group=group)
+    rc = recv_c.cpu().numpy().reshape(world, 4).T                                    # [stream, source]
+    out = {}
+    for q, (name, mult, dt) in enumerate(STREAMS):
+        src = bufs[name] if backend == "nccl" else bufs[name].cpu()
+        recv = torch.empty(int(rc[q].sum()) * mult, dtype=src.dtype, device=src.device)
+        dist.all_to_all_single(recv, src, output_split_sizes=(rc[q] * mult).tolist(),
+                               input_split_sizes=(counts[q] * mult).tolist(), group=group)
+        out[name] = recv.to(dev)
+    return out, rc
+
+
+def shard_merge(ctx, recv: dict, rcounts: np.ndarray, world: int, rank: int, n_txn: int):
+    """acc_shard_merge on received device streams; returns the merge view (device result on ctx)."""
+    import ctypes as C
+    from . import _lib as L
+    cnt = [np.ascontiguousarray(rcounts[q], dtype=np.uint64) for q in range(4)]
+    fr = L.FragRecv(L.ACC_MEM_DEVICE, world, rank, n_txn, *(c.ctypes.data for c in cnt),
+                    *(recv[n].data_ptr() if recv[n].numel() else 0 for n, _, _ in STREAMS))
+    view = L.MergeView()
+    ctx.check(ctx._lib.acc_shard_merge(ctx.handle, C.byref(fr), C.byref(view)))
+    return view
+
+
+def merged_to_host(ctx, view) -> dict:
+    """Copy the last merge result on ctx (acc_merge_copy_out) to host arrays."""
+    from .deps import merge_copy_out
+    return merge_copy_out(ctx, view)
+
+
+def home_result_from_full(res, batch: Batch, rank: int, world: int) -> dict:
+    """The single-store KeyDeps of every home txn of `rank` in the acc_merge_view layout (for parity checks)."""
+    ts = home_txns(batch.n_txn, rank, world)
+    key_off, val_off, k2v_off = [0], [0], [0]
+    keys, vals, k2v = [], [], []
+    for t in ts.tolist():
+        k, d, a = res.txn(t)
+        kc = batch.key_code[int(batch.key_off[t]) + k.astype(np.int64)]
+        keys.append(kc); vals.append(d); k2v.append(a)
+        key_off.append(key_off[-1] + len(kc)); val_off.append(val_off[-1] + len(d)); k2v_off.append(k2v_off[-1] + len(a))
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+    return dict(key_off=np.array(key_off, np.uint64), key_code=cat(keys, np.uint64), val_off=np.array(val_off, np.uint64),
+                txn_rank=cat(vals, np.uint32), k2v_off=np.array(k2v_off, np.uint64), k2v=cat(k2v, np.int32))

@@ -7,6 +7,8 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
 void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
 void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
+void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out);
+void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
 }  // namespace acc
 
 extern "C" {
@@ -134,6 +136,26 @@ int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out)
             ACC_HIP(hipMemcpyAsync(out->rng_end, v.rng_end, (size_t)v.n_ranges * 8, k, ctx->stream));
         }
         ctx->sync();
+    });
+}
+
+int acc_shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::shard_pack(ctx, in, out);
+    });
+}
+
+int acc_shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::shard_merge(ctx, in, out_view);
+        ctx->merge_view = *out_view;
+        ctx->merge_valid = true;
     });
 }
 

@@ -21,6 +21,10 @@
  *                          -> RangeDeps.Builder                       primitives/RangeDeps.java:873-891
  *                          for every txn of a mixed key/range batch (PreAccept.calculatePartialDeps
  *                          messages/PreAccept.java:245-265; SearchableRangeList stabbing core/utils/SearchableRangeList.java:89-116).
+ *   acc_shard_pack /       per-node reduce of per-CommandStore PartialDeps across GPUs (PreAccept.reduce
+ *   acc_shard_merge        messages/PreAccept.java:141-156, CommandStores.mapReduce local/CommandStores.java:575-592):
+ *                          fragments to the txn's home GPU (all-to-all(v) by the host over RCCL), then KeyDeps.with
+ *                          folded in shard order = the batched KeyDeps.merge below.
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -245,6 +249,41 @@ typedef struct acc_merge_out {
 } acc_merge_out;
 
 int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out);
+
+/* ---- Key-range CommandStore shards across GPUs (PreAccept.reduce) ----
+ * acc_shard_pack: the last acc_keydeps_batch result of this shard (the same `in`) as fragments for the txns' home
+ * ranks (home(t) = t mod world). A fragment = header (t, nk, nv, no) + nk key codes + nv TxnIds (batch indices) +
+ * no Java keysToTxnIds ints; only txns with a non-empty shard KeyDeps send one (PartialDeps.with skips empties).
+ * Streams are destination-major: destination d owns elements [x_off[d], x_off[d+1]) of each stream. The caller
+ * supplies the four stream buffers (two-call sizing: with a capacity below the need, ACC_E_CAP after writing the
+ * four host offset arrays, whose last entries are the totals) and four HOST offset arrays of world+1 entries. */
+typedef struct acc_frag_streams {
+    uint32_t  world;
+    uint32_t  mem;                                   /* placement of hdr/keys/vals/k2v */
+    uint64_t  cap_frag, cap_keys, cap_vals, cap_k2v; /* capacities: fragments (hdr = 4 u32 each), elements */
+    uint32_t *hdr;
+    uint64_t *keys;
+    uint32_t *vals;
+    int32_t  *k2v;
+    uint64_t *frag_off, *key_off, *val_off, *k2v_off;   /* host [world+1], written */
+} acc_frag_streams;
+
+int acc_shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out);
+
+/* acc_shard_merge: what this rank received, the four streams concatenated in source-rank (= shard) order, with the
+ * per-source element counts (host arrays of `world` entries). Result: the merged KeyDeps of every home txn
+ * t = rank + g * world (group g), in the acc_merge_view layout (txn ranks = batch indices). */
+typedef struct acc_frag_recv {
+    uint32_t mem;              /* placement of hdr/keys/vals/k2v */
+    uint32_t world, rank, n_txn;
+    const uint64_t *n_frag, *n_keys, *n_vals, *n_k2v;   /* host [world] */
+    const uint32_t *hdr;
+    const uint64_t *keys;
+    const uint32_t *vals;
+    const int32_t  *k2v;
+} acc_frag_recv;
+
+int acc_shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *out_view);
 
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
