@@ -12,8 +12,12 @@
 --config 4 (configs[3]): RangeDeps of 10M range txns (1 EndInclusive range each, log-uniform widths <= 2^16)
 interleaved with 10M key txns x 4 keys over the int32 key space; a step = one acc_rangedeps_batch.
 
-Multi-GPU: each rank is one CommandStore shard holding its own snapshot (independent seed), no data-path
-collective: weak scaling. Prints ONE JSON line on rank 0.
+Multi-GPU (--config 2, N > 1): one global batch of N x 1M txns x 8 keys, zipf(0.99) over N x 1M keys (seeded
+permutation), key range-sharded over the N GPUs the way CommandStores shard a node (EvenSplit); each rank is one
+CommandStore holding the txns that touch its keys. A step = the store's acc_keydeps_batch + acc_shard_pack + the
+all-to-all(v) of per-txn fragments to the txn's home GPU (RCCL over xGMI) + acc_shard_merge (PartialDeps.with fold =
+batched KeyDeps.merge): PreAccept.reduce on device. Weak scaling (~8M pairs per GPU); value = global pairs / the
+slowest rank's time. --config 4 at N > 1 runs independent snapshots per rank. Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -131,9 +135,12 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal hook (tests only): every rank on GPU 0 with gloo, to exercise the N > 1 path on a one-GPU box
+    if os.environ.get("ACC_BENCH_REHEARSE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if os.environ.get("ACC_BENCH_REHEARSE") == "1" else "nccl")
     return world, rank, local, torch.device("cuda", local)
 
 
@@ -154,7 +161,7 @@ def timed_steps(args, world, dev, step):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     return elapsed
@@ -208,6 +215,67 @@ def run_config2(args, world, rank, local, dev):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = keydeps_cpu_baseline(batch)
+    return ctx, timing, elapsed, result
+
+
+def run_config2_sharded(args, world, rank, local, dev):
+    import torch
+    from accord_amd import sharded as S
+    from accord_amd import workload as W
+    from accord_amd.deps import Context
+
+    n_global = int(1_000_000 * args.scale) * world
+    batch = W.keydeps_batch(n_global, 8, max(1000, n_global), W.CONFIG_SEEDS["2"], "zipf", 0.99, status_model="model")
+    bounds = S.even_split(batch.key_code, world)
+    sub, g = S.store_batch(batch, bounds, rank)
+    bi, keep = S.batch_in_device(sub, dev)
+    gidx = torch.from_numpy(g.astype(np.int32)).to(dev)
+    del batch
+    ctx = Context(local, timing=True)
+    info = {}
+
+    def fn():
+        v = ctx.keydeps_batch_raw(bi)
+        bufs, counts = S.shard_pack(ctx, bi, world, dev, gidx)
+        torch.cuda.synchronize(dev)
+        recv, rc = S.exchange_streams(bufs, counts)
+        mv = S.shard_merge(ctx, recv, rc, world, rank, n_global)
+        info["kd"], info["counts"], info["merge"] = v, counts, mv
+        return v
+
+    step = Step(ctx, fn)
+    elapsed = timed_steps(args, world, dev, step)
+    view = info["kd"]
+    timing = ctx.timing()
+    b_in, b_out = keydeps_bytes(sub.n_txn, sub.n_pairs, view.total_keys, view.total_edges, view.total_deps)
+    sent = info["counts"]
+    sent_bytes = int(16 * sent[0].sum() + 8 * sent[1].sum() + 4 * sent[2].sum() + 4 * sent[3].sum())
+    import torch.distributed as dist
+    loc = torch.tensor([sub.n_pairs, sent_bytes], dtype=torch.float64,
+                       device=dev if dist.get_backend() == "nccl" else "cpu")
+    tot = loc.clone()
+    dist.all_reduce(tot)
+    mx = loc.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    result = {
+        "metric": "txn-key conflict pairs resolved/sec (node)",
+        "value": round(n_global * 8 * args.steps / elapsed, 1),
+        "unit": "txn-key pairs/s",
+        "dtype": "u32/u64 (integer)",
+        "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) status model)",
+        "config": {
+            "workload": f"config2 x{world} range-sharded (config-3 shape): KeyDeps of {n_global} txns x 8 keys, "
+                        f"zipf(0.99) over {n_global} keys, key ranges EvenSplit over {world} GPUs (one CommandStore each), "
+                        "PreAccept.reduce of per-store PartialDeps by RCCL all-to-all(v) + on-device KeyDeps.merge",
+            "n_txn_global": n_global,
+            "pairs_global": n_global * 8,
+            "pairs_per_gpu_max": int(mx[0].item()),
+            "parallelism": f"key-range shards x{world} (CommandStores) + all-to-all(v) reduce",
+        },
+        "exchange": {"bytes_sent_total": int(tot[1].item()), "bytes_sent_max_rank": int(mx[1].item()),
+                     "backend": dist.get_backend() + (" (RCCL over xGMI)" if dist.get_backend() == "nccl" else "")},
+        "roofline": roofline(b_in + b_out, timing, args.steps),
+    }
     return ctx, timing, elapsed, result
 
 
@@ -268,7 +336,7 @@ def main():
     args = ap.parse_args()
 
     world, rank, local, dev = dist_setup(args)
-    run = {"2": run_config2, "4": run_config4}[args.config]
+    run = {"2": run_config2 if world == 1 else run_config2_sharded, "4": run_config4}[args.config]
     ctx, timing, elapsed, result = run(args, world, rank, local, dev)
     out = {
         "metric": result.pop("metric"),

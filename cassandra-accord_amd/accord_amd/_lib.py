@@ -114,7 +114,8 @@ class FragStreams(C.Structure):
     _fields_ = [("world", C.c_uint32), ("mem", C.c_uint32),
                 ("cap_frag", C.c_uint64), ("cap_keys", C.c_uint64), ("cap_vals", C.c_uint64), ("cap_k2v", C.c_uint64),
                 ("hdr", C.c_void_p), ("keys", C.c_void_p), ("vals", C.c_void_p), ("k2v", C.c_void_p),
-                ("frag_off", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("k2v_off", C.c_void_p)]
+                ("frag_off", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("k2v_off", C.c_void_p),
+                ("txn_global", C.c_void_p)]
 
 
 class FragRecv(C.Structure):

@@ -136,9 +136,24 @@ def batch_in_device(batch: Batch, dev):
     return bi, t
 
 
-def shard_pack(ctx, bi, world: int, dev):
+def store_batch(batch: Batch, bounds: np.ndarray, rank: int):
+    """The CommandStore's own batch: only the txns with at least one key in [bounds[rank], bounds[rank+1]), keys
+    restricted to the shard, in TxnId order; plus each kept txn's global index (u32)."""
+    local = shard_batch(batch, bounds, rank)
+    cnt = np.diff(local.key_off.astype(np.int64))
+    keep = np.nonzero(cnt > 0)[0]
+    off = np.zeros(len(keep) + 1, dtype=np.uint32)
+    np.cumsum(cnt[keep], out=off[1:])
+    sub = Batch(batch.txn_msb[keep], batch.txn_lsb[keep], batch.txn_node[keep], batch.exe_msb[keep],
+                batch.exe_lsb[keep], batch.exe_node[keep], batch.status[keep], off, local.key_code,
+                dict(batch.meta, shard=rank, store_local=True))
+    return sub, keep.astype(np.uint32)
+
+
+def shard_pack(ctx, bi, world: int, dev, txn_global=None):
     """Fragments of the last acc_keydeps_batch on ctx for every home rank: (streams dict of torch tensors on dev,
-    per-destination element counts [4, world] int64 numpy)."""
+    per-destination element counts [4, world] int64 numpy). txn_global: optional device u32/int32 tensor mapping
+    the batch's txns to global indices (store-local batches)."""
     import ctypes as C
     import torch
     from . import _lib as L
@@ -146,6 +161,7 @@ def shard_pack(ctx, bi, world: int, dev):
     fs = L.FragStreams()
     fs.world, fs.mem = world, L.ACC_MEM_DEVICE
     fs.frag_off, fs.key_off, fs.val_off, fs.k2v_off = (o.ctypes.data for o in offs)
+    fs.txn_global = txn_global.data_ptr() if txn_global is not None else None
     rc = ctx._lib.acc_shard_pack(ctx.handle, C.byref(bi), C.byref(fs))
     if rc != L.ACC_E_CAP:
         ctx.check(rc)

@@ -99,6 +99,45 @@ __device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
     return op(wave_prefix, excl);
 }
 
+// ---------------------------------------------------------------- sorting networks
+
+// ascending bitonic sort of one value per lane across the 64 lanes of a wave
+template <class T>
+__device__ __forceinline__ T bitonic_reg(T x)
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const T y = shfl_xor(x, (int)jj);
+            const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
+            const T mn = x < y ? x : y, mx = x < y ? y : x;
+            x = (lower == up) ? mn : mx;
+        }
+    }
+    return x;
+}
+
+// ascending bitonic sort of n2 (power of two) values in LDS or global memory by a whole workgroup of BLOCK threads
+template <class T>
+__device__ void block_bitonic(T *a, uint32_t n2)
+{
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
+                const uint32_t l = i ^ jj;
+                if (l > i) {
+                    const T x = a[i], y = a[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) { a[i] = y; a[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // ---------------------------------------------------------------- device-wide scan
 //
 // Single-pass scan with decoupled look-back: tiles take tickets in launch order, publish their aggregate,

@@ -384,22 +384,6 @@ __device__ __forceinline__ void txn_range(const Out &o, uint32_t t, uint64_t &e0
     e1 = o.q_off[o.P + r1];
 }
 
-__device__ __forceinline__ uint64_t bitonic_reg(uint64_t x)
-{
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint64_t y = shfl_xor(x, (int)jj);
-            const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
-            const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
-            x = (lower == up) ? mn : mx;
-        }
-    }
-    return x;
-}
-
 // Wave tier: one wave per txn with <= 64 raw entries; also routes the larger txns (sizes pass).
 template <bool WRITE>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_wave(uint32_t n, Out o)
@@ -473,23 +457,6 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_wave(uint32_t n, Out o)
 __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *lds, uint32_t &total)
 {
     return block_exclusive(v, OpAdd<uint32_t>(), lds, total);
-}
-
-__device__ void block_bitonic(uint64_t *a, uint32_t n2)
-{
-    for (uint32_t k = 2; k <= n2; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
-                const uint32_t l = i ^ jj;
-                if (l > i) {
-                    const uint64_t x = a[i], y = a[l];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) { a[i] = y; a[l] = x; }
-                }
-            }
-            __syncthreads();
-        }
-    }
 }
 
 // One workgroup per txn over buffers A, B of n2 >= m elements (LDS for the block tier, global scratch beyond).

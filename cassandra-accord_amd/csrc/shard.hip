@@ -20,24 +20,21 @@ namespace sh {
 // dest-major position of txn t: dest d = t mod world, slot t / world within the dest's G = ceil(n / world) slots
 __device__ __forceinline__ uint32_t dm_index(uint32_t t, uint32_t world, uint32_t G) { return (t % world) * G + t / world; }
 
-__global__ __launch_bounds__(BLOCK) void k_sh_sizes(uint32_t n, uint32_t world, uint32_t G, const uint64_t *__restrict__ kd_off,
-                                                    const uint64_t *__restrict__ u_off, const uint64_t *__restrict__ arena_off,
-                                                    uint64_t *__restrict__ c_frag, uint64_t *__restrict__ c_key,
-                                                    uint64_t *__restrict__ c_val, uint64_t *__restrict__ c_k2v)
+// counts at the dest-major slot of every batch txn (slots of global txns not in this batch stay zero)
+__global__ __launch_bounds__(BLOCK) void k_sh_sizes(uint32_t n, uint32_t world, uint32_t G, const uint32_t *__restrict__ gidx,
+                                                    const uint64_t *__restrict__ kd_off, const uint64_t *__restrict__ u_off,
+                                                    const uint64_t *__restrict__ arena_off, uint64_t *__restrict__ c_frag,
+                                                    uint64_t *__restrict__ c_key, uint64_t *__restrict__ c_val,
+                                                    uint64_t *__restrict__ c_k2v)
 {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;   // dest-major index
-    if (i >= world * G) return;
-    const uint32_t d = i / G, s = i % G;
-    const uint64_t t = (uint64_t)s * world + d;
-    uint64_t nk = 0, nv = 0, no = 0;
-    if (t < n) {
-        nk = kd_off[t + 1] - kd_off[t];         // KeyDeps.isEmpty <=> no keys (keys without deps are dropped)
-        if (nk) { nv = u_off[t + 1] - u_off[t]; no = arena_off[t + 1] - arena_off[t]; }
-    }
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t i = dm_index(gidx ? gidx[t] : t, world, G);
+    const uint64_t nk = kd_off[t + 1] - kd_off[t];   // KeyDeps.isEmpty <=> no keys (keys without deps are dropped)
     c_frag[i] = nk ? 1 : 0;
     c_key[i] = nk;
-    c_val[i] = nv;
-    c_k2v[i] = no;
+    c_val[i] = nk ? u_off[t + 1] - u_off[t] : 0;
+    c_k2v[i] = nk ? arena_off[t + 1] - arena_off[t] : 0;
 }
 
 // one wave per txn with a fragment: header + key codes + TxnIds + keysToTxnIds at the stream offsets
@@ -45,7 +42,8 @@ __global__ __launch_bounds__(BLOCK) void k_sh_pack(uint32_t n, uint32_t world, u
                                                    const uint64_t *__restrict__ key_code, const uint64_t *__restrict__ kd_off,
                                                    const uint32_t *__restrict__ key_idx, const uint64_t *__restrict__ u_off,
                                                    const uint32_t *__restrict__ dep_txn, const uint64_t *__restrict__ arena_off,
-                                                   const int32_t *__restrict__ arena, const uint64_t *__restrict__ o_frag,
+                                                   const int32_t *__restrict__ arena, const uint32_t *__restrict__ gidx,
+                                                   const uint64_t *__restrict__ o_frag,
                                                    const uint64_t *__restrict__ o_key, const uint64_t *__restrict__ o_val,
                                                    const uint64_t *__restrict__ o_k2v, uint32_t *__restrict__ hdr,
                                                    uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
@@ -55,13 +53,15 @@ __global__ __launch_bounds__(BLOCK) void k_sh_pack(uint32_t n, uint32_t world, u
     if (t >= n) return;
     const uint64_t k0 = kd_off[t], nk = kd_off[t + 1] - k0;
     if (nk == 0) return;
-    const uint32_t i = dm_index(t, world, G);
+    const uint32_t tg = gidx ? gidx[t] : t;
+    const uint32_t i = dm_index(tg, world, G);
     const uint64_t v0 = u_off[t], nv = u_off[t + 1] - v0, a0 = arena_off[t], no = arena_off[t + 1] - a0;
     const uint64_t f = o_frag[i], ok = o_key[i], ov = o_val[i], oo = o_k2v[i];
-    if (lane < 4) hdr[4 * f + lane] = lane == 0 ? t : lane == 1 ? (uint32_t)nk : lane == 2 ? (uint32_t)nv : (uint32_t)no;
+    if (lane < 4) hdr[4 * f + lane] = lane == 0 ? tg : lane == 1 ? (uint32_t)nk : lane == 2 ? (uint32_t)nv : (uint32_t)no;
     const uint32_t kb = key_off[t];
     for (uint64_t j = lane; j < nk; j += 64) keys[ok + j] = key_code[kb + key_idx[k0 + j]];
-    for (uint64_t j = lane; j < nv; j += 64) vals[ov + j] = dep_txn[v0 + j];
+    // the global map is increasing (a store's txns are a TxnId-ordered subsequence), so lists stay sorted
+    for (uint64_t j = lane; j < nv; j += 64) vals[ov + j] = gidx ? gidx[dep_txn[v0 + j]] : dep_txn[v0 + j];
     for (uint64_t j = lane; j < no; j += 64) k2v[oo + j] = arena[a0 + j];
 }
 
@@ -120,6 +120,177 @@ __global__ __launch_bounds__(BLOCK) void k_sh_gather(uint64_t F, const uint32_t 
     for (uint64_t j = lane; j < no; j += 64) m_k2v[ro[r] + j] = k2v[so[f] + j];
 }
 
+// ---------------------------------------------------------------- fused reduce (disjoint, shard-ordered keys)
+//
+// Replies of one home txn come from different shards in shard order, and shards own ascending disjoint key ranges,
+// so PartialDeps.with over them (linearUnion of KeyDeps) is: keys = concatenation, txnIds = sorted union of the
+// replies' txnIds, each keysToTxnIds entry re-indexed into that union, header = running entry counts. The order
+// assumption is checked (err) and the general batched merge runs instead when it does not hold.
+
+constexpr uint32_t FUSE_WAVE = 64;     // raw TxnIds per txn for the wave tier
+constexpr uint32_t FUSE_BLOCK = 8192;  // workgroup tier (LDS)
+
+struct Fuse {
+    uint32_t ng;
+    const uint64_t *grp_off, *rk, *rv, *ro;        // replies (gathered layout)
+    const uint64_t *keys;
+    const uint32_t *vals;
+    const int32_t *k2v;
+    uint64_t *c_nk, *c_nu, *c_no;                  // sizes per group
+    const uint64_t *key_out, *val_out, *k2v_out;   // offsets (write pass)
+    uint64_t *m_keys;
+    uint32_t *m_vals;
+    int32_t *m_k2v;
+    uint32_t *blk_list, *glb_list;
+    uint64_t *gstat;                               // [0] block groups, [1] global groups, [2] scratch u32, [3] order err
+    const uint64_t *glb_off;
+    uint32_t *scratch;
+};
+
+__device__ __forceinline__ uint32_t lb_u32(const uint32_t *a, uint32_t n, uint32_t v)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// copy keys + re-index keysToTxnIds of group g given its union u[0..U) (LDS or global); `tid`/`nth` = this thread's
+// index among the cooperating threads (a wave or a workgroup)
+__device__ __forceinline__ void fuse_emit(const Fuse &f, uint32_t g, const uint32_t *u, uint32_t U, uint32_t tid, uint32_t nth)
+{
+    const uint64_t r0 = f.grp_off[g], r1 = f.grp_off[g + 1];
+    const uint64_t kb0 = f.rk[r0], NK = f.rk[r1] - kb0, ob0 = f.ro[r0];
+    const uint64_t ko = f.key_out[g], oo = f.k2v_out[g];
+    for (uint64_t j = tid; j < NK; j += nth) f.m_keys[ko + j] = f.keys[kb0 + j];
+    for (uint64_t r = r0; r < r1; ++r) {
+        const uint64_t nk = f.rk[r + 1] - f.rk[r], no = f.ro[r + 1] - f.ro[r];
+        const uint64_t kb = f.rk[r] - kb0, eb = (f.ro[r] - ob0) - kb;   // keys / entries of earlier replies
+        const int32_t *src = f.k2v + f.ro[r];
+        const uint32_t *vals = f.vals + f.rv[r];
+        for (uint64_t j = tid; j < nk; j += nth) f.m_k2v[oo + kb + j] = (int32_t)(NK + eb + ((uint64_t)src[j] - nk));
+        for (uint64_t i = tid; i < no - nk; i += nth)
+            f.m_k2v[oo + NK + eb + i] = (int32_t)lb_u32(u, U, vals[src[nk + i]]);
+    }
+}
+
+// key order check of group g (disjoint ascending across its replies) by the cooperating threads
+__device__ __forceinline__ bool fuse_keys_ordered(const Fuse &f, uint32_t g, uint32_t tid, uint32_t nth)
+{
+    const uint64_t r0 = f.grp_off[g], r1 = f.grp_off[g + 1];
+    bool ok = true;
+    for (uint64_t r = r0 + 1 + tid; r < r1; r += nth)
+        if (f.rk[r] > f.rk[r - 1] && f.rk[r + 1] > f.rk[r] && f.keys[f.rk[r] - 1] >= f.keys[f.rk[r]]) ok = false;
+    return ok;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(BLOCK) void k_fuse_wave(Fuse f)
+{
+    __shared__ uint32_t su[WAVES][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t g = blockIdx.x * WAVES + wave;
+    if (g >= f.ng) return;
+    const uint64_t r0 = f.grp_off[g], r1 = f.grp_off[g + 1];
+    const uint64_t nraw = f.rv[r1] - f.rv[r0];
+    if (!WRITE) {
+        const bool ok = __all(fuse_keys_ordered(f, g, lane, 64));
+        if (!ok && lane == 0) atomicOr((unsigned long long *)&f.gstat[3], 1ull);
+    }
+    if (nraw > FUSE_WAVE) {
+        if (!WRITE && lane == 0) {
+            if (nraw <= FUSE_BLOCK) f.blk_list[atomicAdd((unsigned long long *)&f.gstat[0], 1ull)] = g;
+            else {
+                f.glb_list[atomicAdd((unsigned long long *)&f.gstat[1], 1ull)] = g;
+                uint64_t n2 = 64; while (n2 < nraw) n2 <<= 1;
+                atomicAdd((unsigned long long *)&f.gstat[2], 2 * n2);
+            }
+        }
+        return;
+    }
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t x = lane < nraw ? f.vals[f.rv[r0] + lane] : 0xFFFFFFFFu;
+    x = bitonic_reg(x);
+    const uint32_t prev = shfl_up(x, 1);
+    const bool nw = lane < nraw && (lane == 0 || x != prev);
+    const uint64_t nb = __ballot(nw);
+    const uint32_t U = (uint32_t)__popcll(nb);
+    if (!WRITE) {
+        if (lane == 0) {
+            f.c_nk[g] = f.rk[r1] - f.rk[r0];
+            f.c_nu[g] = U;
+            f.c_no[g] = f.ro[r1] - f.ro[r0];
+        }
+        return;
+    }
+    const uint32_t pos = (uint32_t)__popcll(nb & lt);
+    if (nw) { su[wave][pos] = x; f.m_vals[f.val_out[g] + pos] = x; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    fuse_emit(f, g, su[wave], U, lane, 64);
+}
+
+// one workgroup per group: sort the raw TxnIds (A), compact the union (B), re-index
+template <bool WRITE>
+__device__ void fuse_block(const Fuse &f, uint32_t g, uint32_t *A, uint32_t *B, uint32_t *red)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t r0 = f.grp_off[g], r1 = f.grp_off[g + 1];
+    const uint32_t nraw = (uint32_t)(f.rv[r1] - f.rv[r0]);
+    uint32_t n2 = 64;
+    while (n2 < nraw) n2 <<= 1;
+    for (uint32_t i = tid; i < n2; i += BLOCK) A[i] = i < nraw ? f.vals[f.rv[r0] + i] : 0xFFFFFFFFu;
+    __syncthreads();
+    block_bitonic(A, n2);
+    const uint32_t per = (n2 + BLOCK - 1) / BLOCK;
+    const uint32_t lo = tid * per, hi = min(lo + per, n2);
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i) c += (i < nraw && (i == 0 || A[i] != A[i - 1])) ? 1u : 0u;
+    uint32_t U;
+    uint32_t p = block_exclusive(c, OpAdd<uint32_t>(), red, U);
+    if (!WRITE) {
+        if (tid == 0) { f.c_nk[g] = f.rk[r1] - f.rk[r0]; f.c_nu[g] = U; f.c_no[g] = f.ro[r1] - f.ro[r0]; }
+        return;
+    }
+    for (uint32_t i = lo; i < hi; ++i)
+        if (i < nraw && (i == 0 || A[i] != A[i - 1])) { B[p] = A[i]; f.m_vals[f.val_out[g] + p] = A[i]; ++p; }
+    __syncthreads();
+    fuse_emit(f, g, B, U, tid, BLOCK);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(BLOCK) void k_fuse_block(Fuse f)
+{
+    __shared__ uint32_t A[FUSE_BLOCK], B[FUSE_BLOCK];
+    __shared__ uint32_t red[WAVES];
+    fuse_block<WRITE>(f, f.blk_list[blockIdx.x], A, B, red);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(BLOCK) void k_fuse_global(Fuse f)
+{
+    __shared__ uint32_t red[WAVES];
+    const uint32_t g = f.glb_list[blockIdx.x];
+    const uint64_t nraw = f.rv[f.grp_off[g + 1]] - f.rv[f.grp_off[g]];
+    uint64_t n2 = 64;
+    while (n2 < nraw) n2 <<= 1;
+    uint32_t *A = f.scratch + f.glb_off[blockIdx.x];
+    fuse_block<WRITE>(f, g, A, A + n2, red);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fuse_glb_sizes(uint32_t ng, Fuse f, uint64_t *__restrict__ sz)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= ng) return;
+    const uint32_t g = f.glb_list[i];
+    const uint64_t nraw = f.rv[f.grp_off[g + 1]] - f.rv[f.grp_off[g]];
+    uint64_t n2 = 64;
+    while (n2 < nraw) n2 <<= 1;
+    sz[i] = 2 * n2;
+}
+
 }  // namespace sh
 
 using namespace sh;
@@ -138,14 +309,27 @@ void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
     const size_t P = (size_t)in->n_pairs;
     const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
     const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
-    const uint32_t G = (n + world - 1) / world;
+    const uint32_t *gidx = out->txn_global ? stage_in(ctx, "sh_gidx", out->txn_global, n, in->mem) : nullptr;
+    uint32_t n_global = n;
+    if (gidx && n) {
+        uint32_t last = 0;
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gidx + (n - 1), 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        memcpy(&last, ctx->pinned, 4);
+        n_global = last + 1;
+    }
+    const uint32_t G = (n_global + world - 1) / world;
     const size_t M = (size_t)world * G;
     uint64_t *c[4], *o[4];
     const char *cn[4] = { "sh_c_frag", "sh_c_key", "sh_c_val", "sh_c_k2v" };
     const char *on[4] = { "sh_o_frag", "sh_o_key", "sh_o_val", "sh_o_k2v" };
-    for (int q = 0; q < 4; ++q) { c[q] = ctx->get<uint64_t>(cn[q], M); o[q] = ctx->get<uint64_t>(on[q], M + 1); }
-    launch(ctx, "sh_sizes", k_sh_sizes, dim3(grid_for(M, BLOCK)), dim3(BLOCK), 0, n, world, G, v.kd_off, v.u_off, v.arena_off,
-           c[0], c[1], c[2], c[3]);
+    for (int q = 0; q < 4; ++q) {
+        c[q] = ctx->get<uint64_t>(cn[q], M);
+        o[q] = ctx->get<uint64_t>(on[q], M + 1);
+        ACC_HIP(hipMemsetAsync(c[q], 0, M * sizeof(uint64_t), st));
+    }
+    launch(ctx, "sh_sizes", k_sh_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, world, G, gidx, v.kd_off, v.u_off,
+           v.arena_off, c[0], c[1], c[2], c[3]);
     for (int q = 0; q < 4; ++q) scan<uint64_t, OpAdd<uint64_t>>(ctx, c[q], o[q], M, true, o[q] + M);
     // per-destination boundaries (slot d * G of each stream's offsets) -> host
     uint64_t *bounds = ctx->get<uint64_t>("sh_bounds", 4 * ((size_t)world + 1));
@@ -175,7 +359,7 @@ void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
         k2v = ctx->get<int32_t>("sh_k2v", NO);
     }
     launch(ctx, "sh_pack", k_sh_pack, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, world, G, key_off, key_code, v.kd_off,
-           v.key_idx, v.u_off, v.dep_txn, v.arena_off, v.arena, (const uint64_t *)o[0], (const uint64_t *)o[1],
+           v.key_idx, v.u_off, v.dep_txn, v.arena_off, v.arena, gidx, (const uint64_t *)o[0], (const uint64_t *)o[1],
            (const uint64_t *)o[2], (const uint64_t *)o[3], hdr, keys, vals, k2v);
     if (out->mem == ACC_MEM_HOST) {
         if (F) ACC_HIP(hipMemcpyAsync(out->hdr, hdr, 16 * F, hipMemcpyDeviceToHost, st));
@@ -233,11 +417,62 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     launch(ctx, "shr_gather", k_sh_gather, dim3((unsigned)((F + WAVES - 1) / WAVES)), dim3(BLOCK), 0, F, (const uint32_t *)fs.vals,
            (const uint64_t *)sk, (const uint64_t *)sv, (const uint64_t *)so, (const uint64_t *)rk, (const uint64_t *)rv,
            (const uint64_t *)ro, keys, vals, k2v, m_keys, m_vals, m_k2v);
+    // ---- fused reduce: sizes (and the key-order check), offsets, writes
+    Fuse fz{};
+    fz.ng = n_groups; fz.grp_off = grp_off; fz.rk = rk; fz.rv = rv; fz.ro = ro; fz.keys = m_keys; fz.vals = m_vals;
+    fz.k2v = m_k2v;
+    fz.c_nk = ctx->get<uint64_t>("shm_c_nk", n_groups);
+    fz.c_nu = ctx->get<uint64_t>("shm_c_nu", n_groups);
+    fz.c_no = ctx->get<uint64_t>("shm_c_no", n_groups);
+    fz.blk_list = ctx->get<uint32_t>("shm_blk", n_groups);
+    fz.glb_list = ctx->get<uint32_t>("shm_glb", n_groups);
+    fz.gstat = ctx->get<uint64_t>("shm_gstat", 4);
+    ACC_HIP(hipMemsetAsync(fz.gstat, 0, 4 * 8, st));
+    const unsigned gw = (n_groups + WAVES - 1) / WAVES;
+    launch(ctx, "shm_fuse_wave_sizes", k_fuse_wave<false>, dim3(gw), dim3(BLOCK), 0, fz);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, fz.gstat, 4 * 8, hipMemcpyDeviceToHost, st));
     ctx->sync();
     if (ctx->pinned[0]) fail(ACC_E_ARG, "received a fragment for a txn that is not homed on this rank");
-    acc_merge_in mi{ ACC_MEM_DEVICE, n_groups, F, grp_off, rk, m_keys, rv, m_vals, ro, m_k2v };
-    keydeps_merge(ctx, &mi, view);
+    const uint64_t nblk = ctx->pinned[1], nglb = ctx->pinned[2], glb_elems = ctx->pinned[3];
+    if (ctx->pinned[4]) {
+        // replies of a txn are not in ascending disjoint key order (not a key-range split): general merge
+        ctx->stat("shard.general_merge", 1);
+        acc_merge_in mi{ ACC_MEM_DEVICE, n_groups, F, grp_off, rk, m_keys, rv, m_vals, ro, m_k2v };
+        keydeps_merge(ctx, &mi, view);
+        return;
+    }
+    ctx->stat("shard.general_merge", 0);
+    if (nblk) launch(ctx, "shm_fuse_block_sizes", k_fuse_block<false>, dim3((unsigned)nblk), dim3(BLOCK), 0, fz);
+    if (nglb) {
+        uint64_t *gsz = ctx->get<uint64_t>("shm_glb_sz", nglb);
+        uint64_t *goff = ctx->get<uint64_t>("shm_glb_off", nglb + 1);
+        launch(ctx, "shm_glb_sizes", k_fuse_glb_sizes, dim3(grid_for(nglb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nglb, fz, gsz);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, gsz, goff, nglb, true, goff + nglb);
+        fz.glb_off = goff;
+        fz.scratch = ctx->get<uint32_t>("shm_scratch", glb_elems);
+        launch(ctx, "shm_fuse_global_sizes", k_fuse_global<false>, dim3((unsigned)nglb), dim3(BLOCK), 0, fz);
+    }
+    uint64_t *key_out = ctx->get<uint64_t>("shm_key_off", (size_t)n_groups + 1);
+    uint64_t *val_out = ctx->get<uint64_t>("shm_val_off", (size_t)n_groups + 1);
+    uint64_t *k2v_out = ctx->get<uint64_t>("shm_k2v_off", (size_t)n_groups + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, fz.c_nk, key_out, n_groups, true, key_out + n_groups);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, fz.c_nu, val_out, n_groups, true, val_out + n_groups);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, fz.c_no, k2v_out, n_groups, true, k2v_out + n_groups);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, val_out + n_groups, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t NU = ctx->pinned[0];
+    fz.key_out = key_out; fz.val_out = val_out; fz.k2v_out = k2v_out;
+    fz.m_keys = ctx->get<uint64_t>("shm_keys", NK);
+    fz.m_vals = ctx->get<uint32_t>("shm_vals", NU);
+    fz.m_k2v = ctx->get<int32_t>("shm_k2v", NO);
+    launch(ctx, "shm_fuse_wave", k_fuse_wave<true>, dim3(gw), dim3(BLOCK), 0, fz);
+    if (nblk) launch(ctx, "shm_fuse_block", k_fuse_block<true>, dim3((unsigned)nblk), dim3(BLOCK), 0, fz);
+    if (nglb) launch(ctx, "shm_fuse_global", k_fuse_global<true>, dim3((unsigned)nglb), dim3(BLOCK), 0, fz);
+    ctx->sync();
+    *view = acc_merge_view{ n_groups, NK, NU, NO, NO, key_out, fz.m_keys, val_out, fz.m_vals, k2v_out, fz.m_k2v };
+    ctx->merge_view = *view;
+    ctx->merge_valid = true;
 }
 
 }  // namespace acc

@@ -252,7 +252,7 @@ int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out);
 
 /* ---- Key-range CommandStore shards across GPUs (PreAccept.reduce) ----
  * acc_shard_pack: the last acc_keydeps_batch result of this shard (the same `in`) as fragments for the txns' home
- * ranks (home(t) = t mod world). A fragment = header (t, nk, nv, no) + nk key codes + nv TxnIds (batch indices) +
+ * ranks (home(t) = t mod world, t the global index). A fragment = header (t, nk, nv, no) + nk key codes + nv TxnIds (batch indices) +
  * no Java keysToTxnIds ints; only txns with a non-empty shard KeyDeps send one (PartialDeps.with skips empties).
  * Streams are destination-major: destination d owns elements [x_off[d], x_off[d+1]) of each stream. The caller
  * supplies the four stream buffers (two-call sizing: with a capacity below the need, ACC_E_CAP after writing the
@@ -266,6 +266,8 @@ typedef struct acc_frag_streams {
     uint32_t *vals;
     int32_t  *k2v;
     uint64_t *frag_off, *key_off, *val_off, *k2v_off;   /* host [world+1], written */
+    const uint32_t *txn_global; /* optional [N], placement of the batch: global index of each batch txn (a store's
+                                   batch holds only the txns touching its keys, in TxnId order); null = identity */
 } acc_frag_streams;
 
 int acc_shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out);

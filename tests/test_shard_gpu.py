@@ -21,8 +21,11 @@ def _check_home(merged, expect, label):
         np.testing.assert_array_equal(merged[f], expect[f], err_msg=f"{label} {f}")
 
 
+@pytest.mark.parametrize("store_local,reverse", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_shard_reduce_single_process(world):
+def test_shard_reduce_single_process(world, store_local, reverse):
+    """reverse: sources concatenated in descending shard order, so a txn's replies are not in ascending key order
+    and the fused reduce must hand over to the general KeyDeps.merge (same canonical result)."""
     import torch
     from accord_amd import sharded as S
     from accord_amd.deps import Context
@@ -33,25 +36,33 @@ def test_shard_reduce_single_process(world):
         bounds = S.even_split(b.key_code, world)
         sent, counts, keep = [], [], []
         for s in range(world):
-            local = S.shard_batch(b, bounds, s)
+            gidx = None
+            if store_local:   # the store's batch holds only the txns touching its keys
+                local, g = S.store_batch(b, bounds, s)
+                gidx = torch.from_numpy(g.astype(np.int32)).to(dev)
+                keep.append(gidx)
+            else:
+                local = S.shard_batch(b, bounds, s)
             bi, t = S.batch_in_device(local, dev)
             keep.append(t)
             ctx.keydeps_batch_raw(bi)
-            bufs, c = S.shard_pack(ctx, bi, world, dev)
+            bufs, c = S.shard_pack(ctx, bi, world, dev, gidx)
             sent.append(bufs)
             counts.append(c)
         for h in range(world):
             recv, rc = {}, np.zeros((4, world), np.int64)
+            order = list(range(world))[::-1] if reverse else list(range(world))
             for q, (name, mult, _) in enumerate(S.STREAMS):
                 parts = []
-                for s in range(world):
+                for i, s in enumerate(order):
                     off = np.concatenate([[0], np.cumsum(counts[s][q])]) * mult
                     parts.append(sent[s][name][int(off[h]):int(off[h + 1])])
-                    rc[q, s] = counts[s][q][h]
+                    rc[q, i] = counts[s][q][h]
                 recv[name] = torch.cat(parts)
             view = S.shard_merge(ctx, recv, rc, world, h, b.n_txn)
             merged = S.merged_to_host(ctx, view)
             _check_home(merged, S.home_result_from_full(full, b, h, world), f"world {world} home {h}")
+            assert ctx.stats()["shard.general_merge"] == (1 if reverse and world > 1 else 0)
 
 
 def _free_port():
