@@ -1,6 +1,6 @@
 """Summarise a profiles/collect.sh run into a committed per-round file.
 
-    python profiles/summarize.py gpurun_out/prof_r01 profiles/r01 --steps 7
+    python profiles/summarize.py gpurun_out/prof_r01_c2 profiles/r01_config2 --steps 7
 
 Writes <prefix>_kernel_stats.csv (the rocprofv3 --stats table, accord kernels first), and <prefix>_summary.json:
 per-kernel average duration, per-step device time and per-step HBM traffic from the FETCH_SIZE / WRITE_SIZE
@@ -17,8 +17,17 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.match(r"(?:acc::)?([A-Za-z0-9_]+)", name)
-    return m.group(1) if m else name
+    """'void acc::rd::k_rd_stab<false>(acc::rd::View, ...)' -> 'k_rd_stab<false>'; 'acc::k_v2_count(...)' ->
+    'k_v2_count'."""
+    n = name[5:] if name.startswith("void ") else name
+    n = n.split("(")[0]
+    n = re.sub(r"\b(?:acc|rd|sh)::", "", n)
+    n = re.sub(r"\s+", "", n)
+    return n
+
+
+def is_acc(name):
+    return "acc::" in name.split("(")[0]
 
 
 def load_counters(path, counter):
@@ -26,9 +35,9 @@ def load_counters(path, counter):
     calls = defaultdict(int)
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] != counter or not r["Kernel_Name"].startswith("acc::"):
+            if r["Counter_Name"] != counter or not is_acc(r["Kernel_Name"]):
                 continue
-            k = short(r["Kernel_Name"][5:])
+            k = short(r["Kernel_Name"])
             tot[k] += float(r["Counter_Value"]) * 1024.0
             calls[k] += 1
     return tot, calls
@@ -38,18 +47,18 @@ def main():
     src, prefix = sys.argv[1], sys.argv[2]
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 7
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-    acc = [r for r in rows if r["Name"].startswith("acc::")]
+    acc = [r for r in rows if is_acc(r["Name"])]
     with open(prefix + "_kernel_stats.csv", "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "calls", "total_ns", "avg_ns", "min_ns", "max_ns", "pct"])
-        for r in acc + [r for r in rows if not r["Name"].startswith("acc::")]:
-            w.writerow([short(r["Name"][5:] if r["Name"].startswith("acc::") else r["Name"]), r["Calls"],
+        for r in acc + [r for r in rows if not is_acc(r["Name"])]:
+            w.writerow([short(r["Name"]), r["Calls"],
                         r["TotalDurationNs"], r["AverageNs"], r["MinNs"], r["MaxNs"], r["Percentage"]])
-    fetch, _ = load_counters(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write, _ = load_counters(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    fetch, fcalls = load_counters(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, wcalls = load_counters(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
     for r in acc:
-        k = short(r["Name"][5:])
+        k = short(r["Name"])
         d = kernels.setdefault(k, dict(calls=0, total_ns=0.0))
         d["calls"] += int(r["Calls"])
         d["total_ns"] += float(r["TotalDurationNs"])
@@ -58,6 +67,8 @@ def main():
         d["ms_per_step"] = d["total_ns"] / steps / 1e6
         d["hbm_read_bytes_per_step"] = 2.0 * fetch.get(k, 0.0) / steps
         d["hbm_write_bytes_per_step"] = write.get(k, 0.0) / steps
+        d["hbm_read_bytes_per_launch"] = 2.0 * fetch.get(k, 0.0) / max(fcalls.get(k, 0), 1)
+        d["hbm_write_bytes_per_launch"] = write.get(k, 0.0) / max(wcalls.get(k, 0), 1)
     out = dict(
         source=src, steps_profiled=steps,
         kernel_ms_per_step=sum(d["ms_per_step"] for d in kernels.values()),
