@@ -76,6 +76,7 @@ struct acc_ctx {
     acc_keydeps_view kd_view{};
     acc_merge_view merge_view{};
     acc_rangedeps_view rd_view{};
+    uint64_t rd_ent_hint = 0;   // RangeDeps raw pairs of the last batch (output capacity of the stabbing pass)
     bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;

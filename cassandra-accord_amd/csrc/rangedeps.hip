@@ -31,7 +31,6 @@ namespace rd {
 
 constexpr int NCLS = 33;          // width classes 0..32 (4^32 = 2^64 covers every u64 width)
 constexpr int TILE = 1024;        // entries per LDS tile in the stabbing pass
-constexpr uint32_t WAVE_E = 64;   // wave tier: raw entries per txn
 constexpr uint32_t BLOCK_E = 8192;  // workgroup tier (LDS)
 
 enum : uint64_t {
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_prep(uint32_t n, const uint64_t *_
 __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, const uint32_t *__restrict__ eflag,
                                                       const uint32_t *__restrict__ eidx, const uint32_t *__restrict__ rowner,
                                                       const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
-                                                      const uint32_t *__restrict__ rank, const uint64_t *__restrict__ tl,
+                                                      const uint4 *__restrict__ tinfo, const uint64_t *__restrict__ tl,
                                                       Runs rs_plan, Runs re_plan, int e_bits, int split,
                                                       uint64_t *__restrict__ e_s, uint64_t *__restrict__ e_e,
                                                       uint32_t *__restrict__ e_rank, uint8_t *__restrict__ e_kind,
@@ -154,7 +153,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, co
     const uint64_t s = rs[j], e = re[j];
     e_s[i] = s;
     e_e[i] = e;
-    e_rank[i] = rank[t];
+    e_rank[i] = tinfo[t].y;   // TxnId position of the range command
     e_kind[i] = (uint8_t)((tl[t] >> 1) & 7u);
     const uint64_t sc = pext_runs(s, rs_plan), ec = pext_runs(e, re_plan);
     if (split) { dkey[i] = sc; ekey[i] = ec; }      // two-key LSD: end first, then start (stable)
@@ -224,32 +223,79 @@ __global__ __launch_bounds__(BLOCK) void k_rd_class_cols(uint32_t ne, const uint
     cs_kind[p] = e_kind[i];
 }
 
-// query low bounds (keys of key txns, starts of range txns' ranges), compacted, for the query sort
-__global__ __launch_bounds__(BLOCK) void k_rd_query_keys(uint32_t P, uint32_t R, const uint64_t *__restrict__ key_code,
-                                                         const uint64_t *__restrict__ rs, Runs plan,
-                                                         uint64_t *__restrict__ qkey)
+// ---------------------------------------------------------------- txn columns
+
+// isT[r] = 1 where r is the rank of a TxnId (the dictionary ranks every TxnId and executeAt of the batch)
+__global__ __launch_bounds__(BLOCK) void k_rd_txnflag(uint32_t n, const uint32_t *__restrict__ rank, uint32_t *__restrict__ isT)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) isT[rank[t]] = 1;
+}
+
+// Per txn {lim, tpos, witness mask, is range}: tpos = position of its TxnId among the batch's TxnIds (TxnId order),
+// lim = number of TxnIds below its executeAt, so C.txnId < T.executeAt <=> tpos(C) < lim(T) (STARTED_BEFORE,
+// InMemoryCommandStore.java:897-898). txn_of_tpos inverts tpos (identity for a batch given in TxnId order).
+__global__ __launch_bounds__(BLOCK) void k_rd_txncols(uint32_t n, const uint32_t *__restrict__ rank, const uint32_t *__restrict__ tcnt,
+                                                      const uint64_t *__restrict__ tl, uint4 *__restrict__ tinfo,
+                                                      uint32_t *__restrict__ txn_of_tpos)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t tpos = tcnt[rank[t]], lim = tcnt[rank[n + t]];
+    tinfo[t] = make_uint4(lim, tpos, witnesses((uint32_t)(tl[t] >> 1) & 7u), (uint32_t)(tl[t] & 1u));
+    txn_of_tpos[tpos] = t;
+}
+
+// ---------------------------------------------------------------- queries
+
+// query q: a key of a key txn (q < P) or a range of a range txn (q >= P); [lo, hi] its bounds
+struct QRec {
+    uint64_t lo, hi;
+    uint32_t lim, tpos;
+    uint32_t flags;   // witness mask | is-range << 8
+    uint32_t q;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const uint64_t *__restrict__ key_code,
+                                                   const uint32_t *__restrict__ owner, const uint64_t *__restrict__ rs,
+                                                   const uint64_t *__restrict__ re, const uint32_t *__restrict__ rowner,
+                                                   const uint4 *__restrict__ tinfo, Runs plan, QRec *__restrict__ rec,
+                                                   uint64_t *__restrict__ qkey)
 {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
     if (q >= P + R) return;
-    qkey[q] = pext_runs(q < P ? key_code[q] : rs[q - P], plan);
+    QRec r;
+    uint32_t t;
+    if (q < P) { r.lo = r.hi = key_code[q]; t = owner[q]; }
+    else { r.lo = rs[q - P]; r.hi = re[q - P]; t = rowner[q - P]; }
+    const uint4 ti = tinfo[t];
+    r.lim = ti.x; r.tpos = ti.y; r.flags = ti.z | (ti.w << 8); r.q = q;
+    rec[q] = r;
+    qkey[q] = pext_runs(r.lo, plan);
 }
 
-// ---------------------------------------------------------------- stabbing (count / emit)
+__global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Q, const uint32_t *__restrict__ perm, const QRec *__restrict__ rec,
+                                                    QRec *__restrict__ srec)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < Q) srec[i] = rec[perm[i]];
+}
+
+// ---------------------------------------------------------------- stabbing
 
 struct View {
-    uint32_t n, P, R, Q;
+    uint32_t Q;
     int end_inclusive;
-    const uint32_t *qperm;        // queries sorted by low bound
-    const uint64_t *key_code;
-    const uint32_t *owner;        // txn of key pair
-    const uint64_t *rs, *re;
-    const uint32_t *rowner;       // txn of range
-    const uint32_t *rank;         // [2n]
-    const uint64_t *tl;
+    const QRec *srec;             // queries sorted by low bound
     const uint64_t *cs_s, *cs_e;  // entries by (class, start)
-    const uint2 *cs_info;         // (range id, TxnId rank)
+    const uint2 *cs_info;         // (range id, TxnId position)
     const uint8_t *cs_kind;
     const uint32_t *class_off;    // [NCLS + 1]
+    uint64_t *cursor;             // global output cursor
+    uint64_t cap;                 // capacity of ent
+    uint64_t *ent;                // (range id << 32 | TxnId position) per emitted pair
+    uint64_t *q_off;              // per query (original index): first entry
+    uint32_t *q_cnt;              // per query: entries
 };
 
 __device__ __forceinline__ uint32_t lower_bound_s(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v)
@@ -269,45 +315,26 @@ __device__ __forceinline__ uint32_t upper_bound_s(const uint64_t *a, uint32_t lo
     return lo;
 }
 
-template <bool EMIT>
-__global__ __launch_bounds__(BLOCK) void k_rd_stab(View v, uint32_t *__restrict__ cnt, const uint64_t *__restrict__ q_off,
-                                                   uint64_t *__restrict__ ent)
-{
-    __shared__ uint64_t t_s[TILE], t_e[TILE];
-    __shared__ uint2 t_info[TILE];
-    __shared__ uint8_t t_kind[TILE];
-    __shared__ uint64_t s_hi[WAVES];
-    __shared__ uint64_t s_lo;
-    __shared__ uint32_t s_b0, s_b1;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t i = blockIdx.x * BLOCK + tid;
-    const bool valid = i < v.Q;
-    uint32_t q = 0, t = 0;
-    uint64_t lo = 0, hi = 0;
-    bool isr = false;
-    if (valid) {
-        q = v.qperm[i];
-        if (q < v.P) { lo = hi = v.key_code[q]; t = v.owner[q]; }
-        else { lo = v.rs[q - v.P]; hi = v.re[q - v.P]; t = v.rowner[q - v.P]; isr = true; }
-    }
-    const uint32_t exec_rank = valid ? v.rank[v.n + t] : 0u;
-    const uint32_t txn_rank = valid ? v.rank[t] : 0u;
-    const uint32_t wm = valid ? witnesses((uint32_t)(v.tl[t] >> 1) & 7u) : 0u;
-    // block window: queries are sorted by lo, so thread 0 holds the smallest; hi needs a max
-    uint64_t h = valid ? hi : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { uint64_t o = shfl_xor(h, d); h = o > h ? o : h; }
-    if (lane_id() == 0) s_hi[tid >> 6] = h;
-    if (tid == 0) s_lo = lo;
-    __syncthreads();
-    uint64_t hi_max = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) hi_max = s_hi[w] > hi_max ? s_hi[w] : hi_max;
-    const uint64_t lo_min = s_lo;
+struct StabTile {
+    uint64_t s[TILE], e[TILE];
+    uint2 info[TILE];
+    uint8_t kind[TILE];
+    uint64_t hi[WAVES];
+    uint64_t lo;
+    uint32_t b0, b1;
+    uint32_t red[WAVES];
+    uint64_t base;
+};
 
+// One pass over the block's windows: EMIT = false counts this query's pairs, EMIT = true writes them at out.
+template <bool EMIT>
+__device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t lo_min,
+                                              uint64_t hi_max, uint64_t out)
+{
+    const uint32_t tid = threadIdx.x;
+    const bool isr = (r.flags >> 8) & 1u;
+    const uint32_t wm = r.flags & 0xFFu;
     uint32_t count = 0;
-    uint64_t out = 0;
-    if (EMIT && valid) out = q_off[q];
     for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
         const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
         if (a0 == a1) continue;
@@ -315,167 +342,249 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v, uint32_t *__restrict_
         if (tid == 0) {
             const uint64_t wlo = lo_min > W ? lo_min - W : 0;
             const uint32_t b0 = lower_bound_s(v.cs_s, a0, a1, wlo);
-            s_b0 = b0;
-            s_b1 = upper_bound_s(v.cs_s, b0, a1, hi_max);
+            T.b0 = b0;
+            T.b1 = upper_bound_s(v.cs_s, b0, a1, hi_max);
         }
         __syncthreads();
-        const uint32_t b0 = s_b0, b1 = s_b1;
+        const uint32_t b0 = T.b0, b1 = T.b1;
         __syncthreads();
-        const uint64_t qwlo = lo > W ? lo - W : 0;
+        const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
         for (uint32_t base = b0; base < b1; base += TILE) {
             const uint32_t len = min((uint32_t)TILE, b1 - base);
             for (uint32_t k = tid; k < len; k += BLOCK) {
-                t_s[k] = v.cs_s[base + k];
-                t_e[k] = v.cs_e[base + k];
-                t_info[k] = v.cs_info[base + k];
-                t_kind[k] = v.cs_kind[base + k];
+                T.s[k] = v.cs_s[base + k];
+                T.e[k] = v.cs_e[base + k];
+                T.info[k] = v.cs_info[base + k];
+                T.kind[k] = v.cs_kind[base + k];
             }
             __syncthreads();
             if (valid) {
                 // this query's own window inside the tile: starts in [lo - W, hi]
-                uint32_t k = lower_bound_s(t_s, 0, len, qwlo);
-                for (; k < len; ++k) {
-                    const uint64_t s = t_s[k];
-                    if (s > hi) break;
-                    const uint64_t e = t_e[k];
+                for (uint32_t k = lower_bound_s(T.s, 0, len, qwlo); k < len; ++k) {
+                    const uint64_t s = T.s[k];
+                    if (s > r.hi) break;
+                    const uint64_t e = T.e[k];
                     bool hit;
-                    if (isr) hit = s < hi && e > lo;                              // Range.compareIntersecting == 0
-                    else if (v.end_inclusive) hit = s < lo && lo <= e;            // EndInclusive.contains (s, e]
-                    else hit = s <= lo && lo < e;                                 // StartInclusive.contains [s, e)
+                    if (isr) hit = s < r.hi && e > r.lo;                           // Range.compareIntersecting == 0
+                    else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;         // EndInclusive.contains (s, e]
+                    else hit = s <= r.lo && r.lo < e;                              // StartInclusive.contains [s, e)
                     if (!hit) continue;
-                    const uint2 info = t_info[k];
-                    if (info.y >= exec_rank || info.y == txn_rank) continue;     // STARTED_BEFORE; p1
-                    if (!((wm >> t_kind[k]) & 1u)) continue;                     // testKind
-                    if (EMIT) ent[out + count] = ((uint64_t)info.x << 32) | info.y;
+                    const uint2 info = T.info[k];
+                    if (info.y >= r.lim || info.y == r.tpos) continue;            // STARTED_BEFORE; p1
+                    if (!((wm >> T.kind[k]) & 1u)) continue;                      // testKind
+                    if (EMIT) v.ent[out + count] = ((uint64_t)info.x << 32) | info.y;
                     ++count;
                 }
             }
             __syncthreads();
         }
     }
-    if (!EMIT && valid) cnt[q] = count;
+    return count;
+}
+
+// A workgroup of 256 consecutive (sorted) queries: count every query's pairs over the block's windows, take one
+// slice of the output with one atomic, then emit (the windows' tiles are re-read, L2-warm). Each query's pairs
+// land contiguously at q_off[q].
+__global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
+{
+    __shared__ StabTile T;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t i = blockIdx.x * BLOCK + tid;
+    const bool valid = i < v.Q;
+    QRec r{};
+    if (valid) r = v.srec[i];
+    uint64_t h = valid ? r.hi : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = shfl_xor(h, d); h = o > h ? o : h; }
+    if (lane_id() == 0) T.hi[tid >> 6] = h;
+    if (tid == 0) T.lo = r.lo;   // sorted: thread 0 holds the block's smallest low bound
+    __syncthreads();
+    uint64_t hi_max = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) hi_max = T.hi[w] > hi_max ? T.hi[w] : hi_max;
+    const uint64_t lo_min = T.lo;
+    const uint32_t count = stab_pass<false>(v, T, valid, r, lo_min, hi_max, 0);
+    uint32_t total;
+    const uint32_t mine = block_exclusive(count, OpAdd<uint32_t>(), T.red, total);
+    if (tid == 0) T.base = atomicAdd((unsigned long long *)v.cursor, (unsigned long long)total);
+    __syncthreads();
+    const uint64_t base = T.base;
+    if (valid) { v.q_off[r.q] = base + mine; v.q_cnt[r.q] = count; }
+    if (base + total > v.cap) return;   // uniform: the host re-runs with a larger capacity
+    stab_pass<true>(v, T, valid, r, lo_min, hi_max, base + mine);
 }
 
 // ---------------------------------------------------------------- per-txn build
 
 struct Out {
+    uint32_t n, P;
     const uint32_t *key_off, *rng_off;
-    uint32_t P;
-    const uint64_t *q_off;        // [P + R + 1]
+    const uint64_t *q_off;
+    const uint32_t *q_cnt;
     const uint64_t *ent;
-    const uint32_t *txn_of_rank;
-    uint32_t *rd_cnt, *u_cnt;     // sizes pass
+    const uint32_t *txn_of_tpos;  // null: batch in TxnId order (tpos = batch index)
+    const uint64_t *raw_off;      // [n + 1] raw entries per txn (scratch placement)
+    uint32_t *s_arena, *s_rid, *s_dep;   // scratch at 2 raw_off / raw_off / raw_off
+    uint32_t *rd_cnt, *u_cnt;
     uint64_t *a_cnt;
-    const uint64_t *arena_off, *rd_off, *u_off;   // write pass
+    const uint32_t *list;         // txns of the tier (build kernels)
+    const uint64_t *glb_off;      // scratch offsets of the global tier (u64 elements)
+    uint64_t *gscratch;
+    // compaction
+    const uint64_t *arena_off, *rd_off, *u_off;
     int32_t *arena;
     uint32_t *range_id, *dep_txn;
-    uint32_t *blk_list, *glb_list;
-    const uint64_t *glb_off;      // scratch offsets of the global tier (u64 elements)
-    uint64_t *scratch;
-    uint64_t *gstat;              // [0] block-tier txns, [1] global-tier txns, [2] global scratch elements
 };
 
-__device__ __forceinline__ void txn_range(const Out &o, uint32_t t, uint64_t &e0, uint64_t &e1)
+__device__ __forceinline__ void txn_queries(const Out &o, uint32_t t, uint32_t &q0, uint32_t &q1)
 {
     const uint32_t k0 = o.key_off[t], k1 = o.key_off[t + 1];
-    if (k1 > k0) { e0 = o.q_off[k0]; e1 = o.q_off[k1]; return; }
-    const uint32_t r0 = o.rng_off[t], r1 = o.rng_off[t + 1];
-    e0 = o.q_off[o.P + r0];
-    e1 = o.q_off[o.P + r1];
+    if (k1 > k0) { q0 = k0; q1 = k1; return; }
+    q0 = o.P + o.rng_off[t];
+    q1 = o.P + o.rng_off[t + 1];
 }
 
-// Wave tier: one wave per txn with <= 64 raw entries; also routes the larger txns (sizes pass).
-template <bool WRITE>
-__global__ __launch_bounds__(BLOCK) void k_rd_build_wave(uint32_t n, Out o)
+__device__ __forceinline__ uint32_t dep_of(const Out &o, uint32_t tpos) { return o.txn_of_tpos ? o.txn_of_tpos[tpos] : tpos; }
+
+__global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t *__restrict__ m_raw, uint32_t *__restrict__ tier)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    uint32_t q0, q1;
+    txn_queries(o, t, q0, q1);
+    uint64_t m = 0;
+    for (uint32_t q = q0; q < q1; ++q) m += o.q_cnt[q];
+    m_raw[t] = m;
+    // tiers: 0 none, 1 <= 16 (16-lane groups), 2 <= 64 (wave), 3..9 LDS workgroups of 128..8192, 10 global
+    uint32_t tr;
+    if (m == 0) tr = 0;
+    else if (m <= 16) tr = 1;
+    else if (m <= 64) tr = 2;
+    else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
+    else tr = 10;
+    tier[t] = tr;
+    if (m == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rd_tier_hist(uint32_t n, const uint32_t *__restrict__ tier, uint32_t *__restrict__ hist)
+{
+    __shared__ uint32_t h[16];
+    if (threadIdx.x < 16) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) atomicAdd(&h[tier[t]], 1u);
+    __syncthreads();
+    if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// Groups of S lanes (S = 16 or 64), one txn each: load, sort (range id, TxnId position), dedupe, TxnId union and
+// index, range groups; results to the scratch regions of the txn.
+template <int S>
+__global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
 {
     __shared__ uint32_t slot[WAVES][64];
+    constexpr int G = 64 / S;
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t t = blockIdx.x * WAVES + wave;
-    if (t >= n) return;
-    uint64_t e0, e1;
-    txn_range(o, t, e0, e1);
-    const uint64_t m = e1 - e0;
-    if (m > WAVE_E) {
-        if (!WRITE && lane == 0) {
-            if (m <= BLOCK_E) o.blk_list[atomicAdd((unsigned long long *)&o.gstat[0], 1ull)] = t;
-            else {
-                o.glb_list[atomicAdd((unsigned long long *)&o.gstat[1], 1ull)] = t;
-                uint64_t n2 = 1; while (n2 < m) n2 <<= 1;
-                atomicAdd((unsigned long long *)&o.gstat[2], 2 * n2);
-            }
-        }
-        return;
-    }
-    if (m == 0) {
-        if (!WRITE && lane == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
-        return;
-    }
+    const uint32_t grp = lane / S, sub = lane & (S - 1);
+    const uint32_t li = (blockIdx.x * WAVES + wave) * G + grp;
+    const bool live = li < cnt;
+    const uint32_t t = live ? o.list[li] : 0;
+    const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint64_t x = lane < m ? o.ent[e0 + lane] : ~0ull;
-    x = bitonic_reg(x);
+    uint64_t m = 0, x = ~0ull;
+    if (live) {
+        uint32_t q0, q1;
+        txn_queries(o, t, q0, q1);
+        for (uint32_t q = q0; q < q1; ++q) {
+            const uint32_t c = o.q_cnt[q];
+            if (sub >= m && sub < m + c) x = o.ent[o.q_off[q] + (sub - m)];
+            m += c;
+        }
+    }
+    // sort within the group (groups are lane-aligned: the xor partners of k <= S stay inside)
+#pragma unroll
+    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint64_t y = shfl_xor(x, (int)jj);
+            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
+            const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+            x = (lower == up) ? mn : mx;
+        }
+    }
     const uint64_t prev = shfl_up(x, 1);
-    const bool valid = lane < m && (lane == 0 || x != prev);          // dedupe identical (range, txn)
-    const uint64_t vb = __ballot(valid);
+    const bool valid = live && sub < m && (sub == 0 || x != prev);       // dedupe identical (range, txn)
+    const uint64_t vb = __ballot(valid) & gmask;
     const uint32_t M = (uint32_t)__popcll(vb);
     const uint32_t pos = (uint32_t)__popcll(vb & lt);
-    const uint32_t rid = (uint32_t)(x >> 32), rk = (uint32_t)x;
-    // RangeDeps.txnIds: distinct ranks, ascending; each entry's index into them
-    uint64_t y = valid ? (((uint64_t)rk << 6) | pos) : ~0ull;
-    y = bitonic_reg(y);
-    const uint64_t yprev = shfl_up(y, 1);
-    const bool yin = lane < M;
-    const bool ynew = yin && (lane == 0 || (y >> 6) != (yprev >> 6));
-    const uint64_t nb = __ballot(ynew);
-    const uint32_t U = (uint32_t)__popcll(nb);
-    const uint32_t uidx = (uint32_t)__popcll(nb & lt) + (ynew ? 1u : 0u) - 1u;
-    // ranges: a new group where the range id changes
-    const bool rnew = valid && (lane == 0 || (uint32_t)(prev >> 32) != rid);
-    const uint64_t rb = __ballot(rnew);
-    const uint32_t Rd = (uint32_t)__popcll(rb);
-    if (!WRITE) {
-        if (lane == 0) { o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M; }
-        return;
-    }
-    if (yin) slot[wave][(uint32_t)(y & 63u)] = uidx;
-    if (ynew) o.dep_txn[o.u_off[t] + uidx] = o.txn_of_rank[(uint32_t)(y >> 6)];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const uint64_t abase = o.arena_off[t];
-    const uint32_t g = (uint32_t)__popcll(rb & lt) + (rnew ? 1u : 0u) - 1u;
-    // rangesToTxnIds header: group g - 1 ends where group g starts; the last group ends at Rd + M
-    if (valid) {
-        o.arena[abase + Rd + pos] = (int32_t)slot[wave][pos];
-        if (rnew) {
-            o.range_id[o.rd_off[t] + g] = rid;
-            if (g > 0) o.arena[abase + g - 1] = (int32_t)(Rd + pos);
+    const uint32_t rid = (uint32_t)(x >> 32), tp = (uint32_t)x;
+    uint64_t y = valid ? (((uint64_t)tp << 8) | pos) : ~0ull;
+#pragma unroll
+    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint64_t z = shfl_xor(y, (int)jj);
+            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
+            const uint64_t mn = y < z ? y : z, mx = y < z ? z : y;
+            y = (lower == up) ? mn : mx;
         }
     }
-    if (lane == 0) o.arena[abase + Rd - 1] = (int32_t)(Rd + M);
+    const uint64_t yprev = shfl_up(y, 1);
+    const bool ynew = live && sub < M && (sub == 0 || (y >> 8) != (yprev >> 8));
+    const uint64_t nb = __ballot(ynew) & gmask;
+    const uint32_t U = (uint32_t)__popcll(nb);
+    const bool yin = live && sub < M;
+    const uint32_t uidx = (uint32_t)__popcll(nb & lt) + (ynew ? 1u : 0u) - 1u;   // index of this entry's TxnId
+    const bool rnew = valid && (sub == 0 || (uint32_t)(prev >> 32) != rid);
+    const uint64_t rb = __ballot(rnew) & gmask;
+    const uint32_t Rd = (uint32_t)__popcll(rb);
+    const uint32_t g0 = grp * S;
+    if (yin) slot[wave][g0 + (uint32_t)(y & 0xFFu)] = uidx;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (!live || m == 0) return;
+    const uint64_t ra = o.raw_off[t];
+    uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
+    if (ynew) sd[uidx] = dep_of(o, (uint32_t)(y >> 8));
+    const uint32_t g = (uint32_t)__popcll(rb & lt);
+    if (valid) {
+        sa[Rd + pos] = slot[wave][g0 + pos];
+        if (rnew) {
+            sr[g] = rid;
+            if (g > 0) sa[g - 1] = Rd + pos;
+        }
+    }
+    if (sub == 0) {
+        sa[Rd - 1] = Rd + M;
+        o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M;
+    }
 }
 
-// block-wide exclusive scan of per-thread counts (256 threads)
-__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *lds, uint32_t &total)
-{
-    return block_exclusive(v, OpAdd<uint32_t>(), lds, total);
-}
-
-// One workgroup per txn over buffers A, B of n2 >= m elements (LDS for the block tier, global scratch beyond).
-template <bool WRITE>
-__device__ void build_block(const Out &o, uint32_t t, uint64_t e0, uint32_t m, uint64_t *A, uint64_t *B, uint32_t *red)
+// One workgroup per txn over buffers A, B of n2 >= m elements (LDS sized to the tier, or global scratch)
+__device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, uint32_t *red)
 {
     const uint32_t tid = threadIdx.x;
+    uint32_t q0, q1;
+    txn_queries(o, t, q0, q1);
+    uint32_t m = 0;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t c = o.q_cnt[q];
+        const uint64_t off = o.q_off[q];
+        for (uint32_t k = tid; k < c; k += BLOCK) A[m + k] = o.ent[off + k];
+        m += c;
+    }
     uint32_t n2 = 64;
     while (n2 < m) n2 <<= 1;
-    for (uint32_t i = tid; i < n2; i += BLOCK) A[i] = i < m ? o.ent[e0 + i] : ~0ull;
+    for (uint32_t i = m + tid; i < n2; i += BLOCK) A[i] = ~0ull;
     __syncthreads();
     block_bitonic(A, n2);
-    // dedupe + compact into B; each thread owns a contiguous slice of n2 / BLOCK (or 1) elements
+    // dedupe + compact into B; each thread owns a contiguous slice
     const uint32_t per = (n2 + BLOCK - 1) / BLOCK;
     const uint32_t lo = tid * per, hi = min(lo + per, n2);
     uint32_t c = 0;
     for (uint32_t i = lo; i < hi; ++i) c += (i < m && (i == 0 || A[i] != A[i - 1])) ? 1u : 0u;
     uint32_t M;
-    uint32_t p = block_excl(c, red, M);
+    uint32_t p = block_exclusive(c, OpAdd<uint32_t>(), red, M);
     for (uint32_t i = lo; i < hi; ++i)
         if (i < m && (i == 0 || A[i] != A[i - 1])) B[p++] = A[i];
     __syncthreads();
@@ -484,22 +593,21 @@ __device__ void build_block(const Out &o, uint32_t t, uint64_t e0, uint32_t m, u
     for (uint32_t i = tid; i < n2m; i += BLOCK) A[i] = i < M ? (((uint64_t)(uint32_t)B[i] << 32) | i) : ~0ull;
     __syncthreads();
     block_bitonic(A, n2m);
-    // distinct TxnId ranks -> index; B[e] becomes (range id << 32 | index)
+    // distinct TxnId positions -> index; B[e] becomes (range id << 32 | index)
+    const uint64_t ra = o.raw_off[t];
+    uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
     const uint32_t per2 = (n2m + BLOCK - 1) / BLOCK;
     const uint32_t lo2 = tid * per2, hi2 = min(lo2 + per2, n2m);
     c = 0;
     for (uint32_t i = lo2; i < hi2; ++i) c += (i < M && (i == 0 || (A[i] >> 32) != (A[i - 1] >> 32))) ? 1u : 0u;
     uint32_t U;
-    uint32_t u = block_excl(c, red, U);
-    if (WRITE) {
-        const uint64_t ub = o.u_off[t];
-        for (uint32_t i = lo2; i < hi2; ++i) {
-            if (i >= M) break;
-            const bool nw = i == 0 || (A[i] >> 32) != (A[i - 1] >> 32);
-            if (nw) { o.dep_txn[ub + u] = o.txn_of_rank[(uint32_t)(A[i] >> 32)]; ++u; }
-            const uint32_t e = (uint32_t)A[i];
-            B[e] = (B[e] & 0xFFFFFFFF00000000ull) | (u - 1);
-        }
+    uint32_t u = block_exclusive(c, OpAdd<uint32_t>(), red, U);
+    for (uint32_t i = lo2; i < hi2; ++i) {
+        if (i >= M) break;
+        const bool nw = i == 0 || (A[i] >> 32) != (A[i - 1] >> 32);
+        if (nw) { sd[u] = dep_of(o, (uint32_t)(A[i] >> 32)); ++u; }
+        const uint32_t e = (uint32_t)A[i];
+        B[e] = (B[e] & 0xFFFFFFFF00000000ull) | (u - 1);
     }
     __syncthreads();
     // range groups over B[0, M)
@@ -508,56 +616,59 @@ __device__ void build_block(const Out &o, uint32_t t, uint64_t e0, uint32_t m, u
     c = 0;
     for (uint32_t e = lo3; e < hi3; ++e) c += (e == 0 || (B[e] >> 32) != (B[e - 1] >> 32)) ? 1u : 0u;
     uint32_t Rd;
-    uint32_t g = block_excl(c, red, Rd);
-    if (!WRITE) {
-        if (tid == 0) { o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M; }
-        return;
-    }
-    const uint64_t abase = o.arena_off[t], rbase = o.rd_off[t];
+    uint32_t g = block_exclusive(c, OpAdd<uint32_t>(), red, Rd);
     for (uint32_t e = lo3; e < hi3; ++e) {
         const uint32_t rid = (uint32_t)(B[e] >> 32);
         const bool nw = e == 0 || (B[e - 1] >> 32) != rid;
-        if (nw) { o.range_id[rbase + g] = rid; ++g; }
-        o.arena[abase + Rd + e] = (int32_t)(uint32_t)B[e];
+        if (nw) { sr[g] = rid; ++g; }
+        sa[Rd + e] = (uint32_t)B[e];
         const bool last = e + 1 == M || (uint32_t)(B[e + 1] >> 32) != rid;
-        if (last) o.arena[abase + g - 1] = (int32_t)(Rd + e + 1);
+        if (last) sa[g - 1] = Rd + e + 1;
     }
+    if (tid == 0) { o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M; }
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(BLOCK) void k_rd_build_block(Out o)
+__global__ __launch_bounds__(BLOCK) void k_rd_build_block(Out o, uint32_t n2)
 {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const uint32_t t = o.blk_list[blockIdx.x];
-    uint64_t e0, e1;
-    txn_range(o, t, e0, e1);
     // all LDS dynamic (no static __shared__ ahead of it: the base stays 16-B aligned, Guideline 17)
-    build_block<WRITE>(o, t, e0, (uint32_t)(e1 - e0), lds, lds + BLOCK_E, reinterpret_cast<uint32_t *>(lds + 2 * BLOCK_E));
+    build_block(o, o.list[blockIdx.x], lds, lds + n2, reinterpret_cast<uint32_t *>(lds + 2 * n2));
 }
 
-template <bool WRITE>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_global(Out o)
 {
-    const uint32_t t = o.glb_list[blockIdx.x];
-    uint64_t e0, e1;
-    txn_range(o, t, e0, e1);
-    uint64_t *A = o.scratch + o.glb_off[blockIdx.x];
-    uint32_t n2 = 64;
-    while (n2 < e1 - e0) n2 <<= 1;
     __shared__ uint32_t red[WAVES];
-    build_block<WRITE>(o, t, e0, (uint32_t)(e1 - e0), A, A + n2, red);
+    const uint32_t t = o.list[blockIdx.x];
+    uint64_t *A = o.gscratch + o.glb_off[blockIdx.x];
+    const uint64_t m = o.raw_off[t + 1] - o.raw_off[t];
+    uint64_t n2 = 64;
+    while (n2 < m) n2 <<= 1;
+    build_block(o, t, A, A + n2, red);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, const uint32_t *__restrict__ glb_list, Out o,
-                                                        uint64_t *__restrict__ sz)
+__global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, Out o, uint64_t *__restrict__ sz)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= ng) return;
-    uint64_t e0, e1;
-    txn_range(o, glb_list[i], e0, e1);
+    const uint32_t t = o.list[i];
+    const uint64_t m = o.raw_off[t + 1] - o.raw_off[t];
     uint64_t n2 = 64;
-    while (n2 < e1 - e0) n2 <<= 1;
+    while (n2 < m) n2 <<= 1;
     sz[i] = 2 * n2;
+}
+
+// scratch -> Java-layout CSR: 16 lanes per txn
+__global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
+{
+    const uint32_t gi = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
+    if (gi >= n) return;
+    const uint32_t t = gi;
+    const uint64_t ra = o.raw_off[t];
+    const uint64_t na = o.a_cnt[t], nr = o.rd_cnt[t], nu = o.u_cnt[t];
+    const uint64_t ao = o.arena_off[t], ro = o.rd_off[t], uo = o.u_off[t];
+    for (uint64_t j = sub; j < na; j += 16) o.arena[ao + j] = (int32_t)o.s_arena[2 * ra + j];
+    for (uint64_t j = sub; j < nr; j += 16) o.range_id[ro + j] = o.s_rid[ra + j];
+    for (uint64_t j = sub; j < nu; j += 16) o.dep_txn[uo + j] = o.s_dep[ra + j];
 }
 
 }  // namespace rd
@@ -587,18 +698,18 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint64_t *arena_off = ctx->get<uint64_t>("rd_arena_off", (size_t)n + 1);
     uint64_t *rd_off = ctx->get<uint64_t>("rd_rd_off", (size_t)n + 1);
     uint64_t *u_off = ctx->get<uint64_t>("rd_u_off", (size_t)n + 1);
-    auto empty_result = [&]() {
-        ACC_HIP(hipMemsetAsync(arena_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(rd_off, 0, ((size_t)n + 1) * 8, st));
-        ACC_HIP(hipMemsetAsync(u_off, 0, ((size_t)n + 1) * 8, st));
+    if (n == 0) {
+        ACC_HIP(hipMemsetAsync(arena_off, 0, 8, st));
+        ACC_HIP(hipMemsetAsync(rd_off, 0, 8, st));
+        ACC_HIP(hipMemsetAsync(u_off, 0, 8, st));
         *view = acc_rangedeps_view{ n, 0, 0, 0, 0, 0, ctx->get<uint64_t>("rd_dict_s", 1), ctx->get<uint64_t>("rd_dict_e", 1),
                                     arena_off, ctx->get<int32_t>("rd_arena", 1), rd_off, ctx->get<uint32_t>("rd_range_id", 1),
                                     u_off, ctx->get<uint32_t>("rd_dep_txn", 1) };
         ctx->rd_view = *view;
         ctx->rd_valid = true;
         ctx->sync();
-    };
-    if (n == 0) { empty_result(); return; }
+        return;
+    }
 
     const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
     const uint32_t *rng_off = stage_in(ctx, "in_rng_off", in->rng_off, (size_t)n + 1, in->mem);
@@ -618,6 +729,17 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint32_t *owner = ctx->get<uint32_t>("owner", P);
     Dictionary dict;
     prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict);
+    // TxnId positions and STARTED_BEFORE limits
+    const size_t m2 = 2 * (size_t)n;
+    uint32_t *isT = ctx->get<uint32_t>("rd_isT", m2);
+    uint32_t *tcnt = ctx->get<uint32_t>("rd_tcnt", m2 + 1);
+    ACC_HIP(hipMemsetAsync(isT, 0, m2 * sizeof(uint32_t), st));
+    launch(ctx, "rd_txnflag", k_rd_txnflag, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)dict.rank, isT);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, isT, tcnt, m2, true, tcnt + m2);
+    uint4 *tinfo = ctx->get<uint4>("rd_tinfo", n);
+    uint32_t *txn_of_tpos = ctx->get<uint32_t>("rd_txn_of_tpos", n);
+    launch(ctx, "rd_txncols", k_rd_txncols, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)dict.rank,
+           (const uint32_t *)tcnt, tl, tinfo, txn_of_tpos);
 
     // reference codes for the masks (first range bound / first query bound)
     uint64_t ref[2] = { 0, 0 };
@@ -655,7 +777,6 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     memcpy(hm, ctx->pinned, sizeof hm);
     rd_check_errors(hm[3]);
     const uint32_t NE = R ? *reinterpret_cast<uint32_t *>(ctx->pinned + 4) : 0;
-    const uint32_t *rank = dict.rank;
 
     // ---- 2. range-command entries, stored-range dictionary, class order
     const Runs rs_plan = make_runs(hm[0]), re_plan = make_runs(hm[1]);
@@ -665,8 +786,8 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint64_t *dkey = ctx->get<uint64_t>("rd_dkey", NE), *ekey = ctx->get<uint64_t>("rd_ekey", NE);
     const bool split = rs_plan.bits + re_plan.bits > 64;
     launch(ctx, "rd_entries", k_rd_entries, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, n, (const uint32_t *)eflag,
-           (const uint32_t *)eidx, (const uint32_t *)rowner, rs, re, rank, tl, rs_plan, re_plan, re_plan.bits, split ? 1 : 0,
-           e_s, e_e, e_rank, e_kind, dkey, ekey);
+           (const uint32_t *)eidx, (const uint32_t *)rowner, rs, re, (const uint4 *)tinfo, tl, rs_plan, re_plan, re_plan.bits,
+           split ? 1 : 0, e_s, e_e, e_rank, e_kind, dkey, ekey);
     Sorted ds;
     if (!split) {
         ds = radix_sort(ctx, "rs_rd_dict", dkey, nullptr, NE, rs_plan.bits + re_plan.bits);
@@ -714,60 +835,100 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
            (const uint64_t *)e_s, (const uint64_t *)e_e, (const uint32_t *)e_rank, (const uint8_t *)e_kind,
            (const uint32_t *)rid_of, cs_s, cs_e, cs_info, cs_kind);
 
-    // ---- 3. queries sorted by low bound; stabbing count -> offsets -> emit
+    // ---- 3. query records sorted by low bound; stabbing (one pass, block-sliced output)
     const Runs q_plan = make_runs(hm[2]);
+    QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = ctx->get<QRec>("rd_qrec_sorted", Q);
     uint64_t *qkey = ctx->get<uint64_t>("rd_qkey", Q);
-    launch(ctx, "rd_query_keys", k_rd_query_keys, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
-           rs, q_plan, qkey);
+    launch(ctx, "rd_qrec", k_rd_qrec, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
+           (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey);
     Sorted qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, q_plan.bits);
-    View v;
-    v.n = n; v.P = (uint32_t)P; v.R = (uint32_t)R; v.Q = Q; v.end_inclusive = (int)in->end_inclusive;
-    v.qperm = qs.vals; v.key_code = key_code; v.owner = owner; v.rs = rs; v.re = re; v.rowner = rowner; v.rank = rank;
-    v.tl = tl; v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
-    uint32_t *cnt = ctx->get<uint32_t>("rd_cnt", Q);
-    uint64_t *cnt64 = ctx->get<uint64_t>("rd_cnt64", Q);
-    uint64_t *q_off = ctx->get<uint64_t>("rd_q_off", (size_t)Q + 1);
-    launch(ctx, "rd_stab_count", k_rd_stab<false>, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, v, cnt,
-           (const uint64_t *)nullptr, (uint64_t *)nullptr);
-    launch(ctx, "rd_widen", k_widen_u32, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (size_t)Q, (const uint32_t *)cnt, cnt64);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt64, q_off, Q, true, q_off + Q);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, q_off + Q, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ctx->sync();
-    const uint64_t E = Q ? ctx->pinned[0] : 0;
-    uint64_t *ent = ctx->get<uint64_t>("rd_ent", E);
-    launch(ctx, "rd_stab_emit", k_rd_stab<true>, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, v, cnt, (const uint64_t *)q_off, ent);
+    launch(ctx, "rd_qsort", k_rd_qsort, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, Q, (const uint32_t *)qs.vals,
+           (const QRec *)rec, srec);
+    View v{};
+    v.Q = Q; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
+    v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
+    v.cursor = ctx->get<uint64_t>("rd_cursor", 1);
+    v.q_off = ctx->get<uint64_t>("rd_q_off", Q);
+    v.q_cnt = ctx->get<uint32_t>("rd_q_cnt", Q);
+    uint64_t E = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        // capacity: the last batch's need on this context, at least 16 per query
+        const uint64_t want = std::max<uint64_t>(ctx->rd_ent_hint, 16ull * Q + 1024);
+        v.ent = ctx->get<uint64_t>("rd_ent", want);
+        v.cap = ctx->bufs["rd_ent"].bytes / sizeof(uint64_t);
+        ACC_HIP(hipMemsetAsync(v.cursor, 0, 8, st));
+        launch(ctx, "rd_stab", k_rd_stab, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, v);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, v.cursor, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        E = ctx->pinned[0];
+        ctx->rd_ent_hint = std::max(ctx->rd_ent_hint, E);
+        if (E <= v.cap) break;
+        if (attempt == 1) fail(ACC_E_STATE, "internal: range-deps output grew between passes");
+    }
 
-    // ---- 4. per-txn RangeDeps: sizes, offsets, writes
+    // ---- 4. per-txn RangeDeps: raw sizes and tiers, build into scratch, offsets, compaction
     Out o{};
-    o.key_off = key_off; o.rng_off = rng_off; o.P = (uint32_t)P; o.q_off = q_off; o.ent = ent;
-    o.txn_of_rank = dict.txn_of_rank;
+    o.n = n; o.P = (uint32_t)P; o.key_off = key_off; o.rng_off = rng_off; o.q_off = v.q_off; o.q_cnt = v.q_cnt;
+    o.ent = v.ent;
+    o.txn_of_tpos = dict.batch_sorted ? nullptr : txn_of_tpos;
     o.rd_cnt = ctx->get<uint32_t>("rd_rd_cnt", n);
     o.u_cnt = ctx->get<uint32_t>("rd_u_cnt", n);
     o.a_cnt = ctx->get<uint64_t>("rd_a_cnt", n);
-    o.blk_list = ctx->get<uint32_t>("rd_blk_list", n);
-    o.glb_list = ctx->get<uint32_t>("rd_glb_list", n);
-    o.gstat = ctx->get<uint64_t>("rd_gstat", 4);
-    ACC_HIP(hipMemsetAsync(o.gstat, 0, 4 * sizeof(uint64_t), st));
-    const unsigned gw = (n + WAVES - 1) / WAVES;
-    launch(ctx, "rd_build_wave_sizes", k_rd_build_wave<false>, dim3(gw), dim3(BLOCK), 0, n, o);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, o.gstat, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    uint64_t *m_raw = ctx->get<uint64_t>("rd_m_raw", n);
+    uint32_t *tier = ctx->get<uint32_t>("rd_tier", n);
+    uint64_t *raw_off = ctx->get<uint64_t>("rd_raw_off", (size_t)n + 1);
+    launch(ctx, "rd_tsize", k_rd_tsize, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, o, m_raw, tier);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, m_raw, raw_off, n, true, raw_off + n);
+    o.raw_off = raw_off;
+    uint32_t *thist = ctx->get<uint32_t>("rd_thist", 16);
+    ACC_HIP(hipMemsetAsync(thist, 0, 16 * sizeof(uint32_t), st));
+    launch(ctx, "rd_tier_hist", k_rd_tier_hist, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)tier, thist);
+    // txns grouped by tier: one 8-bit radix pass (stable)
+    uint64_t *tkey = ctx->get<uint64_t>("rd_tkey", n);
+    launch(ctx, "rd_widen", k_widen_u32, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, (size_t)n, (const uint32_t *)tier, tkey);
+    Sorted ts = radix_sort(ctx, "rs_rd_tier", tkey, nullptr, n, 4);
+    uint32_t hh[16];
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, thist, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
-    const uint64_t nblk = ctx->pinned[0], nglb = ctx->pinned[1], glb_elems = ctx->pinned[2];
-    const size_t blk_lds = 2 * (size_t)BLOCK_E * sizeof(uint64_t) + 64;
-    if (nblk) {
-        ACC_HIP(hipFuncSetAttribute((const void *)k_rd_build_block<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blk_lds));
-        ACC_HIP(hipFuncSetAttribute((const void *)k_rd_build_block<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blk_lds));
-        launch(ctx, "rd_build_block_sizes", k_rd_build_block<false>, dim3((unsigned)nblk), dim3(BLOCK), blk_lds, o);
+    memcpy(hh, ctx->pinned, sizeof hh);
+    uint32_t toff[17];
+    toff[0] = 0;
+    for (int i = 0; i < 16; ++i) toff[i + 1] = toff[i] + hh[i];
+    o.s_arena = ctx->get<uint32_t>("rd_s_arena", 2 * E);
+    o.s_rid = ctx->get<uint32_t>("rd_s_rid", E);
+    o.s_dep = ctx->get<uint32_t>("rd_s_dep", E);
+    const uint32_t *tl_sorted = ts.vals;
+    if (hh[1]) {
+        o.list = tl_sorted + toff[1];
+        launch(ctx, "rd_build_s16", k_rd_build_seg<16>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
     }
+    if (hh[2]) {
+        o.list = tl_sorted + toff[2];
+        launch(ctx, "rd_build_s64", k_rd_build_seg<64>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+    }
+    uint64_t nblk = 0;
+    for (int b = 3; b <= 9; ++b) {
+        if (!hh[b]) continue;
+        const uint32_t n2 = 128u << (b - 3);
+        const size_t lds = 2 * (size_t)n2 * sizeof(uint64_t) + 64;
+        if (lds > 64 * 1024)
+            ACC_HIP(hipFuncSetAttribute((const void *)k_rd_build_block, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        o.list = tl_sorted + toff[b];
+        launch(ctx, "rd_build_block", k_rd_build_block, dim3(hh[b]), dim3(BLOCK), lds, o, n2);
+        nblk += hh[b];
+    }
+    const uint32_t nglb = hh[10];
     if (nglb) {
+        o.list = tl_sorted + toff[10];
         uint64_t *gsz = ctx->get<uint64_t>("rd_glb_sz", nglb);
-        uint64_t *goff = ctx->get<uint64_t>("rd_glb_off", nglb + 1);
-        launch(ctx, "rd_glb_sizes", k_rd_glb_sizes, dim3(grid_for(nglb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nglb,
-               (const uint32_t *)o.glb_list, o, gsz);
+        uint64_t *goff = ctx->get<uint64_t>("rd_glb_off", (size_t)nglb + 1);
+        launch(ctx, "rd_glb_sizes", k_rd_glb_sizes, dim3(grid_for(nglb, BLOCK)), dim3(BLOCK), 0, nglb, o, gsz);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, gsz, goff, nglb, true, goff + nglb);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, goff + nglb, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
         o.glb_off = goff;
-        o.scratch = ctx->get<uint64_t>("rd_glb_scratch", glb_elems);
-        launch(ctx, "rd_build_global_sizes", k_rd_build_global<false>, dim3((unsigned)nglb), dim3(BLOCK), 0, o);
+        o.gscratch = ctx->get<uint64_t>("rd_glb_scratch", ctx->pinned[0]);
+        launch(ctx, "rd_build_global", k_rd_build_global, dim3(nglb), dim3(BLOCK), 0, o);
     }
     uint64_t *rd_cnt64 = ctx->get<uint64_t>("rd_rd_cnt64", n), *u_cnt64 = ctx->get<uint64_t>("rd_u_cnt64", n);
     launch(ctx, "rd_widen", k_widen_u32, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, (size_t)n, (const uint32_t *)o.rd_cnt, rd_cnt64);
@@ -786,13 +947,13 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     o.arena = ctx->get<int32_t>("rd_arena", tot_arena);
     o.range_id = ctx->get<uint32_t>("rd_range_id", tot_rd);
     o.dep_txn = ctx->get<uint32_t>("rd_dep_txn", tot_u);
-    launch(ctx, "rd_build_wave", k_rd_build_wave<true>, dim3(gw), dim3(BLOCK), 0, n, o);
-    if (nblk) launch(ctx, "rd_build_block", k_rd_build_block<true>, dim3((unsigned)nblk), dim3(BLOCK), blk_lds, o);
-    if (nglb) launch(ctx, "rd_build_global", k_rd_build_global<true>, dim3((unsigned)nglb), dim3(BLOCK), 0, o);
+    launch(ctx, "rd_compact", k_rd_compact, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, o);
     ctx->stat("rangedeps.entries", NE);
     ctx->stat("rangedeps.stored_ranges", n_dict);
     ctx->stat("rangedeps.queries", Q);
     ctx->stat("rangedeps.raw_entries", E);
+    ctx->stat("rangedeps.s16_txns", hh[1]);
+    ctx->stat("rangedeps.s64_txns", hh[2]);
     ctx->stat("rangedeps.block_txns", nblk);
     ctx->stat("rangedeps.global_txns", nglb);
     ctx->sync();

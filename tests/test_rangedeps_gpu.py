@@ -52,12 +52,28 @@ def test_block_and_global_tiers(ctx):
     import oracle
     rb = rd_cases.dense(7, n=6000, key_bits=9, max_width_log2=7, ranges_per_txn=3)   # txns of 65..8192 entries
     g = ctx.calculate_partial_range_deps(rb)
-    assert ctx.stats()["rangedeps.block_txns"] > 0
+    st = ctx.stats()
+    assert st["rangedeps.block_txns"] > 0 and st["rangedeps.s16_txns"] > 0 and st["rangedeps.s64_txns"] > 0
     assert_same(g, oracle.rangedeps_batch(rb), "block tier")
     rb = rd_cases.global_tier(9000)
     g = ctx.calculate_partial_range_deps(rb)
     assert ctx.stats()["rangedeps.global_txns"] > 0
     assert_same(g, oracle.rangedeps_batch(rb), "global tier")
+
+
+def test_unsorted_batch(ctx):
+    """Txns not given in TxnId order: TxnId positions differ from batch indices (txn_of_tpos path)."""
+    import oracle
+    rb = rd_cases.dense(31, n=3000)
+    perm = np.random.RandomState(5).permutation(rb.n_txn)
+    kb = rb.keys.permuted(perm)
+    cnt = np.diff(rb.rng_off.astype(np.int64))[perm]
+    off = np.zeros(rb.n_txn + 1, np.uint32)
+    np.cumsum(cnt, out=off[1:])
+    starts = rb.rng_off[:-1].astype(np.int64)[perm]
+    idx = np.repeat(starts - off[:-1].astype(np.int64), cnt) + np.arange(int(off[-1]), dtype=np.int64)
+    rb2 = W.RangeBatch(kb, off, rb.rng_start[idx], rb.rng_end[idx], rb.end_inclusive)
+    assert_same(ctx.calculate_partial_range_deps(rb2), oracle.rangedeps_batch(rb2), "unsorted")
 
 
 def test_wide_codes(ctx):
