@@ -315,13 +315,33 @@ __device__ __forceinline__ uint32_t upper_bound_s(const uint64_t *a, uint32_t lo
     return lo;
 }
 
+// 64-ary search by one wave: first index in [lo, hi) whose value is >= v (upper = false) or > v (upper = true).
+// Each round is one parallel probe of 64 positions, so a 1M-entry class takes 4 dependent loads, not 20.
+__device__ __forceinline__ uint32_t wave_search(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v, bool upper)
+{
+    const uint32_t lane = lane_id();
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t p = lo + lane * step;
+        const bool below = p < hi && (upper ? a[p] <= v : a[p] < v);
+        const uint32_t c = (uint32_t)__popcll(__ballot(below));
+        if (c == 0) return lo;
+        const uint32_t base = lo + (c - 1) * step;   // a[base] is below v, the answer is in (base, base + step]
+        lo = base + 1;
+        hi = min(base + step + 1, hi);
+    }
+    const uint32_t p = lo + lane;
+    const bool below = p < hi && (upper ? a[p] <= v : a[p] < v);
+    return lo + (uint32_t)__popcll(__ballot(below));
+}
+
 struct StabTile {
     uint64_t s[TILE], e[TILE];
     uint2 info[TILE];
     uint8_t kind[TILE];
     uint64_t hi[WAVES];
     uint64_t lo;
-    uint32_t b0, b1;
+    uint32_t b0[NCLS], b1[NCLS];   // the block's window per width class
     uint32_t red[WAVES];
     uint64_t base;
 };
@@ -336,18 +356,9 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
     const uint32_t wm = r.flags & 0xFFu;
     uint32_t count = 0;
     for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
-        const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
-        if (a0 == a1) continue;
+        const uint32_t b0 = T.b0[c], b1 = T.b1[c];
+        if (b0 >= b1) continue;
         const uint64_t W = class_width(c);
-        if (tid == 0) {
-            const uint64_t wlo = lo_min > W ? lo_min - W : 0;
-            const uint32_t b0 = lower_bound_s(v.cs_s, a0, a1, wlo);
-            T.b0 = b0;
-            T.b1 = upper_bound_s(v.cs_s, b0, a1, hi_max);
-        }
-        __syncthreads();
-        const uint32_t b0 = T.b0, b1 = T.b1;
-        __syncthreads();
         const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
         for (uint32_t base = b0; base < b1; base += TILE) {
             const uint32_t len = min((uint32_t)TILE, b1 - base);
@@ -403,6 +414,18 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) hi_max = T.hi[w] > hi_max ? T.hi[w] : hi_max;
     const uint64_t lo_min = T.lo;
+    // the block's window per class (starts in [lo_min - 4^c, hi_max]): wave w searches classes w, w + 4, ...
+    for (uint32_t c = tid >> 6; c < (uint32_t)NCLS; c += WAVES) {
+        const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
+        uint32_t b0 = a0, b1 = a0;
+        if (a1 > a0) {
+            const uint64_t W = class_width(c);
+            b0 = wave_search(v.cs_s, a0, a1, lo_min > W ? lo_min - W : 0, false);
+            b1 = wave_search(v.cs_s, b0, a1, hi_max, true);
+        }
+        if (lane_id() == 0) { T.b0[c] = b0; T.b1[c] = b1; }
+    }
+    __syncthreads();
     const uint32_t count = stab_pass<false>(v, T, valid, r, lo_min, hi_max, 0);
     uint32_t total;
     const uint32_t mine = block_exclusive(count, OpAdd<uint32_t>(), T.red, total);
