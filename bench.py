@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bench: batched Accord dependency calculation on MI355X through the C ABI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -11,6 +11,8 @@
 (device pointers) and results left device-resident (acc_keydeps_view).
 --config 4 (configs[3]): RangeDeps of 10M range txns (1 EndInclusive range each, log-uniform widths <= 2^16)
 interleaved with 10M key txns x 4 keys over the int32 key space; a step = one acc_rangedeps_batch.
+--config 5 (configs[4]): KeyDeps.merge of 16,384 coordinated txns x 64 replica replies, then acc_levelise of the
+merged graph by executeAt; a step = one acc_keydeps_merge + one acc_levelise on device-resident inputs.
 
 Multi-GPU (--config 2, N > 1): one global batch of N x 1M txns x 8 keys, zipf(0.99) over N x 1M keys (seeded
 permutation), key range-sharded over the N GPUs the way CommandStores shard a node (EvenSplit); each rank is one
@@ -325,18 +327,116 @@ def run_config4(args, world, rank, local, dev):
     return ctx, timing, elapsed, result
 
 
+def merge_bytes(m, view, n_txn, n_edges):
+    """SURVEY.md §8(d) merge + levelise: every reply's keys / TxnIds / keysToTxnIds and offsets in, the merged
+    per-txn CSR out; levelise reads the merged graph (val_off, TxnIds, executeAt ranks) and writes level + order."""
+    nr = len(m["key_off"]) - 1
+    b_in = 8 * len(m["key_code"]) + 4 * len(m["txn_rank"]) + 4 * len(m["k2v"]) + 24 * (nr + 1) + 8 * (n_txn + 1)
+    b_out = 8 * view.total_keys + 4 * view.total_vals + 4 * view.total_k2v + 24 * (n_txn + 1)
+    b_lv = 8 * (n_txn + 1) + 4 * n_edges + 4 * n_txn + 8 * n_txn
+    return b_in + b_out + b_lv
+
+
+def merge_prefix(m, g):
+    """The first g groups of an acc_merge_in dict (groups and their replies are contiguous)."""
+    r = int(m["grp_off"][g])
+    ko, vo, oo = (int(m[k][r]) for k in ("key_off", "val_off", "k2v_off"))
+    return dict(grp_off=m["grp_off"][:g + 1], key_off=m["key_off"][:r + 1], key_code=m["key_code"][:ko],
+                val_off=m["val_off"][:r + 1], txn_rank=m["txn_rank"][:vo], k2v_off=m["k2v_off"][:r + 1],
+                k2v=m["k2v"][:oo])
+
+
+def merge_cpu_baseline(m, exec_rank, n_in):
+    """The C restatement (LinearMerger fold of linearUnion per txn, then the levelisation walk) on a prefix of the
+    same config-5 batch, single thread; unit = input entries merged/s."""
+    import oracle
+    n = len(m["grp_off"]) - 1
+    g = min(n, max(1, int(os.environ.get("ACC_CPU_GROUPS_MERGE", str(n)))))
+    sub = merge_prefix(m, g)
+    entries = int(len(sub["k2v"]) - (len(sub["key_code"])))
+    t0 = time.perf_counter()
+    ref = oracle.keydeps_merge(sub)
+    t1 = time.perf_counter()
+    er = np.argsort(np.argsort(exec_rank[:g], kind="stable"), kind="stable").astype(np.uint32)
+    dep = ref["txn_rank"]
+    oracle.levelise(ref["val_off"], dep, er)
+    t2 = time.perf_counter()
+    return {
+        "value": round(entries / (t2 - t0), 1),
+        "unit": "input entries/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"first {g} of {n} coordinated txns ({entries} reply entries of {n_in}): KeyDeps.merge "
+                   f"{t1 - t0:.2f} s + levelise of their merged graph {t2 - t1:.3f} s"),
+    }
+
+
+def run_config5(args, world, rank, local, dev):
+    import torch
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import Context, merge_levelise_device
+
+    seed = W.CONFIG_SEEDS["5"] + 0x1000 * rank
+    n_txn = int(16_384 * args.scale)
+    m = W.merge_batch(n_txn=n_txn, replies=64, seed=seed)
+    exec_rank = W.merge_exec_rank(n_txn, seed)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in m.items()}
+    er = torch.from_numpy(exec_rank).to(dev)
+    level = torch.empty(n_txn, dtype=torch.int32, device=dev)
+    order = torch.empty(n_txn, dtype=torch.int32, device=dev)
+    nl = np.zeros(1, np.uint32)
+    torch.cuda.synchronize()
+    mi = L.MergeIn(L.ACC_MEM_DEVICE, n_txn, len(m["key_off"]) - 1,
+                   *(t[k].data_ptr() for k in ("grp_off", "key_off", "key_code", "val_off", "txn_rank", "k2v_off",
+                                               "k2v")))
+    ctx = Context(local, timing=True)
+
+    def fn():
+        view, nl[0] = merge_levelise_device(ctx, mi, er.data_ptr(), level.data_ptr(), order.data_ptr())
+        return view
+
+    step = Step(ctx, fn)
+    elapsed = timed_steps(args, world, dev, step)
+    view = step.view
+    timing = ctx.timing()
+    n_in = int(view.total_in_entries)
+    result = {
+        "metric": "Deps.merge input entries merged/sec + executeAt levelisation (node)",
+        "value": round(n_in * world * args.steps / elapsed, 1),
+        "unit": "input entries/s",
+        "dtype": "u32/u64 (integer)",
+        "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) config 5)",
+        "config": {
+            "workload": f"config5: KeyDeps.merge of {n_txn} coordinated txns x 64 replica replies (zipf keys, each "
+                        "reply drops 10% of the true entries and adds 5% spurious ones), then levelisation of the "
+                        "merged graph by executeAt",
+            "n_txn_per_gpu": n_txn,
+            "replies_per_gpu": n_txn * 64,
+            "input_entries_per_gpu": n_in,
+            "merged_entries_per_gpu": int(view.total_k2v - view.total_keys),
+            "levels": int(nl[0]),
+            "parallelism": f"independent coordinators x{world}",
+        },
+        "roofline": roofline(merge_bytes(m, view, n_txn, int(view.total_vals)), timing, args.steps),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = merge_cpu_baseline(m, exec_rank, n_in)
+    return ctx, timing, elapsed, result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="2", choices=["2", "4"])
+    ap.add_argument("--config", default="2", choices=["2", "4", "5"])
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config (testing only)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
     world, rank, local, dev = dist_setup(args)
-    run = {"2": run_config2 if world == 1 else run_config2_sharded, "4": run_config4}[args.config]
+    run = {"2": run_config2 if world == 1 else run_config2_sharded, "4": run_config4, "5": run_config5}[args.config]
     ctx, timing, elapsed, result = run(args, world, rank, local, dev)
     out = {
         "metric": result.pop("metric"),

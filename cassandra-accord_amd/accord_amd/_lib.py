@@ -139,6 +139,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"accord_amd: HIP library not built ({LIB_PATH}); run __graft_entry__.build()")
+    # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's). Whichever is loaded first serves the
+    # whole process; if ours came first, torch's device init later fails ("No HIP GPUs are available"). Load
+    # torch's first so the library and torch share one HIP runtime (and device buffers) when both are used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     L.acc_create.argtypes = [C.c_int, C.POINTER(Opts), C.POINTER(C.c_void_p)]
     L.acc_create.restype = C.c_int

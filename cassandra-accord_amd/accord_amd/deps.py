@@ -389,3 +389,17 @@ def levelise(ctx: Context, off, dep, exec_rank):
     ctx.check(ctx._lib.acc_levelise(ctx.handle, C.byref(gi), level.ctypes.data_as(L.u32p), order.ctypes.data_as(L.u32p),
                                     nl.ctypes.data_as(L.u32p)))
     return level[:n], order[:n], int(nl[0])
+
+
+def merge_levelise_device(ctx: Context, mi: "L.MergeIn", exec_rank_ptr: int, level_ptr: int, order_ptr: int):
+    """The coordinator path of config 5 on device: KeyDeps.merge of every txn's replies (acc_keydeps_merge,
+    primitives/KeyDeps.java:115-135), then levelisation of the merged graph (deps of txn t = its merged TxnIds, as
+    batch indices) by executeAt (acc_levelise, local/Commands.java:776-830). `mi` and the three pointers are device
+    memory; the merged view stays device-resident on ctx. Returns (merge view, n_levels)."""
+    view = L.MergeView()
+    ctx.check(ctx._lib.acc_keydeps_merge(ctx.handle, C.byref(mi), C.byref(view)))
+    gi = L.GraphIn(L.ACC_MEM_DEVICE, view.n_groups, view.val_off, view.txn_rank, exec_rank_ptr)
+    nl = np.zeros(1, np.uint32)
+    ctx.check(ctx._lib.acc_levelise(ctx.handle, C.byref(gi), C.cast(level_ptr, L.u32p), C.cast(order_ptr, L.u32p),
+                                    nl.ctypes.data_as(L.u32p)))
+    return view, int(nl[0])

@@ -201,6 +201,16 @@ def keydeps_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, dist: s
     return Batch(t_msb, t_lsb, t_node, exe_msb, exe_lsb, exe_node, status, key_off, key_code, meta)
 
 
+def merge_exec_rank(n_txn: int, seed: int = CONFIG_SEEDS["5"], max_bump: int = 50) -> np.ndarray:
+    """executeAt order of config 5's txns: txn t executes at t + U[0, max_bump) (ties by t), as dense ranks; deps on
+    txns with a later executeAt are not waited on (Commands.java:804-810)."""
+    key = np.arange(n_txn, dtype=np.int64) + (stream(seed, 50, n_txn) % np.uint64(max_bump)).astype(np.int64)
+    order = np.lexsort((np.arange(n_txn), key))
+    rank = np.empty(n_txn, dtype=np.uint32)
+    rank[order] = np.arange(n_txn, dtype=np.uint32)
+    return rank
+
+
 def config(name: str, scale: float = 1.0) -> Batch:
     """BASELINE.json configs 1a/1b (10k x 4 over 1k keys) and 2 (1M x 8, zipf 0.99 over 1M keys)."""
     if name == "1a":
@@ -219,14 +229,15 @@ def merge_batch(n_txn: int = 16_384, replies: int = 64, seed: int = CONFIG_SEEDS
                 keys_per_txn: int = 8, deps_per_key: int = 4, p_drop: float = 0.1, p_spurious: float = 0.05) -> dict:
     """Config 5 input in the acc_merge_in layout: group t = coordinated txn t, with `replies` KeyDeps replies.
 
-    Each txn gets a base dependency map (keys_per_txn zipf keys, deps_per_key dep ranks below its own rank),
+    Each txn gets a base dependency map (keys_per_txn zipf keys, deps_per_key deps on earlier txns of the batch,
+    named by batch index = TxnId rank, so the merged deps form the graph that acc_levelise orders),
     standing in for its config-2-style deps; every reply drops each base entry with p_drop and adds
     round(p_spurious * base entries) spurious ones on the txn's keys. Replies are built in the Java layout
     (sorted unique keys / txnId ranks, keysToTxnIds with the end-offset header)."""
     rng_u = lambda salt, n: uniform01(seed, salt, n)  # noqa: E731
     keys = _distinct_keys(seed, n_txn, keys_per_txn, zipf_sampler(seed, 40, n_keys, 0.99, True))
     kc = int_key_code(keys.reshape(-1)).astype(np.int64)
-    t_rank = 2 * np.arange(n_txn, dtype=np.int64) + 2  # ranks of the txns (gaps leave room for other ids)
+    t_rank = np.arange(n_txn, dtype=np.int64)  # txn t's TxnId rank = its index: deps name earlier txns of the batch
     # base entries (t, key, dep)
     bt = np.repeat(np.arange(n_txn, dtype=np.int64), keys_per_txn * deps_per_key)
     bk = np.repeat(kc, deps_per_key)

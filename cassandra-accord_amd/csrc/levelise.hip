@@ -5,15 +5,11 @@
 // else 1 + max level(dep); order = txns sorted by (level, executeAt rank, index).
 //
 // Every counted edge goes from a lower to a higher executeAt rank, so levels are final in executeAt order.
-// One workgroup walks the txns in executeAt order in windows of LV_WIN: each thread owns one txn; deps in
-// earlier windows are final in global memory; deps inside the window are waited for through LDS (level+1,
-// 0 = pending). The earliest pending txn of a window only depends on finished txns, so every spin round
-// retires at least one txn: the wait is bounded by the window's dependency-chain depth, at LDS latency.
+// One workgroup walks the txns in executeAt order (k_lv_walk); a dep's level is awaited by polling its
+// published value, so the walk's length is the graph's dependency-chain depth at LDS latency.
 #include "prims.hpp"
 
 namespace acc {
-
-constexpr int LV_WIN = 1024;
 
 __global__ __launch_bounds__(BLOCK) void k_lv_keys(uint32_t n, const uint32_t *__restrict__ exec_rank, uint64_t *__restrict__ key)
 {
@@ -32,59 +28,72 @@ __global__ __launch_bounds__(BLOCK) void k_lv_check(uint32_t n, const uint64_t *
         if (dep[e] >= n) { atomicOr(err, 2u); return; }
 }
 
-__global__ __launch_bounds__(1024) void k_lv_walk(uint32_t n, const uint32_t *__restrict__ order_exec, const uint32_t *__restrict__ pos,
-                                                  const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
-                                                  const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ level,
-                                                  uint32_t *__restrict__ max_level)
+// One workgroup of LV_THREADS lanes; lane j owns the txns at exec-order positions j, j + LV_THREADS, ... and
+// walks them in that order. Per txn it advances a cursor over the txn's deps: deps with exec rank >= its own
+// are skipped; a counted dep whose level is still unpublished (0) stops the cursor and the lane polls it again
+// on its next iteration (no barrier: lanes and waves progress independently). The txn at the earliest
+// pending position only depends on published txns, so the walk always advances and every lane's loop ends.
+// Published value = level + 1, indexed by txn. kLds: the level and exec-rank columns (8 B per txn) live in
+// LDS (n <= LV_LDS_MAX); otherwise levels are global (agent-scope atomics bypass the non-coherent L1) and
+// exec ranks are read from global.
+constexpr int LV_THREADS = 1024;
+constexpr uint32_t LV_LDS_MAX = 20000;   // 8 B/txn of the 160 KiB LDS
+
+template <bool kLds>
+__global__ __launch_bounds__(LV_THREADS) void k_lv_walk(uint32_t n, const uint32_t *__restrict__ order_exec,
+                                                        const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
+                                                        const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ level_g,
+                                                        uint32_t *__restrict__ max_level)
 {
-    __shared__ uint32_t win[LV_WIN];
-    uint32_t my_max = 0;
-    for (uint32_t w0 = 0; w0 < n; w0 += LV_WIN) {
-        const uint32_t slot = threadIdx.x;
-        const uint32_t i = w0 + slot;
-        win[slot] = 0;
-        __syncthreads();
-        bool active = i < n;
-        uint32_t t = 0, er = 0, base = 0;   // base: 1 + max level of deps in earlier windows (0 = none)
-        uint64_t a = 0, b = 0;
-        if (active) {
-            t = order_exec[i];
-            er = exec_rank[t];
-            a = off[t]; b = off[t + 1];
-            for (uint64_t e = a; e < b; ++e) {
-                uint32_t d = dep[e];
-                if (exec_rank[d] >= er) continue;
-                uint32_t pd = pos[d];
-                if (pd < w0) base = max(base, level[d] + 1);
-            }
-        }
-        bool done = !active;
-        // spin until every in-window dep has published its level
-        while (__syncthreads_or(!done)) {
-            if (!done) {
-                uint32_t l = base;
-                bool ready = true;
-                for (uint64_t e = a; e < b && ready; ++e) {
-                    uint32_t d = dep[e];
-                    if (exec_rank[d] >= er) continue;
-                    uint32_t pd = pos[d];
-                    if (pd < w0) continue;
-                    uint32_t v = __hip_atomic_load(&win[pd - w0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (v == 0) ready = false;
-                    else l = max(l, v);           // v = level(d) + 1
-                }
-                if (ready) {
-                    level[t] = l;                  // level = 1 + max dep level (0 without deps)
-                    __hip_atomic_store(&win[slot], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    my_max = max(my_max, l);
-                    done = true;
-                }
-            }
-        }
+    extern __shared__ uint32_t lds[];
+    uint32_t *lv = kLds ? lds : level_g;             // level + 1 per txn, 0 = pending
+    const uint32_t *er_col = kLds ? lds + n : exec_rank;
+    if (kLds) {
+        for (uint32_t t = threadIdx.x; t < n; t += LV_THREADS) { lds[t] = 0; lds[n + t] = exec_rank[t]; }
         __syncthreads();
     }
+    auto ld = [&](uint32_t d) -> uint32_t {
+        if (kLds) return __hip_atomic_load(&lv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __hip_atomic_load(&lv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    uint32_t my_max = 0;
+    uint32_t i = threadIdx.x;
+    uint32_t t = 0, er = 0, l = 0;
+    uint64_t cur = 0, b = 0;
+    if (i < n) { t = order_exec[i]; er = er_col[t]; cur = off[t]; b = off[t + 1]; }
+    while (__any(i < n)) {
+        if (i < n) {
+            bool pending = false;
+            // four deps per round: independent loads in flight together
+            while (cur < b && !pending) {
+                uint32_t dd[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dd[q] = cur + q < b ? dep[cur + q] : 0xFFFFFFFFu;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (pending || dd[q] == 0xFFFFFFFFu) continue;
+                    if (er_col[dd[q]] >= er) { ++cur; continue; }
+                    uint32_t v = ld(dd[q]);
+                    if (v == 0) { pending = true; continue; }
+                    l = max(l, v);           // v = level(dep) + 1
+                    ++cur;
+                }
+            }
+            if (!pending) {
+                if (kLds) __hip_atomic_store(&lv[t], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else __hip_atomic_store(&lv[t], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                my_max = max(my_max, l);
+                i += LV_THREADS;
+                l = 0;
+                if (i < n) { t = order_exec[i]; er = er_col[t]; cur = off[t]; b = off[t + 1]; }
+            }
+        }
+    }
+    __syncthreads();
+    if (kLds)
+        for (uint32_t u = threadIdx.x; u < n; u += LV_THREADS) level_g[u] = lds[u];
     // block max of levels -> n_levels - 1
-    __shared__ uint32_t red[16];
+    __shared__ uint32_t red[LV_THREADS / 64];
     uint32_t v = my_max;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
@@ -92,9 +101,16 @@ __global__ __launch_bounds__(1024) void k_lv_walk(uint32_t n, const uint32_t *__
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t m = 0;
-        for (int q = 0; q < 16; ++q) m = max(m, red[q]);
+        for (int q = 0; q < LV_THREADS / 64; ++q) m = max(m, red[q]);
         *max_level = m;
     }
+}
+
+// published level + 1 -> level
+__global__ __launch_bounds__(BLOCK) void k_lv_unbias(uint32_t n, uint32_t *__restrict__ level)
+{
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) level[t] -= 1;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_lv_pos(uint32_t n, const uint32_t *__restrict__ order_exec, uint32_t *__restrict__ pos)
@@ -142,8 +158,18 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     if (e0 & 2) fail(ACC_E_ARG, "dependency index out of range");
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);
-    launch(ctx, "lv_walk", k_lv_walk, dim3(1), dim3(1024), 0, n, (const uint32_t *)order_exec, (const uint32_t *)pos, off, dep,
-           exec_rank, level, maxl);
+    if (n <= LV_LDS_MAX) {
+        const size_t lds = (size_t)n * 8;
+        if (lds > 64 * 1024)
+            ACC_HIP(hipFuncSetAttribute((const void *)k_lv_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        launch(ctx, "lv_walk", k_lv_walk<true>, dim3(1), dim3(LV_THREADS), lds, n, (const uint32_t *)order_exec, off, dep,
+               exec_rank, level, maxl);
+    } else {
+        ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
+        launch(ctx, "lv_walk", k_lv_walk<false>, dim3(1), dim3(LV_THREADS), 0, n, (const uint32_t *)order_exec, off, dep,
+               exec_rank, level, maxl);
+    }
+    launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
     const int pbits = bits_for(n - 1);
     launch(ctx, "lv_order_keys", k_lv_order_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)level,
            (const uint32_t *)pos, pbits, key);

@@ -33,11 +33,11 @@ def test_levelise_random(ctx, n, max_deps):
     assert nl == nl2
 
 
-def test_levelise_long_chain(ctx):
-    """A hot-key write chain: every txn depends on its predecessor (depth n, crosses many windows)."""
+@pytest.mark.parametrize("n", [5000, 30000])
+def test_levelise_long_chain(ctx, n):
+    """A hot-key write chain: every txn depends on its predecessor (depth n; 30000 takes the global-memory walk)."""
     import oracle
     from accord_amd.deps import levelise
-    n = 5000
     er = np.arange(n, dtype=np.uint32)[::-1].copy()      # executeAt order reversed vs index
     off = np.concatenate([[0], np.cumsum([1 if t < n - 1 else 0 for t in range(n)])]).astype(np.uint64)
     dep = np.arange(1, n, dtype=np.uint32)              # t depends on t+1 (earlier executeAt)
@@ -64,3 +64,32 @@ def test_levelise_rejects_bad_dep(ctx):
     from accord_amd.deps import IllegalArgumentException, levelise
     with pytest.raises(IllegalArgumentException):
         levelise(ctx, np.array([0, 1], np.uint64), np.array([7], np.uint32), np.array([0], np.uint32))
+
+
+def test_merge_then_levelise_device(ctx):
+    """Config 5 at reduced size through the bench's device chain: merged deps of every coordinated txn
+    (KeyDeps.merge) levelised by executeAt, against the oracle merge + oracle levelise."""
+    import torch
+    import oracle
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import merge_levelise_device
+    n = 3000
+    m = W.merge_batch(n_txn=n, replies=8, seed=0xACC00006, n_keys=4000)
+    er = W.merge_exec_rank(n, 0xACC00006)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in m.items()}
+    er_d = torch.from_numpy(er).to(dev)
+    level = torch.empty(n, dtype=torch.int32, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    mi = L.MergeIn(L.ACC_MEM_DEVICE, n, len(m["key_off"]) - 1,
+                   *(t[k].data_ptr() for k in ("grp_off", "key_off", "key_code", "val_off", "txn_rank", "k2v_off",
+                                               "k2v")))
+    view, nl = merge_levelise_device(ctx, mi, er_d.data_ptr(), level.data_ptr(), order.data_ptr())
+    ctx.sync()
+    ref = oracle.keydeps_merge(m)
+    assert int(view.total_vals) == len(ref["txn_rank"])
+    l2, o2, nl2 = oracle.levelise(ref["val_off"], ref["txn_rank"], er)
+    np.testing.assert_array_equal(level.cpu().numpy().view(np.uint32), l2)
+    np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), o2)
+    assert nl == nl2 and nl > 1
