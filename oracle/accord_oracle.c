@@ -466,6 +466,26 @@ static uint64_t cfk_map_reduce_active(const cfk *c, const batch *B, const ts *st
     return visited;
 }
 
+/* Range.contains bounds over the sorted CFK keys (InMemoryCommandStore.mapReduceForKey :274-289:
+ * commandsForKey.subMap(start, startInclusive, end, endInclusive)): first CFK index with key inside / past the
+ * range. EndInclusive (s, e]: keys > s up to <= e; StartInclusive [s, e): keys >= s up to < e. */
+static size_t cfk_lower(const cfk *cfks, size_t ncfk, uint64_t bound, int strictly_above)
+{
+    size_t a = 0, z = ncfk;
+    while (a < z) {
+        size_t m = (a + z) / 2;
+        if (strictly_above ? cfks[m].key <= bound : cfks[m].key < bound) a = m + 1; else z = m;
+    }
+    return a;
+}
+
+static void keydeps_impl(orc_keydeps_result *R, uint32_t n,
+                         const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                         const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                         const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                         const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end, int end_inclusive,
+                         uint32_t n_shards, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride);
+
 orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
                                       const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
@@ -474,6 +494,32 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       uint32_t query_stride)
 {
     orc_keydeps_result *R = calloc(1, sizeof *R);
+    keydeps_impl(R, n, tmsb, tlsb, tnode, emsb, elsb, enode, status, key_off, key_code, NULL, NULL, NULL, 1,
+                 n_shards, query_lo, query_hi, query_stride);
+    return R;
+}
+
+orc_keydeps_result *orc_keydeps_mixed(uint32_t n,
+                                      const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                      const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                      const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                      const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                      int end_inclusive, uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
+                                      uint32_t query_stride)
+{
+    orc_keydeps_result *R = calloc(1, sizeof *R);
+    keydeps_impl(R, n, tmsb, tlsb, tnode, emsb, elsb, enode, status, key_off, key_code, rng_off, rng_start, rng_end,
+                 end_inclusive, n_shards, query_lo, query_hi, query_stride);
+    return R;
+}
+
+static void keydeps_impl(orc_keydeps_result *R, uint32_t n,
+                         const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                         const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                         const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                         const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end, int end_inclusive,
+                         uint32_t n_shards, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride)
+{
     double t_start = now_s();
     if (query_stride == 0) query_stride = 1;
     err E = { 0, "" };
@@ -493,6 +539,15 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
         if (ts_kind(&B.id[t]) >= K_COUNT) set_err(&E, -1, "Kind.ofOrdinal: invalid kind ordinal");
         for (uint32_t j = key_off[t] + 1; j < key_off[t + 1]; ++j)
             if (key_code[j - 1] >= key_code[j]) set_err(&E, -1, "keys of a txn must be sorted and unique");
+        if (rng_off) {
+            int isr = (int)(tlsb[t] & 1);   /* TxnId.domain() (TxnId.java:134-157) */
+            if (isr && key_off[t + 1] != key_off[t]) set_err(&E, -1, "a range txn cannot list keys");
+            if (!isr && rng_off[t + 1] != rng_off[t]) set_err(&E, -1, "a key txn cannot list ranges");
+            for (uint32_t j = rng_off[t]; j < rng_off[t + 1]; ++j) {
+                if (rng_start[j] >= rng_end[j]) set_err(&E, -1, "range start must be below its end");
+                if (j > rng_off[t] && rng_end[j - 1] > rng_start[j]) set_err(&E, -1, "ranges of a txn must be sorted and non-overlapping");
+            }
+        }
     }
 
     /* Group pairs by key -> one CommandsForKey per key (InMemoryCommandStore.commandsForKey). */
@@ -531,7 +586,7 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
     R->arena_off = calloc(n + 1, sizeof(uint64_t));
     R->kd_off = calloc(n + 1, sizeof(uint64_t));
     R->u_off = calloc(n + 1, sizeof(uint64_t));
-    ivec arena = { 0 }, kidx = { 0 }, deps = { 0 };
+    ivec arena = { 0 }, kidx = { 0 }, deps = { 0 }, kkey = { 0 };
     builder b; b_init(&b, &B);
 
     for (uint32_t t = 0; t < n && !E.code; ++t) {
@@ -556,6 +611,18 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                 while (a < z) { size_t m = (a + z) / 2; if (cfks[m].key < k) a = m + 1; else z = m; }
                 R->visited += cfk_map_reduce_active(&cfks[a], &B, &B.ex[t], (unsigned)wk, p1, &b, &E);
             }
+            /* Range domain (:274-289): ranges.slice(store) in order, every CommandsForKey of the subMap. A range
+             * txn is no CFK member (SafeCommandStore.updateCommandsForKey registers key txns only). */
+            if (rng_off)
+                for (uint32_t r = rng_off[t]; r < rng_off[t + 1]; ++r) {
+                    size_t a = cfk_lower(cfks, ncfk, rng_start[r], end_inclusive);
+                    size_t z = cfk_lower(cfks, ncfk, rng_end[r], end_inclusive);
+                    for (size_t c = a; c < z; ++c) {
+                        uint64_t k = cfks[c].key;
+                        if (k < lo || (!last && k >= hi)) continue;
+                        R->visited += cfk_map_reduce_active(&cfks[c], &B, &B.ex[t], (unsigned)wk, p1, &b, &E);
+                    }
+                }
             kdeps part; if (b_build(&b, &part, &E)) break;
             /* PreAccept.reduce -> PartialDeps.with -> KeyDeps.with (PreAccept.java:141-156) */
             kd_with(&acc, &part, cmp_vals_by_id, &B);
@@ -564,6 +631,23 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
         /* Emit in the ABI layout: key indices into T's keys, deps as batch indices. */
         for (size_t q = 0; q < acc.nk2v; ++q) iv_push(&arena, acc.k2v[q]);
         for (size_t q = 0; q < acc.nkeys; ++q) {
+            iv_push(&kkey, (int64_t)acc.keys[q]);
+            if (rng_off && rng_off[t + 1] > rng_off[t]) {
+                /* range txn: index among the CFK keys its ranges cover, in range order */
+                uint64_t idx = 0;
+                for (uint32_t r = rng_off[t]; r < rng_off[t + 1]; ++r) {
+                    size_t a = cfk_lower(cfks, ncfk, rng_start[r], end_inclusive);
+                    size_t z = cfk_lower(cfks, ncfk, rng_end[r], end_inclusive);
+                    if (z > a && cfks[z - 1].key >= acc.keys[q]) {
+                        while (a < z) { size_t m = (a + z) / 2; if (cfks[m].key < acc.keys[q]) a = m + 1; else z = m; }
+                        idx += a - cfk_lower(cfks, ncfk, rng_start[r], end_inclusive);
+                        break;
+                    }
+                    idx += z - a;
+                }
+                iv_push(&kidx, (int64_t)idx);
+                continue;
+            }
             uint32_t a = key_off[t], z = key_off[t + 1];
             while (a < z) { uint32_t m = (a + z) / 2; if (key_code[m] < acc.keys[q]) a = m + 1; else z = m; }
             iv_push(&kidx, (int64_t)(a - key_off[t]));
@@ -580,20 +664,22 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
     for (size_t q = 0; q < kidx.n; ++q) R->key_idx[q] = (uint32_t)kidx.v[q];
     R->dep_txn = malloc((deps.n + 1) * sizeof(uint32_t));
     for (size_t q = 0; q < deps.n; ++q) R->dep_txn[q] = (uint32_t)deps.v[q];
+    R->kd_key = malloc((kkey.n + 1) * sizeof(uint64_t));
+    for (size_t q = 0; q < kkey.n; ++q) R->kd_key[q] = (uint64_t)kkey.v[q];
     R->error = E.code;
     snprintf(R->message, sizeof R->message, "%s", E.msg);
 
     b_free(&b);
-    free(arena.v); free(kidx.v); free(deps.v);
+    free(arena.v); free(kidx.v); free(deps.v); free(kkey.v);
     for (size_t c = 0; c < ncfk; ++c) { free(cfks[c].txns); free(cfks[c].committed); }
     free(cfks); free(pidx); free(owner); free(shard_lo); free(B.id); free(B.ex);
-    return R;
 }
 
 void orc_keydeps_free(orc_keydeps_result *r)
 {
     if (!r) return;
     free(r->arena_off); free(r->arena); free(r->kd_off); free(r->key_idx); free(r->u_off); free(r->dep_txn);
+    free(r->kd_key);
     free(r);
 }
 

@@ -33,6 +33,7 @@ typedef struct orc_keydeps_result {
     double    query_s;    /* seconds spent in the per-txn calculatePartialDeps loop */
     int       error;      /* 0 ok, -1 IllegalArgument, -2 IllegalState */
     char      message[256];
+    uint64_t *kd_key;     /* [kd_off[n]] KeyDeps.keys as key codes */
 } orc_keydeps_result;
 
 /* Batch PreAccept.calculatePartialDeps over one CommandsForKey snapshot (SURVEY.md §8 batch
@@ -46,6 +47,17 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
                                       const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
                                       uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
+                                      uint32_t query_stride);
+/* The same over a mixed key/range batch (rng_* as orc_rangedeps_batch): range-domain txns are no CommandsForKey
+ * members; as queries they scan every CFK whose key lies in their (store-sliced) ranges
+ * (InMemoryCommandStore.mapReduceForKey :274-289). For a range txn, key_idx indexes the list of CFK keys its
+ * ranges cover (range order); kd_key holds the key codes for every txn. */
+orc_keydeps_result *orc_keydeps_mixed(uint32_t n,
+                                      const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                      const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                      const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                      const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                      int end_inclusive, uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
                                       uint32_t query_stride);
 void orc_keydeps_free(orc_keydeps_result *r);
 

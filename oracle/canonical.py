@@ -200,3 +200,58 @@ def rangedeps_batch(rb, query_lo=0, query_hi=None):
             k2v.extend(pos[d] for d in sorted(m[r], key=lambda d: tid[d]))
         out.append((rids, union, k2v))
     return np.array([r[0] for r in dictionary], np.uint64), np.array([r[1] for r in dictionary], np.uint64), out
+
+
+def keydeps_mixed(rb, query_lo=0, query_hi=None):
+    """KeyDeps of a mixed key/range batch as set definitions. Key txns: as keydeps_batch. A range txn T is no
+    CommandsForKey member (SafeCommandStore.updateCommandsForKey registers key txns only) and, as a query, covers
+    every CFK key inside its ranges (InMemoryCommandStore.mapReduceForKey :274-289: subMap with the Range bound
+    inclusivity), each key's deps being the same set as for a key txn. Returns per txn (key codes, dep txn list,
+    keysToTxnIds)."""
+    b = rb.keys
+    n = b.n_txn
+    tid = [ts_key(b.txn_msb[i], b.txn_lsb[i], b.txn_node[i]) for i in range(n)]
+    tex = [ts_key(b.exe_msb[i], b.exe_lsb[i], b.exe_node[i]) for i in range(n)]
+    kinds = [kind_of(b.txn_lsb[i]) for i in range(n)]
+    status = [int(s) for s in b.status]
+    by_key: dict[int, list[int]] = {}
+    for t in range(n):
+        for j in range(int(b.key_off[t]), int(b.key_off[t + 1])):
+            by_key.setdefault(int(b.key_code[j]), []).append(t)
+    cfk_keys = sorted(by_key)
+    ei = int(rb.end_inclusive)
+    committed = {4, 5, 6}
+    out = []
+    hi = n if query_hi is None else query_hi
+    for t in range(n):
+        if not (query_lo <= t < hi):
+            out.append(([], [], []))
+            continue
+        S = tex[t]
+        wk = WITNESSES[kinds[t]]
+        p1 = None if tex[t] == tid[t] else t
+        qkeys = [int(x) for x in b.key_code[int(b.key_off[t]):int(b.key_off[t + 1])]]
+        for j in range(int(rb.rng_off[t]), int(rb.rng_off[t + 1])):
+            s_, e_ = int(rb.rng_start[j]), int(rb.rng_end[j])
+            qkeys += [k for k in cfk_keys if ((s_ < k <= e_) if ei else (s_ <= k < e_))]
+        per_key = []
+        for k in sorted(set(qkeys)):
+            entries = by_key[k]
+            cw = [tex[d] for d in entries if status[d] in committed and kinds[d] == 1 and tex[d] < S]
+            M = max(cw) if cw else None
+            deps = sorted((d for d in entries
+                           if tid[d] < S and kinds[d] in wk and status[d] not in (0, 7)
+                           and (status[d] not in committed or M is None or tex[d] >= M)
+                           and d != p1), key=lambda d: tid[d])
+            if deps:
+                per_key.append((k, deps))
+        union = sorted({d for _, ds in per_key for d in ds}, key=lambda d: tid[d])
+        pos = {d: i for i, d in enumerate(union)}
+        k2v, end = [], len(per_key)
+        for _, ds in per_key:
+            end += len(ds)
+            k2v.append(end)
+        for _, ds in per_key:
+            k2v.extend(pos[d] for d in ds)
+        out.append(([k for k, _ in per_key], union, k2v))
+    return out

@@ -28,7 +28,7 @@ class KeydepsResult(C.Structure):
                 ("u_off", u64p), ("dep_txn", u32p),
                 ("total_edges", C.c_uint64), ("visited", C.c_uint64),
                 ("queried_pairs", C.c_uint64), ("build_s", C.c_double), ("query_s", C.c_double),
-                ("error", C.c_int), ("message", C.c_char * 256)]
+                ("error", C.c_int), ("message", C.c_char * 256), ("kd_key", u64p)]
 
 
 class MergeResult(C.Structure):
@@ -67,6 +67,9 @@ def lib():
         L.orc_keydeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
                                         C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_keydeps_free.argtypes = [C.POINTER(KeydepsResult)]
+        L.orc_keydeps_mixed.restype = C.POINTER(KeydepsResult)
+        L.orc_keydeps_mixed.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
+                                        u32p, u64p, u64p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_keydeps_merge.restype = C.POINTER(MergeResult)
         L.orc_keydeps_merge.argtypes = [C.c_uint32, u64p, u64p, u64p, u64p, u32p, u64p, i32p]
         L.orc_merge_free.argtypes = [C.POINTER(MergeResult)]
@@ -100,6 +103,7 @@ class KeyDepsBatchOut:
     queried_pairs: int = 0
     build_s: float = 0.0
     query_s: float = 0.0
+    kd_key: np.ndarray | None = None   # KeyDeps.keys as key codes (every txn)
 
     def txn(self, t: int):
         a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
@@ -126,6 +130,29 @@ def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | N
     types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p]
     r = L.orc_keydeps_batch(n, *[_p(a, t) for a, t in zip(arrs, types)], n_shards, query_lo,
                             n if query_hi is None else query_hi, query_stride)
+    return _keydeps_out(L, r, n)
+
+
+def keydeps_mixed(rb, n_shards: int = 1, query_lo: int = 0, query_hi: int | None = None,
+                  query_stride: int = 1) -> KeyDepsBatchOut:
+    """KeyDeps of every queried txn of a mixed key/range batch (accord_oracle.c orc_keydeps_mixed): key txns as
+    keydeps_batch, range txns scan the CommandsForKey of every key inside their ranges."""
+    L = lib()
+    b = rb.keys
+    n = b.n_txn
+    arrs = [np.ascontiguousarray(x) for x in (b.txn_msb.astype(np.uint64), b.txn_lsb.astype(np.uint64),
+                                              b.txn_node.astype(np.int32), b.exe_msb.astype(np.uint64),
+                                              b.exe_lsb.astype(np.uint64), b.exe_node.astype(np.int32),
+                                              b.status.astype(np.uint8), b.key_off.astype(np.uint32),
+                                              b.key_code.astype(np.uint64), rb.rng_off.astype(np.uint32),
+                                              rb.rng_start.astype(np.uint64), rb.rng_end.astype(np.uint64))]
+    types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u64p, u64p]
+    r = L.orc_keydeps_mixed(n, *[_p(a, t) for a, t in zip(arrs, types)], int(rb.end_inclusive), n_shards,
+                            query_lo, n if query_hi is None else query_hi, query_stride)
+    return _keydeps_out(L, r, n)
+
+
+def _keydeps_out(L, r, n) -> KeyDepsBatchOut:
     try:
         R = r.contents
         if R.error:
@@ -138,7 +165,7 @@ def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | N
                               np.ctypeslib.as_array(R.key_idx, (max(nk, 1),))[:nk].copy(), u_off,
                               np.ctypeslib.as_array(R.dep_txn, (max(nd, 1),))[:nd].copy(),
                               int(R.total_edges), int(R.visited), int(R.queried_pairs), float(R.build_s),
-                              float(R.query_s))
+                              float(R.query_s), np.ctypeslib.as_array(R.kd_key, (max(nk, 1),))[:nk].copy())
     finally:
         L.orc_keydeps_free(r)
     return out

@@ -89,3 +89,65 @@ def test_config4_golden():
     o = oracle.rangedeps_batch(rb)
     for k in ("rng_start", "rng_end", "arena_off", "arena", "rd_off", "range_id", "u_off", "dep_txn"):
         np.testing.assert_array_equal(getattr(o, k), z["out_" + k], err_msg=k)
+
+
+# ---- KeyDeps of a mixed batch: range txns scan every CommandsForKey inside their ranges
+# (InMemoryCommandStore.mapReduceForKey :274-289)
+
+def check_mixed(rb, n_shards=1):
+    o = oracle.keydeps_mixed(rb, n_shards=n_shards)
+    c = canonical.keydeps_mixed(rb)
+    for t in range(rb.n_txn):
+        k, d, a = o.txn(t)
+        keys = o.kd_key[o.kd_off[t]:o.kd_off[t + 1]]
+        assert (list(keys), list(d), list(a)) == c[t], t
+    return o
+
+
+@pytest.mark.parametrize("end_inclusive", [1, 0])
+def test_mixed_keydeps_handmade(end_inclusive):
+    rb = rd_cases.handmade(end_inclusive)
+    o = check_mixed(rb)
+    # txn 2 (read over (15,35]) covers keys 18, 20, 21, 30 (end-inclusive) of writes 4 only (5 is a read, later)
+    keys = set(o.kd_key[o.kd_off[2]:o.kd_off[3]].tolist())
+    assert keys == set()   # key txns 4, 5 are after txn 2: TxnId >= startedBefore
+    # txn 10 (read, APPLIED, over (19,31]) sees write 4 on keys 20/21/30 (end-inclusive) or 20/21/30 (start-incl.)
+    k, d, a = o.txn(10)
+    keys = o.kd_key[o.kd_off[10]:o.kd_off[11]].tolist()
+    assert set(d.tolist()) == {4} and keys == [20, 21, 30]
+    # a range txn's key_idx indexes the CFK keys its ranges cover
+    cfk = sorted({int(x) for x in rb.keys.key_code})
+    lo, hi = 19, 31
+    covered = [x for x in cfk if ((lo < x <= hi) if end_inclusive else (lo <= x < hi))]
+    assert [covered[i] for i in k.tolist()] == keys
+    # key txns agree with the key-only path
+    kb = oracle.keydeps_batch(rb.keys)
+    for t in range(rb.n_txn):
+        if int(rb.rng_off[t + 1]) == int(rb.rng_off[t]):
+            for x, y in zip(kb.txn(t), o.txn(t)):
+                np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("seed,ei", [(11, 1), (12, 0), (13, 1)])
+def test_mixed_keydeps_dense(seed, ei):
+    rb = rd_cases.dense(seed, n=600, end_inclusive=ei)
+    o = check_mixed(rb)
+    assert o.total_edges > 0
+
+
+def test_mixed_keydeps_shards_invariant():
+    """KeyDeps of range txns do not depend on the CommandStore split (keys are disjoint across stores)."""
+    rb = rd_cases.dense(21, n=800)
+    a = oracle.keydeps_mixed(rb)
+    for s in (2, 3, 8):
+        b = oracle.keydeps_mixed(rb, n_shards=s)
+        for f in ("arena_off", "arena", "kd_off", "key_idx", "u_off", "dep_txn", "kd_key"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
+
+
+def test_mixed_keydeps_errors():
+    rb = rd_cases.handmade()
+    bad = W.RangeBatch(rb.keys, rb.rng_off, rb.rng_start.copy(), rb.rng_end.copy(), rb.end_inclusive)
+    bad.rng_start[0] = bad.rng_end[0]
+    with pytest.raises(oracle.OracleError):
+        oracle.keydeps_mixed(bad)
