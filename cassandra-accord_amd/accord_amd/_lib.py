@@ -23,7 +23,7 @@ u8p = C.POINTER(C.c_uint8)
 
 # Every symbol declared in include/accord_amd.h (tests check the library exports all of them).
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
-           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
+           "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_mixed", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get"]
 
@@ -47,7 +47,7 @@ class KeydepsView(C.Structure):
                 ("total_arena", C.c_uint64), ("total_keys", C.c_uint64), ("total_deps", C.c_uint64),
                 ("total_edges", C.c_uint64),
                 ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("kd_off", C.c_void_p),
-                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p), ("kd_key", C.c_void_p)]
 
 
 class KeydepsOut(C.Structure):
@@ -55,7 +55,7 @@ class KeydepsOut(C.Structure):
                 ("cap_arena", C.c_uint64), ("cap_keys", C.c_uint64), ("cap_deps", C.c_uint64),
                 ("need_arena", C.c_uint64), ("need_keys", C.c_uint64), ("need_deps", C.c_uint64),
                 ("arena_off", C.c_void_p), ("arena", C.c_void_p), ("kd_off", C.c_void_p),
-                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p)]
+                ("key_idx", C.c_void_p), ("u_off", C.c_void_p), ("dep_txn", C.c_void_p), ("kd_key", C.c_void_p)]
 
 
 class RangeBatchIn(C.Structure):
@@ -163,6 +163,8 @@ def load():
     L.acc_keydeps_batch.restype = C.c_int
     L.acc_keydeps_copy_out.argtypes = [C.c_void_p, C.POINTER(KeydepsOut)]
     L.acc_keydeps_copy_out.restype = C.c_int
+    L.acc_keydeps_mixed.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(KeydepsView)]
+    L.acc_keydeps_mixed.restype = C.c_int
     L.acc_rangedeps_batch.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(RangedepsView)]
     L.acc_rangedeps_batch.restype = C.c_int
     L.acc_rangedeps_copy_out.argtypes = [C.c_void_p, C.POINTER(RangedepsOut)]

@@ -166,6 +166,19 @@ class Context:
         view = self.rangedeps_batch_raw(self.range_batch_in(rb, keep))
         return self.copy_out_range(view)
 
+    def keydeps_mixed_raw(self, batch_in: "L.RangeBatchIn") -> "L.KeydepsView":
+        view = L.KeydepsView()
+        self.check(self._lib.acc_keydeps_mixed(self._h, C.byref(batch_in), C.byref(view)))
+        return view
+
+    def calculate_partial_key_deps_mixed(self, rb) -> "BatchKeyDeps":
+        """PartialDeps.keyDeps of PreAccept.calculatePartialDeps for every txn of a mixed key/range batch: key txns as
+        calculate_partial_deps, range txns over every CommandsForKey inside their ranges
+        (InMemoryCommandStore.mapReduceForKey, impl/InMemoryCommandStore.java:274-289). kd_key holds the key codes."""
+        keep = []
+        view = self.keydeps_mixed_raw(self.range_batch_in(rb, keep))
+        return self.copy_out(view, rb.keys)
+
     def copy_out_range(self, view: "L.RangedepsView") -> "BatchRangeDeps":
         n = view.n_txn
         out = L.RangedepsOut()
@@ -203,9 +216,14 @@ class Context:
         out.cap_arena, out.cap_keys, out.cap_deps = out.need_arena, out.need_keys, out.need_deps
         out.arena_off, out.kd_off, out.u_off = arena_off.ctypes.data, kd_off.ctypes.data, u_off.ctypes.data
         out.arena, out.key_idx, out.dep_txn = arena.ctypes.data, key_idx.ctypes.data, dep_txn.ctypes.data
+        kd_key = None
+        if view.kd_key:
+            kd_key = np.zeros(max(out.need_keys, 1), np.uint64)
+            out.kd_key = kd_key.ctypes.data
         self.check(self._lib.acc_keydeps_copy_out(self._h, C.byref(out)))
         return BatchKeyDeps(arena_off, arena[:out.need_arena], kd_off, key_idx[:out.need_keys], u_off,
-                            dep_txn[:out.need_deps], int(view.total_edges), batch)
+                            dep_txn[:out.need_deps], int(view.total_edges), batch,
+                            None if kd_key is None else kd_key[:out.need_keys])
 
 
 @dataclass
@@ -250,6 +268,7 @@ class BatchKeyDeps:
     dep_txn: np.ndarray
     total_edges: int
     batch: object = None
+    kd_key: np.ndarray | None = None   # key codes (acc_keydeps_mixed)
 
     def txn(self, t: int):
         a = self.arena[self.arena_off[t]:self.arena_off[t + 1]]
@@ -261,7 +280,10 @@ class BatchKeyDeps:
         """KeyDeps of txn t with real key codes and TxnId tuples (needs the input batch)."""
         k, d, a = self.txn(t)
         b = self.batch
-        keys = b.key_code[int(b.key_off[t]) + k.astype(np.int64)]
+        if self.kd_key is not None:
+            keys = self.kd_key[self.kd_off[t]:self.kd_off[t + 1]]
+        else:
+            keys = b.key_code[int(b.key_off[t]) + k.astype(np.int64)]
         txn_ids = [TxnId(int(b.txn_msb[x]), int(b.txn_lsb[x]), int(b.txn_node[x])) for x in d]
         return KeyDeps(keys, txn_ids, a)
 

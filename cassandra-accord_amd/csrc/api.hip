@@ -4,6 +4,7 @@
 
 namespace acc {
 void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view);
+void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view);
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
 void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
 void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
@@ -73,6 +74,15 @@ int acc_keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *ou
     });
 }
 
+int acc_keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::keydeps_mixed(ctx, in, out_view);
+    });
+}
+
 int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)
 {
     if (!ctx) return ACC_E_ARG;
@@ -95,6 +105,8 @@ int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)
         if (v.total_arena) ACC_HIP(hipMemcpyAsync(out->arena, v.arena, v.total_arena * 4, kind, ctx->stream));
         if (v.total_keys) ACC_HIP(hipMemcpyAsync(out->key_idx, v.key_idx, v.total_keys * 4, kind, ctx->stream));
         if (v.total_deps) ACC_HIP(hipMemcpyAsync(out->dep_txn, v.dep_txn, v.total_deps * 4, kind, ctx->stream));
+        if (out->kd_key && v.kd_key && v.total_keys)
+            ACC_HIP(hipMemcpyAsync(out->kd_key, v.kd_key, v.total_keys * 8, kind, ctx->stream));
         ctx->sync();
     });
 }

@@ -424,6 +424,7 @@ struct CfkView {
     const uint32_t *cum_u, *u_pos;
     const uint64_t *tl;
     uint32_t n;
+    const uint32_t *vseg;   // non-null: query j is (owner[j], segment vseg[j]) (range-domain txns, no CFK member)
 };
 
 struct Query {
@@ -445,8 +446,7 @@ __device__ __forceinline__ Query make_query(const CfkView &v, uint32_t j)
 {
     Query q;
     uint32_t t = v.owner[j];
-    uint32_t p = v.pair_pos[j];
-    uint32_t seg = v.seg_incl[p] - 1;
+    uint32_t seg = v.vseg ? v.vseg[j] : v.seg_incl[v.pair_pos[j]] - 1;
     uint32_t s0 = v.seg_start[seg], s1 = v.seg_start[seg + 1];
     uint32_t S = v.rank[v.n + t];          // startedBefore = T.executeAt
     q.trank = v.rank[t];
@@ -1507,14 +1507,28 @@ static void check_errors(uint64_t errs)
 // Exact replay path (v1): committed[] per segment sorted by (executeAt, txn order) and the reference's
 // FAST bisection per query; per-(T,k) lists emitted in order, then the per-T union by binary search.
 // Used when executeAt ties exist (or ACC_OPT_FORCE_REPLAY).
-static void keydeps_v1_tail(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view, uint32_t n, size_t P, int rbits,
-                            const uint8_t *status, const uint64_t *tl, const uint32_t *key_off, const uint32_t *owner,
-                            const uint32_t *rank, const uint32_t *txn_of_rank, uint64_t *g, const uint32_t *seg_incl,
-                            const uint32_t *seg_start, const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info,
-                            const uint32_t *pair_pos)
+// CommandsForKey state of a built batch, kept for the range-domain queries of acc_keydeps_mixed
+struct KdState {
+    bool cfk = false;                 // a CFK exists (P > 0)
+    uint32_t n = 0;
+    size_t P = 0;
+    int rbits = 0;
+    const uint32_t *rank = nullptr, *txn_of_rank = nullptr, *key_off = nullptr, *owner = nullptr;
+    const uint32_t *seg_incl = nullptr, *seg_start = nullptr, *s_rank = nullptr, *s_exec = nullptr;
+    const uint32_t *pair_pos = nullptr, *perm = nullptr;
+    const uint8_t *s_info = nullptr;
+    const uint64_t *tl = nullptr, *key_code = nullptr;
+    uint64_t *g = nullptr;
+    bool v1 = false;                  // the exact-replay columns below are built
+    CfkView v1view{};
+};
+
+// Exact-replay CFK columns: uncommitted/committed flags and counts, segmented executeAt prefix max, committed[] per
+// segment sorted by executeAt (CommandsForKey.java:462-469) with the nearest-Write scan
+static CfkView build_v1_cfk(acc_ctx *ctx, uint32_t n, size_t P, int rbits, const uint64_t *tl, const uint32_t *owner,
+                            const uint32_t *rank, const uint32_t *seg_incl, const uint32_t *seg_start,
+                            const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info, const uint32_t *pair_pos)
 {
-    (void)in;
-    hipStream_t st = ctx->stream;
     const unsigned gP = grid_for(P, BLOCK);
     uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
     uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
@@ -1549,12 +1563,24 @@ static void keydeps_v1_tail(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_vi
     uint32_t *cl_start = ctx->get<uint32_t>("cl_start", P + 1);
     launch(ctx, "seg_committed_start", k_seg_committed_start, dim3(grid_for(P + 1, BLOCK)), dim3(BLOCK), 0, P,
            (const uint32_t *)seg_incl, (const uint32_t *)seg_start, (const uint32_t *)cum_c, cl_start);
-
-    // ---- 4. conflict scan: count, scan, emit
     CfkView v;
     v.seg_start = seg_start; v.s_rank = s_rank; v.s_exec = s_exec; v.seg_incl = seg_incl; v.pair_pos = pair_pos;
     v.owner = owner; v.rank = rank; v.s_info = s_info; v.cl_start = cl_start; v.cl_exec = cl_exec; v.lastw = lastw;
-    v.pmax = pmax; v.cum_u = cum_u; v.u_pos = u_pos; v.tl = tl; v.n = n;
+    v.pmax = pmax; v.cum_u = cum_u; v.u_pos = u_pos; v.tl = tl; v.n = n; v.vseg = nullptr;
+    return v;
+}
+
+static void keydeps_v1_tail(acc_ctx *ctx, acc_keydeps_view *view, uint32_t n, size_t P, int rbits,
+                            const uint64_t *tl, const uint32_t *key_off, const uint32_t *owner,
+                            const uint32_t *rank, const uint32_t *txn_of_rank, uint64_t *g, const uint32_t *seg_incl,
+                            const uint32_t *seg_start, const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info,
+                            const uint32_t *pair_pos, KdState *ks)
+{
+    hipStream_t st = ctx->stream;
+    const unsigned gP = grid_for(P, BLOCK);
+    // ---- 4. conflict scan: count, scan, emit
+    CfkView v = build_v1_cfk(ctx, n, P, rbits, tl, owner, rank, seg_incl, seg_start, s_rank, s_exec, s_info, pair_pos);
+    if (ks) { ks->v1 = true; ks->v1view = v; }
     uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
     uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
     launch(ctx, "query_count", k_query_count, dim3(gP), dim3(BLOCK), 0, P, v, cnt);
@@ -1729,7 +1755,7 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
     memcpy(out.hg, hg, sizeof hg);
 }
 
-void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view, KdState *ks)
 {
     if (!in || !view) fail(ACC_E_ARG, "null argument");
     if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
@@ -1853,9 +1879,15 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     ctx->stat("keydeps.path_replay", ties || (ctx->flags & ACC_OPT_FORCE_REPLAY) ? 1 : 0);
     ctx->stat("keydeps.exec_ties", ties ? 1 : 0);
     ctx->stat("keydeps.batch_sorted", batch_sorted ? 1 : 0);
+    if (ks) {
+        ks->cfk = true; ks->n = n; ks->P = P; ks->rbits = rbits; ks->rank = rank; ks->txn_of_rank = txn_of_rank;
+        ks->key_off = key_off; ks->owner = owner; ks->seg_incl = seg_incl; ks->seg_start = seg_start;
+        ks->s_rank = s_rank; ks->s_exec = s_exec; ks->pair_pos = pair_pos; ks->perm = ps.vals; ks->s_info = s_info;
+        ks->tl = tl; ks->key_code = key_code; ks->g = g;
+    }
     if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
-        keydeps_v1_tail(ctx, in, view, n, P, rbits, status, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
-                        s_rank, s_exec, s_info, pair_pos);
+        keydeps_v1_tail(ctx, view, n, P, rbits, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
+                        s_rank, s_exec, s_info, pair_pos, ks);
         return;
     }
     const uint32_t nbc = htot[6];
@@ -1978,6 +2010,346 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
     ctx->sync();
     *view = acc_keydeps_view{ n, ctx->pinned[0], ctx->pinned[1], ctx->pinned[2], E, arena_off, arena, kd_off,
                               key_idx, u_off, dep_txn };
+    ctx->kd_view = *view;
+    ctx->kd_valid = true;
+}
+
+
+void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
+{
+    keydeps_core(ctx, in, view, nullptr);
+}
+
+// ---------------------------------------------------------------- KeyDeps of a mixed key/range batch
+//
+// A range-domain txn T is no CommandsForKey member (SafeCommandStore.updateCommandsForKey registers key txns only,
+// local/SafeCommandStore.java:217-240); as a query it visits every CFK whose key lies inside its store-sliced ranges
+// (impl/InMemoryCommandStore.java:274-289: commandsForKey.subMap(start, startInclusive, end, endInclusive)) and runs
+// the same mapReduceActive there. The key txns' results come from keydeps_core; each range txn's covered CFK keys
+// become "virtual" queries (T, segment) answered by the exact-replay scan (make_query / run_query), then one sort of
+// (txn, TxnId rank) gives every range txn's TxnId union and indices.
+
+constexpr uint64_t MX_ERR_DOMAIN = 1, MX_ERR_EMPTY = 2, MX_ERR_UNSORTED = 4, MX_ERR_OFF = 8;
+
+// validation (TxnId.domain(), Range start < end, Ranges.ofSortedAndDeoverlapped) and, per range, its run of covered
+// segments [ra, ra + rcnt) over the sorted CFK keys
+__global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t *__restrict__ tl,
+                                                     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ rng_off,
+                                                     const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
+                                                     uint32_t end_inclusive, const uint64_t *__restrict__ seg_key, uint32_t nseg,
+                                                     uint32_t *__restrict__ ra, uint64_t *__restrict__ rcnt,
+                                                     uint64_t *__restrict__ errs)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const bool isr = (tl[t] & 1u) != 0;
+    const uint32_t r0 = rng_off[t], r1 = rng_off[t + 1];
+    uint64_t e = 0;
+    if (r1 < r0) e |= MX_ERR_OFF;
+    else {
+        if (isr && key_off[t + 1] != key_off[t]) e |= MX_ERR_DOMAIN;
+        if (!isr && r1 != r0) e |= MX_ERR_DOMAIN;
+        for (uint32_t j = r0; j < r1; ++j) {
+            const uint64_t s = rs[j], x = re[j];
+            if (s >= x) e |= MX_ERR_EMPTY;
+            if (j > r0 && re[j - 1] > s) e |= MX_ERR_UNSORTED;
+            // EndInclusive (s, x]: keys > s .. <= x; StartInclusive [s, x): keys >= s .. < x
+            uint32_t lo = 0, hi = nseg;
+            while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (end_inclusive ? seg_key[m] <= s : seg_key[m] < s) lo = m + 1; else hi = m; }
+            const uint32_t a = lo;
+            hi = nseg;
+            while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (end_inclusive ? seg_key[m] <= x : seg_key[m] < x) lo = m + 1; else hi = m; }
+            ra[j] = a;
+            rcnt[j] = e ? 0 : (uint64_t)(lo - a);
+        }
+    }
+    if (e) atomicOr((unsigned long long *)errs, (unsigned long long)e);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mx_seg_keys(uint32_t nseg, const uint32_t *__restrict__ seg_start,
+                                                       const uint32_t *__restrict__ perm, const uint64_t *__restrict__ key_code,
+                                                       uint64_t *__restrict__ seg_key)
+{
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s < nseg) seg_key[s] = key_code[perm[seg_start[s]]];
+}
+
+// per txn: first virtual query (u32 CSR over the virtual query space)
+__global__ __launch_bounds__(BLOCK) void k_mx_voff(uint32_t n, const uint32_t *__restrict__ rng_off, const uint64_t *__restrict__ r_off,
+                                                   uint32_t *__restrict__ voff)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t <= n) voff[t] = (uint32_t)r_off[rng_off[t]];
+}
+
+// virtual queries j -> (owner txn, segment); MX_SPAN consecutive j per thread: one search, then a walk
+constexpr uint32_t MX_SPAN = 16;
+__global__ __launch_bounds__(BLOCK) void k_mx_vqueries(uint64_t V, uint32_t R, uint32_t n, const uint64_t *__restrict__ r_off,
+                                                       const uint32_t *__restrict__ ra, const uint32_t *__restrict__ rng_off,
+                                                       uint32_t *__restrict__ vowner, uint32_t *__restrict__ vseg)
+{
+    const uint64_t j0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * MX_SPAN;
+    if (j0 >= V) return;
+    uint32_t lo = 0, hi = R;   // last range r with r_off[r] <= j0 (and a non-empty run)
+    while (lo < hi) { uint32_t m = (lo + hi + 1) >> 1; if (r_off[m] <= j0) lo = m; else hi = m - 1; }
+    uint32_t r = lo;
+    uint32_t tlo = 0, thi = n;   // owner: last t with rng_off[t] <= r
+    while (tlo < thi) { uint32_t m = (tlo + thi + 1) >> 1; if (rng_off[m] <= r) tlo = m; else thi = m - 1; }
+    uint32_t t = tlo;
+    const uint64_t j1 = j0 + MX_SPAN < V ? j0 + MX_SPAN : V;
+    for (uint64_t j = j0; j < j1; ++j) {
+        while (r_off[r + 1] <= j) ++r;
+        while (rng_off[t + 1] <= r) ++t;
+        vowner[j] = t;
+        vseg[j] = ra[r] + (uint32_t)(j - r_off[r]);
+    }
+}
+
+// sort keys (txn, TxnId rank) of the emitted entries (emission order = (txn, key, rank) already)
+__global__ __launch_bounds__(BLOCK) void k_mx_sortkeys(uint64_t E, const uint32_t *__restrict__ deps, const uint32_t *__restrict__ list_of,
+                                                       const uint32_t *__restrict__ vowner, int rbits, uint64_t *__restrict__ key)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e < E) key[e] = ((uint64_t)vowner[list_of[e]] << rbits) | deps[e];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mx_uflag(uint64_t E, const uint64_t *__restrict__ sk, uint32_t *__restrict__ f)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < E) f[i] = i == 0 || sk[i] != sk[i - 1];
+}
+
+struct MxKv {   // the key-txn KeyDeps (keydeps_core's view)
+    const uint64_t *arena_off, *kd_off, *u_off;
+    const int32_t *arena;
+    const uint32_t *key_idx, *dep_txn;
+};
+struct MxV {    // the virtual-query space of the range txns
+    const uint32_t *voff, *vowner, *vseg, *vcnz, *ucum;
+    const uint64_t *vcnt, *vdep_off, *seg_key;
+};
+struct MxOut {
+    uint64_t *arena_off, *kd_off, *u_off;
+    int32_t *arena;
+    uint32_t *key_idx, *dep_txn;
+    uint64_t *kd_key;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, MxV x, uint64_t *__restrict__ a_cnt,
+                                                    uint64_t *__restrict__ kd_cnt, uint64_t *__restrict__ u_cnt)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
+    const uint64_t e0 = x.vdep_off[j0], e1 = x.vdep_off[j1];
+    const uint64_t kd = x.vcnz[j1] - x.vcnz[j0];
+    a_cnt[t] = (kv.arena_off[t + 1] - kv.arena_off[t]) + kd + (e1 - e0);
+    kd_cnt[t] = (kv.kd_off[t + 1] - kv.kd_off[t]) + kd;
+    u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (x.ucum[e1] - x.ucum[e0]);
+}
+
+// key txns: copy keydeps_core's result into the combined layout (16 lanes per txn) with key codes
+__global__ __launch_bounds__(BLOCK) void k_mx_copy_keytxns(uint32_t n, MxKv kv, const uint32_t *__restrict__ key_off,
+                                                           const uint64_t *__restrict__ key_code, MxOut o)
+{
+    const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
+    if (t >= n) return;
+    const uint64_t a0 = kv.arena_off[t], na = kv.arena_off[t + 1] - a0;
+    const uint64_t k0 = kv.kd_off[t], nk = kv.kd_off[t + 1] - k0;
+    const uint64_t u0 = kv.u_off[t], nu = kv.u_off[t + 1] - u0;
+    const uint64_t ao = o.arena_off[t], ko = o.kd_off[t], uo = o.u_off[t];
+    for (uint64_t i = sub; i < na; i += 16) o.arena[ao + i] = kv.arena[a0 + i];
+    for (uint64_t i = sub; i < nk; i += 16) {
+        const uint32_t ki = kv.key_idx[k0 + i];
+        o.key_idx[ko + i] = ki;
+        o.kd_key[ko + i] = key_code[key_off[t] + ki];
+    }
+    for (uint64_t i = sub; i < nu; i += 16) o.dep_txn[uo + i] = kv.dep_txn[u0 + i];
+}
+
+// range txns, per emitted entry in (txn, rank) order: index in the txn's TxnId union, arena value, TxnId array
+__global__ __launch_bounds__(BLOCK) void k_mx_entries(uint64_t E, const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sperm,
+                                                      const uint32_t *__restrict__ uflag, const uint32_t *__restrict__ list_of,
+                                                      MxV x, const uint32_t *__restrict__ txn_of_rank, int rbits, MxOut o)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= E) return;
+    const uint32_t e = sperm[i];
+    const uint32_t t = x.vowner[list_of[e]];
+    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
+    const uint64_t e0 = x.vdep_off[j0];
+    const uint32_t idx = x.ucum[i] + uflag[i] - 1 - x.ucum[e0];
+    const uint32_t kd = x.vcnz[j1] - x.vcnz[j0];
+    o.arena[o.arena_off[t] + kd + (e - e0)] = (int32_t)idx;
+    if (uflag[i]) o.dep_txn[o.u_off[t] + idx] = txn_of_rank[(uint32_t)(sk[i] & ((1ull << rbits) - 1))];
+}
+
+// range txns, per non-empty virtual query: KeyDeps.keys entry (covered-key index + code) and the end-offset header
+__global__ __launch_bounds__(BLOCK) void k_mx_keys(uint64_t V, MxV x, MxOut o)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= V || x.vcnt[j] == 0) return;
+    const uint32_t t = x.vowner[j];
+    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
+    const uint32_t slot = x.vcnz[j] - x.vcnz[j0];
+    const uint32_t kd = x.vcnz[j1] - x.vcnz[j0];
+    o.key_idx[o.kd_off[t] + slot] = (uint32_t)j - j0;
+    o.kd_key[o.kd_off[t] + slot] = x.seg_key[x.vseg[j]];
+    o.arena[o.arena_off[t] + slot] = (int32_t)(kd + (x.vdep_off[j + 1] - x.vdep_off[j0]));
+}
+
+void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view)
+{
+    if (!in || !view) fail(ACC_E_ARG, "null argument");
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    if (in->end_inclusive > 1) fail(ACC_E_ARG, "end_inclusive must be 0 (StartInclusive) or 1 (EndInclusive)");
+    const uint32_t n = in->n_txn;
+    const size_t R = (size_t)in->n_ranges;
+    if (R >= 0xFFFFFFFFull) fail(ACC_E_ARG, "n_ranges must be < 2^32");
+    hipStream_t st = ctx->stream;
+    ctx->kd_valid = false;
+
+    // ---- key txns (and the CFK snapshot): keydeps_core over the key part of the batch
+    acc_batch_in kin{ n, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
+    acc_keydeps_view kv{};
+    KdState ks;
+    keydeps_core(ctx, &kin, &kv, &ks);
+    ctx->kd_valid = false;
+    if (n == 0) {
+        kv.kd_key = ctx->get<uint64_t>("mx_kd_key", 1);
+        *view = kv;
+        ctx->kd_view = kv;
+        ctx->kd_valid = true;
+        return;
+    }
+    const uint32_t *key_off = stage_in(ctx, "in_key_off", in->key_off, (size_t)n + 1, in->mem);
+    const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, (size_t)in->n_pairs, in->mem);
+    const uint64_t *tl = stage_in(ctx, "in_tl", in->txn_id.lsb, n, in->mem);
+    const uint32_t *rng_off = stage_in(ctx, "in_rng_off", in->rng_off, (size_t)n + 1, in->mem);
+    const uint64_t *rs = stage_in(ctx, "in_rng_start", in->rng_start, R, in->mem);
+    const uint64_t *re = stage_in(ctx, "in_rng_end", in->rng_end, R, in->mem);
+
+    // ---- covered segments per range
+    uint32_t nseg = 0;
+    if (ks.cfk) {
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, ks.seg_incl + ks.P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        nseg = (uint32_t)(ctx->pinned[0] & 0xFFFFFFFFu);
+    }
+    uint64_t *seg_key = ctx->get<uint64_t>("mx_seg_key", (size_t)nseg + 1);
+    if (nseg)
+        launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
+               ks.key_code, seg_key);
+    uint32_t *ra = ctx->get<uint32_t>("mx_ra", R + 1);
+    uint64_t *rcnt = ctx->get<uint64_t>("mx_rcnt", R + 1);
+    uint64_t *r_off = ctx->get<uint64_t>("mx_r_off", R + 2);
+    uint64_t *errs = ctx->get<uint64_t>("mx_errs", 1);
+    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+    launch(ctx, "mx_ranges", k_mx_ranges, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, key_off, rng_off, rs, re,
+           in->end_inclusive, (const uint64_t *)seg_key, nseg, ra, rcnt, errs);
+    if (R) scan<uint64_t, OpAdd<uint64_t>>(ctx, rcnt, r_off, R, true, r_off + R);
+    else ACC_HIP(hipMemsetAsync(r_off, 0, 8, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, r_off + R, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t merr = ctx->pinned[0];
+    if (merr & MX_ERR_DOMAIN) fail(ACC_E_ARG, "a range-domain txn lists keys or a key-domain txn lists ranges (TxnId.domain())");
+    if (merr & MX_ERR_EMPTY) fail(ACC_E_ARG, "range start must be below its end (Range: start >= end)");
+    if (merr & MX_ERR_UNSORTED) fail(ACC_E_ARG, "ranges of a txn must be sorted and deoverlapped (Ranges.ofSortedAndDeoverlapped)");
+    if (merr & MX_ERR_OFF) fail(ACC_E_ARG, "rng_off must be non-decreasing");
+    const uint64_t V = ctx->pinned[1];
+    if (V >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 (range txn, covered key) queries in one batch");
+    ctx->stat("keydeps.range_key_queries", V);
+
+    // ---- virtual queries (T, segment) and the exact-replay scan over them
+    uint32_t *voff = ctx->get<uint32_t>("mx_voff", (size_t)n + 1);
+    launch(ctx, "mx_voff", k_mx_voff, dim3(grid_for((size_t)n + 1, BLOCK)), dim3(BLOCK), 0, n, rng_off, (const uint64_t *)r_off, voff);
+    uint32_t *vowner = ctx->get<uint32_t>("mx_vowner", V + 1);
+    uint32_t *vseg = ctx->get<uint32_t>("mx_vseg", V + 1);
+    uint64_t *vcnt = ctx->get<uint64_t>("mx_vcnt", V + 1);
+    uint64_t *vdep_off = ctx->get<uint64_t>("mx_vdep_off", V + 1);
+    uint32_t *vnz = ctx->get<uint32_t>("mx_vnz", V + 1);
+    uint32_t *vcnz = ctx->get<uint32_t>("mx_vcnz", V + 1);
+    uint64_t Ex = 0;
+    if (V) {
+        launch(ctx, "mx_vqueries", k_mx_vqueries, dim3(grid_for((V + MX_SPAN - 1) / MX_SPAN, BLOCK)), dim3(BLOCK), 0, V,
+               (uint32_t)R, n, (const uint64_t *)r_off, (const uint32_t *)ra, rng_off, vowner, vseg);
+        if (!ks.v1) {
+            ks.v1view = build_v1_cfk(ctx, n, ks.P, ks.rbits, ks.tl, ks.owner, ks.rank, ks.seg_incl, ks.seg_start, ks.s_rank,
+                                     ks.s_exec, ks.s_info, ks.pair_pos);
+            ks.v1 = true;
+        }
+        CfkView v = ks.v1view;
+        v.owner = vowner;
+        v.vseg = vseg;
+        const unsigned gV = grid_for(V, BLOCK);
+        launch(ctx, "mx_query_count", k_query_count, dim3(gV), dim3(BLOCK), 0, (size_t)V, v, vcnt);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, vcnt, vdep_off, V, true, vdep_off + V);
+        launch(ctx, "mx_nonempty", k_nonempty, dim3(gV), dim3(BLOCK), 0, (size_t)V, (const uint64_t *)vcnt, vnz);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, vnz, vcnz, V, true, vcnz + V);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, vdep_off + V, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        Ex = ctx->pinned[0];
+        if (Ex >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 range-txn KeyDeps entries in one batch");
+    } else {
+        ACC_HIP(hipMemsetAsync(vdep_off, 0, 8, st));
+        ACC_HIP(hipMemsetAsync(vcnz, 0, 4, st));
+    }
+    uint32_t *deps = ctx->get<uint32_t>("mx_deps", Ex + 1);
+    uint32_t *list_of = ctx->get<uint32_t>("mx_list_of", Ex + 1);
+    uint32_t *uflag = ctx->get<uint32_t>("mx_uflag", Ex + 1);
+    uint32_t *ucum = ctx->get<uint32_t>("mx_ucum", Ex + 1);
+    Sorted so{ nullptr, nullptr };
+    const int tbits = bits_for(n);
+    if (tbits + ks.rbits > 64) fail(ACC_E_CAP, "batch too large for the (txn, TxnId rank) composite key");
+    if (Ex) {
+        CfkView v = ks.v1view;
+        v.owner = vowner;
+        v.vseg = vseg;
+        launch(ctx, "mx_query_emit", k_query_emit, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, (size_t)V, v,
+               (const uint64_t *)vdep_off, deps, list_of);
+        uint64_t *skey = ctx->get<uint64_t>("mx_skey", Ex);
+        launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)deps,
+               (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, skey);
+        so = radix_sort(ctx, "mx_rs", skey, nullptr, Ex, tbits + ks.rbits);
+        launch(ctx, "mx_uflag", k_mx_uflag, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys, uflag);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, uflag, ucum, Ex, true, ucum + Ex);
+    } else {
+        ACC_HIP(hipMemsetAsync(ucum, 0, 4, st));
+    }
+
+    // ---- combined offsets, key txns copied, range txns written
+    MxKv mkv{ kv.arena_off, kv.kd_off, kv.u_off, kv.arena, kv.key_idx, kv.dep_txn };
+    MxV x{ voff, vowner, vseg, vcnz, ucum, vcnt, vdep_off, seg_key };
+    uint64_t *a_cnt = ctx->get<uint64_t>("mx_a_cnt", n);
+    uint64_t *kd_cnt = ctx->get<uint64_t>("mx_kd_cnt", n);
+    uint64_t *u_cnt = ctx->get<uint64_t>("mx_u_cnt", n);
+    launch(ctx, "mx_sizes", k_mx_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, mkv, x, a_cnt, kd_cnt, u_cnt);
+    MxOut o;
+    o.arena_off = ctx->get<uint64_t>("mx_arena_off", (size_t)n + 1);
+    o.kd_off = ctx->get<uint64_t>("mx_kd_off", (size_t)n + 1);
+    o.u_off = ctx->get<uint64_t>("mx_u_off", (size_t)n + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, o.arena_off, n, true, o.arena_off + n);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, o.kd_off, n, true, o.kd_off + n);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, o.u_off, n, true, o.u_off + n);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, o.arena_off + n, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, o.kd_off + n, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, o.u_off + n, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t TA = ctx->pinned[0], TK = ctx->pinned[1], TU = ctx->pinned[2];
+    o.arena = ctx->get<int32_t>("mx_arena", TA + 1);
+    o.key_idx = ctx->get<uint32_t>("mx_key_idx", TK + 1);
+    o.kd_key = ctx->get<uint64_t>("mx_kd_key", TK + 1);
+    o.dep_txn = ctx->get<uint32_t>("mx_dep_txn", TU + 1);
+    launch(ctx, "mx_copy_keytxns", k_mx_copy_keytxns, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, key_off,
+           key_code, o);
+    if (Ex)
+        launch(ctx, "mx_entries", k_mx_entries, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys,
+               (const uint32_t *)so.vals, (const uint32_t *)uflag, (const uint32_t *)list_of, x, ks.txn_of_rank, ks.rbits, o);
+    if (V) launch(ctx, "mx_keys", k_mx_keys, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, V, x, o);
+    ctx->sync();
+    *view = acc_keydeps_view{ n, TA, TK, TU, kv.total_edges + Ex, o.arena_off, o.arena, o.kd_off, o.key_idx, o.u_off,
+                              o.dep_txn, o.kd_key };
     ctx->kd_view = *view;
     ctx->kd_valid = true;
 }

@@ -126,6 +126,7 @@ typedef struct acc_keydeps_view {
     const uint32_t *key_idx;
     const uint64_t *u_off;
     const uint32_t *dep_txn;
+    const uint64_t *kd_key;   /* [total_keys] KeyDeps.keys as key codes (acc_keydeps_mixed; null after acc_keydeps_batch) */
 } acc_keydeps_view;
 
 /* Caller-owned output buffers (two-call sizing: capacities in elements; a call with null offset
@@ -141,6 +142,7 @@ typedef struct acc_keydeps_out {
     uint32_t *key_idx;        /* [cap_keys] */
     uint64_t *u_off;          /* [N+1] */
     uint32_t *dep_txn;        /* [cap_deps] */
+    uint64_t *kd_key;         /* optional [cap_keys]: key codes, copied when non-null and the result has them */
 } acc_keydeps_out;
 
 /* ---- context ---- */
@@ -205,6 +207,15 @@ typedef struct acc_rangedeps_out {
 } acc_rangedeps_out;
 
 int acc_rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *out_view);
+
+/* KeyDeps of every txn of a mixed key/range batch (the same input as acc_rangedeps_batch). Key txns: exactly
+ * acc_keydeps_batch. A range-domain txn is no CommandsForKey member (SafeCommandStore.updateCommandsForKey registers
+ * key txns only, local/SafeCommandStore.java:217-240); as a query it runs CommandsForKey.mapReduceActive on every CFK
+ * whose key lies in its ranges with the Range bound inclusivity (InMemoryCommandStore.mapReduceForKey,
+ * impl/InMemoryCommandStore.java:274-289). Replaces the key part of PreAccept.calculatePartialDeps for range txns
+ * (messages/PreAccept.java:245-265). The view is acc_keydeps_view with kd_key filled for every txn; for a range txn,
+ * key_idx indexes the list of CFK keys its ranges cover (range order). Copy out with acc_keydeps_copy_out. */
+int acc_keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *out_view);
 int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out);
 
 /* ---- Deps.merge over many replies per txn ----
