@@ -322,9 +322,32 @@ def run_config4(args, world, rank, local, dev):
         "dep_entries_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
         "roofline": roofline(b_in + b_out, timing, args.steps),
     }
+    if os.environ.get("ACC_BENCH_MIXED", "1") != "0":
+        result["keydeps_mixed"] = mixed_keydeps_leg(bi, local)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = rangedeps_cpu_baseline(rb)
     return ctx, timing, elapsed, result
+
+
+def mixed_keydeps_leg(bi, local, calls=3):
+    """The key half of the same mixed batch's PartialDeps (acc_keydeps_mixed: key txns' CommandsForKey scans plus every
+    range txn over the CFKs inside its range), timed separately on its own context: 1 warmup + `calls` timed calls."""
+    import torch
+    from accord_amd.deps import Context
+    with Context(local, timing=True) as c:
+        c.keydeps_mixed_raw(bi)
+        c.timing_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            v = c.keydeps_mixed_raw(bi)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1000.0 / calls
+        tm = c.timing()
+        top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:6]
+        return {"ms_per_call": round(ms, 3), "range_key_queries": int(c.stats().get("keydeps.range_key_queries", 0)),
+                "dep_entries": int(v.total_edges), "kd_keys": int(v.total_keys),
+                "top_kernels_ms": {k: round(x[0] / calls, 3) for k, x in top}}
 
 
 def merge_bytes(m, view, n_txn, n_edges):
