@@ -11,6 +11,8 @@
 //   2. three stable radix sorts of compacted composite keys;
 //   3. unique + per-group counts (scans) -> per-group CSR in Java layout; each (key, value) entry becomes
 //      the index of the value in the group's txnId array (binary search within the group).
+#include <algorithm>
+
 #include "prims.hpp"
 
 namespace acc {
@@ -61,6 +63,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_prep(uint64_t R, const uint64_t *__
                 if (i > va && txn_rank[i - 1] >= txn_rank[i]) err |= 4;   // txnIds sorted unique
             }
             if (nk && (uint64_t)(uint32_t)k2v[oa + nk - 1] != no) err |= 8;   // last offset == length
+            if (!nk && no) err |= 8;                                           // entries without keys
             uint64_t prev_end = nk;
             for (uint64_t i = 0; i < nk && !(err & 8); ++i) {
                 uint64_t end = (uint64_t)(uint32_t)k2v[oa + i];
@@ -247,6 +250,292 @@ __global__ __launch_bounds__(BLOCK) void k_m_key_of_slot(uint64_t R, const uint6
     }
 }
 
+// ---------------------------------------------------------------- LDS tier: one workgroup per group
+//
+// A group whose replies fit (<= ML_REP replies, <= ML_KC key slots, <= ML_VC TxnId slots, <= ML_OC keysToTxnIds
+// slots; config 5: 64 replies, 512 / ~2000 / ~2500) is merged entirely in LDS: its key, TxnId and (key, TxnId)
+// records are loaded once with coalesced reads, bitonic-sorted and de-duplicated in LDS, and the Java-layout result is
+// written to scratch at the group's input offsets (the union is never larger than the input), then compacted. The
+// per-reply validation of k_m_prep (KeyDeps ctor / checkValid) is done on the same loaded records.
+
+constexpr int ML_REP = 256, ML_KC = 1024, ML_VC = 4096, ML_OC = 4096;
+
+// per group: does it fit the LDS tier (offsets monotone, sizes within the caps)? g[3] |= 1 if some group does not
+__global__ __launch_bounds__(BLOCK) void k_m_fit(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
+                                                 const uint64_t *__restrict__ val_off, const uint64_t *__restrict__ k2v_off,
+                                                 uint64_t *__restrict__ g, uint64_t *__restrict__ gmax)
+{
+    const uint32_t gi = blockIdx.x * BLOCK + threadIdx.x;
+    bool bad = false;
+    if (gi < ng) {
+        const uint64_t r0 = grp_off[gi], r1 = grp_off[gi + 1];
+        if (r1 < r0 || r1 - r0 > ML_REP) bad = true;
+        else {
+            for (uint64_t r = r0; r < r1 && !bad; ++r)
+                if (key_off[r + 1] < key_off[r] || val_off[r + 1] < val_off[r] || k2v_off[r + 1] < k2v_off[r] ||
+                    k2v_off[r + 1] - k2v_off[r] < key_off[r + 1] - key_off[r])
+                    bad = true;
+            if (!bad)
+                bad = key_off[r1] - key_off[r0] > ML_KC || val_off[r1] - val_off[r0] > ML_VC ||
+                      k2v_off[r1] - k2v_off[r0] > ML_OC;
+        }
+    }
+    block_or1(bad ? 1ull : 0ull, &g[3]);
+    if (gi < ng && !bad) {
+        const uint64_t r0 = grp_off[gi], r1 = grp_off[gi + 1];
+        atomicMax((unsigned long long *)&gmax[0], (unsigned long long)(key_off[r1] - key_off[r0]));
+        atomicMax((unsigned long long *)&gmax[1], (unsigned long long)(val_off[r1] - val_off[r0]));
+        atomicMax((unsigned long long *)&gmax[2], (unsigned long long)(k2v_off[r1] - k2v_off[r0]));
+        atomicMax((unsigned long long *)&gmax[3], (unsigned long long)((k2v_off[r1] - k2v_off[r0]) - (key_off[r1] - key_off[r0])));
+    }
+}
+
+template <class T>
+__device__ __forceinline__ void lds_bitonic(T *s, uint32_t np)
+{
+    for (uint32_t k = 2; k <= np; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < np; i += BLOCK) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    T a = s[i], b = s[ixj];
+                    if ((a > b) == ((i & k) == 0)) { s[i] = b; s[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// order-preserving in-place unique of the sorted s[0..np) (pads last); returns the count. np = BLOCK * per.
+template <class T, int MAXI>
+__device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t np, T pad, uint32_t *scan_lds)
+{
+    const uint32_t per = np / BLOCK, base = threadIdx.x * per;
+    T x[MAXI];
+    uint32_t f = 0, c = 0;
+#pragma unroll
+    for (int q = 0; q < MAXI; ++q) {
+        if ((uint32_t)q < per) {
+            const uint32_t i = base + q;
+            x[q] = s[i];
+            const bool u = x[q] != pad && (i == 0 || s[i - 1] != x[q]);
+            f |= (uint32_t)u << q;
+            c += u;
+        }
+    }
+    uint32_t total;
+    uint32_t o = block_exclusive(c, OpAdd<uint32_t>(), scan_lds, total);
+#pragma unroll
+    for (int q = 0; q < MAXI; ++q)
+        if ((uint32_t)q < per && ((f >> q) & 1u)) s[o++] = x[q];
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ uint32_t pow2_at_least(uint32_t n)
+{
+    uint32_t p = BLOCK;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+__device__ __forceinline__ uint32_t lds_ub(const uint32_t *a, uint32_t n, uint32_t v)   // first index with a[i] > v
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (a[m] <= v) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+struct MlOut {
+    uint64_t *s_key;
+    uint32_t *s_val;
+    int32_t *s_k2v;
+    uint64_t *cnt_k, *cnt_v, *cnt_o;
+    uint64_t *errs;
+};
+
+// LDS plan of k_m_lds (dynamic shared memory, sized by the largest group of the launch)
+struct MlPlan {
+    uint32_t kc, vc, oc;      // max key / TxnId / keysToTxnIds slots of a group
+    uint32_t sp;              // sort area, u32 units: max(2 * pow2(kc), pow2(vc), pow2(oc - keys))
+    uint32_t bytes;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
+                                                 const uint64_t *__restrict__ key_code, const uint64_t *__restrict__ val_off,
+                                                 const uint32_t *__restrict__ txn_rank, const uint64_t *__restrict__ k2v_off,
+                                                 const int32_t *__restrict__ k2v, MlPlan pl, MlOut o)
+{
+    extern __shared__ uint64_t dsm[];
+    // [rawk: kc u64][sort: sp u32][rawv: vc u32][rawo: oc u32][hdr: kc u32]
+    uint64_t *rawk = dsm;
+    uint32_t *sort32 = reinterpret_cast<uint32_t *>(dsm + pl.kc);
+    uint64_t *sort64 = reinterpret_cast<uint64_t *>(sort32);
+    uint32_t *rawv = sort32 + pl.sp;
+    uint32_t *rawo = rawv + pl.vc;
+    uint32_t *hdr = rawo + pl.oc;
+    __shared__ uint32_t rk[ML_REP + 1], rv[ML_REP + 1], ro[ML_REP + 1];
+    __shared__ uint32_t scan_lds[WAVES];
+    const uint32_t gi = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t R0 = grp_off[gi];
+    const uint32_t nrep = (uint32_t)(grp_off[gi + 1] - R0);
+    const uint64_t KA = key_off[R0], VA = val_off[R0], OA = k2v_off[R0];
+    for (uint32_t r = tid; r <= nrep; r += BLOCK) {
+        rk[r] = (uint32_t)(key_off[R0 + r] - KA);
+        rv[r] = (uint32_t)(val_off[R0 + r] - VA);
+        ro[r] = (uint32_t)(k2v_off[R0 + r] - OA);
+    }
+    __syncthreads();
+    const uint32_t NK = rk[nrep], NV = rv[nrep], NO = ro[nrep], NE = NO - NK;
+    // one coalesced pass over the group's three input ranges
+    for (uint32_t i = tid; i < NK; i += BLOCK) rawk[i] = key_code[KA + i];
+    for (uint32_t i = tid; i < NV; i += BLOCK) rawv[i] = txn_rank[VA + i];
+    for (uint32_t i = tid; i < NO; i += BLOCK) rawo[i] = (uint32_t)k2v[OA + i];
+    __syncthreads();
+    uint64_t err = 0;
+    const uint64_t PADK = ~0ull;
+    const uint32_t PAD32 = 0xFFFFFFFFu;
+    // ---- keys: sort, unique, write, map every key slot to its merged index
+    const uint32_t NKP = pow2_at_least(NK);
+    for (uint32_t i = tid; i < NKP; i += BLOCK) {
+        uint64_t x = PADK;
+        if (i < NK) {
+            const uint32_t r = lds_ub(rk, nrep + 1, i) - 1;
+            if (i > rk[r] && rawk[i - 1] >= rawk[i]) err |= 2;   // Keys sorted unique
+            if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawk[i];
+        }
+        sort64[i] = x;
+    }
+    __syncthreads();
+    lds_bitonic(sort64, NKP);
+    const uint32_t Kg = lds_unique<uint64_t, ML_KC / BLOCK>(sort64, NKP, PADK, scan_lds);
+    uint32_t kmap[ML_KC / BLOCK];
+#pragma unroll
+    for (int q = 0; q < ML_KC / BLOCK; ++q) {
+        const uint32_t i = tid + q * BLOCK;
+        if (i < Kg) o.s_key[KA + i] = sort64[i];
+        if (i < NK) {
+            const uint64_t kc = rawk[i];
+            uint32_t a = 0, b = Kg;
+            while (a < b) { uint32_t m = (a + b) >> 1; if (sort64[m] < kc) a = m + 1; else b = m; }
+            kmap[q] = a;
+        }
+    }
+    __syncthreads();
+    uint32_t *kidx = reinterpret_cast<uint32_t *>(rawk);   // key slot -> merged key index
+#pragma unroll
+    for (int q = 0; q < ML_KC / BLOCK; ++q) {
+        const uint32_t i = tid + q * BLOCK;
+        if (i < NK) kidx[i] = kmap[q];
+    }
+    // ---- TxnIds: same
+    const uint32_t NVP = pow2_at_least(NV);
+    for (uint32_t i = tid; i < NVP; i += BLOCK) {
+        uint32_t x = PAD32;
+        if (i < NV) {
+            const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
+            if (i > rv[r] && rawv[i - 1] >= rawv[i]) err |= 4;   // txnIds sorted unique
+            if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawv[i];
+        }
+        sort32[i] = x;
+    }
+    __syncthreads();
+    lds_bitonic(sort32, NVP);
+    const uint32_t Ug = lds_unique<uint32_t, ML_VC / BLOCK>(sort32, NVP, PAD32, scan_lds);
+    for (uint32_t i = tid; i < NV; i += BLOCK) {
+        const uint32_t v = rawv[i];
+        uint32_t a = 0, b = Ug;
+        while (a < b) { uint32_t m = (a + b) >> 1; if (sort32[m] < v) a = m + 1; else b = m; }
+        rawv[i] = a;   // each thread rewrites only its own slots
+    }
+    for (uint32_t u = tid; u < Ug; u += BLOCK) o.s_val[VA + u] = sort32[u];
+    __syncthreads();
+    // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
+    const uint32_t NEP = pow2_at_least(NE);
+    for (uint32_t e = tid + NE; e < NEP; e += BLOCK) sort32[e] = PAD32;
+    for (uint32_t q = tid; q < NO; q += BLOCK) {
+        const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
+        const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
+        const uint32_t qq = q - ro[r];
+        const uint32_t *h = rawo + ro[r];
+        if (nk == 0) { err |= 8; continue; }   // keysToTxnIds entries without keys
+        if (qq < nk) {
+            const uint32_t e = h[qq], prev = qq == 0 ? nk : h[qq - 1];
+            if (e < prev || e > no || (qq + 1 == nk && e != no)) err |= 8;
+            continue;
+        }
+        uint32_t lo = 0, hi = nk;   // key slot: number of headers <= qq
+        while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] <= qq) lo = m + 1; else hi = m; }
+        const uint32_t i = lo < nk ? lo : nk - 1;
+        const uint32_t start = i == 0 ? nk : h[i - 1];
+        const int32_t xv = (int32_t)h[qq];
+        uint32_t x = PAD32;
+        if (xv < 0 || (uint32_t)xv >= nv) err |= 16;
+        else {
+            if (qq > start && (int32_t)h[qq - 1] >= xv) err |= 32;
+            if (no != nk) x = (kidx[rk[r] + i] << 16) | rawv[rv[r] + (uint32_t)xv];
+        }
+        sort32[q - rk[r + 1]] = x;
+    }
+    for (uint32_t k = tid; k < Kg; k += BLOCK) hdr[k] = 0;
+    __syncthreads();
+    lds_bitonic(sort32, NEP);
+    const uint32_t Eu = lds_unique<uint32_t, ML_VC / BLOCK>(sort32, NEP, PAD32, scan_lds);
+    for (uint32_t c = tid; c < Eu; c += BLOCK) {
+        const uint32_t kk = sort32[c] >> 16;
+        if (c + 1 == Eu || (sort32[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
+        o.s_k2v[OA + Kg + c] = (int32_t)(sort32[c] & 0xFFFFu);
+    }
+    __syncthreads();
+    // keys without entries: end offset = the previous key's (prefix max, starting at Kg)
+    {
+        const uint32_t per = (Kg + BLOCK - 1) / BLOCK, base = tid * per;
+        uint32_t m = 0;
+        for (uint32_t q = 0; q < per && base + q < Kg; ++q) m = max(m, hdr[base + q]);
+        uint32_t total;
+        uint32_t run = block_exclusive(m, OpMax<uint32_t>(), scan_lds, total);
+        run = max(run, Kg);
+        for (uint32_t q = 0; q < per && base + q < Kg; ++q) {
+            run = max(run, hdr[base + q]);
+            o.s_k2v[OA + base + q] = (int32_t)run;
+        }
+    }
+    if (tid == 0) {
+        o.cnt_k[gi] = Kg;
+        o.cnt_v[gi] = Ug;
+        o.cnt_o[gi] = Kg + Eu;
+    }
+    block_or1(err, o.errs);
+}
+
+// scratch (at input offsets) -> final CSR: one wave per group
+__global__ __launch_bounds__(BLOCK) void k_m_lds_compact(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
+                                                         const uint64_t *__restrict__ val_off, const uint64_t *__restrict__ k2v_off,
+                                                         MlOut o, const uint64_t *__restrict__ ko, const uint64_t *__restrict__ vo,
+                                                         const uint64_t *__restrict__ oo, uint64_t *__restrict__ out_key,
+                                                         uint32_t *__restrict__ out_val, int32_t *__restrict__ out_k2v)
+{
+    const uint32_t gi = (blockIdx.x * BLOCK + threadIdx.x) >> 6, lane = lane_id();
+    if (gi >= ng) return;
+    const uint64_t R0 = grp_off[gi];
+    const uint64_t KA = key_off[R0], VA = val_off[R0], OA = k2v_off[R0];
+    const uint64_t nk = ko[gi + 1] - ko[gi], nv = vo[gi + 1] - vo[gi], no = oo[gi + 1] - oo[gi];
+    for (uint64_t i = lane; i < nk; i += 64) out_key[ko[gi] + i] = o.s_key[KA + i];
+    for (uint64_t i = lane; i < nv; i += 64) out_val[vo[gi] + i] = o.s_val[VA + i];
+    for (uint64_t i = lane; i < no; i += 64) out_k2v[oo[gi] + i] = o.s_k2v[OA + i];
+}
+
+static void merge_checks(uint64_t err)
+{
+    if (err & 1) fail(ACC_E_ARG, "merge offsets must be non-decreasing and k2v hold a header per key");
+    if (err & 2) fail(ACC_E_ARG, "Keys of a KeyDeps must be sorted and unique");
+    if (err & 4) fail(ACC_E_ARG, "txnIds of a KeyDeps must be sorted and unique");
+    if (err & 8) fail(ACC_E_ARG, "Last key in keyToTxnId does not point to the end of the array");
+    if (err & 16) fail(ACC_E_ARG, "keyToTxnId entry out of range of txnIds");
+    if (err & 32) fail(ACC_E_STATE, "Duplicate value found for key (RelationMultiMap.checkValid)");
+}
+
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
 {
     if (!in || !view) fail(ACC_E_ARG, "null argument");
@@ -272,21 +561,71 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
     const uint32_t *txn_rank = stage_in(ctx, "m_txn_rank", in->txn_rank, NV, in->mem);
     const int32_t *k2v = stage_in(ctx, "m_k2v", in->k2v, NO, in->mem);
 
-    uint32_t *grp_of = ctx->get<uint32_t>("m_grp_of", R);
     uint64_t *g = ctx->get<uint64_t>("m_g", 4);
     ACC_HIP(hipMemsetAsync(g, 0, 4 * 8, st));
+    if (ng && !(ctx->flags & ACC_OPT_FORCE_REPLAY)) {
+        // ---- LDS tier when every group fits
+        uint64_t *gmax = ctx->get<uint64_t>("m_gmax", 4);
+        ACC_HIP(hipMemsetAsync(gmax, 0, 4 * 8, st));
+        launch(ctx, "m_fit", k_m_fit, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, grp_off, key_off, val_off, k2v_off, g, gmax);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, g + 3, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gmax, 4 * 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        if (ctx->pinned[0] == 0) {
+            auto p2 = [](uint64_t n) { uint64_t p = BLOCK; while (p < n) p <<= 1; return p; };
+            MlPlan pl;
+            pl.kc = (uint32_t)ctx->pinned[1];
+            pl.vc = (uint32_t)ctx->pinned[2];
+            pl.oc = (uint32_t)ctx->pinned[3];
+            pl.sp = (uint32_t)std::max({ 2 * p2(pl.kc), p2(pl.vc), p2(ctx->pinned[4]) });
+            pl.kc = (pl.kc + 1) & ~1u;   // keep the u32 areas after rawk 8-byte aligned
+            pl.bytes = 8 * pl.kc + 4 * pl.sp + 4 * pl.vc + 4 * pl.oc + 4 * pl.kc;
+            MlOut mo;
+            mo.s_key = ctx->get<uint64_t>("m_s_key", NK + 1);
+            mo.s_val = ctx->get<uint32_t>("m_s_val", NV + 1);
+            mo.s_k2v = ctx->get<int32_t>("m_s_k2v", NO + 1);
+            mo.cnt_k = ctx->get<uint64_t>("m_cnt_k", ng);
+            mo.cnt_v = ctx->get<uint64_t>("m_cnt_v", ng);
+            mo.cnt_o = ctx->get<uint64_t>("m_cnt_o", ng);
+            mo.errs = g + 2;
+            launch(ctx, "m_lds", k_m_lds, dim3(ng), dim3(BLOCK), pl.bytes, ng, grp_off, key_off, key_code, val_off, txn_rank,
+                   k2v_off, k2v, pl, mo);
+            uint64_t *ko = ctx->get<uint64_t>("m_k_gstart", (size_t)ng + 1);
+            uint64_t *vo = ctx->get<uint64_t>("m_v_gstart", (size_t)ng + 1);
+            uint64_t *oo = ctx->get<uint64_t>("m_out_k2v_off", (size_t)ng + 1);
+            scan<uint64_t, OpAdd<uint64_t>>(ctx, mo.cnt_k, ko, ng, true, ko + ng);
+            scan<uint64_t, OpAdd<uint64_t>>(ctx, mo.cnt_v, vo, ng, true, vo + ng);
+            scan<uint64_t, OpAdd<uint64_t>>(ctx, mo.cnt_o, oo, ng, true, oo + ng);
+            ACC_HIP(hipMemcpyAsync(ctx->pinned, g + 2, 8, hipMemcpyDeviceToHost, st));
+            ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, ko + ng, 8, hipMemcpyDeviceToHost, st));
+            ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, vo + ng, 8, hipMemcpyDeviceToHost, st));
+            ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, oo + ng, 8, hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            merge_checks(ctx->pinned[0]);
+            const uint64_t TK = ctx->pinned[1], TV = ctx->pinned[2], TO = ctx->pinned[3];
+            uint64_t *out_key = ctx->get<uint64_t>("m_out_key", TK + 1);
+            uint32_t *out_val = ctx->get<uint32_t>("m_out_val", TV + 1);
+            int32_t *out_k2v = ctx->get<int32_t>("m_out_k2v", TO + 1);
+            launch(ctx, "m_lds_compact", k_m_lds_compact, dim3(grid_for((size_t)ng * 64, BLOCK)), dim3(BLOCK), 0, ng, grp_off,
+                   key_off, val_off, k2v_off, mo, (const uint64_t *)ko, (const uint64_t *)vo, (const uint64_t *)oo, out_key,
+                   out_val, out_k2v);
+            ctx->sync();
+            ctx->stat("merge.lds_tier", 1);
+            *view = acc_merge_view{ ng, TK, TV, TO, NO, ko, out_key, vo, out_val, oo, out_k2v };
+            ctx->merge_view = *view;
+            ctx->merge_valid = true;
+            return;
+        }
+    }
+    ctx->stat("merge.lds_tier", 0);
+    uint32_t *grp_of = ctx->get<uint32_t>("m_grp_of", R);
     launch(ctx, "m_replies", k_m_replies, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, grp_off, grp_of);
     launch(ctx, "m_prep", k_m_prep, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, key_off, key_code, val_off, txn_rank,
            k2v_off, k2v, g);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 3 * 8, hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t kmask = ctx->pinned[0], vmask = ctx->pinned[1], err = ctx->pinned[2];
-    if (err & 1) fail(ACC_E_ARG, "merge offsets must be non-decreasing and k2v hold a header per key");
-    if (err & 2) fail(ACC_E_ARG, "Keys of a KeyDeps must be sorted and unique");
-    if (err & 4) fail(ACC_E_ARG, "txnIds of a KeyDeps must be sorted and unique");
-    if (err & 8) fail(ACC_E_ARG, "Last key in keyToTxnId does not point to the end of the array");
-    if (err & 16) fail(ACC_E_ARG, "keyToTxnId entry out of range of txnIds");
-    if (err & 32) fail(ACC_E_STATE, "Duplicate value found for key (RelationMultiMap.checkValid)");
+    merge_checks(err);
 
     MergePlan plan;
     plan.rk = make_runs(kmask);

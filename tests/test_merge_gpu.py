@@ -75,3 +75,39 @@ def test_merge_config5_shape(ctx):
     ref = oracle.keydeps_merge(m)
     for k in ref:
         np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+
+
+def test_merge_lds_tier_vs_global_path(ctx):
+    """The LDS tier (every group fits) and the global sort path (forced) give identical arrays; a group beyond the
+    LDS caps sends the batch to the global path."""
+    import oracle
+    from accord_amd import workload as W
+    from accord_amd.deps import Context, keydeps_merge
+    m = W.merge_batch(n_txn=3000, replies=64, seed=0xACC00016, n_keys=5000)
+    a = keydeps_merge(ctx, m)
+    assert ctx.stats()["merge.lds_tier"] == 1
+    with Context(0, force_replay=True) as c2:
+        b = keydeps_merge(c2, m)
+        assert c2.stats()["merge.lds_tier"] == 0
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(a[k], ref[k], err_msg=k)
+        np.testing.assert_array_equal(b[k], ref[k], err_msg=k)
+    rng = np.random.RandomState(7)
+    groups = [[gen_keydeps(rng) for _ in range(300)]] + [[gen_keydeps(rng) for _ in range(5)] for _ in range(10)]
+    out = keydeps_merge(ctx, pack_groups(groups))
+    assert ctx.stats()["merge.lds_tier"] == 0
+    check_groups(out, groups)
+
+
+@pytest.mark.parametrize("force_global", [False, True])
+def test_merge_errors_both_paths(force_global):
+    from accord_amd.deps import Context, IllegalArgumentException, IllegalStateException, keydeps_merge
+    with Context(0, force_replay=force_global) as c:
+        for bad, exc in ((([9, 5], [3], [3, 4, 0, 0]), IllegalArgumentException),     # keys not sorted
+                         (([5, 9], [7, 3], [3, 4, 0, 1]), IllegalArgumentException),   # txnIds not sorted
+                         (([5, 9], [3], [3, 4, 0, 1]), IllegalArgumentException),      # entry out of range
+                         (([5], [3, 7], [3, 1, 1]), IllegalStateException),            # duplicate value per key
+                         (([5, 9], [3], [2, 2, 0]), IllegalArgumentException)):        # last offset != length
+            with pytest.raises(exc):
+                keydeps_merge(c, pack_groups([[gen_keydeps(np.random.RandomState(1))], [bad]]))
