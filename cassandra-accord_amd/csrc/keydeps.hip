@@ -939,6 +939,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
 // the runs are gathered flattened by all lanes, T itself and non-qualifying R3 entries are dropped.
 
 constexpr int NRUN = 7;
+constexpr int TINY_E = 16, TINY_K = 16;
 constexpr int SMALL_E = 64, SMALL_K = 32;
 constexpr int MED_E = 1024, MED_K = 64;
 constexpr int BIG_K = 64;
@@ -1144,10 +1145,11 @@ __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t pre
 __global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
                                                     const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
                                                     uint64_t *__restrict__ a_cnt, uint32_t *__restrict__ med_list,
-                                                    uint32_t *__restrict__ big_list, uint64_t *__restrict__ gstat)
+                                                    uint32_t *__restrict__ big_list, uint32_t *__restrict__ small_list,
+                                                    uint64_t *__restrict__ gstat)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool med = false, big = false;
+    bool med = false, big = false, sml = false;
     if (t < n) {
         uint32_t j0 = key_off[t], j1 = key_off[t + 1];
         uint64_t kd = cnz[j1] - cnz[j0];
@@ -1155,35 +1157,147 @@ __global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *
         kd_cnt[t] = kd;
         a_cnt[t] = kd + E;
         uint32_t nk = j1 - j0;
+        bool tiny = E <= TINY_E && nk <= TINY_K;
         bool small = E <= SMALL_E && nk <= SMALL_K;
+        sml = small && !tiny;
         med = !small && E <= MED_E && nk <= MED_K;
         big = !small && !med && E > 0;
     }
-    // wave-aggregated appends (list order is irrelevant: every txn writes only its own outputs)
-    const uint64_t lt = lane_id() == 0 ? 0ull : (~0ull >> (64 - lane_id()));
-    uint64_t bm = __ballot(med), bb = __ballot(big);
-    uint32_t basem = 0, baseb = 0;
-    if (lane_id() == 0) {
-        if (bm) basem = (uint32_t)atomicAdd((unsigned long long *)&gstat[0], (unsigned long long)__popcll(bm));
-        if (bb) baseb = (uint32_t)atomicAdd((unsigned long long *)&gstat[1], (unsigned long long)__popcll(bb));
+    // block-aggregated appends: one atomic per list per block (list order is irrelevant: every txn writes only its
+    // own outputs)
+    __shared__ uint32_t lds[WAVES];
+    __shared__ uint32_t base[3];
+    const uint32_t packed = (med ? 1u : 0u) | (big ? 1u << 10 : 0u) | (sml ? 1u << 20 : 0u);   // <= 256 per field
+    uint32_t total;
+    const uint32_t pre = block_exclusive(packed, OpAdd<uint32_t>(), lds, total);
+    if (threadIdx.x == 0) {
+        const uint32_t cm = total & 1023u, cb = (total >> 10) & 1023u, cs = total >> 20;
+        base[0] = cm ? (uint32_t)atomicAdd((unsigned long long *)&gstat[0], (unsigned long long)cm) : 0u;
+        base[1] = cb ? (uint32_t)atomicAdd((unsigned long long *)&gstat[1], (unsigned long long)cb) : 0u;
+        base[2] = cs ? (uint32_t)atomicAdd((unsigned long long *)&gstat[5], (unsigned long long)cs) : 0u;
     }
-    basem = shfl_idx(basem, 0);
-    baseb = shfl_idx(baseb, 0);
-    if (med) med_list[basem + __popcll(bm & lt)] = t;
-    if (big) big_list[baseb + __popcll(bb & lt)] = t;
+    __syncthreads();
+    if (med) med_list[base[0] + (pre & 1023u)] = t;
+    if (big) big_list[base[1] + ((pre >> 10) & 1023u)] = t;
+    if (sml) small_list[base[2] + (pre >> 20)] = t;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_write_small(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+// Tiny tier (E <= 16 entries, <= 16 keys; most txns of a CommandsForKey snapshot): four txns per wave, one 16-lane
+// group each. Same steps as the small tier (runs from the count-pass records, flattened gather, register bitonic,
+// emit) on group-masked ballots and 16-lane shuffles. Also writes u_cnt = 0 for txns without deps.
+__global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ RunsT<TINY_K> sruns[BLOCK / 16];
+    __shared__ uint64_t sbuf[BLOCK / 16][TINY_E];
+    const uint32_t lane = lane_id(), sub = lane & 15u, grp = threadIdx.x >> 4, g0 = lane & 48u;
+    const uint64_t gmask = 0xFFFFull << g0;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t t = blockIdx.x * (BLOCK / 16) + grp;
+    bool act = t < n;
+    TxnCtx c{};
+    if (act) {
+        const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
+        const uint64_t E64 = o.dep_off[j1] - o.dep_off[j0];
+        if (E64 == 0) { if (sub == 0) o.u_cnt[t] = 0; act = false; }
+        else if (E64 > TINY_E || j1 - j0 > TINY_K) act = false;
+    }
+    if (act) c = txn_ctx(v, o, t);
+    RunsT<TINY_K> &R = sruns[grp];
+    uint64_t *buf = sbuf[grp];
+    uint32_t ktot = 0;
+    if (act && sub < c.nk) {
+        if (cnt[c.j0 + sub] != 0) {
+            const uint4 *r = o.rec + 4 * (size_t)(c.j0 + sub);
+            const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+            const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
+            const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
+            uint32_t acc = 0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) { R.start[sub][q] = a[q]; R.pre[sub][q] = acc; acc += l[q]; }
+            R.start[sub][6] = r3.x; R.pre[sub][6] = acc; acc += r3.y;
+            R.pre[sub][7] = acc;
+            R.m[sub] = r3.z;
+            ktot = acc;
+        } else {
+            for (int q = 0; q <= NRUN; ++q) R.pre[sub][q] = 0;
+            R.m[sub] = NO_M;
+        }
+    }
+    uint32_t incl = ktot;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (sub >= d) incl += u;
+    }
+    if (act && sub < c.nk) R.kbase[sub] = incl - ktot;
+    const uint32_t total = __shfl(incl, (int)(g0 + 15), 64);
+    if (act && sub == 0) R.kbase[c.nk] = total;
+    uint32_t maxtot = act ? total : 0;
+#pragma unroll
+    for (int d = 16; d < 64; d <<= 1) maxtot = max(maxtot, (uint32_t)__shfl_xor(maxtot, d, 64));
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    uint32_t cursor = 0;
+    for (uint32_t c0 = 0; c0 < maxtot; c0 += 16) {
+        const uint32_t e = c0 + sub;
+        bool keep = false;
+        uint32_t x = 0, k = 0;
+        if (act && e < total) keep = fetch_elem(R, v, c, e, x, k);
+        const uint64_t bal = __ballot(keep) & gmask;
+        if (keep) {
+            const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+            if (slot < TINY_E) buf[slot] = ((uint64_t)x << 16) | k;
+        }
+        cursor += (uint32_t)__popcll(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (act && cursor != c.E) {
+        if (sub == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
+        act = false;
+    }
+    const bool in = act && sub < c.E;
+    uint64_t x = in ? buf[sub] : ~0ull;
+#pragma unroll
+    for (uint32_t k = 2; k <= 16; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint64_t y = shfl_xor64(x, (int)jj);
+            const bool up = (sub & k) == 0, lower = (sub & jj) == 0;
+            const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+            x = (lower == up) ? lo : hi;
+        }
+    }
+    const uint64_t prev = shfl_up(x, 1);
+    const uint32_t val = (uint32_t)(x >> 16), kj = (uint32_t)(x & 0xFFFFu);
+    const bool nw = in && (sub == 0 || (uint32_t)(prev >> 16) != val);
+    const uint64_t bal = __ballot(nw) & gmask;
+    const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+    uint64_t peers = __ballot(in) & gmask;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint64_t bb = __ballot((kj >> b) & 1u);
+        peers &= ((kj >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t before = (uint32_t)__popcll(peers & lt);
+    if (in) {
+        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+        const uint64_t kbase = o.dep_off[c.j0 + kj] - c.e0;
+        o.arena[abase + kbase + before] = (int32_t)idx;
+        if (nw) o.dep_scratch[c.e0 + idx] = o.txn_of_rank[val];
+    }
+    if (act && sub == 0) o.u_cnt[t] = (uint32_t)__popcll(bal);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_write_small(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
+                                                          const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ uint64_t sbuf[WAVES][SMALL_E];
     __shared__ RunsT<SMALL_K> sruns[WAVES];
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t t = blockIdx.x * WAVES + wave;
-    if (t >= n) return;
-    const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
-    const uint64_t E64 = o.dep_off[j1] - o.dep_off[j0];
-    if (E64 == 0) { if (lane == 0) o.u_cnt[t] = 0; return; }
-    if (E64 > SMALL_E || j1 - j0 > SMALL_K) return;
+    const uint32_t i = blockIdx.x * WAVES + wave;
+    if (i >= cnt_list) return;
+    const uint32_t t = list[i];
     TxnCtx c = txn_ctx(v, o, t);
     RunsT<SMALL_K> &R = sruns[wave];
     uint64_t *buf = sbuf[wave];
@@ -1925,19 +2039,21 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *med_list = ctx->get<uint32_t>("v2_med_list", n);
     uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", n);
     uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", n);
+    uint32_t *small_list = ctx->get<uint32_t>("v2_small_list", n);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 8);
     ACC_HIP(hipMemsetAsync(gstat, 0, 8 * sizeof(uint64_t), st));
     launch(ctx, "v2_sizes", k_v2_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
-           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, gstat);
+           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, small_list, gstat);
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, kd_off, n, true, kd_off + n);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, arena_off, n, true, arena_off + n);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, dep_off + P, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gstat, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, gstat + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
-    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2];
+    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2], nsmall = ctx->pinned[3];
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
 
     // ---- write pass (three tiers)
@@ -1949,8 +2065,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
     wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
-    launch(ctx, "v2_write_small", k_v2_write_small, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, vv,
+    launch(ctx, "v2_write_tiny", k_v2_write_tiny, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, vv,
            (const uint64_t *)cnt, wo);
+    if (nsmall)
+        launch(ctx, "v2_write_small", k_v2_write_small, dim3((unsigned)((nsmall + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+               (uint32_t)nsmall, (const uint32_t *)small_list, vv, (const uint64_t *)cnt, wo);
     if (nmed)
         launch(ctx, "v2_write_medium", k_v2_write_medium, dim3((unsigned)((nmed + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
                (uint32_t)nmed, (const uint32_t *)med_list, vv, (const uint64_t *)cnt, wo);
@@ -1964,6 +2083,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ctx->sync();
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
     const uint64_t nfb = ctx->pinned[3], efb = ctx->pinned[4];
+    ctx->stat("keydeps.small_txns", nsmall);
     ctx->stat("keydeps.medium_txns", nmed);
     ctx->stat("keydeps.big_txns", nbig);
     ctx->stat("keydeps.fallback_txns", nfb);
