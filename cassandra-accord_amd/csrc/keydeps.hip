@@ -943,7 +943,8 @@ constexpr int TINY_E = 16, TINY_K = 16;
 constexpr int SMALL_E = 64, SMALL_K = 32;
 constexpr int MED_E = 1024, MED_K = 64;
 constexpr int BIG_K = 64;
-constexpr int BIG_E = 8192;                 // entries per block in LDS (64 KiB)
+constexpr int BIG_E = 8192;                 // raw entries per block in LDS (32 KiB of u32 records)
+constexpr int HUGE_E = 32768;               // second big launch (128 KiB)
 
 struct V2Out {
     const uint32_t *key_off;
@@ -953,8 +954,9 @@ struct V2Out {
     int32_t *arena;
     uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
     uint64_t *u_cnt;
-    uint32_t *med_list, *big_list, *fb_list;
-    uint64_t *gstat;         // [0] medium, [1] big, [2] count mismatches, [3] fallback txns, [4] fallback entries
+    uint32_t *med_list, *big_list, *fb_list, *huge_list;
+    uint64_t *gstat;         // [0] medium, [1] big, [2] count mismatches, [3] fallback txns, [4] fallback entries,
+                             // [5] small, [6] huge (second big launch)
 };
 
 template <int MAXK>
@@ -1364,46 +1366,70 @@ __device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, u
 // quarter of the sorted entries with per-key / distinct-value bases from a per-wave count pass.
 constexpr int BIG_GU = 4;   // independent loads in flight per thread during the gather
 
-__global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
+__global__ __launch_bounds__(BLOCK) void k_v2_route_fb(uint32_t nbig, const uint32_t *__restrict__ big_list,
+                                                       const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
+                                                       uint32_t *__restrict__ fb_list, uint64_t *__restrict__ gstat)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nbig) return;
+    const uint32_t t = big_list[i];
+    fb_list[atomicAdd((unsigned long long *)&gstat[3], 1ull)] = t;
+    atomicAdd((unsigned long long *)&gstat[4], (unsigned long long)(dep_off[key_off[t + 1]] - dep_off[key_off[t]]));
+}
+
+// Sort records are u32 (TxnId rank << 6 | key index): half the LDS of u64 records, twice the blocks per CU. The
+// host takes this tier only when ranks fit 25 bits (2N <= 2^25). CAP = raw run elements per block: 8192 (32 KiB,
+// routed by k_v2_sizes) or 32768 (128 KiB, txns the first launch passes on via gstat[6] / huge_list); beyond that
+// the global path.
+template <int CAP, int NT>
+__global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
                                                         const uint64_t *__restrict__ cnt, V2Out o)
 {
-    __shared__ uint64_t buf[BIG_E];
+    __shared__ uint32_t buf[CAP];
     __shared__ RunsT<BIG_K> R;
     __shared__ uint32_t s_kept;
-    __shared__ uint32_t wk_cnt[WAVES][BIG_K];
-    __shared__ uint32_t wdist[WAVES];
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t wk_cnt[NW][BIG_K];
+    __shared__ uint32_t wdist[NW];
     const uint32_t b = blockIdx.x;
+    if (CAP > BIG_E) cnt_list = (uint32_t)o.gstat[6];   // second launch: the count written by the first
     if (b >= cnt_list) return;
     const uint32_t t = list[b];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     TxnCtx c = txn_ctx(v, o, t);
-    bool oversize = c.nk > BIG_K || c.E > BIG_E;
+    bool oversize = c.nk > BIG_K || c.E > CAP;
     if (!oversize) {
         if (tid < 64) compute_runs(R, v, o, cnt, c);
-        if (tid < BIG_K) { wk_cnt[0][tid] = 0; wk_cnt[1][tid] = 0; wk_cnt[2][tid] = 0; wk_cnt[3][tid] = 0; }
+        if (tid < BIG_K)
+            for (int w = 0; w < NW; ++w) wk_cnt[w][tid] = 0;
         if (tid == 0) s_kept = 0;
         __syncthreads();
-        oversize = R.total > BIG_E;
+        oversize = R.total > CAP;
     }
     if (oversize) {
         if (tid == 0) {
-            uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[3], 1ull);
-            atomicAdd((unsigned long long *)&o.gstat[4], (unsigned long long)c.E);
-            o.fb_list[f] = t;
+            if (CAP == BIG_E && c.nk <= BIG_K) {
+                uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[6], 1ull);
+                o.huge_list[f] = t;
+            } else {
+                uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[3], 1ull);
+                atomicAdd((unsigned long long *)&o.gstat[4], (unsigned long long)c.E);
+                o.fb_list[f] = t;
+            }
         }
         return;
     }
     const uint32_t total = R.total;
     uint32_t n2 = 128;
     while (n2 < total) n2 <<= 1;
-    // ---- gather: raw element e -> buf[e] (sentinel when dropped)
+    // ---- gather: raw element e -> buf[e] (all-ones sentinel when dropped)
     uint32_t kept = 0;
-    for (uint32_t e0 = tid; e0 < n2; e0 += BIG_GU * BLOCK) {
+    for (uint32_t e0 = tid; e0 < n2; e0 += BIG_GU * NT) {
         uint32_t idx[BIG_GU], kk[BIG_GU], x[BIG_GU];
         bool r3[BIG_GU], in[BIG_GU];
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u) {
-            const uint32_t e = e0 + u * BLOCK;
+            const uint32_t e = e0 + u * NT;
             in[u] = e < total;
             idx[u] = 0; kk[u] = 0; r3[u] = false;
             if (in[u]) locate_elem(R, c.nk, e, idx[u], kk[u], r3[u]);
@@ -1412,11 +1438,11 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const
         for (int u = 0; u < BIG_GU; ++u) x[u] = in[u] ? (r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u) {
-            const uint32_t e = e0 + u * BLOCK;
+            const uint32_t e = e0 + u * NT;
             bool keep = in[u] && !(c.bq && x[u] == c.trank);
             if (keep && r3[u]) keep = v.bc_exec[idx[u]] >= R.m[kk[u]] && ((c.wk >> v.bc_kind[idx[u]]) & 1u);
             kept += keep;
-            if (e < n2) buf[e] = keep ? (((uint64_t)x[u] << 16) | kk[u]) : ~0ull;
+            if (e < n2) buf[e] = keep ? ((x[u] << 6) | kk[u]) : 0xFFFFFFFFu;
         }
     }
     kept = wave_inclusive(kept, OpAdd<uint32_t>());
@@ -1429,10 +1455,10 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const
     // ---- bitonic sort over n2 (one compare-exchange per pair index)
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t pi = tid; pi < (n2 >> 1); pi += BLOCK) {
+            for (uint32_t pi = tid; pi < (n2 >> 1); pi += NT) {
                 const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
                 const uint32_t l = i | jj;
-                uint64_t xa = buf[i], ya = buf[l];
+                const uint32_t xa = buf[i], ya = buf[l];
                 const bool up = (i & k) == 0;
                 if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
             }
@@ -1441,38 +1467,37 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_big(uint32_t cnt_list, const
     }
     // ---- emit: wave w owns sorted positions [w*Q, (w+1)*Q), Q a multiple of 64
     const uint32_t E = c.E;
-    const uint32_t Q = ((E + WAVES * 64 - 1) / (WAVES * 64)) * 64;
+    const uint32_t Q = ((E + NW * 64 - 1) / (NW * 64)) * 64;
     const uint32_t q_lo = min(E, wave * Q), q_hi = min(E, q_lo + Q);
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t nd = 0;
     for (uint32_t q0 = q_lo; q0 < q_hi; q0 += 64) {
         const uint32_t q = q0 + lane;
         const bool in = q < q_hi;
-        const uint64_t xq = in ? buf[q] : 0;
-        const bool nw = in && (q == 0 || (uint32_t)(buf[q - 1] >> 16) != (uint32_t)(xq >> 16));
+        const uint32_t xq = in ? buf[q] : 0;
+        const bool nw = in && (q == 0 || (buf[q - 1] >> 6) != (xq >> 6));
         nd += (uint32_t)__popcll(__ballot(nw));
-        if (in) atomicAdd(&wk_cnt[wave][(uint32_t)(xq & 0xFFFFu)], 1u);
+        if (in) atomicAdd(&wk_cnt[wave][xq & 63u], 1u);
     }
     if (lane == 0) wdist[wave] = nd;
     __syncthreads();
     if (tid < BIG_K) {   // exclusive prefix over waves, per key
         uint32_t run = 0;
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) { uint32_t x = wk_cnt[w][tid]; wk_cnt[w][tid] = run; run += x; }
+        for (int w = 0; w < NW; ++w) { uint32_t x = wk_cnt[w][tid]; wk_cnt[w][tid] = run; run += x; }
     }
     __syncthreads();
     uint32_t distinct = 0;
     for (int w = 0; w < (int)wave; ++w) distinct += wdist[w];
     const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+    auto widen = [](uint32_t r) { return ((uint64_t)(r >> 6) << 16) | (r & 63u); };
     for (uint32_t q0 = q_lo; q0 < q_hi; q0 += 64) {
         const uint32_t q = q0 + lane;
         const bool in = q < q_hi;
-        const uint64_t xq = in ? buf[q] : 0;
-        const uint64_t prev = (in && q > 0) ? buf[q - 1] : 0;
+        const uint64_t xq = in ? widen(buf[q]) : 0;
+        const uint64_t prev = (in && q > 0) ? widen(buf[q - 1]) : 0;
         distinct = emit_chunk(xq, in, prev, q > 0, distinct, wk_cnt[wave], o, c, abase);
     }
-    if (wave == WAVES - 1 && lane == 0) o.u_cnt[t] = distinct;
-    (void)lt;
+    if (wave == NW - 1 && lane == 0) o.u_cnt[t] = distinct;
 }
 
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
@@ -2065,6 +2090,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
     wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+    wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig + 1);
     launch(ctx, "v2_write_tiny", k_v2_write_tiny, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, vv,
            (const uint64_t *)cnt, wo);
     if (nsmall)
@@ -2073,15 +2099,23 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     if (nmed)
         launch(ctx, "v2_write_medium", k_v2_write_medium, dim3((unsigned)((nmed + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
                (uint32_t)nmed, (const uint32_t *)med_list, vv, (const uint64_t *)cnt, wo);
-    if (nbig)
-        launch(ctx, "v2_write_big", k_v2_write_big, dim3((unsigned)nbig), dim3(BLOCK), 0, (uint32_t)nbig,
+    if (nbig && rbits + 6 <= 31) {
+        launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3((unsigned)nbig), dim3(BLOCK), 0, (uint32_t)nbig,
                (const uint32_t *)big_list, vv, (const uint64_t *)cnt, wo);
+        launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3((unsigned)nbig), dim3(1024), 0, (uint32_t)nbig,
+               (const uint32_t *)wo.huge_list, vv, (const uint64_t *)cnt, wo);
+    } else if (nbig) {
+        // ranks beyond 25 bits: every big txn takes the global path
+        launch(ctx, "v2_route_fb", k_v2_route_fb, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, (uint32_t)nbig,
+               (const uint32_t *)big_list, key_off, (const uint64_t *)dep_off, fb_list, gstat);
+    }
     launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
            key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
            (const uint64_t *)arena_off, key_idx, arena);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+    ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
     const uint64_t nfb = ctx->pinned[3], efb = ctx->pinned[4];
     ctx->stat("keydeps.small_txns", nsmall);
     ctx->stat("keydeps.medium_txns", nmed);

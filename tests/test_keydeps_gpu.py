@@ -133,7 +133,7 @@ def set_kind(b, idx, kind):
     b.exe_msb[idx], b.exe_lsb[idx], b.exe_node[idx] = b.txn_msb[idx], b.txn_lsb[idx], b.txn_node[idx]
 
 
-@pytest.mark.parametrize("hot_every,tail", [(10, 5), (40, 3)])
+@pytest.mark.parametrize("hot_every,tail", [(10, 5), (40, 3), (2, 3)])
 def test_tiers_medium_big_fallback(ctx, hot_every, tail):
     """One hot key of committed Reads closed by a few PREACCEPTED Writes: those Writes depend on every
     earlier entry (E up to ~9000), exercising the block tier (E <= 8192) and the global-sort tier."""
@@ -151,7 +151,9 @@ def test_tiers_medium_big_fallback(ctx, hot_every, tail):
     assert_same(g, o, b.n_txn, "tiers")
     st = ctx.stats()
     if st.get("keydeps.path_replay") == 0 and hot_every == 10:
-        assert st["keydeps.fallback_txns"] > 0
+        assert st["keydeps.huge_txns"] > 0         # E ~9000: the 32768-record block tier
+    if st.get("keydeps.path_replay") == 0 and hot_every == 2:
+        assert st["keydeps.fallback_txns"] > 0     # E ~45000: the global-sort tier
 
 
 def test_path_selection():
