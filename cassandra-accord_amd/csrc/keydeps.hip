@@ -1148,10 +1148,10 @@ __global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *
                                                     const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
                                                     uint64_t *__restrict__ a_cnt, uint32_t *__restrict__ med_list,
                                                     uint32_t *__restrict__ big_list, uint32_t *__restrict__ small_list,
-                                                    uint64_t *__restrict__ gstat)
+                                                    uint32_t *__restrict__ g32_list, uint64_t *__restrict__ gstat)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool med = false, big = false, sml = false;
+    bool med = false, big = false, sml = false, mid = false;
     if (t < n) {
         uint32_t j0 = key_off[t], j1 = key_off[t + 1];
         uint64_t kd = cnz[j1] - cnz[j0];
@@ -1160,51 +1160,60 @@ __global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *
         a_cnt[t] = kd + E;
         uint32_t nk = j1 - j0;
         bool tiny = E <= TINY_E && nk <= TINY_K;
+        bool g32 = !tiny && E <= 32 && nk <= 32;
         bool small = E <= SMALL_E && nk <= SMALL_K;
-        sml = small && !tiny;
+        sml = small && !tiny && !g32;
+        mid = g32;
         med = !small && E <= MED_E && nk <= MED_K;
         big = !small && !med && E > 0;
     }
     // block-aggregated appends: one atomic per list per block (list order is irrelevant: every txn writes only its
     // own outputs)
-    __shared__ uint32_t lds[WAVES];
-    __shared__ uint32_t base[3];
-    const uint32_t packed = (med ? 1u : 0u) | (big ? 1u << 10 : 0u) | (sml ? 1u << 20 : 0u);   // <= 256 per field
-    uint32_t total;
-    const uint32_t pre = block_exclusive(packed, OpAdd<uint32_t>(), lds, total);
-    if (threadIdx.x == 0) {
-        const uint32_t cm = total & 1023u, cb = (total >> 10) & 1023u, cs = total >> 20;
-        base[0] = cm ? (uint32_t)atomicAdd((unsigned long long *)&gstat[0], (unsigned long long)cm) : 0u;
-        base[1] = cb ? (uint32_t)atomicAdd((unsigned long long *)&gstat[1], (unsigned long long)cb) : 0u;
-        base[2] = cs ? (uint32_t)atomicAdd((unsigned long long *)&gstat[5], (unsigned long long)cs) : 0u;
+    __shared__ uint64_t lds[WAVES];
+    __shared__ uint32_t base[4];
+    // 10-bit fields (<= 256 per block): medium, big, small, 32-lane group
+    const uint64_t packed = (med ? 1ull : 0ull) | (big ? 1ull << 10 : 0ull) | (sml ? 1ull << 20 : 0ull) | (mid ? 1ull << 30 : 0ull);
+    uint64_t total;
+    const uint64_t pre = block_exclusive(packed, OpAdd<uint64_t>(), lds, total);
+    if (threadIdx.x < 4) {
+        const int slot[4] = { 0, 1, 5, 7 };
+        const uint32_t cnt = (uint32_t)((total >> (10 * threadIdx.x)) & 1023u);
+        base[threadIdx.x] = cnt ? (uint32_t)atomicAdd((unsigned long long *)&gstat[slot[threadIdx.x]], (unsigned long long)cnt) : 0u;
     }
     __syncthreads();
-    if (med) med_list[base[0] + (pre & 1023u)] = t;
-    if (big) big_list[base[1] + ((pre >> 10) & 1023u)] = t;
-    if (sml) small_list[base[2] + (pre >> 20)] = t;
+    if (med) med_list[base[0] + (uint32_t)(pre & 1023u)] = t;
+    if (big) big_list[base[1] + (uint32_t)((pre >> 10) & 1023u)] = t;
+    if (sml) small_list[base[2] + (uint32_t)((pre >> 20) & 1023u)] = t;
+    if (mid) g32_list[base[3] + (uint32_t)((pre >> 30) & 1023u)] = t;
 }
 
-// Tiny tier (E <= 16 entries, <= 16 keys; most txns of a CommandsForKey snapshot): four txns per wave, one 16-lane
-// group each. Same steps as the small tier (runs from the count-pass records, flattened gather, register bitonic,
-// emit) on group-masked ballots and 16-lane shuffles. Also writes u_cnt = 0 for txns without deps.
-__global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+// Group tiers: G = 16 (E <= 16, <= 16 keys; over every txn, also writes u_cnt = 0 for txns without deps) and G = 32
+// (16 < E <= 32, <= 32 keys; over a routed list): 64 / G txns per wave, one G-lane group each. Same steps as the
+// small tier (runs from the count-pass records, flattened gather, register bitonic, emit) on group-masked ballots and
+// G-lane shuffles.
+template <int G, bool LIST>
+__global__ __launch_bounds__(BLOCK) void k_v2_write_group(uint32_t n, const uint32_t *__restrict__ list, V2View v,
+                                                          const uint64_t *__restrict__ cnt, V2Out o)
 {
-    __shared__ RunsT<TINY_K> sruns[BLOCK / 16];
-    __shared__ uint64_t sbuf[BLOCK / 16][TINY_E];
-    const uint32_t lane = lane_id(), sub = lane & 15u, grp = threadIdx.x >> 4, g0 = lane & 48u;
-    const uint64_t gmask = 0xFFFFull << g0;
+    constexpr int GPB = BLOCK / G;
+    constexpr int KB = G == 16 ? 4 : 5;   // key index bits
+    __shared__ RunsT<G> sruns[GPB];
+    __shared__ uint64_t sbuf[GPB][G];
+    const uint32_t lane = lane_id(), sub = lane & (G - 1), grp = threadIdx.x / G, g0 = lane & (64 - G);
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << g0;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t t = blockIdx.x * (BLOCK / 16) + grp;
-    bool act = t < n;
+    const uint32_t i = blockIdx.x * GPB + grp;
+    bool act = i < n;
+    const uint32_t t = act ? (LIST ? list[i] : i) : 0u;
     TxnCtx c{};
     if (act) {
         const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
         const uint64_t E64 = o.dep_off[j1] - o.dep_off[j0];
         if (E64 == 0) { if (sub == 0) o.u_cnt[t] = 0; act = false; }
-        else if (E64 > TINY_E || j1 - j0 > TINY_K) act = false;
+        else if (E64 > (uint64_t)G || j1 - j0 > (uint32_t)G) act = false;
     }
     if (act) c = txn_ctx(v, o, t);
-    RunsT<TINY_K> &R = sruns[grp];
+    RunsT<G> &R = sruns[grp];
     uint64_t *buf = sbuf[grp];
     uint32_t ktot = 0;
     if (act && sub < c.nk) {
@@ -1227,20 +1236,20 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, c
     }
     uint32_t incl = ktot;
 #pragma unroll
-    for (uint32_t d = 1; d < 16; d <<= 1) {
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
         const uint32_t u = __shfl_up(incl, d, 64);
         if (sub >= d) incl += u;
     }
     if (act && sub < c.nk) R.kbase[sub] = incl - ktot;
-    const uint32_t total = __shfl(incl, (int)(g0 + 15), 64);
+    const uint32_t total = __shfl(incl, (int)(g0 + G - 1), 64);
     if (act && sub == 0) R.kbase[c.nk] = total;
     uint32_t maxtot = act ? total : 0;
 #pragma unroll
-    for (int d = 16; d < 64; d <<= 1) maxtot = max(maxtot, (uint32_t)__shfl_xor(maxtot, d, 64));
+    for (int d = G; d < 64; d <<= 1) maxtot = max(maxtot, (uint32_t)__shfl_xor(maxtot, d, 64));
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     uint32_t cursor = 0;
-    for (uint32_t c0 = 0; c0 < maxtot; c0 += 16) {
+    for (uint32_t c0 = 0; c0 < maxtot; c0 += G) {
         const uint32_t e = c0 + sub;
         bool keep = false;
         uint32_t x = 0, k = 0;
@@ -1248,7 +1257,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, c
         const uint64_t bal = __ballot(keep) & gmask;
         if (keep) {
             const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-            if (slot < TINY_E) buf[slot] = ((uint64_t)x << 16) | k;
+            if (slot < (uint32_t)G) buf[slot] = ((uint64_t)x << 16) | k;
         }
         cursor += (uint32_t)__popcll(bal);
     }
@@ -1261,7 +1270,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, c
     const bool in = act && sub < c.E;
     uint64_t x = in ? buf[sub] : ~0ull;
 #pragma unroll
-    for (uint32_t k = 2; k <= 16; k <<= 1) {
+    for (uint32_t k = 2; k <= (uint32_t)G; k <<= 1) {
 #pragma unroll
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
             const uint64_t y = shfl_xor64(x, (int)jj);
@@ -1277,7 +1286,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_tiny(uint32_t n, V2View v, c
     const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
     uint64_t peers = __ballot(in) & gmask;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < KB; ++b) {
         const uint64_t bb = __ballot((kj >> b) & 1u);
         peers &= ((kj >> b) & 1u) ? bb : ~bb;
     }
@@ -2065,10 +2074,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", n);
     uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", n);
     uint32_t *small_list = ctx->get<uint32_t>("v2_small_list", n);
+    uint32_t *g32_list = ctx->get<uint32_t>("v2_g32_list", n);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 8);
     ACC_HIP(hipMemsetAsync(gstat, 0, 8 * sizeof(uint64_t), st));
     launch(ctx, "v2_sizes", k_v2_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
-           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, small_list, gstat);
+           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, small_list, g32_list, gstat);
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, kd_off, n, true, kd_off + n);
@@ -2076,9 +2086,10 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ACC_HIP(hipMemcpyAsync(ctx->pinned, dep_off + P, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gstat, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, gstat + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, gstat + 7, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
-    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2], nsmall = ctx->pinned[3];
+    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2], nsmall = ctx->pinned[3], ng32 = ctx->pinned[4];
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
 
     // ---- write pass (three tiers)
@@ -2091,8 +2102,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
     wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
     wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig + 1);
-    launch(ctx, "v2_write_tiny", k_v2_write_tiny, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, vv,
-           (const uint64_t *)cnt, wo);
+    launch(ctx, "v2_write_g16", k_v2_write_group<16, false>, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n,
+           (const uint32_t *)nullptr, vv, (const uint64_t *)cnt, wo);
+    if (ng32)
+        launch(ctx, "v2_write_g32", k_v2_write_group<32, true>, dim3((unsigned)((ng32 + BLOCK / 32 - 1) / (BLOCK / 32))),
+               dim3(BLOCK), 0, (uint32_t)ng32, (const uint32_t *)g32_list, vv, (const uint64_t *)cnt, wo);
     if (nsmall)
         launch(ctx, "v2_write_small", k_v2_write_small, dim3((unsigned)((nsmall + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
                (uint32_t)nsmall, (const uint32_t *)small_list, vv, (const uint64_t *)cnt, wo);
@@ -2117,6 +2131,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
     ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
     const uint64_t nfb = ctx->pinned[3], efb = ctx->pinned[4];
+    ctx->stat("keydeps.g32_txns", ng32);
     ctx->stat("keydeps.small_txns", nsmall);
     ctx->stat("keydeps.medium_txns", nmed);
     ctx->stat("keydeps.big_txns", nbig);
