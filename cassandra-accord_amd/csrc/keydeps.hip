@@ -2294,7 +2294,7 @@ struct MxKv {   // the key-txn KeyDeps (keydeps_core's view)
     const uint32_t *key_idx, *dep_txn;
 };
 struct MxV {    // the virtual-query space of the range txns
-    const uint32_t *voff, *vowner, *vseg, *vcnz, *ucum;
+    const uint32_t *voff, *vowner, *vseg, *vcnz, *ucnt;
     const uint64_t *vcnt, *vdep_off, *seg_key;
 };
 struct MxOut {
@@ -2303,6 +2303,120 @@ struct MxOut {
     uint32_t *key_idx, *dep_txn;
     uint64_t *kd_key;
 };
+// per-txn TxnId union of the emitted entries: idx_of_e[e] = index of entry e's TxnId in its txn's union,
+// dep_scr[e0 + i] = batch index of the i-th union TxnId, ucnt[t] = union size
+struct MxU {
+    const uint32_t *deps, *voff;
+    const uint64_t *vdep_off;
+    const uint32_t *txn_of_rank;
+    uint32_t *idx_of_e, *dep_scr, *ucnt;
+};
+
+// per txn: entry count routing: E <= 64 -> wave tier (every txn); 64 < E <= MX_BLK_E -> block list; beyond -> flag
+constexpr uint32_t MX_BLK_E = 4096;
+__global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint32_t *__restrict__ voff, const uint64_t *__restrict__ vdep_off,
+                                                    uint32_t *__restrict__ blk_list, uint64_t *__restrict__ gst)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    bool blk = false, over = false;
+    if (t < n) {
+        const uint64_t E = vdep_off[voff[t + 1]] - vdep_off[voff[t]];
+        blk = E > 64 && E <= MX_BLK_E;
+        over = E > MX_BLK_E;
+    }
+    __shared__ uint32_t lds[WAVES];
+    __shared__ uint32_t base;
+    uint32_t total;
+    const uint32_t pre = block_exclusive(blk ? 1u : 0u, OpAdd<uint32_t>(), lds, total);
+    if (threadIdx.x == 0) base = total ? (uint32_t)atomicAdd((unsigned long long *)&gst[0], (unsigned long long)total) : 0u;
+    __syncthreads();
+    if (blk) blk_list[base + pre] = t;
+    if (over) atomicOr((unsigned long long *)&gst[1], 1ull);
+}
+
+// wave per txn, E <= 64: register bitonic of (rank << 32 | local entry)
+__global__ __launch_bounds__(BLOCK) void k_mx_union_wave(uint32_t n, MxU u)
+{
+    const uint32_t lane = lane_id(), t = blockIdx.x * WAVES + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const uint64_t e0 = u.vdep_off[u.voff[t]], E = u.vdep_off[u.voff[t + 1]] - e0;
+    if (E == 0) { if (lane == 0) u.ucnt[t] = 0; return; }
+    if (E > 64) return;
+    const bool in = lane < E;
+    uint64_t x = in ? (((uint64_t)u.deps[e0 + lane] << 32) | lane) : ~0ull;
+    x = wave_bitonic_reg(x);
+    const uint64_t prev = shfl_up(x, 1);
+    const bool nw = in && (lane == 0 || (prev >> 32) != (x >> 32));
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t bal = __ballot(nw);
+    const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+    if (in) {
+        u.idx_of_e[e0 + (uint32_t)x] = idx;
+        if (nw) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(x >> 32)];
+    }
+    if (lane == 0) u.ucnt[t] = (uint32_t)__popcll(bal);
+}
+
+// block per listed txn, 64 < E <= MX_BLK_E: LDS bitonic
+__global__ __launch_bounds__(BLOCK) void k_mx_union_block(const uint32_t *__restrict__ list, const uint64_t *__restrict__ gst, MxU u)
+{
+    __shared__ uint64_t buf[MX_BLK_E];
+    __shared__ uint32_t lds[WAVES];
+    const uint32_t b = blockIdx.x;
+    if (b >= (uint32_t)gst[0]) return;
+    const uint32_t t = list[b], tid = threadIdx.x;
+    const uint64_t e0 = u.vdep_off[u.voff[t]];
+    const uint32_t E = (uint32_t)(u.vdep_off[u.voff[t + 1]] - e0);
+    uint32_t n2 = 128;
+    while (n2 < E) n2 <<= 1;
+    for (uint32_t i = tid; i < n2; i += BLOCK) buf[i] = i < E ? (((uint64_t)u.deps[e0 + i] << 32) | i) : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1)
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t pi = tid; pi < (n2 >> 1); pi += BLOCK) {
+                const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1)), l = i | jj;
+                const uint64_t xa = buf[i], ya = buf[l];
+                if ((xa > ya) == ((i & k) == 0)) { buf[i] = ya; buf[l] = xa; }
+            }
+            __syncthreads();
+        }
+    // distinct index: chunked scan of the "new value" flags (contiguous chunks per thread)
+    const uint32_t per = (E + BLOCK - 1) / BLOCK, lo = min(E, tid * per), hi = min(E, lo + per);
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i) c += i == 0 || (buf[i] >> 32) != (buf[i - 1] >> 32);
+    uint32_t total;
+    uint32_t run = block_exclusive(c, OpAdd<uint32_t>(), lds, total);
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint64_t x = buf[i];
+        const bool nw = i == 0 || (x >> 32) != (buf[i - 1] >> 32);
+        run += nw;
+        u.idx_of_e[e0 + (uint32_t)x] = run - 1;
+        if (nw) u.dep_scr[e0 + run - 1] = u.txn_of_rank[(uint32_t)(x >> 32)];
+    }
+    if (tid == 0) u.ucnt[t] = total;
+}
+
+// global fallback (some txn beyond MX_BLK_E): from the (txn, rank) sort
+__global__ __launch_bounds__(BLOCK) void k_mx_union_sorted(uint64_t E, const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sperm,
+                                                           const uint32_t *__restrict__ uflag, const uint32_t *__restrict__ ucum,
+                                                           const uint32_t *__restrict__ list_of, const uint32_t *__restrict__ vowner,
+                                                           int rbits, MxU u)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= E) return;
+    const uint32_t e = sperm[i];
+    const uint32_t t = vowner[list_of[e]];
+    const uint64_t e0 = u.vdep_off[u.voff[t]];
+    const uint32_t idx = ucum[i] + uflag[i] - 1 - ucum[e0];
+    u.idx_of_e[e] = idx;
+    if (uflag[i]) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(sk[i] & ((1ull << rbits) - 1))];
+}
+__global__ __launch_bounds__(BLOCK) void k_mx_ucnt_sorted(uint32_t n, const uint32_t *__restrict__ voff, const uint64_t *__restrict__ vdep_off,
+                                                          const uint32_t *__restrict__ ucum, uint32_t *__restrict__ ucnt)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) ucnt[t] = ucum[vdep_off[voff[t + 1]]] - ucum[vdep_off[voff[t]]];
+}
 
 __global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, MxV x, uint64_t *__restrict__ a_cnt,
                                                     uint64_t *__restrict__ kd_cnt, uint64_t *__restrict__ u_cnt)
@@ -2314,12 +2428,14 @@ __global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, MxV x, 
     const uint64_t kd = x.vcnz[j1] - x.vcnz[j0];
     a_cnt[t] = (kv.arena_off[t + 1] - kv.arena_off[t]) + kd + (e1 - e0);
     kd_cnt[t] = (kv.kd_off[t + 1] - kv.kd_off[t]) + kd;
-    u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (x.ucum[e1] - x.ucum[e0]);
+    u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (e1 > e0 ? x.ucnt[t] : 0u);
 }
 
-// key txns: copy keydeps_core's result into the combined layout (16 lanes per txn) with key codes
-__global__ __launch_bounds__(BLOCK) void k_mx_copy_keytxns(uint32_t n, MxKv kv, const uint32_t *__restrict__ key_off,
-                                                           const uint64_t *__restrict__ key_code, MxOut o)
+// key txns: copy keydeps_core's result into the combined layout (16 lanes per txn) with key codes; range txns: their
+// union TxnIds from dep_scr
+__global__ __launch_bounds__(BLOCK) void k_mx_copy(uint32_t n, MxKv kv, MxV x, const uint32_t *__restrict__ dep_scr,
+                                                   const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
+                                                   MxOut o)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
     if (t >= n) return;
@@ -2334,23 +2450,24 @@ __global__ __launch_bounds__(BLOCK) void k_mx_copy_keytxns(uint32_t n, MxKv kv, 
         o.kd_key[ko + i] = key_code[key_off[t] + ki];
     }
     for (uint64_t i = sub; i < nu; i += 16) o.dep_txn[uo + i] = kv.dep_txn[u0 + i];
+    const uint64_t e0 = x.vdep_off[x.voff[t]], e1 = x.vdep_off[x.voff[t + 1]];
+    if (e1 > e0) {
+        const uint32_t nx = x.ucnt[t];
+        for (uint32_t i = sub; i < nx; i += 16) o.dep_txn[uo + nu + i] = dep_scr[e0 + i];
+    }
 }
 
-// range txns, per emitted entry in (txn, rank) order: index in the txn's TxnId union, arena value, TxnId array
-__global__ __launch_bounds__(BLOCK) void k_mx_entries(uint64_t E, const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sperm,
-                                                      const uint32_t *__restrict__ uflag, const uint32_t *__restrict__ list_of,
-                                                      MxV x, const uint32_t *__restrict__ txn_of_rank, int rbits, MxOut o)
+// range txns, per emitted entry: the arena value (index in the txn's TxnId union)
+__global__ __launch_bounds__(BLOCK) void k_mx_arena(uint64_t E, const uint32_t *__restrict__ list_of, const uint32_t *__restrict__ idx_of_e,
+                                                    MxV x, MxOut o)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= E) return;
-    const uint32_t e = sperm[i];
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
     const uint32_t t = x.vowner[list_of[e]];
     const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
     const uint64_t e0 = x.vdep_off[j0];
-    const uint32_t idx = x.ucum[i] + uflag[i] - 1 - x.ucum[e0];
     const uint32_t kd = x.vcnz[j1] - x.vcnz[j0];
-    o.arena[o.arena_off[t] + kd + (e - e0)] = (int32_t)idx;
-    if (uflag[i]) o.dep_txn[o.u_off[t] + idx] = txn_of_rank[(uint32_t)(sk[i] & ((1ull << rbits) - 1))];
+    o.arena[o.arena_off[t] + kd + (e - e0)] = (int32_t)idx_of_e[e];
 }
 
 // range txns, per non-empty virtual query: KeyDeps.keys entry (covered-key index + code) and the end-offset header
@@ -2466,30 +2583,53 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     }
     uint32_t *deps = ctx->get<uint32_t>("mx_deps", Ex + 1);
     uint32_t *list_of = ctx->get<uint32_t>("mx_list_of", Ex + 1);
-    uint32_t *uflag = ctx->get<uint32_t>("mx_uflag", Ex + 1);
-    uint32_t *ucum = ctx->get<uint32_t>("mx_ucum", Ex + 1);
-    Sorted so{ nullptr, nullptr };
-    const int tbits = bits_for(n);
-    if (tbits + ks.rbits > 64) fail(ACC_E_CAP, "batch too large for the (txn, TxnId rank) composite key");
+    uint32_t *ucnt = ctx->get<uint32_t>("mx_ucnt", (size_t)n + 1);
+    uint32_t *idx_of_e = ctx->get<uint32_t>("mx_idx_of_e", Ex + 1);
+    uint32_t *dep_scr = ctx->get<uint32_t>("mx_dep_scr", Ex + 1);
+    MxU mu{ deps, voff, vdep_off, ks.txn_of_rank, idx_of_e, dep_scr, ucnt };
     if (Ex) {
         CfkView v = ks.v1view;
         v.owner = vowner;
         v.vseg = vseg;
         launch(ctx, "mx_query_emit", k_query_emit, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, (size_t)V, v,
                (const uint64_t *)vdep_off, deps, list_of);
-        uint64_t *skey = ctx->get<uint64_t>("mx_skey", Ex);
-        launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)deps,
-               (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, skey);
-        so = radix_sort(ctx, "mx_rs", skey, nullptr, Ex, tbits + ks.rbits);
-        launch(ctx, "mx_uflag", k_mx_uflag, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys, uflag);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, uflag, ucum, Ex, true, ucum + Ex);
-    } else {
-        ACC_HIP(hipMemsetAsync(ucum, 0, 4, st));
+        // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
+        uint32_t *blk_list = ctx->get<uint32_t>("mx_blk_list", n);
+        uint64_t *gst = ctx->get<uint64_t>("mx_gst", 2);
+        ACC_HIP(hipMemsetAsync(gst, 0, 16, st));
+        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)voff,
+               (const uint64_t *)vdep_off, blk_list, gst);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 16, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        const uint64_t nblk = ctx->pinned[0];
+        ctx->stat("keydeps.range_block_txns", nblk);
+        if (!ctx->pinned[1]) {
+            launch(ctx, "mx_union_wave", k_mx_union_wave, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, mu);
+            if (nblk)
+                launch(ctx, "mx_union_block", k_mx_union_block, dim3((unsigned)nblk), dim3(BLOCK), 0,
+                       (const uint32_t *)blk_list, (const uint64_t *)gst, mu);
+        } else {
+            const int tbits = bits_for(n);
+            if (tbits + ks.rbits > 64) fail(ACC_E_CAP, "batch too large for the (txn, TxnId rank) composite key");
+            uint64_t *skey = ctx->get<uint64_t>("mx_skey", Ex);
+            uint32_t *uflag = ctx->get<uint32_t>("mx_uflag", Ex + 1);
+            uint32_t *ucum = ctx->get<uint32_t>("mx_ucum", Ex + 1);
+            launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)deps,
+                   (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, skey);
+            Sorted so = radix_sort(ctx, "mx_rs", skey, nullptr, Ex, tbits + ks.rbits);
+            launch(ctx, "mx_uflag", k_mx_uflag, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys, uflag);
+            scan<uint32_t, OpAdd<uint32_t>>(ctx, uflag, ucum, Ex, true, ucum + Ex);
+            launch(ctx, "mx_union_sorted", k_mx_union_sorted, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex,
+                   (const uint64_t *)so.keys, (const uint32_t *)so.vals, (const uint32_t *)uflag, (const uint32_t *)ucum,
+                   (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, mu);
+            launch(ctx, "mx_ucnt_sorted", k_mx_ucnt_sorted, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)voff,
+                   (const uint64_t *)vdep_off, (const uint32_t *)ucum, ucnt);
+        }
     }
 
     // ---- combined offsets, key txns copied, range txns written
     MxKv mkv{ kv.arena_off, kv.kd_off, kv.u_off, kv.arena, kv.key_idx, kv.dep_txn };
-    MxV x{ voff, vowner, vseg, vcnz, ucum, vcnt, vdep_off, seg_key };
+    MxV x{ voff, vowner, vseg, vcnz, ucnt, vcnt, vdep_off, seg_key };
     uint64_t *a_cnt = ctx->get<uint64_t>("mx_a_cnt", n);
     uint64_t *kd_cnt = ctx->get<uint64_t>("mx_kd_cnt", n);
     uint64_t *u_cnt = ctx->get<uint64_t>("mx_u_cnt", n);
@@ -2510,11 +2650,11 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     o.key_idx = ctx->get<uint32_t>("mx_key_idx", TK + 1);
     o.kd_key = ctx->get<uint64_t>("mx_kd_key", TK + 1);
     o.dep_txn = ctx->get<uint32_t>("mx_dep_txn", TU + 1);
-    launch(ctx, "mx_copy_keytxns", k_mx_copy_keytxns, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, key_off,
-           key_code, o);
+    launch(ctx, "mx_copy", k_mx_copy, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, x,
+           (const uint32_t *)dep_scr, key_off, key_code, o);
     if (Ex)
-        launch(ctx, "mx_entries", k_mx_entries, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys,
-               (const uint32_t *)so.vals, (const uint32_t *)uflag, (const uint32_t *)list_of, x, ks.txn_of_rank, ks.rbits, o);
+        launch(ctx, "mx_arena", k_mx_arena, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)list_of,
+               (const uint32_t *)idx_of_e, x, o);
     if (V) launch(ctx, "mx_keys", k_mx_keys, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, V, x, o);
     ctx->sync();
     *view = acc_keydeps_view{ n, TA, TK, TU, kv.total_edges + Ex, o.arena_off, o.arena, o.kd_off, o.key_idx, o.u_off,

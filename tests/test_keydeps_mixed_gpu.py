@@ -119,3 +119,16 @@ def test_errors(ctx):
     rb.keys.key_code[:] = [1]
     with pytest.raises(IllegalArgumentException):
         ctx.calculate_partial_key_deps_mixed(rb)
+
+
+def test_union_tiers(ctx):
+    """Range txns whose entries exceed the wave tier (block tier) and the block tier (global (txn, rank) sort)."""
+    import oracle
+    n_keys = 5000
+    txns = [dict(kind=W.WRITE, keys=[10 * i + 5]) for i in range(n_keys)]
+    txns += [dict(kind=W.WRITE, ranges=[(0, 10 * 300)])]            # ~300 entries: block tier
+    txns += [dict(kind=W.READ, ranges=[(0, 10 * n_keys + 10)])]     # 5000 entries: beyond the block tier
+    rb = rd_cases.build(txns)
+    g = ctx.calculate_partial_key_deps_mixed(rb)
+    assert ctx.stats()["keydeps.range_block_txns"] >= 1
+    assert_same(g, oracle.keydeps_mixed(rb), "union tiers")
