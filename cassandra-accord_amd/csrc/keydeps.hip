@@ -442,11 +442,17 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *a, uint32_t 
     return lo;
 }
 
+__device__ __forceinline__ Query make_query_ts(const CfkView &v, uint32_t t, uint32_t seg);
+
 __device__ __forceinline__ Query make_query(const CfkView &v, uint32_t j)
 {
+    return make_query_ts(v, v.owner[j], v.vseg ? v.vseg[j] : v.seg_incl[v.pair_pos[j]] - 1);
+}
+
+// the query of txn t against CFK segment seg
+__device__ __forceinline__ Query make_query_ts(const CfkView &v, uint32_t t, uint32_t seg)
+{
     Query q;
-    uint32_t t = v.owner[j];
-    uint32_t seg = v.vseg ? v.vseg[j] : v.seg_incl[v.pair_pos[j]] - 1;
     uint32_t s0 = v.seg_start[seg], s1 = v.seg_start[seg + 1];
     uint32_t S = v.rank[v.n + t];          // startedBefore = T.executeAt
     q.trank = v.rank[t];
@@ -2199,14 +2205,16 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
 // (txn, TxnId rank) gives every range txn's TxnId union and indices.
 
 constexpr uint64_t MX_ERR_DOMAIN = 1, MX_ERR_EMPTY = 2, MX_ERR_UNSORTED = 4, MX_ERR_OFF = 8;
+constexpr uint32_t MX_PIECE = 32;   // covered segments per work piece
 
 // validation (TxnId.domain(), Range start < end, Ranges.ofSortedAndDeoverlapped) and, per range, its run of covered
-// segments [ra, ra + rcnt) over the sorted CFK keys
+// segments [ra, ra + rcnt) over the sorted CFK keys, its owner and its number of work pieces
 __global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t *__restrict__ tl,
                                                      const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ rng_off,
                                                      const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
                                                      uint32_t end_inclusive, const uint64_t *__restrict__ seg_key, uint32_t nseg,
-                                                     uint32_t *__restrict__ ra, uint64_t *__restrict__ rcnt,
+                                                     uint32_t *__restrict__ ra, uint32_t *__restrict__ rowner,
+                                                     uint64_t *__restrict__ rcnt, uint64_t *__restrict__ rpieces,
                                                      uint64_t *__restrict__ errs)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
@@ -2228,8 +2236,11 @@ __global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t 
             const uint32_t a = lo;
             hi = nseg;
             while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (end_inclusive ? seg_key[m] <= x : seg_key[m] < x) lo = m + 1; else hi = m; }
+            const uint32_t c = e ? 0u : lo - a;
             ra[j] = a;
-            rcnt[j] = e ? 0 : (uint64_t)(lo - a);
+            rowner[j] = t;
+            rcnt[j] = c;
+            rpieces[j] = (c + MX_PIECE - 1) / MX_PIECE;
         }
     }
     if (e) atomicOr((unsigned long long *)errs, (unsigned long long)e);
@@ -2243,43 +2254,102 @@ __global__ __launch_bounds__(BLOCK) void k_mx_seg_keys(uint32_t nseg, const uint
     if (s < nseg) seg_key[s] = key_code[perm[seg_start[s]]];
 }
 
-// per txn: first virtual query (u32 CSR over the virtual query space)
-__global__ __launch_bounds__(BLOCK) void k_mx_voff(uint32_t n, const uint32_t *__restrict__ rng_off, const uint64_t *__restrict__ r_off,
-                                                   uint32_t *__restrict__ voff)
+// work pieces: piece p = (range, first covered segment), at most MX_PIECE segments each
+__global__ __launch_bounds__(BLOCK) void k_mx_pieces(uint32_t R, const uint64_t *__restrict__ poff, uint32_t *__restrict__ prange)
+{
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= R) return;
+    for (uint64_t p = poff[j]; p < poff[j + 1]; ++p) prange[p] = j;
+}
+
+struct MxP {   // pieces
+    const uint32_t *prange, *ra, *rowner, *rng_off;
+    const uint64_t *poff, *rcnt, *r_off, *seg_key;
+};
+
+// 32 lanes per piece, one covered segment (one query) per lane
+__device__ __forceinline__ uint32_t mx_scan32(uint32_t x, uint32_t sub)   // inclusive, within the 32-lane half
+{
+#pragma unroll
+    for (uint32_t d = 1; d < 32; d <<= 1) {
+        const uint32_t u = __shfl_up(x, d, 64);
+        if (sub >= d) x += u;
+    }
+    return x;
+}
+
+// count pass: entries and non-empty keys per piece
+__global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkView v, uint64_t *__restrict__ pe_cnt,
+                                                     uint32_t *__restrict__ pk_cnt)
+{
+    const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
+    const uint32_t sub = threadIdx.x & 31u, g0 = lane_id() & 32u;
+    uint32_t c = 0;
+    if (p < NP) {
+        const uint32_t j = pc.prange[p], t = pc.rowner[j];
+        const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
+        const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
+        if (sub < nk) c = run_query<false>(v, make_query_ts(v, t, pc.ra[j] + k0 + sub), nullptr);
+    }
+    const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
+    const uint32_t te = __shfl(ce, (int)(g0 + 31), 64), tk = __shfl(ck, (int)(g0 + 31), 64);
+    if (p < NP && sub == 0) { pe_cnt[p] = te; pk_cnt[p] = tk; }
+}
+
+struct MxE {   // emitted entries and key records of the range txns
+    uint32_t *deps, *owner;          // [Ex]: TxnId rank, owning txn
+    uint32_t *kx_idx, *kx_end;       // [Kx]: covered-key index, end offset within the txn's entries
+    uint64_t *kx_code;               // [Kx]: key code
+};
+
+__global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView v, const uint64_t *__restrict__ pe_off,
+                                                    const uint32_t *__restrict__ pk_off, const uint64_t *__restrict__ etoff, MxE x)
+{
+    const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
+    const uint32_t sub = threadIdx.x & 31u;
+    uint32_t c = 0, j = 0, t = 0, seg = 0, k0 = 0;
+    Query qq{};
+    bool act = false;
+    if (p < NP) {
+        j = pc.prange[p];
+        t = pc.rowner[j];
+        k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
+        const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
+        act = sub < nk;
+        if (act) {
+            seg = pc.ra[j] + k0 + sub;
+            qq = make_query_ts(v, t, seg);
+            c = run_query<false>(v, qq, nullptr);
+        }
+    }
+    const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
+    if (!act || c == 0) return;
+    const uint64_t e = pe_off[p] + (ce - c);
+    run_query<true>(v, qq, x.deps + e);
+    for (uint32_t i = 0; i < c; ++i) x.owner[e + i] = t;
+    const uint32_t kr = pk_off[p] + ck - 1;
+    x.kx_idx[kr] = (uint32_t)(pc.r_off[j] - pc.r_off[pc.rng_off[t]] + k0 + sub);
+    x.kx_code[kr] = pc.seg_key[seg];
+    x.kx_end[kr] = (uint32_t)(e + c - etoff[t]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mx_toff(uint32_t n, const uint32_t *__restrict__ rng_off, const uint64_t *__restrict__ poff,
+                                                   const uint64_t *__restrict__ pe_off, const uint32_t *__restrict__ pk_off,
+                                                   uint64_t *__restrict__ etoff, uint32_t *__restrict__ ktoff)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t <= n) voff[t] = (uint32_t)r_off[rng_off[t]];
+    if (t > n) return;
+    const uint64_t p = poff[rng_off[t]];
+    etoff[t] = pe_off[p];
+    ktoff[t] = pk_off[p];
 }
 
-// virtual queries j -> (owner txn, segment); MX_SPAN consecutive j per thread: one search, then a walk
-constexpr uint32_t MX_SPAN = 16;
-__global__ __launch_bounds__(BLOCK) void k_mx_vqueries(uint64_t V, uint32_t R, uint32_t n, const uint64_t *__restrict__ r_off,
-                                                       const uint32_t *__restrict__ ra, const uint32_t *__restrict__ rng_off,
-                                                       uint32_t *__restrict__ vowner, uint32_t *__restrict__ vseg)
-{
-    const uint64_t j0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * MX_SPAN;
-    if (j0 >= V) return;
-    uint32_t lo = 0, hi = R;   // last range r with r_off[r] <= j0 (and a non-empty run)
-    while (lo < hi) { uint32_t m = (lo + hi + 1) >> 1; if (r_off[m] <= j0) lo = m; else hi = m - 1; }
-    uint32_t r = lo;
-    uint32_t tlo = 0, thi = n;   // owner: last t with rng_off[t] <= r
-    while (tlo < thi) { uint32_t m = (tlo + thi + 1) >> 1; if (rng_off[m] <= r) tlo = m; else thi = m - 1; }
-    uint32_t t = tlo;
-    const uint64_t j1 = j0 + MX_SPAN < V ? j0 + MX_SPAN : V;
-    for (uint64_t j = j0; j < j1; ++j) {
-        while (r_off[r + 1] <= j) ++r;
-        while (rng_off[t + 1] <= r) ++t;
-        vowner[j] = t;
-        vseg[j] = ra[r] + (uint32_t)(j - r_off[r]);
-    }
-}
-
-// sort keys (txn, TxnId rank) of the emitted entries (emission order = (txn, key, rank) already)
-__global__ __launch_bounds__(BLOCK) void k_mx_sortkeys(uint64_t E, const uint32_t *__restrict__ deps, const uint32_t *__restrict__ list_of,
-                                                       const uint32_t *__restrict__ vowner, int rbits, uint64_t *__restrict__ key)
+// sort keys (txn, TxnId rank) of the emitted entries (fallback union)
+__global__ __launch_bounds__(BLOCK) void k_mx_sortkeys(uint64_t E, const uint32_t *__restrict__ deps, const uint32_t *__restrict__ owner,
+                                                       int rbits, uint64_t *__restrict__ key)
 {
     const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (e < E) key[e] = ((uint64_t)vowner[list_of[e]] << rbits) | deps[e];
+    if (e < E) key[e] = ((uint64_t)owner[e] << rbits) | deps[e];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mx_uflag(uint64_t E, const uint64_t *__restrict__ sk, uint32_t *__restrict__ f)
@@ -2293,10 +2363,6 @@ struct MxKv {   // the key-txn KeyDeps (keydeps_core's view)
     const int32_t *arena;
     const uint32_t *key_idx, *dep_txn;
 };
-struct MxV {    // the virtual-query space of the range txns
-    const uint32_t *voff, *vowner, *vseg, *vcnz, *ucnt;
-    const uint64_t *vcnt, *vdep_off, *seg_key;
-};
 struct MxOut {
     uint64_t *arena_off, *kd_off, *u_off;
     int32_t *arena;
@@ -2306,21 +2372,21 @@ struct MxOut {
 // per-txn TxnId union of the emitted entries: idx_of_e[e] = index of entry e's TxnId in its txn's union,
 // dep_scr[e0 + i] = batch index of the i-th union TxnId, ucnt[t] = union size
 struct MxU {
-    const uint32_t *deps, *voff;
-    const uint64_t *vdep_off;
+    const uint32_t *deps;
+    const uint64_t *etoff;
     const uint32_t *txn_of_rank;
     uint32_t *idx_of_e, *dep_scr, *ucnt;
 };
 
 // per txn: entry count routing: E <= 64 -> wave tier (every txn); 64 < E <= MX_BLK_E -> block list; beyond -> flag
 constexpr uint32_t MX_BLK_E = 4096;
-__global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint32_t *__restrict__ voff, const uint64_t *__restrict__ vdep_off,
-                                                    uint32_t *__restrict__ blk_list, uint64_t *__restrict__ gst)
+__global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint64_t *__restrict__ etoff, uint32_t *__restrict__ blk_list,
+                                                    uint64_t *__restrict__ gst)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     bool blk = false, over = false;
     if (t < n) {
-        const uint64_t E = vdep_off[voff[t + 1]] - vdep_off[voff[t]];
+        const uint64_t E = etoff[t + 1] - etoff[t];
         blk = E > 64 && E <= MX_BLK_E;
         over = E > MX_BLK_E;
     }
@@ -2339,7 +2405,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_wave(uint32_t n, MxU u)
 {
     const uint32_t lane = lane_id(), t = blockIdx.x * WAVES + (threadIdx.x >> 6);
     if (t >= n) return;
-    const uint64_t e0 = u.vdep_off[u.voff[t]], E = u.vdep_off[u.voff[t + 1]] - e0;
+    const uint64_t e0 = u.etoff[t], E = u.etoff[t + 1] - e0;
     if (E == 0) { if (lane == 0) u.ucnt[t] = 0; return; }
     if (E > 64) return;
     const bool in = lane < E;
@@ -2365,8 +2431,8 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_block(const uint32_t *__rest
     const uint32_t b = blockIdx.x;
     if (b >= (uint32_t)gst[0]) return;
     const uint32_t t = list[b], tid = threadIdx.x;
-    const uint64_t e0 = u.vdep_off[u.voff[t]];
-    const uint32_t E = (uint32_t)(u.vdep_off[u.voff[t + 1]] - e0);
+    const uint64_t e0 = u.etoff[t];
+    const uint32_t E = (uint32_t)(u.etoff[t + 1] - e0);
     uint32_t n2 = 128;
     while (n2 < E) n2 <<= 1;
     for (uint32_t i = tid; i < n2; i += BLOCK) buf[i] = i < E ? (((uint64_t)u.deps[e0 + i] << 32) | i) : ~0ull;
@@ -2399,89 +2465,71 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_block(const uint32_t *__rest
 // global fallback (some txn beyond MX_BLK_E): from the (txn, rank) sort
 __global__ __launch_bounds__(BLOCK) void k_mx_union_sorted(uint64_t E, const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sperm,
                                                            const uint32_t *__restrict__ uflag, const uint32_t *__restrict__ ucum,
-                                                           const uint32_t *__restrict__ list_of, const uint32_t *__restrict__ vowner,
-                                                           int rbits, MxU u)
+                                                           const uint32_t *__restrict__ owner, int rbits, MxU u)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= E) return;
     const uint32_t e = sperm[i];
-    const uint32_t t = vowner[list_of[e]];
-    const uint64_t e0 = u.vdep_off[u.voff[t]];
+    const uint64_t e0 = u.etoff[owner[e]];
     const uint32_t idx = ucum[i] + uflag[i] - 1 - ucum[e0];
     u.idx_of_e[e] = idx;
     if (uflag[i]) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(sk[i] & ((1ull << rbits) - 1))];
 }
-__global__ __launch_bounds__(BLOCK) void k_mx_ucnt_sorted(uint32_t n, const uint32_t *__restrict__ voff, const uint64_t *__restrict__ vdep_off,
-                                                          const uint32_t *__restrict__ ucum, uint32_t *__restrict__ ucnt)
+__global__ __launch_bounds__(BLOCK) void k_mx_ucnt_sorted(uint32_t n, const uint64_t *__restrict__ etoff, const uint32_t *__restrict__ ucum,
+                                                          uint32_t *__restrict__ ucnt)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t < n) ucnt[t] = ucum[vdep_off[voff[t + 1]]] - ucum[vdep_off[voff[t]]];
+    if (t < n) ucnt[t] = ucum[etoff[t + 1]] - ucum[etoff[t]];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, MxV x, uint64_t *__restrict__ a_cnt,
-                                                    uint64_t *__restrict__ kd_cnt, uint64_t *__restrict__ u_cnt)
+__global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, const uint64_t *__restrict__ etoff,
+                                                    const uint32_t *__restrict__ ktoff, const uint32_t *__restrict__ ucnt,
+                                                    uint64_t *__restrict__ a_cnt, uint64_t *__restrict__ kd_cnt,
+                                                    uint64_t *__restrict__ u_cnt)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= n) return;
-    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
-    const uint64_t e0 = x.vdep_off[j0], e1 = x.vdep_off[j1];
-    const uint64_t kd = x.vcnz[j1] - x.vcnz[j0];
-    a_cnt[t] = (kv.arena_off[t + 1] - kv.arena_off[t]) + kd + (e1 - e0);
+    const uint64_t ex = etoff[t + 1] - etoff[t];
+    const uint64_t kd = ktoff[t + 1] - ktoff[t];
+    a_cnt[t] = (kv.arena_off[t + 1] - kv.arena_off[t]) + kd + ex;
     kd_cnt[t] = (kv.kd_off[t + 1] - kv.kd_off[t]) + kd;
-    u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (e1 > e0 ? x.ucnt[t] : 0u);
+    u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (ex ? ucnt[t] : 0u);
 }
 
-// key txns: copy keydeps_core's result into the combined layout (16 lanes per txn) with key codes; range txns: their
-// union TxnIds from dep_scr
-__global__ __launch_bounds__(BLOCK) void k_mx_copy(uint32_t n, MxKv kv, MxV x, const uint32_t *__restrict__ dep_scr,
-                                                   const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
-                                                   MxOut o)
+// the combined layout, 16 lanes per txn: key txns copied from keydeps_core's result (with key codes), range txns from
+// their key records, per-entry union indices and union TxnIds
+__global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const uint64_t *__restrict__ etoff,
+                                                    const uint32_t *__restrict__ ktoff, const uint32_t *__restrict__ ucnt, MxE x,
+                                                    const uint32_t *__restrict__ idx_of_e, const uint32_t *__restrict__ dep_scr,
+                                                    const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
+                                                    MxOut o)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
     if (t >= n) return;
-    const uint64_t a0 = kv.arena_off[t], na = kv.arena_off[t + 1] - a0;
-    const uint64_t k0 = kv.kd_off[t], nk = kv.kd_off[t + 1] - k0;
-    const uint64_t u0 = kv.u_off[t], nu = kv.u_off[t + 1] - u0;
     const uint64_t ao = o.arena_off[t], ko = o.kd_off[t], uo = o.u_off[t];
-    for (uint64_t i = sub; i < na; i += 16) o.arena[ao + i] = kv.arena[a0 + i];
-    for (uint64_t i = sub; i < nk; i += 16) {
-        const uint32_t ki = kv.key_idx[k0 + i];
-        o.key_idx[ko + i] = ki;
-        o.kd_key[ko + i] = key_code[key_off[t] + ki];
+    const uint64_t e0 = etoff[t], ex = etoff[t + 1] - e0;
+    if (ex == 0) {
+        const uint64_t a0 = kv.arena_off[t], na = kv.arena_off[t + 1] - a0;
+        const uint64_t k0 = kv.kd_off[t], nk = kv.kd_off[t + 1] - k0;
+        const uint64_t u0 = kv.u_off[t], nu = kv.u_off[t + 1] - u0;
+        for (uint64_t i = sub; i < na; i += 16) o.arena[ao + i] = kv.arena[a0 + i];
+        for (uint64_t i = sub; i < nk; i += 16) {
+            const uint32_t ki = kv.key_idx[k0 + i];
+            o.key_idx[ko + i] = ki;
+            o.kd_key[ko + i] = key_code[key_off[t] + ki];
+        }
+        for (uint64_t i = sub; i < nu; i += 16) o.dep_txn[uo + i] = kv.dep_txn[u0 + i];
+        return;
     }
-    for (uint64_t i = sub; i < nu; i += 16) o.dep_txn[uo + i] = kv.dep_txn[u0 + i];
-    const uint64_t e0 = x.vdep_off[x.voff[t]], e1 = x.vdep_off[x.voff[t + 1]];
-    if (e1 > e0) {
-        const uint32_t nx = x.ucnt[t];
-        for (uint32_t i = sub; i < nx; i += 16) o.dep_txn[uo + nu + i] = dep_scr[e0 + i];
+    const uint32_t k0 = ktoff[t], kd = ktoff[t + 1] - k0;
+    for (uint32_t i = sub; i < kd; i += 16) {
+        o.key_idx[ko + i] = x.kx_idx[k0 + i];
+        o.kd_key[ko + i] = x.kx_code[k0 + i];
+        o.arena[ao + i] = (int32_t)(kd + x.kx_end[k0 + i]);
     }
-}
-
-// range txns, per emitted entry: the arena value (index in the txn's TxnId union)
-__global__ __launch_bounds__(BLOCK) void k_mx_arena(uint64_t E, const uint32_t *__restrict__ list_of, const uint32_t *__restrict__ idx_of_e,
-                                                    MxV x, MxOut o)
-{
-    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= E) return;
-    const uint32_t t = x.vowner[list_of[e]];
-    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
-    const uint64_t e0 = x.vdep_off[j0];
-    const uint32_t kd = x.vcnz[j1] - x.vcnz[j0];
-    o.arena[o.arena_off[t] + kd + (e - e0)] = (int32_t)idx_of_e[e];
-}
-
-// range txns, per non-empty virtual query: KeyDeps.keys entry (covered-key index + code) and the end-offset header
-__global__ __launch_bounds__(BLOCK) void k_mx_keys(uint64_t V, MxV x, MxOut o)
-{
-    const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= V || x.vcnt[j] == 0) return;
-    const uint32_t t = x.vowner[j];
-    const uint32_t j0 = x.voff[t], j1 = x.voff[t + 1];
-    const uint32_t slot = x.vcnz[j] - x.vcnz[j0];
-    const uint32_t kd = x.vcnz[j1] - x.vcnz[j0];
-    o.key_idx[o.kd_off[t] + slot] = (uint32_t)j - j0;
-    o.kd_key[o.kd_off[t] + slot] = x.seg_key[x.vseg[j]];
-    o.arena[o.arena_off[t] + slot] = (int32_t)(kd + (x.vdep_off[j + 1] - x.vdep_off[j0]));
+    for (uint64_t i = sub; i < ex; i += 16) o.arena[ao + kd + i] = (int32_t)idx_of_e[e0 + i];
+    const uint32_t nx = ucnt[t];
+    for (uint32_t i = sub; i < nx; i += 16) o.dep_txn[uo + i] = dep_scr[e0 + i];
 }
 
 void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view)
@@ -2515,7 +2563,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     const uint64_t *rs = stage_in(ctx, "in_rng_start", in->rng_start, R, in->mem);
     const uint64_t *re = stage_in(ctx, "in_rng_end", in->rng_end, R, in->mem);
 
-    // ---- covered segments per range
+    // ---- covered segments per range, work pieces
     uint32_t nseg = 0;
     if (ks.cfk) {
         ACC_HIP(hipMemcpyAsync(ctx->pinned, ks.seg_incl + ks.P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2527,78 +2575,87 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
                ks.key_code, seg_key);
     uint32_t *ra = ctx->get<uint32_t>("mx_ra", R + 1);
+    uint32_t *rowner = ctx->get<uint32_t>("mx_rowner", R + 1);
     uint64_t *rcnt = ctx->get<uint64_t>("mx_rcnt", R + 1);
+    uint64_t *rpieces = ctx->get<uint64_t>("mx_rpieces", R + 1);
     uint64_t *r_off = ctx->get<uint64_t>("mx_r_off", R + 2);
+    uint64_t *poff = ctx->get<uint64_t>("mx_poff", R + 2);
     uint64_t *errs = ctx->get<uint64_t>("mx_errs", 1);
     ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
     launch(ctx, "mx_ranges", k_mx_ranges, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, key_off, rng_off, rs, re,
-           in->end_inclusive, (const uint64_t *)seg_key, nseg, ra, rcnt, errs);
-    if (R) scan<uint64_t, OpAdd<uint64_t>>(ctx, rcnt, r_off, R, true, r_off + R);
-    else ACC_HIP(hipMemsetAsync(r_off, 0, 8, st));
+           in->end_inclusive, (const uint64_t *)seg_key, nseg, ra, rowner, rcnt, rpieces, errs);
+    if (R) {
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, rcnt, r_off, R, true, r_off + R);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, rpieces, poff, R, true, poff + R);
+    } else {
+        ACC_HIP(hipMemsetAsync(r_off, 0, 8, st));
+        ACC_HIP(hipMemsetAsync(poff, 0, 8, st));
+    }
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, r_off + R, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, poff + R, 8, hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t merr = ctx->pinned[0];
     if (merr & MX_ERR_DOMAIN) fail(ACC_E_ARG, "a range-domain txn lists keys or a key-domain txn lists ranges (TxnId.domain())");
     if (merr & MX_ERR_EMPTY) fail(ACC_E_ARG, "range start must be below its end (Range: start >= end)");
     if (merr & MX_ERR_UNSORTED) fail(ACC_E_ARG, "ranges of a txn must be sorted and deoverlapped (Ranges.ofSortedAndDeoverlapped)");
     if (merr & MX_ERR_OFF) fail(ACC_E_ARG, "rng_off must be non-decreasing");
-    const uint64_t V = ctx->pinned[1];
+    const uint64_t V = ctx->pinned[1], NP = ctx->pinned[2];
     if (V >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 (range txn, covered key) queries in one batch");
     ctx->stat("keydeps.range_key_queries", V);
 
-    // ---- virtual queries (T, segment) and the exact-replay scan over them
-    uint32_t *voff = ctx->get<uint32_t>("mx_voff", (size_t)n + 1);
-    launch(ctx, "mx_voff", k_mx_voff, dim3(grid_for((size_t)n + 1, BLOCK)), dim3(BLOCK), 0, n, rng_off, (const uint64_t *)r_off, voff);
-    uint32_t *vowner = ctx->get<uint32_t>("mx_vowner", V + 1);
-    uint32_t *vseg = ctx->get<uint32_t>("mx_vseg", V + 1);
-    uint64_t *vcnt = ctx->get<uint64_t>("mx_vcnt", V + 1);
-    uint64_t *vdep_off = ctx->get<uint64_t>("mx_vdep_off", V + 1);
-    uint32_t *vnz = ctx->get<uint32_t>("mx_vnz", V + 1);
-    uint32_t *vcnz = ctx->get<uint32_t>("mx_vcnz", V + 1);
-    uint64_t Ex = 0;
-    if (V) {
-        launch(ctx, "mx_vqueries", k_mx_vqueries, dim3(grid_for((V + MX_SPAN - 1) / MX_SPAN, BLOCK)), dim3(BLOCK), 0, V,
-               (uint32_t)R, n, (const uint64_t *)r_off, (const uint32_t *)ra, rng_off, vowner, vseg);
+    // ---- count and emit per piece with the exact-replay scan
+    uint32_t *prange = ctx->get<uint32_t>("mx_prange", NP + 1);
+    uint64_t *pe_cnt = ctx->get<uint64_t>("mx_pe_cnt", NP + 1);
+    uint64_t *pe_off = ctx->get<uint64_t>("mx_pe_off", NP + 2);
+    uint32_t *pk_cnt = ctx->get<uint32_t>("mx_pk_cnt", NP + 1);
+    uint32_t *pk_off = ctx->get<uint32_t>("mx_pk_off", NP + 2);
+    uint64_t *etoff = ctx->get<uint64_t>("mx_etoff", (size_t)n + 1);
+    uint32_t *ktoff = ctx->get<uint32_t>("mx_ktoff", (size_t)n + 1);
+    MxP pc{ prange, ra, rowner, rng_off, poff, rcnt, r_off, seg_key };
+    uint64_t Ex = 0, Kx = 0;
+    CfkView v{};
+    if (NP) {
         if (!ks.v1) {
             ks.v1view = build_v1_cfk(ctx, n, ks.P, ks.rbits, ks.tl, ks.owner, ks.rank, ks.seg_incl, ks.seg_start, ks.s_rank,
                                      ks.s_exec, ks.s_info, ks.pair_pos);
             ks.v1 = true;
         }
-        CfkView v = ks.v1view;
-        v.owner = vowner;
-        v.vseg = vseg;
-        const unsigned gV = grid_for(V, BLOCK);
-        launch(ctx, "mx_query_count", k_query_count, dim3(gV), dim3(BLOCK), 0, (size_t)V, v, vcnt);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, vcnt, vdep_off, V, true, vdep_off + V);
-        launch(ctx, "mx_nonempty", k_nonempty, dim3(gV), dim3(BLOCK), 0, (size_t)V, (const uint64_t *)vcnt, vnz);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, vnz, vcnz, V, true, vcnz + V);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, vdep_off + V, 8, hipMemcpyDeviceToHost, st));
+        v = ks.v1view;
+        launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff, prange);
+        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, pe_cnt, pe_off, NP, true, pe_off + NP);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, pk_cnt, pk_off, NP, true, pk_off + NP);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, pe_off + NP, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, pk_off + NP, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
         Ex = ctx->pinned[0];
+        Kx = ctx->pinned[1] & 0xFFFFFFFFull;
         if (Ex >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 range-txn KeyDeps entries in one batch");
     } else {
-        ACC_HIP(hipMemsetAsync(vdep_off, 0, 8, st));
-        ACC_HIP(hipMemsetAsync(vcnz, 0, 4, st));
+        ACC_HIP(hipMemsetAsync(pe_off, 0, 8, st));
+        ACC_HIP(hipMemsetAsync(pk_off, 0, 4, st));
     }
-    uint32_t *deps = ctx->get<uint32_t>("mx_deps", Ex + 1);
-    uint32_t *list_of = ctx->get<uint32_t>("mx_list_of", Ex + 1);
+    launch(ctx, "mx_toff", k_mx_toff, dim3(grid_for((size_t)n + 1, BLOCK)), dim3(BLOCK), 0, n, rng_off, (const uint64_t *)poff,
+           (const uint64_t *)pe_off, (const uint32_t *)pk_off, etoff, ktoff);
+    MxE mx;
+    mx.deps = ctx->get<uint32_t>("mx_deps", Ex + 1);
+    mx.owner = ctx->get<uint32_t>("mx_owner", Ex + 1);
+    mx.kx_idx = ctx->get<uint32_t>("mx_kx_idx", Kx + 1);
+    mx.kx_end = ctx->get<uint32_t>("mx_kx_end", Kx + 1);
+    mx.kx_code = ctx->get<uint64_t>("mx_kx_code", Kx + 1);
     uint32_t *ucnt = ctx->get<uint32_t>("mx_ucnt", (size_t)n + 1);
     uint32_t *idx_of_e = ctx->get<uint32_t>("mx_idx_of_e", Ex + 1);
     uint32_t *dep_scr = ctx->get<uint32_t>("mx_dep_scr", Ex + 1);
-    MxU mu{ deps, voff, vdep_off, ks.txn_of_rank, idx_of_e, dep_scr, ucnt };
+    MxU mu{ mx.deps, etoff, ks.txn_of_rank, idx_of_e, dep_scr, ucnt };
     if (Ex) {
-        CfkView v = ks.v1view;
-        v.owner = vowner;
-        v.vseg = vseg;
-        launch(ctx, "mx_query_emit", k_query_emit, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, (size_t)V, v,
-               (const uint64_t *)vdep_off, deps, list_of);
+        launch(ctx, "mx_pemit", k_mx_pemit, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, (const uint64_t *)pe_off,
+               (const uint32_t *)pk_off, (const uint64_t *)etoff, mx);
         // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
         uint32_t *blk_list = ctx->get<uint32_t>("mx_blk_list", n);
         uint64_t *gst = ctx->get<uint64_t>("mx_gst", 2);
         ACC_HIP(hipMemsetAsync(gst, 0, 16, st));
-        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)voff,
-               (const uint64_t *)vdep_off, blk_list, gst);
+        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, blk_list, gst);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 16, hipMemcpyDeviceToHost, st));
         ctx->sync();
         const uint64_t nblk = ctx->pinned[0];
@@ -2614,26 +2671,26 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
             uint64_t *skey = ctx->get<uint64_t>("mx_skey", Ex);
             uint32_t *uflag = ctx->get<uint32_t>("mx_uflag", Ex + 1);
             uint32_t *ucum = ctx->get<uint32_t>("mx_ucum", Ex + 1);
-            launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)deps,
-                   (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, skey);
+            launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)mx.deps,
+                   (const uint32_t *)mx.owner, ks.rbits, skey);
             Sorted so = radix_sort(ctx, "mx_rs", skey, nullptr, Ex, tbits + ks.rbits);
             launch(ctx, "mx_uflag", k_mx_uflag, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint64_t *)so.keys, uflag);
             scan<uint32_t, OpAdd<uint32_t>>(ctx, uflag, ucum, Ex, true, ucum + Ex);
             launch(ctx, "mx_union_sorted", k_mx_union_sorted, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex,
                    (const uint64_t *)so.keys, (const uint32_t *)so.vals, (const uint32_t *)uflag, (const uint32_t *)ucum,
-                   (const uint32_t *)list_of, (const uint32_t *)vowner, ks.rbits, mu);
-            launch(ctx, "mx_ucnt_sorted", k_mx_ucnt_sorted, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)voff,
-                   (const uint64_t *)vdep_off, (const uint32_t *)ucum, ucnt);
+                   (const uint32_t *)mx.owner, ks.rbits, mu);
+            launch(ctx, "mx_ucnt_sorted", k_mx_ucnt_sorted, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff,
+                   (const uint32_t *)ucum, ucnt);
         }
     }
 
-    // ---- combined offsets, key txns copied, range txns written
+    // ---- combined offsets and the combined layout
     MxKv mkv{ kv.arena_off, kv.kd_off, kv.u_off, kv.arena, kv.key_idx, kv.dep_txn };
-    MxV x{ voff, vowner, vseg, vcnz, ucnt, vcnt, vdep_off, seg_key };
     uint64_t *a_cnt = ctx->get<uint64_t>("mx_a_cnt", n);
     uint64_t *kd_cnt = ctx->get<uint64_t>("mx_kd_cnt", n);
     uint64_t *u_cnt = ctx->get<uint64_t>("mx_u_cnt", n);
-    launch(ctx, "mx_sizes", k_mx_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, mkv, x, a_cnt, kd_cnt, u_cnt);
+    launch(ctx, "mx_sizes", k_mx_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
+           (const uint32_t *)ktoff, (const uint32_t *)ucnt, a_cnt, kd_cnt, u_cnt);
     MxOut o;
     o.arena_off = ctx->get<uint64_t>("mx_arena_off", (size_t)n + 1);
     o.kd_off = ctx->get<uint64_t>("mx_kd_off", (size_t)n + 1);
@@ -2650,12 +2707,9 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     o.key_idx = ctx->get<uint32_t>("mx_key_idx", TK + 1);
     o.kd_key = ctx->get<uint64_t>("mx_kd_key", TK + 1);
     o.dep_txn = ctx->get<uint32_t>("mx_dep_txn", TU + 1);
-    launch(ctx, "mx_copy", k_mx_copy, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, x,
-           (const uint32_t *)dep_scr, key_off, key_code, o);
-    if (Ex)
-        launch(ctx, "mx_arena", k_mx_arena, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)list_of,
-               (const uint32_t *)idx_of_e, x, o);
-    if (V) launch(ctx, "mx_keys", k_mx_keys, dim3(grid_for(V, BLOCK)), dim3(BLOCK), 0, V, x, o);
+    launch(ctx, "mx_write", k_mx_write, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
+           (const uint32_t *)ktoff, (const uint32_t *)ucnt, mx, (const uint32_t *)idx_of_e, (const uint32_t *)dep_scr, key_off,
+           key_code, o);
     ctx->sync();
     *view = acc_keydeps_view{ n, TA, TK, TU, kv.total_edges + Ex, o.arena_off, o.arena, o.kd_off, o.key_idx, o.u_off,
                               o.dep_txn, o.kd_key };
