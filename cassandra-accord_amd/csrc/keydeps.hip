@@ -2379,25 +2379,64 @@ struct MxU {
 };
 
 // per txn: entry count routing: E <= 64 -> wave tier (every txn); 64 < E <= MX_BLK_E -> block list; beyond -> flag
-constexpr uint32_t MX_BLK_E = 4096;
+constexpr uint32_t MX_MID_E = 512, MX_BLK_E = 4096;
 __global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint64_t *__restrict__ etoff, uint32_t *__restrict__ blk_list,
-                                                    uint64_t *__restrict__ gst)
+                                                    uint32_t *__restrict__ mid_list, uint64_t *__restrict__ gst)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool blk = false, over = false;
+    bool blk = false, over = false, mid = false;
     if (t < n) {
         const uint64_t E = etoff[t + 1] - etoff[t];
-        blk = E > 64 && E <= MX_BLK_E;
+        mid = E > 64 && E <= MX_MID_E;
+        blk = E > MX_MID_E && E <= MX_BLK_E;
         over = E > MX_BLK_E;
     }
     __shared__ uint32_t lds[WAVES];
-    __shared__ uint32_t base;
+    __shared__ uint32_t base[2];
     uint32_t total;
-    const uint32_t pre = block_exclusive(blk ? 1u : 0u, OpAdd<uint32_t>(), lds, total);
-    if (threadIdx.x == 0) base = total ? (uint32_t)atomicAdd((unsigned long long *)&gst[0], (unsigned long long)total) : 0u;
+    const uint32_t pre = block_exclusive((blk ? 1u : 0u) | (mid ? 1u << 16 : 0u), OpAdd<uint32_t>(), lds, total);
+    if (threadIdx.x < 2) {
+        const uint32_t c = threadIdx.x == 0 ? (total & 0xFFFFu) : (total >> 16);
+        base[threadIdx.x] = c ? (uint32_t)atomicAdd((unsigned long long *)&gst[threadIdx.x == 0 ? 0 : 2], (unsigned long long)c) : 0u;
+    }
     __syncthreads();
-    if (blk) blk_list[base + pre] = t;
+    if (blk) blk_list[base[0] + (pre & 0xFFFFu)] = t;
+    if (mid) mid_list[base[1] + (pre >> 16)] = t;
     if (over) atomicOr((unsigned long long *)&gst[1], 1ull);
+}
+
+// wave per listed txn, 64 < E <= MX_MID_E: one wave's LDS bitonic
+__global__ __launch_bounds__(BLOCK) void k_mx_union_mid(const uint32_t *__restrict__ list, const uint64_t *__restrict__ gst, MxU u)
+{
+    __shared__ uint64_t sbuf[WAVES][MX_MID_E];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6, i = blockIdx.x * WAVES + w;
+    if (i >= (uint32_t)gst[2]) return;
+    const uint32_t t = list[i];
+    uint64_t *buf = sbuf[w];
+    const uint64_t e0 = u.etoff[t];
+    const uint32_t E = (uint32_t)(u.etoff[t + 1] - e0);
+    uint32_t n2 = 128;
+    while (n2 < E) n2 <<= 1;
+    for (uint32_t q = lane; q < n2; q += 64) buf[q] = q < E ? (((uint64_t)u.deps[e0 + q] << 32) | q) : ~0ull;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    wave_bitonic_lds(buf, n2);
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t distinct = 0;
+    for (uint32_t q0 = 0; q0 < E; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool in = q < E;
+        const uint64_t x = in ? buf[q] : 0;
+        const bool nw = in && (q == 0 || (buf[q - 1] >> 32) != (x >> 32));
+        const uint64_t bal = __ballot(nw);
+        const uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+        if (in) {
+            u.idx_of_e[e0 + (uint32_t)x] = idx;
+            if (nw) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(x >> 32)];
+        }
+        distinct += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) u.ucnt[t] = distinct;
 }
 
 // wave per txn, E <= 64: register bitonic of (rank << 32 | local entry)
@@ -2653,15 +2692,21 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
                (const uint32_t *)pk_off, (const uint64_t *)etoff, mx);
         // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
         uint32_t *blk_list = ctx->get<uint32_t>("mx_blk_list", n);
-        uint64_t *gst = ctx->get<uint64_t>("mx_gst", 2);
-        ACC_HIP(hipMemsetAsync(gst, 0, 16, st));
-        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, blk_list, gst);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 16, hipMemcpyDeviceToHost, st));
+        uint32_t *mid_list = ctx->get<uint32_t>("mx_mid_list", n);
+        uint64_t *gst = ctx->get<uint64_t>("mx_gst", 3);
+        ACC_HIP(hipMemsetAsync(gst, 0, 24, st));
+        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, blk_list,
+               mid_list, gst);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 24, hipMemcpyDeviceToHost, st));
         ctx->sync();
-        const uint64_t nblk = ctx->pinned[0];
+        const uint64_t nblk = ctx->pinned[0], nmid = ctx->pinned[2];
         ctx->stat("keydeps.range_block_txns", nblk);
+        ctx->stat("keydeps.range_mid_txns", nmid);
         if (!ctx->pinned[1]) {
             launch(ctx, "mx_union_wave", k_mx_union_wave, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, mu);
+            if (nmid)
+                launch(ctx, "mx_union_mid", k_mx_union_mid, dim3((unsigned)((nmid + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+                       (const uint32_t *)mid_list, (const uint64_t *)gst, mu);
             if (nblk)
                 launch(ctx, "mx_union_block", k_mx_union_block, dim3((unsigned)nblk), dim3(BLOCK), 0,
                        (const uint32_t *)blk_list, (const uint64_t *)gst, mu);

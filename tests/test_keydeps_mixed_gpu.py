@@ -126,9 +126,14 @@ def test_union_tiers(ctx):
     import oracle
     n_keys = 5000
     txns = [dict(kind=W.WRITE, keys=[10 * i + 5]) for i in range(n_keys)]
-    txns += [dict(kind=W.WRITE, ranges=[(0, 10 * 300)])]            # ~300 entries: block tier
+    txns += [dict(kind=W.WRITE, ranges=[(0, 10 * 300)])]            # ~300 entries: wave-LDS tier
+    txns += [dict(kind=W.WRITE, ranges=[(0, 10 * 2000)])]           # ~2000 entries: block tier
     txns += [dict(kind=W.READ, ranges=[(0, 10 * n_keys + 10)])]     # 5000 entries: beyond the block tier
     rb = rd_cases.build(txns)
     g = ctx.calculate_partial_key_deps_mixed(rb)
-    assert ctx.stats()["keydeps.range_block_txns"] >= 1
+    assert_same(g, oracle.keydeps_mixed(rb), "union tiers + fallback")
+    rb = rd_cases.build(txns[:-1])
+    g = ctx.calculate_partial_key_deps_mixed(rb)
+    st = ctx.stats()
+    assert st["keydeps.range_block_txns"] >= 1 and st["keydeps.range_mid_txns"] >= 1
     assert_same(g, oracle.keydeps_mixed(rb), "union tiers")
