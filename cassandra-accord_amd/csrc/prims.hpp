@@ -120,12 +120,12 @@ __device__ __forceinline__ T bitonic_reg(T x)
 }
 
 // ascending bitonic sort of n2 (power of two) values in LDS or global memory by a whole workgroup of BLOCK threads
-template <class T>
+template <class T, int NT = BLOCK>
 __device__ void block_bitonic(T *a, uint32_t n2)
 {
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
+            for (uint32_t i = threadIdx.x; i < n2; i += NT) {
                 const uint32_t l = i ^ jj;
                 if (l > i) {
                     const T x = a[i], y = a[l];

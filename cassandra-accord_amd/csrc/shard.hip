@@ -129,6 +129,7 @@ __global__ __launch_bounds__(BLOCK) void k_sh_gather(uint64_t F, const uint32_t 
 
 constexpr uint32_t FUSE_WAVE = 64;     // raw TxnIds per txn for the wave tier
 constexpr uint32_t FUSE_BLOCK = 8192;  // workgroup tier (LDS)
+constexpr uint32_t FUSE_BIG = 32768;   // 1024-thread workgroup tier (128 KiB of LDS)
 
 struct Fuse {
     uint32_t ng;
@@ -141,8 +142,9 @@ struct Fuse {
     uint64_t *m_keys;
     uint32_t *m_vals;
     int32_t *m_k2v;
-    uint32_t *blk_list, *glb_list;
-    uint64_t *gstat;                               // [0] block groups, [1] global groups, [2] scratch u32, [3] order err
+    uint32_t *blk_list, *glb_list, *big_list;
+    uint64_t *gstat;                               // [0] block groups, [1] global groups, [2] scratch u32, [3] order err,
+                                                   // [4] big groups
     const uint64_t *glb_off;
     uint32_t *scratch;
 };
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(BLOCK) void k_fuse_wave(Fuse f)
     if (nraw > FUSE_WAVE) {
         if (!WRITE && lane == 0) {
             if (nraw <= FUSE_BLOCK) f.blk_list[atomicAdd((unsigned long long *)&f.gstat[0], 1ull)] = g;
+            else if (nraw <= FUSE_BIG) f.big_list[atomicAdd((unsigned long long *)&f.gstat[4], 1ull)] = g;
             else {
                 f.glb_list[atomicAdd((unsigned long long *)&f.gstat[1], 1ull)] = g;
                 uint64_t n2 = 64; while (n2 < nraw) n2 <<= 1;
@@ -266,6 +269,54 @@ __global__ __launch_bounds__(BLOCK) void k_fuse_block(Fuse f)
     __shared__ uint32_t A[FUSE_BLOCK], B[FUSE_BLOCK];
     __shared__ uint32_t red[WAVES];
     fuse_block<WRITE>(f, f.blk_list[blockIdx.x], A, B, red);
+}
+
+// 1024-thread workgroup per group (FUSE_BLOCK < raw TxnIds <= FUSE_BIG): sort in LDS, union compacted in place
+template <bool WRITE>
+__global__ __launch_bounds__(1024) void k_fuse_big(Fuse f)
+{
+    constexpr int NT = 1024, NW = NT / 64, PER = FUSE_BIG / NT;
+    __shared__ uint32_t A[FUSE_BIG];
+    __shared__ uint32_t red[NW];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint32_t g = f.big_list[blockIdx.x];
+    const uint64_t r0 = f.grp_off[g], r1 = f.grp_off[g + 1];
+    const uint32_t nraw = (uint32_t)(f.rv[r1] - f.rv[r0]);
+    uint32_t n2 = NT;
+    while (n2 < nraw) n2 <<= 1;
+    for (uint32_t i = tid; i < n2; i += NT) A[i] = i < nraw ? f.vals[f.rv[r0] + i] : 0xFFFFFFFFu;
+    __syncthreads();
+    block_bitonic<uint32_t, NT>(A, n2);
+    const uint32_t per = n2 / NT, lo = tid * per;
+    uint32_t x[PER];
+    uint32_t fl = 0, c = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if ((uint32_t)q < per) {
+            const uint32_t i = lo + q;
+            x[q] = A[i];
+            const bool nw = i < nraw && (i == 0 || A[i - 1] != x[q]);
+            fl |= (uint32_t)nw << q;
+            c += nw;
+        }
+    // block exclusive scan over 16 waves
+    uint32_t incl = c;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t u = __shfl_up(incl, d, 64); if (lane >= d) incl += u; }
+    if (lane == 63) red[wave] = incl;
+    __syncthreads();
+    uint32_t p = incl - c, U = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) { const uint32_t r = red[w]; if (w < (int)wave) p += r; U += r; }
+    if (!WRITE) {
+        if (tid == 0) { f.c_nk[g] = f.rk[r1] - f.rk[r0]; f.c_nu[g] = U; f.c_no[g] = f.ro[r1] - f.ro[r0]; }
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if ((uint32_t)q < per && ((fl >> q) & 1u)) { A[p] = x[q]; f.m_vals[f.val_out[g] + p] = x[q]; ++p; }
+    __syncthreads();
+    fuse_emit(f, g, A, U, tid, NT);
 }
 
 template <bool WRITE>
@@ -426,15 +477,18 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     fz.c_no = ctx->get<uint64_t>("shm_c_no", n_groups);
     fz.blk_list = ctx->get<uint32_t>("shm_blk", n_groups);
     fz.glb_list = ctx->get<uint32_t>("shm_glb", n_groups);
-    fz.gstat = ctx->get<uint64_t>("shm_gstat", 4);
-    ACC_HIP(hipMemsetAsync(fz.gstat, 0, 4 * 8, st));
+    fz.big_list = ctx->get<uint32_t>("shm_big", n_groups);
+    fz.gstat = ctx->get<uint64_t>("shm_gstat", 5);
+    ACC_HIP(hipMemsetAsync(fz.gstat, 0, 5 * 8, st));
     const unsigned gw = (n_groups + WAVES - 1) / WAVES;
     launch(ctx, "shm_fuse_wave_sizes", k_fuse_wave<false>, dim3(gw), dim3(BLOCK), 0, fz);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 8, hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, fz.gstat, 4 * 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, fz.gstat, 5 * 8, hipMemcpyDeviceToHost, st));
     ctx->sync();
     if (ctx->pinned[0]) fail(ACC_E_ARG, "received a fragment for a txn that is not homed on this rank");
-    const uint64_t nblk = ctx->pinned[1], nglb = ctx->pinned[2], glb_elems = ctx->pinned[3];
+    const uint64_t nblk = ctx->pinned[1], nglb = ctx->pinned[2], glb_elems = ctx->pinned[3], nbig = ctx->pinned[5];
+    ctx->stat("shard.big_groups", nbig);
+    ctx->stat("shard.global_groups", nglb);
     if (ctx->pinned[4]) {
         // replies of a txn are not in ascending disjoint key order (not a key-range split): general merge
         ctx->stat("shard.general_merge", 1);
@@ -444,6 +498,7 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     }
     ctx->stat("shard.general_merge", 0);
     if (nblk) launch(ctx, "shm_fuse_block_sizes", k_fuse_block<false>, dim3((unsigned)nblk), dim3(BLOCK), 0, fz);
+    if (nbig) launch(ctx, "shm_fuse_big_sizes", k_fuse_big<false>, dim3((unsigned)nbig), dim3(1024), 0, fz);
     if (nglb) {
         uint64_t *gsz = ctx->get<uint64_t>("shm_glb_sz", nglb);
         uint64_t *goff = ctx->get<uint64_t>("shm_glb_off", nglb + 1);
@@ -468,6 +523,7 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     fz.m_k2v = ctx->get<int32_t>("shm_k2v", NO);
     launch(ctx, "shm_fuse_wave", k_fuse_wave<true>, dim3(gw), dim3(BLOCK), 0, fz);
     if (nblk) launch(ctx, "shm_fuse_block", k_fuse_block<true>, dim3((unsigned)nblk), dim3(BLOCK), 0, fz);
+    if (nbig) launch(ctx, "shm_fuse_big", k_fuse_big<true>, dim3((unsigned)nbig), dim3(1024), 0, fz);
     if (nglb) launch(ctx, "shm_fuse_global", k_fuse_global<true>, dim3((unsigned)nglb), dim3(BLOCK), 0, fz);
     ctx->sync();
     *view = acc_merge_view{ n_groups, NK, NU, NO, NO, key_out, fz.m_keys, val_out, fz.m_vals, k2v_out, fz.m_k2v };

@@ -26,11 +26,34 @@ def _check_home(merged, expect, label):
 def test_shard_reduce_single_process(world, store_local, reverse):
     """reverse: sources concatenated in descending shard order, so a txn's replies are not in ascending key order
     and the fused reduce must hand over to the general KeyDeps.merge (same canonical result)."""
+    b = W.keydeps_batch(20000, 8, 20000, 0x5EED + world, "zipf", 0.99, status_model="model", window=2000)
+    _run_single(b, world, store_local, reverse)
+
+
+def test_shard_reduce_big_groups():
+    """Home txns whose replies carry 8192..32768 TxnIds (the 1024-thread fused-reduce tier): a hot key of committed
+    Reads closed by PREACCEPTED Writes that depend on all of them."""
+    def set_kind(idx, kind):
+        b.txn_lsb[idx] = (b.txn_lsb[idx] & ~np.uint64(0xE)) | np.uint64(kind << 1)
+        b.exe_msb[idx], b.exe_lsb[idx], b.exe_node[idx] = b.txn_msb[idx], b.txn_lsb[idx], b.txn_node[idx]
+    b = W.keydeps_batch(60000, 1, 1_000_000, 0xB16, "uniform", status_model="model", window=0)
+    hot = np.arange(0, b.n_txn, 4)
+    b.key_code[hot] = W.int_key_code(np.array([1 << 30]))[0]
+    set_kind(hot, W.READ)
+    b.status[hot] = W.APPLIED
+    last = hot[-3:]
+    set_kind(last, W.WRITE)
+    b.status[last] = W.PREACCEPTED
+    stats = _run_single(b, 2, True, False)
+    assert stats["shard.big_groups"] > 0
+
+
+def _run_single(b, world, store_local, reverse):
     import torch
     from accord_amd import sharded as S
     from accord_amd.deps import Context
     dev = torch.device("cuda", 0)
-    b = W.keydeps_batch(20000, 8, 20000, 0x5EED + world, "zipf", 0.99, status_model="model", window=2000)
+    stats = {}
     with Context(0) as ctx:
         full = ctx.calculate_partial_deps(b)
         bounds = S.even_split(b.key_code, world)
@@ -63,6 +86,9 @@ def test_shard_reduce_single_process(world, store_local, reverse):
             merged = S.merged_to_host(ctx, view)
             _check_home(merged, S.home_result_from_full(full, b, h, world), f"world {world} home {h}")
             assert ctx.stats()["shard.general_merge"] == (1 if reverse and world > 1 else 0)
+            for k, v in ctx.stats().items():
+                stats[k] = max(stats.get(k, 0), v)
+    return stats
 
 
 def _free_port():
