@@ -37,6 +37,7 @@ __global__ __launch_bounds__(BLOCK) void k_lv_check(uint32_t n, const uint64_t *
 // LDS (n <= LV_LDS_MAX); otherwise levels are global (agent-scope atomics bypass the non-coherent L1) and
 // exec ranks are read from global.
 constexpr int LV_THREADS = 1024;
+constexpr int LV_UNROLL = 4;
 constexpr uint32_t LV_LDS_MAX = 20000;   // 8 B/txn of the 160 KiB LDS
 
 template <bool kLds>
@@ -64,13 +65,13 @@ __global__ __launch_bounds__(LV_THREADS) void k_lv_walk(uint32_t n, const uint32
     while (__any(i < n)) {
         if (i < n) {
             bool pending = false;
-            // four deps per round: independent loads in flight together
+            // LV_UNROLL deps per round: independent global loads in flight together
             while (cur < b && !pending) {
-                uint32_t dd[4];
+                uint32_t dd[LV_UNROLL];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) dd[q] = cur + q < b ? dep[cur + q] : 0xFFFFFFFFu;
+                for (int q = 0; q < LV_UNROLL; ++q) dd[q] = cur + q < b ? dep[cur + q] : 0xFFFFFFFFu;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < LV_UNROLL; ++q) {
                     if (pending || dd[q] == 0xFFFFFFFFu) continue;
                     if (er_col[dd[q]] >= er) { ++cur; continue; }
                     uint32_t v = ld(dd[q]);
