@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bench: batched Accord dependency calculation on MI355X through the C ABI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -9,6 +9,9 @@
 1M keys, read/write mix, status model of SURVEY.md §8(d). A step = one acc_keydeps_batch over the whole batch
 (PreAccept.calculatePartialDeps for every txn of a CommandsForKey snapshot) with inputs already resident in HBM
 (device pointers) and results left device-resident (acc_keydeps_view).
+--config 3 (configs[2]): 100M txn-key pairs (12.5M txns x 8 keys, zipf(0.99) over 2^24 keys, status model): on one GPU
+one acc_keydeps_batch over the whole batch; at N > 1 the same global batch range-sharded over the N GPUs (strong
+scaling) through the multi-GPU path below.
 --config 4 (configs[3]): RangeDeps of 10M range txns (1 EndInclusive range each, log-uniform widths <= 2^16)
 interleaved with 10M key txns x 4 keys over the int32 key space; a step = one acc_rangedeps_batch.
 --config 5 (configs[4]): KeyDeps.merge of 16,384 coordinated txns x 64 replica replies, then acc_levelise of the
@@ -50,12 +53,13 @@ def rangedeps_bytes(n_txn, n_pairs, n_ranges, sum_rd, sum_e, sum_u, n_dict):
     return b_in, b_out
 
 
-def profile_traffic(kernel):
+def profile_traffic(kernel, config=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprof summary (profiles/*_summary.json: FETCH_SIZE
     x 2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+    pattern = f"*_config{config}_summary.json" if config else "*_summary.json"
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
         try:
             d = json.load(open(p))
         except Exception:
@@ -66,7 +70,7 @@ def profile_traffic(kernel):
     return best
 
 
-def roofline(step_bytes, timing, steps):
+def roofline(step_bytes, timing, steps, config=None):
     """Contract roofline for the dominant kernel: achieved = algorithmic bytes of the batch one launch processes /
     that kernel's average launch (HIP events on the context stream). step_* = the same bytes over the device time of
     every kernel of the step (the whole pipeline as one launch: the stricter figure)."""
@@ -75,7 +79,7 @@ def roofline(step_bytes, timing, steps):
     dom_avg_ms = dom_total / max(dom_launches, 1)
     achieved = step_bytes / (dom_avg_ms / 1000.0) / 1e9
     step_achieved = step_bytes / (kernel_ms / 1000.0) / 1e9
-    tr = profile_traffic(dom_name)
+    tr = profile_traffic(dom_name, config)
     return {
         "bound": "hbm",
         "kernel": dom_name,
@@ -183,9 +187,11 @@ def run_config2(args, world, rank, local, dev):
     from accord_amd import workload as W
     from accord_amd.deps import Context
 
-    seed = W.CONFIG_SEEDS["2"] + 0x1000 * rank
-    n_txn = int(1_000_000 * args.scale)
-    batch = W.keydeps_batch(n_txn, 8, max(1000, n_txn), seed, "zipf", 0.99, status_model="model")
+    c3 = args.config == "3"
+    seed = W.CONFIG_SEEDS["3z" if c3 else "2"] + 0x1000 * rank
+    n_txn = int((12_500_000 if c3 else 1_000_000) * args.scale)
+    n_keys = int((1 << 24) * args.scale) if c3 else n_txn
+    batch = W.keydeps_batch(n_txn, 8, max(1000, n_keys), seed, "zipf", 0.99, status_model="model")
     t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in batch.arrays().items()}
     torch.cuda.synchronize()
     bi = L.BatchIn(batch.n_txn, L.ACC_MEM_DEVICE, batch.n_pairs,
@@ -205,17 +211,19 @@ def run_config2(args, world, rank, local, dev):
         "dtype": "u32/u64 (integer)",
         "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) status model)",
         "config": {
-            "workload": "config2: KeyDeps batch, 1M txns x 8 keys, zipf(0.99) over 1M keys, p_write 0.5, "
-                        "uncommitted window 10k, per-GPU CommandStore snapshot",
+            "workload": ("config3 on one GPU: KeyDeps batch of 100M txn-key pairs (12.5M txns x 8 keys), zipf(0.99) "
+                         "over 2^24 keys, p_write 0.5, uncommitted window 10k, one CommandStore snapshot") if c3 else
+                        ("config2: KeyDeps batch, 1M txns x 8 keys, zipf(0.99) over 1M keys, p_write 0.5, "
+                         "uncommitted window 10k, per-GPU CommandStore snapshot"),
             "n_txn_per_gpu": batch.n_txn,
             "pairs_per_gpu": batch.n_pairs,
             "dep_edges_per_gpu": int(view.total_edges),
             "parallelism": f"keyspace shards x{world} (independent CommandStores)",
         },
         "dep_edges_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
-        "roofline": roofline(b_in + b_out, timing, args.steps),
+        "roofline": roofline(b_in + b_out, timing, args.steps, args.config),
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not c3:   # config 3: the O(prefix) CPU scan takes hours
         result["cpu_baseline"] = keydeps_cpu_baseline(batch)
     return ctx, timing, elapsed, result
 
@@ -226,8 +234,11 @@ def run_config2_sharded(args, world, rank, local, dev):
     from accord_amd import workload as W
     from accord_amd.deps import Context
 
-    n_global = int(1_000_000 * args.scale) * world
-    batch = W.keydeps_batch(n_global, 8, max(1000, n_global), W.CONFIG_SEEDS["2"], "zipf", 0.99, status_model="model")
+    c3 = args.config == "3"   # config 3: 100M pairs in total over the N GPUs (strong scaling); else N x config 2
+    n_global = int(12_500_000 * args.scale) if c3 else int(1_000_000 * args.scale) * world
+    n_keys = int((1 << 24) * args.scale) if c3 else n_global
+    batch = W.keydeps_batch(n_global, 8, max(1000, n_keys), W.CONFIG_SEEDS["3z" if c3 else "2"], "zipf", 0.99,
+                            status_model="model")
     bounds = S.even_split(batch.key_code, world)
     sub, g = S.store_batch(batch, bounds, rank)
     bi, keep = S.batch_in_device(sub, dev)
@@ -266,8 +277,8 @@ def run_config2_sharded(args, world, rank, local, dev):
         "dtype": "u32/u64 (integer)",
         "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) status model)",
         "config": {
-            "workload": f"config2 x{world} range-sharded (config-3 shape): KeyDeps of {n_global} txns x 8 keys, "
-                        f"zipf(0.99) over {n_global} keys, key ranges EvenSplit over {world} GPUs (one CommandStore each), "
+            "workload": f"{'config3' if c3 else f'config2 x{world}'} range-sharded: KeyDeps of {n_global} txns x 8 keys, "
+                        f"zipf(0.99) over {n_keys} keys, key ranges EvenSplit over {world} GPUs (one CommandStore each), "
                         "PreAccept.reduce of per-store PartialDeps by RCCL all-to-all(v) + on-device KeyDeps.merge",
             "n_txn_global": n_global,
             "pairs_global": n_global * 8,
@@ -276,7 +287,7 @@ def run_config2_sharded(args, world, rank, local, dev):
         },
         "exchange": {"bytes_sent_total": int(tot[1].item()), "bytes_sent_max_rank": int(mx[1].item()),
                      "backend": dist.get_backend() + (" (RCCL over xGMI)" if dist.get_backend() == "nccl" else "")},
-        "roofline": roofline(b_in + b_out, timing, args.steps),
+        "roofline": roofline(b_in + b_out, timing, args.steps, args.config),
     }
     return ctx, timing, elapsed, result
 
@@ -320,7 +331,7 @@ def run_config4(args, world, rank, local, dev):
             "parallelism": f"keyspace shards x{world} (independent CommandStores)",
         },
         "dep_entries_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
-        "roofline": roofline(b_in + b_out, timing, args.steps),
+        "roofline": roofline(b_in + b_out, timing, args.steps, args.config),
     }
     if os.environ.get("ACC_BENCH_MIXED", "1") != "0":
         result["keydeps_mixed"] = mixed_keydeps_leg(bi, local)
@@ -441,7 +452,7 @@ def run_config5(args, world, rank, local, dev):
             "levels": int(nl[0]),
             "parallelism": f"independent coordinators x{world}",
         },
-        "roofline": roofline(merge_bytes(m, view, n_txn, int(view.total_vals)), timing, args.steps),
+        "roofline": roofline(merge_bytes(m, view, n_txn, int(view.total_vals)), timing, args.steps, args.config),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = merge_cpu_baseline(m, exec_rank, n_in)
@@ -453,13 +464,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="2", choices=["2", "4", "5"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4", "5"])
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config (testing only)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
     world, rank, local, dev = dist_setup(args)
-    run = {"2": run_config2 if world == 1 else run_config2_sharded, "4": run_config4, "5": run_config5}[args.config]
+    keyed = run_config2 if world == 1 else run_config2_sharded
+    run = {"2": keyed, "3": keyed, "4": run_config4, "5": run_config5}[args.config]
     ctx, timing, elapsed, result = run(args, world, rank, local, dev)
     out = {
         "metric": result.pop("metric"),
@@ -470,7 +482,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1000.0 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == "3" and world > 1 else "weak",
         "vs_baseline": None,
     }
     out.update(result)
