@@ -325,8 +325,17 @@ __global__ __launch_bounds__(BLOCK) void k_txn_info(uint32_t n, const uint32_t *
     tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), 0u);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, const uint32_t *__restrict__ perm, const uint32_t *__restrict__ owner,
-                                                      const uint4 *__restrict__ tinfo, const uint32_t *__restrict__ seg_incl,
+// per-pair copy of its txn's record, written in pair order (owner[] is monotone, so both reads stream): the CFK
+// gather then does ONE random 16-B read per pair instead of the dependent owner[j] -> tinfo[owner[j]] pair
+__global__ __launch_bounds__(BLOCK) void k_pair_tinfo(size_t P, const uint32_t *__restrict__ owner, const uint4 *__restrict__ tinfo,
+                                                      uint4 *__restrict__ ptinfo)
+{
+    size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j < P) ptinfo[j] = tinfo[owner[j]];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, const uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
+                                                      const uint32_t *__restrict__ seg_incl,
                                                       const uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ seg_start,
                                                       uint32_t *__restrict__ s_rank, uint32_t *__restrict__ s_exec,
                                                       uint8_t *__restrict__ s_info, uint32_t *__restrict__ pair_pos)
@@ -334,14 +343,22 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, const uint32_t *
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
     uint32_t j = perm[p];
-    uint4 ti = tinfo[owner[j]];
+    uint4 ti = ptinfo[j];
     uint32_t seg = seg_incl[p] - 1;
     if (seg_flag[p]) seg_start[seg] = (uint32_t)p;
     if (p == P - 1) seg_start[seg + 1] = (uint32_t)P;
     s_rank[p] = ti.x;
     s_exec[p] = ti.y;
     s_info[p] = (uint8_t)ti.z;
-    pair_pos[j] = (uint32_t)p;
+    if (pair_pos) pair_pos[j] = (uint32_t)p;
+}
+
+// inverse of the CFK permutation, only for the consumers that address pairs by index (exact replay, the global
+// write tier, the range-domain KeyDeps): a random 4-B scatter per pair the common path does not pay
+__global__ __launch_bounds__(BLOCK) void k_pair_pos(size_t P, const uint32_t *__restrict__ perm, uint32_t *__restrict__ pair_pos)
+{
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p < P) pair_pos[perm[p]] = (uint32_t)p;
 }
 
 // v1 only: committed / uncommitted flags and the segmented prefix-max input
@@ -1996,9 +2013,17 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
     uint4 *tinfo = ctx->get<uint4>("tinfo", n);
     launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
-    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals,
-           (const uint32_t *)owner, (const uint4 *)tinfo, (const uint32_t *)seg_incl,
-           (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info, pair_pos);
+    uint4 *ptinfo = ctx->get<uint4>("pair_tinfo", P);
+    launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
+    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, (const uint4 *)ptinfo,
+           (const uint32_t *)seg_incl, (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info,
+           ks ? pair_pos : (uint32_t *)nullptr);
+    bool have_pair_pos = ks != nullptr;
+    auto need_pair_pos = [&]() {
+        if (have_pair_pos) return;
+        launch(ctx, "pair_pos", k_pair_pos, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, pair_pos);
+        have_pair_pos = true;
+    };
     const int segbits = bits_for(P);
     // ---- v2 structures (class lists, prefix counts, bumped committed list)
     const uint32_t nt = (uint32_t)((P + V2_TILE - 1) / V2_TILE);
@@ -2040,6 +2065,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ks->tl = tl; ks->key_code = key_code; ks->g = g;
     }
     if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
+        need_pair_pos();
         keydeps_v1_tail(ctx, view, n, P, rbits, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
                         s_rank, s_exec, s_info, pair_pos, ks);
         return;
@@ -2145,6 +2171,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ctx->stat("keydeps.fallback_entries", efb);
     ctx->stat("keydeps.bumped_committed", nbc);
     if (nfb) {
+        need_pair_pos();
         // txns whose dependency-rank range exceeds the bitmap tier (or > 64 keys): gather to global memory,
         // sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
         uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
