@@ -50,6 +50,11 @@ void acc_destroy(acc_ctx *ctx)
     for (void *p : ctx->graveyard) (void)hipFree(p);
     for (auto &p : ctx->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < acc_ctx::NAUX; ++i) {
+        if (ctx->aux[i]) { (void)hipStreamSynchronize(ctx->aux[i]); (void)hipStreamDestroy(ctx->aux[i]); }
+        if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+    }
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -52,6 +52,15 @@ struct PendingEvent {
 struct acc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // side streams for independent launches (the KeyDeps write tiers): forked from / joined into `stream`
+    static constexpr int NAUX = 3;
+    hipStream_t aux[NAUX] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
+    hipStream_t launch_stream = nullptr;   // where acc::launch enqueues (nullptr = `stream`)
+    // decoupled look-back scan status, double buffered: each scan zeroes the words the previous scan dirtied in
+    // the other buffer, so no memset launch precedes a scan (acc::scan, prims.hpp)
+    size_t scan_cap = 0, scan_dirty[2] = {0, 0};
+    int scan_par = 0;
     uint32_t flags = 0;
     std::string last_error;
     std::unordered_map<std::string, acc::Buf> bufs;
@@ -134,6 +143,31 @@ struct acc_ctx {
         pending.clear();
     }
 
+    hipStream_t cur() const { return launch_stream ? launch_stream : stream; }
+
+    // aux streams 0..k-1 wait for everything enqueued on the main stream so far
+    void fork(int k)
+    {
+        if (!fork_ev) {
+            ACC_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+            for (int i = 0; i < NAUX; ++i) {
+                ACC_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
+                ACC_HIP(hipEventCreateWithFlags(&join_ev[i], hipEventDisableTiming));
+            }
+        }
+        ACC_HIP(hipEventRecord(fork_ev, stream));
+        for (int i = 0; i < k; ++i) ACC_HIP(hipStreamWaitEvent(aux[i], fork_ev, 0));
+    }
+    // the main stream waits for aux streams 0..k-1
+    void join(int k)
+    {
+        for (int i = 0; i < k; ++i) {
+            ACC_HIP(hipEventRecord(join_ev[i], aux[i]));
+            ACC_HIP(hipStreamWaitEvent(stream, join_ev[i], 0));
+        }
+        launch_stream = nullptr;
+    }
+
     void sync()
     {
         ACC_HIP(hipStreamSynchronize(stream));
@@ -145,7 +179,7 @@ struct acc_ctx {
 
 namespace acc {
 
-// Launch a kernel on the context stream; with ACC_OPT_TIMING, bracket it with HIP events recorded on
+// Launch a kernel on the context stream (or the side stream selected by launch_stream); with ACC_OPT_TIMING, bracket it with HIP events recorded on
 // that same stream (so the interval is the kernel's own device time).
 template <class K, class... Args>
 inline void launch(acc_ctx *ctx, const char *name, K kernel, dim3 grid, dim3 block, size_t shmem, Args... args)
@@ -157,12 +191,12 @@ inline void launch(acc_ctx *ctx, const char *name, K kernel, dim3 grid, dim3 blo
         pe.slot = ctx->slot(name);
         pe.start = ctx->take_event();
         pe.stop = ctx->take_event();
-        ACC_HIP(hipEventRecord(pe.start, ctx->stream));
+        ACC_HIP(hipEventRecord(pe.start, ctx->cur()));
     }
-    hipLaunchKernelGGL(kernel, grid, block, shmem, ctx->stream, args...);
+    hipLaunchKernelGGL(kernel, grid, block, shmem, ctx->cur(), args...);
     ACC_HIP(hipGetLastError());
     if (timed) {
-        ACC_HIP(hipEventRecord(pe.stop, ctx->stream));
+        ACC_HIP(hipEventRecord(pe.stop, ctx->cur()));
         ctx->pending.push_back(pe);
     }
 }

@@ -2134,6 +2134,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
     wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
     wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig + 1);
+    // Tiers run back to back on the context stream. Side streams (acc_ctx::fork/join) were measured at -2% step time
+    // on config 2 but stretch every tier's own duration, which hides the per-kernel roofline attribution.
     launch(ctx, "v2_write_g16", k_v2_write_group<16, false>, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n,
            (const uint32_t *)nullptr, vv, (const uint64_t *)cnt, wo);
     if (ng32)
@@ -2150,7 +2152,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                (const uint32_t *)big_list, vv, (const uint64_t *)cnt, wo);
         launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3((unsigned)nbig), dim3(1024), 0, (uint32_t)nbig,
                (const uint32_t *)wo.huge_list, vv, (const uint64_t *)cnt, wo);
-    } else if (nbig) {
+    }
+    if (nbig && !(rbits + 6 <= 31)) {
         // ranks beyond 25 bits: every big txn takes the global path
         launch(ctx, "v2_route_fb", k_v2_route_fb, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, (uint32_t)nbig,
                (const uint32_t *)big_list, key_off, (const uint64_t *)dep_off, fb_list, gstat);

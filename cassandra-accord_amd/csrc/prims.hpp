@@ -161,7 +161,7 @@ __device__ __forceinline__ uint64_t scan_status_load(const uint64_t *p)
 template <class T, class Op, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *__restrict__ out, size_t n, int exclusive,
                                                  T *__restrict__ total_out, uint32_t *__restrict__ ticket,
-                                                 uint64_t *__restrict__ status)
+                                                 uint64_t *__restrict__ status, uint64_t *__restrict__ other, uint32_t other_n)
 {
     constexpr int TILE = BLOCK * ITEMS;
     __shared__ T tile[TILE + TILE / 32];
@@ -169,6 +169,11 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
     __shared__ uint32_t s_b;
     __shared__ T s_prefix;
     const uint32_t tid = threadIdx.x, lane = lane_id();
+    if (other_n) {   // reset the other status buffer for the next scan (it is not read by this one)
+        const uint32_t chunk = (other_n + gridDim.x - 1) / gridDim.x;
+        const uint32_t lo = blockIdx.x * chunk, hi = min(other_n, lo + chunk);
+        for (uint32_t i = lo + tid; i < hi; i += BLOCK) other[i] = 0;
+    }
     if (tid == 0) s_b = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t b = s_b;
@@ -253,11 +258,28 @@ void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_
     }
     const size_t nb = (n + TILE - 1) / TILE;
     if (nb > 0xFFFFFFFFull) fail(ACC_E_CAP, "scan too large");
-    uint64_t *status = ctx->get<uint64_t>("scan_status", nb + 1);
+    // stream order is what makes the double-buffered status safe: every scan runs on the context stream
+    if (ctx->launch_stream) fail(ACC_E_STATE, "internal: scan launched on a side stream");
+    const size_t need = nb + 1;
+    uint64_t *buf[2];
+    if (need > ctx->scan_cap) {
+        for (int i = 0; i < 2; ++i) {
+            buf[i] = ctx->get<uint64_t>(i ? "scan_status1" : "scan_status0", need);
+            ACC_HIP(hipMemsetAsync(buf[i], 0, need * sizeof(uint64_t), ctx->stream));
+        }
+        ctx->scan_cap = need;
+        ctx->scan_dirty[0] = ctx->scan_dirty[1] = 0;
+    } else {
+        for (int i = 0; i < 2; ++i) buf[i] = ctx->get<uint64_t>(i ? "scan_status1" : "scan_status0", need);
+    }
+    const int p = ctx->scan_par;
+    uint64_t *status = buf[p];
     uint32_t *ticket = reinterpret_cast<uint32_t *>(status + nb);
-    ACC_HIP(hipMemsetAsync(status, 0, (nb + 1) * sizeof(uint64_t), ctx->stream));
     launch(ctx, "scan", k_scan_1p<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, out, n, (int)exclusive, total_out,
-           ticket, status);
+           ticket, status, buf[p ^ 1], (uint32_t)ctx->scan_dirty[p ^ 1]);
+    ctx->scan_dirty[p] = need;
+    ctx->scan_dirty[p ^ 1] = 0;
+    ctx->scan_par = p ^ 1;
 }
 
 // ---------------------------------------------------------------- bit compaction plan

@@ -921,16 +921,17 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     o.s_rid = ctx->get<uint32_t>("rd_s_rid", E);
     o.s_dep = ctx->get<uint32_t>("rd_s_dep", E);
     const uint32_t *tl_sorted = ts.vals;
+    // tiers own disjoint txns (disjoint scratch): LDS workgroup tiers on side stream 1, 16-lane groups on side
+    // stream 0, waves on the main stream, all concurrently
+    ctx->fork(2);
     if (hh[1]) {
+        ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[1];
         launch(ctx, "rd_build_s16", k_rd_build_seg<16>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
     }
-    if (hh[2]) {
-        o.list = tl_sorted + toff[2];
-        launch(ctx, "rd_build_s64", k_rd_build_seg<64>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
-    }
     uint64_t nblk = 0;
-    for (int b = 3; b <= 9; ++b) {
+    ctx->launch_stream = ctx->aux[1];
+    for (int b = 9; b >= 3; --b) {
         if (!hh[b]) continue;
         const uint32_t n2 = 128u << (b - 3);
         const size_t lds = 2 * (size_t)n2 * sizeof(uint64_t) + 64;
@@ -940,6 +941,12 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
         launch(ctx, "rd_build_block", k_rd_build_block, dim3(hh[b]), dim3(BLOCK), lds, o, n2);
         nblk += hh[b];
     }
+    ctx->launch_stream = nullptr;
+    if (hh[2]) {
+        o.list = tl_sorted + toff[2];
+        launch(ctx, "rd_build_s64", k_rd_build_seg<64>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+    }
+    ctx->join(2);
     const uint32_t nglb = hh[10];
     if (nglb) {
         o.list = tl_sorted + toff[10];

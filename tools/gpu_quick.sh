@@ -8,7 +8,7 @@ sel=${1:-}
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${sel:+-k "$sel"} \
     > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed $?"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/gpu_tests.log
-for cfg in 2 3; do
+for cfg in ${CFGS:-2 3}; do
     ACC_BENCH_KERNELS=1 timeout -k 10 400 python -u bench.py --config $cfg --no-cpu > gpurun_out/bench_c$cfg.log 2>&1 \
         || { echo "bench c$cfg failed"; tail -30 gpurun_out/bench_c$cfg.log; exit 1; }
     python -c "
