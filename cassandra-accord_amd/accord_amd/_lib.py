@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libaccord_amd.so")
+# ACC_LIB_PATH: another build of the same library (A/B timing of two kernel variants in one GPU session)
+LIB_PATH = os.environ.get("ACC_LIB_PATH") or os.path.join(HERE, "libaccord_amd.so")
 
 ACC_OK, ACC_E_ARG, ACC_E_STATE, ACC_E_NOMEM, ACC_E_DEVICE, ACC_E_CAP = 0, -1, -2, -3, -4, -5
 ACC_MEM_HOST, ACC_MEM_DEVICE = 0, 1

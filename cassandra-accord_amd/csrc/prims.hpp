@@ -250,7 +250,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
 template <class T, class Op>
 void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr)
 {
-    constexpr int ITEMS = sizeof(T) == 8 ? 4 : 8;
+    constexpr int ITEMS = sizeof(T) == 8 ? 16 : 32;   // 4096 / 8192-element tiles: fewer look-back hops
     constexpr size_t TILE = (size_t)BLOCK * ITEMS;
     if (n == 0) {
         if (total_out) ACC_HIP(hipMemsetAsync(total_out, 0, sizeof(T), ctx->stream));
