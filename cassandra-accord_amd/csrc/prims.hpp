@@ -354,18 +354,31 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_hist(const uint64_t *__rest
 }
 
 // Stable scatter: element order inside a tile is (k, wave, lane); ranks come from 8 ballots per
-// wave (peer mask of equal digits) plus a per-digit running count across waves and k steps.
+// wave (peer mask of equal digits) plus a per-digit running count across waves and k steps. The tile is first
+// reordered by digit in LDS (48 KiB: keys + values), then written out digit run by digit run, so neighbouring
+// lanes store to neighbouring addresses (~16 elements per digit per tile) instead of one element per digit.
 static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       size_t n, int shift, const uint32_t *__restrict__ hist_scanned,
                                                       uint32_t ntiles, int iota_vals)
 {
+    __shared__ uint64_t sk[RS_TILE];
+    __shared__ uint32_t sv[RS_TILE];
     __shared__ uint32_t cnt[WAVES][256];
     __shared__ uint32_t wpre[WAVES][256];
-    __shared__ uint32_t run[256];
+    __shared__ uint32_t run[256], lbase[256], gbase[256];
+    __shared__ uint32_t red[WAVES];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    run[tid] = hist_scanned[(size_t)tid * ntiles + blockIdx.x];
+    // this tile's count of digit tid = difference of neighbouring entries of the exclusive (digit, tile) scan
+    const size_t hi = (size_t)tid * ntiles + blockIdx.x;
+    const uint32_t g0 = hist_scanned[hi];
+    const uint32_t g1 = hi + 1 < (size_t)256 * ntiles ? hist_scanned[hi + 1] : (uint32_t)n;
+    uint32_t tile_total;
+    const uint32_t lb = block_exclusive(g1 - g0, OpAdd<uint32_t>(), red, tile_total);
+    lbase[tid] = lb;
+    gbase[tid] = g0;
+    run[tid] = lb;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) cnt[w][tid] = 0;
     __syncthreads();
@@ -398,9 +411,17 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__r
         __syncthreads();
         if (valid) {
             uint32_t dst = wpre[wave][d] + rank;
-            kout[dst] = key;
-            vout[dst] = val;
+            sk[dst] = key;
+            sv[dst] = val;
         }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < tile_total; i += BLOCK) {
+        const uint64_t key = sk[i];
+        const uint32_t d = (uint32_t)(key >> shift) & 255u;
+        const uint32_t dst = gbase[d] + (i - lbase[d]);
+        kout[dst] = key;
+        vout[dst] = sv[i];
     }
 }
 
