@@ -841,6 +841,41 @@ __global__ __launch_bounds__(BLOCK) void k_v2_bcs_cols(uint32_t nbc, const uint6
     lastw_in[i] = bc_kind[svals[i]] == 1 ? i + 1 : 0;
 }
 
+// The eight per-tile column scans of the multi-scan (7 counts: exclusive sums; the last-unbumped-committed-Write
+// column: exclusive max) in ONE launch, one workgroup per column, carrying the running value across chunks.
+constexpr int V2TS_ITEMS = 32;
+__global__ __launch_bounds__(BLOCK) void k_v2_tile_scans(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t nt,
+                                                         uint32_t *__restrict__ totals)
+{
+    __shared__ uint32_t red[WAVES];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    const bool mx = q == 7;
+    const uint32_t *a = in + (size_t)q * nt;
+    uint32_t *o = out + (size_t)q * nt;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nt; base += BLOCK * V2TS_ITEMS) {
+        uint32_t v[V2TS_ITEMS];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < V2TS_ITEMS; ++i) {
+            const uint32_t idx = base + tid * V2TS_ITEMS + i;
+            v[i] = idx < nt ? a[idx] : 0u;
+            acc = mx ? max(acc, v[i]) : acc + v[i];
+        }
+        uint32_t tot;
+        const uint32_t pre = mx ? block_exclusive(acc, OpMax<uint32_t>(), red, tot) : block_exclusive(acc, OpAdd<uint32_t>(), red, tot);
+        uint32_t run = mx ? max(carry, pre) : carry + pre;
+#pragma unroll
+        for (int i = 0; i < V2TS_ITEMS; ++i) {
+            const uint32_t idx = base + tid * V2TS_ITEMS + i;
+            if (idx < nt) o[idx] = run;
+            run = mx ? max(run, v[i]) : run + v[i];
+        }
+        carry = mx ? max(carry, tot) : carry + tot;
+    }
+    if (tid == 0) totals[q] = carry;
+}
+
 struct V2View {
     const uint32_t *perm, *pair_pos, *seg_incl, *seg_start, *s_rank, *s_exec;
     const uint8_t *s_info;
@@ -2033,9 +2068,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *bases = ctx->get<uint32_t>("v2_bases", 16);
     launch(ctx, "v2_reduce", k_v2_reduce, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
            (const uint8_t *)s_info, tile_sums, nt);
-    for (int q = 0; q < 7; ++q)
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, tile_sums + (size_t)q * nt, tile_pref + (size_t)q * nt, nt, true, totals + q);
-    scan<uint32_t, OpMax<uint32_t>>(ctx, tile_sums + (size_t)7 * nt, tile_pref + (size_t)7 * nt, nt, true, totals + 7);
+    launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
     launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
     V2Cols cols;
     cols.rows = ctx->get<uint4>("v2_rows", 2 * (P + 1));
