@@ -238,3 +238,24 @@ def test_config2_sample_and_properties(ctx):
     last_hdr = g.arena[(g.arena_off[:-1].astype(np.int64) + kd - 1)[nz]]
     np.testing.assert_array_equal(last_hdr, al[nz])
     assert int(g.total_edges) == int(al.sum() - kd.sum())
+
+
+def test_runs_vs_replay_beyond_one_scan_chunk():
+    """9.6M pairs (> 8192 tiles of 1024 positions): the per-tile column scans carry across chunks. The run-based
+    path is compared bit-for-bit with the independent FAST-bisection replay path on every txn, and with the oracle on
+    a sample of the hottest (latest) txns."""
+    import oracle
+    from accord_amd.deps import Context
+    b = W.keydeps_batch(1_200_000, 8, 1_200_000, 0xC4A1, "zipf", 0.99, status_model="model")
+    assert b.n_pairs > 8192 * 1024
+    with Context(0) as c:
+        g = c.calculate_partial_deps(b)
+        assert c.stats().get("keydeps.path_replay", 0) == 0
+    with Context(0, force_replay=True) as c:
+        r = c.calculate_partial_deps(b)
+    assert_same(g, r, b.n_txn, "runs vs replay")
+    n = b.n_txn
+    o = oracle.keydeps_batch(b, query_lo=n - 200, query_hi=n)
+    for t in range(n - 200, n):
+        for x, y, what in zip(g.txn(t), o.txn(t), ("keys", "txnIds", "keysToTxnIds")):
+            np.testing.assert_array_equal(x, y, err_msg=f"txn {t} {what}")
