@@ -1690,12 +1690,14 @@ __global__ __launch_bounds__(BLOCK) void k_v2_compact(uint32_t n, const uint32_t
                                                       const uint64_t *__restrict__ u_off, const uint32_t *__restrict__ dep_scratch,
                                                       uint32_t *__restrict__ dep_txn)
 {
-    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t t = blockIdx.x * WAVES + wave;
+    // 16 lanes per txn (a txn has ~33 TxnIds on config 2: a whole wave per txn left most lanes idle)
+    constexpr uint32_t G = 16;
+    const uint32_t g = threadIdx.x & (G - 1);
+    const uint32_t t = blockIdx.x * (BLOCK / G) + threadIdx.x / G;
     if (t >= n) return;
     uint64_t src = dep_off[key_off[t]];
     uint64_t dst = u_off[t], len = u_off[t + 1] - dst;
-    for (uint64_t i = lane; i < len; i += 64) dep_txn[dst + i] = dep_scratch[src + i];
+    for (uint64_t i = g; i < len; i += G) dep_txn[dst + i] = dep_scratch[src + i];
 }
 
 // ---------------------------------------------------------------- host orchestration
@@ -2240,7 +2242,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
     uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
-    launch(ctx, "v2_compact", k_v2_compact, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
+    launch(ctx, "v2_compact", k_v2_compact, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
            (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
