@@ -2196,6 +2196,19 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
            key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
            (const uint64_t *)arena_off, key_idx, arena);
+    // TxnId-union offsets, compaction and totals are enqueued before the tier statistics are read, so the common
+    // case (no txn for the global tier) costs one host sync here; with global-tier txns they are redone after it.
+    uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
+    uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
+    auto finish = [&]() {
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
+        launch(ctx, "v2_compact", k_v2_compact, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, key_off,
+               (const uint64_t *)dep_off, (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    };
+    finish();
     ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
@@ -2238,17 +2251,10 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
                (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
                (const uint64_t *)fb_off, rbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
+        finish();
+        ctx->sync();
     }
-    uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
-    uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
-    launch(ctx, "v2_compact", k_v2_compact, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
-           (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ctx->sync();
-    *view = acc_keydeps_view{ n, ctx->pinned[0], ctx->pinned[1], ctx->pinned[2], E, arena_off, arena, kd_off,
+    *view = acc_keydeps_view{ n, ctx->pinned[8], ctx->pinned[9], ctx->pinned[10], E, arena_off, arena, kd_off,
                               key_idx, u_off, dep_txn };
     ctx->kd_view = *view;
     ctx->kd_valid = true;
