@@ -26,7 +26,8 @@ u8p = C.POINTER(C.c_uint8)
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
            "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_mixed", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
-           "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get"]
+           "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
+           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out"]
 
 
 class Opts(C.Structure):
@@ -125,6 +126,67 @@ class FragRecv(C.Structure):
                 ("hdr", C.c_void_p), ("keys", C.c_void_p), ("vals", C.c_void_p), ("k2v", C.c_void_p)]
 
 
+class RmmIn(C.Structure):
+    _fields_ = [("key_off", C.c_void_p), ("key_a", C.c_void_p), ("key_b", C.c_void_p), ("val_off", C.c_void_p),
+                ("txn", TsCols), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class DepsMergeIn(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n_groups", C.c_uint32), ("n_replies", C.c_uint64), ("grp_off", C.c_void_p),
+                ("key_deps", RmmIn), ("range_deps", RmmIn)]
+
+
+class RmmView(C.Structure):
+    _fields_ = [("total_keys", C.c_uint64), ("total_vals", C.c_uint64), ("total_k2v", C.c_uint64),
+                ("key_off", C.c_void_p), ("key_a", C.c_void_p), ("key_b", C.c_void_p),
+                ("val_off", C.c_void_p), ("txn_msb", C.c_void_p), ("txn_lsb", C.c_void_p), ("txn_node", C.c_void_p),
+                ("txn_src", C.c_void_p), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class DepsMergeView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("total_in_entries", C.c_uint64), ("key_deps", RmmView),
+                ("range_deps", RmmView)]
+
+
+class RmmOut(C.Structure):
+    _fields_ = [("mem", C.c_uint32),
+                ("cap_keys", C.c_uint64), ("cap_vals", C.c_uint64), ("cap_k2v", C.c_uint64),
+                ("need_keys", C.c_uint64), ("need_vals", C.c_uint64), ("need_k2v", C.c_uint64),
+                ("key_off", C.c_void_p), ("key_a", C.c_void_p), ("key_b", C.c_void_p),
+                ("val_off", C.c_void_p), ("txn_msb", C.c_void_p), ("txn_lsb", C.c_void_p), ("txn_node", C.c_void_p),
+                ("txn_src", C.c_void_p), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class RmmBatch(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n_groups", C.c_uint32), ("key_off", C.c_void_p), ("key_a", C.c_void_p),
+                ("key_b", C.c_void_p), ("val_off", C.c_void_p), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class CsrView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("total", C.c_uint64), ("off", C.c_void_p), ("ints", C.c_void_p)]
+
+
+class RangesIn(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("start", C.c_void_p), ("end", C.c_void_p), ("end_inclusive", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class SliceView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("total_keys", C.c_uint64), ("total_vals", C.c_uint64),
+                ("total_k2v", C.c_uint64), ("key_off", C.c_void_p), ("key_idx", C.c_void_p), ("val_off", C.c_void_p),
+                ("val_idx", C.c_void_p), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
+
+
+class StabIn(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n_queries", C.c_uint32), ("grp", C.c_void_p), ("q_start", C.c_void_p),
+                ("q_end", C.c_void_p), ("end_inclusive", C.c_uint32), ("want_txns", C.c_uint32)]
+
+
+class StabView(C.Structure):
+    _fields_ = [("n_queries", C.c_uint32), ("total_ranges", C.c_uint64), ("total_txns", C.c_uint64),
+                ("range_off", C.c_void_p), ("range_idx", C.c_void_p), ("txn_off", C.c_void_p), ("txn_idx", C.c_void_p)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -180,6 +242,18 @@ def load():
     L.acc_merge_copy_out.restype = C.c_int
     L.acc_levelise.argtypes = [C.c_void_p, C.POINTER(GraphIn), u32p, u32p, u32p]
     L.acc_levelise.restype = C.c_int
+    L.acc_deps_merge.argtypes = [C.c_void_p, C.POINTER(DepsMergeIn), C.POINTER(DepsMergeView)]
+    L.acc_deps_merge.restype = C.c_int
+    L.acc_rmm_copy_out.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(RmmView), C.POINTER(RmmOut)]
+    L.acc_rmm_copy_out.restype = C.c_int
+    L.acc_rmm_invert.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(CsrView)]
+    L.acc_rmm_invert.restype = C.c_int
+    L.acc_rmm_slice.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(RangesIn), C.POINTER(SliceView)]
+    L.acc_rmm_slice.restype = C.c_int
+    L.acc_rangedeps_stab.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(StabIn), C.POINTER(StabView)]
+    L.acc_rangedeps_stab.restype = C.c_int
+    L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
+    L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]
     L.acc_timing_count.restype = C.c_int
     L.acc_timing_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double),

@@ -425,3 +425,131 @@ def merge_levelise_device(ctx: Context, mi: "L.MergeIn", exec_rank_ptr: int, lev
     ctx.check(ctx._lib.acc_levelise(ctx.handle, C.byref(gi), C.cast(level_ptr, L.u32p), C.cast(order_ptr, L.u32p),
                                     nl.ctypes.data_as(L.u32p)))
     return view, int(nl[0])
+
+
+# ---------------------------------------------------------------- Deps.merge over raw deps objects
+
+RMM_FIELDS = (("key_off", np.uint64), ("key_a", np.uint64), ("key_b", np.uint64), ("val_off", np.uint64),
+              ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("k2v_off", np.uint64), ("k2v", np.int32))
+
+
+def _rmm_in(half, keep: list) -> "L.RmmIn":
+    """acc_rmm_in over host arrays of one half: dict(key_off, key_a, [key_b], val_off, msb, lsb, node, k2v_off, k2v)."""
+    if half is None:
+        return L.RmmIn()
+    a = {k: np.ascontiguousarray(half[k], dtype=dt) for k, dt in RMM_FIELDS if half.get(k) is not None}
+    keep.append(a)
+    p = lambda k: a[k].ctypes.data if k in a and a[k].size else (a[k].ctypes.data if k in a else None)  # noqa: E731
+    return L.RmmIn(p("key_off"), p("key_a"), p("key_b"), p("val_off"), L.TsCols(p("msb"), p("lsb"), p("node")),
+                   p("k2v_off"), p("k2v"))
+
+
+def rmm_copy_out(ctx: Context, n_groups: int, view: "L.RmmView", with_b: bool) -> dict:
+    """Host copy of one acc_rmm_view (acc_rmm_copy_out, two-call sizing)."""
+    out = L.RmmOut()
+    out.mem = L.ACC_MEM_HOST
+    rc = ctx._lib.acc_rmm_copy_out(ctx.handle, n_groups, C.byref(view), C.byref(out))
+    if rc not in (L.ACC_OK, L.ACC_E_CAP):
+        ctx.check(rc)
+    nk, nv, no = out.need_keys, out.need_vals, out.need_k2v
+    r = dict(key_off=np.zeros(n_groups + 1, np.uint64), val_off=np.zeros(n_groups + 1, np.uint64),
+             k2v_off=np.zeros(n_groups + 1, np.uint64), key_a=np.zeros(max(nk, 1), np.uint64),
+             msb=np.zeros(max(nv, 1), np.uint64), lsb=np.zeros(max(nv, 1), np.uint64), node=np.zeros(max(nv, 1), np.int32),
+             src=np.zeros(max(nv, 1), np.uint32), k2v=np.zeros(max(no, 1), np.int32))
+    if with_b:
+        r["key_b"] = np.zeros(max(nk, 1), np.uint64)
+    out.cap_keys, out.cap_vals, out.cap_k2v = nk, nv, no
+    for f, k in (("key_off", "key_off"), ("val_off", "val_off"), ("k2v_off", "k2v_off"), ("key_a", "key_a"),
+                 ("txn_msb", "msb"), ("txn_lsb", "lsb"), ("txn_node", "node"), ("txn_src", "src"), ("k2v", "k2v")):
+        setattr(out, f, r[k].ctypes.data)
+    if with_b:
+        out.key_b = r["key_b"].ctypes.data
+    ctx.check(ctx._lib.acc_rmm_copy_out(ctx.handle, n_groups, C.byref(view), C.byref(out)))
+    for k, n in (("key_a", nk), ("key_b", nk), ("msb", nv), ("lsb", nv), ("node", nv), ("src", nv), ("k2v", no)):
+        if k in r:
+            r[k] = r[k][:n]
+    return r
+
+
+def deps_merge(ctx: Context, m: dict) -> dict:
+    """Deps.merge (primitives/Deps.java:256-260) of every group's replies on the GPU. `m` = dict(grp_off, key=half|None,
+    range=half|None) with halves in the SerializerSupport layout (see _rmm_in); returns dict(key=..., range=...) of
+    merged halves (per-group CSR: key_off/key_a[/key_b], val_off/msb/lsb/node/src, k2v_off/k2v)."""
+    keep = []
+    grp_off = np.ascontiguousarray(m["grp_off"], dtype=np.uint64)
+    keep.append(grp_off)
+    ng = len(grp_off) - 1
+    nr = int(grp_off[-1]) if ng >= 0 else 0
+    di = L.DepsMergeIn(L.ACC_MEM_HOST, ng, nr, grp_off.ctypes.data, _rmm_in(m.get("key"), keep),
+                       _rmm_in(m.get("range"), keep))
+    view = L.DepsMergeView()
+    ctx.check(ctx._lib.acc_deps_merge(ctx.handle, C.byref(di), C.byref(view)))
+    return dict(key=rmm_copy_out(ctx, ng, view.key_deps, False), range=rmm_copy_out(ctx, ng, view.range_deps, True),
+                total_in_entries=int(view.total_in_entries))
+
+
+# ---------------------------------------------------------------- RelationMultiMap helpers (invert, slice, stab)
+
+def device_array(ctx: Context, ptr, n: int, dtype) -> np.ndarray:
+    """Host copy of n elements at a device pointer of a result view (acc_copy_out)."""
+    out = np.zeros(max(int(n), 1), dtype=dtype)
+    if n:
+        ctx.check(ctx._lib.acc_copy_out(ctx.handle, out.ctypes.data, ptr, int(n) * out.itemsize, L.ACC_MEM_HOST))
+    return out[:int(n)]
+
+
+def _rmm_batch(m: dict, keep: list) -> "L.RmmBatch":
+    """acc_rmm_batch over host arrays: dict(key_off, key_a, [key_b], val_off, k2v_off, k2v)."""
+    a = {k: np.ascontiguousarray(m[k], dtype=dt) for k, dt in
+         (("key_off", np.uint64), ("key_a", np.uint64), ("key_b", np.uint64), ("val_off", np.uint64),
+          ("k2v_off", np.uint64), ("k2v", np.int32)) if m.get(k) is not None}
+    keep.append(a)
+    p = lambda k: a[k].ctypes.data if k in a else None  # noqa: E731
+    return L.RmmBatch(L.ACC_MEM_HOST, len(a["key_off"]) - 1, p("key_off"), p("key_a"), p("key_b"), p("val_off"),
+                      p("k2v_off"), p("k2v"))
+
+
+def rmm_invert(ctx: Context, m: dict):
+    """RelationMultiMap.invert of every group (acc_rmm_invert): (off[n_groups+1], ints) = txnIdsToKeys per group."""
+    keep = []
+    b = _rmm_batch(m, keep)
+    v = L.CsrView()
+    ctx.check(ctx._lib.acc_rmm_invert(ctx.handle, C.byref(b), C.byref(v)))
+    return device_array(ctx, v.off, v.n_groups + 1, np.uint64), device_array(ctx, v.ints, v.total, np.int32)
+
+
+def rmm_slice(ctx: Context, m: dict, sel_off, sel_start, sel_end, end_inclusive: bool = True) -> dict:
+    """KeyDeps.slice / RangeDeps.slice (+ trimUnusedValues) of every group against its own select Ranges."""
+    keep = []
+    b = _rmm_batch(m, keep)
+    so, ss, se = (np.ascontiguousarray(x, dtype=np.uint64) for x in (sel_off, sel_start, sel_end))
+    keep.append((so, ss, se))
+    sel = L.RangesIn(so.ctypes.data, ss.ctypes.data, se.ctypes.data, int(end_inclusive), 0)
+    v = L.SliceView()
+    ctx.check(ctx._lib.acc_rmm_slice(ctx.handle, C.byref(b), C.byref(sel), C.byref(v)))
+    g = v.n_groups + 1
+    return dict(key_off=device_array(ctx, v.key_off, g, np.uint64), key_idx=device_array(ctx, v.key_idx, v.total_keys, np.uint32),
+                val_off=device_array(ctx, v.val_off, g, np.uint64), val_idx=device_array(ctx, v.val_idx, v.total_vals, np.uint32),
+                k2v_off=device_array(ctx, v.k2v_off, g, np.uint64), k2v=device_array(ctx, v.k2v, v.total_k2v, np.int32))
+
+
+def rangedeps_stab(ctx: Context, m: dict, grp, q_start, q_end=None, end_inclusive: bool = True, want_txns: bool = True):
+    """Stabbing queries over built RangeDeps (acc_rangedeps_stab): per query the ascending range indices (and, with
+    want_txns, the sorted unique TxnId indices = RangeDeps.computeTxnIds)."""
+    keep = []
+    b = _rmm_batch(m, keep)
+    grp = np.ascontiguousarray(grp, dtype=np.uint32)
+    qs = np.ascontiguousarray(q_start, dtype=np.uint64)
+    qe = np.ascontiguousarray(q_end, dtype=np.uint64) if q_end is not None else None
+    keep.append((grp, qs, qe))
+    qi = L.StabIn(L.ACC_MEM_HOST, len(grp), grp.ctypes.data, qs.ctypes.data, qe.ctypes.data if qe is not None else None,
+                  int(end_inclusive), int(want_txns))
+    v = L.StabView()
+    ctx.check(ctx._lib.acc_rangedeps_stab(ctx.handle, C.byref(b), C.byref(qi), C.byref(v)))
+    n = v.n_queries + 1
+    out = dict(range_off=device_array(ctx, v.range_off, n, np.uint64),
+               range_idx=device_array(ctx, v.range_idx, v.total_ranges, np.uint32))
+    if want_txns:
+        out["txn_off"] = device_array(ctx, v.txn_off, n, np.uint64)
+        out["txn_idx"] = device_array(ctx, v.txn_idx, v.total_txns, np.uint32)
+    return out

@@ -204,7 +204,13 @@ def exchange_streams(bufs: dict, counts: np.ndarray, group=None):
 def shard_merge(ctx, recv: dict, rcounts: np.ndarray, world: int, rank: int, n_txn: int):
     """acc_shard_merge on received device streams; returns the merge view (device result on ctx)."""
     import ctypes as C
+    import torch
     from . import _lib as L
+    # all_to_all_single only orders torch's current stream after the collective; the library reads `recv` on its own
+    # (non-blocking) stream, so wait for the collective to land before handing the buffers over
+    dev = recv["hdr"].device
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
     cnt = [np.ascontiguousarray(rcounts[q], dtype=np.uint64) for q in range(4)]
     fr = L.FragRecv(L.ACC_MEM_DEVICE, world, rank, n_txn, *(c.ctypes.data for c in cnt),
                     *(recv[n].data_ptr() if recv[n].numel() else 0 for n, _, _ in STREAMS))

@@ -297,6 +297,21 @@ def merge_batch(n_txn: int = 16_384, replies: int = 64, seed: int = CONFIG_SEEDS
                 k2v_off=k2v_off, k2v=k2v)
 
 
+def raw_txn_ids(rank: np.ndarray):
+    """The TxnIds behind config-5 txn ranks (batch index t = rank t): epoch 1, hlc t+1, Write, node 1 + t mod 8, in
+    compareTo order of the rank (Timestamp.java:81-89)."""
+    r = np.asarray(rank, dtype=np.uint64)
+    return encode_ts(np.ones_like(r), r + np.uint64(1), np.full_like(r, WRITE << 1), (1 + (r % np.uint64(8))).astype(np.int32))
+
+
+def merge_batch_raw(m: dict) -> dict:
+    """A merge_batch (rank-space acc_merge_in layout) as the raw SerializerSupport half of acc_deps_merge: key codes,
+    TxnId columns (raw_txn_ids) and the same keysToTxnIds."""
+    msb, lsb, node = raw_txn_ids(m["txn_rank"])
+    return dict(key_off=m["key_off"], key_a=m["key_code"], val_off=m["val_off"], msb=msb, lsb=lsb, node=node,
+                k2v_off=m["k2v_off"], k2v=m["k2v"])
+
+
 @dataclass
 class RangeBatch:
     """A mixed key/range snapshot: `keys` is the acc_batch_in part (key-domain txns

@@ -10,6 +10,10 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *o
 void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
 void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
+void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *view);
+void rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out);
+void rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out);
+void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q, acc_stab_view *out);
 }  // namespace acc
 
 extern "C" {
@@ -207,6 +211,89 @@ int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out)
         if (v.total_keys) ACC_HIP(hipMemcpyAsync(out->key_code, v.key_code, v.total_keys * 8, kind, ctx->stream));
         if (v.total_vals) ACC_HIP(hipMemcpyAsync(out->txn_rank, v.txn_rank, v.total_vals * 4, kind, ctx->stream));
         if (v.total_k2v) ACC_HIP(hipMemcpyAsync(out->k2v, v.k2v, v.total_k2v * 4, kind, ctx->stream));
+        ctx->sync();
+    });
+}
+
+int acc_deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::deps_merge(ctx, in, out_view);
+    });
+}
+
+int acc_rmm_copy_out(acc_ctx *ctx, uint32_t n_groups, const acc_rmm_view *v, acc_rmm_out *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        if (!out || !v) acc::fail(ACC_E_ARG, "null argument");
+        if (out->mem != ACC_MEM_HOST && out->mem != ACC_MEM_DEVICE) acc::fail(ACC_E_ARG, "bad mem");
+        out->need_keys = v->total_keys;
+        out->need_vals = v->total_vals;
+        out->need_k2v = v->total_k2v;
+        if (!out->key_off || !out->val_off || !out->k2v_off)
+            acc::fail(ACC_E_CAP, "sizing call (null offset arrays); required sizes written to need_*");
+        if (out->cap_keys < v->total_keys || out->cap_vals < v->total_vals || out->cap_k2v < v->total_k2v)
+            acc::fail(ACC_E_CAP, "output capacity too small; required sizes written to need_*");
+        const hipMemcpyKind k = out->mem == ACC_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        const size_t n1 = (size_t)n_groups + 1;
+        hipStream_t st = ctx->stream;
+        ACC_HIP(hipMemcpyAsync(out->key_off, v->key_off, n1 * 8, k, st));
+        ACC_HIP(hipMemcpyAsync(out->val_off, v->val_off, n1 * 8, k, st));
+        ACC_HIP(hipMemcpyAsync(out->k2v_off, v->k2v_off, n1 * 8, k, st));
+        if (v->total_keys) {
+            if (out->key_a) ACC_HIP(hipMemcpyAsync(out->key_a, v->key_a, v->total_keys * 8, k, st));
+            if (out->key_b && v->key_b) ACC_HIP(hipMemcpyAsync(out->key_b, v->key_b, v->total_keys * 8, k, st));
+        }
+        if (v->total_vals) {
+            if (out->txn_msb) ACC_HIP(hipMemcpyAsync(out->txn_msb, v->txn_msb, v->total_vals * 8, k, st));
+            if (out->txn_lsb) ACC_HIP(hipMemcpyAsync(out->txn_lsb, v->txn_lsb, v->total_vals * 8, k, st));
+            if (out->txn_node) ACC_HIP(hipMemcpyAsync(out->txn_node, v->txn_node, v->total_vals * 4, k, st));
+            if (out->txn_src && v->txn_src) ACC_HIP(hipMemcpyAsync(out->txn_src, v->txn_src, v->total_vals * 4, k, st));
+        }
+        if (v->total_k2v && out->k2v) ACC_HIP(hipMemcpyAsync(out->k2v, v->k2v, v->total_k2v * 4, k, st));
+        ctx->sync();
+    });
+}
+
+int acc_rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::rmm_invert(ctx, in, out_view);
+    });
+}
+
+int acc_rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::rmm_slice(ctx, in, select, out_view);
+    });
+}
+
+int acc_rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *range_deps, const acc_stab_in *queries, acc_stab_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::rangedeps_stab(ctx, range_deps, queries, out_view);
+    });
+}
+
+int acc_copy_out(acc_ctx *ctx, void *dst, const void *src_device, size_t bytes, uint32_t mem)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        if (mem != ACC_MEM_HOST && mem != ACC_MEM_DEVICE) acc::fail(ACC_E_ARG, "bad mem");
+        if (!bytes) return;
+        if (!dst || !src_device) acc::fail(ACC_E_ARG, "null pointer");
+        ACC_HIP(hipMemcpyAsync(dst, src_device, bytes, mem == ACC_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
+                               ctx->stream));
         ctx->sync();
     });
 }

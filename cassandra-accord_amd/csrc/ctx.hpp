@@ -85,14 +85,26 @@ struct acc_ctx {
     acc_keydeps_view kd_view{};
     acc_merge_view merge_view{};
     acc_rangedeps_view rd_view{};
+    acc_deps_merge_view dm_view{};
+    bool dm_valid = false;
     uint64_t rd_ent_hint = 0;   // RangeDeps raw pairs of the last batch (output capacity of the stabbing pass)
     bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;
 
+    // buffer-name namespace (NsScope): lets one call run a sub-pipeline twice (e.g. the KeyDeps and RangeDeps halves
+    // of Deps.merge) without the second run overwriting the first one's results
+    std::string ns;
+
     // Grow-only named device buffer. Contents are NOT preserved across growth.
     template <class T>
     T *get(const char *name, size_t count)
+    {
+        return get_raw<T>(ns.empty() ? std::string(name) : ns + name, count);
+    }
+    // the same, outside any namespace (state shared by every sub-pipeline: the scan status buffers)
+    template <class T>
+    T *get_raw(const std::string &name, size_t count)
     {
         size_t bytes = count * sizeof(T);
         if (bytes == 0) bytes = 16;
@@ -178,6 +190,14 @@ struct acc_ctx {
 };
 
 namespace acc {
+
+// Scoped buffer-name namespace on a context (see acc_ctx::ns).
+struct NsScope {
+    acc_ctx *ctx;
+    std::string saved;
+    NsScope(acc_ctx *c, const char *prefix) : ctx(c), saved(c->ns) { ctx->ns = saved + prefix; }
+    ~NsScope() { ctx->ns = saved; }
+};
 
 // Launch a kernel on the context stream (or the side stream selected by launch_stream); with ACC_OPT_TIMING, bracket it with HIP events recorded on
 // that same stream (so the interval is the kernel's own device time).

@@ -15,6 +15,18 @@ struct Dictionary {
     uint64_t hg[8] = {};              // prep words: ts word masks [0..2], key mask [3], errors [4], unsorted [5]
 };
 
+// Dense order ranks of n composite keys of nw (1..3) u64 words, most significant first, compared unsigned after
+// (word & and_mask[k]) ^ xor_mask[k] (null masks: identity). rank[i] in [0, count); first[r] = smallest index of rank r
+// (want_first). count is left on device (count_dev) for the caller's next sync. Buffers named "<tag>.*".
+struct DenseRank {
+    uint32_t *rank = nullptr;
+    uint32_t *first = nullptr;
+    uint64_t *count_dev = nullptr;
+    uint64_t count = 0;
+};
+DenseRank dense_rank(acc_ctx *ctx, const char *tag, size_t n, int nw, const uint64_t *const *words, const uint64_t *and_mask,
+                     const uint64_t *xor_mask, bool want_first);
+
 // key_off/key_code: the key-domain part (P pairs); owner[P] receives the txn of every pair; g[8] scratch words.
 void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
                      const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,

@@ -1572,7 +1572,7 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const ui
 __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const uint32_t *__restrict__ big_list,
                                                          const uint64_t *__restrict__ big_off, V2View v,
                                                          const uint64_t *__restrict__ cnt, const uint32_t *__restrict__ key_off,
-                                                         int rbits, uint64_t *__restrict__ gkey)
+                                                         int rbits, int kbits, uint64_t *__restrict__ gkey)
 {
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t b = blockIdx.x * WAVES + wave;
@@ -1582,7 +1582,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
     // reuse the wave appenders with an unbounded global buffer: WCAP guard off via a large cursor window
     const uint32_t lane = lane_id();
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint64_t tb = (uint64_t)b << (rbits + 16);
+    const uint64_t tb = (uint64_t)b << (rbits + kbits);
     uint32_t cursor = 0;
     const uint32_t j0 = key_off[t], j1 = key_off[t + 1];
     for (uint32_t j = j0; j < j1; ++j) {
@@ -1614,7 +1614,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
                     if (r3) keep = keep && v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u);
                 }
                 uint64_t bal = __ballot(keep);
-                if (keep) out[cursor + (uint32_t)__popcll(bal & lt)] = tb | ((uint64_t)x << 16) | kj;
+                if (keep) out[cursor + (uint32_t)__popcll(bal & lt)] = tb | ((uint64_t)x << kbits) | kj;
                 cursor += (uint32_t)__popcll(bal);
             }
         }
@@ -1622,17 +1622,17 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const ui
 }
 
 // sorted by (txn, value, key): dense rank of value within txn; TxnId array for first occurrences
-__global__ __launch_bounds__(BLOCK) void k_v2_big_newflag(uint64_t m, const uint64_t *__restrict__ skey, int rbits,
+__global__ __launch_bounds__(BLOCK) void k_v2_big_newflag(uint64_t m, const uint64_t *__restrict__ skey, int kbits,
                                                           uint32_t *__restrict__ flag)
 {
     uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
-    flag[i] = i == 0 || (skey[i] >> 16) != (skey[i - 1] >> 16);
+    flag[i] = i == 0 || (skey[i] >> kbits) != (skey[i - 1] >> kbits);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_v2_big_rank(uint64_t m, const uint64_t *__restrict__ skey, const uint32_t *__restrict__ incl,
                                                        const uint32_t *__restrict__ big_list, const uint64_t *__restrict__ big_off,
-                                                       int rbits, const uint32_t *__restrict__ key_off,
+                                                       int rbits, int kbits, const uint32_t *__restrict__ key_off,
                                                        const uint64_t *__restrict__ dep_off, const uint32_t *__restrict__ txn_of_rank,
                                                        uint32_t *__restrict__ dep_scratch, uint64_t *__restrict__ u_cnt,
                                                        uint32_t *__restrict__ idx_by_pos1, uint64_t *__restrict__ key2)
@@ -1640,43 +1640,51 @@ __global__ __launch_bounds__(BLOCK) void k_v2_big_rank(uint64_t m, const uint64_
     uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
     uint64_t x = skey[i];
-    uint32_t b = (uint32_t)(x >> (rbits + 16));
-    uint32_t val = (uint32_t)((x >> 16) & ((1ull << rbits) - 1));
-    uint32_t kj = (uint32_t)(x & 0xFFFFu);
+    uint32_t b = (uint32_t)(x >> (rbits + kbits));
+    uint32_t val = (uint32_t)((x >> kbits) & ((1ull << rbits) - 1));
+    uint32_t kj = (uint32_t)(x & ((1ull << kbits) - 1));
     uint64_t start = big_off[b];
     uint32_t base_incl = start == 0 ? 0 : incl[start - 1];
     uint32_t idx = incl[i] - base_incl - 1;
     uint32_t t = big_list[b];
-    bool nw = i == start || (skey[i] >> 16) != (skey[i - 1] >> 16);
+    bool nw = i == start || (skey[i] >> kbits) != (skey[i - 1] >> kbits);
     if (nw) dep_scratch[dep_off[key_off[t]] + idx] = txn_of_rank[val];
     if (i + 1 == big_off[b + 1]) u_cnt[t] = idx + 1;
     idx_by_pos1[i] = idx;
     // arena order of the txn: (key, value); value of the second sort = this position
-    key2[i] = ((uint64_t)b << (16 + rbits)) | ((uint64_t)kj << rbits) | val;
+    key2[i] = ((uint64_t)b << (kbits + rbits)) | ((uint64_t)kj << rbits) | val;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_v2_big_arena(uint64_t m, const uint32_t *__restrict__ sval2, const uint64_t *__restrict__ skey2,
                                                         const uint32_t *__restrict__ idx_by_pos1, const uint32_t *__restrict__ big_list,
-                                                        const uint64_t *__restrict__ big_off, int rbits,
+                                                        const uint64_t *__restrict__ big_off, int rbits, int kbits,
                                                         const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ cnz,
                                                         const uint64_t *__restrict__ arena_off, int32_t *__restrict__ arena)
 {
     uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
-    uint32_t b = (uint32_t)(skey2[i] >> (16 + rbits));
+    uint32_t b = (uint32_t)(skey2[i] >> (kbits + rbits));
     uint32_t t = big_list[b];
     uint32_t kd = cnz[key_off[t + 1]] - cnz[key_off[t]];
     arena[arena_off[t] + kd + (i - big_off[b])] = (int32_t)idx_by_pos1[sval2[i]];
 }
 
+// per fallback txn: raw entry count; maxk[0] = the largest key count of a fallback txn (width of the key field of the
+// global-tier sort keys: a txn may list any number of keys, Keys has no cap)
 __global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t *__restrict__ fb_list,
                                                     const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                    uint64_t *__restrict__ fb_e)
+                                                    uint64_t *__restrict__ fb_e, uint64_t *__restrict__ maxk)
 {
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= nfb) return;
-    uint32_t t = fb_list[i];
-    fb_e[i] = dep_off[key_off[t + 1]] - dep_off[key_off[t]];
+    uint64_t nk = 0;
+    if (i < nfb) {
+        uint32_t t = fb_list[i];
+        fb_e[i] = dep_off[key_off[t + 1]] - dep_off[key_off[t]];
+        nk = key_off[t + 1] - key_off[t];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nk = max(nk, shfl_xor(nk, d));
+    if (lane_id() == 0 && nk) atomicMax((unsigned long long *)maxk, (unsigned long long)nk);
 }
 
 
@@ -2227,30 +2235,35 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         // sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
         uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
         uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
+        uint64_t *fb_maxk = ctx->get<uint64_t>("v2_fb_maxk", 1);
+        ACC_HIP(hipMemsetAsync(fb_maxk, 0, sizeof(uint64_t), st));
         launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
-               (const uint32_t *)fb_list, key_off, (const uint64_t *)dep_off, fb_e);
+               (const uint32_t *)fb_list, key_off, (const uint64_t *)dep_off, fb_e, fb_maxk);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, fb_maxk, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
         const int bbits = bits_for(nfb - 1);
-        if (bbits + rbits + 16 > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
+        const int kbits = std::max(1, bits_for(ctx->pinned[0] - 1));   // key index within its txn
+        if (bbits + rbits + kbits > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
         uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
         launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
                (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)cnt, key_off,
-               rbits, gkey);
-        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + 16);
+               rbits, kbits, gkey);
+        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + kbits);
         uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
         uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
         launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
-               (const uint64_t *)s1.keys, rbits, nflag);
+               (const uint64_t *)s1.keys, kbits, nflag);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
         uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
         uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
         launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
-               (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, key_off,
+               (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, kbits, key_off,
                (const uint64_t *)dep_off, (const uint32_t *)txn_of_rank, dep_scratch, u_cnt, idx1, key2);
-        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + 16 + rbits);
+        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
         launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
                (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
-               (const uint64_t *)fb_off, rbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
+               (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
         finish();
         ctx->sync();
     }

@@ -13,7 +13,7 @@
 //      the index of the value in the group's txnId array (binary search within the group).
 #include <algorithm>
 
-#include "prims.hpp"
+#include "dict.hpp"
 
 namespace acc {
 
@@ -631,8 +631,32 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
     plan.rk = make_runs(kmask);
     plan.rv = make_runs(vmask);
     const int gb = bits_for(ng ? ng - 1 : 0) + 1;   // +1: real records stay below the all-ones pad
+    // Wide key codes (hashed keys use every bit) leave no room for the group field: sort on dense ranks of the codes
+    // (and of the TxnId ranks) instead; the outputs still carry the caller's codes.
+    const uint64_t *ekey = key_code;
+    const uint32_t *eval = txn_rank;
+    if (gb + plan.rk.bits + plan.rv.bits > 64) {
+        const uint64_t *kw[1] = { key_code };
+        DenseRank kd = dense_rank(ctx, "m_kdict", NK, 1, kw, nullptr, nullptr, false);
+        uint64_t *kr64 = ctx->get<uint64_t>("m_kr64", NK);
+        launch(ctx, "m_widen", k_widen, dim3(grid_for(NK, BLOCK)), dim3(BLOCK), 0, NK, (const uint32_t *)kd.rank, kr64);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, kd.count_dev, 8, hipMemcpyDeviceToHost, st));
+        uint64_t *vw64 = ctx->get<uint64_t>("m_vw64", NV);
+        launch(ctx, "m_widen", k_widen, dim3(grid_for(NV, BLOCK)), dim3(BLOCK), 0, NV, txn_rank, vw64);
+        const uint64_t *vw[1] = { vw64 };
+        DenseRank vd = dense_rank(ctx, "m_vdict", NV, 1, vw, nullptr, nullptr, false);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, vd.count_dev, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        ekey = kr64;
+        eval = vd.rank;
+        plan.rk = make_runs(ctx->pinned[0] > 1 ? (1ull << bits_for(ctx->pinned[0] - 1)) - 1 : 0);
+        plan.rv = make_runs(ctx->pinned[1] > 1 ? (1ull << bits_for(ctx->pinned[1] - 1)) - 1 : 0);
+        ctx->stat("merge.dense_keys", 1);
+    } else {
+        ctx->stat("merge.dense_keys", 0);
+    }
     const int kb = plan.rk.bits, vb = plan.rv.bits;
-    if (gb + kb + vb > 64) fail(ACC_E_CAP, "merge composite key exceeds 64 bits");
+    if (gb + kb + vb > 64) fail(ACC_E_CAP, "merge composite key exceeds 64 bits (groups x distinct keys x distinct TxnIds)");
     plan.gshift_k = kb; plan.gshift_v = vb; plan.gshift_kv = kb + vb; plan.vshift_kv = vb;
     auto ones = [](int b) { return b >= 64 ? ~0ull : ((1ull << b) - 1); };
     plan.pad_k = ones(gb + kb); plan.pad_v = ones(gb + vb); plan.pad_kv = ones(gb + kb + vb);
@@ -643,7 +667,7 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
     uint32_t *key_of_slot = ctx->get<uint32_t>("m_key_of_slot", NO);
     uint32_t *val_of_slot = ctx->get<uint32_t>("m_val_of_slot", NO);
     launch(ctx, "m_expand", k_m_expand, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, (const uint32_t *)grp_of, key_off,
-           key_code, val_off, txn_rank, k2v_off, k2v, plan, sk, sv, skv);
+           ekey, val_off, eval, k2v_off, k2v, plan, sk, sv, skv);
     launch(ctx, "m_key_of_slot", k_m_key_of_slot, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, R, key_off, val_off, k2v_off,
            k2v, key_of_slot, val_of_slot);
     Sorted ssk = radix_sort(ctx, "m_rs_k", sk, nullptr, NK, gb + kb);

@@ -5,6 +5,8 @@
 
 #include "ctx.hpp"
 
+#include <algorithm>
+
 namespace acc {
 
 constexpr int BLOCK = 256;
@@ -264,13 +266,13 @@ void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_
     uint64_t *buf[2];
     if (need > ctx->scan_cap) {
         for (int i = 0; i < 2; ++i) {
-            buf[i] = ctx->get<uint64_t>(i ? "scan_status1" : "scan_status0", need);
+            buf[i] = ctx->get_raw<uint64_t>(i ? "scan_status1" : "scan_status0", need);
             ACC_HIP(hipMemsetAsync(buf[i], 0, need * sizeof(uint64_t), ctx->stream));
         }
         ctx->scan_cap = need;
         ctx->scan_dirty[0] = ctx->scan_dirty[1] = 0;
     } else {
-        for (int i = 0; i < 2; ++i) buf[i] = ctx->get<uint64_t>(i ? "scan_status1" : "scan_status0", need);
+        for (int i = 0; i < 2; ++i) buf[i] = ctx->get_raw<uint64_t>(i ? "scan_status1" : "scan_status0", need);
     }
     const int p = ctx->scan_par;
     uint64_t *status = buf[p];

@@ -427,6 +427,7 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     const uint32_t world = in->world, home = in->rank, n = in->n_txn;
     if (world == 0 || home >= world) fail(ACC_E_ARG, "rank must be below world");
     hipStream_t st = ctx->stream;
+    ctx->merge_valid = false;   // a failing call must not leave the previous result readable as if current
     const uint32_t n_groups = n > home ? (n - home + world - 1) / world : 0;   // home txns t = home, home + world, ...
     uint64_t F = 0, NK = 0, NV = 0, NO = 0;
     for (uint32_t s = 0; s < world; ++s) {

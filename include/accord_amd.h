@@ -261,6 +261,145 @@ typedef struct acc_merge_out {
 
 int acc_merge_copy_out(acc_ctx *ctx, acc_merge_out *out);
 
+/* ---- Deps.merge over raw deps objects ----
+ * Deps.merge(List, getter) (primitives/Deps.java:256-260) = KeyDeps.merge (primitives/KeyDeps.java:115-135) and
+ * RangeDeps.merge (primitives/RangeDeps.java:101-134) of the replies of each coordinated txn (group g owns replies
+ * [grp_off[g], grp_off[g+1])), folded left to right by a LinearMerger (utils/RelationMultiMap.java:284-406), empty
+ * replies skipped. Each reply half is given as the arrays KeyDeps/RangeDeps.SerializerSupport expose
+ * (primitives/KeyDeps.java:55-73, primitives/RangeDeps.java:55-73): keys (or ranges), the TxnId[] as raw columns and the
+ * Java keysToTxnIds / rangesToTxnIds int[] verbatim. TxnIds are ranked on device (Timestamp.compareTo / equals); an
+ * equals-tie whose raw bits differ (flags outside IDENTITY_LSB) keeps the instance the Java fold keeps
+ * (SortedArrays.linearUnion utils/SortedArrays.java:152-281, RelationMultiMap.linearUnion :561-816). */
+typedef struct acc_rmm_in {
+    const uint64_t *key_off;   /* [n_replies+1]; null: the half is absent (every result is NONE) */
+    const uint64_t *key_a;     /* KeyDeps: key codes; RangeDeps: Range.start codes */
+    const uint64_t *key_b;     /* RangeDeps: Range.end codes (Range::compare = (start, end), Range.java:310-317); KeyDeps: null */
+    const uint64_t *val_off;   /* [n_replies+1] */
+    acc_ts_cols     txn;       /* TxnId[] of every reply, raw */
+    const uint64_t *k2v_off;   /* [n_replies+1] */
+    const int32_t  *k2v;       /* keysToTxnIds / rangesToTxnIds int[] of every reply */
+} acc_rmm_in;
+
+typedef struct acc_deps_merge_in {
+    uint32_t mem;              /* ACC_MEM_HOST or ACC_MEM_DEVICE for every pointer */
+    uint32_t n_groups;
+    uint64_t n_replies;
+    const uint64_t *grp_off;   /* [n_groups+1] */
+    acc_rmm_in key_deps;
+    acc_rmm_in range_deps;
+} acc_deps_merge_in;
+
+/* A merged half per group g (device pointers owned by the context, valid until its next compute call):
+ * keys/ranges key_a[key_off[g]..key_off[g+1]) (+ key_b), TxnIds txn_*[val_off[g]..], ints k2v[k2v_off[g]..].
+ * txn_src = an input slot (index into the half's TxnId columns) holding the kept instance's raw bits. */
+typedef struct acc_rmm_view {
+    uint64_t total_keys, total_vals, total_k2v;
+    const uint64_t *key_off;  const uint64_t *key_a;  const uint64_t *key_b;
+    const uint64_t *val_off;  const uint64_t *txn_msb; const uint64_t *txn_lsb; const int32_t *txn_node;
+    const uint32_t *txn_src;
+    const uint64_t *k2v_off;  const int32_t  *k2v;
+} acc_rmm_view;
+
+typedef struct acc_deps_merge_view {
+    uint32_t n_groups;
+    uint64_t total_in_entries;          /* keysToTxnIds + rangesToTxnIds entries over every reply */
+    acc_rmm_view key_deps, range_deps;
+} acc_deps_merge_view;
+
+int acc_deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *out_view);
+
+/* Copy any acc_rmm_view of this context into caller buffers (two-call sizing: null offset arrays or a capacity below
+ * the need -> ACC_E_CAP after writing need_*). key_b / txn_src are copied when both the view and the caller have them. */
+typedef struct acc_rmm_out {
+    uint32_t  mem;
+    uint64_t  cap_keys, cap_vals, cap_k2v;
+    uint64_t  need_keys, need_vals, need_k2v;   /* written */
+    uint64_t *key_off;  uint64_t *key_a;  uint64_t *key_b;        /* [n_groups+1], [cap_keys] x2 */
+    uint64_t *val_off;  uint64_t *txn_msb; uint64_t *txn_lsb; int32_t *txn_node; uint32_t *txn_src;   /* [cap_vals] */
+    uint64_t *k2v_off;  int32_t  *k2v;                            /* [cap_k2v] */
+} acc_rmm_out;
+
+int acc_rmm_copy_out(acc_ctx *ctx, uint32_t n_groups, const acc_rmm_view *view, acc_rmm_out *out);
+
+/* ---- RelationMultiMap helpers over a batch of built deps objects (one KeyDeps or RangeDeps per group) ----
+ * The arrays of KeyDeps/RangeDeps.SerializerSupport (primitives/KeyDeps.java:55-73, primitives/RangeDeps.java:55-73);
+ * the TxnIds themselves are not needed (val_off gives their count per group). key_b null = KeyDeps (key codes),
+ * non-null = RangeDeps (Range start/end codes sorted by Range::compare). */
+typedef struct acc_rmm_batch {
+    uint32_t mem;              /* ACC_MEM_HOST or ACC_MEM_DEVICE for every pointer (and for acc_ranges_in) */
+    uint32_t n_groups;
+    const uint64_t *key_off;   /* [n_groups+1] */
+    const uint64_t *key_a;     /* key codes | Range.start codes */
+    const uint64_t *key_b;     /* null | Range.end codes */
+    const uint64_t *val_off;   /* [n_groups+1] TxnIds per group */
+    const uint64_t *k2v_off;   /* [n_groups+1] */
+    const int32_t  *k2v;       /* keysToTxnIds / rangesToTxnIds int[] per group */
+} acc_rmm_batch;
+
+/* Per-group int[] result (device pointers owned by the context): ints[off[g] .. off[g+1]). */
+typedef struct acc_csr_view {
+    uint32_t n_groups;
+    uint64_t total;
+    const uint64_t *off;
+    const int32_t  *ints;
+} acc_csr_view;
+
+/* RelationMultiMap.invert (utils/RelationMultiMap.java:907-938) of every group: KeyDeps.txnIdsToKeys
+ * (primitives/KeyDeps.java:350-362) / RangeDeps txnIdsToRanges: per group the Java int[] of nv end offsets (from nv)
+ * followed by the key indices of each TxnId in ascending key order. */
+int acc_rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out_view);
+
+/* Ranges per group (sorted, deoverlapped; Ranges.ofSortedAndDeoverlapped): [off[g], off[g+1]) of start/end. */
+typedef struct acc_ranges_in {
+    const uint64_t *off;       /* [n_groups+1] */
+    const uint64_t *start;
+    const uint64_t *end;
+    uint32_t end_inclusive;    /* Range.EndInclusive (s, e] = 1; StartInclusive [s, e) = 0 (Range.java:40-138) */
+    uint32_t reserved;
+} acc_ranges_in;
+
+/* Slice result per group: the selected key indices (into the group's keys, ascending), the kept TxnId indices (into
+ * the group's txnIds, ascending) and the new keysToTxnIds int[] over the kept TxnIds. */
+typedef struct acc_slice_view {
+    uint32_t n_groups;
+    uint64_t total_keys, total_vals, total_k2v;
+    const uint64_t *key_off;  const uint32_t *key_idx;
+    const uint64_t *val_off;  const uint32_t *val_idx;
+    const uint64_t *k2v_off;  const int32_t  *k2v;
+} acc_slice_view;
+
+/* KeyDeps.slice(Ranges) (primitives/KeyDeps.java:189-236: keys contained in the ranges) / RangeDeps.slice(Ranges)
+ * (primitives/RangeDeps.java:545-565: ranges intersecting them) with trimUnusedValues
+ * (utils/RelationMultiMap.java:491-532), each group against its own select Ranges; the reference's short cuts are kept
+ * (empty input, nothing selected, everything selected = `return this` without trimming). */
+int acc_rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out_view);
+
+/* Stabbing queries over built RangeDeps (SearchableRangeList.forEach, utils/SearchableRangeList.java:89-116;
+ * RangeDeps.forEach / computeTxnIds, primitives/RangeDeps.java:152-412, 629-643): query q against group grp[q]:
+ * a key (q_end null: Range.contains with the bound type) or a range [q_start, q_end) (compareIntersecting == 0). */
+typedef struct acc_stab_in {
+    uint32_t mem;
+    uint32_t n_queries;
+    const uint32_t *grp;       /* [n_queries] */
+    const uint64_t *q_start;   /* [n_queries] key codes | range starts */
+    const uint64_t *q_end;     /* [n_queries] range ends, or null for key queries */
+    uint32_t end_inclusive;
+    uint32_t want_txns;        /* also produce computeTxnIds (sorted unique TxnId indices) */
+} acc_stab_in;
+
+typedef struct acc_stab_view {
+    uint32_t n_queries;
+    uint64_t total_ranges, total_txns;
+    const uint64_t *range_off; const uint32_t *range_idx;   /* ascending range indices per query */
+    const uint64_t *txn_off;   const uint32_t *txn_idx;     /* want_txns: ascending TxnId indices per query */
+} acc_stab_view;
+
+int acc_rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *range_deps, const acc_stab_in *queries, acc_stab_view *out_view);
+
+/* Copy `bytes` from a device pointer of a result view into caller memory (mem = ACC_MEM_HOST / ACC_MEM_DEVICE), on the
+ * context stream, synchronously: lets a host without HIP bindings read any view. */
+int acc_copy_out(acc_ctx *ctx, void *dst, const void *src_device, size_t bytes, uint32_t mem);
+
 /* ---- Key-range CommandStore shards across GPUs (PreAccept.reduce) ----
  * acc_shard_pack: the last acc_keydeps_batch result of this shard (the same `in`) as fragments for the txns' home
  * ranks (home(t) = t mod world, t the global index). A fragment = header (t, nk, nv, no) + nk key codes + nv TxnIds (batch indices) +

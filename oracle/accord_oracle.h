@@ -113,6 +113,50 @@ orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
                                           int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride);
 void orc_rangedeps_free(orc_rangedeps_result *r);
 
+/* ---- accord_oracle_rmm.c: RelationMultiMap operations on whole deps objects over raw values ---- */
+
+/* KeyDeps.merge / RangeDeps.merge (LinearMerger fold of linearUnion) per group of replies with raw TxnId columns;
+ * keys are (key_a, 0) codes or (key_a, key_b) = (start, end) ranges (is_range). val_src = input slot of the TxnId
+ * instance the Java keeps (SortedArrays.linearUnion / RelationMultiMap.linearUnion identity rules). */
+typedef struct orc_rmm_merge_result {
+    uint32_t  n_groups;
+    uint64_t *key_off;  uint64_t *key_a; uint64_t *key_b;
+    uint64_t *val_off;  uint64_t *val_src; uint64_t *val_msb; uint64_t *val_lsb; int32_t *val_node;
+    uint64_t *k2v_off;  int32_t  *k2v;
+    int       error;
+    char      message[256];
+} orc_rmm_merge_result;
+orc_rmm_merge_result *orc_rmm_merge(uint32_t n_groups, const uint64_t *grp_off, int is_range,
+                                    const uint64_t *key_off, const uint64_t *key_a, const uint64_t *key_b,
+                                    const uint64_t *val_off, const uint64_t *vmsb, const uint64_t *vlsb, const int32_t *vnode,
+                                    const uint64_t *k2v_off, const int32_t *k2v);
+void orc_rmm_merge_free(orc_rmm_merge_result *r);
+
+/* RelationMultiMap.invert, batched (trg_off[n_groups+1], trg sized sum(ntrg + entries)). Returns 0 / -1. */
+int orc_invert(uint32_t n_groups, const uint64_t *src_off, const int32_t *src, const uint64_t *nsrc, const uint64_t *ntrg,
+               uint64_t *trg_off, int32_t *trg);
+
+/* KeyDeps.slice / RangeDeps.slice + trimUnusedValues per group (select ranges sel[sel_off[g]..sel_off[g+1])). */
+typedef struct orc_slice_result {
+    uint32_t  n_groups;
+    uint64_t *key_off; uint32_t *key_idx;   /* selected key indices (into the group's keys) */
+    uint64_t *val_off; uint32_t *val_idx;   /* kept TxnId indices (into the group's txnIds) */
+    uint64_t *k2v_off; int32_t  *k2v;
+} orc_slice_result;
+orc_slice_result *orc_rmm_slice(uint32_t n_groups, int is_range, int end_inclusive,
+                                const uint64_t *key_off, const uint64_t *key_a, const uint64_t *key_b,
+                                const uint64_t *val_off, const uint64_t *k2v_off, const int32_t *k2v,
+                                const uint64_t *sel_off, const uint64_t *sel_s, const uint64_t *sel_e);
+void orc_slice_free(orc_slice_result *r);
+
+/* Stabbing queries over built RangeDeps: per query the ascending indices of group grp[q]'s ranges containing the
+ * key qs[q] (is_key_query) or intersecting [qs[q], qe[q]). */
+typedef struct orc_stab_result { uint64_t *off; uint32_t *idx; } orc_stab_result;
+orc_stab_result *orc_rmm_stab(uint32_t n_queries, const uint32_t *grp, const uint64_t *qs, const uint64_t *qe,
+                              int is_key_query, int end_inclusive, const uint64_t *rng_off, const uint64_t *rs,
+                              const uint64_t *re);
+void orc_stab_free(orc_stab_result *r);
+
 /* Timestamp.compareTo (Timestamp.java:208-217) — exported for tests. */
 int orc_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
 

@@ -39,6 +39,22 @@ class MergeResult(C.Structure):
                 ("error", C.c_int), ("message", C.c_char * 256)]
 
 
+class RmmMergeResult(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32),
+                ("key_off", u64p), ("key_a", u64p), ("key_b", u64p),
+                ("val_off", u64p), ("val_src", u64p), ("val_msb", u64p), ("val_lsb", u64p), ("val_node", i32p),
+                ("k2v_off", u64p), ("k2v", i32p), ("error", C.c_int), ("message", C.c_char * 256)]
+
+
+class SliceResult(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("key_off", u64p), ("key_idx", u32p), ("val_off", u64p), ("val_idx", u32p),
+                ("k2v_off", u64p), ("k2v", i32p)]
+
+
+class StabResult(C.Structure):
+    _fields_ = [("off", u64p), ("idx", u32p)]
+
+
 class RangedepsResult(C.Structure):
     _fields_ = [("n_txn", C.c_uint32),
                 ("n_ranges", C.c_uint32), ("rng_start", u64p), ("rng_end", u64p),
@@ -79,6 +95,17 @@ def lib():
         L.orc_rangedeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
                                           u32p, u64p, u64p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_rangedeps_free.argtypes = [C.POINTER(RangedepsResult)]
+        L.orc_rmm_merge.restype = C.POINTER(RmmMergeResult)
+        L.orc_rmm_merge.argtypes = [C.c_uint32, u64p, C.c_int, u64p, u64p, u64p, u64p, u64p, u64p, i32p, u64p, i32p]
+        L.orc_rmm_merge_free.argtypes = [C.POINTER(RmmMergeResult)]
+        L.orc_invert.restype = C.c_int
+        L.orc_invert.argtypes = [C.c_uint32, u64p, i32p, u64p, u64p, u64p, i32p]
+        L.orc_rmm_slice.restype = C.POINTER(SliceResult)
+        L.orc_rmm_slice.argtypes = [C.c_uint32, C.c_int, C.c_int, u64p, u64p, u64p, u64p, u64p, i32p, u64p, u64p, u64p]
+        L.orc_slice_free.argtypes = [C.POINTER(SliceResult)]
+        L.orc_rmm_stab.restype = C.POINTER(StabResult)
+        L.orc_rmm_stab.argtypes = [C.c_uint32, u32p, u64p, u64p, C.c_int, C.c_int, u64p, u64p, u64p]
+        L.orc_stab_free.argtypes = [C.POINTER(StabResult)]
         L.orc_ts_compare.restype = C.c_int
         L.orc_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
@@ -272,3 +299,96 @@ def levelise(off: np.ndarray, dep: np.ndarray, exec_rank: np.ndarray):
 
 def ts_compare(a, b) -> int:
     return lib().orc_ts_compare(*a, *b)
+
+
+def _arr(ptr, n, dt):
+    return np.ctypeslib.as_array(ptr, (max(int(n), 1),))[:int(n)].astype(dt, copy=True)
+
+
+def rmm_merge(grp_off, half: dict, is_range: bool) -> dict:
+    """KeyDeps.merge / RangeDeps.merge per group over raw TxnIds (accord_oracle_rmm.c orc_rmm_merge). `half` holds
+    key_off, key_a, [key_b], val_off, msb, lsb, node, k2v_off, k2v (the acc_rmm_in layout)."""
+    L = lib()
+    grp_off = np.ascontiguousarray(grp_off, dtype=np.uint64)
+    g = len(grp_off) - 1
+    a = {k: np.ascontiguousarray(half[k], dtype=dt) for k, dt in
+         (("key_off", np.uint64), ("key_a", np.uint64), ("val_off", np.uint64), ("msb", np.uint64), ("lsb", np.uint64),
+          ("node", np.int32), ("k2v_off", np.uint64), ("k2v", np.int32))}
+    kb = np.ascontiguousarray(half["key_b"], dtype=np.uint64) if is_range else None
+    r = L.orc_rmm_merge(g, _p(grp_off, u64p), int(is_range), _p(a["key_off"], u64p), _p(a["key_a"], u64p),
+                        _p(kb, u64p) if kb is not None else None, _p(a["val_off"], u64p), _p(a["msb"], u64p),
+                        _p(a["lsb"], u64p), _p(a["node"], i32p), _p(a["k2v_off"], u64p), _p(a["k2v"], i32p))
+    try:
+        R = r.contents
+        if R.error:
+            raise OracleError(R.error, R.message.decode())
+        ko = _arr(R.key_off, g + 1, np.uint64)
+        vo = _arr(R.val_off, g + 1, np.uint64)
+        oo = _arr(R.k2v_off, g + 1, np.uint64)
+        nk, nv, no = int(ko[-1]), int(vo[-1]), int(oo[-1])
+        out = dict(key_off=ko, val_off=vo, k2v_off=oo, key_a=_arr(R.key_a, nk, np.uint64),
+                   src=_arr(R.val_src, nv, np.uint64), msb=_arr(R.val_msb, nv, np.uint64),
+                   lsb=_arr(R.val_lsb, nv, np.uint64), node=_arr(R.val_node, nv, np.int32), k2v=_arr(R.k2v, no, np.int32))
+        if is_range:
+            out["key_b"] = _arr(R.key_b, nk, np.uint64)
+    finally:
+        L.orc_rmm_merge_free(r)
+    return out
+
+
+def invert(src_off, src, nsrc, ntrg):
+    """RelationMultiMap.invert per group (accord_oracle_rmm.c orc_invert): returns (trg_off, trg)."""
+    L = lib()
+    src_off = np.ascontiguousarray(src_off, dtype=np.uint64)
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    nsrc = np.ascontiguousarray(nsrc, dtype=np.uint64)
+    ntrg = np.ascontiguousarray(ntrg, dtype=np.uint64)
+    g = len(src_off) - 1
+    total = int(ntrg.sum()) + int(src_off[-1]) - int(nsrc.sum())
+    trg_off = np.zeros(g + 1, np.uint64)
+    trg = np.zeros(max(total, 1), np.int32)
+    rc = L.orc_invert(g, _p(src_off, u64p), _p(src, i32p), _p(nsrc, u64p), _p(ntrg, u64p), _p(trg_off, u64p),
+                      _p(trg, i32p))
+    if rc:
+        raise OracleError(rc, "invert: entry out of range")
+    return trg_off, trg[:total]
+
+
+def rmm_slice(m: dict, sel_off, sel_s, sel_e, is_range: bool, end_inclusive: bool) -> dict:
+    """KeyDeps.slice / RangeDeps.slice + trimUnusedValues per group (accord_oracle_rmm.c orc_rmm_slice)."""
+    L = lib()
+    a = {k: np.ascontiguousarray(m[k], dtype=dt) for k, dt in
+         (("key_off", np.uint64), ("key_a", np.uint64), ("val_off", np.uint64), ("k2v_off", np.uint64), ("k2v", np.int32))}
+    kb = np.ascontiguousarray(m["key_b"], dtype=np.uint64) if is_range else None
+    so, ss, se = (np.ascontiguousarray(x, dtype=np.uint64) for x in (sel_off, sel_s, sel_e))
+    g = len(a["key_off"]) - 1
+    r = L.orc_rmm_slice(g, int(is_range), int(end_inclusive), _p(a["key_off"], u64p), _p(a["key_a"], u64p),
+                        _p(kb, u64p) if kb is not None else None, _p(a["val_off"], u64p), _p(a["k2v_off"], u64p),
+                        _p(a["k2v"], i32p), _p(so, u64p), _p(ss, u64p), _p(se, u64p))
+    try:
+        R = r.contents
+        ko, vo, oo = (_arr(x, g + 1, np.uint64) for x in (R.key_off, R.val_off, R.k2v_off))
+        out = dict(key_off=ko, val_off=vo, k2v_off=oo, key_idx=_arr(R.key_idx, ko[-1], np.uint32),
+                   val_idx=_arr(R.val_idx, vo[-1], np.uint32), k2v=_arr(R.k2v, oo[-1], np.int32))
+    finally:
+        L.orc_slice_free(r)
+    return out
+
+
+def rmm_stab(grp, qs, qe, is_key_query: bool, end_inclusive: bool, rng_off, rs, re):
+    """Stabbing queries over built RangeDeps (accord_oracle_rmm.c orc_rmm_stab): (off, ascending range indices)."""
+    L = lib()
+    grp = np.ascontiguousarray(grp, dtype=np.uint32)
+    qs = np.ascontiguousarray(qs, dtype=np.uint64)
+    qe = np.ascontiguousarray(qe if qe is not None else qs, dtype=np.uint64)
+    ro, rs_, re_ = (np.ascontiguousarray(x, dtype=np.uint64) for x in (rng_off, rs, re))
+    n = len(grp)
+    r = L.orc_rmm_stab(n, _p(grp, u32p), _p(qs, u64p), _p(qe, u64p), int(is_key_query), int(end_inclusive),
+                       _p(ro, u64p), _p(rs_, u64p), _p(re_, u64p))
+    try:
+        R = r.contents
+        off = _arr(R.off, n + 1, np.uint64)
+        idx = _arr(R.idx, off[-1], np.uint32)
+    finally:
+        L.orc_stab_free(r)
+    return off, idx

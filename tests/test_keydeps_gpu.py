@@ -259,3 +259,27 @@ def test_runs_vs_replay_beyond_one_scan_chunk():
     for t in range(n - 200, n):
         for x, y, what in zip(g.txn(t), o.txn(t), ("keys", "txnIds", "keysToTxnIds")):
             np.testing.assert_array_equal(x, y, err_msg=f"txn {t} {what}")
+
+
+def test_txn_with_more_than_65536_keys(ctx):
+    """A txn listing 70,000 keys (Keys has no cap) with deps on many of them: the global write tier's key-index field is
+    sized from the batch (17 bits here), not fixed at 16 bits."""
+    import oracle
+    rng = np.random.RandomState(65)
+    n, big, nk_big = 300, 200, 70_000
+    kinds = rng.choice([W.READ, W.WRITE], size=n)
+    msb, lsb, node = W.encode_ts(np.ones(n), np.arange(1, n + 1), kinds.astype(np.uint64) << np.uint64(1),
+                                 1 + np.arange(n) % 8)
+    lsb[big] = (lsb[big] & ~np.uint64(0xE)) | np.uint64(W.WRITE << 1)
+    keys = []
+    for t in range(n):
+        keys.append(np.arange(nk_big) if t == big else np.sort(rng.choice(nk_big, size=6, replace=False)))
+    off = np.zeros(n + 1, np.uint32)
+    np.cumsum([len(k) for k in keys], out=off[1:])
+    b = W.Batch(msb, lsb, node.astype(np.int32), msb.copy(), lsb.copy(), node.astype(np.int32).copy(),
+                np.full(n, W.PREACCEPTED, np.uint8), off, W.int_key_code(np.concatenate(keys)))
+    g = ctx.calculate_partial_deps(b)
+    o = oracle.keydeps_batch(b)
+    k, d, a = o.txn(big)
+    assert len(d) > 100 and int(np.max(k)) > 65536
+    assert_same(g, o, b.n_txn, ">65536 keys")

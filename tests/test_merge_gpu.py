@@ -111,3 +111,44 @@ def test_merge_errors_both_paths(force_global):
                          (([5, 9], [3], [2, 2, 0]), IllegalArgumentException)):        # last offset != length
             with pytest.raises(exc):
                 keydeps_merge(c, pack_groups([[gen_keydeps(np.random.RandomState(1))], [bad]]))
+
+
+def test_merge_wide_key_codes_general_path(ctx):
+    """Full-width u64 key codes (hashed keys) on the general radix path (> 256 replies in a group, beyond the LDS tier):
+    the composite sort runs on dense ranks of the codes instead of failing with ACC_E_CAP."""
+    import oracle
+    from accord_amd.deps import keydeps_merge
+    rng = np.random.RandomState(77)
+    wide = rng.randint(0, 2**63, size=400, dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(1)
+    groups = []
+    for g in range(3):
+        reps = []
+        for _ in range(300 if g == 0 else 5):
+            keys, vals, kv = gen_keydeps(rng, n_keys_range=(2, 20), total_range=(1, 60))
+            reps.append(([int(wide[k]) for k in keys], vals, kv))
+        groups.append(reps)
+    # the remapped codes no longer follow the original key order: re-sort each reply's keys
+    m = pack_groups([[_sorted_reply(r) for r in g] for g in groups])
+    out = keydeps_merge(ctx, m)
+    assert ctx.stats().get("merge.lds_tier") == 0
+    assert ctx.stats().get("merge.dense_keys") == 1
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+
+
+def _sorted_reply(r):
+    """Re-sort a reply whose key codes were remapped (order changed): keys ascending, the header and the per-key
+    index lists moved with their keys."""
+    keys, vals, kv = r
+    nk = len(keys)
+    lists, prev = [], nk
+    for i in range(nk):
+        lists.append(kv[prev:kv[i]])
+        prev = kv[i]
+    order = sorted(range(nk), key=lambda i: keys[i])
+    hdr, body = [], []
+    for i in order:
+        body += list(lists[i])
+        hdr.append(nk + len(body))
+    return [keys[i] for i in order], vals, hdr + body
