@@ -4,7 +4,8 @@
 
 Writes <prefix>_kernel_stats.csv (the rocprofv3 --stats table, accord kernels first), and <prefix>_summary.json:
 per-kernel average duration, per-step device time and per-step HBM traffic from the FETCH_SIZE / WRITE_SIZE
-passes. FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B); both counters are KB.
+passes. FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B) for the upper bound and kept
+as is for the lower bound (`*_raw`; random gathers are not the calibrated pattern, see tools/calib_fetch.hip); KB units.
 `steps` = warmup + timed steps of the profiled bench command (every pipeline kernel of a step runs once per step
 or a fixed number of times, so totals / steps are per-step figures).
 """
@@ -66,6 +67,7 @@ def main():
         d["avg_ns"] = d["total_ns"] / d["calls"]
         d["ms_per_step"] = d["total_ns"] / steps / 1e6
         d["hbm_read_bytes_per_step"] = 2.0 * fetch.get(k, 0.0) / steps
+        d["hbm_read_bytes_per_step_raw"] = fetch.get(k, 0.0) / steps
         d["hbm_write_bytes_per_step"] = write.get(k, 0.0) / steps
         d["hbm_read_bytes_per_launch"] = 2.0 * fetch.get(k, 0.0) / max(fcalls.get(k, 0), 1)
         d["hbm_write_bytes_per_launch"] = write.get(k, 0.0) / max(wcalls.get(k, 0), 1)
@@ -74,6 +76,7 @@ def main():
         kernel_ms_per_step=sum(d["ms_per_step"] for d in kernels.values()),
         hbm_read_bytes_per_step=sum(d["hbm_read_bytes_per_step"] for d in kernels.values()),
         hbm_write_bytes_per_step=sum(d["hbm_write_bytes_per_step"] for d in kernels.values()),
+        hbm_read_bytes_per_step_raw=sum(d["hbm_read_bytes_per_step_raw"] for d in kernels.values()),
         kernels=dict(sorted(kernels.items(), key=lambda kv: -kv[1]["total_ns"])),
     )
     out["hbm_bytes_per_step"] = out["hbm_read_bytes_per_step"] + out["hbm_write_bytes_per_step"]
