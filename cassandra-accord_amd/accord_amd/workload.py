@@ -136,8 +136,34 @@ def zipf_sampler(seed: int, salt: int, n_keys: int, s: float, permute: bool):
     if permute:
         perm = np.argsort(stream(seed, salt + 7, n_keys), kind="stable").astype(np.int64)
 
+    table = []
+
+    def inverse_cdf(u):
+        """searchsorted(cdf, u, 'right') through a 2^24-bucket table of cdf indices (bucket bounds bracket the answer
+        within a few ranks; random probes of a 128 MB cdf miss the cache at every level of a plain binary search)."""
+        if not table:
+            nb = 1 << 24
+            table.append(np.searchsorted(cdf, np.arange(nb + 1, dtype=np.float64) / nb, side="right").astype(np.int64))
+        idx = table[0]
+        b = (u * float(len(idx) - 1)).astype(np.int64)
+        lo, hi = idx[b], np.minimum(idx[b + 1], len(cdf))
+        act = np.nonzero(lo < hi)[0]
+        la, ha, ua = lo[act], hi[act], u[act]
+        while len(la):
+            mid = (la + ha) >> 1
+            c = cdf[mid] <= ua
+            la = np.where(c, mid + 1, la)
+            ha = np.where(c, ha, mid)
+            done = la >= ha
+            if done.any():
+                lo[act[done]] = la[done]
+                keep = ~done
+                act, la, ha, ua = act[keep], la[keep], ha[keep], ua[keep]
+        return lo
+
     def sample(offset, n):
-        r = np.searchsorted(cdf, uniform01(seed, salt, n, offset), side="right")
+        u = uniform01(seed, salt, n, offset)
+        r = inverse_cdf(u) if n > (1 << 20) else np.searchsorted(cdf, u, side="right")
         r = np.minimum(r, n_keys - 1)
         return perm[r] if perm is not None else r
     return sample

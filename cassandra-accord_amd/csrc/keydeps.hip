@@ -885,6 +885,7 @@ struct V2View {
     const uint8_t *bc_kind;
     const uint32_t *bcs_exec, *bcs_lastw;
     const uint4 *tinfo;   // per txn: rank, executeAt rank, status | kind << 3
+    const uint32_t *rec32;   // the count pass's per-pair records as u32 (inline entries)
 };
 
 struct Row { uint32_t c[8]; };
@@ -952,10 +953,24 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     return q;
 }
 
-// per-pair run record for the write pass, stored by pair index j (the write pass reads a txn's records
-// contiguously): starts a[6] and lengths l[6] of R1/R2 per class (witnessed classes only), R3 = [bs, bs + bl)
-// filtered by executeAt >= M. 64 B = 4 x uint4.
+// per-pair record for the write pass, stored by pair index j (the write pass reads a txn's records contiguously; a
+// whole 64-B granule per record, so the scatter is full-line writes):
+//   inline  (E <= REC_INLINE): the pair's dependency entries themselves (TxnId ranks, T and filtered R3 entries
+//           already dropped), word 15 = REC_INLINE_FLAG | E. Gathered here in CFK position order, where neighbouring
+//           pairs of a segment read the same class-list lines, instead of by the write pass in txn order;
+//   runs    (otherwise): starts a[6] and lengths l[6] of R1/R2 per class (witnessed classes only), R3 = [bs, bs + bl)
+//           filtered by executeAt >= M; word 15 = 0.
 constexpr uint32_t NO_M = 0xFFFFFFFFu;
+constexpr uint32_t INLINE_M = 0xFFFFFFFEu;   // RunsT::m marker of an inline record
+constexpr uint32_t REC_INLINE = 15;
+constexpr uint32_t REC_INLINE_FLAG = 0x80000000u;
+
+__device__ __forceinline__ void inl_put(uint32_t (&buf)[16], uint32_t &n, uint32_t x)
+{
+#pragma unroll
+    for (uint32_t s = 0; s < REC_INLINE; ++s) if (s == n) buf[s] = x;   // static register indices (no scratch)
+    ++n;
+}
 
 __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out, uint4 *__restrict__ rec)
 {
@@ -981,10 +996,31 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
     }
     const uint32_t j = v.perm[p];
     uint4 *r = rec + 4 * (size_t)j;
-    r[0] = make_uint4(a[0], a[1], a[2], a[3]);
-    r[1] = make_uint4(a[4], a[5], l[0], l[1]);
-    r[2] = make_uint4(l[2], l[3], l[4], l[5]);
-    r[3] = make_uint4(q.bstart, q.has_m ? q.bend - q.bstart : 0u, q.has_m ? q.m : NO_M, 0u);
+    if (e <= REC_INLINE) {
+        uint32_t buf[16] = {};
+        uint32_t n = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < 6; ++q2)
+            for (uint32_t i = 0; i < l[q2]; ++i) {
+                const uint32_t x = v.list_rank[a[q2] + i];
+                if (!(q.bq && x == q.trank)) inl_put(buf, n, x);
+            }
+        if (q.has_m)
+            for (uint32_t i = q.bstart; i < q.bend; ++i)
+                if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) {
+                    const uint32_t x = v.bc_rank[i];
+                    if (!(q.bq && x == q.trank)) inl_put(buf, n, x);
+                }
+        r[0] = make_uint4(buf[0], buf[1], buf[2], buf[3]);
+        r[1] = make_uint4(buf[4], buf[5], buf[6], buf[7]);
+        r[2] = make_uint4(buf[8], buf[9], buf[10], buf[11]);
+        r[3] = make_uint4(buf[12], buf[13], buf[14], REC_INLINE_FLAG | (uint32_t)e);
+    } else {
+        r[0] = make_uint4(a[0], a[1], a[2], a[3]);
+        r[1] = make_uint4(a[4], a[5], l[0], l[1]);
+        r[2] = make_uint4(l[2], l[3], l[4], l[5]);
+        r[3] = make_uint4(q.bstart, q.has_m ? q.bend - q.bstart : 0u, q.has_m ? q.m : NO_M, 0u);
+    }
     cnt_out[j] = e;
 }
 
@@ -1048,6 +1084,34 @@ __device__ __forceinline__ TxnCtx txn_ctx(const V2View &v, const V2Out &o, uint3
     return c;
 }
 
+// Key k's runs from its 64-B record (record index jk); an inline record is one run of its own entries (m = INLINE_M,
+// start = the record index). Returns the key's raw length.
+template <int MAXK>
+__device__ __forceinline__ uint32_t load_record(RunsT<MAXK> &R, const uint4 *rec, uint32_t jk, uint32_t k)
+{
+    const uint4 *r = rec + 4 * (size_t)jk;
+    const uint4 r3 = r[3];
+    if (r3.w & REC_INLINE_FLAG) {
+        const uint32_t e = r3.w & ~REC_INLINE_FLAG;
+        R.start[k][0] = jk;
+        R.pre[k][0] = 0;
+#pragma unroll
+        for (int q = 1; q <= NRUN; ++q) R.pre[k][q] = e;
+        R.m[k] = INLINE_M;
+        return e;
+    }
+    const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
+    const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
+    const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) { R.start[k][q] = a[q]; R.pre[k][q] = acc; acc += l[q]; }
+    R.start[k][6] = r3.x; R.pre[k][6] = acc; acc += r3.y;
+    R.pre[k][7] = acc;
+    R.m[k] = r3.z;
+    return acc;
+}
+
 // Called by ONE wave: lane k < nk fills the runs of key k from its 64-B record. Returns the flattened raw length.
 template <int MAXK>
 __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o, const uint64_t *cnt, const TxnCtx &c)
@@ -1055,17 +1119,7 @@ __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o
     const uint32_t lane = lane_id();
     uint32_t ktot = 0;
     if (lane < c.nk && cnt[c.j0 + lane] != 0) {
-        const uint4 *r = o.rec + 4 * (size_t)(c.j0 + lane);
-        const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-        const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
-        const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
-        uint32_t acc = 0;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) { R.start[lane][q] = a[q]; R.pre[lane][q] = acc; acc += l[q]; }
-        R.start[lane][6] = r3.x; R.pre[lane][6] = acc; acc += r3.y;
-        R.pre[lane][7] = acc;
-        R.m[lane] = r3.z;
-        ktot = acc;
+        ktot = load_record(R, o.rec, c.j0 + lane, lane);
     } else if (lane < c.nk) {
         for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
         R.m[lane] = NO_M;
@@ -1089,6 +1143,10 @@ __device__ __forceinline__ bool fetch_elem(const RunsT<MAXK> &R, const V2View &v
     while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
     k = lo;
     uint32_t off = e - R.kbase[k];
+    if (R.m[k] == INLINE_M) {   // inline record: the entry itself (filters applied by the count pass)
+        x = v.rec32[16 * (size_t)R.start[k][0] + off];
+        return true;
+    }
     uint32_t r = 0;
     while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
     uint32_t idx = R.start[k][r] + (off - R.pre[k][r]);
@@ -1276,17 +1334,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_group(uint32_t n, const uint
     uint32_t ktot = 0;
     if (act && sub < c.nk) {
         if (cnt[c.j0 + sub] != 0) {
-            const uint4 *r = o.rec + 4 * (size_t)(c.j0 + sub);
-            const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-            const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
-            const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
-            uint32_t acc = 0;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) { R.start[sub][q] = a[q]; R.pre[sub][q] = acc; acc += l[q]; }
-            R.start[sub][6] = r3.x; R.pre[sub][6] = acc; acc += r3.y;
-            R.pre[sub][7] = acc;
-            R.m[sub] = r3.z;
-            ktot = acc;
+            ktot = load_record(R, o.rec, c.j0 + sub, sub);
         } else {
             for (int q = 0; q <= NRUN; ++q) R.pre[sub][q] = 0;
             R.m[sub] = NO_M;
@@ -1416,12 +1464,15 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_medium(uint32_t cnt_list, co
 
 // Locate element e of the flattened runs (LDS only): source index, key, R3 flag.
 template <int MAXK>
-__device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, uint32_t e, uint32_t &idx, uint32_t &k, bool &r3)
+__device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, uint32_t e, uint32_t &idx, uint32_t &k, bool &r3,
+                                            bool &inl)
 {
     uint32_t lo = 0, hi = nk;
     while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (R.kbase[mid] <= e) lo = mid; else hi = mid; }
     k = lo;
     uint32_t off = e - R.kbase[k];
+    inl = R.m[k] == INLINE_M;
+    if (inl) { idx = 16 * R.start[k][0] + off; r3 = false; return; }
     uint32_t r = 0;
     while (r + 1 < NRUN && R.pre[k][r + 1] <= off) ++r;
     idx = R.start[k][r] + (off - R.pre[k][r]);
@@ -1493,20 +1544,21 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const ui
     uint32_t kept = 0;
     for (uint32_t e0 = tid; e0 < n2; e0 += BIG_GU * NT) {
         uint32_t idx[BIG_GU], kk[BIG_GU], x[BIG_GU];
-        bool r3[BIG_GU], in[BIG_GU];
+        bool r3[BIG_GU], in[BIG_GU], il[BIG_GU];
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u) {
             const uint32_t e = e0 + u * NT;
             in[u] = e < total;
-            idx[u] = 0; kk[u] = 0; r3[u] = false;
-            if (in[u]) locate_elem(R, c.nk, e, idx[u], kk[u], r3[u]);
+            idx[u] = 0; kk[u] = 0; r3[u] = false; il[u] = false;
+            if (in[u]) locate_elem(R, c.nk, e, idx[u], kk[u], r3[u], il[u]);
         }
 #pragma unroll
-        for (int u = 0; u < BIG_GU; ++u) x[u] = in[u] ? (r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
+        for (int u = 0; u < BIG_GU; ++u)
+            x[u] = in[u] ? (il[u] ? v.rec32[idx[u]] : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u) {
             const uint32_t e = e0 + u * NT;
-            bool keep = in[u] && !(c.bq && x[u] == c.trank);
+            bool keep = in[u] && (il[u] || !(c.bq && x[u] == c.trank));
             if (keep && r3[u]) keep = v.bc_exec[idx[u]] >= R.m[kk[u]] && ((c.wk >> v.bc_kind[idx[u]]) & 1u);
             kept += keep;
             if (e < n2) buf[e] = keep ? ((x[u] << 6) | kk[u]) : 0xFFFFFFFFu;
@@ -2137,6 +2189,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
     uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
     uint4 *rec = ctx->get<uint4>("v2_rec", 4 * P);
+    vv.rec32 = reinterpret_cast<const uint32_t *>(rec);
     launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt, rec);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt, dep_off, P, true, dep_off + P);
     uint32_t *nz = ctx->get<uint32_t>("nz", P);

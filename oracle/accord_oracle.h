@@ -48,6 +48,13 @@ orc_keydeps_result *orc_keydeps_batch(uint32_t n,
                                       const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
                                       uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
                                       uint32_t query_stride);
+/* The same with an explicit query set: txn t is evaluated iff query_mask[t] != 0 (one snapshot build for a scattered
+ * sample). */
+orc_keydeps_result *orc_keydeps_batch_qmask(uint32_t n,
+                                            const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                            const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                            const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                            const uint8_t *query_mask);
 /* The same over a mixed key/range batch (rng_* as orc_rangedeps_batch): range-domain txns are no CommandsForKey
  * members; as queries they scan every CFK whose key lies in their (store-sliced) ranges
  * (InMemoryCommandStore.mapReduceForKey :274-289). For a range txn, key_idx indexes the list of CFK keys its

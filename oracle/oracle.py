@@ -83,6 +83,8 @@ def lib():
         L.orc_keydeps_batch.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
                                         C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_keydeps_free.argtypes = [C.POINTER(KeydepsResult)]
+        L.orc_keydeps_batch_qmask.restype = C.POINTER(KeydepsResult)
+        L.orc_keydeps_batch_qmask.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u8p]
         L.orc_keydeps_mixed.restype = C.POINTER(KeydepsResult)
         L.orc_keydeps_mixed.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
                                         u32p, u64p, u64p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -146,9 +148,20 @@ class OracleError(RuntimeError):
 
 
 def keydeps_batch(batch, n_shards: int = 1, query_lo: int = 0, query_hi: int | None = None,
-                  query_stride: int = 1) -> KeyDepsBatchOut:
+                  query_stride: int = 1, queries=None) -> KeyDepsBatchOut:
+    """orc_keydeps_batch; `queries` (txn indices) selects an explicit query set instead of lo/hi/stride."""
     L = lib()
     n = batch.n_txn
+    if queries is not None:
+        mask = np.zeros(max(n, 1), np.uint8)
+        mask[np.asarray(queries, dtype=np.int64)] = 1
+        arrs = [np.ascontiguousarray(x) for x in (batch.txn_msb.astype(np.uint64), batch.txn_lsb.astype(np.uint64),
+                                                  batch.txn_node.astype(np.int32), batch.exe_msb.astype(np.uint64),
+                                                  batch.exe_lsb.astype(np.uint64), batch.exe_node.astype(np.int32),
+                                                  batch.status.astype(np.uint8), batch.key_off.astype(np.uint32),
+                                                  batch.key_code.astype(np.uint64), mask)]
+        types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u8p]
+        return _keydeps_out(L, L.orc_keydeps_batch_qmask(n, *[_p(a, t) for a, t in zip(arrs, types)]), n)
     arrs = [np.ascontiguousarray(x) for x in (batch.txn_msb.astype(np.uint64), batch.txn_lsb.astype(np.uint64),
                                               batch.txn_node.astype(np.int32), batch.exe_msb.astype(np.uint64),
                                               batch.exe_lsb.astype(np.uint64), batch.exe_node.astype(np.int32),

@@ -1,0 +1,136 @@
+"""BASELINE.json configs at their full size on one MI355X, checked against the oracle on bounded samples plus
+size-independent layout properties over every txn (the O(prefix) / O(range commands) restatements are
+too slow for every query at these sizes).
+
+  config 3: 100M txn-key pairs (12.5M txns x 8 keys over 2^24 keys), zipf(0.99) and uniform;
+  config 4: 10M range txns + 10M key txns x 4 keys (RangeDeps);
+  config 5: 16,384 coordinated txns x 64 replies: KeyDeps.merge + levelisation, every array compared.
+
+The oracle samples run on a sub-batch that keeps every txn (TxnIds, statuses, executeAts) but only the keys of the sampled
+txns: a txn's KeyDeps depend only on the CommandsForKey of its own keys, so the sampled txns' results are unchanged."""
+import numpy as np
+import pytest
+
+from accord_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from accord_amd.deps import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def keys_of(b, ts):
+    idx = np.concatenate([np.arange(int(b.key_off[t]), int(b.key_off[t + 1])) for t in ts])
+    return np.unique(b.key_code[idx])
+
+
+def sub_batch(b, keyset):
+    """Every txn of b, keys restricted to `keyset` (sorted unique codes)."""
+    keep = np.isin(b.key_code, keyset)
+    cnt = np.add.reduceat(keep.astype(np.int64), b.key_off[:-1].astype(np.int64))
+    cnt[np.diff(b.key_off.astype(np.int64)) == 0] = 0
+    off = np.zeros(b.n_txn + 1, np.uint32)
+    np.cumsum(cnt, out=off[1:])
+    return W.Batch(b.txn_msb, b.txn_lsb, b.txn_node, b.exe_msb, b.exe_lsb, b.exe_node, b.status, off, b.key_code[keep])
+
+
+def check_properties(g, b):
+    """Layout properties over every txn (KeyDeps.java:150-172): the header's last end offset is the arena length, TxnIds
+    ascend strictly (batch in TxnId order: index order), a non-bumped txn depends only on earlier txns, key indices
+    ascend inside the txn's keys, entries index the txn's TxnIds."""
+    n = b.n_txn
+    kd = np.diff(g.kd_off.astype(np.int64))
+    al = np.diff(g.arena_off.astype(np.int64))
+    nu = np.diff(g.u_off.astype(np.int64))
+    nz = kd > 0
+    assert ((nu > 0) == nz).all()
+    last_hdr = g.arena[(g.arena_off[:-1].astype(np.int64) + kd - 1)[nz]]
+    np.testing.assert_array_equal(last_hdr, al[nz])
+    assert int(g.total_edges) == int(al.sum() - kd.sum())
+    owner = np.repeat(np.arange(n, dtype=np.int64), nu)
+    d = g.dep_txn.astype(np.int64)
+    same = owner[1:] == owner[:-1]
+    assert (d[1:][same] > d[:-1][same]).all()
+    unbumped = (b.exe_msb == b.txn_msb) & (b.exe_lsb == b.txn_lsb) & (b.exe_node == b.txn_node)
+    assert (d[unbumped[owner]] < owner[unbumped[owner]]).all()
+    kown = np.repeat(np.arange(n, dtype=np.int64), kd)
+    ki = g.key_idx.astype(np.int64)
+    ks = kown[1:] == kown[:-1]
+    assert (ki[1:][ks] > ki[:-1][ks]).all()
+    assert (ki < np.diff(b.key_off.astype(np.int64))[kown]).all()
+
+
+def compare_sample(g, b, ranges):
+    import oracle
+    ts = np.concatenate([np.arange(lo, hi, st) for lo, hi, st in ranges])
+    o = oracle.keydeps_batch(sub_batch(b, keys_of(b, ts)), queries=ts)
+    for t in ts.tolist():
+        for x, y, what in zip(g.txn(t), o.txn(t), ("keys", "txnIds", "keysToTxnIds")):
+            np.testing.assert_array_equal(x, y, err_msg=f"txn {t} {what}")
+
+
+@pytest.mark.parametrize("dist", ["zipf", "uniform"])
+def test_config3_full(ctx, dist):
+    """BASELINE config 3 on one GPU: 100M txn-key pairs. Oracle sample: the 150 latest txns (uncommitted window, the
+    hottest outputs) and 150 txns strided over the batch."""
+    n = 12_500_000
+    b = W.keydeps_batch(n, 8, 1 << 24, W.CONFIG_SEEDS["3z" if dist == "zipf" else "3u"], dist, 0.99, status_model="model")
+    assert b.n_pairs == 100_000_000
+    g = ctx.calculate_partial_deps(b)
+    assert ctx.stats().get("keydeps.path_replay", 0) == 0
+    check_properties(g, b)
+    compare_sample(g, b, [(n - 150, n, 1), (7, n, n // 150)])
+
+
+def test_config4_full(ctx):
+    """BASELINE config 4: RangeDeps of 10M range txns + 10M key txns at full size; every txn's structure, and the oracle
+    (a walk of all 10M range commands per query) on 100 strided txns."""
+    import oracle
+    rb = W.config4(1.0)
+    g = ctx.calculate_partial_range_deps(rb)
+    n = rb.n_txn
+    nr = np.diff(g.rd_off.astype(np.int64))
+    na = np.diff(g.arena_off.astype(np.int64))
+    nu = np.diff(g.u_off.astype(np.int64))
+    assert (na >= nr).all() and ((na > nr) == (nr > 0)).all() and ((nu > 0) == (nr > 0)).all()
+    ds, de = g.rng_start.astype(np.uint64), g.rng_end.astype(np.uint64)
+    assert ((ds[1:] > ds[:-1]) | ((ds[1:] == ds[:-1]) & (de[1:] > de[:-1]))).all()
+    stride = n // 100 + 1
+    o = oracle.rangedeps_batch(rb, query_lo=3, query_hi=n, query_stride=stride)
+    for t in range(3, n, stride):
+        for x, y in zip(g.txn(t), o.txn(t)):
+            np.testing.assert_array_equal(x, y, err_msg=f"txn {t}")
+
+
+def test_config5_full(ctx):
+    """BASELINE config 5 at full size through the bench's device chain: every array of the merged view (keys, TxnIds,
+    keysToTxnIds of all 16,384 coordinated txns) and the level / order of the levelised graph, against the oracle."""
+    import torch
+    import oracle
+    from accord_amd import _lib as L
+    from accord_amd.deps import merge_copy_out, merge_levelise_device
+    n = 16_384
+    m = W.merge_batch(n_txn=n, replies=64)
+    er = W.merge_exec_rank(n)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in m.items()}
+    er_d = torch.from_numpy(er).to(dev)
+    level = torch.empty(n, dtype=torch.int32, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    mi = L.MergeIn(L.ACC_MEM_DEVICE, n, len(m["key_off"]) - 1,
+                   *(t[k].data_ptr() for k in ("grp_off", "key_off", "key_code", "val_off", "txn_rank", "k2v_off", "k2v")))
+    view, nl = merge_levelise_device(ctx, mi, er_d.data_ptr(), level.data_ptr(), order.data_ptr())
+    ctx.sync()
+    got = merge_copy_out(ctx, view)
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    l2, o2, nl2 = oracle.levelise(ref["val_off"], ref["txn_rank"], er)
+    np.testing.assert_array_equal(level.cpu().numpy().view(np.uint32), l2)
+    np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), o2)
+    assert nl == nl2
