@@ -5,8 +5,8 @@
 // else 1 + max level(dep); order = txns sorted by (level, executeAt rank, index).
 //
 // Every counted edge goes from a lower to a higher executeAt rank, so levels are final in executeAt order.
-// One workgroup walks the txns in executeAt order (k_lv_walk); a dep's level is awaited by polling its
-// published value, so the walk's length is the graph's dependency-chain depth at LDS latency.
+// A persistent grid of waves walks the txns in executeAt order, one txn per wave (k_lv_waves); a dep's level is
+// awaited by polling its published value.
 #include "prims.hpp"
 
 namespace acc {
@@ -28,83 +28,68 @@ __global__ __launch_bounds__(BLOCK) void k_lv_check(uint32_t n, const uint64_t *
         if (dep[e] >= n) { atomicOr(err, 2u); return; }
 }
 
-// One workgroup of LV_THREADS lanes; lane j owns the txns at exec-order positions j, j + LV_THREADS, ... and
-// walks them in that order. Per txn it advances a cursor over the txn's deps: deps with exec rank >= its own
-// are skipped; a counted dep whose level is still unpublished (0) stops the cursor and the lane polls it again
-// on its next iteration (no barrier: lanes and waves progress independently). The txn at the earliest
-// pending position only depends on published txns, so the walk always advances and every lane's loop ends.
-// Published value = level + 1, indexed by txn. kLds: the level and exec-rank columns (8 B per txn) live in
-// LDS (n <= LV_LDS_MAX); otherwise levels are global (agent-scope atomics bypass the non-coherent L1) and
-// exec ranks are read from global.
-constexpr int LV_THREADS = 1024;
-constexpr int LV_UNROLL = 4;
-constexpr uint32_t LV_LDS_MAX = 20000;   // 8 B/txn of the 160 KiB LDS
+// Wave-per-txn walk: every wave of a persistent grid takes tickets (positions in executeAt order) from one counter;
+// for its txn, the 64 lanes read the dep list 64 at a time, keep the deps with an earlier executeAt (Commands.
+// updateWaitingOn drops the others, local/Commands.java:804-810), read their published levels (level + 1, agent scope:
+// the XCDs' L2s are not coherent) and re-poll the ones still unpublished, then the wave publishes 1 + max. A dep always
+// has an earlier ticket, held by a running wave, so the earliest pending txn only waits on published ones and every
+// wave's loop ends. The critical path is the graph's dependency depth at one memory round trip per level (~2 us:
+// config 5's 709 levels in 1.5 ms); the deps of a txn are read in parallel. (A tiled variant resolving intra-tile hops
+// in LDS measured 7x slower: each wave then walks its share of the tile serially at global-load latency.)
+constexpr int LV_PEND = 4;   // unpublished deps a lane tracks in registers before it waits in place
 
-template <bool kLds>
-__global__ __launch_bounds__(LV_THREADS) void k_lv_walk(uint32_t n, const uint32_t *__restrict__ order_exec,
-                                                        const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
-                                                        const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ level_g,
-                                                        uint32_t *__restrict__ max_level)
+__device__ __forceinline__ uint32_t lv_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__global__ __launch_bounds__(BLOCK) void k_lv_waves(uint32_t n, const uint32_t *__restrict__ order_exec, const uint64_t *__restrict__ off,
+                                                    const uint32_t *__restrict__ dep, const uint32_t *__restrict__ exec_rank,
+                                                    uint32_t *__restrict__ lv, uint32_t *__restrict__ ticket,
+                                                    uint32_t *__restrict__ max_level)
 {
-    extern __shared__ uint32_t lds[];
-    uint32_t *lv = kLds ? lds : level_g;             // level + 1 per txn, 0 = pending
-    const uint32_t *er_col = kLds ? lds + n : exec_rank;
-    if (kLds) {
-        for (uint32_t t = threadIdx.x; t < n; t += LV_THREADS) { lds[t] = 0; lds[n + t] = exec_rank[t]; }
-        __syncthreads();
-    }
-    auto ld = [&](uint32_t d) -> uint32_t {
-        if (kLds) return __hip_atomic_load(&lv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return __hip_atomic_load(&lv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
+    const uint32_t lane = lane_id();
     uint32_t my_max = 0;
-    uint32_t i = threadIdx.x;
-    uint32_t t = 0, er = 0, l = 0;
-    uint64_t cur = 0, b = 0;
-    if (i < n) { t = order_exec[i]; er = er_col[t]; cur = off[t]; b = off[t + 1]; }
-    while (__any(i < n)) {
-        if (i < n) {
-            bool pending = false;
-            // LV_UNROLL deps per round: independent global loads in flight together
-            while (cur < b && !pending) {
-                uint32_t dd[LV_UNROLL];
+    while (true) {
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(ticket, 1u);
+        i = __shfl(i, 0, 64);
+        if (i >= n) break;
+        const uint32_t t = order_exec[i];
+        const uint32_t er = exec_rank[t];
+        const uint64_t a = off[t], b = off[t + 1];
+        uint32_t l = 0;
+        uint32_t pend[LV_PEND];
+        uint32_t np = 0;
+        for (uint64_t c = a; c < b; c += 64) {
+            const uint64_t e = c + lane;
+            if (e < b) {
+                const uint32_t d = dep[e];
+                if (exec_rank[d] < er) {
+                    uint32_t v = lv_load(&lv[d]);
+                    if (v) l = max(l, v);
+                    else if (np < LV_PEND) {
 #pragma unroll
-                for (int q = 0; q < LV_UNROLL; ++q) dd[q] = cur + q < b ? dep[cur + q] : 0xFFFFFFFFu;
-#pragma unroll
-                for (int q = 0; q < LV_UNROLL; ++q) {
-                    if (pending || dd[q] == 0xFFFFFFFFu) continue;
-                    if (er_col[dd[q]] >= er) { ++cur; continue; }
-                    uint32_t v = ld(dd[q]);
-                    if (v == 0) { pending = true; continue; }
-                    l = max(l, v);           // v = level(dep) + 1
-                    ++cur;
+                        for (int q = 0; q < LV_PEND; ++q) if ((uint32_t)q == np) pend[q] = d;
+                        ++np;
+                    } else {
+                        while ((v = lv_load(&lv[d])) == 0) __builtin_amdgcn_s_sleep(1);
+                        l = max(l, v);
+                    }
                 }
             }
-            if (!pending) {
-                if (kLds) __hip_atomic_store(&lv[t], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else __hip_atomic_store(&lv[t], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                my_max = max(my_max, l);
-                i += LV_THREADS;
-                l = 0;
-                if (i < n) { t = order_exec[i]; er = er_col[t]; cur = off[t]; b = off[t + 1]; }
+        }
+#pragma unroll
+        for (int q = 0; q < LV_PEND; ++q) {
+            if ((uint32_t)q < np) {
+                uint32_t v;
+                while ((v = lv_load(&lv[pend[q]])) == 0) __builtin_amdgcn_s_sleep(1);
+                l = max(l, v);
             }
         }
-    }
-    __syncthreads();
-    if (kLds)
-        for (uint32_t u = threadIdx.x; u < n; u += LV_THREADS) level_g[u] = lds[u];
-    // block max of levels -> n_levels - 1
-    __shared__ uint32_t red[LV_THREADS / 64];
-    uint32_t v = my_max;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0;
-        for (int q = 0; q < LV_THREADS / 64; ++q) m = max(m, red[q]);
-        *max_level = m;
+        for (int d = 32; d >= 1; d >>= 1) l = max(l, (uint32_t)__shfl_xor(l, d, 64));
+        if (lane == 0) __hip_atomic_store(&lv[t], l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        my_max = max(my_max, l);
     }
+    if (lane == 0 && my_max) atomicMax(max_level, my_max);
 }
 
 // published level + 1 -> level
@@ -158,18 +143,13 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     if (e0 & 1) fail(ACC_E_ARG, "graph offsets must be non-decreasing");
     if (e0 & 2) fail(ACC_E_ARG, "dependency index out of range");
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
-    uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);
-    if (n <= LV_LDS_MAX) {
-        const size_t lds = (size_t)n * 8;
-        if (lds > 64 * 1024)
-            ACC_HIP(hipFuncSetAttribute((const void *)k_lv_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        launch(ctx, "lv_walk", k_lv_walk<true>, dim3(1), dim3(LV_THREADS), lds, n, (const uint32_t *)order_exec, off, dep,
-               exec_rank, level, maxl);
-    } else {
-        ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
-        launch(ctx, "lv_walk", k_lv_walk<false>, dim3(1), dim3(LV_THREADS), 0, n, (const uint32_t *)order_exec, off, dep,
-               exec_rank, level, maxl);
-    }
+    uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
+    ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
+    ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
+    // a persistent grid of up to 4096 waves (16 per CU): enough txns in flight to cover the memory round trips
+    const uint32_t waves = std::min<uint32_t>(n, 4096u);
+    launch(ctx, "lv_walk", k_lv_waves, dim3((waves + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep,
+           exec_rank, level, maxl + 1, maxl);
     launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
     const int pbits = bits_for(n - 1);
     launch(ctx, "lv_order_keys", k_lv_order_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)level,

@@ -33,7 +33,7 @@ def test_levelise_random(ctx, n, max_deps):
     assert nl == nl2
 
 
-@pytest.mark.parametrize("n", [5000, 30000])
+@pytest.mark.parametrize("n", [5000, 30000, 200000])
 def test_levelise_long_chain(ctx, n):
     """A hot-key write chain: every txn depends on its predecessor (depth n; 30000 takes the global-memory walk)."""
     import oracle
@@ -93,3 +93,35 @@ def test_merge_then_levelise_device(ctx):
     np.testing.assert_array_equal(level.cpu().numpy().view(np.uint32), l2)
     np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), o2)
     assert nl == nl2 and nl > 1
+
+
+def test_levelise_one_million(ctx):
+    """1M txns, deps mostly on recent txns in executeAt order (a hot-key write chain runs through them), plus random
+    far deps and deps executing later (ignored): the persistent multi-workgroup walk against the oracle."""
+    import oracle
+    from accord_amd.deps import levelise
+    rng = np.random.RandomState(2024)
+    n, k = 1_000_000, 6
+    er = rng.permutation(n).astype(np.uint32)
+    pos = np.argsort(er).astype(np.int64)             # txn at executeAt position p
+    src = np.repeat(np.arange(n, dtype=np.int64), k)
+    p = er[src].astype(np.int64)
+    back = np.minimum(p, rng.randint(1, 3000, size=n * k))
+    near = pos[np.maximum(p - back, 0)]
+    far = rng.randint(0, n, size=n * k)
+    d = np.where(rng.rand(n * k) < 0.9, near, far)
+    chain = pos[np.maximum(p[::k] - 1, 0)]            # each txn also depends on its exec predecessor: depth ~n/k... ~n
+    allsrc = np.concatenate([src, np.arange(n)])
+    alld = np.concatenate([d, chain])
+    o = np.lexsort((alld, allsrc))
+    allsrc, alld = allsrc[o], alld[o]
+    keep = np.ones(len(alld), bool)
+    keep[1:] = (allsrc[1:] != allsrc[:-1]) | (alld[1:] != alld[:-1])
+    allsrc, alld = allsrc[keep], alld[keep]
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(np.bincount(allsrc, minlength=n), out=off[1:])
+    lv, order, nl = levelise(ctx, off, alld.astype(np.uint32), er)
+    l2, o2, nl2 = oracle.levelise(off, alld.astype(np.uint32), er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == nl2 and nl > 1000
