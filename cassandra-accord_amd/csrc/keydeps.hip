@@ -19,6 +19,8 @@
 //   5. build       per-T union of the per-key lists, indices into it, Java keysToTxnIds layout.
 #include "dict.hpp"
 
+#include <vector>
+
 namespace acc {
 
 // Timestamp words: w0 = msb (unsigned), w1 = lsb & IDENTITY_LSB (lowHlc then identity flags, unsigned
@@ -972,11 +974,10 @@ __device__ __forceinline__ void inl_put(uint32_t (&buf)[16], uint32_t &n, uint32
     ++n;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t *__restrict__ cnt_out, uint4 *__restrict__ rec)
+__device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
+                                                  uint4 *__restrict__ rec, uint32_t *__restrict__ bigflag)
 {
-    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= P) return;
-    V2Query q = v2_query(v, (uint32_t)p);
+    V2Query q = v2_query(v, p);
     uint32_t a[6] = {}, l[6] = {};
     uint64_t e = 0;
 #pragma unroll
@@ -1019,9 +1020,25 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
         r[0] = make_uint4(a[0], a[1], a[2], a[3]);
         r[1] = make_uint4(a[4], a[5], l[0], l[1]);
         r[2] = make_uint4(l[2], l[3], l[4], l[5]);
-        r[3] = make_uint4(q.bstart, q.has_m ? q.bend - q.bstart : 0u, q.has_m ? q.m : NO_M, 0u);
+        r[3] = make_uint4(q.bstart, q.has_m ? q.bend - q.bstart : 0u, q.has_m ? q.m : NO_M, (uint32_t)e);
+        bigflag[owner[j]] = 1u;
     }
-    cnt_out[j] = e;
+    return e;
+}
+
+// Also: bigflag[T] = 1 for txns with a run record (they take the v2 tiers, the rest the stream pass) and per-block
+// entry totals (blk_e) for the batch's E.
+__global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, const uint32_t *__restrict__ owner,
+                                                    uint4 *__restrict__ rec, uint32_t *__restrict__ bigflag,
+                                                    uint64_t *__restrict__ blk_e)
+{
+    __shared__ uint64_t lds[WAVES];
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t e = 0;
+    if (p < P) e = v2_count_one(v, (uint32_t)p, owner, rec, bigflag);
+    uint64_t total;
+    block_exclusive(e, OpAdd<uint64_t>(), lds, total);
+    if (threadIdx.x == 0) blk_e[blockIdx.x] = total;
 }
 
 // ---- write pass, three tiers by E_T (dependency entries of the txn; 98.7% of config-2 txns have <= 64):
@@ -1033,8 +1050,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, uint64_t
 // the runs are gathered flattened by all lanes, T itself and non-qualifying R3 entries are dropped.
 
 constexpr int NRUN = 7;
-constexpr int TINY_E = 16, TINY_K = 16;
-constexpr int SMALL_E = 64, SMALL_K = 32;
 constexpr int MED_E = 1024, MED_K = 64;
 constexpr int BIG_K = 64;
 constexpr int BIG_E = 8192;                 // raw entries per block in LDS (32 KiB of u32 records)
@@ -1259,207 +1274,41 @@ __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t pre
     return distinct + (uint32_t)__popcll(bal);
 }
 
-// Tier routing (run once per txn after the count pass) + per-txn sizes.
-__global__ __launch_bounds__(BLOCK) void k_v2_sizes(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                    const uint32_t *__restrict__ cnz, uint64_t *__restrict__ kd_cnt,
-                                                    uint64_t *__restrict__ a_cnt, uint32_t *__restrict__ med_list,
-                                                    uint32_t *__restrict__ big_list, uint32_t *__restrict__ small_list,
-                                                    uint32_t *__restrict__ g32_list, uint64_t *__restrict__ gstat)
-{
-    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool med = false, big = false, sml = false, mid = false;
-    if (t < n) {
-        uint32_t j0 = key_off[t], j1 = key_off[t + 1];
-        uint64_t kd = cnz[j1] - cnz[j0];
-        uint64_t E = dep_off[j1] - dep_off[j0];
-        kd_cnt[t] = kd;
-        a_cnt[t] = kd + E;
-        uint32_t nk = j1 - j0;
-        bool tiny = E <= TINY_E && nk <= TINY_K;
-        bool g32 = !tiny && E <= 32 && nk <= 32;
-        bool small = E <= SMALL_E && nk <= SMALL_K;
-        sml = small && !tiny && !g32;
-        mid = g32;
-        med = !small && E <= MED_E && nk <= MED_K;
-        big = !small && !med && E > 0;
-    }
-    // block-aggregated appends: one atomic per list per block (list order is irrelevant: every txn writes only its
-    // own outputs)
-    __shared__ uint64_t lds[WAVES];
-    __shared__ uint32_t base[4];
-    // 10-bit fields (<= 256 per block): medium, big, small, 32-lane group
-    const uint64_t packed = (med ? 1ull : 0ull) | (big ? 1ull << 10 : 0ull) | (sml ? 1ull << 20 : 0ull) | (mid ? 1ull << 30 : 0ull);
-    uint64_t total;
-    const uint64_t pre = block_exclusive(packed, OpAdd<uint64_t>(), lds, total);
-    if (threadIdx.x < 4) {
-        const int slot[4] = { 0, 1, 5, 7 };
-        const uint32_t cnt = (uint32_t)((total >> (10 * threadIdx.x)) & 1023u);
-        base[threadIdx.x] = cnt ? (uint32_t)atomicAdd((unsigned long long *)&gstat[slot[threadIdx.x]], (unsigned long long)cnt) : 0u;
-    }
-    __syncthreads();
-    if (med) med_list[base[0] + (uint32_t)(pre & 1023u)] = t;
-    if (big) big_list[base[1] + (uint32_t)((pre >> 10) & 1023u)] = t;
-    if (sml) small_list[base[2] + (uint32_t)((pre >> 20) & 1023u)] = t;
-    if (mid) g32_list[base[3] + (uint32_t)((pre >> 30) & 1023u)] = t;
-}
-
-// Group tiers: G = 16 (E <= 16, <= 16 keys; over every txn, also writes u_cnt = 0 for txns without deps) and G = 32
-// (16 < E <= 32, <= 32 keys; over a routed list): 64 / G txns per wave, one G-lane group each. Same steps as the
-// small tier (runs from the count-pass records, flattened gather, register bitonic, emit) on group-masked ballots and
-// G-lane shuffles.
-template <int G, bool LIST>
-__global__ __launch_bounds__(BLOCK) void k_v2_write_group(uint32_t n, const uint32_t *__restrict__ list, V2View v,
-                                                          const uint64_t *__restrict__ cnt, V2Out o)
-{
-    constexpr int GPB = BLOCK / G;
-    constexpr int KB = G == 16 ? 4 : 5;   // key index bits
-    __shared__ RunsT<G> sruns[GPB];
-    __shared__ uint64_t sbuf[GPB][G];
-    const uint32_t lane = lane_id(), sub = lane & (G - 1), grp = threadIdx.x / G, g0 = lane & (64 - G);
-    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << g0;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t i = blockIdx.x * GPB + grp;
-    bool act = i < n;
-    const uint32_t t = act ? (LIST ? list[i] : i) : 0u;
-    TxnCtx c{};
-    if (act) {
-        const uint32_t j0 = o.key_off[t], j1 = o.key_off[t + 1];
-        const uint64_t E64 = o.dep_off[j1] - o.dep_off[j0];
-        if (E64 == 0) { if (sub == 0) o.u_cnt[t] = 0; act = false; }
-        else if (E64 > (uint64_t)G || j1 - j0 > (uint32_t)G) act = false;
-    }
-    if (act) c = txn_ctx(v, o, t);
-    RunsT<G> &R = sruns[grp];
-    uint64_t *buf = sbuf[grp];
-    uint32_t ktot = 0;
-    if (act && sub < c.nk) {
-        if (cnt[c.j0 + sub] != 0) {
-            ktot = load_record(R, o.rec, c.j0 + sub, sub);
-        } else {
-            for (int q = 0; q <= NRUN; ++q) R.pre[sub][q] = 0;
-            R.m[sub] = NO_M;
-        }
-    }
-    uint32_t incl = ktot;
-#pragma unroll
-    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
-        const uint32_t u = __shfl_up(incl, d, 64);
-        if (sub >= d) incl += u;
-    }
-    if (act && sub < c.nk) R.kbase[sub] = incl - ktot;
-    const uint32_t total = __shfl(incl, (int)(g0 + G - 1), 64);
-    if (act && sub == 0) R.kbase[c.nk] = total;
-    uint32_t maxtot = act ? total : 0;
-#pragma unroll
-    for (int d = G; d < 64; d <<= 1) maxtot = max(maxtot, (uint32_t)__shfl_xor(maxtot, d, 64));
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    uint32_t cursor = 0;
-    for (uint32_t c0 = 0; c0 < maxtot; c0 += G) {
-        const uint32_t e = c0 + sub;
-        bool keep = false;
-        uint32_t x = 0, k = 0;
-        if (act && e < total) keep = fetch_elem(R, v, c, e, x, k);
-        const uint64_t bal = __ballot(keep) & gmask;
-        if (keep) {
-            const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-            if (slot < (uint32_t)G) buf[slot] = ((uint64_t)x << 16) | k;
-        }
-        cursor += (uint32_t)__popcll(bal);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (act && cursor != c.E) {
-        if (sub == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
-        act = false;
-    }
-    const bool in = act && sub < c.E;
-    uint64_t x = in ? buf[sub] : ~0ull;
-#pragma unroll
-    for (uint32_t k = 2; k <= (uint32_t)G; k <<= 1) {
-#pragma unroll
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint64_t y = shfl_xor64(x, (int)jj);
-            const bool up = (sub & k) == 0, lower = (sub & jj) == 0;
-            const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
-            x = (lower == up) ? lo : hi;
-        }
-    }
-    const uint64_t prev = shfl_up(x, 1);
-    const uint32_t val = (uint32_t)(x >> 16), kj = (uint32_t)(x & 0xFFFFu);
-    const bool nw = in && (sub == 0 || (uint32_t)(prev >> 16) != val);
-    const uint64_t bal = __ballot(nw) & gmask;
-    const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
-    uint64_t peers = __ballot(in) & gmask;
-#pragma unroll
-    for (int b = 0; b < KB; ++b) {
-        const uint64_t bb = __ballot((kj >> b) & 1u);
-        peers &= ((kj >> b) & 1u) ? bb : ~bb;
-    }
-    const uint32_t before = (uint32_t)__popcll(peers & lt);
-    if (in) {
-        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
-        const uint64_t kbase = o.dep_off[c.j0 + kj] - c.e0;
-        o.arena[abase + kbase + before] = (int32_t)idx;
-        if (nw) o.dep_scratch[c.e0 + idx] = o.txn_of_rank[val];
-    }
-    if (act && sub == 0) o.u_cnt[t] = (uint32_t)__popcll(bal);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_v2_write_small(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
-                                                          const uint64_t *__restrict__ cnt, V2Out o)
-{
-    __shared__ uint64_t sbuf[WAVES][SMALL_E];
-    __shared__ RunsT<SMALL_K> sruns[WAVES];
-    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t i = blockIdx.x * WAVES + wave;
-    if (i >= cnt_list) return;
-    const uint32_t t = list[i];
-    TxnCtx c = txn_ctx(v, o, t);
-    RunsT<SMALL_K> &R = sruns[wave];
-    uint64_t *buf = sbuf[wave];
-    uint32_t total = compute_runs(R, v, o, cnt, c);
-    uint32_t got = gather_to(buf, SMALL_E, R, v, c, total);
-    if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
-    const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
-    uint64_t x = lane < c.E ? buf[lane] : ~0ull;
-    x = wave_bitonic_reg(x);
-    uint64_t prev = shfl_up(x, 1);
-    uint32_t distinct = emit_chunk(x, lane < c.E, prev, lane > 0, 0, R.kc, o, c, abase);
-    if (lane == 0) o.u_cnt[t] = distinct;
-}
-
-__global__ __launch_bounds__(BLOCK) void k_v2_write_medium(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
-                                                           const uint64_t *__restrict__ cnt, V2Out o)
+// Persistent over the routed list (count on the device: the v3 routing runs after the last host sync).
+__global__ __launch_bounds__(BLOCK) void k_v2_write_medium(const uint64_t *__restrict__ cnt_dev, const uint32_t *__restrict__ list,
+                                                           V2View v, const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ uint64_t sbuf[WAVES][MED_E];
     __shared__ RunsT<MED_K> sruns[WAVES];
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t i = blockIdx.x * WAVES + wave;
-    if (i >= cnt_list) return;
-    const uint32_t t = list[i];
-    TxnCtx c = txn_ctx(v, o, t);
+    const uint32_t cnt_list = (uint32_t)*cnt_dev;
     RunsT<MED_K> &R = sruns[wave];
     uint64_t *buf = sbuf[wave];
-    uint32_t total = compute_runs(R, v, o, cnt, c);
-    uint32_t got = gather_to(buf, MED_E, R, v, c, total);
-    if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); return; }
-    const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
-    uint32_t n2 = 128;
-    while (n2 < c.E) n2 <<= 1;
-    for (uint32_t q = c.E + lane; q < n2; q += 64) buf[q] = ~0ull;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    wave_bitonic_lds(buf, n2);
-    uint32_t distinct = 0;
-    for (uint32_t q0 = 0; q0 < c.E; q0 += 64) {
-        uint32_t q = q0 + lane;
-        bool in = q < c.E;
-        uint64_t x = in ? buf[q] : 0;
-        uint64_t prev = q > 0 ? buf[q - 1] : 0;
-        distinct = emit_chunk(x, in, prev, q > 0, distinct, R.kc, o, c, abase);
+    for (uint32_t i = blockIdx.x * WAVES + wave; i < cnt_list; i += gridDim.x * WAVES) {
+        const uint32_t t = list[i];
+        TxnCtx c = txn_ctx(v, o, t);
+        uint32_t total = compute_runs(R, v, o, cnt, c);
+        uint32_t got = gather_to(buf, MED_E, R, v, c, total);
+        if (got != c.E) { if (lane == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull); continue; }
+        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+        uint32_t n2 = 128;
+        while (n2 < c.E) n2 <<= 1;
+        for (uint32_t q = c.E + lane; q < n2; q += 64) buf[q] = ~0ull;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        wave_bitonic_lds(buf, n2);
+        uint32_t distinct = 0;
+        for (uint32_t q0 = 0; q0 < c.E; q0 += 64) {
+            uint32_t q = q0 + lane;
+            bool in = q < c.E;
+            uint64_t x = in ? buf[q] : 0;
+            uint64_t prev = q > 0 ? buf[q - 1] : 0;
+            distinct = emit_chunk(x, in, prev, q > 0, distinct, R.kc, o, c, abase);
+        }
+        if (lane == 0) o.u_cnt[t] = distinct;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (lane == 0) o.u_cnt[t] = distinct;
 }
 
 // Locate element e of the flattened runs (LDS only): source index, key, R3 flag.
@@ -1484,43 +1333,33 @@ __device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, u
 // quarter of the sorted entries with per-key / distinct-value bases from a per-wave count pass.
 constexpr int BIG_GU = 4;   // independent loads in flight per thread during the gather
 
-__global__ __launch_bounds__(BLOCK) void k_v2_route_fb(uint32_t nbig, const uint32_t *__restrict__ big_list,
-                                                       const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                       uint32_t *__restrict__ fb_list, uint64_t *__restrict__ gstat)
-{
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= nbig) return;
-    const uint32_t t = big_list[i];
-    fb_list[atomicAdd((unsigned long long *)&gstat[3], 1ull)] = t;
-    atomicAdd((unsigned long long *)&gstat[4], (unsigned long long)(dep_off[key_off[t + 1]] - dep_off[key_off[t]]));
-}
-
 // Sort records are u32 (TxnId rank << 6 | key index): half the LDS of u64 records, twice the blocks per CU. The
 // host takes this tier only when ranks fit 25 bits (2N <= 2^25). CAP = raw run elements per block: 8192 (32 KiB,
-// routed by k_v2_sizes) or 32768 (128 KiB, txns the first launch passes on via gstat[6] / huge_list); beyond that
+// routed by k_v3_bigfill) or 32768 (128 KiB, txns the first launch passes on via gstat[6] / huge_list); beyond that
 // the global path.
 template <int CAP, int NT>
-__global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const uint32_t *__restrict__ list, V2View v,
-                                                        const uint64_t *__restrict__ cnt, V2Out o)
+struct BigLds {
+    uint32_t buf[CAP];
+    RunsT<BIG_K> R;
+    uint32_t s_kept;
+    uint32_t wk_cnt[NT / 64][BIG_K];
+    uint32_t wdist[NT / 64];
+};
+
+template <int CAP, int NT>
+__device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const uint64_t *__restrict__ cnt, const V2Out &o)
 {
-    __shared__ uint32_t buf[CAP];
-    __shared__ RunsT<BIG_K> R;
-    __shared__ uint32_t s_kept;
+    uint32_t *buf = L.buf;
+    RunsT<BIG_K> &R = L.R;
     constexpr int NW = NT / 64;
-    __shared__ uint32_t wk_cnt[NW][BIG_K];
-    __shared__ uint32_t wdist[NW];
-    const uint32_t b = blockIdx.x;
-    if (CAP > BIG_E) cnt_list = (uint32_t)o.gstat[6];   // second launch: the count written by the first
-    if (b >= cnt_list) return;
-    const uint32_t t = list[b];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     TxnCtx c = txn_ctx(v, o, t);
     bool oversize = c.nk > BIG_K || c.E > CAP;
     if (!oversize) {
         if (tid < 64) compute_runs(R, v, o, cnt, c);
         if (tid < BIG_K)
-            for (int w = 0; w < NW; ++w) wk_cnt[w][tid] = 0;
-        if (tid == 0) s_kept = 0;
+            for (int w = 0; w < NW; ++w) L.wk_cnt[w][tid] = 0;
+        if (tid == 0) L.s_kept = 0;
         __syncthreads();
         oversize = R.total > CAP;
     }
@@ -1565,9 +1404,9 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const ui
         }
     }
     kept = wave_inclusive(kept, OpAdd<uint32_t>());
-    if (lane == 63) atomicAdd(&s_kept, kept);
+    if (lane == 63) atomicAdd(&L.s_kept, kept);
     __syncthreads();
-    if (s_kept != c.E) {
+    if (L.s_kept != c.E) {
         if (tid == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
         return;
     }
@@ -1595,18 +1434,18 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const ui
         const uint32_t xq = in ? buf[q] : 0;
         const bool nw = in && (q == 0 || (buf[q - 1] >> 6) != (xq >> 6));
         nd += (uint32_t)__popcll(__ballot(nw));
-        if (in) atomicAdd(&wk_cnt[wave][xq & 63u], 1u);
+        if (in) atomicAdd(&L.wk_cnt[wave][xq & 63u], 1u);
     }
-    if (lane == 0) wdist[wave] = nd;
+    if (lane == 0) L.wdist[wave] = nd;
     __syncthreads();
     if (tid < BIG_K) {   // exclusive prefix over waves, per key
         uint32_t run = 0;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) { uint32_t x = wk_cnt[w][tid]; wk_cnt[w][tid] = run; run += x; }
+        for (int w = 0; w < NW; ++w) { uint32_t x = L.wk_cnt[w][tid]; L.wk_cnt[w][tid] = run; run += x; }
     }
     __syncthreads();
     uint32_t distinct = 0;
-    for (int w = 0; w < (int)wave; ++w) distinct += wdist[w];
+    for (int w = 0; w < (int)wave; ++w) distinct += L.wdist[w];
     const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
     auto widen = [](uint32_t r) { return ((uint64_t)(r >> 6) << 16) | (r & 63u); };
     for (uint32_t q0 = q_lo; q0 < q_hi; q0 += 64) {
@@ -1614,9 +1453,23 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(uint32_t cnt_list, const ui
         const bool in = q < q_hi;
         const uint64_t xq = in ? widen(buf[q]) : 0;
         const uint64_t prev = (in && q > 0) ? widen(buf[q - 1]) : 0;
-        distinct = emit_chunk(xq, in, prev, q > 0, distinct, wk_cnt[wave], o, c, abase);
+        distinct = emit_chunk(xq, in, prev, q > 0, distinct, L.wk_cnt[wave], o, c, abase);
     }
     if (wave == NW - 1 && lane == 0) o.u_cnt[t] = distinct;
+}
+
+// Persistent over the routed list: blocks loop (a grid of one block per listed txn made the 128-KiB launch pay a
+// block launch + exit per big txn). CAP = BIG_E reads its count from gstat[1], CAP = HUGE_E from gstat[6].
+template <int CAP, int NT>
+__global__ __launch_bounds__(NT) void k_v2_write_big(const uint32_t *__restrict__ list, V2View v,
+                                                     const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ BigLds<CAP, NT> L;
+    const uint32_t cnt_list = (uint32_t)o.gstat[CAP > BIG_E ? 6 : 1];
+    for (uint32_t b = blockIdx.x; b < cnt_list; b += gridDim.x) {
+        big_one<CAP, NT>(L, list[b], v, cnt, o);
+        __syncthreads();
+    }
 }
 
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
@@ -1740,24 +1593,568 @@ __global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t
 }
 
 
-__global__ __launch_bounds__(BLOCK) void k_u32_from_u64(size_t n, const uint64_t *__restrict__ in, uint32_t *__restrict__ out)
+
+// ---------------------------------------------------------------- v3: streaming write pass
+//
+// A txn with at most ST_K keys, at most ST_N2 dependency entries and at most ST_RAW raw run elements (config 2: ~99%
+// of txns) is finished by one kernel, k_v3_stream: a tile of ST_T txns per block, ST_G lanes per txn, takes the
+// inline entries of its count-pass records and gathers the entries of its run records, sorts the (rank, key) entries
+// in LDS, counts the distinct TxnIds, takes the tile's output offsets (arena, keys, TxnIds) from a decoupled look-back
+// over the previous tiles' sizes and writes the final KeyDeps arrays (arena_off / kd_off / u_off, arena, key_idx,
+// dep_txn) directly: one read of 64 B of record per pair, writes of the outputs only.
+// The other ("big") txns take the v2 tiers into scratch arrays addressed by prefix sums over the big txns in txn
+// order (k_v3_bigfill gives them per-pair offsets, so the tiers' indexing is unchanged), report their sizes to the
+// stream pass, and k_v3_bigcopy moves them into place.
+
+constexpr int ST_G = 16;                      // lanes per txn
+constexpr int ST_K = 16;                      // keys of a stream txn
+constexpr int ST_N2 = 128;                    // dependency entries of a stream txn (LDS sort buffer, power of two)
+constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream txn
+
+// Big-txn classification, ST_G lanes per txn: more than ST_K keys, or (txns with a run record only: bigflag = 1 from
+// the count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
+__global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *__restrict__ key_off,
+                                                   const uint32_t *__restrict__ rec32, uint32_t raw_cap, uint32_t e_cap,
+                                                   uint32_t *__restrict__ bigflag)
 {
-    size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i < n) out[i] = (uint32_t)in[i];
+    const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / ST_G, sub = threadIdx.x & (ST_G - 1);
+    if (t >= n) return;
+    const uint32_t j0 = key_off[t], nk = key_off[t + 1] - j0;
+    bool big = nk > (uint32_t)ST_K;
+    if (!big && bigflag[t]) {   // group-uniform branch: shuffles stay inside the group
+        uint32_t e = 0, raw = 0;
+        if (sub < nk) {
+            const uint32_t *r = rec32 + 16 * (size_t)(j0 + sub);
+            const uint32_t w = r[15];
+            if (w & REC_INLINE_FLAG) { e = w & ~REC_INLINE_FLAG; raw = 0; }
+            else { e = w; raw = r[6] + r[7] + r[8] + r[9] + r[10] + r[11] + r[13]; }
+        }
+#pragma unroll
+        for (int d = 1; d < ST_G; d <<= 1) { e += __shfl_xor(e, d, 64); raw += __shfl_xor(raw, d, 64); }
+        big = e > e_cap || raw > raw_cap;
+    }
+    if (sub == 0) bigflag[t] = big ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_compact(uint32_t n, const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ dep_off,
-                                                      const uint64_t *__restrict__ u_off, const uint32_t *__restrict__ dep_scratch,
-                                                      uint32_t *__restrict__ dep_txn)
+__global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t *__restrict__ bigflag,
+                                                      const uint32_t *__restrict__ bpos, uint32_t *__restrict__ blist)
 {
-    // 16 lanes per txn (a txn has ~33 TxnIds on config 2: a whole wave per txn left most lanes idle)
-    constexpr uint32_t G = 16;
-    const uint32_t g = threadIdx.x & (G - 1);
-    const uint32_t t = blockIdx.x * (BLOCK / G) + threadIdx.x / G;
-    if (t >= n) return;
-    uint64_t src = dep_off[key_off[t]];
-    uint64_t dst = u_off[t], len = u_off[t + 1] - dst;
-    for (uint64_t i = g; i < len; i += G) dep_txn[dst + i] = dep_scratch[src + i];
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n && bigflag[t]) blist[bpos[t]] = t;
+}
+
+// per big txn (one wave each, list order): dependency entries E and non-empty keys Kd from the records' word 15
+__global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_t *__restrict__ blist,
+                                                    const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ rec32,
+                                                    uint64_t *__restrict__ lE, uint64_t *__restrict__ lK, uint64_t *__restrict__ lA)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= nbig) return;
+    const uint32_t t = blist[i], j0 = key_off[t], j1 = key_off[t + 1];
+    uint64_t E = 0, K = 0;
+    for (uint32_t j = j0 + lane; j < j1; j += 64) {
+        const uint32_t e = rec32[16 * (size_t)j + 15] & ~REC_INLINE_FLAG;
+        E += e;
+        K += e != 0;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { E += shfl_xor(E, d); K += shfl_xor(K, d); }
+    if (lane == 0) { lE[i] = E; lK[i] = K; lA[i] = E + K; }
+}
+
+// tier routing of the big txns (thread per list entry, one atomic per list per block): medium (E <= MED_E, <= MED_K
+// keys), the u32-record block tier (when ranks fit 25 bits) or the global path
+__global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_t *__restrict__ blist,
+                                                    const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ lE,
+                                                    int big_ok, uint32_t *__restrict__ med_list, uint32_t *__restrict__ big_list,
+                                                    uint32_t *__restrict__ fb_list, uint64_t *__restrict__ gstat)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    bool med = false, bg = false, fb = false;
+    uint32_t t = 0;
+    uint64_t E = 0;
+    if (i < nbig) {
+        t = blist[i];
+        E = lE[i];
+        const uint32_t nk = key_off[t + 1] - key_off[t];
+        med = E > 0 && E <= (uint64_t)MED_E && nk <= (uint32_t)MED_K;
+        bg = E > 0 && !med && big_ok;
+        fb = E > 0 && !med && !big_ok;
+    }
+    __shared__ uint64_t lds[WAVES];
+    __shared__ uint64_t base[3];
+    const uint64_t packed = (med ? 1ull : 0ull) | (bg ? 1ull << 12 : 0ull) | (fb ? 1ull << 24 : 0ull);
+    uint64_t total;
+    const uint64_t pre = block_exclusive(packed, OpAdd<uint64_t>(), lds, total);
+    uint64_t efb = fb ? E : 0;
+    uint64_t efb_tot;
+    __syncthreads();
+    block_exclusive(efb, OpAdd<uint64_t>(), lds, efb_tot);
+    if (threadIdx.x < 3) {
+        const int slot[3] = { 0, 1, 3 };
+        const uint64_t cnt = (total >> (12 * threadIdx.x)) & 4095u;
+        base[threadIdx.x] = cnt ? atomicAdd((unsigned long long *)&gstat[slot[threadIdx.x]], (unsigned long long)cnt) : 0ull;
+    }
+    if (threadIdx.x == 0 && efb_tot) atomicAdd((unsigned long long *)&gstat[4], (unsigned long long)efb_tot);
+    __syncthreads();
+    if (med) med_list[base[0] + (pre & 4095u)] = t;
+    if (bg) big_list[base[1] + ((pre >> 12) & 4095u)] = t;
+    if (fb) fb_list[base[2] + ((pre >> 24) & 4095u)] = t;
+}
+
+struct V3Big {
+    const uint32_t *blist, *key_off, *rec32;
+    const uint64_t *dB, *kB, *aB;             // exclusive prefixes over the list: scratch bases
+    uint64_t *vdep_off, *vcnt;                // per pair of a big txn (dep_off / cnt of the v2 tiers)
+    uint32_t *vcnz;                           // per pair of a big txn (cnz)
+    uint64_t *varena, *bK, *bE, *u_cnt;       // per txn (big txns only)
+    int32_t *arena_scr;
+    uint32_t *key_scr;
+};
+
+// per big txn (one wave): the v2 tiers' per-pair offsets, the KeyDeps headers and key indices into scratch, and the
+// sizes the stream pass reads
+__global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= nbig) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t t = b.blist[i], j0 = b.key_off[t], j1 = b.key_off[t + 1], nk = j1 - j0;
+    const uint64_t dbase = b.dB[i], kbase = b.kB[i], abase = b.aB[i];
+    const uint64_t E = b.dB[i + 1] - dbase, Kd = b.kB[i + 1] - kbase;
+    uint64_t ecur = 0, kcur = 0;
+    for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
+        const uint32_t j = j0 + c0 + lane;
+        const bool in = c0 + lane < nk;
+        const uint32_t e = in ? (b.rec32[16 * (size_t)j + 15] & ~REC_INLINE_FLAG) : 0u;
+        const uint64_t einc = wave_inclusive((uint64_t)e, OpAdd<uint64_t>());
+        const uint64_t nzb = __ballot(e != 0);
+        const uint32_t kb = (uint32_t)__popcll(nzb & lt);
+        if (in) {
+            const uint64_t eoff = ecur + einc - e;
+            b.vdep_off[j] = dbase + eoff;
+            b.vcnt[j] = e;
+            b.vcnz[j] = (uint32_t)(kbase + kcur + kb);
+            if (e) {
+                b.arena_scr[abase + kcur + kb] = (int32_t)(Kd + eoff + e);
+                b.key_scr[kbase + kcur + kb] = c0 + lane;
+            }
+        }
+        ecur += shfl_idx(einc, 63);
+        kcur += (uint64_t)__popcll(nzb);
+    }
+    if (lane == 0) {
+        b.vdep_off[j1] = dbase + E;
+        b.vcnz[j1] = (uint32_t)(kbase + Kd);
+        b.varena[t] = abase;
+        b.bK[t] = Kd;
+        b.bE[t] = E;
+        b.u_cnt[t] = 0;
+    }
+}
+
+struct V3Stream {
+    V2View v;
+    const uint32_t *key_off, *bigflag, *txn_of_rank;
+    const uint4 *rec;
+    const uint64_t *bK, *bE;                  // sizes of the big txns
+    uint64_t *arena_off, *kd_off, *u_cnt_out;
+    int32_t *arena;
+    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's entry offset, compacted by k_v3_ucompact
+    uint64_t *status;                         // 2 x ntiles look-back words: arena, keys
+    uint32_t *ticket;
+    uint64_t *err;                            // gather count mismatches
+    uint32_t n, ntiles;
+};
+
+// exclusive prefixes of tile b for NC chains (status words [q * ntiles + tile]) from the look-back over the tiles < b:
+// one full wave, LB_U words per lane and chain in flight (a window of 64 * LB_U tiles per round: the inclusive frontier
+// advances by up to a window per round trip, so small tiles need a wide window); each chain stops at its own nearest
+// inclusive word.
+constexpr int LB_U = 4;
+
+template <int NC>
+__device__ __forceinline__ void lookback_n(const uint64_t *status, uint32_t ntiles, uint32_t b, uint64_t (&pre)[NC])
+{
+    const uint32_t lane = lane_id();
+    bool done[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) { pre[q] = 0; done[q] = false; }
+    int64_t j = (int64_t)b - 1;
+    while (true) {
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) all = all && done[q];
+        if (all) break;
+        uint64_t w[NC][LB_U];
+#pragma unroll
+        for (int q = 0; q < NC; ++q)
+#pragma unroll
+            for (int u = 0; u < LB_U; ++u) {
+                const int64_t idx = j - (int64_t)lane - 64 * u;
+                w[q][u] = (done[q] || idx < 0) ? SCAN_INC : scan_status_load(&status[(size_t)q * ntiles + idx]);
+            }
+        while (true) {
+            bool wait = false;
+#pragma unroll
+            for (int q = 0; q < NC; ++q)
+#pragma unroll
+                for (int u = 0; u < LB_U; ++u) wait = wait || (w[q][u] >> 62) == 0;
+            if (!wait) break;
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int q = 0; q < NC; ++q)
+#pragma unroll
+                for (int u = 0; u < LB_U; ++u)
+                    if ((w[q][u] >> 62) == 0) w[q][u] = scan_status_load(&status[(size_t)q * ntiles + (j - (int64_t)lane - 64 * u)]);
+        }
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+            if (done[q]) continue;
+            uint64_t x = 0;
+#pragma unroll
+            for (int u = 0; u < LB_U; ++u) {
+                if (done[q]) break;
+                const uint64_t inc = __ballot((w[q][u] >> 62) == 2);
+                const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;
+                x += lane <= stop ? (w[q][u] & SCAN_VAL) : 0ull;
+                if (inc) done[q] = true;
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) x += shfl_xor(x, d);
+            pre[q] += x;
+        }
+        j -= 64 * LB_U;
+    }
+}
+
+// inclusive prefix over the ST_G lanes of a group
+__device__ __forceinline__ uint32_t group_inclusive(uint32_t x, uint32_t sub)
+{
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)ST_G; d <<= 1) {
+        const uint32_t u = __shfl_up(x, d, 64);
+        if (sub >= d) x += u;
+    }
+    return x;
+}
+
+#ifdef ACC_PHASE_PROF
+// tuning build only (tools/build_prof.sh): per-phase wave cycles of k_v3_stream, one row of 8 per wave (no atomics)
+__device__ unsigned long long *g_st_prof;
+#define ST_PH(i) ph[i] = clock64()
+#else
+#define ST_PH(i) ((void)0)
+#endif
+
+// EntT: u32 (rank << 4 | key) when ranks fit 28 bits, else u64
+template <class EntT, int NT>
+__global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
+{
+    constexpr int TT = NT / ST_G;   // txns per tile
+#ifdef ACC_PHASE_PROF
+    uint64_t ph[8];
+#endif
+    ST_PH(0);
+    __shared__ EntT ent[TT][ST_N2];
+    __shared__ uint32_t kc[TT][ST_K];
+    __shared__ uint32_t kbase[TT][ST_K];
+    __shared__ uint64_t tsz[2][TT];
+    __shared__ uint16_t stA[TT][ST_K + ST_N2];
+    __shared__ uint32_t s_tile;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (ST_G - 1), grp = tid / ST_G, g0 = lane & (64 - ST_G);
+    const uint64_t gmask = ((1ull << ST_G) - 1) << g0;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    if (tid == 0) s_tile = atomicAdd(s.ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t t = tile * TT + grp;
+    const bool valid = t < s.n;
+    TxnCtx c{};
+    bool big = false;
+    if (valid) {
+        c.t = t;
+        c.j0 = s.key_off[t]; c.j1 = s.key_off[t + 1]; c.nk = c.j1 - c.j0;
+        big = s.bigflag[t] != 0;
+        if (!big) {
+            const uint4 ti = s.v.tinfo[t];
+            c.trank = ti.x;
+            c.bq = ti.y != c.trank;
+            c.wk = witnesses(ti.z >> 3);
+        }
+    }
+    const bool sm = valid && !big;
+    EntT *buf = ent[grp];
+    ST_PH(1);
+    // ---- records: inline entries straight to LDS; a run record's runs stay in its lane's registers
+    uint32_t e = 0, rawk = 0;
+    bool run = false;
+    uint4 r0 = {}, r1 = {}, r2 = {}, r3 = {};
+    if (sm && sub < c.nk) {
+        const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
+        r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
+        if (r3.w & REC_INLINE_FLAG) {
+            e = r3.w & ~REC_INLINE_FLAG;
+        } else {
+            run = true;
+            e = r3.w;
+            rawk = r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
+        }
+    }
+    const uint32_t ein = run ? 0u : e;
+    const uint32_t e_incl = group_inclusive(e, sub), in_incl = group_inclusive(ein, sub);
+    const uint32_t E = __shfl(e_incl, (int)(g0 + ST_G - 1), 64);
+    const uint32_t E_in = __shfl(in_incl, (int)(g0 + ST_G - 1), 64);
+    const uint64_t nzb = __ballot(e != 0) & gmask;
+    const uint32_t Kd = (uint32_t)__popcll(nzb);
+    // ---- sizes (known from the count pass: A = Kd + E, K = Kd), tile aggregate published before the gather and sort
+    uint64_t A = 0, K = 0;
+    if (sm) { A = (uint64_t)Kd + E; K = Kd; }
+    else if (valid) { K = s.bK[t]; A = K + s.bE[t]; }
+    if (sub == 0) { tsz[0][grp] = A; tsz[1][grp] = K; }
+    __syncthreads();
+    uint64_t tv[2] = { 0, 0 }, ttot[2] = { 0, 0 };
+    if (tid < 64) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint64_t x = lane < (uint32_t)TT ? tsz[q][lane] : 0ull;
+            const uint64_t inc = wave_inclusive(x, OpAdd<uint64_t>());
+            tv[q] = inc - x;
+            ttot[q] = shfl_idx(inc, 63);
+        }
+        const uint64_t mine = lane == 0 ? ttot[0] : ttot[1];
+        if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], mine | (tile == 0 ? SCAN_INC : SCAN_AGG));
+    }
+    kbase[grp][sub] = e_incl - e;
+    kc[grp][sub] = 0;
+    if (sm && !run) {
+        const uint32_t w[15] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z };
+        const uint32_t b0 = in_incl - ein;
+#pragma unroll
+        for (uint32_t q = 0; q < REC_INLINE; ++q)
+            if (q < e) buf[b0 + q] = ((EntT)w[q] << 4) | (EntT)sub;
+    }
+    ST_PH(2);
+    // ---- run records, one key at a time (its runs broadcast from the owning lane): the group gathers the flattened
+    // runs R1/R2 per class and R3, dropping T itself and R3 entries below M or of unwitnessed kinds, after the inline
+    // entries
+    const uint64_t runmask = __ballot(sm && run) & gmask;
+    const uint32_t nrun = (uint32_t)__popcll(runmask);
+    uint32_t wnrun = nrun;
+#pragma unroll
+    for (int d = ST_G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
+    uint32_t cursor = E_in;
+    uint64_t rem = runmask;
+    for (uint32_t ri = 0; ri < wnrun; ++ri) {
+        const bool has = rem != 0;
+        const int src = has ? (int)__builtin_ctzll(rem) : (int)lane;
+        rem &= rem - 1;
+        uint32_t st[NRUN], len[NRUN];
+        st[0] = __shfl(r0.x, src, 64); st[1] = __shfl(r0.y, src, 64); st[2] = __shfl(r0.z, src, 64);
+        st[3] = __shfl(r0.w, src, 64); st[4] = __shfl(r1.x, src, 64); st[5] = __shfl(r1.y, src, 64);
+        st[6] = __shfl(r3.x, src, 64);
+        len[0] = __shfl(r1.z, src, 64); len[1] = __shfl(r1.w, src, 64); len[2] = __shfl(r2.x, src, 64);
+        len[3] = __shfl(r2.y, src, 64); len[4] = __shfl(r2.z, src, 64); len[5] = __shfl(r2.w, src, 64);
+        len[6] = __shfl(r3.y, src, 64);
+        const uint32_t mk = __shfl(r3.z, src, 64);
+        const uint32_t raw = has ? __shfl(rawk, src, 64) : 0u;
+        const uint32_t kj = (uint32_t)(src - (int)g0);
+        uint32_t wr = raw;
+#pragma unroll
+        for (int d = ST_G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
+        for (uint32_t c0 = 0; c0 < wr; c0 += ST_G) {
+            const uint32_t off = c0 + sub;
+            bool keep = false;
+            uint32_t x = 0;
+            if (off < raw) {
+                uint32_t idx = 0, acc = 0;
+                bool r3run = false, found = false;
+#pragma unroll
+                for (int q = 0; q < NRUN; ++q) {
+                    if (!found && off < acc + len[q]) { found = true; idx = st[q] + (off - acc); r3run = q == 6; }
+                    acc += len[q];
+                }
+                if (r3run) {
+                    x = s.v.bc_rank[idx];
+                    keep = s.v.bc_exec[idx] >= mk && ((c.wk >> s.v.bc_kind[idx]) & 1u);
+                } else {
+                    x = s.v.list_rank[idx];
+                    keep = true;
+                }
+                keep = keep && !(c.bq && x == c.trank);
+            }
+            const uint64_t bal = __ballot(keep) & gmask;
+            if (keep) {
+                const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
+                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x << 4) | (EntT)kj;
+            }
+            cursor += (uint32_t)__popcll(bal);
+        }
+    }
+    ST_PH(3);
+    bool ok = sm;
+    if (sm && cursor != E) {
+        if (sub == 0) atomicAdd((unsigned long long *)s.err, 1ull);
+        ok = false;
+    }
+    uint32_t n2 = 16;
+    while (n2 < E) n2 <<= 1;
+    if (!ok) n2 = 0;
+    for (uint32_t q = E + sub; q < n2; q += ST_G) buf[q] = ~(EntT)0;
+    uint32_t wn2 = n2, wE = ok ? E : 0;
+#pragma unroll
+    for (int d = ST_G; d < 64; d <<= 1) {
+        wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
+        wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // ---- bitonic sort of each group's n2 entries (loop bounds uniform over the wave)
+    for (uint32_t k = 2; k <= wn2; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            if (k <= n2) {
+                for (uint32_t pi = sub; pi < (n2 >> 1); pi += ST_G) {
+                    const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
+                    const uint32_t l = i | jj;
+                    const EntT xa = buf[i], ya = buf[l];
+                    const bool up = (i & k) == 0;
+                    if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
+    ST_PH(4);
+    // ---- KeyDeps in LDS, before the look-back (its wait hides the TxnId gathers): the arena (header ints and per-key
+    // TxnId indices) staged as u16; the distinct TxnIds go straight to the txn's fixed scratch slot t * ST_N2
+    uint32_t distinct = 0;
+    if (ok && e != 0) stA[grp][(uint32_t)__popcll(nzb & lt)] = (uint16_t)(Kd + e_incl);
+    for (uint32_t q0 = 0; q0 < wE; q0 += ST_G) {
+        const uint32_t q = q0 + sub;
+        const bool in = ok && q < E;
+        const EntT x = in ? buf[q] : (EntT)0;
+        const EntT pv = (in && q > 0) ? buf[q - 1] : (EntT)0;
+        const uint32_t kj = (uint32_t)(x & 15u);
+        const bool nw = in && (q == 0 || (x >> 4) != (pv >> 4));
+        const uint64_t bal = __ballot(nw) & gmask;
+        const uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+        uint64_t peers = __ballot(in) & gmask;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const uint64_t m = __ballot((kj >> bb) & 1u);
+            peers &= ((kj >> bb) & 1u) ? m : ~m;
+        }
+        const uint32_t before = (uint32_t)__popcll(peers & lt);
+        if (in) {
+            stA[grp][Kd + kbase[grp][kj] + kc[grp][kj] + before] = (uint16_t)idx;
+            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = s.txn_of_rank[(uint32_t)(x >> 4)];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (in && before == 0) kc[grp][kj] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        distinct += (uint32_t)__popcll(bal);
+    }
+    if (ok && sub == 0) s.u_cnt_out[t] = distinct;
+    ST_PH(5);
+    // ---- tile offsets: look-back (by now the previous tiles have mostly published inclusive prefixes)
+    __syncthreads();
+    if (tid < 64) {
+        uint64_t pre[2] = { 0, 0 };
+        if (tile != 0) {
+            lookback_n<2>(s.status, s.ntiles, tile, pre);
+            const uint64_t mine = lane == 0 ? ttot[0] : ttot[1];
+            const uint64_t pm = lane == 0 ? pre[0] : pre[1];
+            if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (pm + mine) | SCAN_INC);
+        }
+        if (lane < (uint32_t)TT) { tsz[0][lane] = pre[0] + tv[0]; tsz[1][lane] = pre[1] + tv[1]; }
+    }
+    __syncthreads();
+    if (!valid) return;
+    const uint64_t aoff = tsz[0][grp], koff = tsz[1][grp];
+    if (sub == 0) {
+        s.arena_off[t] = aoff; s.kd_off[t] = koff;
+        if (t + 1 == s.n) { s.arena_off[t + 1] = aoff + A; s.kd_off[t + 1] = koff + K; }
+    }
+    if (ok) {
+        for (uint32_t q = sub; q < (uint32_t)A; q += ST_G) s.arena[aoff + q] = (int32_t)stA[grp][q];
+        if (e != 0) s.key_idx[koff + (uint32_t)__popcll(nzb & lt)] = sub;
+    }
+#ifdef ACC_PHASE_PROF
+    ST_PH(6);
+    if (lane == 0) {
+        unsigned long long *row = g_st_prof + 8 * ((size_t)tile * (NT / 64) + (tid >> 6));
+        for (int i = 0; i < 6; ++i) row[i] = ph[i + 1] - ph[i];
+        row[7] = 1;
+    }
+#endif
+}
+
+// big txns' arena and key scratch -> final arrays (one wave per big txn; their TxnIds go through k_v3_ucompact)
+__global__ __launch_bounds__(BLOCK) void k_v3_bigcopy(uint32_t nbig, const uint32_t *__restrict__ blist,
+                                                      const uint64_t *__restrict__ varena, const uint64_t *__restrict__ kB,
+                                                      const uint64_t *__restrict__ arena_off, const uint64_t *__restrict__ kd_off,
+                                                      const int32_t *__restrict__ arena_scr, const uint32_t *__restrict__ key_scr,
+                                                      int32_t *__restrict__ arena, uint32_t *__restrict__ key_idx)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= nbig) return;
+    const uint32_t t = blist[i];
+    const uint64_t A = arena_off[t + 1] - arena_off[t], K = kd_off[t + 1] - kd_off[t];
+    const uint64_t as = varena[t], ad = arena_off[t], ks = kB[i], kd = kd_off[t];
+    for (uint64_t q = lane; q < A; q += 64) arena[ad + q] = arena_scr[as + q];
+    for (uint64_t q = lane; q < K; q += 64) key_idx[kd + q] = key_scr[ks + q];
+}
+
+// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: at its entry offset arena_off - kd_off in
+// dep_scr; big txns: at vdep_off of its first pair in dep_big) to dep_txn[u_off[t] ...). A block takes a fixed chunk
+// of UC_CHUNK outputs (the uncommitted window's txns are consecutive and hold most TxnIds: partitioning by txns left a
+// few blocks with most of the work), finds the txns spanning it by binary search over u_off, and strides over the
+// chunk in windows of BLOCK txns (u_off / source bases in LDS, each output's txn by binary search there).
+constexpr uint32_t UC_CHUNK = 4096;
+
+__device__ __forceinline__ uint32_t last_le(const uint64_t *a, uint32_t n, uint64_t x)   // largest i < n with a[i] <= x
+{
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (a[m] <= x) lo = m; else hi = m; }
+    return lo;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_t *__restrict__ u_off,
+                                                       const uint64_t *__restrict__ arena_off, const uint64_t *__restrict__ kd_off,
+                                                       const uint32_t *__restrict__ bigflag, const uint32_t *__restrict__ key_off,
+                                                       const uint64_t *__restrict__ vdep_off, const uint32_t *__restrict__ dep_scr,
+                                                       const uint32_t *__restrict__ dep_big, uint32_t *__restrict__ dep_txn)
+{
+    __shared__ uint64_t uo[BLOCK + 1];
+    __shared__ uint64_t src[BLOCK];
+    __shared__ uint32_t s_t[2];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t total = u_off[n];
+    const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
+    if (c0 >= total) return;
+    const uint64_t c1 = min(total, c0 + UC_CHUNK);
+    if (tid == 0) { s_t[0] = last_le(u_off, n, c0); s_t[1] = last_le(u_off, n, c1 - 1); }
+    __syncthreads();
+    const uint32_t tlo = s_t[0], thi = s_t[1];
+    for (uint32_t tw = tlo; tw <= thi; tw += BLOCK) {
+        const uint32_t nt = min((uint32_t)BLOCK, thi + 1 - tw);
+        __syncthreads();
+        if (tid < nt) {
+            const uint32_t t = tw + tid;
+            uo[tid] = u_off[t];
+            src[tid] = bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_N2;
+        }
+        if (tid == 0) uo[nt] = u_off[tw + nt];
+        __syncthreads();
+        const uint64_t lo = max(c0, uo[0]), hi = min(c1, uo[nt]);
+        for (uint64_t i = lo + tid; i < hi; i += BLOCK) {
+            const uint32_t a = last_le(uo, nt, i);
+            const uint64_t sb = src[a], off = i - uo[a];
+            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
+        }
+    }
 }
 
 // ---------------------------------------------------------------- host orchestration
@@ -2185,141 +2582,206 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm;
     vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw;
 
-    // ---- count, offsets
-    uint64_t *cnt = ctx->get<uint64_t>("cnt", P);
-    uint64_t *dep_off = ctx->get<uint64_t>("dep_off", P + 1);
+    // ---- count pass: per-pair records, big-txn flags, E
+    if (P >= 0x80000000ull) fail(ACC_E_CAP, "n_pairs must be < 2^31 (count-pass record format)");
     uint4 *rec = ctx->get<uint4>("v2_rec", 4 * P);
     vv.rec32 = reinterpret_cast<const uint32_t *>(rec);
-    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, cnt, rec);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, cnt, dep_off, P, true, dep_off + P);
-    uint32_t *nz = ctx->get<uint32_t>("nz", P);
-    uint32_t *cnz = ctx->get<uint32_t>("cnz", P + 1);
-    launch(ctx, "nonempty", k_nonempty, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, nz);
-    scan<uint32_t, OpAdd<uint32_t>>(ctx, nz, cnz, P, true, cnz + P);
-    uint64_t *kd_cnt = ctx->get<uint64_t>("kd_cnt", n);
-    uint64_t *a_cnt = ctx->get<uint64_t>("a_cnt", n);
-    uint32_t *med_list = ctx->get<uint32_t>("v2_med_list", n);
-    uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", n);
-    uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", n);
-    uint32_t *small_list = ctx->get<uint32_t>("v2_small_list", n);
-    uint32_t *g32_list = ctx->get<uint32_t>("v2_g32_list", n);
+    uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
+    uint32_t *bpos = ctx->get<uint32_t>("v3_bpos", n);
+    uint64_t *blk_e = ctx->get<uint64_t>("v3_blk_e", gP);
+    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 2);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 8);
+    ACC_HIP(hipMemsetAsync(bigflag, 0, (size_t)n * 4, st));
+    ACC_HIP(hipMemsetAsync(tot, 0, 2 * sizeof(uint64_t), st));
     ACC_HIP(hipMemsetAsync(gstat, 0, 8 * sizeof(uint64_t), st));
-    launch(ctx, "v2_sizes", k_v2_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint64_t *)dep_off,
-           (const uint32_t *)cnz, kd_cnt, a_cnt, med_list, big_list, small_list, g32_list, gstat);
-    uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
-    uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, kd_off, n, true, kd_off + n);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, arena_off, n, true, arena_off + n);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, dep_off + P, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gstat, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, gstat + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, gstat + 7, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, rec, bigflag, blk_e);
+    const char *rc_env = getenv("ACC_ST_RAW");
+    const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
+    const char *ec_env = getenv("ACC_ST_ECAP");
+    const uint32_t e_cap = ec_env ? std::min<uint32_t>((uint32_t)atoi(ec_env), ST_N2) : ST_N2;
+    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, raw_cap, e_cap, bigflag);
+    uint32_t *nbig_dev = reinterpret_cast<uint32_t *>(tot + 1);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, bigflag, bpos, n, true, nbig_dev);
+    uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, blk_e, blk_pre, gP, true, tot);
+    uint32_t *blist = ctx->get<uint32_t>("v3_blist", n);
+    launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bigflag,
+           (const uint32_t *)bpos, blist);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
-    const uint64_t nmed = ctx->pinned[1], nbig = ctx->pinned[2], nsmall = ctx->pinned[3], ng32 = ctx->pinned[4];
+    const uint32_t nbig = (uint32_t)ctx->pinned[1];
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
 
-    // ---- write pass (three tiers)
     int32_t *arena = ctx->get<int32_t>("arena", P + E);
     uint32_t *key_idx = ctx->get<uint32_t>("key_idx", P);
-    uint32_t *dep_scratch = ctx->get<uint32_t>("v2_dep_scratch", E);
-    uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
-    V2Out wo;
-    wo.key_off = key_off; wo.dep_off = dep_off; wo.arena_off = arena_off; wo.cnz = cnz; wo.txn_of_rank = txn_of_rank;
-    wo.arena = arena; wo.dep_scratch = dep_scratch; wo.u_cnt = u_cnt; wo.gstat = gstat;
-    wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
-    wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig + 1);
-    // Tiers run back to back on the context stream. Side streams (acc_ctx::fork/join) were measured at -2% step time
-    // on config 2 but stretch every tier's own duration, which hides the per-kernel roofline attribution.
-    launch(ctx, "v2_write_g16", k_v2_write_group<16, false>, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n,
-           (const uint32_t *)nullptr, vv, (const uint64_t *)cnt, wo);
-    if (ng32)
-        launch(ctx, "v2_write_g32", k_v2_write_group<32, true>, dim3((unsigned)((ng32 + BLOCK / 32 - 1) / (BLOCK / 32))),
-               dim3(BLOCK), 0, (uint32_t)ng32, (const uint32_t *)g32_list, vv, (const uint64_t *)cnt, wo);
-    if (nsmall)
-        launch(ctx, "v2_write_small", k_v2_write_small, dim3((unsigned)((nsmall + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
-               (uint32_t)nsmall, (const uint32_t *)small_list, vv, (const uint64_t *)cnt, wo);
-    if (nmed)
-        launch(ctx, "v2_write_medium", k_v2_write_medium, dim3((unsigned)((nmed + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
-               (uint32_t)nmed, (const uint32_t *)med_list, vv, (const uint64_t *)cnt, wo);
-    if (nbig && rbits + 6 <= 31) {
-        launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3((unsigned)nbig), dim3(BLOCK), 0, (uint32_t)nbig,
-               (const uint32_t *)big_list, vv, (const uint64_t *)cnt, wo);
-        launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3((unsigned)nbig), dim3(1024), 0, (uint32_t)nbig,
-               (const uint32_t *)wo.huge_list, vv, (const uint64_t *)cnt, wo);
-    }
-    if (nbig && !(rbits + 6 <= 31)) {
-        // ranks beyond 25 bits: every big txn takes the global path
-        launch(ctx, "v2_route_fb", k_v2_route_fb, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, (uint32_t)nbig,
-               (const uint32_t *)big_list, key_off, (const uint64_t *)dep_off, fb_list, gstat);
-    }
-    launch(ctx, "write_keys", k_write_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)cnt, (const uint32_t *)owner,
-           key_off, (const uint64_t *)dep_off, (const uint32_t *)cnz, (const uint64_t *)kd_off,
-           (const uint64_t *)arena_off, key_idx, arena);
-    // TxnId-union offsets, compaction and totals are enqueued before the tier statistics are read, so the common
-    // case (no txn for the global tier) costs one host sync here; with global-tier txns they are redone after it.
-    uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
-    auto finish = [&]() {
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
-        launch(ctx, "v2_compact", k_v2_compact, dim3((n + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, n, key_off,
-               (const uint64_t *)dep_off, (const uint64_t *)u_off, (const uint32_t *)dep_scratch, dep_txn);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
+    uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
+    uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
+    uint64_t *bK = ctx->get<uint64_t>("v3_bK", n);
+    uint64_t *bE = ctx->get<uint64_t>("v3_bE", n);
+    uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
+    uint64_t *lB = nullptr, *varena = nullptr, *vdep_off = nullptr;
+    int32_t *arena_scr = nullptr;
+    uint32_t *key_scr = nullptr, *dep_scr = nullptr;
+    uint64_t nfb = 0, efb = 0, nmed = 0, nbig2 = 0;
+    ctx->stat("keydeps.huge_txns", 0);
+    // ---- big txns: v2 tiers into scratch
+    if (nbig) {
+        const unsigned gB = (nbig + WAVES - 1) / WAVES;
+        uint64_t *lE = ctx->get<uint64_t>("v3_lE", nbig), *lK = ctx->get<uint64_t>("v3_lK", nbig), *lA = ctx->get<uint64_t>("v3_lA", nbig);
+        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, vv.rec32, lE, lK, lA);
+        uint64_t *dB = ctx->get<uint64_t>("v3_dB", (size_t)nbig + 1), *kB = ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1);
+        lB = ctx->get<uint64_t>("v3_aB", (size_t)nbig + 1);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, lE, dB, nbig, true, dB + nbig);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, lK, kB, nbig, true, kB + nbig);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, lA, lB, nbig, true, lB + nbig);
+        vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
+        uint64_t *vcnt = ctx->get<uint64_t>("cnt", P);
+        uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
+        varena = ctx->get<uint64_t>("v3_varena", n);
+        arena_scr = ctx->get<int32_t>("v3_arena_scr", P + E);
+        key_scr = ctx->get<uint32_t>("v3_key_scr", P);
+        dep_scr = ctx->get<uint32_t>("v2_dep_scratch", E);
+        uint32_t *med_list = ctx->get<uint32_t>("v2_med_list", nbig);
+        uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", nbig);
+        uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
+        V3Big bg;
+        bg.blist = blist; bg.key_off = key_off; bg.rec32 = vv.rec32; bg.dB = dB; bg.kB = kB; bg.aB = lB;
+        bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.varena = varena; bg.bK = bK; bg.bE = bE; bg.u_cnt = u_cnt;
+        bg.arena_scr = arena_scr; bg.key_scr = key_scr;
+        launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
+               key_off, (const uint64_t *)lE, (int)(rbits + 6 <= 31), med_list, big_list, fb_list, gstat);
+        launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
+        V2Out wo;
+        wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = varena; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
+        wo.arena = arena_scr; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
+        wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+        wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
+        // persistent grids over device-side list counts (routing happened after the last host sync)
+        launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
+               (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
+        if (rbits + 6 <= 31) {
+            launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
+                   (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
+            launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 256)), dim3(1024), 0,
+                   (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
+        }
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+        nmed = ctx->pinned[0]; nbig2 = ctx->pinned[1];
+        nfb = ctx->pinned[3]; efb = ctx->pinned[4];
+        ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
+        if (nfb) {
+            need_pair_pos();
+            // txns beyond the block tiers (> 64 keys, > HUGE_E raw entries, or ranks beyond 25 bits): gather to global
+            // memory, sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
+            uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
+            uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
+            uint64_t *fb_maxk = ctx->get<uint64_t>("v2_fb_maxk", 1);
+            ACC_HIP(hipMemsetAsync(fb_maxk, 0, sizeof(uint64_t), st));
+            launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
+                   (const uint32_t *)fb_list, key_off, (const uint64_t *)vdep_off, fb_e, fb_maxk);
+            scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
+            ACC_HIP(hipMemcpyAsync(ctx->pinned, fb_maxk, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            const int bbits = bits_for(nfb - 1);
+            const int kbits = std::max(1, bits_for(ctx->pinned[0] - 1));   // key index within its txn
+            if (bbits + rbits + kbits > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
+            uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
+            launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+                   (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)vcnt, key_off,
+                   rbits, kbits, gkey);
+            Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + kbits);
+            uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
+            uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
+            launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
+                   (const uint64_t *)s1.keys, kbits, nflag);
+            scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
+            uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
+            uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
+            launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
+                   (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, kbits, key_off,
+                   (const uint64_t *)vdep_off, (const uint32_t *)txn_of_rank, dep_scr, u_cnt, idx1, key2);
+            Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
+            launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
+                   (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
+                   (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)vcnz, (const uint64_t *)varena, arena_scr);
+        }
+    }
+    // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch)
+    const char *nt_env = getenv("ACC_ST_NT");
+    int st_nt = nt_env ? atoi(nt_env) : 512;
+    if (rbits > 28 && st_nt > 512) st_nt = 512;
+    const uint32_t tt = (uint32_t)st_nt / ST_G;
+    const uint32_t ntiles = (n + tt - 1) / tt;
+    uint64_t *lb_status = ctx->get<uint64_t>("v3_status", 2 * (size_t)ntiles + 1);
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(lb_status + 2 * (size_t)ntiles);
+    ACC_HIP(hipMemsetAsync(lb_status, 0, (2 * (size_t)ntiles + 1) * sizeof(uint64_t), st));
+    uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);
+    V3Stream sp;
+    sp.v = vv; sp.err = gstat + 5;
+    sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.bK = bK; sp.bE = bE;
+    sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
+    sp.dep_scr = dep_st; sp.status = lb_status; sp.ticket = ticket; sp.n = n; sp.ntiles = ntiles;
+    auto stream = [&](auto ent_tag) {
+        using EntT = decltype(ent_tag);
+        if constexpr (sizeof(EntT) == 4) {
+            if (st_nt == 1024) { launch(ctx, "v3_stream", k_v3_stream<EntT, 1024>, dim3(ntiles), dim3(1024), 0, sp); return; }
+        }
+        if (st_nt == 512) launch(ctx, "v3_stream", k_v3_stream<EntT, 512>, dim3(ntiles), dim3(512), 0, sp);
+        else launch(ctx, "v3_stream", k_v3_stream<EntT, 256>, dim3(ntiles), dim3(256), 0, sp);
     };
-    finish();
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+#ifdef ACC_PHASE_PROF
+    const size_t prof_rows = (size_t)ntiles * (st_nt / 64);
+    unsigned long long *prof_buf = ctx->get<unsigned long long>("v3_prof", 8 * prof_rows);
+    ACC_HIP(hipMemsetAsync(prof_buf, 0, 8 * prof_rows * sizeof(unsigned long long), st));
+    ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_st_prof), &prof_buf, sizeof prof_buf, 0, hipMemcpyHostToDevice, st));
+#endif
+    if (rbits <= 28) stream(uint32_t{});
+    else stream(uint64_t{});
+#ifdef ACC_PHASE_PROF
+    {
+        std::vector<unsigned long long> h(8 * prof_rows);
+        ACC_HIP(hipMemcpyAsync(h.data(), prof_buf, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipStreamSynchronize(st));
+        double sum[6] = {}, mx[6] = {};
+        size_t w = 0;
+        for (size_t r = 0; r < prof_rows; ++r) {
+            if (!h[8 * r + 7]) continue;
+            ++w;
+            for (int i = 0; i < 6; ++i) { sum[i] += (double)h[8 * r + i]; mx[i] = std::max(mx[i], (double)h[8 * r + i]); }
+        }
+        const double d = w ? (double)w : 1.0;
+        fprintf(stderr, "[st_phase] waves=%zu avg cycles: setup %.0f records %.0f gather %.0f sort %.0f emit-lds %.0f lookback+copy %.0f | max: %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                w, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
+    }
+#endif
+    if (nbig)
+        launch(ctx, "v3_bigcopy", k_v3_bigcopy, dim3((nbig + WAVES - 1) / WAVES), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
+               (const uint64_t *)varena, (const uint64_t *)ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1),
+               (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const int32_t *)arena_scr, (const uint32_t *)key_scr,
+               arena, key_idx);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
+    launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n, (const uint64_t *)u_off,
+           (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
+           (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr, dep_txn);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 11, gstat + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
-    if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
-    ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
-    const uint64_t nfb = ctx->pinned[3], efb = ctx->pinned[4];
-    ctx->stat("keydeps.g32_txns", ng32);
-    ctx->stat("keydeps.small_txns", nsmall);
+    if (ctx->pinned[11]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
+    ctx->stat("keydeps.stream_txns", n - nbig);
+    ctx->stat("keydeps.big_path_txns", nbig);
     ctx->stat("keydeps.medium_txns", nmed);
-    ctx->stat("keydeps.big_txns", nbig);
+    ctx->stat("keydeps.big_txns", nbig2);
     ctx->stat("keydeps.fallback_txns", nfb);
     ctx->stat("keydeps.fallback_entries", efb);
     ctx->stat("keydeps.bumped_committed", nbc);
-    if (nfb) {
-        need_pair_pos();
-        // txns whose dependency-rank range exceeds the bitmap tier (or > 64 keys): gather to global memory,
-        // sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
-        uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
-        uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
-        uint64_t *fb_maxk = ctx->get<uint64_t>("v2_fb_maxk", 1);
-        ACC_HIP(hipMemsetAsync(fb_maxk, 0, sizeof(uint64_t), st));
-        launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
-               (const uint32_t *)fb_list, key_off, (const uint64_t *)dep_off, fb_e, fb_maxk);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, fb_maxk, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        const int bbits = bits_for(nfb - 1);
-        const int kbits = std::max(1, bits_for(ctx->pinned[0] - 1));   // key index within its txn
-        if (bbits + rbits + kbits > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
-        uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
-        launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
-               (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)cnt, key_off,
-               rbits, kbits, gkey);
-        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + kbits);
-        uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
-        uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
-        launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
-               (const uint64_t *)s1.keys, kbits, nflag);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
-        uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
-        uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
-        launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
-               (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, kbits, key_off,
-               (const uint64_t *)dep_off, (const uint32_t *)txn_of_rank, dep_scratch, u_cnt, idx1, key2);
-        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
-        launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
-               (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
-               (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)cnz, (const uint64_t *)arena_off, arena);
-        finish();
-        ctx->sync();
-    }
+    (void)lB;
     *view = acc_keydeps_view{ n, ctx->pinned[8], ctx->pinned[9], ctx->pinned[10], E, arena_off, arena, kd_off,
                               key_idx, u_off, dep_txn };
     ctx->kd_view = *view;

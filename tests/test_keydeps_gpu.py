@@ -163,7 +163,7 @@ def test_path_selection():
     with Context(0, timing=True) as c:
         c.calculate_partial_deps(b)
         names = set(c.timing())
-    assert "v2_write_small" in names and "query_emit" not in names
+    assert "v3_stream" in names and "query_emit" not in names
     com = np.where((b.status >= W.COMMITTED) & (b.status <= W.APPLIED))[0][:2]
     b.exe_msb[com] = b.exe_msb[com[0]]
     b.exe_lsb[com] = b.txn_lsb[com].max() + (np.uint64(7) << np.uint64(16))
