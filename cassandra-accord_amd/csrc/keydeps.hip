@@ -1839,6 +1839,54 @@ __device__ __forceinline__ uint32_t group_inclusive(uint32_t x, uint32_t sub)
     return x;
 }
 
+template <class T>
+__device__ __forceinline__ T gshfl_xor(T v, int m)
+{
+    if constexpr (sizeof(T) == 8) return shfl_xor64(v, m);
+    else return (T)__shfl_xor(v, m, 64);
+}
+
+// Sorts buf[0, 16 * R) of a ST_G-lane group ascending (positions >= n_valid read as all-ones pads) with R entries per
+// lane in registers, element i = r * 16 + sub: partners at distance < 16 are lanes of the group (shuffles), the others
+// registers of the same lane. Writes the sorted entries back.
+template <class EntT, int R>
+__device__ __forceinline__ void group_reg_sort(EntT *buf, uint32_t sub, uint32_t n_valid)
+{
+    EntT v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * ST_G + sub;
+        v[r] = i < n_valid ? buf[i] : ~(EntT)0;
+    }
+#pragma unroll
+    for (uint32_t k = 2; k <= (uint32_t)(ST_G * R); k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            if (jj >= (uint32_t)ST_G) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int r2 = r ^ (int)(jj / ST_G);
+                    if (r2 > r) {
+                        const bool up = (((uint32_t)r * ST_G + sub) & k) == 0;
+                        const EntT a = v[r], b = v[r2];
+                        if ((a > b) == up) { v[r] = b; v[r2] = a; }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const EntT y = gshfl_xor(v[r], (int)jj);
+                    const bool up = (((uint32_t)r * ST_G + sub) & k) == 0, lower = (sub & jj) == 0;
+                    const EntT lo = v[r] < y ? v[r] : y, hi = v[r] < y ? y : v[r];
+                    v[r] = (lower == up) ? lo : hi;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[r * ST_G + sub] = v[r];
+}
+
 #ifdef ACC_PHASE_PROF
 // tuning build only (tools/build_prof.sh): per-phase wave cycles of k_v3_stream, one row of 8 per wave (no atomics)
 __device__ unsigned long long *g_st_prof;
@@ -1859,16 +1907,16 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     __shared__ EntT ent[TT][ST_N2];
     __shared__ uint32_t kc[TT][ST_K];
     __shared__ uint32_t kbase[TT][ST_K];
-    __shared__ uint64_t tsz[2][TT];
     __shared__ uint16_t stA[TT][ST_K + ST_N2];
     __shared__ uint32_t s_tile;
     const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (ST_G - 1), grp = tid / ST_G, g0 = lane & (64 - ST_G);
     const uint64_t gmask = ((1ull << ST_G) - 1) << g0;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    // one ticket per block (launch-order independent), one look-back tile per wave: no block barrier after this one
     if (tid == 0) s_tile = atomicAdd(s.ticket, 1u);
     __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint32_t t = tile * TT + grp;
+    const uint32_t tile = s_tile * (NT / 64) + (tid >> 6);   // wave tile: 64 / ST_G txns
+    const uint32_t t = tile * (64 / ST_G) + (lane >> 4);
     const bool valid = t < s.n;
     TxnCtx c{};
     bool big = false;
@@ -1911,20 +1959,14 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     uint64_t A = 0, K = 0;
     if (sm) { A = (uint64_t)Kd + E; K = Kd; }
     else if (valid) { K = s.bK[t]; A = K + s.bE[t]; }
-    if (sub == 0) { tsz[0][grp] = A; tsz[1][grp] = K; }
-    __syncthreads();
-    uint64_t tv[2] = { 0, 0 }, ttot[2] = { 0, 0 };
-    if (tid < 64) {
+    uint64_t excl[2] = { 0, 0 }, wtot[2] = { 0, 0 };
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint64_t x = lane < (uint32_t)TT ? tsz[q][lane] : 0ull;
-            const uint64_t inc = wave_inclusive(x, OpAdd<uint64_t>());
-            tv[q] = inc - x;
-            ttot[q] = shfl_idx(inc, 63);
-        }
-        const uint64_t mine = lane == 0 ? ttot[0] : ttot[1];
-        if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], mine | (tile == 0 ? SCAN_INC : SCAN_AGG));
+    for (int g = 0; g < 64 / ST_G; ++g) {
+        const uint64_t ag = shfl_idx(A, g * ST_G), kg = shfl_idx(K, g * ST_G);
+        if ((uint32_t)g < (lane >> 4)) { excl[0] += ag; excl[1] += kg; }
+        wtot[0] += ag; wtot[1] += kg;
     }
+    if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (lane == 0 ? wtot[0] : wtot[1]) | (tile == 0 ? SCAN_INC : SCAN_AGG));
     kbase[grp][sub] = e_incl - e;
     kc[grp][sub] = 0;
     if (sm && !run) {
@@ -1997,34 +2039,43 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
         if (sub == 0) atomicAdd((unsigned long long *)s.err, 1ull);
         ok = false;
     }
-    uint32_t n2 = 16;
-    while (n2 < E) n2 <<= 1;
-    if (!ok) n2 = 0;
-    for (uint32_t q = E + sub; q < n2; q += ST_G) buf[q] = ~(EntT)0;
-    uint32_t wn2 = n2, wE = ok ? E : 0;
+    uint32_t wE = ok ? E : 0;
 #pragma unroll
-    for (int d = ST_G; d < 64; d <<= 1) {
-        wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
-        wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
+    for (int d = ST_G; d < 64; d <<= 1) wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // ---- sort each group's entries: registers + shuffles up to 64 entries (wave-uniform choice), LDS bitonic beyond
+    if (wE <= 16) group_reg_sort<EntT, 1>(buf, sub, ok ? E : 0);
+    else if (wE <= 32) group_reg_sort<EntT, 2>(buf, sub, ok ? E : 0);
+    else if (wE <= 64) group_reg_sort<EntT, 4>(buf, sub, ok ? E : 0);
+    else {
+        uint32_t n2 = 16;
+        while (n2 < E) n2 <<= 1;
+        if (!ok) n2 = 0;
+        for (uint32_t q = E + sub; q < n2; q += ST_G) buf[q] = ~(EntT)0;
+        uint32_t wn2 = n2;
+#pragma unroll
+        for (int d = ST_G; d < 64; d <<= 1) wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (uint32_t k = 2; k <= wn2; k <<= 1) {
+            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                if (k <= n2) {
+                    for (uint32_t pi = sub; pi < (n2 >> 1); pi += ST_G) {
+                        const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
+                        const uint32_t l = i | jj;
+                        const EntT xa = buf[i], ya = buf[l];
+                        const bool up = (i & k) == 0;
+                        if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            }
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // ---- bitonic sort of each group's n2 entries (loop bounds uniform over the wave)
-    for (uint32_t k = 2; k <= wn2; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            if (k <= n2) {
-                for (uint32_t pi = sub; pi < (n2 >> 1); pi += ST_G) {
-                    const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
-                    const uint32_t l = i | jj;
-                    const EntT xa = buf[i], ya = buf[l];
-                    const bool up = (i & k) == 0;
-                    if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        }
-    }
     ST_PH(4);
     // ---- KeyDeps in LDS, before the look-back (its wait hides the TxnId gathers): the arena (header ints and per-key
     // TxnId indices) staged as u16; the distinct TxnIds go straight to the txn's fixed scratch slot t * ST_N2
@@ -2059,20 +2110,13 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     if (ok && sub == 0) s.u_cnt_out[t] = distinct;
     ST_PH(5);
     // ---- tile offsets: look-back (by now the previous tiles have mostly published inclusive prefixes)
-    __syncthreads();
-    if (tid < 64) {
-        uint64_t pre[2] = { 0, 0 };
-        if (tile != 0) {
-            lookback_n<2>(s.status, s.ntiles, tile, pre);
-            const uint64_t mine = lane == 0 ? ttot[0] : ttot[1];
-            const uint64_t pm = lane == 0 ? pre[0] : pre[1];
-            if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (pm + mine) | SCAN_INC);
-        }
-        if (lane < (uint32_t)TT) { tsz[0][lane] = pre[0] + tv[0]; tsz[1][lane] = pre[1] + tv[1]; }
+    uint64_t pre[2] = { 0, 0 };
+    if (tile != 0) {
+        lookback_n<2>(s.status, s.ntiles, tile, pre);
+        if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (lane == 0 ? pre[0] + wtot[0] : pre[1] + wtot[1]) | SCAN_INC);
     }
-    __syncthreads();
     if (!valid) return;
-    const uint64_t aoff = tsz[0][grp], koff = tsz[1][grp];
+    const uint64_t aoff = pre[0] + excl[0], koff = pre[1] + excl[1];
     if (sub == 0) {
         s.arena_off[t] = aoff; s.kd_off[t] = koff;
         if (t + 1 == s.n) { s.arena_off[t + 1] = aoff + A; s.kd_off[t + 1] = koff + K; }
@@ -2084,7 +2128,7 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
 #ifdef ACC_PHASE_PROF
     ST_PH(6);
     if (lane == 0) {
-        unsigned long long *row = g_st_prof + 8 * ((size_t)tile * (NT / 64) + (tid >> 6));
+        unsigned long long *row = g_st_prof + 8 * (size_t)tile;
         for (int i = 0; i < 6; ++i) row[i] = ph[i + 1] - ph[i];
         row[7] = 1;
     }
@@ -2716,7 +2760,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     int st_nt = nt_env ? atoi(nt_env) : 512;
     if (rbits > 28 && st_nt > 512) st_nt = 512;
     const uint32_t tt = (uint32_t)st_nt / ST_G;
-    const uint32_t ntiles = (n + tt - 1) / tt;
+    const uint32_t nblocks = (n + tt - 1) / tt;
+    const uint32_t ntiles = nblocks * (uint32_t)(st_nt / 64);   // look-back tiles: one per wave
     uint64_t *lb_status = ctx->get<uint64_t>("v3_status", 2 * (size_t)ntiles + 1);
     uint32_t *ticket = reinterpret_cast<uint32_t *>(lb_status + 2 * (size_t)ntiles);
     ACC_HIP(hipMemsetAsync(lb_status, 0, (2 * (size_t)ntiles + 1) * sizeof(uint64_t), st));
@@ -2729,13 +2774,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     auto stream = [&](auto ent_tag) {
         using EntT = decltype(ent_tag);
         if constexpr (sizeof(EntT) == 4) {
-            if (st_nt == 1024) { launch(ctx, "v3_stream", k_v3_stream<EntT, 1024>, dim3(ntiles), dim3(1024), 0, sp); return; }
+            if (st_nt == 1024) { launch(ctx, "v3_stream", k_v3_stream<EntT, 1024>, dim3(nblocks), dim3(1024), 0, sp); return; }
         }
-        if (st_nt == 512) launch(ctx, "v3_stream", k_v3_stream<EntT, 512>, dim3(ntiles), dim3(512), 0, sp);
-        else launch(ctx, "v3_stream", k_v3_stream<EntT, 256>, dim3(ntiles), dim3(256), 0, sp);
+        if (st_nt == 512) launch(ctx, "v3_stream", k_v3_stream<EntT, 512>, dim3(nblocks), dim3(512), 0, sp);
+        else launch(ctx, "v3_stream", k_v3_stream<EntT, 256>, dim3(nblocks), dim3(256), 0, sp);
     };
 #ifdef ACC_PHASE_PROF
-    const size_t prof_rows = (size_t)ntiles * (st_nt / 64);
+    const size_t prof_rows = (size_t)ntiles;
     unsigned long long *prof_buf = ctx->get<unsigned long long>("v3_prof", 8 * prof_rows);
     ACC_HIP(hipMemsetAsync(prof_buf, 0, 8 * prof_rows * sizeof(unsigned long long), st));
     ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_st_prof), &prof_buf, sizeof prof_buf, 0, hipMemcpyHostToDevice, st));
