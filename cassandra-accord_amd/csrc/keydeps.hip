@@ -1334,17 +1334,136 @@ __device__ __forceinline__ void locate_elem(const RunsT<MAXK> &R, uint32_t nk, u
 constexpr int BIG_GU = 4;   // independent loads in flight per thread during the gather
 
 // Sort records are u32 (TxnId rank << 6 | key index): half the LDS of u64 records, twice the blocks per CU. The
-// host takes this tier only when ranks fit 25 bits (2N <= 2^25). CAP = raw run elements per block: 8192 (32 KiB,
-// routed by k_v3_bigfill) or 32768 (128 KiB, txns the first launch passes on via gstat[6] / huge_list); beyond that
-// the global path.
+// host takes these tiers only when ranks fit 25 bits (2N <= 2^25). CAP = raw run elements per block: MED_CAP (routed
+// by k_v3_route), BIG_E (the txns beyond MED_CAP, routed or passed on by the first launch via gstat[1]), HUGE_E
+// (txns the BIG_E launch passes on via gstat[6] / huge_list); beyond that the global path.
+// MED_CAP / BIG_E sort by merging: a key's entries are at most NRUN runs that are each sorted by TxnId rank (CFK
+// position order within a class list; inline records are sorted by one thread), so after compacting the kept
+// entries a merge tree over the non-empty runs (log2 of the run count levels, merge-path partitions per thread)
+// sorts them in a few LDS passes instead of the O(n log^2 n) of a bitonic network. HUGE_E keeps the bitonic sort
+// in place (no room for a second buffer).
+constexpr int MED_CAP = 1024;
+constexpr int RUN_SLOTS = NRUN * BIG_K;
+
+template <int CAP>
+constexpr bool big_merges() { return CAP <= BIG_E; }
+
 template <int CAP, int NT>
 struct BigLds {
     uint32_t buf[CAP];
+    uint32_t tmp[big_merges<CAP>() ? CAP : 1];
+    uint32_t rs[big_merges<CAP>() ? RUN_SLOTS + 1 : 1];
+    uint32_t ss[big_merges<CAP>() ? RUN_SLOTS : 1];   // compacted start of each (key, run) slot
     RunsT<BIG_K> R;
-    uint32_t s_kept;
+    uint32_t s_kept, s_nr;
     uint32_t wk_cnt[NT / 64][BIG_K];
     uint32_t wdist[NT / 64];
 };
+
+// Sorts the kept entries of buf[0, total) (dropped = all-ones) into ascending order; returns the array holding the
+// E sorted entries (buf or tmp). Block-wide; R = the txn's runs (raw layout: key-major, runs in slot order).
+template <int CAP, int NT>
+__device__ uint32_t *big_merge_sort(BigLds<CAP, NT> &L, uint32_t nk, uint32_t total, uint32_t E)
+{
+    uint32_t *buf = L.buf, *tmp = L.tmp, *rs = L.rs;
+    const RunsT<BIG_K> &R = L.R;
+    const uint32_t tid = threadIdx.x;
+    __shared__ uint32_t lds[NT / 64];
+    // ---- compaction (order kept): tmp[kept index] = entry; buf[raw e] = kept entries before e
+    const uint32_t CHR = (total + NT - 1) / NT;
+    const uint32_t r0 = min(total, tid * CHR), r1 = min(total, r0 + CHR);
+    uint32_t cnt = 0;
+    for (uint32_t e = r0; e < r1; ++e) cnt += buf[e] != 0xFFFFFFFFu;
+    uint32_t tot;
+    uint32_t pos = block_exclusive(cnt, OpAdd<uint32_t>(), lds, tot);
+    for (uint32_t e = r0; e < r1; ++e) {
+        const uint32_t x = buf[e];
+        buf[e] = pos;
+        if (x != 0xFFFFFFFFu) tmp[pos++] = x;
+    }
+    __syncthreads();
+    // ---- run slots (key k, run q) -> compacted starts; inline keys (one unsorted slot of <= REC_INLINE) sorted here
+    for (uint32_t k = tid; k < nk; k += NT) {
+        const uint32_t kb = R.kbase[k];
+        uint32_t st[NRUN + 1];
+#pragma unroll
+        for (int q = 0; q <= NRUN; ++q) {
+            const uint32_t raw = kb + R.pre[k][q];
+            st[q] = raw >= total ? E : buf[raw];
+        }
+        if (R.m[k] == INLINE_M) {
+            for (uint32_t i = st[0] + 1; i < st[NRUN]; ++i) {   // insertion sort
+                const uint32_t x = tmp[i];
+                uint32_t j = i;
+                while (j > st[0] && tmp[j - 1] > x) { tmp[j] = tmp[j - 1]; --j; }
+                tmp[j] = x;
+            }
+        }
+        // slot starts; a slot's end is the next slot's start (raw layout is key-major, slot-ordered)
+#pragma unroll
+        for (int q = 0; q < NRUN; ++q) L.ss[k * NRUN + q] = st[q];
+    }
+    __syncthreads();
+    // ---- non-empty runs -> rs[0, NR), rs[NR] = E (one wave; slots in order)
+    if (tid < 64) {
+        const uint32_t lane = lane_id();
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const uint32_t ns = nk * NRUN;
+        uint32_t nr = 0;
+        for (uint32_t s0 = 0; s0 < ns; s0 += 64) {
+            const uint32_t sl = s0 + lane;
+            uint32_t a = 0, b = 0;
+            if (sl < ns) {
+                a = L.ss[sl];
+                b = sl + 1 < ns ? L.ss[sl + 1] : E;
+            }
+            const bool ne = sl < ns && b > a;
+            const uint64_t bal = __ballot(ne);
+            if (ne) rs[nr + (uint32_t)__popcll(bal & lt)] = a;
+            nr += (uint32_t)__popcll(bal);
+        }
+        if (lane == 0) { rs[nr] = E; L.s_nr = nr; }
+    }
+    __syncthreads();
+    uint32_t NR = L.s_nr;
+    uint32_t *src = tmp, *dst = buf;
+    const uint32_t CH = (E + NT - 1) / NT;
+    while (NR > 1) {
+        const uint32_t NP = (NR + 1) / 2;
+        const uint32_t o0 = min(E, tid * CH), o1 = min(E, o0 + CH);
+        if (o0 < o1) {
+            uint32_t lo = 0, hi = NP;   // last pair with start <= o0
+            while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (rs[2 * m] <= o0) lo = m; else hi = m; }
+            uint32_t p = lo, q = o0;
+            while (q < o1) {
+                const uint32_t a0 = rs[2 * p], a1 = rs[min(2 * p + 1, NR)], b1 = rs[min(2 * p + 2, NR)];
+                const uint32_t la = a1 - a0, lb = b1 - a1, end = min(o1, b1), d = q - a0;
+                uint32_t i0 = d > lb ? d - lb : 0, i1 = min(d, la);
+                while (i0 < i1) {
+                    const uint32_t m = (i0 + i1) >> 1;
+                    if (src[a0 + m] < src[a1 + d - 1 - m]) i0 = m + 1; else i1 = m;
+                }
+                uint32_t i = i0, j = d - i0;
+                for (; q < end; ++q) {
+                    const bool takeA = j >= lb || (i < la && src[a0 + i] < src[a1 + j]);
+                    dst[q] = takeA ? src[a0 + i] : src[a1 + j];
+                    i += takeA; j += !takeA;
+                }
+                ++p;
+            }
+        }
+        __syncthreads();
+        uint32_t nv = 0;
+        if (tid < NP) nv = rs[2 * tid];
+        __syncthreads();
+        if (tid < NP) rs[tid] = nv;
+        if (tid == 0) rs[NP] = E;
+        __syncthreads();
+        NR = NP;
+        uint32_t *sw = src; src = dst; dst = sw;
+    }
+    return src;
+}
 
 template <int CAP, int NT>
 __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const uint64_t *__restrict__ cnt, const V2Out &o)
@@ -1365,7 +1484,10 @@ __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const u
     }
     if (oversize) {
         if (tid == 0) {
-            if (CAP == BIG_E && c.nk <= BIG_K) {
+            if (CAP == MED_CAP && c.nk <= BIG_K) {
+                uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[1], 1ull);
+                o.big_list[f] = t;
+            } else if (CAP == BIG_E && c.nk <= BIG_K) {
                 uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[6], 1ull);
                 o.huge_list[f] = t;
             } else {
@@ -1410,17 +1532,21 @@ __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const u
         if (tid == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
         return;
     }
-    // ---- bitonic sort over n2 (one compare-exchange per pair index)
-    for (uint32_t k = 2; k <= n2; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t pi = tid; pi < (n2 >> 1); pi += NT) {
-                const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
-                const uint32_t l = i | jj;
-                const uint32_t xa = buf[i], ya = buf[l];
-                const bool up = (i & k) == 0;
-                if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
+    if constexpr (big_merges<CAP>()) {
+        buf = big_merge_sort<CAP, NT>(L, c.nk, total, c.E);
+    } else {
+        // ---- bitonic sort over n2 (one compare-exchange per pair index)
+        for (uint32_t k = 2; k <= n2; k <<= 1) {
+            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t pi = tid; pi < (n2 >> 1); pi += NT) {
+                    const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
+                    const uint32_t l = i | jj;
+                    const uint32_t xa = buf[i], ya = buf[l];
+                    const bool up = (i & k) == 0;
+                    if ((xa > ya) == up) { buf[i] = ya; buf[l] = xa; }
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
     }
     // ---- emit: wave w owns sorted positions [w*Q, (w+1)*Q), Q a multiple of 64
@@ -1459,13 +1585,14 @@ __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const u
 }
 
 // Persistent over the routed list: blocks loop (a grid of one block per listed txn made the 128-KiB launch pay a
-// block launch + exit per big txn). CAP = BIG_E reads its count from gstat[1], CAP = HUGE_E from gstat[6].
+// block launch + exit per big txn). CAP = MED_CAP reads its count from gstat[0], BIG_E from gstat[1], HUGE_E from
+// gstat[6].
 template <int CAP, int NT>
 __global__ __launch_bounds__(NT) void k_v2_write_big(const uint32_t *__restrict__ list, V2View v,
                                                      const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ BigLds<CAP, NT> L;
-    const uint32_t cnt_list = (uint32_t)o.gstat[CAP > BIG_E ? 6 : 1];
+    const uint32_t cnt_list = (uint32_t)o.gstat[CAP > BIG_E ? 6 : CAP == MED_CAP ? 0 : 1];
     for (uint32_t b = blockIdx.x; b < cnt_list; b += gridDim.x) {
         big_one<CAP, NT>(L, list[b], v, cnt, o);
         __syncthreads();
@@ -2704,13 +2831,18 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync)
-        launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
-               (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
         if (rbits + 6 <= 31) {
+            launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
+                   (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
+
             launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
                    (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
             launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 256)), dim3(1024), 0,
                    (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
+        } else {
+            // ranks beyond 25 bits: u64 records in the wave tier (k_v3_route sends everything else to the global path)
+            launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
+                   (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
         }
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
