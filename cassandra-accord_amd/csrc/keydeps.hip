@@ -1053,7 +1053,7 @@ constexpr int NRUN = 7;
 constexpr int MED_E = 1024, MED_K = 64;
 constexpr int BIG_K = 64;
 constexpr int BIG_E = 8192;                 // raw entries per block in LDS (32 KiB of u32 records)
-constexpr int HUGE_E = 32768;               // second big launch (128 KiB)
+constexpr int HUGE_E = 16384;               // second big launch (64 KiB + a 64 KiB merge buffer)
 
 struct V2Out {
     const uint32_t *key_off;
@@ -1346,7 +1346,7 @@ constexpr int MED_CAP = 1024;
 constexpr int RUN_SLOTS = NRUN * BIG_K;
 
 template <int CAP>
-constexpr bool big_merges() { return CAP <= BIG_E; }
+constexpr bool big_merges() { return CAP <= HUGE_E; }
 
 template <int CAP, int NT>
 struct BigLds {
@@ -1375,7 +1375,7 @@ __device__ uint32_t *big_merge_sort(BigLds<CAP, NT> &L, uint32_t nk, uint32_t to
     uint32_t cnt = 0;
     for (uint32_t e = r0; e < r1; ++e) cnt += buf[e] != 0xFFFFFFFFu;
     uint32_t tot;
-    uint32_t pos = block_exclusive(cnt, OpAdd<uint32_t>(), lds, tot);
+    uint32_t pos = block_exclusive<uint32_t, OpAdd<uint32_t>, NT / 64>(cnt, OpAdd<uint32_t>(), lds, tot);
     for (uint32_t e = r0; e < r1; ++e) {
         const uint32_t x = buf[e];
         buf[e] = pos;
@@ -2830,11 +2830,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         wo.arena = arena_scr; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
         wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
-        // persistent grids over device-side list counts (routing happened after the last host sync)
+        // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
+        // on a side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
+        ctx->fork(1);
+        ctx->launch_stream = ctx->aux[0];
         if (rbits + 6 <= 31) {
             launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
-
             launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
                    (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
             launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 256)), dim3(1024), 0,
@@ -2844,48 +2846,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
             launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
                    (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
         }
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
-        nmed = ctx->pinned[0]; nbig2 = ctx->pinned[1];
-        nfb = ctx->pinned[3]; efb = ctx->pinned[4];
-        ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
-        if (nfb) {
-            need_pair_pos();
-            // txns beyond the block tiers (> 64 keys, > HUGE_E raw entries, or ranks beyond 25 bits): gather to global
-            // memory, sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
-            uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
-            uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
-            uint64_t *fb_maxk = ctx->get<uint64_t>("v2_fb_maxk", 1);
-            ACC_HIP(hipMemsetAsync(fb_maxk, 0, sizeof(uint64_t), st));
-            launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
-                   (const uint32_t *)fb_list, key_off, (const uint64_t *)vdep_off, fb_e, fb_maxk);
-            scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
-            ACC_HIP(hipMemcpyAsync(ctx->pinned, fb_maxk, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-            ctx->sync();
-            const int bbits = bits_for(nfb - 1);
-            const int kbits = std::max(1, bits_for(ctx->pinned[0] - 1));   // key index within its txn
-            if (bbits + rbits + kbits > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
-            uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
-            launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
-                   (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)vcnt, key_off,
-                   rbits, kbits, gkey);
-            Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + kbits);
-            uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
-            uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
-            launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
-                   (const uint64_t *)s1.keys, kbits, nflag);
-            scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
-            uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
-            uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
-            launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
-                   (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, kbits, key_off,
-                   (const uint64_t *)vdep_off, (const uint32_t *)txn_of_rank, dep_scr, u_cnt, idx1, key2);
-            Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
-            launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
-                   (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
-                   (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)vcnz, (const uint64_t *)varena, arena_scr);
-        }
+        ctx->launch_stream = nullptr;
     }
     // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch)
     const char *nt_env = getenv("ACC_ST_NT");
@@ -2936,21 +2897,73 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                 w, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
     }
 #endif
-    if (nbig)
-        launch(ctx, "v3_bigcopy", k_v3_bigcopy, dim3((nbig + WAVES - 1) / WAVES), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
-               (const uint64_t *)varena, (const uint64_t *)ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1),
-               (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const int32_t *)arena_scr, (const uint32_t *)key_scr,
-               arena, key_idx);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
-    launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n, (const uint64_t *)u_off,
-           (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
-           (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr, dep_txn);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 11, gstat + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ctx->sync();
-    if (ctx->pinned[11]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
+    if (nbig) ctx->join(1);
+    // ---- big txns' arena / keys into place, TxnId offsets and compaction. With global-path txns (known only after
+    // the tiers ran) this is redone once they are written, so the common case pays one host sync here.
+    auto finish = [&]() {
+        if (nbig)
+            launch(ctx, "v3_bigcopy", k_v3_bigcopy, dim3((nbig + WAVES - 1) / WAVES), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
+                   (const uint64_t *)varena, (const uint64_t *)ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1),
+                   (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const int32_t *)arena_scr, (const uint32_t *)key_scr,
+                   arena, key_idx);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
+        launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n,
+               (const uint64_t *)u_off, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
+               (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr, dep_txn);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+    };
+    finish();
+    if (ctx->pinned[5]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
+    if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+    if (nbig) {
+        nmed = ctx->pinned[0]; nbig2 = ctx->pinned[1];
+        nfb = ctx->pinned[3]; efb = ctx->pinned[4];
+        ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
+    }
+    if (nfb) {
+        need_pair_pos();
+        uint64_t *vcnt = ctx->get<uint64_t>("cnt", P);
+        uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
+        uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
+        // txns beyond the block tiers (> 64 keys, > HUGE_E raw entries, or ranks beyond 25 bits): gather to global
+        // memory, sort by (txn, value, key) for the TxnId array and by (txn, key, value) for the arena order
+        uint64_t *fb_e = ctx->get<uint64_t>("v2_fb_e", nfb);
+        uint64_t *fb_off = ctx->get<uint64_t>("v2_fb_off", nfb + 1);
+        uint64_t *fb_maxk = ctx->get<uint64_t>("v2_fb_maxk", 1);
+        ACC_HIP(hipMemsetAsync(fb_maxk, 0, sizeof(uint64_t), st));
+        launch(ctx, "v2_fb_sizes", k_fb_sizes, dim3(grid_for(nfb, BLOCK)), dim3(BLOCK), 0, (uint32_t)nfb,
+               (const uint32_t *)fb_list, key_off, (const uint64_t *)vdep_off, fb_e, fb_maxk);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, fb_e, fb_off, nfb, true, fb_off + nfb);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, fb_maxk, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        const int bbits = bits_for(nfb - 1);
+        const int kbits = std::max(1, bits_for(ctx->pinned[0] - 1));   // key index within its txn
+        if (bbits + rbits + kbits > 64) fail(ACC_E_CAP, "too many oversized txns for the global KeyDeps path");
+        uint64_t *gkey = ctx->get<uint64_t>("v2_gkey", efb);
+        launch(ctx, "v2_big_gather", k_v2_big_gather, dim3((unsigned)((nfb + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
+               (uint32_t)nfb, (const uint32_t *)fb_list, (const uint64_t *)fb_off, vv, (const uint64_t *)vcnt, key_off,
+               rbits, kbits, gkey);
+        Sorted s1 = radix_sort(ctx, "rs_big1", gkey, nullptr, efb, bbits + rbits + kbits);
+        uint32_t *nflag = ctx->get<uint32_t>("v2_big_nflag", efb);
+        uint32_t *nincl = ctx->get<uint32_t>("v2_big_nincl", efb);
+        launch(ctx, "v2_big_newflag", k_v2_big_newflag, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
+               (const uint64_t *)s1.keys, kbits, nflag);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, nflag, nincl, efb, false);
+        uint32_t *idx1 = ctx->get<uint32_t>("v2_big_idx1", efb);
+        uint64_t *key2 = ctx->get<uint64_t>("v2_big_key2", efb);
+        launch(ctx, "v2_big_rank", k_v2_big_rank, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb, (const uint64_t *)s1.keys,
+               (const uint32_t *)nincl, (const uint32_t *)fb_list, (const uint64_t *)fb_off, rbits, kbits, key_off,
+               (const uint64_t *)vdep_off, (const uint32_t *)txn_of_rank, dep_scr, u_cnt, idx1, key2);
+        Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
+        launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
+               (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
+               (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)vcnz, (const uint64_t *)varena, arena_scr);
+        finish();
+    }
     ctx->stat("keydeps.stream_txns", n - nbig);
     ctx->stat("keydeps.big_path_txns", nbig);
     ctx->stat("keydeps.medium_txns", nmed);

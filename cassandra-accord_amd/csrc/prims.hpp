@@ -78,8 +78,8 @@ __device__ __forceinline__ T wave_inclusive(T v, Op op)
 }
 
 // Block-wide exclusive scan of per-thread values; returns the exclusive prefix of this thread and
-// the block total. `lds` holds WAVES elements.
-template <class T, class Op>
+// the block total. `lds` holds NWV elements; NWV = the block's wave count (blockDim.x / 64).
+template <class T, class Op, int NWV = WAVES>
 __device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
 {
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
@@ -89,7 +89,7 @@ __device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
     T wave_prefix = Op::identity();
     T tot = Op::identity();
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) {
+    for (int w = 0; w < NWV; ++w) {
         T x = lds[w];
         if (w < (int)wave) wave_prefix = op(wave_prefix, x);
         tot = op(tot, x);
