@@ -27,7 +27,7 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_mixed", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
-           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out"]
+           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce"]
 
 
 class Opts(C.Structure):
@@ -192,6 +192,10 @@ class GraphIn(C.Structure):
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
 
 
+# acc_alltoallv_fn: int (*)(void *user, const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes)
+AllToAllvFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.POINTER(C.c_uint64))
+ACC_COMM_ID_BYTES = 128
+
 _lib = None
 
 
@@ -252,6 +256,16 @@ def load():
     L.acc_rmm_slice.restype = C.c_int
     L.acc_rangedeps_stab.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(StabIn), C.POINTER(StabView)]
     L.acc_rangedeps_stab.restype = C.c_int
+    L.acc_comm_unique_id.argtypes = [C.c_void_p]
+    L.acc_comm_unique_id.restype = C.c_int
+    L.acc_comm_init_rccl.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.POINTER(C.c_void_p)]
+    L.acc_comm_init_rccl.restype = C.c_int
+    L.acc_comm_init_host.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, AllToAllvFn, C.c_void_p, C.POINTER(C.c_void_p)]
+    L.acc_comm_init_host.restype = C.c_int
+    L.acc_comm_destroy.argtypes = [C.c_void_p]
+    L.acc_comm_destroy.restype = None
+    L.acc_shard_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn), C.c_void_p, C.c_uint32, C.POINTER(MergeView)]
+    L.acc_shard_reduce.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
     L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]

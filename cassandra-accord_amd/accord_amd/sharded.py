@@ -238,3 +238,201 @@ def home_result_from_full(res, batch: Batch, rank: int, world: int) -> dict:
     cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
     return dict(key_off=np.array(key_off, np.uint64), key_code=cat(keys, np.uint64), val_off=np.array(val_off, np.uint64),
                 txn_rank=cat(vals, np.uint32), k2v_off=np.array(k2v_off, np.uint64), k2v=cat(k2v, np.int32))
+
+
+# ---------------------------------------------------------------- range-sharded RangeDeps (range commands per store)
+#
+# A CommandStore keeps each range command's ranges sliced to its own ranges (InMemoryCommandStore's update hook:
+# keysOrRanges.slice(ranges().allBetween(...), Minimal), impl/InMemoryCommandStore.java:739-761), so a range spanning
+# two stores is two stored ranges; a query txn's RangeDeps from each store lists those pieces, and PreAccept.reduce
+# folds the stores' PartialDeps with RangeDeps.with (= RelationMultiMap.linearUnion over Range::compare,
+# primitives/RangeDeps.java:567-582) in store order. The same split is given to the oracle for parity.
+
+def store_ranges_bound(bounds: np.ndarray, rank: int, end_inclusive: int):
+    """The store's range over integer key codes, in the batch's Range bound type: keys [lo, hi) are
+    (lo - 1, hi - 1] for Range.EndInclusive, [lo, hi) for Range.StartInclusive (Range.java:40-138)."""
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    return (lo - 1, hi - 1) if end_inclusive else (lo, hi)
+
+
+def slice_ranges(start: np.ndarray, end: np.ndarray, slo: int, shi: int):
+    """Ranges.slice(store, Minimal) of ranges against one store range of the same bound type: the intersections
+    (max(start, slo), min(end, shi)) that are non-empty, in order. Returns (keep mask, new start, new end)."""
+    s = np.maximum(start.astype(np.int64), slo)   # codes < 2^63
+    e = np.minimum(end.astype(np.int64), shi)
+    return s < e, s, e
+
+
+def store_range_batch(rb, bounds: np.ndarray, rank: int):
+    """The store's mixed batch: key txns with keys in the store (restricted to them), range txns whose ranges
+    intersect the store (sliced to it), every other txn dropped; TxnId order kept. Returns (RangeBatch, global index
+    u32 of each kept txn)."""
+    from .workload import RangeBatch
+    b = rb.keys
+    n = b.n_txn
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    kc = b.key_code.astype(np.int64)
+    kin = (kc >= lo) & (kc < hi)
+    kown = np.repeat(np.arange(n), np.diff(b.key_off.astype(np.int64)))
+    kcnt = np.bincount(kown[kin], minlength=n)
+    slo, shi = store_ranges_bound(bounds, rank, rb.end_inclusive)
+    rown = np.repeat(np.arange(n), np.diff(rb.rng_off.astype(np.int64)))
+    rkeep, rs, re = slice_ranges(rb.rng_start, rb.rng_end, slo, shi)
+    rcnt = np.bincount(rown[rkeep], minlength=n)
+    keep = np.nonzero((kcnt > 0) | (rcnt > 0))[0]
+    key_off = np.zeros(len(keep) + 1, np.uint32)
+    np.cumsum(kcnt[keep], out=key_off[1:])
+    rng_off = np.zeros(len(keep) + 1, np.uint32)
+    np.cumsum(rcnt[keep], out=rng_off[1:])
+    sel_k = kin & np.isin(kown, keep)
+    sel_r = rkeep & np.isin(rown, keep)
+    kb = Batch(b.txn_msb[keep], b.txn_lsb[keep], b.txn_node[keep], b.exe_msb[keep], b.exe_lsb[keep], b.exe_node[keep],
+               b.status[keep], key_off, b.key_code[sel_k], dict(b.meta, store=rank))
+    sub = RangeBatch(kb, rng_off, rs[sel_r].astype(np.uint64), re[sel_r].astype(np.uint64), rb.end_inclusive,
+                     dict(rb.meta, store=rank))
+    return sub, keep.astype(np.uint32)
+
+
+def pack_range_fragments(res, gidx: np.ndarray, world: int):
+    """Per destination rank one int64 stream of RangeDeps fragments [t, nr, nv, no, (start, end) x nr, txnIds...,
+    rangesToTxnIds...] for every store txn with a non-empty RangeDeps (t and txnIds as global indices; empty
+    fragments skipped as RangeDeps.with skips empties). `res` = per-store result in the acc_rangedeps_view layout."""
+    n = len(gidx)
+    nr = np.diff(res.rd_off.astype(np.int64))
+    streams = [[] for _ in range(world)]
+    for t in np.nonzero(nr > 0)[0].tolist():
+        r, d, a = res.txn(t)
+        g = int(gidx[t])
+        se = np.stack([res.rng_start[r].astype(np.int64), res.rng_end[r].astype(np.int64)], 1).reshape(-1)
+        streams[g % world].append(np.concatenate([[g, len(r), len(d), len(a)], se, gidx[d].astype(np.int64),
+                                                  a.astype(np.int64)]))
+    return [np.concatenate(s) if s else np.zeros(0, np.int64) for s in streams]
+
+
+def unpack_range_merge(recv: np.ndarray, recv_counts: np.ndarray, home: np.ndarray, batch) -> dict:
+    """Received RangeDeps fragments -> Deps.merge input (acc_rmm_in layout, raw TxnIds) with one group per home txn,
+    its replies in source-rank (= store) order: the order of PreAccept.reduce's RangeDeps.with fold."""
+    frags = {}
+    pos = 0
+    for src, c in enumerate(recv_counts.tolist()):
+        end = pos + c
+        while pos < end:
+            t, nr, nv, no = (int(x) for x in recv[pos:pos + 4])
+            body = recv[pos + 4:pos + 4 + 2 * nr + nv + no]
+            frags.setdefault(t, []).append((src, body[:2 * nr], body[2 * nr:2 * nr + nv], body[2 * nr + nv:]))
+            pos += 4 + 2 * nr + nv + no
+    grp_off, key_off, val_off, k2v_off = [0], [0], [0], [0]
+    ka, kb_, vals, k2v = [], [], [], []
+    for t in home.tolist():
+        for _, se, v, kv in sorted(frags.get(t, []), key=lambda f: f[0]):
+            ka.append(se[0::2]); kb_.append(se[1::2]); vals.append(v); k2v.append(kv)
+            key_off.append(key_off[-1] + len(se) // 2)
+            val_off.append(val_off[-1] + len(v))
+            k2v_off.append(k2v_off[-1] + len(kv))
+        grp_off.append(len(key_off) - 1)
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+    v = cat(vals, np.int64)
+    kbk = batch.keys if hasattr(batch, "keys") else batch
+    return dict(grp_off=np.array(grp_off, np.uint64),
+                half=dict(key_off=np.array(key_off, np.uint64), key_a=cat(ka, np.uint64), key_b=cat(kb_, np.uint64),
+                          val_off=np.array(val_off, np.uint64), msb=kbk.txn_msb[v].astype(np.uint64),
+                          lsb=kbk.txn_lsb[v].astype(np.uint64), node=kbk.txn_node[v].astype(np.int32),
+                          k2v_off=np.array(k2v_off, np.uint64), k2v=cat(k2v, np.int32)))
+
+
+def range_reduce_local(rb, world: int, compute) -> dict:
+    """All `world` stores in one process (oracle-side reference and single-GPU parity): per store `compute(store
+    batch)` -> per-txn RangeDeps, fragments to every home rank, and per home rank the Deps.merge input. Returns
+    {rank: merge input}."""
+    bounds = even_split(np.concatenate([rb.keys.key_code, rb.rng_start, rb.rng_end]).astype(np.uint64), world)
+    streams = [[] for _ in range(world)]
+    for s in range(world):
+        sub, gidx = store_range_batch(rb, bounds, s)
+        out = pack_range_fragments(compute(sub), gidx, world)
+        for d in range(world):
+            streams[d].append(out[d])
+    res = {}
+    for d in range(world):
+        recv = np.concatenate(streams[d]) if streams[d] else np.zeros(0, np.int64)
+        counts = np.array([len(x) for x in streams[d]], np.int64)
+        res[d] = unpack_range_merge(recv, counts, home_txns(rb.n_txn, d, world), rb)
+    return res
+
+
+# ---------------------------------------------------------------- acc_comm / acc_shard_reduce (exchange behind the ABI)
+
+class Comm:
+    """An acc_comm: RCCL (Comm.rccl: rank 0's acc_comm_unique_id shared through torch.distributed) or the host
+    transport over a torch.distributed group (Comm.host: the library stages the streams in host memory and calls back
+    for an all-to-all(v) of bytes; a JVM host would plug in its own messaging here)."""
+
+    def __init__(self, ctx, handle, keep=None):
+        self.ctx, self.handle, self._keep = ctx, handle, keep
+
+    @classmethod
+    def rccl(cls, ctx, world: int, rank: int, group=None):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        from . import _lib as L
+        uid = np.zeros(L.ACC_COMM_ID_BYTES, np.uint8)
+        if rank == 0:
+            ctx.check(ctx._lib.acc_comm_unique_id(uid.ctypes.data))
+        if world > 1:
+            t = torch.from_numpy(uid.astype(np.int64))
+            dist.broadcast(t, 0, group=group)
+            uid = t.numpy().astype(np.uint8)
+        h = C.c_void_p()
+        ctx.check(ctx._lib.acc_comm_init_rccl(ctx.handle, world, rank, uid.ctypes.data, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def host(cls, ctx, world: int, rank: int, group=None):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        from . import _lib as L
+
+        def a2av(user, send, send_bytes, recv, recv_bytes):
+            try:
+                sb = [int(send_bytes[i]) for i in range(world)]
+                rbytes = [int(recv_bytes[i]) for i in range(world)]
+                src = np.ctypeslib.as_array((C.c_uint8 * max(sum(sb), 1)).from_address(send)) if sum(sb) else \
+                    np.zeros(0, np.uint8)
+                out = torch.empty(sum(rbytes), dtype=torch.uint8)
+                dist.all_to_all_single(out, torch.from_numpy(src[:sum(sb)].copy()), output_split_sizes=rbytes,
+                                       input_split_sizes=sb, group=group)
+                if sum(rbytes):
+                    C.memmove(recv, out.numpy().ctypes.data, sum(rbytes))
+                return 0
+            except Exception:  # noqa: BLE001 - reported to the library as a transport failure
+                return 1
+
+        fn = L.AllToAllvFn(a2av)
+        h = C.c_void_p()
+        ctx.check(ctx._lib.acc_comm_init_host(ctx.handle, world, rank, fn, None, C.byref(h)))
+        return cls(ctx, h, keep=fn)
+
+    def close(self):
+        if self.handle:
+            self.ctx._lib.acc_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def shard_reduce(ctx, comm: Comm, bi, n_global: int, txn_global=None):
+    """acc_shard_reduce: PreAccept.reduce of the last acc_keydeps_batch on ctx (batch `bi`) over `comm`; returns the
+    merge view of this rank's home txns. txn_global: u32 array (host or device, same placement as bi) or None."""
+    import ctypes as C
+    from . import _lib as L
+    ptr = None
+    if txn_global is not None:
+        ptr = txn_global.data_ptr() if hasattr(txn_global, "data_ptr") else np.ascontiguousarray(txn_global).ctypes.data
+    view = L.MergeView()
+    ctx.check(ctx._lib.acc_shard_reduce(ctx.handle, comm.handle, C.byref(bi), ptr, n_global, C.byref(view)))
+    return view

@@ -8,7 +8,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
 void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
 void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
-void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out);
+void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
 void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *view);
 void rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out);
@@ -165,7 +165,7 @@ int acc_shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
     if (!ctx) return ACC_E_ARG;
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
-        acc::shard_pack(ctx, in, out);
+        acc::shard_pack(ctx, in, out, false);
     });
 }
 

@@ -346,7 +346,9 @@ __global__ __launch_bounds__(BLOCK) void k_fuse_glb_sizes(uint32_t ng, Fuse f, u
 
 using namespace sh;
 
-void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
+// ctx_alloc: the four streams are allocated from the context (device) once their sizes are known and returned in
+// out->hdr/keys/vals/k2v (acc_shard_reduce); otherwise they are the caller's (two-call sizing).
+void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc)
 {
     if (!in || !out) fail(ACC_E_ARG, "null argument");
     const uint32_t world = out->world;
@@ -395,6 +397,14 @@ void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out)
     for (int q = 0; q < 4; ++q) memcpy(dst[q], hb.data() + q * (world + 1), (world + 1) * sizeof(uint64_t));
     const uint64_t F = hb[world], NK = hb[(world + 1) + world], NV = hb[2 * (world + 1) + world],
                    NO = hb[3 * (world + 1) + world];
+    if (ctx_alloc) {
+        out->mem = ACC_MEM_DEVICE;
+        out->hdr = ctx->get<uint32_t>("cm_s_hdr", 4 * F);
+        out->keys = ctx->get<uint64_t>("cm_s_keys", NK);
+        out->vals = ctx->get<uint32_t>("cm_s_vals", NV);
+        out->k2v = ctx->get<int32_t>("cm_s_k2v", NO);
+        out->cap_frag = F; out->cap_keys = NK; out->cap_vals = NV; out->cap_k2v = NO;
+    }
     if (out->cap_frag < F || out->cap_keys < NK || out->cap_vals < NV || out->cap_k2v < NO || (F && !out->hdr) ||
         (NK && !out->keys) || (NV && !out->vals) || (NO && !out->k2v))
         fail(ACC_E_CAP, "fragment stream capacity too small (offsets written)");

@@ -437,6 +437,28 @@ typedef struct acc_frag_recv {
 
 int acc_shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *out_view);
 
+/* ---- The exchange between CommandStores on different GPUs, behind the ABI ----
+ * acc_comm: a communicator of `world` ranks (one GPU and one acc_ctx each). Two transports:
+ *   RCCL (acc_comm_init_rccl): rank 0 makes an id with acc_comm_unique_id and the host distributes the 128 bytes
+ *     (any channel); device buffers move point to point over xGMI;
+ *   host (acc_comm_init_host): the caller's all-to-all(v) of host bytes (e.g. a JVM node's own messaging): fn gets
+ *     send[] with send_bytes[d] bytes for rank d (concatenated in rank order) and fills recv[] with recv_bytes[s]
+ *     bytes from each rank s; returns 0 on success.
+ * acc_shard_reduce: PreAccept.reduce of the store KeyDeps (messages/PreAccept.java:141-156, PartialDeps.with) for the
+ * last acc_keydeps_batch on ctx over `in` (the same batch): acc_shard_pack, one exchange of the element counts, one
+ * all-to-all(v) of the four fragment streams, acc_shard_merge; every rank calls it (collective). txn_global / n_global
+ * as acc_frag_streams.txn_global and the global txn count; the result is acc_shard_merge's view. */
+#define ACC_COMM_ID_BYTES 128
+typedef struct acc_comm acc_comm;
+typedef int (*acc_alltoallv_fn)(void *user, const void *send, const uint64_t *send_bytes, void *recv,
+                                const uint64_t *recv_bytes);
+int  acc_comm_unique_id(uint8_t *id_out);   /* [ACC_COMM_ID_BYTES]; ACC_E_DEVICE without RCCL */
+int  acc_comm_init_rccl(acc_ctx *ctx, uint32_t world, uint32_t rank, const uint8_t *id, acc_comm **out);
+int  acc_comm_init_host(acc_ctx *ctx, uint32_t world, uint32_t rank, acc_alltoallv_fn fn, void *user, acc_comm **out);
+void acc_comm_destroy(acc_comm *comm);
+int  acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
+                      acc_merge_view *out_view);
+
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
  * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).
