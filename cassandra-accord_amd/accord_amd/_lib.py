@@ -16,6 +16,18 @@ ACC_OK, ACC_E_ARG, ACC_E_STATE, ACC_E_NOMEM, ACC_E_DEVICE, ACC_E_CAP = 0, -1, -2
 ACC_MEM_HOST, ACC_MEM_DEVICE = 0, 1
 ACC_OPT_TIMING = 1
 ACC_OPT_FORCE_REPLAY = 2
+# SafeCommandStore.TestStartedAt / TestDep / TestStatus ordinals (local/SafeCommandStore.java:63-70)
+ACC_STARTED_BEFORE, ACC_STARTED_AFTER, ACC_STARTED_ANY = 0, 1, 2
+ACC_DEP_WITH, ACC_DEP_WITHOUT, ACC_DEP_ANY = 0, 1, 2
+ACC_STATUS_ANY, ACC_STATUS_IS_PROPOSED, ACC_STATUS_IS_STABLE = 0, 1, 2
+ACC_FULL_EXECUTES_AFTER = 1
+# the four BeginRecovery scans (messages/BeginRecovery.java:334-378): (started_at, test_dep, test_status, executes_after)
+RECOVERY_SCANS = {
+    "acceptedOrCommittedStartedBeforeWithoutWitnessing": (ACC_STARTED_BEFORE, ACC_DEP_WITHOUT, ACC_STATUS_IS_PROPOSED, True),
+    "stableStartedBeforeAndWitnessed": (ACC_STARTED_BEFORE, ACC_DEP_WITH, ACC_STATUS_IS_STABLE, False),
+    "hasAcceptedOrCommittedStartedAfterWithoutWitnessing": (ACC_STARTED_AFTER, ACC_DEP_WITHOUT, ACC_STATUS_IS_PROPOSED, False),
+    "hasStableExecutesAfterWithoutWitnessing": (ACC_STARTED_ANY, ACC_DEP_WITHOUT, ACC_STATUS_IS_STABLE, False),
+}
 
 u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)
@@ -27,7 +39,8 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_mixed", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
-           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce"]
+           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
+           "acc_map_reduce_full"]
 
 
 class Opts(C.Structure):
@@ -187,6 +200,13 @@ class StabView(C.Structure):
                 ("range_off", C.c_void_p), ("range_idx", C.c_void_p), ("txn_off", C.c_void_p), ("txn_idx", C.c_void_p)]
 
 
+class RecoveryIn(C.Structure):
+    _fields_ = [("n_query", C.c_uint32), ("mem", C.c_uint32), ("test_txn", TsCols), ("key_off", C.c_void_p),
+                ("key_code", C.c_void_p), ("missing_off", C.c_void_p), ("missing_txn", C.c_void_p),
+                ("n_missing", C.c_uint64), ("started_at", C.c_uint8), ("test_dep", C.c_uint8),
+                ("test_status", C.c_uint8), ("flags", C.c_uint8), ("test_kinds", C.c_int32)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -266,6 +286,8 @@ def load():
     L.acc_comm_destroy.restype = None
     L.acc_shard_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn), C.c_void_p, C.c_uint32, C.POINTER(MergeView)]
     L.acc_shard_reduce.restype = C.c_int
+    L.acc_map_reduce_full.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(RecoveryIn), C.POINTER(KeydepsView)]
+    L.acc_map_reduce_full.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
     L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]

@@ -179,6 +179,36 @@ class Context:
         view = self.keydeps_mixed_raw(self.range_batch_in(rb, keep))
         return self.copy_out(view, rb.keys)
 
+    def map_reduce_full(self, batch, missing_off, missing_txn, queries: dict, started_at: int, test_dep: int,
+                        test_status: int, test_kinds: int = -1, executes_after: bool = False) -> "BatchKeyDeps":
+        """SafeCommandStore.mapReduceFull (local/CommandsForKey.java:553-612 per key) for a batch of recovery queries
+        against the CommandsForKey snapshot `batch` (acc_map_reduce_full). queries = dict(msb, lsb, node, key_off,
+        key_code): the testTxnId and keys of each query; missing_off / missing_txn: per input pair of `batch`, the
+        entry's missing[] TxnIds as batch indices sorted by TxnId. Tests are TestStartedAt / TestDep / TestStatus
+        ordinals (ACC_STARTED_* / ACC_DEP_* / ACC_STATUS_*). Returns the per-query Deps.Builder KeyDeps."""
+        keep = []
+        a = dict(tm=np.ascontiguousarray(batch.txn_msb, dtype=np.uint64), tl=np.ascontiguousarray(batch.txn_lsb, dtype=np.uint64),
+                 tn=np.ascontiguousarray(batch.txn_node, dtype=np.int32), em=np.ascontiguousarray(batch.exe_msb, dtype=np.uint64),
+                 el=np.ascontiguousarray(batch.exe_lsb, dtype=np.uint64), en=np.ascontiguousarray(batch.exe_node, dtype=np.int32),
+                 st=np.ascontiguousarray(batch.status, dtype=np.uint8), ko=np.ascontiguousarray(batch.key_off, dtype=np.uint32),
+                 kc=np.ascontiguousarray(batch.key_code, dtype=np.uint64),
+                 mo=np.ascontiguousarray(missing_off, dtype=np.uint32), mt=np.ascontiguousarray(missing_txn, dtype=np.uint32),
+                 qm=np.ascontiguousarray(queries["msb"], dtype=np.uint64), ql=np.ascontiguousarray(queries["lsb"], dtype=np.uint64),
+                 qn=np.ascontiguousarray(queries["node"], dtype=np.int32),
+                 qo=np.ascontiguousarray(queries["key_off"], dtype=np.uint32),
+                 qk=np.ascontiguousarray(queries["key_code"], dtype=np.uint64))
+        keep.append(a)
+        p = lambda k: a[k].ctypes.data  # noqa: E731
+        n = int(a["st"].shape[0])
+        bi = L.BatchIn(n, L.ACC_MEM_HOST, int(a["ko"][-1]) if n else 0, L.TsCols(p("tm"), p("tl"), p("tn")),
+                       L.TsCols(p("em"), p("el"), p("en")), p("st"), p("ko"), p("kc"))
+        ri = L.RecoveryIn(len(a["qm"]), L.ACC_MEM_HOST, L.TsCols(p("qm"), p("ql"), p("qn")), p("qo"), p("qk"), p("mo"),
+                          p("mt"), len(a["mt"]), started_at, test_dep, test_status,
+                          L.ACC_FULL_EXECUTES_AFTER if executes_after else 0, test_kinds)
+        view = L.KeydepsView()
+        self.check(self._lib.acc_map_reduce_full(self._h, C.byref(bi), C.byref(ri), C.byref(view)))
+        return self.copy_out(view, None)
+
     def copy_out_range(self, view: "L.RangedepsView") -> "BatchRangeDeps":
         n = view.n_txn
         out = L.RangedepsOut()

@@ -32,4 +32,25 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
                      const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
                      const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out);
 
+// The CommandsForKey snapshot of a key batch (keydeps.hip stages 1-3) for the scans other than mapReduceActive: pairs
+// sorted by (key, TxnId rank) = one segment per key, entries in CommandsForKey.txns order. cfk = false when the batch has
+// no pairs. Device pointers owned by the context, valid until its next compute call.
+struct CfkSnapshot {
+    bool cfk = false;
+    uint32_t n = 0, nseg = 0;
+    size_t P = 0;
+    int rbits = 0;
+    const uint32_t *rank = nullptr;         // [2n] dictionary ranks (TxnIds, then executeAts)
+    const uint32_t *txn_of_rank = nullptr;  // TxnId rank -> batch index
+    const uint32_t *seg_start = nullptr;    // [nseg] first entry of each segment
+    const uint64_t *seg_key = nullptr;      // [nseg] key code of each segment, ascending
+    const uint32_t *s_rank = nullptr, *s_exec = nullptr;   // [P] TxnId / executeAt rank per entry
+    const uint8_t *s_info = nullptr;        // [P] status | kind << 3
+    const uint32_t *perm = nullptr;         // [P] entry -> input pair index
+    const uint64_t *tm = nullptr, *tl = nullptr, *em = nullptr, *el = nullptr;   // staged inputs
+    const int32_t *tn = nullptr, *en = nullptr;
+    const uint32_t *key_off = nullptr;
+};
+void cfk_snapshot(acc_ctx *ctx, const acc_batch_in *in, CfkSnapshot &out);
+
 }  // namespace acc

@@ -2354,6 +2354,8 @@ struct KdState {
     const uint32_t *pair_pos = nullptr, *perm = nullptr;
     const uint8_t *s_info = nullptr;
     const uint64_t *tl = nullptr, *key_code = nullptr;
+    const uint64_t *tm = nullptr, *em = nullptr, *el = nullptr;
+    const int32_t *tn = nullptr, *en = nullptr;
     uint64_t *g = nullptr;
     bool v1 = false;                  // the exact-replay columns below are built
     CfkView v1view{};
@@ -2591,7 +2593,8 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
     memcpy(out.hg, hg, sizeof hg);
 }
 
-static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view, KdState *ks)
+static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view, KdState *ks,
+                         bool cfk_only = false)
 {
     if (!in || !view) fail(ACC_E_ARG, "null argument");
     if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
@@ -2726,7 +2729,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ks->key_off = key_off; ks->owner = owner; ks->seg_incl = seg_incl; ks->seg_start = seg_start;
         ks->s_rank = s_rank; ks->s_exec = s_exec; ks->pair_pos = pair_pos; ks->perm = ps.vals; ks->s_info = s_info;
         ks->tl = tl; ks->key_code = key_code; ks->g = g;
+        ks->tm = tm; ks->tn = tn; ks->em = em; ks->el = el; ks->en = en;
     }
+    if (cfk_only) return;
     if (ties || (ctx->flags & ACC_OPT_FORCE_REPLAY)) {
         need_pair_pos();
         keydeps_v1_tail(ctx, view, n, P, rbits, tl, key_off, owner, rank, txn_of_rank, g, seg_incl, seg_start,
@@ -3549,6 +3554,30 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
                               o.dep_txn, o.kd_key };
     ctx->kd_view = *view;
     ctx->kd_valid = true;
+}
+
+// ---------------------------------------------------------------- CFK snapshot for the other scans (recovery.hip)
+
+void cfk_snapshot(acc_ctx *ctx, const acc_batch_in *in, CfkSnapshot &out)
+{
+    acc_keydeps_view kv{};
+    KdState ks;
+    keydeps_core(ctx, in, &kv, &ks, true);
+    ctx->kd_valid = false;
+    out = CfkSnapshot{};
+    out.n = in->n_txn;
+    out.P = (size_t)in->n_pairs;
+    if (!ks.cfk) return;
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, ks.seg_incl + ks.P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    const uint32_t nseg = (uint32_t)(ctx->pinned[0] & 0xFFFFFFFFu);   // seg_incl = inclusive count of segment starts
+    uint64_t *seg_key = ctx->get<uint64_t>("snap_seg_key", nseg);
+    launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
+           ks.key_code, seg_key);
+    out.cfk = true; out.nseg = nseg; out.rbits = ks.rbits; out.rank = ks.rank; out.txn_of_rank = ks.txn_of_rank;
+    out.seg_start = ks.seg_start; out.seg_key = seg_key; out.s_rank = ks.s_rank; out.s_exec = ks.s_exec;
+    out.s_info = ks.s_info; out.perm = ks.perm; out.tm = ks.tm; out.tl = ks.tl; out.tn = ks.tn; out.em = ks.em;
+    out.el = ks.el; out.en = ks.en; out.key_off = ks.key_off;
 }
 
 }  // namespace acc

@@ -25,6 +25,12 @@
  *   acc_shard_merge        messages/PreAccept.java:141-156, CommandStores.mapReduce local/CommandStores.java:575-592):
  *                          fragments to the txn's home GPU (all-to-all(v) by the host over RCCL), then KeyDeps.with
  *                          folded in shard order = the batched KeyDeps.merge below.
+ *   acc_map_reduce_full    the recovery scans of BeginRecovery        messages/BeginRecovery.java:334-378
+ *                          -> SafeCommandStore.mapReduceFull          local/SafeCommandStore.java:285
+ *                          -> InMemorySafeStore.mapReduceFull         impl/InMemoryCommandStore.java:874-881 (key part)
+ *                          -> CommandsForKey.mapReduceFull            local/CommandsForKey.java:553-612
+ *                          -> Deps.Builder                            primitives/Deps.java:46-96
+ *                          for a batch of recovery queries against one CommandsForKey snapshot.
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -458,6 +464,50 @@ int  acc_comm_init_host(acc_ctx *ctx, uint32_t world, uint32_t rank, acc_alltoal
 void acc_comm_destroy(acc_comm *comm);
 int  acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
                       acc_merge_view *out_view);
+
+/* ---- Recovery scans: CommandsForKey.mapReduceFull over a batch of queries (SURVEY.md §8(f) N3 = A7) ----
+ * The snapshot is an acc_batch_in (one CommandsForKey per key, as for acc_keydeps_batch) plus, per input pair j
+ * (txn t, key k), the entry's TxnInfoWithMissing.missing (local/CommandsForKey.java:385-410): the TxnIds of that CFK
+ * the txn's deps do not include, as batch indices sorted by TxnId, missing_txn[missing_off[j] .. missing_off[j+1]).
+ * Every query q is one (testTxnId, keys) call of SafeCommandStore.mapReduceFull with the call-wide tests:
+ *   started_at  TestStartedAt ordinal: 0 STARTED_BEFORE (txnId < testTxnId), 1 STARTED_AFTER (from the binarySearch
+ *               insert position, testTxnId itself included when it is on the key), 2 ANY
+ *   test_dep    TestDep ordinal: 0 WITH, 1 WITHOUT (testTxnId absent / present in missing), 2 ANY_DEPS; WITH and
+ *               WITHOUT also need InternalStatus.hasInfo and executeAt > testTxnId; WITH skips keys where testTxnId
+ *               is no CFK member
+ *   test_status TestStatus ordinal: 0 ANY_STATUS (not TRANSITIVELY_KNOWN), 1 IS_PROPOSED (ACCEPTED, COMMITTED),
+ *               2 IS_STABLE (STABLE, APPLIED)
+ *   test_kinds  Kinds as a mask over Kind ordinals, or -1 for testTxnId.kind().witnessedBy() (Txn.java:247-262)
+ *   flags       ACC_FULL_EXECUTES_AFTER: the map keeps only executeAt > testTxnId (BeginRecovery.java:339-341)
+ * The result per query is the Deps.Builder KeyDeps of every (key, txnId) the map visited, in the acc_keydeps_view
+ * layout (key_idx into the query's keys, dep_txn = batch indices); the boolean recovery predicates
+ * (hasAcceptedOrCommittedStartedAfterWithoutWitnessing, hasStableExecutesAfterWithoutWitnessing) are
+ * u_off[q+1] > u_off[q]. acc_keydeps_copy_out copies it. Range commands are not part of the snapshot. */
+#define ACC_STARTED_BEFORE 0
+#define ACC_STARTED_AFTER  1
+#define ACC_STARTED_ANY    2
+#define ACC_DEP_WITH       0
+#define ACC_DEP_WITHOUT    1
+#define ACC_DEP_ANY        2
+#define ACC_STATUS_ANY         0
+#define ACC_STATUS_IS_PROPOSED 1
+#define ACC_STATUS_IS_STABLE   2
+#define ACC_FULL_EXECUTES_AFTER 1u
+
+typedef struct acc_recovery_in {
+    uint32_t    n_query;
+    uint32_t    mem;            /* placement of the query arrays and of missing_off / missing_txn */
+    acc_ts_cols test_txn;       /* [n_query] testTxnId of each query (any TxnId, batch member or not) */
+    const uint32_t *key_off;    /* [n_query+1] */
+    const uint64_t *key_code;   /* keys of each query, sorted unique (Keys) */
+    const uint32_t *missing_off;/* [n_pairs+1] of the snapshot */
+    const uint32_t *missing_txn;/* [n_missing] batch indices */
+    uint64_t    n_missing;
+    uint8_t     started_at, test_dep, test_status, flags;
+    int32_t     test_kinds;
+} acc_recovery_in;
+
+int acc_map_reduce_full(acc_ctx *ctx, const acc_batch_in *snapshot, const acc_recovery_in *q, acc_keydeps_view *out_view);
 
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order

@@ -1004,3 +1004,179 @@ void orc_rangedeps_free(orc_rangedeps_result *r)
     free(r->u_off); free(r->dep_txn);
     free(r);
 }
+
+/* ------------------------------------------------------------------ recovery scan (mapReduceFull) */
+
+/* Kind.witnessedBy() (Txn.java:247-262) as a Kinds mask; -1 where it throws (LocalOnly, invalid ordinals). */
+static int kind_witnessed_by(int kind)
+{
+    switch (kind) {
+    case K_EREAD:              return 0;                                                   /* Nothing */
+    case K_READ:               return (1 << K_WRITE) | (1 << K_SYNC) | (1 << K_XSYNC);     /* WsOrSyncPoints */
+    case K_WRITE:              return (int)KINDS_ANY_VISIBLE;                              /* AnyGloballyVisible */
+    case K_SYNC: case K_XSYNC: return 1 << K_XSYNC;                                        /* ExclusiveSyncPoints */
+    default:                   return -1;
+    }
+}
+
+/* java.util.Arrays.binarySearch over a TxnId-sorted list of batch indices: found? */
+static int txn_list_contains(const batch *B, const uint32_t *list, size_t nl, const ts *key)
+{
+    long low = 0, high = (long)nl - 1;
+    while (low <= high) {
+        long mid = (long)(((unsigned long)low + (unsigned long)high) >> 1);
+        int c = ts_cmp(&B->id[list[mid]], key);
+        if (c < 0) low = mid + 1;
+        else if (c > 0) high = mid - 1;
+        else return 1;
+    }
+    return 0;
+}
+
+/* CommandsForKey.mapReduceFull (CommandsForKey.java:553-612) for one key, feeding a Deps.Builder with the map
+ * functions of BeginRecovery (messages/BeginRecovery.java:334-378): every visited txn is added, or (exec_after) only
+ * those with executeAt > testTxnId. missing(t) = the TxnInfoWithMissing.missing of this CFK's entry for t. */
+static void cfk_map_reduce_full(const cfk *c, const batch *B, const ts *test, unsigned test_kinds, int started_at,
+                                int test_dep, int test_status, int exec_after, const uint32_t *miss_off,
+                                const uint32_t *miss_txn, builder *b)
+{
+    /* Arrays.binarySearch(txns, testTxnId) */
+    long low = 0, high = (long)c->ntxns - 1, found = -1;
+    while (low <= high) {
+        long mid = (long)(((unsigned long)low + (unsigned long)high) >> 1);
+        int cc = ts_cmp(&B->id[c->txns[mid]], test);
+        if (cc < 0) low = mid + 1;
+        else if (cc > 0) high = mid - 1;
+        else { found = mid; break; }
+    }
+    int is_known = found >= 0;
+    if (!is_known && test_dep == 0 /* WITH */) return;
+    long insert_pos = is_known ? found : low;
+    long start, end;
+    switch (started_at) {
+    case 0:  start = 0; end = insert_pos; break;                     /* STARTED_BEFORE */
+    case 1:  start = insert_pos; end = (long)c->ntxns; break;        /* STARTED_AFTER */
+    default: start = 0; end = (long)c->ntxns; break;                 /* ANY */
+    }
+    for (long i = start; i < end; ++i) {
+        int64_t t = c->txns[i];
+        int kind = ts_kind(&B->id[t]);
+        if (!((test_kinds >> kind) & 1u)) continue;
+        int s = B->status[t];
+        switch (test_status) {
+        case 1: if (s == ST_ACC || s == ST_COMMITTED) break; else continue;       /* IS_PROPOSED */
+        case 2: if (s >= ST_STABLE && s < ST_INVALID) break; else continue;       /* IS_STABLE */
+        default: if (s == ST_TK) continue; break;                                 /* ANY_STATUS */
+        }
+        const ts *ex = &B->ex[t];
+        if (test_dep != 2 /* ANY_DEPS */) {
+            int has_info = s >= ST_ACC && s <= ST_APPLIED;                         /* InternalStatus.hasInfo */
+            if (!has_info) continue;
+            if (ts_cmp(ex, test) <= 0) continue;
+            /* the pair (t, key) of this CFK: t's keys are sorted, so a binary search finds it */
+            uint32_t a = B->key_off[t], z = B->key_off[t + 1];
+            while (a < z) { uint32_t m = (a + z) / 2; if (B->key_code[m] < c->key) a = m + 1; else z = m; }
+            int has_as_dep = !txn_list_contains(B, miss_txn + miss_off[a], miss_off[a + 1] - miss_off[a], test);
+            if (has_as_dep != (test_dep == 0)) continue;
+        }
+        if (exec_after && ts_cmp(ex, test) <= 0) continue;
+        b_add(b, c->key, t);
+    }
+}
+
+orc_keydeps_result *orc_map_reduce_full(uint32_t n,
+                                        const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                        const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                        const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                        const uint32_t *miss_off, const uint32_t *miss_txn,
+                                        uint32_t nq, const uint64_t *qmsb, const uint64_t *qlsb, const int32_t *qnode,
+                                        const uint32_t *qkey_off, const uint64_t *qkey_code,
+                                        int started_at, int test_dep, int test_status, int test_kinds, int exec_after)
+{
+    orc_keydeps_result *R = calloc(1, sizeof *R);
+    double t0 = now_s();
+    err E = { 0, "" };
+    batch B = { n, malloc((n + 1) * sizeof(ts)), malloc((n + 1) * sizeof(ts)), status, key_off, key_code };
+    for (uint32_t i = 0; i < n; ++i) {
+        B.id[i] = (ts){ tmsb[i], tlsb[i], tnode[i] };
+        B.ex[i] = (ts){ emsb[i], elsb[i], enode[i] };
+        if (status[i] > ST_INVALID) set_err(&E, -1, "invalid InternalStatus ordinal");
+    }
+    uint64_t P = n ? key_off[n] : 0;
+    for (uint64_t j = 0; j < P && !E.code; ++j)
+        for (uint32_t x = miss_off[j]; x < miss_off[j + 1]; ++x) {
+            if (miss_txn[x] >= n) { set_err(&E, -1, "missing[] entry is not a batch txn"); break; }
+            if (x > miss_off[j] && ts_cmp(&B.id[miss_txn[x - 1]], &B.id[miss_txn[x]]) >= 0) {
+                set_err(&E, -1, "missing[] must be sorted unique by TxnId"); break;
+            }
+        }
+    int64_t *pidx = malloc((P + 1) * sizeof *pidx);
+    for (uint64_t j = 0; j < P; ++j) pidx[j] = (int64_t)j;
+    radix_sort_by_u64(pidx, P, key_code);
+    size_t ncfk = 0, nkeys = 0;
+    for (uint64_t s = 0; s < P; ++s) nkeys += s == 0 || key_code[pidx[s]] != key_code[pidx[s - 1]];
+    cfk *cfks = calloc(nkeys + 1, sizeof *cfks);
+    int64_t *owner = malloc((P + 1) * sizeof *owner);
+    for (uint32_t t = 0; t < n; ++t) for (uint32_t j = key_off[t]; j < key_off[t + 1]; ++j) owner[j] = t;
+    for (uint64_t s = 0; s < P; ) {
+        uint64_t e2 = s;
+        while (e2 < P && key_code[pidx[e2]] == key_code[pidx[s]]) ++e2;
+        cfk *c = &cfks[ncfk++];
+        c->key = key_code[pidx[s]];
+        c->ntxns = e2 - s;
+        c->txns = malloc(c->ntxns * sizeof *c->txns);
+        for (uint64_t q = s; q < e2; ++q) c->txns[q - s] = owner[pidx[q]];
+        cfk_init(c, &B);
+        s = e2;
+    }
+    R->build_s = now_s() - t0;
+    double t1 = now_s();
+    R->n_txn = nq;
+    R->arena_off = calloc(nq + 1, sizeof(uint64_t));
+    R->kd_off = calloc(nq + 1, sizeof(uint64_t));
+    R->u_off = calloc(nq + 1, sizeof(uint64_t));
+    ivec arena = { 0 }, kidx = { 0 }, deps = { 0 };
+    builder b; b_init(&b, &B);
+    for (uint32_t q = 0; q < nq && !E.code; ++q) {
+        R->arena_off[q] = arena.n; R->kd_off[q] = kidx.n; R->u_off[q] = deps.n;
+        ts test = { qmsb[q], qlsb[q], qnode[q] };
+        int kinds = test_kinds >= 0 ? test_kinds : kind_witnessed_by(ts_kind(&test));
+        if (kinds < 0) { set_err(&E, -2, "Kind.witnessedBy(): unhandled kind (AssertionError)"); break; }
+        for (uint32_t j = qkey_off[q] + 1; j < qkey_off[q + 1]; ++j)
+            if (qkey_code[j - 1] >= qkey_code[j]) set_err(&E, -1, "keys of a query must be sorted and unique");
+        b_reset(&b);
+        for (uint32_t j = qkey_off[q]; j < qkey_off[q + 1] && !E.code; ++j) {
+            size_t a = 0, z = ncfk;
+            while (a < z) { size_t m = (a + z) / 2; if (cfks[m].key < qkey_code[j]) a = m + 1; else z = m; }
+            if (a == ncfk || cfks[a].key != qkey_code[j]) continue;     /* no CommandsForKey for this key */
+            ++R->queried_pairs;
+            cfk_map_reduce_full(&cfks[a], &B, &test, (unsigned)kinds, started_at, test_dep, test_status, exec_after,
+                                miss_off, miss_txn, &b);
+        }
+        kdeps d; if (b_build(&b, &d, &E)) break;
+        for (size_t x = 0; x < d.nk2v; ++x) iv_push(&arena, d.k2v[x]);
+        for (size_t x = 0; x < d.nkeys; ++x) {
+            uint32_t a = qkey_off[q], z = qkey_off[q + 1];
+            while (a < z) { uint32_t m = (a + z) / 2; if (qkey_code[m] < d.keys[x]) a = m + 1; else z = m; }
+            iv_push(&kidx, (int64_t)(a - qkey_off[q]));
+        }
+        for (size_t x = 0; x < d.nvals; ++x) iv_push(&deps, d.vals[x]);
+        R->total_edges += d.nk2v - d.nkeys;
+        kd_free(&d);
+    }
+    R->arena_off[nq] = arena.n; R->kd_off[nq] = kidx.n; R->u_off[nq] = deps.n;
+    R->query_s = now_s() - t1;
+    R->arena = malloc((arena.n + 1) * sizeof(int32_t));
+    for (size_t x = 0; x < arena.n; ++x) R->arena[x] = (int32_t)arena.v[x];
+    R->key_idx = malloc((kidx.n + 1) * sizeof(uint32_t));
+    for (size_t x = 0; x < kidx.n; ++x) R->key_idx[x] = (uint32_t)kidx.v[x];
+    R->dep_txn = malloc((deps.n + 1) * sizeof(uint32_t));
+    for (size_t x = 0; x < deps.n; ++x) R->dep_txn[x] = (uint32_t)deps.v[x];
+    R->error = E.code;
+    snprintf(R->message, sizeof R->message, "%s", E.msg);
+    b_free(&b);
+    free(arena.v); free(kidx.v); free(deps.v);
+    for (size_t c = 0; c < ncfk; ++c) { free(cfks[c].txns); free(cfks[c].committed); }
+    free(cfks); free(pidx); free(owner); free(B.id); free(B.ex);
+    return R;
+}

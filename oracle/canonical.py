@@ -255,3 +255,78 @@ def keydeps_mixed(rb, query_lo=0, query_hi=None):
             k2v.extend(pos[d] for d in ds)
         out.append(([k for k, _ in per_key], union, k2v))
     return out
+
+
+# Kind.witnessedBy() (Txn.java:247-262): EphemeralRead -> Nothing, Read -> WsOrSyncPoints, Write ->
+# AnyGloballyVisible, SyncPoint / ExclusiveSyncPoint -> ExclusiveSyncPoints
+WITNESSED_BY = {2: set(), 0: {1, 3, 4}, 1: {0, 1, 3, 4}, 3: {4}, 4: {4}}
+
+
+def map_reduce_full(b, miss_off, miss_txn, queries, started_at, test_dep, test_status, test_kinds=None,
+                    exec_after=False):
+    """Recovery scans as sets (CommandsForKey.mapReduceFull, CommandsForKey.java:553-612): for query (X, keys) and key
+    k, the txns D on k with
+      * window: D < X (STARTED_BEFORE), D >= X (STARTED_AFTER, X itself included when it is on k), any (ANY); and when
+        X is not on k and test_dep is WITH, nothing;
+      * D.kind in X.kind.witnessedBy() (or the explicit mask);
+      * status: ACCEPTED/COMMITTED (IS_PROPOSED), STABLE/APPLIED (IS_STABLE), not TRANSITIVELY_KNOWN (ANY_STATUS);
+      * unless ANY_DEPS: D has info (ACCEPTED..APPLIED), D.executeAt > X, and (X not in D.missing on k) == WITH;
+      * exec_after: D.executeAt > X.
+    Returns per query (key_idx list, dep batch indices, keysToTxnIds) like keydeps_batch."""
+    n = b.n_txn
+    tid = [ts_key(b.txn_msb[i], b.txn_lsb[i], b.txn_node[i]) for i in range(n)]
+    tex = [ts_key(b.exe_msb[i], b.exe_lsb[i], b.exe_node[i]) for i in range(n)]
+    kinds = [kind_of(b.txn_lsb[i]) for i in range(n)]
+    status = [int(s) for s in b.status]
+    on_key: dict[int, dict[int, int]] = {}   # key -> {txn: pair index}
+    for t in range(n):
+        for j in range(int(b.key_off[t]), int(b.key_off[t + 1])):
+            on_key.setdefault(int(b.key_code[j]), {})[t] = j
+    out = []
+    for q in range(len(queries["msb"])):
+        X = ts_key(queries["msb"][q], queries["lsb"][q], queries["node"][q])
+        mask = WITNESSED_BY[kind_of(queries["lsb"][q])] if test_kinds is None else \
+            {k for k in range(8) if (test_kinds >> k) & 1}
+        per_key = []
+        keys = [int(x) for x in queries["key_code"][int(queries["key_off"][q]):int(queries["key_off"][q + 1])]]
+        for ki, k in enumerate(keys):
+            members = on_key.get(k, {})
+            known = any(tid[d] == X for d in members)
+            if not known and test_dep == 0:
+                continue
+            deps = []
+            for d, j in members.items():
+                if started_at == 0 and not tid[d] < X:
+                    continue
+                if started_at == 1 and not tid[d] >= X:
+                    continue
+                if kinds[d] not in mask:
+                    continue
+                s = status[d]
+                if test_status == 1 and s not in (3, 4):
+                    continue
+                if test_status == 2 and s not in (5, 6):
+                    continue
+                if test_status == 0 and s == 0:
+                    continue
+                if test_dep != 2:
+                    if s not in (3, 4, 5, 6) or not tex[d] > X:
+                        continue
+                    missing = {tid[int(m)] for m in miss_txn[int(miss_off[j]):int(miss_off[j + 1])]}
+                    if (X not in missing) != (test_dep == 0):
+                        continue
+                if exec_after and not tex[d] > X:
+                    continue
+                deps.append(d)
+            if deps:
+                per_key.append((ki, sorted(deps, key=lambda d: tid[d])))
+        union = sorted({d for _, ds in per_key for d in ds}, key=lambda d: tid[d])
+        pos = {d: i for i, d in enumerate(union)}
+        k2v, end = [], len(per_key)
+        for _, ds in per_key:
+            end += len(ds)
+            k2v.append(end)
+        for _, ds in per_key:
+            k2v.extend(pos[d] for d in ds)
+        out.append(([ki for ki, _ in per_key], union, k2v))
+    return out

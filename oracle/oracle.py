@@ -108,6 +108,10 @@ def lib():
         L.orc_rmm_stab.restype = C.POINTER(StabResult)
         L.orc_rmm_stab.argtypes = [C.c_uint32, u32p, u64p, u64p, C.c_int, C.c_int, u64p, u64p, u64p]
         L.orc_stab_free.argtypes = [C.POINTER(StabResult)]
+        L.orc_map_reduce_full.restype = C.POINTER(KeydepsResult)
+        L.orc_map_reduce_full.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u32p,
+                                          C.c_uint32, u64p, u64p, i32p, u32p, u64p,
+                                          C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
         L.orc_ts_compare.restype = C.c_int
         L.orc_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
@@ -192,6 +196,31 @@ def keydeps_mixed(rb, n_shards: int = 1, query_lo: int = 0, query_hi: int | None
     return _keydeps_out(L, r, n)
 
 
+def map_reduce_full(batch, miss_off, miss_txn, queries, started_at: int, test_dep: int, test_status: int,
+                    test_kinds: int = -1, exec_after: bool = False) -> KeyDepsBatchOut:
+    """orc_map_reduce_full: CommandsForKey.mapReduceFull (CommandsForKey.java:553-612) per key of each recovery query,
+    into a Deps.Builder (BeginRecovery.java:334-378). queries = dict(msb, lsb, node, key_off, key_code); results per
+    query in the acc_keydeps_view layout (dep_txn = batch indices)."""
+    L = lib()
+    n = batch.n_txn
+    nq = len(queries["msb"])
+    arrs = [np.ascontiguousarray(x) for x in (batch.txn_msb.astype(np.uint64), batch.txn_lsb.astype(np.uint64),
+                                              batch.txn_node.astype(np.int32), batch.exe_msb.astype(np.uint64),
+                                              batch.exe_lsb.astype(np.uint64), batch.exe_node.astype(np.int32),
+                                              batch.status.astype(np.uint8), batch.key_off.astype(np.uint32),
+                                              batch.key_code.astype(np.uint64), np.asarray(miss_off, np.uint32),
+                                              np.append(np.asarray(miss_txn, np.uint32), np.uint32(0)))]
+    types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u32p]
+    qa = [np.ascontiguousarray(np.append(np.asarray(queries[k], dt), dt(0))) if k != "key_off" else
+          np.ascontiguousarray(np.asarray(queries[k], dt))
+          for k, dt in (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("key_off", np.uint32),
+                        ("key_code", np.uint64))]
+    qt = [u64p, u64p, i32p, u32p, u64p]
+    r = L.orc_map_reduce_full(n, *[_p(a, t) for a, t in zip(arrs, types)], nq, *[_p(a, t) for a, t in zip(qa, qt)],
+                              started_at, test_dep, test_status, test_kinds, int(exec_after))
+    return _keydeps_out(L, r, nq)
+
+
 def _keydeps_out(L, r, n) -> KeyDepsBatchOut:
     try:
         R = r.contents
@@ -205,7 +234,8 @@ def _keydeps_out(L, r, n) -> KeyDepsBatchOut:
                               np.ctypeslib.as_array(R.key_idx, (max(nk, 1),))[:nk].copy(), u_off,
                               np.ctypeslib.as_array(R.dep_txn, (max(nd, 1),))[:nd].copy(),
                               int(R.total_edges), int(R.visited), int(R.queried_pairs), float(R.build_s),
-                              float(R.query_s), np.ctypeslib.as_array(R.kd_key, (max(nk, 1),))[:nk].copy())
+                              float(R.query_s),
+                              np.ctypeslib.as_array(R.kd_key, (max(nk, 1),))[:nk].copy() if R.kd_key else None)
     finally:
         L.orc_keydeps_free(r)
     return out
