@@ -21,6 +21,7 @@ ACC_STARTED_BEFORE, ACC_STARTED_AFTER, ACC_STARTED_ANY = 0, 1, 2
 ACC_DEP_WITH, ACC_DEP_WITHOUT, ACC_DEP_ANY = 0, 1, 2
 ACC_STATUS_ANY, ACC_STATUS_IS_PROPOSED, ACC_STATUS_IS_STABLE = 0, 1, 2
 ACC_FULL_EXECUTES_AFTER = 1
+ACC_LATEST_PROPOSAL, ACC_LATEST_COMMIT = 0, 1
 # the four BeginRecovery scans (messages/BeginRecovery.java:334-378): (started_at, test_dep, test_status, executes_after)
 RECOVERY_SCANS = {
     "acceptedOrCommittedStartedBeforeWithoutWitnessing": (ACC_STARTED_BEFORE, ACC_DEP_WITHOUT, ACC_STATUS_IS_PROPOSED, True),
@@ -40,7 +41,7 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
-           "acc_map_reduce_full"]
+           "acc_map_reduce_full", "acc_latest_deps_merge"]
 
 
 class Opts(C.Structure):
@@ -207,6 +208,19 @@ class RecoveryIn(C.Structure):
                 ("test_status", C.c_uint8), ("flags", C.c_uint8), ("test_kinds", C.c_int32)]
 
 
+class LatestIn(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("mode", C.c_uint32), ("grp_off", C.c_void_p), ("iv_off", C.c_void_p),
+                ("iv_start", C.c_void_p), ("iv_end", C.c_void_p), ("known", C.c_void_p), ("ballot", TsCols),
+                ("coord_deps", C.c_void_p), ("local_deps", C.c_void_p), ("txn_id", TsCols), ("execute_at", TsCols),
+                ("end_inclusive", C.c_uint32), ("deps_mem", C.c_uint32), ("n_deps", C.c_uint32),
+                ("key_deps", RmmIn), ("range_deps", RmmIn)]
+
+
+class LatestView(C.Structure):
+    _fields_ = [("deps", DepsMergeView), ("total_sufficient", C.c_uint64), ("sufficient_off", u64p),
+                ("sufficient_start", u64p), ("sufficient_end", u64p)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -288,6 +302,8 @@ def load():
     L.acc_shard_reduce.restype = C.c_int
     L.acc_map_reduce_full.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(RecoveryIn), C.POINTER(KeydepsView)]
     L.acc_map_reduce_full.restype = C.c_int
+    L.acc_latest_deps_merge.argtypes = [C.c_void_p, C.POINTER(LatestIn), C.POINTER(LatestView)]
+    L.acc_latest_deps_merge.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
     L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]

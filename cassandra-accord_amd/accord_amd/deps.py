@@ -583,3 +583,49 @@ def rangedeps_stab(ctx: Context, m: dict, grp, q_start, q_end=None, end_inclusiv
         out["txn_off"] = device_array(ctx, v.txn_off, n, np.uint64)
         out["txn_idx"] = device_array(ctx, v.txn_idx, v.total_txns, np.uint32)
     return out
+
+
+# ---------------------------------------------------------------- LatestDeps (recovery merge)
+
+def latest_deps_merge(ctx: Context, groups, key_objs: dict | None, range_objs: dict | None, end_inclusive: bool = True,
+                      commit: bool = False, txn_ids=None, execute_ats=None) -> dict:
+    """LatestDeps.mergeProposal / mergeCommit (primitives/LatestDeps.java:306-326) for every recovering txn
+    (acc_latest_deps_merge). groups[g] = the replies, each a list of intervals (start, end, KnownDeps ordinal,
+    ballot (msb, lsb, node), coordinatedDeps id, localDeps id) with ids into the deps objects (-1 = null); key_objs /
+    range_objs = the objects' halves in the Deps.merge layout (one slot per id). Returns dict(key=..., range=...,
+    sufficient=[[(start, end)...] per group])."""
+    keep = []
+    grp_off, iv_off = [0], [0]
+    cols = {k: [] for k in ("s", "e", "known", "bm", "bl", "bn", "cd", "ld")}
+    for replies in groups:
+        for ivs in replies:
+            for (s, e, known, ballot, cd, ld) in ivs:
+                for k, v in zip(("s", "e", "known", "bm", "bl", "bn", "cd", "ld"), (s, e, known, *ballot, cd, ld)):
+                    cols[k].append(v)
+            iv_off.append(len(cols["s"]))
+        grp_off.append(len(iv_off) - 1)
+    a = dict(grp=np.array(grp_off, np.uint32), ivo=np.array(iv_off, np.uint32), s=np.array(cols["s"], np.uint64),
+             e=np.array(cols["e"], np.uint64), known=np.array(cols["known"], np.uint8), bm=np.array(cols["bm"], np.uint64),
+             bl=np.array(cols["bl"], np.uint64), bn=np.array(cols["bn"], np.int32), cd=np.array(cols["cd"], np.int32),
+             ld=np.array(cols["ld"], np.int32))
+    ng = len(groups)
+    tid = [np.ascontiguousarray([t[i] for t in (txn_ids or [])] or [0], dtype=dt) for i, dt in
+           enumerate((np.uint64, np.uint64, np.int32))]
+    exe = [np.ascontiguousarray([t[i] for t in (execute_ats or [])] or [0], dtype=dt) for i, dt in
+           enumerate((np.uint64, np.uint64, np.int32))]
+    keep += [a, tid, exe]
+    p = lambda x: x.ctypes.data  # noqa: E731
+    nd = max(len(key_objs["key_off"]) - 1 if key_objs else 0, len(range_objs["key_off"]) - 1 if range_objs else 0)
+    li = L.LatestIn(ng, L.ACC_LATEST_COMMIT if commit else L.ACC_LATEST_PROPOSAL, p(a["grp"]), p(a["ivo"]), p(a["s"]),
+                    p(a["e"]), p(a["known"]), L.TsCols(p(a["bm"]), p(a["bl"]), p(a["bn"])), p(a["cd"]), p(a["ld"]),
+                    L.TsCols(*(p(x) for x in tid)), L.TsCols(*(p(x) for x in exe)), int(end_inclusive), L.ACC_MEM_HOST,
+                    nd, _rmm_in(key_objs, keep), _rmm_in(range_objs, keep))
+    v = L.LatestView()
+    ctx.check(ctx._lib.acc_latest_deps_merge(ctx.handle, C.byref(li), C.byref(v)))
+    ns = int(v.total_sufficient)
+    so = np.ctypeslib.as_array(v.sufficient_off, (ng + 1,)).copy() if ng else np.zeros(1, np.uint64)
+    ss = np.ctypeslib.as_array(v.sufficient_start, (ns,)).copy() if ns else np.zeros(0, np.uint64)
+    se = np.ctypeslib.as_array(v.sufficient_end, (ns,)).copy() if ns else np.zeros(0, np.uint64)
+    suff = [[(int(ss[x]), int(se[x])) for x in range(int(so[g]), int(so[g + 1]))] for g in range(ng)]
+    return dict(key=rmm_copy_out(ctx, ng, v.deps.key_deps, False), range=rmm_copy_out(ctx, ng, v.deps.range_deps, True),
+                sufficient=suff)

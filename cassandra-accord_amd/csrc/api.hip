@@ -15,6 +15,7 @@ void rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out);
 void rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out);
 void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q, acc_stab_view *out);
 void map_reduce_full(acc_ctx *ctx, const acc_batch_in *in, const acc_recovery_in *q, acc_keydeps_view *view);
+void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *view);
 }  // namespace acc
 
 extern "C" {
@@ -96,7 +97,19 @@ int acc_keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_vi
 int acc_map_reduce_full(acc_ctx *ctx, const acc_batch_in *snapshot, const acc_recovery_in *q, acc_keydeps_view *out_view)
 {
     if (!ctx) return ACC_E_ARG;
-    return acc_guard(ctx, [&] { acc::map_reduce_full(ctx, snapshot, q, out_view); });
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::map_reduce_full(ctx, snapshot, q, out_view);
+    });
+}
+
+int acc_latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::latest_deps_merge(ctx, in, out_view);
+    });
 }
 
 int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)

@@ -91,6 +91,8 @@ struct acc_ctx {
     bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;
+    // sufficientFor of the last acc_latest_deps_merge (host)
+    std::vector<uint64_t> latest_suff_off, latest_suff_s, latest_suff_e;
 
     // buffer-name namespace (NsScope): lets one call run a sub-pipeline twice (e.g. the KeyDeps and RangeDeps halves
     // of Deps.merge) without the second run overwriting the first one's results

@@ -31,6 +31,9 @@
  *                          -> CommandsForKey.mapReduceFull            local/CommandsForKey.java:553-612
  *                          -> Deps.Builder                            primitives/Deps.java:46-96
  *                          for a batch of recovery queries against one CommandsForKey snapshot.
+ *   acc_latest_deps_merge  LatestDeps.mergeProposal / mergeCommit     primitives/LatestDeps.java:306-326
+ *                          (Recover.java:295-355): the interval fold of the replies, then KeyDeps/RangeDeps.slice of
+ *                          every selected deps object to its interval and the batched Deps.merge of the slices.
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -508,6 +511,47 @@ typedef struct acc_recovery_in {
 } acc_recovery_in;
 
 int acc_map_reduce_full(acc_ctx *ctx, const acc_batch_in *snapshot, const acc_recovery_in *q, acc_keydeps_view *out_view);
+
+/* ---- Recovery merge of LatestDeps replies ----
+ * Group g = one recovering txn with replies [grp_off[g], grp_off[g+1]), each a LatestDeps (primitives/LatestDeps.java):
+ * reply r owns intervals [iv_off[r], iv_off[r+1]) = RoutingKey ranges [iv_start, iv_end) ascending and disjoint (gaps =
+ * null entries), each with a KnownDeps ordinal (local/Status.java:539-578: DepsUnknown 0, DepsProposed 1,
+ * DepsCommitted 2, DepsErased 3, DepsKnown 4, NoDeps 5), a Ballot and its coordinatedDeps / localDeps as ids of deps
+ * objects (-1 = null). Ids stand for Java object identity: MergeBuilder.tryMergeEqual compares deps by reference
+ * (LatestDeps.java:420-435), so equal ids must mean the same object. Deps object d = key_deps / range_deps reply slot d
+ * in the acc_rmm_in layout of Deps.merge (n_deps slots). The interval descriptors are host arrays; the deps arrays are in
+ * deps_mem. mode ACC_LATEST_PROPOSAL = mergeProposal (:350-358), ACC_LATEST_COMMIT = mergeCommit(txn_id[g],
+ * execute_at[g]) (:360-369), which also yields sufficientFor. Ranges are end_inclusive (s, e] or [s, e). */
+#define ACC_LATEST_PROPOSAL 0u
+#define ACC_LATEST_COMMIT   1u
+typedef struct acc_latest_in {
+    uint32_t n_groups;
+    uint32_t mode;
+    const uint32_t *grp_off;          /* [n_groups+1] */
+    const uint32_t *iv_off;           /* [n_replies+1] */
+    const uint64_t *iv_start, *iv_end;
+    const uint8_t  *known;
+    acc_ts_cols     ballot;
+    const int32_t  *coord_deps;       /* coordinatedDeps id per interval, -1 = null */
+    const int32_t  *local_deps;       /* localDeps id per interval, -1 = null */
+    acc_ts_cols     txn_id, execute_at;   /* [n_groups], ACC_LATEST_COMMIT only */
+    uint32_t        end_inclusive;
+    uint32_t        deps_mem;
+    uint32_t        n_deps;
+    acc_rmm_in      key_deps, range_deps;
+} acc_latest_in;
+
+/* deps: per group the merged Deps (device views as acc_deps_merge, copied with acc_rmm_copy_out); sufficientFor per group
+ * (mergeCommit): ranges sufficient_start/end[sufficient_off[g] .. sufficient_off[g+1]), HOST pointers owned by the
+ * context, valid until its next call. */
+typedef struct acc_latest_view {
+    acc_deps_merge_view deps;
+    uint64_t        total_sufficient;
+    const uint64_t *sufficient_off;
+    const uint64_t *sufficient_start, *sufficient_end;
+} acc_latest_view;
+
+int acc_latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *out_view);
 
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order

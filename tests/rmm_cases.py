@@ -51,9 +51,35 @@ def flip_bits(rng, t, p):
     return (msb, lsb, node)
 
 
-def random_keys(rng, n, is_range, wide, nemesis=False, identical=False, span=1000):
-    """n distinct keys: u64 codes, or ranges (start < end) sorted by Range::compare (start, end)."""
+def int_hash_key(key: int) -> int:
+    """IntHashKey.hash (tst/impl/IntHashKey.java:255-263): CRC32 over update(key), update(key >> 8), update(key >> 16),
+    update(key >> 24) (CRC32.update(int) takes the low byte), masked to 16 bits. IntHashKey.compareTo orders by this
+    hash alone (:275-279), so it is the key's order-preserving code and keys with equal hashes compare equal."""
+    import zlib
+    k = key & 0xFFFFFFFF
+    return zlib.crc32(bytes([k & 0xFF, (k >> 8) & 0xFF, (k >> 16) & 0xFF, (k >> 24) & 0xFF])) & 0xFFFF
+
+
+def int_hash_collisions(limit=1 << 17):
+    """pairs (a, b), a < b < limit, of ints whose IntHashKey hashes are equal"""
+    seen, out = {}, []
+    for k in range(limit):
+        h = int_hash_key(k)
+        if h in seen:
+            out.append((seen[h], k))
+        else:
+            seen[h] = k
+    return out
+
+
+def random_keys(rng, n, is_range, wide, nemesis=False, identical=False, span=1000, inthash=False):
+    """n distinct keys: u64 codes, or ranges (start < end) sorted by Range::compare (start, end). inthash: KeyDepsTest's
+    IntHashKey.key(random.nextInt(keyRange)) codes (distinct by compareTo, i.e. by hash)."""
     keys = set()
+    if inthash and not is_range:
+        while len(keys) < n:
+            keys.add(int_hash_key(int(rng.integers(0, max(span, n + 10)))))
+        return sorted(keys)
     hi = (1 << 64) - 1 if wide else span
     while len(keys) < n:
         if not is_range:
@@ -104,14 +130,15 @@ def build_half(replies, is_range):
 
 
 def gen_groups(seed, n_groups, replies, is_range=False, n_keys=12, n_txn=30, p_drop=0.3, p_flip=0.0, p_empty=0.1,
-               p_extra=0.1, p_keyonly=0.05, wide=False, nemesis=False, identical=False, max_replies=None, counts=None):
+               p_extra=0.1, p_keyonly=0.05, wide=False, nemesis=False, identical=False, max_replies=None, counts=None,
+               inthash=False):
     """Groups of replies, each reply a random sub-relation of the group's truth relation (+ unreferenced TxnIds, keys
     without entries, empty replies, raw-bit flips of equal TxnIds). Returns (grp_off, half)."""
     rng = np.random.default_rng(seed)
     grp_off, reps = [0], []
     for _ in range(n_groups):
         pool = txn_pool(rng, n_txn, wide=wide, domain=1 if is_range else 0)
-        keys = random_keys(rng, n_keys, is_range, wide, nemesis, identical)
+        keys = random_keys(rng, n_keys, is_range, wide, nemesis, identical, inthash=inthash)
         truth = {i: sorted(rng.choice(n_txn, size=int(rng.integers(1, min(n_txn, 8) + 1)), replace=False).tolist())
                  for i in range(len(keys))}
         nr = replies if max_replies is None else int(rng.integers(1, max_replies + 1))

@@ -51,6 +51,16 @@ def test_deps_merge_both_halves(ctx, seed, kw):
     check_half(out["range"], grp_off, rh, True)
 
 
+def test_keydeps_merge_inthash_keys(ctx):
+    """KeyDepsTest.Deps.generate key space (tst/primitives/KeyDepsTest.java:315-374): IntHashKey.key(nextInt(keyRange))
+    ordered by its 16-bit CRC32 hash only (tst/impl/IntHashKey.java:255-279), TxnIds (epoch < 3, hlc < 500, node < 4)."""
+    from accord_amd.deps import deps_merge
+    for seed in (41, 42, 43):
+        grp_off, kh = RC.gen_groups(seed, 25, 12, is_range=False, n_keys=150, n_txn=200, inthash=True, p_flip=0.1)
+        out = deps_merge(ctx, dict(grp_off=grp_off, key=kh))
+        check_half(out["key"], grp_off, kh, False)
+
+
 @pytest.mark.parametrize("gen", ["nemesis", "identical"])
 def test_rangedeps_merge_reference_generators(ctx, gen):
     """RangeDepsTest.generateNemesisRanges / generateIdenticalTxns shapes (tst/primitives/RangeDepsTest.java:166-192):

@@ -66,6 +66,38 @@ def test_config1_golden(ctx):
             np.testing.assert_array_equal(getattr(g, k), z["out_" + k], err_msg=f"{name} {k}")
 
 
+def inthash_batch(b, key_ints):
+    """The batch with IntHashKey keys: each pair's int key -> its 16-bit hash code (IntHashKey.compareTo orders by the
+    hash alone, tst/impl/IntHashKey.java:275-279); a txn's Keys are sorted unique by that order, so keys of one txn
+    whose hashes collide collapse to one (Keys.of dedups by compareTo)."""
+    import rmm_cases as RC
+    codes = np.array([RC.int_hash_key(int(k)) for k in key_ints], np.uint64)
+    off, kc = [0], []
+    for t in range(b.n_txn):
+        ks = sorted(set(int(x) for x in codes[int(b.key_off[t]):int(b.key_off[t + 1])]))
+        kc.extend(ks)
+        off.append(len(kc))
+    return W.Batch(b.txn_msb, b.txn_lsb, b.txn_node, b.exe_msb, b.exe_lsb, b.exe_node, b.status,
+                   np.array(off, np.uint32), np.array(kc, np.uint64))
+
+
+def test_inthash_keys(ctx):
+    """IntHashKey key space (KeyDepsTest's key type): codes are 16-bit hashes, so distinct int keys with colliding
+    hashes share one CommandsForKey, and key order is hash order, not int order."""
+    import oracle
+    import rmm_cases as RC
+    rng = np.random.default_rng(9)
+    b = W.keydeps_batch(4000, 4, 1000, 0x4A5, "uniform", status_model="model", window=900)
+    pairs = RC.int_hash_collisions(1 << 17)[:200]
+    pool = np.array([k for p in pairs for k in p] + list(rng.integers(0, 1 << 20, size=600)), np.int64)
+    key_ints = pool[rng.integers(0, len(pool), size=b.n_pairs)]
+    hb = inthash_batch(b, key_ints)
+    g = ctx.calculate_partial_deps(hb)
+    o = oracle.keydeps_batch(hb)
+    assert_same(g, o, hb.n_txn, "inthash")
+    assert g.total_edges > 0
+
+
 def test_zipf_hot_keys(ctx):
     """Skewed keys (hot CFK segments) with the status model; multi-pass rank and pair sorts."""
     import oracle

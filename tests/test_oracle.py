@@ -151,3 +151,19 @@ def test_workload_is_deterministic():
         np.testing.assert_array_equal(v, b.arrays()[k])
     kc = a.key_code.reshape(-1, 8)
     assert (np.diff(kc.astype(np.int64), axis=1) > 0).all()
+
+
+def test_oracle_matches_canonical_inthash_keys():
+    """IntHashKey codes (KeyDepsTest's key type, ordered by a 16-bit CRC32 hash, tst/impl/IntHashKey.java:255-279) with
+    colliding int keys sharing one CommandsForKey."""
+    import rmm_cases as RC
+    from test_keydeps_gpu import inthash_batch
+    rng = np.random.default_rng(3)
+    b = W.keydeps_batch(600, 4, 200, 0x4A6, "uniform", status_model="model", window=300)
+    pairs = RC.int_hash_collisions(1 << 17)[:40]
+    pool = np.array([k for p in pairs for k in p] + list(rng.integers(0, 1 << 20, size=60)), np.int64)
+    hb = inthash_batch(b, pool[rng.integers(0, len(pool), size=b.n_pairs)])
+    o = oracle.keydeps_batch(hb)
+    c = canonical.keydeps_batch(hb)
+    for t in range(hb.n_txn):
+        assert same_txn(o, c, t), t

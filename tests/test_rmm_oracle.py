@@ -15,6 +15,7 @@ import rmm_cases as RC
     (5, dict(identical=True, p_flip=0.2)),
     (6, dict(p_empty=0.6, p_keyonly=0.4)),
     (7, dict(max_replies=9, n_keys=3, n_txn=6)),
+    (8, dict(inthash=True, n_keys=40, p_flip=0.2)),
 ])
 def test_merge_oracle_is_canonical_union(is_range, seed, kw):
     """KeyDeps.merge / RangeDeps.merge == canonical union (KeyDepsTest.testMergedProperty :275-283) over raw TxnIds."""
