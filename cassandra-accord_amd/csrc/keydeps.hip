@@ -1738,29 +1738,42 @@ constexpr int ST_K = 16;                      // keys of a stream txn
 constexpr int ST_N2 = 128;                    // dependency entries of a stream txn (LDS sort buffer, power of two)
 constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream txn
 
-// Big-txn classification, ST_G lanes per txn: more than ST_K keys, or (txns with a run record only: bigflag = 1 from
-// the count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
+// Per txn, ST_G lanes: its KeyDeps sizes A = Kd + E (arena ints) and K = Kd (keys with >= 1 dependency) from the
+// count-pass records' word 15 (the exclusive scans of A and K are the txns' arena / key offsets, so the stream pass needs
+// no look-back), and the big-txn classification: more than ST_K keys, or (txns with a run record: bigflag = 1 from the
+// count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
 __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *__restrict__ key_off,
                                                    const uint32_t *__restrict__ rec32, uint32_t raw_cap, uint32_t e_cap,
-                                                   uint32_t *__restrict__ bigflag)
+                                                   uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
+                                                   uint64_t *__restrict__ szK)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / ST_G, sub = threadIdx.x & (ST_G - 1);
-    if (t >= n) return;
+    if (t >= n) return;   // group-uniform: shuffles stay inside the group
     const uint32_t j0 = key_off[t], nk = key_off[t + 1] - j0;
-    bool big = nk > (uint32_t)ST_K;
-    if (!big && bigflag[t]) {   // group-uniform branch: shuffles stay inside the group
-        uint32_t e = 0, raw = 0;
-        if (sub < nk) {
-            const uint32_t *r = rec32 + 16 * (size_t)(j0 + sub);
+    const bool run_rec = bigflag[t] != 0;
+    uint32_t e = 0, kd = 0, raw = 0;
+    for (uint32_t c0 = 0; c0 < nk; c0 += ST_G) {
+        if (c0 + sub < nk) {
+            const uint32_t *r = rec32 + 16 * (size_t)(j0 + c0 + sub);
             const uint32_t w = r[15];
-            if (w & REC_INLINE_FLAG) { e = w & ~REC_INLINE_FLAG; raw = 0; }
-            else { e = w; raw = r[6] + r[7] + r[8] + r[9] + r[10] + r[11] + r[13]; }
+            const uint32_t ej = w & ~REC_INLINE_FLAG;
+            e += ej;
+            kd += ej != 0;
+            if (run_rec && !(w & REC_INLINE_FLAG)) raw += r[6] + r[7] + r[8] + r[9] + r[10] + r[11] + r[13];
         }
-#pragma unroll
-        for (int d = 1; d < ST_G; d <<= 1) { e += __shfl_xor(e, d, 64); raw += __shfl_xor(raw, d, 64); }
-        big = e > e_cap || raw > raw_cap;
     }
-    if (sub == 0) bigflag[t] = big ? 1u : 0u;
+#pragma unroll
+    for (int d = 1; d < ST_G; d <<= 1) {
+        e += __shfl_xor(e, d, 64);
+        kd += __shfl_xor(kd, d, 64);
+        raw += __shfl_xor(raw, d, 64);
+    }
+    const bool big = nk > (uint32_t)ST_K || (run_rec && (e > e_cap || raw > raw_cap));
+    if (sub == 0) {
+        bigflag[t] = big ? 1u : 0u;
+        szA[t] = (uint64_t)kd + e;
+        szK[t] = kd;
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t *__restrict__ bigflag,
@@ -1885,75 +1898,13 @@ struct V3Stream {
     const uint32_t *key_off, *bigflag, *txn_of_rank;
     const uint4 *rec;
     const uint64_t *bK, *bE;                  // sizes of the big txns
-    uint64_t *arena_off, *kd_off, *u_cnt_out;
+    const uint64_t *arena_off, *kd_off;       // from the size scans
+    uint64_t *u_cnt_out;
     int32_t *arena;
     uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's entry offset, compacted by k_v3_ucompact
-    uint64_t *status;                         // 2 x ntiles look-back words: arena, keys
-    uint32_t *ticket;
     uint64_t *err;                            // gather count mismatches
     uint32_t n, ntiles;
 };
-
-// exclusive prefixes of tile b for NC chains (status words [q * ntiles + tile]) from the look-back over the tiles < b:
-// one full wave, LB_U words per lane and chain in flight (a window of 64 * LB_U tiles per round: the inclusive frontier
-// advances by up to a window per round trip, so small tiles need a wide window); each chain stops at its own nearest
-// inclusive word.
-constexpr int LB_U = 4;
-
-template <int NC>
-__device__ __forceinline__ void lookback_n(const uint64_t *status, uint32_t ntiles, uint32_t b, uint64_t (&pre)[NC])
-{
-    const uint32_t lane = lane_id();
-    bool done[NC];
-#pragma unroll
-    for (int q = 0; q < NC; ++q) { pre[q] = 0; done[q] = false; }
-    int64_t j = (int64_t)b - 1;
-    while (true) {
-        bool all = true;
-#pragma unroll
-        for (int q = 0; q < NC; ++q) all = all && done[q];
-        if (all) break;
-        uint64_t w[NC][LB_U];
-#pragma unroll
-        for (int q = 0; q < NC; ++q)
-#pragma unroll
-            for (int u = 0; u < LB_U; ++u) {
-                const int64_t idx = j - (int64_t)lane - 64 * u;
-                w[q][u] = (done[q] || idx < 0) ? SCAN_INC : scan_status_load(&status[(size_t)q * ntiles + idx]);
-            }
-        while (true) {
-            bool wait = false;
-#pragma unroll
-            for (int q = 0; q < NC; ++q)
-#pragma unroll
-                for (int u = 0; u < LB_U; ++u) wait = wait || (w[q][u] >> 62) == 0;
-            if (!wait) break;
-            __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int q = 0; q < NC; ++q)
-#pragma unroll
-                for (int u = 0; u < LB_U; ++u)
-                    if ((w[q][u] >> 62) == 0) w[q][u] = scan_status_load(&status[(size_t)q * ntiles + (j - (int64_t)lane - 64 * u)]);
-        }
-#pragma unroll
-        for (int q = 0; q < NC; ++q) {
-            if (done[q]) continue;
-            uint64_t x = 0;
-#pragma unroll
-            for (int u = 0; u < LB_U; ++u) {
-                if (done[q]) break;
-                const uint64_t inc = __ballot((w[q][u] >> 62) == 2);
-                const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;
-                x += lane <= stop ? (w[q][u] & SCAN_VAL) : 0ull;
-                if (inc) done[q] = true;
-            }
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) x += shfl_xor(x, d);
-            pre[q] += x;
-        }
-        j -= 64 * LB_U;
-    }
-}
 
 // inclusive prefix over the ST_G lanes of a group
 __device__ __forceinline__ uint32_t group_inclusive(uint32_t x, uint32_t sub)
@@ -2024,7 +1975,7 @@ __device__ unsigned long long *g_st_prof;
 
 // EntT: u32 (rank << 4 | key) when ranks fit 28 bits, else u64
 template <class EntT, int NT>
-__global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
+__global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
 {
     constexpr int TT = NT / ST_G;   // txns per tile
 #ifdef ACC_PHASE_PROF
@@ -2035,28 +1986,28 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     __shared__ uint32_t kc[TT][ST_K];
     __shared__ uint32_t kbase[TT][ST_K];
     __shared__ uint16_t stA[TT][ST_K + ST_N2];
-    __shared__ uint32_t s_tile;
     const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (ST_G - 1), grp = tid / ST_G, g0 = lane & (64 - ST_G);
     const uint64_t gmask = ((1ull << ST_G) - 1) << g0;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    // one ticket per block (launch-order independent), one look-back tile per wave: no block barrier after this one
-    if (tid == 0) s_tile = atomicAdd(s.ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile * (NT / 64) + (tid >> 6);   // wave tile: 64 / ST_G txns
+    // no block barriers: every wave is independent (its txns' arena / key offsets come from the size scans)
+    const uint32_t tile = blockIdx.x * (NT / 64) + (tid >> 6);   // wave tile: 64 / ST_G txns
     const uint32_t t = tile * (64 / ST_G) + (lane >> 4);
     const bool valid = t < s.n;
     TxnCtx c{};
     bool big = false;
+    uint64_t aoff = 0, koff = 0;
     if (valid) {
         c.t = t;
-        c.j0 = s.key_off[t]; c.j1 = s.key_off[t + 1]; c.nk = c.j1 - c.j0;
-        big = s.bigflag[t] != 0;
-        if (!big) {
-            const uint4 ti = s.v.tinfo[t];
-            c.trank = ti.x;
-            c.bq = ti.y != c.trank;
-            c.wk = witnesses(ti.z >> 3);
-        }
+        // independent loads issued together (the txn record is read even for big txns, which ignore it)
+        c.j0 = s.key_off[t]; c.j1 = s.key_off[t + 1];
+        const uint32_t bf = s.bigflag[t];
+        const uint4 ti = s.v.tinfo[t];
+        aoff = s.arena_off[t]; koff = s.kd_off[t];
+        c.nk = c.j1 - c.j0;
+        big = bf != 0;
+        c.trank = ti.x;
+        c.bq = ti.y != c.trank;
+        c.wk = witnesses(ti.z >> 3);
     }
     const bool sm = valid && !big;
     EntT *buf = ent[grp];
@@ -2082,18 +2033,7 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     const uint32_t E_in = __shfl(in_incl, (int)(g0 + ST_G - 1), 64);
     const uint64_t nzb = __ballot(e != 0) & gmask;
     const uint32_t Kd = (uint32_t)__popcll(nzb);
-    // ---- sizes (known from the count pass: A = Kd + E, K = Kd), tile aggregate published before the gather and sort
-    uint64_t A = 0, K = 0;
-    if (sm) { A = (uint64_t)Kd + E; K = Kd; }
-    else if (valid) { K = s.bK[t]; A = K + s.bE[t]; }
-    uint64_t excl[2] = { 0, 0 }, wtot[2] = { 0, 0 };
-#pragma unroll
-    for (int g = 0; g < 64 / ST_G; ++g) {
-        const uint64_t ag = shfl_idx(A, g * ST_G), kg = shfl_idx(K, g * ST_G);
-        if ((uint32_t)g < (lane >> 4)) { excl[0] += ag; excl[1] += kg; }
-        wtot[0] += ag; wtot[1] += kg;
-    }
-    if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (lane == 0 ? wtot[0] : wtot[1]) | (tile == 0 ? SCAN_INC : SCAN_AGG));
+    const uint64_t A = sm ? (uint64_t)Kd + E : 0;
     kbase[grp][sub] = e_incl - e;
     kc[grp][sub] = 0;
     if (sm && !run) {
@@ -2204,8 +2144,8 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     ST_PH(4);
-    // ---- KeyDeps in LDS, before the look-back (its wait hides the TxnId gathers): the arena (header ints and per-key
-    // TxnId indices) staged as u16; the distinct TxnIds go straight to the txn's fixed scratch slot t * ST_N2
+    // ---- KeyDeps in LDS: the arena (header ints and per-key TxnId indices) staged as u16; the distinct TxnIds go
+    // straight to the txn's fixed scratch slot t * ST_N2
     uint32_t distinct = 0;
     if (ok && e != 0) stA[grp][(uint32_t)__popcll(nzb & lt)] = (uint16_t)(Kd + e_incl);
     for (uint32_t q0 = 0; q0 < wE; q0 += ST_G) {
@@ -2236,18 +2176,8 @@ __global__ __launch_bounds__(NT) void k_v3_stream(V3Stream s)
     }
     if (ok && sub == 0) s.u_cnt_out[t] = distinct;
     ST_PH(5);
-    // ---- tile offsets: look-back (by now the previous tiles have mostly published inclusive prefixes)
-    uint64_t pre[2] = { 0, 0 };
-    if (tile != 0) {
-        lookback_n<2>(s.status, s.ntiles, tile, pre);
-        if (lane < 2) scan_status_store(&s.status[(size_t)lane * s.ntiles + tile], (lane == 0 ? pre[0] + wtot[0] : pre[1] + wtot[1]) | SCAN_INC);
-    }
+    // ---- the staged arena and key indices to their places
     if (!valid) return;
-    const uint64_t aoff = pre[0] + excl[0], koff = pre[1] + excl[1];
-    if (sub == 0) {
-        s.arena_off[t] = aoff; s.kd_off[t] = koff;
-        if (t + 1 == s.n) { s.arena_off[t + 1] = aoff + A; s.kd_off[t + 1] = koff + K; }
-    }
     if (ok) {
         for (uint32_t q = sub; q < (uint32_t)A; q += ST_G) s.arena[aoff + q] = (int32_t)stA[grp][q];
         if (e != 0) s.key_idx[koff + (uint32_t)__popcll(nzb & lt)] = sub;
@@ -2306,12 +2236,20 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
     const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
     if (c0 >= total) return;
     const uint64_t c1 = min(total, c0 + UC_CHUNK);
-    if (tid == 0) { s_t[0] = last_le(u_off, n, c0); s_t[1] = last_le(u_off, n, c1 - 1); }
-    __syncthreads();
-    const uint32_t tlo = s_t[0], thi = s_t[1];
-    for (uint32_t tw = tlo; tw <= thi; tw += BLOCK) {
-        const uint32_t nt = min((uint32_t)BLOCK, thi + 1 - tw);
+    if (tid == 0) s_t[1] = last_le(u_off, n, c1 - 1);
+    uint64_t pos = c0;
+    while (pos < c1) {
+        // the window starts at the txn holding output `pos` (runs of txns without TxnIds are jumped over, so sparse
+        // batches, e.g. the range txns of a mixed batch, cost nothing here)
         __syncthreads();
+        if (tid == 0) {
+            uint32_t lo = 0, hi = s_t[1] + 1;
+            while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (u_off[m] <= pos) lo = m; else hi = m; }
+            s_t[0] = lo;
+        }
+        __syncthreads();
+        const uint32_t tw = s_t[0], thi = s_t[1];
+        const uint32_t nt = min((uint32_t)BLOCK, thi + 1 - tw);
         if (tid < nt) {
             const uint32_t t = tw + tid;
             uo[tid] = u_off[t];
@@ -2319,12 +2257,13 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
         }
         if (tid == 0) uo[nt] = u_off[tw + nt];
         __syncthreads();
-        const uint64_t lo = max(c0, uo[0]), hi = min(c1, uo[nt]);
-        for (uint64_t i = lo + tid; i < hi; i += BLOCK) {
+        const uint64_t hi = min(c1, uo[nt]);
+        for (uint64_t i = pos + tid; i < hi; i += BLOCK) {
             const uint32_t a = last_le(uo, nt, i);
             const uint64_t sb = src[a], off = i - uo[a];
             dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
         }
+        pos = hi;
     }
 }
 
@@ -2775,7 +2714,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
     const char *ec_env = getenv("ACC_ST_ECAP");
     const uint32_t e_cap = ec_env ? std::min<uint32_t>((uint32_t)atoi(ec_env), ST_N2) : ST_N2;
-    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, raw_cap, e_cap, bigflag);
+    uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
+    uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
+    uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
+    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, raw_cap,
+           e_cap, bigflag, szA, szK);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, szA, arena_off, n, true, arena_off + n);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, szK, kd_off, n, true, kd_off + n);
     uint32_t *nbig_dev = reinterpret_cast<uint32_t *>(tot + 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, bigflag, bpos, n, true, nbig_dev);
     uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
@@ -2792,8 +2737,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     int32_t *arena = ctx->get<int32_t>("arena", P + E);
     uint32_t *key_idx = ctx->get<uint32_t>("key_idx", P);
     uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
-    uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
-    uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     uint64_t *bK = ctx->get<uint64_t>("v3_bK", n);
     uint64_t *bE = ctx->get<uint64_t>("v3_bE", n);
@@ -2859,16 +2802,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     if (rbits > 28 && st_nt > 512) st_nt = 512;
     const uint32_t tt = (uint32_t)st_nt / ST_G;
     const uint32_t nblocks = (n + tt - 1) / tt;
-    const uint32_t ntiles = nblocks * (uint32_t)(st_nt / 64);   // look-back tiles: one per wave
-    uint64_t *lb_status = ctx->get<uint64_t>("v3_status", 2 * (size_t)ntiles + 1);
-    uint32_t *ticket = reinterpret_cast<uint32_t *>(lb_status + 2 * (size_t)ntiles);
-    ACC_HIP(hipMemsetAsync(lb_status, 0, (2 * (size_t)ntiles + 1) * sizeof(uint64_t), st));
+    const uint32_t ntiles = nblocks * (uint32_t)(st_nt / 64);   // waves (phase-profile rows)
     uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);
     V3Stream sp;
     sp.v = vv; sp.err = gstat + 5;
     sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.bK = bK; sp.bE = bE;
     sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
-    sp.dep_scr = dep_st; sp.status = lb_status; sp.ticket = ticket; sp.n = n; sp.ntiles = ntiles;
+    sp.dep_scr = dep_st; sp.n = n; sp.ntiles = ntiles;
     auto stream = [&](auto ent_tag) {
         using EntT = decltype(ent_tag);
         if constexpr (sizeof(EntT) == 4) {
