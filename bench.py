@@ -403,6 +403,7 @@ def run_config4(args, world, rank, local, dev):
     }
     if os.environ.get("ACC_BENCH_MIXED", "1") != "0":
         result["keydeps_mixed"] = mixed_keydeps_leg(bi, local)
+        result["partial_deps"] = partial_deps_leg(bi, local)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = rangedeps_cpu_baseline(rb)
     return ctx, timing, elapsed, result
@@ -426,6 +427,27 @@ def mixed_keydeps_leg(bi, local, calls=3):
         top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:6]
         return {"ms_per_call": round(ms, 3), "range_key_queries": int(c.stats().get("keydeps.range_key_queries", 0)),
                 "dep_entries": int(v.total_edges), "kd_keys": int(v.total_keys),
+                "top_kernels_ms": {k: round(x[0] / calls, 3) for k, x in top}}
+
+
+def partial_deps_leg(bi, local, calls=3):
+    """The whole PartialDeps of the same mixed batch as ONE timed step (acc_partial_deps_batch: the KeyDeps half of
+    acc_keydeps_mixed and the RangeDeps half of acc_rangedeps_batch over one shared dictionary pass): 1 warmup +
+    `calls` timed calls on its own context."""
+    import torch
+    from accord_amd.deps import Context
+    with Context(local, timing=True) as c:
+        c.partial_deps_batch_raw(bi)
+        c.timing_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            kv, rv = c.partial_deps_batch_raw(bi)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1000.0 / calls
+        tm = c.timing()
+        top = sorted(tm.items(), key=lambda kv_: -kv_[1][0])[:8]
+        return {"ms_per_step": round(ms, 3), "key_dep_entries": int(kv.total_edges), "range_dep_entries": int(rv.total_edges),
                 "top_kernels_ms": {k: round(x[0] / calls, 3) for k, x in top}}
 
 

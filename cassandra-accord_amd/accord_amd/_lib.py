@@ -41,7 +41,7 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
-           "acc_map_reduce_full", "acc_latest_deps_merge"]
+           "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch"]
 
 
 class Opts(C.Structure):
@@ -268,6 +268,8 @@ def load():
     L.acc_keydeps_mixed.restype = C.c_int
     L.acc_rangedeps_batch.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(RangedepsView)]
     L.acc_rangedeps_batch.restype = C.c_int
+    L.acc_partial_deps_batch.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(KeydepsView), C.POINTER(RangedepsView)]
+    L.acc_partial_deps_batch.restype = C.c_int
     L.acc_rangedeps_copy_out.argtypes = [C.c_void_p, C.POINTER(RangedepsOut)]
     L.acc_rangedeps_copy_out.restype = C.c_int
     L.acc_shard_pack.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(FragStreams)]

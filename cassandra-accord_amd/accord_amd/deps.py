@@ -209,6 +209,18 @@ class Context:
         self.check(self._lib.acc_map_reduce_full(self._h, C.byref(bi), C.byref(ri), C.byref(view)))
         return self.copy_out(view, None)
 
+    def partial_deps_batch_raw(self, batch_in: "L.RangeBatchIn"):
+        kv, rv = L.KeydepsView(), L.RangedepsView()
+        self.check(self._lib.acc_partial_deps_batch(self._h, C.byref(batch_in), C.byref(kv), C.byref(rv)))
+        return kv, rv
+
+    def calculate_partial_deps_mixed(self, rb):
+        """The whole PartialDeps (KeyDeps, RangeDeps) of every txn of a mixed key/range batch in one call
+        (acc_partial_deps_batch): PreAccept.calculatePartialDeps through PartialDeps.Builder."""
+        keep = []
+        kv, rv = self.partial_deps_batch_raw(self.range_batch_in(rb, keep))
+        return self.copy_out(kv, rb.keys), self.copy_out_range(rv)
+
     def copy_out_range(self, view: "L.RangedepsView") -> "BatchRangeDeps":
         n = view.n_txn
         out = L.RangedepsOut()

@@ -1,13 +1,13 @@
 // api.hip — the extern "C" surface of include/accord_amd.h: context lifecycle, error text, result
 // copy-out with two-call sizing, and kernel timing read-out.
-#include "prims.hpp"
+#include "dict.hpp"
 
 namespace acc {
 void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view);
-void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view);
+void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view, SharedDict *shared = nullptr);
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
 void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
-void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view);
+void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view, const SharedDict *shared = nullptr);
 void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
 void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *view);
@@ -109,6 +109,20 @@ int acc_latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         acc::latest_deps_merge(ctx, in, out_view);
+    });
+}
+
+int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *key_view,
+                           acc_rangedeps_view *range_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        if (!key_view || !range_view) acc::fail(ACC_E_ARG, "null argument");
+        acc::SharedDict sd;
+        acc::keydeps_mixed(ctx, in, key_view, &sd);
+        acc::rangedeps_batch(ctx, in, range_view, &sd);
+        ctx->kd_valid = true;   // both views stay readable (distinct buffers)
     });
 }
 

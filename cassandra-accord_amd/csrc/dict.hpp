@@ -53,4 +53,12 @@ struct CfkSnapshot {
 };
 void cfk_snapshot(acc_ctx *ctx, const acc_batch_in *in, CfkSnapshot &out);
 
+// The dictionary of a batch computed by one half of PartialDeps, handed to the other (acc_partial_deps_batch): valid
+// when the KeyDeps half ran prep_dictionary (the batch has key pairs).
+struct SharedDict {
+    bool valid = false;
+    Dictionary dict;
+    const uint32_t *owner = nullptr;   // [P] txn of every key pair
+};
+
 }  // namespace acc

@@ -2296,6 +2296,8 @@ struct KdState {
     const uint64_t *tm = nullptr, *em = nullptr, *el = nullptr;
     const int32_t *tn = nullptr, *en = nullptr;
     uint64_t *g = nullptr;
+    bool have_dict = false;
+    Dictionary dict;
     bool v1 = false;                  // the exact-replay columns below are built
     CfkView v1view{};
 };
@@ -2574,6 +2576,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *owner = ctx->get<uint32_t>("owner", P);
     Dictionary dict;
     prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict);
+    if (ks) { ks->have_dict = true; ks->dict = dict; ks->owner = owner; }
     uint64_t hg[8];
     memcpy(hg, dict.hg, sizeof hg);
     const bool batch_sorted = dict.batch_sorted;
@@ -3305,7 +3308,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
     for (uint32_t i = sub; i < nx; i += 16) o.dep_txn[uo + i] = dep_scr[e0 + i];
 }
 
-void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view)
+void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view, SharedDict *shared)
 {
     if (!in || !view) fail(ACC_E_ARG, "null argument");
     if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
@@ -3322,6 +3325,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     KdState ks;
     keydeps_core(ctx, &kin, &kv, &ks);
     ctx->kd_valid = false;
+    if (shared) { shared->valid = ks.have_dict; shared->dict = ks.dict; shared->owner = ks.owner; }
     if (n == 0) {
         kv.kd_key = ctx->get<uint64_t>("mx_kd_key", 1);
         *view = kv;

@@ -706,7 +706,7 @@ static void rd_check_errors(uint64_t errs)
     if (errs & ERR_RNG_OFF) fail(ACC_E_ARG, "rng_off must be non-decreasing");
 }
 
-void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view)
+void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_view *view, const SharedDict *shared)
 {
     if (!in || !view) fail(ACC_E_ARG, "null argument");
     if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
@@ -748,10 +748,20 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     const uint64_t *re = stage_in(ctx, "in_rng_end", in->rng_end, R, in->mem);
 
     // ---- 1. prep + dictionary (also validates keys, statuses, kinds, TxnId order and uniqueness)
-    uint64_t *g = ctx->get<uint64_t>("g", 8);
-    uint32_t *owner = ctx->get<uint32_t>("owner", P);
+    // (acc_partial_deps_batch: the KeyDeps half already built it over the same batch)
+    const uint32_t *owner;
     Dictionary dict;
-    prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict);
+    if (shared && shared->valid) {
+        dict = shared->dict;
+        owner = shared->owner;
+        ctx->stat("rangedeps.shared_dictionary", 1);
+    } else {
+        uint64_t *g = ctx->get<uint64_t>("g", 8);
+        uint32_t *own = ctx->get<uint32_t>("owner", P);
+        prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, own, g, dict);
+        owner = own;
+        ctx->stat("rangedeps.shared_dictionary", 0);
+    }
     // TxnId positions and STARTED_BEFORE limits
     const size_t m2 = 2 * (size_t)n;
     uint32_t *isT = ctx->get<uint32_t>("rd_isT", m2);

@@ -25,6 +25,8 @@
  *   acc_shard_merge        messages/PreAccept.java:141-156, CommandStores.mapReduce local/CommandStores.java:575-592):
  *                          fragments to the txn's home GPU (all-to-all(v) by the host over RCCL), then KeyDeps.with
  *                          folded in shard order = the batched KeyDeps.merge below.
+ *   acc_partial_deps_batch both halves of PartialDeps of a mixed batch in one call (KeyDeps + RangeDeps through
+ *                          PartialDeps.Builder primitives/PartialDeps.java:31-45), one shared dictionary pass.
  *   acc_map_reduce_full    the recovery scans of BeginRecovery        messages/BeginRecovery.java:334-378
  *                          -> SafeCommandStore.mapReduceFull          local/SafeCommandStore.java:285
  *                          -> InMemorySafeStore.mapReduceFull         impl/InMemoryCommandStore.java:874-881 (key part)
@@ -226,6 +228,14 @@ int acc_rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedep
  * key_idx indexes the list of CFK keys its ranges cover (range order). Copy out with acc_keydeps_copy_out. */
 int acc_keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *out_view);
 int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out);
+/* The whole PartialDeps of every txn of a mixed batch in one call (PreAccept.calculatePartialDeps,
+ * messages/PreAccept.java:245-265, routing each emitted (key | range, TxnId) through PartialDeps.Builder,
+ * primitives/PartialDeps.java:31-45 / Deps.AbstractBuilder.add primitives/Deps.java:56-71): the KeyDeps half of
+ * acc_keydeps_mixed and the RangeDeps half of acc_rangedeps_batch, sharing one dictionary pass (and its validation) and
+ * the staged inputs. Both views stay valid until the next compute call; acc_keydeps_copy_out / acc_rangedeps_copy_out
+ * copy them. */
+int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *key_view,
+                           acc_rangedeps_view *range_view);
 
 /* ---- Deps.merge over many replies per txn ----
  * Input: R = n_groups groups (one coordinated txn each); group g owns replies

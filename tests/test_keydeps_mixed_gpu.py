@@ -137,3 +137,26 @@ def test_union_tiers(ctx):
     st = ctx.stats()
     assert st["keydeps.range_block_txns"] >= 1 and st["keydeps.range_mid_txns"] >= 1
     assert_same(g, oracle.keydeps_mixed(rb), "union tiers")
+
+
+@pytest.mark.parametrize("end_inclusive", [1, 0])
+def test_partial_deps_fused(ctx, end_inclusive):
+    """acc_partial_deps_batch: both PartialDeps halves in one call over one dictionary pass, identical to the two
+    separate calls and to the oracle's KeyDeps and RangeDeps."""
+    import oracle
+    rb = rd_cases.dense(77, n=5000, end_inclusive=end_inclusive, ranges_per_txn=2)
+    k, r = ctx.calculate_partial_deps_mixed(rb)
+    assert ctx.stats()["rangedeps.shared_dictionary"] == 1
+    assert_same(k, oracle.keydeps_mixed(rb), "fused key half")
+    r2 = ctx.calculate_partial_range_deps(rb)
+    assert ctx.stats()["rangedeps.shared_dictionary"] == 0
+    for f in ("rng_start", "rng_end", "arena_off", "arena", "rd_off", "range_id", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(r, f), getattr(r2, f), err_msg=f)
+    o = oracle.rangedeps_batch(rb)
+    for f in ("arena_off", "arena", "rd_off", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(r, f), getattr(o, f), err_msg=f)
+    # a batch without key pairs: the RangeDeps half builds its own dictionary
+    only = rd_cases.dense(78, n=600, end_inclusive=end_inclusive, p_range=1.0)
+    k, r = ctx.calculate_partial_deps_mixed(only)
+    assert ctx.stats()["rangedeps.shared_dictionary"] == 0
+    assert_same(k, oracle.keydeps_mixed(only), "range-only key half")
