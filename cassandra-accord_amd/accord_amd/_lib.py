@@ -41,7 +41,8 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
-           "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch"]
+           "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch",
+           "acc_deps_from_json", "acc_deps_to_json"]
 
 
 class Opts(C.Structure):
@@ -221,6 +222,25 @@ class LatestView(C.Structure):
                 ("sufficient_start", u64p), ("sufficient_end", u64p)]
 
 
+class JsonIn(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("n_docs", C.c_uint32), ("bytes", C.c_void_p), ("doc_off", C.c_void_p)]
+
+
+class JsonDepsView(C.Structure):
+    _fields_ = [("n_docs", C.c_uint32), ("deps", DepsMergeView), ("n_dict", C.c_uint64), ("dict_kind", C.c_void_p),
+                ("dict_null", C.c_void_p), ("dict_value", C.c_void_p), ("dict_hash", C.c_void_p)]
+
+
+class JsonOutIn(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("key_deps", RmmView), ("range_deps", RmmView), ("n_dict", C.c_uint64),
+                ("dict_kind", C.c_void_p), ("dict_null", C.c_void_p), ("dict_value", C.c_void_p)]
+
+
+class JsonOut(C.Structure):
+    _fields_ = [("mem", C.c_uint32), ("cap_bytes", C.c_uint64), ("need_bytes", C.c_uint64), ("bytes", C.c_void_p),
+                ("doc_off", C.c_void_p)]
+
+
 class GraphIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n", C.c_uint32),
                 ("off", C.c_void_p), ("dep", C.c_void_p), ("exec_rank", C.c_void_p)]
@@ -306,6 +326,10 @@ def load():
     L.acc_map_reduce_full.restype = C.c_int
     L.acc_latest_deps_merge.argtypes = [C.c_void_p, C.POINTER(LatestIn), C.POINTER(LatestView)]
     L.acc_latest_deps_merge.restype = C.c_int
+    L.acc_deps_from_json.argtypes = [C.c_void_p, C.POINTER(JsonIn), C.POINTER(JsonDepsView)]
+    L.acc_deps_from_json.restype = C.c_int
+    L.acc_deps_to_json.argtypes = [C.c_void_p, C.POINTER(JsonOutIn), C.POINTER(JsonOut)]
+    L.acc_deps_to_json.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
     L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]

@@ -641,3 +641,43 @@ def latest_deps_merge(ctx: Context, groups, key_objs: dict | None, range_objs: d
     suff = [[(int(ss[x]), int(se[x])) for x in range(int(so[g]), int(so[g + 1]))] for g in range(ng)]
     return dict(key=rmm_copy_out(ctx, ng, v.deps.key_deps, False), range=rmm_copy_out(ctx, ng, v.deps.range_deps, True),
                 sufficient=suff)
+
+
+# ---------------------------------------------------------------- Deps wire format (Maelstrom JSON)
+
+def deps_from_json(ctx: Context, docs: list[bytes], with_view: bool = False):
+    """Json.DEPS_ADAPTER.read of every document on device (acc_deps_from_json): dict(key=..., range=...) per-document
+    Deps halves (key codes = dictionary ranks) and the dictionary (kind, null, value, hash per rank)."""
+    blob = np.frombuffer(b"".join(docs), dtype=np.uint8) if docs else np.zeros(0, np.uint8)
+    off = np.zeros(len(docs) + 1, np.uint64)
+    if docs:
+        np.cumsum([len(x) for x in docs], out=off[1:])
+    blob = np.ascontiguousarray(blob)
+    ji = L.JsonIn(L.ACC_MEM_HOST, len(docs), blob.ctypes.data if blob.size else None, off.ctypes.data)
+    v = L.JsonDepsView()
+    ctx.check(ctx._lib.acc_deps_from_json(ctx.handle, C.byref(ji), C.byref(v)))
+    nd = int(v.n_dict)
+    out = dict(key=rmm_copy_out(ctx, len(docs), v.deps.key_deps, False),
+               range=rmm_copy_out(ctx, len(docs), v.deps.range_deps, True),
+               dict_kind=device_array(ctx, v.dict_kind, nd, np.uint8), dict_null=device_array(ctx, v.dict_null, nd, np.uint8),
+               dict_value=device_array(ctx, v.dict_value, nd, np.uint64), dict_hash=device_array(ctx, v.dict_hash, nd, np.int32))
+    if with_view:
+        out["view"] = v
+    return out
+
+
+def deps_to_json(ctx: Context, view) -> list[bytes]:
+    """Json.DEPS_ADAPTER.write of every document of an acc_json_deps_view on device (acc_deps_to_json)."""
+    oi = L.JsonOutIn(view.n_docs, view.deps.key_deps, view.deps.range_deps, view.n_dict, view.dict_kind, view.dict_null,
+                     view.dict_value)
+    o = L.JsonOut()
+    o.mem = L.ACC_MEM_HOST
+    rc = ctx._lib.acc_deps_to_json(ctx.handle, C.byref(oi), C.byref(o))
+    if rc not in (L.ACC_OK, L.ACC_E_CAP):
+        ctx.check(rc)
+    buf = np.zeros(max(int(o.need_bytes), 1), np.uint8)
+    off = np.zeros(view.n_docs + 1, np.uint64)
+    o.cap_bytes, o.bytes, o.doc_off = int(o.need_bytes), buf.ctypes.data, off.ctypes.data
+    ctx.check(ctx._lib.acc_deps_to_json(ctx.handle, C.byref(oi), C.byref(o)))
+    raw = buf.tobytes()
+    return [raw[int(off[i]):int(off[i + 1])] for i in range(view.n_docs)]

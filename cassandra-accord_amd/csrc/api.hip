@@ -16,6 +16,8 @@ void rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *selec
 void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q, acc_stab_view *out);
 void map_reduce_full(acc_ctx *ctx, const acc_batch_in *in, const acc_recovery_in *q, acc_keydeps_view *view);
 void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *view);
+void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *view);
+void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
 }  // namespace acc
 
 extern "C" {
@@ -123,6 +125,24 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
         acc::keydeps_mixed(ctx, in, key_view, &sd);
         acc::rangedeps_batch(ctx, in, range_view, &sd);
         ctx->kd_valid = true;   // both views stay readable (distinct buffers)
+    });
+}
+
+int acc_deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::deps_from_json(ctx, in, out_view);
+    });
+}
+
+int acc_deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::deps_to_json(ctx, in, out);
     });
 }
 

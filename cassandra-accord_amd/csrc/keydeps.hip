@@ -2236,34 +2236,39 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
     const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
     if (c0 >= total) return;
     const uint64_t c1 = min(total, c0 + UC_CHUNK);
-    if (tid == 0) s_t[1] = last_le(u_off, n, c1 - 1);
-    uint64_t pos = c0;
-    while (pos < c1) {
-        // the window starts at the txn holding output `pos` (runs of txns without TxnIds are jumped over, so sparse
-        // batches, e.g. the range txns of a mixed batch, cost nothing here)
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t lo = 0, hi = s_t[1] + 1;
-            while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (u_off[m] <= pos) lo = m; else hi = m; }
-            s_t[0] = lo;
+    if (tid == 0) { s_t[0] = last_le(u_off, n, c0); s_t[1] = last_le(u_off, n, c1 - 1); }
+    __syncthreads();
+    const uint32_t tlo = s_t[0], thi = s_t[1];
+    auto source = [&](uint32_t t) {
+        return bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_N2;
+    };
+    if (thi - tlo >= 8 * BLOCK) {
+        // sparse chunk (long runs of txns without TxnIds, e.g. the range txns of a mixed batch): every output finds its
+        // txn by a binary search of u_off over the chunk's txn span
+        for (uint64_t i = c0 + tid; i < c1; i += BLOCK) {
+            uint32_t lo = tlo, hi = thi + 1;
+            while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (u_off[m] <= i) lo = m; else hi = m; }
+            const uint64_t sb = source(lo), off = i - u_off[lo];
+            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
         }
-        __syncthreads();
-        const uint32_t tw = s_t[0], thi = s_t[1];
+        return;
+    }
+    // dense chunk: windows of BLOCK txns, offsets and sources staged in LDS
+    for (uint32_t tw = tlo; tw <= thi; tw += BLOCK) {
         const uint32_t nt = min((uint32_t)BLOCK, thi + 1 - tw);
+        __syncthreads();
         if (tid < nt) {
-            const uint32_t t = tw + tid;
-            uo[tid] = u_off[t];
-            src[tid] = bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_N2;
+            uo[tid] = u_off[tw + tid];
+            src[tid] = source(tw + tid);
         }
         if (tid == 0) uo[nt] = u_off[tw + nt];
         __syncthreads();
-        const uint64_t hi = min(c1, uo[nt]);
-        for (uint64_t i = pos + tid; i < hi; i += BLOCK) {
+        const uint64_t lo = max(c0, uo[0]), hi = min(c1, uo[nt]);
+        for (uint64_t i = lo + tid; i < hi; i += BLOCK) {
             const uint32_t a = last_le(uo, nt, i);
             const uint64_t sb = src[a], off = i - uo[a];
             dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
         }
-        pos = hi;
     }
 }
 

@@ -36,6 +36,8 @@
  *   acc_latest_deps_merge  LatestDeps.mergeProposal / mergeCommit     primitives/LatestDeps.java:306-326
  *                          (Recover.java:295-355): the interval fold of the replies, then KeyDeps/RangeDeps.slice of
  *                          every selected deps object to its interval and the batched Deps.merge of the slices.
+ *   acc_deps_from_json /   Json.DEPS_ADAPTER read / write             accord-maelstrom/.../maelstrom/Json.java:316-398
+ *   acc_deps_to_json       (the in-tree Deps wire format) parsed / written on device, with the KeyDeps / RangeDeps Builder.
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -562,6 +564,53 @@ typedef struct acc_latest_view {
 } acc_latest_view;
 
 int acc_latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *out_view);
+
+/* ---- Deps wire format: Maelstrom JSON <-> device ----
+ * acc_deps_from_json: a batch of JSON documents, each one Deps as Json.DEPS_ADAPTER writes it
+ * (accord-maelstrom/.../Json.java:316-398: {"keyDeps":[[datum,[msb,lsb,node]],...],"rangeDeps":[[start,end,[msb,lsb,node]],...]})
+ * concatenated in bytes[doc_off[d] .. doc_off[d+1]), parsed on device and built per document (KeyDeps / RangeDeps
+ * Builder, Json.java:356-392) into the per-document Deps of `deps` (acc_rmm_view halves; copy with acc_rmm_copy_out).
+ * Keys are datums (mael/Datum.java); their codes in `deps` are dense ranks of every datum of the batch in
+ * Datum.compareTo order (hash first, COMPARE_BY_HASH), with the dictionary rank -> (Datum.Kind ordinal, null, value,
+ * hash). LONG (integer literals) and HASH datums are supported; STRING / DOUBLE datums give ACC_E_ARG.
+ * acc_deps_to_json: the inverse for any acc_rmm_view pair of this context whose key codes index such a dictionary
+ * (e.g. a Deps.merge of ingested replies): Gson's compact DEPS_ADAPTER text per group, two-call sizing on need_bytes. */
+typedef struct acc_json_in {
+    uint32_t mem;
+    uint32_t n_docs;
+    const uint8_t  *bytes;
+    const uint64_t *doc_off;   /* [n_docs+1] */
+} acc_json_in;
+
+typedef struct acc_json_deps_view {
+    uint32_t n_docs;
+    acc_deps_merge_view deps;
+    uint64_t n_dict;
+    const uint8_t  *dict_kind;   /* Datum.Kind ordinal: STRING 0, LONG 1, DOUBLE 2, HASH 3 */
+    const uint8_t  *dict_null;   /* value == null (the +Inf sentinel) */
+    const uint64_t *dict_value;  /* LONG: the long; HASH: the hash as u32 */
+    const int32_t  *dict_hash;   /* Datum.hash(value) */
+} acc_json_deps_view;
+
+int acc_deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *out_view);
+
+typedef struct acc_json_out_in {
+    uint32_t n_groups;
+    acc_rmm_view key_deps, range_deps;      /* device views (key_off null = absent half) */
+    uint64_t n_dict;
+    const uint8_t  *dict_kind, *dict_null;  /* device */
+    const uint64_t *dict_value;
+} acc_json_out_in;
+
+typedef struct acc_json_out {
+    uint32_t  mem;
+    uint64_t  cap_bytes;
+    uint64_t  need_bytes;      /* written */
+    uint8_t  *bytes;           /* [cap_bytes] */
+    uint64_t *doc_off;         /* [n_groups+1] */
+} acc_json_out;
+
+int acc_deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
 
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
