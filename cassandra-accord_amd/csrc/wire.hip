@@ -262,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void k_json_reply_offs(uint64_t R, Sing s, u
     roff[r] = s.rb[lo] + min(q, s.nr[lo]);
 }
 
-// singleton halves: entry i = one key (its datum rank), one TxnId, keysToTxnIds [1, 0]
+// singleton halves: entry i = one key (its datum rank), one TxnId, keysToTxnIds [2, 0]
 __global__ __launch_bounds__(BLOCK) void k_json_singletons(uint64_t NK, uint64_t NR, const uint32_t *__restrict__ rank,
                                                            const Txn *__restrict__ kt, const Txn *__restrict__ rt,
                                                            uint64_t *__restrict__ kkey, uint64_t *__restrict__ km,
@@ -276,14 +276,14 @@ __global__ __launch_bounds__(BLOCK) void k_json_singletons(uint64_t NK, uint64_t
         kkey[i] = rank[i];
         const Txn t = kt[i];
         km[i] = t.msb; kl[i] = t.lsb; kn[i] = t.node;
-        kk2v[2 * i] = 1; kk2v[2 * i + 1] = 0;
+        kk2v[2 * i] = 2; kk2v[2 * i + 1] = 0;
     }
     if (i < NR) {
         rka[i] = rank[NK + i];
         rkb[i] = rank[NK + NR + i];
         const Txn t = rt[i];
         rm[i] = t.msb; rl[i] = t.lsb; rn[i] = t.node;
-        rk2v[2 * i] = 1; rk2v[2 * i + 1] = 0;
+        rk2v[2 * i] = 2; rk2v[2 * i + 1] = 0;
     }
 }
 
