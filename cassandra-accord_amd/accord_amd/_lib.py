@@ -42,7 +42,8 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
            "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch",
-           "acc_deps_from_json", "acc_deps_to_json"]
+           "acc_deps_from_json", "acc_deps_to_json",
+           "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view"]
 
 
 class Opts(C.Structure):
@@ -330,6 +331,14 @@ def load():
     L.acc_deps_from_json.restype = C.c_int
     L.acc_deps_to_json.argtypes = [C.c_void_p, C.POINTER(JsonOutIn), C.POINTER(JsonOut)]
     L.acc_deps_to_json.restype = C.c_int
+    L.acc_cfk_create.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.acc_cfk_create.restype = C.c_int
+    L.acc_cfk_destroy.argtypes = [C.c_void_p]
+    L.acc_cfk_destroy.restype = None
+    L.acc_cfk_update.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn)]
+    L.acc_cfk_update.restype = C.c_int
+    L.acc_cfk_view.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn)]
+    L.acc_cfk_view.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
     L.acc_copy_out.restype = C.c_int
     L.acc_timing_count.argtypes = [C.c_void_p]

@@ -681,3 +681,61 @@ def deps_to_json(ctx: Context, view) -> list[bytes]:
     ctx.check(ctx._lib.acc_deps_to_json(ctx.handle, C.byref(oi), C.byref(o)))
     raw = buf.tobytes()
     return [raw[int(off[i]):int(off[i + 1])] for i in range(view.n_docs)]
+
+
+# ---------------------------------------------------------------- device-resident CommandsForKey store
+
+class CfkStore:
+    """A CommandsForKey store kept in HBM and updated by batches of commands (acc_cfk_*): CommandsForKey.update for
+    every key of every command (local/CommandsForKey.java:652-706)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx.check(ctx._lib.acc_cfk_create(ctx.handle, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.ctx._lib.acc_cfk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def update(self, batch):
+        """Apply a batch of commands (host arrays in the acc_batch_in layout)."""
+        a = dict(tm=np.ascontiguousarray(batch.txn_msb, dtype=np.uint64), tl=np.ascontiguousarray(batch.txn_lsb, dtype=np.uint64),
+                 tn=np.ascontiguousarray(batch.txn_node, dtype=np.int32), em=np.ascontiguousarray(batch.exe_msb, dtype=np.uint64),
+                 el=np.ascontiguousarray(batch.exe_lsb, dtype=np.uint64), en=np.ascontiguousarray(batch.exe_node, dtype=np.int32),
+                 st=np.ascontiguousarray(batch.status, dtype=np.uint8), ko=np.ascontiguousarray(batch.key_off, dtype=np.uint32),
+                 kc=np.ascontiguousarray(batch.key_code, dtype=np.uint64))
+        p = lambda k: a[k].ctypes.data  # noqa: E731
+        n = int(a["st"].shape[0])
+        bi = L.BatchIn(n, L.ACC_MEM_HOST, int(a["ko"][-1]) if n else 0, L.TsCols(p("tm"), p("tl"), p("tn")),
+                       L.TsCols(p("em"), p("el"), p("en")), p("st"), p("ko"), p("kc"))
+        self.ctx.check(self.ctx._lib.acc_cfk_update(self.ctx.handle, self._h, C.byref(bi)))
+
+    def view(self) -> "L.BatchIn":
+        """The store as an acc_batch_in of device pointers (valid until the next update)."""
+        v = L.BatchIn()
+        self.ctx.check(self.ctx._lib.acc_cfk_view(self.ctx.handle, self._h, C.byref(v)))
+        return v
+
+    def snapshot(self):
+        """Host copy of the store (a workload.Batch)."""
+        from .workload import Batch
+        v = self.view()
+        n, P = int(v.n_txn), int(v.n_pairs)
+        g = lambda ptr, cnt, dt: device_array(self.ctx, ptr, cnt, dt)  # noqa: E731
+        return Batch(g(v.txn_id.msb, n, np.uint64), g(v.txn_id.lsb, n, np.uint64), g(v.txn_id.node, n, np.int32),
+                     g(v.execute_at.msb, n, np.uint64), g(v.execute_at.lsb, n, np.uint64), g(v.execute_at.node, n, np.int32),
+                     g(v.status, n, np.uint8), g(v.key_off, n + 1, np.uint32), g(v.key_code, P, np.uint64))
+
+    def calculate_partial_deps(self) -> "BatchKeyDeps":
+        """PreAccept.calculatePartialDeps for every txn of the store, read in place (no host round trip)."""
+        view = self.ctx.keydeps_batch_raw(self.view())
+        return self.ctx.copy_out(view, None)

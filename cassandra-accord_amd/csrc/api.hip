@@ -18,6 +18,10 @@ void map_reduce_full(acc_ctx *ctx, const acc_batch_in *in, const acc_recovery_in
 void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *view);
 void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *view);
 void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
+void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in);
+void cfk_view(acc_cfk *cfk, acc_batch_in *out);
+void cfk_free(acc_cfk *cfk);
+acc_cfk *cfk_new(int device);
 }  // namespace acc
 
 extern "C" {
@@ -143,6 +147,33 @@ int acc_deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out)
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         acc::deps_to_json(ctx, in, out);
+    });
+}
+
+int acc_cfk_create(acc_ctx *ctx, acc_cfk **out)
+{
+    if (!ctx || !out) return ACC_E_ARG;
+    *out = nullptr;
+    return acc_guard(ctx, [&] { *out = acc::cfk_new(ctx->device); });
+}
+
+void acc_cfk_destroy(acc_cfk *cfk) { acc::cfk_free(cfk); }
+
+int acc_cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *delta)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::cfk_update(ctx, cfk, delta);
+    });
+}
+
+int acc_cfk_view(acc_ctx *ctx, acc_cfk *cfk, acc_batch_in *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::cfk_view(cfk, out);
     });
 }
 

@@ -1,0 +1,368 @@
+// cfk.hip — a device-resident CommandsForKey store maintained incrementally:
+// CommandsForKey.update(prev, next) (local/CommandsForKey.java:652-706), as SafeCommandStore.updateCommandsForKey calls it
+// for every key of a command (local/SafeCommandStore.java:217-240), applied to a batch of commands at once.
+//
+// The store keeps the snapshot that acc_keydeps_batch / acc_map_reduce_full / acc_shard_* read, resident in HBM across
+// batches: per txn (sorted by TxnId) TxnId, executeAt, InternalStatus and its keys (txn-major CSR, keys ascending).
+// An update of D commands costs O(n + P) streaming passes plus O(D log n) searches instead of re-staging the whole
+// snapshot from the host:
+//   1. delta TxnIds dense-ranked (Timestamp.compareTo) -> sorted delta order (duplicates -> ACC_E_ARG);
+//   2. each delta txn searched among the stored TxnIds: present -> update in place (the status must not go back:
+//      newStatus < cur is the reference's IllegalStateException "stale status"; equal status without info is a no-op;
+//      executeAt = txnId when the new status has no info, TxnInfo.create :669-670), absent -> insert;
+//   3. stored txn j moves to j + #(inserted TxnIds below it); inserted txn m (delta order) lands at its insert position
+//      + m; key lists merge (a command registers on keys it was not yet on);
+//   4. key offsets by one scan, then every column is written once into the other buffer set, and the sets swap.
+#include "dict.hpp"
+
+struct acc_cfk {
+    int device = 0;
+    uint32_t n = 0;
+    uint64_t P = 0;
+    struct Set {
+        uint64_t *tm = nullptr, *tl = nullptr, *em = nullptr, *el = nullptr, *key_code = nullptr;
+        int32_t *tn = nullptr, *en = nullptr;
+        uint8_t *status = nullptr;
+        uint32_t *key_off = nullptr;
+        size_t cap_n = 0, cap_p = 0;
+    } set[2];
+    int cur = 0;
+};
+
+namespace acc {
+
+namespace cf {
+
+constexpr uint64_t IDENTITY_LSB = 0xFFFFFFFFFFFF001EULL;
+enum : uint64_t { E_STATUS = 1, E_KIND = 2, E_KEYS = 4, E_STALE = 8, E_OFF = 16, E_DUP = 32 };
+
+__device__ __forceinline__ int ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn)
+{
+    if (am != bm) return am < bm ? -1 : 1;
+    const uint64_t a1 = al & IDENTITY_LSB, b1 = bl & IDENTITY_LSB;
+    if (a1 != b1) return a1 < b1 ? -1 : 1;
+    if (an != bn) return an < bn ? -1 : 1;
+    return 0;
+}
+
+__host__ __device__ inline bool has_info(uint32_t s) { return s >= ACC_ST_ACCEPTED && s <= ACC_ST_APPLIED; }
+
+struct Delta {
+    const uint64_t *tm, *tl, *em, *el, *key_code;
+    const int32_t *tn, *en;
+    const uint8_t *status;
+    const uint32_t *key_off;
+    uint32_t D;
+};
+
+struct Store {
+    const uint64_t *tm, *tl, *em, *el, *key_code;
+    const int32_t *tn, *en;
+    const uint8_t *status;
+    const uint32_t *key_off;
+    uint32_t n;
+};
+
+struct Out {
+    uint64_t *tm, *tl, *em, *el, *key_code;
+    int32_t *tn, *en;
+    uint8_t *status;
+    uint32_t *key_off;
+};
+
+}  // namespace cf
+
+using namespace cf;
+
+__global__ __launch_bounds__(BLOCK) void k_cf_validate(Delta d, uint64_t *__restrict__ errs, uint64_t *__restrict__ w0,
+                                                       uint64_t *__restrict__ w1, uint64_t *__restrict__ w2)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= d.D) return;
+    uint64_t e = 0;
+    if (d.status[i] > ACC_ST_INVALID_OR_TRUNCATED) e |= E_STATUS;
+    if (((d.tl[i] >> 1) & 7u) > ACC_KIND_LOCAL_ONLY) e |= E_KIND;
+    const uint32_t k0 = d.key_off[i], k1 = d.key_off[i + 1];
+    if (k1 < k0) e |= E_OFF;
+    else
+        for (uint32_t j = k0 + 1; j < k1; ++j)
+            if (d.key_code[j - 1] >= d.key_code[j]) { e |= E_KEYS; break; }
+    w0[i] = d.tm[i];
+    w1[i] = d.tl[i] & IDENTITY_LSB;
+    w2[i] = (uint64_t)((uint32_t)d.tn[i] ^ 0x80000000u);
+    if (e) atomicOr((unsigned long long *)errs, (unsigned long long)e);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cf_order(uint32_t D, const uint32_t *__restrict__ rank, uint32_t *__restrict__ ord)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < D) ord[rank[i]] = i;
+}
+
+// sorted delta txn k: its lower bound among the stored TxnIds, found or not, the status rule, the new-txn flag
+__global__ __launch_bounds__(BLOCK) void k_cf_locate(Delta d, Store s, const uint32_t *__restrict__ ord, uint32_t *__restrict__ pos,
+                                                     uint32_t *__restrict__ isnew, int32_t *__restrict__ upd_of_old,
+                                                     uint64_t *__restrict__ errs)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= d.D) return;
+    const uint32_t i = ord[k];
+    const uint64_t xm = d.tm[i], xl = d.tl[i];
+    const int32_t xn = d.tn[i];
+    const uint32_t kind = (uint32_t)(xl >> 1) & 7u;
+    if ((xl & 1u) || kind == ACC_KIND_EPHEMERAL_READ || kind == ACC_KIND_LOCAL_ONLY) {
+        // only key-domain, globally visible txns are CommandsForKey members (SafeCommandStore.java:224)
+        pos[k] = 0;
+        isnew[k] = 0;
+        return;
+    }
+    uint32_t lo = 0, hi = s.n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ts_cmp(s.tm[m], s.tl[m], s.tn[m], xm, xl, xn) < 0) lo = m + 1; else hi = m;
+    }
+    const bool found = lo < s.n && ts_cmp(s.tm[lo], s.tl[lo], s.tn[lo], xm, xl, xn) == 0;
+    pos[k] = lo;
+    isnew[k] = found ? 0u : 1u;
+    if (found) {
+        if (d.status[i] < s.status[lo]) atomicOr((unsigned long long *)errs, (unsigned long long)E_STALE);
+        upd_of_old[lo] = (int32_t)i;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cf_newpos(uint32_t D, const uint32_t *__restrict__ isnew, const uint32_t *__restrict__ newx,
+                                                     const uint32_t *__restrict__ pos, uint32_t *__restrict__ newpos)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < D && isnew[k]) newpos[newx[k]] = pos[k];
+}
+
+__device__ __forceinline__ uint32_t merged_count(const uint64_t *a, uint32_t na, const uint64_t *b, uint32_t nb)
+{
+    uint32_t i = 0, j = 0, c = 0;
+    while (i < na && j < nb) {
+        if (a[i] < b[j]) ++i;
+        else if (b[j] < a[i]) ++j;
+        else { ++i; ++j; }
+        ++c;
+    }
+    return c + (na - i) + (nb - j);
+}
+
+// new index and key count of every stored txn (updated or not) and every inserted txn
+__global__ __launch_bounds__(BLOCK) void k_cf_counts(Delta d, Store s, const int32_t *__restrict__ upd_of_old, uint32_t nnew,
+                                                     const uint32_t *__restrict__ newpos, const uint32_t *__restrict__ ord,
+                                                     const uint32_t *__restrict__ isnew, const uint32_t *__restrict__ newx,
+                                                     const uint32_t *__restrict__ pos, uint32_t *__restrict__ kcount)
+{
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x < s.n) {
+        uint32_t lo = 0, hi = nnew;   // inserted TxnIds below stored txn x: insert positions <= x
+        while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (newpos[m] <= x) lo = m + 1; else hi = m; }
+        const uint32_t dst = x + lo;
+        const uint32_t a0 = s.key_off[x], na = s.key_off[x + 1] - a0;
+        const int32_t u = upd_of_old[x];
+        kcount[dst] = u < 0 ? na
+                            : merged_count(s.key_code + a0, na, d.key_code + d.key_off[u], d.key_off[u + 1] - d.key_off[u]);
+    }
+    if (x < d.D && isnew[x]) {
+        const uint32_t i = ord[x];
+        kcount[pos[x] + newx[x]] = d.key_off[i + 1] - d.key_off[i];
+    }
+}
+
+__device__ __forceinline__ void put_txn(const Out &o, uint32_t t, uint64_t tm, uint64_t tl, int32_t tn, uint64_t em, uint64_t el,
+                                        int32_t en, uint8_t st)
+{
+    o.tm[t] = tm; o.tl[t] = tl; o.tn[t] = tn; o.em[t] = em; o.el[t] = el; o.en[t] = en; o.status[t] = st;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cf_write(Delta d, Store s, const int32_t *__restrict__ upd_of_old, uint32_t nnew,
+                                                    const uint32_t *__restrict__ newpos, const uint32_t *__restrict__ ord,
+                                                    const uint32_t *__restrict__ isnew, const uint32_t *__restrict__ newx,
+                                                    const uint32_t *__restrict__ pos, Out o)
+{
+    const uint32_t x = blockIdx.x * BLOCK + threadIdx.x;
+    if (x < s.n) {
+        uint32_t lo = 0, hi = nnew;
+        while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (newpos[m] <= x) lo = m + 1; else hi = m; }
+        const uint32_t dst = x + lo;
+        const uint32_t a0 = s.key_off[x], na = s.key_off[x + 1] - a0;
+        const int32_t u = upd_of_old[x];
+        uint64_t em = s.em[x], el = s.el[x];
+        int32_t en = s.en[x];
+        uint8_t st = s.status[x];
+        uint64_t *out = o.key_code + o.key_off[dst];
+        if (u < 0) {
+            for (uint32_t j = 0; j < na; ++j) out[j] = s.key_code[a0 + j];
+        } else {
+            const uint8_t ns = d.status[u];
+            // CommandsForKey.update :674-703: a higher status, or the same status with info, replaces the entry
+            if (ns > st || has_info(ns)) {
+                st = ns;
+                if (has_info(ns)) { em = d.em[u]; el = d.el[u]; en = d.en[u]; }
+                else { em = s.tm[x]; el = s.tl[x]; en = s.tn[x]; }
+            }
+            const uint64_t *b = d.key_code + d.key_off[u];
+            const uint32_t nb = d.key_off[u + 1] - d.key_off[u];
+            const uint64_t *a = s.key_code + a0;
+            uint32_t i = 0, j = 0, c = 0;
+            while (i < na || j < nb) {
+                if (j >= nb || (i < na && a[i] < b[j])) out[c++] = a[i++];
+                else if (i >= na || b[j] < a[i]) out[c++] = b[j++];
+                else { out[c++] = a[i++]; ++j; }
+            }
+        }
+        put_txn(o, dst, s.tm[x], s.tl[x], s.tn[x], em, el, en, st);
+    }
+    if (x < d.D && isnew[x]) {
+        const uint32_t i = ord[x], dst = pos[x] + newx[x];
+        const uint8_t ns = d.status[i];
+        // TxnInfo.create(txnId, status, txnId) for statuses without info (:669-670)
+        if (has_info(ns)) put_txn(o, dst, d.tm[i], d.tl[i], d.tn[i], d.em[i], d.el[i], d.en[i], ns);
+        else put_txn(o, dst, d.tm[i], d.tl[i], d.tn[i], d.tm[i], d.tl[i], d.tn[i], ns);
+        uint64_t *out = o.key_code + o.key_off[dst];
+        for (uint32_t j = d.key_off[i]; j < d.key_off[i + 1]; ++j) out[j - d.key_off[i]] = d.key_code[j];
+    }
+}
+
+namespace {
+
+template <class T>
+void realloc_dev(T *&p, size_t count)
+{
+    if (p) ACC_HIP(hipFree(p));
+    p = nullptr;
+    ACC_HIP(hipMalloc(&p, count * sizeof(T)));
+}
+
+// capacity for n txns (txn columns, n + 1 key offsets) and P key codes; contents are not kept
+void reserve(acc_cfk::Set &s, size_t n, size_t P)
+{
+    if (n + 2 > s.cap_n) {
+        const size_t c = n + n / 4 + 64;
+        realloc_dev(s.tm, c); realloc_dev(s.tl, c); realloc_dev(s.em, c); realloc_dev(s.el, c);
+        realloc_dev(s.tn, c); realloc_dev(s.en, c); realloc_dev(s.status, c); realloc_dev(s.key_off, c);
+        s.cap_n = c;
+    }
+    if (P + 1 > s.cap_p) {
+        const size_t c = P + P / 4 + 64;
+        realloc_dev(s.key_code, c);
+        s.cap_p = c;
+    }
+}
+
+}  // namespace
+
+void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
+{
+    if (!cfk || !in) fail(ACC_E_ARG, "null argument");
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    hipStream_t st = ctx->stream;
+    const uint32_t D = in->n_txn;
+    const size_t Pd = (size_t)in->n_pairs;
+    Delta d{};
+    d.D = D;
+    d.key_off = stage_in(ctx, "cf_key_off", in->key_off, (size_t)D + 1, in->mem);
+    d.tm = stage_in(ctx, "cf_tm", in->txn_id.msb, D, in->mem);
+    d.tl = stage_in(ctx, "cf_tl", in->txn_id.lsb, D, in->mem);
+    d.tn = stage_in(ctx, "cf_tn", in->txn_id.node, D, in->mem);
+    d.em = stage_in(ctx, "cf_em", in->execute_at.msb, D, in->mem);
+    d.el = stage_in(ctx, "cf_el", in->execute_at.lsb, D, in->mem);
+    d.en = stage_in(ctx, "cf_en", in->execute_at.node, D, in->mem);
+    d.status = stage_in(ctx, "cf_status", in->status, D, in->mem);
+    d.key_code = stage_in(ctx, "cf_key_code", in->key_code, Pd, in->mem);
+    if (D == 0) return;
+    uint64_t *errs = ctx->get<uint64_t>("cf_errs", 1);
+    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+    uint64_t *w[3] = { ctx->get<uint64_t>("cf_w0", D), ctx->get<uint64_t>("cf_w1", D), ctx->get<uint64_t>("cf_w2", D) };
+    launch(ctx, "cf_validate", k_cf_validate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, errs, w[0], w[1], w[2]);
+    const uint64_t *words[3] = { w[0], w[1], w[2] };
+    DenseRank dr = dense_rank(ctx, "cf_dr", D, 3, words, nullptr, nullptr, false);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, dr.count_dev, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, d.key_off + D, 4, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    uint64_t e = ctx->pinned[0];
+    if (e & E_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal (> INVALID_OR_TRUNCATED)");
+    if (e & E_KIND) fail(ACC_E_ARG, "Kind.ofOrdinal: invalid kind ordinal in TxnId flags");
+    if (e & E_OFF) fail(ACC_E_ARG, "key_off must be non-decreasing");
+    if (e & E_KEYS) fail(ACC_E_ARG, "keys of a txn must be sorted and unique (Keys.ofSortedUnique)");
+    if (ctx->pinned[1] != D) fail(ACC_E_ARG, "TxnIds of one update must be distinct");
+    if ((ctx->pinned[2] & 0xFFFFFFFFull) != Pd) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
+
+    acc_cfk::Set &S = cfk->set[cfk->cur];
+    const uint32_t n = cfk->n;
+    Store s{ S.tm, S.tl, S.em, S.el, S.key_code, S.tn, S.en, S.status, S.key_off, n };
+    uint32_t *ord = ctx->get<uint32_t>("cf_ord", D);
+    launch(ctx, "cf_order", k_cf_order, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, D, (const uint32_t *)dr.rank, ord);
+    uint32_t *pos = ctx->get<uint32_t>("cf_pos", D), *isnew = ctx->get<uint32_t>("cf_isnew", D);
+    uint32_t *newx = ctx->get<uint32_t>("cf_newx", (size_t)D + 1);
+    int32_t *upd = ctx->get<int32_t>("cf_upd", (size_t)n + 1);
+    ACC_HIP(hipMemsetAsync(upd, 0xFF, ((size_t)n + 1) * 4, st));
+    launch(ctx, "cf_locate", k_cf_locate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, s, (const uint32_t *)ord, pos, isnew, upd, errs);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, isnew, newx, D, true, newx + D);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, newx + D, 4, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    if (ctx->pinned[0] & E_STALE)
+        fail(ACC_E_STATE, "Attempted update to CommandsForKey with a stale status (CommandsForKey.update :680-688)");
+    const uint32_t nnew = (uint32_t)(ctx->pinned[1] & 0xFFFFFFFFu);
+    uint32_t *newpos = ctx->get<uint32_t>("cf_newpos", (size_t)nnew + 1);
+    launch(ctx, "cf_newpos", k_cf_newpos, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, D, (const uint32_t *)isnew,
+           (const uint32_t *)newx, (const uint32_t *)pos, newpos);
+    const uint32_t n2 = n + nnew;
+    uint32_t *kcount = ctx->get<uint32_t>("cf_kcount", (size_t)n2 + 1);
+    const uint32_t gx = grid_for(std::max(n, D), BLOCK);
+    launch(ctx, "cf_counts", k_cf_counts, dim3(gx), dim3(BLOCK), 0, d, s, (const int32_t *)upd, nnew, (const uint32_t *)newpos,
+           (const uint32_t *)ord, (const uint32_t *)isnew, (const uint32_t *)newx, (const uint32_t *)pos, kcount);
+    acc_cfk::Set &T = cfk->set[cfk->cur ^ 1];
+    reserve(T, n2, 0);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, kcount, T.key_off, n2, true, T.key_off + n2);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, T.key_off + n2, 4, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t P2 = ctx->pinned[0] & 0xFFFFFFFFull;
+    if (P2 >= 0xFFFFFFFFull - 1) fail(ACC_E_CAP, "CommandsForKey store too large (pairs >= 2^32)");
+    reserve(T, n2, P2);
+    Out o{ T.tm, T.tl, T.em, T.el, T.key_code, T.tn, T.en, T.status, T.key_off };
+    launch(ctx, "cf_write", k_cf_write, dim3(gx), dim3(BLOCK), 0, d, s, (const int32_t *)upd, nnew, (const uint32_t *)newpos,
+           (const uint32_t *)ord, (const uint32_t *)isnew, (const uint32_t *)newx, (const uint32_t *)pos, o);
+    ctx->sync();
+    cfk->cur ^= 1;
+    cfk->n = n2;
+    cfk->P = P2;
+    ctx->stat("cfk.inserted", nnew);
+    ctx->stat("cfk.updated", D - nnew);
+}
+
+acc_cfk *cfk_new(int device)
+{
+    acc_cfk *c = new acc_cfk();
+    c->device = device;
+    return c;
+}
+
+void cfk_free(acc_cfk *cfk)
+{
+    if (!cfk) return;
+    (void)hipSetDevice(cfk->device);
+    for (auto &s : cfk->set) {
+        (void)hipFree(s.tm); (void)hipFree(s.tl); (void)hipFree(s.em); (void)hipFree(s.el); (void)hipFree(s.key_code);
+        (void)hipFree(s.tn); (void)hipFree(s.en); (void)hipFree(s.status); (void)hipFree(s.key_off);
+    }
+    delete cfk;
+}
+
+void cfk_view(acc_cfk *cfk, acc_batch_in *out)
+{
+    if (!cfk || !out) fail(ACC_E_ARG, "null argument");
+    acc_cfk::Set &S = cfk->set[cfk->cur];
+    if (!S.key_off) {   // empty store: a valid zero-txn batch
+        reserve(S, 0, 0);
+        ACC_HIP(hipMemset(S.key_off, 0, 4));
+    }
+    *out = acc_batch_in{ cfk->n, ACC_MEM_DEVICE, cfk->P, acc_ts_cols{ S.tm, S.tl, S.tn }, acc_ts_cols{ S.em, S.el, S.en },
+                         S.status, S.key_off, S.key_code };
+}
+
+}  // namespace acc

@@ -38,6 +38,8 @@
  *                          every selected deps object to its interval and the batched Deps.merge of the slices.
  *   acc_deps_from_json /   Json.DEPS_ADAPTER read / write             accord-maelstrom/.../maelstrom/Json.java:316-398
  *   acc_deps_to_json       (the in-tree Deps wire format) parsed / written on device, with the KeyDeps / RangeDeps Builder.
+ *   acc_cfk_*              CommandsForKey.update for batches of commands   local/CommandsForKey.java:652-706
+ *                          against a CFK store kept in HBM (SafeCommandStore.updateCommandsForKey :217-240).
  *   acc_levelise           execution-order restatement of Commands.updateWaitingOn local/Commands.java:776-830
  *                          (deterministic wavefront schedule).
  *
@@ -611,6 +613,21 @@ typedef struct acc_json_out {
 } acc_json_out;
 
 int acc_deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
+
+/* ---- A device-resident CommandsForKey store, updated incrementally ----
+ * acc_cfk_update applies CommandsForKey.update(prev, next) (local/CommandsForKey.java:652-706) for every key of every
+ * command of `delta`, as SafeCommandStore.updateCommandsForKey does (local/SafeCommandStore.java:217-240; key-domain,
+ * globally visible kinds only, others are ignored): an absent TxnId is inserted (executeAt = txnId unless the status
+ * carries info), a present one is updated in place and registered on any new keys; a status lower than the stored one
+ * is the reference's stale-status IllegalStateException (ACC_E_STATE), an equal status without info changes nothing.
+ * The store stays in HBM between calls; acc_cfk_view describes it as an acc_batch_in of DEVICE pointers (txns in TxnId
+ * order, keys ascending per txn) that acc_keydeps_batch / acc_map_reduce_full / acc_shard_pack take as they are. The
+ * view is valid until the next acc_cfk_update on that store. One store is used by one context at a time. */
+typedef struct acc_cfk acc_cfk;
+int  acc_cfk_create(acc_ctx *ctx, acc_cfk **out);
+void acc_cfk_destroy(acc_cfk *cfk);
+int  acc_cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *delta);
+int  acc_cfk_view(acc_ctx *ctx, acc_cfk *cfk, acc_batch_in *out);
 
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
