@@ -81,9 +81,11 @@ def roofline(step_bytes, timing, steps, ms_per_step, config, variant=""):
         traffic = int(prof.get("hbm_bytes_per_step", 0)) or None
         if "hbm_read_bytes_per_step_raw" in prof:
             traffic_raw = int(prof["hbm_read_bytes_per_step_raw"] + prof["hbm_write_bytes_per_step"])
-        k = prof.get("kernels", {}).get("k_" + dom_name) or prof.get("kernels", {}).get(dom_name)
-        if k:
-            dom_prof_ms = round(k["avg_ns"] / 1e6, 4)
+        # rocprof names carry template arguments (k_v3_stream<unsignedint,512>): match the launch tag on the base name
+        ks = [v for name, v in prof.get("kernels", {}).items() if name.split("<")[0] in ("k_" + dom_name, dom_name)]
+        if ks:
+            calls = sum(v["calls"] for v in ks)
+            dom_prof_ms = round(sum(v["total_ns"] for v in ks) / max(calls, 1) / 1e6, 4)
     return {
         "bound": "hbm",
         "kernel": "pipeline: every kernel of one step (algorithmic bytes of the step / timed ms_per_step)",

@@ -998,14 +998,28 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
     const uint32_t j = v.perm[p];
     uint4 *r = rec + 4 * (size_t)j;
     if (e <= REC_INLINE) {
-        uint32_t buf[16] = {};
-        uint32_t n = 0;
+        // the six class runs hold L6 <= e + 1 <= 16 elements (T itself is dropped at most once): all their loads are
+        // issued together (static slots, predicated), not one dependent load per element
+        uint32_t pre[6], L6 = 0;
 #pragma unroll
-        for (int q2 = 0; q2 < 6; ++q2)
-            for (uint32_t i = 0; i < l[q2]; ++i) {
-                const uint32_t x = v.list_rank[a[q2] + i];
-                if (!(q.bq && x == q.trank)) inl_put(buf, n, x);
-            }
+        for (int q2 = 0; q2 < 6; ++q2) { pre[q2] = L6; L6 += l[q2]; }
+        uint32_t xs[REC_INLINE + 1];
+#pragma unroll
+        for (uint32_t s = 0; s <= REC_INLINE; ++s) {
+            uint32_t idx = a[0] + s;
+#pragma unroll
+            for (int q2 = 1; q2 < 6; ++q2)
+                if (s >= pre[q2]) idx = a[q2] + (s - pre[q2]);   // empty runs are overridden by the next one
+            xs[s] = s < L6 ? v.list_rank[idx] : 0u;
+        }
+        uint32_t d = L6;   // position of T among them (at most one)
+#pragma unroll
+        for (uint32_t s = 0; s <= REC_INLINE; ++s)
+            if (q.bq && s < L6 && xs[s] == q.trank) d = s;
+        uint32_t buf[16] = {};
+#pragma unroll
+        for (uint32_t s = 0; s < REC_INLINE; ++s) buf[s] = s < d ? xs[s] : xs[s + 1];
+        uint32_t n = L6 - (d < L6 ? 1u : 0u);
         if (q.has_m)
             for (uint32_t i = q.bstart; i < q.bend; ++i)
                 if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) {
@@ -1737,6 +1751,10 @@ constexpr int ST_G = 16;                      // lanes per txn
 constexpr int ST_K = 16;                      // keys of a stream txn
 constexpr int ST_N2 = 128;                    // dependency entries of a stream txn (LDS sort buffer, power of two)
 constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream txn
+#ifndef ACC_ST_U
+#define ACC_ST_U 4
+#endif
+constexpr int ST_U = ACC_ST_U;                // raw elements per lane whose loads are in flight together
 
 // Per txn, ST_G lanes: its KeyDeps sizes A = Kd + E (arena ints) and K = Kd (keys with >= 1 dependency) from the
 // count-pass records' word 15 (the exclusive scans of A and K are the txns' arena / key offsets, so the stream pass needs
@@ -1901,7 +1919,7 @@ struct V3Stream {
     const uint64_t *arena_off, *kd_off;       // from the size scans
     uint64_t *u_cnt_out;
     int32_t *arena;
-    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's entry offset, compacted by k_v3_ucompact
+    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnId ranks at the txn's slot, mapped + compacted by k_v3_ucompact
     uint64_t *err;                            // gather count mismatches
     uint32_t n, ntiles;
 };
@@ -2044,58 +2062,68 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
             if (q < e) buf[b0 + q] = ((EntT)w[q] << 4) | (EntT)sub;
     }
     ST_PH(2);
-    // ---- run records, one key at a time (its runs broadcast from the owning lane): the group gathers the flattened
-    // runs R1/R2 per class and R3, dropping T itself and R3 entries below M or of unwitnessed kinds, after the inline
-    // entries
-    const uint64_t runmask = __ballot(sm && run) & gmask;
-    const uint32_t nrun = (uint32_t)__popcll(runmask);
-    uint32_t wnrun = nrun;
+    // ---- run records: the group's runs flattened (run keys in lane order; within a key R1/R2 per class, then R3).
+    // Lane sub takes elements sub, sub + ST_G, ...; ST_U elements per round are located (key lane by a shuffle
+    // search over the group's inclusive raw counts, run by the key lane's cumulative run ends) and all their loads
+    // issued before any is used, so a group pays one memory latency per ST_G * ST_U raw elements instead of one per
+    // ST_G elements of each key. T itself and R3 entries below M or of unwitnessed kinds are dropped.
+    uint32_t rst[NRUN], rce[NRUN];
+    {
+        const uint32_t len[NRUN] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r3.y };
+        rst[0] = r0.x; rst[1] = r0.y; rst[2] = r0.z; rst[3] = r0.w; rst[4] = r1.x; rst[5] = r1.y; rst[6] = r3.x;
+        const uint32_t incl = group_inclusive(rawk, sub);   // rawk = 0 outside run lanes of stream txns
+        uint32_t acc = incl - rawk;
 #pragma unroll
-    for (int d = ST_G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
+        for (int q = 0; q < NRUN; ++q) { acc += run ? len[q] : 0u; rce[q] = acc; }
+    }
+    const uint32_t RAW = __shfl(rce[NRUN - 1], (int)(g0 + ST_G - 1), 64);
+    uint32_t wRAW = RAW;
+#pragma unroll
+    for (int d = ST_G; d < 64; d <<= 1) wRAW = max(wRAW, (uint32_t)__shfl_xor(wRAW, d, 64));
     uint32_t cursor = E_in;
-    uint64_t rem = runmask;
-    for (uint32_t ri = 0; ri < wnrun; ++ri) {
-        const bool has = rem != 0;
-        const int src = has ? (int)__builtin_ctzll(rem) : (int)lane;
-        rem &= rem - 1;
-        uint32_t st[NRUN], len[NRUN];
-        st[0] = __shfl(r0.x, src, 64); st[1] = __shfl(r0.y, src, 64); st[2] = __shfl(r0.z, src, 64);
-        st[3] = __shfl(r0.w, src, 64); st[4] = __shfl(r1.x, src, 64); st[5] = __shfl(r1.y, src, 64);
-        st[6] = __shfl(r3.x, src, 64);
-        len[0] = __shfl(r1.z, src, 64); len[1] = __shfl(r1.w, src, 64); len[2] = __shfl(r2.x, src, 64);
-        len[3] = __shfl(r2.y, src, 64); len[4] = __shfl(r2.z, src, 64); len[5] = __shfl(r2.w, src, 64);
-        len[6] = __shfl(r3.y, src, 64);
-        const uint32_t mk = __shfl(r3.z, src, 64);
-        const uint32_t raw = has ? __shfl(rawk, src, 64) : 0u;
-        const uint32_t kj = (uint32_t)(src - (int)g0);
-        uint32_t wr = raw;
+    for (uint32_t c0 = 0; c0 < wRAW; c0 += ST_G * ST_U) {
+        uint32_t x[ST_U], ex[ST_U], kd[ST_U], kk[ST_U], mk[ST_U];
+        bool in[ST_U], r3q[ST_U];
 #pragma unroll
-        for (int d = ST_G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
-        for (uint32_t c0 = 0; c0 < wr; c0 += ST_G) {
-            const uint32_t off = c0 + sub;
-            bool keep = false;
-            uint32_t x = 0;
-            if (off < raw) {
-                uint32_t idx = 0, acc = 0;
-                bool r3run = false, found = false;
+        for (int u = 0; u < ST_U; ++u) {
+            const uint32_t off = c0 + (uint32_t)u * ST_G + sub;
+            in[u] = off < RAW;
+            uint32_t k = 0;   // key lane: lanes of the group whose runs end at or before off
 #pragma unroll
-                for (int q = 0; q < NRUN; ++q) {
-                    if (!found && off < acc + len[q]) { found = true; idx = st[q] + (off - acc); r3run = q == 6; }
-                    acc += len[q];
-                }
-                if (r3run) {
-                    x = s.v.bc_rank[idx];
-                    keep = s.v.bc_exec[idx] >= mk && ((c.wk >> s.v.bc_kind[idx]) & 1u);
-                } else {
-                    x = s.v.list_rank[idx];
-                    keep = true;
-                }
-                keep = keep && !(c.bq && x == c.trank);
+            for (uint32_t step = ST_G / 2; step >= 1; step >>= 1) {
+                const uint32_t end = __shfl(rce[NRUN - 1], (int)(g0 + k + step - 1), 64);
+                if (end <= off) k += step;
             }
+            k = min(k, (uint32_t)ST_G - 1);
+            const int src = (int)(g0 + k);
+            // cumulative ends of key k's runs: run q = the first with end > off
+            uint32_t ends[NRUN], sts[NRUN];
+#pragma unroll
+            for (int r = 0; r < NRUN; ++r) { ends[r] = __shfl(rce[r], src, 64); sts[r] = __shfl(rst[r], src, 64); }
+            uint32_t q = 0, start = 0;
+            uint32_t prev = ends[NRUN - 1] - __shfl(rawk, src, 64);   // start of key k in the flattened space
+#pragma unroll
+            for (int r = 0; r < NRUN; ++r) if (ends[r] <= off) { q = (uint32_t)r + 1; prev = ends[r]; }
+            q = min(q, (uint32_t)NRUN - 1);
+#pragma unroll
+            for (int r = 0; r < NRUN; ++r) if ((uint32_t)r == q) start = sts[r];
+            mk[u] = __shfl(r3.z, src, 64);
+            kk[u] = k;
+            r3q[u] = q == NRUN - 1;
+            const uint32_t idx = start + (off - prev);
+            const uint32_t *colp = r3q[u] ? s.v.bc_rank : s.v.list_rank;
+            x[u] = in[u] ? colp[idx] : 0u;
+            ex[u] = in[u] && r3q[u] ? s.v.bc_exec[idx] : 0u;
+            kd[u] = in[u] && r3q[u] ? (uint32_t)s.v.bc_kind[idx] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < ST_U; ++u) {
+            bool keep = in[u] && (!r3q[u] || (ex[u] >= mk[u] && ((c.wk >> kd[u]) & 1u)));
+            keep = keep && !(c.bq && x[u] == c.trank);
             const uint64_t bal = __ballot(keep) & gmask;
             if (keep) {
                 const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x << 4) | (EntT)kj;
+                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x[u] << 4) | (EntT)kk[u];
             }
             cursor += (uint32_t)__popcll(bal);
         }
@@ -2166,7 +2194,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
         const uint32_t before = (uint32_t)__popcll(peers & lt);
         if (in) {
             stA[grp][Kd + kbase[grp][kj] + kc[grp][kj] + before] = (uint16_t)idx;
-            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = s.txn_of_rank[(uint32_t)(x >> 4)];
+            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = (uint32_t)(x >> 4);   // rank: k_v3_ucompact maps it to the TxnId
         }
         __builtin_amdgcn_wave_barrier();
         if (in && before == 0) kc[grp][kj] += (uint32_t)__popcll(peers);
@@ -2226,7 +2254,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
                                                        const uint64_t *__restrict__ arena_off, const uint64_t *__restrict__ kd_off,
                                                        const uint32_t *__restrict__ bigflag, const uint32_t *__restrict__ key_off,
                                                        const uint64_t *__restrict__ vdep_off, const uint32_t *__restrict__ dep_scr,
-                                                       const uint32_t *__restrict__ dep_big, uint32_t *__restrict__ dep_txn)
+                                                       const uint32_t *__restrict__ dep_big, const uint32_t *__restrict__ txn_of_rank,
+                                                       uint32_t *__restrict__ dep_txn)
 {
     __shared__ uint64_t uo[BLOCK + 1];
     __shared__ uint64_t src[BLOCK];
@@ -2249,7 +2278,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
             uint32_t lo = tlo, hi = thi + 1;
             while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (u_off[m] <= i) lo = m; else hi = m; }
             const uint64_t sb = source(lo), off = i - u_off[lo];
-            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
+            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : txn_of_rank[dep_scr[sb + off]];
         }
         return;
     }
@@ -2267,7 +2296,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
         for (uint64_t i = lo + tid; i < hi; i += BLOCK) {
             const uint32_t a = last_le(uo, nt, i);
             const uint64_t sb = src[a], off = i - uo[a];
-            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
+            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : txn_of_rank[dep_scr[sb + off]];
         }
     }
 }
@@ -2862,7 +2891,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
         launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n,
                (const uint64_t *)u_off, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
-               (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr, dep_txn);
+               (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr,
+               (const uint32_t *)txn_of_rank, dep_txn);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));

@@ -92,6 +92,167 @@ __global__ __launch_bounds__(BLOCK) void k_lv_waves(uint32_t n, const uint32_t *
     if (lane == 0 && my_max) atomicMax(max_level, my_max);
 }
 
+// ---- LDS tier (n <= LV_LDS_MAX_N): one 1024-thread workgroup walks the whole graph with every level in LDS, so a
+// dependency hop costs an LDS round trip instead of a cross-XCD memory round trip (~2 us per level above).
+//
+// 1. k_lv_fcount / k_lv_fwrite (whole GPU, wave per exec-order position i): the waiting deps of txn order_exec[i]
+//    (exec rank below its own, Commands.java:804-810) as their exec-order positions, u16, in exec order: a CSR
+//    (foff, fdep) the walker streams front to back.
+// 2. k_lv_lds: fdep is consumed in chunks of CH entries; round c walks the positions whose lists end in chunk c
+//    (rstart[c] .. rstart[c+1]) while chunk c+1 is in flight into registers, then stored to LDS (three chunk slots:
+//    a list of <= CH entries spans chunks c-1 and c; longer lists are read from HBM). Group g (16 lanes) of the
+//    workgroup takes positions rstart[c] + g + 64 j; a wave's four groups advance together and re-read their deps'
+//    levels until every one is published, which always terminates: the smallest unfinished position has all of its
+//    deps finished and its wave is on it.
+constexpr int LV_LDS = 69632;          // u16 slots of LDS: levels (level + 1, 0 = unpublished) + three chunk slots
+constexpr int LV_FB = 2048;            // foff entries of a round staged in LDS (x2 buffers); beyond: read from HBM
+constexpr uint32_t LV_LDS_MAX_N = 65535;
+constexpr int LV_NT = 1024;
+constexpr int LV_G = 16;               // lanes per position
+constexpr int LV_GROUPS = LV_NT / LV_G;
+constexpr uint32_t LV_CH_MAX = 16384;  // entries per chunk
+constexpr int LV_PF = LV_CH_MAX / 8 / LV_NT;   // uint4 of a chunk per thread
+
+__global__ __launch_bounds__(BLOCK) void k_lv_fcount(uint32_t n, const uint32_t *__restrict__ order_exec,
+                                                     const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
+                                                     const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ cnt)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= n) return;
+    const uint32_t t = order_exec[i], er = exec_rank[t];
+    const uint64_t a = off[t], b = off[t + 1];
+    uint32_t c = 0;
+    for (uint64_t e = a + lane; e < b; e += 64) c += exec_rank[dep[e]] < er;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane == 0) cnt[i] = c;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_lv_fwrite(uint32_t n, const uint32_t *__restrict__ order_exec,
+                                                     const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
+                                                     const uint32_t *__restrict__ exec_rank, const uint32_t *__restrict__ pos,
+                                                     const uint32_t *__restrict__ foff, uint16_t *__restrict__ fdep)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= n) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t t = order_exec[i], er = exec_rank[t];
+    const uint64_t a = off[t], b = off[t + 1];
+    uint32_t w = foff[i];
+    for (uint64_t c0 = a; c0 < b; c0 += 64) {
+        const uint64_t e = c0 + lane;
+        uint32_t d = 0;
+        bool keep = false;
+        if (e < b) { d = dep[e]; keep = exec_rank[d] < er; }
+        const uint64_t bal = __ballot(keep);
+        if (keep) fdep[w + (uint32_t)__popcll(bal & lt)] = (uint16_t)pos[d];
+        w += (uint32_t)__popcll(bal);
+    }
+}
+
+// rstart[c] = first position whose list ends in chunk >= c (lists ending at entry 0 count as chunk 0); rstart[R] = n
+__global__ __launch_bounds__(BLOCK) void k_lv_rounds(uint32_t n, uint32_t R, int ch_shift, const uint32_t *__restrict__ foff,
+                                                     uint32_t *__restrict__ rstart)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    auto round_of = [&](uint32_t j) { const uint32_t e = foff[j + 1]; return e == 0 ? 0u : (e - 1) >> ch_shift; };
+    const uint32_t r = round_of(i);
+    const uint32_t rp = i == 0 ? 0u : round_of(i - 1) + 1;
+    for (uint32_t c = i == 0 ? 0u : rp; c <= r; ++c) rstart[c] = i;
+    if (i == n - 1)
+        for (uint32_t c = r + 1; c <= R; ++c) rstart[c] = n;
+}
+
+__device__ __forceinline__ uint32_t lv_lds_ld(const uint16_t *p) { return *(const volatile uint16_t *)p; }
+
+__global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, uint32_t R, int ch_shift, uint32_t Ef,
+                                                  const uint32_t *__restrict__ foff, const uint16_t *__restrict__ fdep,
+                                                  const uint32_t *__restrict__ rstart, const uint32_t *__restrict__ order_exec,
+                                                  uint32_t *__restrict__ level, uint32_t *__restrict__ max_level)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t L[LV_LDS];
+    __shared__ uint32_t fb[2][LV_FB];   // foff of the round's positions (double-buffered)
+    const uint32_t CH = 1u << ch_shift;
+    uint16_t *lvl = L, *slots = L + npad;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_G - 1), wave = tid >> 6, gi = lane >> 4;
+    for (uint32_t i = tid; i < n; i += LV_NT) lvl[i] = 0;
+    // chunk c -> slot c % 3: CH / 8 uint4 of fdep (reads may run past Ef into the buffer's padding)
+    const uint32_t nv = CH / 8;
+    const uint4 *src4 = reinterpret_cast<const uint4 *>(fdep);
+    uint4 *dst4 = reinterpret_cast<uint4 *>(slots);
+    if (Ef) for (uint32_t v = tid; v < nv; v += LV_NT) dst4[v] = src4[v];
+    uint32_t r0 = rstart[0], r1 = R >= 1 ? rstart[1] : n, r2 = R >= 2 ? rstart[2] : n;
+    for (uint32_t v = tid; v < LV_FB && r0 + v <= r1; v += LV_NT) fb[0][v] = foff[r0 + v];
+    __syncthreads();
+    uint32_t my_max = 0;
+    for (uint32_t c = 0; c < R; ++c) {
+        // in flight during the walk: chunk c + 1 of fdep, foff of round c + 1, rstart[c + 3]
+        static_assert(LV_PF == 2 && LV_FB == 2 * LV_NT, "two prefetch slots per thread");
+        uint4 pf0 = {}, pf1 = {};
+        uint32_t pfo0 = 0, pfo1 = 0;
+        const bool pfc = (uint64_t)(c + 1) * CH < Ef;
+        const uint4 *nsrc = src4 + (size_t)(c + 1) * nv;
+        if (pfc && tid < nv) pf0 = nsrc[tid];
+        if (pfc && tid + LV_NT < nv) pf1 = nsrc[tid + LV_NT];
+        const bool pfr = c + 1 < R;
+        if (pfr && r1 + tid <= r2) pfo0 = foff[r1 + tid];
+        if (pfr && r1 + tid + LV_NT <= r2) pfo1 = foff[r1 + tid + LV_NT];
+        const uint32_t r3 = c + 3 <= R ? rstart[c + 3] : n;
+        const uint32_t p0 = r0, p1 = r1;
+        const uint32_t *fo = fb[c & 1];
+        const uint64_t lo_res = c == 0 ? 0ull : (uint64_t)(c - 1) * CH;   // first entry resident in LDS
+        for (uint32_t base = p0 + 4 * wave; base < p1; base += LV_GROUPS) {
+            // wave w holds positions base + {0..3}; the waves stride by 64 positions
+            const uint32_t i = base + gi;
+            const bool valid = i < p1;
+            uint32_t a = 0, b = 0;
+            if (valid) {
+                const uint32_t k = i - p0;
+                if (k + 1 < LV_FB) { a = fo[k]; b = fo[k + 1]; }
+                else { a = foff[i]; b = foff[i + 1]; }
+            }
+            bool done = !valid;
+            while (true) {
+                if (!done) {   // group-uniform
+                    uint32_t m = 0;
+                    bool pend = false;
+                    for (uint32_t e = a + sub; e < b; e += LV_G) {
+                        const uint32_t p = e >= lo_res ? slots[(size_t)((e >> ch_shift) % 3) * CH + (e & (CH - 1))]
+                                                       : (uint32_t)fdep[e];
+                        const uint32_t v = lv_lds_ld(&lvl[p]);
+                        pend |= v == 0;
+                        m = max(m, v);
+                    }
+                    uint32_t pd = pend ? 1u : 0u;
+#pragma unroll
+                    for (int d = 1; d < LV_G; d <<= 1) {
+                        m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                        pd |= (uint32_t)__shfl_xor(pd, d, 64);
+                    }
+                    if (!pd) {
+                        if (sub == 0) *(volatile uint16_t *)&lvl[i] = (uint16_t)(m + 1);
+                        my_max = max(my_max, m);
+                        done = true;
+                    }
+                }
+                if (__all(done)) break;
+            }
+        }
+        uint4 *ndst = dst4 + (size_t)((c + 1) % 3) * nv;
+        if (pfc && tid < nv) ndst[tid] = pf0;
+        if (pfc && tid + LV_NT < nv) ndst[tid + LV_NT] = pf1;
+        if (pfr && r1 + tid <= r2) fb[(c + 1) & 1][tid] = pfo0;
+        if (pfr && r1 + tid + LV_NT <= r2) fb[(c + 1) & 1][tid + LV_NT] = pfo1;
+        r0 = r1; r1 = r2; r2 = r3;
+        __syncthreads();
+    }
+    for (uint32_t i = tid; i < n; i += LV_NT) level[order_exec[i]] = (uint32_t)lvl[i] - 1u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor(my_max, d, 64));
+    if (lane == 0 && my_max) atomicMax(max_level, my_max);
+}
+
 // published level + 1 -> level
 __global__ __launch_bounds__(BLOCK) void k_lv_unbias(uint32_t n, uint32_t *__restrict__ level)
 {
@@ -144,13 +305,46 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     if (e0 & 2) fail(ACC_E_ARG, "dependency index out of range");
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
-    ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
     ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
-    // a persistent grid of up to 4096 waves (16 per CU): enough txns in flight to cover the memory round trips
-    const uint32_t waves = std::min<uint32_t>(n, 4096u);
-    launch(ctx, "lv_walk", k_lv_waves, dim3((waves + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep,
-           exec_rank, level, maxl + 1, maxl);
-    launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
+    // tier: the whole graph's levels in one workgroup's LDS when they fit (chunk size CH: a power of two, three
+    // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
+    const uint32_t npad = (n + 7u) & ~7u;
+    uint32_t ch = 0;
+    if (n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
+        const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
+        uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
+        if (const char *ce = getenv("ACC_LV_CH")) cap = std::min<uint32_t>(cap, (uint32_t)std::max(1, atoi(ce)));
+        ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
+    }
+    if (ch) {
+        uint32_t *fcnt = ctx->get<uint32_t>("lv_fcnt", n);
+        uint32_t *foff = ctx->get<uint32_t>("lv_foff", (size_t)n + 1);
+        const unsigned gw = (n + WAVES - 1) / WAVES;
+        launch(ctx, "lv_fcount", k_lv_fcount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank, fcnt);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, fcnt, foff, n, true, foff + n);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, foff + n, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        uint32_t Ef;
+        memcpy(&Ef, ctx->pinned, 4);
+        uint16_t *fdep = ctx->get<uint16_t>("lv_fdep", (size_t)Ef + ch);   // + one chunk of padding for whole-chunk reads
+        launch(ctx, "lv_fwrite", k_lv_fwrite, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
+               (const uint32_t *)pos, (const uint32_t *)foff, fdep);
+        const int ch_shift = 31 - __builtin_clz(ch);
+        const uint32_t R = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)Ef + ch - 1) >> ch_shift));
+        uint32_t *rstart = ctx->get<uint32_t>("lv_rstart", (size_t)R + 1);
+        launch(ctx, "lv_rounds", k_lv_rounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, R, ch_shift, (const uint32_t *)foff, rstart);
+        launch(ctx, "lv_walk", k_lv_lds, dim3(1), dim3(LV_NT), 0, n, npad, R, ch_shift, Ef, (const uint32_t *)foff,
+               (const uint16_t *)fdep, (const uint32_t *)rstart, (const uint32_t *)order_exec, level, maxl);
+        ctx->stat("levelise.lds_rounds", R);
+    } else {
+        ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
+        // a persistent grid of up to 4096 waves (16 per CU): enough txns in flight to cover the memory round trips
+        const uint32_t waves = std::min<uint32_t>(n, 4096u);
+        launch(ctx, "lv_walk", k_lv_waves, dim3((waves + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep,
+               exec_rank, level, maxl + 1, maxl);
+        launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
+        ctx->stat("levelise.lds_rounds", 0);
+    }
     const int pbits = bits_for(n - 1);
     launch(ctx, "lv_order_keys", k_lv_order_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)level,
            (const uint32_t *)pos, pbits, key);

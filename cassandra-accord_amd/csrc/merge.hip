@@ -254,7 +254,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_key_of_slot(uint64_t R, const uint6
 //
 // A group whose replies fit (<= ML_REP replies, <= ML_KC key slots, <= ML_VC TxnId slots, <= ML_OC keysToTxnIds
 // slots; config 5: 64 replies, 512 / ~2000 / ~2500) is merged entirely in LDS: its key, TxnId and (key, TxnId)
-// records are loaded once with coalesced reads, bitonic-sorted and de-duplicated in LDS, and the Java-layout result is
+// records are loaded once with coalesced reads, merged (every reply's run is sorted) and de-duplicated in LDS, and the Java-layout result is
 // written to scratch at the group's input offsets (the union is never larger than the input), then compacted. The
 // per-reply validation of k_m_prep (KeyDeps ctor / checkValid) is done on the same loaded records.
 
@@ -290,20 +290,60 @@ __global__ __launch_bounds__(BLOCK) void k_m_fit(uint32_t ng, const uint64_t *__
     }
 }
 
+// Block-wide merge of NR sorted runs of src[0, N) (run r = [rs[r], rs[r + 1]), rs[NR] = N; rs is overwritten):
+// ceil(log2 NR) levels, each merging run pairs with merge-path partitions of ceil(N / BLOCK) outputs per thread,
+// ping-ponging between src and dst. Returns the buffer holding the sorted N elements. Every KeyDeps.merge input is
+// already sorted per reply (keys, TxnIds, and (key, TxnId) entries once mapped through the monotone merged indices),
+// so this replaces a bitonic network's O(log^2 N) barrier stages by O(log NR).
 template <class T>
-__device__ __forceinline__ void lds_bitonic(T *s, uint32_t np)
+__device__ T *lds_merge_runs(T *src, T *dst, uint32_t *rs, uint32_t NR, uint32_t N)
 {
-    for (uint32_t k = 2; k <= np; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < np; i += BLOCK) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    T a = s[i], b = s[ixj];
-                    if ((a > b) == ((i & k) == 0)) { s[i] = b; s[ixj] = a; }
+    const uint32_t tid = threadIdx.x;
+    const uint32_t CH = (N + BLOCK - 1) / BLOCK;
+    while (NR > 1) {
+        const uint32_t NP = (NR + 1) / 2;
+        const uint32_t o0 = min(N, tid * CH), o1 = min(N, o0 + CH);
+        if (o0 < o1) {
+            uint32_t lo = 0, hi = NP;   // last pair starting at or before o0
+            while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (rs[2 * m] <= o0) lo = m; else hi = m; }
+            uint32_t p = lo, q = o0;
+            while (q < o1) {
+                const uint32_t a0 = rs[2 * p], a1 = rs[min(2 * p + 1, NR)], b1 = rs[min(2 * p + 2, NR)];
+                const uint32_t la = a1 - a0, lb = b1 - a1, end = min(o1, b1), d = q - a0;
+                uint32_t i0 = d > lb ? d - lb : 0, i1 = min(d, la);
+                while (i0 < i1) {
+                    const uint32_t m = (i0 + i1) >> 1;
+                    if (src[a0 + m] < src[a1 + d - 1 - m]) i0 = m + 1; else i1 = m;
                 }
+                uint32_t i = i0, j = d - i0;
+                for (; q < end; ++q) {
+                    const bool takeA = j >= lb || (i < la && src[a0 + i] < src[a1 + j]);
+                    dst[q] = takeA ? src[a0 + i] : src[a1 + j];
+                    i += takeA; j += !takeA;
+                }
+                ++p;
             }
-            __syncthreads();
         }
+        __syncthreads();
+        const uint32_t nv = tid < NP ? rs[2 * tid] : 0u;
+        __syncthreads();
+        if (tid < NP) rs[tid] = nv;
+        if (tid == 0) rs[NP] = N;
+        __syncthreads();
+        NR = NP;
+        T *sw = src; src = dst; dst = sw;
+    }
+    return src;
+}
+
+// pads s[N, up to a multiple of BLOCK) for lds_unique
+template <class T>
+__device__ __forceinline__ uint32_t lds_pad_block(T *s, uint32_t N, T pad)
+{
+    const uint32_t np = (N + BLOCK - 1) / BLOCK * BLOCK;
+    for (uint32_t i = N + threadIdx.x; i < np; i += BLOCK) s[i] = pad;
+    __syncthreads();
+    return np;
 }
 
 // order-preserving in-place unique of the sorted s[0..np) (pads last); returns the count. np = BLOCK * per.
@@ -330,13 +370,6 @@ __device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t np, T pad, uint32_
         if ((uint32_t)q < per && ((f >> q) & 1u)) s[o++] = x[q];
     __syncthreads();
     return total;
-}
-
-__device__ __forceinline__ uint32_t pow2_at_least(uint32_t n)
-{
-    uint32_t p = BLOCK;
-    while (p < n) p <<= 1;
-    return p;
 }
 
 __device__ __forceinline__ uint32_t lds_ub(const uint32_t *a, uint32_t n, uint32_t v)   // first index with a[i] > v
@@ -367,15 +400,18 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
                                                  const int32_t *__restrict__ k2v, MlPlan pl, MlOut o)
 {
     extern __shared__ uint64_t dsm[];
-    // [rawk: kc u64][sort: sp u32][rawv: vc u32][rawo: oc u32][hdr: kc u32]
+    // [rawk: kc u64][sort: 2 x sp u32 (merge ping-pong)][rawv: vc u32][rawo: oc u32][hdr: kc u32]
     uint64_t *rawk = dsm;
     uint32_t *sort32 = reinterpret_cast<uint32_t *>(dsm + pl.kc);
+    uint32_t *sort32b = sort32 + pl.sp;
     uint64_t *sort64 = reinterpret_cast<uint64_t *>(sort32);
-    uint32_t *rawv = sort32 + pl.sp;
+    uint64_t *sort64b = reinterpret_cast<uint64_t *>(sort32b);
+    uint32_t *rawv = sort32 + 2 * pl.sp;
     uint32_t *rawo = rawv + pl.vc;
     uint32_t *hdr = rawo + pl.oc;
     __shared__ uint32_t rk[ML_REP + 1], rv[ML_REP + 1], ro[ML_REP + 1];
     __shared__ uint32_t scan_lds[WAVES];
+    __shared__ uint32_t rsm[ML_REP + 1];   // run starts of the merge tree
     const uint32_t gi = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     const uint64_t R0 = grp_off[gi];
@@ -397,8 +433,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
     const uint64_t PADK = ~0ull;
     const uint32_t PAD32 = 0xFFFFFFFFu;
     // ---- keys: sort, unique, write, map every key slot to its merged index
-    const uint32_t NKP = pow2_at_least(NK);
-    for (uint32_t i = tid; i < NKP; i += BLOCK) {
+    for (uint32_t i = tid; i < NK; i += BLOCK) {
         uint64_t x = PADK;
         if (i < NK) {
             const uint32_t r = lds_ub(rk, nrep + 1, i) - 1;
@@ -407,18 +442,19 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort64[i] = x;
     }
+    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = rk[r];
     __syncthreads();
-    lds_bitonic(sort64, NKP);
-    const uint32_t Kg = lds_unique<uint64_t, ML_KC / BLOCK>(sort64, NKP, PADK, scan_lds);
+    uint64_t *ks = lds_merge_runs(sort64, sort64b, rsm, nrep, NK);
+    const uint32_t Kg = lds_unique<uint64_t, ML_KC / BLOCK>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
     uint32_t kmap[ML_KC / BLOCK];
 #pragma unroll
     for (int q = 0; q < ML_KC / BLOCK; ++q) {
         const uint32_t i = tid + q * BLOCK;
-        if (i < Kg) o.s_key[KA + i] = sort64[i];
+        if (i < Kg) o.s_key[KA + i] = ks[i];
         if (i < NK) {
             const uint64_t kc = rawk[i];
             uint32_t a = 0, b = Kg;
-            while (a < b) { uint32_t m = (a + b) >> 1; if (sort64[m] < kc) a = m + 1; else b = m; }
+            while (a < b) { uint32_t m = (a + b) >> 1; if (ks[m] < kc) a = m + 1; else b = m; }
             kmap[q] = a;
         }
     }
@@ -430,8 +466,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         if (i < NK) kidx[i] = kmap[q];
     }
     // ---- TxnIds: same
-    const uint32_t NVP = pow2_at_least(NV);
-    for (uint32_t i = tid; i < NVP; i += BLOCK) {
+    for (uint32_t i = tid; i < NV; i += BLOCK) {
         uint32_t x = PAD32;
         if (i < NV) {
             const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
@@ -440,20 +475,19 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort32[i] = x;
     }
+    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = rv[r];
     __syncthreads();
-    lds_bitonic(sort32, NVP);
-    const uint32_t Ug = lds_unique<uint32_t, ML_VC / BLOCK>(sort32, NVP, PAD32, scan_lds);
+    uint32_t *vs = lds_merge_runs(sort32, sort32b, rsm, nrep, NV);
+    const uint32_t Ug = lds_unique<uint32_t, ML_VC / BLOCK>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
     for (uint32_t i = tid; i < NV; i += BLOCK) {
         const uint32_t v = rawv[i];
         uint32_t a = 0, b = Ug;
-        while (a < b) { uint32_t m = (a + b) >> 1; if (sort32[m] < v) a = m + 1; else b = m; }
+        while (a < b) { uint32_t m = (a + b) >> 1; if (vs[m] < v) a = m + 1; else b = m; }
         rawv[i] = a;   // each thread rewrites only its own slots
     }
-    for (uint32_t u = tid; u < Ug; u += BLOCK) o.s_val[VA + u] = sort32[u];
+    for (uint32_t u = tid; u < Ug; u += BLOCK) o.s_val[VA + u] = vs[u];
     __syncthreads();
     // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
-    const uint32_t NEP = pow2_at_least(NE);
-    for (uint32_t e = tid + NE; e < NEP; e += BLOCK) sort32[e] = PAD32;
     for (uint32_t q = tid; q < NO; q += BLOCK) {
         const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
         const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
@@ -479,13 +513,14 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         sort32[q - rk[r + 1]] = x;
     }
     for (uint32_t k = tid; k < Kg; k += BLOCK) hdr[k] = 0;
+    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
     __syncthreads();
-    lds_bitonic(sort32, NEP);
-    const uint32_t Eu = lds_unique<uint32_t, ML_VC / BLOCK>(sort32, NEP, PAD32, scan_lds);
+    uint32_t *es = lds_merge_runs(sort32, sort32b, rsm, nrep, NE);
+    const uint32_t Eu = lds_unique<uint32_t, ML_VC / BLOCK>(es, lds_pad_block(es, NE, PAD32), PAD32, scan_lds);
     for (uint32_t c = tid; c < Eu; c += BLOCK) {
-        const uint32_t kk = sort32[c] >> 16;
-        if (c + 1 == Eu || (sort32[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
-        o.s_k2v[OA + Kg + c] = (int32_t)(sort32[c] & 0xFFFFu);
+        const uint32_t kk = es[c] >> 16;
+        if (c + 1 == Eu || (es[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
+        o.s_k2v[OA + Kg + c] = (int32_t)(es[c] & 0xFFFFu);
     }
     __syncthreads();
     // keys without entries: end offset = the previous key's (prefix max, starting at Kg)
@@ -572,14 +607,14 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gmax, 4 * 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
         if (ctx->pinned[0] == 0) {
-            auto p2 = [](uint64_t n) { uint64_t p = BLOCK; while (p < n) p <<= 1; return p; };
+            auto rb = [](uint64_t n) { return std::max<uint64_t>(BLOCK, (n + BLOCK - 1) / BLOCK * BLOCK); };
             MlPlan pl;
             pl.kc = (uint32_t)ctx->pinned[1];
             pl.vc = (uint32_t)ctx->pinned[2];
             pl.oc = (uint32_t)ctx->pinned[3];
-            pl.sp = (uint32_t)std::max({ 2 * p2(pl.kc), p2(pl.vc), p2(ctx->pinned[4]) });
+            pl.sp = (uint32_t)std::max({ 2 * rb(pl.kc), rb(pl.vc), rb(ctx->pinned[4]) });   // one merge buffer (u32)
             pl.kc = (pl.kc + 1) & ~1u;   // keep the u32 areas after rawk 8-byte aligned
-            pl.bytes = 8 * pl.kc + 4 * pl.sp + 4 * pl.vc + 4 * pl.oc + 4 * pl.kc;
+            pl.bytes = 8 * pl.kc + 8 * pl.sp + 4 * pl.vc + 4 * pl.oc + 4 * pl.kc;
             MlOut mo;
             mo.s_key = ctx->get<uint64_t>("m_s_key", NK + 1);
             mo.s_val = ctx->get<uint32_t>("m_s_val", NV + 1);

@@ -516,12 +516,34 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint64_t m = 0, x = ~0ull;
     if (live) {
+        // the txn's queries S at a time: one load round for their counts and offsets, a shuffle search for the
+        // query holding entry `sub`, one load round for the entry (not two dependent loads per query)
         uint32_t q0, q1;
         txn_queries(o, t, q0, q1);
-        for (uint32_t q = q0; q < q1; ++q) {
-            const uint32_t c = o.q_cnt[q];
-            if (sub >= m && sub < m + c) x = o.ent[o.q_off[q] + (sub - m)];
-            m += c;
+        const int gb = (int)(grp * S);
+        for (uint32_t qc = q0; qc < q1; qc += S) {   // group-uniform
+            const uint32_t q = qc + sub;
+            uint32_t c = 0;
+            uint64_t qo = 0;
+            if (q < q1) { c = o.q_cnt[q]; qo = o.q_off[q]; }
+            uint32_t incl = c;
+#pragma unroll
+            for (int d = 1; d < S; d <<= 1) {
+                const uint32_t u = __shfl_up(incl, d, 64);
+                if (sub >= (uint32_t)d) incl += u;
+            }
+            const uint32_t total = __shfl(incl, gb + S - 1, 64);
+            uint32_t j = 0;   // lanes whose queries end at or before entry sub
+#pragma unroll
+            for (int step = S / 2; step >= 1; step >>= 1) {
+                const uint32_t end = (uint32_t)m + __shfl(incl, gb + (int)j + step - 1, 64);
+                if (end <= sub) j += step;
+            }
+            j = min(j, (uint32_t)S - 1);
+            const uint64_t qoj = shfl_idx(qo, gb + (int)j);
+            const uint32_t startj = (uint32_t)m + __shfl(incl - c, gb + (int)j, 64);
+            if (sub >= m && sub < m + total) x = o.ent[qoj + (sub - startj)];
+            m += total;
         }
     }
     // sort within the group (groups are lane-aligned: the xor partners of k <= S stay inside)

@@ -35,7 +35,7 @@ def test_levelise_random(ctx, n, max_deps):
 
 @pytest.mark.parametrize("n", [5000, 30000, 200000])
 def test_levelise_long_chain(ctx, n):
-    """A hot-key write chain: every txn depends on its predecessor (depth n; 30000 takes the global-memory walk)."""
+    """A hot-key write chain: every txn depends on its predecessor (depth n; 200000 takes the persistent-wave walk)."""
     import oracle
     from accord_amd.deps import levelise
     er = np.arange(n, dtype=np.uint32)[::-1].copy()      # executeAt order reversed vs index
@@ -125,3 +125,40 @@ def test_levelise_one_million(ctx):
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
     assert nl == nl2 and nl > 1000
+
+
+@pytest.mark.parametrize("env,n,max_deps", [
+    ({"ACC_LV_CH": "64"}, 2000, 300),      # LDS tier, 64-entry chunks: lists longer than a chunk read from HBM
+    ({"ACC_LV_CH": "256"}, 20000, 12),     # many rounds, rounds of > 2048 positions (foff from HBM)
+    ({"ACC_LV_WAVES": "1"}, 5000, 30),     # the persistent-wave walk at a size the LDS tier would take
+    ({}, 65535, 6),                        # largest LDS-tier graph (u16 levels and positions)
+    ({}, 65536, 6),                        # smallest persistent-wave graph
+])
+def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps):
+    import oracle
+    from accord_amd.deps import levelise
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    off, dep, er = random_graph(np.random.RandomState(n + max_deps), n, max_deps)
+    lv, order, nl = levelise(ctx, off, dep, er)
+    l2, o2, nl2 = oracle.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == nl2
+
+
+def test_levelise_dense_prefix_chain(ctx):
+    """Every txn depends on all earlier txns by executeAt (depth n, lists up to n - 1 entries spanning chunks)."""
+    import oracle
+    from accord_amd.deps import levelise
+    n = 700
+    er = np.random.RandomState(7).permutation(n).astype(np.uint32)
+    pos = np.argsort(er)
+    deps = [np.sort(pos[:er[t]]) for t in range(n)]
+    off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
+    dep = np.concatenate(deps).astype(np.uint32)
+    lv, order, nl = levelise(ctx, off, dep, er)
+    l2, o2, nl2 = oracle.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == n
