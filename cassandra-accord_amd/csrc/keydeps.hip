@@ -989,8 +989,16 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         l[2 * c + 1] = q.rp.c[3 + c] - q.rm.c[3 + c];
         e += l[2 * c] + l[2 * c + 1];
     }
-    for (uint32_t i = q.bstart; i < q.bend; ++i)
-        if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) ++e;
+    for (uint32_t i = q.bstart; i < q.bend; i += 4) {   // R3 candidates, four loads in flight
+        uint32_t ex[4], kd[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            ex[u] = i + u < q.bend ? v.bc_exec[i + u] : 0u;
+            kd[u] = i + u < q.bend ? (uint32_t)v.bc_kind[i + u] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) e += (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u)) ? 1u : 0u;
+    }
     if (q.bq) {
         uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
@@ -1021,11 +1029,20 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         for (uint32_t s = 0; s < REC_INLINE; ++s) buf[s] = s < d ? xs[s] : xs[s + 1];
         uint32_t n = L6 - (d < L6 ? 1u : 0u);
         if (q.has_m)
-            for (uint32_t i = q.bstart; i < q.bend; ++i)
-                if (v.bc_exec[i] >= q.m && ((q.wk >> v.bc_kind[i]) & 1u)) {
-                    const uint32_t x = v.bc_rank[i];
-                    if (!(q.bq && x == q.trank)) inl_put(buf, n, x);
+            for (uint32_t i = q.bstart; i < q.bend; i += 4) {   // R3 candidates, four at a time
+                uint32_t ex[4], kd[4], xr[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const bool in = i + u < q.bend;
+                    ex[u] = in ? v.bc_exec[i + u] : 0u;
+                    kd[u] = in ? (uint32_t)v.bc_kind[i + u] : 0u;
+                    xr[u] = in ? v.bc_rank[i + u] : 0u;
                 }
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u)
+                    if (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u) && !(q.bq && xr[u] == q.trank))
+                        inl_put(buf, n, xr[u]);
+            }
         r[0] = make_uint4(buf[0], buf[1], buf[2], buf[3]);
         r[1] = make_uint4(buf[4], buf[5], buf[6], buf[7]);
         r[2] = make_uint4(buf[8], buf[9], buf[10], buf[11]);
@@ -2236,8 +2253,9 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigcopy(uint32_t nbig, const uint3
     for (uint64_t q = lane; q < K; q += 64) key_idx[kd + q] = key_scr[ks + q];
 }
 
-// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: at its entry offset arena_off - kd_off in
-// dep_scr; big txns: at vdep_off of its first pair in dep_big) to dep_txn[u_off[t] ...). A block takes a fixed chunk
+// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: TxnId ranks at its slot t * ST_N2 of
+// dep_scr, mapped through txn_of_rank here; big txns: TxnIds at vdep_off of its first pair in dep_big) to
+// dep_txn[u_off[t] ...). A block takes a fixed chunk
 // of UC_CHUNK outputs (the uncommitted window's txns are consecutive and hold most TxnIds: partitioning by txns left a
 // few blocks with most of the work), finds the txns spanning it by binary search over u_off, and strides over the
 // chunk in windows of BLOCK txns (u_off / source bases in LDS, each output's txn by binary search there).
@@ -2293,10 +2311,27 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
         if (tid == 0) uo[nt] = u_off[tw + nt];
         __syncthreads();
         const uint64_t lo = max(c0, uo[0]), hi = min(c1, uo[nt]);
-        for (uint64_t i = lo + tid; i < hi; i += BLOCK) {
-            const uint32_t a = last_le(uo, nt, i);
-            const uint64_t sb = src[a], off = i - uo[a];
-            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : txn_of_rank[dep_scr[sb + off]];
+        constexpr int U = 4;   // outputs per thread whose scratch and TxnId loads are in flight together
+        for (uint64_t i0 = lo + tid; i0 < hi; i0 += U * BLOCK) {
+            uint32_t x[U];
+            bool big[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = i0 + (uint64_t)u * BLOCK;
+                x[u] = 0; big[u] = false;
+                if (i < hi) {
+                    const uint32_t a = last_le(uo, nt, i);
+                    const uint64_t sb = src[a], off = i - uo[a];
+                    big[u] = (sb >> 63) != 0;
+                    x[u] = big[u] ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i0 + (uint64_t)u * BLOCK < hi && !big[u]) x[u] = txn_of_rank[x[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i0 + (uint64_t)u * BLOCK < hi) dep_txn[i0 + (uint64_t)u * BLOCK] = x[u];
         }
     }
 }
@@ -2817,8 +2852,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
         // on a side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
-        ctx->fork(1);
-        ctx->launch_stream = ctx->aux[0];
+        const bool side = !getenv("ACC_KD_SERIAL");   // tuning switch: the tiers in order on the main stream
+        if (side) {
+            ctx->fork(1);
+            ctx->launch_stream = ctx->aux[0];
+        }
         if (rbits + 6 <= 31) {
             launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
@@ -2879,7 +2917,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                 w, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
     }
 #endif
-    if (nbig) ctx->join(1);
+    if (nbig && !getenv("ACC_KD_SERIAL")) ctx->join(1);
     // ---- big txns' arena / keys into place, TxnId offsets and compaction. With global-path txns (known only after
     // the tiers ran) this is redone once they are written, so the common case pays one host sync here.
     auto finish = [&]() {

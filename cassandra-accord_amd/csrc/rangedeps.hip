@@ -346,7 +346,40 @@ struct StabTile {
     uint64_t base;
 };
 
-// One pass over the block's windows: EMIT = false counts this query's pairs, EMIT = true writes them at out.
+// One pass over the block's windows: EMIT = false counts this query's pairs, EMIT = true writes them at out. The
+// (class, tile) sequence is software-pipelined: the next tile's entries are loaded into registers while the current
+// one is scanned from LDS, so a block pays one memory latency per pass instead of one per tile.
+constexpr int ST_PT = TILE / BLOCK;   // tile entries per thread
+
+struct StabRegs {
+    uint64_t s[ST_PT], e[ST_PT];
+    uint2 info[ST_PT];
+    uint32_t kind[ST_PT];
+};
+
+__device__ __forceinline__ void stab_load(const View &v, StabRegs &g, uint32_t base, uint32_t len)
+{
+#pragma unroll
+    for (int u = 0; u < ST_PT; ++u) {
+        const uint32_t k = threadIdx.x + (uint32_t)u * BLOCK;
+        if (k < len) {
+            g.s[u] = v.cs_s[base + k];
+            g.e[u] = v.cs_e[base + k];
+            g.info[u] = v.cs_info[base + k];
+            g.kind[u] = v.cs_kind[base + k];
+        }
+    }
+}
+
+// next non-empty (class, tile) after (c, base) (c = NCLS: none)
+__device__ __forceinline__ void stab_next(const StabTile &T, uint32_t &c, uint32_t &base)
+{
+    base += TILE;
+    if (c < (uint32_t)NCLS && base < T.b1[c]) return;
+    for (++c; c < (uint32_t)NCLS; ++c)
+        if (T.b0[c] < T.b1[c]) { base = T.b0[c]; return; }
+}
+
 template <bool EMIT>
 __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t lo_min,
                                               uint64_t hi_max, uint64_t out)
@@ -355,40 +388,44 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
     const bool isr = (r.flags >> 8) & 1u;
     const uint32_t wm = r.flags & 0xFFu;
     uint32_t count = 0;
-    for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
-        const uint32_t b0 = T.b0[c], b1 = T.b1[c];
-        if (b0 >= b1) continue;
-        const uint64_t W = class_width(c);
-        const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
-        for (uint32_t base = b0; base < b1; base += TILE) {
-            const uint32_t len = min((uint32_t)TILE, b1 - base);
-            for (uint32_t k = tid; k < len; k += BLOCK) {
-                T.s[k] = v.cs_s[base + k];
-                T.e[k] = v.cs_e[base + k];
-                T.info[k] = v.cs_info[base + k];
-                T.kind[k] = v.cs_kind[base + k];
-            }
-            __syncthreads();
-            if (valid) {
-                // this query's own window inside the tile: starts in [lo - W, hi]
-                for (uint32_t k = lower_bound_s(T.s, 0, len, qwlo); k < len; ++k) {
-                    const uint64_t s = T.s[k];
-                    if (s > r.hi) break;
-                    const uint64_t e = T.e[k];
-                    bool hit;
-                    if (isr) hit = s < r.hi && e > r.lo;                           // Range.compareIntersecting == 0
-                    else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;         // EndInclusive.contains (s, e]
-                    else hit = s <= r.lo && r.lo < e;                              // StartInclusive.contains [s, e)
-                    if (!hit) continue;
-                    const uint2 info = T.info[k];
-                    if (info.y >= r.lim || info.y == r.tpos) continue;            // STARTED_BEFORE; p1
-                    if (!((wm >> T.kind[k]) & 1u)) continue;                      // testKind
-                    if (EMIT) v.ent[out + count] = ((uint64_t)info.x << 32) | info.y;
-                    ++count;
-                }
-            }
-            __syncthreads();
+    uint32_t c = 0, base = 0;
+    while (c < (uint32_t)NCLS && T.b0[c] >= T.b1[c]) ++c;
+    if (c < (uint32_t)NCLS) base = T.b0[c];
+    StabRegs g;
+    if (c < (uint32_t)NCLS) stab_load(v, g, base, min((uint32_t)TILE, T.b1[c] - base));
+    while (c < (uint32_t)NCLS) {
+        const uint32_t len = min((uint32_t)TILE, T.b1[c] - base);
+#pragma unroll
+        for (int u = 0; u < ST_PT; ++u) {
+            const uint32_t k = tid + (uint32_t)u * BLOCK;
+            if (k < len) { T.s[k] = g.s[u]; T.e[k] = g.e[u]; T.info[k] = g.info[u]; T.kind[k] = (uint8_t)g.kind[u]; }
         }
+        __syncthreads();
+        uint32_t c2 = c, base2 = base;
+        stab_next(T, c2, base2);
+        if (c2 < (uint32_t)NCLS) stab_load(v, g, base2, min((uint32_t)TILE, T.b1[c2] - base2));
+        if (valid) {
+            const uint64_t W = class_width(c);
+            const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
+            // this query's own window inside the tile: starts in [lo - W, hi]
+            for (uint32_t k = lower_bound_s(T.s, 0, len, qwlo); k < len; ++k) {
+                const uint64_t s = T.s[k];
+                if (s > r.hi) break;
+                const uint64_t e = T.e[k];
+                bool hit;
+                if (isr) hit = s < r.hi && e > r.lo;                           // Range.compareIntersecting == 0
+                else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;         // EndInclusive.contains (s, e]
+                else hit = s <= r.lo && r.lo < e;                              // StartInclusive.contains [s, e)
+                if (!hit) continue;
+                const uint2 info = T.info[k];
+                if (info.y >= r.lim || info.y == r.tpos) continue;            // STARTED_BEFORE; p1
+                if (!((wm >> T.kind[k]) & 1u)) continue;                      // testKind
+                if (EMIT) v.ent[out + count] = ((uint64_t)info.x << 32) | info.y;
+                ++count;
+            }
+        }
+        __syncthreads();
+        c = c2; base = base2;
     }
     return count;
 }
@@ -606,17 +643,44 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
 }
 
 // One workgroup per txn over buffers A, B of n2 >= m elements (LDS sized to the tier, or global scratch)
-__device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, uint32_t *red)
+// qs / qo: LDS of BLOCK + 1 / BLOCK entries (query starts in the txn's raw list, query offsets in ent)
+__device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, uint32_t *red, uint32_t *qs, uint64_t *qo)
 {
     const uint32_t tid = threadIdx.x;
     uint32_t q0, q1;
     txn_queries(o, t, q0, q1);
     uint32_t m = 0;
-    for (uint32_t q = q0; q < q1; ++q) {
-        const uint32_t c = o.q_cnt[q];
-        const uint64_t off = o.q_off[q];
-        for (uint32_t k = tid; k < c; k += BLOCK) A[m + k] = o.ent[off + k];
-        m += c;
+    const uint32_t nq = q1 - q0;
+    if (nq <= (uint32_t)BLOCK) {
+        // every query's count and offset in one load round, then the raw entries four loads per thread at a time
+        uint32_t c = 0;
+        uint64_t off = 0;
+        if (tid < nq) { c = o.q_cnt[q0 + tid]; off = o.q_off[q0 + tid]; }
+        const uint32_t st = block_exclusive(c, OpAdd<uint32_t>(), red, m);
+        if (tid < nq) { qs[tid] = st; qo[tid] = off; }
+        __syncthreads();
+        for (uint32_t k0 = tid; k0 < m; k0 += 4 * BLOCK) {
+            uint64_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * BLOCK;
+                x[u] = 0;
+                if (k < m) {
+                    uint32_t lo = 0, hi = nq;   // last query starting at or before k
+                    while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (qs[md] <= k) lo = md; else hi = md; }
+                    x[u] = o.ent[qo[lo] + (k - qs[lo])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) if (k0 + (uint32_t)u * BLOCK < m) A[k0 + (uint32_t)u * BLOCK] = x[u];
+        }
+    } else {
+        for (uint32_t q = q0; q < q1; ++q) {
+            const uint32_t c = o.q_cnt[q];
+            const uint64_t off = o.q_off[q];
+            for (uint32_t k = tid; k < c; k += BLOCK) A[m + k] = o.ent[off + k];
+            m += c;
+        }
     }
     uint32_t n2 = 64;
     while (n2 < m) n2 <<= 1;
@@ -676,19 +740,24 @@ __device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, 
 __global__ __launch_bounds__(BLOCK) void k_rd_build_block(Out o, uint32_t n2)
 {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    // all LDS dynamic (no static __shared__ ahead of it: the base stays 16-B aligned, Guideline 17)
-    build_block(o, o.list[blockIdx.x], lds, lds + n2, reinterpret_cast<uint32_t *>(lds + 2 * n2));
+    // all LDS dynamic (no static __shared__ ahead of it: the base stays 16-B aligned, Guideline 17):
+    // [A: n2 u64][B: n2 u64][qo: BLOCK u64][red: 16 u32][qs: BLOCK + 1 u32]
+    uint64_t *qo = lds + 2 * n2;
+    uint32_t *red = reinterpret_cast<uint32_t *>(qo + BLOCK);
+    build_block(o, o.list[blockIdx.x], lds, lds + n2, red, red + 16, qo);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rd_build_global(Out o)
 {
     __shared__ uint32_t red[WAVES];
+    __shared__ uint32_t qs[BLOCK + 1];
+    __shared__ uint64_t qo[BLOCK];
     const uint32_t t = o.list[blockIdx.x];
     uint64_t *A = o.gscratch + o.glb_off[blockIdx.x];
     const uint64_t m = o.raw_off[t + 1] - o.raw_off[t];
     uint64_t n2 = 64;
     while (n2 < m) n2 <<= 1;
-    build_block(o, t, A, A + n2, red);
+    build_block(o, t, A, A + n2, red, qs, qo);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, Out o, uint64_t *__restrict__ sz)
@@ -711,9 +780,21 @@ __global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
     const uint64_t ra = o.raw_off[t];
     const uint64_t na = o.a_cnt[t], nr = o.rd_cnt[t], nu = o.u_cnt[t];
     const uint64_t ao = o.arena_off[t], ro = o.rd_off[t], uo = o.u_off[t];
-    for (uint64_t j = sub; j < na; j += 16) o.arena[ao + j] = (int32_t)o.s_arena[2 * ra + j];
-    for (uint64_t j = sub; j < nr; j += 16) o.range_id[ro + j] = o.s_rid[ra + j];
-    for (uint64_t j = sub; j < nu; j += 16) o.dep_txn[uo + j] = o.s_dep[ra + j];
+    // first round: up to 64 arena ints, 16 range ids and 16 TxnIds loaded together (one latency for most txns),
+    // then the rest
+    const uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
+    uint32_t a[4], r = 0, u = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = sub + 16u * k < na ? sa[sub + 16u * k] : 0u;
+    if (sub < nr) r = sr[sub];
+    if (sub < nu) u = sd[sub];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) if (sub + 16u * k < na) o.arena[ao + sub + 16u * k] = (int32_t)a[k];
+    if (sub < nr) o.range_id[ro + sub] = r;
+    if (sub < nu) o.dep_txn[uo + sub] = u;
+    for (uint64_t j = 64 + sub; j < na; j += 16) o.arena[ao + j] = (int32_t)sa[j];
+    for (uint64_t j = 16 + sub; j < nr; j += 16) o.range_id[ro + j] = sr[j];
+    for (uint64_t j = 16 + sub; j < nu; j += 16) o.dep_txn[uo + j] = sd[j];
 }
 
 }  // namespace rd
@@ -966,7 +1047,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     for (int b = 9; b >= 3; --b) {
         if (!hh[b]) continue;
         const uint32_t n2 = 128u << (b - 3);
-        const size_t lds = 2 * (size_t)n2 * sizeof(uint64_t) + 64;
+        const size_t lds = 2 * (size_t)n2 * sizeof(uint64_t) + BLOCK * 8 + 64 + (BLOCK + 1) * 4;
         if (lds > 64 * 1024)
             ACC_HIP(hipFuncSetAttribute((const void *)k_rd_build_block, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         o.list = tl_sorted + toff[b];
