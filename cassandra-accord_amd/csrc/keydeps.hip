@@ -1768,10 +1768,6 @@ constexpr int ST_G = 16;                      // lanes per txn
 constexpr int ST_K = 16;                      // keys of a stream txn
 constexpr int ST_N2 = 128;                    // dependency entries of a stream txn (LDS sort buffer, power of two)
 constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream txn
-#ifndef ACC_ST_U
-#define ACC_ST_U 4
-#endif
-constexpr int ST_U = ACC_ST_U;                // raw elements per lane whose loads are in flight together
 
 // Per txn, ST_G lanes: its KeyDeps sizes A = Kd + E (arena ints) and K = Kd (keys with >= 1 dependency) from the
 // count-pass records' word 15 (the exclusive scans of A and K are the txns' arena / key offsets, so the stream pass needs
@@ -1936,7 +1932,7 @@ struct V3Stream {
     const uint64_t *arena_off, *kd_off;       // from the size scans
     uint64_t *u_cnt_out;
     int32_t *arena;
-    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnId ranks at the txn's slot, mapped + compacted by k_v3_ucompact
+    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's slot t * ST_N2, compacted by k_v3_ucompact
     uint64_t *err;                            // gather count mismatches
     uint32_t n, ntiles;
 };
@@ -2079,68 +2075,58 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
             if (q < e) buf[b0 + q] = ((EntT)w[q] << 4) | (EntT)sub;
     }
     ST_PH(2);
-    // ---- run records: the group's runs flattened (run keys in lane order; within a key R1/R2 per class, then R3).
-    // Lane sub takes elements sub, sub + ST_G, ...; ST_U elements per round are located (key lane by a shuffle
-    // search over the group's inclusive raw counts, run by the key lane's cumulative run ends) and all their loads
-    // issued before any is used, so a group pays one memory latency per ST_G * ST_U raw elements instead of one per
-    // ST_G elements of each key. T itself and R3 entries below M or of unwitnessed kinds are dropped.
-    uint32_t rst[NRUN], rce[NRUN];
-    {
-        const uint32_t len[NRUN] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r3.y };
-        rst[0] = r0.x; rst[1] = r0.y; rst[2] = r0.z; rst[3] = r0.w; rst[4] = r1.x; rst[5] = r1.y; rst[6] = r3.x;
-        const uint32_t incl = group_inclusive(rawk, sub);   // rawk = 0 outside run lanes of stream txns
-        uint32_t acc = incl - rawk;
+    // ---- run records, one key at a time (its runs broadcast from the owning lane): the group gathers the flattened
+    // runs R1/R2 per class and R3, dropping T itself and R3 entries below M or of unwitnessed kinds, after the inline
+    // entries
+    const uint64_t runmask = __ballot(sm && run) & gmask;
+    const uint32_t nrun = (uint32_t)__popcll(runmask);
+    uint32_t wnrun = nrun;
 #pragma unroll
-        for (int q = 0; q < NRUN; ++q) { acc += run ? len[q] : 0u; rce[q] = acc; }
-    }
-    const uint32_t RAW = __shfl(rce[NRUN - 1], (int)(g0 + ST_G - 1), 64);
-    uint32_t wRAW = RAW;
-#pragma unroll
-    for (int d = ST_G; d < 64; d <<= 1) wRAW = max(wRAW, (uint32_t)__shfl_xor(wRAW, d, 64));
+    for (int d = ST_G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
     uint32_t cursor = E_in;
-    for (uint32_t c0 = 0; c0 < wRAW; c0 += ST_G * ST_U) {
-        uint32_t x[ST_U], ex[ST_U], kd[ST_U], kk[ST_U], mk[ST_U];
-        bool in[ST_U], r3q[ST_U];
+    uint64_t rem = runmask;
+    for (uint32_t ri = 0; ri < wnrun; ++ri) {
+        const bool has = rem != 0;
+        const int src = has ? (int)__builtin_ctzll(rem) : (int)lane;
+        rem &= rem - 1;
+        uint32_t st[NRUN], len[NRUN];
+        st[0] = __shfl(r0.x, src, 64); st[1] = __shfl(r0.y, src, 64); st[2] = __shfl(r0.z, src, 64);
+        st[3] = __shfl(r0.w, src, 64); st[4] = __shfl(r1.x, src, 64); st[5] = __shfl(r1.y, src, 64);
+        st[6] = __shfl(r3.x, src, 64);
+        len[0] = __shfl(r1.z, src, 64); len[1] = __shfl(r1.w, src, 64); len[2] = __shfl(r2.x, src, 64);
+        len[3] = __shfl(r2.y, src, 64); len[4] = __shfl(r2.z, src, 64); len[5] = __shfl(r2.w, src, 64);
+        len[6] = __shfl(r3.y, src, 64);
+        const uint32_t mk = __shfl(r3.z, src, 64);
+        const uint32_t raw = has ? __shfl(rawk, src, 64) : 0u;
+        const uint32_t kj = (uint32_t)(src - (int)g0);
+        uint32_t wr = raw;
 #pragma unroll
-        for (int u = 0; u < ST_U; ++u) {
-            const uint32_t off = c0 + (uint32_t)u * ST_G + sub;
-            in[u] = off < RAW;
-            uint32_t k = 0;   // key lane: lanes of the group whose runs end at or before off
+        for (int d = ST_G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
+        for (uint32_t c0 = 0; c0 < wr; c0 += ST_G) {
+            const uint32_t off = c0 + sub;
+            bool keep = false;
+            uint32_t x = 0;
+            if (off < raw) {
+                uint32_t idx = 0, acc = 0;
+                bool r3run = false, found = false;
 #pragma unroll
-            for (uint32_t step = ST_G / 2; step >= 1; step >>= 1) {
-                const uint32_t end = __shfl(rce[NRUN - 1], (int)(g0 + k + step - 1), 64);
-                if (end <= off) k += step;
+                for (int q = 0; q < NRUN; ++q) {
+                    if (!found && off < acc + len[q]) { found = true; idx = st[q] + (off - acc); r3run = q == 6; }
+                    acc += len[q];
+                }
+                if (r3run) {
+                    x = s.v.bc_rank[idx];
+                    keep = s.v.bc_exec[idx] >= mk && ((c.wk >> s.v.bc_kind[idx]) & 1u);
+                } else {
+                    x = s.v.list_rank[idx];
+                    keep = true;
+                }
+                keep = keep && !(c.bq && x == c.trank);
             }
-            k = min(k, (uint32_t)ST_G - 1);
-            const int src = (int)(g0 + k);
-            // cumulative ends of key k's runs: run q = the first with end > off
-            uint32_t ends[NRUN], sts[NRUN];
-#pragma unroll
-            for (int r = 0; r < NRUN; ++r) { ends[r] = __shfl(rce[r], src, 64); sts[r] = __shfl(rst[r], src, 64); }
-            uint32_t q = 0, start = 0;
-            uint32_t prev = ends[NRUN - 1] - __shfl(rawk, src, 64);   // start of key k in the flattened space
-#pragma unroll
-            for (int r = 0; r < NRUN; ++r) if (ends[r] <= off) { q = (uint32_t)r + 1; prev = ends[r]; }
-            q = min(q, (uint32_t)NRUN - 1);
-#pragma unroll
-            for (int r = 0; r < NRUN; ++r) if ((uint32_t)r == q) start = sts[r];
-            mk[u] = __shfl(r3.z, src, 64);
-            kk[u] = k;
-            r3q[u] = q == NRUN - 1;
-            const uint32_t idx = start + (off - prev);
-            const uint32_t *colp = r3q[u] ? s.v.bc_rank : s.v.list_rank;
-            x[u] = in[u] ? colp[idx] : 0u;
-            ex[u] = in[u] && r3q[u] ? s.v.bc_exec[idx] : 0u;
-            kd[u] = in[u] && r3q[u] ? (uint32_t)s.v.bc_kind[idx] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < ST_U; ++u) {
-            bool keep = in[u] && (!r3q[u] || (ex[u] >= mk[u] && ((c.wk >> kd[u]) & 1u)));
-            keep = keep && !(c.bq && x[u] == c.trank);
             const uint64_t bal = __ballot(keep) & gmask;
             if (keep) {
                 const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x[u] << 4) | (EntT)kk[u];
+                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x << 4) | (EntT)kj;
             }
             cursor += (uint32_t)__popcll(bal);
         }
@@ -2211,7 +2197,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
         const uint32_t before = (uint32_t)__popcll(peers & lt);
         if (in) {
             stA[grp][Kd + kbase[grp][kj] + kc[grp][kj] + before] = (uint16_t)idx;
-            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = (uint32_t)(x >> 4);   // rank: k_v3_ucompact maps it to the TxnId
+            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = s.txn_of_rank[(uint32_t)(x >> 4)];
         }
         __builtin_amdgcn_wave_barrier();
         if (in && before == 0) kc[grp][kj] += (uint32_t)__popcll(peers);
@@ -2253,9 +2239,25 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigcopy(uint32_t nbig, const uint3
     for (uint64_t q = lane; q < K; q += 64) key_idx[kd + q] = key_scr[ks + q];
 }
 
-// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: TxnId ranks at its slot t * ST_N2 of
-// dep_scr, mapped through txn_of_rank here; big txns: TxnIds at vdep_off of its first pair in dep_big) to
-// dep_txn[u_off[t] ...). A block takes a fixed chunk
+// Sparse batches (a mixed batch's range txns have no KeyDeps of their own here): the txns with TxnIds, compacted with
+// their u_off, so k_v3_ucompact's chunks span a few txns each instead of long runs of empty ones.
+__global__ __launch_bounds__(BLOCK) void k_v3_neflag(uint32_t n, const uint64_t *__restrict__ u_cnt, uint32_t *__restrict__ flag)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n) flag[t] = u_cnt[t] != 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v3_nelist(uint32_t n, const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                     const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ u_off,
+                                                     uint32_t *__restrict__ ne_t, uint64_t *__restrict__ ne_uoff)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n && flag[t]) { ne_t[pos[t]] = t; ne_uoff[pos[t]] = u_off[t]; }
+    if (t == 0) ne_uoff[*cnt] = u_off[n];
+}
+
+// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: at its slot t * ST_N2 of dep_scr; big
+// txns: at vdep_off of its first pair in dep_big) to dep_txn[u_off[t] ...). A block takes a fixed chunk
 // of UC_CHUNK outputs (the uncommitted window's txns are consecutive and hold most TxnIds: partitioning by txns left a
 // few blocks with most of the work), finds the txns spanning it by binary search over u_off, and strides over the
 // chunk in windows of BLOCK txns (u_off / source bases in LDS, each output's txn by binary search there).
@@ -2268,17 +2270,21 @@ __device__ __forceinline__ uint32_t last_le(const uint64_t *a, uint32_t n, uint6
     return lo;
 }
 
+// tmap (optional): the txns are tmap[0, *n_dev) with offsets u_off[0, *n_dev] (the non-empty txns of a sparse batch,
+// k_v3_nelist), else 0..n-1 over the batch's u_off.
 __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_t *__restrict__ u_off,
                                                        const uint64_t *__restrict__ arena_off, const uint64_t *__restrict__ kd_off,
                                                        const uint32_t *__restrict__ bigflag, const uint32_t *__restrict__ key_off,
                                                        const uint64_t *__restrict__ vdep_off, const uint32_t *__restrict__ dep_scr,
-                                                       const uint32_t *__restrict__ dep_big, const uint32_t *__restrict__ txn_of_rank,
+                                                       const uint32_t *__restrict__ dep_big,
+                                                       const uint32_t *__restrict__ tmap, const uint32_t *__restrict__ n_dev,
                                                        uint32_t *__restrict__ dep_txn)
 {
     __shared__ uint64_t uo[BLOCK + 1];
     __shared__ uint64_t src[BLOCK];
     __shared__ uint32_t s_t[2];
     const uint32_t tid = threadIdx.x;
+    if (tmap) n = *n_dev;
     const uint64_t total = u_off[n];
     const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
     if (c0 >= total) return;
@@ -2286,7 +2292,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
     if (tid == 0) { s_t[0] = last_le(u_off, n, c0); s_t[1] = last_le(u_off, n, c1 - 1); }
     __syncthreads();
     const uint32_t tlo = s_t[0], thi = s_t[1];
-    auto source = [&](uint32_t t) {
+    auto source = [&](uint32_t j) {
+        const uint32_t t = tmap ? tmap[j] : j;
         return bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_N2;
     };
     if (thi - tlo >= 8 * BLOCK) {
@@ -2296,7 +2303,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
             uint32_t lo = tlo, hi = thi + 1;
             while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (u_off[m] <= i) lo = m; else hi = m; }
             const uint64_t sb = source(lo), off = i - u_off[lo];
-            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : txn_of_rank[dep_scr[sb + off]];
+            dep_txn[i] = (sb >> 63) ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
         }
         return;
     }
@@ -2326,9 +2333,6 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
                     x[u] = big[u] ? dep_big[(sb & ~(1ull << 63)) + off] : dep_scr[sb + off];
                 }
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (i0 + (uint64_t)u * BLOCK < hi && !big[u]) x[u] = txn_of_rank[x[u]];
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (i0 + (uint64_t)u * BLOCK < hi) dep_txn[i0 + (uint64_t)u * BLOCK] = x[u];
@@ -2367,6 +2371,7 @@ struct KdState {
     uint64_t *g = nullptr;
     bool have_dict = false;
     Dictionary dict;
+    bool sparse = false;              // the batch has many txns without keys (a mixed batch's range txns)
     bool v1 = false;                  // the exact-replay columns below are built
     CfkView v1view{};
 };
@@ -2927,10 +2932,22 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                    (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const int32_t *)arena_scr, (const uint32_t *)key_scr,
                    arena, key_idx);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
+        const uint32_t *tmap = nullptr, *ne_cnt = nullptr;
+        const uint64_t *uo = u_off;
+        if (ks && ks->sparse) {
+            uint32_t *flag = ctx->get<uint32_t>("v3_ne_flag", n), *pos = ctx->get<uint32_t>("v3_ne_pos", n);
+            uint32_t *cnt = ctx->get<uint32_t>("v3_ne_cnt", 1), *ne_t = ctx->get<uint32_t>("v3_ne_t", n);
+            uint64_t *ne_uoff = ctx->get<uint64_t>("v3_ne_uoff", (size_t)n + 1);
+            launch(ctx, "v3_neflag", k_v3_neflag, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)u_cnt, flag);
+            scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, pos, n, true, cnt);
+            launch(ctx, "v3_nelist", k_v3_nelist, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)flag,
+                   (const uint32_t *)pos, (const uint32_t *)cnt, (const uint64_t *)u_off, ne_t, ne_uoff);
+            tmap = ne_t; ne_cnt = cnt; uo = ne_uoff;
+        }
         launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n,
-               (const uint64_t *)u_off, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
+               uo, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
                (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr,
-               (const uint32_t *)txn_of_rank, dep_txn);
+               tmap, ne_cnt, dep_txn);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -3396,6 +3413,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     acc_batch_in kin{ n, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
     acc_keydeps_view kv{};
     KdState ks;
+    ks.sparse = R > 0;
     keydeps_core(ctx, &kin, &kv, &ks);
     ctx->kd_valid = false;
     if (shared) { shared->valid = ks.have_dict; shared->dict = ks.dict; shared->owner = ks.owner; }

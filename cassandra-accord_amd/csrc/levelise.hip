@@ -213,26 +213,61 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, uin
                 else { a = foff[i]; b = foff[i + 1]; }
             }
             bool done = !valid;
+            // first pass: every entry once (four LDS loads in flight per lane); deps still unpublished are kept in
+            // registers (up to LV_PEND per lane) and later passes re-read only those, so a dependency hop costs one
+            // LDS round trip, not a re-scan of the list
+            uint32_t m = 0, np = 0, pend[LV_PEND];
+            bool ovf = false, scanned = false;
+#pragma unroll
+            for (int q = 0; q < LV_PEND; ++q) pend[q] = 0;
             while (true) {
                 if (!done) {   // group-uniform
-                    uint32_t m = 0;
-                    bool pend = false;
-                    for (uint32_t e = a + sub; e < b; e += LV_G) {
-                        const uint32_t p = e >= lo_res ? slots[(size_t)((e >> ch_shift) % 3) * CH + (e & (CH - 1))]
-                                                       : (uint32_t)fdep[e];
-                        const uint32_t v = lv_lds_ld(&lvl[p]);
-                        pend |= v == 0;
-                        m = max(m, v);
+                    if (!scanned || ovf) {
+                        m = 0; np = 0; ovf = false;
+                        for (uint32_t e0 = a + sub; e0 < b; e0 += 4 * LV_G) {
+                            uint32_t p[4], v[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const uint32_t e = e0 + (uint32_t)u * LV_G;
+                                p[u] = e < b ? (e >= lo_res ? slots[(size_t)((e >> ch_shift) % 3) * CH + (e & (CH - 1))]
+                                                            : (uint32_t)fdep[e])
+                                             : 0u;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) v[u] = e0 + (uint32_t)u * LV_G < b ? lv_lds_ld(&lvl[p[u]]) : 0u;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (e0 + (uint32_t)u * LV_G >= b) continue;
+                                if (v[u]) { m = max(m, v[u]); continue; }
+#pragma unroll
+                                for (int q = 0; q < LV_PEND; ++q) if ((uint32_t)q == np) pend[q] = p[u];
+                                if (np < LV_PEND) ++np; else ovf = true;
+                            }
+                        }
+                        scanned = true;
+                    } else if (np) {
+                        uint32_t keep[LV_PEND], nk = 0;
+#pragma unroll
+                        for (int q = 0; q < LV_PEND; ++q) keep[q] = (uint32_t)q < np ? lv_lds_ld(&lvl[pend[q]]) : 0u;
+#pragma unroll
+                        for (int q = 0; q < LV_PEND; ++q) {
+                            if ((uint32_t)q >= np) continue;
+                            if (keep[q]) { m = max(m, keep[q]); continue; }
+#pragma unroll
+                            for (int r = 0; r < LV_PEND; ++r) if ((uint32_t)r == nk) pend[r] = pend[q];
+                            ++nk;
+                        }
+                        np = nk;
                     }
-                    uint32_t pd = pend ? 1u : 0u;
+                    uint32_t mm = m, pd = (np || ovf) ? 1u : 0u;
 #pragma unroll
                     for (int d = 1; d < LV_G; d <<= 1) {
-                        m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                        mm = max(mm, (uint32_t)__shfl_xor(mm, d, 64));
                         pd |= (uint32_t)__shfl_xor(pd, d, 64);
                     }
                     if (!pd) {
-                        if (sub == 0) *(volatile uint16_t *)&lvl[i] = (uint16_t)(m + 1);
-                        my_max = max(my_max, m);
+                        if (sub == 0) *(volatile uint16_t *)&lvl[i] = (uint16_t)(mm + 1);
+                        my_max = max(my_max, mm);
                         done = true;
                     }
                 }
