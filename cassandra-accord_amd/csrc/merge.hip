@@ -17,16 +17,17 @@
 
 namespace acc {
 
+template <int NWV = WAVES>
 __device__ __forceinline__ void block_or1(uint64_t v, uint64_t *dst)
 {
-    __shared__ uint64_t part[WAVES];
+    __shared__ uint64_t part[NWV];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v |= shfl_idx(v, (int)(lane_id() ^ d));
     if (lane_id() == 0) part[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t x = 0;
-        for (int q = 0; q < WAVES; ++q) x |= part[q];
+        for (int q = 0; q < NWV; ++q) x |= part[q];
         if (x) atomicOr((unsigned long long *)dst, (unsigned long long)x);
     }
 }
@@ -259,6 +260,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_key_of_slot(uint64_t R, const uint6
 // per-reply validation of k_m_prep (KeyDeps ctor / checkValid) is done on the same loaded records.
 
 constexpr int ML_REP = 256, ML_KC = 1024, ML_VC = 4096, ML_OC = 4096;
+constexpr int ML_NT = 512;   // threads per group: more waves per CU for the LDS-latency-bound merge tree and searches
 
 // per group: does it fit the LDS tier (offsets monotone, sizes within the caps)? g[3] |= 1 if some group does not
 __global__ __launch_bounds__(BLOCK) void k_m_fit(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_fit(uint32_t ng, const uint64_t *__
 }
 
 // Block-wide merge of NR sorted runs of src[0, N) (run r = [rs[r], rs[r + 1]), rs[NR] = N; rs is overwritten):
-// ceil(log2 NR) levels, each merging run pairs with merge-path partitions of ceil(N / BLOCK) outputs per thread,
+// ceil(log2 NR) levels, each merging run pairs with merge-path partitions of ceil(N / ML_NT) outputs per thread,
 // ping-ponging between src and dst. Returns the buffer holding the sorted N elements. Every KeyDeps.merge input is
 // already sorted per reply (keys, TxnIds, and (key, TxnId) entries once mapped through the monotone merged indices),
 // so this replaces a bitonic network's O(log^2 N) barrier stages by O(log NR).
@@ -299,7 +301,7 @@ template <class T>
 __device__ T *lds_merge_runs(T *src, T *dst, uint32_t *rs, uint32_t NR, uint32_t N)
 {
     const uint32_t tid = threadIdx.x;
-    const uint32_t CH = (N + BLOCK - 1) / BLOCK;
+    const uint32_t CH = (N + ML_NT - 1) / ML_NT;
     while (NR > 1) {
         const uint32_t NP = (NR + 1) / 2;
         const uint32_t o0 = min(N, tid * CH), o1 = min(N, o0 + CH);
@@ -336,21 +338,21 @@ __device__ T *lds_merge_runs(T *src, T *dst, uint32_t *rs, uint32_t NR, uint32_t
     return src;
 }
 
-// pads s[N, up to a multiple of BLOCK) for lds_unique
+// pads s[N, up to a multiple of ML_NT) for lds_unique
 template <class T>
 __device__ __forceinline__ uint32_t lds_pad_block(T *s, uint32_t N, T pad)
 {
-    const uint32_t np = (N + BLOCK - 1) / BLOCK * BLOCK;
-    for (uint32_t i = N + threadIdx.x; i < np; i += BLOCK) s[i] = pad;
+    const uint32_t np = (N + ML_NT - 1) / ML_NT * ML_NT;
+    for (uint32_t i = N + threadIdx.x; i < np; i += ML_NT) s[i] = pad;
     __syncthreads();
     return np;
 }
 
-// order-preserving in-place unique of the sorted s[0..np) (pads last); returns the count. np = BLOCK * per.
+// order-preserving in-place unique of the sorted s[0..np) (pads last); returns the count. np = ML_NT * per.
 template <class T, int MAXI>
 __device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t np, T pad, uint32_t *scan_lds)
 {
-    const uint32_t per = np / BLOCK, base = threadIdx.x * per;
+    const uint32_t per = np / ML_NT, base = threadIdx.x * per;
     T x[MAXI];
     uint32_t f = 0, c = 0;
 #pragma unroll
@@ -364,7 +366,7 @@ __device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t np, T pad, uint32_
         }
     }
     uint32_t total;
-    uint32_t o = block_exclusive(c, OpAdd<uint32_t>(), scan_lds, total);
+    uint32_t o = block_exclusive<uint32_t, OpAdd<uint32_t>, ML_NT / 64>(c, OpAdd<uint32_t>(), scan_lds, total);
 #pragma unroll
     for (int q = 0; q < MAXI; ++q)
         if ((uint32_t)q < per && ((f >> q) & 1u)) s[o++] = x[q];
@@ -394,7 +396,7 @@ struct MlPlan {
     uint32_t bytes;
 };
 
-__global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
+__global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
                                                  const uint64_t *__restrict__ key_code, const uint64_t *__restrict__ val_off,
                                                  const uint32_t *__restrict__ txn_rank, const uint64_t *__restrict__ k2v_off,
                                                  const int32_t *__restrict__ k2v, MlPlan pl, MlOut o)
@@ -410,14 +412,14 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
     uint32_t *rawo = rawv + pl.vc;
     uint32_t *hdr = rawo + pl.oc;
     __shared__ uint32_t rk[ML_REP + 1], rv[ML_REP + 1], ro[ML_REP + 1];
-    __shared__ uint32_t scan_lds[WAVES];
+    __shared__ uint32_t scan_lds[ML_NT / 64];
     __shared__ uint32_t rsm[ML_REP + 1];   // run starts of the merge tree
     const uint32_t gi = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     const uint64_t R0 = grp_off[gi];
     const uint32_t nrep = (uint32_t)(grp_off[gi + 1] - R0);
     const uint64_t KA = key_off[R0], VA = val_off[R0], OA = k2v_off[R0];
-    for (uint32_t r = tid; r <= nrep; r += BLOCK) {
+    for (uint32_t r = tid; r <= nrep; r += ML_NT) {
         rk[r] = (uint32_t)(key_off[R0 + r] - KA);
         rv[r] = (uint32_t)(val_off[R0 + r] - VA);
         ro[r] = (uint32_t)(k2v_off[R0 + r] - OA);
@@ -425,15 +427,15 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
     __syncthreads();
     const uint32_t NK = rk[nrep], NV = rv[nrep], NO = ro[nrep], NE = NO - NK;
     // one coalesced pass over the group's three input ranges
-    for (uint32_t i = tid; i < NK; i += BLOCK) rawk[i] = key_code[KA + i];
-    for (uint32_t i = tid; i < NV; i += BLOCK) rawv[i] = txn_rank[VA + i];
-    for (uint32_t i = tid; i < NO; i += BLOCK) rawo[i] = (uint32_t)k2v[OA + i];
+    for (uint32_t i = tid; i < NK; i += ML_NT) rawk[i] = key_code[KA + i];
+    for (uint32_t i = tid; i < NV; i += ML_NT) rawv[i] = txn_rank[VA + i];
+    for (uint32_t i = tid; i < NO; i += ML_NT) rawo[i] = (uint32_t)k2v[OA + i];
     __syncthreads();
     uint64_t err = 0;
     const uint64_t PADK = ~0ull;
     const uint32_t PAD32 = 0xFFFFFFFFu;
     // ---- keys: sort, unique, write, map every key slot to its merged index
-    for (uint32_t i = tid; i < NK; i += BLOCK) {
+    for (uint32_t i = tid; i < NK; i += ML_NT) {
         uint64_t x = PADK;
         if (i < NK) {
             const uint32_t r = lds_ub(rk, nrep + 1, i) - 1;
@@ -442,14 +444,14 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort64[i] = x;
     }
-    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = rk[r];
+    for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rk[r];
     __syncthreads();
     uint64_t *ks = lds_merge_runs(sort64, sort64b, rsm, nrep, NK);
-    const uint32_t Kg = lds_unique<uint64_t, ML_KC / BLOCK>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
-    uint32_t kmap[ML_KC / BLOCK];
+    const uint32_t Kg = lds_unique<uint64_t, ML_KC / ML_NT>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
+    uint32_t kmap[ML_KC / ML_NT];
 #pragma unroll
-    for (int q = 0; q < ML_KC / BLOCK; ++q) {
-        const uint32_t i = tid + q * BLOCK;
+    for (int q = 0; q < ML_KC / ML_NT; ++q) {
+        const uint32_t i = tid + q * ML_NT;
         if (i < Kg) o.s_key[KA + i] = ks[i];
         if (i < NK) {
             const uint64_t kc = rawk[i];
@@ -461,12 +463,12 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
     __syncthreads();
     uint32_t *kidx = reinterpret_cast<uint32_t *>(rawk);   // key slot -> merged key index
 #pragma unroll
-    for (int q = 0; q < ML_KC / BLOCK; ++q) {
-        const uint32_t i = tid + q * BLOCK;
+    for (int q = 0; q < ML_KC / ML_NT; ++q) {
+        const uint32_t i = tid + q * ML_NT;
         if (i < NK) kidx[i] = kmap[q];
     }
     // ---- TxnIds: same
-    for (uint32_t i = tid; i < NV; i += BLOCK) {
+    for (uint32_t i = tid; i < NV; i += ML_NT) {
         uint32_t x = PAD32;
         if (i < NV) {
             const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
@@ -475,20 +477,20 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort32[i] = x;
     }
-    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = rv[r];
+    for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rv[r];
     __syncthreads();
     uint32_t *vs = lds_merge_runs(sort32, sort32b, rsm, nrep, NV);
-    const uint32_t Ug = lds_unique<uint32_t, ML_VC / BLOCK>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
-    for (uint32_t i = tid; i < NV; i += BLOCK) {
+    const uint32_t Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
+    for (uint32_t i = tid; i < NV; i += ML_NT) {
         const uint32_t v = rawv[i];
         uint32_t a = 0, b = Ug;
         while (a < b) { uint32_t m = (a + b) >> 1; if (vs[m] < v) a = m + 1; else b = m; }
         rawv[i] = a;   // each thread rewrites only its own slots
     }
-    for (uint32_t u = tid; u < Ug; u += BLOCK) o.s_val[VA + u] = vs[u];
+    for (uint32_t u = tid; u < Ug; u += ML_NT) o.s_val[VA + u] = vs[u];
     __syncthreads();
     // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
-    for (uint32_t q = tid; q < NO; q += BLOCK) {
+    for (uint32_t q = tid; q < NO; q += ML_NT) {
         const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
         const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
         const uint32_t qq = q - ro[r];
@@ -512,12 +514,12 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort32[q - rk[r + 1]] = x;
     }
-    for (uint32_t k = tid; k < Kg; k += BLOCK) hdr[k] = 0;
-    for (uint32_t r = tid; r <= nrep; r += BLOCK) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
+    for (uint32_t k = tid; k < Kg; k += ML_NT) hdr[k] = 0;
+    for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
     __syncthreads();
     uint32_t *es = lds_merge_runs(sort32, sort32b, rsm, nrep, NE);
-    const uint32_t Eu = lds_unique<uint32_t, ML_VC / BLOCK>(es, lds_pad_block(es, NE, PAD32), PAD32, scan_lds);
-    for (uint32_t c = tid; c < Eu; c += BLOCK) {
+    const uint32_t Eu = lds_unique<uint32_t, ML_VC / ML_NT>(es, lds_pad_block(es, NE, PAD32), PAD32, scan_lds);
+    for (uint32_t c = tid; c < Eu; c += ML_NT) {
         const uint32_t kk = es[c] >> 16;
         if (c + 1 == Eu || (es[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
         o.s_k2v[OA + Kg + c] = (int32_t)(es[c] & 0xFFFFu);
@@ -525,11 +527,11 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
     __syncthreads();
     // keys without entries: end offset = the previous key's (prefix max, starting at Kg)
     {
-        const uint32_t per = (Kg + BLOCK - 1) / BLOCK, base = tid * per;
+        const uint32_t per = (Kg + ML_NT - 1) / ML_NT, base = tid * per;
         uint32_t m = 0;
         for (uint32_t q = 0; q < per && base + q < Kg; ++q) m = max(m, hdr[base + q]);
         uint32_t total;
-        uint32_t run = block_exclusive(m, OpMax<uint32_t>(), scan_lds, total);
+        uint32_t run = block_exclusive<uint32_t, OpMax<uint32_t>, ML_NT / 64>(m, OpMax<uint32_t>(), scan_lds, total);
         run = max(run, Kg);
         for (uint32_t q = 0; q < per && base + q < Kg; ++q) {
             run = max(run, hdr[base + q]);
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_lds(uint32_t ng, const uint64_t *__
         o.cnt_v[gi] = Ug;
         o.cnt_o[gi] = Kg + Eu;
     }
-    block_or1(err, o.errs);
+    block_or1<ML_NT / 64>(err, o.errs);
 }
 
 // scratch (at input offsets) -> final CSR: one wave per group
@@ -607,7 +609,7 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gmax, 4 * 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
         if (ctx->pinned[0] == 0) {
-            auto rb = [](uint64_t n) { return std::max<uint64_t>(BLOCK, (n + BLOCK - 1) / BLOCK * BLOCK); };
+            auto rb = [](uint64_t n) { return std::max<uint64_t>(ML_NT, (n + ML_NT - 1) / ML_NT * ML_NT); };
             MlPlan pl;
             pl.kc = (uint32_t)ctx->pinned[1];
             pl.vc = (uint32_t)ctx->pinned[2];
@@ -623,7 +625,7 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
             mo.cnt_v = ctx->get<uint64_t>("m_cnt_v", ng);
             mo.cnt_o = ctx->get<uint64_t>("m_cnt_o", ng);
             mo.errs = g + 2;
-            launch(ctx, "m_lds", k_m_lds, dim3(ng), dim3(BLOCK), pl.bytes, ng, grp_off, key_off, key_code, val_off, txn_rank,
+            launch(ctx, "m_lds", k_m_lds, dim3(ng), dim3(ML_NT), pl.bytes, ng, grp_off, key_off, key_code, val_off, txn_rank,
                    k2v_off, k2v, pl, mo);
             uint64_t *ko = ctx->get<uint64_t>("m_k_gstart", (size_t)ng + 1);
             uint64_t *vo = ctx->get<uint64_t>("m_v_gstart", (size_t)ng + 1);
