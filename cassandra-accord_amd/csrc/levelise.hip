@@ -164,6 +164,16 @@ __global__ __launch_bounds__(BLOCK) void k_lv_rounds(uint32_t n, uint32_t R, int
         for (uint32_t c = r + 1; c <= R; ++c) rstart[c] = n;
 }
 
+// max over the 16 lanes of a DPP row (row_ror 1, 2, 4, 8): every lane of the row gets it, no LDS round trips
+__device__ __forceinline__ uint32_t row_max16(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x121, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x122, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x124, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xF, 0xF, false));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t lv_lds_ld(const uint16_t *p) { return *(const volatile uint16_t *)p; }
 
 __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, uint32_t R, int ch_shift, uint32_t Ef,
@@ -259,12 +269,10 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, uin
                         }
                         np = nk;
                     }
-                    uint32_t mm = m, pd = (np || ovf) ? 1u : 0u;
-#pragma unroll
-                    for (int d = 1; d < LV_G; d <<= 1) {
-                        mm = max(mm, (uint32_t)__shfl_xor(mm, d, 64));
-                        pd |= (uint32_t)__shfl_xor(pd, d, 64);
-                    }
+                    // group (= one 16-lane DPP row) max of the levels, pending flag in bit 16
+                    uint32_t mm = row_max16((m & 0xFFFFu) | ((np || ovf) ? 0x10000u : 0u));
+                    const uint32_t pd = mm >> 16;
+                    mm &= 0xFFFFu;
                     if (!pd) {
                         if (sub == 0) *(volatile uint16_t *)&lvl[i] = (uint16_t)(mm + 1);
                         my_max = max(my_max, mm);
