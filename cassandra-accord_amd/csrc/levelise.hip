@@ -122,7 +122,7 @@ __global__ __launch_bounds__(BLOCK) void k_lv_fcount(uint32_t n, const uint32_t 
     const uint32_t t = order_exec[i], er = exec_rank[t];
     const uint64_t a = off[t], b = off[t + 1];
     uint32_t c = 0;
-    for (uint64_t e = a + lane; e < b; e += 64) c += exec_rank[dep[e]] < er;
+    for (uint64_t e = a + lane; e < b; e += 64) { const uint32_t d = dep[e]; c += d < n && exec_rank[d] < er; }   // d >= n: lv_check's error
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
     if (lane == 0) cnt[i] = c;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(BLOCK) void k_lv_fwrite(uint32_t n, const uint32_t 
         const uint64_t e = c0 + lane;
         uint32_t d = 0;
         bool keep = false;
-        if (e < b) { d = dep[e]; keep = exec_rank[d] < er; }
+        if (e < b) { d = dep[e]; keep = d < n && exec_rank[d] < er; }
         const uint64_t bal = __ballot(keep);
         if (keep) fdep[w + (uint32_t)__popcll(bal & lt)] = (uint16_t)pos[d];
         w += (uint32_t)__popcll(bal);
@@ -151,11 +151,17 @@ __global__ __launch_bounds__(BLOCK) void k_lv_fwrite(uint32_t n, const uint32_t 
 }
 
 // rstart[c] = first position whose list ends in chunk >= c (lists ending at entry 0 count as chunk 0); rstart[R] = n
-__global__ __launch_bounds__(BLOCK) void k_lv_rounds(uint32_t n, uint32_t R, int ch_shift, const uint32_t *__restrict__ foff,
+__device__ __forceinline__ uint32_t lv_rounds_of(uint32_t Ef, int ch_shift)
+{
+    return max(1u, (uint32_t)(((uint64_t)Ef + (1u << ch_shift) - 1) >> ch_shift));
+}
+
+__global__ __launch_bounds__(BLOCK) void k_lv_rounds(uint32_t n, int ch_shift, const uint32_t *__restrict__ foff,
                                                      uint32_t *__restrict__ rstart)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
+    const uint32_t R = lv_rounds_of(foff[n], ch_shift);
     auto round_of = [&](uint32_t j) { const uint32_t e = foff[j + 1]; return e == 0 ? 0u : (e - 1) >> ch_shift; };
     const uint32_t r = round_of(i);
     const uint32_t rp = i == 0 ? 0u : round_of(i - 1) + 1;
@@ -176,11 +182,12 @@ __device__ __forceinline__ uint32_t row_max16(uint32_t x)
 
 __device__ __forceinline__ uint32_t lv_lds_ld(const uint16_t *p) { return *(const volatile uint16_t *)p; }
 
-__global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, uint32_t R, int ch_shift, uint32_t Ef,
+__global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int ch_shift,
                                                   const uint32_t *__restrict__ foff, const uint16_t *__restrict__ fdep,
                                                   const uint32_t *__restrict__ rstart, const uint32_t *__restrict__ order_exec,
                                                   uint32_t *__restrict__ level, uint32_t *__restrict__ max_level)
 {
+    const uint32_t Ef = foff[n], R = lv_rounds_of(Ef, ch_shift);   // sizes stay on the device (no host round trip)
     __shared__ __attribute__((aligned(16))) uint16_t L[LV_LDS];
     __shared__ uint32_t fb[2][LV_FB];   // foff of the round's positions (double-buffered)
     const uint32_t CH = 1u << ch_shift;
@@ -340,12 +347,10 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     ACC_HIP(hipMemcpyAsync(order_exec, se.vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
     uint32_t *pos = ctx->get<uint32_t>("lv_pos", n);
     launch(ctx, "lv_pos", k_lv_pos, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, pos);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 4, hipMemcpyDeviceToHost, st));
-    ctx->sync();
-    uint32_t e0;
-    memcpy(&e0, ctx->pinned, 4);
-    if (e0 & 1) fail(ACC_E_ARG, "graph offsets must be non-decreasing");
-    if (e0 & 2) fail(ACC_E_ARG, "dependency index out of range");
+    auto check_err = [&](uint32_t e0) {
+        if (e0 & 1) fail(ACC_E_ARG, "graph offsets must be non-decreasing");
+        if (e0 & 2) fail(ACC_E_ARG, "dependency index out of range");
+    };
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
     ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
@@ -365,36 +370,41 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         const unsigned gw = (n + WAVES - 1) / WAVES;
         launch(ctx, "lv_fcount", k_lv_fcount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank, fcnt);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, fcnt, foff, n, true, foff + n);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, foff + n, 4, hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        uint32_t Ef;
-        memcpy(&Ef, ctx->pinned, 4);
-        uint16_t *fdep = ctx->get<uint16_t>("lv_fdep", (size_t)Ef + ch);   // + one chunk of padding for whole-chunk reads
+        // sized by the unfiltered E (>= the filtered count, which stays on the device) + one chunk of padding for
+        // whole-chunk reads; invalid graphs (lv_check) are walked harmlessly (bad deps are skipped) and fail at the end
+        uint16_t *fdep = ctx->get<uint16_t>("lv_fdep", (size_t)E + ch);
         launch(ctx, "lv_fwrite", k_lv_fwrite, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
                (const uint32_t *)pos, (const uint32_t *)foff, fdep);
         const int ch_shift = 31 - __builtin_clz(ch);
-        const uint32_t R = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)Ef + ch - 1) >> ch_shift));
-        uint32_t *rstart = ctx->get<uint32_t>("lv_rstart", (size_t)R + 1);
-        launch(ctx, "lv_rounds", k_lv_rounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, R, ch_shift, (const uint32_t *)foff, rstart);
-        launch(ctx, "lv_walk", k_lv_lds, dim3(1), dim3(LV_NT), 0, n, npad, R, ch_shift, Ef, (const uint32_t *)foff,
+        uint32_t *rstart = ctx->get<uint32_t>("lv_rstart", (size_t)(E >> ch_shift) + 3);
+        launch(ctx, "lv_rounds", k_lv_rounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, ch_shift, (const uint32_t *)foff, rstart);
+        launch(ctx, "lv_walk", k_lv_lds, dim3(1), dim3(LV_NT), 0, n, npad, ch_shift, (const uint32_t *)foff,
                (const uint16_t *)fdep, (const uint32_t *)rstart, (const uint32_t *)order_exec, level, maxl);
-        ctx->stat("levelise.lds_rounds", R);
+        ctx->stat("levelise.lds_tier", 1);
     } else {
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        uint32_t e0;
+        memcpy(&e0, ctx->pinned, 4);
+        check_err(e0);
         ACC_HIP(hipMemsetAsync(level, 0, (size_t)n * 4, st));
         // a persistent grid of up to 4096 waves (16 per CU): enough txns in flight to cover the memory round trips
         const uint32_t waves = std::min<uint32_t>(n, 4096u);
         launch(ctx, "lv_walk", k_lv_waves, dim3((waves + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep,
                exec_rank, level, maxl + 1, maxl);
         launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
-        ctx->stat("levelise.lds_rounds", 0);
+        ctx->stat("levelise.lds_tier", 0);
     }
     const int pbits = bits_for(n - 1);
     launch(ctx, "lv_order_keys", k_lv_order_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)level,
            (const uint32_t *)pos, pbits, key);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, maxl, 4, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, err, 4, hipMemcpyDeviceToHost, st));
     ctx->sync();
-    uint32_t ml;
+    uint32_t ml, e1;
     memcpy(&ml, ctx->pinned, 4);
+    memcpy(&e1, ctx->pinned + 1, 4);
+    check_err(e1);
     Sorted so = radix_sort(ctx, "lv_rs_order", key, nullptr, n, pbits + bits_for(ml));
     hipMemcpyKind kind = in->mem == ACC_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     ACC_HIP(hipMemcpyAsync(level_out, level, (size_t)n * 4, kind, st));
