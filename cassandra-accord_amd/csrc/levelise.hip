@@ -36,7 +36,10 @@ __global__ __launch_bounds__(BLOCK) void k_lv_check(uint32_t n, const uint64_t *
 // wave's loop ends. The critical path is the graph's dependency depth at one memory round trip per level (~2 us:
 // config 5's 709 levels in 1.5 ms); the deps of a txn are read in parallel. (A tiled variant resolving intra-tile hops
 // in LDS measured 7x slower: each wave then walks its share of the tile serially at global-load latency.)
-constexpr int LV_PEND = 4;   // unpublished deps a lane tracks in registers before it waits in place
+#ifndef ACC_LV_PEND
+#define ACC_LV_PEND 4
+#endif
+constexpr int LV_PEND = ACC_LV_PEND;   // unpublished deps a lane tracks in registers
 
 __device__ __forceinline__ uint32_t lv_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -108,7 +111,10 @@ constexpr int LV_LDS = 69632;          // u16 slots of LDS: levels (level + 1, 0
 constexpr int LV_FB = 2048;            // foff entries of a round staged in LDS (x2 buffers); beyond: read from HBM
 constexpr uint32_t LV_LDS_MAX_N = 65535;
 constexpr int LV_NT = 1024;
-constexpr int LV_G = 16;               // lanes per position
+#ifndef ACC_LV_G
+#define ACC_LV_G 16
+#endif
+constexpr int LV_G = ACC_LV_G;         // lanes per position (16: one DPP row)
 constexpr int LV_GROUPS = LV_NT / LV_G;
 constexpr uint32_t LV_CH_MAX = 16384;  // entries per chunk
 constexpr int LV_PF = LV_CH_MAX / 8 / LV_NT;   // uint4 of a chunk per thread
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     __shared__ uint32_t fb[2][LV_FB];   // foff of the round's positions (double-buffered)
     const uint32_t CH = 1u << ch_shift;
     uint16_t *lvl = L, *slots = L + npad;
-    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_G - 1), wave = tid >> 6, gi = lane >> 4;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_G - 1), wave = tid >> 6, gi = lane / LV_G;
     for (uint32_t i = tid; i < n; i += LV_NT) lvl[i] = 0;
     // chunk c -> slot c % 3: CH / 8 uint4 of fdep (reads may run past Ef into the buffer's padding)
     const uint32_t nv = CH / 8;
@@ -219,8 +225,9 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
         const uint32_t p0 = r0, p1 = r1;
         const uint32_t *fo = fb[c & 1];
         const uint64_t lo_res = c == 0 ? 0ull : (uint64_t)(c - 1) * CH;   // first entry resident in LDS
-        for (uint32_t base = p0 + 4 * wave; base < p1; base += LV_GROUPS) {
-            // wave w holds positions base + {0..3}; the waves stride by 64 positions
+        constexpr uint32_t GPW = 64 / LV_G;   // positions per wave
+        for (uint32_t base = p0 + GPW * wave; base < p1; base += LV_GROUPS) {
+            // wave w holds positions base + {0 .. GPW - 1}; the waves stride by LV_GROUPS positions
             const uint32_t i = base + gi;
             const bool valid = i < p1;
             uint32_t a = 0, b = 0;
@@ -277,7 +284,12 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
                         np = nk;
                     }
                     // group (= one 16-lane DPP row) max of the levels, pending flag in bit 16
-                    uint32_t mm = row_max16((m & 0xFFFFu) | ((np || ovf) ? 0x10000u : 0u));
+                    uint32_t mm = (m & 0xFFFFu) | ((np || ovf) ? 0x10000u : 0u);
+                    if constexpr (LV_G == 16) mm = row_max16(mm);
+                    else {
+#pragma unroll
+                        for (int d = 1; d < LV_G; d <<= 1) mm = max(mm, (uint32_t)__shfl_xor(mm, d, 64));
+                    }
                     const uint32_t pd = mm >> 16;
                     mm &= 0xFFFFu;
                     if (!pd) {
