@@ -916,17 +916,19 @@ struct V2Query {
 __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
 {
     V2Query q;
+    const Row rpp = ld_row(v, p);   // the insert position's row for the ~90% of pairs with executeAt == TxnId, issued
+                                    // with the pair's own columns instead of after the segment lookup
     uint32_t seg = v.seg_incl[p] - 1;
-    q.s0 = v.seg_start[seg];
-    uint32_t s1 = v.seg_start[seg + 1];
     q.trank = v.s_rank[p];
     uint32_t S = v.s_exec[p];
     q.info = v.s_info[p];
+    q.s0 = v.seg_start[seg];
+    uint32_t s1 = v.seg_start[seg + 1];
     q.wk = witnesses(q.info >> 3);
     q.wc = wk_classes(q.wk);
     q.bq = S != q.trank;
     q.pos = q.bq ? lower_bound_u32(v.s_rank, p + 1, s1, S) : p;
-    q.rp = ld_row(v, q.pos);
+    q.rp = q.bq ? ld_row(v, q.pos) : rpp;
     q.r0 = ld_row(v, q.s0);
     // M from the last unbumped committed Write before pos
     uint32_t lu = q.rp.c[RW_LUCW];
@@ -977,6 +979,7 @@ __device__ __forceinline__ void inl_put(uint32_t (&buf)[16], uint32_t &n, uint32
 __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
                                                   uint4 *__restrict__ rec, uint32_t *__restrict__ bigflag)
 {
+    const uint32_t j = v.perm[p];   // independent of the query chain: issued first
     V2Query q = v2_query(v, p);
     uint32_t a[6] = {}, l[6] = {};
     uint64_t e = 0;
@@ -1003,7 +1006,6 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
     }
-    const uint32_t j = v.perm[p];
     uint4 *r = rec + 4 * (size_t)j;
     if (e <= REC_INLINE) {
         // the six class runs hold L6 <= e + 1 <= 16 elements (T itself is dropped at most once): all their loads are

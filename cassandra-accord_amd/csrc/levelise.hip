@@ -258,7 +258,10 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
                                              : 0u;
                             }
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) v[u] = e0 + (uint32_t)u * LV_G < b ? lv_lds_ld(&lvl[p[u]]) : 0u;
+                            // the first pass uses plain loads (batched by the compiler; a stale 0 only marks the dep
+                            // pending), every re-read is volatile
+                            for (int u = 0; u < 4; ++u)
+                                v[u] = e0 + (uint32_t)u * LV_G >= b ? 0u : scanned ? lv_lds_ld(&lvl[p[u]]) : (uint32_t)lvl[p[u]];
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 if (e0 + (uint32_t)u * LV_G >= b) continue;
