@@ -1278,6 +1278,9 @@ __device__ __forceinline__ uint64_t wave_bitonic_reg(uint64_t x)
 }
 
 // Emit one chunk of up to 64 sorted entries (lane holds x). Returns the updated distinct count.
+// TRANSLATE = false: the TxnId rank is written and the caller maps the txn's ranks to TxnIds in one bulk pass (a
+// dependent global load per chunk would otherwise serialise the chunks)
+template <bool TRANSLATE = true>
 __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t prev, bool has_prev, uint32_t distinct,
                                                uint32_t *kc, const V2Out &o, const TxnCtx &c, uint64_t abase)
 {
@@ -1298,7 +1301,7 @@ __device__ __forceinline__ uint32_t emit_chunk(uint64_t x, bool in, uint64_t pre
         uint32_t slot = kc[kj] + before;
         uint64_t kbase = o.dep_off[c.j0 + kj] - c.e0;
         o.arena[abase + kbase + slot] = (int32_t)idx;
-        if (nw) o.dep_scratch[c.e0 + idx] = o.txn_of_rank[val];
+        if (nw) o.dep_scratch[c.e0 + idx] = TRANSLATE ? o.txn_of_rank[val] : val;
     }
     __builtin_amdgcn_wave_barrier();
     if (in && before == 0) kc[kj] += (uint32_t)__popcll(peers);
@@ -1612,9 +1615,24 @@ __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const u
         const bool in = q < q_hi;
         const uint64_t xq = in ? widen(buf[q]) : 0;
         const uint64_t prev = (in && q > 0) ? widen(buf[q - 1]) : 0;
-        distinct = emit_chunk(xq, in, prev, q > 0, distinct, L.wk_cnt[wave], o, c, abase);
+        distinct = emit_chunk<false>(xq, in, prev, q > 0, distinct, L.wk_cnt[wave], o, c, abase);
     }
     if (wave == NW - 1 && lane == 0) o.u_cnt[t] = distinct;
+    __syncthreads();   // the block's rank writes are visible to the block
+    // ranks -> TxnIds over the txn's distinct entries, four independent load chains per thread
+    uint32_t U = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) U += L.wdist[w];
+    uint32_t *dsc = o.dep_scratch + c.e0;
+    for (uint32_t i0 = tid; i0 < U; i0 += 4 * NT) {
+        uint32_t r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = i0 + (uint32_t)u * NT < U ? dsc[i0 + (uint32_t)u * NT] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i0 + (uint32_t)u * NT < U) r[u] = o.txn_of_rank[r[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i0 + (uint32_t)u * NT < U) dsc[i0 + (uint32_t)u * NT] = r[u];
+    }
 }
 
 // Persistent over the routed list: blocks loop (a grid of one block per listed txn made the 128-KiB launch pay a
@@ -1956,7 +1974,6 @@ __device__ __forceinline__ T gshfl_xor(T v, int m)
     if constexpr (sizeof(T) == 8) return shfl_xor64(v, m);
     else return (T)__shfl_xor(v, m, 64);
 }
-
 // Sorts buf[0, 16 * R) of a ST_G-lane group ascending (positions >= n_valid read as all-ones pads) with R entries per
 // lane in registers, element i = r * 16 + sub: partners at distance < 16 are lanes of the group (shuffles), the others
 // registers of the same lane. Writes the sorted entries back.

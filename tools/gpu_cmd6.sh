@@ -1,0 +1,6 @@
+# session check 6: levelise / KeyDeps tier tests, config-5 A/B, then profiles of configs 2 and 5
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_levelise_gpu.py tests/test_keydeps_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t1.log 2>&1 || { tail -30 gpurun_out/t1.log; exit 1; }
+tail -2 gpurun_out/t1.log
+CFGS="5" STEPS=10 bash tools/gpu_abn.sh new nosleep || exit 1
+bash tools/gpu_prof_a.sh
