@@ -2886,7 +2886,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                    (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
             launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
                    (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
-            launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 256)), dim3(1024), 0,
+            launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
                    (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
         } else {
             // ranks beyond 25 bits: u64 records in the wave tier (k_v3_route sends everything else to the global path)

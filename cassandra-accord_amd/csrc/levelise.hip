@@ -245,10 +245,8 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
 #pragma unroll
             for (int q = 0; q < LV_PEND; ++q) pend[q] = 0;
             while (true) {
-                bool fresh = false;   // this pass published a level or made the first scan
                 if (!done) {   // group-uniform
                     if (!scanned || ovf) {
-                        fresh = !scanned;
                         m = 0; np = 0; ovf = false;
                         for (uint32_t e0 = a + sub; e0 < b; e0 += 4 * LV_G) {
                             uint32_t p[4], v[4];
@@ -301,12 +299,9 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
                         if (sub == 0) *(volatile uint16_t *)&lvl[i] = (uint16_t)(mm + 1);
                         my_max = max(my_max, mm);
                         done = true;
-                        fresh = true;
                     }
                 }
                 if (__all(done)) break;
-                // nothing published and nothing scanned this pass: yield the SIMD to the waves that can progress
-                if (!__any(fresh)) __builtin_amdgcn_s_sleep(1);
             }
         }
         uint4 *ndst = dst4 + (size_t)((c + 1) % 3) * nv;
