@@ -9,6 +9,9 @@
 // awaited by polling its published value.
 #include "prims.hpp"
 
+#include <cstdio>
+#include <vector>
+
 namespace acc {
 
 __global__ __launch_bounds__(BLOCK) void k_lv_keys(uint32_t n, const uint32_t *__restrict__ exec_rank, uint64_t *__restrict__ key)
@@ -186,6 +189,11 @@ __device__ __forceinline__ uint32_t row_max16(uint32_t x)
     return x;
 }
 
+#ifdef ACC_LV_PROF
+// tuning build only: per wave, cycles in the walk loops, waiting at the round barriers, and first-scan passes
+__device__ unsigned long long *g_lv_prof;
+#endif
+
 __device__ __forceinline__ uint32_t lv_lds_ld(const uint16_t *p) { return *(const volatile uint16_t *)p; }
 
 __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int ch_shift,
@@ -209,6 +217,9 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     for (uint32_t v = tid; v < LV_FB && r0 + v <= r1; v += LV_NT) fb[0][v] = foff[r0 + v];
     __syncthreads();
     uint32_t my_max = 0;
+#ifdef ACC_LV_PROF
+    unsigned long long prof_walk = 0, prof_wait = 0, prof_pass = 0;
+#endif
     for (uint32_t c = 0; c < R; ++c) {
         // in flight during the walk: chunk c + 1 of fdep, foff of round c + 1, rstart[c + 3]
         static_assert(LV_PF == 2 && LV_FB == 2 * LV_NT, "two prefetch slots per thread");
@@ -225,6 +236,9 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
         const uint32_t p0 = r0, p1 = r1;
         const uint32_t *fo = fb[c & 1];
         const uint64_t lo_res = c == 0 ? 0ull : (uint64_t)(c - 1) * CH;   // first entry resident in LDS
+#ifdef ACC_LV_PROF
+        const unsigned long long t_a = clock64();
+#endif
         constexpr uint32_t GPW = 64 / LV_G;   // positions per wave
         for (uint32_t base = p0 + GPW * wave; base < p1; base += LV_GROUPS) {
             // wave w holds positions base + {0 .. GPW - 1}; the waves stride by LV_GROUPS positions
@@ -301,9 +315,15 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
                         done = true;
                     }
                 }
+#ifdef ACC_LV_PROF
+                ++prof_pass;
+#endif
                 if (__all(done)) break;
             }
         }
+#ifdef ACC_LV_PROF
+        const unsigned long long t_b = clock64();
+#endif
         uint4 *ndst = dst4 + (size_t)((c + 1) % 3) * nv;
         if (pfc && tid < nv) ndst[tid] = pf0;
         if (pfc && tid + LV_NT < nv) ndst[tid + LV_NT] = pf1;
@@ -311,7 +331,16 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
         if (pfr && r1 + tid + LV_NT <= r2) fb[(c + 1) & 1][tid + LV_NT] = pfo1;
         r0 = r1; r1 = r2; r2 = r3;
         __syncthreads();
+#ifdef ACC_LV_PROF
+        if (lane == 0) {
+            prof_walk += t_b - t_a;
+            prof_wait += clock64() - t_b;
+        }
+#endif
     }
+#ifdef ACC_LV_PROF
+    if (lane == 0) { g_lv_prof[3 * wave] = prof_walk; g_lv_prof[3 * wave + 1] = prof_wait; g_lv_prof[3 * wave + 2] = prof_pass; }
+#endif
     for (uint32_t i = tid; i < n; i += LV_NT) level[order_exec[i]] = (uint32_t)lvl[i] - 1u;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor(my_max, d, 64));
@@ -393,9 +422,26 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         const int ch_shift = 31 - __builtin_clz(ch);
         uint32_t *rstart = ctx->get<uint32_t>("lv_rstart", (size_t)(E >> ch_shift) + 3);
         launch(ctx, "lv_rounds", k_lv_rounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, ch_shift, (const uint32_t *)foff, rstart);
+#ifdef ACC_LV_PROF
+        {
+            unsigned long long *pb = ctx->get<unsigned long long>("lv_prof", 3 * 16);
+            ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lv_prof), &pb, sizeof pb, 0, hipMemcpyHostToDevice, st));
+        }
+#endif
         launch(ctx, "lv_walk", k_lv_lds, dim3(1), dim3(LV_NT), 0, n, npad, ch_shift, (const uint32_t *)foff,
                (const uint16_t *)fdep, (const uint32_t *)rstart, (const uint32_t *)order_exec, level, maxl);
         ctx->stat("levelise.lds_tier", 1);
+#ifdef ACC_LV_PROF
+        {
+            unsigned long long *pb = ctx->get<unsigned long long>("lv_prof", 3 * 16);
+            std::vector<unsigned long long> h(48);
+            ACC_HIP(hipMemcpyAsync(h.data(), pb, 48 * 8, hipMemcpyDeviceToHost, st));
+            ACC_HIP(hipStreamSynchronize(st));
+            double w = 0, q = 0, np = 0;
+            for (int i = 0; i < 16; ++i) { w += h[3 * i]; q += h[3 * i + 1]; np += h[3 * i + 2]; }
+            fprintf(stderr, "[lv_prof] per wave avg: walk %.0f cycles, round-barrier wait %.0f cycles, passes %.0f\n", w / 16, q / 16, np / 16);
+        }
+#endif
     } else {
         ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
