@@ -338,16 +338,26 @@ __device__ T *lds_merge_runs(T *src, T *dst, uint32_t *rs, uint32_t NR, uint32_t
     return src;
 }
 
-// order-preserving in-place unique of the sorted s[0..n) (pads last); returns the count. n <= ML_NT * MAXI.
-template <class T, int MAXI>
-__device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t n, T pad, uint32_t *scan_lds)
+// pads s[N, up to a multiple of ML_NT) for lds_unique
+template <class T>
+__device__ __forceinline__ uint32_t lds_pad_block(T *s, uint32_t N, T pad)
 {
-    const uint32_t per = (n + ML_NT - 1) / ML_NT, base = threadIdx.x * per;
+    const uint32_t np = (N + ML_NT - 1) / ML_NT * ML_NT;
+    for (uint32_t i = N + threadIdx.x; i < np; i += ML_NT) s[i] = pad;
+    __syncthreads();
+    return np;
+}
+
+// order-preserving in-place unique of the sorted s[0..np) (pads last); returns the count. np = ML_NT * per.
+template <class T, int MAXI>
+__device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t np, T pad, uint32_t *scan_lds)
+{
+    const uint32_t per = np / ML_NT, base = threadIdx.x * per;
     T x[MAXI];
     uint32_t f = 0, c = 0;
 #pragma unroll
     for (int q = 0; q < MAXI; ++q) {
-        if ((uint32_t)q < per && base + q < n) {
+        if ((uint32_t)q < per) {
             const uint32_t i = base + q;
             x[q] = s[i];
             const bool u = x[q] != pad && (i == 0 || s[i - 1] != x[q]);
@@ -359,7 +369,7 @@ __device__ __forceinline__ uint32_t lds_unique(T *s, uint32_t n, T pad, uint32_t
     uint32_t o = block_exclusive<uint32_t, OpAdd<uint32_t>, ML_NT / 64>(c, OpAdd<uint32_t>(), scan_lds, total);
 #pragma unroll
     for (int q = 0; q < MAXI; ++q)
-        if ((uint32_t)q < per && base + q < n && ((f >> q) & 1u)) s[o++] = x[q];
+        if ((uint32_t)q < per && ((f >> q) & 1u)) s[o++] = x[q];
     __syncthreads();
     return total;
 }
@@ -392,15 +402,15 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
                                                  const int32_t *__restrict__ k2v, MlPlan pl, MlOut o)
 {
     extern __shared__ uint64_t dsm[];
-    // [rawk: kc u64 (later kidx: kc u32 + hdr: kc u32)][sort: 2 x sp u32 (merge ping-pong)][rawv: vc u32][rawo: oc u16]
+    // [rawk: kc u64][sort: 2 x sp u32 (merge ping-pong)][rawv: vc u32][rawo: oc u32][hdr: kc u32]
     uint64_t *rawk = dsm;
     uint32_t *sort32 = reinterpret_cast<uint32_t *>(dsm + pl.kc);
     uint32_t *sort32b = sort32 + pl.sp;
     uint64_t *sort64 = reinterpret_cast<uint64_t *>(sort32);
     uint64_t *sort64b = reinterpret_cast<uint64_t *>(sort32b);
     uint32_t *rawv = sort32 + 2 * pl.sp;
-    uint16_t *rawo = reinterpret_cast<uint16_t *>(rawv + pl.vc);   // keysToTxnIds ints of a fitting group are < 4096
-    uint32_t *hdr = reinterpret_cast<uint32_t *>(rawk) + pl.kc;     // after the key phase
+    uint32_t *rawo = rawv + pl.vc;
+    uint32_t *hdr = rawo + pl.oc;
     __shared__ uint32_t rk[ML_REP + 1], rv[ML_REP + 1], ro[ML_REP + 1];
     __shared__ uint32_t scan_lds[ML_NT / 64];
     __shared__ uint32_t rsm[ML_REP + 1];   // run starts of the merge tree
@@ -419,18 +429,9 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     // one coalesced pass over the group's three input ranges
     for (uint32_t i = tid; i < NK; i += ML_NT) rawk[i] = key_code[KA + i];
     for (uint32_t i = tid; i < NV; i += ML_NT) rawv[i] = txn_rank[VA + i];
-    uint64_t err = 0;
-    for (uint32_t i = tid; i < NO; i += ML_NT) {
-        const int32_t x = k2v[OA + i];
-        if (x < 0 || x > (int32_t)ML_OC) {   // invalid in any slot of a fitting group: header (> no) or value (>= nv)
-            const uint32_t r = lds_ub(ro, nrep + 1, i) - 1;
-            err |= i - ro[r] < rk[r + 1] - rk[r] ? 8 : 16;
-            rawo[i] = 0;
-        } else {
-            rawo[i] = (uint16_t)x;
-        }
-    }
+    for (uint32_t i = tid; i < NO; i += ML_NT) rawo[i] = (uint32_t)k2v[OA + i];
     __syncthreads();
+    uint64_t err = 0;
     const uint64_t PADK = ~0ull;
     const uint32_t PAD32 = 0xFFFFFFFFu;
     // ---- keys: sort, unique, write, map every key slot to its merged index
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rk[r];
     __syncthreads();
     uint64_t *ks = lds_merge_runs(sort64, sort64b, rsm, nrep, NK);
-    const uint32_t Kg = lds_unique<uint64_t, ML_KC / ML_NT>(ks, NK, PADK, scan_lds);
+    const uint32_t Kg = lds_unique<uint64_t, ML_KC / ML_NT>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
     uint32_t kmap[ML_KC / ML_NT];
 #pragma unroll
     for (int q = 0; q < ML_KC / ML_NT; ++q) {
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rv[r];
     __syncthreads();
     uint32_t *vs = lds_merge_runs(sort32, sort32b, rsm, nrep, NV);
-    const uint32_t Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, NV, PAD32, scan_lds);
+    const uint32_t Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
     for (uint32_t i = tid; i < NV; i += ML_NT) {
         const uint32_t v = rawv[i];
         uint32_t a = 0, b = Ug;
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
         const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
         const uint32_t qq = q - ro[r];
-        const uint16_t *h = rawo + ro[r];
+        const uint32_t *h = rawo + ro[r];
         if (nk == 0) { err |= 8; continue; }   // keysToTxnIds entries without keys
         if (qq < nk) {
             const uint32_t e = h[qq], prev = qq == 0 ? nk : h[qq - 1];
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
     __syncthreads();
     uint32_t *es = lds_merge_runs(sort32, sort32b, rsm, nrep, NE);
-    const uint32_t Eu = lds_unique<uint32_t, ML_VC / ML_NT>(es, NE, PAD32, scan_lds);
+    const uint32_t Eu = lds_unique<uint32_t, ML_VC / ML_NT>(es, lds_pad_block(es, NE, PAD32), PAD32, scan_lds);
     for (uint32_t c = tid; c < Eu; c += ML_NT) {
         const uint32_t kk = es[c] >> 16;
         if (c + 1 == Eu || (es[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
@@ -608,14 +609,14 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, gmax, 4 * 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
         if (ctx->pinned[0] == 0) {
+            auto rb = [](uint64_t n) { return std::max<uint64_t>(ML_NT, (n + ML_NT - 1) / ML_NT * ML_NT); };
             MlPlan pl;
             pl.kc = (uint32_t)ctx->pinned[1];
             pl.vc = (uint32_t)ctx->pinned[2];
             pl.oc = (uint32_t)ctx->pinned[3];
+            pl.sp = (uint32_t)std::max({ 2 * rb(pl.kc), rb(pl.vc), rb(ctx->pinned[4]) });   // one merge buffer (u32)
             pl.kc = (pl.kc + 1) & ~1u;   // keep the u32 areas after rawk 8-byte aligned
-            pl.sp = (uint32_t)std::max<uint64_t>({ 2ull * pl.kc, pl.vc, ctx->pinned[4], 2 });   // one merge buffer (u32)
-            pl.sp = (pl.sp + 1) & ~1u;
-            pl.bytes = 8 * pl.kc + 8 * pl.sp + 4 * pl.vc + 2 * pl.oc;
+            pl.bytes = 8 * pl.kc + 8 * pl.sp + 4 * pl.vc + 4 * pl.oc + 4 * pl.kc;
             MlOut mo;
             mo.s_key = ctx->get<uint64_t>("m_s_key", NK + 1);
             mo.s_val = ctx->get<uint32_t>("m_s_val", NV + 1);
