@@ -235,7 +235,10 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
         const uint32_t r3 = c + 3 <= R ? rstart[c + 3] : n;
         const uint32_t p0 = r0, p1 = r1;
         const uint32_t *fo = fb[c & 1];
-        const uint64_t lo_res = c == 0 ? 0ull : (uint64_t)(c - 1) * CH;   // first entry resident in LDS
+        // list entries of this round: chunk c (slot c % 3) and chunk c - 1 (slot (c + 2) % 3) are resident; a list
+        // longer than a chunk may start before them and reads those entries from HBM
+        const uint32_t cur0 = c * CH, prv0 = c == 0 ? 0u : (c - 1) * CH;
+        const uint16_t *scur = slots + (size_t)(c % 3) * CH, *sprv = slots + (size_t)((c + 2) % 3) * CH;
 #ifdef ACC_LV_PROF
         const unsigned long long t_a = clock64();
 #endif
@@ -267,22 +270,29 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const uint32_t e = e0 + (uint32_t)u * LV_G;
-                                p[u] = e < b ? (e >= lo_res ? slots[(size_t)((e >> ch_shift) % 3) * CH + (e & (CH - 1))]
-                                                            : (uint32_t)fdep[e])
-                                             : 0u;
+                                p[u] = 0;
+                                if (e < b) p[u] = e >= cur0 ? scur[e - cur0] : e >= prv0 ? sprv[e - prv0] : (uint32_t)fdep[e];
                             }
-#pragma unroll
                             // the first pass uses plain loads (batched by the compiler; a stale 0 only marks the dep
                             // pending), every re-read is volatile
+#pragma unroll
                             for (int u = 0; u < 4; ++u)
                                 v[u] = e0 + (uint32_t)u * LV_G >= b ? 0u : scanned ? lv_lds_ld(&lvl[p[u]]) : (uint32_t)lvl[p[u]];
+                            bool z = false;
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 if (e0 + (uint32_t)u * LV_G >= b) continue;
-                                if (v[u]) { m = max(m, v[u]); continue; }
+                                m = max(m, v[u]);
+                                z |= v[u] == 0;
+                            }
+                            if (z) {   // rare: keep the unpublished deps for the retries
 #pragma unroll
-                                for (int q = 0; q < LV_PEND; ++q) if ((uint32_t)q == np) pend[q] = p[u];
-                                if (np < LV_PEND) ++np; else ovf = true;
+                                for (int u = 0; u < 4; ++u) {
+                                    if (e0 + (uint32_t)u * LV_G >= b || v[u]) continue;
+#pragma unroll
+                                    for (int q = 0; q < LV_PEND; ++q) if ((uint32_t)q == np) pend[q] = p[u];
+                                    if (np < LV_PEND) ++np; else ovf = true;
+                                }
                             }
                         }
                         scanned = true;

@@ -1,0 +1,7 @@
+# session check 8: levelise tests, config-5 A/B of the cheaper first scan, levelise phase split
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_levelise_gpu.py tests/test_merge_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t1.log 2>&1 || { tail -30 gpurun_out/t1.log; exit 1; }
+tail -2 gpurun_out/t1.log
+CFGS="5" STEPS=10 bash tools/gpu_abn.sh new prelv || exit 1
+ACC_LIB_PATH=tools/prof/lvprof.so timeout -k 10 200 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu > gpurun_out/lvprof.log 2>&1 || { tail -20 gpurun_out/lvprof.log; exit 1; }
+grep lv_prof gpurun_out/lvprof.log | tail -2
