@@ -118,7 +118,6 @@ constexpr int LV_NT = 1024;
 #define ACC_LV_G 16
 #endif
 constexpr int LV_G = ACC_LV_G;         // lanes per position (16: one DPP row)
-constexpr int LV_GROUPS = LV_NT / LV_G;
 constexpr uint32_t LV_CH_MAX = 16384;  // entries per chunk
 constexpr int LV_PF = LV_CH_MAX / 8 / LV_NT;   // uint4 of a chunk per thread
 
@@ -206,7 +205,7 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     __shared__ uint32_t fb[2][LV_FB];   // foff of the round's positions (double-buffered)
     const uint32_t CH = 1u << ch_shift;
     uint16_t *lvl = L, *slots = L + npad;
-    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_G - 1), wave = tid >> 6, gi = lane / LV_G;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_G - 1), gi = lane / LV_G;
     for (uint32_t i = tid; i < n; i += LV_NT) lvl[i] = 0;
     // chunk c -> slot c % 3: CH / 8 uint4 of fdep (reads may run past Ef into the buffer's padding)
     const uint32_t nv = CH / 8;
@@ -243,8 +242,9 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
         const unsigned long long t_a = clock64();
 #endif
         constexpr uint32_t GPW = 64 / LV_G;   // positions per wave
-        for (uint32_t base = p0 + GPW * wave; base < p1; base += LV_GROUPS) {
-            // wave w holds positions base + {0 .. GPW - 1}; the waves stride by LV_GROUPS positions
+        for (uint32_t base = p0 + GPW * (tid >> 6); base < p1; base += LV_NT / LV_G) {
+            // wave w holds positions base + {0 .. GPW - 1}; the waves stride by LV_NT / LV_G positions (a static
+            // split measured faster than claiming positions through an LDS counter)
             const uint32_t i = base + gi;
             const bool valid = i < p1;
             uint32_t a = 0, b = 0;
@@ -349,6 +349,7 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
 #endif
     }
 #ifdef ACC_LV_PROF
+    const uint32_t wave = tid >> 6;
     if (lane == 0) { g_lv_prof[3 * wave] = prof_walk; g_lv_prof[3 * wave + 1] = prof_wait; g_lv_prof[3 * wave + 2] = prof_pass; }
 #endif
     for (uint32_t i = tid; i < n; i += LV_NT) level[order_exec[i]] = (uint32_t)lvl[i] - 1u;
