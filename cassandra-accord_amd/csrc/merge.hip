@@ -12,6 +12,7 @@
 //   3. unique + per-group counts (scans) -> per-group CSR in Java layout; each (key, value) entry becomes
 //      the index of the value in the group's txnId array (binary search within the group).
 #include <algorithm>
+#include <cstdio>
 
 #include "dict.hpp"
 
@@ -396,6 +397,14 @@ struct MlPlan {
     uint32_t bytes;
 };
 
+#ifdef ACC_ML_PROF
+// tuning build only: cycles per phase of k_m_lds summed over workgroups (thread 0's view)
+__device__ unsigned long long *g_ml_prof;
+#define ML_PH(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); atomicAdd(&g_ml_prof[k], t_ - ml_t); ml_t = t_; } } while (0)
+#else
+#define ML_PH(k) ((void)0)
+#endif
+
 __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__restrict__ grp_off, const uint64_t *__restrict__ key_off,
                                                  const uint64_t *__restrict__ key_code, const uint64_t *__restrict__ val_off,
                                                  const uint32_t *__restrict__ txn_rank, const uint64_t *__restrict__ k2v_off,
@@ -416,6 +425,9 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     __shared__ uint32_t rsm[ML_REP + 1];   // run starts of the merge tree
     const uint32_t gi = blockIdx.x;
     const uint32_t tid = threadIdx.x;
+#ifdef ACC_ML_PROF
+    unsigned long long ml_t = clock64();
+#endif
     const uint64_t R0 = grp_off[gi];
     const uint32_t nrep = (uint32_t)(grp_off[gi + 1] - R0);
     const uint64_t KA = key_off[R0], VA = val_off[R0], OA = k2v_off[R0];
@@ -446,6 +458,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     }
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rk[r];
     __syncthreads();
+    ML_PH(0);
     uint64_t *ks = lds_merge_runs(sort64, sort64b, rsm, nrep, NK);
     const uint32_t Kg = lds_unique<uint64_t, ML_KC / ML_NT>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
     uint32_t kmap[ML_KC / ML_NT];
@@ -467,6 +480,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         const uint32_t i = tid + q * ML_NT;
         if (i < NK) kidx[i] = kmap[q];
     }
+    ML_PH(1);
     // ---- TxnIds: same
     for (uint32_t i = tid; i < NV; i += ML_NT) {
         uint32_t x = PAD32;
@@ -479,6 +493,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     }
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rv[r];
     __syncthreads();
+    ML_PH(2);
     uint32_t *vs = lds_merge_runs(sort32, sort32b, rsm, nrep, NV);
     const uint32_t Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
     for (uint32_t i = tid; i < NV; i += ML_NT) {
@@ -489,6 +504,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     }
     for (uint32_t u = tid; u < Ug; u += ML_NT) o.s_val[VA + u] = vs[u];
     __syncthreads();
+    ML_PH(3);
     // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
     for (uint32_t q = tid; q < NO; q += ML_NT) {
         const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
@@ -517,8 +533,10 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     for (uint32_t k = tid; k < Kg; k += ML_NT) hdr[k] = 0;
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
     __syncthreads();
+    ML_PH(4);
     uint32_t *es = lds_merge_runs(sort32, sort32b, rsm, nrep, NE);
     const uint32_t Eu = lds_unique<uint32_t, ML_VC / ML_NT>(es, lds_pad_block(es, NE, PAD32), PAD32, scan_lds);
+    ML_PH(5);
     for (uint32_t c = tid; c < Eu; c += ML_NT) {
         const uint32_t kk = es[c] >> 16;
         if (c + 1 == Eu || (es[c + 1] >> 16) != kk) hdr[kk] = Kg + c + 1;
@@ -543,6 +561,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         o.cnt_v[gi] = Ug;
         o.cnt_o[gi] = Kg + Eu;
     }
+    ML_PH(6);
     block_or1<ML_NT / 64>(err, o.errs);
 }
 
@@ -625,8 +644,23 @@ void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view)
             mo.cnt_v = ctx->get<uint64_t>("m_cnt_v", ng);
             mo.cnt_o = ctx->get<uint64_t>("m_cnt_o", ng);
             mo.errs = g + 2;
+#ifdef ACC_ML_PROF
+            unsigned long long *mlp = ctx->get<unsigned long long>("ml_prof", 8);
+            ACC_HIP(hipMemsetAsync(mlp, 0, 64, st));
+            ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ml_prof), &mlp, sizeof mlp, 0, hipMemcpyHostToDevice, st));
+#endif
             launch(ctx, "m_lds", k_m_lds, dim3(ng), dim3(ML_NT), pl.bytes, ng, grp_off, key_off, key_code, val_off, txn_rank,
                    k2v_off, k2v, pl, mo);
+#ifdef ACC_ML_PROF
+            {
+                unsigned long long h[8];
+                ACC_HIP(hipMemcpyAsync(h, mlp, 64, hipMemcpyDeviceToHost, st));
+                ACC_HIP(hipStreamSynchronize(st));
+                fprintf(stderr, "[ml_prof] per group cycles: stage %.0f keys %.0f tx-prep %.0f tx %.0f ent-prep %.0f ent %.0f out %.0f\n",
+                        h[0] / (double)ng, h[1] / (double)ng, h[2] / (double)ng, h[3] / (double)ng, h[4] / (double)ng,
+                        h[5] / (double)ng, h[6] / (double)ng);
+            }
+#endif
             uint64_t *ko = ctx->get<uint64_t>("m_k_gstart", (size_t)ng + 1);
             uint64_t *vo = ctx->get<uint64_t>("m_v_gstart", (size_t)ng + 1);
             uint64_t *oo = ctx->get<uint64_t>("m_out_k2v_off", (size_t)ng + 1);
