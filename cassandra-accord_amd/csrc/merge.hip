@@ -261,6 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_m_key_of_slot(uint64_t R, const uint6
 // per-reply validation of k_m_prep (KeyDeps ctor / checkValid) is done on the same loaded records.
 
 constexpr int ML_REP = 256, ML_KC = 1024, ML_VC = 4096, ML_OC = 4096;
+constexpr int ML_WB = 1024;   // TxnId bitmap words (rank spans up to 32768)
 constexpr int ML_NT = 512;   // threads per group: more waves per CU for the LDS-latency-bound merge tree and searches
 
 // per group: does it fit the LDS tier (offsets monotone, sizes within the caps)? g[3] |= 1 if some group does not
@@ -423,6 +424,7 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     __shared__ uint32_t rk[ML_REP + 1], rv[ML_REP + 1], ro[ML_REP + 1];
     __shared__ uint32_t scan_lds[ML_NT / 64];
     __shared__ uint32_t rsm[ML_REP + 1];   // run starts of the merge tree
+    __shared__ uint32_t wpre[ML_WB];       // TxnId bitmap: set bits before each word
     const uint32_t gi = blockIdx.x;
     const uint32_t tid = threadIdx.x;
 #ifdef ACC_ML_PROF
@@ -481,29 +483,71 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         if (i < NK) kidx[i] = kmap[q];
     }
     ML_PH(1);
-    // ---- TxnIds: same
+    // ---- TxnIds: the union as a bitmap over the group's rank span when it fits (config 5: the batch's ranks), so
+    // each TxnId's merged index is a word prefix + popcount; otherwise the merge tree + unique + binary searches
+    uint32_t vlo = 0xFFFFFFFFu, vhi = 0;
     for (uint32_t i = tid; i < NV; i += ML_NT) {
         uint32_t x = PAD32;
-        if (i < NV) {
-            const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
-            if (i > rv[r] && rawv[i - 1] >= rawv[i]) err |= 4;   // txnIds sorted unique
-            if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawv[i];
-        }
-        sort32[i] = x;
+        const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
+        if (i > rv[r] && rawv[i - 1] >= rawv[i]) err |= 4;   // txnIds sorted unique
+        if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawv[i];
+        if (x != PAD32) { vlo = min(vlo, x); vhi = max(vhi, x); }
+        sort32b[i] = x;
     }
-    for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rv[r];
-    __syncthreads();
+    uint32_t ghi, glo_inv;
+    (void)block_exclusive<uint32_t, OpMax<uint32_t>, ML_NT / 64>(vhi, OpMax<uint32_t>(), scan_lds, ghi);
+    (void)block_exclusive<uint32_t, OpMax<uint32_t>, ML_NT / 64>(~vlo, OpMax<uint32_t>(), scan_lds, glo_inv);
+    const uint32_t glo = ~glo_inv;
+    const uint64_t span = glo <= ghi ? (uint64_t)ghi - glo + 1 : 0;
+    const uint32_t W = (uint32_t)((span + 31) / 32);
     ML_PH(2);
-    uint32_t *vs = lds_merge_runs(sort32, sort32b, rsm, nrep, NV);
-    const uint32_t Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
-    for (uint32_t i = tid; i < NV; i += ML_NT) {
-        const uint32_t v = rawv[i];
-        uint32_t a = 0, b = Ug;
-        while (a < b) { uint32_t m = (a + b) >> 1; if (vs[m] < v) a = m + 1; else b = m; }
-        rawv[i] = a;   // each thread rewrites only its own slots
+    uint32_t Ug;
+    if (W <= (uint32_t)ML_WB && W <= pl.sp) {   // block-uniform
+        uint32_t *bm = sort32;
+        for (uint32_t w = tid; w < W; w += ML_NT) bm[w] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < NV; i += ML_NT) {
+            const uint32_t x = sort32b[i];
+            if (x != PAD32) atomicOr(&bm[(x - glo) >> 5], 1u << ((x - glo) & 31u));
+        }
+        __syncthreads();
+        const uint32_t per = (W + ML_NT - 1) / ML_NT, w0 = min(W, tid * per), w1 = min(W, w0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; ++w) cnt += (uint32_t)__popc(bm[w]);
+        uint32_t run = block_exclusive<uint32_t, OpAdd<uint32_t>, ML_NT / 64>(cnt, OpAdd<uint32_t>(), scan_lds, Ug);
+        for (uint32_t w = w0; w < w1; ++w) { wpre[w] = run; run += (uint32_t)__popc(bm[w]); }
+        __syncthreads();
+        for (uint32_t i = tid; i < NV; i += ML_NT) {
+            const uint32_t x = sort32b[i];
+            uint32_t idx = 0;   // replies without entries: their TxnIds are never referenced
+            if (x != PAD32) {
+                const uint32_t d = x - glo, w = d >> 5;
+                idx = wpre[w] + (uint32_t)__popc(bm[w] & ((1u << (d & 31u)) - 1u));
+            }
+            rawv[i] = idx;
+        }
+        for (uint32_t w = tid; w < W; w += ML_NT) {
+            uint32_t bits = bm[w], k = wpre[w];
+            while (bits) {
+                o.s_val[VA + k++] = glo + 32u * w + (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1u;
+            }
+        }
+        __syncthreads();
+    } else {
+        for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rv[r];
+        __syncthreads();
+        uint32_t *vs = lds_merge_runs(sort32b, sort32, rsm, nrep, NV);
+        Ug = lds_unique<uint32_t, ML_VC / ML_NT>(vs, lds_pad_block(vs, NV, PAD32), PAD32, scan_lds);
+        for (uint32_t i = tid; i < NV; i += ML_NT) {
+            const uint32_t v = rawv[i];
+            uint32_t a = 0, b = Ug;
+            while (a < b) { uint32_t m = (a + b) >> 1; if (vs[m] < v) a = m + 1; else b = m; }
+            rawv[i] = a;   // each thread rewrites only its own slots
+        }
+        for (uint32_t u = tid; u < Ug; u += ML_NT) o.s_val[VA + u] = vs[u];
+        __syncthreads();
     }
-    for (uint32_t u = tid; u < Ug; u += ML_NT) o.s_val[VA + u] = vs[u];
-    __syncthreads();
     ML_PH(3);
     // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
     for (uint32_t q = tid; q < NO; q += ML_NT) {

@@ -152,3 +152,26 @@ def _sorted_reply(r):
         body += list(lists[i])
         hdr.append(nk + len(body))
     return [keys[i] for i in order], vals, hdr + body
+
+
+@pytest.mark.parametrize("scale", [1, 5, 40, 1 << 18])
+def test_merge_txnid_bitmap_and_merge_tree_paths(ctx, scale):
+    """The LDS tier unions a group's TxnIds through a bitmap when their rank span fits 32768 and through the merge tree
+    otherwise: ranks scaled so that groups fall on either side (and, within one launch, on both)."""
+    import oracle
+    from accord_amd.deps import keydeps_merge
+    rng = np.random.RandomState(7000 + scale)
+    groups = []
+    for gi in range(30):
+        g = []
+        for _ in range(rng.randint(0, 16)):
+            keys, vals, k2v = gen_keydeps(rng)
+            s = scale if gi % 2 == 0 else 1
+            g.append((keys, [v * s + (gi % 3) for v in vals], k2v))
+        groups.append(g)
+    m = pack_groups(groups)
+    out = keydeps_merge(ctx, m)
+    ref = oracle.keydeps_merge(m)
+    for k in ref:
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+    check_groups(out, groups)
