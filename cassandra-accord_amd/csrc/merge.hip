@@ -458,21 +458,40 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         }
         sort64[i] = x;
     }
-    for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = rk[r];
     __syncthreads();
     ML_PH(0);
-    uint64_t *ks = lds_merge_runs(sort64, sort64b, rsm, nrep, NK);
-    const uint32_t Kg = lds_unique<uint64_t, ML_KC / ML_NT>(ks, lds_pad_block(ks, NK, PADK), PADK, scan_lds);
+    // the distinct keys of the replies with entries: a slot is a first occurrence unless an earlier slot holds the
+    // same key (a group's replies repeat the same few keys, so duplicates stop at the first reply); compacted, then
+    // each slot's merged index = the number of distinct keys below it (sorted output without a sort)
+    uint64_t *dk = sort64b;
+    uint32_t fmask = 0, nf = 0;
+#pragma unroll
+    for (int q = 0; q < ML_KC / ML_NT; ++q) {
+        const uint32_t i = tid + q * ML_NT;
+        if (i < NK) {
+            const uint64_t x = sort64[i];
+            bool first = x != PADK;
+            for (uint32_t j = 0; first && j < i; ++j) first = sort64[j] != x;
+            fmask |= (first ? 1u : 0u) << q;
+            nf += first;
+        }
+    }
+    uint32_t Kg;
+    uint32_t fpos = block_exclusive<uint32_t, OpAdd<uint32_t>, ML_NT / 64>(nf, OpAdd<uint32_t>(), scan_lds, Kg);
+#pragma unroll
+    for (int q = 0; q < ML_KC / ML_NT; ++q)
+        if ((fmask >> q) & 1u) dk[fpos++] = sort64[tid + q * ML_NT];
+    __syncthreads();
     uint32_t kmap[ML_KC / ML_NT];
 #pragma unroll
     for (int q = 0; q < ML_KC / ML_NT; ++q) {
         const uint32_t i = tid + q * ML_NT;
-        if (i < Kg) o.s_key[KA + i] = ks[i];
         if (i < NK) {
             const uint64_t kc = rawk[i];
-            uint32_t a = 0, b = Kg;
-            while (a < b) { uint32_t m = (a + b) >> 1; if (ks[m] < kc) a = m + 1; else b = m; }
-            kmap[q] = a;
+            uint32_t below = 0;
+            for (uint32_t j = 0; j < Kg; ++j) below += dk[j] < kc;
+            kmap[q] = below;
+            if ((fmask >> q) & 1u) o.s_key[KA + below] = kc;
         }
     }
     __syncthreads();
@@ -549,7 +568,16 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         __syncthreads();
     }
     ML_PH(3);
-    // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated
+    // ---- (key, TxnId) entries as (merged key << 16 | TxnId index), headers validated. When the group's Kg x Ug
+    // (key, TxnId) grid fits, the entries set bits of a key-major bitmap: key k's TxnIds are then its row's set bits in
+    // order, and every offset a word prefix (no merge, no unique)
+    const uint32_t WU = (Ug + 31) / 32, WE = Kg * WU;
+    const bool ebm = WE <= (uint32_t)ML_WB && WE <= pl.sp;   // block-uniform
+    uint32_t *ebits = sort32b;
+    if (ebm) {
+        for (uint32_t w = tid; w < WE; w += ML_NT) ebits[w] = 0;
+        __syncthreads();
+    }
     for (uint32_t q = tid; q < NO; q += ML_NT) {
         const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
         const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
@@ -572,7 +600,39 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
             if (qq > start && (int32_t)h[qq - 1] >= xv) err |= 32;
             if (no != nk) x = (kidx[rk[r] + i] << 16) | rawv[rv[r] + (uint32_t)xv];
         }
-        sort32[q - rk[r + 1]] = x;
+        if (!ebm) sort32[q - rk[r + 1]] = x;
+        else if (x != PAD32) {
+            const uint32_t u = x & 0xFFFFu;
+            atomicOr(&ebits[(x >> 16) * WU + (u >> 5)], 1u << (u & 31u));
+        }
+    }
+    if (ebm) {
+        __syncthreads();
+        const uint32_t per = (WE + ML_NT - 1) / ML_NT, w0 = min(WE, tid * per), w1 = min(WE, w0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; ++w) cnt += (uint32_t)__popc(ebits[w]);
+        uint32_t Eu;
+        uint32_t run = block_exclusive<uint32_t, OpAdd<uint32_t>, ML_NT / 64>(cnt, OpAdd<uint32_t>(), scan_lds, Eu);
+        for (uint32_t w = w0; w < w1; ++w) { wpre[w] = run; run += (uint32_t)__popc(ebits[w]); }
+        __syncthreads();
+        for (uint32_t k = tid; k < Kg; k += ML_NT)   // header: end offset of key k's TxnId indices
+            o.s_k2v[OA + k] = (int32_t)(Kg + (k + 1 < Kg ? wpre[(k + 1) * WU] : Eu));
+        for (uint32_t w = tid; w < WE; w += ML_NT) {
+            uint32_t bits = ebits[w], c = Kg + wpre[w];
+            const uint32_t ub = 32u * (w % WU);
+            while (bits) {
+                o.s_k2v[OA + c++] = (int32_t)(ub + (uint32_t)__builtin_ctz(bits));
+                bits &= bits - 1u;
+            }
+        }
+        if (tid == 0) {
+            o.cnt_k[gi] = Kg;
+            o.cnt_v[gi] = Ug;
+            o.cnt_o[gi] = Kg + Eu;
+        }
+        ML_PH(6);
+        block_or1<ML_NT / 64>(err, o.errs);
+        return;
     }
     for (uint32_t k = tid; k < Kg; k += ML_NT) hdr[k] = 0;
     for (uint32_t r = tid; r <= nrep; r += ML_NT) rsm[r] = ro[r] - rk[r];   // reply r's entries start there
