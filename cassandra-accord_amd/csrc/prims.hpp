@@ -355,14 +355,38 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_hist(const uint64_t *__rest
     hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
+// One workgroup per digit: the digit's per-tile counts (a column of hist) become its exclusive prefix over the tiles,
+// in place, and total[digit] the column sum. The digits' bases (an exclusive scan of 256 totals) are formed by every
+// scatter block itself, so a pass needs no device-wide look-back scan over 256 x tiles counters.
+static __global__ __launch_bounds__(BLOCK) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t ntiles,
+                                                      uint32_t *__restrict__ total)
+{
+    __shared__ uint32_t red[WAVES];
+    uint32_t *col = hist + (size_t)blockIdx.x * ntiles;
+    constexpr uint32_t PER = 8;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < ntiles; base += BLOCK * PER) {
+        const uint32_t i0 = base + threadIdx.x * PER;
+        uint32_t v[PER], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) { v[j] = i0 + j < ntiles ? col[i0 + j] : 0u; sum += v[j]; }
+        uint32_t tot;
+        uint32_t run = carry + block_exclusive(sum, OpAdd<uint32_t>(), red, tot);
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) if (i0 + j < ntiles) { col[i0 + j] = run; run += v[j]; }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) total[blockIdx.x] = carry;
+}
+
 // Stable scatter: element order inside a tile is (k, wave, lane); ranks come from 8 ballots per
 // wave (peer mask of equal digits) plus a per-digit running count across waves and k steps. The tile is first
 // reordered by digit in LDS (48 KiB: keys + values), then written out digit run by digit run, so neighbouring
 // lanes store to neighbouring addresses (~16 elements per digit per tile) instead of one element per digit.
 static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                      size_t n, int shift, const uint32_t *__restrict__ hist_scanned,
-                                                      uint32_t ntiles, int iota_vals)
+                                                      size_t n, int shift, const uint32_t *__restrict__ colpre,
+                                                      const uint32_t *__restrict__ dtotal, uint32_t ntiles, int iota_vals)
 {
     __shared__ uint64_t sk[RS_TILE];
     __shared__ uint32_t sv[RS_TILE];
@@ -372,12 +396,17 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__r
     __shared__ uint32_t red[WAVES];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    // this tile's count of digit tid = difference of neighbouring entries of the exclusive (digit, tile) scan
+    // this tile's count of digit tid = difference of neighbouring entries of the digit's tile prefix; the digit's
+    // global base = the exclusive scan of the digit totals (256 values, one per thread)
     const size_t hi = (size_t)tid * ntiles + blockIdx.x;
-    const uint32_t g0 = hist_scanned[hi];
-    const uint32_t g1 = hi + 1 < (size_t)256 * ntiles ? hist_scanned[hi + 1] : (uint32_t)n;
+    const uint32_t dt = dtotal[tid];
+    const uint32_t c0 = colpre[hi];
+    const uint32_t c1 = blockIdx.x + 1 < ntiles ? colpre[hi + 1] : dt;
+    uint32_t all;
+    const uint32_t dbase = block_exclusive(dt, OpAdd<uint32_t>(), red, all);
+    const uint32_t g0 = dbase + c0;
     uint32_t tile_total;
-    const uint32_t lb = block_exclusive(g1 - g0, OpAdd<uint32_t>(), red, tile_total);
+    const uint32_t lb = block_exclusive(c1 - c0, OpAdd<uint32_t>(), red, tile_total);
     lbase[tid] = lb;
     gbase[tid] = g0;
     run[tid] = lb;
@@ -461,15 +490,18 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
     }
     uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     uint32_t *hist = ctx->get<uint32_t>(nh, (size_t)256 * ntiles);
+    char nt[48];
+    snprintf(nt, sizeof nt, "%s_dtot", tag);
+    uint32_t *dtot = ctx->get<uint32_t>(nt, 256);
     const uint64_t *kin = keys;
     const uint32_t *vin = vals;
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
         int shift = 8 * p;
         launch(ctx, th, k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, kin, n, shift, hist, ntiles);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, hist, hist, (size_t)256 * ntiles, true);
+        launch(ctx, "rs_colscan", k_rs_colscan, dim3(256), dim3(BLOCK), 0, hist, ntiles, dtot);
         launch(ctx, ts, k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, shift,
-               (const uint32_t *)hist, ntiles, (p == 0 && !vals) ? 1 : 0);
+               (const uint32_t *)hist, (const uint32_t *)dtot, ntiles, (p == 0 && !vals) ? 1 : 0);
         kin = k[cur];
         vin = v[cur];
         cur ^= 1;
