@@ -37,6 +37,13 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
 
+# launch tags whose kernel is one instance of a template launched under several tags (csrc/keydeps.hip tiers)
+TAG_KERNEL = {
+    "v2_write_med": "k_v2_write_big<1024,256>",
+    "v2_write_big": "k_v2_write_big<8192,256>",
+    "v2_write_huge": "k_v2_write_big<16384,1024>",
+}
+
 
 def keydeps_bytes(n_txn, n_pairs, sum_kd, sum_e, sum_u):
     """SURVEY.md §8(d) KeyDeps batch: compulsory traffic, each input read once and each output written once."""
@@ -81,8 +88,14 @@ def roofline(step_bytes, timing, steps, ms_per_step, config, variant=""):
         traffic = int(prof.get("hbm_bytes_per_step", 0)) or None
         if "hbm_read_bytes_per_step_raw" in prof:
             traffic_raw = int(prof["hbm_read_bytes_per_step_raw"] + prof["hbm_write_bytes_per_step"])
-        # rocprof names carry template arguments (k_v3_stream<unsignedint,512>): match the launch tag on the base name
-        ks = [v for name, v in prof.get("kernels", {}).items() if name.split("<")[0] in ("k_" + dom_name, dom_name)]
+        # rocprof names carry template arguments (k_v3_stream<unsignedint,512>): launch tags of one kernel's template
+        # variants map to their instance, the others match on the base name
+        kernels = prof.get("kernels", {})
+        exact = TAG_KERNEL.get(dom_name)
+        if exact and exact in kernels:
+            ks = [kernels[exact]]
+        else:
+            ks = [v for name, v in kernels.items() if name.split("<")[0] in ("k_" + dom_name, dom_name)]
         if ks:
             calls = sum(v["calls"] for v in ks)
             dom_prof_ms = round(sum(v["total_ns"] for v in ks) / max(calls, 1) / 1e6, 4)
