@@ -440,6 +440,13 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     }
     __syncthreads();
     const uint32_t NK = rk[nrep], NV = rv[nrep], NO = ro[nrep], NE = NO - NK;
+    // per-slot loops run reply-major: TR threads per reply (a power of two, nrep * TR <= ML_NT), so a slot's reply is
+    // the thread's own and a keysToTxnIds value's key is found by walking the reply's headers forward, not by binary
+    // searches per slot
+    uint32_t TR = ML_NT;
+    while (TR > 1 && TR * nrep > (uint32_t)ML_NT) TR >>= 1;
+    const uint32_t my_r = tid / TR, my_t = tid % TR;
+    const bool has_r = my_r < nrep;
     // one coalesced pass over the group's three input ranges
     for (uint32_t i = tid; i < NK; i += ML_NT) rawk[i] = key_code[KA + i];
     for (uint32_t i = tid; i < NV; i += ML_NT) rawv[i] = txn_rank[VA + i];
@@ -449,14 +456,13 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     const uint64_t PADK = ~0ull;
     const uint32_t PAD32 = 0xFFFFFFFFu;
     // ---- keys: sort, unique, write, map every key slot to its merged index
-    for (uint32_t i = tid; i < NK; i += ML_NT) {
-        uint64_t x = PADK;
-        if (i < NK) {
-            const uint32_t r = lds_ub(rk, nrep + 1, i) - 1;
+    if (has_r) {
+        const uint32_t r = my_r;
+        const bool live = ro[r + 1] - ro[r] != rk[r + 1] - rk[r];
+        for (uint32_t i = rk[r] + my_t; i < rk[r + 1]; i += TR) {
             if (i > rk[r] && rawk[i - 1] >= rawk[i]) err |= 2;   // Keys sorted unique
-            if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawk[i];
+            sort64[i] = live ? rawk[i] : PADK;
         }
-        sort64[i] = x;
     }
     __syncthreads();
     ML_PH(0);
@@ -505,13 +511,15 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
     // ---- TxnIds: the union as a bitmap over the group's rank span when it fits (config 5: the batch's ranks), so
     // each TxnId's merged index is a word prefix + popcount; otherwise the merge tree + unique + binary searches
     uint32_t vlo = 0xFFFFFFFFu, vhi = 0;
-    for (uint32_t i = tid; i < NV; i += ML_NT) {
-        uint32_t x = PAD32;
-        const uint32_t r = lds_ub(rv, nrep + 1, i) - 1;
-        if (i > rv[r] && rawv[i - 1] >= rawv[i]) err |= 4;   // txnIds sorted unique
-        if (ro[r + 1] - ro[r] != rk[r + 1] - rk[r]) x = rawv[i];
-        if (x != PAD32) { vlo = min(vlo, x); vhi = max(vhi, x); }
-        sort32b[i] = x;
+    if (has_r) {
+        const uint32_t r = my_r;
+        const bool live = ro[r + 1] - ro[r] != rk[r + 1] - rk[r];
+        for (uint32_t i = rv[r] + my_t; i < rv[r + 1]; i += TR) {
+            if (i > rv[r] && rawv[i - 1] >= rawv[i]) err |= 4;   // txnIds sorted unique
+            const uint32_t x = live ? rawv[i] : PAD32;
+            if (x != PAD32) { vlo = min(vlo, x); vhi = max(vhi, x); }
+            sort32b[i] = x;
+        }
     }
     uint32_t ghi, glo_inv;
     (void)block_exclusive<uint32_t, OpMax<uint32_t>, ML_NT / 64>(vhi, OpMax<uint32_t>(), scan_lds, ghi);
@@ -578,32 +586,33 @@ __global__ __launch_bounds__(ML_NT) void k_m_lds(uint32_t ng, const uint64_t *__
         for (uint32_t w = tid; w < WE; w += ML_NT) ebits[w] = 0;
         __syncthreads();
     }
-    for (uint32_t q = tid; q < NO; q += ML_NT) {
-        const uint32_t r = lds_ub(ro, nrep + 1, q) - 1;
+    if (has_r) {
+        const uint32_t r = my_r;
         const uint32_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
-        const uint32_t qq = q - ro[r];
         const uint32_t *h = rawo + ro[r];
-        if (nk == 0) { err |= 8; continue; }   // keysToTxnIds entries without keys
-        if (qq < nk) {
-            const uint32_t e = h[qq], prev = qq == 0 ? nk : h[qq - 1];
-            if (e < prev || e > no || (qq + 1 == nk && e != no)) err |= 8;
-            continue;
-        }
-        uint32_t lo = 0, hi = nk;   // key slot: number of headers <= qq
-        while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] <= qq) lo = m + 1; else hi = m; }
-        const uint32_t i = lo < nk ? lo : nk - 1;
-        const uint32_t start = i == 0 ? nk : h[i - 1];
-        const int32_t xv = (int32_t)h[qq];
-        uint32_t x = PAD32;
-        if (xv < 0 || (uint32_t)xv >= nv) err |= 16;
-        else {
-            if (qq > start && (int32_t)h[qq - 1] >= xv) err |= 32;
-            if (no != nk) x = (kidx[rk[r] + i] << 16) | rawv[rv[r] + (uint32_t)xv];
-        }
-        if (!ebm) sort32[q - rk[r + 1]] = x;
-        else if (x != PAD32) {
-            const uint32_t u = x & 0xFFFFu;
-            atomicOr(&ebits[(x >> 16) * WU + (u >> 5)], 1u << (u & 31u));
+        if (nk == 0 && no != 0) err |= 8;   // keysToTxnIds entries without keys
+        uint32_t kw = 0;   // headers <= qq, advanced monotonically along this thread's slots
+        for (uint32_t qq = my_t; nk != 0 && qq < no; qq += TR) {
+            if (qq < nk) {
+                const uint32_t e = h[qq], prev = qq == 0 ? nk : h[qq - 1];
+                if (e < prev || e > no || (qq + 1 == nk && e != no)) err |= 8;
+                continue;
+            }
+            while (kw < nk && h[kw] <= qq) ++kw;
+            const uint32_t i = kw < nk ? kw : nk - 1;
+            const uint32_t start = i == 0 ? nk : h[i - 1];
+            const int32_t xv = (int32_t)h[qq];
+            uint32_t x = PAD32;
+            if (xv < 0 || (uint32_t)xv >= nv) err |= 16;
+            else {
+                if (qq > start && (int32_t)h[qq - 1] >= xv) err |= 32;
+                if (no != nk) x = (kidx[rk[r] + i] << 16) | rawv[rv[r] + (uint32_t)xv];
+            }
+            if (!ebm) sort32[ro[r] + qq - rk[r + 1]] = x;
+            else if (x != PAD32) {
+                const uint32_t u = x & 0xFFFFu;
+                atomicOr(&ebits[(x >> 16) * WU + (u >> 5)], 1u << (u & 31u));
+            }
         }
     }
     if (ebm) {
