@@ -121,16 +121,23 @@ constexpr int LV_G = ACC_LV_G;         // lanes per position (16: one DPP row)
 constexpr uint32_t LV_CH_MAX = 16384;  // entries per chunk
 constexpr int LV_PF = LV_CH_MAX / 8 / LV_NT;   // uint4 of a chunk per thread
 
+// also the graph validation of k_lv_check (the LDS tier skips that pass): err |= 1 decreasing offsets, 2 a dep >= n
 __global__ __launch_bounds__(BLOCK) void k_lv_fcount(uint32_t n, const uint32_t *__restrict__ order_exec,
                                                      const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
-                                                     const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ cnt)
+                                                     const uint32_t *__restrict__ exec_rank, uint32_t *__restrict__ cnt,
+                                                     uint32_t *__restrict__ err)
 {
     const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
     if (i >= n) return;
     const uint32_t t = order_exec[i], er = exec_rank[t];
     const uint64_t a = off[t], b = off[t + 1];
+    if (b < a && lane == 0) atomicOr(err, 1u);
     uint32_t c = 0;
-    for (uint64_t e = a + lane; e < b; e += 64) { const uint32_t d = dep[e]; c += d < n && exec_rank[d] < er; }   // d >= n: lv_check's error
+    for (uint64_t e = a + lane; e < b; e += 64) {
+        const uint32_t d = dep[e];
+        if (d >= n) { atomicOr(err, 2u); continue; }
+        c += exec_rank[d] < er;
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
     if (lane == 0) cnt[i] = c;
@@ -394,7 +401,17 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     const uint32_t *exec_rank = stage_in(ctx, "lv_exec", in->exec_rank, n, in->mem);
     uint32_t *err = ctx->get<uint32_t>("lv_err", 4);
     ACC_HIP(hipMemsetAsync(err, 0, 16, st));
-    launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
+    // tier: the whole graph's levels in one workgroup's LDS when they fit (chunk size CH: a power of two, three
+    // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
+    const uint32_t npad = (n + 7u) & ~7u;
+    uint32_t ch = 0;
+    if (n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
+        const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
+        uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
+        if (const char *ce = getenv("ACC_LV_CH")) cap = std::min<uint32_t>(cap, (uint32_t)std::max(1, atoi(ce)));
+        ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
+    }
+    if (!ch) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
     uint64_t *key = ctx->get<uint64_t>("lv_key", n);
     launch(ctx, "lv_keys", k_lv_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, exec_rank, key);
     Sorted se = radix_sort(ctx, "lv_rs_exec", key, nullptr, n, 32);
@@ -409,24 +426,16 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
     ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
-    // tier: the whole graph's levels in one workgroup's LDS when they fit (chunk size CH: a power of two, three
-    // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
-    const uint32_t npad = (n + 7u) & ~7u;
-    uint32_t ch = 0;
-    if (n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
-        const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
-        uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
-        if (const char *ce = getenv("ACC_LV_CH")) cap = std::min<uint32_t>(cap, (uint32_t)std::max(1, atoi(ce)));
-        ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
-    }
     if (ch) {
         uint32_t *fcnt = ctx->get<uint32_t>("lv_fcnt", n);
         uint32_t *foff = ctx->get<uint32_t>("lv_foff", (size_t)n + 1);
         const unsigned gw = (n + WAVES - 1) / WAVES;
-        launch(ctx, "lv_fcount", k_lv_fcount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank, fcnt);
+        launch(ctx, "lv_fcount", k_lv_fcount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank, fcnt,
+               err);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, fcnt, foff, n, true, foff + n);
         // sized by the unfiltered E (>= the filtered count, which stays on the device) + one chunk of padding for
-        // whole-chunk reads; invalid graphs (lv_check) are walked harmlessly (bad deps are skipped) and fail at the end
+        // whole-chunk reads; invalid graphs (flagged by k_lv_fcount) are walked harmlessly (bad deps are skipped) and
+        // fail at the end
         uint16_t *fdep = ctx->get<uint16_t>("lv_fdep", (size_t)E + ch);
         launch(ctx, "lv_fwrite", k_lv_fwrite, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
                (const uint32_t *)pos, (const uint32_t *)foff, fdep);
