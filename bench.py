@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 # launch tags whose kernel is one instance of a template launched under several tags (csrc/keydeps.hip tiers)
 TAG_KERNEL = {
     "v2_write_med": "k_v2_write_big<1024,256>",
-    "v2_write_big": "k_v2_write_big<8192,256>",
+    "v2_write_big": "k_v2_write_big<8192,512>",
     "v2_write_huge": "k_v2_write_big<16384,1024>",
 }
 

@@ -2884,7 +2884,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         if (rbits + 6 <= 31) {
             launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
-            launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, BLOCK>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
+            const char *bg_env = getenv("ACC_BIG_GRID");   // tuning: persistent grid of the BIG_E tier
+            const unsigned big_grid = bg_env ? (unsigned)std::max(1, atoi(bg_env)) : 1024u;
+            launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, 512>, dim3(std::min<unsigned>(nbig, big_grid)), dim3(512), 0,
                    (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
             launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
                    (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
