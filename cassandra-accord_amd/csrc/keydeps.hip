@@ -2899,7 +2899,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     }
     // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch)
     const char *nt_env = getenv("ACC_ST_NT");
-    int st_nt = nt_env ? atoi(nt_env) : 512;
+    int st_nt = nt_env ? atoi(nt_env) : 256;   // 256: co-schedules best with the 512-thread block tier (A/B)
     if (rbits > 28 && st_nt > 512) st_nt = 512;
     const uint32_t tt = (uint32_t)st_nt / ST_G;
     const uint32_t nblocks = (n + tt - 1) / tt;
