@@ -182,6 +182,17 @@ struct acc_ctx {
         launch_stream = nullptr;
     }
 
+    // after a failure inside a call: no launch is left pointing at a side stream, and every stream is drained before
+    // the next call (or a sync) frees graveyard buffers a side-stream kernel may still read. Errors are ignored here:
+    // the failure being reported is the first one.
+    void recover() noexcept
+    {
+        launch_stream = nullptr;
+        for (int i = 0; i < NAUX; ++i)
+            if (aux[i]) (void)hipStreamSynchronize(aux[i]);
+        if (stream) (void)hipStreamSynchronize(stream);
+    }
+
     void sync()
     {
         ACC_HIP(hipStreamSynchronize(stream));
@@ -252,13 +263,13 @@ inline int acc_guard(acc_ctx *ctx, F &&body)
         if (ctx) ctx->last_error.clear();
         return ACC_OK;
     } catch (const acc::Error &e) {
-        if (ctx) ctx->last_error = e.msg;
+        if (ctx) { ctx->recover(); ctx->last_error = e.msg; }
         return e.code;
     } catch (const std::bad_alloc &) {
-        if (ctx) ctx->last_error = "host allocation failed";
+        if (ctx) { ctx->recover(); ctx->last_error = "host allocation failed"; }
         return ACC_E_NOMEM;
     } catch (...) {
-        if (ctx) ctx->last_error = "unknown failure";
+        if (ctx) { ctx->recover(); ctx->last_error = "unknown failure"; }
         return ACC_E_STATE;
     }
 }

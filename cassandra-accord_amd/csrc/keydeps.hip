@@ -292,7 +292,8 @@ __global__ __launch_bounds__(BLOCK) void k_exec_ties(uint32_t n, const uint32_t 
 struct PairPlan {
     Runs rk;       // key code compaction
     int rbits;     // txn-rank bits in the composite (0 when the batch is already in TxnId order)
-    int mode;      // 0: key only (sorted batch), 1: (key << rbits) | rank, 2: key only after a rank pre-sort
+    int mode;      // 0: key only (sorted batch), 1: (key << rbits) | rank, 2: key only after a rank pre-sort,
+                   // 3: (key << 32) | pair index, keys-only sort (sorted batch, key within 32 bits)
 };
 
 __global__ __launch_bounds__(BLOCK) void k_pair_keys(size_t P, const uint64_t *__restrict__ key_code,
@@ -305,7 +306,18 @@ __global__ __launch_bounds__(BLOCK) void k_pair_keys(size_t P, const uint64_t *_
     size_t j = perm ? perm[i] : i;
     if (rank_only) { out[i] = rank[owner[j]]; return; }
     uint64_t kc = pext_runs(key_code[j], plan.rk);
-    out[i] = plan.mode == 1 ? ((kc << plan.rbits) | rank[owner[j]]) : kc;
+    out[i] = plan.mode == 1 ? ((kc << plan.rbits) | rank[owner[j]]) : plan.mode == 3 ? ((kc << 32) | i) : kc;
+}
+
+// packed (key << 32 | pair index) sort output: segment-start flags and the permutation
+__global__ __launch_bounds__(BLOCK) void k_seg_flags_packed(size_t P, const uint64_t *__restrict__ sp, uint32_t *__restrict__ flag,
+                                                            uint32_t *__restrict__ perm)
+{
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= P) return;
+    const uint64_t x = sp[p];
+    flag[p] = p == 0 || (x >> 32) != (sp[p - 1] >> 32);
+    perm[p] = (uint32_t)x;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seg_flags(size_t P, const uint64_t *__restrict__ skeys, int key_shift,
@@ -1098,8 +1110,9 @@ struct V2Out {
     uint64_t *u_cnt;
     uint32_t *med_list, *big_list, *fb_list, *huge_list;
     uint64_t *gstat;         // [0] medium, [1] big, [2] count mismatches, [3] fallback txns, [4] fallback entries,
-                             // [5] small, [6] huge (second big launch)
+                             // [5] small, [6] huge (second big launch), [7] / [8] window tier (<= 8 / <= 16 keys)
 };
+constexpr int GSTAT_N = 12;
 
 template <int MAXK>
 struct RunsT {
@@ -1650,6 +1663,210 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(const uint32_t *__restrict_
     }
 }
 
+// ---- window tier: the KeyDeps of a big txn through per-key bitmaps over its rank span, no sorting.
+//
+// A big txn (config 2 / 3: the uncommitted window's txns on hot keys, 10^3-10^4 entries) takes its dependency entries
+// from ranks below its executeAt S. Every entry of key k at rank x in [base, S), base = S - WIN_W * 32, sets bit
+// x - base of key k's bitmap; the union's bitmap is the OR of the keys' bitmaps. A key's entries are distinct TxnIds
+// (its runs are disjoint classes), so the builder's per-key ascending index lists (RelationMultiMap.java:245-257) are
+// the key's set bits in order and each entry's index into the sorted unique TxnIds (:201-226) is a prefix popcount of
+// the union: O(E + keys * span / 32) work instead of a merge sort. Entries below base (a cold key's last committed
+// Write far back) go to a short sorted list that precedes the bitmap span. A txn whose list overflows is passed on to
+// the sorting tier (k_v2_write_big<BIG_E>).
+constexpr uint32_t WIN_W = 512;      // bitmap words per key: 16384 ranks below S
+constexpr uint32_t WIN_OUT = 1024;   // entries below the span
+
+template <int WK>
+struct WinLds {
+    uint32_t bm[WK][WIN_W];
+    uint32_t un[WIN_W];
+    uint16_t pre[WK + 1][WIN_W];   // exclusive prefix popcounts per series (series WK... = the union, index nk)
+    uint32_t out[WIN_OUT];         // (rank << 6 | key) of the entries below the span
+    RunsT<WK> R;
+    uint32_t kc[WK], out_k[WK], ser_tot[WK + 1];
+    uint32_t n_out, kept, d_out, bad;
+};
+
+template <int WK>
+__global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restrict__ list, const uint64_t *__restrict__ cnt_dev,
+                                                       V2View v, const uint64_t *__restrict__ cnt, V2Out o)
+{
+    __shared__ WinLds<WK> L;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+    const uint32_t n_list = (uint32_t)*cnt_dev;
+    RunsT<WK> &R = L.R;
+    for (uint32_t b = blockIdx.x; b < n_list; b += gridDim.x) {
+        const uint32_t t = list[b];
+        const TxnCtx c = txn_ctx(v, o, t);
+        const uint32_t S = v.tinfo[t].y;
+        const uint32_t base = S > WIN_W * 32 ? S - WIN_W * 32 : 0u;
+        const uint32_t nw = (S - base + 31) / 32;
+        if (tid < 64) compute_runs(R, v, o, cnt, c);
+        for (uint32_t i = tid; i < c.nk * WIN_W; i += BLOCK) L.bm[i / WIN_W][i % WIN_W] = 0;
+        if (tid < (uint32_t)WK) { L.kc[tid] = 0; L.out_k[tid] = 0; }
+        if (tid == 0) { L.n_out = 0; L.kept = 0; L.bad = 0; }
+        __syncthreads();
+        const uint32_t total = R.total;
+        // ---- gather: bits of the span, the entries below it to the list
+        uint32_t kept = 0;
+        for (uint32_t e0 = tid; e0 < total; e0 += BIG_GU * BLOCK) {
+            uint32_t idx[BIG_GU], kk[BIG_GU], x[BIG_GU];
+            bool r3[BIG_GU], in[BIG_GU], il[BIG_GU];
+#pragma unroll
+            for (int u = 0; u < BIG_GU; ++u) {
+                const uint32_t e = e0 + u * BLOCK;
+                in[u] = e < total;
+                idx[u] = 0; kk[u] = 0; r3[u] = false; il[u] = false;
+                if (in[u]) locate_elem(R, c.nk, e, idx[u], kk[u], r3[u], il[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < BIG_GU; ++u)
+                x[u] = in[u] ? (il[u] ? v.rec32[idx[u]] : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
+#pragma unroll
+            for (int u = 0; u < BIG_GU; ++u) {
+                bool keep = in[u] && (il[u] || !(c.bq && x[u] == c.trank));
+                if (keep && r3[u]) keep = v.bc_exec[idx[u]] >= R.m[kk[u]] && ((c.wk >> v.bc_kind[idx[u]]) & 1u);
+                if (!keep) continue;
+                ++kept;
+                if (x[u] >= base) {
+                    const uint32_t d = x[u] - base;
+                    if (d < nw * 32) atomicOr(&L.bm[kk[u]][d >> 5], 1u << (d & 31));
+                    else L.bad = 1;   // an entry at or above S: impossible for a scan below S
+                } else {
+                    const uint32_t i = atomicAdd(&L.n_out, 1u);
+                    if (i < WIN_OUT) L.out[i] = (x[u] << 6) | kk[u];
+                    atomicAdd(&L.out_k[kk[u]], 1u);
+                }
+            }
+        }
+        kept = wave_inclusive(kept, OpAdd<uint32_t>());
+        if (lane == 63) atomicAdd(&L.kept, kept);
+        __syncthreads();
+        if (L.kept != c.E || L.bad) {
+            if (tid == 0) atomicAdd((unsigned long long *)&o.gstat[2], 1ull);
+            __syncthreads();
+            continue;
+        }
+        const uint32_t n_out = L.n_out;
+        if (n_out > WIN_OUT) {   // too many entries below the span: the sorting tier
+            if (tid == 0) {
+                const uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[1], 1ull);
+                o.big_list[f] = t;
+            }
+            __syncthreads();
+            continue;
+        }
+        // ---- union words
+        for (uint32_t w = tid; w < nw; w += BLOCK) {
+            uint32_t u = 0;
+            for (uint32_t k = 0; k < c.nk; ++k) u |= L.bm[k][w];
+            L.un[w] = u;
+        }
+        // ---- the entries below the span, sorted (rank, key)
+        if (n_out > 1) {
+            uint32_t n2 = 64;
+            while (n2 < n_out) n2 <<= 1;
+            for (uint32_t q = n_out + tid; q < n2; q += BLOCK) L.out[q] = 0xFFFFFFFFu;
+            __syncthreads();
+            block_bitonic<uint32_t, BLOCK>(L.out, n2);
+        }
+        __syncthreads();
+        // ---- exclusive prefix popcounts of every series (keys 0..nk-1, union = nk): a wave per series, 8 words a lane
+        for (uint32_t s = wave; s <= c.nk; s += WAVES) {
+            const uint32_t *words = s < c.nk ? L.bm[s] : L.un;
+            uint32_t run = 0;
+            for (uint32_t w0 = 0; w0 < nw; w0 += 512) {
+                const uint32_t wl = w0 + lane * 8;
+                uint32_t pc[8], sum = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { pc[i] = wl + i < nw ? (uint32_t)__popc(words[wl + i]) : 0u; sum += pc[i]; }
+                const uint32_t incl = wave_inclusive(sum, OpAdd<uint32_t>());
+                uint32_t r = run + incl - sum;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) if (wl + i < nw) { L.pre[s][wl + i] = (uint16_t)r; r += pc[i]; }
+                run += shfl_idx(incl, 63);
+            }
+            if (lane == 0) L.ser_tot[s] = run;
+        }
+        const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
+        uint32_t *dsc = o.dep_scratch + c.e0;
+        // ---- the sorted entries below the span (one wave): distinct TxnIds first in the union, each key's first slots
+        if (wave == 0 && n_out) {
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            uint32_t distinct = 0;
+            for (uint32_t q0 = 0; q0 < n_out; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                const bool in = q < n_out;
+                const uint32_t xq = in ? L.out[q] : 0u;
+                const uint32_t kj = xq & 63u;
+                const bool nw_ = in && (q == 0 || (L.out[q - 1] >> 6) != (xq >> 6));
+                const uint64_t bal = __ballot(nw_);
+                const uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw_ ? 1u : 0u) - 1u;
+                uint64_t peers = __ballot(in);
+#pragma unroll
+                for (int bb = 0; bb < 6; ++bb) {
+                    const uint64_t m = __ballot((kj >> bb) & 1u);
+                    peers &= ((kj >> bb) & 1u) ? m : ~m;
+                }
+                const uint32_t before = (uint32_t)__popcll(peers & lt);
+                if (in) {
+                    o.arena[abase + (o.dep_off[c.j0 + kj] - c.e0) + L.kc[kj] + before] = (int32_t)idx;
+                    if (nw_) dsc[idx] = o.txn_of_rank[xq >> 6];
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (in && before == 0) L.kc[kj] += (uint32_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                distinct += (uint32_t)__popcll(bal);
+            }
+            if (lane == 0) L.d_out = distinct;
+        } else if (tid == 0) {
+            L.d_out = 0;
+        }
+        __syncthreads();
+        // ---- the span: item (series, word); a key's words give its keysToTxnIds indices (union index = word prefix +
+        // popcount), the union's words its TxnId ranks, mapped to TxnIds below with independent loads in flight
+        const uint32_t d_out = L.d_out, nu = L.ser_tot[c.nk];
+        const uint32_t items = (c.nk + 1) * nw;
+        for (uint32_t i = tid; i < items; i += BLOCK) {
+            const uint32_t s = i / nw, w = i - s * nw;
+            const uint32_t ubase = d_out + L.pre[c.nk][w];
+            if (s == c.nk) {
+                uint32_t bits = L.un[w], j = 0;
+                while (bits) {
+                    dsc[ubase + j] = base + 32 * w + (uint32_t)__builtin_ctz(bits);
+                    bits &= bits - 1;
+                    ++j;
+                }
+            } else {
+                uint32_t bits = L.bm[s][w];
+                if (!bits) continue;
+                const uint32_t uw = L.un[w];
+                int32_t *dst = o.arena + abase + (o.dep_off[c.j0 + s] - c.e0) + L.out_k[s] + L.pre[s][w];
+                uint32_t j = 0;
+                while (bits) {
+                    const uint32_t b2 = (uint32_t)__builtin_ctz(bits);
+                    dst[j] = (int32_t)(ubase + (uint32_t)__popc(uw & ((1u << b2) - 1u)));
+                    bits &= bits - 1;
+                    ++j;
+                }
+            }
+        }
+        __syncthreads();   // the block's rank writes are visible to the block
+        for (uint32_t i0 = d_out + tid; i0 < d_out + nu; i0 += 4 * BLOCK) {
+            uint32_t r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = i0 + (uint32_t)u * BLOCK < d_out + nu ? dsc[i0 + (uint32_t)u * BLOCK] : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) if (i0 + (uint32_t)u * BLOCK < d_out + nu) r[u] = o.txn_of_rank[r[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) if (i0 + (uint32_t)u * BLOCK < d_out + nu) dsc[i0 + (uint32_t)u * BLOCK] = r[u];
+        }
+        if (tid == 0) o.u_cnt[t] = d_out + nu;
+        __syncthreads();
+    }
+}
+
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
 
 __global__ __launch_bounds__(BLOCK) void k_v2_big_gather(uint32_t nbig, const uint32_t *__restrict__ big_list,
@@ -1853,36 +2070,43 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_
     if (lane == 0) { lE[i] = E; lK[i] = K; lA[i] = E + K; }
 }
 
-// tier routing of the big txns (thread per list entry, one atomic per list per block): medium (E <= MED_E, <= MED_K
-// keys), the u32-record block tier (when ranks fit 25 bits) or the global path
+// tier routing of the big txns (thread per list entry, one atomic per list per block). With ranks within 25 bits: the
+// window tier (<= 8 or <= 16 keys; gstat[7] / gstat[8]), else medium (E <= MED_E, <= MED_K keys) or the u32-record
+// block tier; with wider ranks: the u64 wave tier (E <= MED_E, <= MED_K keys) or the global path.
 __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_t *__restrict__ blist,
                                                     const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ lE,
-                                                    int big_ok, uint32_t *__restrict__ med_list, uint32_t *__restrict__ big_list,
-                                                    uint32_t *__restrict__ fb_list, uint64_t *__restrict__ gstat)
+                                                    int big_ok, int win_ok, uint32_t *__restrict__ med_list,
+                                                    uint32_t *__restrict__ big_list, uint32_t *__restrict__ fb_list,
+                                                    uint32_t *__restrict__ w8_list, uint32_t *__restrict__ w16_list,
+                                                    uint64_t *__restrict__ gstat)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    bool med = false, bg = false, fb = false;
+    bool med = false, bg = false, fb = false, w8 = false, w16 = false;
     uint32_t t = 0;
     uint64_t E = 0;
     if (i < nbig) {
         t = blist[i];
         E = lE[i];
         const uint32_t nk = key_off[t + 1] - key_off[t];
-        med = E > 0 && E <= (uint64_t)MED_E && nk <= (uint32_t)MED_K;
-        bg = E > 0 && !med && big_ok;
-        fb = E > 0 && !med && !big_ok;
+        const bool win = E > 0 && big_ok && win_ok && nk <= 16;
+        w8 = win && nk <= 8;
+        w16 = win && nk > 8;
+        med = E > 0 && !win && E <= (uint64_t)MED_E && nk <= (uint32_t)MED_K;
+        bg = E > 0 && !win && !med && big_ok;
+        fb = E > 0 && !win && !med && !big_ok;
     }
     __shared__ uint64_t lds[WAVES];
-    __shared__ uint64_t base[3];
-    const uint64_t packed = (med ? 1ull : 0ull) | (bg ? 1ull << 12 : 0ull) | (fb ? 1ull << 24 : 0ull);
+    __shared__ uint64_t base[5];
+    const uint64_t packed = (med ? 1ull : 0ull) | (bg ? 1ull << 12 : 0ull) | (fb ? 1ull << 24 : 0ull) |
+                            (w8 ? 1ull << 36 : 0ull) | (w16 ? 1ull << 48 : 0ull);
     uint64_t total;
     const uint64_t pre = block_exclusive(packed, OpAdd<uint64_t>(), lds, total);
     uint64_t efb = fb ? E : 0;
     uint64_t efb_tot;
     __syncthreads();
     block_exclusive(efb, OpAdd<uint64_t>(), lds, efb_tot);
-    if (threadIdx.x < 3) {
-        const int slot[3] = { 0, 1, 3 };
+    if (threadIdx.x < 5) {
+        const int slot[5] = { 0, 1, 3, 7, 8 };
         const uint64_t cnt = (total >> (12 * threadIdx.x)) & 4095u;
         base[threadIdx.x] = cnt ? atomicAdd((unsigned long long *)&gstat[slot[threadIdx.x]], (unsigned long long)cnt) : 0ull;
     }
@@ -1891,6 +2115,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
     if (med) med_list[base[0] + (pre & 4095u)] = t;
     if (bg) big_list[base[1] + ((pre >> 12) & 4095u)] = t;
     if (fb) fb_list[base[2] + ((pre >> 24) & 4095u)] = t;
+    if (w8) w8_list[base[3] + ((pre >> 36) & 4095u)] = t;
+    if (w16) w16_list[base[4] + ((pre >> 48) & 4095u)] = t;
 }
 
 struct V3Big {
@@ -2684,7 +2910,20 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     const unsigned gP = grid_for(P, BLOCK);
     Sorted ps;
     int key_shift = 0;
-    if (batch_sorted) {
+    uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
+    bool flags_done = false;
+    if (batch_sorted && pp.rk.bits <= 32 && !getenv("ACC_PAIR_UNPACKED")) {
+        // pair index order is already TxnId order within every key: a stable keys-only sort of (key << 32 | pair index),
+        // 8 B per element; the segment flags pass unpacks the permutation
+        pp.mode = 3;
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+        const uint64_t *sp = radix_sort_keys(ctx, "rs_pair", pkey, P, 32, pp.rk.bits);
+        uint32_t *perm = ctx->get<uint32_t>("pair_perm", P);
+        launch(ctx, "seg_flags", k_seg_flags_packed, dim3(gP), dim3(BLOCK), 0, P, sp, seg_flag, perm);
+        ps = { nullptr, perm };
+        flags_done = true;
+    } else if (batch_sorted) {
         pp.mode = 0;   // pair index order is already TxnId order within every key: stable sort by key
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
@@ -2704,9 +2943,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey);
         ps = radix_sort(ctx, "rs_pair", pkey, byrank.vals, P, pp.rk.bits);
     }
-    uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
     uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P);
-    launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
+    if (!flags_done)
+        launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, seg_flag, seg_incl, P, false);
 
     uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
@@ -2801,10 +3040,10 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *bpos = ctx->get<uint32_t>("v3_bpos", n);
     uint64_t *blk_e = ctx->get<uint64_t>("v3_blk_e", gP);
     uint64_t *tot = ctx->get<uint64_t>("v3_tot", 2);
-    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", 8);
+    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N);
     ACC_HIP(hipMemsetAsync(bigflag, 0, (size_t)n * 4, st));
     ACC_HIP(hipMemsetAsync(tot, 0, 2 * sizeof(uint64_t), st));
-    ACC_HIP(hipMemsetAsync(gstat, 0, 8 * sizeof(uint64_t), st));
+    ACC_HIP(hipMemsetAsync(gstat, 0, GSTAT_N * sizeof(uint64_t), st));
     launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, rec, bigflag, blk_e);
     const char *rc_env = getenv("ACC_ST_RAW");
     const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
@@ -2842,6 +3081,22 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *key_scr = nullptr, *dep_scr = nullptr;
     uint64_t nfb = 0, efb = 0, nmed = 0, nbig2 = 0;
     ctx->stat("keydeps.huge_txns", 0);
+    V2Out wo{};
+    bool win_ok = false, side = false;
+    uint64_t *vcnt = nullptr;
+    uint32_t *med_list = nullptr, *big_list = nullptr, *fb_list = nullptr;
+    // the sorting tiers: medium (<= MED_CAP raw entries), block (<= BIG_E), huge (<= HUGE_E, fed by the block tier)
+    auto sort_tiers = [&](bool with_med) {
+        if (with_med)
+            launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
+                   (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
+        const char *bg_env = getenv("ACC_BIG_GRID");   // tuning: persistent grid of the BIG_E tier
+        const unsigned big_grid = bg_env ? (unsigned)std::max(1, atoi(bg_env)) : 1024u;
+        launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, 512>, dim3(std::min<unsigned>(nbig, big_grid)), dim3(512), 0,
+               (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
+        launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
+               (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
+    };
     // ---- big txns: v2 tiers into scratch
     if (nbig) {
         const unsigned gB = (nbig + WAVES - 1) / WAVES;
@@ -2853,43 +3108,47 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         scan<uint64_t, OpAdd<uint64_t>>(ctx, lK, kB, nbig, true, kB + nbig);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, lA, lB, nbig, true, lB + nbig);
         vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
-        uint64_t *vcnt = ctx->get<uint64_t>("cnt", P);
+        vcnt = ctx->get<uint64_t>("cnt", P);
         uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
         varena = ctx->get<uint64_t>("v3_varena", n);
         arena_scr = ctx->get<int32_t>("v3_arena_scr", P + E);
         key_scr = ctx->get<uint32_t>("v3_key_scr", P);
         dep_scr = ctx->get<uint32_t>("v2_dep_scratch", E);
-        uint32_t *med_list = ctx->get<uint32_t>("v2_med_list", nbig);
-        uint32_t *big_list = ctx->get<uint32_t>("v2_big_list", nbig);
-        uint32_t *fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
+        med_list = ctx->get<uint32_t>("v2_med_list", nbig);
+        big_list = ctx->get<uint32_t>("v2_big_list", nbig);
+        fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
         V3Big bg;
         bg.blist = blist; bg.key_off = key_off; bg.rec32 = vv.rec32; bg.dB = dB; bg.kB = kB; bg.aB = lB;
         bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.varena = varena; bg.bK = bK; bg.bE = bE; bg.u_cnt = u_cnt;
         bg.arena_scr = arena_scr; bg.key_scr = key_scr;
+        const bool big_ok = rbits + 6 <= 31;
+        win_ok = big_ok && !getenv("ACC_NO_WIN");   // tuning switch: the sorting tiers instead of the window tier
         launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
-               key_off, (const uint64_t *)lE, (int)(rbits + 6 <= 31), med_list, big_list, fb_list, gstat);
+               key_off, (const uint64_t *)lE, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
+               ctx->get<uint32_t>("v2_w8_list", nbig), ctx->get<uint32_t>("v2_w16_list", nbig), gstat);
         launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
-        V2Out wo;
         wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = varena; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
         wo.arena = arena_scr; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
         wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
         // on a side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
-        const bool side = !getenv("ACC_KD_SERIAL");   // tuning switch: the tiers in order on the main stream
+        side = !getenv("ACC_KD_SERIAL");   // tuning switch: the tiers in order on the main stream
         if (side) {
             ctx->fork(1);
             ctx->launch_stream = ctx->aux[0];
         }
-        if (rbits + 6 <= 31) {
-            launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
-                   (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
-            const char *bg_env = getenv("ACC_BIG_GRID");   // tuning: persistent grid of the BIG_E tier
-            const unsigned big_grid = bg_env ? (unsigned)std::max(1, atoi(bg_env)) : 1024u;
-            launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, 512>, dim3(std::min<unsigned>(nbig, big_grid)), dim3(512), 0,
-                   (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
-            launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
-                   (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
+        if (win_ok) {
+            // the window tier takes every big txn of <= 16 keys; the sorting tiers run after the next host sync, only
+            // when it passed txns on or some txn has more keys (no launch without work)
+            launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
+                   (const uint32_t *)ctx->get<uint32_t>("v2_w8_list", nbig), (const uint64_t *)(gstat + 7), vv,
+                   (const uint64_t *)vcnt, wo);
+            launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
+                   (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
+                   (const uint64_t *)vcnt, wo);
+        } else if (big_ok) {
+            sort_tiers(true);
         } else {
             // ranks beyond 25 bits: u64 records in the wave tier (k_v3_route sends everything else to the global path)
             launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
@@ -2969,19 +3228,27 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                uo, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
                (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr,
                tmap, ne_cnt, dep_txn);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 9, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 10, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, GSTAT_N * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N + 2, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
     };
     finish();
     if (ctx->pinned[5]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+    if (nbig && win_ok && (ctx->pinned[0] || ctx->pinned[1])) {
+        // txns the window tier could not take (> 16 keys, or too many entries below its span): the sorting tiers now,
+        // on the context stream, then the copies / compaction again
+        sort_tiers(ctx->pinned[0] != 0);
+        finish();
+        if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
+    }
     if (nbig) {
         nmed = ctx->pinned[0]; nbig2 = ctx->pinned[1];
         nfb = ctx->pinned[3]; efb = ctx->pinned[4];
         ctx->stat("keydeps.huge_txns", ctx->pinned[6]);
+        ctx->stat("keydeps.window_txns", ctx->pinned[7] + ctx->pinned[8]);
     }
     if (nfb) {
         need_pair_pos();
@@ -3031,8 +3298,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ctx->stat("keydeps.fallback_entries", efb);
     ctx->stat("keydeps.bumped_committed", nbc);
     (void)lB;
-    *view = acc_keydeps_view{ n, ctx->pinned[8], ctx->pinned[9], ctx->pinned[10], E, arena_off, arena, kd_off,
-                              key_idx, u_off, dep_txn };
+    *view = acc_keydeps_view{ n, ctx->pinned[GSTAT_N], ctx->pinned[GSTAT_N + 1], ctx->pinned[GSTAT_N + 2], E, arena_off,
+                              arena, kd_off, key_idx, u_off, dep_txn };
     ctx->kd_view = *view;
     ctx->kd_valid = true;
 }

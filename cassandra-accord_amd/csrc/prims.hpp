@@ -456,6 +456,184 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_scatter(const uint64_t *__r
     }
 }
 
+// ---- one-sweep LSD radix sort: the digit histograms of every pass in one read of the keys, then ONE launch per pass
+// whose tiles find their digits' global offsets by a decoupled look-back over the earlier tiles (tickets in launch
+// order; a status word per (tile, digit) = count | flag << 30, agent-scope stores and polls: per-XCD L2s are not
+// coherent). Three launches per pass (tile histograms, column scans, scatter) become one, and the per-pass histogram
+// read of the keys goes. Counts must stay below 2^30.
+constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
+constexpr int OS_MAXP = 8;
+
+static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__restrict__ keys, size_t n, int lo, int passes,
+                                                    uint32_t *__restrict__ ghist)
+{
+    __shared__ uint32_t h[WAVES][OS_MAXP][256];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+    const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    for (uint32_t i = tid; i < WAVES * OS_MAXP * 256; i += BLOCK) (&h[0][0][0])[i] = 0;
+    // one tile of RS_TILE keys per block, all its loads issued up front
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+    uint64_t key[RS_ITEMS];
+#pragma unroll
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const size_t e = base + (size_t)k * BLOCK + tid;
+        key[k] = e < n ? keys[e] : 0;
+    }
+    __syncthreads();
+    for (int p = 0; p < passes; ++p) {
+#pragma unroll
+        for (int k = 0; k < RS_ITEMS; ++k) {
+            // one LDS add per distinct digit of the wave (hot digits would serialise per-element atomics)
+            const bool valid = base + (size_t)k * BLOCK + tid < n;
+            const uint32_t d = (uint32_t)(key[k] >> (lo + 8 * p)) & 255u;
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint64_t bal = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? bal : ~bal;
+            }
+            if (valid && (peers & lt_mask) == 0) h[wave][p][d] += (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < (uint32_t)passes * 256; i += BLOCK) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += h[w][i >> 8][i & 255];
+        if (s) atomicAdd(&ghist[i], s);
+    }
+}
+
+__device__ __forceinline__ void os_store(uint32_t *p, uint32_t w) { __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t os_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// KO: keys only (no value arrays; e.g. (key << 32 | index) packed into the key): half the LDS, 8 B per element moved
+template <bool KO>
+static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, size_t n,
+                                                       int shift, const uint32_t *__restrict__ dtotal,
+                                                       uint32_t *__restrict__ status, uint32_t *__restrict__ ticket,
+                                                       int iota_vals)
+{
+    __shared__ uint64_t sk[RS_TILE];
+    __shared__ uint32_t sv[KO ? 1 : RS_TILE];
+    __shared__ uint32_t cnt[WAVES][256];
+    __shared__ uint32_t wpre[WAVES][256];
+    __shared__ uint32_t run[256], lbase[256], gbase[256];
+    __shared__ uint32_t red[WAVES];
+    __shared__ uint32_t s_b;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    if (tid == 0) s_b = atomicAdd(ticket, 1u);
+    run[tid] = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) cnt[w][tid] = 0;
+    __syncthreads();
+    const uint32_t b = s_b;
+    const size_t base = (size_t)b * RS_TILE;
+    // the tile in registers
+    uint64_t key[RS_ITEMS];
+    uint32_t val[RS_ITEMS], lr[RS_ITEMS], pk[RS_ITEMS];
+#pragma unroll
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const size_t e = base + (size_t)k * BLOCK + tid;
+        const bool valid = e < n;
+        key[k] = valid ? kin[e] : 0;
+        if constexpr (!KO) val[k] = valid ? (iota_vals ? (uint32_t)e : vin[e]) : 0;
+    }
+    // the tile's digit counts first (one LDS add per distinct digit of a wave), published at once so later tiles'
+    // look-backs find them early; each element's peer rank in its wave is kept for the stable ranking below
+#pragma unroll
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const bool valid = base + (size_t)k * BLOCK + tid < n;
+        const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            const uint64_t bal = __ballot((d >> bb) & 1u);
+            peers &= ((d >> bb) & 1u) ? bal : ~bal;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
+        pk[k] = rank | ((uint32_t)__popcll(peers) << 16);
+        if (valid && rank == 0) atomicAdd(&run[d], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    const uint32_t c = run[tid];
+    uint32_t *st = status + (size_t)b * 256;
+    os_store(&st[tid], b == 0 ? (c | OS_INC) : (c | OS_AGG));
+    uint32_t tile_total;
+    const uint32_t lb = block_exclusive(c, OpAdd<uint32_t>(), red, tile_total);
+    run[tid] = 0;
+    lbase[tid] = lb;
+    __syncthreads();
+    // stable rank of each element among the tile's elements of its digit: order (k, wave, lane)
+#pragma unroll
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const bool valid = base + (size_t)k * BLOCK + tid < n;
+        const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+        const uint32_t rank = pk[k] & 0xFFFFu;
+        if (valid && rank == 0) cnt[wave][d] = pk[k] >> 16;
+        __syncthreads();
+        {
+            uint32_t r = run[tid];
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                wpre[w][tid] = r;
+                r += cnt[w][tid];
+                cnt[w][tid] = 0;
+            }
+            run[tid] = r;
+        }
+        __syncthreads();
+        lr[k] = wpre[wave][d] + rank;
+    }
+#pragma unroll
+    for (int k = 0; k < RS_ITEMS; ++k) {
+        const size_t e = base + (size_t)k * BLOCK + tid;
+        if (e < n) {
+            const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+            const uint32_t dst = lbase[d] + lr[k];
+            sk[dst] = key[k];
+            if constexpr (!KO) sv[dst] = val[k];
+        }
+    }
+    // the digit's global base = exclusive scan of the digit totals + the earlier tiles' counts (look-back, eight
+    // status words in flight per step)
+    uint32_t all;
+    const uint32_t dbase = block_exclusive(dtotal[tid], OpAdd<uint32_t>(), red, all);
+    uint32_t pre = 0;
+    if (b > 0) {
+        constexpr int LB = 8;
+        for (int64_t j = (int64_t)b - 1;; j -= LB) {
+            uint32_t w[LB];
+#pragma unroll
+            for (int u = 0; u < LB; ++u) w[u] = j - u >= 0 ? os_load(&status[(size_t)(j - u) * 256 + tid]) : OS_INC;
+            bool done = false;
+#pragma unroll
+            for (int u = 0; u < LB; ++u) {
+                if (done) continue;
+                while ((w[u] >> 30) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    w[u] = os_load(&status[(size_t)(j - u) * 256 + tid]);
+                }
+                pre += w[u] & OS_VAL;
+                done = (w[u] >> 30) == 2;
+            }
+            if (done) break;
+        }
+        os_store(&st[tid], (pre + c) | OS_INC);
+    }
+    gbase[tid] = dbase + pre;
+    __syncthreads();
+    for (uint32_t i = tid; i < tile_total; i += BLOCK) {
+        const uint64_t k2 = sk[i];
+        const uint32_t d = (uint32_t)(k2 >> shift) & 255u;
+        const uint32_t dst = gbase[d] + (i - lbase[d]);
+        kout[dst] = k2;
+        if constexpr (!KO) vout[dst] = sv[i];
+    }
+}
+
 static __global__ void k_iota(uint32_t *__restrict__ out, size_t n)
 {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -489,6 +667,30 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         return { k[0], v[0] };
     }
     uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    static const bool legacy = getenv("ACC_RS_LEGACY") != nullptr;   // tuning switch: three launches per pass
+    if (n < (size_t)OS_VAL && passes <= OS_MAXP && !legacy) {
+        // one-sweep: [passes x 256 digit totals][passes tickets][passes x ntiles x 256 status words], zeroed by one fill
+        char nsw[48];
+        snprintf(nsw, sizeof nsw, "%s_os", tag);
+        const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;
+        uint32_t *osb = ctx->get<uint32_t>(nsw, words);
+        ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
+        uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
+        snprintf(th, sizeof th, "%s.ghist", tag);
+        launch(ctx, th, k_rs_ghist, dim3(ntiles), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
+        const uint64_t *kin = keys;
+        const uint32_t *vin = vals;
+        int cur = 0;
+        for (int p = 0; p < passes; ++p) {
+            launch(ctx, ts, k_rs_onesweep<false>, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, 8 * p,
+                   (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256, tickets + p,
+                   (p == 0 && !vals) ? 1 : 0);
+            kin = k[cur];
+            vin = v[cur];
+            cur ^= 1;
+        }
+        return { (uint64_t *)kin, (uint32_t *)vin };
+    }
     uint32_t *hist = ctx->get<uint32_t>(nh, (size_t)256 * ntiles);
     char nt[48];
     snprintf(nt, sizeof nt, "%s_dtot", tag);
@@ -507,6 +709,40 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         cur ^= 1;
     }
     return { (uint64_t *)kin, (uint32_t *)vin };
+}
+
+// Stable sort of n u64 keys by bits [lo, lo + bits) (bits above must be zero; bits below ride along, e.g. an index packed
+// under the key). One-sweep only: n < 2^30. The result lives in the context buffers "<tag>_k?".
+static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uint64_t *keys, size_t n, int lo, int bits)
+{
+    char nk0[40], nk1[40], nsw[48], th[48], ts[48];
+    snprintf(nk0, sizeof nk0, "%s_k0", tag); snprintf(nk1, sizeof nk1, "%s_k1", tag);
+    snprintf(nsw, sizeof nsw, "%s_os", tag);
+    snprintf(th, sizeof th, "%s.ghist", tag);
+    snprintf(ts, sizeof ts, "%s.scatter", tag);
+    uint64_t *k[2] = { ctx->get<uint64_t>(nk0, n), ctx->get<uint64_t>(nk1, n) };
+    const int passes = (bits + 7) / 8;
+    if (n >= (size_t)OS_VAL || passes > OS_MAXP) fail(ACC_E_CAP, "internal: keys-only radix sort beyond its limits");
+    if (n == 0 || passes == 0) {
+        if (n) ACC_HIP(hipMemcpyAsync(k[0], keys, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->cur()));
+        return k[0];
+    }
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;
+    uint32_t *osb = ctx->get<uint32_t>(nsw, words);
+    ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
+    uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
+    launch(ctx, th, k_rs_ghist, dim3(ntiles), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
+    const uint64_t *kin = keys;
+    int cur = 0;
+    for (int p = 0; p < passes; ++p) {
+        launch(ctx, ts, k_rs_onesweep<true>, dim3(ntiles), dim3(BLOCK), 0, kin, (const uint32_t *)nullptr, k[cur],
+               (uint32_t *)nullptr, n, lo + 8 * p, (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256,
+               tickets + p, 0);
+        kin = k[cur];
+        cur ^= 1;
+    }
+    return (uint64_t *)kin;
 }
 
 inline int bits_for(uint64_t max_value)

@@ -188,6 +188,36 @@ def test_tiers_medium_big_fallback(ctx, hot_every, tail):
         assert st["keydeps.fallback_txns"] > 0     # E ~45000: the global-sort tier
 
 
+@pytest.mark.parametrize("nk", [8, 12, 24])
+def test_window_tier(nk):
+    """The uncommitted window's txns on hot keys (E up to thousands) through the per-key bitmap tier (<= 8 and
+    <= 16 keys: k_v2_write_win) or, beyond 16 keys, the sorting tiers run after the host sync: bit-exact with the
+    oracle on the window's txns and, on every txn, with the sorting tiers alone (ACC_NO_WIN)."""
+    import os
+    import oracle
+    from accord_amd.deps import Context
+    b = W.keydeps_batch(40_000, nk, 12_000, 0xB17 + nk, "zipf", 0.99, status_model="model", window=2500)
+    with Context(0) as c:
+        g = c.calculate_partial_deps(b)
+        st = c.stats()
+    if nk <= 16:
+        assert st["keydeps.window_txns"] > 0
+    else:
+        assert st["keydeps.window_txns"] == 0 and st["keydeps.medium_txns"] + st["keydeps.big_txns"] > 0
+    os.environ["ACC_NO_WIN"] = "1"
+    try:
+        with Context(0) as c:
+            s = c.calculate_partial_deps(b)
+    finally:
+        del os.environ["ACC_NO_WIN"]
+    assert_same(g, s, b.n_txn, f"window vs sorting tiers, {nk} keys")
+    n = b.n_txn
+    o = oracle.keydeps_batch(b, query_lo=n - 400, query_hi=n)
+    for t in range(n - 400, n):
+        for x, y, what in zip(g.txn(t), o.txn(t), ("keys", "txnIds", "keysToTxnIds")):
+            np.testing.assert_array_equal(x, y, err_msg=f"txn {t} {what}")
+
+
 def test_path_selection():
     """Tie-free batches take the run-based path; executeAt ties switch to the exact replay."""
     from accord_amd.deps import Context

@@ -10,7 +10,7 @@ for cfg in ${CFGS:-2}; do
     for i in 1 2; do
         for v in "$@"; do
             lib=""; envs=""
-            case "$v" in new) ;; new+serial) envs="ACC_KD_SERIAL=1" ;; new+*) envs="${v#new+}" ;; *) lib=tools/prof/$v.so ;; esac
+            case "$v" in new) ;; new+serial) envs="ACC_KD_SERIAL=1" ;; new+*) envs="${v#new+}"; envs="${envs//,/ }" ;; *) lib=tools/prof/$v.so ;; esac
             env $envs ACC_BENCH_KERNELS=1 ACC_LIB_PATH=$lib timeout -k 10 300 python -u bench.py --config $cfg --steps $steps --warmup 3 --no-cpu \
                 > gpurun_out/abn_c${cfg}_${v}_$i.log 2>&1 || { echo "bench $v c$cfg failed"; tail -20 gpurun_out/abn_c${cfg}_${v}_$i.log; exit 1; }
             python -c "

@@ -13,6 +13,6 @@ for cfg in ${CFGS:-2 3}; do
         || { echo "bench c$cfg failed"; tail -30 gpurun_out/bench_c$cfg.log; exit 1; }
     python -c "
 import json,sys; d=json.loads(open('gpurun_out/bench_c$cfg.log').read().strip().splitlines()[-1])
-print('c$cfg', d['ms_per_step'], d['value'], d['roofline']['kernel'], d['roofline']['kernel_avg_ms'], d['roofline']['frac'])
+print('c$cfg', d['ms_per_step'], d['value'], d['roofline']['dominant_kernel'], d['roofline']['frac'])
 print({k:v for k,v in list(d['kernels_ms_per_step'].items())[:12]})"
 done
