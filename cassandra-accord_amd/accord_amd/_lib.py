@@ -39,8 +39,8 @@ u8p = C.POINTER(C.c_uint8)
 EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_stream", "acc_version",
            "acc_keydeps_batch", "acc_keydeps_copy_out", "acc_keydeps_mixed", "acc_rangedeps_batch", "acc_rangedeps_copy_out",
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
-           "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_stats_count", "acc_stats_get",
-           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_shard_reduce",
+           "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_timing_filter", "acc_stats_count", "acc_stats_get",
+           "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_partial_deps_reduce", "acc_shard_reduce",
            "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch",
            "acc_deps_from_json", "acc_deps_to_json",
            "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view"]
@@ -229,12 +229,14 @@ class JsonIn(C.Structure):
 
 class JsonDepsView(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("deps", DepsMergeView), ("n_dict", C.c_uint64), ("dict_kind", C.c_void_p),
-                ("dict_null", C.c_void_p), ("dict_value", C.c_void_p), ("dict_hash", C.c_void_p)]
+                ("dict_null", C.c_void_p), ("dict_value", C.c_void_p), ("dict_hash", C.c_void_p),
+                ("dict_len", C.c_void_p), ("dict_str", C.c_void_p)]
 
 
 class JsonOutIn(C.Structure):
     _fields_ = [("n_groups", C.c_uint32), ("key_deps", RmmView), ("range_deps", RmmView), ("n_dict", C.c_uint64),
-                ("dict_kind", C.c_void_p), ("dict_null", C.c_void_p), ("dict_value", C.c_void_p)]
+                ("dict_kind", C.c_void_p), ("dict_null", C.c_void_p), ("dict_value", C.c_void_p),
+                ("dict_len", C.c_void_p), ("dict_str", C.c_void_p)]
 
 
 class JsonOut(C.Structure):
@@ -323,6 +325,9 @@ def load():
     L.acc_comm_destroy.restype = None
     L.acc_shard_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn), C.c_void_p, C.c_uint32, C.POINTER(MergeView)]
     L.acc_shard_reduce.restype = C.c_int
+    L.acc_partial_deps_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(RangeBatchIn), C.c_void_p, C.c_uint32,
+                                          C.POINTER(MergeView), C.POINTER(DepsMergeView)]
+    L.acc_partial_deps_reduce.restype = C.c_int
     L.acc_map_reduce_full.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(RecoveryIn), C.POINTER(KeydepsView)]
     L.acc_map_reduce_full.restype = C.c_int
     L.acc_latest_deps_merge.argtypes = [C.c_void_p, C.POINTER(LatestIn), C.POINTER(LatestView)]
@@ -348,6 +353,8 @@ def load():
     L.acc_timing_get.restype = C.c_int
     L.acc_timing_reset.argtypes = [C.c_void_p]
     L.acc_timing_reset.restype = None
+    L.acc_timing_filter.argtypes = [C.c_void_p, C.c_char_p]
+    L.acc_timing_filter.restype = C.c_int
     L.acc_stats_count.argtypes = [C.c_void_p]
     L.acc_stats_count.restype = C.c_int
     L.acc_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64)]

@@ -47,6 +47,7 @@ class Context:
     """One acc_ctx: a HIP stream plus device scratch (one per host thread / CommandStore)."""
 
     def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False):
+        self.timing_enabled = timing
         self._lib = L.load()
         h = C.c_void_p()
         opts = L.Opts((L.ACC_OPT_TIMING if timing else 0) | (L.ACC_OPT_FORCE_REPLAY if force_replay else 0), 0)
@@ -112,6 +113,10 @@ class Context:
 
     def timing_reset(self):
         self._lib.acc_timing_reset(self._h)
+
+    def timing_filter(self, tags=None):
+        """Time only the launches with these tags (None: every launch; ACC_OPT_TIMING contexts)."""
+        self.check(self._lib.acc_timing_filter(self._h, ",".join(tags).encode() if tags else None))
 
     # ---- KeyDeps batch
     def keydeps_batch_raw(self, batch_in: "L.BatchIn") -> "L.KeydepsView":
@@ -660,7 +665,12 @@ def deps_from_json(ctx: Context, docs: list[bytes], with_view: bool = False):
     out = dict(key=rmm_copy_out(ctx, len(docs), v.deps.key_deps, False),
                range=rmm_copy_out(ctx, len(docs), v.deps.range_deps, True),
                dict_kind=device_array(ctx, v.dict_kind, nd, np.uint8), dict_null=device_array(ctx, v.dict_null, nd, np.uint8),
-               dict_value=device_array(ctx, v.dict_value, nd, np.uint64), dict_hash=device_array(ctx, v.dict_hash, nd, np.int32))
+               dict_value=device_array(ctx, v.dict_value, nd, np.uint64), dict_hash=device_array(ctx, v.dict_hash, nd, np.int32),
+               dict_len=device_array(ctx, v.dict_len, nd, np.uint32))
+    # STRING texts: dict_str[value : value + len] of every STRING rank
+    total = int(max((int(o) + int(n) for o, n, k in zip(out["dict_value"], out["dict_len"], out["dict_kind"]) if k == 0),
+                    default=0))
+    out["dict_str"] = device_array(ctx, v.dict_str, total, np.uint8)
     if with_view:
         out["view"] = v
     return out
@@ -669,7 +679,7 @@ def deps_from_json(ctx: Context, docs: list[bytes], with_view: bool = False):
 def deps_to_json(ctx: Context, view) -> list[bytes]:
     """Json.DEPS_ADAPTER.write of every document of an acc_json_deps_view on device (acc_deps_to_json)."""
     oi = L.JsonOutIn(view.n_docs, view.deps.key_deps, view.deps.range_deps, view.n_dict, view.dict_kind, view.dict_null,
-                     view.dict_value)
+                     view.dict_value, view.dict_len, view.dict_str)
     o = L.JsonOut()
     o.mem = L.ACC_MEM_HOST
     rc = ctx._lib.acc_deps_to_json(ctx.handle, C.byref(oi), C.byref(o))

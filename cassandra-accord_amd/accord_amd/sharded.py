@@ -380,8 +380,10 @@ class Comm:
             ctx.check(ctx._lib.acc_comm_unique_id(uid.ctypes.data))
         if world > 1:
             t = torch.from_numpy(uid.astype(np.int64))
+            if dist.get_backend(group) == "nccl":   # the nccl (RCCL) backend moves device tensors only
+                t = t.to(torch.device("cuda", torch.cuda.current_device()))
             dist.broadcast(t, 0, group=group)
-            uid = t.numpy().astype(np.uint8)
+            uid = t.cpu().numpy().astype(np.uint8)
         h = C.c_void_p()
         ctx.check(ctx._lib.acc_comm_init_rccl(ctx.handle, world, rank, uid.ctypes.data, C.byref(h)))
         return cls(ctx, h)
@@ -436,3 +438,18 @@ def shard_reduce(ctx, comm: Comm, bi, n_global: int, txn_global=None):
     view = L.MergeView()
     ctx.check(ctx._lib.acc_shard_reduce(ctx.handle, comm.handle, C.byref(bi), ptr, n_global, C.byref(view)))
     return view
+
+
+def partial_deps_reduce(ctx, comm: Comm, rbi, n_global: int, txn_global=None):
+    """acc_partial_deps_reduce: PreAccept.reduce of both PartialDeps halves of the last acc_partial_deps_batch on ctx
+    (mixed batch `rbi`, an acc_range_batch_in) over `comm`, one exchange; returns (KeyDeps merge view, Deps.merge view
+    whose range half is the RangeDeps.with fold in store order)."""
+    import ctypes as C
+    from . import _lib as L
+    ptr = None
+    if txn_global is not None:
+        ptr = txn_global.data_ptr() if hasattr(txn_global, "data_ptr") else np.ascontiguousarray(txn_global).ctypes.data
+    kv, rv = L.MergeView(), L.DepsMergeView()
+    ctx.check(ctx._lib.acc_partial_deps_reduce(ctx.handle, comm.handle, C.byref(rbi), ptr, n_global, C.byref(kv),
+                                               C.byref(rv)))
+    return kv, rv

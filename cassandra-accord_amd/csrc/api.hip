@@ -415,6 +415,25 @@ void acc_timing_reset(acc_ctx *ctx)
     for (auto &s : ctx->slots) { s.total_ms = 0; s.launches = 0; }
 }
 
+int acc_timing_filter(acc_ctx *ctx, const char *tags_csv)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ctx->time_only.clear();
+        if (!tags_csv) return;
+        std::string cur;
+        for (const char *c = tags_csv;; ++c) {
+            if (*c == ',' || *c == 0) {
+                if (!cur.empty()) ctx->time_only.push_back(cur);
+                cur.clear();
+                if (!*c) break;
+            } else {
+                cur.push_back(*c);
+            }
+        }
+    });
+}
+
 int acc_stats_count(acc_ctx *ctx) { return ctx ? (int)ctx->stats.size() : 0; }
 
 int acc_stats_get(acc_ctx *ctx, int i, const char **name, uint64_t *value)

@@ -74,7 +74,8 @@ struct Out {
 
 using namespace cf;
 
-__global__ __launch_bounds__(BLOCK) void k_cf_validate(Delta d, uint64_t *__restrict__ errs, uint64_t *__restrict__ w0,
+// the key loop stays inside [0, Pd) whatever key_off holds: offsets must start at 0, not decrease and stay within Pd
+__global__ __launch_bounds__(BLOCK) void k_cf_validate(Delta d, uint32_t Pd, uint64_t *__restrict__ errs, uint64_t *__restrict__ w0,
                                                        uint64_t *__restrict__ w1, uint64_t *__restrict__ w2)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(BLOCK) void k_cf_validate(Delta d, uint64_t *__rest
     if (d.status[i] > ACC_ST_INVALID_OR_TRUNCATED) e |= E_STATUS;
     if (((d.tl[i] >> 1) & 7u) > ACC_KIND_LOCAL_ONLY) e |= E_KIND;
     const uint32_t k0 = d.key_off[i], k1 = d.key_off[i + 1];
-    if (k1 < k0) e |= E_OFF;
+    if (k1 < k0 || k1 > Pd || (i == 0 && k0 != 0)) e |= E_OFF;
     else
         for (uint32_t j = k0 + 1; j < k1; ++j)
             if (d.key_code[j - 1] >= d.key_code[j]) { e |= E_KEYS; break; }
@@ -276,7 +277,7 @@ void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
     uint64_t *errs = ctx->get<uint64_t>("cf_errs", 1);
     ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
     uint64_t *w[3] = { ctx->get<uint64_t>("cf_w0", D), ctx->get<uint64_t>("cf_w1", D), ctx->get<uint64_t>("cf_w2", D) };
-    launch(ctx, "cf_validate", k_cf_validate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, errs, w[0], w[1], w[2]);
+    launch(ctx, "cf_validate", k_cf_validate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, (uint32_t)Pd, errs, w[0], w[1], w[2]);
     const uint64_t *words[3] = { w[0], w[1], w[2] };
     DenseRank dr = dense_rank(ctx, "cf_dr", D, 3, words, nullptr, nullptr, false);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
@@ -286,7 +287,7 @@ void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
     uint64_t e = ctx->pinned[0];
     if (e & E_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal (> INVALID_OR_TRUNCATED)");
     if (e & E_KIND) fail(ACC_E_ARG, "Kind.ofOrdinal: invalid kind ordinal in TxnId flags");
-    if (e & E_OFF) fail(ACC_E_ARG, "key_off must be non-decreasing");
+    if (e & E_OFF) fail(ACC_E_ARG, "key_off must start at 0, be non-decreasing and end at n_pairs");
     if (e & E_KEYS) fail(ACC_E_ARG, "keys of a txn must be sorted and unique (Keys.ofSortedUnique)");
     if (ctx->pinned[1] != D) fail(ACC_E_ARG, "TxnIds of one update must be distinct");
     if ((ctx->pinned[2] & 0xFFFFFFFFull) != Pd) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");

@@ -17,6 +17,8 @@
 namespace acc {
 void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
+void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in, const uint32_t *txn_global,
+                         uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view);
 
 struct Rccl {
     bool ok = false;
@@ -102,54 +104,174 @@ static void exchange(acc_comm *c, const uint8_t *send, const std::vector<uint64_
     ctx->sync();
 }
 
+// Fragment streams of one exchange: stream q = elements of esz[q] bytes, destination-major (destination d owns
+// elements [off[q][d], off[q][d+1]) of send[q]). After exchange_streams: recv[q] = what the sources sent, concatenated in
+// source-rank order, n_src[q][s] elements from source s.
+struct Streams {
+    int ns = 0;
+    const void *send[8] = {};
+    std::vector<uint64_t> off[8];
+    uint64_t esz[8] = {};
+    void *recv[8] = {};
+    std::vector<uint64_t> n_src[8];
+};
+
+// ONE size exchange (every stream's element count per peer) and ONE grouped all-to-all(v) carrying every stream: the
+// RCCL transport issues all streams' point-to-point sends / receives inside one ncclGroupStart / End; the host transport
+// hands the caller one byte block per peer (the peer's slice of every stream, concatenated) in a single call.
+static void exchange_streams(acc_comm *c, Streams &S)
+{
+    acc_ctx *ctx = c->ctx;
+    const uint32_t W = c->world;
+    const int ns = S.ns;
+    hipStream_t st = ctx->stream;
+    // ---- sizes
+    uint64_t *cnt_s = ctx->get<uint64_t>("cm_cnt_s", (size_t)ns * W), *cnt_r = ctx->get<uint64_t>("cm_cnt_r", (size_t)ns * W);
+    std::vector<uint64_t> hcs((size_t)ns * W), hcr((size_t)ns * W);
+    for (uint32_t d = 0; d < W; ++d)
+        for (int q = 0; q < ns; ++q) hcs[(size_t)ns * d + q] = S.off[q][d + 1] - S.off[q][d];
+    ACC_HIP(hipMemcpyAsync(cnt_s, hcs.data(), hcs.size() * 8, hipMemcpyHostToDevice, st));
+    std::vector<uint64_t> cs(W + 1), cr(W + 1);
+    for (uint32_t d = 0; d <= W; ++d) cs[d] = cr[d] = 8ull * ns * d;
+    exchange(c, reinterpret_cast<const uint8_t *>(cnt_s), cs, reinterpret_cast<uint8_t *>(cnt_r), cr);
+    ACC_HIP(hipMemcpyAsync(hcr.data(), cnt_r, hcr.size() * 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    // ---- receive buffers (source-major per stream)
+    static const char *rn[8] = { "cm_r0", "cm_r1", "cm_r2", "cm_r3", "cm_r4", "cm_r5", "cm_r6", "cm_r7" };
+    std::vector<uint64_t> rb[8];   // byte offsets per source
+    for (int q = 0; q < ns; ++q) {
+        S.n_src[q].assign(W, 0);
+        rb[q].assign(W + 1, 0);
+        for (uint32_t p = 0; p < W; ++p) {
+            S.n_src[q][p] = hcr[(size_t)ns * p + q];
+            rb[q][p + 1] = rb[q][p] + S.n_src[q][p] * S.esz[q];
+        }
+        S.recv[q] = ctx->get<uint8_t>(rn[q], rb[q][W]);
+    }
+    auto sptr = [&](int q, uint32_t p) {
+        return static_cast<const uint8_t *>(S.send[q]) + (S.off[q][p] - S.off[q][0]) * S.esz[q];
+    };
+    uint64_t sent = 0, got = 0;
+    for (int q = 0; q < ns; ++q) {
+        sent += (S.off[q][W] - S.off[q][0] - (S.off[q][c->rank + 1] - S.off[q][c->rank])) * S.esz[q];
+        got += rb[q][W] - (rb[q][c->rank + 1] - rb[q][c->rank]);
+    }
+    ctx->stat("exchange.bytes_sent", sent);       // to other ranks (the self slice stays on the GPU's own links)
+    ctx->stat("exchange.bytes_received", got);
+    if (c->nc) {
+        Rccl &r = rccl();
+        ACC_NCCL(r.group_start());
+        for (uint32_t p = 0; p < W; ++p)
+            for (int q = 0; q < ns; ++q) {
+                const uint64_t nsb = (S.off[q][p + 1] - S.off[q][p]) * S.esz[q], nrb = rb[q][p + 1] - rb[q][p];
+                if (nsb) ACC_NCCL(r.send(sptr(q, p), nsb, ncclUint8, (int)p, c->nc, st));
+                if (nrb) ACC_NCCL(r.recv(static_cast<uint8_t *>(S.recv[q]) + rb[q][p], nrb, ncclUint8, (int)p, c->nc, st));
+            }
+        ACC_NCCL(r.group_end());
+        return;
+    }
+    // host transport: every stream to the host once, per-peer blocks assembled, one call, scattered back per stream
+    std::vector<std::vector<uint8_t>> hs(ns);
+    for (int q = 0; q < ns; ++q) {
+        const uint64_t nb = (S.off[q][W] - S.off[q][0]) * S.esz[q];
+        hs[q].resize(nb);
+        if (nb) ACC_HIP(hipMemcpyAsync(hs[q].data(), sptr(q, 0), nb, hipMemcpyDeviceToHost, st));
+    }
+    ctx->sync();
+    std::vector<uint64_t> bs(W, 0), br(W, 0);
+    for (uint32_t p = 0; p < W; ++p)
+        for (int q = 0; q < ns; ++q) {
+            bs[p] += (S.off[q][p + 1] - S.off[q][p]) * S.esz[q];
+            br[p] += rb[q][p + 1] - rb[q][p];
+        }
+    uint64_t ts = 0, tr = 0;
+    for (uint32_t p = 0; p < W; ++p) { ts += bs[p]; tr += br[p]; }
+    std::vector<uint8_t> send(ts), recv(tr);
+    uint64_t w = 0;
+    for (uint32_t p = 0; p < W; ++p)
+        for (int q = 0; q < ns; ++q) {
+            const uint64_t a0 = (S.off[q][p] - S.off[q][0]) * S.esz[q], nb = (S.off[q][p + 1] - S.off[q][p]) * S.esz[q];
+            if (nb) memcpy(send.data() + w, hs[q].data() + a0, nb);
+            w += nb;
+        }
+    const int rc = c->fn(c->user, send.data(), bs.data(), recv.data(), br.data());
+    if (rc != 0) fail(ACC_E_STATE, "host transport all-to-all failed (" + std::to_string(rc) + ")");
+    std::vector<std::vector<uint8_t>> hr(ns);
+    for (int q = 0; q < ns; ++q) hr[q].resize(rb[q][W]);
+    uint64_t x = 0;
+    for (uint32_t p = 0; p < W; ++p)
+        for (int q = 0; q < ns; ++q) {
+            const uint64_t nb = rb[q][p + 1] - rb[q][p];
+            if (nb) memcpy(hr[q].data() + rb[q][p], recv.data() + x, nb);
+            x += nb;
+        }
+    for (int q = 0; q < ns; ++q)
+        if (rb[q][W]) ACC_HIP(hipMemcpyAsync(S.recv[q], hr[q].data(), rb[q][W], hipMemcpyHostToDevice, st));
+    ctx->sync();
+}
+
+// the KeyDeps fragments of the last KeyDeps result on ctx, packed into the four streams of S (slots 0..3)
+static void add_key_streams(acc_ctx *ctx, const acc_batch_in *in, const uint32_t *txn_global, uint32_t W, Streams &S)
+{
+    for (int q = 0; q < 4; ++q) S.off[q].assign(W + 1, 0);
+    acc_frag_streams fs{};
+    fs.world = W;
+    fs.mem = ACC_MEM_DEVICE;
+    fs.frag_off = S.off[0].data(); fs.key_off = S.off[1].data(); fs.val_off = S.off[2].data(); fs.k2v_off = S.off[3].data();
+    fs.txn_global = txn_global;
+    shard_pack(ctx, in, &fs, true);
+    S.send[0] = fs.hdr; S.send[1] = fs.keys; S.send[2] = fs.vals; S.send[3] = fs.k2v;
+    S.esz[0] = 16; S.esz[1] = 8; S.esz[2] = 4; S.esz[3] = 4;   // header (4 x u32), key code, TxnId index, int
+    S.ns = 4;
+}
+
+static void merge_key_streams(acc_ctx *ctx, acc_comm *c, uint32_t n_global, const Streams &S, acc_merge_view *view)
+{
+    acc_frag_recv fr{ ACC_MEM_DEVICE, c->world, c->rank, n_global, S.n_src[0].data(), S.n_src[1].data(), S.n_src[2].data(),
+                      S.n_src[3].data(), static_cast<const uint32_t *>(S.recv[0]), static_cast<const uint64_t *>(S.recv[1]),
+                      static_cast<const uint32_t *>(S.recv[2]), static_cast<const int32_t *>(S.recv[3]) };
+    shard_merge(ctx, &fr, view);
+}
+
 void shard_reduce(acc_ctx *ctx, acc_comm *c, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
                   acc_merge_view *view)
 {
     if (!c || !in || !view) fail(ACC_E_ARG, "null argument");
     if (c->ctx != ctx) fail(ACC_E_ARG, "communicator belongs to another context");
-    const uint32_t W = c->world;
-    // ---- pack (destination-major streams, context-owned)
-    std::vector<uint64_t> off[4];
-    for (auto &o : off) o.assign(W + 1, 0);
-    acc_frag_streams fs{};
-    fs.world = W;
-    fs.mem = ACC_MEM_DEVICE;
-    fs.frag_off = off[0].data(); fs.key_off = off[1].data(); fs.val_off = off[2].data(); fs.k2v_off = off[3].data();
-    fs.txn_global = txn_global;
-    shard_pack(ctx, in, &fs, true);
-    const uint64_t esz[4] = { 16, 8, 4, 4 };   // bytes per element: header (4 x u32), key code, TxnId index, int
-    // ---- one size exchange: element counts per stream for every peer
-    uint64_t *cnt_s = ctx->get<uint64_t>("cm_cnt_s", 4 * (size_t)W), *cnt_r = ctx->get<uint64_t>("cm_cnt_r", 4 * (size_t)W);
-    std::vector<uint64_t> hcs(4 * (size_t)W), hcr(4 * (size_t)W);
-    for (uint32_t d = 0; d < W; ++d)
-        for (int q = 0; q < 4; ++q) hcs[4 * d + q] = off[q][d + 1] - off[q][d];
-    ACC_HIP(hipMemcpyAsync(cnt_s, hcs.data(), hcs.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    std::vector<uint64_t> cs(W + 1), cr(W + 1);
-    for (uint32_t d = 0; d <= W; ++d) cs[d] = cr[d] = 32ull * d;
-    exchange(c, reinterpret_cast<const uint8_t *>(cnt_s), cs, reinterpret_cast<uint8_t *>(cnt_r), cr);
-    ACC_HIP(hipMemcpyAsync(hcr.data(), cnt_r, hcr.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    ctx->sync();
-    // ---- the four streams
-    std::vector<uint64_t> n_src[4];
-    void *recv[4];
-    const char *rn[4] = { "cm_r_hdr", "cm_r_keys", "cm_r_vals", "cm_r_k2v" };
-    const void *send[4] = { fs.hdr, fs.keys, fs.vals, fs.k2v };
-    for (int q = 0; q < 4; ++q) {
-        std::vector<uint64_t> os(W + 1), orr(W + 1);
-        n_src[q].assign(W, 0);
-        for (uint32_t p = 0; p < W; ++p) {
-            os[p + 1] = os[p] + (off[q][p + 1] - off[q][p]) * esz[q];
-            n_src[q][p] = hcr[4 * p + q];
-            orr[p + 1] = orr[p] + hcr[4 * p + q] * esz[q];
-        }
-        recv[q] = ctx->get<uint8_t>(rn[q], orr[W]);
-        exchange(c, static_cast<const uint8_t *>(send[q]) + off[q][0] * esz[q], os, static_cast<uint8_t *>(recv[q]), orr);
-    }
-    // ---- KeyDeps.with fold of every home txn (stream order makes the merge wait for the receives)
-    acc_frag_recv fr{ ACC_MEM_DEVICE, W, c->rank, n_global, n_src[0].data(), n_src[1].data(), n_src[2].data(),
-                      n_src[3].data(), static_cast<const uint32_t *>(recv[0]), static_cast<const uint64_t *>(recv[1]),
-                      static_cast<const uint32_t *>(recv[2]), static_cast<const int32_t *>(recv[3]) };
-    shard_merge(ctx, &fr, view);
+    Streams S;
+    add_key_streams(ctx, in, txn_global, c->world, S);
+    exchange_streams(c, S);
+    // KeyDeps.with fold of every home txn (stream order makes the merge wait for the receives)
+    merge_key_streams(ctx, c, n_global, S, view);
+}
+
+void range_pack(acc_ctx *ctx, const acc_range_batch_in *in, const uint32_t *txn_global, uint32_t world, uint32_t n_global,
+                void *send[4], std::vector<uint64_t> off[4]);
+void range_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_global, const std::vector<uint64_t> n_src[4],
+                 void *const recv[4], acc_deps_merge_view *view);
+
+// PreAccept.reduce of a store's whole PartialDeps: both halves' fragments in one exchange (8 streams), then KeyDeps.with
+// (shard_merge) and RangeDeps.with in store order (range_merge) on the home rank
+void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in, const uint32_t *txn_global,
+                         uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view)
+{
+    if (!c || !in || !key_view || !range_view) fail(ACC_E_ARG, "null argument");
+    if (c->ctx != ctx) fail(ACC_E_ARG, "communicator belongs to another context");
+    const acc_batch_in kin{ in->n_txn, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
+    Streams S;
+    add_key_streams(ctx, &kin, txn_global, c->world, S);
+    void *rs[4];
+    std::vector<uint64_t> ro[4];
+    range_pack(ctx, in, txn_global, c->world, n_global, rs, ro);
+    const uint64_t resz[4] = { 16, 16, 24, 4 };   // header (4 x u32), Range (start, end), raw TxnId (msb, lsb, node), int
+    for (int q = 0; q < 4; ++q) { S.send[4 + q] = rs[q]; S.off[4 + q] = ro[q]; S.esz[4 + q] = resz[q]; }
+    S.ns = 8;
+    exchange_streams(c, S);
+    merge_key_streams(ctx, c, n_global, S, key_view);
+    std::vector<uint64_t> rn[4];
+    void *rr[4];
+    for (int q = 0; q < 4; ++q) { rn[q] = S.n_src[4 + q]; rr[q] = S.recv[4 + q]; }
+    range_merge(ctx, c->world, c->rank, n_global, rn, rr, range_view);
 }
 
 }  // namespace acc
@@ -211,7 +333,21 @@ void acc_comm_destroy(acc_comm *c)
 int acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
                      acc_merge_view *out_view)
 {
-    return acc_guard(ctx, [&] { acc::shard_reduce(ctx, comm, in, txn_global, n_global, out_view); });
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::shard_reduce(ctx, comm, in, txn_global, n_global, out_view);
+    });
+}
+
+int acc_partial_deps_reduce(acc_ctx *ctx, acc_comm *comm, const acc_range_batch_in *in, const uint32_t *txn_global,
+                            uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::partial_deps_reduce(ctx, comm, in, txn_global, n_global, key_view, range_view);
+    });
 }
 
 }  // extern "C"

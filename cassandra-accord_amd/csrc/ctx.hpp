@@ -73,6 +73,15 @@ struct acc_ctx {
     std::unordered_map<std::string, int> slot_index;
     std::vector<acc::PendingEvent> pending;
     std::vector<hipEvent_t> event_pool;
+    std::vector<std::string> time_only;   // non-empty: only these launch tags are timed (acc_timing_filter)
+    bool timed(const char *name) const
+    {
+        if (!(flags & ACC_OPT_TIMING)) return false;
+        if (time_only.empty()) return true;
+        for (const auto &t : time_only)
+            if (t == name) return true;
+        return false;
+    }
     // counters of the last call (name -> value), exposed by acc_stats_*
     std::vector<std::pair<std::string, uint64_t>> stats;
     void stat(const char *name, uint64_t value)
@@ -219,7 +228,7 @@ inline void launch(acc_ctx *ctx, const char *name, K kernel, dim3 grid, dim3 blo
 {
     if (grid.x == 0 || grid.y == 0 || grid.z == 0) return;
     PendingEvent pe{};
-    bool timed = (ctx->flags & ACC_OPT_TIMING) != 0;
+    const bool timed = ctx->timed(name);
     if (timed) {
         pe.slot = ctx->slot(name);
         pe.start = ctx->take_event();

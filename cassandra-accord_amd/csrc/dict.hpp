@@ -12,6 +12,7 @@ struct Dictionary {
     int rbits = 0;                    // bits of the largest rank
     bool batch_sorted = false;        // txns given in TxnId order
     bool fast = false;                // sorted-batch dictionary taken
+    bool ties_pending = false;        // its executeAt-tie check (g[6]) is still to be read by the caller
     uint64_t hg[8] = {};              // prep words: ts word masks [0..2], key mask [3], errors [4], unsorted [5]
 };
 
@@ -30,7 +31,10 @@ DenseRank dense_rank(acc_ctx *ctx, const char *tag, size_t n, int nw, const uint
 // key_off/key_code: the key-domain part (P pairs); owner[P] receives the txn of every pair; g[8] scratch words.
 void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
                      const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
-                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out);
+                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out,
+                     bool defer_ties = false);
+void redo_general_dictionary(acc_ctx *ctx, uint32_t n, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                             const uint64_t *em, const uint64_t *el, const int32_t *en, uint64_t *g, Dictionary &d);
 
 // The CommandsForKey snapshot of a key batch (keydeps.hip stages 1-3) for the scans other than mapReduceActive: pairs
 // sorted by (key, TxnId rank) = one segment per key, entries in CommandsForKey.txns order. cfk = false when the batch has

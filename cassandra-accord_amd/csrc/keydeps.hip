@@ -87,43 +87,69 @@ __device__ __forceinline__ void block_or_n(uint64_t (&v)[NW], uint64_t *dst)
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, const uint64_t *__restrict__ tm, const uint64_t *__restrict__ tl,
+// Per txn: executeAt != TxnId flags, varying-bit masks, status / kind checks, TxnId order; per pair (a chunk's txns'
+// pairs are one contiguous range, walked coalesced with each pair's txn found in the chunk's key offsets in LDS):
+// owner[], key order within a txn (Keys.ofSortedUnique), the key-code varying-bit mask. Pair indices are bounded by P
+// (a malformed key_off is reported, never followed out of bounds). Blocks stride over chunks of BLOCK txns and fold
+// their words into g[] once at the end: same-address atomics serialise at the L2 (one per block per word over 4k
+// blocks cost ~0.1 ms).
+__global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const uint64_t *__restrict__ tm, const uint64_t *__restrict__ tl,
                                                     const int32_t *__restrict__ tn, const uint64_t *__restrict__ em,
                                                     const uint64_t *__restrict__ el, const int32_t *__restrict__ en,
                                                     const uint8_t *__restrict__ status, const uint32_t *__restrict__ key_off,
                                                     const uint64_t *__restrict__ key_code, uint32_t *__restrict__ owner,
                                                     uint32_t *__restrict__ bflag, uint64_t *__restrict__ g)
 {
-    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t m0 = 0, m1 = 0, m2 = 0, errs = 0, unsorted = 0;
-    int differs = 0;
-    if (t < n) {
-        // executeAt != txnId (Timestamp.equals): these are the only executeAts the sorted-batch
-        // dictionary has to sort
-        differs = tm[t] != em[t] || ts_w1(tl[t]) != ts_w1(el[t]) || tn[t] != en[t];
-        bflag[t] = (uint32_t)differs;
-        const uint64_t r0 = tm[0], r1 = ts_w1(tl[0]), r2 = ts_w2(tn[0]);
-        m0 = (tm[t] ^ r0) | (em[t] ^ r0);
-        m1 = (ts_w1(tl[t]) ^ r1) | (ts_w1(el[t]) ^ r1);
-        m2 = (ts_w2(tn[t]) ^ r2) | (ts_w2(en[t]) ^ r2);
-        if (status[t] > 7) errs |= ERR_BAD_STATUS;
-        uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
-        if (kind >= 6) errs |= ERR_BAD_KIND;
-        else if (kind == 5) errs |= ERR_LOCAL_ONLY;
-        if (t + 1 < n && ts_cmp(tm[t], tl[t], tn[t], tm[t + 1], tl[t + 1], tn[t + 1]) >= 0) unsorted = 1;
-        uint32_t a = key_off[t], b = key_off[t + 1];
-        if (b < a) errs |= ERR_KEY_OFF;
-        else {
-            for (uint32_t j = a; j < b; ++j) {
-                owner[j] = t;
-                if (j > a && key_code[j - 1] >= key_code[j]) errs |= ERR_KEYS_UNSORTED;
+    __shared__ uint32_t ko[BLOCK + 1];
+    const uint32_t tid = threadIdx.x;
+    uint64_t m0 = 0, m1 = 0, m2 = 0, km = 0, errs = 0, unsorted = 0;
+    uint32_t differs = 0;
+    const uint64_t r0 = tm[0], r1 = ts_w1(tl[0]), r2 = ts_w2(tn[0]);
+    const uint64_t kref = P ? key_code[0] : 0;
+    for (uint32_t t0 = blockIdx.x * BLOCK; t0 < n; t0 += gridDim.x * BLOCK) {
+        const uint32_t t = t0 + tid;
+        const uint32_t tcnt = min((uint32_t)BLOCK, n - t0);
+        __syncthreads();   // the previous chunk's ko[] readers are done
+        if (tid < tcnt) ko[tid] = key_off[t];
+        if (tid == 0) ko[tcnt] = key_off[t0 + tcnt];
+        if (t < n) {
+            // executeAt != txnId (Timestamp.equals): these are the only executeAts the sorted-batch
+            // dictionary has to sort
+            const bool d = tm[t] != em[t] || ts_w1(tl[t]) != ts_w1(el[t]) || tn[t] != en[t];
+            differs += d;
+            bflag[t] = (uint32_t)d;
+            m0 |= (tm[t] ^ r0) | (em[t] ^ r0);
+            m1 |= (ts_w1(tl[t]) ^ r1) | (ts_w1(el[t]) ^ r1);
+            m2 |= (ts_w2(tn[t]) ^ r2) | (ts_w2(en[t]) ^ r2);
+            if (status[t] > 7) errs |= ERR_BAD_STATUS;
+            uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
+            if (kind >= 6) errs |= ERR_BAD_KIND;
+            else if (kind == 5) errs |= ERR_LOCAL_ONLY;
+            if (t + 1 < n && ts_cmp(tm[t], tl[t], tn[t], tm[t + 1], tl[t + 1], tn[t + 1]) >= 0) unsorted = 1;
+        }
+        __syncthreads();
+        const bool bad = tid < tcnt && ko[tid + 1] < ko[tid];
+        if (bad) errs |= ERR_KEY_OFF;
+        if (!__syncthreads_or(bad ? 1 : 0) && P) {
+            const uint32_t a = (uint32_t)min((size_t)ko[0], P), b = (uint32_t)min((size_t)ko[tcnt], P);
+            for (uint32_t j = a + tid; j < b; j += BLOCK) {
+                uint32_t lo = 0, hi = tcnt;   // last txn i with ko[i] <= j (empty txns share their offset with the next)
+                while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (ko[m] <= j) lo = m; else hi = m; }
+                owner[j] = t0 + lo;
+                const uint64_t kc = key_code[j];
+                km |= kc ^ kref;
+                if (j > ko[lo] && key_code[j - 1] >= kc) errs |= ERR_KEYS_UNSORTED;
             }
         }
     }
-    uint64_t v[6] = { m0, m1, m2, 0, errs, unsorted };
+    uint64_t v[6] = { m0, m1, m2, km, errs, unsorted };
     block_or_n<6>(v, g);
-    int nd = __syncthreads_count(differs);
-    if (threadIdx.x == 0 && nd) atomicAdd((unsigned long long *)&g[7], (unsigned long long)nd);
+    __shared__ uint32_t s_nd;
+    if (tid == 0) s_nd = 0;
+    __syncthreads();
+    if (differs) atomicAdd(&s_nd, differs);
+    __syncthreads();
+    if (tid == 0 && s_nd) atomicAdd((unsigned long long *)&g[7], (unsigned long long)s_nd);
 }
 
 // ---- sorted-batch dictionary: TxnIds are already in order; only the differing executeAts (B) are sorted.
@@ -190,17 +216,6 @@ __global__ __launch_bounds__(BLOCK) void k_rank_b_sorted(uint32_t n, uint32_t nb
     }
     uint64_t v[1] = { tie };
     block_or_n<1>(v, g + 6);
-}
-
-// grid-stride: a few hundred blocks, each ORs many codes before its single atomic
-__global__ __launch_bounds__(BLOCK) void k_prep_keys(size_t P, const uint64_t *__restrict__ key_code, uint64_t *__restrict__ g)
-{
-    const uint64_t ref = key_code[0];
-    uint64_t m = 0;
-    for (size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x; j < P; j += (size_t)gridDim.x * BLOCK)
-        m |= key_code[j] ^ ref;
-    uint64_t v[1] = { m };
-    block_or_n<1>(v, g + 3);
 }
 
 // ---------------------------------------------------------------- dictionary (order ranks)
@@ -346,25 +361,6 @@ __global__ __launch_bounds__(BLOCK) void k_pair_tinfo(size_t P, const uint32_t *
 {
     size_t j = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (j < P) ptinfo[j] = tinfo[owner[j]];
-}
-
-__global__ __launch_bounds__(BLOCK) void k_cfk_gather(size_t P, const uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
-                                                      const uint32_t *__restrict__ seg_incl,
-                                                      const uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ seg_start,
-                                                      uint32_t *__restrict__ s_rank, uint32_t *__restrict__ s_exec,
-                                                      uint8_t *__restrict__ s_info, uint32_t *__restrict__ pair_pos)
-{
-    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= P) return;
-    uint32_t j = perm[p];
-    uint4 ti = ptinfo[j];
-    uint32_t seg = seg_incl[p] - 1;
-    if (seg_flag[p]) seg_start[seg] = (uint32_t)p;
-    if (p == P - 1) seg_start[seg + 1] = (uint32_t)P;
-    s_rank[p] = ti.x;
-    s_exec[p] = ti.y;
-    s_info[p] = (uint8_t)ti.z;
-    if (pair_pos) pair_pos[j] = (uint32_t)p;
 }
 
 // inverse of the CFK permutation, only for the consumers that address pairs by index (exact replay, the global
@@ -727,24 +723,51 @@ __device__ __forceinline__ void v2_codes4(size_t P, size_t base, const uint32_t 
         code[i] = base + i < P ? v2_code(rk[i], ex[i], (inf >> (8 * i)) & 0xFFu) : 7u;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_v2_reduce(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
-                                                     const uint8_t *__restrict__ s_info, uint32_t *__restrict__ tile_sums,
-                                                     uint32_t ntiles)
+// The CFK columns of four consecutive positions per thread (s_rank / s_exec / s_info from the per-pair txn records, the
+// segment starts, optionally pair_pos) and the per-tile counts of the class lists (the multi-scan's reduce step) over
+// the same 1024-position tile that k_v2_apply scans.
+__global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
+                                                       const uint32_t *__restrict__ seg_incl, const uint32_t *__restrict__ seg_flag,
+                                                       uint32_t *__restrict__ seg_start, uint32_t *__restrict__ s_rank,
+                                                       uint32_t *__restrict__ s_exec, uint8_t *__restrict__ s_info,
+                                                       uint32_t *__restrict__ pair_pos, uint32_t *__restrict__ tile_sums,
+                                                       uint32_t ntiles)
 {
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t c[NCNT] = {};
     if (base < P) {
-        uint32_t code[V2_ITEMS], rk[V2_ITEMS];
-        v2_codes4(P, base, s_rank, s_exec, s_info, code, rk);
+        uint32_t j[V2_ITEMS], sg[V2_ITEMS], fl[V2_ITEMS];
+        uint4 ti[V2_ITEMS];
 #pragma unroll
         for (int i = 0; i < V2_ITEMS; ++i) {
-            uint32_t l = code[i] & 7u;
+            const bool in = base + i < P;
+            j[i] = in ? perm[base + i] : 0u;
+            sg[i] = in ? seg_incl[base + i] : 0u;
+            fl[i] = in ? seg_flag[base + i] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < V2_ITEMS; ++i) ti[i] = base + i < P ? ptinfo[j[i]] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t inf = 0;
+#pragma unroll
+        for (int i = 0; i < V2_ITEMS; ++i) {
+            const size_t p = base + i;
+            if (p >= P) break;
+            if (fl[i]) seg_start[sg[i] - 1] = (uint32_t)p;
+            if (p == P - 1) seg_start[sg[i]] = (uint32_t)P;
+            if (pair_pos) pair_pos[j[i]] = (uint32_t)p;
+            inf |= (ti[i].z & 0xFFu) << (8 * i);
+            const uint32_t code = v2_code(ti[i].x, ti[i].y, ti[i].z & 0xFFu);
+            const uint32_t l = code & 7u;
 #pragma unroll
             for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
-            c[6] += (code[i] >> 3) & 1u;
-            if ((code[i] >> 4) & 1u) c[7] = (uint32_t)(base + i) + 1;
+            c[6] += (code >> 3) & 1u;
+            if ((code >> 4) & 1u) c[7] = (uint32_t)p + 1;
         }
+        // the column arrays carry V2_ITEMS entries of padding: whole 16-B / 4-B stores
+        *reinterpret_cast<uint4 *>(s_rank + base) = make_uint4(ti[0].x, ti[1].x, ti[2].x, ti[3].x);
+        *reinterpret_cast<uint4 *>(s_exec + base) = make_uint4(ti[0].y, ti[1].y, ti[2].y, ti[3].y);
+        *reinterpret_cast<uint32_t *>(s_info + base) = inf;
     }
 #pragma unroll
     for (int q = 0; q < NCNT; ++q) {
@@ -2011,7 +2034,8 @@ constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream tx
 // no look-back), and the big-txn classification: more than ST_K keys, or (txns with a run record: bigflag = 1 from the
 // count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
 __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *__restrict__ key_off,
-                                                   const uint32_t *__restrict__ rec32, uint32_t raw_cap, uint32_t e_cap,
+                                                   const uint32_t *__restrict__ rec32, uint32_t *__restrict__ psz,
+                                                   uint32_t raw_cap, uint32_t e_cap,
                                                    uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
                                                    uint64_t *__restrict__ szK)
 {
@@ -2019,6 +2043,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
     if (t >= n) return;   // group-uniform: shuffles stay inside the group
     const uint32_t j0 = key_off[t], nk = key_off[t + 1] - j0;
     const bool run_rec = bigflag[t] != 0;
+    const bool maybe_big = run_rec || nk > (uint32_t)ST_K;
     uint32_t e = 0, kd = 0, raw = 0;
     for (uint32_t c0 = 0; c0 < nk; c0 += ST_G) {
         if (c0 + sub < nk) {
@@ -2028,6 +2053,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
             e += ej;
             kd += ej != 0;
             if (run_rec && !(w & REC_INLINE_FLAG)) raw += r[6] + r[7] + r[8] + r[9] + r[10] + r[11] + r[13];
+            if (maybe_big) psz[j0 + c0 + sub] = ej;   // the big txns' per-pair entry counts (k_v3_bigsz, k_v3_bigfill)
         }
     }
 #pragma unroll
@@ -2053,7 +2079,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t
 
 // per big txn (one wave each, list order): dependency entries E and non-empty keys Kd from the records' word 15
 __global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_t *__restrict__ blist,
-                                                    const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ rec32,
+                                                    const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ psz,
                                                     uint64_t *__restrict__ lE, uint64_t *__restrict__ lK, uint64_t *__restrict__ lA)
 {
     const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
@@ -2061,7 +2087,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_
     const uint32_t t = blist[i], j0 = key_off[t], j1 = key_off[t + 1];
     uint64_t E = 0, K = 0;
     for (uint32_t j = j0 + lane; j < j1; j += 64) {
-        const uint32_t e = rec32[16 * (size_t)j + 15] & ~REC_INLINE_FLAG;
+        const uint32_t e = psz[j];
         E += e;
         K += e != 0;
     }
@@ -2120,7 +2146,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
 }
 
 struct V3Big {
-    const uint32_t *blist, *key_off, *rec32;
+    const uint32_t *blist, *key_off;
+    const uint32_t *psz;
     const uint64_t *dB, *kB, *aB;             // exclusive prefixes over the list: scratch bases
     uint64_t *vdep_off, *vcnt;                // per pair of a big txn (dep_off / cnt of the v2 tiers)
     uint32_t *vcnz;                           // per pair of a big txn (cnz)
@@ -2143,7 +2170,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
     for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
         const uint32_t j = j0 + c0 + lane;
         const bool in = c0 + lane < nk;
-        const uint32_t e = in ? (b.rec32[16 * (size_t)j + 15] & ~REC_INLINE_FLAG) : 0u;
+        const uint32_t e = in ? b.psz[j] : 0u;
         const uint64_t einc = wave_inclusive((uint64_t)e, OpAdd<uint64_t>());
         const uint64_t nzb = __ballot(e != 0);
         const uint32_t kb = (uint32_t)__popcll(nzb & lt);
@@ -2737,46 +2764,17 @@ static void keydeps_v1_tail(acc_ctx *ctx, acc_keydeps_view *view, uint32_t n, si
     ctx->kd_valid = true;
 }
 
-// Validation (k_prep_txn: statuses, kinds, key order, TxnId order) and the order-rank dictionary of the 2N
-// timestamps (rank[t] = TxnId of t, rank[n + t] = executeAt of t; equal <=> Timestamp.equals). Shared by the
-// KeyDeps and RangeDeps paths. Throws the first validation error.
-void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
-                     const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
-                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out)
+// The general dictionary: a compacted LSD radix sort of all 2N timestamps (multi-word beyond 64 varying bits), dense
+// ranks by a flag scan, duplicate-TxnId and executeAt-tie checks (g[4], g[6]).
+static void general_ranks(acc_ctx *ctx, uint32_t n, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                          const uint64_t *em, const uint64_t *el, const int32_t *en, const TsPlan &plan, uint64_t *g,
+                          uint32_t *rank, uint32_t *txn_of_rank)
 {
     hipStream_t st = ctx->stream;
-    // ---- 1. prep
-    ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
-    uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
-    launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tm, tl, tn, em, el, en, status,
-           key_off, key_code, owner, bflag, g);
-    launch(ctx, "prep_keys", k_prep_keys, dim3(std::min<unsigned>(grid_for(P, BLOCK), 1024u)), dim3(BLOCK), 0, P,
-           key_code, g);
-    // the last key_off entry must equal P
-    {
-        uint32_t last = 0;
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
-        if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
-    }
-    uint64_t hg[8];
-    memcpy(hg, ctx->pinned, sizeof hg);
-    check_errors(hg[4]);
-    const bool batch_sorted = hg[5] == 0;
-
-    // ---- 2. dictionary: order ranks over 2N timestamps
-    TsPlan plan;
-    plan.r0 = make_runs(hg[0]); plan.r1 = make_runs(hg[1]); plan.r2 = make_runs(hg[2]);
-    plan.b0 = plan.r0.bits; plan.b1 = plan.r1.bits; plan.b2 = plan.r2.bits;
     const size_t m = 2 * (size_t)n;
-    uint32_t *rank = ctx->get<uint32_t>("rank", m);
     uint32_t *flag = ctx->get<uint32_t>("rank_flag", m);
     uint32_t *incl = ctx->get<uint32_t>("rank_incl", m);
     const unsigned gm = grid_for(m, BLOCK);
-    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
-    auto general_ranks = [&]() {
     Sorted ts_sorted;
     if (plan.b0 + plan.b1 + plan.b2 <= 64) {
         uint64_t *ck = ctx->get<uint64_t>("ts_ckey", m);
@@ -2814,15 +2812,69 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
     scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, incl, m, false);
     launch(ctx, "rank_scatter", k_rank_scatter, dim3(gm), dim3(BLOCK), 0, m, n, (const uint32_t *)ts_sorted.vals,
            (const uint32_t *)incl, rank, txn_of_rank);
+    uint32_t *seen = ctx->get<uint32_t>("dup_seen", m);
+    ACC_HIP(hipMemsetAsync(seen, 0, m * sizeof(uint32_t), st));
+    launch(ctx, "dup_txn", k_dup_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
+    launch(ctx, "exec_ties", k_exec_ties, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
+}
+
+static TsPlan ts_plan(const uint64_t *hg)
+{
+    TsPlan plan;
+    plan.r0 = make_runs(hg[0]); plan.r1 = make_runs(hg[1]); plan.r2 = make_runs(hg[2]);
+    plan.b0 = plan.r0.bits; plan.b1 = plan.r1.bits; plan.b2 = plan.r2.bits;
+    return plan;
+}
+
+// A batch whose sorted-batch dictionary met an executeAt tie (g[6], found after the caller's next sync when the check
+// was deferred): the general dictionary instead, in place (same rank buffers). g[6] is then the exact-tie flag.
+void redo_general_dictionary(acc_ctx *ctx, uint32_t n, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                             const uint64_t *em, const uint64_t *el, const int32_t *en, uint64_t *g, Dictionary &d)
+{
+    ACC_HIP(hipMemsetAsync(g + 6, 0, sizeof(uint64_t), ctx->stream));
+    general_ranks(ctx, n, tm, tl, tn, em, el, en, ts_plan(d.hg), g, d.rank, d.txn_of_rank);
+    d.fast = false;
+    d.ties_pending = false;
+    ctx->stat("keydeps.fast_dictionary", 0);
+}
+
+// Validation (k_prep_txn: statuses, kinds, key order, TxnId order) and the order-rank dictionary of the 2N
+// timestamps (rank[t] = TxnId of t, rank[n + t] = executeAt of t; equal <=> Timestamp.equals). Shared by the
+// KeyDeps and RangeDeps paths. Throws the first validation error. defer_ties: the sorted-batch dictionary's tie check
+// (g[6]) is left to the caller's next sync (out.ties_pending), which then calls redo_general_dictionary on a tie.
+void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
+                     const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
+                     const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out,
+                     bool defer_ties)
+{
+    hipStream_t st = ctx->stream;
+    // ---- 1. prep
+    ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
+    uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
+    launch(ctx, "prep_txn", k_prep_txn, dim3(std::min<unsigned>(grid_for(n, BLOCK), 512u)), dim3(BLOCK), 0, n, P, tm, tl, tn, em, el, en, status,
+           key_off, key_code, owner, bflag, g);
+    // the last key_off entry must equal P
     {
-        uint32_t *seen = ctx->get<uint32_t>("dup_seen", m);
-        ACC_HIP(hipMemsetAsync(seen, 0, m * sizeof(uint32_t), st));
-        launch(ctx, "dup_txn", k_dup_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
-        launch(ctx, "exec_ties", k_exec_ties, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, seen, g);
+        uint32_t last = 0;
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
+        if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
     }
-    };
+    uint64_t hg[8];
+    memcpy(hg, ctx->pinned, sizeof hg);
+    check_errors(hg[4]);
+    const bool batch_sorted = hg[5] == 0;
+
+    // ---- 2. dictionary: order ranks over 2N timestamps
+    const TsPlan plan = ts_plan(hg);
+    const size_t m = 2 * (size_t)n;
+    uint32_t *rank = ctx->get<uint32_t>("rank", m);
+    uint32_t *txn_of_rank = ctx->get<uint32_t>("txn_of_rank", m);
     const uint64_t nb = hg[7];
     bool fast_dict = batch_sorted && plan.b0 + plan.b1 + plan.b2 <= 64 && nb < n;
+    out.ties_pending = false;
     if (fast_dict) {
         uint32_t *bidx = ctx->get<uint32_t>("bidx", (size_t)n + 1);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, bflag, bidx, n, true, bidx + n);
@@ -2836,14 +2888,18 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
                (const uint64_t *)tkey, (const uint64_t *)sb.keys, (const uint32_t *)bflag, rank, txn_of_rank, g);
         launch(ctx, "rank_b_sorted", k_rank_b_sorted, dim3(grid_for(nb, BLOCK)), dim3(BLOCK), 0, n, (uint32_t)nb,
                (const uint64_t *)tkey, (const uint64_t *)sb.keys, (const uint32_t *)sb.vals, (const uint32_t *)bsrc, rank, g);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, g + 6, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        if (ctx->pinned[0]) {   // an executeAt equals another timestamp: dense ranks need the general dictionary
-            ACC_HIP(hipMemsetAsync(g + 6, 0, sizeof(uint64_t), st));
-            fast_dict = false;
+        if (defer_ties) {
+            out.ties_pending = true;
+        } else {
+            ACC_HIP(hipMemcpyAsync(ctx->pinned, g + 6, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            if (ctx->pinned[0]) {   // an executeAt equals another timestamp: dense ranks need the general dictionary
+                ACC_HIP(hipMemsetAsync(g + 6, 0, sizeof(uint64_t), st));
+                fast_dict = false;
+            }
         }
     }
-    if (!fast_dict) general_ranks();
+    if (!fast_dict) general_ranks(ctx, n, tm, tl, tn, em, el, en, plan, g, rank, txn_of_rank);
     ctx->stat("keydeps.fast_dictionary", fast_dict ? 1 : 0);
     out.rank = rank;
     out.txn_of_rank = txn_of_rank;
@@ -2894,12 +2950,12 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *g = ctx->get<uint64_t>("g", 8);
     uint32_t *owner = ctx->get<uint32_t>("owner", P);
     Dictionary dict;
-    prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict);
-    if (ks) { ks->have_dict = true; ks->dict = dict; ks->owner = owner; }
+    // the sorted-batch dictionary's tie check is read at the CFK sync below (one host sync fewer)
+    prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, owner, g, dict, true);
     uint64_t hg[8];
     memcpy(hg, dict.hg, sizeof hg);
     const bool batch_sorted = dict.batch_sorted;
-    uint32_t *rank = dict.rank, *txn_of_rank = dict.txn_of_rank;
+    uint32_t *const rank = dict.rank, *const txn_of_rank = dict.txn_of_rank;
     const int rbits = dict.rbits;
 
     // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
@@ -2954,12 +3010,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
     uint4 *tinfo = ctx->get<uint4>("tinfo", n);
-    launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
     uint4 *ptinfo = ctx->get<uint4>("pair_tinfo", P);
-    launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
-    launch(ctx, "cfk_gather", k_cfk_gather, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, (const uint4 *)ptinfo,
-           (const uint32_t *)seg_incl, (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info,
-           ks ? pair_pos : (uint32_t *)nullptr);
     bool have_pair_pos = ks != nullptr;
     auto need_pair_pos = [&]() {
         if (have_pair_pos) return;
@@ -2973,10 +3024,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *tile_pref = ctx->get<uint32_t>("v2_tile_pref", (size_t)NCNT * nt);
     uint32_t *totals = ctx->get<uint32_t>("v2_totals", 16);
     uint32_t *bases = ctx->get<uint32_t>("v2_bases", 16);
-    launch(ctx, "v2_reduce", k_v2_reduce, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
-           (const uint8_t *)s_info, tile_sums, nt);
-    launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
-    launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
     V2Cols cols;
     cols.rows = ctx->get<uint4>("v2_rows", 2 * (P + 1));
     cols.list_rank = ctx->get<uint32_t>("v2_list_rank", P);
@@ -2985,12 +3032,35 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_kind = ctx->get<uint8_t>("v2_bc_kind", P);
     cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
-    launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
-           (const uint8_t *)s_info, (const uint32_t *)seg_incl, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
-           rbits, cols);
+    // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
+    auto build_columns = [&]() {
+        launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
+        launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
+        launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, (const uint4 *)ptinfo,
+               (const uint32_t *)seg_incl, (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info,
+               ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
+        launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
+        launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
+        launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
+               (const uint8_t *)s_info, (const uint32_t *)seg_incl, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
+               rbits, cols);
+    };
+    build_columns();
     ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, g + 4, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
+    if (dict.ties_pending && ctx->pinned[6]) {
+        // an executeAt equals another timestamp: the sorted-batch ranks are not dense ranks; the general dictionary,
+        // then the rank-dependent columns again (the pair order does not depend on ranks in a sorted batch)
+        check_errors(ctx->pinned[4]);
+        redo_general_dictionary(ctx, n, tm, tl, tn, em, el, en, g, dict);
+        build_columns();
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, g + 4, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ctx->sync();
+    }
+    dict.ties_pending = false;
+    if (ks) { ks->have_dict = true; ks->dict = dict; ks->owner = owner; }
     uint32_t htot[8];
     memcpy(htot, ctx->pinned, sizeof htot);
     check_errors(ctx->pinned[4]);
@@ -3044,6 +3114,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ACC_HIP(hipMemsetAsync(bigflag, 0, (size_t)n * 4, st));
     ACC_HIP(hipMemsetAsync(tot, 0, 2 * sizeof(uint64_t), st));
     ACC_HIP(hipMemsetAsync(gstat, 0, GSTAT_N * sizeof(uint64_t), st));
+    uint32_t *psz = ctx->get<uint32_t>("v2_psz", P);   // per pair of a run-record txn: its entry count (k_v3_mark)
     launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, rec, bigflag, blk_e);
     const char *rc_env = getenv("ACC_ST_RAW");
     const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
@@ -3052,7 +3123,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
-    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, raw_cap,
+    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, psz, raw_cap,
            e_cap, bigflag, szA, szK);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, szA, arena_off, n, true, arena_off + n);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, szK, kd_off, n, true, kd_off + n);
@@ -3101,7 +3172,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     if (nbig) {
         const unsigned gB = (nbig + WAVES - 1) / WAVES;
         uint64_t *lE = ctx->get<uint64_t>("v3_lE", nbig), *lK = ctx->get<uint64_t>("v3_lK", nbig), *lA = ctx->get<uint64_t>("v3_lA", nbig);
-        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, vv.rec32, lE, lK, lA);
+        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, (const uint32_t *)psz, lE, lK, lA);
         uint64_t *dB = ctx->get<uint64_t>("v3_dB", (size_t)nbig + 1), *kB = ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1);
         lB = ctx->get<uint64_t>("v3_aB", (size_t)nbig + 1);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, lE, dB, nbig, true, dB + nbig);
@@ -3118,7 +3189,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         big_list = ctx->get<uint32_t>("v2_big_list", nbig);
         fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
         V3Big bg;
-        bg.blist = blist; bg.key_off = key_off; bg.rec32 = vv.rec32; bg.dB = dB; bg.kB = kB; bg.aB = lB;
+        bg.blist = blist; bg.key_off = key_off; bg.psz = psz; bg.dB = dB; bg.kB = kB; bg.aB = lB;
         bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.varena = varena; bg.bK = bK; bg.bE = bE; bg.u_cnt = u_cnt;
         bg.arena_scr = arena_scr; bg.key_scr = key_scr;
         const bool big_ok = rbits + 6 <= 31;

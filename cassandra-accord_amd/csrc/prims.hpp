@@ -471,15 +471,16 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__res
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     for (uint32_t i = tid; i < WAVES * OS_MAXP * 256; i += BLOCK) (&h[0][0][0])[i] = 0;
-    // one tile of RS_TILE keys per block, all its loads issued up front
-    const size_t base = (size_t)blockIdx.x * RS_TILE;
+    __syncthreads();
+    // tiles of RS_TILE keys (all of a tile's loads issued up front), blocks striding over them: the block's counts go to
+    // the global histogram once (every block adding to the same passes x 256 counters serialises at the L2)
+    for (size_t base = (size_t)blockIdx.x * RS_TILE; base < n; base += (size_t)gridDim.x * RS_TILE) {
     uint64_t key[RS_ITEMS];
 #pragma unroll
     for (int k = 0; k < RS_ITEMS; ++k) {
         const size_t e = base + (size_t)k * BLOCK + tid;
         key[k] = e < n ? keys[e] : 0;
     }
-    __syncthreads();
     for (int p = 0; p < passes; ++p) {
 #pragma unroll
         for (int k = 0; k < RS_ITEMS; ++k) {
@@ -494,6 +495,7 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__res
             }
             if (valid && (peers & lt_mask) == 0) h[wave][p][d] += (uint32_t)__popcll(peers);
         }
+    }
     }
     __syncthreads();
     for (uint32_t i = tid; i < (uint32_t)passes * 256; i += BLOCK) {
@@ -677,7 +679,7 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
         uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
         snprintf(th, sizeof th, "%s.ghist", tag);
-        launch(ctx, th, k_rs_ghist, dim3(ntiles), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
+        launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 256u)), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
         const uint64_t *kin = keys;
         const uint32_t *vin = vals;
         int cur = 0;
@@ -732,7 +734,7 @@ static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uin
     uint32_t *osb = ctx->get<uint32_t>(nsw, words);
     ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
     uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
-    launch(ctx, th, k_rs_ghist, dim3(ntiles), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
+    launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 256u)), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
     const uint64_t *kin = keys;
     int cur = 0;
     for (int p = 0; p < passes; ++p) {

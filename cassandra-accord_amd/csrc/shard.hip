@@ -12,8 +12,11 @@
 //            PartialDeps.with folded over the shards (KeyDeps.with = linearUnion, primitives/KeyDeps.java:238-253).
 #include "prims.hpp"
 
+#include <vector>
+
 namespace acc {
 void keydeps_merge(acc_ctx *ctx, const acc_merge_in *in, acc_merge_view *view);
+void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *view);
 
 namespace sh {
 
@@ -42,7 +45,8 @@ __global__ __launch_bounds__(BLOCK) void k_sh_pack(uint32_t n, uint32_t world, u
                                                    const uint64_t *__restrict__ key_code, const uint64_t *__restrict__ kd_off,
                                                    const uint32_t *__restrict__ key_idx, const uint64_t *__restrict__ u_off,
                                                    const uint32_t *__restrict__ dep_txn, const uint64_t *__restrict__ arena_off,
-                                                   const int32_t *__restrict__ arena, const uint32_t *__restrict__ gidx,
+                                                   const int32_t *__restrict__ arena, const uint64_t *__restrict__ kd_key,
+                                                   const uint32_t *__restrict__ gidx,
                                                    const uint64_t *__restrict__ o_frag,
                                                    const uint64_t *__restrict__ o_key, const uint64_t *__restrict__ o_val,
                                                    const uint64_t *__restrict__ o_k2v, uint32_t *__restrict__ hdr,
@@ -59,7 +63,8 @@ __global__ __launch_bounds__(BLOCK) void k_sh_pack(uint32_t n, uint32_t world, u
     const uint64_t f = o_frag[i], ok = o_key[i], ov = o_val[i], oo = o_k2v[i];
     if (lane < 4) hdr[4 * f + lane] = lane == 0 ? tg : lane == 1 ? (uint32_t)nk : lane == 2 ? (uint32_t)nv : (uint32_t)no;
     const uint32_t kb = key_off[t];
-    for (uint64_t j = lane; j < nk; j += 64) keys[ok + j] = key_code[kb + key_idx[k0 + j]];
+    // kd_key (acc_keydeps_mixed / acc_partial_deps_batch): the KeyDeps keys as codes (a range txn's keys are not its own)
+    for (uint64_t j = lane; j < nk; j += 64) keys[ok + j] = kd_key ? kd_key[k0 + j] : key_code[kb + key_idx[k0 + j]];
     // the global map is increasing (a store's txns are a TxnId-ordered subsequence), so lists stay sorted
     for (uint64_t j = lane; j < nv; j += 64) vals[ov + j] = gidx ? gidx[dep_txn[v0 + j]] : dep_txn[v0 + j];
     for (uint64_t j = lane; j < no; j += 64) k2v[oo + j] = arena[a0 + j];
@@ -342,6 +347,85 @@ __global__ __launch_bounds__(BLOCK) void k_fuse_glb_sizes(uint32_t ng, Fuse f, u
     sz[i] = 2 * n2;
 }
 
+// ---- the RangeDeps half: a fragment per txn with a non-empty store RangeDeps = header (t, nr, nv, no), its ranges
+// as (start, end) codes, its TxnIds raw (msb, lsb, node: the home rank holds no other store's batch), its Java
+// rangesToTxnIds ints
+__global__ __launch_bounds__(BLOCK) void k_shr_sizes(uint32_t n, uint32_t world, uint32_t G, const uint32_t *__restrict__ gidx,
+                                                     const uint64_t *__restrict__ rd_off, const uint64_t *__restrict__ u_off,
+                                                     const uint64_t *__restrict__ arena_off, uint64_t *__restrict__ c_frag,
+                                                     uint64_t *__restrict__ c_rng, uint64_t *__restrict__ c_val,
+                                                     uint64_t *__restrict__ c_k2v)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t i = dm_index(gidx ? gidx[t] : t, world, G);
+    const uint64_t nr = rd_off[t + 1] - rd_off[t];   // RangeDeps.isEmpty <=> no ranges
+    c_frag[i] = nr ? 1 : 0;
+    c_rng[i] = nr;
+    c_val[i] = nr ? u_off[t + 1] - u_off[t] : 0;
+    c_k2v[i] = nr ? arena_off[t + 1] - arena_off[t] : 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_shr_pack(uint32_t n, uint32_t world, uint32_t G, acc_rangedeps_view v,
+                                                    const uint64_t *__restrict__ tm, const uint64_t *__restrict__ tl,
+                                                    const int32_t *__restrict__ tn, const uint32_t *__restrict__ gidx,
+                                                    const uint64_t *__restrict__ o_frag, const uint64_t *__restrict__ o_rng,
+                                                    const uint64_t *__restrict__ o_val, const uint64_t *__restrict__ o_k2v,
+                                                    uint32_t *__restrict__ hdr, uint64_t *__restrict__ rng,
+                                                    uint64_t *__restrict__ txn, int32_t *__restrict__ k2v)
+{
+    const uint32_t t = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (t >= n) return;
+    const uint64_t r0 = v.rd_off[t], nr = v.rd_off[t + 1] - r0;
+    if (nr == 0) return;
+    const uint32_t tg = gidx ? gidx[t] : t;
+    const uint32_t i = dm_index(tg, world, G);
+    const uint64_t v0 = v.u_off[t], nv = v.u_off[t + 1] - v0, a0 = v.arena_off[t], no = v.arena_off[t + 1] - a0;
+    const uint64_t f = o_frag[i], orr = o_rng[i], ov = o_val[i], oo = o_k2v[i];
+    if (lane < 4) hdr[4 * f + lane] = lane == 0 ? tg : lane == 1 ? (uint32_t)nr : lane == 2 ? (uint32_t)nv : (uint32_t)no;
+    for (uint64_t j = lane; j < nr; j += 64) {
+        const uint32_t id = v.range_id[r0 + j];
+        rng[2 * (orr + j)] = v.rng_start[id];
+        rng[2 * (orr + j) + 1] = v.rng_end[id];
+    }
+    for (uint64_t j = lane; j < nv; j += 64) {
+        const uint32_t d = v.dep_txn[v0 + j];
+        txn[3 * (ov + j)] = tm[d];
+        txn[3 * (ov + j) + 1] = tl[d];
+        txn[3 * (ov + j) + 2] = (uint64_t)(uint32_t)tn[d];
+    }
+    for (uint64_t j = lane; j < no; j += 64) k2v[oo + j] = v.arena[a0 + j];
+}
+
+// one wave per reply: its ranges, raw TxnIds and ints from the received streams into the Deps.merge input layout
+__global__ __launch_bounds__(BLOCK) void k_shr_gather(uint64_t F, const uint32_t *__restrict__ perm,
+                                                      const uint64_t *__restrict__ sk, const uint64_t *__restrict__ sv,
+                                                      const uint64_t *__restrict__ so, const uint64_t *__restrict__ rk,
+                                                      const uint64_t *__restrict__ rv, const uint64_t *__restrict__ ro,
+                                                      const uint64_t *__restrict__ rng, const uint64_t *__restrict__ txn,
+                                                      const int32_t *__restrict__ k2v, uint64_t *__restrict__ ka,
+                                                      uint64_t *__restrict__ kb, uint64_t *__restrict__ msb,
+                                                      uint64_t *__restrict__ lsb, int32_t *__restrict__ node,
+                                                      int32_t *__restrict__ m_k2v)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    if (r >= F) return;
+    const uint32_t f = perm[r];
+    const uint64_t nk = rk[r + 1] - rk[r], nv = rv[r + 1] - rv[r], no = ro[r + 1] - ro[r];
+    for (uint64_t j = lane; j < nk; j += 64) {
+        ka[rk[r] + j] = rng[2 * (sk[f] + j)];
+        kb[rk[r] + j] = rng[2 * (sk[f] + j) + 1];
+    }
+    for (uint64_t j = lane; j < nv; j += 64) {
+        const uint64_t x = 3 * (sv[f] + j);
+        msb[rv[r] + j] = txn[x];
+        lsb[rv[r] + j] = txn[x + 1];
+        node[rv[r] + j] = (int32_t)(uint32_t)txn[x + 2];
+    }
+    for (uint64_t j = lane; j < no; j += 64) m_k2v[ro[r] + j] = k2v[so[f] + j];
+}
+
 }  // namespace sh
 
 using namespace sh;
@@ -420,7 +504,7 @@ void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, boo
         k2v = ctx->get<int32_t>("sh_k2v", NO);
     }
     launch(ctx, "sh_pack", k_sh_pack, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, world, G, key_off, key_code, v.kd_off,
-           v.key_idx, v.u_off, v.dep_txn, v.arena_off, v.arena, gidx, (const uint64_t *)o[0], (const uint64_t *)o[1],
+           v.key_idx, v.u_off, v.dep_txn, v.arena_off, v.arena, v.kd_key, gidx, (const uint64_t *)o[0], (const uint64_t *)o[1],
            (const uint64_t *)o[2], (const uint64_t *)o[3], hdr, keys, vals, k2v);
     if (out->mem == ACC_MEM_HOST) {
         if (F) ACC_HIP(hipMemcpyAsync(out->hdr, hdr, 16 * F, hipMemcpyDeviceToHost, st));
@@ -542,4 +626,110 @@ void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view)
     ctx->merge_valid = true;
 }
 
+
+// The RangeDeps fragments of the last acc_rangedeps_batch / acc_partial_deps_batch on ctx for the txns' home ranks, in
+// four destination-major context-owned streams (header, ranges, raw TxnIds, ints); off[q] = host [world+1] element
+// offsets.
+void range_pack(acc_ctx *ctx, const acc_range_batch_in *in, const uint32_t *txn_global, uint32_t world, uint32_t n_global,
+                void *send[4], std::vector<uint64_t> off[4])
+{
+    if (!in) fail(ACC_E_ARG, "null argument");
+    if (!ctx->rd_valid) fail(ACC_E_STATE, "no rangedeps result on this context");
+    const acc_rangedeps_view &v = ctx->rd_view;
+    const uint32_t n = v.n_txn;
+    if (in->n_txn != n) fail(ACC_E_ARG, "batch does not match the last rangedeps result");
+    hipStream_t st = ctx->stream;
+    const uint64_t *tm = stage_in(ctx, "shr_in_tm", in->txn_id.msb, n, in->mem);
+    const uint64_t *tl = stage_in(ctx, "shr_in_tl", in->txn_id.lsb, n, in->mem);
+    const int32_t *tn = stage_in(ctx, "shr_in_tn", in->txn_id.node, n, in->mem);
+    const uint32_t *gidx = txn_global ? stage_in(ctx, "shr_gidx", txn_global, n, in->mem) : nullptr;
+    if (!txn_global) n_global = std::max(n_global, n);
+    const uint32_t G = (n_global + world - 1) / world;
+    const size_t M = (size_t)world * G;
+    uint64_t *c[4], *o[4];
+    const char *cn[4] = { "shr_c_frag", "shr_c_rng", "shr_c_val", "shr_c_k2v" };
+    const char *on[4] = { "shr_o_frag", "shr_o_rng", "shr_o_val", "shr_o_k2v" };
+    for (int q = 0; q < 4; ++q) {
+        c[q] = ctx->get<uint64_t>(cn[q], M);
+        o[q] = ctx->get<uint64_t>(on[q], M + 1);
+        ACC_HIP(hipMemsetAsync(c[q], 0, M * sizeof(uint64_t), st));
+    }
+    launch(ctx, "shr_sizes", k_shr_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, world, G, gidx, v.rd_off, v.u_off,
+           v.arena_off, c[0], c[1], c[2], c[3]);
+    for (int q = 0; q < 4; ++q) scan<uint64_t, OpAdd<uint64_t>>(ctx, c[q], o[q], M, true, o[q] + M);
+    uint64_t *bounds = ctx->get<uint64_t>("shr_bounds", 4 * ((size_t)world + 1));
+    for (int q = 0; q < 4; ++q)
+        for (uint32_t d = 0; d <= world; ++d)
+            ACC_HIP(hipMemcpyAsync(bounds + q * (world + 1) + d, o[q] + std::min((size_t)d * G, M), 8,
+                                   hipMemcpyDeviceToDevice, st));
+    std::vector<uint64_t> hb(4 * ((size_t)world + 1));
+    ACC_HIP(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    for (int q = 0; q < 4; ++q) off[q].assign(hb.begin() + q * (world + 1), hb.begin() + (q + 1) * (world + 1));
+    const uint64_t F = off[0][world], NR = off[1][world], NV = off[2][world], NO = off[3][world];
+    uint32_t *hdr = ctx->get<uint32_t>("shr_s_hdr", 4 * F);
+    uint64_t *rng = ctx->get<uint64_t>("shr_s_rng", 2 * NR);
+    uint64_t *txn = ctx->get<uint64_t>("shr_s_txn", 3 * NV);
+    int32_t *k2v = ctx->get<int32_t>("shr_s_k2v", NO);
+    launch(ctx, "shr_pack", k_shr_pack, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, world, G, v, tm, tl, tn, gidx,
+           (const uint64_t *)o[0], (const uint64_t *)o[1], (const uint64_t *)o[2], (const uint64_t *)o[3], hdr, rng, txn, k2v);
+    send[0] = hdr; send[1] = rng; send[2] = txn; send[3] = k2v;
+}
+
+// What the home rank received of the RangeDeps half (streams source-major, per-source element counts): the fragments
+// grouped by home txn in source (= store) order, RangeDeps.with folded over them = the batched Deps.merge of the range
+// half over raw TxnIds (depsmerge.hip; RelationMultiMap.linearUnion over Range::compare, primitives/RangeDeps.java:
+// 567-582). Group g = home txn rank + g * world.
+void range_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_global, const std::vector<uint64_t> n_src[4],
+                 void *const recv[4], acc_deps_merge_view *view)
+{
+    NsScope scope(ctx, "prr.");
+    hipStream_t st = ctx->stream;
+    const uint32_t n_groups = n_global > rank ? (n_global - rank + world - 1) / world : 0;
+    uint64_t F = 0;
+    for (uint32_t s = 0; s < world; ++s) F += n_src[0][s];
+    const uint32_t *hdr = static_cast<const uint32_t *>(recv[0]);
+    uint64_t *f_key = ctx->get<uint64_t>("f_key", F), *f_val = ctx->get<uint64_t>("f_val", F);
+    uint64_t *f_k2v = ctx->get<uint64_t>("f_k2v", F), *gkey = ctx->get<uint64_t>("gkey", F);
+    uint64_t *err = ctx->get<uint64_t>("err", 1);
+    ACC_HIP(hipMemsetAsync(err, 0, 8, st));
+    launch(ctx, "shr_frag", k_sh_frag, dim3(grid_for(F, BLOCK)), dim3(BLOCK), 0, F, world, n_groups, hdr, f_key, f_val, f_k2v,
+           gkey, err);
+    uint64_t *sk = ctx->get<uint64_t>("sk", F + 1), *sv = ctx->get<uint64_t>("sv", F + 1), *so = ctx->get<uint64_t>("so", F + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, f_key, sk, F, true, sk + F);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, f_val, sv, F, true, sv + F);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, f_k2v, so, F, true, so + F);
+    Sorted fs = radix_sort(ctx, "rs", gkey, nullptr, F, bits_for(n_groups ? n_groups - 1 : 0));
+    uint64_t *r_key = ctx->get<uint64_t>("r_key", F), *r_val = ctx->get<uint64_t>("r_val", F), *r_k2v = ctx->get<uint64_t>("r_k2v", F);
+    launch(ctx, "shr_reply_sizes", k_sh_reply_sizes, dim3(grid_for(F, BLOCK)), dim3(BLOCK), 0, F, (const uint32_t *)fs.vals,
+           (const uint64_t *)f_key, (const uint64_t *)f_val, (const uint64_t *)f_k2v, r_key, r_val, r_k2v);
+    uint64_t *rk = ctx->get<uint64_t>("rk", F + 1), *rv = ctx->get<uint64_t>("rv", F + 1), *ro = ctx->get<uint64_t>("ro", F + 1);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, r_key, rk, F, true, rk + F);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, r_val, rv, F, true, rv + F);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, r_k2v, ro, F, true, ro + F);
+    uint64_t *gcnt = ctx->get<uint64_t>("gcnt", (size_t)n_groups + 1), *grp_off = ctx->get<uint64_t>("grp_off", (size_t)n_groups + 1);
+    ACC_HIP(hipMemsetAsync(gcnt, 0, ((size_t)n_groups + 1) * 8, st));
+    launch(ctx, "shr_group_hist", k_sh_group_hist, dim3(grid_for(F, BLOCK)), dim3(BLOCK), 0, F, (const uint64_t *)gkey, gcnt);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, gcnt, grp_off, n_groups, true, grp_off + n_groups);
+    uint64_t NR = 0, NV = 0, NO = 0;
+    for (uint32_t s = 0; s < world; ++s) { NR += n_src[1][s]; NV += n_src[2][s]; NO += n_src[3][s]; }
+    uint64_t *ka = ctx->get<uint64_t>("ka", NR + 1), *kb = ctx->get<uint64_t>("kb", NR + 1);
+    uint64_t *msb = ctx->get<uint64_t>("msb", NV + 1), *lsb = ctx->get<uint64_t>("lsb", NV + 1);
+    int32_t *node = ctx->get<int32_t>("node", NV + 1), *mk2v = ctx->get<int32_t>("k2v", NO + 1);
+    launch(ctx, "shr_gather", k_shr_gather, dim3((unsigned)((F + WAVES - 1) / WAVES)), dim3(BLOCK), 0, F,
+           (const uint32_t *)fs.vals, (const uint64_t *)sk, (const uint64_t *)sv, (const uint64_t *)so, (const uint64_t *)rk,
+           (const uint64_t *)rv, (const uint64_t *)ro, static_cast<const uint64_t *>(recv[1]),
+           static_cast<const uint64_t *>(recv[2]), static_cast<const int32_t *>(recv[3]), ka, kb, msb, lsb, node, mk2v);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    if (ctx->pinned[0]) fail(ACC_E_ARG, "received a RangeDeps fragment for a txn that is not homed on this rank");
+    acc_rmm_in none{};
+    acc_rmm_in rh{ rk, ka, kb, rv, acc_ts_cols{ msb, lsb, node }, ro, mk2v };
+    acc_deps_merge_in dmi{ ACC_MEM_DEVICE, n_groups, F, grp_off, none, rh };
+    const bool kvalid = ctx->merge_valid;
+    const acc_merge_view kview = ctx->merge_view;
+    deps_merge(ctx, &dmi, view);
+    ctx->merge_view = kview;   // the KeyDeps half's view (shard_merge) stays the context's current merge view
+    ctx->merge_valid = kvalid;
+}
 }  // namespace acc

@@ -481,6 +481,16 @@ int  acc_comm_init_host(acc_ctx *ctx, uint32_t world, uint32_t rank, acc_alltoal
 void acc_comm_destroy(acc_comm *comm);
 int  acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
                       acc_merge_view *out_view);
+/* acc_partial_deps_reduce: PreAccept.reduce of a store's whole PartialDeps (messages/PreAccept.java:141-156;
+ * PartialDeps.with = KeyDeps.with + RangeDeps.with, primitives/PartialDeps.java:80-86) for the last
+ * acc_partial_deps_batch on ctx over `in` (the same mixed batch): the KeyDeps fragments (as acc_shard_reduce) and the
+ * RangeDeps fragments (ranges as (start, end) codes, TxnIds raw, rangesToTxnIds) of both halves in ONE size exchange
+ * and ONE grouped all-to-all(v); on the home rank the KeyDeps.with fold (key_view, as acc_shard_reduce) and the
+ * RangeDeps.with fold in store order (RangeDeps.java:567-582; the range half of range_view, raw TxnIds; its key half is
+ * absent). A range command is stored sliced to each store's ranges (impl/InMemoryCommandStore.java:739-761), so the
+ * result depends on the store split exactly as the reference's does. Collective over comm. */
+int  acc_partial_deps_reduce(acc_ctx *ctx, acc_comm *comm, const acc_range_batch_in *in, const uint32_t *txn_global,
+                             uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view);
 
 /* ---- Recovery scans: CommandsForKey.mapReduceFull over a batch of queries (SURVEY.md §8(f) N3 = A7) ----
  * The snapshot is an acc_batch_in (one CommandsForKey per key, as for acc_keydeps_batch) plus, per input pair j
@@ -574,7 +584,10 @@ int acc_latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view
  * Builder, Json.java:356-392) into the per-document Deps of `deps` (acc_rmm_view halves; copy with acc_rmm_copy_out).
  * Keys are datums (mael/Datum.java); their codes in `deps` are dense ranks of every datum of the batch in
  * Datum.compareTo order (hash first, COMPARE_BY_HASH), with the dictionary rank -> (Datum.Kind ordinal, null, value,
- * hash). LONG (integer literals) and HASH datums are supported; STRING / DOUBLE datums give ACC_E_ARG.
+ * hash). Every Datum.Kind: LONG and DOUBLE as Gson reads a number (nextLong, else nextDouble; the decimal conversion
+ * is Double.parseDouble's exactly rounded fast path, other literals give ACC_E_ARG), HASH, and STRING (ASCII text, JSON
+ * escapes resolved; two different texts with one hash and equal first 16 characters give ACC_E_ARG). DOUBLE egress is
+ * Double.toString (shortest round-trip digits, JDK >= 19), STRING egress Gson's HTML-safe escaping.
  * acc_deps_to_json: the inverse for any acc_rmm_view pair of this context whose key codes index such a dictionary
  * (e.g. a Deps.merge of ingested replies): Gson's compact DEPS_ADAPTER text per group, two-call sizing on need_bytes. */
 typedef struct acc_json_in {
@@ -590,8 +603,11 @@ typedef struct acc_json_deps_view {
     uint64_t n_dict;
     const uint8_t  *dict_kind;   /* Datum.Kind ordinal: STRING 0, LONG 1, DOUBLE 2, HASH 3 */
     const uint8_t  *dict_null;   /* value == null (the +Inf sentinel) */
-    const uint64_t *dict_value;  /* LONG: the long; HASH: the hash as u32 */
+    const uint64_t *dict_value;  /* LONG: the long; HASH: the hash as u32; DOUBLE: Double.doubleToLongBits;
+                                    STRING: byte offset of its text in dict_str */
     const int32_t  *dict_hash;   /* Datum.hash(value) */
+    const uint32_t *dict_len;    /* STRING: text length in bytes (ASCII); else 0 */
+    const uint8_t  *dict_str;    /* the STRING texts */
 } acc_json_deps_view;
 
 int acc_deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *out_view);
@@ -602,6 +618,8 @@ typedef struct acc_json_out_in {
     uint64_t n_dict;
     const uint8_t  *dict_kind, *dict_null;  /* device */
     const uint64_t *dict_value;
+    const uint32_t *dict_len;               /* device; STRING datums need both (as acc_json_deps_view) */
+    const uint8_t  *dict_str;
 } acc_json_out_in;
 
 typedef struct acc_json_out {
@@ -649,6 +667,9 @@ int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t
 int  acc_timing_count(acc_ctx *ctx);
 int  acc_timing_get(acc_ctx *ctx, int i, const char **name, double *total_ms, uint64_t *launches);
 void acc_timing_reset(acc_ctx *ctx);
+/* Restrict the per-kernel events to the launches whose tag is in the comma-separated list (NULL or "" = every launch).
+   Each timed launch adds two event records to the stream; a bench times its step with only the kernel it reports. */
+int  acc_timing_filter(acc_ctx *ctx, const char *tags_csv);
 
 /* ---- counters of the last call (e.g. "keydeps.path_replay", "keydeps.big_txns", "keydeps.big_entries") ---- */
 int acc_stats_count(acc_ctx *ctx);

@@ -127,24 +127,57 @@ def test_levelise_one_million(ctx):
     assert nl == nl2 and nl > 1000
 
 
-@pytest.mark.parametrize("env,n,max_deps", [
-    ({"ACC_LV_CH": "64"}, 2000, 300),      # LDS tier, 64-entry chunks: lists longer than a chunk read from HBM
-    ({"ACC_LV_CH": "256"}, 20000, 12),     # many rounds, rounds of > 2048 positions (foff from HBM)
-    ({"ACC_LV_WAVES": "1"}, 5000, 30),     # the persistent-wave walk at a size the LDS tier would take
-    ({}, 65535, 6),                        # largest LDS-tier graph (u16 levels and positions)
-    ({}, 65536, 6),                        # smallest persistent-wave graph
+@pytest.mark.parametrize("env,n,max_deps,tier", [
+    ({}, 2000, 300, 2),                                      # event-driven (Kahn) tier
+    ({}, 24576, 40, 2),                                      # largest Kahn-tier graph
+    ({}, 24577, 12, 1),                                      # smallest LDS-walk graph beyond it
+    ({"ACC_LV_WALK": "1", "ACC_LV_CH": "64"}, 2000, 300, 1),   # LDS walk, 64-entry chunks: long lists read from HBM
+    ({"ACC_LV_WALK": "1", "ACC_LV_CH": "256"}, 20000, 12, 1),  # many rounds, rounds of > 2048 positions
+    ({"ACC_LV_WAVES": "1"}, 5000, 30, 0),                    # the persistent-wave walk at a size the LDS tiers take
+    ({}, 65535, 6, 1),                                       # largest LDS-walk graph (u16 levels and positions)
+    ({}, 65536, 6, 0),                                       # smallest persistent-wave graph
 ])
-def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps):
+def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps, tier):
     import oracle
     from accord_amd.deps import levelise
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     off, dep, er = random_graph(np.random.RandomState(n + max_deps), n, max_deps)
     lv, order, nl = levelise(ctx, off, dep, er)
+    assert ctx.stats().get("levelise.lds_tier") == tier
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
     assert nl == nl2
+
+
+@pytest.mark.parametrize("walk", ["kahn", "lds"])
+def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
+    """A config-5-shaped merged graph (16,384 txns, deps on recent txns, hundreds of levels) through the event-driven
+    tier and the LDS walk: identical levels and order, equal to the oracle."""
+    import oracle
+    from accord_amd.deps import levelise
+    if walk == "lds":
+        monkeypatch.setenv("ACC_LV_WALK", "1")
+    rng = np.random.RandomState(55)
+    n = 16384
+    er = rng.permutation(n).astype(np.uint32)
+    pos = np.argsort(er)
+    deps = []
+    for t in range(n):
+        k = int(er[t])
+        lo = max(0, k - 400)
+        cand = pos[lo:k]
+        deps.append(np.sort(rng.choice(cand, size=min(len(cand), rng.randint(0, 120)), replace=False)) if len(cand) else
+                    np.zeros(0, np.int64))
+    off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
+    dep = np.concatenate(deps).astype(np.uint32)
+    lv, order, nl = levelise(ctx, off, dep, er)
+    assert ctx.stats().get("levelise.lds_tier") == (2 if walk == "kahn" else 1)
+    l2, o2, nl2 = oracle.levelise(off, dep, er)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+    assert nl == nl2 and nl > 100
 
 
 def test_levelise_dense_prefix_chain(ctx):
