@@ -1,11 +1,12 @@
-"""Generate the committed golden fixtures for BASELINE config 1 (10k txns x 4 keys, 1k uniform keys).
+"""Generate the committed golden fixtures: BASELINE config 1 (10k txns x 4 keys, 1k uniform keys), a config-4 scale
+model and a 20,000-txn sample of config 2.
 
 The reference Java cannot be built or run here (no JDK; Gradle needs network), and its own tests hold no
 literal vectors for this path. Expected outputs therefore come from the C restatement
 (oracle/accord_oracle.c), and this script refuses to write a fixture unless the independent canonical
 model (oracle/canonical.py) produces identical arrays for every txn.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [1|2|3|4|all]
 """
 import os
 import sys
@@ -59,9 +60,104 @@ def config4s():
     print(path, os.path.getsize(path), "bytes; edges", o.total_edges)
 
 
+C2_WINDOWS = [(k * 111_111, k * 111_111 + 2_000) for k in range(9)] + [(1_000_000 - 2_000, 1_000_000)]
+
+
+def txn_digest(keys, deps, k2v) -> bytes:
+    """16-byte digest of one txn's KeyDeps (keys as u64 codes, deps as u32 batch indices, keysToTxnIds as i32)"""
+    import hashlib
+    h = hashlib.blake2b(digest_size=16)
+    for a, dt in ((keys, np.uint64), (deps, np.uint32), (k2v, np.int32)):
+        a = np.ascontiguousarray(np.asarray(a).astype(dt))
+        h.update(np.int64(a.size).tobytes())
+        h.update(a.tobytes())
+    return h.digest()
+
+
+def batch_digest(b) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in sorted(b.arrays().items()):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()
+
+
+def config2():
+    """BASELINE config 2 (1M txns x 8 keys, zipf 0.99) on 20,000 query txns: the hottest (last) 2,000 and nine
+    2,000-txn windows spread over the batch, from the C restatement. The hot window holds ~2,300 deps per txn, so the
+    fixture keeps per-txn sizes and a 16-byte digest of each txn's arrays (full arrays for the spread windows), plus
+    the sha256 of the generated input so a changed generator is caught instead of silently compared."""
+    b = W.config("2")
+    txn, sizes, dig, full_k, full_d, full_a, full_t = [], [], [], [], [], [], []
+    for lo, hi in C2_WINDOWS:
+        o = oracle.keydeps_batch(b, query_lo=lo, query_hi=hi)
+        for t in range(lo, hi):
+            k, d, a = o.txn(t)
+            txn.append(t)
+            sizes.append((len(k), len(d), len(a)))
+            dig.append(np.frombuffer(txn_digest(k, d, a), np.uint8))
+            if hi != b.n_txn:
+                full_t.append(t); full_k.append(np.asarray(k, np.uint64)); full_d.append(np.asarray(d, np.uint32))
+                full_a.append(np.asarray(a, np.int32))
+        print("window", lo, hi, "edges", o.total_edges, flush=True)
+    off = lambda xs: np.concatenate([[0], np.cumsum([len(x) for x in xs])]).astype(np.uint64)  # noqa: E731
+    path = os.path.join(HERE, "config2_sample.npz")
+    np.savez_compressed(path, input_sha256=np.frombuffer(bytes.fromhex(batch_digest(b)), np.uint8),
+                        txn=np.array(txn, np.uint32), sizes=np.array(sizes, np.uint32), digest=np.stack(dig),
+                        full_txn=np.array(full_t, np.uint32), full_key_off=off(full_k), full_keys=np.concatenate(full_k),
+                        full_dep_off=off(full_d), full_deps=np.concatenate(full_d), full_k2v_off=off(full_a),
+                        full_k2v=np.concatenate(full_a))
+    print(path, os.path.getsize(path), "bytes;", len(txn), "txns")
+
+
+def sub_batch(b, keyset):
+    """Every txn of b, keys restricted to `keyset` (sorted unique codes)."""
+    keep = np.isin(b.key_code, keyset)
+    cnt = np.add.reduceat(keep.astype(np.int64), b.key_off[:-1].astype(np.int64))
+    cnt[np.diff(b.key_off.astype(np.int64)) == 0] = 0
+    off = np.zeros(b.n_txn + 1, np.uint32)
+    np.cumsum(cnt, out=off[1:])
+    return W.Batch(b.txn_msb, b.txn_lsb, b.txn_node, b.exe_msb, b.exe_lsb, b.exe_node, b.status, off, b.key_code[keep])
+
+
+C3_N = 12_500_000
+C3_SAMPLE = [(C3_N - 1_000, C3_N, 1), (7, C3_N, C3_N // 1_000)]
+
+
+def config3_batch(dist):
+    return W.keydeps_batch(C3_N, 8, 1 << 24, W.CONFIG_SEEDS["3z" if dist == "zipf" else "3u"], dist, 0.99,
+                           status_model="model")
+
+
+def config3():
+    """BASELINE config 3 (12.5M txns x 8 keys over 16M keys, zipf 0.99 and uniform) on 2,000 query txns each: the
+    1,000 latest (the uncommitted window, hottest outputs) and 1,000 strided over the batch, from the C restatement
+    over the sub-batch of the CommandsForKey those txns touch (KeyDeps of a txn depends only on its own keys' CFKs).
+    Per-txn sizes and digests, plus the input sha256."""
+    for dist in ("zipf", "uniform"):
+        b = config3_batch(dist)
+        ts = np.concatenate([np.arange(lo, hi, st) for lo, hi, st in C3_SAMPLE])
+        keys = np.unique(np.concatenate([b.key_code[int(b.key_off[t]):int(b.key_off[t + 1])] for t in ts]))
+        o = oracle.keydeps_batch(sub_batch(b, keys), queries=ts)
+        sizes, dig = [], []
+        for t in ts.tolist():
+            k, d, a = o.txn(t)
+            sizes.append((len(k), len(d), len(a)))
+            dig.append(np.frombuffer(txn_digest(k, d, a), np.uint8))
+        path = os.path.join(HERE, f"config3{dist[0]}_sample.npz")
+        np.savez_compressed(path, input_sha256=np.frombuffer(bytes.fromhex(batch_digest(b)), np.uint8),
+                            txn=ts.astype(np.uint32), sizes=np.array(sizes, np.uint32), digest=np.stack(dig))
+        print(path, os.path.getsize(path), "bytes;", len(ts), "txns; edges", o.total_edges, flush=True)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "4":
-        config4s()
-    else:
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("1", "all"):
         main()
+    if which in ("4", "all"):
         config4s()
+    if which in ("2", "all"):
+        config2()
+    if which in ("3", "all"):
+        config3()

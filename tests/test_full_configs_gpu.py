@@ -6,8 +6,12 @@ too slow for every query at these sizes).
   config 4: 10M range txns + 10M key txns x 4 keys (RangeDeps);
   config 5: 16,384 coordinated txns x 64 replies: KeyDeps.merge + levelisation, every array compared.
 
-The oracle samples run on a sub-batch that keeps every txn (TxnIds, statuses, executeAts) but only the keys of the sampled
-txns: a txn's KeyDeps depend only on the CommandsForKey of its own keys, so the sampled txns' results are unchanged."""
+The config-3 oracle samples are committed fixtures (tests/golden/make_golden.py), computed on a sub-batch that keeps
+every txn (TxnIds, statuses, executeAts) but only the keys of the sampled txns: a txn's KeyDeps depend only on the
+CommandsForKey of its own keys, so the sampled txns' results are unchanged."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -22,21 +26,6 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
-
-
-def keys_of(b, ts):
-    idx = np.concatenate([np.arange(int(b.key_off[t]), int(b.key_off[t + 1])) for t in ts])
-    return np.unique(b.key_code[idx])
-
-
-def sub_batch(b, keyset):
-    """Every txn of b, keys restricted to `keyset` (sorted unique codes)."""
-    keep = np.isin(b.key_code, keyset)
-    cnt = np.add.reduceat(keep.astype(np.int64), b.key_off[:-1].astype(np.int64))
-    cnt[np.diff(b.key_off.astype(np.int64)) == 0] = 0
-    off = np.zeros(b.n_txn + 1, np.uint32)
-    np.cumsum(cnt, out=off[1:])
-    return W.Batch(b.txn_msb, b.txn_lsb, b.txn_node, b.exe_msb, b.exe_lsb, b.exe_node, b.status, off, b.key_code[keep])
 
 
 def check_properties(g, b):
@@ -65,26 +54,24 @@ def check_properties(g, b):
     assert (ki < np.diff(b.key_off.astype(np.int64))[kown]).all()
 
 
-def compare_sample(g, b, ranges):
-    import oracle
-    ts = np.concatenate([np.arange(lo, hi, st) for lo, hi, st in ranges])
-    o = oracle.keydeps_batch(sub_batch(b, keys_of(b, ts)), queries=ts)
-    for t in ts.tolist():
-        for x, y, what in zip(g.txn(t), o.txn(t), ("keys", "txnIds", "keysToTxnIds")):
-            np.testing.assert_array_equal(x, y, err_msg=f"txn {t} {what}")
-
-
 @pytest.mark.parametrize("dist", ["zipf", "uniform"])
 def test_config3_full(ctx, dist):
-    """BASELINE config 3 on one GPU: 100M txn-key pairs. Oracle sample: the 150 latest txns (uncommitted window, the
-    hottest outputs) and 150 txns strided over the batch."""
-    n = 12_500_000
-    b = W.keydeps_batch(n, 8, 1 << 24, W.CONFIG_SEEDS["3z" if dist == "zipf" else "3u"], dist, 0.99, status_model="model")
+    """BASELINE config 3 on one GPU: 100M txn-key pairs. Oracle sample (committed fixture, tests/golden/make_golden.py
+    config3): the 1,000 latest txns (uncommitted window, the hottest outputs) and 1,000 txns strided over the batch,
+    each compared by size and digest of its three arrays."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import batch_digest, config3_batch, txn_digest
+    b = config3_batch(dist)
     assert b.n_pairs == 100_000_000
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"config3{dist[0]}_sample.npz"))
+    assert batch_digest(b) == bytes(fx["input_sha256"]).hex(), "config-3 generator changed"
     g = ctx.calculate_partial_deps(b)
     assert ctx.stats().get("keydeps.path_replay", 0) == 0
     check_properties(g, b)
-    compare_sample(g, b, [(n - 150, n, 1), (7, n, n // 150)])
+    for t, sz, dg in zip(fx["txn"].tolist(), fx["sizes"], fx["digest"]):
+        gk, gd, ga = g.txn(t)
+        assert (len(gk), len(gd), len(ga)) == tuple(int(x) for x in sz), f"txn {t} sizes"
+        assert txn_digest(gk, gd, ga) == bytes(dg), f"txn {t} digest"
 
 
 def test_config4_full(ctx):

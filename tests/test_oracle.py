@@ -167,3 +167,21 @@ def test_oracle_matches_canonical_inthash_keys():
     c = canonical.keydeps_batch(hb)
     for t in range(hb.n_txn):
         assert same_txn(o, c, t), t
+
+
+def test_config2_fixture_reproduces():
+    """The committed config-2 sample (tests/golden/config2_sample.npz): the generator still yields the same 1M-txn batch,
+    and the oracle reproduces a spread window of it (the whole fixture takes ~2 min to regenerate)."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden import batch_digest, txn_digest
+    fx = np.load(os.path.join(HERE, "golden", "config2_sample.npz"))
+    b = W.config("2")
+    assert batch_digest(b) == bytes(fx["input_sha256"]).hex(), "generator drift"
+    assert len(fx["txn"]) >= 20_000
+    lo = 444_444
+    o = oracle.keydeps_batch(b, query_lo=lo, query_hi=lo + 200)
+    pos = {t: i for i, t in enumerate(fx["txn"].tolist())}
+    for t in range(lo, lo + 200):
+        k, d, a = o.txn(t)
+        assert txn_digest(k, d, a) == bytes(fx["digest"][pos[t]]), t
