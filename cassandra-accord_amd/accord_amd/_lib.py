@@ -41,7 +41,7 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_shard_pack", "acc_shard_merge", "acc_keydeps_merge", "acc_merge_copy_out", "acc_levelise",
            "acc_timing_count", "acc_timing_get", "acc_timing_reset", "acc_timing_filter", "acc_stats_count", "acc_stats_get",
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_partial_deps_reduce", "acc_shard_reduce",
-           "acc_map_reduce_full", "acc_latest_deps_merge", "acc_partial_deps_batch",
+           "acc_map_reduce_full", "acc_map_reduce_full_ranges", "acc_latest_deps_merge", "acc_partial_deps_batch",
            "acc_deps_from_json", "acc_deps_to_json",
            "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view"]
 
@@ -210,6 +210,23 @@ class RecoveryIn(C.Structure):
                 ("test_status", C.c_uint8), ("flags", C.c_uint8), ("test_kinds", C.c_int32)]
 
 
+ACC_RCMD_ERASED, ACC_RCMD_HAS_DEPS, ACC_RCMD_HISTORICAL = 1, 2, 4
+
+
+class RangeCmdsIn(C.Structure):
+    _fields_ = [("n_cmd", C.c_uint32), ("mem", C.c_uint32), ("end_inclusive", C.c_uint32), ("txn_id", TsCols),
+                ("execute_at", TsCols), ("status", C.c_void_p), ("flags", C.c_void_p), ("rng_off", C.c_void_p),
+                ("rng_start", C.c_void_p), ("rng_end", C.c_void_p), ("dep_off", C.c_void_p), ("dep_txn", TsCols),
+                ("dep_start", C.c_void_p), ("dep_end", C.c_void_p), ("dep_is_key", C.c_void_p)]
+
+
+class RecoveryRangesIn(C.Structure):
+    _fields_ = [("n_query", C.c_uint32), ("mem", C.c_uint32), ("test_txn", TsCols), ("part_is_range", C.c_void_p),
+                ("part_off", C.c_void_p), ("part_start", C.c_void_p), ("part_end", C.c_void_p),
+                ("started_at", C.c_uint8), ("test_dep", C.c_uint8), ("test_status", C.c_uint8), ("flags", C.c_uint8),
+                ("test_kinds", C.c_int32)]
+
+
 class LatestIn(C.Structure):
     _fields_ = [("n_groups", C.c_uint32), ("mode", C.c_uint32), ("grp_off", C.c_void_p), ("iv_off", C.c_void_p),
                 ("iv_start", C.c_void_p), ("iv_end", C.c_void_p), ("known", C.c_void_p), ("ballot", TsCols),
@@ -330,6 +347,9 @@ def load():
     L.acc_partial_deps_reduce.restype = C.c_int
     L.acc_map_reduce_full.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(RecoveryIn), C.POINTER(KeydepsView)]
     L.acc_map_reduce_full.restype = C.c_int
+    L.acc_map_reduce_full_ranges.argtypes = [C.c_void_p, C.POINTER(RangeCmdsIn), C.POINTER(RecoveryRangesIn),
+                                             C.POINTER(RangedepsView)]
+    L.acc_map_reduce_full_ranges.restype = C.c_int
     L.acc_latest_deps_merge.argtypes = [C.c_void_p, C.POINTER(LatestIn), C.POINTER(LatestView)]
     L.acc_latest_deps_merge.restype = C.c_int
     L.acc_deps_from_json.argtypes = [C.c_void_p, C.POINTER(JsonIn), C.POINTER(JsonDepsView)]

@@ -214,6 +214,40 @@ class Context:
         self.check(self._lib.acc_map_reduce_full(self._h, C.byref(bi), C.byref(ri), C.byref(view)))
         return self.copy_out(view, None)
 
+    def map_reduce_full_ranges(self, cmds: dict, queries: dict, started_at: int, test_dep: int, test_status: int,
+                               test_kinds: int = -1, executes_after: bool = False) -> "BatchRangeDeps":
+        """The range-command half of SafeCommandStore.mapReduceFull: InMemorySafeStore.mapReduceRangesInternal
+        (impl/InMemoryCommandStore.java:883-1016) for a batch of recovery queries (acc_map_reduce_full_ranges).
+        cmds: the store's range-command table sorted by TxnId (txn_*, exe_*, status = Status ordinals, flags =
+        ACC_RCMD_*, rng_off/rng_start/rng_end, dep_off/dep_msb/dep_lsb/dep_node/dep_start/dep_end/dep_is_key =
+        each command's PartialDeps as (TxnId, participant) pairs sorted by TxnId, end_inclusive); queries: msb, lsb,
+        node, is_range, part_off, part_start, part_end (the sliced keys or ranges). Returns per query the Deps.Builder
+        RangeDeps (dep_txn = first table index of the TxnId)."""
+        def arr(src, k, dt):
+            return np.ascontiguousarray(np.asarray(src[k], dtype=dt))
+        c = {k: arr(cmds, k, dt) for k, dt in (("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32),
+                                               ("exe_msb", np.uint64), ("exe_lsb", np.uint64), ("exe_node", np.int32),
+                                               ("status", np.uint8), ("flags", np.uint8), ("rng_off", np.uint32),
+                                               ("rng_start", np.uint64), ("rng_end", np.uint64), ("dep_off", np.uint32),
+                                               ("dep_msb", np.uint64), ("dep_lsb", np.uint64), ("dep_node", np.int32),
+                                               ("dep_start", np.uint64), ("dep_end", np.uint64), ("dep_is_key", np.uint8))}
+        q = {k: arr(queries, k, dt) for k, dt in (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32),
+                                                  ("is_range", np.uint8), ("part_off", np.uint32),
+                                                  ("part_start", np.uint64), ("part_end", np.uint64))}
+        p = lambda d, k: d[k].ctypes.data  # noqa: E731
+        ci = L.RangeCmdsIn(len(c["txn_msb"]), L.ACC_MEM_HOST, int(cmds["end_inclusive"]),
+                           L.TsCols(p(c, "txn_msb"), p(c, "txn_lsb"), p(c, "txn_node")),
+                           L.TsCols(p(c, "exe_msb"), p(c, "exe_lsb"), p(c, "exe_node")), p(c, "status"), p(c, "flags"),
+                           p(c, "rng_off"), p(c, "rng_start"), p(c, "rng_end"), p(c, "dep_off"),
+                           L.TsCols(p(c, "dep_msb"), p(c, "dep_lsb"), p(c, "dep_node")), p(c, "dep_start"),
+                           p(c, "dep_end"), p(c, "dep_is_key"))
+        ri = L.RecoveryRangesIn(len(q["msb"]), L.ACC_MEM_HOST, L.TsCols(p(q, "msb"), p(q, "lsb"), p(q, "node")),
+                                p(q, "is_range"), p(q, "part_off"), p(q, "part_start"), p(q, "part_end"), started_at,
+                                test_dep, test_status, L.ACC_FULL_EXECUTES_AFTER if executes_after else 0, test_kinds)
+        view = L.RangedepsView()
+        self.check(self._lib.acc_map_reduce_full_ranges(self._h, C.byref(ci), C.byref(ri), C.byref(view)))
+        return self.copy_out_range(view)
+
     def partial_deps_batch_raw(self, batch_in: "L.RangeBatchIn"):
         kv, rv = L.KeydepsView(), L.RangedepsView()
         self.check(self._lib.acc_partial_deps_batch(self._h, C.byref(batch_in), C.byref(kv), C.byref(rv)))

@@ -15,6 +15,7 @@ void rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out);
 void rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out);
 void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q, acc_stab_view *out);
 void map_reduce_full(acc_ctx *ctx, const acc_batch_in *in, const acc_recovery_in *q, acc_keydeps_view *view);
+void map_reduce_full_ranges(acc_ctx *ctx, const acc_range_cmds_in *c, const acc_recovery_ranges_in *q, acc_rangedeps_view *view);
 void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *view);
 void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *view);
 void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
@@ -106,6 +107,16 @@ int acc_map_reduce_full(acc_ctx *ctx, const acc_batch_in *snapshot, const acc_re
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         acc::map_reduce_full(ctx, snapshot, q, out_view);
+    });
+}
+
+int acc_map_reduce_full_ranges(acc_ctx *ctx, const acc_range_cmds_in *cmds, const acc_recovery_ranges_in *q,
+                               acc_rangedeps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::map_reduce_full_ranges(ctx, cmds, q, out_view);
     });
 }
 

@@ -33,6 +33,7 @@
  *                          -> CommandsForKey.mapReduceFull            local/CommandsForKey.java:553-612
  *                          -> Deps.Builder                            primitives/Deps.java:46-96
  *                          for a batch of recovery queries against one CommandsForKey snapshot.
+ *   acc_map_reduce_full_ranges  the range-command half of the same scans  impl/InMemoryCommandStore.java:883-1016
  *   acc_latest_deps_merge  LatestDeps.mergeProposal / mergeCommit     primitives/LatestDeps.java:306-326
  *                          (Recover.java:295-355): the interval fold of the replies, then KeyDeps/RangeDeps.slice of
  *                          every selected deps object to its interval and the batched Deps.merge of the slices.
@@ -509,7 +510,8 @@ int  acc_partial_deps_reduce(acc_ctx *ctx, acc_comm *comm, const acc_range_batch
  * The result per query is the Deps.Builder KeyDeps of every (key, txnId) the map visited, in the acc_keydeps_view
  * layout (key_idx into the query's keys, dep_txn = batch indices); the boolean recovery predicates
  * (hasAcceptedOrCommittedStartedAfterWithoutWitnessing, hasStableExecutesAfterWithoutWitnessing) are
- * u_off[q+1] > u_off[q]. acc_keydeps_copy_out copies it. Range commands are not part of the snapshot. */
+ * u_off[q+1] > u_off[q]. acc_keydeps_copy_out copies it. The range commands' half of the same call is
+ * acc_map_reduce_full_ranges below. */
 #define ACC_STARTED_BEFORE 0
 #define ACC_STARTED_AFTER  1
 #define ACC_STARTED_ANY    2
@@ -535,6 +537,60 @@ typedef struct acc_recovery_in {
 } acc_recovery_in;
 
 int acc_map_reduce_full(acc_ctx *ctx, const acc_batch_in *snapshot, const acc_recovery_in *q, acc_keydeps_view *out_view);
+
+/* ---- Recovery scans, range-command half: InMemorySafeStore.mapReduceRangesInternal
+ * (impl/InMemoryCommandStore.java:883-1016), the second half of SafeCommandStore.mapReduceFull (:874-881) ----
+ * The store's range commands are a table of n_cmd entries sorted by TxnId (non-decreasing): the rangeCommands map (a
+ * TreeMap by TxnId) and, flagged ACC_RCMD_HISTORICAL, the historicalRangeCommands map (a TxnId may be in both). Entry c:
+ *   txn_id, execute_at  Command.executeAt() (executeAtOrTxnId where it is null; a historical entry: its TxnId)
+ *   status              Status ordinal (local/Status.java:47-86: NotDefined 0 .. Accepted 3, PreCommitted 4,
+ *                       Committed 5, Stable 6, PreApplied 7, Applied 8, Truncated 9, Invalidated 10)
+ *   flags               ACC_RCMD_ERASED: saveStatus >= Erased, never visited (:891-893); ACC_RCMD_HAS_DEPS:
+ *                       known().deps.hasProposedOrDecidedDeps() (Status.java:601-612); ACC_RCMD_HISTORICAL (:962-1004):
+ *                       visited only when test_status = ANY_STATUS and test_dep = ANY_DEPS, with executeAt = TxnId
+ *   ranges              [rng_off[c], rng_off[c+1]): sorted, non-overlapping, start < end, bound type end_inclusive
+ *   deps                its PartialDeps flattened to (TxnId, participant) pairs sorted by TxnId: dep_txn[dep_off[c] ..
+ *                       dep_off[c+1]), a KeyDeps entry with dep_is_key = 1 and its key in dep_start, a RangeDeps entry
+ *                       with its range [dep_start, dep_end). The WITH / WITHOUT test is Deps.intersects(testTxnId,
+ *                       the entry's ranges) (primitives/Deps.java:112-115, KeyDeps.java:266-285, RangeDeps.java:468-495)
+ * Query q = one (testTxnId, keysOrRanges.slice(slice)) call: participants [part_off[q], part_off[q+1]), keys
+ * (part_is_range[q] = 0: part_start sorted unique) or ranges (1: part_start / part_end sorted, non-overlapping). The
+ * call-wide tests are those of acc_recovery_in (started_at, test_dep, test_status, test_kinds, flags).
+ * Result per query: the RangeDeps of every (range of the command, TxnId) the map visited, built by Deps.Builder, as an
+ * acc_rangedeps_view with query q in place of txn q: the range dictionary is the distinct ranges of the table, dep_txn
+ * the first table index holding that TxnId. The boolean recovery predicates are u_off[q+1] > u_off[q]. Copy out with
+ * acc_rangedeps_copy_out; the view is valid until the next compute call. */
+#define ACC_RCMD_ERASED     1u
+#define ACC_RCMD_HAS_DEPS   2u
+#define ACC_RCMD_HISTORICAL 4u
+
+typedef struct acc_range_cmds_in {
+    uint32_t    n_cmd;
+    uint32_t    mem;             /* placement of every array below */
+    uint32_t    end_inclusive;   /* 1: Range.EndInclusive (s, e]; 0: Range.StartInclusive [s, e) */
+    acc_ts_cols txn_id, execute_at;
+    const uint8_t  *status, *flags;
+    const uint32_t *rng_off;     /* [n_cmd+1] */
+    const uint64_t *rng_start, *rng_end;
+    const uint32_t *dep_off;     /* [n_cmd+1] */
+    acc_ts_cols     dep_txn;
+    const uint64_t *dep_start, *dep_end;
+    const uint8_t  *dep_is_key;
+} acc_range_cmds_in;
+
+typedef struct acc_recovery_ranges_in {
+    uint32_t    n_query;
+    uint32_t    mem;
+    acc_ts_cols test_txn;        /* [n_query] */
+    const uint8_t  *part_is_range;   /* [n_query] */
+    const uint32_t *part_off;        /* [n_query+1] */
+    const uint64_t *part_start, *part_end;
+    uint8_t     started_at, test_dep, test_status, flags;
+    int32_t     test_kinds;
+} acc_recovery_ranges_in;
+
+int acc_map_reduce_full_ranges(acc_ctx *ctx, const acc_range_cmds_in *cmds, const acc_recovery_ranges_in *q,
+                               acc_rangedeps_view *out_view);
 
 /* ---- Recovery merge of LatestDeps replies ----
  * Group g = one recovering txn with replies [grp_off[g], grp_off[g+1]), each a LatestDeps (primitives/LatestDeps.java):

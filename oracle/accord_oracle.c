@@ -1180,3 +1180,188 @@ orc_keydeps_result *orc_map_reduce_full(uint32_t n,
     free(cfks); free(pidx); free(owner); free(B.id); free(B.ex);
     return R;
 }
+
+/* ------------------------------------------------------------------ recovery scan, range-command half */
+
+/* Status ordinals (local/Status.java:47-86) */
+enum { S_ACCEPTED = 3, S_PRECOMMITTED = 4, S_COMMITTED = 5, S_STABLE = 6, S_TRUNCATED = 9, S_MAX = 10 };
+enum { RC_ERASED = 1, RC_HAS_DEPS = 2, RC_HISTORICAL = 4 };
+
+typedef struct rr_table {
+    const batch *B;                 /* id = TxnId, ex = executeAt of each entry */
+    const uint8_t *status, *flags;
+    const uint32_t *rng_off; const uint64_t *rs, *re;
+    const uint32_t *dep_off; const ts *dep; const uint64_t *ds, *de; const uint8_t *dk;
+    int ei;
+} rr_table;
+
+/* Deps.intersects(X, ranges) (primitives/Deps.java:112-115): KeyDeps.intersects (KeyDeps.java:266-285) - a key of
+ * X's KeyDeps entries inside one of the ranges - or RangeDeps.intersects (RangeDeps.java:468-495) - a range of X's
+ * RangeDeps entries intersecting one of them; over the command's PartialDeps flattened to (TxnId, participant) pairs */
+static int rr_deps_intersects(const rr_table *T, uint32_t c, const ts *x)
+{
+    for (uint32_t j = T->dep_off[c]; j < T->dep_off[c + 1]; ++j) {
+        if (!ts_eq(&T->dep[j], x)) continue;
+        for (uint32_t r = T->rng_off[c]; r < T->rng_off[c + 1]; ++r) {
+            if (T->dk[j] ? range_contains(T->rs[r], T->re[r], T->ds[j], T->ei)
+                         : ranges_intersect(T->rs[r], T->re[r], T->ds[j], T->de[j]))
+                return 1;
+        }
+    }
+    return 0;
+}
+
+/* does range (s, e) intersect the sliced participants of the query (Routables.foldl(rangeCommand.ranges, sliced)) */
+static int rr_hits(uint64_t s, uint64_t e, int is_range, const uint64_t *ps, const uint64_t *pe, uint32_t p0, uint32_t p1, int ei)
+{
+    for (uint32_t u = p0; u < p1; ++u)
+        if (is_range ? ranges_intersect(s, e, ps[u], pe[u]) : range_contains(s, e, ps[u], ei)) return 1;
+    return 0;
+}
+
+typedef struct rr_item { int64_t rid, seq, c; ts ex; } rr_item;
+static int cmp_rr_item(int64_t a, int64_t b, const void *ctx)
+{
+    const rr_item *it = ctx;
+    if (it[a].rid != it[b].rid) return it[a].rid < it[b].rid ? -1 : 1;
+    return it[a].seq < it[b].seq ? -1 : it[a].seq > it[b].seq;
+}
+
+/* InMemorySafeStore.mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016) for each recovery query, into a
+ * Deps.Builder with the map functions of BeginRecovery (messages/BeginRecovery.java:334-378): every visited
+ * (range, TxnId) is added, or (exec_after) only those with executeAt > testTxnId. The table holds the rangeCommands
+ * entries and, flagged historical, the historicalRangeCommands entries, sorted by TxnId. */
+orc_rangedeps_result *orc_map_reduce_full_ranges(uint32_t n,
+                                                 const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                                 const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                                 const uint8_t *status, const uint8_t *flags,
+                                                 const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                                 int end_inclusive, const uint32_t *dep_off, const uint64_t *dmsb,
+                                                 const uint64_t *dlsb, const int32_t *dnode, const uint64_t *dep_start,
+                                                 const uint64_t *dep_end, const uint8_t *dep_is_key,
+                                                 uint32_t nq, const uint64_t *qmsb, const uint64_t *qlsb, const int32_t *qnode,
+                                                 const uint8_t *part_is_range, const uint32_t *part_off,
+                                                 const uint64_t *part_start, const uint64_t *part_end,
+                                                 int started_at, int test_dep, int test_status, int test_kinds, int exec_after)
+{
+    orc_rangedeps_result *R = calloc(1, sizeof *R);
+    err E = { 0, "" };
+    batch B = { n, malloc((n + 1) * sizeof(ts)), malloc((n + 1) * sizeof(ts)), NULL, NULL, NULL };
+    for (uint32_t i = 0; i < n; ++i) {
+        B.id[i] = (ts){ tmsb[i], tlsb[i], tnode[i] };
+        B.ex[i] = (ts){ emsb[i], elsb[i], enode[i] };
+        if (status[i] > S_MAX || (flags[i] & ~7u)) set_err(&E, -1, "invalid Status ordinal or flags");
+        if (i > 0 && ts_cmp(&B.id[i - 1], &B.id[i]) > 0) set_err(&E, -1, "the range-command table must be sorted by TxnId");
+    }
+    const uint64_t ND = n ? dep_off[n] : 0;
+    ts *dep = malloc((ND + 1) * sizeof *dep);
+    for (uint64_t j = 0; j < ND; ++j) dep[j] = (ts){ dmsb[j], dlsb[j], dnode[j] };
+    rr_table T = { &B, status, flags, rng_off, rng_start, rng_end, dep_off, dep, dep_start, dep_end, dep_is_key, end_inclusive };
+    /* first table index of each TxnId (the reported dependency) */
+    int64_t *first = malloc((n + 1) * sizeof *first);
+    for (uint32_t i = 0; i < n; ++i) first[i] = (i > 0 && ts_eq(&B.id[i - 1], &B.id[i])) ? first[i - 1] : (int64_t)i;
+    /* the distinct ranges of the table in Range::compare order */
+    const uint64_t NR = n ? rng_off[n] : 0;
+    int64_t *all = malloc((NR + 1) * sizeof *all);
+    for (uint64_t j = 0; j < NR; ++j) all[j] = (int64_t)j;
+    rng_dict D = { rng_start, rng_end };
+    stable_sort(all, NR, cmp_range, &D);
+    uint64_t *ds = malloc((NR + 1) * sizeof *ds), *de = malloc((NR + 1) * sizeof *de);
+    int64_t *rid_of = malloc((NR + 1) * sizeof *rid_of);
+    size_t nd = 0;
+    for (uint64_t q = 0; q < NR; ++q) {
+        uint64_t s = rng_start[all[q]], e = rng_end[all[q]];
+        if (nd == 0 || ds[nd - 1] != s || de[nd - 1] != e) { ds[nd] = s; de[nd] = e; ++nd; }
+        rid_of[all[q]] = (int64_t)nd - 1;
+    }
+    R->n_txn = nq; R->n_ranges = (uint32_t)nd; R->rng_start = ds; R->rng_end = de;
+    R->arena_off = calloc(nq + 1, sizeof(uint64_t));
+    R->rd_off = calloc(nq + 1, sizeof(uint64_t));
+    R->u_off = calloc(nq + 1, sizeof(uint64_t));
+    ivec arena = { 0 }, rids = { 0 }, deps = { 0 };
+    builder b; b_init(&b, &B);
+    rr_item *items = NULL; size_t items_cap = 0;
+    int64_t *order = NULL; size_t order_cap = 0;
+    int64_t *last = malloc((nd + 1) * sizeof *last);   /* per range: table index of its list's last TxnInfo */
+    for (uint32_t q = 0; q < nq && !E.code; ++q) {
+        R->arena_off[q] = arena.n; R->rd_off[q] = rids.n; R->u_off[q] = deps.n;
+        const ts x = { qmsb[q], qlsb[q], qnode[q] };
+        int kinds = test_kinds >= 0 ? test_kinds : kind_witnessed_by(ts_kind(&x));
+        if (kinds < 0) { set_err(&E, ts_kind(&x) == K_LOCAL ? -2 : -1, "Kind.witnessedBy(): unhandled kind"); break; }
+        const uint32_t p0 = part_off[q], p1 = part_off[q + 1];
+        const int isr = part_is_range[q];
+        for (size_t r = 0; r < nd; ++r) last[r] = -1;
+        size_t ni = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            /* pass 0: commandStore.rangeCommands.forEach (:888-960); pass 1: historicalRangeCommands (:962-1004) */
+            if (pass == 1 && !(test_status == 0 && test_dep == 2)) break;
+            for (uint32_t c = 0; c < n; ++c) {
+                const int hist = (flags[c] & RC_HISTORICAL) != 0;
+                if (hist != pass) continue;
+                const ts *id = &B.id[c];
+                if (!hist) {
+                    if (flags[c] & RC_ERASED) continue;                            /* saveStatus >= Erased */
+                    int skip = 0;
+                    switch (started_at) {
+                    case 1: skip = ts_cmp(id, &x) <= 0; break;                     /* STARTED_AFTER */
+                    case 0: if (ts_cmp(id, &x) >= 0) { skip = 1; break; }         /* STARTED_BEFORE ... */
+                        /* fall through */
+                    default: skip = test_dep != 2 && ts_cmp(&B.ex[c], &x) < 0;   /* ... and ANY */
+                    }
+                    if (skip) continue;
+                    const int st = status[c];
+                    if (test_status == 1 && !(st == S_PRECOMMITTED || st == S_COMMITTED || st == S_ACCEPTED)) continue;
+                    if (test_status == 2 && (st < S_STABLE || st >= S_TRUNCATED)) continue;
+                    if (!((kinds >> ts_kind(id)) & 1)) continue;
+                    if (test_dep != 2) {
+                        if (!(flags[c] & RC_HAS_DEPS)) continue;                   /* hasProposedOrDecidedDeps */
+                        if ((test_dep == 0) == !rr_deps_intersects(&T, c, &x)) continue;
+                    }
+                } else {
+                    if (started_at == 1 && ts_cmp(id, &x) <= 0) continue;
+                    if (started_at == 0 && ts_cmp(id, &x) >= 0) continue;
+                    if (!((kinds >> ts_kind(id)) & 1)) continue;
+                }
+                for (uint32_t j = rng_off[c]; j < rng_off[c + 1]; ++j) {
+                    if (!rr_hits(rng_start[j], rng_end[j], isr, part_start, part_end, p0, p1, end_inclusive)) continue;
+                    const int64_t rid = rid_of[j];
+                    /* list.isEmpty() || !list.get(last).txnId.equals(txnId) */
+                    if (last[rid] >= 0 && ts_eq(&B.id[last[rid]], id)) continue;
+                    last[rid] = c;
+                    if (ni == items_cap) { items_cap = items_cap ? 2 * items_cap : 64; items = realloc(items, items_cap * sizeof *items); }
+                    items[ni] = (rr_item){ rid, (int64_t)ni, c, hist ? *id : B.ex[c] };   /* TxnInfo.executeAt */
+                    ++ni;
+                }
+            }
+        }
+        /* TreeMap<Range, List<TxnInfo>> iteration: range order, each list in insertion order; the map */
+        if (ni > order_cap) { order_cap = ni; order = realloc(order, order_cap * sizeof *order); }
+        for (size_t u = 0; u < ni; ++u) order[u] = (int64_t)u;
+        stable_sort(order, ni, cmp_rr_item, items);
+        b_reset(&b);
+        for (size_t u = 0; u < ni; ++u) {
+            const rr_item *it = &items[order[u]];
+            if (exec_after && ts_cmp(&it->ex, &x) <= 0) continue;
+            b_add(&b, (uint64_t)it->rid, first[it->c]);
+        }
+        kdeps part; if (b_build(&b, &part, &E)) break;
+        for (size_t u = 0; u < part.nk2v; ++u) iv_push(&arena, part.k2v[u]);
+        for (size_t u = 0; u < part.nkeys; ++u) iv_push(&rids, (int64_t)part.keys[u]);
+        for (size_t u = 0; u < part.nvals; ++u) iv_push(&deps, part.vals[u]);
+        R->total_edges += part.nk2v - part.nkeys;
+        kd_free(&part);
+    }
+    R->arena_off[nq] = arena.n; R->rd_off[nq] = rids.n; R->u_off[nq] = deps.n;
+    R->arena = malloc((arena.n + 1) * sizeof(int32_t));
+    for (size_t u = 0; u < arena.n; ++u) R->arena[u] = (int32_t)arena.v[u];
+    R->range_id = malloc((rids.n + 1) * sizeof(uint32_t));
+    for (size_t u = 0; u < rids.n; ++u) R->range_id[u] = (uint32_t)rids.v[u];
+    R->dep_txn = malloc((deps.n + 1) * sizeof(uint32_t));
+    for (size_t u = 0; u < deps.n; ++u) R->dep_txn[u] = (uint32_t)deps.v[u];
+    R->error = E.code;
+    snprintf(R->message, sizeof R->message, "%s", E.msg);
+    b_free(&b);
+    free(items); free(order); free(last); free(arena.v); free(rids.v); free(deps.v); free(all); free(rid_of);
+    free(first); free(dep); free(B.id); free(B.ex);
+    return R;
+}

@@ -120,6 +120,22 @@ orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
                                           int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride);
 void orc_rangedeps_free(orc_rangedeps_result *r);
 
+/* InMemorySafeStore.mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016), the range-command half of the
+ * BeginRecovery scans, per query into a Deps.Builder; table and queries as acc_map_reduce_full_ranges
+ * (include/accord_amd.h). Results per query in the orc_rangedeps_result layout (dep_txn = first table index). */
+orc_rangedeps_result *orc_map_reduce_full_ranges(uint32_t n,
+                                                 const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                                 const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                                 const uint8_t *status, const uint8_t *flags,
+                                                 const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                                 int end_inclusive, const uint32_t *dep_off, const uint64_t *dmsb,
+                                                 const uint64_t *dlsb, const int32_t *dnode, const uint64_t *dep_start,
+                                                 const uint64_t *dep_end, const uint8_t *dep_is_key,
+                                                 uint32_t nq, const uint64_t *qmsb, const uint64_t *qlsb, const int32_t *qnode,
+                                                 const uint8_t *part_is_range, const uint32_t *part_off,
+                                                 const uint64_t *part_start, const uint64_t *part_end,
+                                                 int started_at, int test_dep, int test_status, int test_kinds, int exec_after);
+
 /* ---- accord_oracle_rmm.c: RelationMultiMap operations on whole deps objects over raw values ---- */
 
 /* KeyDeps.merge / RangeDeps.merge (LinearMerger fold of linearUnion) per group of replies with raw TxnId columns;

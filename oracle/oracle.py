@@ -108,6 +108,10 @@ def lib():
         L.orc_rmm_stab.restype = C.POINTER(StabResult)
         L.orc_rmm_stab.argtypes = [C.c_uint32, u32p, u64p, u64p, C.c_int, C.c_int, u64p, u64p, u64p]
         L.orc_stab_free.argtypes = [C.POINTER(StabResult)]
+        L.orc_map_reduce_full_ranges.restype = C.POINTER(RangedepsResult)
+        L.orc_map_reduce_full_ranges.argtypes = ([C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u8p, u32p, u64p, u64p,
+                                                  C.c_int, u32p, u64p, u64p, i32p, u64p, u64p, u8p, C.c_uint32, u64p, u64p,
+                                                  i32p, u8p, u32p, u64p, u64p] + [C.c_int] * 5)
         L.orc_map_reduce_full.restype = C.POINTER(KeydepsResult)
         L.orc_map_reduce_full.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u32p,
                                           C.c_uint32, u64p, u64p, i32p, u32p, u64p,
@@ -279,6 +283,10 @@ def rangedeps_batch(rb, query_lo: int = 0, query_hi: int | None = None, query_st
     types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u64p, u64p]
     r = L.orc_rangedeps_batch(n, *[_p(a, t) for a, t in zip(arrs, types)], int(rb.end_inclusive), query_lo,
                               n if query_hi is None else query_hi, query_stride)
+    return _rangedeps_out(L, r, n)
+
+
+def _rangedeps_out(L, r, n) -> RangeDepsBatchOut:
     try:
         R = r.contents
         if R.error:
@@ -297,6 +305,35 @@ def rangedeps_batch(rb, query_lo: int = 0, query_hi: int | None = None, query_st
     finally:
         L.orc_rangedeps_free(r)
     return out
+
+
+RCMD_FIELDS = (("txn_msb", np.uint64), ("txn_lsb", np.uint64), ("txn_node", np.int32), ("exe_msb", np.uint64),
+               ("exe_lsb", np.uint64), ("exe_node", np.int32), ("status", np.uint8), ("flags", np.uint8),
+               ("rng_off", np.uint32), ("rng_start", np.uint64), ("rng_end", np.uint64))
+RCMD_DEP_FIELDS = (("dep_off", np.uint32), ("dep_msb", np.uint64), ("dep_lsb", np.uint64), ("dep_node", np.int32),
+                   ("dep_start", np.uint64), ("dep_end", np.uint64), ("dep_is_key", np.uint8))
+RQ_FIELDS = (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("is_range", np.uint8), ("part_off", np.uint32),
+             ("part_start", np.uint64), ("part_end", np.uint64))
+_CT = {np.uint64: u64p, np.uint32: u32p, np.int32: i32p, np.uint8: u8p}
+
+
+def map_reduce_full_ranges(cmds: dict, queries: dict, started_at: int, test_dep: int, test_status: int,
+                           test_kinds: int = -1, exec_after: bool = False) -> RangeDepsBatchOut:
+    """orc_map_reduce_full_ranges: InMemorySafeStore.mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016)
+    per recovery query into a Deps.Builder (BeginRecovery.java:334-378). cmds / queries: dicts of the RCMD_FIELDS /
+    RCMD_DEP_FIELDS / RQ_FIELDS arrays plus cmds["end_inclusive"]; results per query in the rangedeps layout."""
+    L = lib()
+    n = len(cmds["txn_msb"])
+    nq = len(queries["msb"])
+    pad = lambda k, dt, src: np.ascontiguousarray(np.append(np.asarray(src[k], dt), dt(0)))  # noqa: E731
+    a1 = [pad(k, dt, cmds) for k, dt in RCMD_FIELDS]
+    a2 = [pad(k, dt, cmds) for k, dt in RCMD_DEP_FIELDS]
+    aq = [pad(k, dt, queries) for k, dt in RQ_FIELDS]
+    r = L.orc_map_reduce_full_ranges(n, *[_p(a, _CT[dt]) for a, (_, dt) in zip(a1, RCMD_FIELDS)], int(cmds["end_inclusive"]),
+                                     *[_p(a, _CT[dt]) for a, (_, dt) in zip(a2, RCMD_DEP_FIELDS)], nq,
+                                     *[_p(a, _CT[dt]) for a, (_, dt) in zip(aq, RQ_FIELDS)],
+                                     started_at, test_dep, test_status, test_kinds, int(exec_after))
+    return _rangedeps_out(L, r, nq)
 
 
 def keydeps_merge(m: dict) -> dict:

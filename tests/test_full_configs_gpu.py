@@ -63,7 +63,7 @@ def test_config3_full(ctx, dist):
     from make_golden import batch_digest, config3_batch, txn_digest
     b = config3_batch(dist)
     assert b.n_pairs == 100_000_000
-    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"config3{dist[0]}_sample.npz"))
+    fx = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"config3{dist[0]}_sample.npz")))
     assert batch_digest(b) == bytes(fx["input_sha256"]).hex(), "config-3 generator changed"
     g = ctx.calculate_partial_deps(b)
     assert ctx.stats().get("keydeps.path_replay", 0) == 0

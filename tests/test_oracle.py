@@ -175,7 +175,7 @@ def test_config2_fixture_reproduces():
     import sys
     sys.path.insert(0, os.path.join(HERE, "golden"))
     from make_golden import batch_digest, txn_digest
-    fx = np.load(os.path.join(HERE, "golden", "config2_sample.npz"))
+    fx = dict(np.load(os.path.join(HERE, "golden", "config2_sample.npz")))   # decompress each array once
     b = W.config("2")
     assert batch_digest(b) == bytes(fx["input_sha256"]).hex(), "generator drift"
     assert len(fx["txn"]) >= 20_000

@@ -1,6 +1,8 @@
 """CPU: the C restatement of CommandsForKey.mapReduceFull (oracle/accord_oracle.c orc_map_reduce_full,
 local/CommandsForKey.java:553-612) against the independent set model (oracle/canonical.py map_reduce_full) for every
-TestStartedAt x TestDep x TestStatus combination, explicit Kinds masks and the executeAt > testTxnId map filter."""
+TestStartedAt x TestDep x TestStatus combination, explicit Kinds masks and the executeAt > testTxnId map filter; and the
+range-command half (orc_map_reduce_full_ranges, impl/InMemoryCommandStore.java:883-1016) against answers worked out by
+hand plus its invariants on random tables."""
 import pytest
 
 import canonical
@@ -58,3 +60,28 @@ def test_oracle_errors():
     q2["lsb"][0] = (int(q2["lsb"][0]) & ~0xE & (2**64 - 1)) | (5 << 1)   # LocalOnly testTxnId: witnessedBy() throws
     with pytest.raises(oracle.OracleError):
         oracle.map_reduce_full(b, mo, mt, q2, 0, 1, 1)
+
+
+# ---- the range-command half (orc_map_reduce_full_ranges, impl/InMemoryCommandStore.java:883-1016)
+def test_handmade_answers():
+    cmds, q, expected = RC.range_recovery_handmade()
+    for (sa, td, ts, ea), want in expected.items():
+        got = RC.rangedeps_as_dict(oracle.map_reduce_full_ranges(cmds, q, sa, td, ts, exec_after=ea), 0)
+        assert got == want, ((sa, td, ts, ea), got, want)
+
+
+def test_random_tables_invariants():
+    """Per query: ranges ascending, TxnIds ascending and unique, every entry indexes them; the executeAt filter only
+    removes entries; WITH and WITHOUT partition the entries ANY_DEPS leaves (for non-historical, deps-known commands)."""
+    cmds, q = RC.range_recovery_case(4, n_cmd=200, n_query=60)
+    for sa, td, ts in RC.ALL_TESTS:
+        full = oracle.map_reduce_full_ranges(cmds, q, sa, td, ts)
+        filt = oracle.map_reduce_full_ranges(cmds, q, sa, td, ts, exec_after=True)
+        for i in range(len(q["msb"])):
+            a, b = RC.rangedeps_as_dict(full, i), RC.rangedeps_as_dict(filt, i)
+            keys = list(a)
+            assert keys == sorted(keys)
+            for r, ds in a.items():
+                assert ds == sorted(set(ds))
+            for r, ds in b.items():
+                assert set(ds) <= set(a.get(r, []))
