@@ -365,142 +365,6 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     if (lane == 0 && my_max) atomicMax(max_level, my_max);
 }
 
-// ---- event-driven tier (n <= LV_KAHN_MAX): Kahn's algorithm in one workgroup's LDS. Every txn holds one LDS word
-// (level << 16 | waiting deps left); finishing txn i CASes each successor's word (level = max(level, L(i) + 1), one dep
-// fewer), and the worker that takes a successor's count to zero continues with that successor itself (further ones go
-// to an LDS ready queue). A dependency hop is an LDS CAS plus the successor list's load, with no polling of pending
-// deps and no round barriers; the successor lists are the filtered graph transposed (RelationMultiMap.invert's
-// counting sort, utils/RelationMultiMap.java:907-938) in exec-order positions. Deps: Commands.java:776-830 (a txn
-// waits on the deps with an earlier executeAt).
-constexpr uint32_t LV_KAHN_MAX = 24576;   // LDS words (4 B) + queue (2 B) per txn
-constexpr uint32_t LV_QEMPTY = 0xFFFFu;
-
-// successor counts of the filtered graph (wave per exec-order position; sizes on the device)
-__global__ __launch_bounds__(BLOCK) void k_lv_scount(uint32_t n, const uint32_t *__restrict__ foff, const uint16_t *__restrict__ fdep,
-                                                     uint32_t *__restrict__ scnt)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= n) return;
-    for (uint32_t e = foff[i] + lane; e < foff[i + 1]; e += 64) atomicAdd(&scnt[fdep[e]], 1u);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_lv_sfill(uint32_t n, const uint32_t *__restrict__ foff, const uint16_t *__restrict__ fdep,
-                                                    const uint32_t *__restrict__ soff, uint32_t *__restrict__ scur,
-                                                    uint16_t *__restrict__ succ)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= n) return;
-    for (uint32_t e = foff[i] + lane; e < foff[i + 1]; e += 64) {
-        const uint32_t p = fdep[e];
-        succ[soff[p] + atomicAdd(&scur[p], 1u)] = (uint16_t)i;
-    }
-}
-
-constexpr int LV_KG = 16;   // lanes per worker
-
-__global__ __launch_bounds__(LV_NT) void k_lv_kahn(uint32_t n, const uint32_t *__restrict__ foff, const uint32_t *__restrict__ soff,
-                                                   const uint16_t *__restrict__ succ, const uint32_t *__restrict__ order_exec,
-                                                   uint32_t *__restrict__ level, uint32_t *__restrict__ max_level)
-{
-    __shared__ uint32_t W[LV_KAHN_MAX];
-    __shared__ uint16_t Q[LV_KAHN_MAX];
-    __shared__ uint32_t s_head, s_tail, s_done, s_red[LV_NT / 64];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (LV_KG - 1), g0 = lane & ~(LV_KG - 1u);
-    const uint64_t gmask = ((1ull << LV_KG) - 1) << g0;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    // waiting-dep counts; the txns with none start the queue, in exec order
-    if (tid == 0) { s_head = 0; s_done = 0; }
-    for (uint32_t i = tid; i < n; i += LV_NT) { W[i] = foff[i + 1] - foff[i]; Q[i] = (uint16_t)LV_QEMPTY; }
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += LV_NT) {
-        const uint32_t i = c0 + tid;
-        const bool z = i < n && W[i] == 0;
-        uint32_t tot;
-        const uint32_t pre = block_exclusive<uint32_t, OpAdd<uint32_t>, LV_NT / 64>(z ? 1u : 0u, OpAdd<uint32_t>(), s_red, tot);
-        if (z) Q[base + pre] = (uint16_t)i;
-        base += tot;
-    }
-    if (tid == 0) s_tail = base;
-    __syncthreads();
-    uint32_t my_max = 0;
-    // Per worker (group-uniform) state machine, one step per loop iteration for every group of the wave: the loop's
-    // control flow stays wave-uniform, so no group spins while another group of its wave (which it may wait on) is
-    // masked off. idle: take a queue slot; wait: poll the slot; run: CAS the next LV_KG successors of txn cur.
-    enum : uint32_t { IDLE = 0, WAIT = 1, RUN = 2, FIN = 3 };
-    uint32_t st = IDLE, idx = 0, cur = 0, L = 0, e0 = 0, eb = 0;
-    int next = -1;
-    uint32_t next_l = 0;
-    auto start = [&](uint32_t i, uint32_t li) {   // group-uniform: txn i's level is final
-        cur = i; L = li; st = RUN;
-        e0 = soff[i]; eb = soff[i + 1];
-        next = -1;
-        if (sub == 0) {
-            level[order_exec[i]] = li;
-            atomicAdd(&s_done, 1u);
-        }
-        my_max = max(my_max, li);
-    };
-    while (true) {
-        if (st == IDLE) {
-            uint32_t x = 0;
-            if (sub == 0) x = atomicAdd(&s_head, 1u);
-            idx = (uint32_t)__shfl((int)x, (int)g0, 64);
-            st = idx < n ? WAIT : FIN;
-        }
-        if (st == WAIT) {
-            const uint32_t q = *(volatile uint16_t *)&Q[idx];
-            if (q != LV_QEMPTY) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                start(q, __hip_atomic_load(&W[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16);
-            }
-            else if (*(volatile uint32_t *)&s_done >= n) st = FIN;   // every txn is done: this slot stays unused
-        }
-        bool ready = false;
-        uint32_t s = 0, nl = 0;
-        if (st == RUN) {
-            const uint32_t e = e0 + sub;
-            if (e < eb) {
-                s = succ[e];
-                uint32_t old = W[s], nw;
-                do {
-                    nw = (max(old >> 16, L + 1) << 16) | ((old & 0xFFFFu) - 1u);
-                } while (!__hip_atomic_compare_exchange_strong(&W[s], &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_WORKGROUP));
-                ready = (nw & 0xFFFFu) == 0;
-                nl = nw >> 16;
-            }
-        }
-        uint64_t rb = __ballot(ready) & gmask;
-        if (st == RUN) {
-            if (rb && next < 0) {   // the first successor made ready is this worker's next txn
-                const int src = __builtin_ctzll(rb);
-                next = __shfl((int)s, src, 64);
-                next_l = (uint32_t)__shfl((int)nl, src, 64);
-                if (lane == (uint32_t)src) ready = false;
-                rb &= rb - 1;
-            }
-            if (rb) {   // the others to the ready queue (after their final CAS: release)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                uint32_t slot0 = 0;
-                if (sub == 0) slot0 = atomicAdd(&s_tail, (uint32_t)__popcll(rb));
-                slot0 = (uint32_t)__shfl((int)slot0, (int)g0, 64);
-                if (ready) *(volatile uint16_t *)&Q[slot0 + (uint32_t)__popcll(rb & lt)] = (uint16_t)s;
-            }
-            e0 += LV_KG;
-            if (e0 >= eb) {
-                if (next >= 0) start((uint32_t)next, next_l);
-                else st = IDLE;
-            }
-        }
-        if (__all(st == FIN)) break;
-        if (__all(st == WAIT || st == FIN)) __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor(my_max, d, 64));
-    if (lane == 0 && my_max) atomicMax(max_level, my_max);
-}
-
 // published level + 1 -> level
 __global__ __launch_bounds__(BLOCK) void k_lv_unbias(uint32_t n, uint32_t *__restrict__ level)
 {
@@ -575,22 +439,6 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         uint16_t *fdep = ctx->get<uint16_t>("lv_fdep", (size_t)E + ch);
         launch(ctx, "lv_fwrite", k_lv_fwrite, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
                (const uint32_t *)pos, (const uint32_t *)foff, fdep);
-        if (n <= LV_KAHN_MAX && !getenv("ACC_LV_WALK")) {
-            // event-driven tier: the filtered graph transposed (counting sort), then Kahn's walk in one workgroup
-            uint32_t *scnt = ctx->get<uint32_t>("lv_scnt", 2 * (size_t)n);
-            uint32_t *scur = scnt + n;
-            uint32_t *soff = ctx->get<uint32_t>("lv_soff", (size_t)n + 1);
-            uint16_t *succ = ctx->get<uint16_t>("lv_succ", (size_t)E + 1);
-            ACC_HIP(hipMemsetAsync(scnt, 0, 2 * (size_t)n * sizeof(uint32_t), st));
-            launch(ctx, "lv_scount", k_lv_scount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)foff, (const uint16_t *)fdep, scnt);
-            scan<uint32_t, OpAdd<uint32_t>>(ctx, scnt, soff, n, true, soff + n);
-            launch(ctx, "lv_sfill", k_lv_sfill, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)foff, (const uint16_t *)fdep,
-                   (const uint32_t *)soff, scur, succ);
-            launch(ctx, "lv_walk", k_lv_kahn, dim3(1), dim3(LV_NT), 0, n, (const uint32_t *)foff, (const uint32_t *)soff,
-                   (const uint16_t *)succ, (const uint32_t *)order_exec, level, maxl);
-            ctx->stat("levelise.lds_tier", 2);
-            goto walked;
-        }
         const int ch_shift = 31 - __builtin_clz(ch);
         uint32_t *rstart = ctx->get<uint32_t>("lv_rstart", (size_t)(E >> ch_shift) + 3);
         launch(ctx, "lv_rounds", k_lv_rounds, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, ch_shift, (const uint32_t *)foff, rstart);
@@ -628,7 +476,6 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         launch(ctx, "lv_unbias", k_lv_unbias, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, level);
         ctx->stat("levelise.lds_tier", 0);
     }
-walked:
     const int pbits = bits_for(n - 1);
     launch(ctx, "lv_order_keys", k_lv_order_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)level,
            (const uint32_t *)pos, pbits, key);
