@@ -20,6 +20,7 @@ void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *v
 void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *view);
 void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
 void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in);
+void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
 void cfk_view(acc_cfk *cfk, acc_batch_in *out);
 void cfk_free(acc_cfk *cfk);
 acc_cfk *cfk_new(int device);
@@ -43,7 +44,7 @@ int acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
         ctx->device = device;
         ctx->flags = opts ? opts->flags : 0;
         ACC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        ACC_HIP(hipHostMalloc((void **)&ctx->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault));
+        ACC_HIP(hipHostMalloc((void **)&ctx->pinned, acc_ctx::PINNED_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     });
     if (rc != ACC_OK) {
         acc_destroy(ctx);
@@ -453,6 +454,15 @@ int acc_stats_get(acc_ctx *ctx, int i, const char **name, uint64_t *value)
     if (name) *name = ctx->stats[i].first.c_str();
     if (value) *value = ctx->stats[i].second;
     return ACC_OK;
+}
+
+int acc_cfk_apply(acc_ctx *ctx, const acc_cfk_snap *snap, const acc_cfk_updates *updates, acc_cfk_snap_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::cfk_apply(ctx, snap, updates, out_view);
+    });
 }
 
 }  // extern "C"

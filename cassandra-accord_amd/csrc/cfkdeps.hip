@@ -1,0 +1,788 @@
+// cfkdeps.hip — CommandsForKey.update with each command's deps: missing[] maintenance and the
+// TRANSITIVELY_KNOWN additions (local/CommandsForKey.java:657-1149), for a batch of command updates applied, in batch
+// order, to every CommandsForKey (key) they touch.
+//
+// The state is key-major: per key its TxnInfos (TxnId, executeAt, InternalStatus) in TxnId order, each with its
+// TxnInfoWithMissing.missing (sorted TxnIds). Keys are independent, so the batch runs as one lane per key:
+//   1. the snapshot keys and every (update, key) pair are radix sorted by key code (stable: a key's snapshot first,
+//      then its updates in batch order); distinct keys by a flag scan;
+//   2. per key, working-space bounds (entries: snapshot + one per update + its deps; missing: bounded by the entries
+//      squared) and one scan of them give each key two ping-pong buffers in one pool;
+//   3. one lane per key replays its updates: CommandsForKey.update -> insert / update, computeInfoAndAdditions,
+//      insertInfoAndOneMissing, updateOrInsertWithAdditions with mergeAndFilterMissing / to / insertMissing,
+//      removeMissing — each update rebuilding the key's TxnInfo array into the other buffer, as the Java builds a new
+//      array;
+//   4. final sizes, two scans, and a compaction into the key-major output (keys without entries dropped).
+// Errors: a status going back (IllegalStateException "stale status", ACC_E_STATE), an addition equal to an existing
+// TxnId or depsKnownBefore equal to a TxnId (the reference's checkState, ACC_E_STATE), malformed input (ACC_E_ARG).
+#include "dict.hpp"
+
+namespace acc {
+namespace cd {
+
+constexpr uint64_t IDENTITY_LSB = 0xFFFFFFFFFFFF001EULL;
+enum : uint32_t { TK = 0, PRE = 2, ACC = 3, COMMITTED = 4, APPLIED = 6, INVALID = 7 };
+enum : uint64_t { E_ARG_STATUS = 1, E_ARG_SORT = 2, E_ARG_OFF = 4, E_STALE = 8, E_STATE = 16, E_CAP = 32 };
+
+struct Ts {
+    uint64_t m, l;
+    int32_t n;
+};
+
+__device__ __forceinline__ int cmp(const Ts &a, const Ts &b)
+{
+    if (a.m != b.m) return a.m < b.m ? -1 : 1;
+    const uint64_t a1 = a.l & IDENTITY_LSB, b1 = b.l & IDENTITY_LSB;
+    if (a1 != b1) return a1 < b1 ? -1 : 1;
+    if (a.n != b.n) return a.n < b.n ? -1 : 1;
+    return 0;
+}
+__device__ __forceinline__ uint32_t kind(const Ts &t) { return (uint32_t)(t.l >> 1) & 7u; }
+// Kind.witnesses() (primitives/Txn.java:221-236)
+__device__ __forceinline__ uint32_t witnesses_mask(uint32_t k)
+{
+    switch (k) {
+    case 0: case 2: return 1u << 1;
+    case 1: case 3: return (1u << 0) | (1u << 1);
+    case 4: return (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4);
+    default: return 0;
+    }
+}
+__device__ __forceinline__ bool witnesses(const Ts &owner, const Ts &t) { return (witnesses_mask(kind(owner)) >> kind(t)) & 1u; }
+__device__ __forceinline__ bool has_info(uint32_t s) { return s >= ACC && s <= APPLIED; }
+
+struct Info {
+    Ts id, ex;
+    uint32_t st, self;   // self: executeAt is the TxnId (TxnInfo.create keeps the TxnId object)
+    uint32_t ms, mn;     // missing[] in the buffer's missing area
+};
+// TxnInfo.depsKnownBefore() (:322-325, InternalStatus.depsKnownBefore :260-279): the txn itself or its executeAt
+__device__ __forceinline__ bool dkb_self(const Info &x) { return x.st == PRE || x.st == ACC || x.self; }
+__device__ __forceinline__ const Ts &dkb(const Info &x) { return dkb_self(x) ? x.id : x.ex; }
+
+struct Buf {
+    Info *e;
+    Ts *m;
+    uint32_t n, mtop;
+};
+
+struct Work {   // one key's working space
+    Buf a, b;
+    uint32_t ecap, mcap;
+    Ts *tmiss;      // the new TxnInfo's missing[] (ecap)
+    Ts *adds;       // additions (dcap)
+    Ts *owned;      // insertMissing result (dcap + 1)
+};
+
+__device__ long bsearch_ts(const Ts *a, long from, long to, const Ts &k)   // Arrays.binarySearch
+{
+    long lo = from, hi = to - 1;
+    while (lo <= hi) {
+        const long mid = (long)(((unsigned long)lo + (unsigned long)hi) >> 1);
+        const int c = cmp(a[mid], k);
+        if (c < 0) lo = mid + 1; else if (c > 0) hi = mid - 1; else return mid;
+    }
+    return -(lo + 1);
+}
+__device__ long bsearch_info(const Buf &b, long from, long to, const Ts &k)
+{
+    long lo = from, hi = to - 1;
+    while (lo <= hi) {
+        const long mid = (long)(((unsigned long)lo + (unsigned long)hi) >> 1);
+        const int c = cmp(b.e[mid].id, k);
+        if (c < 0) lo = mid + 1; else if (c > 0) hi = mid - 1; else return mid;
+    }
+    return -(lo + 1);
+}
+
+struct Ctx {
+    Work w;
+    uint64_t err;
+    __device__ bool room_e(uint32_t n) { if (n > w.ecap) { err |= E_CAP; return false; } return true; }
+    __device__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_CAP; return false; } return true; }
+
+    // append entry x of src with its missing[] copied (dropping `drop` when given) to dst
+    __device__ void put(Buf &dst, const Info &x, const Ts *src_m, const Ts *drop)
+    {
+        Info y = x;
+        y.ms = dst.mtop;
+        y.mn = 0;
+        if (x.mn && room_m(dst, x.mn)) {
+            for (uint32_t q = 0; q < x.mn; ++q) {
+                const Ts &t = src_m[x.ms + q];
+                if (drop && cmp(t, *drop) == 0) continue;
+                dst.m[dst.mtop + y.mn++] = t;
+            }
+        }
+        dst.mtop += y.mn;
+        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+    }
+    // x with `ins` inserted into its missing[] (SortedArrays.insert)
+    __device__ void put_with_one(Buf &dst, const Info &x, const Ts *src_m, const Ts &ins)
+    {
+        Info y = x;
+        y.ms = dst.mtop;
+        y.mn = 0;
+        if (!room_m(dst, x.mn + 1)) return;
+        bool done = false;
+        for (uint32_t q = 0; q < x.mn; ++q) {
+            const Ts &t = src_m[x.ms + q];
+            const int c = cmp(t, ins);
+            if (!done && c >= 0) { if (c > 0) dst.m[dst.mtop + y.mn++] = ins; done = true; }
+            dst.m[dst.mtop + y.mn++] = t;
+        }
+        if (!done) dst.m[dst.mtop + y.mn++] = ins;
+        dst.mtop += y.mn;
+        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+    }
+    // mergeAndFilterMissing (:988-1025) of additions[0, count) into x's missing[], written to dst
+    __device__ void put_merged(Buf &dst, const Info &x, const Ts *src_m, const Ts *add, uint32_t count)
+    {
+        const uint32_t kinds = witnesses_mask(kind(x.id));
+        uint32_t keep = 0;
+        for (uint32_t i = 0; i < count; ++i) keep += (kinds >> kind(add[i])) & 1u;
+        if (!keep) { put(dst, x, src_m, nullptr); return; }
+        Info y = x;
+        y.ms = dst.mtop;
+        y.mn = 0;
+        if (!room_m(dst, x.mn + keep)) return;
+        Ts *o = dst.m + dst.mtop;
+        uint32_t i = 0, j = 0, n = 0;
+        while (i < count && j < x.mn) {
+            if ((kinds >> kind(add[i])) & 1u) {
+                if (cmp(add[i], src_m[x.ms + j]) < 0) o[n++] = add[i++];
+                else o[n++] = src_m[x.ms + j++];
+            } else ++i;
+        }
+        for (; i < count; ++i) if ((kinds >> kind(add[i])) & 1u) o[n++] = add[i];
+        while (j < x.mn) o[n++] = src_m[x.ms + j++];
+        if (n != x.mn + keep) err |= E_STATE;   // checkState(count == additionCount + current.length)
+        y.mn = n;
+        dst.mtop += n;
+        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+    }
+    // a new TxnInfo whose missing[] is in w.tmiss
+    __device__ void put_new(Buf &dst, const Info &x, uint32_t nm)
+    {
+        Info y = x;
+        y.ms = dst.mtop;
+        y.mn = 0;
+        if (nm && room_m(dst, nm)) {
+            for (uint32_t q = 0; q < nm; ++q) dst.m[dst.mtop + q] = w.tmiss[q];
+            y.mn = nm;
+        }
+        dst.mtop += y.mn;
+        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+    }
+    __device__ void put_tk(Buf &dst, const Ts &id)   // TxnInfo.create(txnId, TRANSITIVELY_KNOWN, txnId)
+    {
+        Info y;
+        y.id = id; y.ex = id; y.st = TK; y.self = 1; y.ms = dst.mtop; y.mn = 0;
+        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+    }
+
+    // insert(pos, TxnInfo) (:880-897) with insertInfoAndOneMissing (:899-944); the new info's missing[] in tmiss
+    __device__ void insert_plain(const Buf &A, Buf &B, uint32_t pos, const Info &ins, uint32_t nm)
+    {
+        const bool plain = ins.st >= COMMITTED;
+        for (uint32_t i = 0; i < pos; ++i) {
+            const Info &x = A.e[i];
+            if (!plain && has_info(x.st) && cmp(dkb(x), ins.id) > 0 && witnesses(x.id, ins.id)) put_with_one(B, x, A.m, ins.id);
+            else put(B, x, A.m, nullptr);
+        }
+        put_new(B, ins, nm);
+        for (uint32_t i = pos; i < A.n; ++i) {
+            const Info &x = A.e[i];
+            if (!plain && has_info(x.st) && witnesses(x.id, ins.id)) put_with_one(B, x, A.m, ins.id);
+            else put(B, x, A.m, nullptr);
+        }
+    }
+    // update(pos, txnId, cur, new) (:865-875): the entry replaced, removeMissing (:946-972) when it becomes committed
+    __device__ void update_plain(const Buf &A, Buf &B, uint32_t pos, const Info &nw, uint32_t nm)
+    {
+        const bool crossed = A.e[pos].st < COMMITTED && nw.st >= COMMITTED;
+        for (uint32_t i = 0; i < A.n; ++i) {
+            if (i == pos) put_new(B, nw, nm);
+            else put(B, A.e[i], A.m, crossed ? &nw.id : nullptr);
+        }
+    }
+
+    // computeInfoAndAdditions (:1057-1149): the new TxnInfo (missing[] to tmiss) and the deps this CFK lacks (adds)
+    __device__ Info compute_info(const Buf &A, long insert_pos, long update_pos, const Ts &id, uint32_t st, const Ts &ex_in,
+                                 const Ts *deps, uint32_t nd, uint32_t &nm, uint32_t &na)
+    {
+        Info x;
+        x.id = id; x.st = st; x.self = 1; x.ex = id; x.ms = 0; x.mn = 0;
+        if (cmp(ex_in, id) != 0) { x.ex = ex_in; x.self = 0; }
+        const bool self = st == PRE || st == ACC || x.self;
+        long dpos = insert_pos;
+        if (!self) {
+            dpos = bsearch_info(A, insert_pos, (long)A.n, x.ex);
+            if (dpos >= 0) err |= E_STATE;   // checkState(depsKnownBeforePos < 0)
+            dpos = -1 - dpos;
+        }
+        nm = 0; na = 0;
+        long ti = 0;
+        uint32_t di = 0;
+        while (ti < dpos && di < nd) {
+            const Info &t = A.e[ti];
+            const int r = cmp(t.id, deps[di]);
+            if (r == 0) { ++ti; ++di; }
+            else if (r < 0) {
+                if (ti != update_pos && t.st < COMMITTED && witnesses(id, t.id)) w.tmiss[nm++] = t.id;
+                ++ti;
+            } else w.adds[na++] = deps[di++];
+        }
+        for (; ti < dpos; ++ti) {
+            const Info &t = A.e[ti];
+            if (ti != update_pos && t.st < COMMITTED && witnesses(id, t.id)) w.tmiss[nm++] = t.id;
+        }
+        while (di < nd) w.adds[na++] = deps[di++];
+        return x;
+    }
+
+    // updateOrInsertWithAdditions (:772-863)
+    __device__ void with_additions(const Buf &A, Buf &B, long src_insert, long src_update, const Info &winfo, uint32_t nm,
+                                   uint32_t na)
+    {
+        const Ts *add = w.adds;
+        long aip = bsearch_ts(add, 0, (long)na, winfo.id);
+        if (aip >= 0) { err |= E_STATE; return; }
+        aip = -1 - aip;
+        const uint32_t target = (uint32_t)(src_insert + aip);
+        const Ts *msrc = add;
+        const bool insert_self_missing = src_update < 0 && winfo.st < COMMITTED;
+        uint32_t i = 0, j = 0, mcount = 0, mlimit = na, count = 0;
+        while (i < A.n) {
+            if (count == target) {
+                put_new(B, winfo, nm);
+                if ((long)i == src_update) ++i;
+                else if (insert_self_missing) ++mcount;
+                ++count;
+                continue;
+            }
+            const int r = j == na ? -1 : cmp(A.e[i].id, add[j]);
+            if (r < 0) {
+                const Info &x = A.e[i];
+                if ((long)i == src_update) put_new(B, winfo, nm);
+                else if (has_info(x.st)) {
+                    if (insert_self_missing && msrc == add && (mcount != j || (!dkb_self(x) && cmp(dkb(x), winfo.id) > 0))) {
+                        // insertMissing (:979-986)
+                        for (long q = 0; q < aip; ++q) w.owned[q] = add[q];
+                        w.owned[aip] = winfo.id;
+                        for (uint32_t q = (uint32_t)aip; q < na; ++q) w.owned[q + 1] = add[q];
+                        msrc = w.owned;
+                        ++mlimit;
+                    }
+                    // to (:1027-1033)
+                    uint32_t to = mcount;
+                    if (!dkb_self(x)) {
+                        long t = bsearch_ts(msrc, 0, (long)mlimit, dkb(x));
+                        to = (uint32_t)(t < 0 ? -1 - t : t);
+                    }
+                    if (to > 0) put_merged(B, x, A.m, msrc, to);
+                    else put(B, x, A.m, nullptr);
+                } else put(B, x, A.m, nullptr);
+                ++i;
+            } else if (r > 0) {
+                put_tk(B, add[j++]);
+                ++mcount;
+            } else {
+                err |= E_STATE;   // "should be an insertion, but found match when merging with origin"
+                return;
+            }
+            ++count;
+        }
+        if (j < na) {
+            if (count <= target) {
+                while (count < target) { put_tk(B, add[j++]); ++count; }
+                put_new(B, winfo, nm);
+                count = target + 1;
+            }
+            while (j < na) { put_tk(B, add[j++]); ++count; }
+        } else if (count == target) {
+            put_new(B, winfo, nm);
+        }
+    }
+
+    // removeMissing over a whole buffer, in place (:946-972)
+    __device__ void remove_missing(Buf &B, const Ts &id)
+    {
+        for (uint32_t i = 0; i < B.n; ++i) {
+            Info &x = B.e[i];
+            if (!x.mn) continue;
+            const long j = bsearch_ts(B.m + x.ms, 0, (long)x.mn, id);
+            if (j < 0) continue;
+            for (uint32_t q = (uint32_t)j; q + 1 < x.mn; ++q) B.m[x.ms + q] = B.m[x.ms + q + 1];
+            --x.mn;
+        }
+    }
+
+    // CommandsForKey.update(prev, next) (:657-722) on this key; returns true when the state moved to B
+    __device__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, bool ballot_changed, const Ts *deps,
+                          uint32_t nd)
+    {
+        B.n = 0; B.mtop = 0;
+        long pos = bsearch_info(A, 0, (long)A.n, id);
+        if (pos < 0) {
+            pos = -1 - pos;
+            if (has_info(st)) {
+                uint32_t nm, na;
+                const Info ni = compute_info(A, pos, -1, id, st, ex, deps, nd, nm, na);
+                if (na == 0) insert_plain(A, B, (uint32_t)pos, ni, nm);
+                else with_additions(A, B, pos, -1, ni, nm, na);
+            } else {
+                Info ni;
+                ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = 0; ni.mn = 0;
+                insert_plain(A, B, (uint32_t)pos, ni, 0);
+            }
+            return true;
+        }
+        const Info cur = A.e[pos];
+        if (st <= cur.st) {
+            if (cur.st != st) { err |= E_STALE; return false; }   // Invariants.checkState (:681-683)
+            if (!has_info(st) || !ballot_changed) return false;   // acceptedOrCommitted unchanged: this (:684-685)
+        }
+        if (has_info(st)) {
+            uint32_t nm, na;
+            const Info ni = compute_info(A, pos, pos, id, st, ex, deps, nd, nm, na);
+            if (na == 0) update_plain(A, B, (uint32_t)pos, ni, nm);
+            else {
+                with_additions(A, B, pos, pos, ni, nm, na);
+                if (cur.st < COMMITTED && st >= COMMITTED) remove_missing(B, id);
+            }
+        } else {
+            Info ni;
+            ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = 0; ni.mn = 0;
+            update_plain(A, B, (uint32_t)pos, ni, 0);
+        }
+        return true;
+    }
+};
+
+struct Snap {
+    const uint64_t *key;
+    const uint32_t *ent_off, *miss_off;
+    const uint64_t *em, *el, *xm, *xl, *mm, *ml;
+    const int32_t *en, *xn, *mn;
+    const uint8_t *st;
+    uint32_t n_keys;
+    uint64_t n_ent, n_miss;
+};
+struct Upd {
+    const uint64_t *um, *ul, *uxm, *uxl, *key, *dm, *dl;
+    const int32_t *un, *uxn, *dn;
+    const uint8_t *st, *fl;
+    const uint32_t *key_off, *dep_off, *owner;   // owner: update of each (update, key) pair
+    uint32_t n_upd;
+    uint64_t NP, ND;
+};
+
+// validation + the pair -> update map
+__global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__restrict__ owner, uint64_t *__restrict__ err)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t e = 0;
+    if (i < u.n_upd) {
+        const uint32_t a = u.key_off[i], b = u.key_off[i + 1];
+        if (b < a || b > u.NP || (i == 0 && a != 0) || (i + 1 == u.n_upd && b != u.NP)) e |= E_ARG_OFF;
+        else {
+            for (uint32_t j = a; j < b; ++j) {
+                owner[j] = (uint32_t)i;
+                if (j > a && u.key[j - 1] >= u.key[j]) e |= E_ARG_SORT;
+            }
+        }
+        if (u.st[i] > INVALID && u.st[i] != 0xFF) e |= E_ARG_STATUS;
+    }
+    if (i < u.NP) {
+        const uint32_t a = u.dep_off[i], b = u.dep_off[i + 1];
+        if (b < a || b > u.ND || (i == 0 && a != 0) || (i + 1 == u.NP && b != u.ND)) e |= E_ARG_OFF;
+        else
+            for (uint32_t j = a + 1; j < b; ++j)
+                if (cmp(Ts{ u.dm[j - 1], u.dl[j - 1], u.dn[j - 1] }, Ts{ u.dm[j], u.dl[j], u.dn[j] }) >= 0) { e |= E_ARG_SORT; break; }
+    }
+    if (i < s.n_keys) {
+        if (i > 0 && s.key[i - 1] >= s.key[i]) e |= E_ARG_SORT;
+        const uint32_t a = s.ent_off[i], b = s.ent_off[i + 1];
+        if (b < a || b > s.n_ent || (i == 0 && a != 0) || (i + 1 == s.n_keys && b != s.n_ent)) e |= E_ARG_OFF;
+        else
+            for (uint32_t j = a; j < b; ++j) {
+                if (s.st[j] > INVALID) e |= E_ARG_STATUS;
+                if (j > a && cmp(Ts{ s.em[j - 1], s.el[j - 1], s.en[j - 1] }, Ts{ s.em[j], s.el[j], s.en[j] }) >= 0) e |= E_ARG_SORT;
+                const uint32_t m0 = s.miss_off[j], m1 = s.miss_off[j + 1];
+                if (m1 < m0 || m1 > s.n_miss) e |= E_ARG_OFF;
+            }
+    }
+    if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_keys(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
+                                                   const uint64_t *__restrict__ ukey, uint64_t *__restrict__ all)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < nk) all[i] = skey[i];
+    else if (i < nk + NP) all[i] = ukey[i - nk];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_kflag(uint64_t T, const uint64_t *__restrict__ sk, uint32_t *__restrict__ f)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < T) f[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
+}
+
+// per distinct key: its run [kstart, kend) of the sorted elements and its working-space bounds
+__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint64_t T, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fi,
+                                                     const uint32_t *__restrict__ src, uint32_t nk, Snap s, Upd u,
+                                                     uint32_t *__restrict__ kstart, uint64_t *__restrict__ ecap,
+                                                     uint64_t *__restrict__ mcap, uint64_t *__restrict__ dcap)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= T || !f[i]) return;
+    const uint32_t k = fi[i] - 1;
+    kstart[k] = (uint32_t)i;
+    uint64_t e = 0, m = 0, d = 0, grow = 0;
+    for (uint64_t q = i; q < T && (q == i || !f[q]); ++q) {
+        const uint32_t v = src[q];
+        if (v < nk) {
+            e += s.ent_off[v + 1] - s.ent_off[v];
+            m += s.miss_off[s.ent_off[v + 1]] - s.miss_off[s.ent_off[v]];
+        } else {
+            const uint32_t j = v - nk;
+            const uint64_t nd = u.dep_off[j + 1] - u.dep_off[j];
+            e += 1 + nd;
+            d = d > nd ? d : nd;
+            grow += nd + 2;
+        }
+    }
+    ecap[k] = e;
+    const uint64_t sq = e * e, lin = m + e * grow;
+    mcap[k] = sq < lin ? sq : lin;
+    dcap[k] = d + 1;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_kend(uint32_t nkeys, uint64_t T, uint32_t *__restrict__ kstart)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) kstart[nkeys] = (uint32_t)T;
+}
+
+struct Pool {
+    Info *e;
+    Ts *m;
+    const uint64_t *eoff, *moff, *doff;   // exclusive scans of ecap, mcap, dcap
+};
+
+// key k's working space: entries A | B at 2 * eoff[k]; its Ts region at 2 * moff[k] + eoff[k] + 2 * doff[k]: the new
+// TxnInfo's missing[] (ecap), additions (dcap), insertMissing / staged deps (dcap), then the A and B missing areas (mcap)
+__device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
+{
+    const uint64_t e0 = p.eoff[k], m0 = p.moff[k], d0 = p.doff[k], dk = p.doff[k + 1] - d0;
+    w.a.e = p.e + 2 * e0;
+    w.b.e = w.a.e + w.ecap;
+    Ts *R = p.m + 2 * m0 + e0 + 2 * d0;
+    w.tmiss = R;
+    w.adds = R + w.ecap;
+    w.owned = w.adds + dk;
+    w.a.m = w.owned + dk;
+    w.b.m = w.a.m + w.mcap;
+}
+
+// one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
+__global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32_t *__restrict__ kstart,
+                                                    const uint32_t *__restrict__ src, const uint64_t *__restrict__ ecap,
+                                                    const uint64_t *__restrict__ mcap, uint32_t nk, Snap s, Upd u, Pool p,
+                                                    uint8_t *__restrict__ final_b, uint32_t *__restrict__ fin_n,
+                                                    uint32_t *__restrict__ fin_m, uint64_t *__restrict__ err)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys) return;
+    Ctx c;
+    c.err = 0;
+    c.w.ecap = (uint32_t)ecap[k];
+    c.w.mcap = (uint32_t)mcap[k];
+    key_bufs(p, k, c.w);
+    const uint64_t dk = p.doff[k + 1] - p.doff[k];
+    Buf *A = &c.w.a, *B = &c.w.b;
+    A->n = 0; A->mtop = 0;
+    const uint32_t q0 = kstart[k], q1 = kstart[k + 1];
+    for (uint32_t q = q0; q < q1 && !c.err; ++q) {
+        const uint32_t v = src[q];
+        if (v < nk) {   // the snapshot of this key
+            for (uint32_t x = s.ent_off[v]; x < s.ent_off[v + 1]; ++x) {
+                Info y;
+                y.id = Ts{ s.em[x], s.el[x], s.en[x] };
+                y.ex = Ts{ s.xm[x], s.xl[x], s.xn[x] };
+                y.self = cmp(y.ex, y.id) == 0;
+                if (y.self) y.ex = y.id;
+                y.st = s.st[x];
+                y.ms = A->mtop;
+                y.mn = s.miss_off[x + 1] - s.miss_off[x];
+                if (!c.room_m(*A, y.mn) || !c.room_e(A->n + 1)) break;
+                for (uint32_t t = 0; t < y.mn; ++t) {
+                    const uint32_t z = s.miss_off[x] + t;
+                    A->m[A->mtop + t] = Ts{ s.mm[z], s.ml[z], s.mn[z] };
+                }
+                A->mtop += y.mn;
+                A->e[A->n++] = y;
+            }
+            continue;
+        }
+        const uint32_t j = v - nk, i = u.owner[j];
+        const uint32_t st = u.st[i];
+        if (st == 0xFF) continue;   // InternalStatus.from(saveStatus) == null: unchanged
+        const Ts id{ u.um[i], u.ul[i], u.un[i] }, ex{ u.uxm[i], u.uxl[i], u.uxn[i] };
+        // the command's keyDeps.txnIds(key), staged in the owned area: computeInfoAndAdditions reads them (copying
+        // the additions out) before updateOrInsertWithAdditions may write an insertMissing result there
+        const uint32_t da = u.dep_off[j], db = u.dep_off[j + 1];
+        Ts *deps = c.w.owned;
+        if (db - da > dk) { c.err |= E_CAP; break; }
+        for (uint32_t t = da; t < db; ++t) deps[t - da] = Ts{ u.dm[t], u.dl[t], u.dn[t] };
+        if (c.apply(*A, *B, id, ex, st, (u.fl[i] & 1u) != 0, deps, db - da)) {
+            Buf *t = A; A = B; B = t;
+        }
+    }
+    final_b[k] = A == &c.w.a ? 0 : 1;
+    fin_n[k] = A->n;
+    fin_m[k] = A->mtop;
+    if (c.err) atomicOr((unsigned long long *)err, (unsigned long long)c.err);
+}
+
+// output: keys with entries, their entry counts
+__global__ __launch_bounds__(BLOCK) void k_cd_out1(uint32_t nkeys, const uint32_t *__restrict__ fin_n, uint32_t *__restrict__ keep)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < nkeys) keep[k] = fin_n[k] ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_out2(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
+                                                   const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ sk,
+                                                   const uint32_t *__restrict__ fin_n, uint64_t *__restrict__ okey,
+                                                   uint32_t *__restrict__ ocnt)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys || !keep[k]) return;
+    okey[kpos[k]] = sk[kstart[k]];
+    ocnt[kpos[k]] = fin_n[k];
+}
+
+struct Out {
+    uint64_t *em, *el, *xm, *xl, *mm, *ml;
+    int32_t *en, *xn, *mn;
+    uint8_t *st;
+    uint32_t *ent_off, *mcnt, *miss_off;
+};
+
+// entries of every kept key (one lane per key), and each entry's missing count
+__global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
+                                                   const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
+                                                   const uint8_t *__restrict__ final_b, Out o)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys || !keep[k]) return;
+    Work w;
+    w.ecap = (uint32_t)ecap[k];
+    w.mcap = (uint32_t)mcap[k];
+    key_bufs(p, k, w);
+    const Info *E = final_b[k] ? w.b.e : w.a.e;
+    const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
+    for (uint32_t i = 0; i < n; ++i) {
+        const Info &x = E[i];
+        o.em[base + i] = x.id.m; o.el[base + i] = x.id.l; o.en[base + i] = x.id.n;
+        o.xm[base + i] = x.ex.m; o.xl[base + i] = x.ex.l; o.xn[base + i] = x.ex.n;
+        o.st[base + i] = (uint8_t)x.st;
+        o.mcnt[base + i] = x.mn;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
+                                                   const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
+                                                   const uint8_t *__restrict__ final_b, Out o)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys || !keep[k]) return;
+    Work w;
+    w.ecap = (uint32_t)ecap[k];
+    w.mcap = (uint32_t)mcap[k];
+    key_bufs(p, k, w);
+    const Buf &F = final_b[k] ? w.b : w.a;
+    const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
+    for (uint32_t i = 0; i < n; ++i) {
+        const Info &x = F.e[i];
+        uint32_t dst = o.miss_off[base + i];
+        for (uint32_t q = 0; q < x.mn; ++q, ++dst) {
+            const Ts &t = F.m[x.ms + q];
+            o.mm[dst] = t.m; o.ml[dst] = t.l; o.mn[dst] = t.n;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *__restrict__ in, uint64_t *__restrict__ out)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+}  // namespace cd
+
+void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view)
+{
+    using namespace cd;
+    if (!in || !up || !view) fail(ACC_E_ARG, "null argument");
+    for (uint32_t m : { in->mem, up->mem })
+        if (m != ACC_MEM_HOST && m != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    hipStream_t st = ctx->stream;
+    const uint32_t nk = in->n_keys, nu = up->n_upd;
+    const uint64_t NE = in->n_entries, NM = in->n_missing, NP = up->n_pairs, ND = up->n_deps;
+    if (nk == 0 && (NE || NM)) fail(ACC_E_ARG, "entries without keys");
+    if (nu == 0 && (NP || ND)) fail(ACC_E_ARG, "pairs without updates");
+    if (NE >= 0xFFFFFFFFull || NM >= 0xFFFFFFFFull || NP >= 0xFFFFFFFFull || ND >= 0xFFFFFFFFull)
+        fail(ACC_E_CAP, "more than 2^32-1 entries / missing / pairs / deps");
+    Snap s{};
+    s.key = stage_in(ctx, "cd_skey", in->key, nk, in->mem);
+    s.ent_off = stage_in(ctx, "cd_soff", in->ent_off, (size_t)nk + 1, in->mem);
+    s.em = stage_in(ctx, "cd_sem", in->txn_id.msb, NE, in->mem);
+    s.el = stage_in(ctx, "cd_sel", in->txn_id.lsb, NE, in->mem);
+    s.en = stage_in(ctx, "cd_sen", in->txn_id.node, NE, in->mem);
+    s.xm = stage_in(ctx, "cd_sxm", in->execute_at.msb, NE, in->mem);
+    s.xl = stage_in(ctx, "cd_sxl", in->execute_at.lsb, NE, in->mem);
+    s.xn = stage_in(ctx, "cd_sxn", in->execute_at.node, NE, in->mem);
+    s.st = stage_in(ctx, "cd_sst", in->status, NE, in->mem);
+    s.miss_off = stage_in(ctx, "cd_smoff", in->miss_off, NE + 1, in->mem);
+    s.mm = stage_in(ctx, "cd_smm", in->missing.msb, NM, in->mem);
+    s.ml = stage_in(ctx, "cd_sml", in->missing.lsb, NM, in->mem);
+    s.mn = stage_in(ctx, "cd_smn", in->missing.node, NM, in->mem);
+    s.n_keys = nk; s.n_ent = NE; s.n_miss = NM;
+    Upd u{};
+    u.um = stage_in(ctx, "cd_um", up->txn_id.msb, nu, up->mem);
+    u.ul = stage_in(ctx, "cd_ul", up->txn_id.lsb, nu, up->mem);
+    u.un = stage_in(ctx, "cd_un", up->txn_id.node, nu, up->mem);
+    u.uxm = stage_in(ctx, "cd_uxm", up->execute_at.msb, nu, up->mem);
+    u.uxl = stage_in(ctx, "cd_uxl", up->execute_at.lsb, nu, up->mem);
+    u.uxn = stage_in(ctx, "cd_uxn", up->execute_at.node, nu, up->mem);
+    u.st = stage_in(ctx, "cd_ust", up->status, nu, up->mem);
+    u.fl = stage_in(ctx, "cd_ufl", up->flags, nu, up->mem);
+    u.key_off = stage_in(ctx, "cd_ukoff", up->key_off, (size_t)nu + 1, up->mem);
+    u.key = stage_in(ctx, "cd_ukey", up->key, NP, up->mem);
+    u.dep_off = stage_in(ctx, "cd_udoff", up->dep_off, NP + 1, up->mem);
+    u.dm = stage_in(ctx, "cd_udm", up->deps.msb, ND, up->mem);
+    u.dl = stage_in(ctx, "cd_udl", up->deps.lsb, ND, up->mem);
+    u.dn = stage_in(ctx, "cd_udn", up->deps.node, ND, up->mem);
+    u.n_upd = nu; u.NP = NP; u.ND = ND;
+    uint32_t *owner = ctx->get<uint32_t>("cd_owner", NP);
+    u.owner = owner;
+    uint64_t *errs = ctx->get<uint64_t>("cd_errs", 1);
+    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+    const uint64_t gmax = std::max<uint64_t>({ (uint64_t)nk, (uint64_t)nu, NP, 1 });
+    launch(ctx, "cd_check", k_cd_check, dim3(grid_for(gmax, BLOCK)), dim3(BLOCK), 0, s, u, owner, errs);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    auto check = [&](uint64_t e) {
+        if (e & E_ARG_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal");
+        if (e & E_ARG_OFF) fail(ACC_E_ARG, "offsets must be non-decreasing from 0 to their totals");
+        if (e & E_ARG_SORT) fail(ACC_E_ARG, "keys / TxnIds / deps must be sorted unique");
+        if (e & E_STALE) fail(ACC_E_STATE, "stale status update to CommandsForKey (IllegalStateException)");
+        if (e & E_STATE) fail(ACC_E_STATE, "CommandsForKey invariant violated (IllegalStateException)");
+        if (e & E_CAP) fail(ACC_E_STATE, "internal: CommandsForKey working space exceeded");
+    };
+    check(ctx->pinned[0]);
+
+    // ---- 1. keys: the snapshot's and every (update, key) pair's, sorted stably by key code
+    const uint64_t T = nk + NP;
+    uint64_t *all = ctx->get<uint64_t>("cd_all", T);
+    uint32_t nkeys = 0;
+    Sorted so{ nullptr, nullptr };
+    uint32_t *kflag = ctx->get<uint32_t>("cd_kflag", T), *kinc = ctx->get<uint32_t>("cd_kinc", T);
+    if (T) {
+        launch(ctx, "cd_keys", k_cd_keys, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, nk, NP, s.key, u.key, all);
+        so = radix_sort(ctx, "cd_rs", all, nullptr, T, 64);
+        launch(ctx, "cd_kflag", k_cd_kflag, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint64_t *)so.keys, kflag);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, kflag, kinc, T, false);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, kinc + T - 1, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        nkeys = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+    }
+    // ---- 2. working space
+    uint32_t *kstart = ctx->get<uint32_t>("cd_kstart", (size_t)nkeys + 1);
+    uint64_t *ecap = ctx->get<uint64_t>("cd_ecap", nkeys), *mcap = ctx->get<uint64_t>("cd_mcap", nkeys);
+    uint64_t *dcap = ctx->get<uint64_t>("cd_dcap", nkeys);
+    uint64_t *eoff = ctx->get<uint64_t>("cd_eoff", (size_t)nkeys + 1), *moff = ctx->get<uint64_t>("cd_moff", (size_t)nkeys + 1);
+    uint64_t *doff = ctx->get<uint64_t>("cd_doff", (size_t)nkeys + 1);
+    uint64_t Etot = 0, Mtot = 0, Dtot = 0;
+    if (nkeys) {
+        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
+               (const uint32_t *)kinc, (const uint32_t *)so.vals, nk, s, u, kstart, ecap, mcap, dcap);
+        launch(ctx, "cd_kend", k_cd_kend, dim3(1), dim3(BLOCK), 0, nkeys, T, kstart);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, ecap, eoff, nkeys, true, eoff + nkeys);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, dcap, doff, nkeys, true, doff + nkeys);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, eoff + nkeys, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, moff + nkeys, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, doff + nkeys, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        Etot = ctx->pinned[0]; Mtot = ctx->pinned[1]; Dtot = ctx->pinned[2];
+    }
+    const uint64_t pool_bytes = 2 * Etot * sizeof(Info) + (2 * Mtot + Etot + 2 * Dtot) * sizeof(Ts);
+    if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
+    Pool p{ ctx->get<Info>("cd_pool_e", 2 * Etot), ctx->get<Ts>("cd_pool_m", 2 * Mtot + Etot + 2 * Dtot), eoff, moff, doff };
+    uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
+    uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
+    // ---- 3. replay
+    if (nkeys) {
+        launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
+               (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m, errs);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        check(ctx->pinned[0]);
+    }
+    // ---- 4. key-major output
+    uint32_t *keep = ctx->get<uint32_t>("cd_keep", nkeys), *kpos = ctx->get<uint32_t>("cd_kpos", (size_t)nkeys + 1);
+    uint32_t nko = 0;
+    if (nkeys) {
+        launch(ctx, "cd_out1", k_cd_out1, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)fin_n, keep);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, keep, kpos, nkeys, true, kpos + nkeys);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, kpos + nkeys, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        nko = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+    }
+    uint64_t *okey = ctx->get<uint64_t>("cd_okey", nko);
+    uint32_t *ocnt = ctx->get<uint32_t>("cd_ocnt", nko);
+    Out o{};
+    o.ent_off = ctx->get<uint32_t>("cd_oent_off", (size_t)nko + 1);
+    uint64_t NEo = 0, NMo = 0;
+    if (nko) {
+        launch(ctx, "cd_out2", k_cd_out2, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
+               (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, (const uint32_t *)fin_n, okey, ocnt);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, ocnt, o.ent_off, nko, true, o.ent_off + nko);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, o.ent_off + nko, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        NEo = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+    } else {
+        ACC_HIP(hipMemsetAsync(o.ent_off, 0, 4, st));
+    }
+    o.em = ctx->get<uint64_t>("cd_oem", NEo); o.el = ctx->get<uint64_t>("cd_oel", NEo); o.en = ctx->get<int32_t>("cd_oen", NEo);
+    o.xm = ctx->get<uint64_t>("cd_oxm", NEo); o.xl = ctx->get<uint64_t>("cd_oxl", NEo); o.xn = ctx->get<int32_t>("cd_oxn", NEo);
+    o.st = ctx->get<uint8_t>("cd_ost", NEo);
+    o.mcnt = ctx->get<uint32_t>("cd_omcnt", NEo);
+    o.miss_off = ctx->get<uint32_t>("cd_omoff", NEo + 1);
+    if (NEo) {
+        launch(ctx, "cd_out3", k_cd_out3, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
+               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, o.mcnt, o.miss_off, NEo, true, o.miss_off + NEo);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, o.miss_off + NEo, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        NMo = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+    } else {
+        ACC_HIP(hipMemsetAsync(o.miss_off, 0, 4, st));
+    }
+    o.mm = ctx->get<uint64_t>("cd_omm", NMo); o.ml = ctx->get<uint64_t>("cd_oml", NMo); o.mn = ctx->get<int32_t>("cd_omn", NMo);
+    if (NMo)
+        launch(ctx, "cd_out4", k_cd_out4, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
+               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o);
+    ctx->sync();
+    ctx->stat("cfk.keys", nko);
+    ctx->stat("cfk.entries", NEo);
+    ctx->stat("cfk.missing", NMo);
+    *view = acc_cfk_snap_view{ nko, NEo, NMo, okey, o.ent_off, acc_ts_cols{ o.em, o.el, o.en }, acc_ts_cols{ o.xm, o.xl, o.xn },
+                               o.st, o.miss_off, acc_ts_cols{ o.mm, o.ml, o.mn } };
+}
+
+}  // namespace acc

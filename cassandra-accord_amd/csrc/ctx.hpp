@@ -66,7 +66,8 @@ struct acc_ctx {
     std::unordered_map<std::string, acc::Buf> bufs;
     // buffers replaced by a larger allocation while kernels may still read them: freed at the next sync
     std::vector<void *> graveyard;
-    // pinned host staging for small read-backs (sizes, flags)
+    // pinned host staging for small read-backs (sizes, flags); words [PINNED_SLOTS, +512) hold slotted partials
+    static constexpr size_t PINNED_WORDS = 1024, PINNED_SLOTS = 512;
     uint64_t *pinned = nullptr;
     // timing
     std::vector<acc::TimingSlot> slots;

@@ -90,9 +90,11 @@ __device__ __forceinline__ void block_or_n(uint64_t (&v)[NW], uint64_t *dst)
 // Per txn: executeAt != TxnId flags, varying-bit masks, status / kind checks, TxnId order; per pair (a chunk's txns'
 // pairs are one contiguous range, walked coalesced with each pair's txn found in the chunk's key offsets in LDS):
 // owner[], key order within a txn (Keys.ofSortedUnique), the key-code varying-bit mask. Pair indices are bounded by P
-// (a malformed key_off is reported, never followed out of bounds). Blocks stride over chunks of BLOCK txns and fold
-// their words into g[] once at the end: same-address atomics serialise at the L2 (one per block per word over 4k
-// blocks cost ~0.1 ms).
+// (a malformed key_off is reported, never followed out of bounds). One chunk of BLOCK txns per block (full occupancy:
+// a few resident blocks per CU left every chunk's HBM round trips exposed, 0.11 ms for config 2); each block folds its
+// words into one of PREP_SLOTS slot rows of g (same-address atomics serialise at the L2) and the host ORs the rows.
+constexpr uint32_t PREP_SLOTS = 64;   // 64 x 8 words = ctx->pinned's slot area
+
 __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const uint64_t *__restrict__ tm, const uint64_t *__restrict__ tl,
                                                     const int32_t *__restrict__ tn, const uint64_t *__restrict__ em,
                                                     const uint64_t *__restrict__ el, const int32_t *__restrict__ en,
@@ -142,14 +144,15 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const 
             }
         }
     }
+    uint64_t *gs = g + 8 * (blockIdx.x % PREP_SLOTS);
     uint64_t v[6] = { m0, m1, m2, km, errs, unsorted };
-    block_or_n<6>(v, g);
+    block_or_n<6>(v, gs);
     __shared__ uint32_t s_nd;
     if (tid == 0) s_nd = 0;
     __syncthreads();
     if (differs) atomicAdd(&s_nd, differs);
     __syncthreads();
-    if (tid == 0 && s_nd) atomicAdd((unsigned long long *)&g[7], (unsigned long long)s_nd);
+    if (tid == 0 && s_nd) atomicAdd((unsigned long long *)&gs[7], (unsigned long long)s_nd);
 }
 
 // ---- sorted-batch dictionary: TxnIds are already in order; only the differing executeAts (B) are sorted.
@@ -2849,21 +2852,28 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
 {
     hipStream_t st = ctx->stream;
     // ---- 1. prep
+    static_assert(8 * PREP_SLOTS <= acc_ctx::PINNED_WORDS - acc_ctx::PINNED_SLOTS, "slot rows fit the pinned area");
+    uint64_t *gslots = ctx->get<uint64_t>("prep_slots", 8 * PREP_SLOTS);
     ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
+    ACC_HIP(hipMemsetAsync(gslots, 0, 8 * PREP_SLOTS * sizeof(uint64_t), st));
     uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
-    launch(ctx, "prep_txn", k_prep_txn, dim3(std::min<unsigned>(grid_for(n, BLOCK), 512u)), dim3(BLOCK), 0, n, P, tm, tl, tn, em, el, en, status,
-           key_off, key_code, owner, bflag, g);
+    launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, P, tm, tl, tn, em, el, en, status,
+           key_off, key_code, owner, bflag, gslots);
     // the last key_off entry must equal P
+    uint64_t hg[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
     {
         uint32_t last = 0;
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, g, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        uint64_t *hs = ctx->pinned + acc_ctx::PINNED_SLOTS;
+        ACC_HIP(hipMemcpyAsync(hs, gslots, 8 * PREP_SLOTS * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
         memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
         if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
+        for (uint32_t r = 0; r < PREP_SLOTS; ++r) {
+            for (int w = 0; w < 6; ++w) hg[w] |= hs[8 * r + w];
+            hg[7] += hs[8 * r + 7];
+        }
     }
-    uint64_t hg[8];
-    memcpy(hg, ctx->pinned, sizeof hg);
     check_errors(hg[4]);
     const bool batch_sorted = hg[5] == 0;
 
@@ -3215,7 +3225,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
             launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)ctx->get<uint32_t>("v2_w8_list", nbig), (const uint64_t *)(gstat + 7), vv,
                    (const uint64_t *)vcnt, wo);
-            launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 1024)), dim3(BLOCK), 0,
+            // (> 8 keys is rare: a small persistent grid, so an empty list costs one short wave of blocks rather than
+            // 1024 blocks of 56 KiB LDS queueing behind the stream pass)
+            launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 256)), dim3(BLOCK), 0,
                    (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
                    (const uint64_t *)vcnt, wo);
         } else if (big_ok) {

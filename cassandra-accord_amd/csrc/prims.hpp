@@ -469,7 +469,6 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__res
 {
     __shared__ uint32_t h[WAVES][OS_MAXP][256];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
-    const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     for (uint32_t i = tid; i < WAVES * OS_MAXP * 256; i += BLOCK) (&h[0][0][0])[i] = 0;
     __syncthreads();
     // tiles of RS_TILE keys (all of a tile's loads issued up front), blocks striding over them: the block's counts go to
@@ -484,16 +483,17 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__res
     for (int p = 0; p < passes; ++p) {
 #pragma unroll
         for (int k = 0; k < RS_ITEMS; ++k) {
-            // one LDS add per distinct digit of the wave (hot digits would serialise per-element atomics)
+            // a per-wave LDS histogram, one atomic add per element; a digit shared by the whole wave (a hot key's
+            // byte) takes one add instead of 64 serialised ones
             const bool valid = base + (size_t)k * BLOCK + tid < n;
             const uint32_t d = (uint32_t)(key[k] >> (lo + 8 * p)) & 255u;
-            uint64_t peers = __ballot(valid);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const uint64_t bal = __ballot((d >> b) & 1u);
-                peers &= ((d >> b) & 1u) ? bal : ~bal;
+            const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+            const uint64_t vb = __ballot(valid);
+            if (__ballot(valid && d == d0) == vb) {
+                if (lane == 0) h[wave][p][d0] += (uint32_t)__popcll(vb);
+            } else if (valid) {
+                atomicAdd(&h[wave][p][d], 1u);
             }
-            if (valid && (peers & lt_mask) == 0) h[wave][p][d] += (uint32_t)__popcll(peers);
         }
     }
     }
@@ -679,7 +679,7 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
         uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
         snprintf(th, sizeof th, "%s.ghist", tag);
-        launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 256u)), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
+        launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
         const uint64_t *kin = keys;
         const uint32_t *vin = vals;
         int cur = 0;
@@ -734,7 +734,7 @@ static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uin
     uint32_t *osb = ctx->get<uint32_t>(nsw, words);
     ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
     uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
-    launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 256u)), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
+    launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
     const uint64_t *kin = keys;
     int cur = 0;
     for (int p = 0; p < passes; ++p) {

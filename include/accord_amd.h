@@ -703,6 +703,55 @@ void acc_cfk_destroy(acc_cfk *cfk);
 int  acc_cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *delta);
 int  acc_cfk_view(acc_ctx *ctx, acc_cfk *cfk, acc_batch_in *out);
 
+/* ---- CommandsForKey.update with each command's deps (local/CommandsForKey.java:657-1149) ----
+ * The missing[] and TRANSITIVELY_KNOWN half of CommandsForKey maintenance, on a key-major snapshot: key k (sorted unique
+ * codes) holds its TxnInfos [ent_off[k], ent_off[k+1]) in TxnId order (TxnId, executeAt, InternalStatus) and each
+ * TxnInfo its TxnInfoWithMissing.missing [miss_off[e], miss_off[e+1]) (sorted raw TxnIds). A batch of command updates
+ * is applied in array order to every key each lists, as SafeCommandStore.updateCommandsForKey calls
+ * CommandsForKey.update(prev, next) (local/SafeCommandStore.java:217-240): status = the new InternalStatus (0xFF: the
+ * save status maps to none, no change), flags bit 0 = acceptedOrCommitted changed since the previous update (the
+ * reference returns the CFK unchanged for an equal status otherwise), execute_at = Command.executeAt(), and per
+ * (update, key) pair the command's partialDeps().keyDeps.txnIds(key) [dep_off[j], dep_off[j+1]) sorted. Deps the CFK
+ * lacks become TRANSITIVELY_KNOWN entries; TxnIds it holds (uncommitted, witnessed) that a dep list lacks go to that
+ * TxnInfo's missing[]; committing removes a TxnId from every missing[]. A status going back is ACC_E_STATE (the
+ * reference's IllegalStateException). RedundantBefore is empty. The result (keys without entries dropped) is
+ * device-resident until the next compute call, and its missing[] is what acc_map_reduce_full's WITH / WITHOUT tests
+ * read. */
+typedef struct acc_cfk_snap {
+    uint32_t mem, n_keys;
+    uint64_t n_entries, n_missing;
+    const uint64_t *key;         /* [n_keys] */
+    const uint32_t *ent_off;     /* [n_keys+1] */
+    acc_ts_cols txn_id, execute_at;
+    const uint8_t *status;       /* [n_entries] InternalStatus ordinals */
+    const uint32_t *miss_off;    /* [n_entries+1] */
+    acc_ts_cols missing;         /* [n_missing] */
+} acc_cfk_snap;
+
+typedef struct acc_cfk_updates {
+    uint32_t mem, n_upd;
+    uint64_t n_pairs, n_deps;
+    acc_ts_cols txn_id, execute_at;
+    const uint8_t *status, *flags;
+    const uint32_t *key_off;     /* [n_upd+1] */
+    const uint64_t *key;         /* [n_pairs] sorted unique per update */
+    const uint32_t *dep_off;     /* [n_pairs+1] */
+    acc_ts_cols deps;            /* [n_deps] */
+} acc_cfk_updates;
+
+typedef struct acc_cfk_snap_view {
+    uint32_t n_keys;
+    uint64_t n_entries, n_missing;
+    const uint64_t *key;
+    const uint32_t *ent_off;
+    acc_ts_cols txn_id, execute_at;
+    const uint8_t *status;
+    const uint32_t *miss_off;
+    acc_ts_cols missing;
+} acc_cfk_snap_view;
+
+int  acc_cfk_apply(acc_ctx *ctx, const acc_cfk_snap *snap, const acc_cfk_updates *updates, acc_cfk_snap_view *out_view);
+
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
  * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).

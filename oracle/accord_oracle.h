@@ -186,4 +186,32 @@ int orc_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, u
 #ifdef __cplusplus
 }
 #endif
+
+/* ---- accord_oracle_cfk.c: CommandsForKey.update with the command's deps (missing[], TRANSITIVELY_KNOWN additions) ----
+ * Key-major CommandsForKey snapshot (key k: entries [ent_off[k], ent_off[k+1]) sorted by TxnId, each with executeAt,
+ * InternalStatus and missing[] = [miss_off[e], miss_off[e+1]) sorted), then n_upd command updates applied in order to
+ * every key they list (ust = new InternalStatus, 0xFF = none; uflags bit 0 = acceptedOrCommitted changed; per (update,
+ * key) pair the command's partialDeps().keyDeps.txnIds(key) in [udep_off[j], udep_off[j+1])). Result key-major. */
+typedef struct orc_cfk_result {
+    uint32_t n_keys;
+    uint64_t *key; uint32_t *ent_off;
+    uint64_t *emsb, *elsb; int32_t *enode;
+    uint64_t *xmsb, *xlsb; int32_t *xnode;
+    uint8_t *status;
+    uint32_t *miss_off;
+    uint64_t *mmsb, *mlsb; int32_t *mnode;
+    uint64_t n_entries, n_missing;
+    int error; char message[256];
+} orc_cfk_result;
+
+orc_cfk_result *orc_cfk_apply(uint32_t n_keys, const uint64_t *key, const uint32_t *ent_off,
+                              const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                              const uint64_t *xmsb, const uint64_t *xlsb, const int32_t *xnode, const uint8_t *est,
+                              const uint32_t *miss_off, const uint64_t *mmsb, const uint64_t *mlsb, const int32_t *mnode,
+                              uint32_t n_upd, const uint64_t *umsb, const uint64_t *ulsb, const int32_t *unode,
+                              const uint64_t *uxmsb, const uint64_t *uxlsb, const int32_t *uxnode, const uint8_t *ust,
+                              const uint8_t *uflags, const uint32_t *ukey_off, const uint64_t *ukey,
+                              const uint32_t *udep_off, const uint64_t *dmsb, const uint64_t *dlsb, const int32_t *dnode);
+void orc_cfk_free(orc_cfk_result *r);
+
 #endif

@@ -336,6 +336,57 @@ def map_reduce_full_ranges(cmds: dict, queries: dict, started_at: int, test_dep:
     return _rangedeps_out(L, r, nq)
 
 
+CFK_SNAP = (("key", np.uint64), ("ent_off", np.uint32), ("emsb", np.uint64), ("elsb", np.uint64), ("enode", np.int32),
+            ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("status", np.uint8), ("miss_off", np.uint32),
+            ("mmsb", np.uint64), ("mlsb", np.uint64), ("mnode", np.int32))
+CFK_UPD = (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("xmsb", np.uint64), ("xlsb", np.uint64),
+           ("xnode", np.int32), ("status", np.uint8), ("flags", np.uint8), ("key_off", np.uint32), ("key", np.uint64),
+           ("dep_off", np.uint32), ("dmsb", np.uint64), ("dlsb", np.uint64), ("dnode", np.int32))
+
+
+class CfkResult(C.Structure):
+    _fields_ = [("n_keys", C.c_uint32), ("key", u64p), ("ent_off", u32p), ("emsb", u64p), ("elsb", u64p),
+                ("enode", i32p), ("xmsb", u64p), ("xlsb", u64p), ("xnode", i32p), ("status", u8p), ("miss_off", u32p),
+                ("mmsb", u64p), ("mlsb", u64p), ("mnode", i32p), ("n_entries", C.c_uint64), ("n_missing", C.c_uint64),
+                ("error", C.c_int), ("message", C.c_char * 256)]
+
+
+def cfk_apply(snap: dict, upd: dict) -> dict:
+    """orc_cfk_apply: CommandsForKey.update with each command's deps (local/CommandsForKey.java:657-1149) for a batch of
+    updates against a key-major snapshot (CFK_SNAP arrays; empty: key of length 0 and ent_off = [0]). Returns the
+    new key-major snapshot as a dict of the same arrays."""
+    L = lib()
+    if not hasattr(L.orc_cfk_apply, "_set"):
+        L.orc_cfk_apply.restype = C.POINTER(CfkResult)
+        L.orc_cfk_apply.argtypes = ([C.c_uint32] + [_CT[dt] for _, dt in CFK_SNAP] + [C.c_uint32] +
+                                    [_CT[dt] for _, dt in CFK_UPD])
+        L.orc_cfk_free.argtypes = [C.POINTER(CfkResult)]
+        L.orc_cfk_apply._set = True
+    pad = lambda src, k, dt: np.ascontiguousarray(np.append(np.asarray(src[k], dt), dt(0)))  # noqa: E731
+    sa = [pad(snap, k, dt) for k, dt in CFK_SNAP]
+    ua = [pad(upd, k, dt) for k, dt in CFK_UPD]
+    nk = len(snap["key"])
+    nu = len(upd["msb"])
+    r = L.orc_cfk_apply(nk, *[_p(a, _CT[dt]) for a, (_, dt) in zip(sa, CFK_SNAP)], nu,
+                        *[_p(a, _CT[dt]) for a, (_, dt) in zip(ua, CFK_UPD)])
+    try:
+        R = r.contents
+        if R.error:
+            raise OracleError(R.error, R.message.decode())
+        k, ne, nm = int(R.n_keys), int(R.n_entries), int(R.n_missing)
+        arr = lambda p, n, dt: np.ctypeslib.as_array(p, (max(n, 1),))[:n].astype(dt).copy()  # noqa: E731
+        out = dict(key=arr(R.key, k, np.uint64), ent_off=arr(R.ent_off, k + 1, np.uint32))
+        for f, dt in (("emsb", np.uint64), ("elsb", np.uint64), ("enode", np.int32), ("xmsb", np.uint64),
+                      ("xlsb", np.uint64), ("xnode", np.int32), ("status", np.uint8)):
+            out[f] = arr(getattr(R, f), ne, dt)
+        out["miss_off"] = arr(R.miss_off, ne + 1, np.uint32)
+        for f, dt in (("mmsb", np.uint64), ("mlsb", np.uint64), ("mnode", np.int32)):
+            out[f] = arr(getattr(R, f), nm, dt)
+    finally:
+        L.orc_cfk_free(r)
+    return out
+
+
 def keydeps_merge(m: dict) -> dict:
     """KeyDeps.merge per group over the acc_merge_in layout dict (grp_off, key_off, key_code, val_off,
     txn_rank, k2v_off, k2v). Returns the same-named merged arrays per group."""

@@ -1,0 +1,160 @@
+"""Seeded CommandsForKey update sequences with deps — TEST INFRASTRUCTURE.
+
+Commands move through the InternalStatus lifecycle the way SafeCommandStore.updateCommandsForKey sees them
+(local/SafeCommandStore.java:217-240; InternalStatus, local/CommandsForKey.java:194-203): PREACCEPTED (no info), then
+ACCEPTED with proposed deps, COMMITTED / STABLE with decided deps and an executeAt that may be bumped, APPLIED, or
+INVALID_OR_TRUNCATED; some ACCEPTED rounds repeat with a new ballot (acceptedOrCommitted changed). The deps of a command
+on key k (its partialDeps().keyDeps.txnIds(k)) are other txns on k below its depsKnownBefore (TxnId for ACCEPTED,
+executeAt once committed), including txns the store has not seen yet: CommandsForKey adds those as TRANSITIVELY_KNOWN
+and records the ones it knows but the deps lack in missing[].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from accord_amd import workload as W
+
+TK, HIST, PRE, ACC, COMMITTED, STABLE, APPLIED, INVALID = range(8)
+KINDS = np.array([0, 1, 3, 4])   # Read, Write, SyncPoint, ExclusiveSyncPoint
+
+
+def empty_snapshot():
+    z = lambda dt: np.zeros(0, dt)  # noqa: E731
+    return dict(key=z(np.uint64), ent_off=np.zeros(1, np.uint32), emsb=z(np.uint64), elsb=z(np.uint64),
+                enode=z(np.int32), xmsb=z(np.uint64), xlsb=z(np.uint64), xnode=z(np.int32), status=z(np.uint8),
+                miss_off=np.zeros(1, np.uint32), mmsb=z(np.uint64), mlsb=z(np.uint64), mnode=z(np.int32))
+
+
+def _ts_key(m, l, n):
+    return (m, l >> 16, l & 0x1E, n)
+
+
+def cfk_case(seed, n_txn=200, n_keys=12, keys_per=3, p_dep=0.5, p_bump=0.5, p_invalid=0.05, p_reaccept=0.15,
+             p_noop=0.03, window=40):
+    """The updates in the CFK_UPD layout of oracle.py. Events of different txns interleave; each txn's
+    own events stay in lifecycle order."""
+    rng = np.random.default_rng(seed)
+    kind = rng.choice(KINDS, size=n_txn, p=[0.35, 0.45, 0.1, 0.1])
+    tid = [tuple(int(x) for x in W.encode_ts(1, 4 * i + 4, int(kind[i]) << 1, 1 + int(rng.integers(0, 4))))
+           for i in range(n_txn)]
+    keys = [np.sort(rng.choice(n_keys, size=min(keys_per, n_keys), replace=False)) * 10 + 100 for _ in range(n_txn)]
+    on_key = {}
+    for i in range(n_txn):
+        for k in keys[i]:
+            on_key.setdefault(int(k), []).append(i)
+    # per txn: its lifecycle events (status, executeAt, ballot flag)
+    life = []
+    for i in range(n_txn):
+        ev = [(PRE, tid[i], 0)]
+        if rng.random() < p_invalid:
+            ev.append((INVALID, tid[i], 0))
+        else:
+            ev.append((ACC, tid[i], 0))
+            if rng.random() < p_reaccept:
+                ev.append((ACC, tid[i], 1))
+            ex = tid[i]
+            if rng.random() < p_bump:
+                ex = tuple(int(x) for x in W.encode_ts(1, 4 * i + 4 + 2 + 4 * int(rng.integers(0, 8)), 0,
+                                                         1 + int(rng.integers(0, 4))))
+            end = int(rng.integers(0, 4))
+            ev.append((COMMITTED, ex, 0))
+            if end >= 1:
+                ev.append((STABLE, ex, 0))
+            if end >= 2:
+                ev.append((APPLIED, ex, 0))
+        if rng.random() < p_noop:
+            ev.insert(1, (0xFF, tid[i], 0))   # a save status with no InternalStatus
+        if rng.random() < 0.1:
+            ev = ev[1:]                         # first seen already ACCEPTED (or later)
+        life.append(ev)
+    # interleave: txns start roughly in TxnId order, events spread over a window
+    events = []
+    for i in range(n_txn):
+        t = float(i)
+        for e in life[i]:
+            t += rng.exponential(window / 4)
+            events.append((t, i, e))
+    events.sort(key=lambda x: x[0])
+    cols = {k: [] for k in ("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags")}
+    key_off, key_list, dep_off, dm, dl, dn = [0], [], [0], [], [], []
+    for _, i, (st, ex, fl) in events:
+        m, l, n = tid[i]
+        cols["msb"].append(m); cols["lsb"].append(l); cols["node"].append(n)
+        cols["xmsb"].append(ex[0]); cols["xlsb"].append(ex[1]); cols["xnode"].append(ex[2])
+        cols["status"].append(st); cols["flags"].append(fl)
+        dkb = _ts_key(*tid[i]) if st in (PRE, ACC, 0xFF) or ex == tid[i] else _ts_key(*ex)
+        for k in keys[i]:
+            key_list.append(int(k))
+            if st in (ACC, COMMITTED, STABLE, APPLIED):
+                cand = [j for j in on_key[int(k)] if j != i and _ts_key(*tid[j]) < dkb]
+                near = [j for j in cand if j >= i - window]
+                pick = [j for j in near if rng.random() < p_dep]
+                for j in sorted(pick, key=lambda j: _ts_key(*tid[j])):
+                    dm.append(tid[j][0]); dl.append(tid[j][1]); dn.append(tid[j][2])
+            dep_off.append(len(dm))
+        key_off.append(len(key_list))
+    upd = {k: np.array(v, dt) for (k, v), dt in zip(cols.items(), (np.uint64, np.uint64, np.int32, np.uint64, np.uint64,
+                                                                  np.int32, np.uint8, np.uint8))}
+    upd.update(key_off=np.array(key_off, np.uint32), key=np.array(key_list, np.uint64),
+               dep_off=np.array(dep_off, np.uint32), dmsb=np.array(dm, np.uint64), dlsb=np.array(dl, np.uint64),
+               dnode=np.array(dn, np.int32))
+    return upd
+
+
+def split_updates(upd, at):
+    """(first `at` updates, the rest) in the CFK_UPD layout"""
+    ko, do = upd["key_off"].astype(np.int64), upd["dep_off"].astype(np.int64)
+    def part(a, b):
+        out = {k: upd[k][a:b] for k in ("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags")}
+        out["key_off"] = (ko[a:b + 1] - ko[a]).astype(np.uint32)
+        out["key"] = upd["key"][ko[a]:ko[b]]
+        out["dep_off"] = (do[ko[a]:ko[b] + 1] - do[ko[a]]).astype(np.uint32)
+        for f in ("dmsb", "dlsb", "dnode"):
+            out[f] = upd[f][do[ko[a]]:do[ko[b]]]
+        return out
+    n = len(upd["msb"])
+    return part(0, at), part(at, n)
+
+
+def handmade():
+    """Three Writes A < B < C on one key, worked through CommandsForKey.java:657-1149 by hand:
+      1. B PREACCEPTED                         -> [B PRE]
+      2. C ACCEPTED, deps [A] (A unknown)      -> [A TK, B PRE, C ACC missing [B]]   (A added, B missing from C's deps)
+      3. A COMMITTED, no deps                  -> [A COMMITTED, B PRE, C ACC [B]]
+      4. B ACCEPTED, deps [A]                  -> [A COMMITTED, B ACC, C ACC [B]]
+      5. B COMMITTED                           -> [A COMMITTED, B COMMITTED, C ACC]   (removeMissing(B))
+    Returns (updates, [(n_updates applied, expected [(hlc, status, [missing hlcs])])])."""
+    ts = {h: tuple(int(x) for x in W.encode_ts(1, h, 1 << 1, 1)) for h in (4, 8, 12)}
+    steps = [(8, PRE, []), (12, ACC, [4]), (4, COMMITTED, []), (8, ACC, [4]), (8, COMMITTED, [4])]
+    cols = {k: [] for k in ("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags")}
+    key_off, keys, dep_off, dm, dl, dn = [0], [], [0], [], [], []
+    for h, st, deps in steps:
+        m, l, n = ts[h]
+        for k, v in zip(("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags"), (m, l, n, m, l, n, st, 0)):
+            cols[k].append(v)
+        keys.append(500)
+        key_off.append(len(keys))
+        for d in deps:
+            dm.append(ts[d][0]); dl.append(ts[d][1]); dn.append(ts[d][2])
+        dep_off.append(len(dm))
+    upd = {k: np.array(v, dt) for (k, v), dt in zip(cols.items(), (np.uint64, np.uint64, np.int32, np.uint64, np.uint64,
+                                                                  np.int32, np.uint8, np.uint8))}
+    upd.update(key_off=np.array(key_off, np.uint32), key=np.array(keys, np.uint64), dep_off=np.array(dep_off, np.uint32),
+               dmsb=np.array(dm, np.uint64), dlsb=np.array(dl, np.uint64), dnode=np.array(dn, np.int32))
+    expect = [
+        (1, [(8, PRE, [])]),
+        (2, [(4, TK, []), (8, PRE, []), (12, ACC, [8])]),
+        (3, [(4, COMMITTED, []), (8, PRE, []), (12, ACC, [8])]),
+        (4, [(4, COMMITTED, []), (8, ACC, []), (12, ACC, [8])]),
+        (5, [(4, COMMITTED, []), (8, COMMITTED, []), (12, ACC, [])]),
+    ]
+    return upd, expect
+
+
+def describe(snap):
+    """key-major snapshot -> [(hlc, status, [missing hlcs])] of its single key"""
+    out = []
+    for e in range(int(snap["ent_off"][-1])):
+        a, b = int(snap["miss_off"][e]), int(snap["miss_off"][e + 1])
+        out.append((int(snap["elsb"][e]) >> 16, int(snap["status"][e]), [int(x) >> 16 for x in snap["mlsb"][a:b]]))
+    return out
