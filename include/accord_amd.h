@@ -752,6 +752,47 @@ typedef struct acc_cfk_snap_view {
 
 int  acc_cfk_apply(acc_ctx *ctx, const acc_cfk_snap *snap, const acc_cfk_updates *updates, acc_cfk_snap_view *out_view);
 
+/* ---- MaxConflicts and the PreAccept executeAt proposal (local/MaxConflicts.java:31-96,
+ * local/CommandStore.java:280-290 updateMaxConflicts, :320-345 preaccept) ----
+ * A CommandStore's MaxConflicts is the pointwise max of every (keysOrRanges, executeAt) update it received
+ * (MaxConflicts.merge(map, create(keysOrRanges, executeAt)), a ReducingRangeMap folded with Timestamp::max; a key k
+ * enters as its asRange(), which holds exactly k), so MaxConflicts.get(q) is the max executeAt over the updates whose
+ * keys / ranges intersect q's keys / ranges (Range.contains for a key, compareIntersecting for two ranges).
+ * Input: the updates (Command.executeAt() and keys or ranges each; updateMaxConflicts skips an update whose executeAt
+ * does not exceed the previous one, which the max already absorbs). Output per query (a PreAccept of txn_id over its
+ * sliced keys or ranges): max = minNonConflicting = MaxConflicts.get(keys) (all zero = Timestamp.NONE when nothing
+ * intersects) and fast_path = txnId.compareTo(minNonConflicting) >= 0 (preaccept then returns txnId when
+ * permitFastPath and the epoch check hold, the caller's part; otherwise time.uniqueNow(minNonConflicting)). Among
+ * compare-equal timestamps with different raw flag bits, which instance is returned is unspecified. */
+typedef struct acc_conflicts_in {
+    uint32_t mem, n_upd, end_inclusive;
+    uint64_t n_keys, n_ranges;
+    acc_ts_cols execute_at;      /* [n_upd] */
+    const uint32_t *key_off;     /* [n_upd+1] */
+    const uint64_t *key;         /* [n_keys] sorted unique per update */
+    const uint32_t *rng_off;     /* [n_upd+1] */
+    const uint64_t *rng_start, *rng_end;   /* [n_ranges] sorted, non-overlapping per update */
+} acc_conflicts_in;
+
+typedef struct acc_preaccept_in {
+    uint32_t mem, n_query;
+    uint64_t n_parts;
+    acc_ts_cols txn_id;          /* [n_query] */
+    const uint8_t *is_range;     /* [n_query] 0: keys, 1: ranges */
+    const uint32_t *part_off;    /* [n_query+1] */
+    const uint64_t *part_start, *part_end;
+} acc_preaccept_in;
+
+typedef struct acc_preaccept_out {
+    uint32_t mem;
+    uint64_t *max_msb, *max_lsb;
+    int32_t  *max_node;
+    uint8_t  *fast_path;         /* all [n_query], caller-owned */
+} acc_preaccept_out;
+
+int  acc_max_conflicts(acc_ctx *ctx, const acc_conflicts_in *updates, const acc_preaccept_in *queries,
+                       acc_preaccept_out *out);
+
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
  * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).

@@ -214,4 +214,11 @@ orc_cfk_result *orc_cfk_apply(uint32_t n_keys, const uint64_t *key, const uint32
                               const uint32_t *udep_off, const uint64_t *dmsb, const uint64_t *dlsb, const int32_t *dnode);
 void orc_cfk_free(orc_cfk_result *r);
 
+/* MaxConflicts.get + the PreAccept fast-path test for each query (accord_oracle_cfk.c); layout as acc_max_conflicts */
+int orc_max_conflicts(uint32_t n_upd, const uint64_t *xmsb, const uint64_t *xlsb, const int32_t *xnode,
+                      const uint32_t *key_off, const uint64_t *key, const uint32_t *rng_off, const uint64_t *rs,
+                      const uint64_t *re, int end_inclusive, uint32_t nq, const uint64_t *qmsb, const uint64_t *qlsb,
+                      const int32_t *qnode, const uint8_t *is_range, const uint32_t *part_off, const uint64_t *ps,
+                      const uint64_t *pe, uint64_t *omsb, uint64_t *olsb, int32_t *onode, uint8_t *fast);
+
 #endif

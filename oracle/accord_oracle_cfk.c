@@ -446,3 +446,46 @@ void orc_cfk_free(orc_cfk_result *r)
     free(r->xnode); free(r->status); free(r->miss_off); free(r->mmsb); free(r->mlsb); free(r->mnode);
     free(r);
 }
+
+/* ------------------------------------------------------------------ MaxConflicts (local/MaxConflicts.java:31-96) */
+
+/* MaxConflicts.get(keysOrRanges) after merge(create(keysOrRanges_u, executeAt_u)) of every update u, restated
+ * point-wise: the ReducingRangeMap's value at a point is the Timestamp::max of the updates covering it (a key enters
+ * as asRange(), covering exactly itself), and foldl over the query's keys / ranges visits every map entry they
+ * intersect; then CommandStore.preaccept's test txnId.compareTo(minNonConflicting) >= 0 (CommandStore.java:320-345). */
+static int mc_range_contains(uint64_t s, uint64_t e, uint64_t k, int ei) { return ei ? (s < k && k <= e) : (s <= k && k < e); }
+
+int orc_max_conflicts(uint32_t n_upd, const uint64_t *xmsb, const uint64_t *xlsb, const int32_t *xnode,
+                      const uint32_t *key_off, const uint64_t *key, const uint32_t *rng_off, const uint64_t *rs,
+                      const uint64_t *re, int end_inclusive, uint32_t nq, const uint64_t *qmsb, const uint64_t *qlsb,
+                      const int32_t *qnode, const uint8_t *is_range, const uint32_t *part_off, const uint64_t *ps,
+                      const uint64_t *pe, uint64_t *omsb, uint64_t *olsb, int32_t *onode, uint8_t *fast)
+{
+    for (uint32_t q = 0; q < nq; ++q) {
+        int have = 0;
+        cts best = { 0, 0, 0 };
+        for (uint32_t u = 0; u < n_upd; ++u) {
+            int hit = 0;
+            for (uint32_t p = part_off[q]; p < part_off[q + 1] && !hit; ++p) {
+                if (is_range[q]) {
+                    for (uint32_t j = key_off[u]; j < key_off[u + 1] && !hit; ++j)
+                        hit = mc_range_contains(ps[p], pe[p], key[j], end_inclusive);
+                    for (uint32_t j = rng_off[u]; j < rng_off[u + 1] && !hit; ++j)
+                        hit = rs[j] < pe[p] && re[j] > ps[p];
+                } else {
+                    for (uint32_t j = key_off[u]; j < key_off[u + 1] && !hit; ++j) hit = key[j] == ps[p];
+                    for (uint32_t j = rng_off[u]; j < rng_off[u + 1] && !hit; ++j)
+                        hit = mc_range_contains(rs[j], re[j], ps[p], end_inclusive);
+                }
+            }
+            if (!hit) continue;
+            cts x = { xmsb[u], xlsb[u], xnode[u] };
+            if (!have || c_cmp(&best, &x) < 0) best = x;   /* Timestamp.max */
+            have = 1;
+        }
+        omsb[q] = best.msb; olsb[q] = best.lsb; onode[q] = best.node;
+        cts id = { qmsb[q], qlsb[q], qnode[q] };
+        fast[q] = (uint8_t)(c_cmp(&id, &best) >= 0);
+    }
+    return 0;
+}

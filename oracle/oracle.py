@@ -387,6 +387,33 @@ def cfk_apply(snap: dict, upd: dict) -> dict:
     return out
 
 
+MC_UPD = (("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("key_off", np.uint32), ("key", np.uint64),
+          ("rng_off", np.uint32), ("rng_start", np.uint64), ("rng_end", np.uint64))
+MC_Q = (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("is_range", np.uint8), ("part_off", np.uint32),
+        ("part_start", np.uint64), ("part_end", np.uint64))
+
+
+def max_conflicts(upd: dict, q: dict) -> dict:
+    """orc_max_conflicts: MaxConflicts.get(keys) over the updates (local/MaxConflicts.java:31-96) and the fast-path
+    test of CommandStore.preaccept (local/CommandStore.java:320-345) per query: dict(msb, lsb, node, fast)."""
+    L = lib()
+    if not hasattr(L.orc_max_conflicts, "_set"):
+        L.orc_max_conflicts.restype = C.c_int
+        L.orc_max_conflicts.argtypes = ([C.c_uint32] + [_CT[dt] for _, dt in MC_UPD] + [C.c_int, C.c_uint32] +
+                                        [_CT[dt] for _, dt in MC_Q] + [u64p, u64p, i32p, u8p])
+        L.orc_max_conflicts._set = True
+    pad = lambda src, k, dt: np.ascontiguousarray(np.append(np.asarray(src[k], dt), dt(0)))  # noqa: E731
+    ua = [pad(upd, k, dt) for k, dt in MC_UPD]
+    qa = [pad(q, k, dt) for k, dt in MC_Q]
+    nq = len(q["msb"])
+    out = dict(msb=np.zeros(nq + 1, np.uint64), lsb=np.zeros(nq + 1, np.uint64), node=np.zeros(nq + 1, np.int32),
+               fast=np.zeros(nq + 1, np.uint8))
+    L.orc_max_conflicts(len(upd["xmsb"]), *[_p(a, _CT[dt]) for a, (_, dt) in zip(ua, MC_UPD)], int(upd["end_inclusive"]),
+                        nq, *[_p(a, _CT[dt]) for a, (_, dt) in zip(qa, MC_Q)], _p(out["msb"], u64p), _p(out["lsb"], u64p),
+                        _p(out["node"], i32p), _p(out["fast"], u8p))
+    return {k: v[:nq] for k, v in out.items()}
+
+
 def keydeps_merge(m: dict) -> dict:
     """KeyDeps.merge per group over the acc_merge_in layout dict (grp_off, key_off, key_code, val_off,
     txn_rank, k2v_off, k2v). Returns the same-named merged arrays per group."""

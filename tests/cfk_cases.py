@@ -158,3 +158,42 @@ def describe(snap):
         a, b = int(snap["miss_off"][e]), int(snap["miss_off"][e + 1])
         out.append((int(snap["elsb"][e]) >> 16, int(snap["status"][e]), [int(x) >> 16 for x in snap["mlsb"][a:b]]))
     return out
+
+
+def conflicts_case(seed, n_upd=500, n_query=300, span=4000, p_range=0.3, end_inclusive=1):
+    """MaxConflicts updates (executeAt + keys or ranges; distinct executeAts, some bumped past later TxnIds) and
+    PreAccept queries (a TxnId + keys or ranges): TxnIds on even hlcs, queries spread so both fast-path outcomes
+    occur."""
+    rng = np.random.default_rng(seed)
+    upd = dict(end_inclusive=end_inclusive)
+    xm, xl, xn, ko, keys, ro, rs, re_ = [], [], [], [0], [], [0], [], []
+    for i in range(n_upd):
+        m, l, n = (int(x) for x in W.encode_ts(1, 2 * int(rng.integers(0, 3 * n_upd)) + 1, 0, 1 + i % 1000))
+        xm.append(m); xl.append(l); xn.append(n)
+        if rng.random() < p_range:
+            pts = sorted(set(int(x) for x in rng.integers(0, span, size=2 * int(rng.integers(1, 3)))))
+            prs = [(pts[j], pts[j + 1]) for j in range(0, len(pts) - 1, 2)]
+            rs.extend(a for a, _ in prs); re_.extend(b for _, b in prs)
+        else:
+            keys.extend(sorted(set(int(x) for x in rng.integers(0, span, size=int(rng.integers(1, 6))))))
+        ko.append(len(keys)); ro.append(len(rs))
+    upd.update(xmsb=np.array(xm, np.uint64), xlsb=np.array(xl, np.uint64), xnode=np.array(xn, np.int32),
+               key_off=np.array(ko, np.uint32), key=np.array(keys, np.uint64), rng_off=np.array(ro, np.uint32),
+               rng_start=np.array(rs, np.uint64), rng_end=np.array(re_, np.uint64))
+    qm, ql, qn, qr, qo, ps, pe = [], [], [], [], [0], [], []
+    for _ in range(n_query):
+        m, l, n = (int(x) for x in W.encode_ts(1, 2 * int(rng.integers(0, 3 * n_upd)), int(rng.choice(KINDS)) << 1,
+                                               1 + int(rng.integers(0, 4))))
+        qm.append(m); ql.append(l); qn.append(n)
+        if rng.random() < 0.4:
+            pts = sorted(set(int(x) for x in rng.integers(0, span, size=2 * int(rng.integers(1, 3)))))
+            prs = [(pts[j], pts[j + 1]) for j in range(0, len(pts) - 1, 2)]
+            qr.append(1); ps.extend(a for a, _ in prs); pe.extend(b for _, b in prs)
+        else:
+            ks = sorted(set(int(x) for x in rng.integers(0, span, size=int(rng.integers(1, 8)))))
+            qr.append(0); ps.extend(ks); pe.extend([0] * len(ks))
+        qo.append(len(ps))
+    q = dict(msb=np.array(qm, np.uint64), lsb=np.array(ql, np.uint64), node=np.array(qn, np.int32),
+             is_range=np.array(qr, np.uint8), part_off=np.array(qo, np.uint32), part_start=np.array(ps, np.uint64),
+             part_end=np.array(pe, np.uint64))
+    return upd, q

@@ -80,3 +80,31 @@ def test_cfk_deps_empty_and_errors(ctx):
         cfk_apply(ctx, e, back)
     g = cfk_apply(ctx, e, upd)   # the context stays usable
     assert CC.describe(g) == CC.handmade()[1][-1][1]
+
+
+@pytest.mark.parametrize("seed,end_inclusive,n_upd,n_query,span", [(1, 1, 500, 300, 4000), (2, 0, 800, 400, 300),
+                                                                   (3, 1, 20000, 5000, 1 << 20)])
+def test_max_conflicts(ctx, seed, end_inclusive, n_upd, n_query, span):
+    """acc_max_conflicts (MaxConflicts.get + the PreAccept fast-path test) vs the C restatement: key and range updates,
+    key and range queries, both bound types, dense (span 300: every key hot) and sparse key spaces."""
+    from accord_amd.deps import max_conflicts
+    upd, q = CC.conflicts_case(seed, n_upd=n_upd, n_query=n_query, span=span, end_inclusive=end_inclusive)
+    g = max_conflicts(ctx, upd, q)
+    o = oracle.max_conflicts(upd, q)
+    for k in ("msb", "lsb", "node", "fast"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    assert 0 < int(o["fast"].sum()) < n_query
+
+
+def test_max_conflicts_empty(ctx):
+    from accord_amd.deps import IllegalArgumentException, max_conflicts
+    upd, q = CC.conflicts_case(4, n_upd=10, n_query=5)
+    none = dict(end_inclusive=1, xmsb=np.zeros(0, np.uint64), xlsb=np.zeros(0, np.uint64), xnode=np.zeros(0, np.int32),
+                key_off=np.zeros(1, np.uint32), key=np.zeros(0, np.uint64), rng_off=np.zeros(1, np.uint32),
+                rng_start=np.zeros(0, np.uint64), rng_end=np.zeros(0, np.uint64))
+    g = max_conflicts(ctx, none, q)
+    assert not g["msb"].any() and g["fast"].all()   # Timestamp.NONE: every TxnId is a fast path
+    bad = dict(upd)
+    bad["key"] = upd["key"][::-1].copy()
+    with pytest.raises(IllegalArgumentException):
+        max_conflicts(ctx, bad, q)

@@ -52,3 +52,42 @@ def test_stale_status_rejected():
     back["status"][4] = CC.PRE   # B COMMITTED -> PREACCEPTED after ACCEPTED: goes back
     with pytest.raises(oracle.OracleError):
         oracle.cfk_apply(CC.empty_snapshot(), back)
+
+
+def test_max_conflicts_by_hand():
+    """Two updates: key 10 at executeAt hlc 9, range (20, 30] at hlc 15 (EndInclusive); queries: key 10 (-> 9), key 25
+    (-> 15), key 20 (outside (20, 30] -> NONE), range (5, 21] (key 10 and the range -> 15); TxnId hlc 12 against 9 is
+    a fast path, against 15 not."""
+    from accord_amd import workload as W
+    ts = lambda h, f=0: tuple(int(x) for x in W.encode_ts(1, h, f, 1))  # noqa: E731
+    upd = dict(end_inclusive=1, xmsb=np.array([ts(9)[0], ts(15)[0]], np.uint64),
+               xlsb=np.array([ts(9)[1], ts(15)[1]], np.uint64), xnode=np.array([1, 1], np.int32),
+               key_off=np.array([0, 1, 1], np.uint32), key=np.array([10], np.uint64),
+               rng_off=np.array([0, 0, 1], np.uint32), rng_start=np.array([20], np.uint64), rng_end=np.array([30], np.uint64))
+    t12 = ts(12, 1 << 1)
+    q = dict(msb=np.array([t12[0]] * 4, np.uint64), lsb=np.array([t12[1]] * 4, np.uint64), node=np.array([1] * 4, np.int32),
+             is_range=np.array([0, 0, 0, 1], np.uint8), part_off=np.array([0, 1, 2, 3, 4], np.uint32),
+             part_start=np.array([10, 25, 20, 5], np.uint64), part_end=np.array([0, 0, 0, 21], np.uint64))
+    r = oracle.max_conflicts(upd, q)
+    assert [int(x) >> 16 for x in r["lsb"]] == [9, 15, 0, 15]
+    assert r["fast"].tolist() == [1, 0, 1, 0]
+
+
+def test_max_conflicts_is_a_max_over_intersections():
+    """Splitting the updates in two and taking the max of both answers equals the answer over all (merge of maps)."""
+    upd, q = CC.conflicts_case(3, n_upd=200, n_query=100)
+    whole = oracle.max_conflicts(upd, q)
+    n = len(upd["xmsb"]) // 2
+    ko, ro = upd["key_off"].astype(np.int64), upd["rng_off"].astype(np.int64)
+    def part(a, b):
+        return dict(end_inclusive=upd["end_inclusive"], xmsb=upd["xmsb"][a:b], xlsb=upd["xlsb"][a:b], xnode=upd["xnode"][a:b],
+                    key_off=(ko[a:b + 1] - ko[a]).astype(np.uint32), key=upd["key"][ko[a]:ko[b]],
+                    rng_off=(ro[a:b + 1] - ro[a]).astype(np.uint32), rng_start=upd["rng_start"][ro[a]:ro[b]],
+                    rng_end=upd["rng_end"][ro[a]:ro[b]])
+    x, y = oracle.max_conflicts(part(0, n), q), oracle.max_conflicts(part(n, len(upd["xmsb"])), q)
+    for i in range(len(q["msb"])):
+        a = (int(x["msb"][i]), int(x["lsb"][i]) >> 16, int(x["node"][i]))
+        b = (int(y["msb"][i]), int(y["lsb"][i]) >> 16, int(y["node"][i]))
+        w = (int(whole["msb"][i]), int(whole["lsb"][i]) >> 16, int(whole["node"][i]))
+        assert max(a, b) == w
+    assert 0 < int(whole["fast"].sum()) < len(q["msb"])
