@@ -182,8 +182,8 @@ def conflicts_case(seed, n_upd=500, n_query=300, span=4000, p_range=0.3, end_inc
                rng_start=np.array(rs, np.uint64), rng_end=np.array(re_, np.uint64))
     qm, ql, qn, qr, qo, ps, pe = [], [], [], [], [0], [], []
     for _ in range(n_query):
-        m, l, n = (int(x) for x in W.encode_ts(1, 2 * int(rng.integers(0, 3 * n_upd)), int(rng.choice(KINDS)) << 1,
-                                               1 + int(rng.integers(0, 4))))
+        h = 2 * int(rng.integers(0, 3 * n_upd)) if rng.random() < 0.7 else 2 * int(rng.integers(3 * n_upd, 4 * n_upd))
+        m, l, n = (int(x) for x in W.encode_ts(1, h, int(rng.choice(KINDS)) << 1, 1 + int(rng.integers(0, 4))))
         qm.append(m); ql.append(l); qn.append(n)
         if rng.random() < 0.4:
             pts = sorted(set(int(x) for x in rng.integers(0, span, size=2 * int(rng.integers(1, 3)))))
