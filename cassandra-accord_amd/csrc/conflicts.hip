@@ -175,20 +175,20 @@ __global__ __launch_bounds__(BLOCK) void k_mc_query(Qs q, Keys k, Upd u, uint64_
             }
         }
     }
-    // wave max under Timestamp.compareTo
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const Ts o{ (uint64_t)__shfl_xor((long long)best.m, d, 64), (uint64_t)__shfl_xor((long long)best.l, d, 64),
-                    __shfl_xor(best.n, d, 64) };
-        const bool oh = __shfl_xor((int)have, d, 64) != 0;
-        if (oh) {
-            // keep the lower lane's value on equality (a deterministic choice among compare-equal timestamps)
-            const bool mine_first = (lane & (uint32_t)d) == 0;
-            if (!have) { best = o; have = true; }
-            else {
-                const int c = cmp(best, o);
-                if (c < 0 || (c == 0 && !mine_first)) best = o;
-            }
+    // wave max under Timestamp.compareTo: lanes park their maxima in LDS, lane 0 folds them in lane order
+    __shared__ Ts red[WAVES][64];
+    __shared__ uint32_t red_have[WAVES][64];
+    const uint32_t w = threadIdx.x >> 6;
+    red[w][lane] = best;
+    red_have[w][lane] = have ? 1u : 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane == 0) {
+        for (uint32_t l = 1; l < 64; ++l) {
+            if (!red_have[w][l]) continue;
+            const Ts o = red[w][l];
+            best = have ? tmax(best, o) : o;
+            have = true;
         }
     }
     if (lane == 0) {
