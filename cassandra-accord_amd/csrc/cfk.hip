@@ -103,7 +103,7 @@ __global__ __launch_bounds__(BLOCK) void k_cf_order(uint32_t D, const uint32_t *
 // sorted delta txn k: its lower bound among the stored TxnIds, found or not, the status rule, the new-txn flag
 __global__ __launch_bounds__(BLOCK) void k_cf_locate(Delta d, Store s, const uint32_t *__restrict__ ord, uint32_t *__restrict__ pos,
                                                      uint32_t *__restrict__ isnew, int32_t *__restrict__ upd_of_old,
-                                                     uint64_t *__restrict__ errs)
+                                                     uint64_t *__restrict__ errs, uint32_t *__restrict__ skipped)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= d.D) return;
@@ -115,6 +115,7 @@ __global__ __launch_bounds__(BLOCK) void k_cf_locate(Delta d, Store s, const uin
         // only key-domain, globally visible txns are CommandsForKey members (SafeCommandStore.java:224)
         pos[k] = 0;
         isnew[k] = 0;
+        atomicAdd(skipped, 1u);
         return;
     }
     uint32_t lo = 0, hi = s.n;
@@ -301,11 +302,16 @@ void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
     uint32_t *newx = ctx->get<uint32_t>("cf_newx", (size_t)D + 1);
     int32_t *upd = ctx->get<int32_t>("cf_upd", (size_t)n + 1);
     ACC_HIP(hipMemsetAsync(upd, 0xFF, ((size_t)n + 1) * 4, st));
-    launch(ctx, "cf_locate", k_cf_locate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, s, (const uint32_t *)ord, pos, isnew, upd, errs);
+    uint32_t *skipped = ctx->get<uint32_t>("cf_skipped", 1);
+    ACC_HIP(hipMemsetAsync(skipped, 0, 4, st));
+    launch(ctx, "cf_locate", k_cf_locate, dim3(grid_for(D, BLOCK)), dim3(BLOCK), 0, d, s, (const uint32_t *)ord, pos, isnew, upd, errs,
+           skipped);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, isnew, newx, D, true, newx + D);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, newx + D, 4, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, skipped, 4, hipMemcpyDeviceToHost, st));
     ctx->sync();
+    const uint32_t nskip = (uint32_t)(ctx->pinned[2] & 0xFFFFFFFFu);
     if (ctx->pinned[0] & E_STALE)
         fail(ACC_E_STATE, "Attempted update to CommandsForKey with a stale status (CommandsForKey.update :680-688)");
     const uint32_t nnew = (uint32_t)(ctx->pinned[1] & 0xFFFFFFFFu);
@@ -333,7 +339,8 @@ void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
     cfk->n = n2;
     cfk->P = P2;
     ctx->stat("cfk.inserted", nnew);
-    ctx->stat("cfk.updated", D - nnew);
+    ctx->stat("cfk.updated", D - nnew - nskip);
+    ctx->stat("cfk.skipped", nskip);   // range-domain, EphemeralRead, LocalOnly: no CommandsForKey entry
 }
 
 acc_cfk *cfk_new(int device)
