@@ -1710,7 +1710,7 @@ struct WinLds {
     uint32_t out[WIN_OUT];         // (rank << 6 | key) of the entries below the span
     RunsT<WK> R;
     uint32_t kc[WK], out_k[WK], ser_tot[WK + 1];
-    uint32_t n_out, kept, d_out, bad;
+    uint32_t n_out, kept, d_out, bad, minr;
 };
 
 template <int WK>
@@ -1725,12 +1725,32 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
         const uint32_t t = list[b];
         const TxnCtx c = txn_ctx(v, o, t);
         const uint32_t S = v.tinfo[t].y;
-        const uint32_t base = S > WIN_W * 32 ? S - WIN_W * 32 : 0u;
-        const uint32_t nw = (S - base + 31) / 32;
         if (tid < 64) compute_runs(R, v, o, cnt, c);
-        for (uint32_t i = tid; i < c.nk * WIN_W; i += BLOCK) L.bm[i / WIN_W][i % WIN_W] = 0;
         if (tid < (uint32_t)WK) { L.kc[tid] = 0; L.out_k[tid] = 0; }
-        if (tid == 0) { L.n_out = 0; L.kept = 0; L.bad = 0; }
+        if (tid == 0) { L.n_out = 0; L.kept = 0; L.bad = 0; L.minr = 0xFFFFFFFFu; }
+        __syncthreads();
+        // the span's low end: the smallest rank an entry can have (a class run's first entry, an inline record's first
+        // entry, any entry of a short R3 run), so the bitmaps cover only [min, S) instead of 16,384 ranks below S
+        if (tid < c.nk) {
+            const uint32_t k = tid;
+            uint32_t mn = 0xFFFFFFFFu;
+            if (R.m[k] == INLINE_M) {
+                if (R.pre[k][1] > 0) mn = v.rec32[16 * R.start[k][0]];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 6; ++q)
+                    if (R.pre[k][q + 1] > R.pre[k][q]) mn = min(mn, v.list_rank[R.start[k][q]]);
+                const uint32_t l3 = R.pre[k][7] - R.pre[k][6];
+                if (l3 > 256) mn = 0u;
+                else for (uint32_t j = 0; j < l3; ++j) mn = min(mn, v.bc_rank[R.start[k][6] + j]);
+            }
+            atomicMin(&L.minr, mn);
+        }
+        __syncthreads();
+        const uint32_t lo_span = S > WIN_W * 32 ? S - WIN_W * 32 : 0u;
+        const uint32_t base = max(lo_span, min(L.minr, S));
+        const uint32_t nw = (S - base + 31) / 32;
+        for (uint32_t i = tid; i < c.nk * nw; i += BLOCK) L.bm[i / nw][i % nw] = 0;
         __syncthreads();
         const uint32_t total = R.total;
         // ---- gather: bits of the span, the entries below it to the list
