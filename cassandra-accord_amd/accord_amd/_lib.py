@@ -43,7 +43,7 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_partial_deps_reduce", "acc_shard_reduce",
            "acc_map_reduce_full", "acc_map_reduce_full_ranges", "acc_latest_deps_merge", "acc_partial_deps_batch",
            "acc_deps_from_json", "acc_deps_to_json",
-           "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view", "acc_cfk_apply", "acc_max_conflicts"]
+           "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view", "acc_cfk_apply", "acc_cfk_snap_to_batch", "acc_max_conflicts"]
 
 
 class Opts(C.Structure):
@@ -245,6 +245,10 @@ class CfkSnapView(C.Structure):
                 ("miss_off", C.c_void_p), ("missing", TsCols)]
 
 
+class CfkBatchView(C.Structure):
+    _fields_ = [("batch", BatchIn), ("missing_off", C.c_void_p), ("missing_txn", C.c_void_p), ("n_missing", C.c_uint64)]
+
+
 class ConflictsIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n_upd", C.c_uint32), ("end_inclusive", C.c_uint32), ("n_keys", C.c_uint64),
                 ("n_ranges", C.c_uint64), ("execute_at", TsCols), ("key_off", C.c_void_p), ("key", C.c_void_p),
@@ -400,6 +404,8 @@ def load():
     L.acc_cfk_view.restype = C.c_int
     L.acc_cfk_apply.argtypes = [C.c_void_p, C.POINTER(CfkSnap), C.POINTER(CfkUpdates), C.POINTER(CfkSnapView)]
     L.acc_cfk_apply.restype = C.c_int
+    L.acc_cfk_snap_to_batch.argtypes = [C.c_void_p, C.POINTER(CfkSnap), C.POINTER(CfkBatchView)]
+    L.acc_cfk_snap_to_batch.restype = C.c_int
     L.acc_max_conflicts.argtypes = [C.c_void_p, C.POINTER(ConflictsIn), C.POINTER(PreacceptIn), C.POINTER(PreacceptOut)]
     L.acc_max_conflicts.restype = C.c_int
     L.acc_copy_out.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]

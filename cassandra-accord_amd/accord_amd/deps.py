@@ -48,6 +48,7 @@ class Context:
 
     def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False):
         self.timing_enabled = timing
+        self.device = device
         self._lib = L.load()
         h = C.c_void_p()
         opts = L.Opts((L.ACC_OPT_TIMING if timing else 0) | (L.ACC_OPT_FORCE_REPLAY if force_replay else 0), 0)
@@ -729,12 +730,12 @@ def deps_to_json(ctx: Context, view) -> list[bytes]:
 
 # ---------------------------------------------------------------- CommandsForKey.update with deps (key-major)
 
-def cfk_apply(ctx: Context, snap: dict, upd: dict) -> dict:
+def cfk_apply(ctx: Context, snap: dict, upd: dict, keep_device: bool = False):
     """CommandsForKey.update(prev, next) with each command's deps (local/CommandsForKey.java:657-1149) for a batch of
     updates against a key-major snapshot (acc_cfk_apply): missing[] maintenance and TRANSITIVELY_KNOWN additions.
     snap: key, ent_off, emsb/elsb/enode (TxnIds), xmsb/xlsb/xnode (executeAts), status, miss_off, mmsb/mlsb/mnode;
     upd: msb/lsb/node, xmsb/xlsb/xnode, status, flags, key_off, key, dep_off, dmsb/dlsb/dnode. Returns the new
-    snapshot in the same layout (host copies)."""
+    snapshot in the same layout (host copies), or with keep_device its device-resident acc_cfk_snap_view."""
     a = {k: np.ascontiguousarray(np.asarray(snap[k], dt)) for k, dt in (
         ("key", np.uint64), ("ent_off", np.uint32), ("emsb", np.uint64), ("elsb", np.uint64), ("enode", np.int32),
         ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("status", np.uint8), ("miss_off", np.uint32),
@@ -753,6 +754,8 @@ def cfk_apply(ctx: Context, snap: dict, upd: dict) -> dict:
                       L.TsCols(p(b, "dmsb"), p(b, "dlsb"), p(b, "dnode")))
     v = L.CfkSnapView()
     ctx.check(ctx._lib.acc_cfk_apply(ctx.handle, C.byref(si), C.byref(ui), C.byref(v)))
+    if keep_device:
+        return v
     nk, ne, nm = int(v.n_keys), int(v.n_entries), int(v.n_missing)
     return dict(key=device_array(ctx, v.key, nk, np.uint64), ent_off=device_array(ctx, v.ent_off, nk + 1, np.uint32),
                 emsb=device_array(ctx, v.txn_id.msb, ne, np.uint64), elsb=device_array(ctx, v.txn_id.lsb, ne, np.uint64),
@@ -761,6 +764,66 @@ def cfk_apply(ctx: Context, snap: dict, upd: dict) -> dict:
                 status=device_array(ctx, v.status, ne, np.uint8), miss_off=device_array(ctx, v.miss_off, ne + 1, np.uint32),
                 mmsb=device_array(ctx, v.missing.msb, nm, np.uint64), mlsb=device_array(ctx, v.missing.lsb, nm, np.uint64),
                 mnode=device_array(ctx, v.missing.node, nm, np.int32))
+
+
+def _view_as_snap(v) -> "L.CfkSnap":
+    return L.CfkSnap(L.ACC_MEM_DEVICE, v.n_keys, v.n_entries, v.n_missing, v.key, v.ent_off, v.txn_id, v.execute_at,
+                     v.status, v.miss_off, v.missing)
+
+
+def cfk_snap_to_batch(ctx: Context, snap) -> "L.CfkBatchView":
+    """acc_cfk_snap_to_batch: the txn-major snapshot and per-pair missing[] batch indices acc_map_reduce_full reads,
+    in HBM. snap: a device-resident acc_cfk_snap_view (cfk_apply(..., keep_device=True)) or a host dict in the
+    cfk_apply snapshot layout."""
+    out = L.CfkBatchView()
+    if isinstance(snap, dict):
+        a = {k: np.ascontiguousarray(np.asarray(snap[k], dt)) for k, dt in (
+            ("key", np.uint64), ("ent_off", np.uint32), ("emsb", np.uint64), ("elsb", np.uint64), ("enode", np.int32),
+            ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("status", np.uint8),
+            ("miss_off", np.uint32), ("mmsb", np.uint64), ("mlsb", np.uint64), ("mnode", np.int32))}
+        p = lambda k: a[k].ctypes.data  # noqa: E731
+        si = L.CfkSnap(L.ACC_MEM_HOST, len(a["key"]), len(a["status"]), len(a["mmsb"]), p("key"), p("ent_off"),
+                       L.TsCols(p("emsb"), p("elsb"), p("enode")), L.TsCols(p("xmsb"), p("xlsb"), p("xnode")),
+                       p("status"), p("miss_off"), L.TsCols(p("mmsb"), p("mlsb"), p("mnode")))
+    else:
+        si = _view_as_snap(snap)
+    ctx.check(ctx._lib.acc_cfk_snap_to_batch(ctx.handle, C.byref(si), C.byref(out)))
+    return out
+
+
+def cfk_batch_host(ctx: Context, bv) -> tuple:
+    """Host copies of an acc_cfk_batch_view: (Batch, missing_off, missing_txn)."""
+    b = bv.batch
+    n, p = int(b.n_txn), int(b.n_pairs)
+    from .workload import Batch
+    batch = Batch(device_array(ctx, b.txn_id.msb, n, np.uint64), device_array(ctx, b.txn_id.lsb, n, np.uint64),
+                  device_array(ctx, b.txn_id.node, n, np.int32), device_array(ctx, b.execute_at.msb, n, np.uint64),
+                  device_array(ctx, b.execute_at.lsb, n, np.uint64), device_array(ctx, b.execute_at.node, n, np.int32),
+                  device_array(ctx, b.status, n, np.uint8), device_array(ctx, b.key_off, n + 1, np.uint32),
+                  device_array(ctx, b.key_code, p, np.uint64))
+    return (batch, device_array(ctx, bv.missing_off, p + 1, np.uint32),
+            device_array(ctx, bv.missing_txn, int(bv.n_missing), np.uint32))
+
+
+def cfk_map_reduce_full(ctx: Context, bv, queries: dict, started_at: int, test_dep: int, test_status: int,
+                        test_kinds: int = -1, executes_after: bool = False) -> "BatchKeyDeps":
+    """SafeCommandStore.mapReduceFull over the store's CommandsForKey state in place: acc_map_reduce_full reading the
+    acc_cfk_batch_view bv (cfk_snap_to_batch) straight from HBM. The query arrays are uploaded with torch (the
+    acc_recovery_in arrays share the missing[] placement, ACC_MEM_DEVICE)."""
+    import torch
+    dev = torch.device("cuda", ctx.device)
+    t = {k: torch.from_numpy(np.ascontiguousarray(queries[k], dtype=dt)).to(dev) for k, dt in (
+        ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("key_off", np.uint32), ("key_code", np.uint64))}
+    torch.cuda.synchronize(dev)
+    p = lambda k: t[k].data_ptr()  # noqa: E731
+    ri = L.RecoveryIn(int(t["msb"].shape[0]), L.ACC_MEM_DEVICE, L.TsCols(p("msb"), p("lsb"), p("node")), p("key_off"),
+                      p("key_code"), bv.missing_off, bv.missing_txn, int(bv.n_missing), started_at, test_dep,
+                      test_status, L.ACC_FULL_EXECUTES_AFTER if executes_after else 0, test_kinds)
+    view = L.KeydepsView()
+    ctx.check(ctx._lib.acc_map_reduce_full(ctx.handle, C.byref(bv.batch), C.byref(ri), C.byref(view)))
+    out = ctx.copy_out(view, None)
+    del t
+    return out
 
 
 def max_conflicts(ctx: Context, upd: dict, q: dict) -> dict:

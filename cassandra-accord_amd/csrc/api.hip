@@ -21,6 +21,7 @@ void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *vie
 void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
 void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in);
 void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view);
 void max_conflicts(acc_ctx *ctx, const acc_conflicts_in *u, const acc_preaccept_in *q, acc_preaccept_out *out);
 void cfk_view(acc_cfk *cfk, acc_batch_in *out);
 void cfk_free(acc_cfk *cfk);
@@ -463,6 +464,15 @@ int acc_cfk_apply(acc_ctx *ctx, const acc_cfk_snap *snap, const acc_cfk_updates 
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         acc::cfk_apply(ctx, snap, updates, out_view);
+    });
+}
+
+int acc_cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *snap, acc_cfk_batch_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::cfk_snap_to_batch(ctx, snap, out_view);
     });
 }
 

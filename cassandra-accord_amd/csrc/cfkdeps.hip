@@ -621,7 +621,202 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
     if (i < n) out[i] = in[i];
 }
 
+// ---- the key-major state as the txn-major snapshot of acc_map_reduce_full (acc_cfk_snap_to_batch)
+// Entries are sorted by TxnId with three stable radix sorts (node, then lsb's identity bits, then msb: the Timestamp
+// order of cmp); entries of one TxnId keep key order, so each txn's keys come out sorted.
+__global__ __launch_bounds__(BLOCK) void k_cb_node(uint64_t NE, const int32_t *__restrict__ en, uint64_t *__restrict__ k)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < NE) k[i] = (uint32_t)en[i] ^ 0x80000000u;
+}
+__global__ __launch_bounds__(BLOCK) void k_cb_lsb(uint64_t NE, const uint32_t *__restrict__ perm, const uint64_t *__restrict__ el,
+                                                  uint64_t *__restrict__ k)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < NE) {
+        const uint64_t l = el[perm[i]];
+        k[i] = ((l >> 16) << 4) | ((l >> 1) & 0xFu);   // the 52 bits of l & IDENTITY_LSB, order kept
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_cb_msb(uint64_t NE, const uint32_t *__restrict__ perm, const uint64_t *__restrict__ em,
+                                                  uint64_t *__restrict__ k)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < NE) k[i] = em[perm[i]];
+}
+// owner key of every entry (upper bound in ent_off)
+__global__ __launch_bounds__(BLOCK) void k_cb_owner(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ ent_off,
+                                                    uint32_t *__restrict__ owner)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= NE) return;
+    uint32_t lo = 0, hi = nk;   // first k with ent_off[k+1] > e
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ent_off[mid + 1] > e) hi = mid; else lo = mid + 1;
+    }
+    owner[e] = lo;
+}
+// first-of-TxnId flags; later entries of a TxnId must carry its executeAt and InternalStatus
+__global__ __launch_bounds__(BLOCK) void k_cb_flag(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
+                                                   const uint32_t *__restrict__ owner, uint32_t *__restrict__ flag,
+                                                   uint64_t *__restrict__ err)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= NE) return;
+    const uint32_t e = perm[i];
+    uint32_t f = 1;
+    if (i > 0) {
+        const uint32_t p = perm[i - 1];
+        if (cmp(Ts{ s.em[e], s.el[e], s.en[e] }, Ts{ s.em[p], s.el[p], s.en[p] }) == 0) {
+            f = 0;
+            uint64_t bad = 0;
+            if (s.st[e] != s.st[p] || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ s.xm[p], s.xl[p], s.xn[p] }) != 0) bad |= E_STATE;
+            if (owner[e] <= owner[p]) bad |= E_ARG_SORT;
+            if (bad) atomicOr((unsigned long long *)err, (unsigned long long)bad);
+        }
+    }
+    flag[i] = f;
+}
+struct BatchOut {
+    uint64_t *tm, *tl, *xm, *xl, *kc;
+    int32_t *tn, *xn;
+    uint8_t *st;
+    uint32_t *ko, *mcnt;
+};
+__global__ __launch_bounds__(BLOCK) void k_cb_txn(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
+                                                  const uint32_t *__restrict__ owner, const uint32_t *__restrict__ flag,
+                                                  const uint32_t *__restrict__ tinc, BatchOut b)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= NE) return;
+    const uint32_t e = perm[i];
+    b.kc[i] = s.key[owner[e]];
+    b.mcnt[i] = s.miss_off[e + 1] - s.miss_off[e];
+    if (flag[i]) {
+        const uint32_t t = tinc[i] - 1;
+        b.tm[t] = s.em[e]; b.tl[t] = s.el[e]; b.tn[t] = s.en[e];
+        b.xm[t] = s.xm[e]; b.xl[t] = s.xl[e]; b.xn[t] = s.xn[e];
+        b.st[t] = s.st[e];
+        b.ko[t] = (uint32_t)i;
+    }
+    if (i + 1 == NE) b.ko[tinc[i]] = (uint32_t)NE;
+}
+// each pair's missing[] TxnIds as batch indices (binary search over the batch's TxnIds)
+__global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
+                                                   const uint32_t *__restrict__ tinc, BatchOut b,
+                                                   const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
+                                                   uint64_t *__restrict__ err)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= NE) return;
+    const uint32_t e = perm[i], n = tinc[NE - 1];
+    const uint32_t m0 = s.miss_off[e], m1 = s.miss_off[e + 1];
+    uint32_t w = mo[i];
+    for (uint32_t j = m0; j < m1; ++j) {
+        const Ts k{ s.mm[j], s.ml[j], s.mn[j] };
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cmp(Ts{ b.tm[mid], b.tl[mid], b.tn[mid] }, k) < 0) lo = mid + 1; else hi = mid;
+        }
+        if (lo == n || cmp(Ts{ b.tm[lo], b.tl[lo], b.tn[lo] }, k) != 0) {
+            atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
+            lo = 0;
+        }
+        if (j > m0 && lo <= mt[w - 1]) atomicOr((unsigned long long *)err, (unsigned long long)E_ARG_SORT);
+        mt[w++] = lo;
+    }
+}
+
 }  // namespace cd
+
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view)
+{
+    using namespace cd;
+    if (!in || !view) fail(ACC_E_ARG, "null argument");
+    if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
+    hipStream_t st = ctx->stream;
+    const uint32_t nk = in->n_keys;
+    const uint64_t NE = in->n_entries, NM = in->n_missing;
+    if (nk == 0 && (NE || NM)) fail(ACC_E_ARG, "entries without keys");
+    if (NE >= 0xFFFFFFFFull || NM >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 entries / missing");
+    Snap s{};
+    s.key = stage_in(ctx, "cb_skey", in->key, nk, in->mem);
+    s.ent_off = stage_in(ctx, "cb_soff", in->ent_off, (size_t)nk + 1, in->mem);
+    s.em = stage_in(ctx, "cb_sem", in->txn_id.msb, NE, in->mem);
+    s.el = stage_in(ctx, "cb_sel", in->txn_id.lsb, NE, in->mem);
+    s.en = stage_in(ctx, "cb_sen", in->txn_id.node, NE, in->mem);
+    s.xm = stage_in(ctx, "cb_sxm", in->execute_at.msb, NE, in->mem);
+    s.xl = stage_in(ctx, "cb_sxl", in->execute_at.lsb, NE, in->mem);
+    s.xn = stage_in(ctx, "cb_sxn", in->execute_at.node, NE, in->mem);
+    s.st = stage_in(ctx, "cb_sst", in->status, NE, in->mem);
+    s.miss_off = stage_in(ctx, "cb_smoff", in->miss_off, NE + 1, in->mem);
+    s.mm = stage_in(ctx, "cb_smm", in->missing.msb, NM, in->mem);
+    s.ml = stage_in(ctx, "cb_sml", in->missing.lsb, NM, in->mem);
+    s.mn = stage_in(ctx, "cb_smn", in->missing.node, NM, in->mem);
+    s.n_keys = nk; s.n_ent = NE; s.n_miss = NM;
+    uint64_t *errs = ctx->get<uint64_t>("cb_errs", 1);
+    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+    BatchOut b{};
+    b.tm = ctx->get<uint64_t>("cb_tm", NE); b.tl = ctx->get<uint64_t>("cb_tl", NE); b.tn = ctx->get<int32_t>("cb_tn", NE);
+    b.xm = ctx->get<uint64_t>("cb_xm", NE); b.xl = ctx->get<uint64_t>("cb_xl", NE); b.xn = ctx->get<int32_t>("cb_xn", NE);
+    b.st = ctx->get<uint8_t>("cb_st", NE);
+    b.ko = ctx->get<uint32_t>("cb_ko", NE + 1);
+    b.kc = ctx->get<uint64_t>("cb_kc", NE);
+    b.mcnt = ctx->get<uint32_t>("cb_mcnt", NE);
+    uint32_t *mo = ctx->get<uint32_t>("cb_mo", NE + 1), *mt = ctx->get<uint32_t>("cb_mt", NM);
+    uint32_t n_txn = 0;
+    if (NE == 0) {
+        ACC_HIP(hipMemsetAsync(b.ko, 0, 4, st));
+        ACC_HIP(hipMemsetAsync(mo, 0, 4, st));
+        ctx->sync();
+    } else {
+        Upd none{};
+        launch(ctx, "cb_check", k_cd_check, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, s, none, (uint32_t *)nullptr, errs);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        if (ctx->pinned[0] & E_ARG_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal");
+        if (ctx->pinned[0] & E_ARG_OFF) fail(ACC_E_ARG, "offsets must be non-decreasing from 0 to their totals");
+        if (ctx->pinned[0] & E_ARG_SORT) fail(ACC_E_ARG, "keys / TxnIds must be sorted unique");
+        const dim3 g(grid_for(NE, BLOCK));
+        uint64_t *k = ctx->get<uint64_t>("cb_key", NE);
+        uint32_t *owner = ctx->get<uint32_t>("cb_owner", NE), *flag = ctx->get<uint32_t>("cb_flag", NE);
+        uint32_t *tinc = ctx->get<uint32_t>("cb_tinc", NE);
+        launch(ctx, "cb_node", k_cb_node, g, dim3(BLOCK), 0, NE, s.en, k);
+        Sorted r = radix_sort(ctx, "cb_rs1", k, nullptr, NE, 32);
+        launch(ctx, "cb_lsb", k_cb_lsb, g, dim3(BLOCK), 0, NE, (const uint32_t *)r.vals, s.el, k);
+        r = radix_sort(ctx, "cb_rs2", k, r.vals, NE, 52);
+        launch(ctx, "cb_msb", k_cb_msb, g, dim3(BLOCK), 0, NE, (const uint32_t *)r.vals, s.em, k);
+        r = radix_sort(ctx, "cb_rs3", k, r.vals, NE, 64);
+        const uint32_t *perm = r.vals;
+        launch(ctx, "cb_owner", k_cb_owner, g, dim3(BLOCK), 0, NE, nk, s.ent_off, owner);
+        launch(ctx, "cb_flag", k_cb_flag, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)owner, flag, errs);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, tinc, NE, false);
+        launch(ctx, "cb_txn", k_cb_txn, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)owner, (const uint32_t *)flag,
+               (const uint32_t *)tinc, b);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, b.mcnt, mo, NE, true, mo + NE);
+        if (NM)
+            launch(ctx, "cb_miss", k_cb_miss, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)tinc, b, (const uint32_t *)mo, mt, errs);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, tinc + NE - 1, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        const uint64_t e = ctx->pinned[0];
+        if (e & E_STATE)
+            fail(ACC_E_STATE, "a TxnId with different executeAt / InternalStatus on two keys, or a missing[] TxnId "
+                              "that is no CommandsForKey entry");
+        if (e & E_ARG_SORT) fail(ACC_E_ARG, "a TxnId twice on one key, or a missing[] not sorted unique");
+        n_txn = (uint32_t)(ctx->pinned[1] & 0xFFFFFFFFu);
+    }
+    ctx->stat("cfk_batch.txns", n_txn);
+    ctx->stat("cfk_batch.pairs", NE);
+    acc_batch_in &o = view->batch;
+    o.n_txn = n_txn; o.mem = ACC_MEM_DEVICE; o.n_pairs = NE;
+    o.txn_id = acc_ts_cols{ b.tm, b.tl, b.tn };
+    o.execute_at = acc_ts_cols{ b.xm, b.xl, b.xn };
+    o.status = b.st; o.key_off = b.ko; o.key_code = b.kc;
+    view->missing_off = mo; view->missing_txn = mt; view->n_missing = NM;
+}
 
 void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view)
 {

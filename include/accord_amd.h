@@ -752,6 +752,23 @@ typedef struct acc_cfk_snap_view {
 
 int  acc_cfk_apply(acc_ctx *ctx, const acc_cfk_snap *snap, const acc_cfk_updates *updates, acc_cfk_snap_view *out_view);
 
+/* The key-major CommandsForKey state as the txn-major snapshot acc_map_reduce_full scans, without leaving HBM (the
+ * recovery scan of SafeCommandStore.mapReduceFull reads the store's CFKs, local/CommandsForKey.java:553-612): each
+ * distinct TxnId of snap is one batch txn (TxnId order) whose keys are the keys holding it, with the executeAt and
+ * InternalStatus its TxnInfos carry — equal on every key, as a store's CFKs all see the command's one status, else
+ * ACC_E_STATE — and each (txn, key) pair's TxnInfoWithMissing.missing becomes batch indices (a missing TxnId that is no
+ * entry of the store: ACC_E_STATE). snap may be an acc_cfk_apply result (mem = ACC_MEM_DEVICE). The output is DEVICE
+ * memory owned by the context, valid until the next acc_cfk_snap_to_batch; acc_map_reduce_full reads it in place
+ * (its acc_recovery_in with mem = ACC_MEM_DEVICE and this missing_off / missing_txn). */
+typedef struct acc_cfk_batch_view {
+    acc_batch_in    batch;        /* mem = ACC_MEM_DEVICE */
+    const uint32_t *missing_off;  /* [batch.n_pairs+1] */
+    const uint32_t *missing_txn;  /* [n_missing] batch indices, sorted per pair */
+    uint64_t        n_missing;
+} acc_cfk_batch_view;
+
+int  acc_cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *snap, acc_cfk_batch_view *out_view);
+
 /* ---- MaxConflicts and the PreAccept executeAt proposal (local/MaxConflicts.java:31-96,
  * local/CommandStore.java:280-290 updateMaxConflicts, :320-345 preaccept) ----
  * A CommandStore's MaxConflicts is the pointwise max of every (keysOrRanges, executeAt) update it received

@@ -197,3 +197,71 @@ def conflicts_case(seed, n_upd=500, n_query=300, span=4000, p_range=0.3, end_inc
              is_range=np.array(qr, np.uint8), part_off=np.array(qo, np.uint32), part_start=np.array(ps, np.uint64),
              part_end=np.array(pe, np.uint64))
     return upd, q
+
+
+def snap_as_batch(snap):
+    """The key-major CFK state as the txn-major snapshot acc_map_reduce_full scans, restated on the host (what
+    acc_cfk_snap_to_batch builds): one txn per distinct TxnId in TxnId order, its keys = the keys holding it, its
+    executeAt / InternalStatus from its first key (all must agree), each pair's missing[] as batch indices.
+    Returns (Batch, missing_off, missing_txn)."""
+    nk = len(snap["key"])
+    off = snap["ent_off"].astype(np.int64)
+    owner = np.repeat(np.arange(nk), np.diff(off))
+    tk = [_ts_key(int(m), int(l), int(n)) for m, l, n in zip(snap["emsb"], snap["elsb"], snap["enode"])]
+    order = sorted(range(len(tk)), key=lambda e: (tk[e], owner[e]))
+    first, key_off, key_code, pairs = [], [], [], []
+    for i, e in enumerate(order):
+        if i == 0 or tk[e] != tk[order[i - 1]]:
+            first.append(e)
+            key_off.append(i)
+        else:
+            p = first[-1]
+            assert snap["status"][e] == snap["status"][p]
+            assert _ts_key(int(snap["xmsb"][e]), int(snap["xlsb"][e]), int(snap["xnode"][e])) == \
+                _ts_key(int(snap["xmsb"][p]), int(snap["xlsb"][p]), int(snap["xnode"][p]))
+        key_code.append(int(snap["key"][owner[e]]))
+        pairs.append(e)
+    key_off.append(len(order))
+    index = {tk[e]: t for t, e in enumerate(first)}
+    mo, mt = [0], []
+    for e in pairs:
+        for j in range(int(snap["miss_off"][e]), int(snap["miss_off"][e + 1])):
+            mt.append(index[_ts_key(int(snap["mmsb"][j]), int(snap["mlsb"][j]), int(snap["mnode"][j]))])
+        mo.append(len(mt))
+    f = np.array(first, np.int64)
+    b = W.Batch(snap["emsb"][f].astype(np.uint64), snap["elsb"][f].astype(np.uint64), snap["enode"][f].astype(np.int32),
+                snap["xmsb"][f].astype(np.uint64), snap["xlsb"][f].astype(np.uint64), snap["xnode"][f].astype(np.int32),
+                snap["status"][f].astype(np.uint8), np.array(key_off, np.uint32), np.array(key_code, np.uint64))
+    return b, np.array(mo, np.uint32), np.array(mt, np.uint32)
+
+
+def recovery_queries(b, seed, n_query=80):
+    """BeginRecovery-style queries over a CFK state: a member's TxnId on its keys (plus maybe another key or one
+    without a CFK), a foreign TxnId on an odd hlc, or a bumped executeAt."""
+    rng = np.random.default_rng(seed)
+    n = b.n_txn
+    codes = np.unique(b.key_code) if len(b.key_code) else np.array([100], np.uint64)
+    qm, ql, qn, qo, qk = [], [], [], [0], []
+    for _ in range(n_query):
+        r = rng.random()
+        if r < 0.55 and n:
+            t = int(rng.integers(0, n))
+            m, l, nd = int(b.txn_msb[t]), int(b.txn_lsb[t]), int(b.txn_node[t])
+            ks = set(int(x) for x in b.key_code[int(b.key_off[t]):int(b.key_off[t + 1])])
+            if rng.random() < 0.4:
+                ks.add(int(rng.choice(codes)))
+            if rng.random() < 0.2:
+                ks.add(7)
+        elif r < 0.85 or not n:
+            m, l, nd = (int(x) for x in W.encode_ts(1, 2 * int(rng.integers(0, 4 * n + 8)) + 1,
+                                                    int(rng.choice(KINDS)) << 1, 1 + int(rng.integers(0, 4))))
+            ks = set(int(x) for x in rng.choice(codes, size=min(len(codes), int(rng.integers(1, 5))), replace=False))
+        else:
+            t = int(rng.integers(0, n))
+            m, l, nd = int(b.exe_msb[t]), int(b.exe_lsb[t]), int(b.exe_node[t])
+            ks = set(int(x) for x in rng.choice(codes, size=min(len(codes), int(rng.integers(1, 5))), replace=False))
+        qm.append(m); ql.append(l); qn.append(nd)
+        qk.extend(sorted(ks))
+        qo.append(len(qk))
+    return dict(msb=np.array(qm, np.uint64), lsb=np.array(ql, np.uint64), node=np.array(qn, np.int32),
+                key_off=np.array(qo, np.uint32), key_code=np.array(qk, np.uint64))

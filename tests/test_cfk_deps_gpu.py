@@ -108,3 +108,65 @@ def test_max_conflicts_empty(ctx):
     bad["key"] = upd["key"][::-1].copy()
     with pytest.raises(IllegalArgumentException):
         max_conflicts(ctx, bad, q)
+
+
+FIELDS = ("arena_off", "arena", "kd_off", "key_idx", "u_off", "dep_txn")
+
+
+@pytest.mark.parametrize("seed,n_txn,n_keys", [(4, 160, 10), (6, 1500, 40)])
+def test_cfk_recovery_in_place(ctx, seed, n_txn, n_keys):
+    """acc_cfk_apply -> acc_cfk_snap_to_batch -> acc_map_reduce_full with nothing leaving HBM, against the C
+    restatements on the host restatement of the same conversion: the txn-major snapshot and missing[] indices bit for
+    bit, then every TestStartedAt x TestDep x TestStatus scan."""
+    import recovery_cases as RC
+    from accord_amd.deps import cfk_apply, cfk_batch_host, cfk_map_reduce_full, cfk_snap_to_batch
+    upd = CC.cfk_case(seed, n_txn=n_txn, n_keys=n_keys)
+    seen = 0
+    for frac in (0.4, 1.0):
+        head, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
+        v = cfk_apply(ctx, CC.empty_snapshot(), head, keep_device=True)
+        bv = cfk_snap_to_batch(ctx, v)
+        b, mo, mt = CC.snap_as_batch(oracle.cfk_apply(CC.empty_snapshot(), head))
+        gb, gmo, gmt = cfk_batch_host(ctx, bv)
+        for f in ("txn_msb", "txn_lsb", "txn_node", "exe_msb", "exe_lsb", "exe_node", "status", "key_off", "key_code"):
+            np.testing.assert_array_equal(getattr(gb, f), getattr(b, f), err_msg=f)
+        np.testing.assert_array_equal(gmo, mo)
+        np.testing.assert_array_equal(gmt, mt)
+        seen += len(mt)
+        q = CC.recovery_queries(b, seed, 120)
+        for sa, td, ts in RC.ALL_TESTS:
+            g = cfk_map_reduce_full(ctx, bv, q, sa, td, ts)
+            o = oracle.map_reduce_full(b, mo, mt, q, sa, td, ts)
+            for f in FIELDS:
+                np.testing.assert_array_equal(getattr(g, f), getattr(o, f), err_msg=f"{frac} {f} {(sa, td, ts)}")
+    assert seen
+
+
+def test_cfk_snap_to_batch_errors(ctx):
+    from accord_amd.deps import IllegalArgumentException, IllegalStateException, cfk_snap_to_batch
+    upd = CC.cfk_case(7, n_txn=80, n_keys=6)
+    snap = oracle.cfk_apply(CC.empty_snapshot(), upd)
+    e = cfk_snap_to_batch(ctx, CC.empty_snapshot())
+    assert e.batch.n_txn == 0 and e.batch.n_pairs == 0
+    ok = cfk_snap_to_batch(ctx, snap)
+    assert ok.batch.n_pairs == len(snap["status"])
+    # one TxnId with two statuses on two keys
+    b, _, _ = CC.snap_as_batch(snap)
+    t = int(np.nonzero(np.diff(b.key_off.astype(np.int64)) > 1)[0][0])
+    tid = (b.txn_msb[t], b.txn_lsb[t], b.txn_node[t])
+    e0 = [i for i in range(len(snap["status"])) if (snap["emsb"][i], snap["elsb"][i], snap["enode"][i]) == tid][0]
+    bad = {k: v.copy() for k, v in snap.items()}
+    bad["status"][e0] = CC.INVALID if bad["status"][e0] != CC.INVALID else CC.APPLIED
+    with pytest.raises(IllegalStateException):
+        cfk_snap_to_batch(ctx, bad)
+    # a missing[] TxnId that is no entry of the store
+    if len(snap["mmsb"]):
+        bad = {k: v.copy() for k, v in snap.items()}
+        bad["mlsb"][0] = np.uint64(int(bad["mlsb"][0]) ^ (1 << 17))
+        with pytest.raises(IllegalStateException):
+            cfk_snap_to_batch(ctx, bad)
+    bad = {k: v.copy() for k, v in snap.items()}
+    bad["ent_off"][1] = bad["ent_off"][-1] + 1
+    with pytest.raises(IllegalArgumentException):
+        cfk_snap_to_batch(ctx, bad)
+    assert cfk_snap_to_batch(ctx, snap).batch.n_txn == ok.batch.n_txn   # the context stays usable

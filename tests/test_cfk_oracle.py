@@ -91,3 +91,27 @@ def test_max_conflicts_is_a_max_over_intersections():
         w = (int(whole["msb"][i]), int(whole["lsb"][i]) >> 16, int(whole["node"][i]))
         assert max(a, b) == w
     assert 0 < int(whole["fast"].sum()) < len(q["msb"])
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_recovery_scan_over_cfk_state(seed):
+    """The recovery scans over the state CommandsForKey.update built (missing[] from the deps, TRANSITIVELY_KNOWN
+    entries, bumped executeAts): the C restatement of mapReduceFull agrees with the set model on it, mid-sequence and
+    at the end, and every TxnId carries one status on all its keys (what acc_cfk_snap_to_batch relies on)."""
+    import canonical
+    import recovery_cases as RC
+    upd = CC.cfk_case(seed, n_txn=160, n_keys=10)
+    seen_missing = seen_tk = 0
+    for frac in (0.3, 0.6, 1.0):
+        head, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
+        snap = oracle.cfk_apply(CC.empty_snapshot(), head)
+        b, mo, mt = CC.snap_as_batch(snap)
+        seen_missing += len(mt)
+        seen_tk += int((b.status == CC.TK).sum())
+        q = CC.recovery_queries(b, seed, 50)
+        nq = len(q["msb"])
+        for sa, td, ts in RC.ALL_TESTS:
+            o = oracle.map_reduce_full(b, mo, mt, q, sa, td, ts)
+            c = canonical.map_reduce_full(b, mo, mt, q, sa, td, ts)
+            assert RC.canonical_rows(o, nq) == c, (frac, sa, td, ts)
+    assert seen_missing and seen_tk
