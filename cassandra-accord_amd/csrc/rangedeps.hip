@@ -30,7 +30,13 @@ namespace acc {
 namespace rd {
 
 constexpr int NCLS = 33;          // width classes 0..32 (4^32 = 2^64 covers every u64 width)
-constexpr int TILE = 1024;        // entries per LDS tile in the stabbing pass
+#ifndef ACC_RD_TILE
+#define ACC_RD_TILE 512
+#endif
+#ifndef ACC_RD_POOL
+#define ACC_RD_POOL 2048
+#endif
+constexpr int TILE = ACC_RD_TILE;   // entries per LDS tile in the stabbing pass
 constexpr uint32_t BLOCK_E = 8192;  // workgroup tier (LDS)
 
 enum : uint64_t {
@@ -274,11 +280,24 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
     qkey[q] = pext_runs(r.lo, plan);
 }
 
+// sorted records, and per block of BLOCK sorted queries (the stabbing blocks) the largest high bound
 __global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Q, const uint32_t *__restrict__ perm, const QRec *__restrict__ rec,
-                                                    QRec *__restrict__ srec)
+                                                    QRec *__restrict__ srec, uint64_t *__restrict__ bhi)
 {
+    __shared__ uint64_t wh[WAVES];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < Q) srec[i] = rec[perm[i]];
+    uint64_t h = 0;
+    if (i < Q) { const QRec r = rec[perm[i]]; srec[i] = r; h = r.hi; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = shfl_xor(h, d); h = o > h ? o : h; }
+    if (lane_id() == 0) wh[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t m = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) m = wh[w] > m ? wh[w] : m;
+        bhi[blockIdx.x] = m;
+    }
 }
 
 // ---------------------------------------------------------------- stabbing
@@ -291,6 +310,7 @@ struct View {
     const uint2 *cs_info;         // (range id, TxnId position)
     const uint8_t *cs_kind;
     const uint32_t *class_off;    // [NCLS + 1]
+    const uint32_t *win;          // per block: b0[NCLS], b1[NCLS] (k_rd_stab_win)
     uint64_t *cursor;             // global output cursor
     uint64_t cap;                 // capacity of ent
     uint64_t *ent;                // (range id << 32 | TxnId position) per emitted pair
@@ -342,6 +362,7 @@ struct StabTile {
     uint64_t hi[WAVES];
     uint64_t lo;
     uint32_t b0[NCLS], b1[NCLS];   // the block's window per width class
+    uint32_t pre[NCLS + 1];        // flat tile: class c at [pre[c], pre[c + 1])
     uint32_t red[WAVES];
     uint64_t base;
 };
@@ -381,8 +402,8 @@ __device__ __forceinline__ void stab_next(const StabTile &T, uint32_t &c, uint32
 }
 
 template <bool EMIT>
-__device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t lo_min,
-                                              uint64_t hi_max, uint64_t out)
+__device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
+                                              uint64_t *stage)
 {
     const uint32_t tid = threadIdx.x;
     const bool isr = (r.flags >> 8) & 1u;
@@ -420,7 +441,10 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
                 const uint2 info = T.info[k];
                 if (info.y >= r.lim || info.y == r.tpos) continue;            // STARTED_BEFORE; p1
                 if (!((wm >> T.kind[k]) & 1u)) continue;                      // testKind
-                if (EMIT) v.ent[out + count] = ((uint64_t)info.x << 32) | info.y;
+                if (EMIT) {
+                    const uint64_t x = ((uint64_t)info.x << 32) | info.y;
+                    if (stage) stage[out + count] = x; else v.ent[out + count] = x;
+                }
                 ++count;
             }
         }
@@ -430,48 +454,141 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
     return count;
 }
 
-// A workgroup of 256 consecutive (sorted) queries: count every query's pairs over the block's windows, take one
-// slice of the output with one atomic, then emit (the windows' tiles are re-read, L2-warm). Each query's pairs
-// land contiguously at q_off[q].
+// The stabbing blocks' windows: one thread per (block, width class) and bound, a plain binary search over the class's
+// starts (starts in [lo_min - 4^c, hi_max] for the block's sorted queries). Thousands of independent searches keep the
+// loads in flight, where a search inside the stabbing block would stall it for every dependent round.
+__global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const QRec *__restrict__ srec,
+                                                       const uint64_t *__restrict__ bhi, View v, uint32_t *__restrict__ win)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= (uint64_t)nsb * NCLS) return;
+    const uint32_t blk = (uint32_t)(g / NCLS), c = (uint32_t)(g % NCLS);
+    const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
+    uint32_t b0 = a0, b1 = a0;
+    if (a1 > a0) {
+        const uint64_t lo = srec[(size_t)blk * BLOCK].lo, hi = bhi[blk], W = class_width(c);
+        b0 = lower_bound_s(v.cs_s, a0, a1, lo > W ? lo - W : 0);
+        b1 = upper_bound_s(v.cs_s, b0, a1, hi);
+    }
+    win[(size_t)blk * 2 * NCLS + c] = b0;
+    win[(size_t)blk * 2 * NCLS + NCLS + c] = b1;
+}
+
+// Every class's window of the block in one tile (when they fit TILE together): one load round for the block.
+// Count pass (pool != null): each hit is also appended to the block's LDS pool (wave-aggregated slot claims) with its
+// thread, so a block whose hits fit the pool needs no second scan. Emit pass: hits to ent at out.
+constexpr uint32_t POOL = ACC_RD_POOL;
+struct StabPool {
+    uint64_t x[POOL];
+    uint8_t q[POOL];
+    uint32_t n;
+    uint32_t cur[BLOCK];
+};
+
+template <bool EMIT>
+__device__ __forceinline__ uint32_t stab_flat(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
+                                              StabPool *pool)
+{
+    uint32_t count = 0;
+    if (!valid) return 0;
+    const bool isr = (r.flags >> 8) & 1u;
+    const uint32_t wm = r.flags & 0xFFu;
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
+        const uint32_t p0 = T.pre[c], p1 = T.pre[c + 1];
+        if (p0 == p1) continue;
+        const uint64_t W = class_width(c);
+        const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
+        for (uint32_t k = lower_bound_s(T.s, p0, p1, qwlo); k < p1; ++k) {
+            const uint64_t s = T.s[k];
+            if (s > r.hi) break;
+            const uint64_t e = T.e[k];
+            bool hit;
+            if (isr) hit = s < r.hi && e > r.lo;                           // Range.compareIntersecting == 0
+            else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;         // EndInclusive.contains (s, e]
+            else hit = s <= r.lo && r.lo < e;                              // StartInclusive.contains [s, e)
+            const uint2 info = T.info[k];
+            hit = hit && info.y < r.lim && info.y != r.tpos                // STARTED_BEFORE; p1
+                  && ((wm >> T.kind[k]) & 1u);                             // testKind
+            const uint64_t x = ((uint64_t)info.x << 32) | info.y;
+            if (EMIT) {
+                if (hit) v.ent[out + count] = x;
+            } else if (pool) {
+                const uint64_t bm = __ballot(hit);
+                if (bm) {
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(bm);
+                    uint32_t b = 0;
+                    if (lane == leader) b = atomicAdd(&pool->n, (uint32_t)__popcll(bm));
+                    b = __shfl(b, (int)leader, 64);
+                    const uint32_t slot = b + (uint32_t)__popcll(bm & lt);
+                    if (hit && slot < POOL) { pool->x[slot] = x; pool->q[slot] = (uint8_t)threadIdx.x; }
+                }
+            }
+            count += hit ? 1u : 0u;
+        }
+    }
+    return count;
+}
+
+// A workgroup of BLOCK consecutive (sorted) queries over its precomputed windows: count every query's pairs, take the
+// block's output slice with one atomic, write them. When the windows fit one tile they are loaded once, and when the
+// block's hits fit the LDS pool the count pass has already gathered them: they are placed into each query's run of the
+// slice (a per-query cursor) with no second scan. Otherwise the (class, tile) sequence is scanned again to emit.
 __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
 {
     __shared__ StabTile T;
+    __shared__ StabPool pool;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * BLOCK + tid;
     const bool valid = i < v.Q;
     QRec r{};
     if (valid) r = v.srec[i];
-    uint64_t h = valid ? r.hi : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = shfl_xor(h, d); h = o > h ? o : h; }
-    if (lane_id() == 0) T.hi[tid >> 6] = h;
-    if (tid == 0) T.lo = r.lo;   // sorted: thread 0 holds the block's smallest low bound
+    if (tid < (uint32_t)NCLS) {
+        T.b0[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + tid];
+        T.b1[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + NCLS + tid];
+    }
+    if (tid == 0) pool.n = 0;
     __syncthreads();
-    uint64_t hi_max = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) hi_max = T.hi[w] > hi_max ? T.hi[w] : hi_max;
-    const uint64_t lo_min = T.lo;
-    // the block's window per class (starts in [lo_min - 4^c, hi_max]): wave w searches classes w, w + 4, ...
-    for (uint32_t c = tid >> 6; c < (uint32_t)NCLS; c += WAVES) {
-        const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
-        uint32_t b0 = a0, b1 = a0;
-        if (a1 > a0) {
-            const uint64_t W = class_width(c);
-            b0 = wave_search(v.cs_s, a0, a1, lo_min > W ? lo_min - W : 0, false);
-            b1 = wave_search(v.cs_s, b0, a1, hi_max, true);
-        }
-        if (lane_id() == 0) { T.b0[c] = b0; T.b1[c] = b1; }
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (int c = 0; c < NCLS; ++c) { T.pre[c] = a; a += T.b1[c] - T.b0[c]; }
+        T.pre[NCLS] = a;
     }
     __syncthreads();
-    const uint32_t count = stab_pass<false>(v, T, valid, r, lo_min, hi_max, 0);
+    const uint32_t wtot = T.pre[NCLS];
+    const bool flat = wtot <= (uint32_t)TILE;
+    uint32_t count;
+    if (flat) {
+        for (uint32_t k = tid; k < wtot; k += BLOCK) {
+            uint32_t lo = 0, hi = NCLS;   // the class holding flat position k: last c with pre[c] <= k
+            while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (T.pre[md] <= k) lo = md; else hi = md; }
+            const uint32_t src = T.b0[lo] + (k - T.pre[lo]);
+            T.s[k] = v.cs_s[src]; T.e[k] = v.cs_e[src]; T.info[k] = v.cs_info[src]; T.kind[k] = v.cs_kind[src];
+        }
+        __syncthreads();
+        count = stab_flat<false>(v, T, valid, r, 0, &pool);
+    } else {
+        count = stab_pass<false>(v, T, valid, r, 0, nullptr);
+    }
     uint32_t total;
     const uint32_t mine = block_exclusive(count, OpAdd<uint32_t>(), T.red, total);
     if (tid == 0) T.base = atomicAdd((unsigned long long *)v.cursor, (unsigned long long)total);
+    pool.cur[tid] = mine;
     __syncthreads();
     const uint64_t base = T.base;
     if (valid) { v.q_off[r.q] = base + mine; v.q_cnt[r.q] = count; }
     if (base + total > v.cap) return;   // uniform: the host re-runs with a larger capacity
-    stab_pass<true>(v, T, valid, r, lo_min, hi_max, base + mine);
+    if (flat && total <= POOL) {
+        for (uint32_t k = tid; k < total; k += BLOCK) {
+            const uint32_t pos = atomicAdd(&pool.cur[pool.q[k]], 1u);
+            v.ent[base + pos] = pool.x[k];
+        }
+    } else if (flat) {
+        stab_flat<true>(v, T, valid, r, base + mine, nullptr);
+    } else {
+        stab_pass<true>(v, T, valid, r, base + mine, nullptr);
+    }
 }
 
 // ---------------------------------------------------------------- per-txn build
@@ -515,10 +632,12 @@ __global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t 
     uint64_t m = 0;
     for (uint32_t q = q0; q < q1; ++q) m += o.q_cnt[q];
     m_raw[t] = m;
-    // tiers: 0 none, 1 <= 16 (16-lane groups), 2 <= 64 (wave), 3..9 LDS workgroups of 128..8192, 10 global
+    // tiers: 0 none, 1 <= 16 (16-lane groups), 11 <= 32 (half waves), 2 <= 64 (wave), 3..9 LDS workgroups of
+    // 128..8192, 10 global
     uint32_t tr;
     if (m == 0) tr = 0;
     else if (m <= 16) tr = 1;
+    else if (m <= 32) tr = 11;
     else if (m <= 64) tr = 2;
     else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
     else tr = 10;
@@ -537,7 +656,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_tier_hist(uint32_t n, const uint32
     if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
-// Groups of S lanes (S = 16 or 64), one txn each: load, sort (range id, TxnId position), dedupe, TxnId union and
+// Groups of S lanes (S = 16, 32 or 64), one txn each: load, sort (range id, TxnId position), dedupe, TxnId union and
 // index, range groups; results to the scratch regions of the txn.
 template <int S>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
@@ -978,28 +1097,37 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     launch(ctx, "rd_qrec", k_rd_qrec, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
            (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey);
     Sorted qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, q_plan.bits);
-    launch(ctx, "rd_qsort", k_rd_qsort, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, Q, (const uint32_t *)qs.vals,
-           (const QRec *)rec, srec);
+    const uint32_t nsb = (uint32_t)grid_for(Q, BLOCK);
+    uint64_t *bhi = ctx->get<uint64_t>("rd_bhi", nsb);
+    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Q, (const uint32_t *)qs.vals, (const QRec *)rec, srec, bhi);
     View v{};
     v.Q = Q; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
     v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
-    v.cursor = ctx->get<uint64_t>("rd_cursor", 1);
     v.q_off = ctx->get<uint64_t>("rd_q_off", Q);
     v.q_cnt = ctx->get<uint32_t>("rd_q_cnt", Q);
+    v.cursor = ctx->get<uint64_t>("rd_cursor", 1);
+    uint32_t *win = ctx->get<uint32_t>("rd_win", (size_t)nsb * 2 * NCLS);
+    v.win = win;
     uint64_t E = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        // capacity: the last batch's need on this context, at least 16 per query
-        const uint64_t want = std::max<uint64_t>(ctx->rd_ent_hint, 16ull * Q + 1024);
-        v.ent = ctx->get<uint64_t>("rd_ent", want);
-        v.cap = ctx->bufs["rd_ent"].bytes / sizeof(uint64_t);
-        ACC_HIP(hipMemsetAsync(v.cursor, 0, 8, st));
-        launch(ctx, "rd_stab", k_rd_stab, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, v);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, v.cursor, 8, hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        E = ctx->pinned[0];
-        ctx->rd_ent_hint = std::max(ctx->rd_ent_hint, E);
-        if (E <= v.cap) break;
-        if (attempt == 1) fail(ACC_E_STATE, "internal: range-deps output grew between passes");
+    if (Q) {
+        launch(ctx, "rd_stab_win", k_rd_stab_win, dim3(grid_for((uint64_t)nsb * NCLS, BLOCK)), dim3(BLOCK), 0, nsb,
+               (const QRec *)srec, (const uint64_t *)bhi, v, win);
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            // capacity: the last batch's need on this context, at least 16 per query
+            const uint64_t want = std::max<uint64_t>(ctx->rd_ent_hint, 16ull * Q + 1024);
+            v.ent = ctx->get<uint64_t>("rd_ent", want);
+            v.cap = ctx->bufs["rd_ent"].bytes / sizeof(uint64_t);
+            ACC_HIP(hipMemsetAsync(v.cursor, 0, 8, st));
+            launch(ctx, "rd_stab", k_rd_stab, dim3(nsb), dim3(BLOCK), 0, v);
+            ACC_HIP(hipMemcpyAsync(ctx->pinned, v.cursor, 8, hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            E = ctx->pinned[0];
+            ctx->rd_ent_hint = std::max(ctx->rd_ent_hint, E);
+            if (E <= v.cap) break;
+            if (attempt == 1) fail(ACC_E_STATE, "internal: range-deps output grew between passes");
+        }
+    } else {
+        v.ent = ctx->get<uint64_t>("rd_ent", 0);
     }
 
     // ---- 4. per-txn RangeDeps: raw sizes and tiers, build into scratch, offsets, compaction
@@ -1041,6 +1169,11 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[1];
         launch(ctx, "rd_build_s16", k_rd_build_seg<16>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+    }
+    if (hh[11]) {
+        ctx->launch_stream = ctx->aux[0];
+        o.list = tl_sorted + toff[11];
+        launch(ctx, "rd_build_s32", k_rd_build_seg<32>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
     }
     uint64_t nblk = 0;
     ctx->launch_stream = ctx->aux[1];
@@ -1096,6 +1229,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     ctx->stat("rangedeps.queries", Q);
     ctx->stat("rangedeps.raw_entries", E);
     ctx->stat("rangedeps.s16_txns", hh[1]);
+    ctx->stat("rangedeps.s32_txns", hh[11]);
     ctx->stat("rangedeps.s64_txns", hh[2]);
     ctx->stat("rangedeps.block_txns", nblk);
     ctx->stat("rangedeps.global_txns", nglb);

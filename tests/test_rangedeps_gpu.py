@@ -54,6 +54,7 @@ def test_block_and_global_tiers(ctx):
     g = ctx.calculate_partial_range_deps(rb)
     st = ctx.stats()
     assert st["rangedeps.block_txns"] > 0 and st["rangedeps.s16_txns"] > 0 and st["rangedeps.s64_txns"] > 0
+    assert st["rangedeps.s32_txns"] > 0
     assert_same(g, oracle.rangedeps_batch(rb), "block tier")
     rb = rd_cases.global_tier(9000)
     g = ctx.calculate_partial_range_deps(rb)
