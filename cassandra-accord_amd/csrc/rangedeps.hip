@@ -31,12 +31,12 @@ namespace rd {
 
 constexpr int NCLS = 33;          // width classes 0..32 (4^32 = 2^64 covers every u64 width)
 #ifndef ACC_RD_TILE
-#define ACC_RD_TILE 512
+#define ACC_RD_TILE 256
 #endif
 #ifndef ACC_RD_POOL
-#define ACC_RD_POOL 2048
+#define ACC_RD_POOL 1024
 #endif
-constexpr int TILE = ACC_RD_TILE;   // entries per LDS tile in the stabbing pass
+constexpr int TILE = ACC_RD_TILE;   // entries per LDS tile in the stabbing pass (LDS per block sets the occupancy)
 constexpr uint32_t BLOCK_E = 8192;  // workgroup tier (LDS)
 
 enum : uint64_t {
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
                                                    const uint32_t *__restrict__ owner, const uint64_t *__restrict__ rs,
                                                    const uint64_t *__restrict__ re, const uint32_t *__restrict__ rowner,
                                                    const uint4 *__restrict__ tinfo, Runs plan, QRec *__restrict__ rec,
-                                                   uint64_t *__restrict__ qkey)
+                                                   uint64_t *__restrict__ qkey, uint32_t rbit)
 {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
     if (q >= P + R) return;
@@ -277,26 +277,46 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
     const uint4 ti = tinfo[t];
     r.lim = ti.x; r.tpos = ti.y; r.flags = ti.z | (ti.w << 8); r.q = q;
     rec[q] = r;
-    qkey[q] = pext_runs(r.lo, plan);
+    // range queries after the key queries (rbit < 64): a range query scans its whole span, so mixing the two in one
+    // wave would leave the key lanes idle behind it
+    qkey[q] = pext_runs(r.lo, plan) | (q >= P && rbit < 64 ? 1ull << rbit : 0ull);
 }
 
 // sorted records, and per block of BLOCK sorted queries (the stabbing blocks) the largest high bound
-__global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Q, const uint32_t *__restrict__ perm, const QRec *__restrict__ rec,
-                                                    QRec *__restrict__ srec, uint64_t *__restrict__ bhi)
+// Sorted position j of a range query lands at j + (Pp - P) (Pp = P rounded up to a block): no block mixes key and
+// range queries, so no block's window spans both sorted runs. The gap holds PAD records.
+constexpr uint32_t QPAD = 1u << 31;
+__global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uint32_t Pp, const uint32_t *__restrict__ perm,
+                                                    const QRec *__restrict__ rec, QRec *__restrict__ srec,
+                                                    uint64_t *__restrict__ blo, uint64_t *__restrict__ bhi)
 {
-    __shared__ uint64_t wh[WAVES];
+    __shared__ uint64_t wh[WAVES], wl[WAVES];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    uint64_t h = 0;
-    if (i < Q) { const QRec r = rec[perm[i]]; srec[i] = r; h = r.hi; }
+    uint64_t h = 0, l = ~0ull;
+    if (i < Qp) {
+        if (i >= P && i < Pp) {
+            QRec r{};
+            r.flags = QPAD;
+            srec[i] = r;
+        } else {
+            const QRec r = rec[perm[i < P ? i : i - (Pp - P)]];
+            srec[i] = r; h = r.hi; l = r.lo;
+        }
+    }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = shfl_xor(h, d); h = o > h ? o : h; }
-    if (lane_id() == 0) wh[threadIdx.x >> 6] = h;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = shfl_xor(h, d), p = shfl_xor(l, d);
+        h = o > h ? o : h;
+        l = p < l ? p : l;
+    }
+    if (lane_id() == 0) { wh[threadIdx.x >> 6] = h; wl[threadIdx.x >> 6] = l; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint64_t m = 0;
+        uint64_t m = 0, n = ~0ull;
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) m = wh[w] > m ? wh[w] : m;
+        for (int w = 0; w < WAVES; ++w) { m = wh[w] > m ? wh[w] : m; n = wl[w] < n ? wl[w] : n; }
         bhi[blockIdx.x] = m;
+        blo[blockIdx.x] = n;
     }
 }
 
@@ -371,6 +391,7 @@ struct StabTile {
 // (class, tile) sequence is software-pipelined: the next tile's entries are loaded into registers while the current
 // one is scanned from LDS, so a block pays one memory latency per pass instead of one per tile.
 constexpr int ST_PT = TILE / BLOCK;   // tile entries per thread
+static_assert(TILE >= BLOCK && TILE % BLOCK == 0, "a tile is whole rounds of the block");
 
 struct StabRegs {
     uint64_t s[ST_PT], e[ST_PT];
@@ -457,7 +478,7 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
 // The stabbing blocks' windows: one thread per (block, width class) and bound, a plain binary search over the class's
 // starts (starts in [lo_min - 4^c, hi_max] for the block's sorted queries). Thousands of independent searches keep the
 // loads in flight, where a search inside the stabbing block would stall it for every dependent round.
-__global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const QRec *__restrict__ srec,
+__global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const uint64_t *__restrict__ blo,
                                                        const uint64_t *__restrict__ bhi, View v, uint32_t *__restrict__ win)
 {
     const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -466,7 +487,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const QRec 
     const uint32_t a0 = v.class_off[c], a1 = v.class_off[c + 1];
     uint32_t b0 = a0, b1 = a0;
     if (a1 > a0) {
-        const uint64_t lo = srec[(size_t)blk * BLOCK].lo, hi = bhi[blk], W = class_width(c);
+        const uint64_t lo = blo[blk], hi = bhi[blk], W = class_width(c);
         b0 = lower_bound_s(v.cs_s, a0, a1, lo > W ? lo - W : 0);
         b1 = upper_bound_s(v.cs_s, b0, a1, hi);
     }
@@ -541,9 +562,9 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
     __shared__ StabPool pool;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * BLOCK + tid;
-    const bool valid = i < v.Q;
     QRec r{};
-    if (valid) r = v.srec[i];
+    if (i < v.Q) r = v.srec[i];
+    const bool valid = i < v.Q && !(r.flags & QPAD);
     if (tid < (uint32_t)NCLS) {
         T.b0[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + tid];
         T.b1[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + NCLS + tid];
@@ -1092,16 +1113,21 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
 
     // ---- 3. query records sorted by low bound; stabbing (one pass, block-sliced output)
     const Runs q_plan = make_runs(hm[2]);
-    QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = ctx->get<QRec>("rd_qrec_sorted", Q);
+    QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = nullptr;
     uint64_t *qkey = ctx->get<uint64_t>("rd_qkey", Q);
     launch(ctx, "rd_qrec", k_rd_qrec, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
-           (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey);
-    Sorted qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, q_plan.bits);
-    const uint32_t nsb = (uint32_t)grid_for(Q, BLOCK);
-    uint64_t *bhi = ctx->get<uint64_t>("rd_bhi", nsb);
-    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Q, (const uint32_t *)qs.vals, (const QRec *)rec, srec, bhi);
+           (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey,
+           (uint32_t)q_plan.bits);
+    Sorted qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, q_plan.bits < 64 ? q_plan.bits + 1 : 64);
+    const uint32_t Pp = q_plan.bits < 64 && P && R ? (uint32_t)((P + BLOCK - 1) / BLOCK * BLOCK) : (uint32_t)P;
+    const uint32_t Qp = Q + (Pp - (uint32_t)P);
+    const uint32_t nsb = (uint32_t)grid_for(Qp, BLOCK);
+    uint64_t *bhi = ctx->get<uint64_t>("rd_bhi", nsb), *blo = ctx->get<uint64_t>("rd_blo", nsb);
+    srec = ctx->get<QRec>("rd_qrec_sorted", Qp);
+    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Qp, (uint32_t)P, Pp, (const uint32_t *)qs.vals,
+           (const QRec *)rec, srec, blo, bhi);
     View v{};
-    v.Q = Q; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
+    v.Q = Qp; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
     v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
     v.q_off = ctx->get<uint64_t>("rd_q_off", Q);
     v.q_cnt = ctx->get<uint32_t>("rd_q_cnt", Q);
@@ -1111,7 +1137,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint64_t E = 0;
     if (Q) {
         launch(ctx, "rd_stab_win", k_rd_stab_win, dim3(grid_for((uint64_t)nsb * NCLS, BLOCK)), dim3(BLOCK), 0, nsb,
-               (const QRec *)srec, (const uint64_t *)bhi, v, win);
+               (const uint64_t *)blo, (const uint64_t *)bhi, v, win);
         for (int attempt = 0; attempt < 2; ++attempt) {
             // capacity: the last batch's need on this context, at least 16 per query
             const uint64_t want = std::max<uint64_t>(ctx->rd_ent_hint, 16ull * Q + 1024);
