@@ -601,10 +601,22 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
     if (valid) { v.q_off[r.q] = base + mine; v.q_cnt[r.q] = count; }
     if (base + total > v.cap) return;   // uniform: the host re-runs with a larger capacity
     if (flat && total <= POOL) {
-        for (uint32_t k = tid; k < total; k += BLOCK) {
-            const uint32_t pos = atomicAdd(&pool.cur[pool.q[k]], 1u);
-            v.ent[base + pos] = pool.x[k];
+        // each pooled hit's place in its query's run (per-query cursors), the pool permuted in place through
+        // registers, then the slice written in whole lines
+        constexpr int PT = (POOL + BLOCK - 1) / BLOCK;
+        uint64_t xv[PT];
+        uint32_t pv[PT];
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const uint32_t k = tid + (uint32_t)u * BLOCK;
+            if (k < total) { pv[u] = atomicAdd(&pool.cur[pool.q[k]], 1u); xv[u] = pool.x[k]; }
         }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+            if (tid + (uint32_t)u * BLOCK < total) pool.x[pv[u]] = xv[u];
+        __syncthreads();
+        for (uint32_t k = tid; k < total; k += BLOCK) v.ent[base + k] = pool.x[k];
     } else if (flat) {
         stab_flat<true>(v, T, valid, r, base + mine, nullptr);
     } else {
