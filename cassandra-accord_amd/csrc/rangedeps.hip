@@ -701,6 +701,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint32_t li = (blockIdx.x * WAVES + wave) * G + grp;
     const bool live = li < cnt;
     const uint32_t t = live ? o.list[li] : 0;
+    const uint64_t ra = live ? o.raw_off[t] : 0;   // issued now: its latency hides under the gather and the sorts
     const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint64_t m = 0, x = ~0ull;
@@ -777,7 +778,6 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (!live || m == 0) return;
-    const uint64_t ra = o.raw_off[t];
     uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
     if (ynew) sd[uidx] = dep_of(o, (uint32_t)(y >> 8));
     const uint32_t g = (uint32_t)__popcll(rb & lt);
@@ -923,30 +923,35 @@ __global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, Out o, uint
     sz[i] = 2 * n2;
 }
 
-// scratch -> Java-layout CSR: 16 lanes per txn
+// scratch -> Java-layout CSR. A workgroup owns BLOCK consecutive txns, whose output runs are one contiguous range of
+// each output array: a thread per output element finds its txn among the block's offsets in LDS and copies from that
+// txn's scratch, so every write (and most reads) is a whole-line access.
+__device__ __forceinline__ void compact_array(uint32_t nt, const uint64_t *off, const uint64_t *src_base,
+                                              const uint32_t *src, uint32_t *dst)
+{
+    const uint64_t j0 = off[0], j1 = off[nt];
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += BLOCK) {
+        uint32_t lo = 0, hi = nt;   // last txn k with off[k] <= j
+        while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (off[md] <= j) lo = md; else hi = md; }
+        dst[j] = src[src_base[lo] + (j - off[lo])];
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
 {
-    const uint32_t gi = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
-    if (gi >= n) return;
-    const uint32_t t = gi;
-    const uint64_t ra = o.raw_off[t];
-    const uint64_t na = o.a_cnt[t], nr = o.rd_cnt[t], nu = o.u_cnt[t];
-    const uint64_t ao = o.arena_off[t], ro = o.rd_off[t], uo = o.u_off[t];
-    // first round: up to 64 arena ints, 16 range ids and 16 TxnIds loaded together (one latency for most txns),
-    // then the rest
-    const uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
-    uint32_t a[4], r = 0, u = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = sub + 16u * k < na ? sa[sub + 16u * k] : 0u;
-    if (sub < nr) r = sr[sub];
-    if (sub < nu) u = sd[sub];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) if (sub + 16u * k < na) o.arena[ao + sub + 16u * k] = (int32_t)a[k];
-    if (sub < nr) o.range_id[ro + sub] = r;
-    if (sub < nu) o.dep_txn[uo + sub] = u;
-    for (uint64_t j = 64 + sub; j < na; j += 16) o.arena[ao + j] = (int32_t)sa[j];
-    for (uint64_t j = 16 + sub; j < nr; j += 16) o.range_id[ro + j] = sr[j];
-    for (uint64_t j = 16 + sub; j < nu; j += 16) o.dep_txn[uo + j] = sd[j];
+    __shared__ uint64_t ao[BLOCK + 1], ro[BLOCK + 1], uo[BLOCK + 1], sa[BLOCK], sr[BLOCK];
+    const uint32_t t0 = blockIdx.x * BLOCK, nt = min((uint32_t)BLOCK, n - t0), tid = threadIdx.x;
+    if (tid < nt) {
+        const uint32_t t = t0 + tid;
+        ao[tid] = o.arena_off[t]; ro[tid] = o.rd_off[t]; uo[tid] = o.u_off[t];
+        const uint64_t ra = o.raw_off[t];
+        sa[tid] = 2 * ra; sr[tid] = ra;
+    }
+    if (tid == 0) { ao[nt] = o.arena_off[t0 + nt]; ro[nt] = o.rd_off[t0 + nt]; uo[nt] = o.u_off[t0 + nt]; }   // the block's ends
+    __syncthreads();
+    compact_array(nt, ao, sa, o.s_arena, reinterpret_cast<uint32_t *>(o.arena));
+    compact_array(nt, ro, sr, o.s_rid, o.range_id);
+    compact_array(nt, uo, sr, o.s_dep, o.dep_txn);
 }
 
 }  // namespace rd
@@ -1261,7 +1266,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     o.arena = ctx->get<int32_t>("rd_arena", tot_arena);
     o.range_id = ctx->get<uint32_t>("rd_range_id", tot_rd);
     o.dep_txn = ctx->get<uint32_t>("rd_dep_txn", tot_u);
-    launch(ctx, "rd_compact", k_rd_compact, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, o);
+    if (n) launch(ctx, "rd_compact", k_rd_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, o);
     ctx->stat("rangedeps.entries", NE);
     ctx->stat("rangedeps.stored_ranges", n_dict);
     ctx->stat("rangedeps.queries", Q);
