@@ -3496,9 +3496,9 @@ __device__ __forceinline__ uint32_t mx_scan32(uint32_t x, uint32_t sub)   // inc
     return x;
 }
 
-// count pass: entries and non-empty keys per piece
+// count pass: entries and non-empty keys per piece; each lane's count is kept (qc) so the emit pass runs the scan once
 __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkView v, uint64_t *__restrict__ pe_cnt,
-                                                     uint32_t *__restrict__ pk_cnt)
+                                                     uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u, g0 = lane_id() & 32u;
@@ -3508,6 +3508,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkVie
         const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
         const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
         if (sub < nk) c = run_query<false>(v, make_query_ts(v, t, pc.ra[j] + k0 + sub), nullptr);
+        qc[p * 32 + sub] = c;
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
     const uint32_t te = __shfl(ce, (int)(g0 + 31), 64), tk = __shfl(ck, (int)(g0 + 31), 64);
@@ -3521,7 +3522,8 @@ struct MxE {   // emitted entries and key records of the range txns
 };
 
 __global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView v, const uint64_t *__restrict__ pe_off,
-                                                    const uint32_t *__restrict__ pk_off, const uint64_t *__restrict__ etoff, MxE x)
+                                                    const uint32_t *__restrict__ pk_off, const uint64_t *__restrict__ etoff, MxE x,
+                                                    const uint32_t *__restrict__ qc)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u;
@@ -3537,7 +3539,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView
         if (act) {
             seg = pc.ra[j] + k0 + sub;
             qq = make_query_ts(v, t, seg);
-            c = run_query<false>(v, qq, nullptr);
+            c = qc[p * 32 + sub];
         }
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
@@ -3874,6 +3876,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     MxP pc{ prange, ra, rowner, rng_off, poff, rcnt, r_off, seg_key };
     uint64_t Ex = 0, Kx = 0;
     CfkView v{};
+    uint32_t *qc = ctx->get<uint32_t>("mx_qc", NP * 32);
     if (NP) {
         if (!ks.v1) {
             ks.v1view = build_v1_cfk(ctx, n, ks.P, ks.rbits, ks.tl, ks.owner, ks.rank, ks.seg_incl, ks.seg_start, ks.s_rank,
@@ -3882,7 +3885,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         }
         v = ks.v1view;
         launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff, prange);
-        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt);
+        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, pe_cnt, pe_off, NP, true, pe_off + NP);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, pk_cnt, pk_off, NP, true, pk_off + NP);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, pe_off + NP, 8, hipMemcpyDeviceToHost, st));
@@ -3909,7 +3912,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     MxU mu{ mx.deps, etoff, ks.txn_of_rank, idx_of_e, dep_scr, ucnt };
     if (Ex) {
         launch(ctx, "mx_pemit", k_mx_pemit, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, (const uint64_t *)pe_off,
-               (const uint32_t *)pk_off, (const uint64_t *)etoff, mx);
+               (const uint32_t *)pk_off, (const uint64_t *)etoff, mx, (const uint32_t *)qc);
         // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
         uint32_t *blk_list = ctx->get<uint32_t>("mx_blk_list", n);
         uint32_t *mid_list = ctx->get<uint32_t>("mx_mid_list", n);
