@@ -38,13 +38,15 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
 
 # KeyDeps tiers launched on a side stream, concurrently with the stream pass (csrc/keydeps.hip keydeps_core)
-SIDE_STREAM_TAGS = {"v2_write_med", "v2_write_big", "v2_write_huge", "v2_write_medium"}
+SIDE_STREAM_TAGS = {"v2_write_med", "v2_write_big", "v2_write_huge", "v2_write_medium", "v2_write_win", "v2_write_win16"}
 
 # launch tags whose kernel is one instance of a template launched under several tags (csrc/keydeps.hip tiers)
 TAG_KERNEL = {
     "v2_write_med": "k_v2_write_big<1024,256>",
     "v2_write_big": "k_v2_write_big<8192,512>",
     "v2_write_huge": "k_v2_write_big<16384,1024>",
+    "v2_write_win": "k_v2_write_win<8>",
+    "v2_write_win16": "k_v2_write_win<16>",
 }
 
 

@@ -551,6 +551,19 @@ orc_keydeps_result *orc_keydeps_mixed(uint32_t n,
     return R;
 }
 
+orc_keydeps_result *orc_keydeps_mixed_qmask(uint32_t n,
+                                            const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                            const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                            const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                            const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                            int end_inclusive, const uint8_t *query_mask)
+{
+    orc_keydeps_result *R = calloc(1, sizeof *R);
+    keydeps_impl(R, n, tmsb, tlsb, tnode, emsb, elsb, enode, status, key_off, key_code, rng_off, rng_start, rng_end,
+                 end_inclusive, 1, 0, n, 1, query_mask);
+    return R;
+}
+
 static void keydeps_impl(orc_keydeps_result *R, uint32_t n,
                          const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
@@ -867,12 +880,43 @@ static int cmp_rd_item(int64_t a, int64_t b, const void *c)
     return ts_cmp(&X->B->id[X->it[a].txn], &X->B->id[X->it[b].txn]);
 }
 
+static orc_rangedeps_result *rangedeps_impl(uint32_t n,
+                                          const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                          const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                          const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                          int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride,
+                                          const uint8_t *qmask);
+
 orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
                                           const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
                                           const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
                                           const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
                                           const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
                                           int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride)
+{
+    return rangedeps_impl(n, tmsb, tlsb, tnode, emsb, elsb, enode, status, key_off, key_code, rng_off, rng_start,
+                          rng_end, end_inclusive, query_lo, query_hi, query_stride, NULL);
+}
+
+orc_rangedeps_result *orc_rangedeps_batch_qmask(uint32_t n,
+                                                const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                                const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                                const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                                const uint32_t *rng_off, const uint64_t *rng_start,
+                                                const uint64_t *rng_end, int end_inclusive, const uint8_t *query_mask)
+{
+    return rangedeps_impl(n, tmsb, tlsb, tnode, emsb, elsb, enode, status, key_off, key_code, rng_off, rng_start,
+                          rng_end, end_inclusive, 0, n, 1, query_mask);
+}
+
+static orc_rangedeps_result *rangedeps_impl(uint32_t n,
+                                          const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                          const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                          const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                          int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride,
+                                          const uint8_t *qmask)
 {
     orc_rangedeps_result *R = calloc(1, sizeof *R);
     if (query_stride == 0) query_stride = 1;
@@ -932,6 +976,7 @@ orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
     for (uint32_t t = 0; t < n && !E.code; ++t) {
         R->arena_off[t] = arena.n; R->rd_off[t] = rids.n; R->u_off[t] = deps.n;
         if (t < query_lo || t >= query_hi || (t - query_lo) % query_stride) continue;
+        if (qmask && !qmask[t]) continue;
         ++R->queried;
         int wk = kind_witnesses(ts_kind(&B.id[t]));
         if (wk < 0) { set_err(&E, -2, "Kind.witnesses(): unhandled kind (AssertionError)"); break; }

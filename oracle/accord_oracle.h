@@ -66,6 +66,13 @@ orc_keydeps_result *orc_keydeps_mixed(uint32_t n,
                                       const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
                                       int end_inclusive, uint32_t n_shards, uint32_t query_lo, uint32_t query_hi,
                                       uint32_t query_stride);
+/* orc_keydeps_mixed with an explicit query set (query_mask[t] != 0). */
+orc_keydeps_result *orc_keydeps_mixed_qmask(uint32_t n,
+                                            const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                            const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                            const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                            const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
+                                            int end_inclusive, const uint8_t *query_mask);
 void orc_keydeps_free(orc_keydeps_result *r);
 
 /* KeyDeps.merge (KeyDeps.java:115-135) over groups of replies in the acc_merge_in layout
@@ -118,6 +125,13 @@ orc_rangedeps_result *orc_rangedeps_batch(uint32_t n,
                                           const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
                                           const uint32_t *rng_off, const uint64_t *rng_start, const uint64_t *rng_end,
                                           int end_inclusive, uint32_t query_lo, uint32_t query_hi, uint32_t query_stride);
+/* orc_rangedeps_batch with an explicit query set (query_mask[t] != 0). */
+orc_rangedeps_result *orc_rangedeps_batch_qmask(uint32_t n,
+                                                const uint64_t *tmsb, const uint64_t *tlsb, const int32_t *tnode,
+                                                const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                                                const uint8_t *status, const uint32_t *key_off, const uint64_t *key_code,
+                                                const uint32_t *rng_off, const uint64_t *rng_start,
+                                                const uint64_t *rng_end, int end_inclusive, const uint8_t *query_mask);
 void orc_rangedeps_free(orc_rangedeps_result *r);
 
 /* InMemorySafeStore.mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016), the range-command half of the

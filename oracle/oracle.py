@@ -88,6 +88,12 @@ def lib():
         L.orc_keydeps_mixed.restype = C.POINTER(KeydepsResult)
         L.orc_keydeps_mixed.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
                                         u32p, u64p, u64p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_keydeps_mixed_qmask.restype = C.POINTER(KeydepsResult)
+        L.orc_keydeps_mixed_qmask.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
+                                              u32p, u64p, u64p, C.c_int, u8p]
+        L.orc_rangedeps_batch_qmask.restype = C.POINTER(RangedepsResult)
+        L.orc_rangedeps_batch_qmask.argtypes = [C.c_uint32, u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p,
+                                                u32p, u64p, u64p, C.c_int, u8p]
         L.orc_keydeps_merge.restype = C.POINTER(MergeResult)
         L.orc_keydeps_merge.argtypes = [C.c_uint32, u64p, u64p, u64p, u64p, u32p, u64p, i32p]
         L.orc_merge_free.argtypes = [C.POINTER(MergeResult)]
@@ -198,6 +204,42 @@ def keydeps_mixed(rb, n_shards: int = 1, query_lo: int = 0, query_hi: int | None
     r = L.orc_keydeps_mixed(n, *[_p(a, t) for a, t in zip(arrs, types)], int(rb.end_inclusive), n_shards,
                             query_lo, n if query_hi is None else query_hi, query_stride)
     return _keydeps_out(L, r, n)
+
+
+def _mixed_arrays(rb):
+    b = rb.keys
+    arrs = [np.ascontiguousarray(x) for x in (b.txn_msb.astype(np.uint64), b.txn_lsb.astype(np.uint64),
+                                              b.txn_node.astype(np.int32), b.exe_msb.astype(np.uint64),
+                                              b.exe_lsb.astype(np.uint64), b.exe_node.astype(np.int32),
+                                              b.status.astype(np.uint8), b.key_off.astype(np.uint32),
+                                              b.key_code.astype(np.uint64), rb.rng_off.astype(np.uint32),
+                                              rb.rng_start.astype(np.uint64), rb.rng_end.astype(np.uint64))]
+    types = [u64p, u64p, i32p, u64p, u64p, i32p, u8p, u32p, u64p, u32p, u64p, u64p]
+    return [_p(a, t) for a, t in zip(arrs, types)], arrs
+
+
+def _qmask(n, queries):
+    mask = np.zeros(max(n, 1), np.uint8)
+    mask[np.asarray(queries, dtype=np.int64)] = 1
+    return mask
+
+
+def keydeps_mixed_queries(rb, queries) -> KeyDepsBatchOut:
+    """keydeps_mixed on an explicit query set (txn indices), one snapshot build (orc_keydeps_mixed_qmask)."""
+    L = lib()
+    n = rb.n_txn
+    ptrs, keep = _mixed_arrays(rb)
+    mask = _qmask(n, queries)
+    return _keydeps_out(L, L.orc_keydeps_mixed_qmask(n, *ptrs, int(rb.end_inclusive), _p(mask, u8p)), n)
+
+
+def rangedeps_batch_queries(rb, queries) -> "RangeDepsBatchOut":
+    """rangedeps_batch on an explicit query set (txn indices), one table build (orc_rangedeps_batch_qmask)."""
+    L = lib()
+    n = rb.n_txn
+    ptrs, keep = _mixed_arrays(rb)
+    mask = _qmask(n, queries)
+    return _rangedeps_out(L, L.orc_rangedeps_batch_qmask(n, *ptrs, int(rb.end_inclusive), _p(mask, u8p)), n)
 
 
 def map_reduce_full(batch, miss_off, miss_txn, queries, started_at: int, test_dep: int, test_status: int,

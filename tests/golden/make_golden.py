@@ -151,8 +151,73 @@ def config3():
         print(path, os.path.getsize(path), "bytes;", len(ts), "txns; edges", o.total_edges, flush=True)
 
 
+C4_N = 20_000_000
+
+
+def config4_samples(rb):
+    """The query txns of the config-4 fixture: RangeDeps of 2,000 txns (the 1,000 latest, where the uncommitted window
+    is, and 1,000 strided over the batch, key and range txns alike) and mixed KeyDeps of 1,500 txns (1,000 range txns:
+    the 500 latest and 500 strided over all range txns, plus 500 strided key txns)."""
+    n = rb.n_txn
+    rd = np.unique(np.concatenate([np.arange(n - 1_000, n), np.arange(11, n, n // 1_000)[:1_000]]))
+    isr = rb.is_range()
+    rt = np.flatnonzero(isr)
+    kt = np.flatnonzero(~isr)
+    mx = np.unique(np.concatenate([rt[-500:], rt[13::len(rt) // 500][:500], kt[17::len(kt) // 500][:500]]))
+    return rd, mx
+
+
+def range_digest(ranges, deps, r2v) -> bytes:
+    """16-byte digest of one txn's RangeDeps (ranges as (start, end) u64 code pairs, deps as u32 batch indices,
+    rangesToTxnIds as i32)"""
+    return txn_digest(np.asarray(ranges, np.uint64).reshape(-1), deps, r2v)
+
+
+def config4():
+    """BASELINE config 4 at full size (10M range txns + 10M key txns x 4 keys): per-txn sizes and 16-byte digests of
+    the RangeDeps of 2,000 txns and of the mixed KeyDeps (range txns over the CommandsForKey inside their ranges,
+    InMemoryCommandStore.java:274-289) of 1,500 txns, from the C restatement, plus the input's sha256. The oracle walks
+    all 10M range commands per RangeDeps query, so the sample is what a few minutes of CPU buy."""
+    rb = W.config4(1.0)
+    assert rb.n_txn == C4_N
+    rd, mx = config4_samples(rb)
+    sizes, dig = [], []
+    o = oracle.rangedeps_batch_queries(rb, rd)
+    for t in rd.tolist():
+        r, d, a = o.txn(t)
+        rr = np.stack([o.rng_start[r], o.rng_end[r]], 1) if len(r) else np.zeros((0, 2), np.uint64)
+        sizes.append((len(r), len(d), len(a)))
+        dig.append(np.frombuffer(range_digest(rr, d, a), np.uint8))
+    print("rangedeps", len(rd), "txns, edges", o.total_edges, flush=True)
+    msizes, mdig = [], []
+    om = oracle.keydeps_mixed_queries(rb, mx)
+    for t in mx.tolist():
+        k, d, a = om.txn(t)
+        kk = om.kd_key[int(om.kd_off[t]):int(om.kd_off[t + 1])]
+        msizes.append((len(k), len(d), len(a)))
+        mdig.append(np.frombuffer(txn_digest(kk, d, a), np.uint8))
+    print("mixed keydeps", len(mx), "txns, edges", om.total_edges, flush=True)
+    path = os.path.join(HERE, "config4_sample.npz")
+    np.savez_compressed(path, input_sha256=np.frombuffer(bytes.fromhex(range_batch_digest(rb)), np.uint8),
+                        rd_txn=rd.astype(np.uint32), rd_sizes=np.array(sizes, np.uint32), rd_digest=np.stack(dig),
+                        mx_txn=mx.astype(np.uint32), mx_sizes=np.array(msizes, np.uint32), mx_digest=np.stack(mdig))
+    print(path, os.path.getsize(path), "bytes", flush=True)
+
+
+def range_batch_digest(rb) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in sorted(rb.arrays().items()):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    h.update(np.int32(rb.end_inclusive).tobytes())
+    return h.hexdigest()
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("4f", "all"):
+        config4()
     if which in ("1", "all"):
         main()
     if which in ("4", "all"):

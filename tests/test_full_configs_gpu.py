@@ -94,6 +94,35 @@ def test_config4_full(ctx):
             np.testing.assert_array_equal(x, y, err_msg=f"txn {t}")
 
 
+def test_config4_fixture_full(ctx):
+    """BASELINE config 4 at full size against the committed oracle fixture (tests/golden/make_golden.py config4):
+    the RangeDeps of 2,000 txns and the mixed KeyDeps (range txns over the CommandsForKey inside their ranges,
+    InMemoryCommandStore.java:274-289) of 1,500 txns, by size and digest; and the fused acc_partial_deps_batch is the
+    two separate calls, every array of every txn (PartialDeps.Builder routes both halves, Deps.java:46-96)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import range_batch_digest, range_digest, txn_digest
+    rb = W.config4(1.0)
+    fx = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config4_sample.npz")))
+    assert range_batch_digest(rb) == bytes(fx["input_sha256"]).hex(), "config-4 generator changed"
+    rd = ctx.calculate_partial_range_deps(rb)
+    for t, sz, dg in zip(fx["rd_txn"].tolist(), fx["rd_sizes"], fx["rd_digest"]):
+        r, d, a = rd.txn(t)
+        rr = np.stack([rd.rng_start[r], rd.rng_end[r]], 1) if len(r) else np.zeros((0, 2), np.uint64)
+        assert (len(r), len(d), len(a)) == tuple(int(x) for x in sz), f"rangedeps txn {t} sizes"
+        assert range_digest(rr, d, a) == bytes(dg), f"rangedeps txn {t} digest"
+    kd = ctx.calculate_partial_key_deps_mixed(rb)
+    for t, sz, dg in zip(fx["mx_txn"].tolist(), fx["mx_sizes"], fx["mx_digest"]):
+        k, d, a = kd.txn(t)
+        kk = kd.kd_key[int(kd.kd_off[t]):int(kd.kd_off[t + 1])]
+        assert (len(k), len(d), len(a)) == tuple(int(x) for x in sz), f"mixed keydeps txn {t} sizes"
+        assert txn_digest(kk, d, a) == bytes(dg), f"mixed keydeps txn {t} digest"
+    pk, pr = ctx.calculate_partial_deps_mixed(rb)
+    for f in ("arena_off", "arena", "kd_off", "key_idx", "u_off", "dep_txn", "kd_key"):
+        np.testing.assert_array_equal(getattr(pk, f), getattr(kd, f), err_msg=f"fused KeyDeps {f}")
+    for f in ("rng_start", "rng_end", "arena_off", "arena", "rd_off", "range_id", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(pr, f), getattr(rd, f), err_msg=f"fused RangeDeps {f}")
+
+
 def test_config5_full(ctx):
     """BASELINE config 5 at full size through the bench's device chain: every array of the merged view (keys, TxnIds,
     keysToTxnIds of all 16,384 coordinated txns) and the level / order of the levelised graph, against the oracle."""
