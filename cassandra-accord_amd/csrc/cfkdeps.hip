@@ -319,7 +319,8 @@ struct Ctx {
     }
 
     // CommandsForKey.update(prev, next) (:657-722) on this key; returns true when the state moved to B
-    __device__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, bool ballot_changed, const Ts *deps,
+    // fl: bit 0 = acceptedOrCommitted changed, bit 1 = next.status() == AcceptedInvalidate
+    __device__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, const Ts *deps,
                           uint32_t nd)
     {
         B.n = 0; B.mtop = 0;
@@ -340,8 +341,9 @@ struct Ctx {
         }
         const Info cur = A.e[pos];
         if (st <= cur.st) {
-            if (cur.st != st) { err |= E_STALE; return false; }   // Invariants.checkState (:681-683)
-            if (!has_info(st) || !ballot_changed) return false;   // acceptedOrCommitted unchanged: this (:684-685)
+            // Invariants.checkState(cur.status == newStatus || next.status() == AcceptedInvalidate) (:681-686)
+            if (cur.st != st && !(fl & 2u)) { err |= E_STALE; return false; }
+            if (!has_info(st) || !(fl & 1u)) return false;   // acceptedOrCommitted unchanged: this (:687-688)
         }
         if (has_info(st)) {
             uint32_t nm, na;
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
         Ts *deps = c.w.owned;
         if (db - da > dk) { c.err |= E_CAP; break; }
         for (uint32_t t = da; t < db; ++t) deps[t - da] = Ts{ u.dm[t], u.dl[t], u.dn[t] };
-        if (c.apply(*A, *B, id, ex, st, (u.fl[i] & 1u) != 0, deps, db - da)) {
+        if (c.apply(*A, *B, id, ex, st, u.fl[i], deps, db - da)) {
             Buf *t = A; A = B; B = t;
         }
     }

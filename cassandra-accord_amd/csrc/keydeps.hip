@@ -791,13 +791,17 @@ __global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__rest
     }
 }
 
-// Row layout of the per-position prefix columns: row p = 8 u32 (32 B, one sector) =
-//   [0..5] exclusive prefix counts of the 6 class lists, [6] bumped-committed count, [7] last unbumped committed
-//   Write (pos+1, prefix max). A query reads whole rows at s0 / s1 / pos / posM: one line each.
+// The per-position prefix columns as a rank directory: one 64-B chunk per RD_W = 32 CFK positions, = one HBM line
+// (16 MB at config 2's 8M positions, instead of a 32-B row per position): words 0-7 = the 8 running values at the
+// chunk's first position (exclusive prefix counts of the 6 class lists, the bumped-committed count, the last unbumped
+// committed Write as pos+1: prefix max), words 8-15 = one bit plane per column over the chunk's positions (list
+// membership, bumped committed, unbumped committed Write). A query's "row" at p is the chunk's running values plus the
+// popcounts of the planes below p (the last set bit for the Write column): one line read and a few ALU ops.
 constexpr int RW_CBC = 6, RW_LUCW = 7;
+constexpr uint32_t RD_W = 32;
 
 struct V2Cols {
-    uint4 *rows;          // [P+1] rows of 8 u32, as 2 x uint4
+    uint4 *rdir;          // [P / RD_W + 1] chunks of 16 u32, as 4 x uint4
     uint32_t *list_rank;  // class lists (TxnId ranks), list l at bases[l]
     uint32_t *bc_rank, *bc_exec;  // bumped committed, position order
     uint8_t *bc_kind;
@@ -833,6 +837,36 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         if (q < 7) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
         else { uint32_t e = block_exclusive(c[q], OpMax<uint32_t>(), lds, total); run[q] = e > pre ? e : pre; }
     }
+    // rank directory: the chunk's running values from its first thread (RD_W / V2_ITEMS = 8 threads per chunk), the bit
+    // planes OR-reduced over those 8 threads (threads past P contribute nothing)
+    static_assert(RD_W == 8 * V2_ITEMS, "eight threads per directory chunk");
+    {
+        uint32_t pl[NCNT] = {};
+#pragma unroll
+        for (int i = 0; i < V2_ITEMS; ++i) {
+            const uint32_t l = code[i] & 7u;
+#pragma unroll
+            for (int q = 0; q < NLIST; ++q) pl[q] |= (l == (uint32_t)q ? 1u : 0u) << i;
+            pl[6] |= ((code[i] >> 3) & 1u) << i;
+            pl[7] |= ((code[i] >> 4) & 1u) << i;
+        }
+        const uint32_t sh = V2_ITEMS * (threadIdx.x & 7u);
+#pragma unroll
+        for (int q = 0; q < NCNT; ++q) {
+            uint32_t x = pl[q] << sh;
+            x |= __shfl_xor(x, 1, 64);
+            x |= __shfl_xor(x, 2, 64);
+            x |= __shfl_xor(x, 4, 64);
+            pl[q] = x;
+        }
+        if ((threadIdx.x & 7u) == 0 && base < P) {
+            uint4 *ch = o.rdir + 4 * (base / RD_W);
+            ch[0] = make_uint4(run[0], run[1], run[2], run[3]);
+            ch[1] = make_uint4(run[4], run[5], run[6], run[7]);
+            ch[2] = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+            ch[3] = make_uint4(pl[4], pl[5], pl[6], pl[7]);
+        }
+    }
     if (base >= P) return;
     uint32_t lb[NLIST];
 #pragma unroll
@@ -841,8 +875,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     for (int i = 0; i < V2_ITEMS; ++i) {
         size_t p = base + i;
         if (p >= P) break;
-        o.rows[2 * p] = make_uint4(run[0], run[1], run[2], run[3]);
-        o.rows[2 * p + 1] = make_uint4(run[4], run[5], run[6], run[7]);
         uint32_t l = code[i] & 7u;
         uint32_t r = rk[i];
         if (l < NLIST) {
@@ -863,9 +895,13 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
             o.bc_key[b] = ((uint64_t)seg << rbits) | e;
         }
         if ((code[i] >> 4) & 1u) run[7] = (uint32_t)p + 1;
-        if (p == P - 1) {
-            o.rows[2 * P] = make_uint4(run[0], run[1], run[2], run[3]);
-            o.rows[2 * P + 1] = make_uint4(run[4], run[5], run[6], run[7]);
+        if (p == P - 1 && P % RD_W == 0) {
+            // position P opens a chunk of its own: its running values and empty planes
+            uint4 *ch = o.rdir + 4 * (P / RD_W);
+            ch[0] = make_uint4(run[0], run[1], run[2], run[3]);
+            ch[1] = make_uint4(run[4], run[5], run[6], run[7]);
+            ch[2] = make_uint4(0u, 0u, 0u, 0u);
+            ch[3] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
 }
@@ -919,28 +955,38 @@ __global__ __launch_bounds__(BLOCK) void k_v2_tile_scans(const uint32_t *__restr
 struct V2View {
     const uint32_t *perm, *pair_pos, *seg_incl, *seg_start, *s_rank, *s_exec;
     const uint8_t *s_info;
-    const uint4 *rows;
+    const uint4 *rdir;
     const uint32_t *list_rank, *bases;
     const uint32_t *bc_rank, *bc_exec, *bc_pm;
     const uint8_t *bc_kind;
     const uint32_t *bcs_exec, *bcs_lastw;
     const uint4 *tinfo;   // per txn: rank, executeAt rank, status | kind << 3
-    const uint32_t *rec32;   // the count pass's per-pair records as u32 (inline entries)
+    const uint32_t *irec32;  // the count pass's inline records as u32 (IREC_W words per pair; word 7 = E | flag)
+    const uint4 *rec;        // the count pass's 64-B records (runs; inline entries beyond IREC_N)
 };
 
 struct Row { uint32_t c[8]; };
 
+// the 8 running values at CFK position p from its rank-directory chunk
 __device__ __forceinline__ Row ld_row(const V2View &v, uint32_t p)
 {
-    uint4 a = v.rows[2 * (size_t)p], b = v.rows[2 * (size_t)p + 1];
-    Row r;
-    r.c[0] = a.x; r.c[1] = a.y; r.c[2] = a.z; r.c[3] = a.w;
-    r.c[4] = b.x; r.c[5] = b.y; r.c[6] = b.z; r.c[7] = b.w;
-    return r;
+    const uint4 *ch = v.rdir + 4 * (size_t)(p / RD_W);
+    const uint4 a = ch[0], b = ch[1], c = ch[2], d = ch[3];
+    const uint32_t r = p % RD_W, mask = (1u << r) - 1u;
+    Row o;
+    o.c[0] = a.x + __popc(c.x & mask); o.c[1] = a.y + __popc(c.y & mask);
+    o.c[2] = a.z + __popc(c.z & mask); o.c[3] = a.w + __popc(c.w & mask);
+    o.c[4] = b.x + __popc(d.x & mask); o.c[5] = b.y + __popc(d.y & mask);
+    o.c[6] = b.z + __popc(d.z & mask);
+    const uint32_t w = d.w & mask;
+    o.c[7] = w ? (p - r) + (31u - (uint32_t)__clz(w)) + 1u : b.w;
+    return o;
 }
 __device__ __forceinline__ uint32_t ld_cbc(const V2View &v, uint32_t p)
 {
-    return reinterpret_cast<const uint32_t *>(v.rows)[8 * (size_t)p + RW_CBC];
+    const uint32_t *ch = reinterpret_cast<const uint32_t *>(v.rdir) + 16 * (size_t)(p / RD_W);
+    const uint32_t r = p % RD_W;
+    return ch[RW_CBC] + __popc(ch[8 + RW_CBC] & ((1u << r) - 1u));
 }
 
 struct V2Query {
@@ -995,17 +1041,28 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     return q;
 }
 
-// per-pair record for the write pass, stored by pair index j (the write pass reads a txn's records contiguously; a
-// whole 64-B granule per record, so the scatter is full-line writes):
-//   inline  (E <= REC_INLINE): the pair's dependency entries themselves (TxnId ranks, T and filtered R3 entries
-//           already dropped), word 15 = REC_INLINE_FLAG | E. Gathered here in CFK position order, where neighbouring
-//           pairs of a segment read the same class-list lines, instead of by the write pass in txn order;
-//   runs    (otherwise): starts a[6] and lengths l[6] of R1/R2 per class (witnessed classes only), R3 = [bs, bs + bl)
-//           filtered by executeAt >= M; word 15 = 0.
+// per-pair results for the write pass, stored by pair index j (the write pass reads a txn's pairs contiguously):
+//   irec[j] (32 B, every pair): word 7 = E, | REC_INLINE_FLAG for an inline record (the mark pass reads this word);
+//           inline (E <= REC_INLINE): the pair's dependency entries themselves (TxnId ranks, T and filtered R3 entries
+//           already dropped), the first IREC_N in words 0-6, the rest (E > IREC_N) in words 0-7 of rec[j]. Gathered
+//           here in CFK position order, where neighbouring pairs of a segment read the same class-list lines, instead
+//           of by the write pass in txn order;
+//   rec[j]  (64 B, run pairs, E > REC_INLINE): starts a[6] and lengths l[6] of R1/R2 per class (witnessed classes only),
+//           R3 = [bs, bs + bl) filtered by executeAt >= M; word 15 = E.
+// An inline entry is addressed as 16 * j + off (inl_entry).
 constexpr uint32_t NO_M = 0xFFFFFFFFu;
 constexpr uint32_t INLINE_M = 0xFFFFFFFEu;   // RunsT::m marker of an inline record
 constexpr uint32_t REC_INLINE = 15;
+constexpr uint32_t IREC_W = 8;               // u32 words per 32-B record
+constexpr uint32_t IREC_N = 7;               // inline entries held by the 32-B record
 constexpr uint32_t REC_INLINE_FLAG = 0x80000000u;
+
+// inline entry off of pair j (idx = 16 * j + off)
+__device__ __forceinline__ uint32_t inl_entry(const uint32_t *irec32, const uint4 *rec, uint32_t idx)
+{
+    const uint32_t j = idx >> 4, off = idx & 15u;
+    return off < IREC_N ? irec32[IREC_W * (size_t)j + off] : reinterpret_cast<const uint32_t *>(rec)[16 * (size_t)j + off - IREC_N];
+}
 
 __device__ __forceinline__ void inl_put(uint32_t (&buf)[16], uint32_t &n, uint32_t x)
 {
@@ -1014,8 +1071,13 @@ __device__ __forceinline__ void inl_put(uint32_t (&buf)[16], uint32_t &n, uint32
     ++n;
 }
 
+struct RecOut {
+    uint4 *rec;         // run records, 4 x uint4 per pair
+    uint4 *irec;        // inline records / E words, 2 x uint4 per pair
+};
+
 __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
-                                                  uint4 *__restrict__ rec, uint32_t *__restrict__ bigflag)
+                                                  const RecOut &ro, uint32_t *__restrict__ bigflag)
 {
     const uint32_t j = v.perm[p];   // independent of the query chain: issued first
     V2Query q = v2_query(v, p);
@@ -1044,9 +1106,8 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
     }
-    uint4 *r = rec + 4 * (size_t)j;
     if (e <= REC_INLINE) {
-        // the six class runs hold L6 <= e + 1 <= 16 elements (T itself is dropped at most once): all their loads are
+        // the six class runs hold L6 <= e + 1 <= 8 elements (T itself is dropped at most once): all their loads are
         // issued together (static slots, predicated), not one dependent load per element
         uint32_t pre[6], L6 = 0;
 #pragma unroll
@@ -1083,11 +1144,19 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
                     if (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u) && !(q.bq && xr[u] == q.trank))
                         inl_put(buf, n, xr[u]);
             }
+        uint4 *r = ro.irec + 2 * (size_t)j;
         r[0] = make_uint4(buf[0], buf[1], buf[2], buf[3]);
-        r[1] = make_uint4(buf[4], buf[5], buf[6], buf[7]);
-        r[2] = make_uint4(buf[8], buf[9], buf[10], buf[11]);
-        r[3] = make_uint4(buf[12], buf[13], buf[14], REC_INLINE_FLAG | (uint32_t)e);
+        r[1] = make_uint4(buf[4], buf[5], buf[6], REC_INLINE_FLAG | (uint32_t)e);
+        if (e > IREC_N) {
+            uint4 *r2 = ro.rec + 4 * (size_t)j;
+            r2[0] = make_uint4(buf[7], buf[8], buf[9], buf[10]);
+            r2[1] = make_uint4(buf[11], buf[12], buf[13], buf[14]);
+        }
     } else {
+        uint4 *ir = ro.irec + 2 * (size_t)j;
+        ir[0] = make_uint4(0u, 0u, 0u, 0u);
+        ir[1] = make_uint4(0u, 0u, 0u, (uint32_t)e);
+        uint4 *r = ro.rec + 4 * (size_t)j;
         r[0] = make_uint4(a[0], a[1], a[2], a[3]);
         r[1] = make_uint4(a[4], a[5], l[0], l[1]);
         r[2] = make_uint4(l[2], l[3], l[4], l[5]);
@@ -1100,13 +1169,13 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
 // Also: bigflag[T] = 1 for txns with a run record (they take the v2 tiers, the rest the stream pass) and per-block
 // entry totals (blk_e) for the batch's E.
 __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, const uint32_t *__restrict__ owner,
-                                                    uint4 *__restrict__ rec, uint32_t *__restrict__ bigflag,
+                                                    RecOut ro, uint32_t *__restrict__ bigflag,
                                                     uint64_t *__restrict__ blk_e)
 {
     __shared__ uint64_t lds[WAVES];
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t e = 0;
-    if (p < P) e = v2_count_one(v, (uint32_t)p, owner, rec, bigflag);
+    if (p < P) e = v2_count_one(v, (uint32_t)p, owner, ro, bigflag);
     uint64_t total;
     block_exclusive(e, OpAdd<uint64_t>(), lds, total);
     if (threadIdx.x == 0) blk_e[blockIdx.x] = total;
@@ -1130,7 +1199,8 @@ struct V2Out {
     const uint32_t *key_off;
     const uint64_t *dep_off, *arena_off;
     const uint32_t *cnz, *txn_of_rank;
-    const uint4 *rec;        // 4 x uint4 per pair (k_v2_count)
+    const uint4 *rec;        // run records, 4 x uint4 per pair (k_v2_count)
+    const uint32_t *irec32;  // inline records, IREC_W words per pair (word 7 = E | REC_INLINE_FLAG)
     int32_t *arena;
     uint32_t *dep_scratch;   // at dep_off[j0] + idx, compacted later
     uint64_t *u_cnt;
@@ -1171,15 +1241,14 @@ __device__ __forceinline__ TxnCtx txn_ctx(const V2View &v, const V2Out &o, uint3
     return c;
 }
 
-// Key k's runs from its 64-B record (record index jk); an inline record is one run of its own entries (m = INLINE_M,
-// start = the record index). Returns the key's raw length.
+// Key k's runs from its record (pair index jk); an inline record is one run of its own entries (m = INLINE_M,
+// start = the pair index). Returns the key's raw length.
 template <int MAXK>
-__device__ __forceinline__ uint32_t load_record(RunsT<MAXK> &R, const uint4 *rec, uint32_t jk, uint32_t k)
+__device__ __forceinline__ uint32_t load_record(RunsT<MAXK> &R, const uint4 *rec, const uint32_t *irec32, uint32_t jk, uint32_t k)
 {
-    const uint4 *r = rec + 4 * (size_t)jk;
-    const uint4 r3 = r[3];
-    if (r3.w & REC_INLINE_FLAG) {
-        const uint32_t e = r3.w & ~REC_INLINE_FLAG;
+    const uint32_t w = irec32[IREC_W * (size_t)jk + 7];
+    if (w & REC_INLINE_FLAG) {
+        const uint32_t e = w & ~REC_INLINE_FLAG;
         R.start[k][0] = jk;
         R.pre[k][0] = 0;
 #pragma unroll
@@ -1187,7 +1256,8 @@ __device__ __forceinline__ uint32_t load_record(RunsT<MAXK> &R, const uint4 *rec
         R.m[k] = INLINE_M;
         return e;
     }
-    const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
+    const uint4 *r = rec + 4 * (size_t)jk;
+    const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
     const uint32_t a[6] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y };
     const uint32_t l[6] = { r1.z, r1.w, r2.x, r2.y, r2.z, r2.w };
     uint32_t acc = 0;
@@ -1206,7 +1276,7 @@ __device__ uint32_t compute_runs(RunsT<MAXK> &R, const V2View &v, const V2Out &o
     const uint32_t lane = lane_id();
     uint32_t ktot = 0;
     if (lane < c.nk && cnt[c.j0 + lane] != 0) {
-        ktot = load_record(R, o.rec, c.j0 + lane, lane);
+        ktot = load_record(R, o.rec, o.irec32, c.j0 + lane, lane);
     } else if (lane < c.nk) {
         for (int q = 0; q <= NRUN; ++q) R.pre[lane][q] = 0;
         R.m[lane] = NO_M;
@@ -1231,7 +1301,7 @@ __device__ __forceinline__ bool fetch_elem(const RunsT<MAXK> &R, const V2View &v
     k = lo;
     uint32_t off = e - R.kbase[k];
     if (R.m[k] == INLINE_M) {   // inline record: the entry itself (filters applied by the count pass)
-        x = v.rec32[16 * (size_t)R.start[k][0] + off];
+        x = inl_entry(v.irec32, v.rec, 16 * R.start[k][0] + off);
         return true;
     }
     uint32_t r = 0;
@@ -1590,7 +1660,7 @@ __device__ void big_one(BigLds<CAP, NT> &L, uint32_t t, const V2View &v, const u
         }
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u)
-            x[u] = in[u] ? (il[u] ? v.rec32[idx[u]] : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
+            x[u] = in[u] ? (il[u] ? inl_entry(v.irec32, v.rec, idx[u]) : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
 #pragma unroll
         for (int u = 0; u < BIG_GU; ++u) {
             const uint32_t e = e0 + u * NT;
@@ -1735,7 +1805,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             const uint32_t k = tid;
             uint32_t mn = 0xFFFFFFFFu;
             if (R.m[k] == INLINE_M) {
-                if (R.pre[k][1] > 0) mn = v.rec32[16 * R.start[k][0]];
+                if (R.pre[k][1] > 0) mn = v.irec32[IREC_W * (size_t)R.start[k][0]];
             } else {
 #pragma unroll
                 for (int q = 0; q < 6; ++q)
@@ -1767,7 +1837,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             }
 #pragma unroll
             for (int u = 0; u < BIG_GU; ++u)
-                x[u] = in[u] ? (il[u] ? v.rec32[idx[u]] : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
+                x[u] = in[u] ? (il[u] ? inl_entry(v.irec32, v.rec, idx[u]) : r3[u] ? v.bc_rank[idx[u]] : v.list_rank[idx[u]]) : 0u;
 #pragma unroll
             for (int u = 0; u < BIG_GU; ++u) {
                 bool keep = in[u] && (il[u] || !(c.bq && x[u] == c.trank));
@@ -2057,10 +2127,11 @@ constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream tx
 // no look-back), and the big-txn classification: more than ST_K keys, or (txns with a run record: bigflag = 1 from the
 // count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
 __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *__restrict__ key_off,
-                                                   const uint32_t *__restrict__ rec32, uint32_t *__restrict__ psz,
+                                                   const uint32_t *__restrict__ irec32, const uint4 *__restrict__ rec,
+                                                   uint32_t *__restrict__ psz,
                                                    uint32_t raw_cap, uint32_t e_cap,
                                                    uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
-                                                   uint64_t *__restrict__ szK)
+                                                   uint64_t *__restrict__ szK, uint64_t *__restrict__ any16)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / ST_G, sub = threadIdx.x & (ST_G - 1);
     if (t >= n) return;   // group-uniform: shuffles stay inside the group
@@ -2070,12 +2141,15 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
     uint32_t e = 0, kd = 0, raw = 0;
     for (uint32_t c0 = 0; c0 < nk; c0 += ST_G) {
         if (c0 + sub < nk) {
-            const uint32_t *r = rec32 + 16 * (size_t)(j0 + c0 + sub);
-            const uint32_t w = r[15];
+            const uint32_t w = irec32[IREC_W * (size_t)(j0 + c0 + sub) + 7];
             const uint32_t ej = w & ~REC_INLINE_FLAG;
             e += ej;
             kd += ej != 0;
-            if (run_rec && !(w & REC_INLINE_FLAG)) raw += r[6] + r[7] + r[8] + r[9] + r[10] + r[11] + r[13];
+            if (run_rec && !(w & REC_INLINE_FLAG)) {
+                const uint4 *r = rec + 4 * (size_t)(j0 + c0 + sub);
+                const uint4 r1 = r[1], r2 = r[2], r3 = r[3];
+                raw += r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
+            }
             if (maybe_big) psz[j0 + c0 + sub] = ej;   // the big txns' per-pair entry counts (k_v3_bigsz, k_v3_bigfill)
         }
     }
@@ -2090,6 +2164,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
         bigflag[t] = big ? 1u : 0u;
         szA[t] = (uint64_t)kd + e;
         szK[t] = kd;
+        // a big txn of 9-16 keys with entries: the 16-key window tier has work (read at the host sync after the scans)
+        if (big && e && nk > 8 && nk <= 16 && !*any16) atomicOr((unsigned long long *)any16, 1ull);
     }
 }
 
@@ -2223,7 +2299,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
 struct V3Stream {
     V2View v;
     const uint32_t *key_off, *bigflag, *txn_of_rank;
-    const uint4 *rec;
+    const uint4 *rec, *irec;
     const uint64_t *bK, *bE;                  // sizes of the big txns
     const uint64_t *arena_off, *kd_off;       // from the size scans
     uint64_t *u_cnt_out;
@@ -2343,13 +2419,20 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
     bool run = false;
     uint4 r0 = {}, r1 = {}, r2 = {}, r3 = {};
     if (sm && sub < c.nk) {
-        const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
-        r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
-        if (r3.w & REC_INLINE_FLAG) {
-            e = r3.w & ~REC_INLINE_FLAG;
+        const uint4 *ir = s.irec + 2 * (size_t)(c.j0 + sub);
+        r0 = ir[0]; r1 = ir[1];
+        const uint32_t w = r1.w;
+        if (w & REC_INLINE_FLAG) {
+            e = w & ~REC_INLINE_FLAG;
+            if (e > IREC_N) {   // entries 7.. in the first half of the 64-B slot
+                const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
+                r2 = r[0]; r3 = r[1];
+            }
         } else {
+            const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
+            r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
             run = true;
-            e = r3.w;
+            e = w;
             rawk = r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
         }
     }
@@ -2363,7 +2446,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
     kbase[grp][sub] = e_incl - e;
     kc[grp][sub] = 0;
     if (sm && !run) {
-        const uint32_t w[15] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z };
+        const uint32_t w[REC_INLINE] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z, r3.w };
         const uint32_t b0 = in_incl - ein;
 #pragma unroll
         for (uint32_t q = 0; q < REC_INLINE; ++q)
@@ -3055,7 +3138,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *totals = ctx->get<uint32_t>("v2_totals", 16);
     uint32_t *bases = ctx->get<uint32_t>("v2_bases", 16);
     V2Cols cols;
-    cols.rows = ctx->get<uint4>("v2_rows", 2 * (P + 1));
+    cols.rdir = ctx->get<uint4>("v2_rdir", 4 * (P / RD_W + 1));
     cols.list_rank = ctx->get<uint32_t>("v2_list_rank", P);
     cols.bc_rank = ctx->get<uint32_t>("v2_bc_rank", P);
     cols.bc_exec = ctx->get<uint32_t>("v2_bc_exec", P);
@@ -3128,24 +3211,29 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
 
     V2View vv;
     vv.perm = ps.vals; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
-    vv.s_rank = s_rank; vv.s_exec = s_exec; vv.s_info = s_info; vv.rows = cols.rows; vv.tinfo = tinfo;
+    vv.s_rank = s_rank; vv.s_exec = s_exec; vv.s_info = s_info; vv.rdir = cols.rdir; vv.tinfo = tinfo;
     vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm;
     vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw;
 
     // ---- count pass: per-pair records, big-txn flags, E
     if (P >= 0x80000000ull) fail(ACC_E_CAP, "n_pairs must be < 2^31 (count-pass record format)");
-    uint4 *rec = ctx->get<uint4>("v2_rec", 4 * P);
-    vv.rec32 = reinterpret_cast<const uint32_t *>(rec);
+    RecOut ro;
+    ro.rec = ctx->get<uint4>("v2_rec", 4 * P);
+    ro.irec = ctx->get<uint4>("v2_irec", 2 * P);
+    uint4 *rec = ro.rec;
+    vv.irec32 = reinterpret_cast<const uint32_t *>(ro.irec);
+    vv.rec = ro.rec;
+
     uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
     uint32_t *bpos = ctx->get<uint32_t>("v3_bpos", n);
     uint64_t *blk_e = ctx->get<uint64_t>("v3_blk_e", gP);
-    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 2);
+    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N);
     ACC_HIP(hipMemsetAsync(bigflag, 0, (size_t)n * 4, st));
-    ACC_HIP(hipMemsetAsync(tot, 0, 2 * sizeof(uint64_t), st));
+    ACC_HIP(hipMemsetAsync(tot, 0, 3 * sizeof(uint64_t), st));
     ACC_HIP(hipMemsetAsync(gstat, 0, GSTAT_N * sizeof(uint64_t), st));
     uint32_t *psz = ctx->get<uint32_t>("v2_psz", P);   // per pair of a run-record txn: its entry count (k_v3_mark)
-    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, rec, bigflag, blk_e);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
     const char *rc_env = getenv("ACC_ST_RAW");
     const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
     const char *ec_env = getenv("ACC_ST_ECAP");
@@ -3153,8 +3241,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
-    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.rec32, psz, raw_cap,
-           e_cap, bigflag, szA, szK);
+    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.irec32, (const uint4 *)rec, psz, raw_cap,
+           e_cap, bigflag, szA, szK, tot + 2);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, szA, arena_off, n, true, arena_off + n);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, szK, kd_off, n, true, kd_off + n);
     uint32_t *nbig_dev = reinterpret_cast<uint32_t *>(tot + 1);
@@ -3164,10 +3252,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *blist = ctx->get<uint32_t>("v3_blist", n);
     launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bigflag,
            (const uint32_t *)bpos, blist);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
     const uint32_t nbig = (uint32_t)ctx->pinned[1];
+    const bool any16 = ctx->pinned[2] != 0;
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
 
     int32_t *arena = ctx->get<int32_t>("arena", P + E);
@@ -3230,7 +3319,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
         wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = varena; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
         wo.arena = arena_scr; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
-        wo.rec = rec; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+        wo.rec = rec; wo.irec32 = vv.irec32; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
         // on a side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
@@ -3245,11 +3334,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
             launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)ctx->get<uint32_t>("v2_w8_list", nbig), (const uint64_t *)(gstat + 7), vv,
                    (const uint64_t *)vcnt, wo);
-            // (> 8 keys is rare: a small persistent grid, so an empty list costs one short wave of blocks rather than
-            // 1024 blocks of 56 KiB LDS queueing behind the stream pass)
-            launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 256)), dim3(BLOCK), 0,
-                   (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
-                   (const uint64_t *)vcnt, wo);
+            // (> 8 keys is rare: a small persistent grid, launched only when the mark pass saw a big txn of 9-16 keys)
+            if (any16)
+                launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 256)), dim3(BLOCK), 0,
+                       (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
+                       (const uint64_t *)vcnt, wo);
         } else if (big_ok) {
             sort_tiers(true);
         } else {
@@ -3269,7 +3358,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);
     V3Stream sp;
     sp.v = vv; sp.err = gstat + 5;
-    sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.bK = bK; sp.bE = bE;
+    sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.irec = ro.irec; sp.bK = bK; sp.bE = bE;
     sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
     sp.dep_scr = dep_st; sp.n = n; sp.ntiles = ntiles;
     auto stream = [&](auto ent_tag) {

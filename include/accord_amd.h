@@ -710,11 +710,13 @@ int  acc_cfk_view(acc_ctx *ctx, acc_cfk *cfk, acc_batch_in *out);
  * is applied in array order to every key each lists, as SafeCommandStore.updateCommandsForKey calls
  * CommandsForKey.update(prev, next) (local/SafeCommandStore.java:217-240): status = the new InternalStatus (0xFF: the
  * save status maps to none, no change), flags bit 0 = acceptedOrCommitted changed since the previous update (the
- * reference returns the CFK unchanged for an equal status otherwise), execute_at = Command.executeAt(), and per
+ * reference returns the CFK unchanged for an equal status otherwise), flags bit 1 = next.status() == AcceptedInvalidate
+ * (Commands.acceptInvalidate may move an Accepted command to AcceptedInvalidateWithDefinition = PREACCEPTED: no stale
+ * status check, the CFK stays unchanged, CommandsForKey.java:681-688), execute_at = Command.executeAt(), and per
  * (update, key) pair the command's partialDeps().keyDeps.txnIds(key) [dep_off[j], dep_off[j+1]) sorted. Deps the CFK
  * lacks become TRANSITIVELY_KNOWN entries; TxnIds it holds (uncommitted, witnessed) that a dep list lacks go to that
  * TxnInfo's missing[]; committing removes a TxnId from every missing[]. A status going back is ACC_E_STATE (the
- * reference's IllegalStateException). RedundantBefore is empty. The result (keys without entries dropped) is
+ * reference's IllegalStateException) unless flags bit 1 is set. RedundantBefore is empty. The result (keys without entries dropped) is
  * device-resident until the next compute call, and its missing[] is what acc_map_reduce_full's WITH / WITHOUT tests
  * read. */
 typedef struct acc_cfk_snap {

@@ -299,7 +299,8 @@ static void update_or_insert_with_additions(cfk *c, long src_insert, long src_up
     c->n = count;
 }
 
-static void apply_one(cfk *c, const cts *id, const cts *ex, int st, int ballot_changed, const cts *deps, size_t nd, cerr *e)
+/* fl: bit 0 = acceptedOrCommitted changed since the previous update, bit 1 = next.status() == AcceptedInvalidate */
+static void apply_one(cfk *c, const cts *id, const cts *ex, int st, int fl, const cts *deps, size_t nd, cerr *e)
 {
     long pos = bsearch_info(c, 0, (long)c->n, id);
     if (pos < 0) {
@@ -317,9 +318,9 @@ static void apply_one(cfk *c, const cts *id, const cts *ex, int st, int ballot_c
     }
     info *cur = &c->t[pos];
     if (st <= cur->st) {
-        /* Invariants.checkState(cur.status == newStatus || AcceptedInvalidate) (:681-683) */
-        if (cur->st != st) { c_fail(e, -2, "stale status update to CommandsForKey (IllegalStateException)"); return; }
-        if (!has_info(st) || !ballot_changed) return;      /* acceptedOrCommitted unchanged: this (:684-685) */
+        /* Invariants.checkState(cur.status == newStatus || next.status() == AcceptedInvalidate) (:681-686) */
+        if (cur->st != st && !(fl & 2)) { c_fail(e, -2, "stale status update to CommandsForKey (IllegalStateException)"); return; }
+        if (!has_info(st) || !(fl & 1)) return;            /* acceptedOrCommitted unchanged: this (:687-688) */
     }
     const int prev_st = cur->st;
     if (has_info(st)) {
@@ -394,7 +395,7 @@ orc_cfk_result *orc_cfk_apply(uint32_t n_keys, const uint64_t *key, const uint32
             cts *deps = malloc((nd + 1) * sizeof *deps);
             for (size_t q = 0; q < nd; ++q) deps[q] = (cts){ dmsb[udep_off[j] + q], dlsb[udep_off[j] + q], dnode[udep_off[j] + q] };
             for (size_t q = 1; q < nd; ++q) if (c_cmp(&deps[q - 1], &deps[q]) >= 0) c_fail(&E, -1, "deps must be sorted unique");
-            if (!E.code) apply_one(&cs[a], &id, &ex, ust[u], uflags[u] & 1, deps, nd, &E);
+            if (!E.code) apply_one(&cs[a], &id, &ex, ust[u], uflags[u], deps, nd, &E);
             free(deps);
         }
     }

@@ -30,7 +30,7 @@ def _ts_key(m, l, n):
 
 
 def cfk_case(seed, n_txn=200, n_keys=12, keys_per=3, p_dep=0.5, p_bump=0.5, p_invalid=0.05, p_reaccept=0.15,
-             p_noop=0.03, window=40):
+             p_noop=0.03, window=40, p_accinv=0.1):
     """The updates in the CFK_UPD layout of oracle.py. Events of different txns interleave; each txn's
     own events stay in lifecycle order."""
     rng = np.random.default_rng(seed)
@@ -50,6 +50,11 @@ def cfk_case(seed, n_txn=200, n_keys=12, keys_per=3, p_dep=0.5, p_bump=0.5, p_in
             ev.append((INVALID, tid[i], 0))
         else:
             ev.append((ACC, tid[i], 0))
+            if rng.random() < p_accinv:
+                # a recovery's Commands.acceptInvalidate (Commands.java:267-297): AcceptedInvalidateWithDefinition maps
+                # to PREACCEPTED, below the CFK's ACCEPTED (flags bit 1: no stale check, no change), then a new Accept
+                ev.append((PRE, tid[i], 2))
+                ev.append((ACC, tid[i], 1))
             if rng.random() < p_reaccept:
                 ev.append((ACC, tid[i], 1))
             ex = tid[i]
