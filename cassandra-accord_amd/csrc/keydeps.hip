@@ -2115,7 +2115,7 @@ __global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t
 // dep_txn) directly: one read of 64 B of record per pair, writes of the outputs only.
 // The other ("big") txns take the v2 tiers into scratch arrays addressed by prefix sums over the big txns in txn
 // order (k_v3_bigfill gives them per-pair offsets, so the tiers' indexing is unchanged), report their sizes to the
-// stream pass, and k_v3_bigcopy moves them into place.
+// stream pass; their KeyDeps headers, key indices and entries go straight to the final arrays.
 
 constexpr int ST_G = 16;                      // lanes per txn
 constexpr int ST_K = 16;                      // keys of a stream txn
@@ -2176,23 +2176,19 @@ __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t
     if (t < n && bigflag[t]) blist[bpos[t]] = t;
 }
 
-// per big txn (one wave each, list order): dependency entries E and non-empty keys Kd from the records' word 15
+// per big txn (one wave each, list order): dependency entries E from the per-pair counts of the mark pass
 __global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_t *__restrict__ blist,
                                                     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ psz,
-                                                    uint64_t *__restrict__ lE, uint64_t *__restrict__ lK, uint64_t *__restrict__ lA)
+                                                    uint64_t *__restrict__ lE)
 {
     const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
     if (i >= nbig) return;
     const uint32_t t = blist[i], j0 = key_off[t], j1 = key_off[t + 1];
-    uint64_t E = 0, K = 0;
-    for (uint32_t j = j0 + lane; j < j1; j += 64) {
-        const uint32_t e = psz[j];
-        E += e;
-        K += e != 0;
-    }
+    uint64_t E = 0;
+    for (uint32_t j = j0 + lane; j < j1; j += 64) E += psz[j];
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { E += shfl_xor(E, d); K += shfl_xor(K, d); }
-    if (lane == 0) { lE[i] = E; lK[i] = K; lA[i] = E + K; }
+    for (int d = 32; d >= 1; d >>= 1) E += shfl_xor(E, d);
+    if (lane == 0) lE[i] = E;
 }
 
 // tier routing of the big txns (thread per list entry, one atomic per list per block). With ranks within 25 bits: the
@@ -2247,24 +2243,25 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
 struct V3Big {
     const uint32_t *blist, *key_off;
     const uint32_t *psz;
-    const uint64_t *dB, *kB, *aB;             // exclusive prefixes over the list: scratch bases
+    const uint64_t *dB;                       // exclusive prefix of E over the list: TxnId scratch bases
+    const uint64_t *arena_off, *kd_off;       // the batch's final offsets (from the mark pass's scans)
     uint64_t *vdep_off, *vcnt;                // per pair of a big txn (dep_off / cnt of the v2 tiers)
     uint32_t *vcnz;                           // per pair of a big txn (cnz)
-    uint64_t *varena, *bK, *bE, *u_cnt;       // per txn (big txns only)
-    int32_t *arena_scr;
-    uint32_t *key_scr;
+    uint64_t *u_cnt;                          // per txn (big txns only)
+    int32_t *arena;
+    uint32_t *key_idx;
 };
 
-// per big txn (one wave): the v2 tiers' per-pair offsets, the KeyDeps headers and key indices into scratch, and the
-// sizes the stream pass reads
+// per big txn (one wave): the v2 tiers' per-pair offsets, and the KeyDeps header and key indices straight into the
+// final arena / key_idx (the tiers then write the entries at arena_off[t] too: no copy into place afterwards)
 __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
 {
     const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
     if (i >= nbig) return;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t t = b.blist[i], j0 = b.key_off[t], j1 = b.key_off[t + 1], nk = j1 - j0;
-    const uint64_t dbase = b.dB[i], kbase = b.kB[i], abase = b.aB[i];
-    const uint64_t E = b.dB[i + 1] - dbase, Kd = b.kB[i + 1] - kbase;
+    const uint64_t dbase = b.dB[i], kbase = b.kd_off[t], abase = b.arena_off[t];
+    const uint64_t E = b.dB[i + 1] - dbase, Kd = b.kd_off[t + 1] - kbase;
     uint64_t ecur = 0, kcur = 0;
     for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
         const uint32_t j = j0 + c0 + lane;
@@ -2279,8 +2276,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
             b.vcnt[j] = e;
             b.vcnz[j] = (uint32_t)(kbase + kcur + kb);
             if (e) {
-                b.arena_scr[abase + kcur + kb] = (int32_t)(Kd + eoff + e);
-                b.key_scr[kbase + kcur + kb] = c0 + lane;
+                b.arena[abase + kcur + kb] = (int32_t)(Kd + eoff + e);
+                b.key_idx[kbase + kcur + kb] = c0 + lane;
             }
         }
         ecur += shfl_idx(einc, 63);
@@ -2289,9 +2286,6 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
     if (lane == 0) {
         b.vdep_off[j1] = dbase + E;
         b.vcnz[j1] = (uint32_t)(kbase + Kd);
-        b.varena[t] = abase;
-        b.bK[t] = Kd;
-        b.bE[t] = E;
         b.u_cnt[t] = 0;
     }
 }
@@ -2300,7 +2294,6 @@ struct V3Stream {
     V2View v;
     const uint32_t *key_off, *bigflag, *txn_of_rank;
     const uint4 *rec, *irec;
-    const uint64_t *bK, *bE;                  // sizes of the big txns
     const uint64_t *arena_off, *kd_off;       // from the size scans
     uint64_t *u_cnt_out;
     int32_t *arena;
@@ -2599,22 +2592,6 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
         row[7] = 1;
     }
 #endif
-}
-
-// big txns' arena and key scratch -> final arrays (one wave per big txn; their TxnIds go through k_v3_ucompact)
-__global__ __launch_bounds__(BLOCK) void k_v3_bigcopy(uint32_t nbig, const uint32_t *__restrict__ blist,
-                                                      const uint64_t *__restrict__ varena, const uint64_t *__restrict__ kB,
-                                                      const uint64_t *__restrict__ arena_off, const uint64_t *__restrict__ kd_off,
-                                                      const int32_t *__restrict__ arena_scr, const uint32_t *__restrict__ key_scr,
-                                                      int32_t *__restrict__ arena, uint32_t *__restrict__ key_idx)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= nbig) return;
-    const uint32_t t = blist[i];
-    const uint64_t A = arena_off[t + 1] - arena_off[t], K = kd_off[t + 1] - kd_off[t];
-    const uint64_t as = varena[t], ad = arena_off[t], ks = kB[i], kd = kd_off[t];
-    for (uint64_t q = lane; q < A; q += 64) arena[ad + q] = arena_scr[as + q];
-    for (uint64_t q = lane; q < K; q += 64) key_idx[kd + q] = key_scr[ks + q];
 }
 
 // Sparse batches (a mixed batch's range txns have no KeyDeps of their own here): the txns with TxnIds, compacted with
@@ -3263,12 +3240,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *key_idx = ctx->get<uint32_t>("key_idx", P);
     uint32_t *dep_txn = ctx->get<uint32_t>("dep_txn", E);
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
-    uint64_t *bK = ctx->get<uint64_t>("v3_bK", n);
-    uint64_t *bE = ctx->get<uint64_t>("v3_bE", n);
     uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
-    uint64_t *lB = nullptr, *varena = nullptr, *vdep_off = nullptr;
-    int32_t *arena_scr = nullptr;
-    uint32_t *key_scr = nullptr, *dep_scr = nullptr;
+    uint64_t *vdep_off = nullptr;
+    uint32_t *dep_scr = nullptr;
     uint64_t nfb = 0, efb = 0, nmed = 0, nbig2 = 0;
     ctx->stat("keydeps.huge_txns", 0);
     V2Out wo{};
@@ -3287,38 +3261,31 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
                (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
     };
-    // ---- big txns: v2 tiers into scratch
+    // ---- big txns: v2 tiers, headers / key indices / entries into the final arrays, TxnIds into scratch
     if (nbig) {
         const unsigned gB = (nbig + WAVES - 1) / WAVES;
-        uint64_t *lE = ctx->get<uint64_t>("v3_lE", nbig), *lK = ctx->get<uint64_t>("v3_lK", nbig), *lA = ctx->get<uint64_t>("v3_lA", nbig);
-        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, (const uint32_t *)psz, lE, lK, lA);
-        uint64_t *dB = ctx->get<uint64_t>("v3_dB", (size_t)nbig + 1), *kB = ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1);
-        lB = ctx->get<uint64_t>("v3_aB", (size_t)nbig + 1);
+        uint64_t *lE = ctx->get<uint64_t>("v3_lE", nbig);
+        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, (const uint32_t *)psz, lE);
+        uint64_t *dB = ctx->get<uint64_t>("v3_dB", (size_t)nbig + 1);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, lE, dB, nbig, true, dB + nbig);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, lK, kB, nbig, true, kB + nbig);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, lA, lB, nbig, true, lB + nbig);
         vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
         vcnt = ctx->get<uint64_t>("cnt", P);
         uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
-        varena = ctx->get<uint64_t>("v3_varena", n);
-        arena_scr = ctx->get<int32_t>("v3_arena_scr", P + E);
-        key_scr = ctx->get<uint32_t>("v3_key_scr", P);
         dep_scr = ctx->get<uint32_t>("v2_dep_scratch", E);
         med_list = ctx->get<uint32_t>("v2_med_list", nbig);
         big_list = ctx->get<uint32_t>("v2_big_list", nbig);
         fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
         V3Big bg;
-        bg.blist = blist; bg.key_off = key_off; bg.psz = psz; bg.dB = dB; bg.kB = kB; bg.aB = lB;
-        bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.varena = varena; bg.bK = bK; bg.bE = bE; bg.u_cnt = u_cnt;
-        bg.arena_scr = arena_scr; bg.key_scr = key_scr;
+        bg.blist = blist; bg.key_off = key_off; bg.psz = psz; bg.dB = dB; bg.arena_off = arena_off; bg.kd_off = kd_off;
+        bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.u_cnt = u_cnt; bg.arena = arena; bg.key_idx = key_idx;
         const bool big_ok = rbits + 6 <= 31;
         win_ok = big_ok && !getenv("ACC_NO_WIN");   // tuning switch: the sorting tiers instead of the window tier
         launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
                key_off, (const uint64_t *)lE, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
                ctx->get<uint32_t>("v2_w8_list", nbig), ctx->get<uint32_t>("v2_w16_list", nbig), gstat);
         launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
-        wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = varena; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
-        wo.arena = arena_scr; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
+        wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = arena_off; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
+        wo.arena = arena; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
         wo.rec = rec; wo.irec32 = vv.irec32; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
@@ -3358,7 +3325,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);
     V3Stream sp;
     sp.v = vv; sp.err = gstat + 5;
-    sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.irec = ro.irec; sp.bK = bK; sp.bE = bE;
+    sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.irec = ro.irec;
     sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
     sp.dep_scr = dep_st; sp.n = n; sp.ntiles = ntiles;
     auto stream = [&](auto ent_tag) {
@@ -3398,11 +3365,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     // ---- big txns' arena / keys into place, TxnId offsets and compaction. With global-path txns (known only after
     // the tiers ran) this is redone once they are written, so the common case pays one host sync here.
     auto finish = [&]() {
-        if (nbig)
-            launch(ctx, "v3_bigcopy", k_v3_bigcopy, dim3((nbig + WAVES - 1) / WAVES), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
-                   (const uint64_t *)varena, (const uint64_t *)ctx->get<uint64_t>("v3_kB", (size_t)nbig + 1),
-                   (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const int32_t *)arena_scr, (const uint32_t *)key_scr,
-                   arena, key_idx);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, u_off, n, true, u_off + n);
         const uint32_t *tmap = nullptr, *ne_cnt = nullptr;
         const uint64_t *uo = u_off;
@@ -3479,7 +3441,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         Sorted s2 = radix_sort(ctx, "rs_big2", key2, nullptr, efb, bbits + kbits + rbits);
         launch(ctx, "v2_big_arena", k_v2_big_arena, dim3(grid_for(efb, BLOCK)), dim3(BLOCK), 0, efb,
                (const uint32_t *)s2.vals, (const uint64_t *)s2.keys, (const uint32_t *)idx1, (const uint32_t *)fb_list,
-               (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)vcnz, (const uint64_t *)varena, arena_scr);
+               (const uint64_t *)fb_off, rbits, kbits, key_off, (const uint32_t *)vcnz, (const uint64_t *)arena_off, arena);
         finish();
     }
     ctx->stat("keydeps.stream_txns", n - nbig);
@@ -3489,7 +3451,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ctx->stat("keydeps.fallback_txns", nfb);
     ctx->stat("keydeps.fallback_entries", efb);
     ctx->stat("keydeps.bumped_committed", nbc);
-    (void)lB;
     *view = acc_keydeps_view{ n, ctx->pinned[GSTAT_N], ctx->pinned[GSTAT_N + 1], ctx->pinned[GSTAT_N + 2], E, arena_off,
                               arena, kd_off, key_idx, u_off, dep_txn };
     ctx->kd_view = *view;
