@@ -104,7 +104,7 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const 
 {
     __shared__ uint32_t ko[BLOCK + 1];
     const uint32_t tid = threadIdx.x;
-    uint64_t m0 = 0, m1 = 0, m2 = 0, km = 0, errs = 0, unsorted = 0;
+    uint64_t m0 = 0, m1 = 0, m2 = 0, km = 0, errs = 0, unsorted = 0, ornk = 0;
     uint32_t differs = 0;
     const uint64_t r0 = tm[0], r1 = ts_w1(tl[0]), r2 = ts_w2(tn[0]);
     const uint64_t kref = P ? key_code[0] : 0;
@@ -132,6 +132,7 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const 
         __syncthreads();
         const bool bad = tid < tcnt && ko[tid + 1] < ko[tid];
         if (bad) errs |= ERR_KEY_OFF;
+        else if (tid < tcnt) ornk |= ko[tid + 1] - ko[tid];   // bounds the keys per txn (pair packing)
         if (!__syncthreads_or(bad ? 1 : 0) && P) {
             const uint32_t a = (uint32_t)min((size_t)ko[0], P), b = (uint32_t)min((size_t)ko[tcnt], P);
             for (uint32_t j = a + tid; j < b; j += BLOCK) {
@@ -145,8 +146,8 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const 
         }
     }
     uint64_t *gs = g + 8 * (blockIdx.x % PREP_SLOTS);
-    uint64_t v[6] = { m0, m1, m2, km, errs, unsorted };
-    block_or_n<6>(v, gs);
+    uint64_t v[7] = { m0, m1, m2, km, errs, unsorted, ornk };
+    block_or_n<7>(v, gs);
     __shared__ uint32_t s_nd;
     if (tid == 0) s_nd = 0;
     __syncthreads();
@@ -311,11 +312,15 @@ struct PairPlan {
     Runs rk;       // key code compaction
     int rbits;     // txn-rank bits in the composite (0 when the batch is already in TxnId order)
     int mode;      // 0: key only (sorted batch), 1: (key << rbits) | rank, 2: key only after a rank pre-sort,
-                   // 3: (key << 32) | pair index, keys-only sort (sorted batch, key within 32 bits)
+                   // 3: (key << 32) | pair index, keys-only sort (sorted batch, key within 32 bits);
+                   // 4: (key << 32) | owner << sb | slot (mode 3 with the pair's txn packed: the CFK columns gather the
+                   //    16-MB txn records directly instead of a 16-B per-pair copy)
+    int sb;        // mode 4: bits of the key slot within its txn
 };
 
 __global__ __launch_bounds__(BLOCK) void k_pair_keys(size_t P, const uint64_t *__restrict__ key_code,
-                                                     const uint32_t *__restrict__ owner, const uint32_t *__restrict__ rank,
+                                                     const uint32_t *__restrict__ owner, const uint32_t *__restrict__ key_off,
+                                                     const uint32_t *__restrict__ rank,
                                                      const uint32_t *__restrict__ perm, PairPlan plan,
                                                      int rank_only, uint64_t *__restrict__ out)
 {
@@ -324,18 +329,28 @@ __global__ __launch_bounds__(BLOCK) void k_pair_keys(size_t P, const uint64_t *_
     size_t j = perm ? perm[i] : i;
     if (rank_only) { out[i] = rank[owner[j]]; return; }
     uint64_t kc = pext_runs(key_code[j], plan.rk);
+    if (plan.mode == 4) {
+        const uint32_t t = owner[j];
+        out[i] = (kc << 32) | ((uint64_t)t << plan.sb) | (uint64_t)(j - key_off[t]);
+        return;
+    }
     out[i] = plan.mode == 1 ? ((kc << plan.rbits) | rank[owner[j]]) : plan.mode == 3 ? ((kc << 32) | i) : kc;
 }
 
 // packed (key << 32 | pair index) sort output: segment-start flags and the permutation
+// sb >= 0 (mode 4): the low word is owner << sb | slot; the pair index is key_off[owner] + slot, the owner goes to pown
 __global__ __launch_bounds__(BLOCK) void k_seg_flags_packed(size_t P, const uint64_t *__restrict__ sp, uint32_t *__restrict__ flag,
-                                                            uint32_t *__restrict__ perm)
+                                                            uint32_t *__restrict__ perm, int sb, const uint32_t *__restrict__ key_off,
+                                                            uint32_t *__restrict__ pown)
 {
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
     const uint64_t x = sp[p];
     flag[p] = p == 0 || (x >> 32) != (sp[p - 1] >> 32);
-    perm[p] = (uint32_t)x;
+    if (sb < 0) { perm[p] = (uint32_t)x; return; }
+    const uint32_t t = (uint32_t)x >> sb, slot = (uint32_t)x & ((1u << sb) - 1u);
+    perm[p] = key_off[t] + slot;
+    pown[p] = t;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seg_flags(size_t P, const uint64_t *__restrict__ skeys, int key_shift,
@@ -684,7 +699,9 @@ __global__ __launch_bounds__(BLOCK) void k_write_keys(size_t P, const uint64_t *
 // [segmented prefix max], predecessor of S among bumped committed Writes [small sorted list]).
 
 constexpr int NLIST = 6;   // U_R, U_W, U_S, C_R, C_W, C_S
-constexpr int NCNT = 8;    // 6 list counts, bumped-committed count, last-unbumped-committed-write max
+constexpr int NCNT = 9;    // 6 list counts, bumped-committed count, last-unbumped-committed-write max, segment starts
+constexpr int NRD = 8;     // the rank directory's columns (all but the segment count)
+__device__ __forceinline__ bool cnt_is_max(int q) { return q == 7; }
 
 // Kind class for the Kinds predicates (Txn.java:140-152): Read 0, Write 1, SyncPoint/ExclusiveSyncPoint 2;
 // EphemeralRead and LocalOnly are witnessed by no predicate (3 = none).
@@ -729,9 +746,10 @@ __device__ __forceinline__ void v2_codes4(size_t P, size_t base, const uint32_t 
 // The CFK columns of four consecutive positions per thread (s_rank / s_exec / s_info from the per-pair txn records, the
 // segment starts, optionally pair_pos) and the per-tile counts of the class lists (the multi-scan's reduce step) over
 // the same 1024-position tile that k_v2_apply scans.
+// pown (mode 4): each position's owner txn, its record read from tinfo (16 B per txn) instead of ptinfo (per pair)
 __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
-                                                       const uint32_t *__restrict__ seg_incl, const uint32_t *__restrict__ seg_flag,
-                                                       uint32_t *__restrict__ seg_start, uint32_t *__restrict__ s_rank,
+                                                       const uint32_t *__restrict__ pown, const uint4 *__restrict__ tinfo,
+                                                       const uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ s_rank,
                                                        uint32_t *__restrict__ s_exec, uint8_t *__restrict__ s_info,
                                                        uint32_t *__restrict__ pair_pos, uint32_t *__restrict__ tile_sums,
                                                        uint32_t ntiles)
@@ -740,25 +758,27 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t 
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t c[NCNT] = {};
     if (base < P) {
-        uint32_t j[V2_ITEMS], sg[V2_ITEMS], fl[V2_ITEMS];
+        uint32_t j[V2_ITEMS], fl[V2_ITEMS];
         uint4 ti[V2_ITEMS];
 #pragma unroll
         for (int i = 0; i < V2_ITEMS; ++i) {
             const bool in = base + i < P;
-            j[i] = in ? perm[base + i] : 0u;
-            sg[i] = in ? seg_incl[base + i] : 0u;
+            j[i] = in ? (pown ? pown[base + i] : perm[base + i]) : 0u;
             fl[i] = in ? seg_flag[base + i] : 0u;
         }
 #pragma unroll
-        for (int i = 0; i < V2_ITEMS; ++i) ti[i] = base + i < P ? ptinfo[j[i]] : make_uint4(0u, 0u, 0u, 0u);
+        for (int i = 0; i < V2_ITEMS; ++i) ti[i] = base + i < P ? (pown ? tinfo[j[i]] : ptinfo[j[i]]) : make_uint4(0u, 0u, 0u, 0u);
+        if (pown && pair_pos) {
+#pragma unroll
+            for (int i = 0; i < V2_ITEMS; ++i) j[i] = base + i < P ? perm[base + i] : 0u;
+        }
         uint32_t inf = 0;
 #pragma unroll
         for (int i = 0; i < V2_ITEMS; ++i) {
             const size_t p = base + i;
             if (p >= P) break;
-            if (fl[i]) seg_start[sg[i] - 1] = (uint32_t)p;
-            if (p == P - 1) seg_start[sg[i]] = (uint32_t)P;
             if (pair_pos) pair_pos[j[i]] = (uint32_t)p;
+            c[8] += fl[i] != 0;
             inf |= (ti[i].z & 0xFFu) << (8 * i);
             const uint32_t code = v2_code(ti[i].x, ti[i].y, ti[i].z & 0xFFu);
             const uint32_t l = code & 7u;
@@ -775,7 +795,7 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t 
 #pragma unroll
     for (int q = 0; q < NCNT; ++q) {
         uint32_t total;
-        if (q < 7) block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
+        if (!cnt_is_max(q)) block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
         else block_exclusive(c[q], OpMax<uint32_t>(), lds, total);
         if (threadIdx.x == 0) tile_sums[(size_t)q * ntiles + blockIdx.x] = total;
     }
@@ -810,14 +830,16 @@ struct V2Cols {
 };
 
 __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
-                                                    const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ seg_incl,
+                                                    const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ seg_flag,
                                                     const uint32_t *__restrict__ tile_pref, const uint32_t *__restrict__ bases,
-                                                    uint32_t ntiles, int rbits, V2Cols o)
+                                                    uint32_t ntiles, int rbits, V2Cols o, uint32_t *__restrict__ seg_incl,
+                                                    uint32_t *__restrict__ seg_start)
 {
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t code[V2_ITEMS] = { 7u, 7u, 7u, 7u }, rk[V2_ITEMS] = {};
     uint32_t c[NCNT] = {};
+    uint32_t fl[V2_ITEMS] = {};
     if (base < P) {
         v2_codes4(P, base, s_rank, s_exec, s_info, code, rk);
 #pragma unroll
@@ -827,6 +849,8 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
             for (int q = 0; q < NLIST; ++q) c[q] += l == (uint32_t)q;
             c[6] += (code[i] >> 3) & 1u;
             if ((code[i] >> 4) & 1u) c[7] = (uint32_t)(base + i) + 1;
+            fl[i] = base + i < P ? seg_flag[base + i] : 0u;
+            c[8] += fl[i] != 0;
         }
     }
     uint32_t run[NCNT];
@@ -834,14 +858,14 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     for (int q = 0; q < NCNT; ++q) {
         uint32_t total;
         uint32_t pre = tile_pref[(size_t)q * ntiles + blockIdx.x];
-        if (q < 7) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
+        if (!cnt_is_max(q)) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
         else { uint32_t e = block_exclusive(c[q], OpMax<uint32_t>(), lds, total); run[q] = e > pre ? e : pre; }
     }
     // rank directory: the chunk's running values from its first thread (RD_W / V2_ITEMS = 8 threads per chunk), the bit
     // planes OR-reduced over those 8 threads (threads past P contribute nothing)
     static_assert(RD_W == 8 * V2_ITEMS, "eight threads per directory chunk");
     {
-        uint32_t pl[NCNT] = {};
+        uint32_t pl[NRD] = {};
 #pragma unroll
         for (int i = 0; i < V2_ITEMS; ++i) {
             const uint32_t l = code[i] & 7u;
@@ -852,7 +876,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         }
         const uint32_t sh = V2_ITEMS * (threadIdx.x & 7u);
 #pragma unroll
-        for (int q = 0; q < NCNT; ++q) {
+        for (int q = 0; q < NRD; ++q) {
             uint32_t x = pl[q] << sh;
             x |= __shfl_xor(x, 1, 64);
             x |= __shfl_xor(x, 2, 64);
@@ -871,6 +895,18 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     uint32_t lb[NLIST];
 #pragma unroll
     for (int l = 0; l < NLIST; ++l) lb[l] = bases[l];
+    uint32_t segi[V2_ITEMS];
+#pragma unroll
+    for (int i = 0; i < V2_ITEMS; ++i) {   // segment numbers (seg_incl = inclusive count of segment starts) and starts
+        const size_t p = base + i;
+        if (p >= P) break;
+        if (fl[i]) seg_start[run[8]] = (uint32_t)p;
+        run[8] += fl[i] != 0;
+        segi[i] = run[8];
+        if (p == P - 1) seg_start[run[8]] = (uint32_t)P;
+    }
+    if (base + V2_ITEMS <= P) *reinterpret_cast<uint4 *>(seg_incl + base) = make_uint4(segi[0], segi[1], segi[2], segi[3]);
+    else for (int i = 0; i < V2_ITEMS; ++i) if (base + i < P) seg_incl[base + i] = segi[i];
 #pragma unroll
     for (int i = 0; i < V2_ITEMS; ++i) {
         size_t p = base + i;
@@ -887,7 +923,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         }
         if ((code[i] >> 3) & 1u) {
             uint32_t b = run[6]++;
-            uint32_t seg = seg_incl[p] - 1, e = s_exec[p];
+            uint32_t seg = segi[i] - 1, e = s_exec[p];
             o.bc_rank[b] = r;
             o.bc_exec[b] = e;
             o.bc_kind[b] = (uint8_t)(s_info[p] >> 3);
@@ -2950,7 +2986,7 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
         memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
         if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
         for (uint32_t r = 0; r < PREP_SLOTS; ++r) {
-            for (int w = 0; w < 6; ++w) hg[w] |= hs[8 * r + w];
+            for (int w = 0; w < 7; ++w) hg[w] |= hs[8 * r + w];
             hg[7] += hs[8 * r + 7];
         }
     }
@@ -3058,41 +3094,46 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     int key_shift = 0;
     uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
     bool flags_done = false;
+    uint32_t *pown = nullptr;
+    pp.sb = std::max(1, bits_for(hg[6]));   // bounds the key slot within a txn (hg[6] = OR of the key counts)
     if (batch_sorted && pp.rk.bits <= 32 && !getenv("ACC_PAIR_UNPACKED")) {
         // pair index order is already TxnId order within every key: a stable keys-only sort of (key << 32 | pair index),
-        // 8 B per element; the segment flags pass unpacks the permutation
-        pp.mode = 3;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+        // 8 B per element; the segment flags pass unpacks the permutation. Mode 4 packs (owner, slot) instead of the
+        // pair index, so the segment flags pass also hands the CFK gather each position's txn
+        const bool m4 = bits_for((uint64_t)n - 1) + pp.sb <= 32 && !getenv("ACC_PAIR_NO_OWNER");
+        pp.mode = m4 ? 4 : 3;
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
         const uint64_t *sp = radix_sort_keys(ctx, "rs_pair", pkey, P, 32, pp.rk.bits);
         uint32_t *perm = ctx->get<uint32_t>("pair_perm", P);
-        launch(ctx, "seg_flags", k_seg_flags_packed, dim3(gP), dim3(BLOCK), 0, P, sp, seg_flag, perm);
+        if (m4) pown = ctx->get<uint32_t>("pair_own", P);
+        launch(ctx, "seg_flags", k_seg_flags_packed, dim3(gP), dim3(BLOCK), 0, P, sp, seg_flag, perm, m4 ? pp.sb : -1, key_off,
+               pown);
         ps = { nullptr, perm };
         flags_done = true;
     } else if (batch_sorted) {
         pp.mode = 0;   // pair index order is already TxnId order within every key: stable sort by key
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
         ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits);
     } else if (pp.rk.bits + rbits <= 64) {
         pp.mode = 1;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
         ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits + rbits);
         key_shift = rbits;
     } else {
         pp.mode = 2;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 1, pkey);
         Sorted byrank = radix_sort(ctx, "rs_pair_r", pkey, nullptr, P, rbits);
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner,
+        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey);
         ps = radix_sort(ctx, "rs_pair", pkey, byrank.vals, P, pp.rk.bits);
     }
-    uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P);
+    uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P + V2_ITEMS);   // written by k_v2_apply (the multi-scan's column 8)
     if (!flags_done)
         launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
-    scan<uint32_t, OpAdd<uint32_t>>(ctx, seg_flag, seg_incl, P, false);
 
     uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
     uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P + V2_ITEMS);   // padded for the 16-B column loads
@@ -3100,7 +3141,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
     uint4 *tinfo = ctx->get<uint4>("tinfo", n);
-    uint4 *ptinfo = ctx->get<uint4>("pair_tinfo", P);
+    uint4 *ptinfo = pown ? nullptr : ctx->get<uint4>("pair_tinfo", P);
     bool have_pair_pos = ks != nullptr;
     auto need_pair_pos = [&]() {
         if (have_pair_pos) return;
@@ -3125,15 +3166,15 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
         launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
-        launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
+        if (!pown)
+            launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
         launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, (const uint4 *)ptinfo,
-               (const uint32_t *)seg_incl, (const uint32_t *)seg_flag, seg_start, s_rank, s_exec, s_info,
-               ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
+               (const uint32_t *)pown, (const uint4 *)tinfo, (const uint32_t *)seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
         launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
-               (const uint8_t *)s_info, (const uint32_t *)seg_incl, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
-               rbits, cols);
+               (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
+               rbits, cols, seg_incl, seg_start);
     };
     build_columns();
     ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
