@@ -359,18 +359,19 @@ def run_config2_sharded(args, world, rank, local, dev):
     c3 = args.config == "3"   # config 3: 100M pairs in total over the N GPUs (strong scaling); else N x config 2
     n_global = int(12_500_000 * args.scale) if c3 else int(1_000_000 * args.scale) * world
     n_keys = int((1 << 24) * args.scale) if c3 else n_global
-    batch = W.keydeps_batch(n_global, 8, max(1000, n_keys), W.CONFIG_SEEDS["3z" if c3 else "2"], "zipf", 0.99,
-                            status_model="model")
-    bounds = S.even_split(batch.key_code, world)
-    sub, g = S.store_batch(batch, bounds, rank)
+    # setup (untimed): each rank draws 1/N of the global batch's keys and receives its key range's (txn, key) pairs by
+    # one all-to-all(v) (sharded.keydeps_store_batch: the same store batch as slicing the single-host generator's)
+    import torch.distributed as dist
+    t_gen = time.perf_counter()
+    sub, g, bounds = S.keydeps_store_batch(n_global, 8, max(1000, n_keys), W.CONFIG_SEEDS["3z" if c3 else "2"], "zipf",
+                                           world, rank, device=dev if dist.get_backend() == "nccl" else None)
+    t_gen = time.perf_counter() - t_gen
     bi, keep = S.batch_in_device(sub, dev)
     gidx = torch.from_numpy(g.astype(np.int32)).to(dev)
-    del batch
     ctx = Context(local, timing=True)
     info = {}
     # the exchange behind the C ABI (what a JVM host calls): an acc_comm over RCCL (its 128-byte id broadcast once at
     # setup) and acc_shard_reduce = pack + one size exchange + one grouped all-to-all(v) + KeyDeps.with fold
-    import torch.distributed as dist
     comm, exchange = None, "acc_comm (RCCL over xGMI) + acc_shard_reduce"
     try:
         if dist.get_backend() == "gloo":   # the one-GPU rehearsal: every rank on GPU 0, the host transport over gloo
@@ -422,6 +423,7 @@ def run_config2_sharded(args, world, rank, local, dev):
             "n_txn_global": n_global,
             "pairs_global": n_global * 8,
             "pairs_per_gpu_max": int(mx[0].item()),
+            "setup_store_batch_s": round(t_gen, 2),
             "parallelism": f"key-range shards x{world} (CommandStores) + all-to-all(v) reduce",
         },
         "exchange": {"bytes_sent_total": int(tot[1].item()), "bytes_sent_max_rank": int(mx[1].item()),

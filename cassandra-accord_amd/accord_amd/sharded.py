@@ -150,6 +150,80 @@ def store_batch(batch: Batch, bounds: np.ndarray, rank: int):
     return sub, keep.astype(np.uint32)
 
 
+def run_key_rows(gens):
+    """Drive distinct_key_rows generators of consecutive slices in one process (the exchange is a prefix sum)."""
+    nds = [next(g) for g in gens]
+    out = [None] * len(gens)
+    while True:
+        total = sum(nds)
+        before = np.concatenate([[0], np.cumsum(nds)[:-1]]).astype(np.int64).tolist()
+        nxt = []
+        for q, g in enumerate(gens):
+            try:
+                nxt.append(g.send((before[q], total)))
+            except StopIteration as e:
+                out[q] = e.value
+                nxt.append(None)
+        if total == 0:
+            return out
+        nds = nxt
+
+
+def keydeps_store_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, key_dist: str, world: int, rank: int,
+                        group=None, device=None, **kw):
+    """This rank's CommandStore batch of W.keydeps_batch(n_txn, ...) split by EvenSplit over `world` stores, without
+    any rank building the whole batch: rank r draws the keys of txns [r n / world, (r+1) n / world) (the duplicate
+    redraws coordinated by an all-gather of per-rank counts, so the keys are bit-identical to the single-host
+    generator's), the key-code bounds come from an all-reduce, each (txn, key) pair goes to its key's store in one
+    all-to-all(v), and the store regenerates the TxnId / executeAt / status columns of its txns from their global
+    indices. Returns (store batch, global txn indices u32, bounds) = store_batch(keydeps_batch(...), bounds, rank)."""
+    import torch
+    import torch.distributed as dist
+    from . import workload as W
+    dev = device or torch.device("cpu")
+    lo, hi = n_txn * rank // world, n_txn * (rank + 1) // world
+    sampler = W.key_sampler(seed, key_dist, n_keys, kw.get("zipf_s", 0.99), kw.get("permute_keys", True))
+    gen = W.distinct_key_rows(n_txn, keys_per_txn, sampler, lo, hi)
+    nd = next(gen)
+    while True:
+        t = torch.tensor([nd], dtype=torch.int64, device=dev)
+        allc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(allc, t, group=group)
+        c = [int(x.item()) for x in allc]
+        try:
+            nd = gen.send((sum(c[:rank]), sum(c)))
+        except StopIteration as e:
+            keys = e.value
+            break
+    kc = W.int_key_code(keys.reshape(-1))
+    mm = torch.tensor([int(kc.min()) if len(kc) else (1 << 62), -(int(kc.max()) if len(kc) else 0)], dtype=torch.int64,
+                      device=dev)
+    dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
+    kmin, kmax = int(mm[0].item()), -int(mm[1].item())
+    span = kmax - kmin + 1
+    bounds = np.array([kmin + (span * s) // world for s in range(world)] + [kmax + 1], dtype=np.uint64)
+    txn = np.repeat(np.arange(lo, hi, dtype=np.int64), keys_per_txn)
+    owner = np.searchsorted(bounds[1:-1], kc, side="right")
+    order = np.argsort(owner, kind="stable")
+    send_cnt = np.bincount(owner, minlength=world).astype(np.int64)
+    payload = np.stack([txn[order], kc[order].astype(np.int64)], 1).reshape(-1)
+    sc = torch.from_numpy(send_cnt * 2).to(dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv = torch.empty(int(rc.sum().item()), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, torch.from_numpy(payload).to(dev), output_split_sizes=rc.tolist(),
+                           input_split_sizes=sc.tolist(), group=group)
+    r = recv.cpu().numpy().reshape(-1, 2)
+    rt, rk = r[:, 0], r[:, 1].astype(np.uint64)   # source slices in rank order: txn order, keys sorted per txn
+    g, cnt = np.unique(rt, return_counts=True)
+    off = np.zeros(len(g) + 1, dtype=np.uint32)
+    np.cumsum(cnt, out=off[1:])
+    cols = W.keydeps_txn_columns(n_txn, g, seed, kw.get("status_model", "model"), kw.get("window", 10_000),
+                                 kw.get("p_write", 0.5), kw.get("p_syncpoint", 0.0))
+    sub = W.Batch(*cols, off, rk, dict(n_txn=n_txn, shard=rank, store_local=True))
+    return sub, g.astype(np.uint32), bounds
+
+
 def shard_pack(ctx, bi, world: int, dev, txn_global=None):
     """Fragments of the last acc_keydeps_batch on ctx for every home rank: (streams dict of torch tensors on dev,
     per-destination element counts [4, world] int64 numpy). txn_global: optional device u32/int32 tensor mapping

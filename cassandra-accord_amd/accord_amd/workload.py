@@ -57,6 +57,18 @@ def uniform01(seed: int, salt: int, n: int, offset: int = 0) -> np.ndarray:
     return (stream(seed, salt, n, offset) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
 
 
+def stream_at(seed: int, salt: int, idx: np.ndarray) -> np.ndarray:
+    """The outputs of stream `salt` at counters idx (stream(seed, salt, n)[idx] without the other counters)."""
+    base = np.uint64((seed ^ (salt * 0x632BE59BD9B4E019)) & 0xFFFFFFFFFFFFFFFF)
+    ctr = np.asarray(idx, dtype=np.uint64) + np.uint64(1)
+    with np.errstate(over="ignore"):
+        return mix64(base + ctr * GAMMA)
+
+
+def uniform01_at(seed: int, salt: int, idx: np.ndarray) -> np.ndarray:
+    return (stream_at(seed, salt, idx) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
 def int_key_code(keys: np.ndarray) -> np.ndarray:
     """IntKey order-preserving code: u32(key ^ 0x80000000) as u64."""
     return (keys.astype(np.int64) + (1 << 31)).astype(np.uint64)
@@ -185,46 +197,79 @@ def keydeps_batch(n_txn: int, keys_per_txn: int, n_keys: int, seed: int, dist: s
     INVALID_OR_TRUNCATED and 0.1% TRANSITIVELY_KNOWN).
     """
     i = np.arange(n_txn, dtype=np.int64)
-    u_kind = uniform01(seed, 1, n_txn)
+    cols = keydeps_txn_columns(n_txn, i, seed, status_model, window, p_write, p_syncpoint)
+    sampler = key_sampler(seed, dist, n_keys, zipf_s, permute_keys)
+    keys = _distinct_keys(seed, n_txn, keys_per_txn, sampler)
+    key_off = (np.arange(n_txn + 1, dtype=np.int64) * keys_per_txn).astype(np.uint32)
+    key_code = int_key_code(keys.reshape(-1))
+    meta = dict(n_txn=n_txn, keys_per_txn=keys_per_txn, n_keys=n_keys, seed=seed, dist=dist, zipf_s=zipf_s,
+                status_model=status_model, window=window, p_write=p_write)
+    return Batch(*cols, key_off, key_code, meta)
+
+
+def key_sampler(seed: int, dist: str, n_keys: int, zipf_s: float = 0.99, permute_keys: bool = True):
+    if dist == "uniform":
+        return uniform_sampler(seed, 10, n_keys)
+    if dist == "zipf":
+        return zipf_sampler(seed, 10, n_keys, zipf_s, permute_keys)
+    raise ValueError(dist)
+
+
+def keydeps_txn_columns(n_txn: int, i: np.ndarray, seed: int, status_model: str = "model", window: int = 10_000,
+                        p_write: float = 0.5, p_syncpoint: float = 0.0):
+    """The per-txn columns of keydeps_batch (TxnId, executeAt, InternalStatus) at global txn indices i of an n_txn
+    batch: every one is a function of i alone (counter-based streams), so any subset is generated on its own."""
+    i = np.asarray(i, dtype=np.int64)
+    m = len(i)
+    u_kind = uniform01_at(seed, 1, i)
     kind = np.where(u_kind < p_write, WRITE, READ).astype(np.int64)
     if p_syncpoint > 0:
-        kind = np.where(uniform01(seed, 2, n_txn) < p_syncpoint, SYNC_POINT, kind)
+        kind = np.where(uniform01_at(seed, 2, i) < p_syncpoint, SYNC_POINT, kind)
     flags = (kind << 1) | 0  # domain Key = 0
-    t_msb, t_lsb, t_node = encode_ts(np.ones(n_txn), i + 1, flags, 1 + (i % 8))
+    t_msb, t_lsb, t_node = encode_ts(np.ones(m), i + 1, flags, 1 + (i % 8))
 
     if status_model == "preaccepted":
-        status = np.full(n_txn, PREACCEPTED, dtype=np.uint8)
+        status = np.full(m, PREACCEPTED, dtype=np.uint8)
     elif status_model == "model":
-        u = uniform01(seed, 3, n_txn)
+        u = uniform01_at(seed, 3, i)
         in_window = i >= n_txn - window
         status = np.where(in_window, np.where(u < 0.7, PREACCEPTED, ACCEPTED),
                           np.where(u < 0.8, APPLIED, np.where(u < 0.9, STABLE, COMMITTED))).astype(np.uint8)
-        u2 = uniform01(seed, 4, n_txn)
+        u2 = uniform01_at(seed, 4, i)
         status = np.where(u2 < 0.001, INVALID_OR_TRUNCATED,
                           np.where(u2 < 0.002, TRANSITIVELY_KNOWN, status)).astype(np.uint8)
     else:
         raise ValueError(status_model)
 
     committed = (status >= COMMITTED) & (status <= APPLIED)
-    bump = committed & (uniform01(seed, 5, n_txn) < 0.1)
-    bump_by = 1 + (stream(seed, 6, n_txn) % np.uint64(1000)).astype(np.int64)
-    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(n_txn), i + 1 + bump_by, np.zeros(n_txn), 1000 + (i % 1024))  # no ties: |i - i' | < 1024
+    bump = committed & (uniform01_at(seed, 5, i) < 0.1)
+    bump_by = 1 + (stream_at(seed, 6, i) % np.uint64(1000)).astype(np.int64)
+    e_msb, e_lsb_b, e_node_b = encode_ts(np.ones(m), i + 1 + bump_by, np.zeros(m), 1000 + (i % 1024))  # no ties: |i - i' | < 1024
     exe_msb = np.where(bump, e_msb, t_msb).astype(np.uint64)
     exe_lsb = np.where(bump, e_lsb_b, t_lsb).astype(np.uint64)
     exe_node = np.where(bump, e_node_b, t_node).astype(np.int32)
+    return t_msb, t_lsb, t_node, exe_msb, exe_lsb, exe_node, status
 
-    if dist == "uniform":
-        sampler = uniform_sampler(seed, 10, n_keys)
-    elif dist == "zipf":
-        sampler = zipf_sampler(seed, 10, n_keys, zipf_s, permute_keys)
-    else:
-        raise ValueError(dist)
-    keys = _distinct_keys(seed, n_txn, keys_per_txn, sampler)
-    key_off = (np.arange(n_txn + 1, dtype=np.int64) * keys_per_txn).astype(np.uint32)
-    key_code = int_key_code(keys.reshape(-1))
-    meta = dict(n_txn=n_txn, keys_per_txn=keys_per_txn, n_keys=n_keys, seed=seed, dist=dist, zipf_s=zipf_s,
-                status_model=status_model, window=window, p_write=p_write)
-    return Batch(t_msb, t_lsb, t_node, exe_msb, exe_lsb, exe_node, status, key_off, key_code, meta)
+
+def distinct_key_rows(n_txn: int, k: int, sample, lo: int, hi: int):
+    """Rows [lo, hi) of _distinct_keys(seed, n_txn, k, sample), generated without the other rows: a generator that
+    yields this slice's duplicate count of each redraw round and is sent back (duplicates in earlier rows of the
+    batch, duplicates in the whole batch) for it; the slices' callers exchange those counts (an all-gather across the
+    ranks holding consecutive slices). Returns the rows (StopIteration.value)."""
+    keys = sample(lo * k, (hi - lo) * k).reshape(hi - lo, k)
+    offset = n_txn * k
+    for _ in range(200):
+        keys.sort(axis=1)
+        dup = np.zeros_like(keys, dtype=bool)
+        dup[:, 1:] = keys[:, 1:] == keys[:, :-1]
+        nd = int(dup.sum())
+        before, total = yield nd
+        if total == 0:
+            return keys
+        if nd:
+            keys[dup] = sample(offset + before, nd)
+        offset += total
+    raise RuntimeError("could not draw distinct keys")
 
 
 def merge_exec_rank(n_txn: int, seed: int = CONFIG_SEEDS["5"], max_bump: int = 50) -> np.ndarray:

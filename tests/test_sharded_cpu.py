@@ -78,3 +78,50 @@ def test_even_split_covers_domain():
     kc = np.array([5, 9, 100, 1000], dtype=np.uint64)
     b = S.even_split(kc, 4)
     assert b[0] == 5 and b[-1] == 1001 and (np.diff(b.astype(np.int64)) > 0).all()
+
+
+def _store_slice_worker(rank, world, port, dist_name, errq):
+    sys.path[:0] = [os.path.join(ROOT, "cassandra-accord_amd"), os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+    from accord_amd import sharded as S
+    from accord_amd import workload as W
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, k, nk, seed = 6000, 8, 700, 0xACC0_0002
+        sub, g, bounds = S.keydeps_store_batch(n, k, nk, seed, dist_name, world, rank, window=900)
+        full = W.keydeps_batch(n, k, nk, seed, dist_name, 0.99, status_model="model", window=900)
+        b2 = S.even_split(full.key_code, world)
+        assert np.array_equal(bounds, b2), (bounds, b2)
+        ref, g2 = S.store_batch(full, b2, rank)
+        assert np.array_equal(g, g2)
+        for f, v in ref.arrays().items():
+            assert np.array_equal(getattr(sub, f), v), f
+        dist.barrier()
+    except Exception as e:  # surface the failure to the parent
+        errq.put(f"rank {rank}: {e!r}")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dist_name", [(3, "zipf"), (8, "zipf"), (2, "uniform")])
+def test_store_slice_generation_equals_full_batch(world, dist_name):
+    """bench.py --gpus N at N > 1: each rank draws 1/N of the txns' keys (duplicate redraws coordinated by an
+    all-gather) and receives its key range's pairs by one all-to-all(v); the store batch equals
+    store_batch(keydeps_batch(...)) of the single-host generator, array for array."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_store_slice_worker, args=(r, world, port, dist_name, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
