@@ -826,30 +826,79 @@ def cfk_map_reduce_full(ctx: Context, bv, queries: dict, started_at: int, test_d
     return out
 
 
+def _conflicts_in(upd: dict, keep: list) -> "L.ConflictsIn":
+    a = {k: np.ascontiguousarray(np.asarray(upd[k], dt)) for k, dt in (
+        ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("key_off", np.uint32), ("key", np.uint64),
+        ("rng_off", np.uint32), ("rng_start", np.uint64), ("rng_end", np.uint64))}
+    keep.append(a)
+    p = lambda k: a[k].ctypes.data  # noqa: E731
+    return L.ConflictsIn(L.ACC_MEM_HOST, len(a["xmsb"]), int(upd["end_inclusive"]), len(a["key"]), len(a["rng_start"]),
+                         L.TsCols(p("xmsb"), p("xlsb"), p("xnode")), p("key_off"), p("key"), p("rng_off"), p("rng_start"),
+                         p("rng_end"))
+
+
+def _preaccept_io(q: dict, keep: list):
+    b = {k: np.ascontiguousarray(np.asarray(q[k], dt)) for k, dt in (
+        ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("is_range", np.uint8), ("part_off", np.uint32),
+        ("part_start", np.uint64), ("part_end", np.uint64))}
+    keep.append(b)
+    p = lambda k: b[k].ctypes.data  # noqa: E731
+    nq = len(b["msb"])
+    qi = L.PreacceptIn(L.ACC_MEM_HOST, nq, len(b["part_start"]), L.TsCols(p("msb"), p("lsb"), p("node")),
+                       p("is_range"), p("part_off"), p("part_start"), p("part_end"))
+    out = dict(msb=np.zeros(max(nq, 1), np.uint64), lsb=np.zeros(max(nq, 1), np.uint64),
+               node=np.zeros(max(nq, 1), np.int32), fast=np.zeros(max(nq, 1), np.uint8))
+    o = L.PreacceptOut(L.ACC_MEM_HOST, out["msb"].ctypes.data, out["lsb"].ctypes.data, out["node"].ctypes.data,
+                       out["fast"].ctypes.data)
+    return qi, o, out, nq
+
+
 def max_conflicts(ctx: Context, upd: dict, q: dict) -> dict:
     """MaxConflicts.get(keys) per PreAccept query and the fast-path test (acc_max_conflicts; local/MaxConflicts.java,
     local/CommandStore.java:320-345). upd: xmsb/xlsb/xnode (executeAt), key_off/key, rng_off/rng_start/rng_end,
     end_inclusive; q: msb/lsb/node (TxnId), is_range, part_off, part_start, part_end. Returns dict(msb, lsb, node,
     fast)."""
-    a = {k: np.ascontiguousarray(np.asarray(upd[k], dt)) for k, dt in (
-        ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("key_off", np.uint32), ("key", np.uint64),
-        ("rng_off", np.uint32), ("rng_start", np.uint64), ("rng_end", np.uint64))}
-    b = {k: np.ascontiguousarray(np.asarray(q[k], dt)) for k, dt in (
-        ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("is_range", np.uint8), ("part_off", np.uint32),
-        ("part_start", np.uint64), ("part_end", np.uint64))}
-    p = lambda d, k: d[k].ctypes.data  # noqa: E731
-    ui = L.ConflictsIn(L.ACC_MEM_HOST, len(a["xmsb"]), int(upd["end_inclusive"]), len(a["key"]), len(a["rng_start"]),
-                       L.TsCols(p(a, "xmsb"), p(a, "xlsb"), p(a, "xnode")), p(a, "key_off"), p(a, "key"),
-                       p(a, "rng_off"), p(a, "rng_start"), p(a, "rng_end"))
-    nq = len(b["msb"])
-    qi = L.PreacceptIn(L.ACC_MEM_HOST, nq, len(b["part_start"]), L.TsCols(p(b, "msb"), p(b, "lsb"), p(b, "node")),
-                       p(b, "is_range"), p(b, "part_off"), p(b, "part_start"), p(b, "part_end"))
-    out = dict(msb=np.zeros(max(nq, 1), np.uint64), lsb=np.zeros(max(nq, 1), np.uint64),
-               node=np.zeros(max(nq, 1), np.int32), fast=np.zeros(max(nq, 1), np.uint8))
-    o = L.PreacceptOut(L.ACC_MEM_HOST, out["msb"].ctypes.data, out["lsb"].ctypes.data, out["node"].ctypes.data,
-                       out["fast"].ctypes.data)
+    keep = []
+    ui = _conflicts_in(upd, keep)
+    qi, o, out, nq = _preaccept_io(q, keep)
     ctx.check(ctx._lib.acc_max_conflicts(ctx.handle, C.byref(ui), C.byref(qi), C.byref(o)))
     return {k: v[:nq] for k, v in out.items()}
+
+
+class MaxConflictsMap:
+    """A CommandStore's MaxConflicts kept on the device (acc_maxconflicts_*): update() merges a batch of commands'
+    (keysOrRanges, executeAt), get() answers PreAccept queries (MaxConflicts.get + the fast-path test)."""
+
+    def __init__(self, ctx: Context, end_inclusive: int = 1):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx.check(ctx._lib.acc_maxconflicts_create(ctx.handle, int(end_inclusive), C.byref(h)))
+        self.h = h
+
+    def update(self, upd: dict):
+        keep = []
+        ui = _conflicts_in(upd, keep)
+        self.ctx.check(self.ctx._lib.acc_maxconflicts_update(self.ctx.handle, self.h, C.byref(ui)))
+
+    def get(self, q: dict) -> dict:
+        keep = []
+        qi, o, out, nq = _preaccept_io(q, keep)
+        self.ctx.check(self.ctx._lib.acc_maxconflicts_get(self.ctx.handle, self.h, C.byref(qi), C.byref(o)))
+        return {k: v[:nq] for k, v in out.items()}
+
+    def size(self) -> int:
+        return int(self.ctx._lib.acc_maxconflicts_size(self.h))
+
+    def close(self):
+        if self.h:
+            self.ctx._lib.acc_maxconflicts_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 # ---------------------------------------------------------------- device-resident CommandsForKey store

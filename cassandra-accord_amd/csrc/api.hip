@@ -23,6 +23,11 @@ void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in);
 void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
 void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view);
 void max_conflicts(acc_ctx *ctx, const acc_conflicts_in *u, const acc_preaccept_in *q, acc_preaccept_out *out);
+acc_maxconflicts *mc_new(int device, uint32_t end_inclusive);
+void mc_free(acc_maxconflicts *m);
+uint64_t mc_size(const acc_maxconflicts *m);
+void mc_update(acc_ctx *ctx, acc_maxconflicts *m, const acc_conflicts_in *u);
+void mc_get(acc_ctx *ctx, const acc_maxconflicts *m, const acc_preaccept_in *q, acc_preaccept_out *out);
 void cfk_view(acc_cfk *cfk, acc_batch_in *out);
 void cfk_free(acc_cfk *cfk);
 acc_cfk *cfk_new(int device);
@@ -484,5 +489,35 @@ int acc_max_conflicts(acc_ctx *ctx, const acc_conflicts_in *updates, const acc_p
         acc::max_conflicts(ctx, updates, queries, out);
     });
 }
+
+
+int acc_maxconflicts_create(acc_ctx *ctx, uint32_t end_inclusive, acc_maxconflicts **out)
+{
+    if (!ctx || !out) return ACC_E_ARG;
+    *out = nullptr;
+    return acc_guard(ctx, [&] { *out = acc::mc_new(ctx->device, end_inclusive); });
+}
+
+void acc_maxconflicts_destroy(acc_maxconflicts *map) { acc::mc_free(map); }
+
+int acc_maxconflicts_update(acc_ctx *ctx, acc_maxconflicts *map, const acc_conflicts_in *updates)
+{
+    if (!ctx || !map) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::mc_update(ctx, map, updates);
+    });
+}
+
+int acc_maxconflicts_get(acc_ctx *ctx, acc_maxconflicts *map, const acc_preaccept_in *queries, acc_preaccept_out *out)
+{
+    if (!ctx || !map) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::mc_get(ctx, map, queries, out);
+    });
+}
+
+uint64_t acc_maxconflicts_size(const acc_maxconflicts *map) { return acc::mc_size(map); }
 
 }  // extern "C"

@@ -812,6 +812,21 @@ typedef struct acc_preaccept_out {
 int  acc_max_conflicts(acc_ctx *ctx, const acc_conflicts_in *updates, const acc_preaccept_in *queries,
                        acc_preaccept_out *out);
 
+/* A CommandStore's MaxConflicts kept on the device across calls (the store's one map, CommandStore.maxConflicts,
+ * local/CommandStore.java:270-290): disjoint intervals over the key codes with a Timestamp each (ReducingRangeMap).
+ * acc_maxconflicts_update merges a batch of commands' (keysOrRanges, executeAt) into it (MaxConflicts.update =
+ * ReducingIntervalMap.merge with Timestamp::max; a batch equals its commands applied one by one in any order);
+ * acc_maxconflicts_get answers PreAccept queries as acc_max_conflicts does, in O(log map) per key or range (the
+ * acc_max_conflicts form rebuilds the map from the store's whole update history on every call). end_inclusive fixes
+ * the map's Range bound type; updates must carry the same. Not thread-safe; one context at a time. */
+typedef struct acc_maxconflicts acc_maxconflicts;
+int  acc_maxconflicts_create(acc_ctx *ctx, uint32_t end_inclusive, acc_maxconflicts **out);
+void acc_maxconflicts_destroy(acc_maxconflicts *map);
+int  acc_maxconflicts_update(acc_ctx *ctx, acc_maxconflicts *map, const acc_conflicts_in *updates);
+int  acc_maxconflicts_get(acc_ctx *ctx, acc_maxconflicts *map, const acc_preaccept_in *queries, acc_preaccept_out *out);
+/* intervals currently held (ReducingRangeMap.size) */
+uint64_t acc_maxconflicts_size(const acc_maxconflicts *map);
+
 /* ---- Levelisation of a dependency graph by executeAt ----
  * Graph over n txns: deps of txn t = dep[off[t] .. off[t+1]) (batch indices); exec_rank[t] = order
  * rank of t.executeAt. Edges whose dep has exec_rank >= exec_rank[t] are ignored (Commands.java:804-810).

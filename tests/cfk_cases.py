@@ -204,6 +204,15 @@ def conflicts_case(seed, n_upd=500, n_query=300, span=4000, p_range=0.3, end_inc
     return upd, q
 
 
+def conflicts_slice(upd, a, b):
+    """updates [a, b) of a conflicts_case update list, same layout"""
+    ko, ro = upd["key_off"].astype(np.int64), upd["rng_off"].astype(np.int64)
+    return dict(end_inclusive=upd["end_inclusive"], xmsb=upd["xmsb"][a:b], xlsb=upd["xlsb"][a:b], xnode=upd["xnode"][a:b],
+                key_off=(ko[a:b + 1] - ko[a]).astype(np.uint32), key=upd["key"][ko[a]:ko[b]],
+                rng_off=(ro[a:b + 1] - ro[a]).astype(np.uint32), rng_start=upd["rng_start"][ro[a]:ro[b]],
+                rng_end=upd["rng_end"][ro[a]:ro[b]])
+
+
 def snap_as_batch(snap):
     """The key-major CFK state as the txn-major snapshot acc_map_reduce_full scans, restated on the host (what
     acc_cfk_snap_to_batch builds): one txn per distinct TxnId in TxnId order, its keys = the keys holding it, its

@@ -96,6 +96,61 @@ def test_max_conflicts(ctx, seed, end_inclusive, n_upd, n_query, span):
     assert 0 < int(o["fast"].sum()) < n_query
 
 
+@pytest.mark.parametrize("seed,end_inclusive,span,batches", [(5, 1, 4000, 4), (6, 0, 300, 7), (7, 1, 1 << 40, 3)])
+def test_max_conflicts_persistent(ctx, seed, end_inclusive, span, batches):
+    """acc_maxconflicts_*: the store's MaxConflicts kept on the device and merged batch by batch
+    (CommandStore.updateMaxConflicts, local/CommandStore.java:280-290); after each batch every query equals the C
+    restatement over all updates so far (MaxConflicts.merge is a pointwise Timestamp::max, MaxConflicts.java:62-65)."""
+    from accord_amd.deps import MaxConflictsMap
+    upd, q = CC.conflicts_case(seed, n_upd=3000, n_query=800, span=span, end_inclusive=end_inclusive)
+    n = len(upd["xmsb"])
+    cuts = [n * b // batches for b in range(batches + 1)]
+    m = MaxConflictsMap(ctx, end_inclusive)
+    try:
+        for b in range(batches):
+            m.update(CC.conflicts_slice(upd, cuts[b], cuts[b + 1]))
+            g = m.get(q)
+            o = oracle.max_conflicts(CC.conflicts_slice(upd, 0, cuts[b + 1]), q)
+            for k in ("msb", "lsb", "node", "fast"):
+                np.testing.assert_array_equal(g[k], o[k], err_msg=f"batch {b} {k}")
+            assert 0 < m.size() <= 2 * (int(upd["key_off"][cuts[b + 1]]) + int(upd["rng_off"][cuts[b + 1]]))
+        # the map is the store's state: an empty batch and a bad batch leave it as it is
+        with pytest.raises(Exception):
+            bad = CC.conflicts_slice(upd, 0, 5)
+            bad["key"] = bad["key"][::-1].copy()
+            m.update(bad)
+        np.testing.assert_array_equal(m.get(q)["msb"], oracle.max_conflicts(upd, q)["msb"])
+    finally:
+        m.close()
+
+
+def test_max_conflicts_code_space_ends(ctx):
+    """Keys and ranges at both ends of the u64 code space (0, 2^64 - 1) through the persistent map."""
+    from accord_amd.deps import MaxConflictsMap
+    import accord_amd.workload as W
+    top = (1 << 64) - 1
+    for ei in (1, 0):
+        ts = [tuple(int(x) for x in W.encode_ts(1, h, 0, 1)) for h in (10, 20, 30, 40)]
+        upd = dict(end_inclusive=ei, xmsb=np.array([t[0] for t in ts], np.uint64), xlsb=np.array([t[1] for t in ts], np.uint64),
+                   xnode=np.array([t[2] for t in ts], np.int32), key_off=np.array([0, 1, 2, 2, 2], np.uint32),
+                   key=np.array([0, top], np.uint64), rng_off=np.array([0, 0, 0, 1, 2], np.uint32),
+                   rng_start=np.array([0, top - 5], np.uint64), rng_end=np.array([3, top], np.uint64))
+        qk = [0, 1, 2, 3, 4, top - 5, top - 4, top - 1, top]
+        q = dict(msb=np.full(len(qk) + 1, ts[0][0], np.uint64), lsb=np.full(len(qk) + 1, ts[0][1], np.uint64),
+                 node=np.full(len(qk) + 1, 1, np.int32), is_range=np.array([0] * len(qk) + [1], np.uint8),
+                 part_off=np.arange(len(qk) + 2, dtype=np.uint32),
+                 part_start=np.array(qk + [0], np.uint64), part_end=np.array(qk + [top], np.uint64))
+        m = MaxConflictsMap(ctx, ei)
+        try:
+            m.update(upd)
+            g = m.get(q)
+        finally:
+            m.close()
+        o = oracle.max_conflicts(upd, q)
+        for k in ("msb", "lsb", "node", "fast"):
+            np.testing.assert_array_equal(g[k], o[k], err_msg=f"ei {ei} {k}")
+
+
 def test_max_conflicts_empty(ctx):
     from accord_amd.deps import IllegalArgumentException, max_conflicts
     upd, q = CC.conflicts_case(4, n_upd=10, n_query=5)
