@@ -6,12 +6,16 @@
 // TxnInfoWithMissing.missing (sorted TxnIds). Keys are independent, so the batch runs as one lane per key:
 //   1. the snapshot keys and every (update, key) pair are radix sorted by key code (stable: a key's snapshot first,
 //      then its updates in batch order); distinct keys by a flag scan;
-//   2. per key, working-space bounds (entries: snapshot + one per update + its deps; missing: bounded by the entries
-//      squared) and one scan of them give each key two ping-pong buffers in one pool;
+//   2. per key, working-space bounds (entries: snapshot + one per update + its deps, exact; missing: a linear first
+//      guess below the proven bound, min(entries^2, snapshot missing + entries x (deps + 2) per update)) and one scan
+//      of them give each key two ping-pong buffers in one pool;
 //   3. one lane per key replays its updates: CommandsForKey.update -> insert / update, computeInfoAndAdditions,
 //      insertInfoAndOneMissing, updateOrInsertWithAdditions with mergeAndFilterMissing / to / insertMissing,
 //      removeMissing — each update rebuilding the key's TxnInfo array into the other buffer, as the Java builds a new
 //      array;
+//      a key whose missing[] outgrows its guess is flagged; the flagged keys' guesses grow 4x (up to the proven bound)
+//      and the replay runs again, so a hot key with thousands of dep-carrying updates costs the space it really uses,
+//      not the quadratic bound;
 //   4. final sizes, two scans, and a compaction into the key-major output (keys without entries dropped).
 // Errors: a status going back (IllegalStateException "stale status", ACC_E_STATE), an addition equal to an existing
 // TxnId or depsKnownBefore equal to a TxnId (the reference's checkState, ACC_E_STATE), malformed input (ACC_E_ARG).
@@ -22,7 +26,7 @@ namespace cd {
 
 constexpr uint64_t IDENTITY_LSB = 0xFFFFFFFFFFFF001EULL;
 enum : uint32_t { TK = 0, PRE = 2, ACC = 3, COMMITTED = 4, APPLIED = 6, INVALID = 7 };
-enum : uint64_t { E_ARG_STATUS = 1, E_ARG_SORT = 2, E_ARG_OFF = 4, E_STALE = 8, E_STATE = 16, E_CAP = 32 };
+enum : uint64_t { E_ARG_STATUS = 1, E_ARG_SORT = 2, E_ARG_OFF = 4, E_STALE = 8, E_STATE = 16, E_CAP = 32, E_MCAP = 64 };
 
 struct Ts {
     uint64_t m, l;
@@ -99,7 +103,8 @@ struct Ctx {
     Work w;
     uint64_t err;
     __device__ bool room_e(uint32_t n) { if (n > w.ecap) { err |= E_CAP; return false; } return true; }
-    __device__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_CAP; return false; } return true; }
+    // missing areas: beyond the key's current guess (E_MCAP: grown and replayed by the host)
+    __device__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_MCAP; return false; } return true; }
 
     // append entry x of src with its missing[] copied (dropping `drop` when given) to dst
     __device__ void put(Buf &dst, const Info &x, const Ts *src_m, const Ts *drop)
@@ -436,7 +441,8 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kflag(uint64_t T, const uint64_t *
 __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint64_t T, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fi,
                                                      const uint32_t *__restrict__ src, uint32_t nk, Snap s, Upd u,
                                                      uint32_t *__restrict__ kstart, uint64_t *__restrict__ ecap,
-                                                     uint64_t *__restrict__ mcap, uint64_t *__restrict__ dcap)
+                                                     uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
+                                                     uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= T || !f[i]) return;
@@ -457,9 +463,25 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint64_t T, const uint32_t 
         }
     }
     ecap[k] = e;
-    const uint64_t sq = e * e, lin = m + e * grow;
-    mcap[k] = sq < lin ? sq : lin;
+    // every missing[] entry is an uncommitted TxnId of the key held by an entry with info: at most e per entry, and an
+    // update adds at most its deps + 2 to each entry
+    const uint64_t sq = e * e, lin = m + e * grow, bound = sq < lin ? sq : lin, guess = m + 4 * e + 64;
+    mmax[k] = bound;
+    mcap[k] = guess < bound ? guess : bound;
     dcap[k] = d + 1;
+    ovf[k] = 0;
+}
+
+// keys whose missing[] outgrew the guess: 4x, up to the proven bound (at the bound: an internal error)
+__global__ __launch_bounds__(BLOCK) void k_cd_grow(uint32_t nkeys, uint32_t *__restrict__ ovf, uint64_t *__restrict__ mcap,
+                                                   const uint64_t *__restrict__ mmax, uint64_t *__restrict__ err)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys || !ovf[k]) return;
+    ovf[k] = 0;
+    if (mcap[k] >= mmax[k]) { atomicOr((unsigned long long *)err, (unsigned long long)E_CAP); return; }
+    const uint64_t g = 4 * mcap[k];
+    mcap[k] = g < mmax[k] ? g : mmax[k];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_cd_kend(uint32_t nkeys, uint64_t T, uint32_t *__restrict__ kstart)
@@ -493,7 +515,8 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
                                                     const uint32_t *__restrict__ src, const uint64_t *__restrict__ ecap,
                                                     const uint64_t *__restrict__ mcap, uint32_t nk, Snap s, Upd u, Pool p,
                                                     uint8_t *__restrict__ final_b, uint32_t *__restrict__ fin_n,
-                                                    uint32_t *__restrict__ fin_m, uint64_t *__restrict__ err)
+                                                    uint32_t *__restrict__ fin_m, uint32_t *__restrict__ ovf,
+                                                    uint64_t *__restrict__ err)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys) return;
@@ -545,6 +568,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
     final_b[k] = A == &c.w.a ? 0 : 1;
     fin_n[k] = A->n;
     fin_m[k] = A->mtop;
+    if (c.err & E_MCAP) { ovf[k] = 1; c.err = E_MCAP; }   // anything else this key reports shows again on the replay
     if (c.err) atomicOr((unsigned long long *)err, (unsigned long long)c.err);
 }
 
@@ -624,27 +648,13 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 }
 
 // ---- the key-major state as the txn-major snapshot of acc_map_reduce_full (acc_cfk_snap_to_batch)
-// Entries are sorted by TxnId with three stable radix sorts (node, then lsb's identity bits, then msb: the Timestamp
-// order of cmp); entries of one TxnId keep key order, so each txn's keys come out sorted.
+// Entries are sorted by TxnId with the dense-rank dictionary's stable radix sort of the compacted (msb, lsb & IDENTITY_LSB,
+// node) bits (the Timestamp order of cmp; only the bits that vary across the entries, so a few passes instead of the 19
+// of three full-width sorts); entries of one TxnId keep key order, so each txn's keys come out sorted.
 __global__ __launch_bounds__(BLOCK) void k_cb_node(uint64_t NE, const int32_t *__restrict__ en, uint64_t *__restrict__ k)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i < NE) k[i] = (uint32_t)en[i] ^ 0x80000000u;
-}
-__global__ __launch_bounds__(BLOCK) void k_cb_lsb(uint64_t NE, const uint32_t *__restrict__ perm, const uint64_t *__restrict__ el,
-                                                  uint64_t *__restrict__ k)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i < NE) {
-        const uint64_t l = el[perm[i]];
-        k[i] = ((l >> 16) << 4) | ((l >> 1) & 0xFu);   // the 52 bits of l & IDENTITY_LSB, order kept
-    }
-}
-__global__ __launch_bounds__(BLOCK) void k_cb_msb(uint64_t NE, const uint32_t *__restrict__ perm, const uint64_t *__restrict__ em,
-                                                  uint64_t *__restrict__ k)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i < NE) k[i] = em[perm[i]];
 }
 // owner key of every entry (upper bound in ent_off)
 __global__ __launch_bounds__(BLOCK) void k_cb_owner(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ ent_off,
@@ -785,13 +795,18 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         uint64_t *k = ctx->get<uint64_t>("cb_key", NE);
         uint32_t *owner = ctx->get<uint32_t>("cb_owner", NE), *flag = ctx->get<uint32_t>("cb_flag", NE);
         uint32_t *tinc = ctx->get<uint32_t>("cb_tinc", NE);
+        // entries in Timestamp order (stable: a TxnId's entries stay in key order) through the dense-rank dictionary's
+        // sort of the compacted (msb, lsb & IDENTITY_LSB, node) bits: a few radix passes over the bits that vary
         launch(ctx, "cb_node", k_cb_node, g, dim3(BLOCK), 0, NE, s.en, k);
-        Sorted r = radix_sort(ctx, "cb_rs1", k, nullptr, NE, 32);
-        launch(ctx, "cb_lsb", k_cb_lsb, g, dim3(BLOCK), 0, NE, (const uint32_t *)r.vals, s.el, k);
-        r = radix_sort(ctx, "cb_rs2", k, r.vals, NE, 52);
-        launch(ctx, "cb_msb", k_cb_msb, g, dim3(BLOCK), 0, NE, (const uint32_t *)r.vals, s.em, k);
-        r = radix_sort(ctx, "cb_rs3", k, r.vals, NE, 64);
-        const uint32_t *perm = r.vals;
+        const uint64_t *words[3] = { s.em, s.el, k };
+        const uint64_t wand[3] = { ~0ull, 0xFFFFFFFFFFFF001EULL, ~0ull };
+        DenseRank dr = dense_rank(ctx, "cb_dr", NE, 3, words, wand, nullptr, false);
+        const uint32_t *perm = dr.perm;
+        if (!perm) {   // every entry carries one TxnId: identity order
+            uint32_t *id = ctx->get<uint32_t>("cb_iota", NE);
+            launch(ctx, "cb_iota", k_iota, g, dim3(BLOCK), 0, id, (size_t)NE);
+            perm = id;
+        }
         launch(ctx, "cb_owner", k_cb_owner, g, dim3(BLOCK), 0, NE, nk, s.ent_off, owner);
         launch(ctx, "cb_flag", k_cb_flag, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)owner, flag, errs);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, tinc, NE, false);
@@ -900,13 +915,14 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     // ---- 2. working space
     uint32_t *kstart = ctx->get<uint32_t>("cd_kstart", (size_t)nkeys + 1);
     uint64_t *ecap = ctx->get<uint64_t>("cd_ecap", nkeys), *mcap = ctx->get<uint64_t>("cd_mcap", nkeys);
-    uint64_t *dcap = ctx->get<uint64_t>("cd_dcap", nkeys);
+    uint64_t *dcap = ctx->get<uint64_t>("cd_dcap", nkeys), *mmax = ctx->get<uint64_t>("cd_mmax", nkeys);
+    uint32_t *ovf = ctx->get<uint32_t>("cd_ovf", nkeys);
     uint64_t *eoff = ctx->get<uint64_t>("cd_eoff", (size_t)nkeys + 1), *moff = ctx->get<uint64_t>("cd_moff", (size_t)nkeys + 1);
     uint64_t *doff = ctx->get<uint64_t>("cd_doff", (size_t)nkeys + 1);
     uint64_t Etot = 0, Mtot = 0, Dtot = 0;
     if (nkeys) {
         launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
-               (const uint32_t *)kinc, (const uint32_t *)so.vals, nk, s, u, kstart, ecap, mcap, dcap);
+               (const uint32_t *)kinc, (const uint32_t *)so.vals, nk, s, u, kstart, ecap, mcap, mmax, dcap, ovf);
         launch(ctx, "cd_kend", k_cd_kend, dim3(1), dim3(BLOCK), 0, nkeys, T, kstart);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, ecap, eoff, nkeys, true, eoff + nkeys);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
@@ -917,19 +933,35 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ctx->sync();
         Etot = ctx->pinned[0]; Mtot = ctx->pinned[1]; Dtot = ctx->pinned[2];
     }
-    const uint64_t pool_bytes = 2 * Etot * sizeof(Info) + (2 * Mtot + Etot + 2 * Dtot) * sizeof(Ts);
-    if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
-    Pool p{ ctx->get<Info>("cd_pool_e", 2 * Etot), ctx->get<Ts>("cd_pool_m", 2 * Mtot + Etot + 2 * Dtot), eoff, moff, doff };
     uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
     uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
-    // ---- 3. replay
-    if (nkeys) {
+    // ---- 3. replay, again with grown missing areas while some key outgrows its guess
+    Pool p{};
+    uint32_t regrow = 0;
+    for (;; ++regrow) {
+        const uint64_t pool_bytes = 2 * Etot * sizeof(Info) + (2 * Mtot + Etot + 2 * Dtot) * sizeof(Ts);
+        if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
+        p = Pool{ ctx->get<Info>("cd_pool_e", 2 * Etot), ctx->get<Ts>("cd_pool_m", 2 * Mtot + Etot + 2 * Dtot), eoff, moff, doff };
+        if (!nkeys) break;
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
-               (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m, errs);
+               (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m,
+               ovf, errs);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
+        const uint64_t e = ctx->pinned[0];
+        check(e & ~E_MCAP);
+        if (!(e & E_MCAP)) break;
+        ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+        launch(ctx, "cd_grow", k_cd_grow, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, ovf, mcap,
+               (const uint64_t *)mmax, errs);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, moff + nkeys, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
         check(ctx->pinned[0]);
+        Mtot = ctx->pinned[1];
     }
+    ctx->stat("cfk.apply_regrow", regrow);
     // ---- 4. key-major output
     uint32_t *keep = ctx->get<uint32_t>("cd_keep", nkeys), *kpos = ctx->get<uint32_t>("cd_kpos", (size_t)nkeys + 1);
     uint32_t nko = 0;

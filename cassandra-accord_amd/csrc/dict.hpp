@@ -22,6 +22,7 @@ struct Dictionary {
 struct DenseRank {
     uint32_t *rank = nullptr;
     uint32_t *first = nullptr;
+    const uint32_t *perm = nullptr;   // the stable sorted order of the n keys (nullptr: identity, every key equal)
     uint64_t *count_dev = nullptr;
     uint64_t count = 0;
 };

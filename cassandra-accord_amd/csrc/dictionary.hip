@@ -165,6 +165,7 @@ DenseRank dense_rank(acc_ctx *ctx, const char *tag, size_t n, int nw, const uint
     launch(ctx, "dict_scatter", k_dict_scatter, dim3(gn), dim3(BLOCK), 0, n, perm, (const uint32_t *)flag, (const uint32_t *)incl,
            out.rank, out.first, out.count_dev);
     out.count = ~0ull;   // on device until the caller's next sync (count_dev)
+    out.perm = perm;
     return out;
 }
 

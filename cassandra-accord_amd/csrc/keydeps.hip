@@ -532,7 +532,8 @@ __device__ __forceinline__ Query make_query_ts(const CfkView &v, uint32_t t, uin
     return q;
 }
 
-template <bool EMIT>
+// EMIT: every entry to out[0..c); FIRST (count pass): only the first entry, to out[0]
+template <bool EMIT, bool FIRST = false>
 __device__ __forceinline__ uint32_t run_query(const CfkView &v, const Query &q, uint32_t *__restrict__ out)
 {
     uint32_t c = 0;
@@ -544,6 +545,7 @@ __device__ __forceinline__ uint32_t run_query(const CfkView &v, const Query &q, 
         uint32_t r = v.s_rank[p];
         if (q.p1 && r == q.trank) continue;
         if (EMIT) out[c] = r;
+        else if (FIRST && c == 0) out[0] = r;
         ++c;
     }
     // [scanStart, insertPos): the reference's per-entry switch (CommandsForKey.java:628-647)
@@ -556,6 +558,7 @@ __device__ __forceinline__ uint32_t run_query(const CfkView &v, const Query &q, 
         uint32_t r = v.s_rank[p];
         if (q.p1 && r == q.trank) continue;
         if (EMIT) out[c] = r;
+        else if (FIRST && c == 0) out[0] = r;
         ++c;
     }
     return c;
@@ -3516,12 +3519,46 @@ void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view)
 constexpr uint64_t MX_ERR_DOMAIN = 1, MX_ERR_EMPTY = 2, MX_ERR_UNSORTED = 4, MX_ERR_OFF = 8;
 constexpr uint32_t MX_PIECE = 32;   // covered segments per work piece
 
+// Bucket directory of the sorted CFK keys: bucket(x) = (x - seg_key[0]) >> shift over 2^tbits buckets, the shift
+// making the key span fit; bstart[b] = first segment whose bucket is >= b (b in [0, 2^tbits]). A bound search then
+// bisects one bucket (a few keys) instead of all segments: 2-3 dependent loads instead of ~25.
+__device__ __forceinline__ uint32_t mx_shift(const uint64_t *seg_key, uint32_t nseg, uint32_t tbits)
+{
+    const uint64_t span = seg_key[nseg - 1] - seg_key[0];
+    const uint32_t sb = span ? 64u - (uint32_t)__clzll((long long)span) : 0u;
+    return sb > tbits ? sb - tbits : 0u;
+}
+
+// keys per bucket (bcnt zeroed); an exclusive scan of them is bstart
+__global__ __launch_bounds__(BLOCK) void k_mx_buckets(uint32_t nseg, uint32_t tbits, const uint64_t *__restrict__ seg_key,
+                                                      uint32_t *__restrict__ bcnt)
+{
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nseg) return;
+    const uint32_t sh = mx_shift(seg_key, nseg, tbits);
+    atomicAdd(&bcnt[(seg_key[i] - seg_key[0]) >> sh], 1u);
+}
+
+// first segment m in [0, nseg) with seg_key[m] > x (upper) / >= x (!upper)
+__device__ __forceinline__ uint32_t mx_bound(const uint64_t *seg_key, const uint32_t *bstart, uint32_t nseg, uint32_t sh,
+                                             uint32_t tbits, uint64_t x, bool upper)
+{
+    const uint64_t k0 = seg_key[0];
+    if (x < k0) return 0;
+    uint64_t b = (x - k0) >> sh;
+    if (b >= (1ull << tbits)) return nseg;
+    uint32_t lo = bstart[b], hi = bstart[b + 1];
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (upper ? seg_key[m] <= x : seg_key[m] < x) lo = m + 1; else hi = m; }
+    return lo;
+}
+
 // validation (TxnId.domain(), Range start < end, Ranges.ofSortedAndDeoverlapped) and, per range, its run of covered
 // segments [ra, ra + rcnt) over the sorted CFK keys, its owner and its number of work pieces
 __global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t *__restrict__ tl,
                                                      const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ rng_off,
                                                      const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
                                                      uint32_t end_inclusive, const uint64_t *__restrict__ seg_key, uint32_t nseg,
+                                                     const uint32_t *__restrict__ bstart, uint32_t tbits,
                                                      uint32_t *__restrict__ ra, uint32_t *__restrict__ rowner,
                                                      uint64_t *__restrict__ rcnt, uint64_t *__restrict__ rpieces,
                                                      uint64_t *__restrict__ errs)
@@ -3540,12 +3577,13 @@ __global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t 
             if (s >= x) e |= MX_ERR_EMPTY;
             if (j > r0 && re[j - 1] > s) e |= MX_ERR_UNSORTED;
             // EndInclusive (s, x]: keys > s .. <= x; StartInclusive [s, x): keys >= s .. < x
-            uint32_t lo = 0, hi = nseg;
-            while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (end_inclusive ? seg_key[m] <= s : seg_key[m] < s) lo = m + 1; else hi = m; }
-            const uint32_t a = lo;
-            hi = nseg;
-            while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (end_inclusive ? seg_key[m] <= x : seg_key[m] < x) lo = m + 1; else hi = m; }
-            const uint32_t c = e ? 0u : lo - a;
+            uint32_t a = 0, b = 0;
+            if (nseg) {
+                const uint32_t sh = mx_shift(seg_key, nseg, tbits);
+                a = mx_bound(seg_key, bstart, nseg, sh, tbits, s, end_inclusive != 0);
+                b = mx_bound(seg_key, bstart, nseg, sh, tbits, x, end_inclusive != 0);
+            }
+            const uint32_t c = (e || b < a) ? 0u : b - a;
             ra[j] = a;
             rowner[j] = t;
             rcnt[j] = c;
@@ -3587,23 +3625,77 @@ __device__ __forceinline__ uint32_t mx_scan32(uint32_t x, uint32_t sub)   // inc
     return x;
 }
 
-// count pass: entries and non-empty keys per piece; each lane's count is kept (qc) so the emit pass runs the scan once
+// count pass: entries and non-empty keys per piece. Each lane keeps its count in qc, or, for a single entry (nearly
+// every non-empty (range txn, key) query: one conflicting key txn), the entry itself with MX_ONE set, so the emit pass
+// replays the scan only for the rare lanes with two or more entries
+constexpr uint32_t MX_ONE = 0x80000000u;
+__device__ __forceinline__ uint32_t mx_qcount(uint32_t q) { return (q & MX_ONE) ? 1u : q; }
+
+// A segment holding one CFK entry (nearly every covered key of a sparse key space) is answered in place: with
+// s1 = s0 + 1, make_query_ts / run_query reduce to one test of that entry. Its committed[] is itself or empty, so any
+// maxCommittedBefore M is its own executeAt, which the prefix-max prune (executeAt < M) never removes; nothing of the
+// segment lies below scanStart = s0; the scan [s0, insertPos) is the entry exactly when its TxnId is below T.executeAt.
+// Queries over longer segments go to a list (dlist, wave-aggregated appends) that k_mx_pdefer answers densely, adding
+// into the piece totals; dlist null: every query in place.
 __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkView v, uint64_t *__restrict__ pe_cnt,
-                                                     uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc)
+                                                     uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack,
+                                                     uint32_t *__restrict__ dlist, uint32_t *__restrict__ dcnt)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u, g0 = lane_id() & 32u;
     uint32_t c = 0;
+    bool dfr = false;
     if (p < NP) {
         const uint32_t j = pc.prange[p], t = pc.rowner[j];
         const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
         const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
-        if (sub < nk) c = run_query<false>(v, make_query_ts(v, t, pc.ra[j] + k0 + sub), nullptr);
-        qc[p * 32 + sub] = c;
+        uint32_t f = 0;
+        if (sub < nk) {
+            const uint32_t seg = pc.ra[j] + k0 + sub;
+            const uint32_t s0 = v.seg_start[seg], s1 = v.seg_start[seg + 1];
+            if (dlist && s1 - s0 == 1) {
+                const uint32_t S = v.rank[v.n + t], trank = v.rank[t];
+                const uint32_t wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u);
+                const uint32_t r = v.s_rank[s0], info = v.s_info[s0], st = info & 7u;
+                c = (r < S && ((wk >> (info >> 3)) & 1u) && st != 0 && st != 7 && !(S != trank && r == trank)) ? 1u : 0u;
+                f = r;
+            } else if (dlist) dfr = true;
+            else c = run_query<false, true>(v, make_query_ts(v, t, seg), &f);
+        }
+        qc[p * 32 + sub] = (pack && c == 1) ? (MX_ONE | f) : c;
+    }
+    const uint64_t db = __ballot(dfr);
+    if (db) {
+        uint32_t base = 0;
+        const uint32_t lead = (uint32_t)__ffsll((unsigned long long)db) - 1;
+        if (lane_id() == lead) base = atomicAdd(dcnt, (uint32_t)__popcll(db));
+        base = __shfl(base, (int)lead, 64);
+        if (dfr) dlist[base + (uint32_t)__popcll(db & ((1ull << lane_id()) - 1))] = (uint32_t)(p * 32 + sub);
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
     const uint32_t te = __shfl(ce, (int)(g0 + 31), 64), tk = __shfl(ck, (int)(g0 + 31), 64);
     if (p < NP && sub == 0) { pe_cnt[p] = te; pk_cnt[p] = tk; }
+}
+
+// the deferred queries (segments of two or more entries): the exact-replay scan, one lane each, over a grid-stride
+// loop bounded by the device-side count
+__global__ __launch_bounds__(BLOCK) void k_mx_pdefer(MxP pc, CfkView v, const uint32_t *__restrict__ dlist,
+                                                     const uint32_t *__restrict__ dcnt, uint64_t *__restrict__ pe_cnt,
+                                                     uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack)
+{
+    const uint32_t nd = *dcnt;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nd; i += gridDim.x * BLOCK) {
+        const uint32_t q = dlist[i], p = q >> 5, sub = q & 31u;
+        const uint32_t j = pc.prange[p], t = pc.rowner[j];
+        const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
+        uint32_t f = 0;
+        const uint32_t c = run_query<false, true>(v, make_query_ts(v, t, pc.ra[j] + k0 + sub), &f);
+        qc[q] = (pack && c == 1) ? (MX_ONE | f) : c;
+        if (c) {
+            atomicAdd((unsigned long long *)&pe_cnt[p], (unsigned long long)c);
+            atomicAdd(&pk_cnt[p], 1u);
+        }
+    }
 }
 
 struct MxE {   // emitted entries and key records of the range txns
@@ -3618,8 +3710,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u;
-    uint32_t c = 0, j = 0, t = 0, seg = 0, k0 = 0;
-    Query qq{};
+    uint32_t c = 0, q = 0, j = 0, t = 0, seg = 0, k0 = 0;
     bool act = false;
     if (p < NP) {
         j = pc.prange[p];
@@ -3629,14 +3720,15 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView
         act = sub < nk;
         if (act) {
             seg = pc.ra[j] + k0 + sub;
-            qq = make_query_ts(v, t, seg);
-            c = qc[p * 32 + sub];
+            q = qc[p * 32 + sub];
+            c = mx_qcount(q);
         }
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
     if (!act || c == 0) return;
     const uint64_t e = pe_off[p] + (ce - c);
-    run_query<true>(v, qq, x.deps + e);
+    if (q & MX_ONE) x.deps[e] = q & ~MX_ONE;
+    else run_query<true>(v, make_query_ts(v, t, seg), x.deps + e);
     for (uint32_t i = 0; i < c; ++i) x.owner[e + i] = t;
     const uint32_t kr = pk_off[p] + ck - 1;
     x.kx_idx[kr] = (uint32_t)(pc.r_off[j] - pc.r_off[pc.rng_off[t]] + k0 + sub);
@@ -3689,31 +3781,82 @@ struct MxU {
     uint32_t *idx_of_e, *dep_scr, *ucnt;
 };
 
-// per txn: entry count routing: E <= 64 -> wave tier (every txn); 64 < E <= MX_BLK_E -> block list; beyond -> flag
+// per txn: entry count routing into tier lists (txns without entries: none): E <= 16, <= 32, <= 64 (lane groups),
+// <= MX_MID_E (wave, LDS), <= MX_BLK_E (block); beyond: the sorted fallback (flag gst[1]).
+// gst: [0] block count, [1] fallback flag, [2] mid count, [3..5] 16 / 32 / 64-lane counts
 constexpr uint32_t MX_MID_E = 512, MX_BLK_E = 4096;
-__global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint64_t *__restrict__ etoff, uint32_t *__restrict__ blk_list,
-                                                    uint32_t *__restrict__ mid_list, uint64_t *__restrict__ gst)
+struct MxLists {
+    uint32_t *l[5];   // 16, 32, 64, mid, block
+};
+__global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint64_t *__restrict__ etoff, MxLists L,
+                                                    uint64_t *__restrict__ gst)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    bool blk = false, over = false, mid = false;
+    int c = -1;
     if (t < n) {
         const uint64_t E = etoff[t + 1] - etoff[t];
-        mid = E > 64 && E <= MX_MID_E;
-        blk = E > MX_MID_E && E <= MX_BLK_E;
-        over = E > MX_BLK_E;
+        if (E == 0) c = -1;
+        else if (E <= 16) c = 0;
+        else if (E <= 32) c = 1;
+        else if (E <= 64) c = 2;
+        else if (E <= MX_MID_E) c = 3;
+        else if (E <= MX_BLK_E) c = 4;
+        else { c = -1; atomicOr((unsigned long long *)&gst[1], 1ull); }
     }
-    __shared__ uint32_t lds[WAVES];
-    __shared__ uint32_t base[2];
-    uint32_t total;
-    const uint32_t pre = block_exclusive((blk ? 1u : 0u) | (mid ? 1u << 16 : 0u), OpAdd<uint32_t>(), lds, total);
-    if (threadIdx.x < 2) {
-        const uint32_t c = threadIdx.x == 0 ? (total & 0xFFFFu) : (total >> 16);
-        base[threadIdx.x] = c ? (uint32_t)atomicAdd((unsigned long long *)&gst[threadIdx.x == 0 ? 0 : 2], (unsigned long long)c) : 0u;
+    __shared__ uint32_t wcnt[5][WAVES], base[5];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint64_t bal[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        bal[k] = __ballot(c == k);
+        if (lane == 0) wcnt[k][w] = (uint32_t)__popcll(bal[k]);
     }
     __syncthreads();
-    if (blk) blk_list[base[0] + (pre & 0xFFFFu)] = t;
-    if (mid) mid_list[base[1] + (pre >> 16)] = t;
-    if (over) atomicOr((unsigned long long *)&gst[1], 1ull);
+    if (threadIdx.x < 5) {
+        uint32_t tot = 0;
+        for (int q = 0; q < WAVES; ++q) { const uint32_t x = wcnt[threadIdx.x][q]; wcnt[threadIdx.x][q] = tot; tot += x; }
+        const int slot = threadIdx.x == 4 ? 0 : threadIdx.x == 3 ? 2 : 3 + (int)threadIdx.x;
+        base[threadIdx.x] = tot ? (uint32_t)atomicAdd((unsigned long long *)&gst[slot], (unsigned long long)tot) : 0u;
+    }
+    __syncthreads();
+    if (c >= 0) L.l[c][base[c] + wcnt[c][w] + (uint32_t)__popcll(bal[c] & lt)] = t;
+}
+
+// groups of S lanes (S = 16, 32, 64), one listed txn each (E <= S): register bitonic of (rank << 32 | local entry)
+template <int S>
+__global__ __launch_bounds__(BLOCK) void k_mx_union_seg(const uint32_t *__restrict__ list, const uint64_t *__restrict__ cnt, MxU u)
+{
+    constexpr uint32_t G = 64 / S;
+    const uint32_t lane = lane_id(), grp = lane / S, sub = lane & (S - 1);
+    const uint32_t li = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * G + grp;
+    const bool live = li < (uint32_t)*cnt;
+    const uint32_t t = live ? list[li] : 0;
+    const uint64_t e0 = live ? u.etoff[t] : 0;
+    const uint32_t E = live ? (uint32_t)(u.etoff[t + 1] - e0) : 0;
+    const bool in = sub < E;
+    uint64_t x = in ? (((uint64_t)u.deps[e0 + sub] << 32) | sub) : ~0ull;
+#pragma unroll
+    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint64_t y = shfl_xor(x, (int)jj);
+            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
+            const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+            x = (lower == up) ? mn : mx;
+        }
+    }
+    const uint64_t prev = shfl_up(x, 1);
+    const bool nw = in && (sub == 0 || (prev >> 32) != (x >> 32));
+    const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t bal = __ballot(nw) & gmask;
+    const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+    if (in) {
+        u.idx_of_e[e0 + (uint32_t)x] = idx;
+        if (nw) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(x >> 32)];
+    }
+    if (live && sub == 0) u.ucnt[t] = (uint32_t)__popcll(bal);
 }
 
 // wave per listed txn, 64 < E <= MX_MID_E: one wave's LDS bitonic
@@ -3748,29 +3891,6 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_mid(const uint32_t *__restri
         distinct += (uint32_t)__popcll(bal);
     }
     if (lane == 0) u.ucnt[t] = distinct;
-}
-
-// wave per txn, E <= 64: register bitonic of (rank << 32 | local entry)
-__global__ __launch_bounds__(BLOCK) void k_mx_union_wave(uint32_t n, MxU u)
-{
-    const uint32_t lane = lane_id(), t = blockIdx.x * WAVES + (threadIdx.x >> 6);
-    if (t >= n) return;
-    const uint64_t e0 = u.etoff[t], E = u.etoff[t + 1] - e0;
-    if (E == 0) { if (lane == 0) u.ucnt[t] = 0; return; }
-    if (E > 64) return;
-    const bool in = lane < E;
-    uint64_t x = in ? (((uint64_t)u.deps[e0 + lane] << 32) | lane) : ~0ull;
-    x = wave_bitonic_reg(x);
-    const uint64_t prev = shfl_up(x, 1);
-    const bool nw = in && (lane == 0 || (prev >> 32) != (x >> 32));
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint64_t bal = __ballot(nw);
-    const uint32_t idx = (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
-    if (in) {
-        u.idx_of_e[e0 + (uint32_t)x] = idx;
-        if (nw) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(x >> 32)];
-    }
-    if (lane == 0) u.ucnt[t] = (uint32_t)__popcll(bal);
 }
 
 // block per listed txn, 64 < E <= MX_BLK_E: LDS bitonic
@@ -3846,40 +3966,63 @@ __global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, const u
     u_cnt[t] = (kv.u_off[t + 1] - kv.u_off[t]) + (ex ? ucnt[t] : 0u);
 }
 
-// the combined layout, 16 lanes per txn: key txns copied from keydeps_core's result (with key codes), range txns from
-// their key records, per-entry union indices and union TxnIds
+// the combined layout. A workgroup owns BLOCK consecutive txns, whose output runs are one contiguous range of each
+// output array: a thread per output element finds its txn among the block's offsets in LDS and reads from that txn's
+// source (key txns: keydeps_core's result, with key codes; range txns: their key records, per-entry union indices and
+// union TxnIds), so every write is a whole-line access.
 __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const uint64_t *__restrict__ etoff,
-                                                    const uint32_t *__restrict__ ktoff, const uint32_t *__restrict__ ucnt, MxE x,
+                                                    const uint32_t *__restrict__ ktoff, MxE x,
                                                     const uint32_t *__restrict__ idx_of_e, const uint32_t *__restrict__ dep_scr,
                                                     const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ key_code,
                                                     MxOut o)
 {
-    const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) >> 4, sub = threadIdx.x & 15u;
-    if (t >= n) return;
-    const uint64_t ao = o.arena_off[t], ko = o.kd_off[t], uo = o.u_off[t];
-    const uint64_t e0 = etoff[t], ex = etoff[t + 1] - e0;
-    if (ex == 0) {
-        const uint64_t a0 = kv.arena_off[t], na = kv.arena_off[t + 1] - a0;
-        const uint64_t k0 = kv.kd_off[t], nk = kv.kd_off[t + 1] - k0;
-        const uint64_t u0 = kv.u_off[t], nu = kv.u_off[t + 1] - u0;
-        for (uint64_t i = sub; i < na; i += 16) o.arena[ao + i] = kv.arena[a0 + i];
-        for (uint64_t i = sub; i < nk; i += 16) {
-            const uint32_t ki = kv.key_idx[k0 + i];
-            o.key_idx[ko + i] = ki;
-            o.kd_key[ko + i] = key_code[key_off[t] + ki];
+    __shared__ uint64_t ao[BLOCK + 1], ko[BLOCK + 1], uo[BLOCK + 1];   // output offsets
+    __shared__ uint64_t sa[BLOCK], sk[BLOCK], su[BLOCK];                // source bases: arena / keys / TxnIds
+    __shared__ uint32_t kdn[BLOCK], kofs[BLOCK];                        // range txn: key records; key txn: key_off
+    const uint32_t t0 = blockIdx.x * BLOCK, nt = min((uint32_t)BLOCK, n - t0), tid = threadIdx.x;
+    if (tid < nt) {
+        const uint32_t t = t0 + tid;
+        ao[tid] = o.arena_off[t]; ko[tid] = o.kd_off[t]; uo[tid] = o.u_off[t];
+        const uint64_t e0 = etoff[t], ex = etoff[t + 1] - e0;
+        if (ex) {
+            const uint32_t k0 = ktoff[t];
+            kdn[tid] = ktoff[t + 1] - k0;
+            sa[tid] = e0; sk[tid] = k0; su[tid] = e0;
+        } else {
+            kdn[tid] = 0xFFFFFFFFu;   // a key txn
+            sa[tid] = kv.arena_off[t]; sk[tid] = kv.kd_off[t]; su[tid] = kv.u_off[t];
+            kofs[tid] = key_off[t];
         }
-        for (uint64_t i = sub; i < nu; i += 16) o.dep_txn[uo + i] = kv.dep_txn[u0 + i];
-        return;
     }
-    const uint32_t k0 = ktoff[t], kd = ktoff[t + 1] - k0;
-    for (uint32_t i = sub; i < kd; i += 16) {
-        o.key_idx[ko + i] = x.kx_idx[k0 + i];
-        o.kd_key[ko + i] = x.kx_code[k0 + i];
-        o.arena[ao + i] = (int32_t)(kd + x.kx_end[k0 + i]);
+    if (tid == 0) { ao[nt] = o.arena_off[t0 + nt]; ko[nt] = o.kd_off[t0 + nt]; uo[nt] = o.u_off[t0 + nt]; }
+    __syncthreads();
+    for (uint64_t j = ao[0] + tid; j < ao[nt]; j += BLOCK) {
+        const uint32_t a = last_le(ao, nt, j);
+        const uint64_t i = j - ao[a];
+        const uint32_t kd = kdn[a];
+        int32_t v;
+        if (kd == 0xFFFFFFFFu) v = kv.arena[sa[a] + i];
+        else if (i < kd) v = (int32_t)(kd + x.kx_end[sk[a] + i]);
+        else v = (int32_t)idx_of_e[sa[a] + i - kd];
+        o.arena[j] = v;
     }
-    for (uint64_t i = sub; i < ex; i += 16) o.arena[ao + kd + i] = (int32_t)idx_of_e[e0 + i];
-    const uint32_t nx = ucnt[t];
-    for (uint32_t i = sub; i < nx; i += 16) o.dep_txn[uo + i] = dep_scr[e0 + i];
+    for (uint64_t j = ko[0] + tid; j < ko[nt]; j += BLOCK) {
+        const uint32_t a = last_le(ko, nt, j);
+        const uint64_t i = j - ko[a];
+        if (kdn[a] == 0xFFFFFFFFu) {
+            const uint32_t ki = kv.key_idx[sk[a] + i];
+            o.key_idx[j] = ki;
+            o.kd_key[j] = key_code[kofs[a] + ki];
+        } else {
+            o.key_idx[j] = x.kx_idx[sk[a] + i];
+            o.kd_key[j] = x.kx_code[sk[a] + i];
+        }
+    }
+    for (uint64_t j = uo[0] + tid; j < uo[nt]; j += BLOCK) {
+        const uint32_t a = last_le(uo, nt, j);
+        const uint64_t i = j - uo[a];
+        o.dep_txn[j] = kdn[a] == 0xFFFFFFFFu ? kv.dep_txn[su[a] + i] : dep_scr[su[a] + i];
+    }
 }
 
 void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *view, SharedDict *shared)
@@ -3926,16 +4069,28 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     if (nseg)
         launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
                ks.key_code, seg_key);
+    // bucket directory: about one key per bucket
+    const uint32_t tbits = nseg ? (uint32_t)std::min(26, std::max(0, bits_for(nseg) - 1)) : 0u;
+    const size_t nbk = (size_t)1 << tbits;
+    uint32_t *bstart = ctx->get<uint32_t>("mx_bstart", nbk + 1);
+    if (nseg) {
+        uint32_t *bcnt = ctx->get<uint32_t>("mx_bcnt", nbk);
+        ACC_HIP(hipMemsetAsync(bcnt, 0, nbk * sizeof(uint32_t), st));
+        launch(ctx, "mx_buckets", k_mx_buckets, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, tbits,
+               (const uint64_t *)seg_key, bcnt);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, bcnt, bstart, nbk, true, bstart + nbk);
+    }
     uint32_t *ra = ctx->get<uint32_t>("mx_ra", R + 1);
     uint32_t *rowner = ctx->get<uint32_t>("mx_rowner", R + 1);
     uint64_t *rcnt = ctx->get<uint64_t>("mx_rcnt", R + 1);
     uint64_t *rpieces = ctx->get<uint64_t>("mx_rpieces", R + 1);
     uint64_t *r_off = ctx->get<uint64_t>("mx_r_off", R + 2);
     uint64_t *poff = ctx->get<uint64_t>("mx_poff", R + 2);
-    uint64_t *errs = ctx->get<uint64_t>("mx_errs", 1);
-    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
+    uint64_t *errs = ctx->get<uint64_t>("mx_errs", 2);   // [0] errors, [1] deferred-query count (k_mx_pcount)
+    ACC_HIP(hipMemsetAsync(errs, 0, 16, st));
+    uint32_t *dcnt = reinterpret_cast<uint32_t *>(errs + 1);
     launch(ctx, "mx_ranges", k_mx_ranges, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, key_off, rng_off, rs, re,
-           in->end_inclusive, (const uint64_t *)seg_key, nseg, ra, rowner, rcnt, rpieces, errs);
+           in->end_inclusive, (const uint64_t *)seg_key, nseg, (const uint32_t *)bstart, tbits, ra, rowner, rcnt, rpieces, errs);
     if (R) {
         scan<uint64_t, OpAdd<uint64_t>>(ctx, rcnt, r_off, R, true, r_off + R);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, rpieces, poff, R, true, poff + R);
@@ -3976,7 +4131,14 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         }
         v = ks.v1view;
         launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff, prange);
-        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc);
+        const uint32_t pack = ks.rbits <= 31;
+        const bool defer = NP * 32 < 0xFFFFFFFFull && !getenv("ACC_MX_NO_DEFER");   // tuning switch: every query in place
+        uint32_t *dlist = defer ? ctx->get<uint32_t>("mx_dlist", NP * 32) : nullptr;
+        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc,
+               pack, dlist, dcnt);
+        if (defer)
+            launch(ctx, "mx_pdefer", k_mx_pdefer, dim3(std::min<unsigned>(grid_for(NP * 32, BLOCK), 4096u)), dim3(BLOCK), 0, pc, v,
+                   (const uint32_t *)dlist, (const uint32_t *)dcnt, pe_cnt, pk_cnt, qc, pack);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, pe_cnt, pe_off, NP, true, pe_off + NP);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, pk_cnt, pk_off, NP, true, pk_off + NP);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, pe_off + NP, 8, hipMemcpyDeviceToHost, st));
@@ -4005,19 +4167,29 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         launch(ctx, "mx_pemit", k_mx_pemit, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, (const uint64_t *)pe_off,
                (const uint32_t *)pk_off, (const uint64_t *)etoff, mx, (const uint32_t *)qc);
         // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
-        uint32_t *blk_list = ctx->get<uint32_t>("mx_blk_list", n);
-        uint32_t *mid_list = ctx->get<uint32_t>("mx_mid_list", n);
-        uint64_t *gst = ctx->get<uint64_t>("mx_gst", 3);
-        ACC_HIP(hipMemsetAsync(gst, 0, 24, st));
-        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, blk_list,
-               mid_list, gst);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 24, hipMemcpyDeviceToHost, st));
+        MxLists L;
+        static const char *lnames[5] = { "mx_l16", "mx_l32", "mx_l64", "mx_mid_list", "mx_blk_list" };
+        for (int k = 0; k < 5; ++k) L.l[k] = ctx->get<uint32_t>(lnames[k], n);
+        uint32_t *const mid_list = L.l[3], *const blk_list = L.l[4];
+        uint64_t *gst = ctx->get<uint64_t>("mx_gst", 6);
+        ACC_HIP(hipMemsetAsync(gst, 0, 48, st));
+        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, L, gst);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 48, hipMemcpyDeviceToHost, st));
         ctx->sync();
         const uint64_t nblk = ctx->pinned[0], nmid = ctx->pinned[2];
+        const uint64_t nsmall[3] = { ctx->pinned[3], ctx->pinned[4], ctx->pinned[5] };
         ctx->stat("keydeps.range_block_txns", nblk);
         ctx->stat("keydeps.range_mid_txns", nmid);
         if (!ctx->pinned[1]) {
-            launch(ctx, "mx_union_wave", k_mx_union_wave, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, n, mu);
+            if (nsmall[0])
+                launch(ctx, "mx_union_s16", k_mx_union_seg<16>, dim3((unsigned)((nsmall[0] + 4 * WAVES - 1) / (4 * WAVES))),
+                       dim3(BLOCK), 0, (const uint32_t *)L.l[0], (const uint64_t *)(gst + 3), mu);
+            if (nsmall[1])
+                launch(ctx, "mx_union_s32", k_mx_union_seg<32>, dim3((unsigned)((nsmall[1] + 2 * WAVES - 1) / (2 * WAVES))),
+                       dim3(BLOCK), 0, (const uint32_t *)L.l[1], (const uint64_t *)(gst + 4), mu);
+            if (nsmall[2])
+                launch(ctx, "mx_union_s64", k_mx_union_seg<64>, dim3((unsigned)((nsmall[2] + WAVES - 1) / WAVES)),
+                       dim3(BLOCK), 0, (const uint32_t *)L.l[2], (const uint64_t *)(gst + 5), mu);
             if (nmid)
                 launch(ctx, "mx_union_mid", k_mx_union_mid, dim3((unsigned)((nmid + WAVES - 1) / WAVES)), dim3(BLOCK), 0,
                        (const uint32_t *)mid_list, (const uint64_t *)gst, mu);
@@ -4066,9 +4238,8 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     o.key_idx = ctx->get<uint32_t>("mx_key_idx", TK + 1);
     o.kd_key = ctx->get<uint64_t>("mx_kd_key", TK + 1);
     o.dep_txn = ctx->get<uint32_t>("mx_dep_txn", TU + 1);
-    launch(ctx, "mx_write", k_mx_write, dim3(grid_for((size_t)n * 16, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
-           (const uint32_t *)ktoff, (const uint32_t *)ucnt, mx, (const uint32_t *)idx_of_e, (const uint32_t *)dep_scr, key_off,
-           key_code, o);
+    launch(ctx, "mx_write", k_mx_write, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
+           (const uint32_t *)ktoff, mx, (const uint32_t *)idx_of_e, (const uint32_t *)dep_scr, key_off, key_code, o);
     ctx->sync();
     *view = acc_keydeps_view{ n, TA, TK, TU, kv.total_edges + Ex, o.arena_off, o.arena, o.kd_off, o.key_idx, o.u_off,
                               o.dep_txn, o.kd_key };

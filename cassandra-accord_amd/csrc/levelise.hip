@@ -365,6 +365,184 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     if (lane == 0 && my_max) atomicMax(max_level, my_max);
 }
 
+// ---- windowed tier (default): the exec order cut into windows of LW positions. A dep of position i is "far" when it
+// lies two or more windows back, "prev" when it lies in the window before i's, "cur" in i's own window. One launch per
+// window w: block 0 walks window w with one lane per position, the window's levels and its cur lists (u16 window
+// offsets) in LDS, so a dependency hop inside the window is an LDS round trip; the prev deps are final in HBM and read
+// once; meanwhile blocks 1.. reduce the far deps of window w + 1 (all in windows <= w - 1, final before this launch)
+// to one max per position on the rest of the GPU. The single-CU walk thus reads only the cur deps from LDS (config 5:
+// ~13% of the 2.5M filtered edges) instead of every list. Published levels are level + 1 (0 = unpublished); the walk
+// of a window ends when every lane has published, which always happens: the smallest unfinished position's cur deps
+// are all earlier positions, already published.
+constexpr uint32_t LW = 1024;          // positions per window = walker threads
+constexpr uint32_t LW_GW = LW / 64;    // gatherer waves per 1024-thread block (one wave per position)
+constexpr uint32_t LW_CL = 61440;      // cur-list entries of a window held in LDS (u16; beyond: read from HBM)
+
+// per position: far / prev / cur dep counts (waiting deps only: exec rank below its own, Commands.java:804-810); also
+// the graph validation (err |= 1 decreasing offsets, 2 a dep >= n)
+__global__ __launch_bounds__(BLOCK) void k_lw_count(uint32_t n, const uint32_t *__restrict__ order_exec,
+                                                    const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
+                                                    const uint32_t *__restrict__ exec_rank, const uint32_t *__restrict__ pos,
+                                                    uint64_t *__restrict__ cnt_far, uint64_t *__restrict__ cnt_prev,
+                                                    uint64_t *__restrict__ cnt_cur, uint32_t *__restrict__ err)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= n) return;
+    const uint32_t t = order_exec[i], er = exec_rank[t], wi = i / LW;
+    const uint64_t a = off[t], b = off[t + 1];
+    if (b < a && lane == 0) atomicOr(err, 1u);
+    uint32_t cf = 0, cp = 0, cc = 0;
+    for (uint64_t e = a + lane; e < b; e += 64) {
+        const uint32_t d = dep[e];
+        if (d >= n) { atomicOr(err, 2u); continue; }
+        if (exec_rank[d] >= er) continue;
+        const uint32_t wd = pos[d] / LW;
+        if (wd == wi) ++cc; else if (wd + 1 == wi) ++cp; else ++cf;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        cf += __shfl_xor(cf, d, 64); cp += __shfl_xor(cp, d, 64); cc += __shfl_xor(cc, d, 64);
+    }
+    if (lane == 0) { cnt_far[i] = cf; cnt_prev[i] = cp; cnt_cur[i] = cc; }
+}
+
+// the far and prev lists (exec-order positions, u32) and the cur lists (offsets in the window, u16), in exec order
+__global__ __launch_bounds__(BLOCK) void k_lw_write(uint32_t n, const uint32_t *__restrict__ order_exec,
+                                                    const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
+                                                    const uint32_t *__restrict__ exec_rank, const uint32_t *__restrict__ pos,
+                                                    const uint64_t *__restrict__ foff, const uint64_t *__restrict__ poff,
+                                                    const uint64_t *__restrict__ coff, uint32_t *__restrict__ far,
+                                                    uint32_t *__restrict__ prev, uint16_t *__restrict__ cur)
+{
+    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
+    if (i >= n) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t t = order_exec[i], er = exec_rank[t], wi = i / LW;
+    const uint64_t a = off[t], b = off[t + 1];
+    uint64_t wf = foff[i], wp = poff[i], wc = coff[i];
+    for (uint64_t c0 = a; c0 < b; c0 += 64) {
+        const uint64_t e = c0 + lane;
+        uint32_t p = 0, wd = 0;
+        bool keep = false;
+        if (e < b) {
+            const uint32_t d = dep[e];
+            if (d < n && exec_rank[d] < er) { p = pos[d]; wd = p / LW; keep = true; }
+        }
+        const bool kc = keep && wd == wi, kp = keep && wd + 1 == wi, kf = keep && !kc && !kp;
+        const uint64_t bf = __ballot(kf), bp = __ballot(kp), bc = __ballot(kc);
+        if (kf) far[wf + (uint64_t)__popcll(bf & lt)] = p;
+        if (kp) prev[wp + (uint64_t)__popcll(bp & lt)] = p;
+        if (kc) cur[wc + (uint64_t)__popcll(bc & lt)] = (uint16_t)(p - wi * LW);
+        wf += (uint64_t)__popcll(bf); wp += (uint64_t)__popcll(bp); wc += (uint64_t)__popcll(bc);
+    }
+}
+
+__device__ __forceinline__ uint32_t lw_lds_ld(const uint32_t *p) { return *(const volatile uint32_t *)p; }
+
+struct LwLists {
+    const uint64_t *foff, *poff, *coff;
+    const uint32_t *far, *prev;
+    const uint16_t *cur;
+};
+
+// one window step (launch w): block 0 walks window w, blocks 1.. gather the far maxima of window w + 1
+__global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists g, uint32_t *__restrict__ base,
+                                                uint32_t *__restrict__ lvlp, const uint32_t *__restrict__ order_exec,
+                                                uint32_t *__restrict__ level, uint32_t *__restrict__ max_level)
+{
+    const uint32_t tid = threadIdx.x, lane = lane_id();
+    if (blockIdx.x > 0) {
+        // gatherer: a wave per position of window w + 1, max of the far deps' published levels (0 = no far dep)
+        const uint32_t j = (w + 1) * LW + (blockIdx.x - 1) * LW_GW + (tid >> 6);
+        if (j >= n || w + 1 < 2) return;
+        const uint64_t a = g.foff[j], b = g.foff[j + 1];
+        uint32_t m = 0;
+        for (uint64_t e = a + lane; e < b; e += 4 * 64) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { const uint64_t q = e + (uint64_t)u * 64; v[u] = q < b ? lvlp[g.far[q]] : 0u; }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m = max(m, v[u]);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+        if (lane == 0) base[j] = m;
+        return;
+    }
+    __shared__ uint32_t L[LW];
+    __shared__ uint16_t CL[LW_CL];
+    __shared__ uint32_t red[LW / 64];
+    const uint32_t w0 = w * LW, wend = min(n, w0 + LW), i = w0 + tid;
+    const bool valid = i < n;
+    // the window's cur lists (contiguous in exec order) into LDS
+    const uint64_t cbase = g.coff[w0], ctot = g.coff[wend] - cbase;
+    const uint32_t cin = (uint32_t)min<uint64_t>(ctot, LW_CL);
+    for (uint32_t e = tid; e < cin; e += LW) CL[e] = g.cur[cbase + e];
+    L[tid] = 0;
+    // prev deps: final in HBM, eight loads in flight
+    uint32_t m = (valid && w >= 2) ? base[i] : 0u;
+    if (valid) {
+        const uint64_t a = g.poff[i], b = g.poff[i + 1];
+        for (uint64_t e0 = a; e0 < b; e0 += 8) {
+            uint32_t p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = e0 + u < b ? g.prev[e0 + u] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) if (p[u] != 0xFFFFFFFFu) m = max(m, lvlp[p[u]]);
+        }
+    }
+    __syncthreads();
+    uint64_t ca = 0, cb = 0;
+    if (valid) { ca = g.coff[i] - cbase; cb = g.coff[i + 1] - cbase; }
+    auto cur_at = [&](uint64_t e) -> uint32_t { return e < cin ? (uint32_t)CL[e] : (uint32_t)g.cur[cbase + e]; };
+    // the cur list with a cursor: entries are consumed in list order (about exec order, so about publication order), one
+    // batch of LW_B per round, stopping at the first unpublished entry (resumed there next round): every round of a wave
+    // is two dependent LDS loads long whatever the lanes' list lengths, so a dependency hop costs about one round (a
+    // lane has consumed its older, already published entries while it waited for the latest)
+    constexpr int LW_B = 8;
+    uint64_t e = ca;
+    bool done = !valid;
+    uint32_t my = 0;
+    while (true) {
+        if (!done) {
+            uint32_t p[LW_B], v[LW_B];
+#pragma unroll
+            for (int u = 0; u < LW_B; ++u) p[u] = e + u < cb ? cur_at(e + u) : 0xFFFFu;
+#pragma unroll
+            for (int u = 0; u < LW_B; ++u) v[u] = p[u] == 0xFFFFu ? 1u : lw_lds_ld(&L[p[u]]);
+            uint32_t adv = 0;
+            bool blocked = false;
+#pragma unroll
+            for (int u = 0; u < LW_B; ++u) {
+                if (blocked || p[u] == 0xFFFFu) continue;
+                if (!v[u]) { blocked = true; continue; }
+                m = max(m, v[u]);
+                ++adv;
+            }
+            e += adv;
+            if (e >= cb) {
+                *(volatile uint32_t *)&L[tid] = m + 1;
+                my = m;
+                done = true;
+            }
+        }
+        if (__all(done)) break;
+    }
+    if (valid) {
+        lvlp[i] = m + 1;
+        level[order_exec[i]] = m;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) my = max(my, (uint32_t)__shfl_xor(my, d, 64));
+    if (lane == 0) red[tid >> 6] = my;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t mx = 0;
+        for (uint32_t q = 0; q < LW / 64; ++q) mx = max(mx, red[q]);
+        if (mx) atomicMax(max_level, mx);
+    }
+}
+
 // published level + 1 -> level
 __global__ __launch_bounds__(BLOCK) void k_lv_unbias(uint32_t n, uint32_t *__restrict__ level)
 {
@@ -405,13 +583,16 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
     const uint32_t npad = (n + 7u) & ~7u;
     uint32_t ch = 0;
-    if (n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
+    // tiers: the windowed walk (default); ACC_LV_LDS: the whole-graph LDS walk (n <= 65535); ACC_LV_WAVES: the
+    // persistent-wave walk
+    const bool windowed = !getenv("ACC_LV_LDS") && !getenv("ACC_LV_WAVES");
+    if (!windowed && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
         const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
         uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
         if (const char *ce = getenv("ACC_LV_CH")) cap = std::min<uint32_t>(cap, (uint32_t)std::max(1, atoi(ce)));
         ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
     }
-    if (!ch) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
+    if (!ch && !windowed) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
     uint64_t *key = ctx->get<uint64_t>("lv_key", n);
     launch(ctx, "lv_keys", k_lv_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, exec_rank, key);
     Sorted se = radix_sort(ctx, "lv_rs_exec", key, nullptr, n, 32);
@@ -426,7 +607,36 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
     ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
-    if (ch) {
+    if (windowed) {
+        uint64_t *cf = ctx->get<uint64_t>("lw_cf", n), *cp = ctx->get<uint64_t>("lw_cp", n), *cc = ctx->get<uint64_t>("lw_cc", n);
+        const unsigned gw = (n + WAVES - 1) / WAVES;
+        launch(ctx, "lv_fcount", k_lw_count, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
+               (const uint32_t *)pos, cf, cp, cc, err);
+        LwLists ls;
+        uint64_t *foff = ctx->get<uint64_t>("lw_foff", (size_t)n + 1), *poff = ctx->get<uint64_t>("lw_poff", (size_t)n + 1);
+        uint64_t *coff = ctx->get<uint64_t>("lw_coff", (size_t)n + 1);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, cf, foff, n, true, foff + n);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, cp, poff, n, true, poff + n);
+        scan<uint64_t, OpAdd<uint64_t>>(ctx, cc, coff, n, true, coff + n);
+        // the lists sized by the unfiltered E (their sums stay on the device); invalid graphs (flagged by the count
+        // pass) are walked harmlessly (bad deps are skipped) and fail at the end
+        const uint64_t cap = std::max<uint64_t>(E, 1);
+        uint32_t *far = ctx->get<uint32_t>("lw_far", cap), *prev = ctx->get<uint32_t>("lw_prev", cap);
+        uint16_t *cur = ctx->get<uint16_t>("lw_cur", cap);
+        launch(ctx, "lv_fwrite", k_lw_write, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
+               (const uint32_t *)pos, (const uint64_t *)foff, (const uint64_t *)poff, (const uint64_t *)coff, far, prev, cur);
+        ls.foff = foff; ls.poff = poff; ls.coff = coff; ls.far = far; ls.prev = prev; ls.cur = cur;
+        uint32_t *base = ctx->get<uint32_t>("lw_base", n), *lvlp = ctx->get<uint32_t>("lw_lvlp", n);
+        const uint32_t nw = (n + LW - 1) / LW;
+        for (uint32_t w = 0; w < nw; ++w) {
+            // gatherers only when window w + 1 exists and has far deps (w + 1 >= 2)
+            const uint32_t nxt = (w + 2 <= nw && w + 1 >= 2) ? std::min<uint32_t>(LW, n - (w + 1) * LW) : 0u;
+            const unsigned gb = 1 + (nxt + LW_GW - 1) / LW_GW;
+            launch(ctx, "lv_walk", k_lw_step, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec, level,
+                   maxl);
+        }
+        ctx->stat("levelise.lds_tier", 2);
+    } else if (ch) {
         uint32_t *fcnt = ctx->get<uint32_t>("lv_fcnt", n);
         uint32_t *foff = ctx->get<uint32_t>("lv_foff", (size_t)n + 1);
         const unsigned gw = (n + WAVES - 1) / WAVES;

@@ -732,11 +732,16 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
             j = min(j, (uint32_t)S - 1);
             const uint64_t qoj = shfl_idx(qo, gb + (int)j);
             const uint32_t startj = (uint32_t)m + __shfl(incl - c, gb + (int)j, 64);
+#ifdef ACC_RD_PROBE_NOGATHER
+            if (sub >= m && sub < m + total) x = ((uint64_t)(qoj & 0xFFFFF) << 32) | (sub - startj);
+#else
             if (sub >= m && sub < m + total) x = o.ent[qoj + (sub - startj)];
+#endif
             m += total;
         }
     }
     // sort within the group (groups are lane-aligned: the xor partners of k <= S stay inside)
+#ifndef ACC_RD_PROBE_NOSORT1
 #pragma unroll
     for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
 #pragma unroll
@@ -747,6 +752,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
             x = (lower == up) ? mn : mx;
         }
     }
+#endif
     const uint64_t prev = shfl_up(x, 1);
     const bool valid = live && sub < m && (sub == 0 || x != prev);       // dedupe identical (range, txn)
     const uint64_t vb = __ballot(valid) & gmask;
@@ -754,6 +760,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint32_t pos = (uint32_t)__popcll(vb & lt);
     const uint32_t rid = (uint32_t)(x >> 32), tp = (uint32_t)x;
     uint64_t y = valid ? (((uint64_t)tp << 8) | pos) : ~0ull;
+#ifndef ACC_RD_PROBE_NOSORT2
 #pragma unroll
     for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
 #pragma unroll
@@ -764,6 +771,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
             y = (lower == up) ? mn : mx;
         }
     }
+#endif
     const uint64_t yprev = shfl_up(y, 1);
     const bool ynew = live && sub < M && (sub == 0 || (y >> 8) != (yprev >> 8));
     const uint64_t nb = __ballot(ynew) & gmask;

@@ -67,6 +67,28 @@ def test_cfk_deps_chained_batches(ctx):
         same(snap, oracle.cfk_apply(CC.empty_snapshot(), head), f"after {c} updates")
 
 
+@pytest.fixture(scope="module", params=[0.0, 0.5], ids=["no_deps", "half_deps"])
+def hot_key_case(request):
+    """One hot key, 2,000 txns / ~8,800 updates with events spread over the whole batch (everything in flight at once):
+    with p_dep 0.5 the deps total ~3.3M (the quadratic working-space bound of round 3 was ~1e13 Ts); with p_dep 0 the
+    missing[] arrays (~150K-250K TxnIds) outgrow the linear first guess, so the replay regrows them."""
+    upd = CC.cfk_case(11, n_txn=2000, n_keys=1, keys_per=1, window=2000, p_dep=request.param)
+    return request.param, upd
+
+
+@pytest.mark.parametrize("frac", [0.3, 0.6, 1.0])
+def test_cfk_deps_hot_key(ctx, hot_key_case, frac):
+    from accord_amd.deps import cfk_apply
+    p_dep, upd = hot_key_case
+    part, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
+    g = cfk_apply(ctx, CC.empty_snapshot(), part)
+    o = oracle.cfk_apply(CC.empty_snapshot(), part)
+    same(g, o, f"hot key p_dep {p_dep} frac {frac}")
+    if p_dep == 0.0 and frac < 1.0:
+        assert len(o["mmsb"]) > 100_000
+        assert ctx.stats()["cfk.apply_regrow"] > 0
+
+
 def test_cfk_deps_empty_and_errors(ctx):
     from accord_amd.deps import IllegalStateException, cfk_apply
     e = CC.empty_snapshot()

@@ -113,8 +113,10 @@ def _worker(rank, world, port, end_inclusive, errq):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,end_inclusive", [(2, 1), (3, 0)])
+@pytest.mark.parametrize("world,end_inclusive", [(2, 1), (3, 0), (8, 1)])
 def test_partial_deps_reduce_host_transport(world, end_inclusive):
+    """World 2, 3 and 8 (the node's 8 CommandStores, CommandStores.java:575-592) over the host transport, every rank on
+    GPU 0: each home rank's reduced PartialDeps against the oracle's fold over the same store split."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
@@ -123,7 +125,7 @@ def test_partial_deps_reduce_host_transport(world, end_inclusive):
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=200)
+        p.join(timeout=240)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
