@@ -25,6 +25,7 @@ batched KeyDeps.merge): PreAccept.reduce on device. Weak scaling (~8M pairs per 
 slowest rank's time. --config 4 at N > 1 runs independent snapshots per rank. Prints ONE JSON line on rank 0.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -347,7 +348,68 @@ def run_config2(args, world, rank, local, dev):
         # config 3: the O(prefix) scans of the 5M-txn hot key make each sampled query cost ~10 ms: sparser sample
         result["cpu_baseline"] = (keydeps_cpu_baseline(batch, "config 3", "ACC_CPU_STRIDE3", 20_000) if c3 else
                                   keydeps_cpu_baseline(batch, "config 2"))
+    if rank == 0 and world == 1 and not c3 and args.scale == 1.0 and os.environ.get("ACC_BENCH_CFK", "1") != "0":
+        result["cfk_apply"] = cfk_apply_leg(local)
     return ctx, timing, elapsed, result
+
+
+def cfk_apply_leg(local, calls=3):
+    """N4: a config-2-sized CommandsForKey update stream (workload.cfk_update_stream: 1M txns x 8
+    uniform keys, ~2M updates / 16M (update, key) pairs / 63M deps, Accept then commit / stable / apply / invalidate,
+    interleaved) applied by ONE acc_cfk_apply call to an empty key-major store, inputs resident in HBM; then
+    acc_cfk_snap_to_batch of the result (the txn-major view acc_map_reduce_full reads). 1 warmup + `calls` timed calls
+    on its own context."""
+    import torch
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import Context, _view_as_snap
+    t0 = time.perf_counter()
+    u = W.cfk_update_stream(1_000_000)
+    t_gen = time.perf_counter() - t0
+    dev = torch.device("cuda", local)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in u.items()}
+    z64 = torch.zeros(1, dtype=torch.int64, device=dev)
+    z32 = torch.zeros(1, dtype=torch.int32, device=dev)
+    zp = z64.data_ptr()
+    snap = L.CfkSnap(L.ACC_MEM_DEVICE, 0, 0, 0, zp, z32.data_ptr(), L.TsCols(zp, zp, zp), L.TsCols(zp, zp, zp), zp,
+                     z32.data_ptr(), L.TsCols(zp, zp, zp))
+    ptr = lambda k: d[k].data_ptr()  # noqa: E731
+    ui = L.CfkUpdates(L.ACC_MEM_DEVICE, len(u["msb"]), len(u["key"]), len(u["dmsb"]),
+                      L.TsCols(ptr("msb"), ptr("lsb"), ptr("node")), L.TsCols(ptr("xmsb"), ptr("xlsb"), ptr("xnode")),
+                      ptr("status"), ptr("flags"), ptr("key_off"), ptr("key"), ptr("dep_off"),
+                      L.TsCols(ptr("dmsb"), ptr("dlsb"), ptr("dnode")))
+    torch.cuda.synchronize()
+    with Context(local, timing=True) as c:
+        v = L.CfkSnapView()
+        c.check(c._lib.acc_cfk_apply(c.handle, C.byref(snap), C.byref(ui), C.byref(v)))
+        c.timing_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            c.check(c._lib.acc_cfk_apply(c.handle, C.byref(snap), C.byref(ui), C.byref(v)))
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1000.0 / calls
+        tm = c.timing()
+        top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:5]
+        regrow = int(c.stats().get("cfk.apply_regrow", 0))
+        out = L.CfkBatchView()
+        si = _view_as_snap(v)
+        c.check(c._lib.acc_cfk_snap_to_batch(c.handle, C.byref(si), C.byref(out)))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            c.check(c._lib.acc_cfk_snap_to_batch(c.handle, C.byref(si), C.byref(out)))
+        torch.cuda.synchronize()
+        ms_b = (time.perf_counter() - t0) * 1000.0 / calls
+        n_upd, n_pairs, n_deps = len(u["msb"]), len(u["key"]), len(u["dmsb"])
+        return {"workload": "workload.cfk_update_stream(1M txns x 8 uniform keys over 1M keys, deps = latest 16 txns "
+                            "below on the key, final status at lag 64): one acc_cfk_apply to an empty store",
+                "updates": n_upd, "update_key_pairs": n_pairs, "deps": n_deps,
+                "ms_per_call": round(ms, 3), "update_key_pairs_per_s": round(n_pairs / ms * 1e3, 1),
+                "deps_per_s": round(n_deps / ms * 1e3, 1), "apply_regrow_rounds": regrow,
+                "out_keys": int(v.n_keys), "out_entries": int(v.n_entries), "out_missing": int(v.n_missing),
+                "snap_to_batch_ms": round(ms_b, 3), "setup_gen_s": round(t_gen, 2),
+                "top_kernels_ms": {k: round(x[0] / calls, 3) for k, x in top}}
 
 
 def run_config2_sharded(args, world, rank, local, dev):

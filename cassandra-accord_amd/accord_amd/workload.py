@@ -481,3 +481,61 @@ def config4(scale: float = 1.0, **kw) -> RangeBatch:
     """BASELINE config 4: 10M range txns (1 EndInclusive range each) interleaved 50/50 with 10M key txns x 4
     keys over the int32 key space (scale multiplies the txn count)."""
     return rangedeps_batch(int(20_000_000 * scale), CONFIG_SEEDS["4"], **kw)
+
+
+def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = None, seed: int = CONFIG_SEEDS["2"] + 7,
+                      max_deps: int = 16, lag: int = 64) -> dict:
+    """A CommandsForKey update stream of config-2 size (acc_cfk_apply's CFK_UPD layout), for the N4 bench leg: the txns
+    of keydeps_batch(n_txn, keys_per_txn, n_keys, uniform keys, status model) as SafeCommandStore.updateCommandsForKey
+    sees them (local/SafeCommandStore.java:217-240): an Accept (ACCEPTED, executeAt = TxnId) at time i, then the final
+    status (COMMITTED / STABLE / APPLIED with the batch's executeAt, or INVALID_OR_TRUNCATED) at time i + lag; txns whose
+    final status is PREACCEPTED / TRANSITIVELY_KNOWN only pre-accept, ACCEPTED ones only accept. The deps of a txn on
+    a key (its keyDeps.txnIds(key)) are the latest max_deps txns below it on that key, every one already known to the
+    key's CFK. Uniform keys: a zipf hot key's CFK grows with its whole history (CommandsForKey.update copies the key's
+    arrays, linear per update), which the reference bounds by pruning, outside the §8 path."""
+    n_keys = n_keys or n_txn
+    b = keydeps_batch(n_txn, keys_per_txn, n_keys, seed, "uniform", status_model="model")
+    st = b.status.astype(np.int64)
+    K = keys_per_txn
+    # deps per (txn, key) pair: the latest max_deps txns below it on the key (pairs sorted by (key, txn))
+    P = b.n_pairs
+    pair_txn = np.repeat(np.arange(n_txn, dtype=np.int64), K)
+    order = np.lexsort((pair_txn, b.key_code))
+    sk = b.key_code[order]
+    new = np.ones(P, bool)
+    new[1:] = sk[1:] != sk[:-1]
+    seg_start = np.maximum.accumulate(np.where(new, np.arange(P), 0))
+    r = np.arange(P) - seg_start                       # position within the key
+    pos = np.empty(P, np.int64)
+    pos[order] = np.arange(P)                          # sorted position of each pair
+    ndep_pair = np.minimum(r, max_deps)[pos]           # per pair (txn-major)
+    txn_sorted = pair_txn[order]
+    # events: (time, txn, kind) kind 0 = first update, 1 = final update
+    first = np.where(st == PREACCEPTED, PREACCEPTED, np.where((st == TRANSITIVELY_KNOWN) | (st == INVALID_OR_TRUNCATED),
+                                                               PREACCEPTED, ACCEPTED))
+    has_final = (st >= COMMITTED) & (st <= INVALID_OR_TRUNCATED)
+    ev_txn = np.concatenate([np.arange(n_txn), np.nonzero(has_final)[0]])
+    ev_kind = np.concatenate([np.zeros(n_txn, np.int64), np.ones(int(has_final.sum()), np.int64)])
+    ev_time = np.where(ev_kind == 0, 2 * ev_txn, 2 * (ev_txn + lag) + 1)
+    o = np.argsort(ev_time, kind="stable")
+    ev_txn, ev_kind = ev_txn[o], ev_kind[o]
+    U = len(ev_txn)
+    ust = np.where(ev_kind == 0, first[ev_txn], st[ev_txn]).astype(np.uint8)
+    final_exec = (ev_kind == 1) & (ust != INVALID_OR_TRUNCATED)
+    xmsb = np.where(final_exec, b.exe_msb[ev_txn], b.txn_msb[ev_txn]).astype(np.uint64)
+    xlsb = np.where(final_exec, b.exe_lsb[ev_txn], b.txn_lsb[ev_txn]).astype(np.uint64)
+    xnode = np.where(final_exec, b.exe_node[ev_txn], b.txn_node[ev_txn]).astype(np.int32)
+    with_deps = (ust >= ACCEPTED) & (ust <= APPLIED)
+    # (update, key) pairs in update order
+    up_pair = (ev_txn[:, None] * K + np.arange(K)[None, :]).reshape(-1)
+    cnt = np.where(np.repeat(with_deps, K), ndep_pair[up_pair], 0).astype(np.int64)
+    dep_off = np.zeros(U * K + 1, np.int64)
+    np.cumsum(cnt, out=dep_off[1:])
+    D = int(dep_off[-1])
+    first_src = np.repeat(pos[up_pair] - cnt, cnt)
+    dsrc = first_src + (np.arange(D, dtype=np.int64) - np.repeat(dep_off[:-1], cnt))
+    dtx = txn_sorted[dsrc]
+    return dict(msb=b.txn_msb[ev_txn], lsb=b.txn_lsb[ev_txn], node=b.txn_node[ev_txn], xmsb=xmsb, xlsb=xlsb, xnode=xnode,
+                status=ust, flags=np.ones(U, np.uint8), key_off=(np.arange(U + 1, dtype=np.int64) * K).astype(np.uint32),
+                key=b.key_code[up_pair], dep_off=dep_off.astype(np.uint32), dmsb=b.txn_msb[dtx], dlsb=b.txn_lsb[dtx],
+                dnode=b.txn_node[dtx])

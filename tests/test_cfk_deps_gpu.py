@@ -69,10 +69,12 @@ def test_cfk_deps_chained_batches(ctx):
 
 @pytest.fixture(scope="module", params=[0.0, 0.5], ids=["no_deps", "half_deps"])
 def hot_key_case(request):
-    """One hot key, 2,000 txns / ~8,800 updates with events spread over the whole batch (everything in flight at once):
-    with p_dep 0.5 the deps total ~3.3M (the quadratic working-space bound of round 3 was ~1e13 Ts); with p_dep 0 the
-    missing[] arrays (~150K-250K TxnIds) outgrow the linear first guess, so the replay regrows them."""
-    upd = CC.cfk_case(11, n_txn=2000, n_keys=1, keys_per=1, window=2000, p_dep=request.param)
+    """One hot key, 600 txns / ~2,700 updates with events spread over the whole batch (everything in flight at once):
+    with p_dep 0.5 the deps total ~120K and the quadratic working-space bound of round 3 was ~1e10-1e11 Ts (0.4-2 TB,
+    the call failed); with p_dep 0 the missing[] arrays (12K-23K TxnIds) outgrow the linear first guess, so the replay
+    regrows them. (A key's updates replay serially in one lane, so a hot key costs its whole history per update: the
+    size here keeps that to seconds.)"""
+    upd = CC.cfk_case(11, n_txn=600, n_keys=1, keys_per=1, window=600, p_dep=request.param)
     return request.param, upd
 
 
@@ -85,8 +87,21 @@ def test_cfk_deps_hot_key(ctx, hot_key_case, frac):
     o = oracle.cfk_apply(CC.empty_snapshot(), part)
     same(g, o, f"hot key p_dep {p_dep} frac {frac}")
     if p_dep == 0.0 and frac < 1.0:
-        assert len(o["mmsb"]) > 100_000
+        assert len(o["mmsb"]) > 10_000
         assert ctx.stats()["cfk.apply_regrow"] > 0
+
+
+def test_cfk_update_stream(ctx):
+    """The bench leg's update stream (workload.cfk_update_stream: Accept with deps, then commit / stable / apply /
+    invalidate with deps, interleaved) at 20,000 txns x 4 keys, applied in one call and in two chained halves."""
+    from accord_amd import workload as W
+    from accord_amd.deps import cfk_apply
+    upd = W.cfk_update_stream(20_000, 4, 3_000)
+    o = oracle.cfk_apply(CC.empty_snapshot(), upd)
+    assert len(o["mmsb"]) > 0 and (o["status"] >= CC.COMMITTED).any()
+    same(cfk_apply(ctx, CC.empty_snapshot(), upd), o, "update stream")
+    a, b = CC.split_updates(upd, len(upd["msb"]) // 2)
+    same(cfk_apply(ctx, cfk_apply(ctx, CC.empty_snapshot(), a), b), o, "update stream, chained halves")
 
 
 def test_cfk_deps_empty_and_errors(ctx):
