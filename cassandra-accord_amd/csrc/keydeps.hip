@@ -390,15 +390,23 @@ __global__ __launch_bounds__(BLOCK) void k_pair_pos(size_t P, const uint32_t *__
 }
 
 // v1 only: committed / uncommitted flags and the segmented prefix-max input
+// multi_seg (non-null): committed[] lists only for segments of two or more entries (the mixed path answers
+// single-entry segments without them, k_mx_pcount)
 __global__ __launch_bounds__(BLOCK) void k_v1_flags(size_t P, const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ s_exec,
-                                                    const uint32_t *__restrict__ seg_incl, uint32_t *__restrict__ cflag,
-                                                    uint32_t *__restrict__ uflag, uint64_t *__restrict__ pmax_in)
+                                                    const uint32_t *__restrict__ seg_incl, const uint32_t *__restrict__ multi_seg,
+                                                    uint32_t *__restrict__ cflag, uint32_t *__restrict__ uflag,
+                                                    uint64_t *__restrict__ pmax_in)
 {
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
     uint32_t st = s_info[p] & 7u;
     bool c = st >= 4 && st <= 6;
-    cflag[p] = c;
+    if (multi_seg) {
+        const uint32_t sg = seg_incl[p] - 1;
+        cflag[p] = c && multi_seg[sg + 1] - multi_seg[sg] >= 2;
+    } else {
+        cflag[p] = c;
+    }
     uflag[p] = st >= 1 && st <= 3;
     // segmented prefix-max via a segment-id prefix: max over (seg << 32 | exec+1) never crosses segments
     pmax_in[p] = ((uint64_t)(seg_incl[p] - 1) << 32) | (c ? (uint64_t)s_exec[p] + 1 : 0);
@@ -416,7 +424,7 @@ __global__ __launch_bounds__(BLOCK) void k_committed_keys(size_t P, const uint32
                                                           const uint32_t *__restrict__ seg_incl, const uint32_t *__restrict__ s_exec,
                                                           const uint32_t *__restrict__ uflag, const uint32_t *__restrict__ cum_u,
                                                           int ebits, int bits, uint64_t *__restrict__ ckey,
-                                                          uint32_t *__restrict__ cpos, uint32_t *__restrict__ u_pos)
+                                                          uint32_t *__restrict__ cpos, uint32_t *__restrict__ u_pos, int pads)
 {
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p >= P) return;
@@ -426,7 +434,7 @@ __global__ __launch_bounds__(BLOCK) void k_committed_keys(size_t P, const uint32
         ckey[c] = ((uint64_t)(seg_incl[p] - 1) << ebits) | s_exec[p];
         cpos[c] = (uint32_t)p;
     }
-    if (p >= nc) {
+    if (pads && p >= nc) {
         ckey[p] = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
         cpos[p] = 0xFFFFFFFFu;
     }
@@ -2772,15 +2780,19 @@ struct KdState {
 
 // Exact-replay CFK columns: uncommitted/committed flags and counts, segmented executeAt prefix max, committed[] per
 // segment sorted by executeAt (CommandsForKey.java:462-469) with the nearest-Write scan
+// multi_only: committed[] lists of the segments with two or more entries only, sorted at their exact size (one host
+// sync): the mixed path's single-entry segments never read them
 static CfkView build_v1_cfk(acc_ctx *ctx, uint32_t n, size_t P, int rbits, const uint64_t *tl, const uint32_t *owner,
                             const uint32_t *rank, const uint32_t *seg_incl, const uint32_t *seg_start,
-                            const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info, const uint32_t *pair_pos)
+                            const uint32_t *s_rank, const uint32_t *s_exec, const uint8_t *s_info, const uint32_t *pair_pos,
+                            bool multi_only = false)
 {
     const unsigned gP = grid_for(P, BLOCK);
     uint32_t *cflag = ctx->get<uint32_t>("cflag", P);
     uint32_t *uflag = ctx->get<uint32_t>("uflag", P);
     uint64_t *pmax_in = ctx->get<uint64_t>("pmax_in", P);
-    launch(ctx, "v1_flags", k_v1_flags, dim3(gP), dim3(BLOCK), 0, P, s_info, s_exec, seg_incl, cflag, uflag, pmax_in);
+    launch(ctx, "v1_flags", k_v1_flags, dim3(gP), dim3(BLOCK), 0, P, s_info, s_exec, seg_incl,
+           multi_only ? seg_start : (const uint32_t *)nullptr, cflag, uflag, pmax_in);
     uint32_t *cum_c = ctx->get<uint32_t>("cum_c", P + 1);
     uint32_t *cum_u = ctx->get<uint32_t>("cum_u", P + 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, cflag, cum_c, P, true, cum_c + P);
@@ -2799,8 +2811,15 @@ static CfkView build_v1_cfk(acc_ctx *ctx, uint32_t n, size_t P, int rbits, const
     uint32_t *u_pos = ctx->get<uint32_t>("u_pos", P);
     launch(ctx, "committed_keys", k_committed_keys, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)cflag,
            (const uint32_t *)cum_c, (const uint32_t *)seg_incl, (const uint32_t *)s_exec, (const uint32_t *)uflag,
-           (const uint32_t *)cum_u, rbits, cbits, ckey, cpos, u_pos);
-    Sorted cs = radix_sort(ctx, "rs_cl", ckey, cpos, P, cbits);
+           (const uint32_t *)cum_u, rbits, cbits, ckey, cpos, u_pos, multi_only ? 0 : 1);
+    size_t NC = P;
+    if (multi_only) {
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, cum_c + P, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+        NC = (size_t)(ctx->pinned[0] & 0xFFFFFFFFu);
+        ctx->stat("keydeps.v1_committed_sorted", NC);
+    }
+    Sorted cs = radix_sort(ctx, "rs_cl", ckey, cpos, NC, cbits);
     uint32_t *cl_exec = ctx->get<uint32_t>("cl_exec", P);
     uint32_t *lastw_in = ctx->get<uint32_t>("lastw_in", P);
     uint32_t *lastw = ctx->get<uint32_t>("lastw", P);
@@ -3635,11 +3654,17 @@ __device__ __forceinline__ uint32_t mx_qcount(uint32_t q) { return (q & MX_ONE) 
 // s1 = s0 + 1, make_query_ts / run_query reduce to one test of that entry. Its committed[] is itself or empty, so any
 // maxCommittedBefore M is its own executeAt, which the prefix-max prune (executeAt < M) never removes; nothing of the
 // segment lies below scanStart = s0; the scan [s0, insertPos) is the entry exactly when its TxnId is below T.executeAt.
-// Queries over longer segments go to a list (dlist, wave-aggregated appends) that k_mx_pdefer answers densely, adding
-// into the piece totals; dlist null: every query in place.
+// Queries over longer segments go to deferred lists that k_mx_pdefer answers densely, adding into the piece totals:
+// MX_DSLOTS lists (block b appends to list b % MX_DSLOTS with wave-aggregated atomics on that list's counter, so the
+// appends spread over many addresses), list s holding at most dcap entries (its blocks' lanes); dlist null: every
+// query in place.
+constexpr uint32_t MX_DSLOTS = 1024;
+// prec[p] (for the emit pass, one load instead of a chain): owner txn, first segment, covered-key index of the
+// first segment within the txn's keys, queries
 __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkView v, uint64_t *__restrict__ pe_cnt,
                                                      uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack,
-                                                     uint32_t *__restrict__ dlist, uint32_t *__restrict__ dcnt)
+                                                     uint32_t *__restrict__ dlist, uint32_t *__restrict__ dcnt, uint32_t dcap,
+                                                     uint4 *__restrict__ prec)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u, g0 = lane_id() & 32u;
@@ -3649,6 +3674,8 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkVie
         const uint32_t j = pc.prange[p], t = pc.rowner[j];
         const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
         const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
+        if (sub == 0)
+            prec[p] = make_uint4(t, pc.ra[j] + k0, (uint32_t)(pc.r_off[j] - pc.r_off[pc.rng_off[t]] + k0), nk);
         uint32_t f = 0;
         if (sub < nk) {
             const uint32_t seg = pc.ra[j] + k0 + sub;
@@ -3666,26 +3693,28 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkVie
     }
     const uint64_t db = __ballot(dfr);
     if (db) {
+        const uint32_t slot = blockIdx.x % MX_DSLOTS;
         uint32_t base = 0;
         const uint32_t lead = (uint32_t)__ffsll((unsigned long long)db) - 1;
-        if (lane_id() == lead) base = atomicAdd(dcnt, (uint32_t)__popcll(db));
+        if (lane_id() == lead) base = atomicAdd(&dcnt[slot], (uint32_t)__popcll(db));
         base = __shfl(base, (int)lead, 64);
-        if (dfr) dlist[base + (uint32_t)__popcll(db & ((1ull << lane_id()) - 1))] = (uint32_t)(p * 32 + sub);
+        if (dfr) dlist[(size_t)slot * dcap + base + (uint32_t)__popcll(db & ((1ull << lane_id()) - 1))] = (uint32_t)(p * 32 + sub);
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
     const uint32_t te = __shfl(ce, (int)(g0 + 31), 64), tk = __shfl(ck, (int)(g0 + 31), 64);
     if (p < NP && sub == 0) { pe_cnt[p] = te; pk_cnt[p] = tk; }
 }
 
-// the deferred queries (segments of two or more entries): the exact-replay scan, one lane each, over a grid-stride
-// loop bounded by the device-side count
+// the deferred queries (segments of two or more entries): the exact-replay scan, one lane each; blockIdx.y = list,
+// a grid-stride loop over its device-side count
 __global__ __launch_bounds__(BLOCK) void k_mx_pdefer(MxP pc, CfkView v, const uint32_t *__restrict__ dlist,
-                                                     const uint32_t *__restrict__ dcnt, uint64_t *__restrict__ pe_cnt,
+                                                     const uint32_t *__restrict__ dcnt, uint32_t dcap, uint64_t *__restrict__ pe_cnt,
                                                      uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack)
 {
-    const uint32_t nd = *dcnt;
+    const uint32_t nd = dcnt[blockIdx.y];
+    const uint32_t *lst = dlist + (size_t)blockIdx.y * dcap;
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nd; i += gridDim.x * BLOCK) {
-        const uint32_t q = dlist[i], p = q >> 5, sub = q & 31u;
+        const uint32_t q = lst[i], p = q >> 5, sub = q & 31u;
         const uint32_t j = pc.prange[p], t = pc.rowner[j];
         const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
         uint32_t f = 0;
@@ -3700,40 +3729,35 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pdefer(MxP pc, CfkView v, const ui
 
 struct MxE {   // emitted entries and key records of the range txns
     uint32_t *deps, *owner;          // [Ex]: TxnId rank, owning txn
-    uint32_t *kx_idx, *kx_end;       // [Kx]: covered-key index, end offset within the txn's entries
+    uint32_t *kx_idx, *kx_end;       // [Kx]: covered-key index, end of its entries (absolute entry index)
     uint64_t *kx_code;               // [Kx]: key code
 };
 
-__global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, MxP pc, CfkView v, const uint64_t *__restrict__ pe_off,
-                                                    const uint32_t *__restrict__ pk_off, const uint64_t *__restrict__ etoff, MxE x,
-                                                    const uint32_t *__restrict__ qc)
+__global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, const uint4 *__restrict__ prec, const uint64_t *__restrict__ seg_key,
+                                                    CfkView v, const uint64_t *__restrict__ pe_off,
+                                                    const uint32_t *__restrict__ pk_off, MxE x, const uint32_t *__restrict__ qc)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u;
-    uint32_t c = 0, q = 0, j = 0, t = 0, seg = 0, k0 = 0;
+    uint32_t c = 0, q = 0;
+    uint4 pr = make_uint4(0, 0, 0, 0);
     bool act = false;
     if (p < NP) {
-        j = pc.prange[p];
-        t = pc.rowner[j];
-        k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
-        const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
-        act = sub < nk;
-        if (act) {
-            seg = pc.ra[j] + k0 + sub;
-            q = qc[p * 32 + sub];
-            c = mx_qcount(q);
-        }
+        pr = prec[p];
+        q = qc[p * 32 + sub];
+        act = sub < pr.w;
+        c = act ? mx_qcount(q) : 0u;
     }
     const uint32_t ce = mx_scan32(c, sub), ck = mx_scan32(c != 0 ? 1u : 0u, sub);
     if (!act || c == 0) return;
     const uint64_t e = pe_off[p] + (ce - c);
+    const uint32_t seg = pr.y + sub;
     if (q & MX_ONE) x.deps[e] = q & ~MX_ONE;
-    else run_query<true>(v, make_query_ts(v, t, seg), x.deps + e);
-    for (uint32_t i = 0; i < c; ++i) x.owner[e + i] = t;
+    else run_query<true>(v, make_query_ts(v, pr.x, seg), x.deps + e);
     const uint32_t kr = pk_off[p] + ck - 1;
-    x.kx_idx[kr] = (uint32_t)(pc.r_off[j] - pc.r_off[pc.rng_off[t]] + k0 + sub);
-    x.kx_code[kr] = pc.seg_key[seg];
-    x.kx_end[kr] = (uint32_t)(e + c - etoff[t]);
+    x.kx_idx[kr] = pr.z + sub;
+    x.kx_code[kr] = seg_key[seg];
+    x.kx_end[kr] = (uint32_t)(e + c);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mx_toff(uint32_t n, const uint32_t *__restrict__ rng_off, const uint64_t *__restrict__ poff,
@@ -3745,6 +3769,14 @@ __global__ __launch_bounds__(BLOCK) void k_mx_toff(uint32_t n, const uint32_t *_
     const uint64_t p = poff[rng_off[t]];
     etoff[t] = pe_off[p];
     ktoff[t] = pk_off[p];
+}
+
+// the owning txn of every emitted entry (fallback union only)
+__global__ __launch_bounds__(BLOCK) void k_mx_owner(uint32_t n, const uint64_t *__restrict__ etoff, uint32_t *__restrict__ owner)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n) return;
+    for (uint64_t e = etoff[t]; e < etoff[t + 1]; ++e) owner[e] = t;
 }
 
 // sort keys (txn, TxnId rank) of the emitted entries (fallback union)
@@ -4002,7 +4034,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
         const uint32_t kd = kdn[a];
         int32_t v;
         if (kd == 0xFFFFFFFFu) v = kv.arena[sa[a] + i];
-        else if (i < kd) v = (int32_t)(kd + x.kx_end[sk[a] + i]);
+        else if (i < kd) v = (int32_t)(kd + (x.kx_end[sk[a] + i] - (uint32_t)sa[a]));
         else v = (int32_t)idx_of_e[sa[a] + i - kd];
         o.arena[j] = v;
     }
@@ -4086,9 +4118,8 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     uint64_t *rpieces = ctx->get<uint64_t>("mx_rpieces", R + 1);
     uint64_t *r_off = ctx->get<uint64_t>("mx_r_off", R + 2);
     uint64_t *poff = ctx->get<uint64_t>("mx_poff", R + 2);
-    uint64_t *errs = ctx->get<uint64_t>("mx_errs", 2);   // [0] errors, [1] deferred-query count (k_mx_pcount)
-    ACC_HIP(hipMemsetAsync(errs, 0, 16, st));
-    uint32_t *dcnt = reinterpret_cast<uint32_t *>(errs + 1);
+    uint64_t *errs = ctx->get<uint64_t>("mx_errs", 1);
+    ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
     launch(ctx, "mx_ranges", k_mx_ranges, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, key_off, rng_off, rs, re,
            in->end_inclusive, (const uint64_t *)seg_key, nseg, (const uint32_t *)bstart, tbits, ra, rowner, rcnt, rpieces, errs);
     if (R) {
@@ -4123,22 +4154,29 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     uint64_t Ex = 0, Kx = 0;
     CfkView v{};
     uint32_t *qc = ctx->get<uint32_t>("mx_qc", NP * 32);
+    uint4 *prec = ctx->get<uint4>("mx_prec", NP + 1);
     if (NP) {
+        const uint32_t pack = ks.rbits <= 31;
+        const bool defer = NP * 32 < 0xFFFFFFFFull && !getenv("ACC_MX_NO_DEFER");   // tuning switch: every query in place
         if (!ks.v1) {
+            // with deferral and packed single results the exact-replay scan only ever runs on segments of two or more
+            // entries (pcount / pdefer; pemit replays only lanes of two or more entries)
             ks.v1view = build_v1_cfk(ctx, n, ks.P, ks.rbits, ks.tl, ks.owner, ks.rank, ks.seg_incl, ks.seg_start, ks.s_rank,
-                                     ks.s_exec, ks.s_info, ks.pair_pos);
+                                     ks.s_exec, ks.s_info, ks.pair_pos, defer && pack);
             ks.v1 = true;
         }
         v = ks.v1view;
         launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff, prange);
-        const uint32_t pack = ks.rbits <= 31;
-        const bool defer = NP * 32 < 0xFFFFFFFFull && !getenv("ACC_MX_NO_DEFER");   // tuning switch: every query in place
-        uint32_t *dlist = defer ? ctx->get<uint32_t>("mx_dlist", NP * 32) : nullptr;
-        launch(ctx, "mx_pcount", k_mx_pcount, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc,
-               pack, dlist, dcnt);
+        const unsigned gcount = grid_for(NP * 32, BLOCK);
+        const uint32_t dcap = ((gcount + MX_DSLOTS - 1) / MX_DSLOTS) * BLOCK;   // lanes of the blocks of one list
+        uint32_t *dlist = defer ? ctx->get<uint32_t>("mx_dlist", (size_t)MX_DSLOTS * dcap) : nullptr;
+        uint32_t *dcnt = ctx->get<uint32_t>("mx_dcnt", MX_DSLOTS);
+        if (defer) ACC_HIP(hipMemsetAsync(dcnt, 0, MX_DSLOTS * sizeof(uint32_t), st));
+        launch(ctx, "mx_pcount", k_mx_pcount, dim3(gcount), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc, pack, dlist, dcnt, dcap,
+               prec);
         if (defer)
-            launch(ctx, "mx_pdefer", k_mx_pdefer, dim3(std::min<unsigned>(grid_for(NP * 32, BLOCK), 4096u)), dim3(BLOCK), 0, pc, v,
-                   (const uint32_t *)dlist, (const uint32_t *)dcnt, pe_cnt, pk_cnt, qc, pack);
+            launch(ctx, "mx_pdefer", k_mx_pdefer, dim3(8, MX_DSLOTS), dim3(BLOCK), 0, pc, v, (const uint32_t *)dlist,
+                   (const uint32_t *)dcnt, dcap, pe_cnt, pk_cnt, qc, pack);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, pe_cnt, pe_off, NP, true, pe_off + NP);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, pk_cnt, pk_off, NP, true, pk_off + NP);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, pe_off + NP, 8, hipMemcpyDeviceToHost, st));
@@ -4164,8 +4202,8 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     uint32_t *dep_scr = ctx->get<uint32_t>("mx_dep_scr", Ex + 1);
     MxU mu{ mx.deps, etoff, ks.txn_of_rank, idx_of_e, dep_scr, ucnt };
     if (Ex) {
-        launch(ctx, "mx_pemit", k_mx_pemit, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, pc, v, (const uint64_t *)pe_off,
-               (const uint32_t *)pk_off, (const uint64_t *)etoff, mx, (const uint32_t *)qc);
+        launch(ctx, "mx_pemit", k_mx_pemit, dim3(grid_for(NP * 32, BLOCK)), dim3(BLOCK), 0, NP, (const uint4 *)prec,
+               (const uint64_t *)seg_key, v, (const uint64_t *)pe_off, (const uint32_t *)pk_off, mx, (const uint32_t *)qc);
         // per-txn TxnId unions: wave / block tiers, or one (txn, rank) sort when some txn is beyond the block tier
         MxLists L;
         static const char *lnames[5] = { "mx_l16", "mx_l32", "mx_l64", "mx_mid_list", "mx_blk_list" };
@@ -4202,6 +4240,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
             uint64_t *skey = ctx->get<uint64_t>("mx_skey", Ex);
             uint32_t *uflag = ctx->get<uint32_t>("mx_uflag", Ex + 1);
             uint32_t *ucum = ctx->get<uint32_t>("mx_ucum", Ex + 1);
+            launch(ctx, "mx_owner", k_mx_owner, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, mx.owner);
             launch(ctx, "mx_sortkeys", k_mx_sortkeys, dim3(grid_for(Ex, BLOCK)), dim3(BLOCK), 0, Ex, (const uint32_t *)mx.deps,
                    (const uint32_t *)mx.owner, ks.rbits, skey);
             Sorted so = radix_sort(ctx, "mx_rs", skey, nullptr, Ex, tbits + ks.rbits);

@@ -445,7 +445,9 @@ struct LwLists {
     const uint16_t *cur;
 };
 
-// one window step (launch w): block 0 walks window w, blocks 1.. gather the far maxima of window w + 1
+// one window step (launch w): block 0 walks window w, blocks 1.. gather the far maxima of window w + 1.
+// POLL = 1: the batch walk for long chains (a blocked lane re-reads one entry per round); else the sliding walk
+template <int POLL>
 __global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists g, uint32_t *__restrict__ base,
                                                 uint32_t *__restrict__ lvlp, const uint32_t *__restrict__ order_exec,
                                                 uint32_t *__restrict__ level, uint32_t *__restrict__ max_level)
@@ -495,38 +497,87 @@ __global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists 
     uint64_t ca = 0, cb = 0;
     if (valid) { ca = g.coff[i] - cbase; cb = g.coff[i + 1] - cbase; }
     auto cur_at = [&](uint64_t e) -> uint32_t { return e < cin ? (uint32_t)CL[e] : (uint32_t)g.cur[cbase + e]; };
-    // the cur list with a cursor: entries are consumed in list order (about exec order, so about publication order), one
-    // batch of LW_B per round, stopping at the first unpublished entry (resumed there next round): every round of a wave
-    // is two dependent LDS loads long whatever the lanes' list lengths, so a dependency hop costs about one round (a
-    // lane has consumed its older, already published entries while it waited for the latest)
     constexpr int LW_B = 8;
-    uint64_t e = ca;
     bool done = !valid;
     uint32_t my = 0;
-    while (true) {
-        if (!done) {
-            uint32_t p[LW_B], v[LW_B];
+    if (POLL != 1) {
+        // graphs with many in-window deps per position: a sliding cursor over the cur list, LW_B entries per round
+        // read afresh (list entries and their levels), consumed up to the first unpublished one (resumed there next
+        // round), so a lane consumes its older, already published entries while it waits for the latest
+        uint64_t e = ca;
+        while (true) {
+            if (!done) {
+                uint32_t p[LW_B], v[LW_B];
 #pragma unroll
-            for (int u = 0; u < LW_B; ++u) p[u] = e + u < cb ? cur_at(e + u) : 0xFFFFu;
+                for (int u = 0; u < LW_B; ++u) p[u] = e + u < cb ? cur_at(e + u) : 0xFFFFu;
 #pragma unroll
-            for (int u = 0; u < LW_B; ++u) v[u] = p[u] == 0xFFFFu ? 1u : lw_lds_ld(&L[p[u]]);
-            uint32_t adv = 0;
-            bool blocked = false;
+                for (int u = 0; u < LW_B; ++u) v[u] = p[u] == 0xFFFFu ? 1u : lw_lds_ld(&L[p[u]]);
+                uint32_t adv = 0;
+                bool blocked = false;
 #pragma unroll
-            for (int u = 0; u < LW_B; ++u) {
-                if (blocked || p[u] == 0xFFFFu) continue;
-                if (!v[u]) { blocked = true; continue; }
-                m = max(m, v[u]);
-                ++adv;
+                for (int u = 0; u < LW_B; ++u) {
+                    if (blocked || p[u] == 0xFFFFu) continue;
+                    if (!v[u]) { blocked = true; continue; }
+                    m = max(m, v[u]);
+                    ++adv;
+                }
+                e += adv;
+                if (e >= cb) {
+                    *(volatile uint32_t *)&L[tid] = m + 1;
+                    my = m;
+                    done = true;
+                }
             }
-            e += adv;
-            if (e >= cb) {
-                *(volatile uint32_t *)&L[tid] = m + 1;
-                my = m;
-                done = true;
-            }
+            if (__all(done)) break;
         }
-        if (__all(done)) break;
+    } else {
+        // few deps per position (long chains): batches of LW_B entries held in registers (read from LDS once per
+        // batch); a "full" round loads the levels of every entry left in the batch and consumes up to the first
+        // unpublished one, then the blocked lane polls that one entry only (one LDS load per round, so the waves
+        // spinning behind the chain leave the LDS to the wave advancing it) and goes back to a full round once it is
+        // published: a hop costs about two short rounds
+        uint64_t e = ca;             // first entry of the batch
+        uint32_t p[LW_B];
+        uint32_t np = 0, k = 0;      // batch size, entries consumed
+        bool full = true;
+        while (true) {
+            if (!done) {
+                if (k == np) {
+                    e += np;
+                    np = (uint32_t)min<uint64_t>(LW_B, cb - e);
+#pragma unroll
+                    for (int u = 0; u < LW_B; ++u) p[u] = (uint32_t)u < np ? cur_at(e + u) : 0u;
+                    k = 0;
+                    full = true;
+                }
+                if (full) {
+                    uint32_t v[LW_B];
+#pragma unroll
+                    for (int u = 0; u < LW_B; ++u) v[u] = ((uint32_t)u >= k && (uint32_t)u < np) ? lw_lds_ld(&L[p[u]]) : 1u;
+                    bool blocked = false;
+#pragma unroll
+                    for (int u = 0; u < LW_B; ++u) {
+                        if (blocked || (uint32_t)u < k || (uint32_t)u >= np) continue;
+                        if (!v[u]) { blocked = true; continue; }
+                        m = max(m, v[u]);
+                        ++k;
+                    }
+                    full = !blocked;
+                } else {
+                    uint32_t pk = p[0];
+#pragma unroll
+                    for (int u = 1; u < LW_B; ++u) if ((uint32_t)u == k) pk = p[u];
+                    const uint32_t v = lw_lds_ld(&L[pk]);
+                    if (v) { m = max(m, v); ++k; full = true; }
+                }
+                if (k == np && e + np >= cb) {
+                    *(volatile uint32_t *)&L[tid] = m + 1;
+                    my = m;
+                    done = true;
+                }
+            }
+            if (__all(done)) break;
+        }
     }
     if (valid) {
         lvlp[i] = m + 1;
@@ -583,9 +634,10 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
     const uint32_t npad = (n + 7u) & ~7u;
     uint32_t ch = 0;
-    // tiers: the windowed walk (default); ACC_LV_LDS: the whole-graph LDS walk (n <= 65535); ACC_LV_WAVES: the
-    // persistent-wave walk
-    const bool windowed = !getenv("ACC_LV_LDS") && !getenv("ACC_LV_WAVES");
+    // tiers: the whole-graph LDS walk (n <= 65535: config 5 0.89 ms, the windowed walk 1.07), the windowed walk beyond
+    // (ACC_LV_WIN forces it; the 1M-txn chain graph: 0.54 us per level, the persistent-wave walk 0.75); ACC_LV_WAVES:
+    // the persistent-wave walk
+    const bool windowed = (n > LV_LDS_MAX_N || getenv("ACC_LV_WIN")) && !getenv("ACC_LV_LDS") && !getenv("ACC_LV_WAVES");
     if (!windowed && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
         const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
         uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
@@ -628,12 +680,20 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         ls.foff = foff; ls.poff = poff; ls.coff = coff; ls.far = far; ls.prev = prev; ls.cur = cur;
         uint32_t *base = ctx->get<uint32_t>("lw_base", n), *lvlp = ctx->get<uint32_t>("lw_lvlp", n);
         const uint32_t nw = (n + LW - 1) / LW;
+        // poll width by the graph's deps per txn (few: long chains, poll one entry; many: poll the batch)
+        int poll = E <= 16ull * n ? 1 : 8;
+        if (const char *pe = getenv("ACC_LV_POLL")) poll = atoi(pe) == 1 ? 1 : 8;   // tuning switch
+        ctx->stat("levelise.poll", (uint64_t)poll);
         for (uint32_t w = 0; w < nw; ++w) {
             // gatherers only when window w + 1 exists and has far deps (w + 1 >= 2)
             const uint32_t nxt = (w + 2 <= nw && w + 1 >= 2) ? std::min<uint32_t>(LW, n - (w + 1) * LW) : 0u;
             const unsigned gb = 1 + (nxt + LW_GW - 1) / LW_GW;
-            launch(ctx, "lv_walk", k_lw_step, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec, level,
-                   maxl);
+            if (poll == 1)
+                launch(ctx, "lv_walk", k_lw_step<1>, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec,
+                       level, maxl);
+            else
+                launch(ctx, "lv_walk", k_lw_step<8>, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec,
+                       level, maxl);
         }
         ctx->stat("levelise.lds_tier", 2);
     } else if (ch) {

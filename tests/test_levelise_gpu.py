@@ -97,7 +97,8 @@ def test_merge_then_levelise_device(ctx):
 
 def test_levelise_one_million(ctx):
     """1M txns, deps mostly on recent txns in executeAt order (a hot-key write chain runs through them), plus random
-    far deps and deps executing later (ignored): the persistent multi-workgroup walk against the oracle."""
+    far deps and deps executing later (ignored): the windowed walk (batch polling, about 1M levels) against the
+    oracle."""
     import oracle
     from accord_amd.deps import levelise
     rng = np.random.RandomState(2024)
@@ -121,6 +122,7 @@ def test_levelise_one_million(ctx):
     off = np.zeros(n + 1, np.uint64)
     np.cumsum(np.bincount(allsrc, minlength=n), out=off[1:])
     lv, order, nl = levelise(ctx, off, alld.astype(np.uint32), er)
+    assert ctx.stats().get("levelise.lds_tier") == 2 and ctx.stats().get("levelise.poll") == 1
     l2, o2, nl2 = oracle.levelise(off, alld.astype(np.uint32), er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
@@ -128,16 +130,20 @@ def test_levelise_one_million(ctx):
 
 
 @pytest.mark.parametrize("env,n,max_deps,tier", [
-    ({}, 2000, 300, 2),                                      # windowed walk (default): two windows
-    ({}, 5000, 30, 2),                                       # windowed walk: far deps gathered for windows 2..4
-    ({}, 1024, 40, 2),                                       # exactly one window
-    ({}, 3073, 900, 2),                                      # a partial last window, long lists
-    ({"ACC_LV_LDS": "1"}, 2000, 300, 1),                     # LDS walk, default chunks
-    ({"ACC_LV_LDS": "1", "ACC_LV_CH": "64"}, 2000, 300, 1),  # LDS walk, 64-entry chunks: long lists read from HBM
-    ({"ACC_LV_LDS": "1", "ACC_LV_CH": "256"}, 20000, 12, 1), # many rounds, rounds of > 2048 positions
+    ({}, 2000, 300, 1),                                      # LDS walk (default up to 65,535 txns), default chunks
+    ({"ACC_LV_CH": "64"}, 2000, 300, 1),                     # LDS walk, 64-entry chunks: long lists read from HBM
+    ({"ACC_LV_CH": "256"}, 20000, 12, 1),                    # many rounds, rounds of > 2048 positions
+    ({}, 65535, 6, 1),                                       # largest LDS-walk graph (u16 levels and positions)
+    ({}, 65536, 6, 2),                                       # beyond the LDS walk: the windowed walk (batch polling)
+    ({"ACC_LV_WIN": "1"}, 2000, 300, 2),                     # windowed walk, sliding cursor: two windows
+    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 2000, 300, 2), # windowed walk, batch polling
+    ({"ACC_LV_WIN": "1"}, 5000, 30, 2),                      # far deps gathered for windows 2..4 (batch polling)
+    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "8"}, 5000, 30, 2),  # the same, sliding cursor
+    ({"ACC_LV_WIN": "1"}, 1024, 40, 2),                      # exactly one window
+    ({"ACC_LV_WIN": "1"}, 3073, 900, 2),                     # a partial last window, long lists
+    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 3073, 900, 2), # the same, batch polling
     ({"ACC_LV_WAVES": "1"}, 5000, 30, 0),                    # the persistent-wave walk at a size the LDS tier takes
-    ({"ACC_LV_LDS": "1"}, 65535, 6, 1),                      # largest LDS-walk graph (u16 levels and positions)
-    ({"ACC_LV_LDS": "1"}, 65536, 6, 0),                      # beyond the LDS walk: the persistent-wave walk
+    ({"ACC_LV_WAVES": "1"}, 65536, 6, 0),                    # the persistent-wave walk beyond it
 ])
 def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps, tier):
     import oracle
@@ -153,7 +159,7 @@ def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps, tier):
     assert nl == nl2
 
 
-@pytest.mark.parametrize("walk", ["windowed", "lds", "waves"])
+@pytest.mark.parametrize("walk", ["windowed", "windowed_poll1", "lds", "waves"])
 def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
     """A config-5-shaped merged graph (16,384 txns, deps on recent txns, hundreds of levels) through the windowed walk,
     the LDS walk and the persistent-wave walk: identical levels and order, equal to the oracle."""
@@ -161,8 +167,10 @@ def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
     from accord_amd.deps import levelise
     if walk == "waves":
         monkeypatch.setenv("ACC_LV_WAVES", "1")
-    if walk == "lds":
-        monkeypatch.setenv("ACC_LV_LDS", "1")
+    if walk.startswith("windowed"):
+        monkeypatch.setenv("ACC_LV_WIN", "1")
+    if walk == "windowed_poll1":
+        monkeypatch.setenv("ACC_LV_POLL", "1")
     rng = np.random.RandomState(55)
     n = 16384
     er = rng.permutation(n).astype(np.uint32)
@@ -177,7 +185,7 @@ def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
     off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
     dep = np.concatenate(deps).astype(np.uint32)
     lv, order, nl = levelise(ctx, off, dep, er)
-    assert ctx.stats().get("levelise.lds_tier") == {"windowed": 2, "lds": 1, "waves": 0}[walk]
+    assert ctx.stats().get("levelise.lds_tier") == {"windowed": 2, "windowed_poll1": 2, "lds": 1, "waves": 0}[walk]
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
