@@ -560,7 +560,7 @@ def mixed_keydeps_leg(bi, local, calls=3):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1000.0 / calls
         tm = c.timing()
-        top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:6]
+        top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:16]
         return {"ms_per_call": round(ms, 3), "range_key_queries": int(c.stats().get("keydeps.range_key_queries", 0)),
                 "dep_entries": int(v.total_edges), "kd_keys": int(v.total_keys),
                 "top_kernels_ms": {k: round(x[0] / calls, 3) for k, x in top}}

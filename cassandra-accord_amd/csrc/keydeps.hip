@@ -3620,18 +3620,30 @@ __global__ __launch_bounds__(BLOCK) void k_mx_seg_keys(uint32_t nseg, const uint
     if (s < nseg) seg_key[s] = key_code[perm[seg_start[s]]];
 }
 
-// work pieces: piece p = (range, first covered segment), at most MX_PIECE segments each
-__global__ __launch_bounds__(BLOCK) void k_mx_pieces(uint32_t R, const uint64_t *__restrict__ poff, uint32_t *__restrict__ prange)
+// work pieces: piece p = (range, first covered segment), at most MX_PIECE segments each. Its record (one thread per
+// range writes its pieces', so the count / emit passes read one record instead of a chain of dependent loads):
+// prec[2p] = (owner txn, first segment, covered-key index of that segment within the txn's keys, queries),
+// prec[2p + 1] = (T.executeAt rank S, T's TxnId rank, T.kind().witnesses() mask | p1 << 8, 0)
+__global__ __launch_bounds__(BLOCK) void k_mx_pieces(uint32_t R, const uint64_t *__restrict__ poff, const uint32_t *__restrict__ ra,
+                                                     const uint32_t *__restrict__ rowner, const uint64_t *__restrict__ rcnt,
+                                                     const uint64_t *__restrict__ r_off, const uint32_t *__restrict__ rng_off,
+                                                     const uint32_t *__restrict__ rank, uint32_t n, const uint64_t *__restrict__ tl,
+                                                     uint4 *__restrict__ prec)
 {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= R) return;
-    for (uint64_t p = poff[j]; p < poff[j + 1]; ++p) prange[p] = j;
+    const uint64_t p0 = poff[j], p1 = poff[j + 1];
+    if (p0 == p1) return;
+    const uint32_t t = rowner[j], a = ra[j], c = (uint32_t)rcnt[j];
+    const uint32_t kb = (uint32_t)(r_off[j] - r_off[rng_off[t]]);
+    const uint32_t S = rank[n + t], tr = rank[t];
+    const uint32_t wk = witnesses((uint32_t)(tl[t] >> 1) & 7u) | (S != tr ? 1u << 8 : 0u);
+    for (uint64_t p = p0; p < p1; ++p) {
+        const uint32_t k0 = (uint32_t)(p - p0) * MX_PIECE;
+        prec[2 * p] = make_uint4(t, a + k0, kb + k0, min(c - k0, MX_PIECE));
+        prec[2 * p + 1] = make_uint4(S, tr, wk, 0);
+    }
 }
-
-struct MxP {   // pieces
-    const uint32_t *prange, *ra, *rowner, *rng_off;
-    const uint64_t *poff, *rcnt, *r_off, *seg_key;
-};
 
 // 32 lanes per piece, one covered segment (one query) per lane
 __device__ __forceinline__ uint32_t mx_scan32(uint32_t x, uint32_t sub)   // inclusive, within the 32-lane half
@@ -3659,35 +3671,28 @@ __device__ __forceinline__ uint32_t mx_qcount(uint32_t q) { return (q & MX_ONE) 
 // appends spread over many addresses), list s holding at most dcap entries (its blocks' lanes); dlist null: every
 // query in place.
 constexpr uint32_t MX_DSLOTS = 1024;
-// prec[p] (for the emit pass, one load instead of a chain): owner txn, first segment, covered-key index of the
-// first segment within the txn's keys, queries
-__global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkView v, uint64_t *__restrict__ pe_cnt,
-                                                     uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack,
-                                                     uint32_t *__restrict__ dlist, uint32_t *__restrict__ dcnt, uint32_t dcap,
-                                                     uint4 *__restrict__ prec)
+__global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, const uint4 *__restrict__ prec, CfkView v,
+                                                     uint64_t *__restrict__ pe_cnt, uint32_t *__restrict__ pk_cnt,
+                                                     uint32_t *__restrict__ qc, uint32_t pack, uint32_t *__restrict__ dlist,
+                                                     uint32_t *__restrict__ dcnt, uint32_t dcap)
 {
     const uint64_t p = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 5;
     const uint32_t sub = threadIdx.x & 31u, g0 = lane_id() & 32u;
     uint32_t c = 0;
     bool dfr = false;
     if (p < NP) {
-        const uint32_t j = pc.prange[p], t = pc.rowner[j];
-        const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
-        const uint32_t nk = min((uint32_t)pc.rcnt[j] - k0, MX_PIECE);
-        if (sub == 0)
-            prec[p] = make_uint4(t, pc.ra[j] + k0, (uint32_t)(pc.r_off[j] - pc.r_off[pc.rng_off[t]] + k0), nk);
+        const uint4 pr = prec[2 * p], pq = prec[2 * p + 1];
         uint32_t f = 0;
-        if (sub < nk) {
-            const uint32_t seg = pc.ra[j] + k0 + sub;
+        if (sub < pr.w) {
+            const uint32_t seg = pr.y + sub;
             const uint32_t s0 = v.seg_start[seg], s1 = v.seg_start[seg + 1];
             if (dlist && s1 - s0 == 1) {
-                const uint32_t S = v.rank[v.n + t], trank = v.rank[t];
-                const uint32_t wk = witnesses((uint32_t)(v.tl[t] >> 1) & 7u);
+                const uint32_t S = pq.x, trank = pq.y, wk = pq.z & 0xFFu;
                 const uint32_t r = v.s_rank[s0], info = v.s_info[s0], st = info & 7u;
-                c = (r < S && ((wk >> (info >> 3)) & 1u) && st != 0 && st != 7 && !(S != trank && r == trank)) ? 1u : 0u;
+                c = (r < S && ((wk >> (info >> 3)) & 1u) && st != 0 && st != 7 && !((pq.z >> 8) && r == trank)) ? 1u : 0u;
                 f = r;
             } else if (dlist) dfr = true;
-            else c = run_query<false, true>(v, make_query_ts(v, t, seg), &f);
+            else c = run_query<false, true>(v, make_query_ts(v, pr.x, seg), &f);
         }
         qc[p * 32 + sub] = (pack && c == 1) ? (MX_ONE | f) : c;
     }
@@ -3707,7 +3712,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pcount(uint64_t NP, MxP pc, CfkVie
 
 // the deferred queries (segments of two or more entries): the exact-replay scan, one lane each; blockIdx.y = list,
 // a grid-stride loop over its device-side count
-__global__ __launch_bounds__(BLOCK) void k_mx_pdefer(MxP pc, CfkView v, const uint32_t *__restrict__ dlist,
+__global__ __launch_bounds__(BLOCK) void k_mx_pdefer(const uint4 *__restrict__ prec, CfkView v, const uint32_t *__restrict__ dlist,
                                                      const uint32_t *__restrict__ dcnt, uint32_t dcap, uint64_t *__restrict__ pe_cnt,
                                                      uint32_t *__restrict__ pk_cnt, uint32_t *__restrict__ qc, uint32_t pack)
 {
@@ -3715,10 +3720,9 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pdefer(MxP pc, CfkView v, const ui
     const uint32_t *lst = dlist + (size_t)blockIdx.y * dcap;
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nd; i += gridDim.x * BLOCK) {
         const uint32_t q = lst[i], p = q >> 5, sub = q & 31u;
-        const uint32_t j = pc.prange[p], t = pc.rowner[j];
-        const uint32_t k0 = (uint32_t)(p - pc.poff[j]) * MX_PIECE;
+        const uint4 pr = prec[2 * (uint64_t)p];
         uint32_t f = 0;
-        const uint32_t c = run_query<false, true>(v, make_query_ts(v, t, pc.ra[j] + k0 + sub), &f);
+        const uint32_t c = run_query<false, true>(v, make_query_ts(v, pr.x, pr.y + sub), &f);
         qc[q] = (pack && c == 1) ? (MX_ONE | f) : c;
         if (c) {
             atomicAdd((unsigned long long *)&pe_cnt[p], (unsigned long long)c);
@@ -3743,7 +3747,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_pemit(uint64_t NP, const uint4 *__
     uint4 pr = make_uint4(0, 0, 0, 0);
     bool act = false;
     if (p < NP) {
-        pr = prec[p];
+        pr = prec[2 * p];
         q = qc[p * 32 + sub];
         act = sub < pr.w;
         c = act ? mx_qcount(q) : 0u;
@@ -4143,18 +4147,16 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     ctx->stat("keydeps.range_key_queries", V);
 
     // ---- count and emit per piece with the exact-replay scan
-    uint32_t *prange = ctx->get<uint32_t>("mx_prange", NP + 1);
     uint64_t *pe_cnt = ctx->get<uint64_t>("mx_pe_cnt", NP + 1);
     uint64_t *pe_off = ctx->get<uint64_t>("mx_pe_off", NP + 2);
     uint32_t *pk_cnt = ctx->get<uint32_t>("mx_pk_cnt", NP + 1);
     uint32_t *pk_off = ctx->get<uint32_t>("mx_pk_off", NP + 2);
     uint64_t *etoff = ctx->get<uint64_t>("mx_etoff", (size_t)n + 1);
     uint32_t *ktoff = ctx->get<uint32_t>("mx_ktoff", (size_t)n + 1);
-    MxP pc{ prange, ra, rowner, rng_off, poff, rcnt, r_off, seg_key };
     uint64_t Ex = 0, Kx = 0;
     CfkView v{};
     uint32_t *qc = ctx->get<uint32_t>("mx_qc", NP * 32);
-    uint4 *prec = ctx->get<uint4>("mx_prec", NP + 1);
+    uint4 *prec = ctx->get<uint4>("mx_prec", 2 * NP + 2);
     if (NP) {
         const uint32_t pack = ks.rbits <= 31;
         const bool defer = NP * 32 < 0xFFFFFFFFull && !getenv("ACC_MX_NO_DEFER");   // tuning switch: every query in place
@@ -4166,16 +4168,18 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
             ks.v1 = true;
         }
         v = ks.v1view;
-        launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff, prange);
+        launch(ctx, "mx_pieces", k_mx_pieces, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, (const uint64_t *)poff,
+               (const uint32_t *)ra, (const uint32_t *)rowner, (const uint64_t *)rcnt, (const uint64_t *)r_off, rng_off, ks.rank,
+               n, ks.tl, prec);
         const unsigned gcount = grid_for(NP * 32, BLOCK);
         const uint32_t dcap = ((gcount + MX_DSLOTS - 1) / MX_DSLOTS) * BLOCK;   // lanes of the blocks of one list
         uint32_t *dlist = defer ? ctx->get<uint32_t>("mx_dlist", (size_t)MX_DSLOTS * dcap) : nullptr;
         uint32_t *dcnt = ctx->get<uint32_t>("mx_dcnt", MX_DSLOTS);
         if (defer) ACC_HIP(hipMemsetAsync(dcnt, 0, MX_DSLOTS * sizeof(uint32_t), st));
-        launch(ctx, "mx_pcount", k_mx_pcount, dim3(gcount), dim3(BLOCK), 0, NP, pc, v, pe_cnt, pk_cnt, qc, pack, dlist, dcnt, dcap,
-               prec);
+        launch(ctx, "mx_pcount", k_mx_pcount, dim3(gcount), dim3(BLOCK), 0, NP, (const uint4 *)prec, v, pe_cnt, pk_cnt, qc, pack,
+               dlist, dcnt, dcap);
         if (defer)
-            launch(ctx, "mx_pdefer", k_mx_pdefer, dim3(8, MX_DSLOTS), dim3(BLOCK), 0, pc, v, (const uint32_t *)dlist,
+            launch(ctx, "mx_pdefer", k_mx_pdefer, dim3(8, MX_DSLOTS), dim3(BLOCK), 0, (const uint4 *)prec, v, (const uint32_t *)dlist,
                    (const uint32_t *)dcnt, dcap, pe_cnt, pk_cnt, qc, pack);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, pe_cnt, pe_off, NP, true, pe_off + NP);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, pk_cnt, pk_off, NP, true, pk_off + NP);

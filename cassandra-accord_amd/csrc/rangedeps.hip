@@ -266,7 +266,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
                                                    const uint32_t *__restrict__ owner, const uint64_t *__restrict__ rs,
                                                    const uint64_t *__restrict__ re, const uint32_t *__restrict__ rowner,
                                                    const uint4 *__restrict__ tinfo, Runs plan, QRec *__restrict__ rec,
-                                                   uint64_t *__restrict__ qkey, uint32_t rbit)
+                                                   uint64_t *__restrict__ qkey, uint32_t rbit, int ibits)
 {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
     if (q >= P + R) return;
@@ -279,14 +279,18 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
     rec[q] = r;
     // range queries after the key queries (rbit < 64): a range query scans its whole span, so mixing the two in one
     // wave would leave the key lanes idle behind it
-    qkey[q] = pext_runs(r.lo, plan) | (q >= P && rbit < 64 ? 1ull << rbit : 0ull);
+    // ibits > 0: the query index packed under the key (a keys-only sort, 8 B per element moved instead of 12)
+    const uint64_t k = pext_runs(r.lo, plan) | (q >= P && rbit < 64 ? 1ull << rbit : 0ull);
+    qkey[q] = ibits ? (k << ibits) | q : k;
 }
 
 // sorted records, and per block of BLOCK sorted queries (the stabbing blocks) the largest high bound
 // Sorted position j of a range query lands at j + (Pp - P) (Pp = P rounded up to a block): no block mixes key and
 // range queries, so no block's window spans both sorted runs. The gap holds PAD records.
 constexpr uint32_t QPAD = 1u << 31;
+// perm: the sorted query indices, or (perm null) the low bits (imask) of the sorted packed keys pk
 __global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uint32_t Pp, const uint32_t *__restrict__ perm,
+                                                    const uint64_t *__restrict__ pk, uint64_t imask,
                                                     const QRec *__restrict__ rec, QRec *__restrict__ srec,
                                                     uint64_t *__restrict__ blo, uint64_t *__restrict__ bhi)
 {
@@ -299,7 +303,8 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uin
             r.flags = QPAD;
             srec[i] = r;
         } else {
-            const QRec r = rec[perm[i < P ? i : i - (Pp - P)]];
+            const uint32_t j = i < P ? i : i - (Pp - P);
+            const QRec r = rec[perm ? perm[j] : (uint32_t)(pk[j] & imask)];
             srec[i] = r; h = r.hi; l = r.lo;
         }
     }
@@ -689,9 +694,30 @@ __global__ __launch_bounds__(BLOCK) void k_rd_tier_hist(uint32_t n, const uint32
     if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
+// bitonic sort within lane groups of S (lane-aligned: the xor partners stay inside), ascending
+template <int S, class T>
+__device__ __forceinline__ T group_sort(T x, uint32_t lane)
+{
+#pragma unroll
+    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const T y = shfl_xor(x, (int)jj);
+            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;
+            const T mn = x < y ? x : y, mx = x < y ? y : x;
+            x = (lower == up) ? mn : mx;
+        }
+    }
+    return x;
+}
+
 // Groups of S lanes (S = 16, 32 or 64), one txn each: load, sort (range id, TxnId position), dedupe, TxnId union and
 // index, range groups; results to the scratch regions of the txn.
-template <int S>
+// NARROW (range ids and TxnId positions below 2^26): both sorts on 32-bit keys, half the cross-lane traffic of the
+// 64-bit network. The first sorts (range id << 6 | lane) and each lane then takes its key's entry; when some range id is
+// held by entries of different TxnIds (commands with identical ranges: rare) the (range id, lane) order may separate
+// duplicates or misorder TxnIds, so that wave sorts the 64-bit entries instead.
+template <int S, bool NARROW>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
 {
     __shared__ uint32_t slot[WAVES][64];
@@ -732,48 +758,38 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
             j = min(j, (uint32_t)S - 1);
             const uint64_t qoj = shfl_idx(qo, gb + (int)j);
             const uint32_t startj = (uint32_t)m + __shfl(incl - c, gb + (int)j, 64);
-#ifdef ACC_RD_PROBE_NOGATHER
-            if (sub >= m && sub < m + total) x = ((uint64_t)(qoj & 0xFFFFF) << 32) | (sub - startj);
-#else
             if (sub >= m && sub < m + total) x = o.ent[qoj + (sub - startj)];
-#endif
             m += total;
         }
     }
-    // sort within the group (groups are lane-aligned: the xor partners of k <= S stay inside)
-#ifndef ACC_RD_PROBE_NOSORT1
-#pragma unroll
-    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
-#pragma unroll
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint64_t y = shfl_xor(x, (int)jj);
-            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
-            const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
-            x = (lower == up) ? mn : mx;
-        }
+    if (NARROW) {
+        uint32_t k1 = (live && sub < m) ? ((uint32_t)(x >> 32) << 6) | sub : 0xFFFFFFFFu;
+        k1 = group_sort<S>(k1, lane);
+        const uint64_t xs = shfl_idx(x, (int)(grp * S + (k1 & 63u)));
+        x = k1 == 0xFFFFFFFFu ? ~0ull : xs;
+        const uint64_t pv = shfl_up(x, 1);
+        const bool mixed = live && sub > 0 && sub < m && (uint32_t)(pv >> 32) == (uint32_t)(x >> 32) && (uint32_t)pv != (uint32_t)x;
+        if (__ballot(mixed)) x = group_sort<S>(x, lane);   // wave-uniform; sorted groups stay as they are
+    } else {
+        x = group_sort<S>(x, lane);
     }
-#endif
     const uint64_t prev = shfl_up(x, 1);
     const bool valid = live && sub < m && (sub == 0 || x != prev);       // dedupe identical (range, txn)
     const uint64_t vb = __ballot(valid) & gmask;
     const uint32_t M = (uint32_t)__popcll(vb);
     const uint32_t pos = (uint32_t)__popcll(vb & lt);
     const uint32_t rid = (uint32_t)(x >> 32), tp = (uint32_t)x;
-    uint64_t y = valid ? (((uint64_t)tp << 8) | pos) : ~0ull;
-#ifndef ACC_RD_PROBE_NOSORT2
-#pragma unroll
-    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
-#pragma unroll
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint64_t z = shfl_xor(y, (int)jj);
-            const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
-            const uint64_t mn = y < z ? y : z, mx = y < z ? z : y;
-            y = (lower == up) ? mn : mx;
-        }
+    // (TxnId position, entry) sorted: the TxnId union and each entry's index
+    uint32_t ytp, ypos;
+    if (NARROW) {
+        const uint32_t y = group_sort<S>(valid ? (tp << 6) | pos : 0xFFFFFFFFu, lane);
+        ytp = y >> 6; ypos = y & 63u;
+    } else {
+        const uint64_t y = group_sort<S>(valid ? (((uint64_t)tp << 8) | pos) : ~0ull, lane);
+        ytp = (uint32_t)(y >> 8); ypos = (uint32_t)y & 0xFFu;
     }
-#endif
-    const uint64_t yprev = shfl_up(y, 1);
-    const bool ynew = live && sub < M && (sub == 0 || (y >> 8) != (yprev >> 8));
+    const uint32_t yprev = __shfl_up(ytp, 1, 64);
+    const bool ynew = live && sub < M && (sub == 0 || ytp != yprev);
     const uint64_t nb = __ballot(ynew) & gmask;
     const uint32_t U = (uint32_t)__popcll(nb);
     const bool yin = live && sub < M;
@@ -782,12 +798,12 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint64_t rb = __ballot(rnew) & gmask;
     const uint32_t Rd = (uint32_t)__popcll(rb);
     const uint32_t g0 = grp * S;
-    if (yin) slot[wave][g0 + (uint32_t)(y & 0xFFu)] = uidx;
+    if (yin) slot[wave][g0 + ypos] = uidx;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (!live || m == 0) return;
     uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
-    if (ynew) sd[uidx] = dep_of(o, (uint32_t)(y >> 8));
+    if (ynew) sd[uidx] = dep_of(o, ytp);
     const uint32_t g = (uint32_t)__popcll(rb & lt);
     if (valid) {
         sa[Rd + pos] = slot[wave][g0 + pos];
@@ -1140,17 +1156,22 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     const Runs q_plan = make_runs(hm[2]);
     QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = nullptr;
     uint64_t *qkey = ctx->get<uint64_t>("rd_qkey", Q);
+    const int qbits = q_plan.bits < 64 ? q_plan.bits + 1 : 64;
+    const int ibits = qbits + bits_for(Q) <= 64 && Q < OS_VAL ? std::max(1, bits_for(Q)) : 0;
     launch(ctx, "rd_qrec", k_rd_qrec, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
            (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey,
-           (uint32_t)q_plan.bits);
-    Sorted qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, q_plan.bits < 64 ? q_plan.bits + 1 : 64);
+           (uint32_t)q_plan.bits, ibits);
+    Sorted qs{ nullptr, nullptr };
+    const uint64_t *qpk = nullptr;
+    if (ibits) qpk = radix_sort_keys(ctx, "rs_rd_q", qkey, Q, ibits, qbits);
+    else qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, qbits);
     const uint32_t Pp = q_plan.bits < 64 && P && R ? (uint32_t)((P + BLOCK - 1) / BLOCK * BLOCK) : (uint32_t)P;
     const uint32_t Qp = Q + (Pp - (uint32_t)P);
     const uint32_t nsb = (uint32_t)grid_for(Qp, BLOCK);
     uint64_t *bhi = ctx->get<uint64_t>("rd_bhi", nsb), *blo = ctx->get<uint64_t>("rd_blo", nsb);
     srec = ctx->get<QRec>("rd_qrec_sorted", Qp);
-    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Qp, (uint32_t)P, Pp, (const uint32_t *)qs.vals,
-           (const QRec *)rec, srec, blo, bhi);
+    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Qp, (uint32_t)P, Pp, (const uint32_t *)qs.vals, qpk,
+           ibits ? (1ull << ibits) - 1 : 0ull, (const QRec *)rec, srec, blo, bhi);
     View v{};
     v.Q = Qp; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
     v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
@@ -1213,18 +1234,27 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     o.s_rid = ctx->get<uint32_t>("rd_s_rid", E);
     o.s_dep = ctx->get<uint32_t>("rd_s_dep", E);
     const uint32_t *tl_sorted = ts.vals;
+    // 32-bit sort keys in the lane-group tiers: range ids (< NE) and TxnId positions (< n) within 26 bits
+    const bool narrow = NE < (1u << 26) && n < (1u << 26) && !getenv("ACC_RD_WIDE");   // tuning switch: 64-bit sorts
+    ctx->stat("rangedeps.narrow_sorts", narrow ? 1 : 0);
     // tiers own disjoint txns (disjoint scratch): LDS workgroup tiers on side stream 1, 16-lane groups on side
     // stream 0, waves on the main stream, all concurrently
     ctx->fork(2);
     if (hh[1]) {
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[1];
-        launch(ctx, "rd_build_s16", k_rd_build_seg<16>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+        if (narrow)
+            launch(ctx, "rd_build_s16", k_rd_build_seg<16, true>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+        else
+            launch(ctx, "rd_build_s16", k_rd_build_seg<16, false>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
     }
     if (hh[11]) {
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[11];
-        launch(ctx, "rd_build_s32", k_rd_build_seg<32>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
+        if (narrow)
+            launch(ctx, "rd_build_s32", k_rd_build_seg<32, true>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
+        else
+            launch(ctx, "rd_build_s32", k_rd_build_seg<32, false>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
     }
     uint64_t nblk = 0;
     ctx->launch_stream = ctx->aux[1];
@@ -1241,7 +1271,10 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     ctx->launch_stream = nullptr;
     if (hh[2]) {
         o.list = tl_sorted + toff[2];
-        launch(ctx, "rd_build_s64", k_rd_build_seg<64>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+        if (narrow)
+            launch(ctx, "rd_build_s64", k_rd_build_seg<64, true>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+        else
+            launch(ctx, "rd_build_s64", k_rd_build_seg<64, false>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
     }
     ctx->join(2);
     const uint32_t nglb = hh[10];
