@@ -363,13 +363,15 @@ __global__ __launch_bounds__(BLOCK) void k_seg_flags(size_t P, const uint64_t *_
 
 // Gather per-position CFK columns; fill seg_start; classify committed (C) / uncommitted (U).
 // per-txn record for the CFK gather: one 16-B random read per pair instead of four
+// .w = key_off[t] (the CFK gather turns (owner, slot) into the pair index from the same 16-B read)
 __global__ __launch_bounds__(BLOCK) void k_txn_info(uint32_t n, const uint32_t *__restrict__ rank, const uint8_t *__restrict__ status,
-                                                    const uint64_t *__restrict__ tl, uint4 *__restrict__ tinfo)
+                                                    const uint64_t *__restrict__ tl, const uint32_t *__restrict__ key_off,
+                                                    uint4 *__restrict__ tinfo)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= n) return;
     uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
-    tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), 0u);
+    tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), key_off[t]);
 }
 
 // per-pair copy of its txn's record, written in pair order (owner[] is monotone, so both reads stream): the CFK
@@ -758,9 +760,13 @@ __device__ __forceinline__ void v2_codes4(size_t P, size_t base, const uint32_t 
 // segment starts, optionally pair_pos) and the per-tile counts of the class lists (the multi-scan's reduce step) over
 // the same 1024-position tile that k_v2_apply scans.
 // pown (mode 4): each position's owner txn, its record read from tinfo (16 B per txn) instead of ptinfo (per pair)
-__global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
-                                                       const uint32_t *__restrict__ pown, const uint4 *__restrict__ tinfo,
-                                                       const uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ s_rank,
+// sp (mode 4, sb >= 0): the sorted packed pair keys (key << 32 | owner << sb | slot) are unpacked here: the segment
+// flags and the pair index perm = key_off[owner] + slot are written, key_off[owner] coming with the owner's record
+// (tinfo[t].w), so each pair costs one random 16-B read. Otherwise perm / seg_flag are inputs and the record is
+// ptinfo[perm].
+__global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, uint32_t *__restrict__ perm, const uint4 *__restrict__ ptinfo,
+                                                       const uint64_t *__restrict__ sp, int sb, const uint4 *__restrict__ tinfo,
+                                                       uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ s_rank,
                                                        uint32_t *__restrict__ s_exec, uint8_t *__restrict__ s_info,
                                                        uint32_t *__restrict__ pair_pos, uint32_t *__restrict__ tile_sums,
                                                        uint32_t ntiles)
@@ -771,17 +777,38 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, const uint32_t 
     if (base < P) {
         uint32_t j[V2_ITEMS], fl[V2_ITEMS];
         uint4 ti[V2_ITEMS];
+        if (sp) {
+            uint64_t x[V2_ITEMS];
+            const uint64_t xp = base > 0 ? sp[base - 1] : 0;
 #pragma unroll
-        for (int i = 0; i < V2_ITEMS; ++i) {
-            const bool in = base + i < P;
-            j[i] = in ? (pown ? pown[base + i] : perm[base + i]) : 0u;
-            fl[i] = in ? seg_flag[base + i] : 0u;
-        }
+            for (int i = 0; i < V2_ITEMS; ++i) x[i] = base + i < P ? sp[base + i] : 0;
+            const uint32_t smask = (1u << sb) - 1u;
 #pragma unroll
-        for (int i = 0; i < V2_ITEMS; ++i) ti[i] = base + i < P ? (pown ? tinfo[j[i]] : ptinfo[j[i]]) : make_uint4(0u, 0u, 0u, 0u);
-        if (pown && pair_pos) {
+            for (int i = 0; i < V2_ITEMS; ++i) {
+                const bool in = base + i < P;
+                const uint64_t prev = i == 0 ? xp : x[i - 1];
+                fl[i] = in && (base + i == 0 || (x[i] >> 32) != (prev >> 32)) ? 1u : 0u;
+                ti[i] = in ? tinfo[(uint32_t)x[i] >> sb] : make_uint4(0u, 0u, 0u, 0u);
+            }
 #pragma unroll
-            for (int i = 0; i < V2_ITEMS; ++i) j[i] = base + i < P ? perm[base + i] : 0u;
+            for (int i = 0; i < V2_ITEMS; ++i) j[i] = ti[i].w + ((uint32_t)x[i] & smask);
+            if (base + V2_ITEMS <= P) {
+                *reinterpret_cast<uint4 *>(seg_flag + base) = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+                *reinterpret_cast<uint4 *>(perm + base) = make_uint4(j[0], j[1], j[2], j[3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < V2_ITEMS; ++i)
+                    if (base + i < P) { seg_flag[base + i] = fl[i]; perm[base + i] = j[i]; }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < V2_ITEMS; ++i) {
+                const bool in = base + i < P;
+                j[i] = in ? perm[base + i] : 0u;
+                fl[i] = in ? seg_flag[base + i] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < V2_ITEMS; ++i) ti[i] = base + i < P ? ptinfo[j[i]] : make_uint4(0u, 0u, 0u, 0u);
         }
         uint32_t inf = 0;
 #pragma unroll
@@ -2416,8 +2443,11 @@ __device__ unsigned long long *g_st_prof;
 #endif
 
 // EntT: u32 (rank << 4 | key) when ranks fit 28 bits, else u64
+#ifndef ACC_ST_WAVES
+#define ACC_ST_WAVES 24   // resident waves per CU the stream pass is compiled for (32: a 64-VGPR budget that spills)
+#endif
 template <class EntT, int NT>
-__global__ __launch_bounds__(NT, 2048 / NT) void k_v3_stream(V3Stream s)
+__global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stream s)
 {
     constexpr int TT = NT / ST_G;   // txns per tile
 #ifdef ACC_PHASE_PROF
@@ -3116,21 +3146,22 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     int key_shift = 0;
     uint32_t *seg_flag = ctx->get<uint32_t>("seg_flag", P);
     bool flags_done = false;
-    uint32_t *pown = nullptr;
+    const uint64_t *sp_m4 = nullptr;   // mode 4: the sorted packed keys, unpacked by the CFK gather
     pp.sb = std::max(1, bits_for(hg[6]));   // bounds the key slot within a txn (hg[6] = OR of the key counts)
     if (batch_sorted && pp.rk.bits <= 32 && !getenv("ACC_PAIR_UNPACKED")) {
         // pair index order is already TxnId order within every key: a stable keys-only sort of (key << 32 | pair index),
         // 8 B per element; the segment flags pass unpacks the permutation. Mode 4 packs (owner, slot) instead of the
-        // pair index, so the segment flags pass also hands the CFK gather each position's txn
+        // pair index and the CFK gather unpacks it (one random read of the owner's record per pair, which carries
+        // key_off[owner] for the pair index)
         const bool m4 = bits_for((uint64_t)n - 1) + pp.sb <= 32 && !getenv("ACC_PAIR_NO_OWNER");
         pp.mode = m4 ? 4 : 3;
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
                (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
         const uint64_t *sp = radix_sort_keys(ctx, "rs_pair", pkey, P, 32, pp.rk.bits);
-        uint32_t *perm = ctx->get<uint32_t>("pair_perm", P);
-        if (m4) pown = ctx->get<uint32_t>("pair_own", P);
-        launch(ctx, "seg_flags", k_seg_flags_packed, dim3(gP), dim3(BLOCK), 0, P, sp, seg_flag, perm, m4 ? pp.sb : -1, key_off,
-               pown);
+        uint32_t *perm = ctx->get<uint32_t>("pair_perm", P + V2_ITEMS);
+        if (m4) sp_m4 = sp;
+        else launch(ctx, "seg_flags", k_seg_flags_packed, dim3(gP), dim3(BLOCK), 0, P, sp, seg_flag, perm, -1, key_off,
+                    (uint32_t *)nullptr);
         ps = { nullptr, perm };
         flags_done = true;
     } else if (batch_sorted) {
@@ -3163,7 +3194,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
     uint4 *tinfo = ctx->get<uint4>("tinfo", n);
-    uint4 *ptinfo = pown ? nullptr : ctx->get<uint4>("pair_tinfo", P);
+    uint4 *ptinfo = sp_m4 ? nullptr : ctx->get<uint4>("pair_tinfo", P);
     bool have_pair_pos = ks != nullptr;
     auto need_pair_pos = [&]() {
         if (have_pair_pos) return;
@@ -3187,11 +3218,12 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
-        launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl, tinfo);
-        if (!pown)
+        launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl,
+               key_off, tinfo);
+        if (!sp_m4)
             launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
-        launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, (const uint4 *)ptinfo,
-               (const uint32_t *)pown, (const uint4 *)tinfo, (const uint32_t *)seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
+        launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, ps.vals, (const uint4 *)ptinfo, sp_m4, pp.sb,
+               (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
         launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
@@ -3548,14 +3580,16 @@ __device__ __forceinline__ uint32_t mx_shift(const uint64_t *seg_key, uint32_t n
     return sb > tbits ? sb - tbits : 0u;
 }
 
-// keys per bucket (bcnt zeroed); an exclusive scan of them is bstart
+// bend[b] = 1 + the last segment of bucket b (written by that segment; 0 for empty buckets, zeroed before): an
+// exclusive max-scan of bend is bstart (keys are sorted, so the segments of buckets <= b are a prefix)
 __global__ __launch_bounds__(BLOCK) void k_mx_buckets(uint32_t nseg, uint32_t tbits, const uint64_t *__restrict__ seg_key,
-                                                      uint32_t *__restrict__ bcnt)
+                                                      uint32_t *__restrict__ bend)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= nseg) return;
     const uint32_t sh = mx_shift(seg_key, nseg, tbits);
-    atomicAdd(&bcnt[(seg_key[i] - seg_key[0]) >> sh], 1u);
+    const uint64_t k0 = seg_key[0], b = (seg_key[i] - k0) >> sh;
+    if (i + 1 == nseg || ((seg_key[i + 1] - k0) >> sh) != b) bend[b] = i + 1;
 }
 
 // first segment m in [0, nseg) with seg_key[m] > x (upper) / >= x (!upper)
@@ -4110,11 +4144,11 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     const size_t nbk = (size_t)1 << tbits;
     uint32_t *bstart = ctx->get<uint32_t>("mx_bstart", nbk + 1);
     if (nseg) {
-        uint32_t *bcnt = ctx->get<uint32_t>("mx_bcnt", nbk);
-        ACC_HIP(hipMemsetAsync(bcnt, 0, nbk * sizeof(uint32_t), st));
+        uint32_t *bend = ctx->get<uint32_t>("mx_bend", nbk);
+        ACC_HIP(hipMemsetAsync(bend, 0, nbk * sizeof(uint32_t), st));
         launch(ctx, "mx_buckets", k_mx_buckets, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, tbits,
-               (const uint64_t *)seg_key, bcnt);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, bcnt, bstart, nbk, true, bstart + nbk);
+               (const uint64_t *)seg_key, bend);
+        scan<uint32_t, OpMax<uint32_t>>(ctx, bend, bstart, nbk, true, bstart + nbk);
     }
     uint32_t *ra = ctx->get<uint32_t>("mx_ra", R + 1);
     uint32_t *rowner = ctx->get<uint32_t>("mx_rowner", R + 1);
