@@ -79,12 +79,13 @@ def profile_summary(config, variant=""):
     return None, None
 
 
-def roofline(step_bytes, step, steps, ms_per_step, config, variant=""):
+def roofline(step_bytes, step, steps, ms_per_step, config, variant="", profiled=True):
     """HBM roofline of the whole step (the pipeline is one launch chain per step): achieved = the step's algorithmic
     bytes (each input read once, each output written once) / the timed ms_per_step; `traffic` = the
     HBM bytes per step of the committed rocprof PMC summary of the same config (FETCH_SIZE x2 + WRITE_SIZE, the upper
     bound; traffic_raw = FETCH_SIZE x1 + WRITE_SIZE, the lower bound: tools/calib_fetch.hip calibration). The dominant
-    kernel is reported beside it with its HIP-event average and the committed rocprof average for the same kernel."""
+    kernel is reported beside it with its HIP-event average and the committed rocprof average for the same kernel.
+    profiled=False (a scaled or store-sharded workload, not the one the committed profile measured): no traffic."""
     timing, dsteps = step.diag, DIAG_STEPS
     if not timing:   # ACC_BENCH_NOTIME probe: no per-kernel events were recorded
         timing, dsteps = {"unrecorded": (ms_per_step * steps, steps)}, steps
@@ -97,7 +98,7 @@ def roofline(step_bytes, step, steps, ms_per_step, config, variant=""):
     dom_total, dom_launches = (step.live or {}).get(dom_name, (timing[dom_name][0] * steps / dsteps,
                                                                 timing[dom_name][1] * steps // dsteps))
     achieved = step_bytes / (ms_per_step / 1000.0) / 1e9
-    prof, prof_path = profile_summary(config, variant)
+    prof, prof_path = profile_summary(config, variant) if profiled else (None, None)
     traffic = traffic_raw = dom_prof_ms = None
     if prof:
         traffic = int(prof.get("hbm_bytes_per_step", 0)) or None
@@ -342,7 +343,8 @@ def run_config2(args, world, rank, local, dev):
             "parallelism": f"keyspace shards x{world} (independent CommandStores)",
         },
         "dep_edges_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
-        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config, variant),
+        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config, variant,
+                             profiled=args.scale == 1.0),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         # config 3: the O(prefix) scans of the 5M-txn hot key make each sampled query cost ~10 ms: sparser sample
@@ -491,7 +493,7 @@ def run_config2_sharded(args, world, rank, local, dev):
         "exchange": {"bytes_sent_total": int(tot[1].item()), "bytes_sent_max_rank": int(mx[1].item()),
                      "path": exchange,
                      "setup_backend": dist.get_backend() + (" (RCCL over xGMI)" if dist.get_backend() == "nccl" else "")},
-        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config),
+        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config, profiled=False),
     }
     return ctx, timing, elapsed, result
 
@@ -535,7 +537,8 @@ def run_config4(args, world, rank, local, dev):
             "parallelism": f"keyspace shards x{world} (independent CommandStores)",
         },
         "dep_entries_per_s": round(int(view.total_edges) * world * args.steps / elapsed, 1),
-        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config),
+        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config,
+                             profiled=args.scale == 1.0),
     }
     if os.environ.get("ACC_BENCH_MIXED", "1") != "0":
         result["keydeps_mixed"] = mixed_keydeps_leg(bi, local)
@@ -706,7 +709,7 @@ def run_config5(args, world, rank, local, dev):
             "parallelism": f"independent coordinators x{world}",
         },
         "roofline": roofline(merge_bytes(m, view, n_txn, int(view.total_vals)), step, args.steps,
-                             elapsed * 1000.0 / args.steps, args.config),
+                             elapsed * 1000.0 / args.steps, args.config, profiled=args.scale == 1.0),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = merge_cpu_baseline(m, exec_rank, n_in)
