@@ -338,6 +338,13 @@ __device__ __forceinline__ uint64_t pext_runs(uint64_t w, const Runs &r)
 
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = BLOCK * RS_ITEMS;
+constexpr int RS_ITEMS_S = 4;                      // one-sweep tiles of mid-size sorts
+constexpr int RS_TILE_S = BLOCK * RS_ITEMS_S;
+inline size_t rs_small_n()                         // ACC_RS_SMALL_N: tuning switch (0: never)
+{
+    static const size_t v = getenv("ACC_RS_SMALL_N") ? (size_t)atoll(getenv("ACC_RS_SMALL_N")) : (size_t)256 << 10;
+    return v;
+}
 
 static __global__ __launch_bounds__(BLOCK) void k_rs_hist(const uint64_t *__restrict__ keys, size_t n, int shift,
                                                    uint32_t *__restrict__ hist, uint32_t ntiles)
@@ -510,15 +517,17 @@ __device__ __forceinline__ void os_store(uint32_t *p, uint32_t w) { __hip_atomic
 __device__ __forceinline__ uint32_t os_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // KO: keys only (no value arrays; e.g. (key << 32 | index) packed into the key): half the LDS, 8 B per element moved
-template <bool KO>
+// ITEMS: keys per thread (tile = BLOCK x ITEMS); 4 for small sorts (< rs_small_n() elements: four times the tiles, so a
+// pass of a few tiles is not bound by their serial rank / scatter work; config 5: 0.063 -> 0.037 ms), 16 otherwise
+template <bool KO, int ITEMS>
 static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, size_t n,
                                                        int shift, const uint32_t *__restrict__ dtotal,
                                                        uint32_t *__restrict__ status, uint32_t *__restrict__ ticket,
                                                        int iota_vals)
 {
-    __shared__ uint64_t sk[RS_TILE];
-    __shared__ uint32_t sv[KO ? 1 : RS_TILE];
+    __shared__ uint64_t sk[(BLOCK * ITEMS)];
+    __shared__ uint32_t sv[KO ? 1 : (BLOCK * ITEMS)];
     __shared__ uint32_t cnt[WAVES][256];
     __shared__ uint32_t wpre[WAVES][256];
     __shared__ uint32_t run[256], lbase[256], gbase[256];
@@ -532,12 +541,12 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__
     for (int w = 0; w < WAVES; ++w) cnt[w][tid] = 0;
     __syncthreads();
     const uint32_t b = s_b;
-    const size_t base = (size_t)b * RS_TILE;
+    const size_t base = (size_t)b * (BLOCK * ITEMS);
     // the tile in registers
-    uint64_t key[RS_ITEMS];
-    uint32_t val[RS_ITEMS], lr[RS_ITEMS], pk[RS_ITEMS];
+    uint64_t key[ITEMS];
+    uint32_t val[ITEMS], lr[ITEMS], pk[ITEMS];
 #pragma unroll
-    for (int k = 0; k < RS_ITEMS; ++k) {
+    for (int k = 0; k < ITEMS; ++k) {
         const size_t e = base + (size_t)k * BLOCK + tid;
         const bool valid = e < n;
         key[k] = valid ? kin[e] : 0;
@@ -546,7 +555,7 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__
     // the tile's digit counts first (one LDS add per distinct digit of a wave), published at once so later tiles'
     // look-backs find them early; each element's peer rank in its wave is kept for the stable ranking below
 #pragma unroll
-    for (int k = 0; k < RS_ITEMS; ++k) {
+    for (int k = 0; k < ITEMS; ++k) {
         const bool valid = base + (size_t)k * BLOCK + tid < n;
         const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
         uint64_t peers = __ballot(valid);
@@ -570,7 +579,7 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__
     __syncthreads();
     // stable rank of each element among the tile's elements of its digit: order (k, wave, lane)
 #pragma unroll
-    for (int k = 0; k < RS_ITEMS; ++k) {
+    for (int k = 0; k < ITEMS; ++k) {
         const bool valid = base + (size_t)k * BLOCK + tid < n;
         const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
         const uint32_t rank = pk[k] & 0xFFFFu;
@@ -590,7 +599,7 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__
         lr[k] = wpre[wave][d] + rank;
     }
 #pragma unroll
-    for (int k = 0; k < RS_ITEMS; ++k) {
+    for (int k = 0; k < ITEMS; ++k) {
         const size_t e = base + (size_t)k * BLOCK + tid;
         if (e < n) {
             const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
@@ -605,7 +614,10 @@ static __global__ __launch_bounds__(BLOCK) void k_rs_onesweep(const uint64_t *__
     const uint32_t dbase = block_exclusive(dtotal[tid], OpAdd<uint32_t>(), red, all);
     uint32_t pre = 0;
     if (b > 0) {
-        constexpr int LB = 8;
+#ifndef ACC_OS_LB
+#define ACC_OS_LB 8
+#endif
+        constexpr int LB = ACC_OS_LB;
         for (int64_t j = (int64_t)b - 1;; j -= LB) {
             uint32_t w[LB];
 #pragma unroll
@@ -668,9 +680,10 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         else launch(ctx, "iota", k_iota, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, v[0], n);
         return { k[0], v[0] };
     }
-    uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     static const bool legacy = getenv("ACC_RS_LEGACY") != nullptr;   // tuning switch: three launches per pass
     if (n < (size_t)OS_VAL && passes <= OS_MAXP && !legacy) {
+        const bool small = n < rs_small_n();
+        const uint32_t ntiles = (uint32_t)((n + (small ? RS_TILE_S : RS_TILE) - 1) / (small ? RS_TILE_S : RS_TILE));
         // one-sweep: [passes x 256 digit totals][passes tickets][passes x ntiles x 256 status words], zeroed by one fill
         char nsw[48];
         snprintf(nsw, sizeof nsw, "%s_os", tag);
@@ -684,15 +697,21 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         const uint32_t *vin = vals;
         int cur = 0;
         for (int p = 0; p < passes; ++p) {
-            launch(ctx, ts, k_rs_onesweep<false>, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, 8 * p,
-                   (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256, tickets + p,
-                   (p == 0 && !vals) ? 1 : 0);
+            if (small)
+                launch(ctx, ts, k_rs_onesweep<false, RS_ITEMS_S>, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, 8 * p,
+                       (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256, tickets + p,
+                       (p == 0 && !vals) ? 1 : 0);
+            else
+                launch(ctx, ts, k_rs_onesweep<false, RS_ITEMS>, dim3(ntiles), dim3(BLOCK), 0, kin, vin, k[cur], v[cur], n, 8 * p,
+                       (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256, tickets + p,
+                       (p == 0 && !vals) ? 1 : 0);
             kin = k[cur];
             vin = v[cur];
             cur ^= 1;
         }
         return { (uint64_t *)kin, (uint32_t *)vin };
     }
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     uint32_t *hist = ctx->get<uint32_t>(nh, (size_t)256 * ntiles);
     char nt[48];
     snprintf(nt, sizeof nt, "%s_dtot", tag);
@@ -729,7 +748,8 @@ static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uin
         if (n) ACC_HIP(hipMemcpyAsync(k[0], keys, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->cur()));
         return k[0];
     }
-    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const bool small = n < rs_small_n();
+    const uint32_t ntiles = (uint32_t)((n + (small ? RS_TILE_S : RS_TILE) - 1) / (small ? RS_TILE_S : RS_TILE));
     const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;
     uint32_t *osb = ctx->get<uint32_t>(nsw, words);
     ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
@@ -738,9 +758,14 @@ static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uin
     const uint64_t *kin = keys;
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
-        launch(ctx, ts, k_rs_onesweep<true>, dim3(ntiles), dim3(BLOCK), 0, kin, (const uint32_t *)nullptr, k[cur],
-               (uint32_t *)nullptr, n, lo + 8 * p, (const uint32_t *)(ghist + (size_t)p * 256), status + (size_t)p * ntiles * 256,
-               tickets + p, 0);
+        if (small)
+            launch(ctx, ts, k_rs_onesweep<true, RS_ITEMS_S>, dim3(ntiles), dim3(BLOCK), 0, kin, (const uint32_t *)nullptr, k[cur],
+                   (uint32_t *)nullptr, n, lo + 8 * p, (const uint32_t *)(ghist + (size_t)p * 256),
+                   status + (size_t)p * ntiles * 256, tickets + p, 0);
+        else
+            launch(ctx, ts, k_rs_onesweep<true, RS_ITEMS>, dim3(ntiles), dim3(BLOCK), 0, kin, (const uint32_t *)nullptr, k[cur],
+                   (uint32_t *)nullptr, n, lo + 8 * p, (const uint32_t *)(ghist + (size_t)p * 256),
+                   status + (size_t)p * ntiles * 256, tickets + p, 0);
         kin = k[cur];
         cur ^= 1;
     }
