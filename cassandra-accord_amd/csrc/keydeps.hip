@@ -62,6 +62,7 @@ enum : uint32_t {
     ERR_KEYS_UNSORTED = 1u << 3,
     ERR_DUP_TXNID = 1u << 4,
     ERR_KEY_OFF = 1u << 5,
+    ERR_KEY_TOTAL = 1u << 6,   // key_off[n] != n_pairs
 };
 
 // g[0..2] ts word masks, g[3] key mask, g[4] error bits, g[5] batch-not-in-TxnId-order flag.
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(BLOCK) void k_prep_txn(uint32_t n, size_t P, const 
     uint32_t differs = 0;
     const uint64_t r0 = tm[0], r1 = ts_w1(tl[0]), r2 = ts_w2(tn[0]);
     const uint64_t kref = P ? key_code[0] : 0;
+    if (blockIdx.x == 0 && tid == 0 && key_off[n] != P) errs |= ERR_KEY_TOTAL;
     for (uint32_t t0 = blockIdx.x * BLOCK; t0 < n; t0 += gridDim.x * BLOCK) {
         const uint32_t t = t0 + tid;
         const uint32_t tcnt = min((uint32_t)BLOCK, n - t0);
@@ -364,12 +366,14 @@ __global__ __launch_bounds__(BLOCK) void k_seg_flags(size_t P, const uint64_t *_
 // Gather per-position CFK columns; fill seg_start; classify committed (C) / uncommitted (U).
 // per-txn record for the CFK gather: one 16-B random read per pair instead of four
 // .w = key_off[t] (the CFK gather turns (owner, slot) into the pair index from the same 16-B read)
+// also zeroes the count pass's big-txn flags (no memset launch)
 __global__ __launch_bounds__(BLOCK) void k_txn_info(uint32_t n, const uint32_t *__restrict__ rank, const uint8_t *__restrict__ status,
                                                     const uint64_t *__restrict__ tl, const uint32_t *__restrict__ key_off,
-                                                    uint4 *__restrict__ tinfo)
+                                                    uint4 *__restrict__ tinfo, uint32_t *__restrict__ bigflag)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= n) return;
+    if (bigflag) bigflag[t] = 0;
     uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
     tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), key_off[t]);
 }
@@ -839,9 +843,13 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, uint32_t *__res
     }
 }
 
-// list bases: list l occupies [base[l], base[l] + total[l]) of the class-list arrays
-__global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__restrict__ bases)
+// list bases: list l occupies [base[l], base[l] + total[l]) of the class-list arrays; also zeroes the count / mark
+// passes' accumulators (z: nz words; no memset launches)
+__global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__restrict__ bases, uint64_t *__restrict__ z0,
+                           uint32_t nz0, uint64_t *__restrict__ z1, uint32_t nz1)
 {
+    for (uint32_t i = threadIdx.x; i < nz0; i += blockDim.x) z0[i] = 0;
+    for (uint32_t i = threadIdx.x; i < nz1; i += blockDim.x) z1[i] = 0;
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         uint32_t b = 0;
         for (int l = 0; l < NLIST; ++l) { bases[l] = b; b += totals[l]; }
@@ -2776,6 +2784,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
 
 static void check_errors(uint64_t errs)
 {
+    if (errs & ERR_KEY_TOTAL) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
     if (errs & ERR_BAD_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal (> INVALID_OR_TRUNCATED)");
     if (errs & ERR_BAD_KIND) fail(ACC_E_ARG, "Kind.ofOrdinal: invalid kind ordinal in TxnId flags");
     if (errs & ERR_KEY_OFF) fail(ACC_E_ARG, "key_off must be non-decreasing");
@@ -3030,13 +3039,10 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
     // the last key_off entry must equal P
     uint64_t hg[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
     {
-        uint32_t last = 0;
+        // (key_off[n] == P is checked by the kernel: ERR_KEY_TOTAL)
         uint64_t *hs = ctx->pinned + acc_ctx::PINNED_SLOTS;
         ACC_HIP(hipMemcpyAsync(hs, gslots, 8 * PREP_SLOTS * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 8, key_off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
-        memcpy(&last, ctx->pinned + 8, sizeof(uint32_t));
-        if (last != P) fail(ACC_E_ARG, "key_off[n_txn] must equal n_pairs");
         for (uint32_t r = 0; r < PREP_SLOTS; ++r) {
             for (int w = 0; w < 7; ++w) hg[w] |= hs[8 * r + w];
             hg[7] += hs[8 * r + 7];
@@ -3216,16 +3222,21 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_kind = ctx->get<uint8_t>("v2_bc_kind", P);
     cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
+    // the count / mark passes' accumulators, zeroed by the column kernels below (k_txn_info, k_v2_bases)
+    uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
+    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
+    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N);
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
         launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl,
-               key_off, tinfo);
+               key_off, tinfo, bigflag);
         if (!sp_m4)
             launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
         launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, ps.vals, (const uint4 *)ptinfo, sp_m4, pp.sb,
                (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
-        launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases);
+        launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases, tot, 3u, gstat,
+               (uint32_t)GSTAT_N);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
                (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
                rbits, cols, seg_incl, seg_start);
@@ -3296,14 +3307,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     vv.irec32 = reinterpret_cast<const uint32_t *>(ro.irec);
     vv.rec = ro.rec;
 
-    uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
     uint32_t *bpos = ctx->get<uint32_t>("v3_bpos", n);
     uint64_t *blk_e = ctx->get<uint64_t>("v3_blk_e", gP);
-    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
-    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N);
-    ACC_HIP(hipMemsetAsync(bigflag, 0, (size_t)n * 4, st));
-    ACC_HIP(hipMemsetAsync(tot, 0, 3 * sizeof(uint64_t), st));
-    ACC_HIP(hipMemsetAsync(gstat, 0, GSTAT_N * sizeof(uint64_t), st));
     uint32_t *psz = ctx->get<uint32_t>("v2_psz", P);   // per pair of a run-record txn: its entry count (k_v3_mark)
     launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
     const char *rc_env = getenv("ACC_ST_RAW");
@@ -3929,7 +3934,76 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_seg(const uint32_t *__restri
     if (live && sub == 0) u.ucnt[t] = (uint32_t)__popcll(bal);
 }
 
-// wave per listed txn, 64 < E <= MX_MID_E: one wave's LDS bitonic
+// R values per lane sorted across the wave (element r * 64 + lane), ascending: partners 64 or more apart are registers
+// of the same lane, the others lanes (shuffles)
+template <int R>
+__device__ __forceinline__ void wave_reg_sort(uint64_t (&v)[R])
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 64u * R; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            if (jj >= 64) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int r2 = r ^ (int)(jj >> 6);
+                    if (r2 > r) {
+                        const bool up = ((((uint32_t)r << 6) | lane) & k) == 0;
+                        const uint64_t a = v[r], b = v[r2];
+                        if ((a > b) == up) { v[r] = b; v[r2] = a; }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint64_t y = shfl_xor(v[r], (int)jj);
+                    const bool up = ((((uint32_t)r << 6) | lane) & k) == 0, lower = (lane & jj) == 0;
+                    const uint64_t mn = v[r] < y ? v[r] : y, mx = v[r] < y ? y : v[r];
+                    v[r] = (lower == up) ? mn : mx;
+                }
+            }
+        }
+    }
+}
+
+// a txn's union over E <= 64 R entries in registers: sort (rank << 32 | entry), distinct ranks -> indices
+template <int R>
+__device__ __forceinline__ void mx_union_regs(const MxU &u, uint32_t t, uint64_t e0, uint32_t E)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint64_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = ((uint32_t)r << 6) | lane;
+        v[r] = i < E ? (((uint64_t)u.deps[e0 + i] << 32) | i) : ~0ull;
+    }
+    wave_reg_sort<R>(v);
+    uint32_t base = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t x = v[r];
+        uint64_t prev = shfl_up(x, 1);
+        if (r > 0) {
+            const uint64_t pl = shfl_idx(v[r - 1], 63);
+            if (lane == 0) prev = pl;
+        }
+        const uint32_t i = ((uint32_t)r << 6) | lane;
+        const bool in = i < E;
+        const bool nw = in && (i == 0 || (prev >> 32) != (x >> 32));
+        const uint64_t bal = __ballot(nw);
+        const uint32_t idx = base + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
+        if (in) {
+            u.idx_of_e[e0 + (uint32_t)x] = idx;
+            if (nw) u.dep_scr[e0 + idx] = u.txn_of_rank[(uint32_t)(x >> 32)];
+        }
+        base += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) u.ucnt[t] = base;
+}
+
+// wave per listed txn, 64 < E <= MX_MID_E: registers up to 256 entries, one wave's LDS bitonic beyond
 __global__ __launch_bounds__(BLOCK) void k_mx_union_mid(const uint32_t *__restrict__ list, const uint64_t *__restrict__ gst, MxU u)
 {
     __shared__ uint64_t sbuf[WAVES][MX_MID_E];
@@ -3939,6 +4013,8 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_mid(const uint32_t *__restri
     uint64_t *buf = sbuf[w];
     const uint64_t e0 = u.etoff[t];
     const uint32_t E = (uint32_t)(u.etoff[t + 1] - e0);
+    if (E <= 128) { mx_union_regs<2>(u, t, e0, E); return; }   // wave-uniform
+    if (E <= 256) { mx_union_regs<4>(u, t, e0, E); return; }
     uint32_t n2 = 128;
     while (n2 < E) n2 <<= 1;
     for (uint32_t q = lane; q < n2; q += 64) buf[q] = q < E ? (((uint64_t)u.deps[e0 + q] << 32) | q) : ~0ull;

@@ -139,6 +139,19 @@ def test_union_tiers(ctx):
     assert_same(g, oracle.keydeps_mixed(rb), "union tiers")
 
 
+def test_union_register_tiers(ctx):
+    """Range txns of 65-128 and 129-256 entries (the register-sort union, 2 and 4 entries per lane) and 16-64 (lane
+    groups), over key txns of three keys each so a range txn meets most of its TxnIds on several keys (dedupe)."""
+    import oracle
+    txns = [dict(kind=W.WRITE, keys=[30 * i + 5, 30 * i + 15, 30 * i + 25]) for i in range(400)]
+    for w in (20, 40, 100, 170, 250):   # covered keys ~ 3 w / ... : entries from ~20 to ~250
+        txns += [dict(kind=W.WRITE, ranges=[(0, 10 * w)]), dict(kind=W.READ, ranges=[(3000, 3000 + 10 * w)])]
+    rb = rd_cases.build(txns)
+    g = ctx.calculate_partial_key_deps_mixed(rb)
+    assert ctx.stats()["keydeps.range_mid_txns"] >= 4
+    assert_same(g, oracle.keydeps_mixed(rb), "register unions")
+
+
 @pytest.mark.parametrize("end_inclusive", [1, 0])
 def test_partial_deps_fused(ctx, end_inclusive):
     """acc_partial_deps_batch: both PartialDeps halves in one call over one dictionary pass, identical to the two
