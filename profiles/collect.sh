@@ -14,6 +14,7 @@ out=$root/gpurun_out/prof_${tag}_c${cfg}${variant}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 export ACC_BENCH_MIXED=0   # profile the config-4 RangeDeps step alone (the mixed-batch KeyDeps leg runs after it)
+export ACC_BENCH_CFK=0     # likewise the config-2 CommandsForKey-update leg
 bench="$root/bench.py --config $cfg --steps 5 --warmup 2 --no-cpu $*"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
     python3 $bench > "$out/trace.log" 2>&1 || { echo "trace pass failed: $?"; tail -5 "$out/trace.log"; exit 1; }

@@ -1,13 +1,15 @@
 """Summarise a profiles/collect.sh run into a committed per-round file.
 
-    python profiles/summarize.py gpurun_out/prof_r01_c2 profiles/r01_config2 --steps 7
+    python profiles/summarize.py gpurun_out/prof_r04_c2 profiles/r04_config2 [--steps 9]
 
 Writes <prefix>_kernel_stats.csv (the rocprofv3 --stats table, accord kernels first), and <prefix>_summary.json:
 per-kernel average duration, per-step device time and per-step HBM traffic from the FETCH_SIZE / WRITE_SIZE
 passes. FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B) for the upper bound and kept
 as is for the lower bound (`*_raw`; random gathers are not the calibrated pattern, see tools/calib_fetch.hip); KB units.
-`steps` = warmup + timed steps of the profiled bench command (every pipeline kernel of a step runs once per step
-or a fixed number of times, so totals / steps are per-step figures).
+`steps` = every step the profiled bench command runs: 2 warmup + 5 timed + bench.DIAG_STEPS (2) untimed diagnostic steps
+= 9 (every pipeline kernel of a step runs once per step or a fixed number of times, so totals / steps are per-step
+figures). Round-3 and earlier summaries divided by 7 (the diagnostic steps were left out), overstating their per-step
+figures by 9/7.
 """
 import csv
 import json
@@ -46,7 +48,7 @@ def load_counters(path, counter):
 
 def main():
     src, prefix = sys.argv[1], sys.argv[2]
-    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 7
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 9
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     acc = [r for r in rows if is_acc(r["Name"])]
     with open(prefix + "_kernel_stats.csv", "w", newline="") as f:

@@ -275,6 +275,16 @@ def test_errors(ctx):
     local.txn_lsb[3] = (local.txn_lsb[3] & ~np.uint64(0xE)) | np.uint64(5 << 1)
     with pytest.raises(IllegalStateException):
         ctx.calculate_partial_deps(local)
+    # key_off[n_txn] != n_pairs (checked on the device by the prep pass, ACC_E_ARG)
+    from accord_amd import _lib as L
+    a = {k: np.ascontiguousarray(v) for k, v in b.arrays().items()}
+    kc = np.concatenate([a["key_code"], a["key_code"][-1:]])   # n_pairs + 1 codes (kept alive for the call)
+    bi = L.BatchIn(b.n_txn, L.ACC_MEM_HOST, b.n_pairs + 1,
+                   L.TsCols(a["txn_msb"].ctypes.data, a["txn_lsb"].ctypes.data, a["txn_node"].ctypes.data),
+                   L.TsCols(a["exe_msb"].ctypes.data, a["exe_lsb"].ctypes.data, a["exe_node"].ctypes.data),
+                   a["status"].ctypes.data, a["key_off"].ctypes.data, kc.ctypes.data)
+    with pytest.raises(IllegalArgumentException, match="n_pairs"):
+        ctx.keydeps_batch_raw(bi)
     # the context stays usable after errors
     g = ctx.calculate_partial_deps(b)
     assert g.arena_off[-1] == len(g.arena)
