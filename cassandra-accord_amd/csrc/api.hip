@@ -1,6 +1,8 @@
 // api.hip — the extern "C" surface of include/accord_amd.h: context lifecycle, error text, result
 // copy-out with two-call sizing, and kernel timing read-out.
 #include "dict.hpp"
+#include <exception>
+#include <thread>
 
 namespace acc {
 void keydeps_batch(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view *view);
@@ -33,11 +35,27 @@ void cfk_free(acc_cfk *cfk);
 acc_cfk *cfk_new(int device);
 }  // namespace acc
 
+namespace {
+// Internal entry points behind acc_create / acc_destroy: the library never calls its own exported names (an
+// acc_create exported by another loaded library, e.g. libgomp's OpenACC acc_create(void *, size_t), would
+// interpose on a PLT call from inside this library).
+int ctx_create(int device, const acc_opts *opts, acc_ctx **out_ctx);
+void ctx_destroy(acc_ctx *ctx);
+}  // namespace
+
 extern "C" {
 
 const char *acc_version(void) { return "accord_amd 0.1 (gfx950)"; }
 
-int acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
+int acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx) { return ctx_create(device, opts, out_ctx); }
+
+void acc_destroy(acc_ctx *ctx) { ctx_destroy(ctx); }
+
+}  // extern "C"
+
+namespace {
+
+int ctx_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
 {
     if (!out_ctx) return ACC_E_ARG;
     *out_ctx = nullptr;
@@ -54,14 +72,14 @@ int acc_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
         ACC_HIP(hipHostMalloc((void **)&ctx->pinned, acc_ctx::PINNED_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     });
     if (rc != ACC_OK) {
-        acc_destroy(ctx);
+        ctx_destroy(ctx);
         return rc;
     }
     *out_ctx = ctx;
     return ACC_OK;
 }
 
-void acc_destroy(acc_ctx *ctx)
+void ctx_destroy(acc_ctx *ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
@@ -78,8 +96,14 @@ void acc_destroy(acc_ctx *ctx)
     if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    acc_ctx *child = ctx->child;
     delete ctx;
+    ctx_destroy(child);
 }
+
+}  // namespace
+
+extern "C" {
 
 const char *acc_last_error(const acc_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
 
@@ -144,9 +168,51 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         if (!key_view || !range_view) acc::fail(ACC_E_ARG, "null argument");
+        if (!ctx->child && !getenv("ACC_PD_SERIAL")) {   // tuning switch: both halves in order on this context
+            acc_opts o{};
+            o.flags = ctx->flags;
+            const int rc = ctx_create(ctx->device, &o, &ctx->child);
+            if (rc != ACC_OK) acc::fail(rc, "cannot create the RangeDeps half's context");
+        }
+        acc_ctx *const child = getenv("ACC_PD_SERIAL") ? nullptr : ctx->child;
+        // the RangeDeps half starts on the child context (own stream, own host thread) as soon as the KeyDeps half's
+        // dictionary is enqueued: its stream waits for that point of this context's stream, and it reads the
+        // dictionary in place (not written again by the KeyDeps half)
         acc::SharedDict sd;
+        std::thread th;
+        int rrc = ACC_OK;
+        hipEvent_t ev = nullptr;
+        struct Join {
+            std::thread &t;
+            hipEvent_t &e;
+            ~Join() { if (t.joinable()) t.join(); if (e) (void)hipEventDestroy(e); }
+        } join{ th, ev };
+        if (child) {
+            child->flags = ctx->flags;
+            sd.ready = [&](const acc::SharedDict &d) {
+                ACC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                ACC_HIP(hipEventRecord(ev, ctx->stream));
+                th = std::thread([&rrc, child, in, range_view, ev, d] {
+                    rrc = acc_guard(child, [&] {
+                        ACC_HIP(hipSetDevice(child->device));
+                        ACC_HIP(hipStreamWaitEvent(child->stream, ev, 0));
+                        acc::rangedeps_batch(child, in, range_view, &d);
+                        child->sync();
+                    });
+                });
+            };
+        }
         acc::keydeps_mixed(ctx, in, key_view, &sd);
-        acc::rangedeps_batch(ctx, in, range_view, &sd);
+        if (th.joinable()) {
+            th.join();
+            if (rrc != ACC_OK) acc::fail(rrc, child->last_error.c_str());
+            ctx->rd_view = child->rd_view;   // child buffers, valid until the next acc_partial_deps_batch on ctx
+            ctx->rd_valid = child->rd_valid;
+            ctx->rd_ent_hint = child->rd_ent_hint;
+            for (const auto &kv : child->stats) ctx->stat(kv.first.c_str(), kv.second);
+        } else {
+            acc::rangedeps_batch(ctx, in, range_view, &sd);   // no key pairs (no dictionary to share), or serial
+        }
         ctx->kd_valid = true;   // both views stay readable (distinct buffers)
     });
 }

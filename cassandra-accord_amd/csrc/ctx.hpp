@@ -61,8 +61,17 @@ struct acc_ctx {
     // the other buffer, so no memset launch precedes a scan (acc::scan, prims.hpp)
     size_t scan_cap = 0, scan_dirty[2] = {0, 0};
     int scan_par = 0;
+    // one-sweep radix status words per sort tag, double buffered the same way (acc::radix_sort, prims.hpp)
+    struct OsState {
+        size_t cap = 0, dirty[2] = {0, 0};
+        int par = 0;
+    };
+    std::unordered_map<std::string, OsState> os_state;
     uint32_t flags = 0;
     std::string last_error;
+    // a second context on the same device (own stream, buffers, pinned staging), created on first use: the RangeDeps
+    // half of acc_partial_deps_batch runs on it from a second host thread, concurrently with the KeyDeps half
+    acc_ctx *child = nullptr;
     std::unordered_map<std::string, acc::Buf> bufs;
     // buffers replaced by a larger allocation while kernels may still read them: freed at the next sync
     std::vector<void *> graveyard;

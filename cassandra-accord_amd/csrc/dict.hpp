@@ -3,6 +3,7 @@
 #pragma once
 
 #include "prims.hpp"
+#include <functional>
 
 namespace acc {
 
@@ -30,6 +31,8 @@ DenseRank dense_rank(acc_ctx *ctx, const char *tag, size_t n, int nw, const uint
                      const uint64_t *xor_mask, bool want_first);
 
 // key_off/key_code: the key-domain part (P pairs); owner[P] receives the txn of every pair; g[8] scratch words.
+// the prep / dictionary flag words: g[0..7], then the prep pass's slotted partials (64 slots x 8 words), zeroed by one fill
+constexpr size_t PREP_G_WORDS = 8 + 64 * 8;
 void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, const uint64_t *tl, const int32_t *tn,
                      const uint64_t *em, const uint64_t *el, const int32_t *en, const uint8_t *status,
                      const uint32_t *key_off, const uint64_t *key_code, uint32_t *owner, uint64_t *g, Dictionary &out,
@@ -64,6 +67,9 @@ struct SharedDict {
     bool valid = false;
     Dictionary dict;
     const uint32_t *owner = nullptr;   // [P] txn of every key pair
+    // called by keydeps_mixed once the dictionary is final (its kernels enqueued on the context stream): starts the
+    // RangeDeps half concurrently with the rest of the KeyDeps half
+    std::function<void(const SharedDict &)> ready;
 };
 
 }  // namespace acc

@@ -423,6 +423,12 @@ __global__ __launch_bounds__(BLOCK) void k_low32(size_t P, const uint64_t *__res
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (p < P) out[p] = (uint32_t)in[p];
 }
+__global__ __launch_bounds__(BLOCK) void k_low32x2(size_t P, const uint64_t *__restrict__ a, uint32_t *__restrict__ a32,
+                                                   const uint64_t *__restrict__ b, uint32_t *__restrict__ b32)
+{
+    size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p < P) { a32[p] = (uint32_t)a[p]; b32[p] = (uint32_t)b[p]; }
+}
 
 // Committed entries -> (seg << ebits | execRank) composite for the stable (seg, executeAt) sort; pads
 // (all ones in `bits`) fill [NC, P) so the sort runs on the host-known size P.
@@ -846,10 +852,12 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, uint32_t *__res
 // list bases: list l occupies [base[l], base[l] + total[l]) of the class-list arrays; also zeroes the count / mark
 // passes' accumulators (z: nz words; no memset launches)
 __global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__restrict__ bases, uint64_t *__restrict__ z0,
-                           uint32_t nz0, uint64_t *__restrict__ z1, uint32_t nz1)
+                           uint32_t nz0, uint64_t *__restrict__ z1, uint32_t nz1, const uint64_t *__restrict__ g,
+                           uint64_t *__restrict__ stage)
 {
     for (uint32_t i = threadIdx.x; i < nz0; i += blockDim.x) z0[i] = 0;
     for (uint32_t i = threadIdx.x; i < nz1; i += blockDim.x) z1[i] = 0;
+    if (threadIdx.x < 3) stage[threadIdx.x] = g[4 + threadIdx.x];   // the dictionary's error / tie words beside the totals
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         uint32_t b = 0;
         for (int l = 0; l < NLIST; ++l) { bases[l] = b; b += totals[l]; }
@@ -879,13 +887,15 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
                                                     const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ seg_flag,
                                                     const uint32_t *__restrict__ tile_pref, const uint32_t *__restrict__ bases,
                                                     uint32_t ntiles, int rbits, V2Cols o, uint32_t *__restrict__ seg_incl,
-                                                    uint32_t *__restrict__ seg_start)
+                                                    uint32_t *__restrict__ seg_start, const uint32_t *__restrict__ perm,
+                                                    const uint64_t *__restrict__ key_code, uint64_t *__restrict__ seg_key)
 {
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t code[V2_ITEMS] = { 7u, 7u, 7u, 7u }, rk[V2_ITEMS] = {};
     uint32_t c[NCNT] = {};
     uint32_t fl[V2_ITEMS] = {};
+    uint64_t kc[V2_ITEMS] = {};
     if (base < P) {
         v2_codes4(P, base, s_rank, s_exec, s_info, code, rk);
 #pragma unroll
@@ -897,6 +907,17 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
             if ((code[i] >> 4) & 1u) c[7] = (uint32_t)(base + i) + 1;
             fl[i] = base + i < P ? seg_flag[base + i] : 0u;
             c[8] += fl[i] != 0;
+        }
+        if (seg_key) {   // segment starts' key codes: the gathers issued here, their latency hidden by the block scans
+            uint32_t pi[V2_ITEMS] = {};
+            if (base + V2_ITEMS <= P) {
+                const uint4 pv = *reinterpret_cast<const uint4 *>(perm + base);
+                pi[0] = pv.x; pi[1] = pv.y; pi[2] = pv.z; pi[3] = pv.w;
+            } else {
+                for (int i = 0; i < V2_ITEMS; ++i) if (base + i < P) pi[i] = perm[base + i];
+            }
+#pragma unroll
+            for (int i = 0; i < V2_ITEMS; ++i) if (fl[i]) kc[i] = key_code[pi[i]];
         }
     }
     uint32_t run[NCNT];
@@ -946,7 +967,10 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     for (int i = 0; i < V2_ITEMS; ++i) {   // segment numbers (seg_incl = inclusive count of segment starts) and starts
         const size_t p = base + i;
         if (p >= P) break;
-        if (fl[i]) seg_start[run[8]] = (uint32_t)p;
+        if (fl[i]) {
+            seg_start[run[8]] = (uint32_t)p;
+            if (seg_key) seg_key[run[8]] = kc[i];   // the segment's key code (range-domain queries)
+        }
         run[8] += fl[i] != 0;
         segi[i] = run[8];
         if (p == P - 1) seg_start[run[8]] = (uint32_t)P;
@@ -991,7 +1015,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
 // bumped committed sorted by (segment, executeAt): exec column and nearest-Write index (+1) per entry
 __global__ __launch_bounds__(BLOCK) void k_v2_bcs_cols(uint32_t nbc, const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ svals,
                                                        const uint8_t *__restrict__ bc_kind, uint64_t rmask,
-                                                       uint32_t *__restrict__ bcs_exec, uint32_t *__restrict__ lastw_in)
+                                                       uint32_t *__restrict__ bcs_exec, uint64_t *__restrict__ lastw_in)
 {
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= nbc) return;
@@ -2251,14 +2275,14 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
     }
 }
 
+
+// per big txn (one wave each, list order): dependency entries E from the per-pair counts of the mark pass
 __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t *__restrict__ bigflag,
                                                       const uint32_t *__restrict__ bpos, uint32_t *__restrict__ blist)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t < n && bigflag[t]) blist[bpos[t]] = t;
 }
-
-// per big txn (one wave each, list order): dependency entries E from the per-pair counts of the mark pass
 __global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_t *__restrict__ blist,
                                                     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ psz,
                                                     uint64_t *__restrict__ lE)
@@ -2718,12 +2742,16 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
                                                        const uint64_t *__restrict__ vdep_off, const uint32_t *__restrict__ dep_scr,
                                                        const uint32_t *__restrict__ dep_big,
                                                        const uint32_t *__restrict__ tmap, const uint32_t *__restrict__ n_dev,
-                                                       uint32_t *__restrict__ dep_txn)
+                                                       uint32_t *__restrict__ dep_txn, const uint64_t *__restrict__ u_all,
+                                                       uint64_t *__restrict__ totals)
 {
     __shared__ uint64_t uo[BLOCK + 1];
     __shared__ uint64_t src[BLOCK];
     __shared__ uint32_t s_t[2];
     const uint32_t tid = threadIdx.x;
+    if (tid == 0 && blockIdx.x == gridDim.x - 1) {   // the batch totals beside the status words: one host copy
+        totals[0] = arena_off[n]; totals[1] = kd_off[n]; totals[2] = u_all[n];
+    }
     if (tmap) n = *n_dev;
     const uint64_t total = u_off[n];
     const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
@@ -2813,6 +2841,7 @@ struct KdState {
     bool have_dict = false;
     Dictionary dict;
     bool sparse = false;              // the batch has many txns without keys (a mixed batch's range txns)
+    const uint64_t *seg_key = nullptr;   // per segment its key code (written by k_v2_apply)
     bool v1 = false;                  // the exact-replay columns below are built
     CfkView v1view{};
 };
@@ -3030,9 +3059,9 @@ void prep_dictionary(acc_ctx *ctx, uint32_t n, size_t P, const uint64_t *tm, con
     hipStream_t st = ctx->stream;
     // ---- 1. prep
     static_assert(8 * PREP_SLOTS <= acc_ctx::PINNED_WORDS - acc_ctx::PINNED_SLOTS, "slot rows fit the pinned area");
-    uint64_t *gslots = ctx->get<uint64_t>("prep_slots", 8 * PREP_SLOTS);
-    ACC_HIP(hipMemsetAsync(g, 0, 8 * sizeof(uint64_t), st));
-    ACC_HIP(hipMemsetAsync(gslots, 0, 8 * PREP_SLOTS * sizeof(uint64_t), st));
+    static_assert(PREP_G_WORDS == 8 + 8 * PREP_SLOTS, "g and the prep slots share one buffer");
+    uint64_t *gslots = g + 8;   // g has PREP_G_WORDS words
+    ACC_HIP(hipMemsetAsync(g, 0, PREP_G_WORDS * sizeof(uint64_t), st));
     uint32_t *bflag = ctx->get<uint32_t>("bflag", n);
     launch(ctx, "prep_txn", k_prep_txn, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, P, tm, tl, tn, em, el, en, status,
            key_off, key_code, owner, bflag, gslots);
@@ -3131,7 +3160,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     const uint64_t *key_code = stage_in(ctx, "in_key_code", in->key_code, P, in->mem);
 
     // ---- 1-2. prep + dictionary
-    uint64_t *g = ctx->get<uint64_t>("g", 8);
+    uint64_t *g = ctx->get<uint64_t>("g", PREP_G_WORDS);
     uint32_t *owner = ctx->get<uint32_t>("owner", P);
     Dictionary dict;
     // the sorted-batch dictionary's tie check is read at the CFK sync below (one host sync fewer)
@@ -3195,6 +3224,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "seg_flags", k_seg_flags, dim3(gP), dim3(BLOCK), 0, P, (const uint64_t *)ps.keys, key_shift, seg_flag);
 
     uint32_t *seg_start = ctx->get<uint32_t>("seg_start", P + 1);
+    uint64_t *seg_key_buf = ks ? ctx->get<uint64_t>("seg_key", P + 1) : nullptr;   // per segment its key code
     uint32_t *s_rank = ctx->get<uint32_t>("s_rank", P + V2_ITEMS);   // padded for the 16-B column loads
     uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P + V2_ITEMS);
     uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
@@ -3225,7 +3255,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     // the count / mark passes' accumulators, zeroed by the column kernels below (k_txn_info, k_v2_bases)
     uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
     uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
-    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N);
+    uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N + 3);   // + the batch totals (k_v3_ucompact)
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
         launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl,
@@ -3236,14 +3266,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
         launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases, tot, 3u, gstat,
-               (uint32_t)GSTAT_N);
+               (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
                (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
-               rbits, cols, seg_incl, seg_start);
+               rbits, cols, seg_incl, seg_start, (const uint32_t *)ps.vals, key_code, seg_key_buf);
     };
     build_columns();
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, g + 4, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));   // + g[4..6] (k_v2_bases)
     ctx->sync();
     if (dict.ties_pending && ctx->pinned[6]) {
         // an executeAt equals another timestamp: the sorted-batch ranks are not dense ranks; the general dictionary,
@@ -3251,8 +3280,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         check_errors(ctx->pinned[4]);
         redo_general_dictionary(ctx, n, tm, tl, tn, em, el, en, g, dict);
         build_columns();
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, g + 4, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
     }
     dict.ties_pending = false;
@@ -3268,7 +3296,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ks->cfk = true; ks->n = n; ks->P = P; ks->rbits = rbits; ks->rank = rank; ks->txn_of_rank = txn_of_rank;
         ks->key_off = key_off; ks->owner = owner; ks->seg_incl = seg_incl; ks->seg_start = seg_start;
         ks->s_rank = s_rank; ks->s_exec = s_exec; ks->pair_pos = pair_pos; ks->perm = ps.vals; ks->s_info = s_info;
-        ks->tl = tl; ks->key_code = key_code; ks->g = g;
+        ks->tl = tl; ks->key_code = key_code; ks->g = g; ks->seg_key = seg_key_buf;
         ks->tm = tm; ks->tn = tn; ks->em = em; ks->el = el; ks->en = en;
     }
     if (cfk_only) return;
@@ -3282,15 +3310,20 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     if (segbits + rbits > 64) fail(ACC_E_ARG, "batch too large for the (segment, executeAt) composite key");
     Sorted bcs = radix_sort(ctx, "rs_bc", cols.bc_key, nullptr, nbc, segbits + rbits);
     uint32_t *bcs_exec = ctx->get<uint32_t>("v2_bcs_exec", nbc);
-    uint32_t *bcs_lw_in = ctx->get<uint32_t>("v2_bcs_lw_in", nbc);
+    uint64_t *bcs_lw_in = ctx->get<uint64_t>("v2_bcs_lw_in64", nbc), *bcs_lw64 = ctx->get<uint64_t>("v2_bcs_lastw64", nbc);
     uint32_t *bcs_lastw = ctx->get<uint32_t>("v2_bcs_lastw", nbc);
     launch(ctx, "v2_bcs_cols", k_v2_bcs_cols, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, nbc, (const uint64_t *)bcs.keys,
            (const uint32_t *)bcs.vals, (const uint8_t *)cols.bc_kind, (uint64_t)((1ull << rbits) - 1), bcs_exec, bcs_lw_in);
-    scan<uint32_t, OpMax<uint32_t>>(ctx, bcs_lw_in, bcs_lastw, nbc, false);
     uint64_t *bc_pm64 = ctx->get<uint64_t>("v2_bc_pm64", nbc);
     uint32_t *bc_pm = ctx->get<uint32_t>("v2_bc_pm", nbc);
-    scan<uint64_t, OpMax<uint64_t>>(ctx, cols.bc_pm_in, bc_pm64, nbc, false);
-    launch(ctx, "low32", k_low32, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, (size_t)nbc, (const uint64_t *)bc_pm64, bc_pm);
+    {   // nearest-Write index and the segmented executeAt maximum: two prefix maxima in one launch, then both to u32
+        const uint64_t *si[2] = { bcs_lw_in, cols.bc_pm_in };
+        uint64_t *so[2] = { bcs_lw64, bc_pm64 };
+        const size_t sn[2] = { nbc, nbc };
+        scan_multi<uint64_t, OpMax<uint64_t>>(ctx, 2, si, so, sn, false, (uint64_t *const *)nullptr);
+    }
+    launch(ctx, "low32", k_low32x2, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, (size_t)nbc, (const uint64_t *)bcs_lw64,
+           bcs_lastw, (const uint64_t *)bc_pm64, bc_pm);
 
     V2View vv;
     vv.perm = ps.vals; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
@@ -3320,12 +3353,17 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
     launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.irec32, (const uint4 *)rec, psz, raw_cap,
            e_cap, bigflag, szA, szK, tot + 2);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, szA, arena_off, n, true, arena_off + n);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, szK, kd_off, n, true, kd_off + n);
+    uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
+    {   // arena / key offsets and the count pass's per-block entry totals: one launch
+        const uint64_t *si[3] = { szA, szK, blk_e };
+        uint64_t *so[3] = { arena_off, kd_off, blk_pre }, *stot[3] = { arena_off + n, kd_off + n, tot };
+        const size_t sn[3] = { n, n, gP };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 3, si, so, sn, true, stot);
+    }
+    // the big-txn list in txn order (k_v3_bigfill's per-txn ranges abut: a big txn writes its end where the next
+    // txn's first pair starts, equal values when the next txn is big too)
     uint32_t *nbig_dev = reinterpret_cast<uint32_t *>(tot + 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, bigflag, bpos, n, true, nbig_dev);
-    uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, blk_e, blk_pre, gP, true, tot);
     uint32_t *blist = ctx->get<uint32_t>("v3_blist", n);
     launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bigflag,
            (const uint32_t *)bpos, blist);
@@ -3481,11 +3519,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n,
                uo, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
                (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr,
-               tmap, ne_cnt, dep_txn);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, GSTAT_N * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N, arena_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N + 1, kd_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + GSTAT_N + 2, u_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+               tmap, ne_cnt, dep_txn, (const uint64_t *)u_off, gstat + GSTAT_N);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, (GSTAT_N + 3) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
     };
     finish();
@@ -3651,13 +3686,6 @@ __global__ __launch_bounds__(BLOCK) void k_mx_ranges(uint32_t n, const uint64_t 
     if (e) atomicOr((unsigned long long *)errs, (unsigned long long)e);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_mx_seg_keys(uint32_t nseg, const uint32_t *__restrict__ seg_start,
-                                                       const uint32_t *__restrict__ perm, const uint64_t *__restrict__ key_code,
-                                                       uint64_t *__restrict__ seg_key)
-{
-    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    if (s < nseg) seg_key[s] = key_code[perm[seg_start[s]]];
-}
 
 // work pieces: piece p = (range, first covered segment), at most MX_PIECE segments each. Its record (one thread per
 // range writes its pieces', so the count / emit passes read one record instead of a chain of dependent loads):
@@ -4104,6 +4132,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, const u
                                                     uint64_t *__restrict__ u_cnt)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t == n) { a_cnt[n] = 0; kd_cnt[n] = 0; u_cnt[n] = 0; }   // the exclusive scans over n + 1 end in the totals
     if (t >= n) return;
     const uint64_t ex = etoff[t + 1] - etoff[t];
     const uint64_t kd = ktoff[t + 1] - ktoff[t];
@@ -4189,7 +4218,10 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     ks.sparse = R > 0;
     keydeps_core(ctx, &kin, &kv, &ks);
     ctx->kd_valid = false;
-    if (shared) { shared->valid = ks.have_dict; shared->dict = ks.dict; shared->owner = ks.owner; }
+    if (shared) {
+        shared->valid = ks.have_dict; shared->dict = ks.dict; shared->owner = ks.owner;
+        if (shared->ready && shared->valid) shared->ready(*shared);
+    }
     if (n == 0) {
         kv.kd_key = ctx->get<uint64_t>("mx_kd_key", 1);
         *view = kv;
@@ -4211,10 +4243,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         ctx->sync();
         nseg = (uint32_t)(ctx->pinned[0] & 0xFFFFFFFFu);
     }
-    uint64_t *seg_key = ctx->get<uint64_t>("mx_seg_key", (size_t)nseg + 1);
-    if (nseg)
-        launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
-               ks.key_code, seg_key);
+    const uint64_t *seg_key = ks.cfk ? ks.seg_key : ctx->get<uint64_t>("mx_seg_key", 1);   // written by k_v2_apply
     // bucket directory: about one key per bucket
     const uint32_t tbits = nseg ? (uint32_t)std::min(26, std::max(0, bits_for(nseg) - 1)) : 0u;
     const size_t nbk = (size_t)1 << tbits;
@@ -4237,8 +4266,10 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     launch(ctx, "mx_ranges", k_mx_ranges, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, key_off, rng_off, rs, re,
            in->end_inclusive, (const uint64_t *)seg_key, nseg, (const uint32_t *)bstart, tbits, ra, rowner, rcnt, rpieces, errs);
     if (R) {
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, rcnt, r_off, R, true, r_off + R);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, rpieces, poff, R, true, poff + R);
+        const uint64_t *si[2] = { rcnt, rpieces };
+        uint64_t *so[2] = { r_off, poff }, *stot[2] = { r_off + R, poff + R };
+        const size_t sn[2] = { R, R };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 2, si, so, sn, true, stot);
     } else {
         ACC_HIP(hipMemsetAsync(r_off, 0, 8, st));
         ACC_HIP(hipMemsetAsync(poff, 0, 8, st));
@@ -4370,21 +4401,23 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
 
     // ---- combined offsets and the combined layout
     MxKv mkv{ kv.arena_off, kv.kd_off, kv.u_off, kv.arena, kv.key_idx, kv.dep_txn };
-    uint64_t *a_cnt = ctx->get<uint64_t>("mx_a_cnt", n);
-    uint64_t *kd_cnt = ctx->get<uint64_t>("mx_kd_cnt", n);
-    uint64_t *u_cnt = ctx->get<uint64_t>("mx_u_cnt", n);
-    launch(ctx, "mx_sizes", k_mx_sizes, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
+    uint64_t *a_cnt = ctx->get<uint64_t>("mx_a_cnt", (size_t)n + 1);
+    uint64_t *kd_cnt = ctx->get<uint64_t>("mx_kd_cnt", (size_t)n + 1);
+    uint64_t *u_cnt = ctx->get<uint64_t>("mx_u_cnt", (size_t)n + 1);
+    launch(ctx, "mx_sizes", k_mx_sizes, dim3(grid_for((size_t)n + 1, BLOCK)), dim3(BLOCK), 0, n, mkv, (const uint64_t *)etoff,
            (const uint32_t *)ktoff, (const uint32_t *)ucnt, a_cnt, kd_cnt, u_cnt);
     MxOut o;
     o.arena_off = ctx->get<uint64_t>("mx_arena_off", (size_t)n + 1);
     o.kd_off = ctx->get<uint64_t>("mx_kd_off", (size_t)n + 1);
     o.u_off = ctx->get<uint64_t>("mx_u_off", (size_t)n + 1);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, a_cnt, o.arena_off, n, true, o.arena_off + n);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, kd_cnt, o.kd_off, n, true, o.kd_off + n);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, u_cnt, o.u_off, n, true, o.u_off + n);
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, o.arena_off + n, 8, hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, o.kd_off + n, 8, hipMemcpyDeviceToHost, st));
-    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, o.u_off + n, 8, hipMemcpyDeviceToHost, st));
+    uint64_t *mtot = ctx->get<uint64_t>("mx_totals", 3);
+    {   // the three combined offset arrays in one launch (over n + 1: the last element is each total), totals staged
+        const uint64_t *si[3] = { a_cnt, kd_cnt, u_cnt };
+        uint64_t *so[3] = { o.arena_off, o.kd_off, o.u_off }, *stot[3] = { mtot, mtot + 1, mtot + 2 };
+        const size_t sn[3] = { (size_t)n + 1, (size_t)n + 1, (size_t)n + 1 };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 3, si, so, sn, true, stot);
+    }
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, mtot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t TA = ctx->pinned[0], TK = ctx->pinned[1], TU = ctx->pinned[2];
     o.arena = ctx->get<int32_t>("mx_arena", TA + 1);
@@ -4415,9 +4448,7 @@ void cfk_snapshot(acc_ctx *ctx, const acc_batch_in *in, CfkSnapshot &out)
     ACC_HIP(hipMemcpyAsync(ctx->pinned, ks.seg_incl + ks.P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
     const uint32_t nseg = (uint32_t)(ctx->pinned[0] & 0xFFFFFFFFu);   // seg_incl = inclusive count of segment starts
-    uint64_t *seg_key = ctx->get<uint64_t>("snap_seg_key", nseg);
-    launch(ctx, "mx_seg_keys", k_mx_seg_keys, dim3(grid_for(nseg, BLOCK)), dim3(BLOCK), 0, nseg, ks.seg_start, ks.perm,
-           ks.key_code, seg_key);
+    const uint64_t *seg_key = ks.seg_key;   // written by k_v2_apply
     out.cfk = true; out.nseg = nseg; out.rbits = ks.rbits; out.rank = ks.rank; out.txn_of_rank = ks.txn_of_rank;
     out.seg_start = ks.seg_start; out.seg_key = seg_key; out.s_rank = ks.s_rank; out.s_exec = ks.s_exec;
     out.s_info = ks.s_info; out.perm = ks.perm; out.tm = ks.tm; out.tl = ks.tl; out.tn = ks.tn; out.em = ks.em;

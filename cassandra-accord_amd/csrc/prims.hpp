@@ -160,9 +160,21 @@ __device__ __forceinline__ uint64_t scan_status_load(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Up to SCAN_MAXA independent arrays per launch (one launch instead of one per array): tickets run over the arrays'
+// tiles in order, so every tile's look-back finds only tiles of its own array that took lower tickets.
+constexpr int SCAN_MAXA = 4;
+template <class T>
+struct ScanArgs {
+    const T *in[SCAN_MAXA];
+    T *out[SCAN_MAXA];
+    T *total[SCAN_MAXA];
+    uint64_t n[SCAN_MAXA];
+    uint32_t cum[SCAN_MAXA + 1];   // first ticket of each array; cum[k] = all tiles
+    int k;
+};
+
 template <class T, class Op, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *__restrict__ out, size_t n, int exclusive,
-                                                 T *__restrict__ total_out, uint32_t *__restrict__ ticket,
+__global__ __launch_bounds__(BLOCK) void k_scan_1p(ScanArgs<T> a, int exclusive, uint32_t *__restrict__ ticket,
                                                  uint64_t *__restrict__ status, uint64_t *__restrict__ other, uint32_t other_n)
 {
     constexpr int TILE = BLOCK * ITEMS;
@@ -178,7 +190,16 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
     }
     if (tid == 0) s_b = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t b = s_b;
+    const uint32_t tk = s_b;
+    int ai = 0;
+#pragma unroll
+    for (int q = 1; q < SCAN_MAXA; ++q) ai += (q < a.k && tk >= a.cum[q]) ? 1 : 0;
+    const uint32_t b = tk - a.cum[ai];
+    const T *__restrict__ in = a.in[ai];
+    T *__restrict__ out = a.out[ai];
+    T *__restrict__ total_out = a.total[ai];
+    const size_t n = a.n[ai];
+    uint64_t *const st = status + a.cum[ai];
     const size_t base = (size_t)b * TILE;
     Op op;
 #pragma unroll
@@ -199,9 +220,9 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
     T total;
     T run = block_exclusive(acc, op, lds, total);
     if (b == 0) {
-        if (tid == 0) scan_status_store(&status[0], (uint64_t)total | SCAN_INC);
+        if (tid == 0) scan_status_store(&st[0], (uint64_t)total | SCAN_INC);
     } else {
-        if (tid == 0) scan_status_store(&status[b], (uint64_t)total | SCAN_AGG);
+        if (tid == 0) scan_status_store(&st[b], (uint64_t)total | SCAN_AGG);
         if (tid < 64) {
             T pre = Op::identity();
             int64_t j = (int64_t)b - 1;
@@ -209,10 +230,10 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
                 const int64_t idx = j - (int64_t)lane;
                 uint64_t w = (uint64_t)Op::identity() | SCAN_INC;
                 if (idx >= 0) {
-                    w = scan_status_load(&status[idx]);
+                    w = scan_status_load(&st[idx]);
                     while ((w >> 62) == 0) {
                         __builtin_amdgcn_s_sleep(1);
-                        w = scan_status_load(&status[idx]);
+                        w = scan_status_load(&st[idx]);
                     }
                 }
                 const uint64_t inc = __ballot((w >> 62) == 2);
@@ -225,7 +246,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
                 j -= 64;
             }
             if (tid == 0) {
-                scan_status_store(&status[b], (uint64_t)op(pre, total) | SCAN_INC);
+                scan_status_store(&st[b], (uint64_t)op(pre, total) | SCAN_INC);
                 s_prefix = pre;
             }
         }
@@ -249,17 +270,30 @@ __global__ __launch_bounds__(BLOCK) void k_scan_1p(const T *__restrict__ in, T *
     }
 }
 
+// k arrays (k <= SCAN_MAXA) scanned by one launch; in[i] / out[i] / n[i] / total_out[i] as scan() below
 template <class T, class Op>
-void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr)
+void scan_multi(acc_ctx *ctx, int k, const T *const *in, T *const *out, const size_t *n, bool exclusive, T *const *total_out)
 {
     constexpr int ITEMS = sizeof(T) == 8 ? 16 : 32;   // 4096 / 8192-element tiles: fewer look-back hops
     constexpr size_t TILE = (size_t)BLOCK * ITEMS;
-    if (n == 0) {
-        if (total_out) ACC_HIP(hipMemsetAsync(total_out, 0, sizeof(T), ctx->stream));
-        return;
+    if (k < 1 || k > SCAN_MAXA) fail(ACC_E_STATE, "internal: scan_multi array count");
+    ScanArgs<T> a{};
+    size_t nb = 0;
+    int m = 0;
+    for (int i = 0; i < k; ++i) {
+        if (n[i] == 0) {   // nothing to scan: the total is the identity of the sum (0)
+            if (total_out && total_out[i]) ACC_HIP(hipMemsetAsync(total_out[i], 0, sizeof(T), ctx->stream));
+            continue;
+        }
+        a.in[m] = in[i]; a.out[m] = out[i]; a.total[m] = total_out ? total_out[i] : nullptr; a.n[m] = n[i];
+        a.cum[m] = (uint32_t)nb;
+        nb += (n[i] + TILE - 1) / TILE;
+        if (nb > 0xFFFFFFF0ull) fail(ACC_E_CAP, "scan too large");
+        ++m;
     }
-    const size_t nb = (n + TILE - 1) / TILE;
-    if (nb > 0xFFFFFFFFull) fail(ACC_E_CAP, "scan too large");
+    if (m == 0) return;
+    a.k = m;
+    for (int i = m; i <= SCAN_MAXA; ++i) a.cum[i] = (uint32_t)nb;
     // stream order is what makes the double-buffered status safe: every scan runs on the context stream
     if (ctx->launch_stream) fail(ACC_E_STATE, "internal: scan launched on a side stream");
     const size_t need = nb + 1;
@@ -277,11 +311,18 @@ void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_
     const int p = ctx->scan_par;
     uint64_t *status = buf[p];
     uint32_t *ticket = reinterpret_cast<uint32_t *>(status + nb);
-    launch(ctx, "scan", k_scan_1p<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, in, out, n, (int)exclusive, total_out,
-           ticket, status, buf[p ^ 1], (uint32_t)ctx->scan_dirty[p ^ 1]);
+    launch(ctx, "scan", k_scan_1p<T, Op, ITEMS>, dim3((unsigned)nb), dim3(BLOCK), 0, a, (int)exclusive, ticket, status,
+           buf[p ^ 1], (uint32_t)ctx->scan_dirty[p ^ 1]);
     ctx->scan_dirty[p] = need;
     ctx->scan_dirty[p ^ 1] = 0;
     ctx->scan_par = p ^ 1;
+}
+
+template <class T, class Op>
+void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_out = nullptr)
+{
+    T *const tot[1] = { total_out };
+    scan_multi<T, Op>(ctx, 1, &in, &out, &n, exclusive, tot);
 }
 
 // ---------------------------------------------------------------- bit compaction plan
@@ -472,10 +513,12 @@ constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1
 constexpr int OS_MAXP = 8;
 
 static __global__ __launch_bounds__(BLOCK) void k_rs_ghist(const uint64_t *__restrict__ keys, size_t n, int lo, int passes,
-                                                    uint32_t *__restrict__ ghist)
+                                                    uint32_t *__restrict__ ghist, uint32_t *__restrict__ other, uint32_t other_n)
 {
     __shared__ uint32_t h[WAVES][OS_MAXP][256];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+    // reset the other status buffer of this sort tag for its next sort (this sort does not read it)
+    for (uint32_t i = blockIdx.x * BLOCK + tid; i < other_n; i += gridDim.x * BLOCK) other[i] = 0;
     for (uint32_t i = tid; i < WAVES * OS_MAXP * 256; i += BLOCK) (&h[0][0][0])[i] = 0;
     __syncthreads();
     // tiles of RS_TILE keys (all of a tile's loads issued up front), blocks striding over them: the block's counts go to
@@ -659,6 +702,38 @@ struct Sorted {
     uint32_t *vals;
 };
 
+// The one-sweep words of a sort tag: [passes x 256 digit totals][passes tickets][passes x ntiles x 256 status words].
+// Two buffers per tag alternate: the histogram kernel of a sort zeroes the words the previous sort dirtied in the other
+// buffer, so no memset precedes a sort (both are zeroed once when they grow). Sorts run on the context stream only.
+struct OsWords {
+    uint32_t *cur, *other;
+    uint32_t other_n;
+    acc_ctx::OsState *st;
+    size_t words;
+    void commit() const   // after the histogram launch: cur is dirty, other is clean
+    {
+        st->dirty[st->par] = words;
+        st->dirty[st->par ^ 1] = 0;
+        st->par ^= 1;
+    }
+};
+static inline OsWords os_words(acc_ctx *ctx, const char *tag, size_t words)
+{
+    if (ctx->launch_stream) fail(ACC_E_STATE, "internal: radix sort launched on a side stream");
+    if (words >= 0xFFFFFFFFull) fail(ACC_E_CAP, "internal: radix sort status beyond 2^32 words");
+    acc_ctx::OsState &s = ctx->os_state[ctx->ns + tag];
+    char n0[56], n1[56];
+    snprintf(n0, sizeof n0, "%s_os0", tag);
+    snprintf(n1, sizeof n1, "%s_os1", tag);
+    uint32_t *b[2] = { ctx->get<uint32_t>(n0, std::max(words, s.cap)), ctx->get<uint32_t>(n1, std::max(words, s.cap)) };
+    if (words > s.cap) {
+        for (int i = 0; i < 2; ++i) ACC_HIP(hipMemsetAsync(b[i], 0, words * sizeof(uint32_t), ctx->stream));
+        s.cap = words;
+        s.dirty[0] = s.dirty[1] = 0;
+    }
+    return OsWords{ b[s.par], b[s.par ^ 1], (uint32_t)s.dirty[s.par ^ 1], &s, words };
+}
+
 // Stable sort of n (key, value) pairs by the low `bits` bits of key (higher bits must be zero).
 // vals == nullptr sorts with values = index. Results live in context buffers "<tag>_k?/_v?" and stay
 // valid until the next sort with the same tag.
@@ -684,15 +759,13 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
     if (n < (size_t)OS_VAL && passes <= OS_MAXP && !legacy) {
         const bool small = n < rs_small_n();
         const uint32_t ntiles = (uint32_t)((n + (small ? RS_TILE_S : RS_TILE) - 1) / (small ? RS_TILE_S : RS_TILE));
-        // one-sweep: [passes x 256 digit totals][passes tickets][passes x ntiles x 256 status words], zeroed by one fill
-        char nsw[48];
-        snprintf(nsw, sizeof nsw, "%s_os", tag);
         const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;
-        uint32_t *osb = ctx->get<uint32_t>(nsw, words);
-        ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
-        uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
+        const OsWords ow = os_words(ctx, tag, words);
+        uint32_t *ghist = ow.cur, *tickets = ow.cur + (size_t)passes * 256, *status = tickets + passes;
         snprintf(th, sizeof th, "%s.ghist", tag);
-        launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, 0, passes, ghist);
+        launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, 0, passes, ghist, ow.other,
+               ow.other_n);
+        ow.commit();
         const uint64_t *kin = keys;
         const uint32_t *vin = vals;
         int cur = 0;
@@ -736,9 +809,8 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
 // under the key). One-sweep only: n < 2^30. The result lives in the context buffers "<tag>_k?".
 static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uint64_t *keys, size_t n, int lo, int bits)
 {
-    char nk0[40], nk1[40], nsw[48], th[48], ts[48];
+    char nk0[40], nk1[40], th[48], ts[48];
     snprintf(nk0, sizeof nk0, "%s_k0", tag); snprintf(nk1, sizeof nk1, "%s_k1", tag);
-    snprintf(nsw, sizeof nsw, "%s_os", tag);
     snprintf(th, sizeof th, "%s.ghist", tag);
     snprintf(ts, sizeof ts, "%s.scatter", tag);
     uint64_t *k[2] = { ctx->get<uint64_t>(nk0, n), ctx->get<uint64_t>(nk1, n) };
@@ -751,10 +823,11 @@ static inline uint64_t *radix_sort_keys(acc_ctx *ctx, const char *tag, const uin
     const bool small = n < rs_small_n();
     const uint32_t ntiles = (uint32_t)((n + (small ? RS_TILE_S : RS_TILE) - 1) / (small ? RS_TILE_S : RS_TILE));
     const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;
-    uint32_t *osb = ctx->get<uint32_t>(nsw, words);
-    ACC_HIP(hipMemsetAsync(osb, 0, words * sizeof(uint32_t), ctx->cur()));
-    uint32_t *ghist = osb, *tickets = osb + (size_t)passes * 256, *status = tickets + passes;
-    launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, lo, passes, ghist);
+    const OsWords ow = os_words(ctx, tag, words);
+    uint32_t *ghist = ow.cur, *tickets = ow.cur + (size_t)passes * 256, *status = tickets + passes;
+    launch(ctx, th, k_rs_ghist, dim3(std::min<unsigned>(ntiles, 1024u)), dim3(BLOCK), 0, keys, n, lo, passes, ghist, ow.other,
+           ow.other_n);
+    ow.commit();
     const uint64_t *kin = keys;
     int cur = 0;
     for (int p = 0; p < passes; ++p) {

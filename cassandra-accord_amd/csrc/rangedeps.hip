@@ -1040,7 +1040,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
         owner = shared->owner;
         ctx->stat("rangedeps.shared_dictionary", 1);
     } else {
-        uint64_t *g = ctx->get<uint64_t>("g", 8);
+        uint64_t *g = ctx->get<uint64_t>("g", PREP_G_WORDS);
         uint32_t *own = ctx->get<uint32_t>("owner", P);
         prep_dictionary(ctx, n, P, tm, tl, tn, em, el, en, status, key_off, key_code, own, g, dict);
         owner = own;

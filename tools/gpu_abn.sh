@@ -17,7 +17,8 @@ for cfg in ${CFGS:-2}; do
 import json; d=json.loads(open('gpurun_out/abn_c${cfg}_${v}_$i.log').read().strip().splitlines()[-1])
 k=d.get('kernels_ms_per_step',{})
 top=sorted(k.items(), key=lambda kv: -kv[1])[:6]
-print('c$cfg $v', d['ms_per_step'], d['roofline']['device_kernel_ms_per_step'], ' '.join('%s=%.3f' % kv for kv in top))"
+mx=d.get('keydeps_mixed',{}).get('ms_per_call'); pd=d.get('partial_deps',{}).get('ms_per_step')
+print('c$cfg $v', d['ms_per_step'], d['roofline']['device_kernel_ms_per_step'], ('mixed=%s fused=%s' % (mx, pd)) if mx else '', ' '.join('%s=%.3f' % kv for kv in top))"
         done
     done
 done
