@@ -43,7 +43,8 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_deps_merge", "acc_rmm_copy_out", "acc_rmm_invert", "acc_rmm_slice", "acc_rangedeps_stab", "acc_copy_out", "acc_comm_unique_id", "acc_comm_init_rccl", "acc_comm_init_host", "acc_comm_destroy", "acc_partial_deps_reduce", "acc_shard_reduce",
            "acc_map_reduce_full", "acc_map_reduce_full_ranges", "acc_latest_deps_merge", "acc_partial_deps_batch",
            "acc_deps_from_json", "acc_deps_to_json",
-           "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view", "acc_cfk_apply", "acc_cfk_snap_to_batch", "acc_max_conflicts",
+           "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view", "acc_cfk_apply", "acc_cfk_snap_to_batch",
+           "acc_cfk_apply_deps", "acc_cfk_state", "acc_cfk_missing", "acc_max_conflicts",
            "acc_maxconflicts_create", "acc_maxconflicts_destroy", "acc_maxconflicts_update", "acc_maxconflicts_get",
            "acc_maxconflicts_size"]
 
@@ -411,6 +412,12 @@ def load():
     L.acc_max_conflicts.argtypes = [C.c_void_p, C.POINTER(ConflictsIn), C.POINTER(PreacceptIn), C.POINTER(PreacceptOut)]
     L.acc_max_conflicts.restype = C.c_int
     try:
+        L.acc_cfk_apply_deps.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(CfkUpdates)]
+        L.acc_cfk_apply_deps.restype = C.c_int
+        L.acc_cfk_state.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(CfkSnap)]
+        L.acc_cfk_state.restype = C.c_int
+        L.acc_cfk_missing.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(CfkBatchView)]
+        L.acc_cfk_missing.restype = C.c_int
         L.acc_maxconflicts_create.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
         L.acc_maxconflicts_create.restype = C.c_int
         L.acc_maxconflicts_destroy.argtypes = [C.c_void_p]

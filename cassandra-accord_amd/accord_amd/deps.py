@@ -730,6 +730,32 @@ def deps_to_json(ctx: Context, view) -> list[bytes]:
 
 # ---------------------------------------------------------------- CommandsForKey.update with deps (key-major)
 
+def _cfk_updates_host(upd: dict) -> dict:
+    return {k: np.ascontiguousarray(np.asarray(upd[k], dt)) for k, dt in (
+        ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("xmsb", np.uint64), ("xlsb", np.uint64),
+        ("xnode", np.int32), ("status", np.uint8), ("flags", np.uint8), ("key_off", np.uint32), ("key", np.uint64),
+        ("dep_off", np.uint32), ("dmsb", np.uint64), ("dlsb", np.uint64), ("dnode", np.int32))}
+
+
+def _cfk_updates_in(b: dict) -> "L.CfkUpdates":
+    p = lambda k: b[k].ctypes.data  # noqa: E731
+    return L.CfkUpdates(L.ACC_MEM_HOST, len(b["msb"]), len(b["key"]), len(b["dmsb"]),
+                        L.TsCols(p("msb"), p("lsb"), p("node")), L.TsCols(p("xmsb"), p("xlsb"), p("xnode")),
+                        p("status"), p("flags"), p("key_off"), p("key"), p("dep_off"),
+                        L.TsCols(p("dmsb"), p("dlsb"), p("dnode")))
+
+
+def _snap_host(ctx: Context, v) -> dict:
+    nk, ne, nm = int(v.n_keys), int(v.n_entries), int(v.n_missing)
+    return dict(key=device_array(ctx, v.key, nk, np.uint64), ent_off=device_array(ctx, v.ent_off, nk + 1, np.uint32),
+                emsb=device_array(ctx, v.txn_id.msb, ne, np.uint64), elsb=device_array(ctx, v.txn_id.lsb, ne, np.uint64),
+                enode=device_array(ctx, v.txn_id.node, ne, np.int32), xmsb=device_array(ctx, v.execute_at.msb, ne, np.uint64),
+                xlsb=device_array(ctx, v.execute_at.lsb, ne, np.uint64), xnode=device_array(ctx, v.execute_at.node, ne, np.int32),
+                status=device_array(ctx, v.status, ne, np.uint8), miss_off=device_array(ctx, v.miss_off, ne + 1, np.uint32),
+                mmsb=device_array(ctx, v.missing.msb, nm, np.uint64), mlsb=device_array(ctx, v.missing.lsb, nm, np.uint64),
+                mnode=device_array(ctx, v.missing.node, nm, np.int32))
+
+
 def cfk_apply(ctx: Context, snap: dict, upd: dict, keep_device: bool = False):
     """CommandsForKey.update(prev, next) with each command's deps (local/CommandsForKey.java:657-1149) for a batch of
     updates against a key-major snapshot (acc_cfk_apply): missing[] maintenance and TRANSITIVELY_KNOWN additions.
@@ -740,30 +766,17 @@ def cfk_apply(ctx: Context, snap: dict, upd: dict, keep_device: bool = False):
         ("key", np.uint64), ("ent_off", np.uint32), ("emsb", np.uint64), ("elsb", np.uint64), ("enode", np.int32),
         ("xmsb", np.uint64), ("xlsb", np.uint64), ("xnode", np.int32), ("status", np.uint8), ("miss_off", np.uint32),
         ("mmsb", np.uint64), ("mlsb", np.uint64), ("mnode", np.int32))}
-    b = {k: np.ascontiguousarray(np.asarray(upd[k], dt)) for k, dt in (
-        ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32), ("xmsb", np.uint64), ("xlsb", np.uint64),
-        ("xnode", np.int32), ("status", np.uint8), ("flags", np.uint8), ("key_off", np.uint32), ("key", np.uint64),
-        ("dep_off", np.uint32), ("dmsb", np.uint64), ("dlsb", np.uint64), ("dnode", np.int32))}
+    b = _cfk_updates_host(upd)
     p = lambda d, k: d[k].ctypes.data  # noqa: E731
     si = L.CfkSnap(L.ACC_MEM_HOST, len(a["key"]), len(a["status"]), len(a["mmsb"]), p(a, "key"), p(a, "ent_off"),
                    L.TsCols(p(a, "emsb"), p(a, "elsb"), p(a, "enode")), L.TsCols(p(a, "xmsb"), p(a, "xlsb"), p(a, "xnode")),
                    p(a, "status"), p(a, "miss_off"), L.TsCols(p(a, "mmsb"), p(a, "mlsb"), p(a, "mnode")))
-    ui = L.CfkUpdates(L.ACC_MEM_HOST, len(b["msb"]), len(b["key"]), len(b["dmsb"]),
-                      L.TsCols(p(b, "msb"), p(b, "lsb"), p(b, "node")), L.TsCols(p(b, "xmsb"), p(b, "xlsb"), p(b, "xnode")),
-                      p(b, "status"), p(b, "flags"), p(b, "key_off"), p(b, "key"), p(b, "dep_off"),
-                      L.TsCols(p(b, "dmsb"), p(b, "dlsb"), p(b, "dnode")))
+    ui = _cfk_updates_in(b)
     v = L.CfkSnapView()
     ctx.check(ctx._lib.acc_cfk_apply(ctx.handle, C.byref(si), C.byref(ui), C.byref(v)))
     if keep_device:
         return v
-    nk, ne, nm = int(v.n_keys), int(v.n_entries), int(v.n_missing)
-    return dict(key=device_array(ctx, v.key, nk, np.uint64), ent_off=device_array(ctx, v.ent_off, nk + 1, np.uint32),
-                emsb=device_array(ctx, v.txn_id.msb, ne, np.uint64), elsb=device_array(ctx, v.txn_id.lsb, ne, np.uint64),
-                enode=device_array(ctx, v.txn_id.node, ne, np.int32), xmsb=device_array(ctx, v.execute_at.msb, ne, np.uint64),
-                xlsb=device_array(ctx, v.execute_at.lsb, ne, np.uint64), xnode=device_array(ctx, v.execute_at.node, ne, np.int32),
-                status=device_array(ctx, v.status, ne, np.uint8), miss_off=device_array(ctx, v.miss_off, ne + 1, np.uint32),
-                mmsb=device_array(ctx, v.missing.msb, nm, np.uint64), mlsb=device_array(ctx, v.missing.lsb, nm, np.uint64),
-                mnode=device_array(ctx, v.missing.node, nm, np.int32))
+    return _snap_host(ctx, v)
 
 
 def _view_as_snap(v) -> "L.CfkSnap":
@@ -957,3 +970,21 @@ class CfkStore:
         """PreAccept.calculatePartialDeps for every txn of the store, read in place (no host round trip)."""
         view = self.ctx.keydeps_batch_raw(self.view())
         return self.ctx.copy_out(view, None)
+
+    def apply_deps(self, upd: dict):
+        """CommandsForKey.update with each command's deps on the store itself (acc_cfk_apply_deps; the cfk_apply
+        update layout): missing[] maintained, the txn-major view and its missing[] indices rebuilt."""
+        b = _cfk_updates_host(upd)
+        self.ctx.check(self.ctx._lib.acc_cfk_apply_deps(self.ctx.handle, self._h, C.byref(_cfk_updates_in(b))))
+
+    def state(self) -> dict:
+        """Host copy of the key-major CommandsForKey state (the cfk_apply snapshot layout)."""
+        s = L.CfkSnap()
+        self.ctx.check(self.ctx._lib.acc_cfk_state(self.ctx.handle, self._h, C.byref(s)))
+        return _snap_host(self.ctx, s)
+
+    def missing_view(self) -> "L.CfkBatchView":
+        """The store's txn-major view with each pair's missing[] as txn indices (device), for cfk_map_reduce_full."""
+        bv = L.CfkBatchView()
+        self.ctx.check(self.ctx._lib.acc_cfk_missing(self.ctx.handle, self._h, C.byref(bv)))
+        return bv

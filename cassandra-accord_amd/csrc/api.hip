@@ -31,6 +31,9 @@ uint64_t mc_size(const acc_maxconflicts *m);
 void mc_update(acc_ctx *ctx, acc_maxconflicts *m, const acc_conflicts_in *u);
 void mc_get(acc_ctx *ctx, const acc_maxconflicts *m, const acc_preaccept_in *q, acc_preaccept_out *out);
 void cfk_view(acc_cfk *cfk, acc_batch_in *out);
+void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up);
+void cfk_state(acc_cfk *cfk, acc_cfk_snap *out);
+void cfk_missing(acc_cfk *cfk, acc_cfk_batch_view *out);
 void cfk_free(acc_cfk *cfk);
 acc_cfk *cfk_new(int device);
 }  // namespace acc
@@ -260,6 +263,27 @@ int acc_cfk_view(acc_ctx *ctx, acc_cfk *cfk, acc_batch_in *out)
         ACC_HIP(hipSetDevice(ctx->device));
         acc::cfk_view(cfk, out);
     });
+}
+
+int acc_cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *updates)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::cfk_apply_deps(ctx, cfk, updates);
+    });
+}
+
+int acc_cfk_state(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_snap *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] { acc::cfk_state(cfk, out); });
+}
+
+int acc_cfk_missing(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_batch_view *out)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] { acc::cfk_missing(cfk, out); });
 }
 
 int acc_keydeps_copy_out(acc_ctx *ctx, acc_keydeps_out *out)

@@ -27,6 +27,23 @@ struct acc_cfk {
         size_t cap_n = 0, cap_p = 0;
     } set[2];
     int cur = 0;
+    // acc_cfk_apply_deps: the same store with every TxnInfo's missing[] — the key-major CommandsForKey state (what
+    // acc_cfk_apply maintains) and, beside the txn-major view above, each (txn, key) pair's missing[] as txn indices
+    // (what acc_map_reduce_full reads). Both are rewritten by every acc_cfk_apply_deps, so the scans and the next update
+    // read the one state in place.
+    bool deps = false;
+    struct KeyMajor {
+        uint32_t nk = 0;
+        uint64_t ne = 0, nm = 0;
+        uint64_t *key = nullptr, *em = nullptr, *el = nullptr, *xm = nullptr, *xl = nullptr, *mm = nullptr, *ml = nullptr;
+        int32_t *en = nullptr, *xn = nullptr, *mn = nullptr;
+        uint8_t *st = nullptr;
+        uint32_t *ent_off = nullptr, *miss_off = nullptr;
+        size_t cap_k = 0, cap_e = 0, cap_m = 0;
+    } km;
+    uint32_t *bmiss_off = nullptr, *bmiss_txn = nullptr;   // [P + 1], [bnm]
+    uint64_t bnm = 0;
+    size_t cap_bmo = 0, cap_bmt = 0;
 };
 
 namespace acc {
@@ -259,6 +276,8 @@ void reserve(acc_cfk::Set &s, size_t n, size_t P)
 void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in)
 {
     if (!cfk || !in) fail(ACC_E_ARG, "null argument");
+    if (cfk->deps)
+        fail(ACC_E_STATE, "the store holds missing[] (acc_cfk_apply_deps): status-only updates would not maintain it");
     if (in->mem != ACC_MEM_HOST && in->mem != ACC_MEM_DEVICE) fail(ACC_E_ARG, "mem must be ACC_MEM_HOST or ACC_MEM_DEVICE");
     hipStream_t st = ctx->stream;
     const uint32_t D = in->n_txn;
@@ -358,7 +377,133 @@ void cfk_free(acc_cfk *cfk)
         (void)hipFree(s.tm); (void)hipFree(s.tl); (void)hipFree(s.em); (void)hipFree(s.el); (void)hipFree(s.key_code);
         (void)hipFree(s.tn); (void)hipFree(s.en); (void)hipFree(s.status); (void)hipFree(s.key_off);
     }
+    auto &k = cfk->km;
+    for (void *p : { (void *)k.key, (void *)k.em, (void *)k.el, (void *)k.xm, (void *)k.xl, (void *)k.mm, (void *)k.ml,
+                     (void *)k.en, (void *)k.xn, (void *)k.mn, (void *)k.st, (void *)k.ent_off, (void *)k.miss_off,
+                     (void *)cfk->bmiss_off, (void *)cfk->bmiss_txn })
+        (void)hipFree(p);
     delete cfk;
+}
+
+void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view);
+void cfk_view(acc_cfk *cfk, acc_batch_in *out);
+
+namespace {
+
+template <class T>
+void grow_dev(T *&p, size_t &cap, size_t count)   // capacity for count elements (at least 1); contents not kept
+{
+    if (count + 1 <= cap && p) return;
+    const size_t c = count + count / 4 + 64;
+    realloc_dev(p, c);
+    cap = c;
+}
+
+template <class T>
+void copy_dev(acc_ctx *ctx, T *dst, const T *src, size_t count)
+{
+    if (count) ACC_HIP(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+}
+
+acc_cfk_snap km_snap(acc_cfk *cfk)
+{
+    const acc_cfk::KeyMajor &k = cfk->km;
+    return acc_cfk_snap{ ACC_MEM_DEVICE, k.nk, k.ne, k.nm, k.key, k.ent_off, acc_ts_cols{ k.em, k.el, k.en },
+                         acc_ts_cols{ k.xm, k.xl, k.xn }, k.st, k.miss_off, acc_ts_cols{ k.mm, k.ml, k.mn } };
+}
+
+}  // namespace
+
+// CommandsForKey.update with the command's deps on the store itself (local/CommandsForKey.java:657-1149 per key, as
+// SafeCommandStore.updateCommandsForKey calls it, local/SafeCommandStore.java:217-240): acc_cfk_apply over the store's
+// key-major state, then the txn-major view and its per-pair missing[] indices rebuilt from the result
+// (acc_cfk_snap_to_batch), both copied into the store only when both succeeded — a rejected batch (stale status, bad
+// offsets, a TxnId whose keys disagree on its status) leaves the store as it was.
+void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
+{
+    if (!cfk || !up) fail(ACC_E_ARG, "null argument");
+    if (!cfk->deps && cfk->n)
+        fail(ACC_E_STATE, "the store holds status-only state (acc_cfk_update): missing[] is maintained from an empty store");
+    acc_cfk::KeyMajor &k = cfk->km;
+    if (!k.ent_off) {   // empty state: offsets [0] (the grown arrays are reallocated below, ent_off / miss_off first)
+        realloc_dev(k.ent_off, 1);
+        realloc_dev(k.miss_off, 1);
+        ACC_HIP(hipMemsetAsync(k.ent_off, 0, 4, ctx->stream));
+        ACC_HIP(hipMemsetAsync(k.miss_off, 0, 4, ctx->stream));
+    }
+    const acc_cfk_snap prev = km_snap(cfk);
+    acc_cfk_snap_view v{};
+    cfk_apply(ctx, &prev, up, &v);
+    const acc_cfk_snap next{ ACC_MEM_DEVICE, v.n_keys, v.n_entries, v.n_missing, v.key, v.ent_off, v.txn_id, v.execute_at,
+                             v.status, v.miss_off, v.missing };
+    acc_cfk_batch_view bv{};
+    cfk_snap_to_batch(ctx, &next, &bv);
+    // ---- both results in the store
+    const uint32_t nk = v.n_keys;
+    const uint64_t ne = v.n_entries, nm = v.n_missing;
+    auto cap_for = [](size_t need) { return need + need / 4 + 64; };
+    if (nk + 1 > k.cap_k || !k.key) {
+        const size_t c = cap_for((size_t)nk + 1);
+        realloc_dev(k.key, c); realloc_dev(k.ent_off, c);
+        k.cap_k = c;
+    }
+    if (ne + 1 > k.cap_e || !k.em) {
+        const size_t c = cap_for(ne + 1);
+        realloc_dev(k.em, c); realloc_dev(k.el, c); realloc_dev(k.en, c); realloc_dev(k.xm, c); realloc_dev(k.xl, c);
+        realloc_dev(k.xn, c); realloc_dev(k.st, c); realloc_dev(k.miss_off, c);
+        k.cap_e = c;
+    }
+    if (nm + 1 > k.cap_m || !k.mm) {
+        const size_t c = cap_for(nm + 1);
+        realloc_dev(k.mm, c); realloc_dev(k.ml, c); realloc_dev(k.mn, c);
+        k.cap_m = c;
+    }
+    copy_dev(ctx, k.key, v.key, nk);
+    copy_dev(ctx, k.ent_off, v.ent_off, (size_t)nk + 1);
+    copy_dev(ctx, k.em, v.txn_id.msb, ne); copy_dev(ctx, k.el, v.txn_id.lsb, ne); copy_dev(ctx, k.en, v.txn_id.node, ne);
+    copy_dev(ctx, k.xm, v.execute_at.msb, ne); copy_dev(ctx, k.xl, v.execute_at.lsb, ne);
+    copy_dev(ctx, k.xn, v.execute_at.node, ne);
+    copy_dev(ctx, k.st, v.status, ne);
+    copy_dev(ctx, k.miss_off, v.miss_off, ne + 1);
+    copy_dev(ctx, k.mm, v.missing.msb, nm); copy_dev(ctx, k.ml, v.missing.lsb, nm); copy_dev(ctx, k.mn, v.missing.node, nm);
+    k.nk = nk; k.ne = ne; k.nm = nm;
+    const acc_batch_in &b = bv.batch;
+    const uint32_t n = b.n_txn;
+    const uint64_t P = b.n_pairs;
+    acc_cfk::Set &S = cfk->set[cfk->cur];
+    reserve(S, n, P);
+    copy_dev(ctx, S.tm, b.txn_id.msb, n); copy_dev(ctx, S.tl, b.txn_id.lsb, n); copy_dev(ctx, S.tn, b.txn_id.node, n);
+    copy_dev(ctx, S.em, b.execute_at.msb, n); copy_dev(ctx, S.el, b.execute_at.lsb, n); copy_dev(ctx, S.en, b.execute_at.node, n);
+    copy_dev(ctx, S.status, b.status, n);
+    copy_dev(ctx, S.key_off, b.key_off, (size_t)n + 1);
+    copy_dev(ctx, S.key_code, b.key_code, P);
+    grow_dev(cfk->bmiss_off, cfk->cap_bmo, P + 1);
+    grow_dev(cfk->bmiss_txn, cfk->cap_bmt, bv.n_missing + 1);
+    copy_dev(ctx, cfk->bmiss_off, bv.missing_off, P + 1);
+    copy_dev(ctx, cfk->bmiss_txn, bv.missing_txn, bv.n_missing);
+    cfk->bnm = bv.n_missing;
+    ctx->sync();
+    cfk->n = n;
+    cfk->P = P;
+    cfk->deps = true;
+}
+
+void cfk_state(acc_cfk *cfk, acc_cfk_snap *out)
+{
+    if (!cfk || !out) fail(ACC_E_ARG, "null argument");
+    if (!cfk->deps) fail(ACC_E_STATE, "the store holds no missing[] state (no acc_cfk_apply_deps yet)");
+    *out = km_snap(cfk);
+}
+
+void cfk_missing(acc_cfk *cfk, acc_cfk_batch_view *out)
+{
+    if (!cfk || !out) fail(ACC_E_ARG, "null argument");
+    if (!cfk->deps) fail(ACC_E_STATE, "the store holds no missing[] state (no acc_cfk_apply_deps yet)");
+    cfk_view(cfk, &out->batch);
+    out->missing_off = cfk->bmiss_off;
+    out->missing_txn = cfk->bmiss_txn;
+    out->n_missing = cfk->bnm;
 }
 
 void cfk_view(acc_cfk *cfk, acc_batch_in *out)

@@ -320,13 +320,31 @@ struct PairPlan {
     int sb;        // mode 4: bits of the key slot within its txn
 };
 
+// the per-txn record k_txn_info writes, done by k_pair_keys' first n threads when tinfo is set (one launch fewer)
+struct TxnInfoArgs {
+    uint32_t n = 0;
+    const uint8_t *status = nullptr;
+    const uint64_t *tl = nullptr;
+    uint4 *tinfo = nullptr;
+    uint32_t *bigflag = nullptr;
+};
+
+__device__ __forceinline__ void txn_info_one(uint32_t t, uint32_t n, const uint32_t *rank, const uint8_t *status,
+                                             const uint64_t *tl, const uint32_t *key_off, uint4 *tinfo, uint32_t *bigflag)
+{
+    if (bigflag) bigflag[t] = 0;
+    const uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
+    tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), key_off[t]);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_pair_keys(size_t P, const uint64_t *__restrict__ key_code,
                                                      const uint32_t *__restrict__ owner, const uint32_t *__restrict__ key_off,
                                                      const uint32_t *__restrict__ rank,
                                                      const uint32_t *__restrict__ perm, PairPlan plan,
-                                                     int rank_only, uint64_t *__restrict__ out)
+                                                     int rank_only, uint64_t *__restrict__ out, TxnInfoArgs ti)
 {
     size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (ti.tinfo && i < ti.n) txn_info_one((uint32_t)i, ti.n, rank, ti.status, ti.tl, key_off, ti.tinfo, ti.bigflag);
     if (i >= P) return;
     size_t j = perm ? perm[i] : i;
     if (rank_only) { out[i] = rank[owner[j]]; return; }
@@ -372,10 +390,7 @@ __global__ __launch_bounds__(BLOCK) void k_txn_info(uint32_t n, const uint32_t *
                                                     uint4 *__restrict__ tinfo, uint32_t *__restrict__ bigflag)
 {
     uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= n) return;
-    if (bigflag) bigflag[t] = 0;
-    uint32_t kind = (uint32_t)(tl[t] >> 1) & 7u;
-    tinfo[t] = make_uint4(rank[t], rank[n + t], (uint32_t)status[t] | (kind << 3), key_off[t]);
+    if (t < n) txn_info_one(t, n, rank, status, tl, key_off, tinfo, bigflag);
 }
 
 // per-pair copy of its txn's record, written in pair order (owner[] is monotone, so both reads stream): the CFK
@@ -508,6 +523,16 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *a, uint32_t 
 }
 
 __device__ __forceinline__ Query make_query_ts(const CfkView &v, uint32_t t, uint32_t seg);
+
+// first i in [lo, hi) with (uint32_t)a[i] >= v, the low words ascending over the range (one segment's prefix maxima)
+__device__ __forceinline__ uint32_t lower_bound_lo32(const uint64_t *a, uint32_t lo, uint32_t hi, uint32_t v)
+{
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((uint32_t)a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
 
 __device__ __forceinline__ Query make_query(const CfkView &v, uint32_t j)
 {
@@ -849,22 +874,6 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, uint32_t *__res
     }
 }
 
-// list bases: list l occupies [base[l], base[l] + total[l]) of the class-list arrays; also zeroes the count / mark
-// passes' accumulators (z: nz words; no memset launches)
-__global__ void k_v2_bases(const uint32_t *__restrict__ totals, uint32_t *__restrict__ bases, uint64_t *__restrict__ z0,
-                           uint32_t nz0, uint64_t *__restrict__ z1, uint32_t nz1, const uint64_t *__restrict__ g,
-                           uint64_t *__restrict__ stage)
-{
-    for (uint32_t i = threadIdx.x; i < nz0; i += blockDim.x) z0[i] = 0;
-    for (uint32_t i = threadIdx.x; i < nz1; i += blockDim.x) z1[i] = 0;
-    if (threadIdx.x < 3) stage[threadIdx.x] = g[4 + threadIdx.x];   // the dictionary's error / tie words beside the totals
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        uint32_t b = 0;
-        for (int l = 0; l < NLIST; ++l) { bases[l] = b; b += totals[l]; }
-        bases[NLIST] = b;
-    }
-}
-
 // The per-position prefix columns as a rank directory: one 64-B chunk per RD_W = 32 CFK positions, = one HBM line
 // (16 MB at config 2's 8M positions, instead of a 32-B row per position): words 0-7 = the 8 running values at the
 // chunk's first position (exclusive prefix counts of the 6 class lists, the bumped-committed count, the last unbumped
@@ -885,12 +894,28 @@ struct V2Cols {
 
 __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__restrict__ s_rank, const uint32_t *__restrict__ s_exec,
                                                     const uint8_t *__restrict__ s_info, const uint32_t *__restrict__ seg_flag,
-                                                    const uint32_t *__restrict__ tile_pref, const uint32_t *__restrict__ bases,
+                                                    const uint32_t *__restrict__ tile_pref, const uint32_t *__restrict__ totals,
                                                     uint32_t ntiles, int rbits, V2Cols o, uint32_t *__restrict__ seg_incl,
                                                     uint32_t *__restrict__ seg_start, const uint32_t *__restrict__ perm,
-                                                    const uint64_t *__restrict__ key_code, uint64_t *__restrict__ seg_key)
+                                                    const uint64_t *__restrict__ key_code, uint64_t *__restrict__ seg_key,
+                                                    const uint64_t *__restrict__ sp, Runs krun, uint64_t rk_mask,
+                                                    uint32_t *__restrict__ bases, uint64_t *__restrict__ z0, uint32_t nz0,
+                                                    uint64_t *__restrict__ z1, uint32_t nz1, const uint64_t *__restrict__ g,
+                                                    uint64_t *__restrict__ stage)
 {
     __shared__ uint32_t lds[WAVES];
+    if (blockIdx.x == 0) {
+        // the list bases for the count pass (list l at [bases[l], bases[l] + totals[l]) of the class-list arrays), the
+        // count / mark passes' accumulators zeroed, the dictionary's error / tie words staged beside the totals
+        if (threadIdx.x == 0) {
+            uint32_t b = 0;
+            for (int l = 0; l < NLIST; ++l) { bases[l] = b; b += totals[l]; }
+            bases[NLIST] = b;
+        }
+        for (uint32_t i = threadIdx.x; i < nz0; i += BLOCK) z0[i] = 0;
+        for (uint32_t i = threadIdx.x; i < nz1; i += BLOCK) z1[i] = 0;
+        if (threadIdx.x < 3) stage[threadIdx.x] = g[4 + threadIdx.x];
+    }
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t code[V2_ITEMS] = { 7u, 7u, 7u, 7u }, rk[V2_ITEMS] = {};
     uint32_t c[NCNT] = {};
@@ -908,7 +933,22 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
             fl[i] = base + i < P ? seg_flag[base + i] : 0u;
             c[8] += fl[i] != 0;
         }
-        if (seg_key) {   // segment starts' key codes: the gathers issued here, their latency hidden by the block scans
+        if (seg_key && sp) {
+            // mode 4: the key code from the sorted pair key itself (its compacted bits deposited back over key_code[0]'s
+            // constant bits; the varying bits all lie in the runs), a sequential read instead of a gather
+            const uint64_t kconst = key_code[0] & ~rk_mask;
+#pragma unroll
+            for (int i = 0; i < V2_ITEMS; ++i)
+                if (fl[i]) {
+                    const uint64_t c = sp[base + i] >> 32;
+                    uint64_t w = kconst;
+                    for (int r = 0; r < krun.n; ++r) {
+                        const uint64_t m = krun.len[r] >= 64 ? ~0ull : ((1ull << krun.len[r]) - 1);
+                        w |= ((c >> krun.dst[r]) & m) << krun.lo[r];
+                    }
+                    kc[i] = w;
+                }
+        } else if (seg_key) {   // segment starts' key codes: the gathers issued here, their latency hidden by the block scans
             uint32_t pi[V2_ITEMS] = {};
             if (base + V2_ITEMS <= P) {
                 const uint4 pv = *reinterpret_cast<const uint4 *>(perm + base);
@@ -960,8 +1000,11 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
     }
     if (base >= P) return;
     uint32_t lb[NLIST];
+    {
+        uint32_t b = 0;
 #pragma unroll
-    for (int l = 0; l < NLIST; ++l) lb[l] = bases[l];
+        for (int l = 0; l < NLIST; ++l) { lb[l] = b; b += totals[l]; }
+    }
     uint32_t segi[V2_ITEMS];
 #pragma unroll
     for (int i = 0; i < V2_ITEMS; ++i) {   // segment numbers (seg_incl = inclusive count of segment starts) and starts
@@ -1063,9 +1106,11 @@ struct V2View {
     const uint8_t *s_info;
     const uint4 *rdir;
     const uint32_t *list_rank, *bases;
-    const uint32_t *bc_rank, *bc_exec, *bc_pm;
+    const uint32_t *bc_rank, *bc_exec;
+    const uint64_t *bc_pm;    // (segment << 32 | executeAt + 1) prefix maxima: the low word within a segment
     const uint8_t *bc_kind;
-    const uint32_t *bcs_exec, *bcs_lastw;
+    const uint32_t *bcs_exec;
+    const uint64_t *bcs_lastw;   // nearest Write index + 1 (prefix maximum, the low word)
     const uint4 *tinfo;   // per txn: rank, executeAt rank, status | kind << 3
     const uint32_t *irec32;  // the count pass's inline records as u32 (IREC_W words per pair; word 7 = E | flag)
     const uint4 *rec;        // the count pass's 64-B records (runs; inline entries beyond IREC_N)
@@ -1132,7 +1177,7 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     if (b1 > b0) {
         uint32_t i = lower_bound_u32(v.bcs_exec, b0, b1, S);
         if (i > b0) {
-            uint32_t w = v.bcs_lastw[i - 1];
+            uint32_t w = (uint32_t)v.bcs_lastw[i - 1];
             if (w > b0) { has_mb = true; mb = v.bcs_exec[w - 1]; }
         }
     }
@@ -1143,7 +1188,7 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     else q.posm = lower_bound_u32(v.s_rank, q.s0, q.pos, q.m);
     q.rm = q.posm == q.s0 ? q.r0 : ld_row(v, q.posm);
     q.bend = q.rm.c[RW_CBC];
-    q.bstart = q.has_m ? lower_bound_u32(v.bc_pm, b0, q.bend, q.m + 1) : q.bend;
+    q.bstart = q.has_m ? lower_bound_lo32(v.bc_pm, b0, q.bend, q.m + 1) : q.bend;
     return q;
 }
 
@@ -2237,7 +2282,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
                                                    uint32_t *__restrict__ psz,
                                                    uint32_t raw_cap, uint32_t e_cap,
                                                    uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
-                                                   uint64_t *__restrict__ szK, uint64_t *__restrict__ any16)
+                                                   uint64_t *__restrict__ szK, uint64_t *__restrict__ any16,
+                                                   uint64_t *__restrict__ eb)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / ST_G, sub = threadIdx.x & (ST_G - 1);
     if (t >= n) return;   // group-uniform: shuffles stay inside the group
@@ -2256,7 +2302,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
                 const uint4 r1 = r[1], r2 = r[2], r3 = r[3];
                 raw += r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
             }
-            if (maybe_big) psz[j0 + c0 + sub] = ej;   // the big txns' per-pair entry counts (k_v3_bigsz, k_v3_bigfill)
+            if (maybe_big) psz[j0 + c0 + sub] = ej;   // the big txns' per-pair entry counts (k_v3_bigfill)
         }
     }
 #pragma unroll
@@ -2270,6 +2316,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
         bigflag[t] = big ? 1u : 0u;
         szA[t] = (uint64_t)kd + e;
         szK[t] = kd;
+        eb[t] = big ? e : 0u;   // the big txns' entries: their TxnId scratch bases by the same multi-scan
         // a big txn of 9-16 keys with entries: the 16-key window tier has work (read at the host sync after the scans)
         if (big && e && nk > 8 && nk <= 16 && !*any16) atomicOr((unsigned long long *)any16, 1ull);
     }
@@ -2283,25 +2330,12 @@ __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t < n && bigflag[t]) blist[bpos[t]] = t;
 }
-__global__ __launch_bounds__(BLOCK) void k_v3_bigsz(uint32_t nbig, const uint32_t *__restrict__ blist,
-                                                    const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ psz,
-                                                    uint64_t *__restrict__ lE)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= nbig) return;
-    const uint32_t t = blist[i], j0 = key_off[t], j1 = key_off[t + 1];
-    uint64_t E = 0;
-    for (uint32_t j = j0 + lane; j < j1; j += 64) E += psz[j];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) E += shfl_xor(E, d);
-    if (lane == 0) lE[i] = E;
-}
 
 // tier routing of the big txns (thread per list entry, one atomic per list per block). With ranks within 25 bits: the
 // window tier (<= 8 or <= 16 keys; gstat[7] / gstat[8]), else medium (E <= MED_E, <= MED_K keys) or the u32-record
 // block tier; with wider ranks: the u64 wave tier (E <= MED_E, <= MED_K keys) or the global path.
 __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_t *__restrict__ blist,
-                                                    const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ lE,
+                                                    const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ eb,
                                                     int big_ok, int win_ok, uint32_t *__restrict__ med_list,
                                                     uint32_t *__restrict__ big_list, uint32_t *__restrict__ fb_list,
                                                     uint32_t *__restrict__ w8_list, uint32_t *__restrict__ w16_list,
@@ -2313,7 +2347,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
     uint64_t E = 0;
     if (i < nbig) {
         t = blist[i];
-        E = lE[i];
+        E = eb[t];
         const uint32_t nk = key_off[t + 1] - key_off[t];
         const bool win = E > 0 && big_ok && win_ok && nk <= 16;
         w8 = win && nk <= 8;
@@ -2349,7 +2383,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
 struct V3Big {
     const uint32_t *blist, *key_off;
     const uint32_t *psz;
-    const uint64_t *dB;                       // exclusive prefix of E over the list: TxnId scratch bases
+    const uint64_t *dB;                       // per txn: exclusive prefix of the big txns' E (TxnId scratch bases)
     const uint64_t *arena_off, *kd_off;       // the batch's final offsets (from the mark pass's scans)
     uint64_t *vdep_off, *vcnt;                // per pair of a big txn (dep_off / cnt of the v2 tiers)
     uint32_t *vcnz;                           // per pair of a big txn (cnz)
@@ -2366,8 +2400,8 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
     if (i >= nbig) return;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t t = b.blist[i], j0 = b.key_off[t], j1 = b.key_off[t + 1], nk = j1 - j0;
-    const uint64_t dbase = b.dB[i], kbase = b.kd_off[t], abase = b.arena_off[t];
-    const uint64_t E = b.dB[i + 1] - dbase, Kd = b.kd_off[t + 1] - kbase;
+    const uint64_t dbase = b.dB[t], kbase = b.kd_off[t], abase = b.arena_off[t];
+    const uint64_t E = b.dB[t + 1] - dbase, Kd = b.kd_off[t + 1] - kbase;
     uint64_t ecur = 0, kcur = 0;
     for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
         const uint32_t j = j0 + c0 + lane;
@@ -3172,6 +3206,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     const int rbits = dict.rbits;
 
     // ---- 3. CFK build: pairs sorted by (key, TxnId rank)
+    uint4 *tinfo = ctx->get<uint4>("tinfo", n);
+    uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
+    bool tinfo_done = false;   // the txn records written by the pair-key launch
     PairPlan pp;
     pp.rk = make_runs(hg[3]);
     pp.rbits = rbits;
@@ -3190,8 +3227,11 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         // key_off[owner] for the pair index)
         const bool m4 = bits_for((uint64_t)n - 1) + pp.sb <= 32 && !getenv("ACC_PAIR_NO_OWNER");
         pp.mode = m4 ? 4 : 3;
-        launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+        TxnInfoArgs ti;   // the txn records (k_txn_info) by the same launch: the ranks are final unless ties turn up
+        ti.n = n; ti.status = status; ti.tl = tl; ti.tinfo = tinfo; ti.bigflag = bigflag;
+        launch(ctx, "pair_keys", k_pair_keys, dim3(grid_for(std::max<size_t>(P, n), BLOCK)), dim3(BLOCK), 0, P, key_code,
+               (const uint32_t *)owner, key_off, (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey, ti);
+        tinfo_done = true;
         const uint64_t *sp = radix_sort_keys(ctx, "rs_pair", pkey, P, 32, pp.rk.bits);
         uint32_t *perm = ctx->get<uint32_t>("pair_perm", P + V2_ITEMS);
         if (m4) sp_m4 = sp;
@@ -3202,21 +3242,21 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     } else if (batch_sorted) {
         pp.mode = 0;   // pair index order is already TxnId order within every key: stable sort by key
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey, TxnInfoArgs{});
         ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits);
     } else if (pp.rk.bits + rbits <= 64) {
         pp.mode = 1;
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey);
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 0, pkey, TxnInfoArgs{});
         ps = radix_sort(ctx, "rs_pair", pkey, nullptr, P, pp.rk.bits + rbits);
         key_shift = rbits;
     } else {
         pp.mode = 2;
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
-               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 1, pkey);
+               (const uint32_t *)rank, (const uint32_t *)nullptr, pp, 1, pkey, TxnInfoArgs{});
         Sorted byrank = radix_sort(ctx, "rs_pair_r", pkey, nullptr, P, rbits);
         launch(ctx, "pair_keys", k_pair_keys, dim3(gP), dim3(BLOCK), 0, P, key_code, (const uint32_t *)owner, key_off,
-               (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey);
+               (const uint32_t *)rank, (const uint32_t *)byrank.vals, pp, 0, pkey, TxnInfoArgs{});
         ps = radix_sort(ctx, "rs_pair", pkey, byrank.vals, P, pp.rk.bits);
     }
     uint32_t *seg_incl = ctx->get<uint32_t>("seg_incl", P + V2_ITEMS);   // written by k_v2_apply (the multi-scan's column 8)
@@ -3229,9 +3269,10 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *s_exec = ctx->get<uint32_t>("s_exec", P + V2_ITEMS);
     uint8_t *s_info = ctx->get<uint8_t>("s_info", P + V2_ITEMS);
     uint32_t *pair_pos = ctx->get<uint32_t>("pair_pos", P);
-    uint4 *tinfo = ctx->get<uint4>("tinfo", n);
     uint4 *ptinfo = sp_m4 ? nullptr : ctx->get<uint4>("pair_tinfo", P);
     bool have_pair_pos = ks != nullptr;
+    uint64_t rk_mask = 0;   // the bits the key compaction keeps (k_v2_apply rebuilds segment key codes from them)
+    for (int r = 0; r < pp.rk.n; ++r) rk_mask |= (pp.rk.len[r] >= 64 ? ~0ull : ((1ull << pp.rk.len[r]) - 1)) << pp.rk.lo[r];
     auto need_pair_pos = [&]() {
         if (have_pair_pos) return;
         launch(ctx, "pair_pos", k_pair_pos, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)ps.vals, pair_pos);
@@ -3252,27 +3293,27 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_kind = ctx->get<uint8_t>("v2_bc_kind", P);
     cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
-    // the count / mark passes' accumulators, zeroed by the column kernels below (k_txn_info, k_v2_bases)
-    uint32_t *bigflag = ctx->get<uint32_t>("v3_bigflag", n);
+    // the count / mark passes' accumulators, zeroed by the column kernels (txn records, k_v2_apply); bigflag above
     uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N + 3);   // + the batch totals (k_v3_ucompact)
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
-        launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status, tl,
-               key_off, tinfo, bigflag);
+        if (!tinfo_done)
+            launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status,
+                   tl, key_off, tinfo, bigflag);
+        tinfo_done = false;   // a second build (the ties re-rank) writes them again
         if (!sp_m4)
             launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
         launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, ps.vals, (const uint4 *)ptinfo, sp_m4, pp.sb,
                (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
-        launch(ctx, "v2_bases", k_v2_bases, dim3(1), dim3(64), 0, (const uint32_t *)totals, bases, tot, 3u, gstat,
-               (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
-               (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)bases, nt,
-               rbits, cols, seg_incl, seg_start, (const uint32_t *)ps.vals, key_code, seg_key_buf);
+               (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)totals, nt,
+               rbits, cols, seg_incl, seg_start, (const uint32_t *)ps.vals, key_code, seg_key_buf, sp_m4, pp.rk, rk_mask,
+               bases, tot, 3u, gstat, (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
     };
     build_columns();
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));   // + g[4..6] (k_v2_bases)
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, totals, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));   // + g[4..6] (k_v2_apply)
     ctx->sync();
     if (dict.ties_pending && ctx->pinned[6]) {
         // an executeAt equals another timestamp: the sorted-batch ranks are not dense ranks; the general dictionary,
@@ -3311,25 +3352,21 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     Sorted bcs = radix_sort(ctx, "rs_bc", cols.bc_key, nullptr, nbc, segbits + rbits);
     uint32_t *bcs_exec = ctx->get<uint32_t>("v2_bcs_exec", nbc);
     uint64_t *bcs_lw_in = ctx->get<uint64_t>("v2_bcs_lw_in64", nbc), *bcs_lw64 = ctx->get<uint64_t>("v2_bcs_lastw64", nbc);
-    uint32_t *bcs_lastw = ctx->get<uint32_t>("v2_bcs_lastw", nbc);
     launch(ctx, "v2_bcs_cols", k_v2_bcs_cols, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, nbc, (const uint64_t *)bcs.keys,
            (const uint32_t *)bcs.vals, (const uint8_t *)cols.bc_kind, (uint64_t)((1ull << rbits) - 1), bcs_exec, bcs_lw_in);
     uint64_t *bc_pm64 = ctx->get<uint64_t>("v2_bc_pm64", nbc);
-    uint32_t *bc_pm = ctx->get<uint32_t>("v2_bc_pm", nbc);
-    {   // nearest-Write index and the segmented executeAt maximum: two prefix maxima in one launch, then both to u32
+    {   // nearest-Write index and the segmented executeAt maximum: two prefix maxima in one launch (read as low words)
         const uint64_t *si[2] = { bcs_lw_in, cols.bc_pm_in };
         uint64_t *so[2] = { bcs_lw64, bc_pm64 };
         const size_t sn[2] = { nbc, nbc };
         scan_multi<uint64_t, OpMax<uint64_t>>(ctx, 2, si, so, sn, false, (uint64_t *const *)nullptr);
     }
-    launch(ctx, "low32", k_low32x2, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, (size_t)nbc, (const uint64_t *)bcs_lw64,
-           bcs_lastw, (const uint64_t *)bc_pm64, bc_pm);
 
     V2View vv;
     vv.perm = ps.vals; vv.pair_pos = pair_pos; vv.seg_incl = seg_incl; vv.seg_start = seg_start;
     vv.s_rank = s_rank; vv.s_exec = s_exec; vv.s_info = s_info; vv.rdir = cols.rdir; vv.tinfo = tinfo;
-    vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm;
-    vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lastw;
+    vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm64;
+    vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lw64;
 
     // ---- count pass: per-pair records, big-txn flags, E
     if (P >= 0x80000000ull) fail(ACC_E_CAP, "n_pairs must be < 2^31 (count-pass record format)");
@@ -3351,14 +3388,15 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
+    uint64_t *eb = ctx->get<uint64_t>("v3_eb", n), *dB = ctx->get<uint64_t>("v3_dB", (size_t)n + 1);
     launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, vv.irec32, (const uint4 *)rec, psz, raw_cap,
-           e_cap, bigflag, szA, szK, tot + 2);
+           e_cap, bigflag, szA, szK, tot + 2, eb);
     uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
-    {   // arena / key offsets and the count pass's per-block entry totals: one launch
-        const uint64_t *si[3] = { szA, szK, blk_e };
-        uint64_t *so[3] = { arena_off, kd_off, blk_pre }, *stot[3] = { arena_off + n, kd_off + n, tot };
-        const size_t sn[3] = { n, n, gP };
-        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 3, si, so, sn, true, stot);
+    {   // arena / key offsets, the count pass's per-block entry totals, the big txns' TxnId scratch bases: one launch
+        const uint64_t *si[4] = { szA, szK, blk_e, eb };
+        uint64_t *so[4] = { arena_off, kd_off, blk_pre, dB }, *stot[4] = { arena_off + n, kd_off + n, tot, dB + n };
+        const size_t sn[4] = { n, n, gP, n };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 4, si, so, sn, true, stot);
     }
     // the big-txn list in txn order (k_v3_bigfill's per-txn ranges abut: a big txn writes its end where the next
     // txn's first pair starts, equal values when the next txn is big too)
@@ -3402,10 +3440,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     // ---- big txns: v2 tiers, headers / key indices / entries into the final arrays, TxnIds into scratch
     if (nbig) {
         const unsigned gB = (nbig + WAVES - 1) / WAVES;
-        uint64_t *lE = ctx->get<uint64_t>("v3_lE", nbig);
-        launch(ctx, "v3_bigsz", k_v3_bigsz, dim3(gB), dim3(BLOCK), 0, nbig, (const uint32_t *)blist, key_off, (const uint32_t *)psz, lE);
-        uint64_t *dB = ctx->get<uint64_t>("v3_dB", (size_t)nbig + 1);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, lE, dB, nbig, true, dB + nbig);
         vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
         vcnt = ctx->get<uint64_t>("cnt", P);
         uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
@@ -3419,7 +3453,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         const bool big_ok = rbits + 6 <= 31;
         win_ok = big_ok && !getenv("ACC_NO_WIN");   // tuning switch: the sorting tiers instead of the window tier
         launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
-               key_off, (const uint64_t *)lE, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
+               key_off, (const uint64_t *)eb, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
                ctx->get<uint32_t>("v2_w8_list", nbig), ctx->get<uint32_t>("v2_w16_list", nbig), gstat);
         launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
         wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = arena_off; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;

@@ -771,6 +771,20 @@ typedef struct acc_cfk_batch_view {
 
 int  acc_cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *snap, acc_cfk_batch_view *out_view);
 
+/* One CommandsForKey store for the update with deps and every scan (the reference keeps one
+ * CommandsForKey per key that CommandsForKey.update writes and mapReduceActive / mapReduceFull read,
+ * local/CommandsForKey.java:614-706, 1085-1149): acc_cfk_apply_deps applies a batch of updates with deps to the acc_cfk
+ * store itself — acc_cfk_apply over the store's key-major state, then the store's txn-major view and its per-pair
+ * missing[] as txn indices rebuilt from the result — so acc_cfk_view (acc_keydeps_batch, acc_shard_pack), acc_cfk_missing
+ * (acc_map_reduce_full: its batch and acc_recovery_in's missing_off / missing_txn with mem = ACC_MEM_DEVICE) and
+ * acc_cfk_state (the key-major state in the acc_cfk_apply layout, DEVICE memory) read one state in place, valid until
+ * the next update of the store. A rejected batch (ACC_E_STATE / ACC_E_ARG) leaves the store unchanged. A store keeps
+ * missing[] from its first acc_cfk_apply_deps on; acc_cfk_update (status-only, no missing[]) is then ACC_E_STATE, and
+ * acc_cfk_apply_deps on a store holding acc_cfk_update state is ACC_E_STATE. */
+int  acc_cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *updates);
+int  acc_cfk_state(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_snap *out);
+int  acc_cfk_missing(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_batch_view *out);
+
 /* ---- MaxConflicts and the PreAccept executeAt proposal (local/MaxConflicts.java:31-96,
  * local/CommandStore.java:280-290 updateMaxConflicts, :320-345 preaccept) ----
  * A CommandStore's MaxConflicts is the pointwise max of every (keysOrRanges, executeAt) update it received

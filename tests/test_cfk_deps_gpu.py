@@ -262,3 +262,54 @@ def test_cfk_snap_to_batch_errors(ctx):
     with pytest.raises(IllegalArgumentException):
         cfk_snap_to_batch(ctx, bad)
     assert cfk_snap_to_batch(ctx, snap).batch.n_txn == ok.batch.n_txn   # the context stays usable
+
+
+def test_cfk_store_one_state(ctx):
+    """One device CommandsForKey store for the update with deps and every scan (acc_cfk_apply_deps; the reference's
+    one CommandsForKey per key, local/CommandsForKey.java:614-706, 1085-1149): three chained batches applied to the
+    store; after each, its key-major state equals the C restatement over all updates so far, its txn-major view and
+    missing[] indices equal the host restatement of that state, and calculatePartialDeps / mapReduceFull read the store
+    in place with the same results as the host batch."""
+    import recovery_cases as RC
+    from accord_amd.deps import CfkStore, IllegalStateException, cfk_batch_host, cfk_map_reduce_full
+    upd = CC.cfk_case(9, n_txn=700, n_keys=30)
+    n = len(upd["msb"])
+    cuts = [0, n // 3, 2 * n // 3, n]
+    st = CfkStore(ctx)
+    try:
+        rest, done = upd, 0
+        for c in cuts[1:]:
+            part, rest = CC.split_updates(rest, c - done)
+            done = c
+            st.apply_deps(part)
+            head, _ = CC.split_updates(upd, c)
+            o = oracle.cfk_apply(CC.empty_snapshot(), head)
+            same(st.state(), o, f"state after {c}")
+            b, mo, mt = CC.snap_as_batch(o)
+            gb, gmo, gmt = cfk_batch_host(ctx, st.missing_view())
+            for f in ("txn_msb", "txn_lsb", "txn_node", "exe_msb", "exe_lsb", "exe_node", "status", "key_off", "key_code"):
+                np.testing.assert_array_equal(getattr(gb, f), getattr(b, f), err_msg=f"{c} {f}")
+            np.testing.assert_array_equal(gmo, mo)
+            np.testing.assert_array_equal(gmt, mt)
+            g = st.calculate_partial_deps()
+            r = ctx.calculate_partial_deps(b)
+            for f in FIELDS:
+                np.testing.assert_array_equal(getattr(g, f), getattr(r, f), err_msg=f"keydeps {c} {f}")
+            q = CC.recovery_queries(b, c, 60)
+            for sa, td, ts in RC.ALL_TESTS[::3]:
+                g = cfk_map_reduce_full(ctx, st.missing_view(), q, sa, td, ts)
+                o2 = oracle.map_reduce_full(b, mo, mt, q, sa, td, ts)
+                for f in FIELDS:
+                    np.testing.assert_array_equal(getattr(g, f), getattr(o2, f), err_msg=f"recovery {c} {f} {(sa, td, ts)}")
+        # a rejected batch leaves the store as it was; status-only updates are refused on a store holding missing[]
+        before = st.state()
+        back = {k: v.copy() for k, v in CC.split_updates(upd, 40)[0].items()}
+        back["status"][:] = CC.PRE
+        back["flags"][:] = 0
+        with pytest.raises(IllegalStateException):
+            st.apply_deps(back)
+        same(st.state(), before, "after a rejected batch")
+        with pytest.raises(IllegalStateException):
+            st.update(b)
+    finally:
+        st.close()
