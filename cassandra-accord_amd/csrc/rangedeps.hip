@@ -149,8 +149,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, co
                                                       const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
                                                       const uint4 *__restrict__ tinfo, const uint64_t *__restrict__ tl,
                                                       Runs rs_plan, Runs re_plan, int e_bits, int split,
-                                                      uint64_t *__restrict__ e_s, uint64_t *__restrict__ e_e,
-                                                      uint32_t *__restrict__ e_rank, uint8_t *__restrict__ e_kind,
+                                                      uint64_t *__restrict__ e_s, uint4 *__restrict__ erec,
                                                       uint64_t *__restrict__ dkey, uint64_t *__restrict__ ekey)
 {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
@@ -158,9 +157,10 @@ __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, co
     const uint32_t i = eidx[j], t = rowner[j];
     const uint64_t s = rs[j], e = re[j];
     e_s[i] = s;
-    e_e[i] = e;
-    e_rank[i] = tinfo[t].y;   // TxnId position of the range command
-    e_kind[i] = (uint8_t)((tl[t] >> 1) & 7u);
+    // the entry's 32-B record: start, end | TxnId position, kind, range id (k_rd_dict_write) — the permuted reads of
+    // the dictionary and class passes take one record per entry instead of a line per column
+    erec[2 * (size_t)i] = make_uint4((uint32_t)s, (uint32_t)(s >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+    erec[2 * (size_t)i + 1] = make_uint4(tinfo[t].y, (uint32_t)((tl[t] >> 1) & 7u), 0u, 0u);
     const uint64_t sc = pext_runs(s, rs_plan), ec = pext_runs(e, re_plan);
     if (split) { dkey[i] = sc; ekey[i] = ec; }      // two-key LSD: end first, then start (stable)
     else dkey[i] = (sc << e_bits) | ec;
@@ -168,23 +168,21 @@ __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, co
 
 // rid per (start, end)-sorted position; dictionary arrays
 __global__ __launch_bounds__(BLOCK) void k_rd_dict_flags(uint32_t ne, const uint32_t *__restrict__ perm,
-                                                         const uint64_t *__restrict__ e_s, const uint64_t *__restrict__ e_e,
-                                                         uint32_t *__restrict__ flag)
+                                                         const uint4 *__restrict__ erec, uint32_t *__restrict__ flag)
 {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= ne) return;
     uint32_t f = 1;
     if (p > 0) {
-        const uint32_t a = perm[p], b = perm[p - 1];
-        f = e_s[a] != e_s[b] || e_e[a] != e_e[b];
+        const uint4 a = erec[2 * (size_t)perm[p]], b = erec[2 * (size_t)perm[p - 1]];
+        f = a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w;
     }
     flag[p] = f;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint32_t *__restrict__ perm,
                                                          const uint32_t *__restrict__ flag, const uint32_t *__restrict__ incl,
-                                                         const uint64_t *__restrict__ e_s, const uint64_t *__restrict__ e_e,
-                                                         uint32_t *__restrict__ rid_of, uint64_t *__restrict__ dict_s,
+                                                         uint4 *__restrict__ erec, uint64_t *__restrict__ dict_s,
                                                          uint64_t *__restrict__ dict_e, Runs rs_plan, int s_bits, int cls_only,
                                                          uint64_t *__restrict__ ckey, uint32_t *__restrict__ cls_hist)
 {
@@ -192,13 +190,28 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint
     if (threadIdx.x < NCLS) h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t c = 0xFFu;
     if (p < ne) {
         const uint32_t i = perm[p], rid = incl[p] - 1;
-        rid_of[i] = rid;
-        if (flag[p]) { dict_s[rid] = e_s[i]; dict_e[rid] = e_e[i]; }
-        const uint32_t c = width_class(e_s[i], e_e[i]);
-        ckey[i] = cls_only ? (uint64_t)c : (((uint64_t)c << s_bits) | pext_runs(e_s[i], rs_plan));
-        atomicAdd(&h[c], 1u);   // LDS histogram; one global atomic per class and block (33 hot words otherwise)
+        const uint4 a = erec[2 * (size_t)i];
+        const uint64_t es = ((uint64_t)a.y << 32) | a.x, ee = ((uint64_t)a.w << 32) | a.z;
+        reinterpret_cast<uint32_t *>(erec + 2 * (size_t)i + 1)[2] = rid;   // the entry's range id
+        if (flag[p]) { dict_s[rid] = es; dict_e[rid] = ee; }
+        c = width_class(es, ee);
+        ckey[i] = cls_only ? (uint64_t)c : (((uint64_t)c << s_bits) | pext_runs(es, rs_plan));
+    }
+    // LDS histogram, one add per distinct class of a wave (per-thread atomics on a few hot words serialise); one global
+    // atomic per class and block
+    {
+        const uint32_t lane = lane_id();
+        uint64_t rem = __ballot(c != 0xFFu);
+        while (rem) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(rem);
+            const uint32_t c0 = (uint32_t)__shfl((int)c, (int)leader, 64);
+            const uint64_t m = __ballot(c == c0) & rem;
+            if (lane == leader) atomicAdd(&h[c0], (uint32_t)__popcll(m));
+            rem &= ~m;
+        }
     }
     __syncthreads();
     if (threadIdx.x < NCLS && h[threadIdx.x]) atomicAdd(&cls_hist[threadIdx.x], h[threadIdx.x]);
@@ -214,19 +227,18 @@ __global__ void k_rd_class_off(const uint32_t *__restrict__ hist, uint32_t *__re
 
 // class-sorted entry columns
 __global__ __launch_bounds__(BLOCK) void k_rd_class_cols(uint32_t ne, const uint32_t *__restrict__ perm,
-                                                         const uint64_t *__restrict__ e_s, const uint64_t *__restrict__ e_e,
-                                                         const uint32_t *__restrict__ e_rank, const uint8_t *__restrict__ e_kind,
-                                                         const uint32_t *__restrict__ rid_of, uint64_t *__restrict__ cs_s,
+                                                         const uint4 *__restrict__ erec, uint64_t *__restrict__ cs_s,
                                                          uint64_t *__restrict__ cs_e, uint2 *__restrict__ cs_info,
                                                          uint8_t *__restrict__ cs_kind)
 {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= ne) return;
     const uint32_t i = perm[p];
-    cs_s[p] = e_s[i];
-    cs_e[p] = e_e[i];
-    cs_info[p] = make_uint2(rid_of[i], e_rank[i]);
-    cs_kind[p] = e_kind[i];
+    const uint4 a = erec[2 * (size_t)i], b = erec[2 * (size_t)i + 1];
+    cs_s[p] = ((uint64_t)a.y << 32) | a.x;
+    cs_e[p] = ((uint64_t)a.w << 32) | a.z;
+    cs_info[p] = make_uint2(b.z, b.x);   // (range id, TxnId position)
+    cs_kind[p] = (uint8_t)b.y;
 }
 
 // ---------------------------------------------------------------- txn columns
@@ -661,38 +673,45 @@ __device__ __forceinline__ void txn_queries(const Out &o, uint32_t t, uint32_t &
 
 __device__ __forceinline__ uint32_t dep_of(const Out &o, uint32_t tpos) { return o.txn_of_tpos ? o.txn_of_tpos[tpos] : tpos; }
 
-__global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t *__restrict__ m_raw, uint32_t *__restrict__ tier)
+// per txn: raw entry count and tier; the tier counts of the batch (hist, zeroed before) by one ballot per tier value
+// and wave and one global add per tier and block (a per-thread LDS atomic on 12 addresses serialised)
+constexpr int RD_TIERS = 12;
+__global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t *__restrict__ m_raw, uint32_t *__restrict__ tier,
+                                                    uint32_t *__restrict__ hist)
 {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= n) return;
-    uint32_t q0, q1;
-    txn_queries(o, t, q0, q1);
-    uint64_t m = 0;
-    for (uint32_t q = q0; q < q1; ++q) m += o.q_cnt[q];
-    m_raw[t] = m;
-    // tiers: 0 none, 1 <= 16 (16-lane groups), 11 <= 32 (half waves), 2 <= 64 (wave), 3..9 LDS workgroups of
-    // 128..8192, 10 global
-    uint32_t tr;
-    if (m == 0) tr = 0;
-    else if (m <= 16) tr = 1;
-    else if (m <= 32) tr = 11;
-    else if (m <= 64) tr = 2;
-    else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
-    else tr = 10;
-    tier[t] = tr;
-    if (m == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
+    __shared__ uint32_t h[WAVES][RD_TIERS];
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x, w = threadIdx.x >> 6, lane = lane_id();
+    uint32_t tr = 0xFFu;
+    if (t < n) {
+        uint32_t q0, q1;
+        txn_queries(o, t, q0, q1);
+        uint64_t m = 0;
+        for (uint32_t q = q0; q < q1; ++q) m += o.q_cnt[q];
+        m_raw[t] = m;
+        // tiers: 0 none, 1 <= 16 (16-lane groups), 11 <= 32 (half waves), 2 <= 64 (wave), 3..9 LDS workgroups of
+        // 128..8192, 10 global
+        if (m == 0) tr = 0;
+        else if (m <= 16) tr = 1;
+        else if (m <= 32) tr = 11;
+        else if (m <= 64) tr = 2;
+        else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
+        else tr = 10;
+        tier[t] = tr;
+        if (m == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
+    }
+#pragma unroll
+    for (int v = 0; v < RD_TIERS; ++v) {
+        const uint32_t c = (uint32_t)__popcll(__ballot(tr == (uint32_t)v));
+        if (lane == 0) h[w][v] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < RD_TIERS) {
+        uint32_t c = 0;
+        for (int q = 0; q < WAVES; ++q) c += h[q][threadIdx.x];
+        if (c) atomicAdd(&hist[threadIdx.x], c);
+    }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rd_tier_hist(uint32_t n, const uint32_t *__restrict__ tier, uint32_t *__restrict__ hist)
-{
-    __shared__ uint32_t h[16];
-    if (threadIdx.x < 16) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t < n) atomicAdd(&h[tier[t]], 1u);
-    __syncthreads();
-    if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
-}
 
 // bitonic sort within lane groups of S (lane-aligned: the xor partners stay inside), ascending
 template <int S, class T>
@@ -1097,14 +1116,13 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
 
     // ---- 2. range-command entries, stored-range dictionary, class order
     const Runs rs_plan = make_runs(hm[0]), re_plan = make_runs(hm[1]);
-    uint64_t *e_s = ctx->get<uint64_t>("rd_e_s", NE), *e_e = ctx->get<uint64_t>("rd_e_e", NE);
-    uint32_t *e_rank = ctx->get<uint32_t>("rd_e_rank", NE);
-    uint8_t *e_kind = ctx->get<uint8_t>("rd_e_kind", NE);
+    uint64_t *e_s = ctx->get<uint64_t>("rd_e_s", NE);
+    uint4 *erec = ctx->get<uint4>("rd_erec", 2 * (size_t)NE);
     uint64_t *dkey = ctx->get<uint64_t>("rd_dkey", NE), *ekey = ctx->get<uint64_t>("rd_ekey", NE);
     const bool split = rs_plan.bits + re_plan.bits > 64;
     launch(ctx, "rd_entries", k_rd_entries, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, n, (const uint32_t *)eflag,
            (const uint32_t *)eidx, (const uint32_t *)rowner, rs, re, (const uint4 *)tinfo, tl, rs_plan, re_plan, re_plan.bits,
-           split ? 1 : 0, e_s, e_e, e_rank, e_kind, dkey, ekey);
+           split ? 1 : 0, e_s, erec, dkey, ekey);
     Sorted ds;
     if (!split) {
         ds = radix_sort(ctx, "rs_rd_dict", dkey, nullptr, NE, rs_plan.bits + re_plan.bits);
@@ -1118,9 +1136,8 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     }
     uint32_t *dflag = ctx->get<uint32_t>("rd_dflag", NE), *dincl = ctx->get<uint32_t>("rd_dincl", NE + 1);
     launch(ctx, "rd_dict_flags", k_rd_dict_flags, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, NE, (const uint32_t *)ds.vals,
-           (const uint64_t *)e_s, (const uint64_t *)e_e, dflag);
+           (const uint4 *)erec, dflag);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, dflag, dincl, NE, false, dincl + NE);
-    uint32_t *rid_of = ctx->get<uint32_t>("rd_rid_of", NE);
     uint64_t *dict_s = ctx->get<uint64_t>("rd_dict_s", NE), *dict_e = ctx->get<uint64_t>("rd_dict_e", NE);
     uint64_t *ckey = ctx->get<uint64_t>("rd_ckey", NE);
     uint32_t *cls = ctx->get<uint32_t>("rd_cls", 2 * (NCLS + 1));
@@ -1128,7 +1145,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     ACC_HIP(hipMemsetAsync(cls_hist, 0, (NCLS + 1) * sizeof(uint32_t), st));
     const bool csplit = rs_plan.bits + 6 > 64;
     launch(ctx, "rd_dict_write", k_rd_dict_write, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, NE, (const uint32_t *)ds.vals,
-           (const uint32_t *)dflag, (const uint32_t *)dincl, (const uint64_t *)e_s, (const uint64_t *)e_e, rid_of, dict_s,
+           (const uint32_t *)dflag, (const uint32_t *)dincl, erec, dict_s,
            dict_e, rs_plan, rs_plan.bits, csplit ? 1 : 0, ckey, cls_hist);
     launch(ctx, "rd_class_off", k_rd_class_off, dim3(1), dim3(64), 0, (const uint32_t *)cls_hist, class_off);
     Sorted cs;
@@ -1149,8 +1166,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint2 *cs_info = ctx->get<uint2>("rd_cs_info", NE);
     uint8_t *cs_kind = ctx->get<uint8_t>("rd_cs_kind", NE);
     launch(ctx, "rd_class_cols", k_rd_class_cols, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, NE, (const uint32_t *)cs.vals,
-           (const uint64_t *)e_s, (const uint64_t *)e_e, (const uint32_t *)e_rank, (const uint8_t *)e_kind,
-           (const uint32_t *)rid_of, cs_s, cs_e, cs_info, cs_kind);
+           (const uint4 *)erec, cs_s, cs_e, cs_info, cs_kind);
 
     // ---- 3. query records sorted by low bound; stabbing (one pass, block-sliced output)
     const Runs q_plan = make_runs(hm[2]);
@@ -1213,12 +1229,11 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint64_t *m_raw = ctx->get<uint64_t>("rd_m_raw", n);
     uint32_t *tier = ctx->get<uint32_t>("rd_tier", n);
     uint64_t *raw_off = ctx->get<uint64_t>("rd_raw_off", (size_t)n + 1);
-    launch(ctx, "rd_tsize", k_rd_tsize, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, o, m_raw, tier);
-    scan<uint64_t, OpAdd<uint64_t>>(ctx, m_raw, raw_off, n, true, raw_off + n);
-    o.raw_off = raw_off;
     uint32_t *thist = ctx->get<uint32_t>("rd_thist", 16);
     ACC_HIP(hipMemsetAsync(thist, 0, 16 * sizeof(uint32_t), st));
-    launch(ctx, "rd_tier_hist", k_rd_tier_hist, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)tier, thist);
+    launch(ctx, "rd_tsize", k_rd_tsize, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, o, m_raw, tier, thist);
+    scan<uint64_t, OpAdd<uint64_t>>(ctx, m_raw, raw_off, n, true, raw_off + n);
+    o.raw_off = raw_off;
     // txns grouped by tier: one 8-bit radix pass (stable)
     uint64_t *tkey = ctx->get<uint64_t>("rd_tkey", n);
     launch(ctx, "rd_widen", k_widen_u32, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, (size_t)n, (const uint32_t *)tier, tkey);
