@@ -4205,32 +4205,72 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
     }
     if (tid == 0) { ao[nt] = o.arena_off[t0 + nt]; ko[nt] = o.kd_off[t0 + nt]; uo[nt] = o.u_off[t0 + nt]; }
     __syncthreads();
-    for (uint64_t j = ao[0] + tid; j < ao[nt]; j += BLOCK) {
-        const uint32_t a = last_le(ao, nt, j);
-        const uint64_t i = j - ao[a];
-        const uint32_t kd = kdn[a];
-        int32_t v;
-        if (kd == 0xFFFFFFFFu) v = kv.arena[sa[a] + i];
-        else if (i < kd) v = (int32_t)(kd + (x.kx_end[sk[a] + i] - (uint32_t)sa[a]));
-        else v = (int32_t)idx_of_e[sa[a] + i - kd];
-        o.arena[j] = v;
-    }
-    for (uint64_t j = ko[0] + tid; j < ko[nt]; j += BLOCK) {
-        const uint32_t a = last_le(ko, nt, j);
-        const uint64_t i = j - ko[a];
-        if (kdn[a] == 0xFFFFFFFFu) {
-            const uint32_t ki = kv.key_idx[sk[a] + i];
-            o.key_idx[j] = ki;
-            o.kd_key[j] = key_code[kofs[a] + ki];
-        } else {
-            o.key_idx[j] = x.kx_idx[sk[a] + i];
-            o.kd_key[j] = x.kx_code[sk[a] + i];
+    // U outputs per thread per round: independent LDS searches and source loads overlap (one dependent chain of ~8 LDS
+    // round trips + a gather per output otherwise)
+    constexpr int U = 4;
+    for (uint64_t j0 = ao[0] + tid; j0 < ao[nt]; j0 += (uint64_t)U * BLOCK) {
+        int32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            v[u] = 0;
+            if (j < ao[nt]) {
+                const uint32_t a = last_le(ao, nt, j);
+                const uint64_t i = j - ao[a];
+                const uint32_t kd = kdn[a];
+                if (kd == 0xFFFFFFFFu) v[u] = kv.arena[sa[a] + i];
+                else if (i < kd) v[u] = (int32_t)(kd + (x.kx_end[sk[a] + i] - (uint32_t)sa[a]));
+                else v[u] = (int32_t)idx_of_e[sa[a] + i - kd];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            if (j < ao[nt]) o.arena[j] = v[u];
         }
     }
-    for (uint64_t j = uo[0] + tid; j < uo[nt]; j += BLOCK) {
-        const uint32_t a = last_le(uo, nt, j);
-        const uint64_t i = j - uo[a];
-        o.dep_txn[j] = kdn[a] == 0xFFFFFFFFu ? kv.dep_txn[su[a] + i] : dep_scr[su[a] + i];
+    for (uint64_t j0 = ko[0] + tid; j0 < ko[nt]; j0 += (uint64_t)U * BLOCK) {
+        uint32_t ki[U];
+        uint64_t kc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            ki[u] = 0; kc[u] = 0;
+            if (j < ko[nt]) {
+                const uint32_t a = last_le(ko, nt, j);
+                const uint64_t i = j - ko[a];
+                if (kdn[a] == 0xFFFFFFFFu) {
+                    ki[u] = kv.key_idx[sk[a] + i];
+                    kc[u] = key_code[kofs[a] + ki[u]];
+                } else {
+                    ki[u] = x.kx_idx[sk[a] + i];
+                    kc[u] = x.kx_code[sk[a] + i];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            if (j < ko[nt]) { o.key_idx[j] = ki[u]; o.kd_key[j] = kc[u]; }
+        }
+    }
+    for (uint64_t j0 = uo[0] + tid; j0 < uo[nt]; j0 += (uint64_t)U * BLOCK) {
+        uint32_t d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            d[u] = 0;
+            if (j < uo[nt]) {
+                const uint32_t a = last_le(uo, nt, j);
+                const uint64_t i = j - uo[a];
+                d[u] = kdn[a] == 0xFFFFFFFFu ? kv.dep_txn[su[a] + i] : dep_scr[su[a] + i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            if (j < uo[nt]) o.dep_txn[j] = d[u];
+        }
     }
 }
 

@@ -970,13 +970,29 @@ __global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, Out o, uint
 // each output array: a thread per output element finds its txn among the block's offsets in LDS and copies from that
 // txn's scratch, so every write (and most reads) is a whole-line access.
 __device__ __forceinline__ void compact_array(uint32_t nt, const uint64_t *off, const uint64_t *src_base,
-                                              const uint32_t *src, uint32_t *dst)
+                                              const uint32_t *__restrict__ src, uint32_t *__restrict__ dst)
 {
-    const uint64_t j0 = off[0], j1 = off[nt];
-    for (uint64_t j = j0 + threadIdx.x; j < j1; j += BLOCK) {
-        uint32_t lo = 0, hi = nt;   // last txn k with off[k] <= j
-        while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (off[md] <= j) lo = md; else hi = md; }
-        dst[j] = src[src_base[lo] + (j - off[lo])];
+    // U outputs per thread per round: their LDS searches and source loads are independent, so they overlap instead of
+    // one dependent chain (8 LDS round trips, then the gather) per output
+    constexpr int U = 4;
+    const uint64_t j1 = off[nt];
+    for (uint64_t j0 = off[0] + threadIdx.x; j0 < j1; j0 += (uint64_t)U * BLOCK) {
+        uint32_t x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            x[u] = 0;
+            if (j < j1) {
+                uint32_t lo = 0, hi = nt;   // last txn k with off[k] <= j
+                while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (off[md] <= j) lo = md; else hi = md; }
+                x[u] = src[src_base[lo] + (j - off[lo])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            if (j < j1) dst[j] = x[u];
+        }
     }
 }
 
