@@ -3925,39 +3925,57 @@ constexpr uint32_t MX_MID_E = 512, MX_BLK_E = 4096;
 struct MxLists {
     uint32_t *l[5];   // 16, 32, 64, mid, block
 };
+// MX_RT chunks of BLOCK txns per workgroup: one list-counter add per list and workgroup (the five counters share one
+// line: per-256-txn adds serialised there); list order is free (each txn writes its own outputs)
+constexpr int MX_RT = 16;
 __global__ __launch_bounds__(BLOCK) void k_mx_route(uint32_t n, const uint64_t *__restrict__ etoff, MxLists L,
                                                     uint64_t *__restrict__ gst)
 {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    int c = -1;
-    if (t < n) {
-        const uint64_t E = etoff[t + 1] - etoff[t];
-        if (E == 0) c = -1;
-        else if (E <= 16) c = 0;
-        else if (E <= 32) c = 1;
-        else if (E <= 64) c = 2;
-        else if (E <= MX_MID_E) c = 3;
-        else if (E <= MX_BLK_E) c = 4;
-        else { c = -1; atomicOr((unsigned long long *)&gst[1], 1ull); }
-    }
-    __shared__ uint32_t wcnt[5][WAVES], base[5];
+    __shared__ uint32_t wcnt[5][MX_RT * WAVES], base[5];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint64_t bal[5];
+    int cs[MX_RT];
+    bool ovf = false;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        bal[k] = __ballot(c == k);
-        if (lane == 0) wcnt[k][w] = (uint32_t)__popcll(bal[k]);
+    for (int r = 0; r < MX_RT; ++r) {
+        const uint32_t t = (blockIdx.x * MX_RT + (uint32_t)r) * BLOCK + threadIdx.x;
+        int c = -1;
+        if (t < n) {
+            const uint64_t E = etoff[t + 1] - etoff[t];
+            if (E == 0) c = -1;
+            else if (E <= 16) c = 0;
+            else if (E <= 32) c = 1;
+            else if (E <= 64) c = 2;
+            else if (E <= MX_MID_E) c = 3;
+            else if (E <= MX_BLK_E) c = 4;
+            else ovf = true;
+        }
+        cs[r] = c;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t cnt = (uint32_t)__popcll(__ballot(c == k));
+            if (lane == 0) wcnt[k][r * WAVES + w] = cnt;
+        }
     }
+    if (ovf) atomicOr((unsigned long long *)&gst[1], 1ull);
     __syncthreads();
     if (threadIdx.x < 5) {
         uint32_t tot = 0;
-        for (int q = 0; q < WAVES; ++q) { const uint32_t x = wcnt[threadIdx.x][q]; wcnt[threadIdx.x][q] = tot; tot += x; }
+        for (int q = 0; q < MX_RT * WAVES; ++q) { const uint32_t x = wcnt[threadIdx.x][q]; wcnt[threadIdx.x][q] = tot; tot += x; }
         const int slot = threadIdx.x == 4 ? 0 : threadIdx.x == 3 ? 2 : 3 + (int)threadIdx.x;
         base[threadIdx.x] = tot ? (uint32_t)atomicAdd((unsigned long long *)&gst[slot], (unsigned long long)tot) : 0u;
     }
     __syncthreads();
-    if (c >= 0) L.l[c][base[c] + wcnt[c][w] + (uint32_t)__popcll(bal[c] & lt)] = t;
+#pragma unroll
+    for (int r = 0; r < MX_RT; ++r) {
+        const int c = cs[r];
+        const uint32_t t = (blockIdx.x * MX_RT + (uint32_t)r) * BLOCK + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint64_t bal = __ballot(c == k);
+            if (c == k) L.l[k][base[k] + wcnt[k][r * WAVES + w] + (uint32_t)__popcll(bal & lt)] = t;
+        }
+    }
 }
 
 // groups of S lanes (S = 16, 32, 64), one listed txn each (E <= S): register bitonic of (rank << 32 | local entry)
@@ -4430,7 +4448,8 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
         uint32_t *const mid_list = L.l[3], *const blk_list = L.l[4];
         uint64_t *gst = ctx->get<uint64_t>("mx_gst", 6);
         ACC_HIP(hipMemsetAsync(gst, 0, 48, st));
-        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, L, gst);
+        launch(ctx, "mx_route", k_mx_route, dim3(grid_for(n, (size_t)BLOCK * MX_RT)), dim3(BLOCK), 0, n, (const uint64_t *)etoff, L,
+               gst);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gst, 48, hipMemcpyDeviceToHost, st));
         ctx->sync();
         const uint64_t nblk = ctx->pinned[0], nmid = ctx->pinned[2];

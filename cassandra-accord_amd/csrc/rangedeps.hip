@@ -29,6 +29,7 @@ namespace acc {
 
 namespace rd {
 
+constexpr int RD_TS = 16;         // chunks of BLOCK txns per workgroup in the per-txn passes with global counters
 constexpr int NCLS = 33;          // width classes 0..32 (4^32 = 2^64 covers every u64 width)
 #ifndef ACC_RD_TILE
 #define ACC_RD_TILE 256
@@ -100,8 +101,10 @@ __global__ __launch_bounds__(BLOCK) void k_rd_prep(uint32_t n, const uint64_t *_
                                                    uint64_t ref_lo, uint32_t *__restrict__ rowner,
                                                    uint32_t *__restrict__ eflag, uint64_t *__restrict__ g)
 {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     uint64_t ms = 0, me = 0, ml = 0, errs = 0;
+    // RD_TS chunks of BLOCK txns per workgroup: one OR per word and workgroup into g (its 4 words share one line)
+    for (int r = 0; r < RD_TS; ++r) {
+    const uint32_t t = (blockIdx.x * RD_TS + (uint32_t)r) * BLOCK + threadIdx.x;
     if (t < n) {
         const bool isr = (tl[t] & 1u) != 0;
         const uint32_t k0 = key_off[t], k1 = key_off[t + 1];
@@ -123,7 +126,14 @@ __global__ __launch_bounds__(BLOCK) void k_rd_prep(uint32_t n, const uint64_t *_
             }
         }
         if (k1 >= k0)
-            for (uint32_t j = k0; j < k1; ++j) ml |= key_code[j] ^ ref_lo;
+            for (uint32_t jb = k0; jb < k1; jb += 8) {   // eight key loads in flight
+                uint64_t kc[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kc[u] = jb + u < k1 ? key_code[jb + u] ^ ref_lo : 0ull;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ml |= kc[u];
+            }
+    }
     }
     __shared__ uint64_t part[WAVES][4];
     uint64_t v[4] = { ms, me, ml, errs };
@@ -189,7 +199,9 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint
     __shared__ uint32_t h[NCLS];
     if (threadIdx.x < NCLS) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    // RD_TS chunks of BLOCK entries per workgroup: one global add per class and workgroup (the 33 counters share two lines)
+    for (int r = 0; r < RD_TS; ++r) {
+    const uint32_t p = (blockIdx.x * RD_TS + (uint32_t)r) * BLOCK + threadIdx.x;
     uint32_t c = 0xFFu;
     if (p < ne) {
         const uint32_t i = perm[p], rid = incl[p] - 1;
@@ -212,6 +224,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint
             if (lane == leader) atomicAdd(&h[c0], (uint32_t)__popcll(m));
             rem &= ~m;
         }
+    }
     }
     __syncthreads();
     if (threadIdx.x < NCLS && h[threadIdx.x]) atomicAdd(&cls_hist[threadIdx.x], h[threadIdx.x]);
@@ -673,37 +686,48 @@ __device__ __forceinline__ void txn_queries(const Out &o, uint32_t t, uint32_t &
 
 __device__ __forceinline__ uint32_t dep_of(const Out &o, uint32_t tpos) { return o.txn_of_tpos ? o.txn_of_tpos[tpos] : tpos; }
 
-// per txn: raw entry count and tier; the tier counts of the batch (hist, zeroed before) by one ballot per tier value
-// and wave and one global add per tier and block (a per-thread LDS atomic on 12 addresses serialised)
+// per txn: raw entry count and tier; the tier counts of the batch (hist, zeroed before): one ballot per tier value and
+// wave, summed over RD_TS chunks of BLOCK txns per workgroup, one global add per tier and workgroup (the 12 counters
+// share one line: per-256-txn adds serialised there, and per-thread LDS atomics on 12 words before that)
 constexpr int RD_TIERS = 12;
 __global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t *__restrict__ m_raw, uint32_t *__restrict__ tier,
                                                     uint32_t *__restrict__ hist)
 {
     __shared__ uint32_t h[WAVES][RD_TIERS];
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x, w = threadIdx.x >> 6, lane = lane_id();
-    uint32_t tr = 0xFFu;
-    if (t < n) {
-        uint32_t q0, q1;
-        txn_queries(o, t, q0, q1);
-        uint64_t m = 0;
-        for (uint32_t q = q0; q < q1; ++q) m += o.q_cnt[q];
-        m_raw[t] = m;
-        // tiers: 0 none, 1 <= 16 (16-lane groups), 11 <= 32 (half waves), 2 <= 64 (wave), 3..9 LDS workgroups of
-        // 128..8192, 10 global
-        if (m == 0) tr = 0;
-        else if (m <= 16) tr = 1;
-        else if (m <= 32) tr = 11;
-        else if (m <= 64) tr = 2;
-        else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
-        else tr = 10;
-        tier[t] = tr;
-        if (m == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
-    }
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    uint32_t acc[RD_TIERS] = {};   // this wave's counts (lane 0)
+    for (int r = 0; r < RD_TS; ++r) {
+        const uint32_t t = (blockIdx.x * RD_TS + (uint32_t)r) * BLOCK + threadIdx.x;
+        uint32_t tr = 0xFFu;
+        if (t < n) {
+            uint32_t q0, q1;
+            txn_queries(o, t, q0, q1);
+            uint64_t m = 0;
+            for (uint32_t qb = q0; qb < q1; qb += 8) {   // eight count loads in flight, not one dependent add per load
+                uint32_t c[8];
 #pragma unroll
-    for (int v = 0; v < RD_TIERS; ++v) {
-        const uint32_t c = (uint32_t)__popcll(__ballot(tr == (uint32_t)v));
-        if (lane == 0) h[w][v] = c;
+                for (int u = 0; u < 8; ++u) c[u] = qb + u < q1 ? o.q_cnt[qb + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) m += c[u];
+            }
+            m_raw[t] = m;
+            // tiers: 0 none, 1 <= 16 (16-lane groups), 11 <= 32 (half waves), 2 <= 64 (wave), 3..9 LDS workgroups of
+            // 128..8192, 10 global
+            if (m == 0) tr = 0;
+            else if (m <= 16) tr = 1;
+            else if (m <= 32) tr = 11;
+            else if (m <= 64) tr = 2;
+            else if (m <= BLOCK_E) { uint32_t n2 = 128, b = 3; while (n2 < m) { n2 <<= 1; ++b; } tr = b; }
+            else tr = 10;
+            tier[t] = tr;
+            if (m == 0) { o.rd_cnt[t] = 0; o.u_cnt[t] = 0; o.a_cnt[t] = 0; }
+        }
+#pragma unroll
+        for (int v = 0; v < RD_TIERS; ++v) acc[v] += (uint32_t)__popcll(__ballot(tr == (uint32_t)v));
     }
+    if (lane == 0)
+#pragma unroll
+        for (int v = 0; v < RD_TIERS; ++v) h[w][v] = acc[v];
     __syncthreads();
     if (threadIdx.x < RD_TIERS) {
         uint32_t c = 0;
@@ -1115,7 +1139,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint32_t *rowner = ctx->get<uint32_t>("rd_rowner", R);
     uint32_t *eflag = ctx->get<uint32_t>("rd_eflag", R);
     uint32_t *eidx = ctx->get<uint32_t>("rd_eidx", R + 1);
-    launch(ctx, "rd_prep", k_rd_prep, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, tl, status, key_off, key_code, rng_off, rs,
+    launch(ctx, "rd_prep", k_rd_prep, dim3(grid_for(n, (size_t)BLOCK * RD_TS)), dim3(BLOCK), 0, n, tl, status, key_off, key_code, rng_off, rs,
            re, ref[0], ref[1], ref_lo, rowner, eflag, rg);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, eflag, eidx, R, true, eidx + R);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, rg, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -1160,7 +1184,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint32_t *cls_hist = cls, *class_off = cls + (NCLS + 1);
     ACC_HIP(hipMemsetAsync(cls_hist, 0, (NCLS + 1) * sizeof(uint32_t), st));
     const bool csplit = rs_plan.bits + 6 > 64;
-    launch(ctx, "rd_dict_write", k_rd_dict_write, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, NE, (const uint32_t *)ds.vals,
+    launch(ctx, "rd_dict_write", k_rd_dict_write, dim3(grid_for(NE, (size_t)BLOCK * RD_TS)), dim3(BLOCK), 0, NE, (const uint32_t *)ds.vals,
            (const uint32_t *)dflag, (const uint32_t *)dincl, erec, dict_s,
            dict_e, rs_plan, rs_plan.bits, csplit ? 1 : 0, ckey, cls_hist);
     launch(ctx, "rd_class_off", k_rd_class_off, dim3(1), dim3(64), 0, (const uint32_t *)cls_hist, class_off);
@@ -1247,7 +1271,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint64_t *raw_off = ctx->get<uint64_t>("rd_raw_off", (size_t)n + 1);
     uint32_t *thist = ctx->get<uint32_t>("rd_thist", 16);
     ACC_HIP(hipMemsetAsync(thist, 0, 16 * sizeof(uint32_t), st));
-    launch(ctx, "rd_tsize", k_rd_tsize, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, o, m_raw, tier, thist);
+    launch(ctx, "rd_tsize", k_rd_tsize, dim3(grid_for(n, (size_t)BLOCK * RD_TS)), dim3(BLOCK), 0, n, o, m_raw, tier, thist);
     scan<uint64_t, OpAdd<uint64_t>>(ctx, m_raw, raw_off, n, true, raw_off + n);
     o.raw_off = raw_off;
     // txns grouped by tier: one 8-bit radix pass (stable)
