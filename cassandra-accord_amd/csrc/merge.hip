@@ -285,12 +285,21 @@ __global__ __launch_bounds__(BLOCK) void k_m_fit(uint32_t ng, const uint64_t *__
         }
     }
     block_or1(bad ? 1ull : 0ull, &g[3]);
+    uint64_t mx[4] = { 0, 0, 0, 0 };
     if (gi < ng && !bad) {
         const uint64_t r0 = grp_off[gi], r1 = grp_off[gi + 1];
-        atomicMax((unsigned long long *)&gmax[0], (unsigned long long)(key_off[r1] - key_off[r0]));
-        atomicMax((unsigned long long *)&gmax[1], (unsigned long long)(val_off[r1] - val_off[r0]));
-        atomicMax((unsigned long long *)&gmax[2], (unsigned long long)(k2v_off[r1] - k2v_off[r0]));
-        atomicMax((unsigned long long *)&gmax[3], (unsigned long long)((k2v_off[r1] - k2v_off[r0]) - (key_off[r1] - key_off[r0])));
+        mx[0] = key_off[r1] - key_off[r0];
+        mx[1] = val_off[r1] - val_off[r0];
+        mx[2] = k2v_off[r1] - k2v_off[r0];
+        mx[3] = (k2v_off[r1] - k2v_off[r0]) - (key_off[r1] - key_off[r0]);
+    }
+    // wave maxima first: four global atomics per wave instead of per group (they share one line)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint64_t x = mx[k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) { const uint64_t y = shfl_idx(x, (int)(lane_id() ^ d)); x = y > x ? y : x; }
+        if (lane_id() == 0 && x) atomicMax((unsigned long long *)&gmax[k], (unsigned long long)x);
     }
 }
 
