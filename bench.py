@@ -39,7 +39,9 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
 
 # KeyDeps tiers launched on a side stream, concurrently with the stream pass (csrc/keydeps.hip keydeps_core)
-SIDE_STREAM_TAGS = {"v2_write_med", "v2_write_big", "v2_write_huge", "v2_write_medium", "v2_write_win", "v2_write_win16"}
+SIDE_STREAM_TAGS = {"v2_write_med", "v2_write_big", "v2_write_huge", "v2_write_medium", "v2_write_win", "v2_write_win16",
+                    # RangeDeps build tiers on side streams beside the wave tier (csrc/rangedeps.hip rangedeps_batch)
+                    "rd_build_s16", "rd_build_s32", "rd_build_block"}
 
 # launch tags whose kernel is one instance of a template launched under several tags (csrc/keydeps.hip tiers)
 TAG_KERNEL = {
@@ -48,6 +50,10 @@ TAG_KERNEL = {
     "v2_write_huge": "k_v2_write_big<16384,1024>",
     "v2_write_win": "k_v2_write_win<8>",
     "v2_write_win16": "k_v2_write_win<16>",
+    # the RangeDeps lane-group tiers: k_rd_build_seg<S, NARROW> (prefix: either sort width)
+    "rd_build_s16": "k_rd_build_seg<16,",
+    "rd_build_s32": "k_rd_build_seg<32,",
+    "rd_build_s64": "k_rd_build_seg<64,",
 }
 
 
@@ -110,6 +116,8 @@ def roofline(step_bytes, step, steps, ms_per_step, config, variant="", profiled=
         exact = TAG_KERNEL.get(dom_name)
         if exact and exact in kernels:
             ks = [kernels[exact]]
+        elif exact and exact.endswith(","):
+            ks = [v for name, v in kernels.items() if name.startswith(exact)]
         else:
             ks = [v for name, v in kernels.items() if name.split("<")[0] in ("k_" + dom_name, dom_name)]
         if ks:
