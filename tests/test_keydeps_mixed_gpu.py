@@ -173,3 +173,26 @@ def test_partial_deps_fused(ctx, end_inclusive):
     k, r = ctx.calculate_partial_deps_mixed(only)
     assert ctx.stats()["rangedeps.shared_dictionary"] == 0
     assert_same(k, oracle.keydeps_mixed(only), "range-only key half")
+
+
+def test_partial_deps_fused_errors_and_repeat(ctx):
+    """acc_partial_deps_batch runs its RangeDeps half on a child context from a second host thread: a rejected batch
+    raises (whichever half finds it first) and leaves the context usable; repeated calls reuse the child and give the
+    same arrays as the first, equal to the oracle."""
+    import oracle
+    from accord_amd.deps import IllegalArgumentException
+    for bad in (rd_cases.build([dict(keys=[3]), dict(ranges=[(5, 5)])]),
+                rd_cases.build([dict(keys=[3]), dict(ranges=[(5, 10), (8, 12)])])):
+        with pytest.raises(IllegalArgumentException):
+            ctx.calculate_partial_deps_mixed(bad)
+    rb = rd_cases.dense(79, n=3000, end_inclusive=1, ranges_per_txn=2)
+    k1, r1 = ctx.calculate_partial_deps_mixed(rb)
+    k2, r2 = ctx.calculate_partial_deps_mixed(rb)
+    for f in ("arena_off", "arena", "kd_off", "key_idx", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(k1, f), getattr(k2, f), err_msg=f)
+    for f in ("rng_start", "rng_end", "arena_off", "arena", "rd_off", "range_id", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(r1, f), getattr(r2, f), err_msg=f)
+    assert_same(k1, oracle.keydeps_mixed(rb), "fused key half after errors")
+    o = oracle.rangedeps_batch(rb)
+    for f in ("arena_off", "arena", "rd_off", "u_off", "dep_txn"):
+        np.testing.assert_array_equal(getattr(r1, f), getattr(o, f), err_msg=f)
