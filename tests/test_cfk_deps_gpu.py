@@ -313,3 +313,28 @@ def test_cfk_store_one_state(ctx):
             st.update(b)
     finally:
         st.close()
+
+
+def test_cfk_store_modes(ctx):
+    """A store keeps missing[] from its first acc_cfk_apply_deps on: deps updates on a store holding status-only state
+    (acc_cfk_update) and the key-major / missing views of such a store are ACC_E_STATE; an empty store takes either."""
+    from accord_amd.deps import CfkStore, IllegalStateException
+    upd = CC.cfk_case(3, n_txn=60, n_keys=5)
+    b, _, _ = CC.snap_as_batch(oracle.cfk_apply(CC.empty_snapshot(), upd))
+    st = CfkStore(ctx)
+    try:
+        st.update(b)                       # status-only state
+        with pytest.raises(IllegalStateException):
+            st.apply_deps(upd)
+        with pytest.raises(IllegalStateException):
+            st.state()
+        with pytest.raises(IllegalStateException):
+            st.missing_view()
+    finally:
+        st.close()
+    st = CfkStore(ctx)
+    try:
+        st.apply_deps(upd)                 # from empty: the deps state
+        same(st.state(), oracle.cfk_apply(CC.empty_snapshot(), upd), "store from empty")
+    finally:
+        st.close()
