@@ -46,7 +46,9 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_cfk_create", "acc_cfk_destroy", "acc_cfk_update", "acc_cfk_view", "acc_cfk_apply", "acc_cfk_snap_to_batch",
            "acc_cfk_apply_deps", "acc_cfk_state", "acc_cfk_missing", "acc_max_conflicts",
            "acc_maxconflicts_create", "acc_maxconflicts_destroy", "acc_maxconflicts_update", "acc_maxconflicts_get",
-           "acc_maxconflicts_size"]
+           "acc_maxconflicts_size",
+           "acc_ranges_of", "acc_ranges_with", "acc_ranges_subtract", "acc_ranges_merge_touching", "acc_ranges_select",
+           "acc_ranges_index_of", "acc_ranges_contains_all_keys", "acc_ranges_contains_all", "acc_rangedeps_is_covered_by"]
 
 
 class Opts(C.Structure):

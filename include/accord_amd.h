@@ -856,6 +856,41 @@ typedef struct acc_graph_in {
 
 int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t *order, uint32_t *n_levels);
 
+/* ---- Ranges algebra (host code, no context; primitives/Ranges.java, AbstractRanges.java) ----
+ * A Ranges is a sorted, deoverlapped list of Range (start, end) key codes of one bound type (Range.EndInclusive (s, e]
+ * or Range.StartInclusive [s, e), Range.java:40-138); operations on ranges alone do not depend on the bound type.
+ * Results go to caller arrays of `cap` entries; *out_n is always the result size (ACC_E_CAP when > cap; bounds:
+ * with / subtract <= a.n + b.n, merge_touching <= a.n, select <= k, of <= in.n). Inputs that must be sorted and
+ * deoverlapped are checked (Ranges.ofSortedAndDeoverlapped: IllegalArgumentException -> ACC_E_ARG). */
+typedef struct acc_rlist {
+    const uint64_t *start;
+    const uint64_t *end;
+    uint32_t n;
+    uint32_t reserved;
+} acc_rlist;
+
+/* Ranges.of(Range...)                          AbstractRanges.java:689-707 (sort by Range::compare, merge overlaps) */
+int acc_ranges_of(const acc_rlist *in, uint64_t *out_start, uint64_t *out_end, uint32_t cap, uint32_t *out_n);
+/* a.with(b) = union(MERGE_OVERLAPPING)         Ranges.java:119-127, AbstractRanges.java:439-585 */
+int acc_ranges_with(const acc_rlist *a, const acc_rlist *b, uint64_t *out_start, uint64_t *out_end, uint32_t cap,
+                    uint32_t *out_n);
+/* a.subtract(b)                                AbstractRanges.java:223-287 */
+int acc_ranges_subtract(const acc_rlist *a, const acc_rlist *b, uint64_t *out_start, uint64_t *out_end, uint32_t cap,
+                        uint32_t *out_n);
+/* a.mergeTouching()                            AbstractRanges.java:637-675 */
+int acc_ranges_merge_touching(const acc_rlist *a, uint64_t *out_start, uint64_t *out_end, uint32_t cap, uint32_t *out_n);
+/* a.select(int[] indexes)                      Ranges.java:76-82 */
+int acc_ranges_select(const acc_rlist *a, const uint32_t *idx, uint32_t k, uint64_t *out_start, uint64_t *out_end,
+                      uint32_t cap, uint32_t *out_n);
+/* a.indexOf(key): index, or -(insertion point) - 1   AbstractRanges.java:51-54 (SortedArrays FAST search) */
+int acc_ranges_index_of(const acc_rlist *a, uint32_t end_inclusive, uint64_t key, int64_t *out_index);
+/* a.containsAll(Keys) (sorted unique key codes) AbstractRanges.java:86-91; a.containsAll(Ranges) :96-101 */
+int acc_ranges_contains_all_keys(const acc_rlist *a, uint32_t end_inclusive, const uint64_t *keys, uint32_t n_keys,
+                                 int32_t *out);
+int acc_ranges_contains_all(const acc_rlist *a, const acc_rlist *b, int32_t *out);
+/* RangeDeps.isCoveredBy(covering) over a RangeDeps' ranges (sorted by Range::compare) primitives/RangeDeps.java:595-613 */
+int acc_rangedeps_is_covered_by(const acc_rlist *range_deps_ranges, const acc_rlist *covering, int32_t *out);
+
 /* ---- timing (ACC_OPT_TIMING) ---- */
 /* Per-kernel accumulated device time since the last reset: name[i], total ms, launch count. */
 int  acc_timing_count(acc_ctx *ctx);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B timing of the in-tree library against tools/prof/base.so on one box: bench lines alternate B, A, B, A.
+# A/B timing of the in-tree library against tools/ab/base.so on one box: bench lines alternate B, A, B, A.
 #   CFG=2 STEPS=50 bash tools/gpu_ab.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 cfg=${CFG:-2}; steps=${STEPS:-50}
 for i in 1 2; do
     for v in base new; do
-        lib=""; [ $v = base ] && lib=tools/prof/base.so
+        lib=""; [ $v = base ] && lib=tools/ab/base.so
         ACC_LIB_PATH=$lib timeout -k 10 300 python -u bench.py --config $cfg --steps $steps --warmup 5 --no-cpu \
             > gpurun_out/ab_${v}_$i.log 2>&1 || { echo "bench $v failed"; tail -20 gpurun_out/ab_${v}_$i.log; exit 1; }
         python -c "
