@@ -48,7 +48,8 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_maxconflicts_create", "acc_maxconflicts_destroy", "acc_maxconflicts_update", "acc_maxconflicts_get",
            "acc_maxconflicts_size",
            "acc_ranges_of", "acc_ranges_with", "acc_ranges_subtract", "acc_ranges_merge_touching", "acc_ranges_select",
-           "acc_ranges_index_of", "acc_ranges_contains_all_keys", "acc_ranges_contains_all", "acc_rangedeps_is_covered_by"]
+           "acc_ranges_index_of", "acc_ranges_contains_all_keys", "acc_ranges_contains_all", "acc_rangedeps_is_covered_by",
+           "acc_partial_deps_covering"]
 
 
 class Opts(C.Structure):
@@ -167,6 +168,17 @@ class RmmView(C.Structure):
 class DepsMergeView(C.Structure):
     _fields_ = [("n_groups", C.c_uint32), ("total_in_entries", C.c_uint64), ("key_deps", RmmView),
                 ("range_deps", RmmView)]
+
+
+class RList(C.Structure):
+    """acc_rlist: a Ranges as parallel (start, end) code arrays"""
+    _fields_ = [("start", C.c_void_p), ("end", C.c_void_p), ("n", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class CoveringView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("n_coverings", C.c_uint32), ("cov_id", C.c_void_p), ("cov_off", C.c_void_p),
+                ("cov_start", C.c_void_p), ("cov_end", C.c_void_p), ("store_mask", C.c_void_p),
+                ("total_ranges", C.c_uint64)]
 
 
 class RmmOut(C.Structure):
@@ -316,6 +328,25 @@ ACC_COMM_ID_BYTES = 128
 _lib = None
 
 
+class _Tolerant:
+    """A tuning build (ACC_LIB_PATH, e.g. an older library timed beside the current one) may lack the newest entry
+    points: their signatures are skipped, and calling one fails with the library's own AttributeError."""
+
+    class _Skip:
+        pass
+
+    def __init__(self, lib):
+        object.__setattr__(self, "_l", lib)
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._l, name)
+        except AttributeError:
+            if name.startswith("acc_"):
+                return _Tolerant._Skip()
+            raise
+
+
 def load():
     """Load libaccord_amd.so; raises if it is missing (no fallback)."""
     global _lib
@@ -331,6 +362,8 @@ def load():
     except ImportError:
         pass
     L = C.CDLL(LIB_PATH)
+    if os.environ.get("ACC_LIB_PATH"):
+        L = _Tolerant(L)
     L.acc_create.argtypes = [C.c_int, C.POINTER(Opts), C.POINTER(C.c_void_p)]
     L.acc_create.restype = C.c_int
     L.acc_destroy.argtypes = [C.c_void_p]
@@ -386,8 +419,11 @@ def load():
     L.acc_shard_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(BatchIn), C.c_void_p, C.c_uint32, C.POINTER(MergeView)]
     L.acc_shard_reduce.restype = C.c_int
     L.acc_partial_deps_reduce.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(RangeBatchIn), C.c_void_p, C.c_uint32,
-                                          C.POINTER(MergeView), C.POINTER(DepsMergeView)]
+                                          C.POINTER(RList), C.POINTER(MergeView), C.POINTER(DepsMergeView),
+                                          C.POINTER(CoveringView)]
     L.acc_partial_deps_reduce.restype = C.c_int
+    L.acc_partial_deps_covering.argtypes = [C.c_void_p, C.POINTER(RangeBatchIn), C.POINTER(RList)]
+    L.acc_partial_deps_covering.restype = C.c_int
     L.acc_map_reduce_full.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(RecoveryIn), C.POINTER(KeydepsView)]
     L.acc_map_reduce_full.restype = C.c_int
     L.acc_map_reduce_full_ranges.argtypes = [C.c_void_p, C.POINTER(RangeCmdsIn), C.POINTER(RecoveryRangesIn),

@@ -514,16 +514,55 @@ def shard_reduce(ctx, comm: Comm, bi, n_global: int, txn_global=None):
     return view
 
 
-def partial_deps_reduce(ctx, comm: Comm, rbi, n_global: int, txn_global=None):
+def _rlist(covering):
+    """(start[], end[]) -> (acc_rlist, the arrays it points into)"""
+    from . import _lib as L
+    s = np.ascontiguousarray(covering[0], dtype=np.uint64)
+    e = np.ascontiguousarray(covering[1], dtype=np.uint64)
+    return L.RList(s.ctypes.data if len(s) else None, e.ctypes.data if len(e) else None, len(s), 0), (s, e)
+
+
+def partial_deps_reduce(ctx, comm: Comm, rbi, n_global: int, txn_global=None, covering=None):
     """acc_partial_deps_reduce: PreAccept.reduce of both PartialDeps halves of the last acc_partial_deps_batch on ctx
     (mixed batch `rbi`, an acc_range_batch_in) over `comm`, one exchange; returns (KeyDeps merge view, Deps.merge view
-    whose range half is the RangeDeps.with fold in store order)."""
+    whose range half is the RangeDeps.with fold in store order), plus the PartialDeps.covering view when this store's
+    `covering` ((start[], end[]): its Ranges) is given."""
     import ctypes as C
     from . import _lib as L
     ptr = None
     if txn_global is not None:
         ptr = txn_global.data_ptr() if hasattr(txn_global, "data_ptr") else np.ascontiguousarray(txn_global).ctypes.data
-    kv, rv = L.MergeView(), L.DepsMergeView()
-    ctx.check(ctx._lib.acc_partial_deps_reduce(ctx.handle, comm.handle, C.byref(rbi), ptr, n_global, C.byref(kv),
-                                               C.byref(rv)))
-    return kv, rv
+    kv, rv, cv = L.MergeView(), L.DepsMergeView(), L.CoveringView()
+    rl, keep = _rlist(covering) if covering is not None else (None, None)
+    ctx.check(ctx._lib.acc_partial_deps_reduce(ctx.handle, comm.handle, C.byref(rbi), ptr, n_global,
+                                               C.byref(rl) if rl is not None else None, C.byref(kv), C.byref(rv),
+                                               C.byref(cv) if rl is not None else None))
+    return (kv, rv, cv) if covering is not None else (kv, rv)
+
+
+def partial_deps_covering(ctx, rbi, covering):
+    """acc_partial_deps_covering: the store's Ranges as every txn's PartialDeps.covering for the last
+    acc_partial_deps_batch on ctx, with the PartialDeps constructor's invariant checks (PartialDeps.java:52-58)."""
+    import ctypes as C
+    rl, keep = _rlist(covering)
+    ctx.check(ctx._lib.acc_partial_deps_covering(ctx.handle, C.byref(rbi), C.byref(rl)))
+
+
+def covering_to_host(ctx, cv):
+    """The covering view on the host: (cov_id[n_groups], store_mask[n_groups], list of (start[], end[]) per distinct
+    covering)."""
+    from . import _lib as L
+    ng, nd = int(cv.n_groups), int(cv.n_coverings)
+    cid = np.zeros(max(ng, 1), np.uint32)
+    msk = np.zeros(max(ng, 1), np.uint64)
+    off = np.zeros(nd + 1, np.uint64)
+    for dst, src, nb in ((cid, cv.cov_id, 4 * ng), (msk, cv.store_mask, 8 * ng), (off, cv.cov_off, 8 * (nd + 1))):
+        if nb:
+            ctx.check(ctx._lib.acc_copy_out(ctx.handle, dst.ctypes.data, src, nb, L.ACC_MEM_HOST))
+    tot = int(off[-1]) if nd else 0
+    cs, ce = np.zeros(max(tot, 1), np.uint64), np.zeros(max(tot, 1), np.uint64)
+    if tot:
+        ctx.check(ctx._lib.acc_copy_out(ctx.handle, cs.ctypes.data, cv.cov_start, 8 * tot, L.ACC_MEM_HOST))
+        ctx.check(ctx._lib.acc_copy_out(ctx.handle, ce.ctypes.data, cv.cov_end, 8 * tot, L.ACC_MEM_HOST))
+    table = [(cs[int(off[i]):int(off[i + 1])].copy(), ce[int(off[i]):int(off[i + 1])].copy()) for i in range(nd)]
+    return cid[:ng], msk[:ng], table

@@ -18,7 +18,8 @@ namespace acc {
 void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
 void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in, const uint32_t *txn_global,
-                         uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view);
+                         uint32_t n_global, const acc_rlist *covering, acc_merge_view *key_view,
+                         acc_deps_merge_view *range_view, acc_covering_view *covering_view);
 
 struct Rccl {
     bool ok = false;
@@ -107,13 +108,14 @@ static void exchange(acc_comm *c, const uint8_t *send, const std::vector<uint64_
 // Fragment streams of one exchange: stream q = elements of esz[q] bytes, destination-major (destination d owns
 // elements [off[q][d], off[q][d+1]) of send[q]). After exchange_streams: recv[q] = what the sources sent, concatenated in
 // source-rank order, n_src[q][s] elements from source s.
+constexpr int MAX_STREAMS = 10;
 struct Streams {
     int ns = 0;
-    const void *send[8] = {};
-    std::vector<uint64_t> off[8];
-    uint64_t esz[8] = {};
-    void *recv[8] = {};
-    std::vector<uint64_t> n_src[8];
+    const void *send[MAX_STREAMS] = {};
+    std::vector<uint64_t> off[MAX_STREAMS];
+    uint64_t esz[MAX_STREAMS] = {};
+    void *recv[MAX_STREAMS] = {};
+    std::vector<uint64_t> n_src[MAX_STREAMS];
 };
 
 // ONE size exchange (every stream's element count per peer) and ONE grouped all-to-all(v) carrying every stream: the
@@ -137,8 +139,9 @@ static void exchange_streams(acc_comm *c, Streams &S)
     ACC_HIP(hipMemcpyAsync(hcr.data(), cnt_r, hcr.size() * 8, hipMemcpyDeviceToHost, st));
     ctx->sync();
     // ---- receive buffers (source-major per stream)
-    static const char *rn[8] = { "cm_r0", "cm_r1", "cm_r2", "cm_r3", "cm_r4", "cm_r5", "cm_r6", "cm_r7" };
-    std::vector<uint64_t> rb[8];   // byte offsets per source
+    static const char *rn[MAX_STREAMS] = { "cm_r0", "cm_r1", "cm_r2", "cm_r3", "cm_r4", "cm_r5", "cm_r6", "cm_r7", "cm_r8",
+                                           "cm_r9" };
+    std::vector<uint64_t> rb[MAX_STREAMS];   // byte offsets per source
     for (int q = 0; q < ns; ++q) {
         S.n_src[q].assign(W, 0);
         rb[q].assign(W + 1, 0);
@@ -249,13 +252,20 @@ void range_pack(acc_ctx *ctx, const acc_range_batch_in *in, const uint32_t *txn_
                 void *send[4], std::vector<uint64_t> off[4]);
 void range_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_global, const std::vector<uint64_t> n_src[4],
                  void *const recv[4], acc_deps_merge_view *view);
+void partial_deps_covering(acc_ctx *ctx, const acc_rlist *covering, uint32_t end_inclusive);
+void covering_pack(acc_ctx *ctx, const acc_rlist *covering, const uint32_t *txn_global_dev, uint32_t n_store, uint32_t world,
+                   void *send[2], std::vector<uint64_t> off[2]);
+void covering_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_global, uint32_t end_inclusive,
+                    const std::vector<uint64_t> &n_part, const void *recv_part, const std::vector<uint64_t> &n_cov,
+                    const void *recv_cov, const acc_merge_view *kv, const acc_deps_merge_view *rv, acc_covering_view *out);
 
 // PreAccept.reduce of a store's whole PartialDeps: both halves' fragments in one exchange (8 streams), then KeyDeps.with
 // (shard_merge) and RangeDeps.with in store order (range_merge) on the home rank
 void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in, const uint32_t *txn_global,
-                         uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view)
+                         uint32_t n_global, const acc_rlist *covering, acc_merge_view *key_view,
+                         acc_deps_merge_view *range_view, acc_covering_view *covering_view)
 {
-    if (!c || !in || !key_view || !range_view) fail(ACC_E_ARG, "null argument");
+    if (!c || !in || !key_view || !range_view || (covering && !covering_view)) fail(ACC_E_ARG, "null argument");
     if (c->ctx != ctx) fail(ACC_E_ARG, "communicator belongs to another context");
     const acc_batch_in kin{ in->n_txn, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
     Streams S;
@@ -266,12 +276,32 @@ void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in
     const uint64_t resz[4] = { 16, 16, 24, 4 };   // header (4 x u32), Range (start, end), raw TxnId (msb, lsb, node), int
     for (int q = 0; q < 4; ++q) { S.send[4 + q] = rs[q]; S.off[4 + q] = ro[q]; S.esz[4 + q] = resz[q]; }
     S.ns = 8;
+    if (covering) {   // the store's txns (u32 global indices) by home rank and its covering ((start, end) pairs)
+        const uint32_t n = in->n_txn;
+        const uint32_t *gidx = nullptr;
+        if (txn_global) gidx = stage_in(ctx, "cov_gidx", txn_global, n, in->mem);
+        else {
+            uint32_t *io = ctx->get<uint32_t>("cov_iota", std::max<uint32_t>(n, 1));
+            if (n) launch(ctx, "iota", k_iota, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, io, (size_t)n);
+            gidx = io;
+            n_global = std::max(n_global, n);
+        }
+        void *cs[2];
+        std::vector<uint64_t> co[2];
+        covering_pack(ctx, covering, gidx, n, c->world, cs, co);
+        S.send[8] = cs[0]; S.off[8] = co[0]; S.esz[8] = 4;
+        S.send[9] = cs[1]; S.off[9] = co[1]; S.esz[9] = 16;
+        S.ns = 10;
+    }
     exchange_streams(c, S);
     merge_key_streams(ctx, c, n_global, S, key_view);
     std::vector<uint64_t> rn[4];
     void *rr[4];
     for (int q = 0; q < 4; ++q) { rn[q] = S.n_src[4 + q]; rr[q] = S.recv[4 + q]; }
     range_merge(ctx, c->world, c->rank, n_global, rn, rr, range_view);
+    if (covering)
+        covering_merge(ctx, c->world, c->rank, n_global, in->end_inclusive, S.n_src[8], S.recv[8], S.n_src[9], S.recv[9],
+                       key_view, range_view, covering_view);
 }
 
 }  // namespace acc
@@ -341,12 +371,23 @@ int acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const
 }
 
 int acc_partial_deps_reduce(acc_ctx *ctx, acc_comm *comm, const acc_range_batch_in *in, const uint32_t *txn_global,
-                            uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view)
+                            uint32_t n_global, const acc_rlist *covering, acc_merge_view *key_view,
+                            acc_deps_merge_view *range_view, acc_covering_view *covering_view)
 {
     if (!ctx) return ACC_E_ARG;
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
-        acc::partial_deps_reduce(ctx, comm, in, txn_global, n_global, key_view, range_view);
+        acc::partial_deps_reduce(ctx, comm, in, txn_global, n_global, covering, key_view, range_view, covering_view);
+    });
+}
+
+int acc_partial_deps_covering(acc_ctx *ctx, const acc_range_batch_in *in, const acc_rlist *covering)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        if (!in) acc::fail(ACC_E_ARG, "null argument");
+        acc::partial_deps_covering(ctx, covering, in->end_inclusive);
     });
 }
 

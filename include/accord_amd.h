@@ -65,6 +65,14 @@
 extern "C" {
 #endif
 
+/* A Ranges: sorted, deoverlapped Range (start, end) key codes of one bound type (primitives/Ranges.java). */
+typedef struct acc_rlist {
+    const uint64_t *start;
+    const uint64_t *end;
+    uint32_t n;
+    uint32_t reserved;
+} acc_rlist;
+
 /* ---- error codes ---- */
 #define ACC_OK          0
 #define ACC_E_ARG      (-1)   /* IllegalArgumentException class */
@@ -482,6 +490,28 @@ int  acc_comm_init_host(acc_ctx *ctx, uint32_t world, uint32_t rank, acc_alltoal
 void acc_comm_destroy(acc_comm *comm);
 int  acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, const uint32_t *txn_global, uint32_t n_global,
                       acc_merge_view *out_view);
+/* PartialDeps.covering (primitives/PartialDeps.java:31-58, 80-86). A store's txns all carry the store's Ranges as
+ * covering (PreAccept.calculatePartialDeps: new PartialDeps.Builder(ranges), messages/PreAccept.java:245-265); the
+ * reduced PartialDeps of a home txn carries the fold that.covering.with(this.covering) over the stores that replied
+ * for it (every store whose batch holds the txn), in store order. Per home txn: cov_id into a table of the distinct
+ * coverings (device memory owned by the context, valid until the next reduce) and the mask of the stores that replied.
+ * Both calls check the PartialDeps constructor's invariants covering.containsAll(keyDeps.keys) and
+ * rangeDeps.isCoveredBy(covering) for every txn (PartialDeps.java:52-58) -> ACC_E_STATE. */
+typedef struct acc_covering_view {
+    uint32_t n_groups;             /* home txns, as the reduce's key view */
+    uint32_t n_coverings;          /* distinct coverings in the table */
+    const uint32_t *cov_id;        /* [n_groups] */
+    const uint64_t *cov_off;       /* [n_coverings+1] into cov_start / cov_end */
+    const uint64_t *cov_start;
+    const uint64_t *cov_end;
+    const uint64_t *store_mask;    /* [n_groups] bit s: store (rank) s replied for the txn */
+    uint64_t total_ranges;
+} acc_covering_view;
+
+/* The store's `covering` (sorted, deoverlapped; the batch's bound type) for the last acc_partial_deps_batch on ctx over
+ * `in` (the same batch): the invariant checks of every txn's PartialDeps(covering, keyDeps, rangeDeps). */
+int  acc_partial_deps_covering(acc_ctx *ctx, const acc_range_batch_in *in, const acc_rlist *covering);
+
 /* acc_partial_deps_reduce: PreAccept.reduce of a store's whole PartialDeps (messages/PreAccept.java:141-156;
  * PartialDeps.with = KeyDeps.with + RangeDeps.with, primitives/PartialDeps.java:80-86) for the last
  * acc_partial_deps_batch on ctx over `in` (the same mixed batch): the KeyDeps fragments (as acc_shard_reduce) and the
@@ -489,9 +519,12 @@ int  acc_shard_reduce(acc_ctx *ctx, acc_comm *comm, const acc_batch_in *in, cons
  * and ONE grouped all-to-all(v); on the home rank the KeyDeps.with fold (key_view, as acc_shard_reduce) and the
  * RangeDeps.with fold in store order (RangeDeps.java:567-582; the range half of range_view, raw TxnIds; its key half is
  * absent). A range command is stored sliced to each store's ranges (impl/InMemoryCommandStore.java:739-761), so the
- * result depends on the store split exactly as the reference's does. Collective over comm. */
+ * result depends on the store split exactly as the reference's does. With `covering` (this store's Ranges; null: no
+ * covering), the same exchange carries the store's txns and covering, and covering_view receives every home txn's
+ * PartialDeps.covering (above). Collective over comm. */
 int  acc_partial_deps_reduce(acc_ctx *ctx, acc_comm *comm, const acc_range_batch_in *in, const uint32_t *txn_global,
-                             uint32_t n_global, acc_merge_view *key_view, acc_deps_merge_view *range_view);
+                             uint32_t n_global, const acc_rlist *covering, acc_merge_view *key_view,
+                             acc_deps_merge_view *range_view, acc_covering_view *covering_view);
 
 /* ---- Recovery scans: CommandsForKey.mapReduceFull over a batch of queries (SURVEY.md §8(f) N3 = A7) ----
  * The snapshot is an acc_batch_in (one CommandsForKey per key, as for acc_keydeps_batch) plus, per input pair j
@@ -862,12 +895,7 @@ int acc_levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level, uint32_t
  * Results go to caller arrays of `cap` entries; *out_n is always the result size (ACC_E_CAP when > cap; bounds:
  * with / subtract <= a.n + b.n, merge_touching <= a.n, select <= k, of <= in.n). Inputs that must be sorted and
  * deoverlapped are checked (Ranges.ofSortedAndDeoverlapped: IllegalArgumentException -> ACC_E_ARG). */
-typedef struct acc_rlist {
-    const uint64_t *start;
-    const uint64_t *end;
-    uint32_t n;
-    uint32_t reserved;
-} acc_rlist;
+/* (acc_rlist is declared at the top of this header) */
 
 /* Ranges.of(Range...)                          AbstractRanges.java:689-707 (sort by Range::compare, merge overlaps) */
 int acc_ranges_of(const acc_rlist *in, uint64_t *out_start, uint64_t *out_end, uint32_t cap, uint32_t *out_n);

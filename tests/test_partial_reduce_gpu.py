@@ -45,20 +45,62 @@ def _expected(rb, world, rank):
     return key, oracle.rmm_merge(m["grp_off"], m["half"], True)
 
 
+def _bounds(rb, world):
+    from accord_amd import sharded as S
+    return S.even_split(np.concatenate([rb.keys.key_code, rb.rng_start, rb.rng_end]).astype(np.uint64), world)
+
+
+def _store_covering(rb, world, rank):
+    """Store `rank`'s Ranges in the batch's bound type (its EvenSplit key range; sharded.store_ranges_bound)"""
+    from accord_amd import sharded as S
+    lo, hi = S.store_ranges_bound(_bounds(rb, world), rank, rb.end_inclusive)
+    return np.array([lo], np.uint64), np.array([hi], np.uint64)
+
+
+def _expected_covering(rb, world, rank):
+    """Per home txn of `rank`: the stores whose batch holds it, and its covering = the fold that.covering.with(
+    this.covering) over them (PartialDeps.java:80-86) -- for disjoint store ranges, a set union that leaves touching
+    ranges of different stores apart (RangesTest.addTest): the stores' ranges in store order."""
+    from accord_amd import sharded as S
+    b = _bounds(rb, world)
+    member = np.zeros((world, rb.n_txn), bool)
+    for s in range(world):
+        member[s, S.store_range_batch(rb, b, s)[1].astype(np.int64)] = True
+    home = S.home_txns(rb.n_txn, rank, world)
+    out = []
+    for t in home.tolist():
+        stores = [s for s in range(world) if member[s, t]]
+        cov = [_store_covering(rb, world, s) for s in stores]
+        mask = sum(1 << s for s in stores)
+        out.append((mask, np.array([c[0][0] for c in cov], np.uint64), np.array([c[1][0] for c in cov], np.uint64)))
+    return out
+
+
 def _run_store(ctx, comm, rb, world, rank):
-    """This rank's store: its sliced batch through acc_partial_deps_batch, then acc_partial_deps_reduce; host copies."""
+    """This rank's store: its sliced batch through acc_partial_deps_batch (+ the store covering's invariant checks),
+    then acc_partial_deps_reduce with the store's covering; host copies."""
     from accord_amd import sharded as S
     from accord_amd.deps import rmm_copy_out
-    bounds = S.even_split(np.concatenate([rb.keys.key_code, rb.rng_start, rb.rng_end]).astype(np.uint64), world)
-    sub, gidx = S.store_range_batch(rb, bounds, rank)
+    sub, gidx = S.store_range_batch(rb, _bounds(rb, world), rank)
     keep = []
     rbi = ctx.range_batch_in(sub, keep)
     ctx.partial_deps_batch_raw(rbi)
-    kv, rv = S.partial_deps_reduce(ctx, comm, rbi, rb.n_txn, gidx.astype(np.uint32))
+    cov = _store_covering(rb, world, rank)
+    S.partial_deps_covering(ctx, rbi, cov)
+    kv, rv, cv = S.partial_deps_reduce(ctx, comm, rbi, rb.n_txn, gidx.astype(np.uint32), covering=cov)
     ng = int(kv.n_groups)
     key = S.merged_to_host(ctx, kv)
     rng = rmm_copy_out(ctx, ng, rv.range_deps, True)
-    return key, rng
+    return key, rng, S.covering_to_host(ctx, cv)
+
+
+def _check_covering(got, want, label):
+    cid, mask, table = got
+    assert len(cid) == len(want), label
+    for i, (m, ws, we) in enumerate(want):
+        assert int(mask[i]) == m, (label, i, int(mask[i]), m)
+        gs, ge = table[int(cid[i])]
+        assert np.array_equal(gs, ws) and np.array_equal(ge, we), (label, i, gs, ge, ws, we)
 
 
 def _check(key, rng, want_key, want_rng, label):
@@ -76,9 +118,10 @@ def test_partial_deps_reduce_rccl_world_one():
     want_key, want_rng = _expected(rb, 1, 0)
     with Context(0) as ctx:
         comm = S.Comm.rccl(ctx, 1, 0)
-        key, rng = _run_store(ctx, comm, rb, 1, 0)
+        key, rng, cov = _run_store(ctx, comm, rb, 1, 0)
         comm.close()
     _check(key, rng, want_key, want_rng, "rccl world 1")
+    _check_covering(cov, _expected_covering(rb, 1, 0), "rccl world 1")
 
 
 def _free_port():
@@ -101,10 +144,11 @@ def _worker(rank, world, port, end_inclusive, errq):
         rb = _batch(0x7B72 + world, 10_000, end_inclusive)
         with Context(0) as ctx:
             comm = S.Comm.host(ctx, world, rank)
-            key, rng = _run_store(ctx, comm, rb, world, rank)
+            key, rng, cov = _run_store(ctx, comm, rb, world, rank)
             comm.close()
         want_key, want_rng = _expected(rb, world, rank)
         _check(key, rng, want_key, want_rng, f"rank {rank}/{world}")
+        _check_covering(cov, _expected_covering(rb, world, rank), f"rank {rank}/{world}")
         dist.barrier()
     except Exception as e:
         errq.put(f"rank {rank}: {e!r}")
@@ -134,3 +178,26 @@ def test_partial_deps_reduce_host_transport(world, end_inclusive):
             p.kill()
     assert not errs, errs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_partial_deps_covering_invariants():
+    """The PartialDeps constructor's checks (PartialDeps.java:52-58): a covering that misses a store key, or a range of
+    a RangeDeps, is IllegalStateException; the store's own covering passes."""
+    from accord_amd import sharded as S
+    from accord_amd.deps import Context, IllegalStateException
+    rb = _batch(0x7C73, 4_000)
+    with Context(0) as ctx:
+        keep = []
+        rbi = ctx.range_batch_in(rb, keep)
+        ctx.partial_deps_batch_raw(rbi)
+        lo, hi = _store_covering(rb, 1, 0)
+        S.partial_deps_covering(ctx, rbi, (lo, hi))
+        kd = ctx.calculate_partial_key_deps_mixed(rb)
+        ctx.partial_deps_batch_raw(rbi)
+        keys = np.unique(kd.kd_key)
+        mid = int(keys[len(keys) // 2])
+        with pytest.raises(IllegalStateException):   # the upper half of the key space uncovered
+            S.partial_deps_covering(ctx, rbi, (lo, np.array([mid - 1], np.uint64)))
+        with pytest.raises(IllegalStateException):   # no covering at all, deps present
+            S.partial_deps_covering(ctx, rbi, (np.zeros(0, np.uint64), np.zeros(0, np.uint64)))
+        S.partial_deps_covering(ctx, rbi, (lo, hi))  # the context stays usable
