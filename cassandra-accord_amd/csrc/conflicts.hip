@@ -102,8 +102,11 @@ __global__ __launch_bounds__(BLOCK) void k_mc_values(Upd u, uint64_t nv, const u
     if (i >= u.n + nv) return;
     uint64_t m, l;
     int32_t nd;
-    if (i < u.n) { m = u.xm[i]; l = u.xl[i]; nd = u.xn[i]; }
-    else { m = vm[i - u.n]; l = vl[i - u.n]; nd = vn[i - u.n]; }
+    // the stored values first, then the updates in batch order: the lowest index of a rank is the instance the
+    // reference's sequential merge keeps (Timestamp.max returns its first argument on compareTo == 0, and
+    // MaxConflicts.merge(existing, update) passes the existing value first; MaxConflicts.java:77-79)
+    if (i < nv) { m = vm[i]; l = vl[i]; nd = vn[i]; }
+    else { m = u.xm[i - nv]; l = u.xl[i - nv]; nd = u.xn[i - nv]; }
     w0[i] = m; w1[i] = l; w2[i] = (uint64_t)((uint32_t)nd ^ 0x80000000u);
 }
 
@@ -121,9 +124,9 @@ __global__ __launch_bounds__(BLOCK) void k_mc_parts(Upd u, const uint32_t *__res
     if (q >= Q) return;
     uint64_t a, b;
     uint32_t v;
-    if (q < u.K) { a = b = u.key[q]; v = kown[q]; }
-    else if (q < u.K + u.R) { range_closed(u.rs[q - u.K], u.re[q - u.K], u.ei, a, b); v = rown[q - u.K]; }
-    else { a = st[q - u.K - u.R]; b = en[q - u.K - u.R]; v = u.n + (uint32_t)(q - u.K - u.R); }
+    if (q < u.K) { a = b = u.key[q]; v = (uint32_t)nv + kown[q]; }
+    else if (q < u.K + u.R) { range_closed(u.rs[q - u.K], u.re[q - u.K], u.ei, a, b); v = (uint32_t)nv + rown[q - u.K]; }
+    else { a = st[q - u.K - u.R]; b = en[q - u.K - u.R]; v = (uint32_t)(q - u.K - u.R); }
     p.a[q] = a; p.b[q] = b; p.val[q] = v;
     p.cut[2 * q] = a;
     p.cut[2 * q + 1] = b == MAXC ? MAXC : b + 1;
@@ -153,17 +156,20 @@ __global__ __launch_bounds__(BLOCK) void k_mc_slots(uint64_t nc, const uint64_t 
     if (i < nc) slot[crank[i]] = cut[i];
 }
 
-// range chmax of (value rank + 1) over the part's slots [i0, i1]: atomicMax on the canonical segment-tree nodes
+// range chmax over the part's slots [i0, i1]: atomicMax on the canonical segment-tree nodes of
+// (value rank + 1) << 32 | ~value index -- the largest value, and among values equal under compareTo the lowest index:
+// the stored instance, then the earliest update of the batch, which is the instance the reference's sequential
+// MaxConflicts.merge(existing, update) keeps (Timestamp.max returns its first argument on a tie, Timestamp.java:265-268)
 __global__ __launch_bounds__(BLOCK) void k_mc_chmax(uint64_t Q, Parts p, const uint32_t *__restrict__ vrank,
                                                     const uint64_t *__restrict__ slot, uint32_t m, uint32_t M,
-                                                    uint32_t *__restrict__ tree)
+                                                    unsigned long long *__restrict__ tree)
 {
     const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (q >= Q) return;
     const uint64_t a = p.a[q], b = p.b[q];
     const uint32_t i0 = lower_u64(slot, m, a);
     const uint32_t i1 = b == MAXC ? m - 1 : lower_u64(slot, m, b + 1) - 1;
-    const uint32_t v = vrank[p.val[q]] + 1;
+    const unsigned long long v = ((unsigned long long)(vrank[p.val[q]] + 1) << 32) | (0xFFFFFFFFu - p.val[q]);
     uint32_t l = i0 + M, r = i1 + M + 1;   // half-open [l, r) over the leaves
     while (l < r) {
         if (l & 1) atomicMax(&tree[l++], v);
@@ -173,25 +179,27 @@ __global__ __launch_bounds__(BLOCK) void k_mc_chmax(uint64_t Q, Parts p, const u
 }
 
 // each slot's value (max on its root path) and the run boundaries of equal non-empty values
-__global__ __launch_bounds__(BLOCK) void k_mc_leaves(uint32_t m, uint32_t M, const uint32_t *__restrict__ tree,
-                                                     uint32_t *__restrict__ sval)
+__global__ __launch_bounds__(BLOCK) void k_mc_leaves(uint32_t m, uint32_t M, const unsigned long long *__restrict__ tree,
+                                                     uint64_t *__restrict__ sval)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
-    uint32_t v = 0;
+    unsigned long long v = 0;
     for (uint32_t nd = i + M; nd >= 1; nd >>= 1) v = max(v, tree[nd]);
     sval[i] = v;
 }
-__global__ __launch_bounds__(BLOCK) void k_mc_runflag(uint32_t m, const uint32_t *__restrict__ sval, uint32_t *__restrict__ f)
+// runs of slots whose values are equal (Timestamp.equals: the same rank) coalesce into one interval holding the run's
+// first instance, as the builder skips an appended value equal to the last one
+__global__ __launch_bounds__(BLOCK) void k_mc_runflag(uint32_t m, const uint64_t *__restrict__ sval, uint32_t *__restrict__ f)
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < m) f[i] = sval[i] != 0 && (i == 0 || sval[i - 1] != sval[i]);
+    if (i < m) f[i] = sval[i] != 0 && (i == 0 || (sval[i - 1] >> 32) != (sval[i] >> 32));
 }
 
 // the new interval list: a run's first slot writes its start and value, its last slot its end
-__global__ __launch_bounds__(BLOCK) void k_mc_emit(uint32_t m, const uint64_t *__restrict__ slot, const uint32_t *__restrict__ sval,
+__global__ __launch_bounds__(BLOCK) void k_mc_emit(uint32_t m, const uint64_t *__restrict__ slot, const uint64_t *__restrict__ sval,
                                                    const uint32_t *__restrict__ f, const uint32_t *__restrict__ fincl,
-                                                   const uint32_t *__restrict__ first, const uint64_t *__restrict__ w0,
+                                                   const uint64_t *__restrict__ w0,
                                                    const uint64_t *__restrict__ w1, const uint64_t *__restrict__ w2,
                                                    uint64_t *__restrict__ st, uint64_t *__restrict__ en, uint64_t *__restrict__ vm,
                                                    uint64_t *__restrict__ vl, int32_t *__restrict__ vn)
@@ -200,11 +208,11 @@ __global__ __launch_bounds__(BLOCK) void k_mc_emit(uint32_t m, const uint64_t *_
     if (i >= m || sval[i] == 0) return;
     const uint32_t k = fincl[i] - 1;
     if (f[i]) {
-        const uint32_t src = first[sval[i] - 1];   // an input instance of the value's rank
+        const uint32_t src = 0xFFFFFFFFu - (uint32_t)sval[i];   // the slot's instance
         st[k] = slot[i];
         vm[k] = w0[src]; vl[k] = w1[src]; vn[k] = (int32_t)((uint32_t)w2[src] ^ 0x80000000u);
     }
-    if (i + 1 == m || sval[i + 1] != sval[i]) en[k] = i + 1 == m ? MAXC : slot[i + 1] - 1;
+    if (i + 1 == m || (sval[i + 1] >> 32) != (sval[i] >> 32)) en[k] = i + 1 == m ? MAXC : slot[i + 1] - 1;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mc_blockmax(uint64_t nv, const uint64_t *__restrict__ vm, const uint64_t *__restrict__ vl,
@@ -260,7 +268,10 @@ __global__ __launch_bounds__(BLOCK) void k_mc_query(Qs q, Map mp, uint64_t *__re
         e |= E_OFF;
         p1 = p0;   // never index through bad offsets
     }
-    for (uint32_t p = p0 + lane; p < p1; p += 64) {
+    // each lane takes a contiguous chunk of the parts, so folding the lanes in order visits the intervals in key order
+    // and a tie keeps the first maximum visited, as foldl with Timestamp::max does (MaxConflicts.get)
+    const uint32_t per = (p1 - p0 + 63) / 64, pa = min(p1, p0 + lane * per), pb = min(p1, pa + per);
+    for (uint32_t p = pa; p < pb; ++p) {
         const uint64_t s = q.ps[p], t = isr ? q.pe[p] : s;
         if (isr && s >= t) { e |= E_RANGE; continue; }
         if (p > p0 && (isr ? q.pe[p - 1] > s : q.ps[p - 1] >= s)) e |= E_SORT;
@@ -396,13 +407,14 @@ void mc_update(acc_ctx *ctx, acc_maxconflicts *M, const acc_conflicts_in *ui)
     // 3. range chmax through a segment tree over the slots
     uint32_t Mp = 1;
     while (Mp < m) Mp <<= 1;
-    uint32_t *tree = ctx->get<uint32_t>("mc_tree", 2 * (size_t)Mp);
-    ACC_HIP(hipMemsetAsync(tree, 0, 2 * (size_t)Mp * 4, st));
+    unsigned long long *tree = ctx->get<unsigned long long>("mc_tree64", 2 * (size_t)Mp);
+    ACC_HIP(hipMemsetAsync(tree, 0, 2 * (size_t)Mp * 8, st));
     launch(ctx, "mc_chmax", k_mc_chmax, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, Q, pt, (const uint32_t *)vr.rank,
            (const uint64_t *)slot, m, Mp, tree);
-    uint32_t *sval = ctx->get<uint32_t>("mc_sval", m), *f = ctx->get<uint32_t>("mc_f", m), *fi = ctx->get<uint32_t>("mc_fi", m);
-    launch(ctx, "mc_leaves", k_mc_leaves, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, Mp, (const uint32_t *)tree, sval);
-    launch(ctx, "mc_runflag", k_mc_runflag, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, (const uint32_t *)sval, f);
+    uint64_t *sval = ctx->get<uint64_t>("mc_sval64", m);
+    uint32_t *f = ctx->get<uint32_t>("mc_f", m), *fi = ctx->get<uint32_t>("mc_fi", m);
+    launch(ctx, "mc_leaves", k_mc_leaves, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, Mp, (const unsigned long long *)tree, sval);
+    launch(ctx, "mc_runflag", k_mc_runflag, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, (const uint64_t *)sval, f);
     uint32_t *nnew = ctx->get<uint32_t>("mc_nnew", 1);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, f, fi, m, false, nnew);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, nnew, 4, hipMemcpyDeviceToHost, st));
@@ -427,8 +439,8 @@ void mc_update(acc_ctx *ctx, acc_maxconflicts *M, const acc_conflicts_in *ui)
         free_new();
         throw;
     }
-    launch(ctx, "mc_emit", k_mc_emit, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, (const uint64_t *)slot, (const uint32_t *)sval,
-           (const uint32_t *)f, (const uint32_t *)fi, (const uint32_t *)vr.first, (const uint64_t *)w0, (const uint64_t *)w1,
+    launch(ctx, "mc_emit", k_mc_emit, dim3(grid_for(m, BLOCK)), dim3(BLOCK), 0, m, (const uint64_t *)slot, (const uint64_t *)sval,
+           (const uint32_t *)f, (const uint32_t *)fi, (const uint64_t *)w0, (const uint64_t *)w1,
            (const uint64_t *)w2, nm.st, nm.en, nm.vm, nm.vl, nm.vn);
     nm.nv = nn;
     nm.cap = cap;

@@ -188,6 +188,41 @@ def test_max_conflicts_code_space_ends(ctx):
             np.testing.assert_array_equal(g[k], o[k], err_msg=f"ei {ei} {k}")
 
 
+def test_max_conflicts_keeps_existing_instance(ctx):
+    """Equal executeAts under compareTo that differ in non-identity flag bits (lsb bit 5 / 6): the merged map keeps the
+    existing instance, then the earliest update of a batch, as MaxConflicts.merge(existing, update) does with
+    Timestamp.max (a.compareTo(b) >= 0 ? a : b; Timestamp.java:265-268, MaxConflicts.java:77-79)."""
+    from accord_amd.deps import MaxConflictsMap
+    import accord_amd.workload as W
+
+    def upd(flags_keys):
+        ts = [tuple(int(x) for x in W.encode_ts(1, 100, f, 1)) for f, _ in flags_keys]
+        ko = np.concatenate([[0], np.cumsum([len(k) for _, k in flags_keys])]).astype(np.uint32)
+        return dict(end_inclusive=1, xmsb=np.array([t[0] for t in ts], np.uint64),
+                    xlsb=np.array([t[1] for t in ts], np.uint64), xnode=np.array([t[2] for t in ts], np.int32),
+                    key_off=ko, key=np.array([k for _, ks in flags_keys for k in ks], np.uint64),
+                    rng_off=np.zeros(len(flags_keys) + 1, np.uint32), rng_start=np.zeros(0, np.uint64),
+                    rng_end=np.zeros(0, np.uint64))
+
+    def get(m, keys):
+        q0 = W.encode_ts(1, 50, 0, 1)
+        n = len(keys)
+        q = dict(msb=np.full(n, q0[0], np.uint64), lsb=np.full(n, q0[1], np.uint64), node=np.full(n, 1, np.int32),
+                 is_range=np.zeros(n, np.uint8), part_off=np.arange(n + 1, dtype=np.uint32),
+                 part_start=np.array(keys, np.uint64), part_end=np.array(keys, np.uint64))
+        return m.get(q)["lsb"] & np.uint64(0xFFFF)
+
+    m = MaxConflictsMap(ctx, 1)
+    try:
+        # isolated keys (no two adjacent: equal neighbours would coalesce into one instance, as the builder does)
+        m.update(upd([(0x20, [5]), (0x40, [20]), (0x80, [20])]))     # within a batch: the earlier update on key 20
+        np.testing.assert_array_equal(get(m, [5, 20]), [0x20, 0x40])
+        m.update(upd([(0x100, [5, 30]), (0x200, [20, 40])]))         # across batches: the stored instance
+        np.testing.assert_array_equal(get(m, [5, 30, 20, 40]), [0x20, 0x100, 0x40, 0x200])
+    finally:
+        m.close()
+
+
 def test_max_conflicts_empty(ctx):
     from accord_amd.deps import IllegalArgumentException, max_conflicts
     upd, q = CC.conflicts_case(4, n_upd=10, n_query=5)
