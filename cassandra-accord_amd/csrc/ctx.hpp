@@ -107,6 +107,7 @@ struct acc_ctx {
     acc_deps_merge_view dm_view{};
     bool dm_valid = false;
     uint64_t rd_ent_hint = 0;   // RangeDeps raw pairs of the last batch (output capacity of the stabbing pass)
+    uint64_t kd_e_hint = 0;     // KeyDeps: capacity for the next batch's E (entries) from the batches seen (optimistic build)
     bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;
