@@ -66,6 +66,30 @@ def test_levelise_rejects_bad_dep(ctx):
         levelise(ctx, np.array([0, 1], np.uint64), np.array([7], np.uint32), np.array([0], np.uint32))
 
 
+@pytest.mark.parametrize("n,env", [(1000, None), (70000, None), (1000, "ACC_LV_WIN"), (1000, "ACC_LV_WAVES")])
+def test_levelise_rejects_decreasing_offsets(ctx, monkeypatch, n, env):
+    """Non-monotone offsets with off[n] == E (every range in bounds on its own, but ranges overlap, so the filtered
+    counts sum past E): each tier must fail with IllegalArgumentException before writing its lists."""
+    from accord_amd.deps import IllegalArgumentException, levelise
+    if env:
+        monkeypatch.setenv(env, "1")
+    E = 10
+    off = np.full(n + 1, E, np.uint64)
+    off[0] = 0
+    off[2] = 0            # txns 0 and 2 both read dep[0:10]: [0, 10, 0, 10, 10, ...]
+    er = np.arange(n, dtype=np.uint32)[::-1].copy()
+    dep = np.arange(n - E, n, dtype=np.uint32)   # all of them earlier in executeAt order than txns 0 and 2
+    with pytest.raises(IllegalArgumentException):
+        levelise(ctx, off, dep, er)
+    # the context stays usable: a valid graph right after
+    off2, dep2, er2 = random_graph(np.random.RandomState(7), 500, 6)
+    import oracle
+    lv, order, nl = levelise(ctx, off2, dep2, er2)
+    l2, o2, nl2 = oracle.levelise(off2, dep2, er2)
+    np.testing.assert_array_equal(lv, l2)
+    np.testing.assert_array_equal(order, o2)
+
+
 def test_merge_then_levelise_device(ctx):
     """Config 5 at reduced size through the bench's device chain: merged deps of every coordinated txn
     (KeyDeps.merge) levelised by executeAt, against the oracle merge + oracle levelise."""
@@ -122,7 +146,7 @@ def test_levelise_one_million(ctx):
     off = np.zeros(n + 1, np.uint64)
     np.cumsum(np.bincount(allsrc, minlength=n), out=off[1:])
     lv, order, nl = levelise(ctx, off, alld.astype(np.uint32), er)
-    assert ctx.stats().get("levelise.lds_tier") == 2 and ctx.stats().get("levelise.poll") == 1
+    assert ctx.stats().get("levelise.lds_tier") == 2 and ctx.stats().get("levelise.poll") == 8
     l2, o2, nl2 = oracle.levelise(off, alld.astype(np.uint32), er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
@@ -130,15 +154,23 @@ def test_levelise_one_million(ctx):
 
 
 @pytest.mark.parametrize("env,n,max_deps,tier", [
-    ({}, 2000, 300, 1),                                      # LDS walk (default up to 65,535 txns), default chunks
+    ({}, 2000, 300, 1),                                      # LDS walk (default below 4,096 txns), default chunks
     ({"ACC_LV_CH": "64"}, 2000, 300, 1),                     # LDS walk, 64-entry chunks: long lists read from HBM
-    ({"ACC_LV_CH": "256"}, 20000, 12, 1),                    # many rounds, rounds of > 2048 positions
-    ({}, 65535, 6, 1),                                       # largest LDS-walk graph (u16 levels and positions)
-    ({}, 65536, 6, 2),                                       # beyond the LDS walk: the windowed walk (batch polling)
-    ({"ACC_LV_WIN": "1"}, 2000, 300, 2),                     # windowed walk, sliding cursor: two windows
+    ({"ACC_LV_LDS": "1", "ACC_LV_CH": "256"}, 20000, 12, 1), # many rounds, rounds of > 2048 positions
+    ({"ACC_LV_LDS": "1"}, 65535, 6, 1),                      # largest LDS-walk graph (u16 levels and positions)
+    ({}, 20000, 12, 1),                                      # the LDS walk up to 65,535 txns
+    ({"ACC_LV_W1": "1"}, 32768, 6, 3),                       # the LDS windowed walk: its largest graph
+    ({"ACC_LV_W1": "1"}, 20000, 12, 3),
+    ({"ACC_LV_W1": "1"}, 1024, 40, 3),                       # exactly one window
+    ({"ACC_LV_W1": "1"}, 3073, 900, 3),                      # a partial last window; windows beyond the successor buffer
+    ({"ACC_LV_W1": "1"}, 1025, 1100, 3),                     # two windows, the first beyond the successor buffer
+    ({"ACC_LV_W1": "1"}, 5000, 30, 3),                       # far deps for windows 2..4
+    ({}, 65536, 6, 2),                                       # beyond the LDS tiers: one launch per window
+    ({"ACC_LV_POLL": "1"}, 65536, 6, 2),                     # the same, batch polling
+    ({"ACC_LV_WIN": "1"}, 2000, 300, 2),                     # windowed walk, pending-set walk: two windows
     ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 2000, 300, 2), # windowed walk, batch polling
-    ({"ACC_LV_WIN": "1"}, 5000, 30, 2),                      # far deps gathered for windows 2..4 (batch polling)
-    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "8"}, 5000, 30, 2),  # the same, sliding cursor
+    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 5000, 30, 2),  # far deps gathered for windows 2..4 (batch polling)
+    ({"ACC_LV_WIN": "1"}, 5000, 30, 2),                      # the same, pending-set walk
     ({"ACC_LV_WIN": "1"}, 1024, 40, 2),                      # exactly one window
     ({"ACC_LV_WIN": "1"}, 3073, 900, 2),                     # a partial last window, long lists
     ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 3073, 900, 2), # the same, batch polling
@@ -159,7 +191,7 @@ def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps, tier):
     assert nl == nl2
 
 
-@pytest.mark.parametrize("walk", ["windowed", "windowed_poll1", "lds", "waves"])
+@pytest.mark.parametrize("walk", ["w1", "windowed", "windowed_poll1", "lds", "waves"])
 def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
     """A config-5-shaped merged graph (16,384 txns, deps on recent txns, hundreds of levels) through the windowed walk,
     the LDS walk and the persistent-wave walk: identical levels and order, equal to the oracle."""
@@ -169,8 +201,12 @@ def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
         monkeypatch.setenv("ACC_LV_WAVES", "1")
     if walk.startswith("windowed"):
         monkeypatch.setenv("ACC_LV_WIN", "1")
-    if walk == "windowed_poll1":
+    if walk.endswith("_poll1"):
         monkeypatch.setenv("ACC_LV_POLL", "1")
+    if walk == "lds":
+        monkeypatch.setenv("ACC_LV_LDS", "1")
+    if walk == "w1":
+        monkeypatch.setenv("ACC_LV_W1", "1")
     rng = np.random.RandomState(55)
     n = 16384
     er = rng.permutation(n).astype(np.uint32)
@@ -185,7 +221,8 @@ def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
     off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
     dep = np.concatenate(deps).astype(np.uint32)
     lv, order, nl = levelise(ctx, off, dep, er)
-    assert ctx.stats().get("levelise.lds_tier") == {"windowed": 2, "windowed_poll1": 2, "lds": 1, "waves": 0}[walk]
+    assert ctx.stats().get("levelise.lds_tier") == {"w1": 3, "windowed": 2, "windowed_poll1": 2,
+                                                    "lds": 1, "waves": 0}[walk]
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
