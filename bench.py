@@ -22,7 +22,8 @@ permutation), key range-sharded over the N GPUs the way CommandStores shard a no
 CommandStore holding the txns that touch its keys. A step = the store's acc_keydeps_batch + acc_shard_pack + the
 all-to-all(v) of per-txn fragments to the txn's home GPU (RCCL over xGMI) + acc_shard_merge (PartialDeps.with fold =
 batched KeyDeps.merge): PreAccept.reduce on device. Weak scaling (~8M pairs per GPU); value = global pairs / the
-slowest rank's time. --config 4 at N > 1 runs independent snapshots per rank. Prints ONE JSON line on rank 0.
+slowest rank's time. --config 4 at N > 1: the config-4 batch EvenSplit over N stores, each step a store's whole
+PartialDeps + acc_partial_deps_reduce (strong scaling). Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes as C
@@ -54,6 +55,11 @@ TAG_KERNEL = {
     "rd_build_s16": "k_rd_build_seg<16,",
     "rd_build_s32": "k_rd_build_seg<32,",
     "rd_build_s64": "k_rd_build_seg<64,",
+    # the levelise walk tiers (levelise.hip: one tag per tier)
+    "lv_walk_lds": "k_lv_lds",
+    "lv_walk_win": "k_lw_step<",
+    "lv_walk_w1": "k_lv_win1<",
+    "lv_walk_waves": "k_lv_waves",
 }
 
 
@@ -116,7 +122,7 @@ def roofline(step_bytes, step, steps, ms_per_step, config, variant="", profiled=
         exact = TAG_KERNEL.get(dom_name)
         if exact and exact in kernels:
             ks = [kernels[exact]]
-        elif exact and exact.endswith(","):
+        elif exact and exact.endswith((",", "<")):
             ks = [v for name, v in kernels.items() if name.startswith(exact)]
         else:
             ks = [v for name, v in kernels.items() if name.split("<")[0] in ("k_" + dom_name, dom_name)]
@@ -495,6 +501,8 @@ def run_config2_sharded(args, world, rank, local, dev):
             "n_txn_global": n_global,
             "pairs_global": n_global * 8,
             "pairs_per_gpu_max": int(mx[0].item()),
+            "pairs_per_gpu_mean": round(float(tot[0].item()) / world, 1),
+            "imbalance_max_over_mean": round(float(mx[0].item()) * world / float(tot[0].item()), 4) if tot[0].item() else None,
             "setup_store_batch_s": round(t_gen, 2),
             "parallelism": f"key-range shards x{world} (CommandStores) + all-to-all(v) reduce",
         },
@@ -554,6 +562,91 @@ def run_config4(args, world, rank, local, dev):
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = rangedeps_cpu_baseline(rb)
     return ctx, timing, elapsed, result
+
+
+def run_config4_sharded(args, world, rank, local, dev):
+    """Config 4 over N CommandStores (N > 1): the one config-4 mixed batch, EvenSplit over N key ranges; each rank
+    holds its store's slice (range commands sliced to the store, impl/InMemoryCommandStore.java:739-761), and a step is
+    the store's whole PartialDeps (acc_partial_deps_batch: KeyDeps of key and range txns + RangeDeps) and PreAccept.reduce
+    across the stores (acc_partial_deps_reduce: one size exchange + one grouped all-to-all(v) over acc_comm, KeyDeps.with
+    / RangeDeps.with / covering folds on the home rank; PreAccept.java:141-156, CommandStores.java:575-592). Strong
+    scaling: value = the global batch's key probes / the slowest rank's step."""
+    import torch
+    import torch.distributed as dist
+    from accord_amd import _lib as L
+    from accord_amd import sharded as S
+    from accord_amd import workload as W
+    from accord_amd.deps import Context
+
+    t_gen = time.perf_counter()
+    rb = W.rangedeps_batch(int(20_000_000 * args.scale), W.CONFIG_SEEDS["4"])
+    bounds = S.even_split(np.concatenate([rb.keys.key_code, rb.rng_start, rb.rng_end]).astype(np.uint64), world)
+    sub, g = S.store_range_batch(rb, bounds, rank)
+    lo, hi = S.store_ranges_bound(bounds, rank, rb.end_inclusive)
+    cov = (np.array([lo], np.uint64), np.array([hi], np.uint64))
+    n_global, probes_global = rb.n_txn, rb.keys.n_pairs + rb.n_ranges
+    del rb
+    t_gen = time.perf_counter() - t_gen
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in sub.arrays().items()}
+    gidx = torch.from_numpy(g.astype(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    P, R = sub.keys.n_pairs, sub.n_ranges
+    bi = L.RangeBatchIn(sub.n_txn, L.ACC_MEM_DEVICE, P, R,
+                        L.TsCols(t["txn_msb"].data_ptr(), t["txn_lsb"].data_ptr(), t["txn_node"].data_ptr()),
+                        L.TsCols(t["exe_msb"].data_ptr(), t["exe_lsb"].data_ptr(), t["exe_node"].data_ptr()),
+                        t["status"].data_ptr(), t["key_off"].data_ptr(), t["key_code"].data_ptr(),
+                        t["rng_off"].data_ptr(), t["rng_start"].data_ptr(), t["rng_end"].data_ptr(),
+                        int(sub.end_inclusive), 0)
+    ctx = Context(local, timing=True)
+    if dist.get_backend() == "gloo":   # the one-GPU rehearsal: every rank on GPU 0, the host transport over gloo
+        comm, exchange = S.Comm.host(ctx, world, rank), "acc_comm (host transport over gloo) + acc_partial_deps_reduce"
+    else:
+        comm, exchange = S.Comm.rccl(ctx, world, rank), "acc_comm (RCCL over xGMI) + acc_partial_deps_reduce"
+    ctx.comm = comm
+    info = {}
+
+    def fn():
+        kv, rv = ctx.partial_deps_batch_raw(bi)
+        info["kv"], info["rv"] = kv, rv
+        info["red"] = S.partial_deps_reduce(ctx, comm, bi, n_global, gidx, covering=cov)
+        return kv
+
+    step = Step(ctx, fn)
+    elapsed = timed_steps(args, world, dev, step)
+    kv, rv = info["kv"], info["rv"]
+    b_in, b_out = rangedeps_bytes(sub.n_txn, P, R, rv.total_ranges, rv.total_edges, rv.total_deps, rv.n_ranges)
+    sent = int(ctx.stats().get("exchange.bytes_sent", 0))
+    loc = torch.tensor([P + R, sent, int(kv.total_edges) + int(rv.total_edges)], dtype=torch.float64,
+                       device=dev if dist.get_backend() == "nccl" else "cpu")
+    tot, mx = loc.clone(), loc.clone()
+    dist.all_reduce(tot)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    mean = float(tot[0].item()) / world
+    result = {
+        "metric": "PartialDeps key probes resolved/sec (node)",
+        "value": round(probes_global * args.steps / elapsed, 1),
+        "unit": "key probes/s",
+        "dtype": "u32/u64 (integer)",
+        "data": "synthetic (seeded SplitMix64, SURVEY.md §8(d) config 4)",
+        "config": {
+            "workload": f"config4 range-sharded: the mixed batch of {n_global} txns (10M range txns, 1 EndInclusive range "
+                        f"each + 10M key txns x 4 keys) EvenSplit over {world} stores; per step each store's "
+                        "acc_partial_deps_batch (KeyDeps + RangeDeps) and acc_partial_deps_reduce (KeyDeps.with, "
+                        "RangeDeps.with and covering folds on the home rank)",
+            "n_txn_global": n_global,
+            "key_probes_global": probes_global,
+            "key_probes_per_gpu_max": int(mx[0].item()),
+            "key_probes_per_gpu_mean": round(mean, 1),
+            "imbalance_max_over_mean": round(float(mx[0].item()) / mean, 4) if mean else None,
+            "dep_entries_total": int(tot[2].item()),
+            "setup_store_batch_s": round(t_gen, 2),
+            "parallelism": f"key-range shards x{world} (CommandStores) + all-to-all(v) PartialDeps reduce",
+        },
+        "exchange": {"bytes_sent_total": int(tot[1].item()), "bytes_sent_max_rank": int(mx[1].item()), "path": exchange,
+                     "setup_backend": dist.get_backend() + (" (RCCL over xGMI)" if dist.get_backend() == "nccl" else "")},
+        "roofline": roofline(b_in + b_out, step, args.steps, elapsed * 1000.0 / args.steps, args.config, profiled=False),
+    }
+    return ctx, step.diag, elapsed, result
 
 
 def mixed_keydeps_leg(bi, local, calls=3):
@@ -738,7 +831,7 @@ def main():
 
     world, rank, local, dev = dist_setup(args)
     keyed = run_config2 if world == 1 else run_config2_sharded
-    run = {"2": keyed, "3": keyed, "4": run_config4, "5": run_config5}[args.config]
+    run = {"2": keyed, "3": keyed, "4": run_config4 if world == 1 else run_config4_sharded, "5": run_config5}[args.config]
     ctx, timing, elapsed, result = run(args, world, rank, local, dev)
     out = {
         "metric": result.pop("metric"),
@@ -749,7 +842,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1000.0 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "strong" if args.config == "3" and world > 1 else "weak",
+        "scaling": "strong" if args.config in ("3", "4") and world > 1 else "weak",
         "vs_baseline": None,
     }
     out.update(result)
