@@ -191,7 +191,8 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
             ~Join() { if (t.joinable()) t.join(); if (e) (void)hipEventDestroy(e); }
         } join{ th, ev };
         if (child) {
-            child->flags = ctx->flags;
+            child->flags = ctx->flags;            // acc_opts holds only flags; the timing filter too
+            child->time_only = ctx->time_only;
             sd.ready = [&](const acc::SharedDict &d) {
                 ACC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 ACC_HIP(hipEventRecord(ev, ctx->stream));
@@ -213,6 +214,16 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
             ctx->rd_valid = child->rd_valid;
             ctx->rd_ent_hint = child->rd_ent_hint;
             for (const auto &kv : child->stats) ctx->stat(kv.first.c_str(), kv.second);
+            // the RangeDeps half's kernel timings (resolved by the child's sync) join this context's, under their own
+            // launch tags: acc_timing readers see both halves of the call
+            for (auto &sl : child->slots) {
+                if (!sl.launches) continue;
+                acc::TimingSlot &d = ctx->slots[ctx->slot(sl.name.c_str())];
+                d.total_ms += sl.total_ms;
+                d.launches += sl.launches;
+                sl.total_ms = 0;
+                sl.launches = 0;
+            }
         } else {
             acc::rangedeps_batch(ctx, in, range_view, &sd);   // no key pairs (no dictionary to share), or serial
         }

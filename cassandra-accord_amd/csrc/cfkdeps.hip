@@ -15,7 +15,8 @@
 //      array;
 //      a key whose missing[] outgrows its guess is flagged; the flagged keys' guesses grow 4x (up to the proven bound)
 //      and the replay runs again, so a hot key with thousands of dep-carrying updates costs the space it really uses,
-//      not the quadratic bound;
+//      not the quadratic bound; from the third round on a flagged key takes the bound at once, so a batch replays at
+//      most four times (every key replays: the pool's layout moves when the flagged keys grow);
 //   4. final sizes, two scans, and a compaction into the key-major output (keys without entries dropped).
 // Errors: a status going back (IllegalStateException "stale status", ACC_E_STATE), an addition equal to an existing
 // TxnId or depsKnownBefore equal to a TxnId (the reference's checkState, ACC_E_STATE), malformed input (ACC_E_ARG).
@@ -472,15 +473,18 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint64_t T, const uint32_t 
     ovf[k] = 0;
 }
 
-// keys whose missing[] outgrew the guess: 4x, up to the proven bound (at the bound: an internal error)
+// keys whose missing[] outgrew the guess: 4x, up to the proven bound (at the bound: an internal error); from the
+// CD_GROW_STEPS-th regrow round on, straight to the bound, so a batch is replayed at most CD_GROW_STEPS + 2 times
+constexpr uint32_t CD_GROW_STEPS = 2;
 __global__ __launch_bounds__(BLOCK) void k_cd_grow(uint32_t nkeys, uint32_t *__restrict__ ovf, uint64_t *__restrict__ mcap,
-                                                   const uint64_t *__restrict__ mmax, uint64_t *__restrict__ err)
+                                                   const uint64_t *__restrict__ mmax, uint64_t *__restrict__ err,
+                                                   uint32_t round)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys || !ovf[k]) return;
     ovf[k] = 0;
     if (mcap[k] >= mmax[k]) { atomicOr((unsigned long long *)err, (unsigned long long)E_CAP); return; }
-    const uint64_t g = 4 * mcap[k];
+    const uint64_t g = round >= CD_GROW_STEPS ? mmax[k] : 4 * mcap[k];
     mcap[k] = g < mmax[k] ? g : mmax[k];
 }
 
@@ -953,7 +957,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         if (!(e & E_MCAP)) break;
         ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
         launch(ctx, "cd_grow", k_cd_grow, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, ovf, mcap,
-               (const uint64_t *)mmax, errs);
+               (const uint64_t *)mmax, errs, regrow);
         scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, moff + nkeys, 8, hipMemcpyDeviceToHost, st));

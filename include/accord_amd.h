@@ -246,7 +246,8 @@ int acc_rangedeps_copy_out(acc_ctx *ctx, acc_rangedeps_out *out);
  * primitives/PartialDeps.java:31-45 / Deps.AbstractBuilder.add primitives/Deps.java:56-71): the KeyDeps half of
  * acc_keydeps_mixed and the RangeDeps half of acc_rangedeps_batch, sharing one dictionary pass (and its validation) and
  * the staged inputs. Both views stay valid until the next compute call; acc_keydeps_copy_out / acc_rangedeps_copy_out
- * copy them. */
+ * copy them. The RangeDeps half runs concurrently on a child context created on first use (own stream and its own
+ * grow-only device buffers, held until acc_destroy of ctx; environment ACC_PD_SERIAL=1 keeps both halves on ctx). */
 int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view *key_view,
                            acc_rangedeps_view *range_view);
 
