@@ -65,21 +65,34 @@ struct Info {
 __device__ __forceinline__ bool dkb_self(const Info &x) { return x.st == PRE || x.st == ACC || x.self; }
 __device__ __forceinline__ const Ts &dkb(const Info &x) { return dkb_self(x) ? x.id : x.ex; }
 
+// The working buffers of the 64 keys of one wave are interleaved element by element (key k = lane k % 64 of wave k / 64:
+// element i of its buffer at [i * CD_W + lane]), so when the lanes walk their keys' arrays side by side -- the replay
+// rebuilds every array per update -- each wave-wide access is one contiguous span instead of 64 scattered lines.
+constexpr long CD_W = 64;
+template <class T>
+struct SP {   // a lane's strided view of an interleaved buffer
+    T *p;
+    __device__ T &operator[](long i) const { return p[i * CD_W]; }
+    __device__ SP operator+(long k) const { return SP{ p + k * CD_W }; }
+    __device__ bool operator==(const SP &o) const { return p == o.p; }
+};
+
 struct Buf {
-    Info *e;
-    Ts *m;
+    SP<Info> e;
+    SP<Ts> m;
     uint32_t n, mtop;
 };
 
 struct Work {   // one key's working space
     Buf a, b;
     uint32_t ecap, mcap;
-    Ts *tmiss;      // the new TxnInfo's missing[] (ecap)
-    Ts *adds;       // additions (dcap)
-    Ts *owned;      // insertMissing result (dcap + 1)
+    SP<Ts> tmiss;   // the new TxnInfo's missing[] (ecap)
+    SP<Ts> adds;    // additions (dcap)
+    SP<Ts> owned;   // insertMissing result (dcap + 1)
 };
 
-__device__ long bsearch_ts(const Ts *a, long from, long to, const Ts &k)   // Arrays.binarySearch
+template <class P>
+__device__ long bsearch_ts(P a, long from, long to, const Ts &k)   // Arrays.binarySearch
 {
     long lo = from, hi = to - 1;
     while (lo <= hi) {
@@ -103,12 +116,12 @@ __device__ long bsearch_info(const Buf &b, long from, long to, const Ts &k)
 struct Ctx {
     Work w;
     uint64_t err;
-    __device__ bool room_e(uint32_t n) { if (n > w.ecap) { err |= E_CAP; return false; } return true; }
+    __device__ __forceinline__ bool room_e(uint32_t n) { if (n > w.ecap) { err |= E_CAP; return false; } return true; }
     // missing areas: beyond the key's current guess (E_MCAP: grown and replayed by the host)
-    __device__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_MCAP; return false; } return true; }
+    __device__ __forceinline__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_MCAP; return false; } return true; }
 
     // append entry x of src with its missing[] copied (dropping `drop` when given) to dst
-    __device__ void put(Buf &dst, const Info &x, const Ts *src_m, const Ts *drop)
+    __device__ __forceinline__ void put(Buf &dst, const Info &x, SP<Ts> src_m, const Ts *drop)
     {
         Info y = x;
         y.ms = dst.mtop;
@@ -124,7 +137,7 @@ struct Ctx {
         if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
     }
     // x with `ins` inserted into its missing[] (SortedArrays.insert)
-    __device__ void put_with_one(Buf &dst, const Info &x, const Ts *src_m, const Ts &ins)
+    __device__ __forceinline__ void put_with_one(Buf &dst, const Info &x, SP<Ts> src_m, const Ts &ins)
     {
         Info y = x;
         y.ms = dst.mtop;
@@ -142,7 +155,7 @@ struct Ctx {
         if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
     }
     // mergeAndFilterMissing (:988-1025) of additions[0, count) into x's missing[], written to dst
-    __device__ void put_merged(Buf &dst, const Info &x, const Ts *src_m, const Ts *add, uint32_t count)
+    __device__ __forceinline__ void put_merged(Buf &dst, const Info &x, SP<Ts> src_m, SP<Ts> add, uint32_t count)
     {
         const uint32_t kinds = witnesses_mask(kind(x.id));
         uint32_t keep = 0;
@@ -152,7 +165,7 @@ struct Ctx {
         y.ms = dst.mtop;
         y.mn = 0;
         if (!room_m(dst, x.mn + keep)) return;
-        Ts *o = dst.m + dst.mtop;
+        SP<Ts> o = dst.m + dst.mtop;
         uint32_t i = 0, j = 0, n = 0;
         while (i < count && j < x.mn) {
             if ((kinds >> kind(add[i])) & 1u) {
@@ -168,7 +181,7 @@ struct Ctx {
         if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
     }
     // a new TxnInfo whose missing[] is in w.tmiss
-    __device__ void put_new(Buf &dst, const Info &x, uint32_t nm)
+    __device__ __forceinline__ void put_new(Buf &dst, const Info &x, uint32_t nm)
     {
         Info y = x;
         y.ms = dst.mtop;
@@ -180,7 +193,7 @@ struct Ctx {
         dst.mtop += y.mn;
         if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
     }
-    __device__ void put_tk(Buf &dst, const Ts &id)   // TxnInfo.create(txnId, TRANSITIVELY_KNOWN, txnId)
+    __device__ __forceinline__ void put_tk(Buf &dst, const Ts &id)   // TxnInfo.create(txnId, TRANSITIVELY_KNOWN, txnId)
     {
         Info y;
         y.id = id; y.ex = id; y.st = TK; y.self = 1; y.ms = dst.mtop; y.mn = 0;
@@ -188,7 +201,7 @@ struct Ctx {
     }
 
     // insert(pos, TxnInfo) (:880-897) with insertInfoAndOneMissing (:899-944); the new info's missing[] in tmiss
-    __device__ void insert_plain(const Buf &A, Buf &B, uint32_t pos, const Info &ins, uint32_t nm)
+    __device__ __forceinline__ void insert_plain(const Buf &A, Buf &B, uint32_t pos, const Info &ins, uint32_t nm)
     {
         const bool plain = ins.st >= COMMITTED;
         for (uint32_t i = 0; i < pos; ++i) {
@@ -204,7 +217,7 @@ struct Ctx {
         }
     }
     // update(pos, txnId, cur, new) (:865-875): the entry replaced, removeMissing (:946-972) when it becomes committed
-    __device__ void update_plain(const Buf &A, Buf &B, uint32_t pos, const Info &nw, uint32_t nm)
+    __device__ __forceinline__ void update_plain(const Buf &A, Buf &B, uint32_t pos, const Info &nw, uint32_t nm)
     {
         const bool crossed = A.e[pos].st < COMMITTED && nw.st >= COMMITTED;
         for (uint32_t i = 0; i < A.n; ++i) {
@@ -214,8 +227,8 @@ struct Ctx {
     }
 
     // computeInfoAndAdditions (:1057-1149): the new TxnInfo (missing[] to tmiss) and the deps this CFK lacks (adds)
-    __device__ Info compute_info(const Buf &A, long insert_pos, long update_pos, const Ts &id, uint32_t st, const Ts &ex_in,
-                                 const Ts *deps, uint32_t nd, uint32_t &nm, uint32_t &na)
+    __device__ __forceinline__ Info compute_info(const Buf &A, long insert_pos, long update_pos, const Ts &id, uint32_t st, const Ts &ex_in,
+                                 SP<Ts> deps, uint32_t nd, uint32_t &nm, uint32_t &na)
     {
         Info x;
         x.id = id; x.st = st; x.self = 1; x.ex = id; x.ms = 0; x.mn = 0;
@@ -248,15 +261,15 @@ struct Ctx {
     }
 
     // updateOrInsertWithAdditions (:772-863)
-    __device__ void with_additions(const Buf &A, Buf &B, long src_insert, long src_update, const Info &winfo, uint32_t nm,
+    __device__ __forceinline__ void with_additions(const Buf &A, Buf &B, long src_insert, long src_update, const Info &winfo, uint32_t nm,
                                    uint32_t na)
     {
-        const Ts *add = w.adds;
+        const SP<Ts> add = w.adds;
         long aip = bsearch_ts(add, 0, (long)na, winfo.id);
         if (aip >= 0) { err |= E_STATE; return; }
         aip = -1 - aip;
         const uint32_t target = (uint32_t)(src_insert + aip);
-        const Ts *msrc = add;
+        SP<Ts> msrc = add;
         const bool insert_self_missing = src_update < 0 && winfo.st < COMMITTED;
         uint32_t i = 0, j = 0, mcount = 0, mlimit = na, count = 0;
         while (i < A.n) {
@@ -312,7 +325,7 @@ struct Ctx {
     }
 
     // removeMissing over a whole buffer, in place (:946-972)
-    __device__ void remove_missing(Buf &B, const Ts &id)
+    __device__ __forceinline__ void remove_missing(Buf &B, const Ts &id)
     {
         for (uint32_t i = 0; i < B.n; ++i) {
             Info &x = B.e[i];
@@ -326,7 +339,7 @@ struct Ctx {
 
     // CommandsForKey.update(prev, next) (:657-722) on this key; returns true when the state moved to B
     // fl: bit 0 = acceptedOrCommitted changed, bit 1 = next.status() == AcceptedInvalidate
-    __device__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, const Ts *deps,
+    __device__ __forceinline__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, SP<Ts> deps,
                           uint32_t nd)
     {
         B.n = 0; B.mtop = 0;
@@ -496,22 +509,53 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kend(uint32_t nkeys, uint64_t T, u
 struct Pool {
     Info *e;
     Ts *m;
-    const uint64_t *eoff, *moff, *doff;   // exclusive scans of ecap, mcap, dcap
+    const uint64_t *ecw, *mcw, *dcw;   // per wave of 64 keys: the largest entry / missing / deps capacity of its keys
+    const uint64_t *eoffw, *toffw;     // exclusive scans over waves of 2 ecw and of 2 mcw + ecw + 2 dcw (per-lane units)
+    const uint32_t *perm;              // slot -> key: keys ordered by entry capacity, so a wave's keys are alike in size
 };
 
-// key k's working space: entries A | B at 2 * eoff[k]; its Ts region at 2 * moff[k] + eoff[k] + 2 * doff[k]: the new
-// TxnInfo's missing[] (ecap), additions (dcap), insertMissing / staged deps (dcap), then the A and B missing areas (mcap)
+// slot k's working space (key p.perm[k]), interleaved with its wave's slots: entries A | B (2 ecw), then its Ts
+// region: the new TxnInfo's missing[] (ecw), additions (dcw), insertMissing / staged deps (dcw), then the A and B missing
+// areas (mcw)
 __device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
 {
-    const uint64_t e0 = p.eoff[k], m0 = p.moff[k], d0 = p.doff[k], dk = p.doff[k + 1] - d0;
-    w.a.e = p.e + 2 * e0;
-    w.b.e = w.a.e + w.ecap;
-    Ts *R = p.m + 2 * m0 + e0 + 2 * d0;
+    const uint32_t wv = k / (uint32_t)CD_W, l = k % (uint32_t)CD_W;
+    const uint64_t ec = p.ecw[wv], mc = p.mcw[wv], dc = p.dcw[wv];
+    w.ecap = (uint32_t)ec;
+    w.mcap = (uint32_t)mc;
+    w.a.e = SP<Info>{ p.e + p.eoffw[wv] * CD_W + l };
+    w.b.e = w.a.e + (long)ec;
+    const SP<Ts> R{ p.m + p.toffw[wv] * CD_W + l };
     w.tmiss = R;
-    w.adds = R + w.ecap;
-    w.owned = w.adds + dk;
-    w.a.m = w.owned + dk;
-    w.b.m = w.a.m + w.mcap;
+    w.adds = R + (long)ec;
+    w.owned = w.adds + (long)dc;
+    w.a.m = w.owned + (long)dc;
+    w.b.m = w.a.m + (long)mc;
+}
+
+// per wave of 64 keys: the largest capacities of its keys and the wave's per-lane region sizes
+__global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_t *__restrict__ perm,
+                                                   const uint64_t *__restrict__ ecap,
+                                                   const uint64_t *__restrict__ mcap, const uint64_t *__restrict__ dcap,
+                                                   uint64_t *__restrict__ ecw, uint64_t *__restrict__ mcw,
+                                                   uint64_t *__restrict__ dcw, uint64_t *__restrict__ esz,
+                                                   uint64_t *__restrict__ tsz)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // slot
+    const uint32_t key = k < nkeys ? perm[k] : 0u;
+    uint64_t e = k < nkeys ? ecap[key] : 0, m = k < nkeys ? mcap[key] : 0, d = k < nkeys ? dcap[key] : 0;
+#pragma unroll
+    for (int x = 32; x >= 1; x >>= 1) {
+        e = max(e, (uint64_t)__shfl_xor((unsigned long long)e, x, 64));
+        m = max(m, (uint64_t)__shfl_xor((unsigned long long)m, x, 64));
+        d = max(d, (uint64_t)__shfl_xor((unsigned long long)d, x, 64));
+    }
+    const uint32_t wv = k / (uint32_t)CD_W;
+    if (lane_id() == 0 && (uint64_t)wv * CD_W < nkeys) {
+        ecw[wv] = e; mcw[wv] = m; dcw[wv] = d;
+        esz[wv] = 2 * e;
+        tsz[wv] = 2 * m + e + 2 * d;
+    }
 }
 
 // one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
@@ -522,16 +566,17 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
                                                     uint32_t *__restrict__ fin_m, uint32_t *__restrict__ ovf,
                                                     uint64_t *__restrict__ err)
 {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nkeys) return;
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    if (slot >= nkeys) return;
+    const uint32_t k = p.perm[slot];
     Ctx c;
     c.err = 0;
-    c.w.ecap = (uint32_t)ecap[k];
-    c.w.mcap = (uint32_t)mcap[k];
-    key_bufs(p, k, c.w);
-    const uint64_t dk = p.doff[k + 1] - p.doff[k];
-    Buf *A = &c.w.a, *B = &c.w.b;
-    A->n = 0; A->mtop = 0;
+    key_bufs(p, slot, c.w);   // the capacities of the wave (>= this key's own)
+    const uint64_t dk = p.dcw[slot / (uint32_t)CD_W];
+    // the current state and the next one by value (a pointer swap would put both in scratch memory)
+    Buf A = c.w.a, B = c.w.b;
+    bool in_a = true;
+    A.n = 0; A.mtop = 0;
     const uint32_t q0 = kstart[k], q1 = kstart[k + 1];
     for (uint32_t q = q0; q < q1 && !c.err; ++q) {
         const uint32_t v = src[q];
@@ -543,15 +588,15 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
                 y.self = cmp(y.ex, y.id) == 0;
                 if (y.self) y.ex = y.id;
                 y.st = s.st[x];
-                y.ms = A->mtop;
+                y.ms = A.mtop;
                 y.mn = s.miss_off[x + 1] - s.miss_off[x];
-                if (!c.room_m(*A, y.mn) || !c.room_e(A->n + 1)) break;
+                if (!c.room_m(A, y.mn) || !c.room_e(A.n + 1)) break;
                 for (uint32_t t = 0; t < y.mn; ++t) {
                     const uint32_t z = s.miss_off[x] + t;
-                    A->m[A->mtop + t] = Ts{ s.mm[z], s.ml[z], s.mn[z] };
+                    A.m[A.mtop + t] = Ts{ s.mm[z], s.ml[z], s.mn[z] };
                 }
-                A->mtop += y.mn;
-                A->e[A->n++] = y;
+                A.mtop += y.mn;
+                A.e[A.n++] = y;
             }
             continue;
         }
@@ -562,16 +607,17 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
         // the command's keyDeps.txnIds(key), staged in the owned area: computeInfoAndAdditions reads them (copying
         // the additions out) before updateOrInsertWithAdditions may write an insertMissing result there
         const uint32_t da = u.dep_off[j], db = u.dep_off[j + 1];
-        Ts *deps = c.w.owned;
+        SP<Ts> deps = c.w.owned;
         if (db - da > dk) { c.err |= E_CAP; break; }
         for (uint32_t t = da; t < db; ++t) deps[t - da] = Ts{ u.dm[t], u.dl[t], u.dn[t] };
-        if (c.apply(*A, *B, id, ex, st, u.fl[i], deps, db - da)) {
-            Buf *t = A; A = B; B = t;
+        if (c.apply(A, B, id, ex, st, u.fl[i], deps, db - da)) {
+            const Buf t = A; A = B; B = t;
+            in_a = !in_a;
         }
     }
-    final_b[k] = A == &c.w.a ? 0 : 1;
-    fin_n[k] = A->n;
-    fin_m[k] = A->mtop;
+    final_b[k] = in_a ? 0 : 1;
+    fin_n[k] = A.n;
+    fin_m[k] = A.mtop;
     if (c.err & E_MCAP) { ovf[k] = 1; c.err = E_MCAP; }   // anything else this key reports shows again on the replay
     if (c.err) atomicOr((unsigned long long *)err, (unsigned long long)c.err);
 }
@@ -606,13 +652,13 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
                                                    const uint8_t *__restrict__ final_b, Out o)
 {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nkeys || !keep[k]) return;
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    if (slot >= nkeys) return;
+    const uint32_t k = p.perm[slot];
+    if (!keep[k]) return;
     Work w;
-    w.ecap = (uint32_t)ecap[k];
-    w.mcap = (uint32_t)mcap[k];
-    key_bufs(p, k, w);
-    const Info *E = final_b[k] ? w.b.e : w.a.e;
+    key_bufs(p, slot, w);
+    const SP<Info> E = final_b[k] ? w.b.e : w.a.e;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
         const Info &x = E[i];
@@ -627,12 +673,12 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
                                                    const uint8_t *__restrict__ final_b, Out o)
 {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nkeys || !keep[k]) return;
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    if (slot >= nkeys) return;
+    const uint32_t k = p.perm[slot];
+    if (!keep[k]) return;
     Work w;
-    w.ecap = (uint32_t)ecap[k];
-    w.mcap = (uint32_t)mcap[k];
-    key_bufs(p, k, w);
+    key_bufs(p, slot, w);
     const Buf &F = final_b[k] ? w.b : w.a;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
@@ -921,21 +967,37 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     uint64_t *ecap = ctx->get<uint64_t>("cd_ecap", nkeys), *mcap = ctx->get<uint64_t>("cd_mcap", nkeys);
     uint64_t *dcap = ctx->get<uint64_t>("cd_dcap", nkeys), *mmax = ctx->get<uint64_t>("cd_mmax", nkeys);
     uint32_t *ovf = ctx->get<uint32_t>("cd_ovf", nkeys);
-    uint64_t *eoff = ctx->get<uint64_t>("cd_eoff", (size_t)nkeys + 1), *moff = ctx->get<uint64_t>("cd_moff", (size_t)nkeys + 1);
-    uint64_t *doff = ctx->get<uint64_t>("cd_doff", (size_t)nkeys + 1);
-    uint64_t Etot = 0, Mtot = 0, Dtot = 0;
+    // per wave of 64 keys (their buffers interleaved): the capacities' maxima and the per-lane region offsets
+    const uint32_t nwv = (nkeys + (uint32_t)CD_W - 1) / (uint32_t)CD_W;
+    uint64_t *ecw = ctx->get<uint64_t>("cd_ecw", nwv), *mcw = ctx->get<uint64_t>("cd_mcw", nwv), *dcw = ctx->get<uint64_t>("cd_dcw", nwv);
+    uint64_t *esz = ctx->get<uint64_t>("cd_esz", nwv), *tsz = ctx->get<uint64_t>("cd_tsz", nwv);
+    uint64_t *eoffw = ctx->get<uint64_t>("cd_eoffw", (size_t)nwv + 1), *toffw = ctx->get<uint64_t>("cd_toffw", (size_t)nwv + 1);
+    uint64_t Ew = 0, Tw = 0;   // per-lane totals (the pools hold CD_W times these)
+    const uint32_t *perm = nullptr;   // slot -> key, by entry capacity (set after the bounds)
+    auto wave_layout = [&]() {
+        launch(ctx, "cd_wcap", k_cd_wcap, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, perm, (const uint64_t *)ecap,
+               (const uint64_t *)mcap, (const uint64_t *)dcap, ecw, mcw, dcw, esz, tsz);
+        const uint64_t *si[2] = { esz, tsz };
+        uint64_t *so[2] = { eoffw, toffw }, *stot[2] = { eoffw + nwv, toffw + nwv };
+        const size_t sn[2] = { nwv, nwv };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 2, si, so, sn, true, stot);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, eoffw + nwv, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, toffw + nwv, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        Ew = ctx->pinned[0]; Tw = ctx->pinned[1];
+    };
     if (nkeys) {
         launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
                (const uint32_t *)kinc, (const uint32_t *)so.vals, nk, s, u, kstart, ecap, mcap, mmax, dcap, ovf);
         launch(ctx, "cd_kend", k_cd_kend, dim3(1), dim3(BLOCK), 0, nkeys, T, kstart);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, ecap, eoff, nkeys, true, eoff + nkeys);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, dcap, doff, nkeys, true, doff + nkeys);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, eoff + nkeys, 8, hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, moff + nkeys, 8, hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, doff + nkeys, 8, hipMemcpyDeviceToHost, st));
+        // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size
+        uint64_t *cmax = ctx->get<uint64_t>("cd_cmax", 1);
+        ACC_HIP(hipMemsetAsync(cmax, 0, 8, st));
+        scan<uint64_t, OpMax<uint64_t>>(ctx, ecap, ctx->get<uint64_t>("cd_cscan", nkeys), nkeys, false, cmax);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, cmax, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
-        Etot = ctx->pinned[0]; Mtot = ctx->pinned[1]; Dtot = ctx->pinned[2];
+        perm = radix_sort(ctx, "cd_rs_cap", ecap, nullptr, nkeys, std::max(1, bits_for(ctx->pinned[0]))).vals;
+        wave_layout();
     }
     uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
     uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
@@ -943,9 +1005,10 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     Pool p{};
     uint32_t regrow = 0;
     for (;; ++regrow) {
-        const uint64_t pool_bytes = 2 * Etot * sizeof(Info) + (2 * Mtot + Etot + 2 * Dtot) * sizeof(Ts);
+        const uint64_t pool_bytes = (uint64_t)CD_W * (Ew * sizeof(Info) + Tw * sizeof(Ts));
         if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
-        p = Pool{ ctx->get<Info>("cd_pool_e", 2 * Etot), ctx->get<Ts>("cd_pool_m", 2 * Mtot + Etot + 2 * Dtot), eoff, moff, doff };
+        p = Pool{ ctx->get<Info>("cd_pool_e", (size_t)CD_W * Ew), ctx->get<Ts>("cd_pool_m", (size_t)CD_W * Tw), ecw, mcw, dcw,
+                  eoffw, toffw, perm };
         if (!nkeys) break;
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
                (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m,
@@ -958,12 +1021,10 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
         launch(ctx, "cd_grow", k_cd_grow, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, ovf, mcap,
                (const uint64_t *)mmax, errs, regrow);
-        scan<uint64_t, OpAdd<uint64_t>>(ctx, mcap, moff, nkeys, true, moff + nkeys);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, moff + nkeys, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
         check(ctx->pinned[0]);
-        Mtot = ctx->pinned[1];
+        wave_layout();
     }
     ctx->stat("cfk.apply_regrow", regrow);
     // ---- 4. key-major output
