@@ -77,6 +77,13 @@ struct SP {   // a lane's strided view of an interleaved buffer
     __device__ bool operator==(const SP &o) const { return p == o.p; }
 };
 
+// the command's keyDeps.txnIds(key) read in place from the update arrays (SoA columns), no staging copy
+struct DepsIn {
+    const uint64_t *m, *l;
+    const int32_t *n;
+    __device__ Ts operator[](long i) const { return Ts{ m[i], l[i], n[i] }; }
+};
+
 struct Buf {
     SP<Info> e;
     SP<Ts> m;
@@ -228,7 +235,7 @@ struct Ctx {
 
     // computeInfoAndAdditions (:1057-1149): the new TxnInfo (missing[] to tmiss) and the deps this CFK lacks (adds)
     __device__ __forceinline__ Info compute_info(const Buf &A, long insert_pos, long update_pos, const Ts &id, uint32_t st, const Ts &ex_in,
-                                 SP<Ts> deps, uint32_t nd, uint32_t &nm, uint32_t &na)
+                                 DepsIn deps, uint32_t nd, uint32_t &nm, uint32_t &na)
     {
         Info x;
         x.id = id; x.st = st; x.self = 1; x.ex = id; x.ms = 0; x.mn = 0;
@@ -245,12 +252,13 @@ struct Ctx {
         uint32_t di = 0;
         while (ti < dpos && di < nd) {
             const Info &t = A.e[ti];
-            const int r = cmp(t.id, deps[di]);
+            const Ts dd = deps[di];
+            const int r = cmp(t.id, dd);
             if (r == 0) { ++ti; ++di; }
             else if (r < 0) {
                 if (ti != update_pos && t.st < COMMITTED && witnesses(id, t.id)) w.tmiss[nm++] = t.id;
                 ++ti;
-            } else w.adds[na++] = deps[di++];
+            } else { w.adds[na++] = dd; ++di; }
         }
         for (; ti < dpos; ++ti) {
             const Info &t = A.e[ti];
@@ -339,7 +347,7 @@ struct Ctx {
 
     // CommandsForKey.update(prev, next) (:657-722) on this key; returns true when the state moved to B
     // fl: bit 0 = acceptedOrCommitted changed, bit 1 = next.status() == AcceptedInvalidate
-    __device__ __forceinline__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, SP<Ts> deps,
+    __device__ __forceinline__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, DepsIn deps,
                           uint32_t nd)
     {
         B.n = 0; B.mtop = 0;
@@ -515,7 +523,7 @@ struct Pool {
 };
 
 // slot k's working space (key p.perm[k]), interleaved with its wave's slots: entries A | B (2 ecw), then its Ts
-// region: the new TxnInfo's missing[] (ecw), additions (dcw), insertMissing / staged deps (dcw), then the A and B missing
+// region: the new TxnInfo's missing[] (ecw), additions (dcw), insertMissing (dcw), then the A and B missing
 // areas (mcw)
 __device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
 {
@@ -604,12 +612,11 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
         const uint32_t st = u.st[i];
         if (st == 0xFF) continue;   // InternalStatus.from(saveStatus) == null: unchanged
         const Ts id{ u.um[i], u.ul[i], u.un[i] }, ex{ u.uxm[i], u.uxl[i], u.uxn[i] };
-        // the command's keyDeps.txnIds(key), staged in the owned area: computeInfoAndAdditions reads them (copying
-        // the additions out) before updateOrInsertWithAdditions may write an insertMissing result there
+        // the command's keyDeps.txnIds(key), read in place; computeInfoAndAdditions copies the additions out (their
+        // area and the insertMissing area hold at most dk entries each)
         const uint32_t da = u.dep_off[j], db = u.dep_off[j + 1];
-        SP<Ts> deps = c.w.owned;
         if (db - da > dk) { c.err |= E_CAP; break; }
-        for (uint32_t t = da; t < db; ++t) deps[t - da] = Ts{ u.dm[t], u.dl[t], u.dn[t] };
+        const DepsIn deps{ u.dm + da, u.dl + da, u.dn + da };
         if (c.apply(A, B, id, ex, st, u.fl[i], deps, db - da)) {
             const Buf t = A; A = B; B = t;
             in_a = !in_a;
