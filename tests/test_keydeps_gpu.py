@@ -112,6 +112,24 @@ def test_zipf_hot_keys(ctx):
     assert_same(g, o, b.n_txn, "zipf")
 
 
+@pytest.mark.parametrize("switch", ["ACC_V2_FASTQ", "ACC_KD_OPT"])
+def test_tuning_switches_parity(monkeypatch, switch):
+    """The KeyDeps tuning switches kept off by default stay bit-exact: the O(1) query columns
+    (ACC_V2_FASTQ) and the optimistic build without the E host sync (ACC_KD_OPT: from a context's second batch on; a
+    larger third batch exceeds the capacity the first two left and takes the exact rebuild)."""
+    import oracle
+    from accord_amd.deps import Context
+    monkeypatch.setenv(switch, "1")
+    c = Context(0)
+    try:
+        for n, seed in ((6000, 0x51), (6000, 0x52), (12000, 0x53)):
+            b = W.keydeps_batch(n, 8, 1500, seed, "zipf", 0.99, status_model="model", window=1200)
+            g = c.calculate_partial_deps(b)
+            assert_same(g, oracle.keydeps_batch(b), b.n_txn, f"{switch} n={n}")
+    finally:
+        c.close()
+
+
 def test_mixed_kinds_and_accept_style(ctx):
     """SyncPoint kinds, random executeAt bumps on uncommitted txns (Accept-style queries with p1)."""
     import oracle
