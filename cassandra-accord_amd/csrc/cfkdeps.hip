@@ -84,8 +84,38 @@ struct DepsIn {
     __device__ Ts operator[](long i) const { return Ts{ m[i], l[i], n[i] }; }
 };
 
+// A TxnInfo as stored: 48 B (status and the executeAt-is-TxnId flag in the top bits of the missing count) instead of the
+// 64-B working struct; read and written whole through a lane's strided view
+struct InfoP {
+    uint64_t im, il, xm, xl;
+    int32_t in, xn;
+    uint32_t ms, mnst;   // missing[] start; count | status << 28 | self << 31
+};
+static_assert(sizeof(InfoP) == 48, "48-B stored TxnInfo");
+constexpr uint32_t MN_MAX = 1u << 28;
+struct EP {
+    InfoP *p;
+    __device__ Info get(long i) const
+    {
+        const InfoP q = p[i * CD_W];
+        Info x;
+        x.id = Ts{ q.im, q.il, q.in };
+        x.ex = Ts{ q.xm, q.xl, q.xn };
+        x.ms = q.ms;
+        x.mn = q.mnst & (MN_MAX - 1);
+        x.st = (q.mnst >> 28) & 7u;
+        x.self = q.mnst >> 31;
+        return x;
+    }
+    __device__ void set(long i, const Info &x) const
+    {
+        p[i * CD_W] = InfoP{ x.id.m, x.id.l, x.ex.m, x.ex.l, x.id.n, x.ex.n, x.ms, x.mn | (x.st << 28) | (x.self << 31) };
+    }
+    __device__ EP operator+(long k) const { return EP{ p + k * CD_W }; }
+};
+
 struct Buf {
-    SP<Info> e;
+    EP e;
     SP<Ts> m;
     uint32_t n, mtop;
 };
@@ -114,7 +144,7 @@ __device__ long bsearch_info(const Buf &b, long from, long to, const Ts &k)
     long lo = from, hi = to - 1;
     while (lo <= hi) {
         const long mid = (long)(((unsigned long)lo + (unsigned long)hi) >> 1);
-        const int c = cmp(b.e[mid].id, k);
+        const int c = cmp(b.e.get(mid).id, k);
         if (c < 0) lo = mid + 1; else if (c > 0) hi = mid - 1; else return mid;
     }
     return -(lo + 1);
@@ -126,6 +156,12 @@ struct Ctx {
     __device__ __forceinline__ bool room_e(uint32_t n) { if (n > w.ecap) { err |= E_CAP; return false; } return true; }
     // missing areas: beyond the key's current guess (E_MCAP: grown and replayed by the host)
     __device__ __forceinline__ bool room_m(const Buf &b, uint32_t add) { if ((uint64_t)b.mtop + add > w.mcap) { err |= E_MCAP; return false; } return true; }
+    // append an entry (its missing count must fit the stored 28 bits)
+    __device__ __forceinline__ void put_e(Buf &dst, const Info &y)
+    {
+        if (y.mn >= MN_MAX) { err |= E_CAP; return; }
+        if (room_e(dst.n + 1)) dst.e.set(dst.n++, y);
+    }
 
     // append entry x of src with its missing[] copied (dropping `drop` when given) to dst
     __device__ __forceinline__ void put(Buf &dst, const Info &x, SP<Ts> src_m, const Ts *drop)
@@ -141,7 +177,7 @@ struct Ctx {
             }
         }
         dst.mtop += y.mn;
-        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+        put_e(dst, y);
     }
     // x with `ins` inserted into its missing[] (SortedArrays.insert)
     __device__ __forceinline__ void put_with_one(Buf &dst, const Info &x, SP<Ts> src_m, const Ts &ins)
@@ -159,7 +195,7 @@ struct Ctx {
         }
         if (!done) dst.m[dst.mtop + y.mn++] = ins;
         dst.mtop += y.mn;
-        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+        put_e(dst, y);
     }
     // mergeAndFilterMissing (:988-1025) of additions[0, count) into x's missing[], written to dst
     __device__ __forceinline__ void put_merged(Buf &dst, const Info &x, SP<Ts> src_m, SP<Ts> add, uint32_t count)
@@ -185,7 +221,7 @@ struct Ctx {
         if (n != x.mn + keep) err |= E_STATE;   // checkState(count == additionCount + current.length)
         y.mn = n;
         dst.mtop += n;
-        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+        put_e(dst, y);
     }
     // a new TxnInfo whose missing[] is in w.tmiss
     __device__ __forceinline__ void put_new(Buf &dst, const Info &x, uint32_t nm)
@@ -198,13 +234,13 @@ struct Ctx {
             y.mn = nm;
         }
         dst.mtop += y.mn;
-        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+        put_e(dst, y);
     }
     __device__ __forceinline__ void put_tk(Buf &dst, const Ts &id)   // TxnInfo.create(txnId, TRANSITIVELY_KNOWN, txnId)
     {
         Info y;
         y.id = id; y.ex = id; y.st = TK; y.self = 1; y.ms = dst.mtop; y.mn = 0;
-        if (room_e(dst.n + 1)) dst.e[dst.n++] = y;
+        put_e(dst, y);
     }
 
     // insert(pos, TxnInfo) (:880-897) with insertInfoAndOneMissing (:899-944); the new info's missing[] in tmiss
@@ -212,13 +248,13 @@ struct Ctx {
     {
         const bool plain = ins.st >= COMMITTED;
         for (uint32_t i = 0; i < pos; ++i) {
-            const Info &x = A.e[i];
+            const Info x = A.e.get(i);
             if (!plain && has_info(x.st) && cmp(dkb(x), ins.id) > 0 && witnesses(x.id, ins.id)) put_with_one(B, x, A.m, ins.id);
             else put(B, x, A.m, nullptr);
         }
         put_new(B, ins, nm);
         for (uint32_t i = pos; i < A.n; ++i) {
-            const Info &x = A.e[i];
+            const Info x = A.e.get(i);
             if (!plain && has_info(x.st) && witnesses(x.id, ins.id)) put_with_one(B, x, A.m, ins.id);
             else put(B, x, A.m, nullptr);
         }
@@ -226,10 +262,10 @@ struct Ctx {
     // update(pos, txnId, cur, new) (:865-875): the entry replaced, removeMissing (:946-972) when it becomes committed
     __device__ __forceinline__ void update_plain(const Buf &A, Buf &B, uint32_t pos, const Info &nw, uint32_t nm)
     {
-        const bool crossed = A.e[pos].st < COMMITTED && nw.st >= COMMITTED;
+        const bool crossed = A.e.get(pos).st < COMMITTED && nw.st >= COMMITTED;
         for (uint32_t i = 0; i < A.n; ++i) {
             if (i == pos) put_new(B, nw, nm);
-            else put(B, A.e[i], A.m, crossed ? &nw.id : nullptr);
+            else put(B, A.e.get(i), A.m, crossed ? &nw.id : nullptr);
         }
     }
 
@@ -251,7 +287,7 @@ struct Ctx {
         long ti = 0;
         uint32_t di = 0;
         while (ti < dpos && di < nd) {
-            const Info &t = A.e[ti];
+            const Info t = A.e.get(ti);
             const Ts dd = deps[di];
             const int r = cmp(t.id, dd);
             if (r == 0) { ++ti; ++di; }
@@ -261,7 +297,7 @@ struct Ctx {
             } else { w.adds[na++] = dd; ++di; }
         }
         for (; ti < dpos; ++ti) {
-            const Info &t = A.e[ti];
+            const Info t = A.e.get(ti);
             if (ti != update_pos && t.st < COMMITTED && witnesses(id, t.id)) w.tmiss[nm++] = t.id;
         }
         while (di < nd) w.adds[na++] = deps[di++];
@@ -288,9 +324,10 @@ struct Ctx {
                 ++count;
                 continue;
             }
-            const int r = j == na ? -1 : cmp(A.e[i].id, add[j]);
+            const Info xi = A.e.get(i);
+            const int r = j == na ? -1 : cmp(xi.id, add[j]);
             if (r < 0) {
-                const Info &x = A.e[i];
+                const Info &x = xi;
                 if ((long)i == src_update) put_new(B, winfo, nm);
                 else if (has_info(x.st)) {
                     if (insert_self_missing && msrc == add && (mcount != j || (!dkb_self(x) && cmp(dkb(x), winfo.id) > 0))) {
@@ -336,12 +373,13 @@ struct Ctx {
     __device__ __forceinline__ void remove_missing(Buf &B, const Ts &id)
     {
         for (uint32_t i = 0; i < B.n; ++i) {
-            Info &x = B.e[i];
+            Info x = B.e.get(i);
             if (!x.mn) continue;
             const long j = bsearch_ts(B.m + x.ms, 0, (long)x.mn, id);
             if (j < 0) continue;
             for (uint32_t q = (uint32_t)j; q + 1 < x.mn; ++q) B.m[x.ms + q] = B.m[x.ms + q + 1];
             --x.mn;
+            B.e.set(i, x);
         }
     }
 
@@ -366,7 +404,7 @@ struct Ctx {
             }
             return true;
         }
-        const Info cur = A.e[pos];
+        const Info cur = A.e.get(pos);
         if (st <= cur.st) {
             // Invariants.checkState(cur.status == newStatus || next.status() == AcceptedInvalidate) (:681-686)
             if (cur.st != st && !(fl & 2u)) { err |= E_STALE; return false; }
@@ -515,7 +553,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kend(uint32_t nkeys, uint64_t T, u
 }
 
 struct Pool {
-    Info *e;
+    InfoP *e;
     Ts *m;
     const uint64_t *ecw, *mcw, *dcw;   // per wave of 64 keys: the largest entry / missing / deps capacity of its keys
     const uint64_t *eoffw, *toffw;     // exclusive scans over waves of 2 ecw and of 2 mcw + ecw + 2 dcw (per-lane units)
@@ -531,7 +569,7 @@ __device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
     const uint64_t ec = p.ecw[wv], mc = p.mcw[wv], dc = p.dcw[wv];
     w.ecap = (uint32_t)ec;
     w.mcap = (uint32_t)mc;
-    w.a.e = SP<Info>{ p.e + p.eoffw[wv] * CD_W + l };
+    w.a.e = EP{ p.e + p.eoffw[wv] * CD_W + l };
     w.b.e = w.a.e + (long)ec;
     const SP<Ts> R{ p.m + p.toffw[wv] * CD_W + l };
     w.tmiss = R;
@@ -604,7 +642,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
                     A.m[A.mtop + t] = Ts{ s.mm[z], s.ml[z], s.mn[z] };
                 }
                 A.mtop += y.mn;
-                A.e[A.n++] = y;
+                c.put_e(A, y);
             }
             continue;
         }
@@ -665,10 +703,10 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_
     if (!keep[k]) return;
     Work w;
     key_bufs(p, slot, w);
-    const SP<Info> E = final_b[k] ? w.b.e : w.a.e;
+    const EP E = final_b[k] ? w.b.e : w.a.e;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
-        const Info &x = E[i];
+        const Info x = E.get(i);
         o.em[base + i] = x.id.m; o.el[base + i] = x.id.l; o.en[base + i] = x.id.n;
         o.xm[base + i] = x.ex.m; o.xl[base + i] = x.ex.l; o.xn[base + i] = x.ex.n;
         o.st[base + i] = (uint8_t)x.st;
@@ -689,7 +727,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_
     const Buf &F = final_b[k] ? w.b : w.a;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
-        const Info &x = F.e[i];
+        const Info x = F.e.get(i);
         uint32_t dst = o.miss_off[base + i];
         for (uint32_t q = 0; q < x.mn; ++q, ++dst) {
             const Ts &t = F.m[x.ms + q];
@@ -1012,9 +1050,9 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     Pool p{};
     uint32_t regrow = 0;
     for (;; ++regrow) {
-        const uint64_t pool_bytes = (uint64_t)CD_W * (Ew * sizeof(Info) + Tw * sizeof(Ts));
+        const uint64_t pool_bytes = (uint64_t)CD_W * (Ew * sizeof(InfoP) + Tw * sizeof(Ts));
         if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
-        p = Pool{ ctx->get<Info>("cd_pool_e", (size_t)CD_W * Ew), ctx->get<Ts>("cd_pool_m", (size_t)CD_W * Tw), ecw, mcw, dcw,
+        p = Pool{ ctx->get<InfoP>("cd_pool_e", (size_t)CD_W * Ew), ctx->get<Ts>("cd_pool_m", (size_t)CD_W * Tw), ecw, mcw, dcw,
                   eoffw, toffw, perm };
         if (!nkeys) break;
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
