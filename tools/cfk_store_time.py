@@ -45,3 +45,17 @@ with Context(0) as c:
         c._lib.acc_cfk_destroy(h)
     print({"updates": len(u["msb"]), "pairs": len(u["key"]), "deps": len(u["dmsb"]), "store_txns": int(v.n_txn),
            "store_pairs": int(v.n_pairs), **res})
+with Context(0, timing=True) as c:   # one more store update with every kernel timed: where its time goes
+    h = C.c_void_p()
+    c.check(c._lib.acc_cfk_create(c.handle, C.byref(h)))
+    c.check(c._lib.acc_cfk_apply_deps(c.handle, h, C.byref(ui)))
+    torch.cuda.synchronize()
+    c.timing_reset()
+    c._lib.acc_cfk_destroy(h)
+    c.check(c._lib.acc_cfk_create(c.handle, C.byref(h)))
+    c.check(c._lib.acc_cfk_apply_deps(c.handle, h, C.byref(ui)))
+    torch.cuda.synchronize()
+    t = c.timing()
+    top = sorted(t.items(), key=lambda kv: -kv[1][0])[:14]
+    print("store update kernels (ms):", {k: round(v[0], 3) for k, v in top}, "sum", round(sum(v[0] for v in t.values()), 3))
+    c._lib.acc_cfk_destroy(h)
