@@ -385,30 +385,94 @@ struct Ctx {
 
     // CommandsForKey.update(prev, next) (:657-722) on this key; returns true when the state moved to B
     // fl: bit 0 = acceptedOrCommitted changed, bit 1 = next.status() == AcceptedInvalidate
-    __device__ __forceinline__ bool apply(const Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, DepsIn deps,
-                          uint32_t nd)
+    // a key's state summary for the in-place fast paths: nlow = entries below COMMITTED (the candidates of a new
+    // TxnInfo's missing[]), maxdkb = an upper bound of depsKnownBefore over the entries with info (the entries
+    // insertInfoAndOneMissing may touch), mlive = the missing[] entries of all entries (what removeMissing would edit)
+    struct Sum {
+        Ts maxdkb;
+        bool any;
+        uint32_t nlow, mlive;
+    };
+    __device__ __forceinline__ void sum_add(Sum &sm, const Info &x)
+    {
+        sm.nlow += x.st < COMMITTED ? 1u : 0u;
+        sm.mlive += x.mn;
+        if (has_info(x.st) && (!sm.any || cmp(dkb(x), sm.maxdkb) > 0)) { sm.maxdkb = dkb(x); sm.any = true; }
+    }
+    __device__ __forceinline__ void sum_of(const Buf &A, Sum &sm)
+    {
+        sm.any = false; sm.nlow = 0; sm.mlive = 0;
+        for (uint32_t i = 0; i < A.n; ++i) sum_add(sm, A.e.get(i));
+    }
+    // every dep among the entries [0, to): computeInfoAndAdditions finds no addition
+    __device__ __forceinline__ bool deps_present(const Buf &A, long to, DepsIn deps, uint32_t nd)
+    {
+        for (uint32_t d = 0; d < nd; ++d)
+            if (bsearch_info(A, 0, to, deps[d]) < 0) return false;
+        return true;
+    }
+
+    // CommandsForKey.update(prev, next) (:657-722) on this key. Returns 0 when the state is unchanged, 1 when the new
+    // state is in B (the Java's new arrays), 2 when A was updated in place: the fast paths below take the cases where
+    // the Java's rebuild copies every other entry unchanged -- an insert at the end that adds nothing to any entry's
+    // missing[] and takes no missing[] itself, or an update of one entry with nothing to remove -- so A's other entries
+    // stay where they are (a replaced entry's missing[] is left behind in the missing area; the next full rebuild
+    // compacts it). fl: bit 0 = acceptedOrCommitted changed, bit 1 = next.status() == AcceptedInvalidate
+    __device__ __forceinline__ int apply(Buf &A, Buf &B, const Ts &id, const Ts &ex, uint32_t st, uint32_t fl, DepsIn deps,
+                                         uint32_t nd, Sum &sm)
     {
         B.n = 0; B.mtop = 0;
         long pos = bsearch_info(A, 0, (long)A.n, id);
         if (pos < 0) {
             pos = -1 - pos;
+            Info ni;
+            ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = A.mtop; ni.mn = 0;
+            if (has_info(st) && cmp(ex, id) != 0) { ni.ex = ex; ni.self = 0; }
+            if (pos == (long)A.n && (st >= COMMITTED || !sm.any || cmp(sm.maxdkb, id) <= 0) &&
+                (!has_info(st) || (sm.nlow == 0 && deps_present(A, (long)A.n, deps, nd))) && room_e(A.n + 1)) {
+                put_e(A, ni);   // insert at the end: no entry gains a missing TxnId, the new one has none
+                sum_add(sm, ni);
+                return 2;
+            }
             if (has_info(st)) {
                 uint32_t nm, na;
-                const Info ni = compute_info(A, pos, -1, id, st, ex, deps, nd, nm, na);
-                if (na == 0) insert_plain(A, B, (uint32_t)pos, ni, nm);
-                else with_additions(A, B, pos, -1, ni, nm, na);
+                const Info nc = compute_info(A, pos, -1, id, st, ex, deps, nd, nm, na);
+                if (na == 0) insert_plain(A, B, (uint32_t)pos, nc, nm);
+                else with_additions(A, B, pos, -1, nc, nm, na);
             } else {
-                Info ni;
-                ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = 0; ni.mn = 0;
+                ni.ms = 0;
                 insert_plain(A, B, (uint32_t)pos, ni, 0);
             }
-            return true;
+            return 1;
         }
         const Info cur = A.e.get(pos);
         if (st <= cur.st) {
             // Invariants.checkState(cur.status == newStatus || next.status() == AcceptedInvalidate) (:681-686)
-            if (cur.st != st && !(fl & 2u)) { err |= E_STALE; return false; }
-            if (!has_info(st) || !(fl & 1u)) return false;   // acceptedOrCommitted unchanged: this (:687-688)
+            if (cur.st != st && !(fl & 2u)) { err |= E_STALE; return 0; }
+            if (!has_info(st) || !(fl & 1u)) return 0;   // acceptedOrCommitted unchanged: this (:687-688)
+        }
+        {   // in place: the entry replaced, no missing[] for it, nothing to remove from the others
+            Info ni;
+            ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = A.mtop; ni.mn = 0;
+            if (has_info(st) && cmp(ex, id) != 0) { ni.ex = ex; ni.self = 0; }
+            const bool crossed = cur.st < COMMITTED && st >= COMMITTED;
+            bool ok = !crossed || sm.mlive == cur.mn;
+            if (ok && has_info(st)) {
+                long dpos = pos;
+                if (!(st == PRE || st == ACC || ni.self)) {
+                    dpos = bsearch_info(A, pos, (long)A.n, ni.ex);
+                    if (dpos >= 0) ok = false;   // the general path reports it (checkState)
+                    else dpos = -1 - dpos;
+                }
+                ok = ok && sm.nlow - (cur.st < COMMITTED ? 1u : 0u) == 0 && deps_present(A, dpos, deps, nd);
+            }
+            if (ok) {
+                A.e.set(pos, ni);
+                sm.nlow = sm.nlow - (cur.st < COMMITTED ? 1u : 0u) + (st < COMMITTED ? 1u : 0u);
+                sm.mlive -= cur.mn;
+                if (has_info(st) && (!sm.any || cmp(dkb(ni), sm.maxdkb) > 0)) { sm.maxdkb = dkb(ni); sm.any = true; }
+                return 2;
+            }
         }
         if (has_info(st)) {
             uint32_t nm, na;
@@ -423,7 +487,7 @@ struct Ctx {
             ni.id = id; ni.ex = id; ni.st = st; ni.self = 1; ni.ms = 0; ni.mn = 0;
             update_plain(A, B, (uint32_t)pos, ni, 0);
         }
-        return true;
+        return 1;
     }
 };
 
@@ -604,16 +668,59 @@ __global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_
     }
 }
 
+// Each sorted (key, update) element's update fields gathered once into a 64-B record at its sorted position (pairs
+// read in pair order, records scattered whole), so the replay reads one record per update instead of a chain of
+// dependent loads (element -> update -> its columns, deps range). Snapshot elements' slots stay unwritten.
+struct UpdRec {
+    uint64_t im, il, xm, xl;
+    int32_t in, xn;
+    uint32_t st_fl;   // status | flags << 8
+    uint32_t da, db;  // deps range
+    uint32_t pad[3];
+};
+static_assert(sizeof(UpdRec) == 64, "64-B update record");
+// the sorted position of every (update, key) pair
+__global__ __launch_bounds__(BLOCK) void k_cd_inv(uint64_t T, const uint32_t *__restrict__ src, uint32_t nk,
+                                                  uint32_t *__restrict__ qpos)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= T) return;
+    const uint32_t v = src[q];
+    if (v >= nk) qpos[v - nk] = (uint32_t)q;
+}
+// thread per pair, in pair order (the update columns read nearly contiguously), record written at its sorted position
+__global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *__restrict__ qpos, Upd u,
+                                                   UpdRec *__restrict__ rec)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= NP) return;
+    const uint32_t i = u.owner[j];
+    UpdRec r;
+    r.im = u.um[i]; r.il = u.ul[i]; r.in = u.un[i];
+    r.xm = u.uxm[i]; r.xl = u.uxl[i]; r.xn = u.uxn[i];
+    r.st_fl = (uint32_t)u.st[i] | ((uint32_t)u.fl[i] << 8);
+    r.da = u.dep_off[j]; r.db = u.dep_off[j + 1];
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    rec[qpos[j]] = r;
+}
+
 // one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
 __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32_t *__restrict__ kstart,
                                                     const uint32_t *__restrict__ src, const uint64_t *__restrict__ ecap,
                                                     const uint64_t *__restrict__ mcap, uint32_t nk, Snap s, Upd u, Pool p,
                                                     uint8_t *__restrict__ final_b, uint32_t *__restrict__ fin_n,
                                                     uint32_t *__restrict__ fin_m, uint32_t *__restrict__ ovf,
-                                                    uint64_t *__restrict__ err)
+                                                    uint64_t *__restrict__ err, unsigned long long *__restrict__ paths,
+                                                    const UpdRec *__restrict__ urec)
 {
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
-    if (slot >= nkeys) return;
+    uint32_t n_fast = 0, n_rebuild = 0;
+    auto count_paths = [&]() {   // per wave: in-place updates, full rebuilds (stats)
+        unsigned long long f = n_fast, r = n_rebuild;
+        for (int d = 32; d >= 1; d >>= 1) { f += __shfl_xor(f, d, 64); r += __shfl_xor(r, d, 64); }
+        if (lane_id() == 0 && (f || r)) { atomicAdd(&paths[0], f); atomicAdd(&paths[1], r); }
+    };
+    if (slot >= nkeys) { count_paths(); return; }
     const uint32_t k = p.perm[slot];
     Ctx c;
     c.err = 0;
@@ -623,6 +730,8 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
     Buf A = c.w.a, B = c.w.b;
     bool in_a = true;
     A.n = 0; A.mtop = 0;
+    Ctx::Sum sm{};
+    bool sum_ok = false;
     const uint32_t q0 = kstart[k], q1 = kstart[k + 1];
     for (uint32_t q = q0; q < q1 && !c.err; ++q) {
         const uint32_t v = src[q];
@@ -646,18 +755,23 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
             }
             continue;
         }
-        const uint32_t j = v - nk, i = u.owner[j];
-        const uint32_t st = u.st[i];
+        const UpdRec ur = urec[q];
+        const uint32_t st = ur.st_fl & 0xFFu, fl = ur.st_fl >> 8;
         if (st == 0xFF) continue;   // InternalStatus.from(saveStatus) == null: unchanged
-        const Ts id{ u.um[i], u.ul[i], u.un[i] }, ex{ u.uxm[i], u.uxl[i], u.uxn[i] };
+        const Ts id{ ur.im, ur.il, ur.in }, ex{ ur.xm, ur.xl, ur.xn };
         // the command's keyDeps.txnIds(key), read in place; computeInfoAndAdditions copies the additions out (their
         // area and the insertMissing area hold at most dk entries each)
-        const uint32_t da = u.dep_off[j], db = u.dep_off[j + 1];
+        const uint32_t da = ur.da, db = ur.db;
         if (db - da > dk) { c.err |= E_CAP; break; }
         const DepsIn deps{ u.dm + da, u.dl + da, u.dn + da };
-        if (c.apply(A, B, id, ex, st, u.fl[i], deps, db - da)) {
+        if (!sum_ok) { c.sum_of(A, sm); sum_ok = true; }
+        const int r = c.apply(A, B, id, ex, st, fl, deps, db - da, sm);
+        n_fast += r == 2;
+        n_rebuild += r == 1;
+        if (r == 1) {
             const Buf t = A; A = B; B = t;
             in_a = !in_a;
+            sum_ok = false;   // recomputed before the next update
         }
     }
     final_b[k] = in_a ? 0 : 1;
@@ -665,6 +779,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32
     fin_m[k] = A.mtop;
     if (c.err & E_MCAP) { ovf[k] = 1; c.err = E_MCAP; }   // anything else this key reports shows again on the replay
     if (c.err) atomicOr((unsigned long long *)err, (unsigned long long)c.err);
+    count_paths();
 }
 
 // output: keys with entries, their entry counts
@@ -1046,6 +1161,12 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     }
     uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
     uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
+    UpdRec *urec = ctx->get<UpdRec>("cd_urec", std::max<uint64_t>(T, 1));
+    if (NP) {
+        uint32_t *qpos = ctx->get<uint32_t>("cd_qpos", NP);
+        launch(ctx, "cd_inv", k_cd_inv, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)so.vals, nk, qpos);
+        launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec);
+    }
     // ---- 3. replay, again with grown missing areas while some key outgrows its guess
     Pool p{};
     uint32_t regrow = 0;
@@ -1055,11 +1176,16 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         p = Pool{ ctx->get<InfoP>("cd_pool_e", (size_t)CD_W * Ew), ctx->get<Ts>("cd_pool_m", (size_t)CD_W * Tw), ecw, mcw, dcw,
                   eoffw, toffw, perm };
         if (!nkeys) break;
+        unsigned long long *paths = ctx->get<unsigned long long>("cd_paths", 2);
+        ACC_HIP(hipMemsetAsync(paths, 0, 16, st));
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
                (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m,
-               ovf, errs);
+               ovf, errs, paths, (const UpdRec *)urec);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, paths, 16, hipMemcpyDeviceToHost, st));
         ctx->sync();
+        ctx->stat("cfk.apply_in_place", ctx->pinned[1]);
+        ctx->stat("cfk.apply_rebuilt", ctx->pinned[2]);
         const uint64_t e = ctx->pinned[0];
         check(e & ~E_MCAP);
         if (!(e & E_MCAP)) break;

@@ -58,4 +58,5 @@ with Context(0, timing=True) as c:   # one more store update with every kernel t
     t = c.timing()
     top = sorted(t.items(), key=lambda kv: -kv[1][0])[:14]
     print("store update kernels (ms):", {k: round(v[0], 3) for k, v in top}, "sum", round(sum(v[0] for v in t.values()), 3))
+    print("paths:", {k: v for k, v in c.stats().items() if k.startswith("cfk.apply")})
     c._lib.acc_cfk_destroy(h)
