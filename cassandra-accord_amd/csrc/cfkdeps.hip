@@ -404,11 +404,20 @@ struct Ctx {
         sm.any = false; sm.nlow = 0; sm.mlive = 0;
         for (uint32_t i = 0; i < A.n; ++i) sum_add(sm, A.e.get(i));
     }
-    // every dep among the entries [0, to): computeInfoAndAdditions finds no addition
+    // every dep among the entries [0, to): computeInfoAndAdditions finds no addition. Walked from the last dep down,
+    // each first tried just below where the one above it was found (a key's deps are usually its latest entries, one
+    // probe each), and searched for otherwise
     __device__ __forceinline__ bool deps_present(const Buf &A, long to, DepsIn deps, uint32_t nd)
     {
-        for (uint32_t d = 0; d < nd; ++d)
-            if (bsearch_info(A, 0, to, deps[d]) < 0) return false;
+        long g = to - 1;
+        for (long d = (long)nd - 1; d >= 0; --d) {
+            const Ts k = deps[d];
+            if (g < 0 || cmp(A.e.get(g).id, k) != 0) {
+                g = bsearch_info(A, 0, to, k);
+                if (g < 0) return false;
+            }
+            --g;
+        }
         return true;
     }
 
@@ -422,7 +431,8 @@ struct Ctx {
                                          uint32_t nd, Sum &sm)
     {
         B.n = 0; B.mtop = 0;
-        long pos = bsearch_info(A, 0, (long)A.n, id);
+        // a TxnId past the key's last one (the usual first update) needs no search
+        long pos = A.n == 0 || cmp(A.e.get(A.n - 1).id, id) < 0 ? -1 - (long)A.n : bsearch_info(A, 0, (long)A.n, id);
         if (pos < 0) {
             pos = -1 - pos;
             Info ni;
@@ -705,7 +715,12 @@ __global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *
 }
 
 // one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
-__global__ __launch_bounds__(BLOCK) void k_cd_apply(uint32_t nkeys, const uint32_t *__restrict__ kstart,
+#ifdef CD_WPE
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CD_WPE))) void k_cd_apply(
+#else
+__global__ __launch_bounds__(BLOCK) void k_cd_apply(
+#endif
+uint32_t nkeys, const uint32_t *__restrict__ kstart,
                                                     const uint32_t *__restrict__ src, const uint64_t *__restrict__ ecap,
                                                     const uint64_t *__restrict__ mcap, uint32_t nk, Snap s, Upd u, Pool p,
                                                     uint8_t *__restrict__ final_b, uint32_t *__restrict__ fin_n,
