@@ -557,12 +557,30 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
     if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
 }
 
+// the smallest and largest key code (rng[0], rng[1]): the key sort orders code - smallest on the bits the span needs
+__global__ __launch_bounds__(BLOCK) void k_cd_krange(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
+                                                     const uint64_t *__restrict__ ukey, uint64_t *__restrict__ rng)
+{
+    unsigned long long lo = ~0ull, hi = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nk + NP; i += (uint64_t)gridDim.x * BLOCK) {
+        const unsigned long long k = i < nk ? skey[i] : ukey[i - nk];
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (lane_id() == 0) { atomicMin((unsigned long long *)&rng[0], lo); atomicMax((unsigned long long *)&rng[1], hi); }
+}
 __global__ __launch_bounds__(BLOCK) void k_cd_keys(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
-                                                   const uint64_t *__restrict__ ukey, uint64_t *__restrict__ all)
+                                                   const uint64_t *__restrict__ ukey, uint64_t base, uint64_t *__restrict__ all)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i < nk) all[i] = skey[i];
-    else if (i < nk + NP) all[i] = ukey[i - nk];
+    if (i < nk) all[i] = skey[i] - base;
+    else if (i < nk + NP) all[i] = ukey[i - nk] - base;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_cd_kflag(uint64_t T, const uint64_t *__restrict__ sk, uint32_t *__restrict__ f)
@@ -806,12 +824,12 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out1(uint32_t nkeys, const uint32_
 
 __global__ __launch_bounds__(BLOCK) void k_cd_out2(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
                                                    const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ sk,
-                                                   const uint32_t *__restrict__ fin_n, uint64_t *__restrict__ okey,
+                                                   uint64_t kbase, const uint32_t *__restrict__ fin_n, uint64_t *__restrict__ okey,
                                                    uint32_t *__restrict__ ocnt)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys || !keep[k]) return;
-    okey[kpos[k]] = sk[kstart[k]];
+    okey[kpos[k]] = sk[kstart[k]] + kbase;
     ocnt[kpos[k]] = fin_n[k];
 }
 
@@ -881,73 +899,61 @@ __global__ __launch_bounds__(BLOCK) void k_cb_node(uint64_t NE, const int32_t *_
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i < NE) k[i] = (uint32_t)en[i] ^ 0x80000000u;
 }
-// owner key of every entry (upper bound in ent_off)
-__global__ __launch_bounds__(BLOCK) void k_cb_owner(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ ent_off,
-                                                    uint32_t *__restrict__ owner)
-{
-    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= NE) return;
-    uint32_t lo = 0, hi = nk;   // first k with ent_off[k+1] > e
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (ent_off[mid + 1] > e) hi = mid; else lo = mid + 1;
-    }
-    owner[e] = lo;
-}
-// first-of-TxnId flags; later entries of a TxnId must carry its executeAt and InternalStatus
-__global__ __launch_bounds__(BLOCK) void k_cb_flag(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
-                                                   const uint32_t *__restrict__ owner, uint32_t *__restrict__ flag,
-                                                   uint64_t *__restrict__ err)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= NE) return;
-    const uint32_t e = perm[i];
-    uint32_t f = 1;
-    if (i > 0) {
-        const uint32_t p = perm[i - 1];
-        if (cmp(Ts{ s.em[e], s.el[e], s.en[e] }, Ts{ s.em[p], s.el[p], s.en[p] }) == 0) {
-            f = 0;
-            uint64_t bad = 0;
-            if (s.st[e] != s.st[p] || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ s.xm[p], s.xl[p], s.xn[p] }) != 0) bad |= E_STATE;
-            if (owner[e] <= owner[p]) bad |= E_ARG_SORT;
-            if (bad) atomicOr((unsigned long long *)err, (unsigned long long)bad);
-        }
-    }
-    flag[i] = f;
-}
 struct BatchOut {
     uint64_t *tm, *tl, *xm, *xl, *kc;
     int32_t *tn, *xn;
     uint8_t *st;
     uint32_t *ko, *mcnt;
 };
-__global__ __launch_bounds__(BLOCK) void k_cb_txn(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
-                                                  const uint32_t *__restrict__ owner, const uint32_t *__restrict__ flag,
-                                                  const uint32_t *__restrict__ tinc, BatchOut b)
+// the sorted position of every entry
+__global__ __launch_bounds__(BLOCK) void k_cb_inv(uint64_t NE, const uint32_t *__restrict__ perm, uint32_t *__restrict__ qpos)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= NE) return;
-    const uint32_t e = perm[i];
-    b.kc[i] = s.key[owner[e]];
-    b.mcnt[i] = s.miss_off[e + 1] - s.miss_off[e];
-    if (flag[i]) {
-        const uint32_t t = tinc[i] - 1;
-        b.tm[t] = s.em[e]; b.tl[t] = s.el[e]; b.tn[t] = s.en[e];
-        b.xm[t] = s.xm[e]; b.xl[t] = s.xl[e]; b.xn[t] = s.xn[e];
-        b.st[t] = s.st[e];
-        b.ko[t] = (uint32_t)i;
+    if (i < NE) qpos[perm[i]] = (uint32_t)i;
+}
+// per TxnId (its first entry in sorted order, which is its first key's): the batch's txn columns and its key run start
+__global__ __launch_bounds__(BLOCK) void k_cb_first(uint64_t NE, const uint64_t *__restrict__ ntxn, const uint32_t *__restrict__ first,
+                                                    const uint32_t *__restrict__ qpos, Snap s, BatchOut b)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t n = *ntxn;
+    if (t >= n) return;
+    const uint32_t e = first[t];
+    b.tm[t] = s.em[e]; b.tl[t] = s.el[e]; b.tn[t] = s.en[e];
+    b.xm[t] = s.xm[e]; b.xl[t] = s.xl[e]; b.xn[t] = s.xn[e];
+    b.st[t] = s.st[e];
+    b.ko[t] = qpos[e];
+    if (t + 1 == n) b.ko[n] = (uint32_t)NE;
+}
+// per entry, in entry order (its columns read contiguously): its key code and missing count at its sorted position,
+// and the check that it carries its TxnId's executeAt and InternalStatus (a TxnId twice on one key is already refused
+// by the per-key sort check)
+__global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ rank,
+                                                  const uint32_t *__restrict__ qpos, Snap s, BatchOut b,
+                                                  uint64_t *__restrict__ err)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= NE) return;
+    uint32_t lo = 0, hi = nk;   // owner key: first k with ent_off[k+1] > e
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s.ent_off[mid + 1] > e) hi = mid; else lo = mid + 1;
     }
-    if (i + 1 == NE) b.ko[tinc[i]] = (uint32_t)NE;
+    const uint32_t t = rank[e], i = qpos[e];
+    b.kc[i] = s.key[lo];
+    b.mcnt[i] = s.miss_off[e + 1] - s.miss_off[e];
+    if (s.st[e] != b.st[t] || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ b.xm[t], b.xl[t], b.xn[t] }) != 0)
+        atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
 }
 // each pair's missing[] TxnIds as batch indices (binary search over the batch's TxnIds)
 __global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
-                                                   const uint32_t *__restrict__ tinc, BatchOut b,
+                                                   const uint64_t *__restrict__ ntxn, BatchOut b,
                                                    const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
                                                    uint64_t *__restrict__ err)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= NE) return;
-    const uint32_t e = perm[i], n = tinc[NE - 1];
+    const uint32_t e = perm[i], n = (uint32_t)*ntxn;
     const uint32_t m0 = s.miss_off[e], m1 = s.miss_off[e + 1];
     uint32_t w = mo[i];
     for (uint32_t j = m0; j < m1; ++j) {
@@ -1018,30 +1024,29 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         if (ctx->pinned[0] & E_ARG_SORT) fail(ACC_E_ARG, "keys / TxnIds must be sorted unique");
         const dim3 g(grid_for(NE, BLOCK));
         uint64_t *k = ctx->get<uint64_t>("cb_key", NE);
-        uint32_t *owner = ctx->get<uint32_t>("cb_owner", NE), *flag = ctx->get<uint32_t>("cb_flag", NE);
-        uint32_t *tinc = ctx->get<uint32_t>("cb_tinc", NE);
+        uint32_t *qpos = ctx->get<uint32_t>("cb_qpos", NE);
         // entries in Timestamp order (stable: a TxnId's entries stay in key order) through the dense-rank dictionary's
         // sort of the compacted (msb, lsb & IDENTITY_LSB, node) bits: a few radix passes over the bits that vary
         launch(ctx, "cb_node", k_cb_node, g, dim3(BLOCK), 0, NE, s.en, k);
         const uint64_t *words[3] = { s.em, s.el, k };
         const uint64_t wand[3] = { ~0ull, 0xFFFFFFFFFFFF001EULL, ~0ull };
-        DenseRank dr = dense_rank(ctx, "cb_dr", NE, 3, words, wand, nullptr, false);
+        DenseRank dr = dense_rank(ctx, "cb_dr", NE, 3, words, wand, nullptr, true);
         const uint32_t *perm = dr.perm;
         if (!perm) {   // every entry carries one TxnId: identity order
             uint32_t *id = ctx->get<uint32_t>("cb_iota", NE);
             launch(ctx, "cb_iota", k_iota, g, dim3(BLOCK), 0, id, (size_t)NE);
             perm = id;
         }
-        launch(ctx, "cb_owner", k_cb_owner, g, dim3(BLOCK), 0, NE, nk, s.ent_off, owner);
-        launch(ctx, "cb_flag", k_cb_flag, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)owner, flag, errs);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, flag, tinc, NE, false);
-        launch(ctx, "cb_txn", k_cb_txn, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)owner, (const uint32_t *)flag,
-               (const uint32_t *)tinc, b);
+        // the batch's txn columns from each TxnId's first entry, then every entry (entry order) checked against them
+        launch(ctx, "cb_inv", k_cb_inv, g, dim3(BLOCK), 0, NE, perm, qpos);
+        launch(ctx, "cb_first", k_cb_first, g, dim3(BLOCK), 0, NE, (const uint64_t *)dr.count_dev, (const uint32_t *)dr.first,
+               (const uint32_t *)qpos, s, b);
+        launch(ctx, "cb_ent", k_cb_ent, g, dim3(BLOCK), 0, NE, nk, (const uint32_t *)dr.rank, (const uint32_t *)qpos, s, b, errs);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, b.mcnt, mo, NE, true, mo + NE);
         if (NM)
-            launch(ctx, "cb_miss", k_cb_miss, g, dim3(BLOCK), 0, NE, perm, s, (const uint32_t *)tinc, b, (const uint32_t *)mo, mt, errs);
+            launch(ctx, "cb_miss", k_cb_miss, g, dim3(BLOCK), 0, NE, perm, s, (const uint64_t *)dr.count_dev, b, (const uint32_t *)mo, mt, errs);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
-        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, tinc + NE - 1, 4, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, dr.count_dev, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
         const uint64_t e = ctx->pinned[0];
         if (e & E_STATE)
@@ -1110,8 +1115,16 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
     const uint64_t gmax = std::max<uint64_t>({ (uint64_t)nk, (uint64_t)nu, NP, 1 });
     launch(ctx, "cd_check", k_cd_check, dim3(grid_for(gmax, BLOCK)), dim3(BLOCK), 0, s, u, owner, errs);
+    uint64_t *krng = ctx->get<uint64_t>("cd_krng", 2);
+    ACC_HIP(hipMemsetAsync(krng, 0xFF, 8, st));
+    ACC_HIP(hipMemsetAsync(krng + 1, 0, 8, st));
+    if (nk + NP)
+        launch(ctx, "cd_krange", k_cd_krange, dim3((unsigned)std::min<uint64_t>(grid_for(nk + NP, BLOCK), 1024)), dim3(BLOCK), 0,
+               nk, NP, s.key, u.key, krng);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, krng, 16, hipMemcpyDeviceToHost, st));
     ctx->sync();
+    const uint64_t kbase = ctx->pinned[1], kspan = ctx->pinned[2] - ctx->pinned[1];
     auto check = [&](uint64_t e) {
         if (e & E_ARG_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal");
         if (e & E_ARG_OFF) fail(ACC_E_ARG, "offsets must be non-decreasing from 0 to their totals");
@@ -1129,8 +1142,8 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     Sorted so{ nullptr, nullptr };
     uint32_t *kflag = ctx->get<uint32_t>("cd_kflag", T), *kinc = ctx->get<uint32_t>("cd_kinc", T);
     if (T) {
-        launch(ctx, "cd_keys", k_cd_keys, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, nk, NP, s.key, u.key, all);
-        so = radix_sort(ctx, "cd_rs", all, nullptr, T, 64);
+        launch(ctx, "cd_keys", k_cd_keys, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, nk, NP, s.key, u.key, kbase, all);
+        so = radix_sort(ctx, "cd_rs", all, nullptr, T, bits_for(kspan));
         launch(ctx, "cd_kflag", k_cd_kflag, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint64_t *)so.keys, kflag);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, kflag, kinc, T, false);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, kinc + T - 1, 4, hipMemcpyDeviceToHost, st));
@@ -1230,7 +1243,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     uint64_t NEo = 0, NMo = 0;
     if (nko) {
         launch(ctx, "cd_out2", k_cd_out2, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-               (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, (const uint32_t *)fin_n, okey, ocnt);
+               (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, kbase, (const uint32_t *)fin_n, okey, ocnt);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, ocnt, o.ent_off, nko, true, o.ent_off + nko);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, o.ent_off + nko, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
