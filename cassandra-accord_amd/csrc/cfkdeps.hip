@@ -589,26 +589,32 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kflag(uint64_t T, const uint64_t *
     if (i < T) f[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
 }
 
-// per distinct key: its run [kstart, kend) of the sorted elements and its working-space bounds
-__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint64_t T, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fi,
-                                                     const uint32_t *__restrict__ src, uint32_t nk, Snap s, Upd u,
-                                                     uint32_t *__restrict__ kstart, uint64_t *__restrict__ ecap,
+// per distinct key: the start of its run [kstart[k], kstart[k + 1]) of the sorted elements
+__global__ __launch_bounds__(BLOCK) void k_cd_kstart(uint64_t T, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fi,
+                                                     uint32_t nkeys, uint32_t *__restrict__ kstart)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < T && f[i]) kstart[fi[i] - 1] = (uint32_t)i;
+    if (i == 0) kstart[nkeys] = (uint32_t)T;
+}
+// per distinct key (a lane per key, so a wave's lanes walk adjacent runs): its working-space bounds. snd: each update
+// element's deps count (k_cd_urec)
+__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart,
+                                                     const uint32_t *__restrict__ src, const uint32_t *__restrict__ snd,
+                                                     uint32_t nk, Snap s, uint64_t *__restrict__ ecap,
                                                      uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
                                                      uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= T || !f[i]) return;
-    const uint32_t k = fi[i] - 1;
-    kstart[k] = (uint32_t)i;
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys) return;
     uint64_t e = 0, m = 0, d = 0, grow = 0;
-    for (uint64_t q = i; q < T && (q == i || !f[q]); ++q) {
+    for (uint32_t q = kstart[k], q1 = kstart[k + 1]; q < q1; ++q) {
         const uint32_t v = src[q];
         if (v < nk) {
             e += s.ent_off[v + 1] - s.ent_off[v];
             m += s.miss_off[s.ent_off[v + 1]] - s.miss_off[s.ent_off[v]];
         } else {
-            const uint32_t j = v - nk;
-            const uint64_t nd = u.dep_off[j + 1] - u.dep_off[j];
+            const uint64_t nd = snd[q];
             e += 1 + nd;
             d = d > nd ? d : nd;
             grow += nd + 2;
@@ -639,17 +645,13 @@ __global__ __launch_bounds__(BLOCK) void k_cd_grow(uint32_t nkeys, uint32_t *__r
     mcap[k] = g < mmax[k] ? g : mmax[k];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_cd_kend(uint32_t nkeys, uint64_t T, uint32_t *__restrict__ kstart)
-{
-    if (blockIdx.x == 0 && threadIdx.x == 0) kstart[nkeys] = (uint32_t)T;
-}
-
 struct Pool {
     InfoP *e;
     Ts *m;
     const uint64_t *ecw, *mcw, *dcw;   // per wave of 64 keys: the largest entry / missing / deps capacity of its keys
     const uint64_t *eoffw, *toffw;     // exclusive scans over waves of 2 ecw and of 2 mcw + ecw + 2 dcw (per-lane units)
     const uint32_t *perm;              // slot -> key: keys ordered by entry capacity, so a wave's keys are alike in size
+    uint32_t *kslot;                   // key -> slot
 };
 
 // slot k's working space (key p.perm[k]), interleaved with its wave's slots: entries A | B (2 ecw), then its Ts
@@ -672,7 +674,7 @@ __device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
 }
 
 // per wave of 64 keys: the largest capacities of its keys and the wave's per-lane region sizes
-__global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_t *__restrict__ perm,
+__global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_t *__restrict__ perm, uint32_t *__restrict__ kslot,
                                                    const uint64_t *__restrict__ ecap,
                                                    const uint64_t *__restrict__ mcap, const uint64_t *__restrict__ dcap,
                                                    uint64_t *__restrict__ ecw, uint64_t *__restrict__ mcw,
@@ -681,6 +683,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // slot
     const uint32_t key = k < nkeys ? perm[k] : 0u;
+    if (k < nkeys) kslot[key] = k;
     uint64_t e = k < nkeys ? ecap[key] : 0, m = k < nkeys ? mcap[key] : 0, d = k < nkeys ? dcap[key] : 0;
 #pragma unroll
     for (int x = 32; x >= 1; x >>= 1) {
@@ -718,7 +721,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_inv(uint64_t T, const uint32_t *__
 }
 // thread per pair, in pair order (the update columns read nearly contiguously), record written at its sorted position
 __global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *__restrict__ qpos, Upd u,
-                                                   UpdRec *__restrict__ rec)
+                                                   UpdRec *__restrict__ rec, uint32_t *__restrict__ snd)
 {
     const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (j >= NP) return;
@@ -729,7 +732,9 @@ __global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *
     r.st_fl = (uint32_t)u.st[i] | ((uint32_t)u.fl[i] << 8);
     r.da = u.dep_off[j]; r.db = u.dep_off[j + 1];
     r.pad[0] = r.pad[1] = r.pad[2] = 0;
-    rec[qpos[j]] = r;
+    const uint32_t q = qpos[j];
+    rec[q] = r;
+    snd[q] = r.db - r.da;
 }
 
 // one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
@@ -845,12 +850,10 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
                                                    const uint8_t *__restrict__ final_b, Out o)
 {
-    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
-    if (slot >= nkeys) return;
-    const uint32_t k = p.perm[slot];
-    if (!keep[k]) return;
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // key order: a wave's lanes write adjacent output runs
+    if (k >= nkeys || !keep[k]) return;
     Work w;
-    key_bufs(p, slot, w);
+    key_bufs(p, p.kslot[k], w);
     const EP E = final_b[k] ? w.b.e : w.a.e;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
@@ -866,12 +869,10 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
                                                    const uint8_t *__restrict__ final_b, Out o)
 {
-    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
-    if (slot >= nkeys) return;
-    const uint32_t k = p.perm[slot];
-    if (!keep[k]) return;
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // key order: a wave's lanes write adjacent output runs
+    if (k >= nkeys || !keep[k]) return;
     Work w;
-    key_bufs(p, slot, w);
+    key_bufs(p, p.kslot[k], w);
     const Buf &F = final_b[k] ? w.b : w.a;
     const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
     for (uint32_t i = 0; i < n; ++i) {
@@ -925,22 +926,24 @@ __global__ __launch_bounds__(BLOCK) void k_cb_first(uint64_t NE, const uint64_t 
     b.ko[t] = qpos[e];
     if (t + 1 == n) b.ko[n] = (uint32_t)NE;
 }
+// owner key of every entry (a lane per key)
+__global__ __launch_bounds__(BLOCK) void k_cb_owner(uint32_t nk, const uint32_t *__restrict__ ent_off, uint32_t *__restrict__ owner)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nk) return;
+    for (uint32_t e = ent_off[k], e1 = ent_off[k + 1]; e < e1; ++e) owner[e] = k;
+}
 // per entry, in entry order (its columns read contiguously): its key code and missing count at its sorted position,
 // and the check that it carries its TxnId's executeAt and InternalStatus (a TxnId twice on one key is already refused
 // by the per-key sort check)
-__global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ rank,
+__global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, const uint32_t *__restrict__ owner, const uint32_t *__restrict__ rank,
                                                   const uint32_t *__restrict__ qpos, Snap s, BatchOut b,
                                                   uint64_t *__restrict__ err)
 {
     const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (e >= NE) return;
-    uint32_t lo = 0, hi = nk;   // owner key: first k with ent_off[k+1] > e
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s.ent_off[mid + 1] > e) hi = mid; else lo = mid + 1;
-    }
     const uint32_t t = rank[e], i = qpos[e];
-    b.kc[i] = s.key[lo];
+    b.kc[i] = s.key[owner[e]];
     b.mcnt[i] = s.miss_off[e + 1] - s.miss_off[e];
     if (s.st[e] != b.st[t] || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ b.xm[t], b.xl[t], b.xn[t] }) != 0)
         atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
@@ -1041,7 +1044,9 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         launch(ctx, "cb_inv", k_cb_inv, g, dim3(BLOCK), 0, NE, perm, qpos);
         launch(ctx, "cb_first", k_cb_first, g, dim3(BLOCK), 0, NE, (const uint64_t *)dr.count_dev, (const uint32_t *)dr.first,
                (const uint32_t *)qpos, s, b);
-        launch(ctx, "cb_ent", k_cb_ent, g, dim3(BLOCK), 0, NE, nk, (const uint32_t *)dr.rank, (const uint32_t *)qpos, s, b, errs);
+        uint32_t *owner = ctx->get<uint32_t>("cb_owner", NE);
+        launch(ctx, "cb_owner", k_cb_owner, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, nk, s.ent_off, owner);
+        launch(ctx, "cb_ent", k_cb_ent, g, dim3(BLOCK), 0, NE, (const uint32_t *)owner, (const uint32_t *)dr.rank, (const uint32_t *)qpos, s, b, errs);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, b.mcnt, mo, NE, true, mo + NE);
         if (NM)
             launch(ctx, "cb_miss", k_cb_miss, g, dim3(BLOCK), 0, NE, perm, s, (const uint64_t *)dr.count_dev, b, (const uint32_t *)mo, mt, errs);
@@ -1162,8 +1167,9 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     uint64_t *eoffw = ctx->get<uint64_t>("cd_eoffw", (size_t)nwv + 1), *toffw = ctx->get<uint64_t>("cd_toffw", (size_t)nwv + 1);
     uint64_t Ew = 0, Tw = 0;   // per-lane totals (the pools hold CD_W times these)
     const uint32_t *perm = nullptr;   // slot -> key, by entry capacity (set after the bounds)
+    uint32_t *kslot = ctx->get<uint32_t>("cd_kslot", nkeys);
     auto wave_layout = [&]() {
-        launch(ctx, "cd_wcap", k_cd_wcap, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, perm, (const uint64_t *)ecap,
+        launch(ctx, "cd_wcap", k_cd_wcap, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, perm, kslot, (const uint64_t *)ecap,
                (const uint64_t *)mcap, (const uint64_t *)dcap, ecw, mcw, dcw, esz, tsz);
         const uint64_t *si[2] = { esz, tsz };
         uint64_t *so[2] = { eoffw, toffw }, *stot[2] = { eoffw + nwv, toffw + nwv };
@@ -1174,10 +1180,19 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ctx->sync();
         Ew = ctx->pinned[0]; Tw = ctx->pinned[1];
     };
+    // each (update, key) pair's update record at its sorted position, and its deps count
+    UpdRec *urec = ctx->get<UpdRec>("cd_urec", std::max<uint64_t>(T, 1));
+    uint32_t *snd = ctx->get<uint32_t>("cd_snd", std::max<uint64_t>(T, 1));
+    if (NP) {
+        uint32_t *qpos = ctx->get<uint32_t>("cd_qpos", NP);
+        launch(ctx, "cd_inv", k_cd_inv, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)so.vals, nk, qpos);
+        launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec, snd);
+    }
     if (nkeys) {
-        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
-               (const uint32_t *)kinc, (const uint32_t *)so.vals, nk, s, u, kstart, ecap, mcap, mmax, dcap, ovf);
-        launch(ctx, "cd_kend", k_cd_kend, dim3(1), dim3(BLOCK), 0, nkeys, T, kstart);
+        launch(ctx, "cd_kstart", k_cd_kstart, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
+               (const uint32_t *)kinc, nkeys, kstart);
+        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
+               (const uint32_t *)so.vals, (const uint32_t *)snd, nk, s, ecap, mcap, mmax, dcap, ovf);
         // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size
         uint64_t *cmax = ctx->get<uint64_t>("cd_cmax", 1);
         ACC_HIP(hipMemsetAsync(cmax, 0, 8, st));
@@ -1189,12 +1204,6 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     }
     uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
     uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
-    UpdRec *urec = ctx->get<UpdRec>("cd_urec", std::max<uint64_t>(T, 1));
-    if (NP) {
-        uint32_t *qpos = ctx->get<uint32_t>("cd_qpos", NP);
-        launch(ctx, "cd_inv", k_cd_inv, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)so.vals, nk, qpos);
-        launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec);
-    }
     // ---- 3. replay, again with grown missing areas while some key outgrows its guess
     Pool p{};
     uint32_t regrow = 0;
@@ -1202,7 +1211,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         const uint64_t pool_bytes = (uint64_t)CD_W * (Ew * sizeof(InfoP) + Tw * sizeof(Ts));
         if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
         p = Pool{ ctx->get<InfoP>("cd_pool_e", (size_t)CD_W * Ew), ctx->get<Ts>("cd_pool_m", (size_t)CD_W * Tw), ecw, mcw, dcw,
-                  eoffw, toffw, perm };
+                  eoffw, toffw, perm, kslot };
         if (!nkeys) break;
         unsigned long long *paths = ctx->get<unsigned long long>("cd_paths", 2);
         ACC_HIP(hipMemsetAsync(paths, 0, 16, st));
