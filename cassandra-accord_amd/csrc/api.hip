@@ -23,7 +23,7 @@ void deps_from_json(acc_ctx *ctx, const acc_json_in *in, acc_json_deps_view *vie
 void deps_to_json(acc_ctx *ctx, const acc_json_out_in *in, acc_json_out *out);
 void cfk_update(acc_ctx *ctx, acc_cfk *cfk, const acc_batch_in *in);
 void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
-void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view);
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view, bool trusted = false);
 void max_conflicts(acc_ctx *ctx, const acc_conflicts_in *u, const acc_preaccept_in *q, acc_preaccept_out *out);
 acc_maxconflicts *mc_new(int device, uint32_t end_inclusive);
 void mc_free(acc_maxconflicts *m);

@@ -386,7 +386,7 @@ void cfk_free(acc_cfk *cfk)
 }
 
 void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, acc_cfk_snap_view *view);
-void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view);
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view, bool trusted = false);
 void cfk_view(acc_cfk *cfk, acc_batch_in *out);
 
 namespace {
@@ -438,7 +438,7 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     const acc_cfk_snap next{ ACC_MEM_DEVICE, v.n_keys, v.n_entries, v.n_missing, v.key, v.ent_off, v.txn_id, v.execute_at,
                              v.status, v.miss_off, v.missing };
     acc_cfk_batch_view bv{};
-    cfk_snap_to_batch(ctx, &next, &bv);
+    cfk_snap_to_batch(ctx, &next, &bv, true);
     // ---- both results in the store
     const uint32_t nk = v.n_keys;
     const uint64_t ne = v.n_entries, nm = v.n_missing;

@@ -520,11 +520,33 @@ struct Upd {
     uint64_t NP, ND;
 };
 
-// validation + the pair -> update map
-__global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__restrict__ owner, uint64_t *__restrict__ err)
+// validation + the pair -> update map; rng (when given): the smallest and largest key code, so the key sort orders
+// code - smallest on the bits the span needs
+__global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__restrict__ owner, uint64_t *__restrict__ err,
+                                                    uint64_t *__restrict__ rng)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t e = 0;
+    if (rng) {
+        unsigned long long lo = ~0ull, hi = 0;
+        if (i < s.n_keys) { lo = s.key[i]; hi = lo; }
+        if (i < u.NP) {
+            const unsigned long long k = u.key[i];
+            lo = k < lo ? k : lo;
+            hi = k > hi ? k : hi;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const unsigned long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+        }
+        if (lane_id() == 0 && lo <= hi) {   // an atomic only where this wave moves a bound (one address for every wave)
+            unsigned long long *r = (unsigned long long *)rng;
+            if (lo < __hip_atomic_load(&r[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&r[0], lo);
+            if (hi > __hip_atomic_load(&r[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&r[1], hi);
+        }
+    }
     if (i < u.n_upd) {
         const uint32_t a = u.key_off[i], b = u.key_off[i + 1];
         if (b < a || b > u.NP || (i == 0 && a != 0) || (i + 1 == u.n_upd && b != u.NP)) e |= E_ARG_OFF;
@@ -558,24 +580,6 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
     if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
 }
 
-// the smallest and largest key code (rng[0], rng[1]): the key sort orders code - smallest on the bits the span needs
-__global__ __launch_bounds__(BLOCK) void k_cd_krange(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
-                                                     const uint64_t *__restrict__ ukey, uint64_t *__restrict__ rng)
-{
-    unsigned long long lo = ~0ull, hi = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nk + NP; i += (uint64_t)gridDim.x * BLOCK) {
-        const unsigned long long k = i < nk ? skey[i] : ukey[i - nk];
-        lo = k < lo ? k : lo;
-        hi = k > hi ? k : hi;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const unsigned long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
-        lo = a < lo ? a : lo;
-        hi = b > hi ? b : hi;
-    }
-    if (lane_id() == 0) { atomicMin((unsigned long long *)&rng[0], lo); atomicMax((unsigned long long *)&rng[1], hi); }
-}
 __global__ __launch_bounds__(BLOCK) void k_cd_keys(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
                                                    const uint64_t *__restrict__ ukey, uint64_t base, uint64_t *__restrict__ all)
 {
@@ -987,7 +991,7 @@ __global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *
 
 }  // namespace cd
 
-void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view)
+void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view *view, bool trusted)
 {
     using namespace cd;
     if (!in || !view) fail(ACC_E_ARG, "null argument");
@@ -1028,13 +1032,16 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         ACC_HIP(hipMemsetAsync(mo, 0, 4, st));
         ctx->sync();
     } else {
-        Upd none{};
-        launch(ctx, "cb_check", k_cd_check, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, s, none, (uint32_t *)nullptr, errs);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        if (ctx->pinned[0] & E_ARG_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal");
-        if (ctx->pinned[0] & E_ARG_OFF) fail(ACC_E_ARG, "offsets must be non-decreasing from 0 to their totals");
-        if (ctx->pinned[0] & E_ARG_SORT) fail(ACC_E_ARG, "keys / TxnIds must be sorted unique");
+        if (!trusted) {   // (acc_cfk_apply_deps hands over acc_cfk_apply's own output: already in this form)
+            Upd none{};
+            launch(ctx, "cb_check", k_cd_check, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, s, none, (uint32_t *)nullptr, errs,
+                   (uint64_t *)nullptr);
+            ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            if (ctx->pinned[0] & E_ARG_STATUS) fail(ACC_E_ARG, "invalid InternalStatus ordinal");
+            if (ctx->pinned[0] & E_ARG_OFF) fail(ACC_E_ARG, "offsets must be non-decreasing from 0 to their totals");
+            if (ctx->pinned[0] & E_ARG_SORT) fail(ACC_E_ARG, "keys / TxnIds must be sorted unique");
+        }
         const dim3 g(grid_for(NE, BLOCK));
         uint64_t *k = ctx->get<uint64_t>("cb_key", NE);
         uint32_t *qpos = ctx->get<uint32_t>("cb_qpos", NE);
@@ -1130,13 +1137,10 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     uint64_t *errs = ctx->get<uint64_t>("cd_errs", 1);
     ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
     const uint64_t gmax = std::max<uint64_t>({ (uint64_t)nk, (uint64_t)nu, NP, 1 });
-    launch(ctx, "cd_check", k_cd_check, dim3(grid_for(gmax, BLOCK)), dim3(BLOCK), 0, s, u, owner, errs);
     uint64_t *krng = ctx->get<uint64_t>("cd_krng", 2);
     ACC_HIP(hipMemsetAsync(krng, 0xFF, 8, st));
     ACC_HIP(hipMemsetAsync(krng + 1, 0, 8, st));
-    if (nk + NP)
-        launch(ctx, "cd_krange", k_cd_krange, dim3((unsigned)std::min<uint64_t>(grid_for(nk + NP, BLOCK), 1024)), dim3(BLOCK), 0,
-               nk, NP, s.key, u.key, krng);
+    launch(ctx, "cd_check", k_cd_check, dim3(grid_for(gmax, BLOCK)), dim3(BLOCK), 0, s, u, owner, errs, krng);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, krng, 16, hipMemcpyDeviceToHost, st));
     ctx->sync();
