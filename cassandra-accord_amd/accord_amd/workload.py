@@ -484,7 +484,7 @@ def config4(scale: float = 1.0, **kw) -> RangeBatch:
 
 
 def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = None, seed: int = CONFIG_SEEDS["2"] + 7,
-                      max_deps: int = 16, lag: int = 64) -> dict:
+                      max_deps: int = 16, lag: int = 64, dist: str = "uniform") -> dict:
     """A CommandsForKey update stream of config-2 size (acc_cfk_apply's CFK_UPD layout), for the N4 bench leg: the txns
     of keydeps_batch(n_txn, keys_per_txn, n_keys, uniform keys, status model) as SafeCommandStore.updateCommandsForKey
     sees them (local/SafeCommandStore.java:217-240): an Accept (ACCEPTED, executeAt = TxnId) at time i, then the final
@@ -492,9 +492,10 @@ def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = No
     final status is PREACCEPTED / TRANSITIVELY_KNOWN only pre-accept, ACCEPTED ones only accept. The deps of a txn on
     a key (its keyDeps.txnIds(key)) are the latest max_deps txns below it on that key, every one already known to the
     key's CFK. Uniform keys: a zipf hot key's CFK grows with its whole history (CommandsForKey.update copies the key's
-    arrays, linear per update), which the reference bounds by pruning, outside the §8 path."""
+    arrays, linear per update), which the reference bounds by pruning, outside the §8 path. dist="zipf": zipf(0.99) keys
+    as config 2 (a hot key's updates take acc_cfk_apply's hot-key closed form)."""
     n_keys = n_keys or n_txn
-    b = keydeps_batch(n_txn, keys_per_txn, n_keys, seed, "uniform", status_model="model")
+    b = keydeps_batch(n_txn, keys_per_txn, n_keys, seed, dist, status_model="model")
     st = b.status.astype(np.int64)
     K = keys_per_txn
     # deps per (txn, key) pair: the latest max_deps txns below it on the key (pairs sorted by (key, txn))

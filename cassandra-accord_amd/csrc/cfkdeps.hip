@@ -608,10 +608,20 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint3
                                                      const uint32_t *__restrict__ src, const uint32_t *__restrict__ snd,
                                                      uint32_t nk, Snap s, uint64_t *__restrict__ ecap,
                                                      uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
-                                                     uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf)
+                                                     uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf,
+                                                     uint32_t hot_thr, int keep_hot, uint8_t *__restrict__ hot,
+                                                     uint32_t *__restrict__ nhot)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys) return;
+    // a key with more than hot_thr elements takes the hot-key path (no lane working space); keep_hot: flags as left by
+    // the hot-key path (its irregular keys cleared)
+    if (!keep_hot) hot[k] = kstart[k + 1] - kstart[k] > hot_thr ? 1 : 0;
+    if (hot[k]) {
+        ecap[k] = 0; mcap[k] = 0; mmax[k] = 0; dcap[k] = 1; ovf[k] = 0;
+        atomicAdd(nhot, 1u);
+        return;
+    }
     uint64_t e = 0, m = 0, d = 0, grow = 0;
     for (uint32_t q = kstart[k], q1 = kstart[k + 1]; q < q1; ++q) {
         const uint32_t v = src[q];
@@ -754,7 +764,7 @@ uint32_t nkeys, const uint32_t *__restrict__ kstart,
                                                     uint8_t *__restrict__ final_b, uint32_t *__restrict__ fin_n,
                                                     uint32_t *__restrict__ fin_m, uint32_t *__restrict__ ovf,
                                                     uint64_t *__restrict__ err, unsigned long long *__restrict__ paths,
-                                                    const UpdRec *__restrict__ urec)
+                                                    const UpdRec *__restrict__ urec, const uint8_t *__restrict__ hot)
 {
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t n_fast = 0, n_rebuild = 0;
@@ -763,7 +773,7 @@ uint32_t nkeys, const uint32_t *__restrict__ kstart,
         for (int d = 32; d >= 1; d >>= 1) { f += __shfl_xor(f, d, 64); r += __shfl_xor(r, d, 64); }
         if (lane_id() == 0 && (f || r)) { atomicAdd(&paths[0], f); atomicAdd(&paths[1], r); }
     };
-    if (slot >= nkeys) { count_paths(); return; }
+    if (slot >= nkeys || hot[p.perm[slot]]) { count_paths(); return; }
     const uint32_t k = p.perm[slot];
     Ctx c;
     c.err = 0;
@@ -853,10 +863,10 @@ struct Out {
 // entries of every kept key (one lane per key), and each entry's missing count
 __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
-                                                   const uint8_t *__restrict__ final_b, Out o)
+                                                   const uint8_t *__restrict__ final_b, Out o, const uint8_t *__restrict__ hot)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // key order: a wave's lanes write adjacent output runs
-    if (k >= nkeys || !keep[k]) return;
+    if (k >= nkeys || !keep[k] || hot[k]) return;
     Work w;
     key_bufs(p, p.kslot[k], w);
     const EP E = final_b[k] ? w.b.e : w.a.e;
@@ -872,10 +882,10 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_
 
 __global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
                                                    const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
-                                                   const uint8_t *__restrict__ final_b, Out o)
+                                                   const uint8_t *__restrict__ final_b, Out o, const uint8_t *__restrict__ hot)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // key order: a wave's lanes write adjacent output runs
-    if (k >= nkeys || !keep[k]) return;
+    if (k >= nkeys || !keep[k] || hot[k]) return;
     Work w;
     key_bufs(p, p.kslot[k], w);
     const Buf &F = final_b[k] ? w.b : w.a;
@@ -894,6 +904,547 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < n) out[i] = in[i];
+}
+
+// ---- hot keys: the replay's closed form, data-parallel over a key's updates
+// A key with more than ACC_CFK_HOT (default 1024) updates in the batch is not replayed by one lane: its final state is
+// computed from the update stream directly. Its TxnInfos are every TxnId its snapshot, its updates or their deps name
+// (a dep the key lacks becomes a TRANSITIVELY_KNOWN entry, updateOrInsertWithAdditions :772-863); each takes the status /
+// executeAt of its last update that changed it (update :657-706: stale checks, unchanged returns). The missing[] of an
+// entry X with info then follows from the reference's edits, which only ever add an uncommitted TxnId t below
+// max(TxnId, depsKnownBefore) of X that X witnesses (computeInfoAndAdditions :1071-1150, insertInfoAndOneMissing :899-944,
+// mergeAndFilterMissing :988-1025) and remove t when it commits (removeMissing :946-972):
+//   X last computed in this batch, with deps D:  { t uncommitted at the end, t != X, t < bound(X), X witnesses t } \ D
+//   X's info from the snapshot:  (snapshot missing[] \ TxnIds committed in this batch)
+//                                u { t new in this batch, uncommitted at the end, t < bound(X), X witnesses t }
+// Statuses only rise, so "uncommitted at the end" is "uncommitted whenever X looked". The shapes the closed form does not
+// cover -- a status going back (AcceptedInvalidate), executeAt below its TxnId, a dep at or above depsKnownBefore or equal
+// to the txn, depsKnownBefore equal to an entry, two encodings of one TxnId -- mark the key irregular: it is replayed by
+// the lane path instead (which also reports the reference's errors exactly).
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t CH_DEFAULT_HOT = 1024;
+enum : uint8_t { HI_SNAP = 0, HI_PAIR = 1, HI_TK = 2 };
+enum : uint8_t { HF_CROSSED = 1, HF_NEW = 2 };
+
+struct HG {   // one (key, TxnId) group: the entry it becomes
+    uint64_t im, il, xm, xl;
+    int32_t in, xn;
+    uint32_t info_q;   // pair of the last recompute (its deps), NONE: none in this batch
+    uint32_t snap_x;   // snapshot entry, NONE: new
+    uint32_t h;
+    uint8_t st, self, present, flags;
+    uint32_t pad[2];
+};
+static_assert(sizeof(HG) == 64, "64-B group record");
+
+__device__ __forceinline__ Ts hg_id(const HG &g) { return Ts{ g.im, g.il, g.in }; }
+__device__ __forceinline__ Ts hg_bound(const HG &g)   // depsKnownBefore (>= the TxnId on a regular key)
+{
+    return (g.st == PRE || g.st == ACC || g.self) ? Ts{ g.im, g.il, g.in } : Ts{ g.xm, g.xl, g.xn };
+}
+
+// per hot key: its item count (snapshot entries + pairs) and whether its run starts with the snapshot element
+__global__ __launch_bounds__(BLOCK) void k_ch_count(uint32_t nh, const uint32_t *__restrict__ hk, const uint32_t *__restrict__ kstart,
+                                                    const uint32_t *__restrict__ src, uint32_t nk, Snap s,
+                                                    uint32_t *__restrict__ icnt, uint32_t *__restrict__ nsnap, uint8_t *__restrict__ hsnap)
+{
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= nh) return;
+    const uint32_t k = hk[h], q0 = kstart[k], q1 = kstart[k + 1];
+    const uint32_t v = src[q0];
+    const bool sn = v < nk;
+    const uint32_t ne = sn ? s.ent_off[v + 1] - s.ent_off[v] : 0u;
+    nsnap[h] = ne;
+    hsnap[h] = sn ? 1 : 0;
+    icnt[h] = ne + (q1 - q0) - (sn ? 1u : 0u);
+}
+
+struct HItems {
+    uint64_t *im, *il, *inode;   // TxnId words (node biased for the dense rank)
+    uint32_t *ih, *isrc;
+    uint8_t *ikind;
+};
+
+// every item of the hot keys: their snapshot entries, then their pairs in batch order
+__global__ __launch_bounds__(BLOCK) void k_ch_items(uint64_t NI, uint32_t nh, const uint32_t *__restrict__ ioff,
+                                                    const uint32_t *__restrict__ hk, const uint32_t *__restrict__ nsnap,
+                                                    const uint8_t *__restrict__ hsnap, const uint32_t *__restrict__ kstart,
+                                                    const uint32_t *__restrict__ src, Snap s, const UpdRec *__restrict__ urec,
+                                                    HItems it)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= NI) return;
+    uint32_t lo = 0, hi = nh;   // last h with ioff[h] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ioff[mid] <= i) lo = mid; else hi = mid;
+    }
+    const uint32_t h = lo, r = (uint32_t)(i - ioff[h]), k = hk[h], q0 = kstart[k];
+    uint64_t m, l;
+    int32_t n;
+    if (r < nsnap[h]) {
+        const uint32_t x = s.ent_off[src[q0]] + r;
+        m = s.em[x]; l = s.el[x]; n = s.en[x];
+        it.isrc[i] = x;
+        it.ikind[i] = HI_SNAP;
+    } else {
+        const uint32_t q = q0 + hsnap[h] + (r - nsnap[h]);
+        const UpdRec &u = urec[q];
+        m = u.im; l = u.il; n = u.in;
+        it.isrc[i] = q;
+        it.ikind[i] = HI_PAIR;
+    }
+    it.im[i] = m; it.il[i] = l; it.inode[i] = (uint32_t)n ^ 0x80000000u;
+    it.ih[i] = h;
+}
+
+// sort keys: (hot key, TxnId rank); group starts
+__global__ __launch_bounds__(BLOCK) void k_ch_skey(uint64_t NI, const uint32_t *__restrict__ ih, const uint32_t *__restrict__ rank,
+                                                   int rb, uint64_t *__restrict__ key)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < NI) key[i] = ((uint64_t)ih[i] << rb) | rank[i];
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_gflag(uint64_t NI, const uint64_t *__restrict__ sk, uint32_t *__restrict__ f)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p < NI) f[p] = (p == 0 || sk[p] != sk[p - 1]) ? 1u : 0u;
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_gstart(uint64_t NI, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fi,
+                                                     uint32_t ng, uint32_t *__restrict__ gstart)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p < NI && f[p]) gstart[fi[p] - 1] = (uint32_t)p;
+    if (p == 0) gstart[ng] = (uint32_t)NI;
+}
+
+// one thread per group: its items in time order through update's status rules (:657-706)
+__global__ __launch_bounds__(BLOCK) void k_ch_walk(uint32_t ng, const uint32_t *__restrict__ gstart, const uint32_t *__restrict__ perm,
+                                                   HItems it, Snap s, const UpdRec *__restrict__ urec, HG *__restrict__ G,
+                                                   uint8_t *__restrict__ mention, uint32_t *__restrict__ irr,
+                                                   uint64_t *__restrict__ err)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= ng) return;
+    const uint32_t p0 = gstart[g], p1 = gstart[g + 1];
+    const uint32_t i0 = perm[p0];
+    const Ts id{ it.im[i0], it.il[i0], (int32_t)(uint32_t)(it.inode[i0] ^ 0x80000000u) };
+    const uint32_t h = it.ih[i0];
+    bool present = false, crossed = false, isnew = true, bad = false;
+    uint32_t st = TK, self = 1, info_q = NONE, snap_x = NONE;
+    Ts ex = id;
+    uint64_t e = 0;
+    for (uint32_t p = p0; p < p1 && !e; ++p) {
+        const uint32_t i = perm[p];
+        mention[p] = 0;
+        if (it.il[i] != id.l) bad = true;   // two encodings of one TxnId
+        const uint8_t kd = it.ikind[i];
+        if (kd == HI_SNAP) {
+            const uint32_t x = it.isrc[i];
+            present = true; isnew = false; snap_x = x;
+            st = s.st[x];
+            ex = Ts{ s.xm[x], s.xl[x], s.xn[x] };
+            self = cmp(ex, id) == 0;
+            if (self) ex = id;
+        } else if (kd == HI_TK) {
+            if (!present) { present = true; st = TK; ex = id; self = 1; }
+        } else {
+            const UpdRec u = urec[it.isrc[i]];
+            const uint32_t sn = u.st_fl & 0xFFu, fl = u.st_fl >> 8;
+            if (sn == 0xFF) continue;
+            if (present) {
+                if (sn <= st) {
+                    if (st != sn && !(fl & 2u)) { e |= E_STALE; break; }
+                    if (!has_info(sn) || !(fl & 1u)) continue;
+                    if (sn < st) bad = true;   // AcceptedInvalidate taking the status back
+                }
+                if (st < COMMITTED && sn >= COMMITTED) crossed = true;
+            }
+            present = true;
+            st = sn;
+            if (has_info(sn)) {
+                ex = Ts{ u.xm, u.xl, u.xn };
+                self = cmp(ex, id) == 0;
+                if (self) ex = id;
+                info_q = it.isrc[i];
+                mention[p] = 1;
+            } else {
+                ex = id; self = 1; info_q = NONE;
+            }
+        }
+    }
+    // executeAt below the TxnId: the reference's edits then differ by position (no depsKnownBefore test after it)
+    if (present && has_info(st) && !(st == PRE || st == ACC || self) && cmp(ex, id) < 0) bad = true;
+    HG r;
+    r.im = id.m; r.il = id.l; r.in = id.n;
+    r.xm = ex.m; r.xl = ex.l; r.xn = ex.n;
+    r.info_q = info_q; r.snap_x = snap_x; r.h = h;
+    r.st = (uint8_t)st; r.self = (uint8_t)self; r.present = present ? 1 : 0;
+    r.flags = (crossed ? HF_CROSSED : 0) | (isnew ? HF_NEW : 0);
+    r.pad[0] = r.pad[1] = 0;
+    G[g] = r;
+    if (bad) irr[h] = 1;
+    if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
+}
+
+// each hot key's first group (groups are in hot-key order; every hot key has one)
+__global__ __launch_bounds__(BLOCK) void k_ch_gofs(uint32_t ng, uint32_t nh, const HG *__restrict__ G, uint32_t *__restrict__ gofs,
+                                                   uint32_t *__restrict__ pflag)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g < ng) {
+        if (g == 0 || G[g].h != G[g - 1].h) gofs[G[g].h] = g;
+        pflag[g] = G[g].present;
+    }
+    if (g == 0) gofs[nh] = ng;
+}
+// entries (the present groups) -> group; each hot key's first entry
+__global__ __launch_bounds__(BLOCK) void k_ch_entries(uint32_t ng, uint32_t nh, uint32_t ne, const HG *__restrict__ G,
+                                                      const uint32_t *__restrict__ pexcl, const uint32_t *__restrict__ gofs,
+                                                      uint32_t *__restrict__ eg, uint32_t *__restrict__ eoff)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g < ng && G[g].present) eg[pexcl[g]] = g;
+    if (g <= nh) eoff[g] = g == nh ? ne : pexcl[gofs[g]];
+}
+// entries still uncommitted (missing[] candidates), and each hot key's first one
+__global__ __launch_bounds__(BLOCK) void k_ch_uflag(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                    uint32_t *__restrict__ uflag)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e < ne) uflag[e] = G[eg[e]].st < COMMITTED ? 1u : 0u;
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_ulist(uint32_t ne, uint32_t nh, uint32_t nu, const uint32_t *__restrict__ uflag,
+                                                    const uint32_t *__restrict__ uexcl, const uint32_t *__restrict__ eoff,
+                                                    uint32_t *__restrict__ ulist, uint32_t *__restrict__ uoff)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e < ne && uflag[e]) ulist[uexcl[e]] = e;
+    if (e <= nh) uoff[e] = e == nh ? nu : (eoff[e] < ne ? uexcl[eoff[e]] : nu);
+}
+
+// the entry of hot key h with TxnId t (NONE when absent)
+__device__ __forceinline__ uint32_t ch_find(const uint32_t *__restrict__ eg, const HG *__restrict__ G, uint32_t e0, uint32_t e1,
+                                            const Ts &t)
+{
+    uint32_t lo = e0, hi = e1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const HG &x = G[eg[mid]];
+        if (cmp(hg_id(x), t) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo < e1 && cmp(hg_id(G[eg[lo]]), t) == 0 ? lo : NONE;
+}
+
+// every recompute's deps: a dep the key does not hold becomes a TRANSITIVELY_KNOWN item (pass 1 counts, pass 2 writes);
+// the shapes outside the closed form mark the key irregular
+__global__ __launch_bounds__(BLOCK) void k_ch_mention(uint64_t NI, const uint8_t *__restrict__ mention, const uint32_t *__restrict__ perm,
+                                                     HItems it, const UpdRec *__restrict__ urec, Upd u, const uint32_t *__restrict__ eg,
+                                                     const HG *__restrict__ G, const uint32_t *__restrict__ eoff,
+                                                     uint32_t *__restrict__ irr, uint32_t *__restrict__ nextra, uint64_t cap,
+                                                     HItems xo)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= NI || !mention[p]) return;
+    const uint32_t i = perm[p], h = it.ih[i];
+    const UpdRec r = urec[it.isrc[i]];
+    const uint32_t st = r.st_fl & 0xFFu;
+    const Ts id{ r.im, r.il, r.in }, ex{ r.xm, r.xl, r.xn };
+    const bool self = st == PRE || st == ACC || cmp(ex, id) == 0;
+    const Ts bound = self ? id : ex;
+    const uint32_t e0 = eoff[h], e1 = eoff[h + 1];
+    bool bad = false;
+    if (!self && (cmp(ex, id) < 0 || ch_find(eg, G, e0, e1, ex) != NONE)) bad = true;
+    for (uint32_t d = r.da; d < r.db && !bad; ++d) {
+        const Ts t{ u.dm[d], u.dl[d], u.dn[d] };
+        if (cmp(t, bound) >= 0 || cmp(t, id) == 0) { bad = true; break; }
+        if (ch_find(eg, G, e0, e1, t) != NONE) continue;
+        const uint32_t w = atomicAdd(nextra, 1u);
+        if (w < cap) {
+            xo.im[w] = t.m; xo.il[w] = t.l; xo.inode[w] = (uint32_t)t.n ^ 0x80000000u;
+            xo.ih[w] = h; xo.isrc[w] = NONE; xo.ikind[w] = HI_TK;
+        }
+    }
+    if (bad) irr[h] = 1;
+}
+
+// the closed-form missing[] of entry e (count only when out is null)
+__device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                               const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                               const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u, Snap s,
+                                               uint64_t *om, uint64_t *ol, int32_t *on)
+{
+    const HG X = G[eg[e]];
+    if (!has_info(X.st)) return 0;
+    const Ts id = hg_id(X), bound = hg_bound(X);
+    const uint32_t wm = witnesses_mask(kind(id));
+    const uint32_t h = X.h, u0 = uoff[h], u1 = uoff[h + 1];
+    uint32_t lo = u0, hi = u1;   // uncommitted entries below the bound: [u0, ub)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cmp(hg_id(G[eg[ulist[mid]]]), bound) < 0) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t ub = lo;
+    uint32_t n = 0;
+    auto put = [&](const HG &t) {
+        if (om) { om[n] = t.im; ol[n] = t.il; on[n] = t.in; }
+        ++n;
+    };
+    if (X.info_q != NONE) {   // computed in this batch: the uncommitted entries below the bound, less its deps
+        const UpdRec r = urec[X.info_q];
+        uint32_t d = r.da;
+        for (uint32_t k = u0; k < ub; ++k) {
+            const HG t = G[eg[ulist[k]]];
+            const Ts tid = hg_id(t);
+            if (cmp(tid, id) == 0 || !((wm >> kind(tid)) & 1u)) continue;
+            while (d < r.db && cmp(Ts{ u.dm[d], u.dl[d], u.dn[d] }, tid) < 0) ++d;
+            if (d < r.db && cmp(Ts{ u.dm[d], u.dl[d], u.dn[d] }, tid) == 0) continue;
+            put(t);
+        }
+        return n;
+    }
+    if (X.snap_x == NONE) return 0;
+    // the snapshot's missing[] (less the TxnIds committed in this batch) merged with the new uncommitted entries
+    const uint32_t m0 = s.miss_off[X.snap_x], m1 = s.miss_off[X.snap_x + 1];
+    const uint32_t e0 = eoff[h], e1 = eoff[h + 1];
+    uint32_t a = m0, k = u0;
+    auto next_new = [&]() {
+        while (k < ub) {
+            const HG &t = G[eg[ulist[k]]];
+            const Ts tid = hg_id(t);
+            if ((t.flags & HF_NEW) && cmp(tid, id) != 0 && ((wm >> kind(tid)) & 1u)) return;
+            ++k;
+        }
+    };
+    auto next_snap = [&]() {
+        while (a < m1) {
+            const uint32_t f = ch_find(eg, G, e0, e1, Ts{ s.mm[a], s.ml[a], s.mn[a] });
+            if (f == NONE || !(G[eg[f]].flags & HF_CROSSED)) return;
+            ++a;
+        }
+    };
+    next_new();
+    next_snap();
+    while (a < m1 || k < ub) {
+        int c;
+        if (a == m1) c = 1;
+        else if (k == ub) c = -1;
+        else c = cmp(Ts{ s.mm[a], s.ml[a], s.mn[a] }, hg_id(G[eg[ulist[k]]]));
+        if (c <= 0) {
+            if (om) { om[n] = s.mm[a]; ol[n] = s.ml[a]; on[n] = s.mn[a]; }
+            ++n;
+            ++a;
+            if (c == 0) ++k;
+        } else {
+            put(G[eg[ulist[k]]]);
+            ++k;
+        }
+        next_new();
+        next_snap();
+    }
+    return n;
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_mcount(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                     const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                                     const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
+                                                     Snap s, uint32_t *__restrict__ mcnt)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e < ne) mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, nullptr, nullptr, nullptr);
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_memit(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                    const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                                    const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
+                                                    Snap s, const uint32_t *__restrict__ moff, uint64_t *__restrict__ mm,
+                                                    uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e < ne) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, mm + moff[e], ml + moff[e], mn + moff[e]);
+}
+// the hot keys' final entry counts (the lane path's fin_n), and the irregular ones back to the lane path
+__global__ __launch_bounds__(BLOCK) void k_ch_fin(uint32_t nh, const uint32_t *__restrict__ hk, const uint32_t *__restrict__ eoff,
+                                                  const uint32_t *__restrict__ irr, uint32_t *__restrict__ fin_n,
+                                                  uint8_t *__restrict__ hot, uint32_t *__restrict__ nirr)
+{
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    if (h >= nh) return;
+    if (irr[h]) { hot[hk[h]] = 0; atomicAdd(nirr, 1u); }
+    else fin_n[hk[h]] = eoff[h + 1] - eoff[h];
+}
+// output: the hot keys' entries and missing[] into the key-major layout
+__global__ __launch_bounds__(BLOCK) void k_ch_out3(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                   const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ hk,
+                                                   const uint32_t *__restrict__ kpos, const uint32_t *__restrict__ mcnt, Out o)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= ne) return;
+    const HG X = G[eg[e]];
+    const uint32_t dst = o.ent_off[kpos[hk[X.h]]] + (e - eoff[X.h]);
+    o.em[dst] = X.im; o.el[dst] = X.il; o.en[dst] = X.in;
+    o.xm[dst] = X.xm; o.xl[dst] = X.xl; o.xn[dst] = X.xn;
+    o.st[dst] = X.st;
+    o.mcnt[dst] = mcnt[e];
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_out4(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                   const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ hk,
+                                                   const uint32_t *__restrict__ kpos, const uint32_t *__restrict__ moff,
+                                                   const uint64_t *__restrict__ mm, const uint64_t *__restrict__ ml,
+                                                   const int32_t *__restrict__ mn, Out o)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t h = G[eg[e]].h;
+    const uint32_t pos = o.ent_off[kpos[hk[h]]] + (e - eoff[h]);
+    uint32_t dst = o.miss_off[pos];
+    for (uint32_t q = moff[e]; q < moff[e + 1]; ++q, ++dst) { o.mm[dst] = mm[q]; o.ml[dst] = ml[q]; o.mn[dst] = mn[q]; }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ch_hflag(uint32_t nkeys, const uint8_t *__restrict__ hot, uint32_t *__restrict__ f)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < nkeys) f[k] = hot[k];
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_hk(uint32_t nkeys, const uint32_t *__restrict__ f, const uint32_t *__restrict__ fx,
+                                                 uint32_t *__restrict__ hk)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < nkeys && f[k]) hk[fx[k]] = k;
+}
+
+struct HotOut {
+    uint32_t nh = 0, ne = 0;
+    uint64_t nm = 0;
+    const uint32_t *hk = nullptr, *eg = nullptr, *eoff = nullptr, *mcnt = nullptr, *moff = nullptr;
+    const HG *G = nullptr;
+    const uint64_t *mm = nullptr, *ml = nullptr;
+    const int32_t *mn = nullptr;
+};
+
+// The hot keys' final states (closed form above). Returns false when some hot keys turned out irregular: their hot
+// flags are cleared and the caller lays the lane path out again with them.
+static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t *kstart, const uint32_t *src, uint32_t nk,
+                     const Snap &s, const Upd &u, const UpdRec *urec, uint32_t *fin_n, uint64_t *errs, HotOut &ho)
+{
+    hipStream_t st = ctx->stream;
+    auto read32 = [&](const uint32_t *p) {
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, p, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        return reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+    };
+    ho = HotOut{};
+    uint32_t *hf = ctx->get<uint32_t>("ch_hf", nkeys), *hx = ctx->get<uint32_t>("ch_hx", (size_t)nkeys + 1);
+    launch(ctx, "ch_hflag", k_ch_hflag, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint8_t *)hot, hf);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, hf, hx, nkeys, true, hx + nkeys);
+    const uint32_t nh = read32(hx + nkeys);
+    if (!nh) return true;
+    uint32_t *hk = ctx->get<uint32_t>("ch_hk", nh);
+    launch(ctx, "ch_hk", k_ch_hk, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)hf, (const uint32_t *)hx, hk);
+    uint32_t *icnt = ctx->get<uint32_t>("ch_icnt", nh), *nsnap = ctx->get<uint32_t>("ch_nsnap", nh);
+    uint32_t *ioff = ctx->get<uint32_t>("ch_ioff", (size_t)nh + 1);
+    uint8_t *hsnap = ctx->get<uint8_t>("ch_hsnap", nh);
+    launch(ctx, "ch_count", k_ch_count, dim3(grid_for(nh, BLOCK)), dim3(BLOCK), 0, nh, (const uint32_t *)hk, kstart, src, nk, s,
+           icnt, nsnap, hsnap);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, icnt, ioff, nh, true, ioff + nh);
+    const uint64_t NI0 = read32(ioff + nh);
+    uint32_t *nextra = ctx->get<uint32_t>("ch_nextra", 1);
+    uint32_t *irr = ctx->get<uint32_t>("ch_irr", nh);
+    uint64_t NX = 0, NI = 0;
+    uint32_t ng = 0, ne = 0;
+    HItems it{};
+    HG *G = nullptr;
+    uint32_t *eg = nullptr, *eoff = nullptr;
+    for (int pass = 0; pass < 2; ++pass) {
+        NI = NI0 + NX;
+        it = HItems{ ctx->get<uint64_t>("ch_im", NI), ctx->get<uint64_t>("ch_il", NI), ctx->get<uint64_t>("ch_inode", NI),
+                     ctx->get<uint32_t>("ch_ih", NI), ctx->get<uint32_t>("ch_isrc", NI), ctx->get<uint8_t>("ch_ikind", NI) };
+        launch(ctx, "ch_items", k_ch_items, dim3(grid_for(NI0, BLOCK)), dim3(BLOCK), 0, NI0, nh, (const uint32_t *)ioff,
+               (const uint32_t *)hk, (const uint32_t *)nsnap, (const uint8_t *)hsnap, kstart, src, s, urec, it);
+        if (NX) {   // the first pass's TRANSITIVELY_KNOWN items after the rest
+            ACC_HIP(hipMemcpyAsync(it.im + NI0, ctx->get<uint64_t>("ch_xim", NX), NX * 8, hipMemcpyDeviceToDevice, st));
+            ACC_HIP(hipMemcpyAsync(it.il + NI0, ctx->get<uint64_t>("ch_xil", NX), NX * 8, hipMemcpyDeviceToDevice, st));
+            ACC_HIP(hipMemcpyAsync(it.inode + NI0, ctx->get<uint64_t>("ch_xinode", NX), NX * 8, hipMemcpyDeviceToDevice, st));
+            ACC_HIP(hipMemcpyAsync(it.ih + NI0, ctx->get<uint32_t>("ch_xih", NX), NX * 4, hipMemcpyDeviceToDevice, st));
+            ACC_HIP(hipMemcpyAsync(it.isrc + NI0, ctx->get<uint32_t>("ch_xisrc", NX), NX * 4, hipMemcpyDeviceToDevice, st));
+            ACC_HIP(hipMemcpyAsync(it.ikind + NI0, ctx->get<uint8_t>("ch_xikind", NX), NX, hipMemcpyDeviceToDevice, st));
+        }
+        // items grouped by (hot key, TxnId), batch order kept inside a group
+        const uint64_t *words[3] = { it.im, it.il, it.inode };
+        const uint64_t wand[3] = { ~0ull, IDENTITY_LSB, ~0ull };
+        DenseRank dr = dense_rank(ctx, "ch_dr", NI, 3, words, wand, nullptr, false);
+        const int rb = std::max(1, bits_for(NI)), hb = std::max(1, bits_for(nh));
+        uint64_t *key = ctx->get<uint64_t>("ch_key", NI);
+        launch(ctx, "ch_skey", k_ch_skey, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint32_t *)it.ih,
+               (const uint32_t *)dr.rank, rb, key);
+        Sorted so = radix_sort(ctx, "ch_rs", key, nullptr, NI, rb + hb);
+        uint32_t *gf = ctx->get<uint32_t>("ch_gf", NI), *gi = ctx->get<uint32_t>("ch_gi", NI);
+        launch(ctx, "ch_gflag", k_ch_gflag, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint64_t *)so.keys, gf);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, gf, gi, NI, false);
+        ng = read32(gi + NI - 1);
+        uint32_t *gstart = ctx->get<uint32_t>("ch_gstart", (size_t)ng + 1);
+        launch(ctx, "ch_gstart", k_ch_gstart, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint32_t *)gf, (const uint32_t *)gi,
+               ng, gstart);
+        G = ctx->get<HG>("ch_G", ng);
+        uint8_t *mention = ctx->get<uint8_t>("ch_mention", NI);
+        ACC_HIP(hipMemsetAsync(mention, 0, NI, st));
+        ACC_HIP(hipMemsetAsync(irr, 0, (size_t)nh * 4, st));
+        launch(ctx, "ch_walk", k_ch_walk, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, (const uint32_t *)gstart,
+               (const uint32_t *)so.vals, it, s, urec, G, mention, irr, errs);
+        uint32_t *gofs = ctx->get<uint32_t>("ch_gofs", (size_t)nh + 1), *pf = ctx->get<uint32_t>("ch_pf", ng);
+        uint32_t *px = ctx->get<uint32_t>("ch_px", (size_t)ng + 1);
+        launch(ctx, "ch_gofs", k_ch_gofs, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, nh, (const HG *)G, gofs, pf);
+        scan<uint32_t, OpAdd<uint32_t>>(ctx, pf, px, ng, true, px + ng);
+        ne = read32(px + ng);
+        eg = ctx->get<uint32_t>("ch_eg", std::max<uint32_t>(ne, 1));
+        eoff = ctx->get<uint32_t>("ch_eoff", (size_t)nh + 1);
+        launch(ctx, "ch_entries", k_ch_entries, dim3(grid_for(std::max<uint64_t>(ng, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0,
+               ng, nh, ne, (const HG *)G, (const uint32_t *)px, (const uint32_t *)gofs, eg, eoff);
+        // the recomputes' deps: the ones no entry holds become TRANSITIVELY_KNOWN items (counted, then written)
+        ACC_HIP(hipMemsetAsync(nextra, 0, 4, st));
+        HItems none{};
+        launch(ctx, "ch_mention", k_ch_mention, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint8_t *)mention,
+               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)eoff, irr, nextra,
+               (uint64_t)0, none);
+        const uint32_t nx = read32(nextra);
+        if (!nx) break;
+        if (pass == 1) fail(ACC_E_STATE, "internal: CommandsForKey hot-key additions did not settle");
+        NX = nx;
+        HItems xo{ ctx->get<uint64_t>("ch_xim", NX), ctx->get<uint64_t>("ch_xil", NX), ctx->get<uint64_t>("ch_xinode", NX),
+                   ctx->get<uint32_t>("ch_xih", NX), ctx->get<uint32_t>("ch_xisrc", NX), ctx->get<uint8_t>("ch_xikind", NX) };
+        ACC_HIP(hipMemsetAsync(nextra, 0, 4, st));
+        launch(ctx, "ch_mention", k_ch_mention, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint8_t *)mention,
+               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)eoff, irr, nextra,
+               NX, xo);
+    }
+    uint32_t *nirr = ctx->get<uint32_t>("ch_nirr", 1);
+    ACC_HIP(hipMemsetAsync(nirr, 0, 4, st));
+    launch(ctx, "ch_fin", k_ch_fin, dim3(grid_for(nh, BLOCK)), dim3(BLOCK), 0, nh, (const uint32_t *)hk, (const uint32_t *)eoff,
+           (const uint32_t *)irr, fin_n, hot, nirr);
+    const uint32_t ni = read32(nirr);
+    ctx->stat("cfk.hot_irregular", ni);
+    if (ni) return false;
+    // the uncommitted entries per hot key, then every entry's missing[]
+    uint32_t *uf = ctx->get<uint32_t>("ch_uf", std::max<uint32_t>(ne, 1)), *ux = ctx->get<uint32_t>("ch_ux", (size_t)ne + 1);
+    launch(ctx, "ch_uflag", k_ch_uflag, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G, uf);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, uf, ux, ne, true, ux + ne);
+    const uint32_t nu = read32(ux + ne);
+    uint32_t *ulist = ctx->get<uint32_t>("ch_ulist", std::max<uint32_t>(nu, 1)), *uoff = ctx->get<uint32_t>("ch_uoff", (size_t)nh + 1);
+    launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nu,
+           (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, ulist, uoff);
+    uint32_t *mcnt = ctx->get<uint32_t>("ch_mcnt", std::max<uint32_t>(ne, 1)), *moff = ctx->get<uint32_t>("ch_moff", (size_t)ne + 1);
+    launch(ctx, "ch_mcount", k_ch_mcount, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
+           (const uint32_t *)eoff, (const uint32_t *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, mcnt, moff, ne, true, moff + ne);
+    const uint64_t nm = read32(moff + ne);
+    uint64_t *mm = ctx->get<uint64_t>("ch_mm", nm), *ml = ctx->get<uint64_t>("ch_ml", nm);
+    int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
+    if (nm)
+        launch(ctx, "ch_memit", k_ch_memit, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
+               (const uint32_t *)eoff, (const uint32_t *)ulist, (const uint32_t *)uoff, urec, u, s, (const uint32_t *)moff, mm, ml, mn);
+    ctx->stat("cfk.hot_keys", nh);
+    ctx->stat("cfk.hot_items", NI);
+    ho.nh = nh; ho.ne = ne; ho.nm = nm;
+    ho.hk = hk; ho.eg = eg; ho.eoff = eoff; ho.mcnt = mcnt; ho.moff = moff; ho.G = G; ho.mm = mm; ho.ml = ml; ho.mn = mn;
+    return true;
 }
 
 // ---- the key-major state as the txn-major snapshot of acc_map_reduce_full (acc_cfk_snap_to_batch)
@@ -1203,22 +1754,37 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         launch(ctx, "cd_inv", k_cd_inv, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)so.vals, nk, qpos);
         launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec, snd);
     }
-    if (nkeys) {
+    uint8_t *hot = ctx->get<uint8_t>("cd_hot", nkeys);
+    uint32_t hot_thr = CH_DEFAULT_HOT;
+    if (const char *e = getenv("ACC_CFK_HOT")) hot_thr = (uint32_t)std::max(1L, strtol(e, nullptr, 10));
+    uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys);
+    HotOut ho;
+    if (nkeys)
         launch(ctx, "cd_kstart", k_cd_kstart, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
                (const uint32_t *)kinc, nkeys, kstart);
+    uint32_t *nhot = ctx->get<uint32_t>("cd_nhot", 1);
+    ctx->stat("cfk.hot_keys", 0);
+    ctx->stat("cfk.hot_irregular", 0);
+    for (int keep_hot = 0; nkeys; keep_hot = 1) {
+        ACC_HIP(hipMemsetAsync(nhot, 0, 4, st));
         launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
-               (const uint32_t *)so.vals, (const uint32_t *)snd, nk, s, ecap, mcap, mmax, dcap, ovf);
+               (const uint32_t *)so.vals, (const uint32_t *)snd, nk, s, ecap, mcap, mmax, dcap, ovf, hot_thr, keep_hot, hot,
+               nhot);
         // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size
         uint64_t *cmax = ctx->get<uint64_t>("cd_cmax", 1);
         ACC_HIP(hipMemsetAsync(cmax, 0, 8, st));
         scan<uint64_t, OpMax<uint64_t>>(ctx, ecap, ctx->get<uint64_t>("cd_cscan", nkeys), nkeys, false, cmax);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, cmax, 8, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, nhot, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
+        const uint32_t nh = (uint32_t)ctx->pinned[1];
         perm = radix_sort(ctx, "cd_rs_cap", ecap, nullptr, nkeys, std::max(1, bits_for(ctx->pinned[0]))).vals;
         wave_layout();
+        // the hot keys' final states; keys found irregular go back to the lane path (layout again)
+        if (!nh || hot_keys(ctx, nkeys, hot, kstart, so.vals, nk, s, u, urec, fin_n, errs, ho)) break;
     }
     uint8_t *final_b = ctx->get<uint8_t>("cd_final_b", nkeys);
-    uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys), *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
+    uint32_t *fin_m = ctx->get<uint32_t>("cd_fin_m", nkeys);
     // ---- 3. replay, again with grown missing areas while some key outgrows its guess
     Pool p{};
     uint32_t regrow = 0;
@@ -1232,7 +1798,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ACC_HIP(hipMemsetAsync(paths, 0, 16, st));
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
                (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m,
-               ovf, errs, paths, (const UpdRec *)urec);
+               ovf, errs, paths, (const UpdRec *)urec, (const uint8_t *)hot);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, paths, 16, hipMemcpyDeviceToHost, st));
         ctx->sync();
@@ -1282,7 +1848,11 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     o.miss_off = ctx->get<uint32_t>("cd_omoff", NEo + 1);
     if (NEo) {
         launch(ctx, "cd_out3", k_cd_out3, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o);
+               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
+               (const uint8_t *)hot);
+        if (ho.ne)
+            launch(ctx, "ch_out3", k_ch_out3, dim3(grid_for(ho.ne, BLOCK)), dim3(BLOCK), 0, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
+                   (const uint32_t *)kpos, ho.mcnt, o);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, o.mcnt, o.miss_off, NEo, true, o.miss_off + NEo);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, o.miss_off + NEo, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
@@ -1292,8 +1862,14 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     }
     o.mm = ctx->get<uint64_t>("cd_omm", NMo); o.ml = ctx->get<uint64_t>("cd_oml", NMo); o.mn = ctx->get<int32_t>("cd_omn", NMo);
     if (NMo)
+    {
         launch(ctx, "cd_out4", k_cd_out4, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o);
+               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
+               (const uint8_t *)hot);
+        if (ho.nm)
+            launch(ctx, "ch_out4", k_ch_out4, dim3(grid_for(ho.ne, BLOCK)), dim3(BLOCK), 0, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
+                   (const uint32_t *)kpos, ho.moff, ho.mm, ho.ml, ho.mn, o);
+    }
     ctx->sync();
     ctx->stat("cfk.keys", nko);
     ctx->stat("cfk.entries", NEo);

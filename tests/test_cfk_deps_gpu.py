@@ -78,17 +78,104 @@ def hot_key_case(request):
     return request.param, upd
 
 
+@pytest.mark.parametrize("path", ["hot", "lane"])
 @pytest.mark.parametrize("frac", [0.3, 0.6, 1.0])
-def test_cfk_deps_hot_key(ctx, hot_key_case, frac):
+def test_cfk_deps_hot_key(ctx, hot_key_case, frac, path, monkeypatch):
+    """The hot key through the hot-key closed form (its ~2,700 updates are above ACC_CFK_HOT's default) and through
+    the one-lane replay (threshold raised)."""
     from accord_amd.deps import cfk_apply
+    if path == "lane":
+        monkeypatch.setenv("ACC_CFK_HOT", "1000000")
     p_dep, upd = hot_key_case
     part, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
     g = cfk_apply(ctx, CC.empty_snapshot(), part)
+    st = ctx.stats()
     o = oracle.cfk_apply(CC.empty_snapshot(), part)
-    same(g, o, f"hot key p_dep {p_dep} frac {frac}")
+    same(g, o, f"hot key p_dep {p_dep} frac {frac} {path}")
+    if path == "hot" and frac > 0.5:
+        assert st["cfk.hot_keys"] == 1 and st["cfk.hot_irregular"] == 0
     if p_dep == 0.0 and frac < 1.0:
         assert len(o["mmsb"]) > 10_000
-        assert ctx.stats()["cfk.apply_regrow"] > 0
+        if path == "lane":
+            assert st["cfk.apply_regrow"] > 0
+
+
+@pytest.fixture(params=["1", "3"], ids=["hot_gt1", "hot_gt3"])
+def hot_all(request, monkeypatch):
+    """Every key with more than 1 (3) sorted elements (its snapshot + its updates) through the hot-key closed form."""
+    monkeypatch.setenv("ACC_CFK_HOT", request.param)
+    return int(request.param)
+
+
+def test_cfk_hot_path_handmade(ctx, hot_all):
+    from accord_amd.deps import cfk_apply
+    upd, expect = CC.handmade()
+    for n, want in expect:
+        first, _ = CC.split_updates(upd, n)
+        g = cfk_apply(ctx, CC.empty_snapshot(), first)
+        assert CC.describe(g) == want, n
+        same(g, oracle.cfk_apply(CC.empty_snapshot(), first), f"handmade {n}")
+
+
+@pytest.mark.parametrize("seed,n_txn,n_keys", [(0, 200, 12), (1, 400, 30), (2, 120, 3), (3, 1500, 200)])
+def test_cfk_hot_path_random(ctx, hot_all, seed, n_txn, n_keys):
+    """Generated lifecycles (TRANSITIVELY_KNOWN additions, re-accepted ballots, bumped executeAts, invalidations):
+    the closed form equals the serial restatement bit for bit."""
+    from accord_amd.deps import cfk_apply
+    upd = CC.cfk_case(seed, n_txn=n_txn, n_keys=n_keys)
+    hot = 0
+    for frac in (0.1, 0.5, 1.0):
+        part, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
+        g = cfk_apply(ctx, CC.empty_snapshot(), part)
+        hot += ctx.stats()["cfk.hot_keys"]
+        same(g, oracle.cfk_apply(CC.empty_snapshot(), part), f"seed {seed} frac {frac}")
+    assert hot > 0
+
+
+def test_cfk_hot_path_chained(ctx, hot_all):
+    """Batches applied to the previous result: the snapshot's missing[] carried (less the TxnIds committed since), new
+    uncommitted TxnIds added."""
+    from accord_amd.deps import cfk_apply
+    upd = CC.cfk_case(7, n_txn=600, n_keys=40)
+    n = len(upd["msb"])
+    cuts = [0, n // 5, n // 2, 3 * n // 4, n]
+    snap = CC.empty_snapshot()
+    rest = upd
+    done = 0
+    for c in cuts[1:]:
+        part, rest = CC.split_updates(rest, c - done)
+        done = c
+        snap = cfk_apply(ctx, snap, part)
+        head, _ = CC.split_updates(upd, c)
+        same(snap, oracle.cfk_apply(CC.empty_snapshot(), head), f"after {c} updates")
+
+
+def test_cfk_hot_path_stream_and_errors(ctx, hot_all):
+    from accord_amd import workload as W
+    from accord_amd.deps import IllegalStateException, cfk_apply
+    upd = W.cfk_update_stream(5_000, 4, 800)
+    o = oracle.cfk_apply(CC.empty_snapshot(), upd)
+    same(cfk_apply(ctx, CC.empty_snapshot(), upd), o, "update stream")
+    a, b = CC.split_updates(upd, len(upd["msb"]) // 3)
+    same(cfk_apply(ctx, cfk_apply(ctx, CC.empty_snapshot(), a), b), o, "update stream, chained")
+    h, _ = CC.handmade()
+    back = {k: v.copy() for k, v in h.items()}
+    back["status"][4] = CC.PRE   # B goes back from ACCEPTED to PREACCEPTED
+    with pytest.raises(IllegalStateException):
+        cfk_apply(ctx, CC.empty_snapshot(), back)
+
+
+def test_cfk_zipf_update_stream(ctx):
+    """A zipf(0.99) update stream (workload.cfk_update_stream, 20,000 txns x 4 keys over 3,000 keys: the hottest key
+    holds ~9K pairs): the hot keys take the closed form, the rest the lanes; equal to the serial restatement."""
+    from accord_amd import workload as W
+    from accord_amd.deps import cfk_apply
+    upd = W.cfk_update_stream(20_000, 4, 3_000, dist="zipf")
+    o = oracle.cfk_apply(CC.empty_snapshot(), upd)
+    g = cfk_apply(ctx, CC.empty_snapshot(), upd)
+    st = ctx.stats()
+    same(g, o, "zipf update stream")
+    assert st["cfk.hot_keys"] > 0 and st["cfk.hot_irregular"] == 0
 
 
 def test_cfk_update_stream(ctx):
