@@ -366,10 +366,13 @@ def run_config2(args, world, rank, local, dev):
                                   keydeps_cpu_baseline(batch, "config 2"))
     if rank == 0 and world == 1 and not c3 and args.scale == 1.0 and os.environ.get("ACC_BENCH_CFK", "1") != "0":
         result["cfk_apply"] = cfk_apply_leg(local)
+        # the same stream shape over zipf(0.99) keys (the hottest key ~835K pairs): the hot keys take acc_cfk_apply's
+        # closed form (csrc/cfkdeps.hip, hot keys)
+        result["cfk_apply_zipf"] = cfk_apply_leg(local, calls=2, dist="zipf")
     return ctx, timing, elapsed, result
 
 
-def cfk_apply_leg(local, calls=3):
+def cfk_apply_leg(local, calls=3, dist="uniform"):
     """N4: a config-2-sized CommandsForKey update stream (workload.cfk_update_stream: 1M txns x 8
     uniform keys, ~2M updates / 16M (update, key) pairs / 63M deps, Accept then commit / stable / apply / invalidate,
     interleaved) applied by ONE acc_cfk_apply call to an empty key-major store, inputs resident in HBM; then
@@ -380,7 +383,7 @@ def cfk_apply_leg(local, calls=3):
     from accord_amd import workload as W
     from accord_amd.deps import Context, _view_as_snap
     t0 = time.perf_counter()
-    u = W.cfk_update_stream(1_000_000)
+    u = W.cfk_update_stream(1_000_000, dist=dist)
     t_gen = time.perf_counter() - t0
     dev = torch.device("cuda", local)
     d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in u.items()}
@@ -407,7 +410,8 @@ def cfk_apply_leg(local, calls=3):
         ms = (time.perf_counter() - t0) * 1000.0 / calls
         tm = c.timing()
         top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:5]
-        regrow = int(c.stats().get("cfk.apply_regrow", 0))
+        cst = c.stats()
+        regrow = int(cst.get("cfk.apply_regrow", 0))
         out = L.CfkBatchView()
         si = _view_as_snap(v)
         c.check(c._lib.acc_cfk_snap_to_batch(c.handle, C.byref(si), C.byref(out)))
@@ -417,9 +421,23 @@ def cfk_apply_leg(local, calls=3):
             c.check(c._lib.acc_cfk_snap_to_batch(c.handle, C.byref(si), C.byref(out)))
         torch.cuda.synchronize()
         ms_b = (time.perf_counter() - t0) * 1000.0 / calls
+        # the unified store's update (acc_cfk_apply_deps: the update, the txn-major view rebuilt, both kept in the
+        # store), each call on a fresh empty store
+        ms_s = []
+        for _ in range(calls + 1):
+            h = C.c_void_p()
+            c.check(c._lib.acc_cfk_create(c.handle, C.byref(h)))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            c.check(c._lib.acc_cfk_apply_deps(c.handle, h, C.byref(ui)))
+            torch.cuda.synchronize()
+            ms_s.append((time.perf_counter() - t0) * 1000.0)
+            c._lib.acc_cfk_destroy(h)
         n_upd, n_pairs, n_deps = len(u["msb"]), len(u["key"]), len(u["dmsb"])
-        return {"workload": "workload.cfk_update_stream(1M txns x 8 uniform keys over 1M keys, deps = latest 16 txns "
+        return {"workload": f"workload.cfk_update_stream(1M txns x 8 {dist} keys over 1M keys, deps = latest 16 txns "
                             "below on the key, final status at lag 64): one acc_cfk_apply to an empty store",
+                "store_update_ms": round(sum(ms_s[1:]) / calls, 3),
+                "hot_keys": int(cst.get("cfk.hot_keys", 0)), "hot_items": int(cst.get("cfk.hot_items", 0)),
                 "updates": n_upd, "update_key_pairs": n_pairs, "deps": n_deps,
                 "ms_per_call": round(ms, 3), "update_key_pairs_per_s": round(n_pairs / ms * 1e3, 1),
                 "deps_per_s": round(n_deps / ms * 1e3, 1), "apply_regrow_rounds": regrow,

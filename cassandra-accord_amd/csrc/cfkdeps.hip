@@ -569,13 +569,17 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
         if (i > 0 && s.key[i - 1] >= s.key[i]) e |= E_ARG_SORT;
         const uint32_t a = s.ent_off[i], b = s.ent_off[i + 1];
         if (b < a || b > s.n_ent || (i == 0 && a != 0) || (i + 1 == s.n_keys && b != s.n_ent)) e |= E_ARG_OFF;
-        else
-            for (uint32_t j = a; j < b; ++j) {
-                if (s.st[j] > INVALID) e |= E_ARG_STATUS;
-                if (j > a && cmp(Ts{ s.em[j - 1], s.el[j - 1], s.en[j - 1] }, Ts{ s.em[j], s.el[j], s.en[j] }) >= 0) e |= E_ARG_SORT;
-                const uint32_t m0 = s.miss_off[j], m1 = s.miss_off[j + 1];
-                if (m1 < m0 || m1 > s.n_miss) e |= E_ARG_OFF;
-            }
+    }
+    if (i < s.n_ent) {   // a thread per entry (a hot key holds hundreds of thousands); its key by a search of the offsets
+        uint32_t lo = 0, hi = s.n_keys;   // last key whose entries start at or before i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s.ent_off[mid] <= i) lo = mid; else hi = mid;
+        }
+        if (s.st[i] > INVALID) e |= E_ARG_STATUS;
+        if (i > s.ent_off[lo] && cmp(Ts{ s.em[i - 1], s.el[i - 1], s.en[i - 1] }, Ts{ s.em[i], s.el[i], s.en[i] }) >= 0) e |= E_ARG_SORT;
+        const uint32_t m0 = s.miss_off[i], m1 = s.miss_off[i + 1];
+        if (m1 < m0 || m1 > s.n_miss) e |= E_ARG_OFF;
     }
     if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
 }
@@ -907,7 +911,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 }
 
 // ---- hot keys: the replay's closed form, data-parallel over a key's updates
-// A key with more than ACC_CFK_HOT (default 1024) updates in the batch is not replayed by one lane: its final state is
+// A key with more than ACC_CFK_HOT (default 64) updates in the batch is not replayed by one lane: its final state is
 // computed from the update stream directly. Its TxnInfos are every TxnId its snapshot, its updates or their deps name
 // (a dep the key lacks becomes a TRANSITIVELY_KNOWN entry, updateOrInsertWithAdditions :772-863); each takes the status /
 // executeAt of its last update that changed it (update :657-706: stale checks, unchanged returns). The missing[] of an
@@ -922,7 +926,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 // to the txn, depsKnownBefore equal to an entry, two encodings of one TxnId -- mark the key irregular: it is replayed by
 // the lane path instead (which also reports the reference's errors exactly).
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t CH_DEFAULT_HOT = 1024;
+constexpr uint32_t CH_DEFAULT_HOT = 64;
 enum : uint8_t { HI_SNAP = 0, HI_PAIR = 1, HI_TK = 2 };
 enum : uint8_t { HF_CROSSED = 1, HF_NEW = 2 };
 
@@ -1114,12 +1118,21 @@ __global__ __launch_bounds__(BLOCK) void k_ch_uflag(uint32_t ne, const uint32_t 
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
     if (e < ne) uflag[e] = G[eg[e]].st < COMMITTED ? 1u : 0u;
 }
+struct UR {   // an uncommitted entry, as the missing[] walks read it
+    uint64_t m, l;
+    int32_t n;
+    uint32_t flags;
+};
 __global__ __launch_bounds__(BLOCK) void k_ch_ulist(uint32_t ne, uint32_t nh, uint32_t nu, const uint32_t *__restrict__ uflag,
                                                     const uint32_t *__restrict__ uexcl, const uint32_t *__restrict__ eoff,
-                                                    uint32_t *__restrict__ ulist, uint32_t *__restrict__ uoff)
+                                                    const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                    UR *__restrict__ ulist, uint32_t *__restrict__ uoff)
 {
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e < ne && uflag[e]) ulist[uexcl[e]] = e;
+    if (e < ne && uflag[e]) {
+        const HG &g = G[eg[e]];
+        ulist[uexcl[e]] = UR{ g.im, g.il, g.in, g.flags };
+    }
     if (e <= nh) uoff[e] = e == nh ? nu : (eoff[e] < ne ? uexcl[eoff[e]] : nu);
 }
 
@@ -1135,12 +1148,46 @@ __device__ __forceinline__ uint32_t ch_find(const uint32_t *__restrict__ eg, con
     }
     return lo < e1 && cmp(hg_id(G[eg[lo]]), t) == 0 ? lo : NONE;
 }
+// the first entry >= t in [lo, e1): galloping from lo (a sorted run of TxnIds looked up in order moves a few steps)
+__device__ __forceinline__ uint32_t ch_lower(const uint32_t *__restrict__ eg, const HG *__restrict__ G, uint32_t lo, uint32_t e1,
+                                             const Ts &t)
+{
+    uint32_t hi = lo, step = 1;
+    while (hi < e1 && cmp(hg_id(G[eg[hi]]), t) < 0) {
+        lo = hi + 1;
+        hi = lo + step < e1 ? lo + step : e1;
+        step <<= 1;
+    }
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cmp(hg_id(G[eg[mid]]), t) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
 
+// the first entry >= t in [e0, hi]: galloping down from hi (t a little below the entry at hi)
+__device__ __forceinline__ uint32_t ch_lower_back(const uint32_t *__restrict__ eg, const HG *__restrict__ G, uint32_t e0, uint32_t hi,
+                                                  const Ts &t)
+{
+    uint32_t lo = hi, step = 1;   // invariant: entries at and after hi are >= t (or hi is the end)
+    while (lo > e0 && cmp(hg_id(G[eg[lo - 1]]), t) >= 0) {
+        hi = lo - 1;
+        lo = hi - e0 > step ? hi - step : e0;
+        step <<= 1;
+    }
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cmp(hg_id(G[eg[mid]]), t) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
 // every recompute's deps: a dep the key does not hold becomes a TRANSITIVELY_KNOWN item (pass 1 counts, pass 2 writes);
-// the shapes outside the closed form mark the key irregular
+// the shapes outside the closed form mark the key irregular. The lookups start at the txn's own entry (its deps sit
+// just below it, its executeAt just above)
 __global__ __launch_bounds__(BLOCK) void k_ch_mention(uint64_t NI, const uint8_t *__restrict__ mention, const uint32_t *__restrict__ perm,
                                                      HItems it, const UpdRec *__restrict__ urec, Upd u, const uint32_t *__restrict__ eg,
-                                                     const HG *__restrict__ G, const uint32_t *__restrict__ eoff,
+                                                     const HG *__restrict__ G, const uint32_t *__restrict__ gincl,
+                                                     const uint32_t *__restrict__ pexcl, const uint32_t *__restrict__ eoff,
                                                      uint32_t *__restrict__ irr, uint32_t *__restrict__ nextra, uint64_t cap,
                                                      HItems xo)
 {
@@ -1152,13 +1199,22 @@ __global__ __launch_bounds__(BLOCK) void k_ch_mention(uint64_t NI, const uint8_t
     const Ts id{ r.im, r.il, r.in }, ex{ r.xm, r.xl, r.xn };
     const bool self = st == PRE || st == ACC || cmp(ex, id) == 0;
     const Ts bound = self ? id : ex;
-    const uint32_t e0 = eoff[h], e1 = eoff[h + 1];
+    const uint32_t e0 = eoff[h], e1 = eoff[h + 1], own = pexcl[gincl[p] - 1];
     bool bad = false;
-    if (!self && (cmp(ex, id) < 0 || ch_find(eg, G, e0, e1, ex) != NONE)) bad = true;
+    if (!self) {
+        if (cmp(ex, id) < 0) bad = true;
+        else {
+            const uint32_t x = ch_lower(eg, G, own, e1, ex);
+            if (x < e1 && cmp(hg_id(G[eg[x]]), ex) == 0) bad = true;
+        }
+    }
+    // deps are sorted: the first one galloping down from the txn's entry, each next one on from the previous
+    uint32_t at = r.db > r.da && !bad ? ch_lower_back(eg, G, e0, own, Ts{ u.dm[r.da], u.dl[r.da], u.dn[r.da] }) : e0;
     for (uint32_t d = r.da; d < r.db && !bad; ++d) {
         const Ts t{ u.dm[d], u.dl[d], u.dn[d] };
         if (cmp(t, bound) >= 0 || cmp(t, id) == 0) { bad = true; break; }
-        if (ch_find(eg, G, e0, e1, t) != NONE) continue;
+        at = ch_lower(eg, G, at, e1, t);
+        if (at < e1 && cmp(hg_id(G[eg[at]]), t) == 0) { ++at; continue; }
         const uint32_t w = atomicAdd(nextra, 1u);
         if (w < cap) {
             xo.im[w] = t.m; xo.il[w] = t.l; xo.inode[w] = (uint32_t)t.n ^ 0x80000000u;
@@ -1170,7 +1226,7 @@ __global__ __launch_bounds__(BLOCK) void k_ch_mention(uint64_t NI, const uint8_t
 
 // the closed-form missing[] of entry e (count only when out is null)
 __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                               const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                               const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u, Snap s,
                                                uint64_t *om, uint64_t *ol, int32_t *on)
 {
@@ -1182,20 +1238,20 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
     uint32_t lo = u0, hi = u1;   // uncommitted entries below the bound: [u0, ub)
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (cmp(hg_id(G[eg[ulist[mid]]]), bound) < 0) lo = mid + 1; else hi = mid;
+        if (cmp(Ts{ ulist[mid].m, ulist[mid].l, ulist[mid].n }, bound) < 0) lo = mid + 1; else hi = mid;
     }
     const uint32_t ub = lo;
     uint32_t n = 0;
-    auto put = [&](const HG &t) {
-        if (om) { om[n] = t.im; ol[n] = t.il; on[n] = t.in; }
+    auto put = [&](const UR &t) {
+        if (om) { om[n] = t.m; ol[n] = t.l; on[n] = t.n; }
         ++n;
     };
     if (X.info_q != NONE) {   // computed in this batch: the uncommitted entries below the bound, less its deps
         const UpdRec r = urec[X.info_q];
         uint32_t d = r.da;
         for (uint32_t k = u0; k < ub; ++k) {
-            const HG t = G[eg[ulist[k]]];
-            const Ts tid = hg_id(t);
+            const UR t = ulist[k];
+            const Ts tid{ t.m, t.l, t.n };
             if (cmp(tid, id) == 0 || !((wm >> kind(tid)) & 1u)) continue;
             while (d < r.db && cmp(Ts{ u.dm[d], u.dl[d], u.dn[d] }, tid) < 0) ++d;
             if (d < r.db && cmp(Ts{ u.dm[d], u.dl[d], u.dn[d] }, tid) == 0) continue;
@@ -1210,8 +1266,8 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
     uint32_t a = m0, k = u0;
     auto next_new = [&]() {
         while (k < ub) {
-            const HG &t = G[eg[ulist[k]]];
-            const Ts tid = hg_id(t);
+            const UR &t = ulist[k];
+            const Ts tid{ t.m, t.l, t.n };
             if ((t.flags & HF_NEW) && cmp(tid, id) != 0 && ((wm >> kind(tid)) & 1u)) return;
             ++k;
         }
@@ -1229,14 +1285,14 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
         int c;
         if (a == m1) c = 1;
         else if (k == ub) c = -1;
-        else c = cmp(Ts{ s.mm[a], s.ml[a], s.mn[a] }, hg_id(G[eg[ulist[k]]]));
+        else c = cmp(Ts{ s.mm[a], s.ml[a], s.mn[a] }, Ts{ ulist[k].m, ulist[k].l, ulist[k].n });
         if (c <= 0) {
             if (om) { om[n] = s.mm[a]; ol[n] = s.ml[a]; on[n] = s.mn[a]; }
             ++n;
             ++a;
             if (c == 0) ++k;
         } else {
-            put(G[eg[ulist[k]]]);
+            put(ulist[k]);
             ++k;
         }
         next_new();
@@ -1245,7 +1301,7 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
     return n;
 }
 __global__ __launch_bounds__(BLOCK) void k_ch_mcount(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                                     const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                                     const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                      const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
                                                      Snap s, uint32_t *__restrict__ mcnt)
 {
@@ -1253,7 +1309,7 @@ __global__ __launch_bounds__(BLOCK) void k_ch_mcount(uint32_t ne, const uint32_t
     if (e < ne) mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, nullptr, nullptr, nullptr);
 }
 __global__ __launch_bounds__(BLOCK) void k_ch_memit(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                                    const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ulist,
+                                                    const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                     const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
                                                     Snap s, const uint32_t *__restrict__ moff, uint64_t *__restrict__ mm,
                                                     uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
@@ -1285,18 +1341,24 @@ __global__ __launch_bounds__(BLOCK) void k_ch_out3(uint32_t ne, const uint32_t *
     o.st[dst] = X.st;
     o.mcnt[dst] = mcnt[e];
 }
-__global__ __launch_bounds__(BLOCK) void k_ch_out4(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+// a thread per missing[] TxnId (its entry by a search of the offsets): the copies stay coalesced whatever the lengths
+__global__ __launch_bounds__(BLOCK) void k_ch_out4(uint64_t nm, uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
                                                    const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ hk,
                                                    const uint32_t *__restrict__ kpos, const uint32_t *__restrict__ moff,
                                                    const uint64_t *__restrict__ mm, const uint64_t *__restrict__ ml,
                                                    const int32_t *__restrict__ mn, Out o)
 {
-    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= ne) return;
-    const uint32_t h = G[eg[e]].h;
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= nm) return;
+    uint32_t lo = 0, hi = ne;   // last e with moff[e] <= q
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (moff[mid] <= q) lo = mid; else hi = mid;
+    }
+    const uint32_t e = lo, h = G[eg[e]].h;
     const uint32_t pos = o.ent_off[kpos[hk[h]]] + (e - eoff[h]);
-    uint32_t dst = o.miss_off[pos];
-    for (uint32_t q = moff[e]; q < moff[e + 1]; ++q, ++dst) { o.mm[dst] = mm[q]; o.ml[dst] = ml[q]; o.mn[dst] = mn[q]; }
+    const uint32_t dst = o.miss_off[pos] + (uint32_t)(q - moff[e]);
+    o.mm[dst] = mm[q]; o.ml[dst] = ml[q]; o.mn[dst] = mn[q];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_ch_hflag(uint32_t nkeys, const uint8_t *__restrict__ hot, uint32_t *__restrict__ f)
@@ -1402,8 +1464,8 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
         ACC_HIP(hipMemsetAsync(nextra, 0, 4, st));
         HItems none{};
         launch(ctx, "ch_mention", k_ch_mention, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint8_t *)mention,
-               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)eoff, irr, nextra,
-               (uint64_t)0, none);
+               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)gi,
+               (const uint32_t *)px, (const uint32_t *)eoff, irr, nextra, (uint64_t)0, none);
         const uint32_t nx = read32(nextra);
         if (!nx) break;
         if (pass == 1) fail(ACC_E_STATE, "internal: CommandsForKey hot-key additions did not settle");
@@ -1412,8 +1474,8 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
                    ctx->get<uint32_t>("ch_xih", NX), ctx->get<uint32_t>("ch_xisrc", NX), ctx->get<uint8_t>("ch_xikind", NX) };
         ACC_HIP(hipMemsetAsync(nextra, 0, 4, st));
         launch(ctx, "ch_mention", k_ch_mention, dim3(grid_for(NI, BLOCK)), dim3(BLOCK), 0, NI, (const uint8_t *)mention,
-               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)eoff, irr, nextra,
-               NX, xo);
+               (const uint32_t *)so.vals, it, urec, u, (const uint32_t *)eg, (const HG *)G, (const uint32_t *)gi,
+               (const uint32_t *)px, (const uint32_t *)eoff, irr, nextra, NX, xo);
     }
     uint32_t *nirr = ctx->get<uint32_t>("ch_nirr", 1);
     ACC_HIP(hipMemsetAsync(nirr, 0, 4, st));
@@ -1427,19 +1489,20 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     launch(ctx, "ch_uflag", k_ch_uflag, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G, uf);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, uf, ux, ne, true, ux + ne);
     const uint32_t nu = read32(ux + ne);
-    uint32_t *ulist = ctx->get<uint32_t>("ch_ulist", std::max<uint32_t>(nu, 1)), *uoff = ctx->get<uint32_t>("ch_uoff", (size_t)nh + 1);
+    UR *ulist = ctx->get<UR>("ch_ulist", std::max<uint32_t>(nu, 1));
+    uint32_t *uoff = ctx->get<uint32_t>("ch_uoff", (size_t)nh + 1);
     launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nu,
-           (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, ulist, uoff);
+           (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, (const uint32_t *)eg, (const HG *)G, ulist, uoff);
     uint32_t *mcnt = ctx->get<uint32_t>("ch_mcnt", std::max<uint32_t>(ne, 1)), *moff = ctx->get<uint32_t>("ch_moff", (size_t)ne + 1);
     launch(ctx, "ch_mcount", k_ch_mcount, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-           (const uint32_t *)eoff, (const uint32_t *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt);
+           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, mcnt, moff, ne, true, moff + ne);
     const uint64_t nm = read32(moff + ne);
     uint64_t *mm = ctx->get<uint64_t>("ch_mm", nm), *ml = ctx->get<uint64_t>("ch_ml", nm);
     int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
     if (nm)
         launch(ctx, "ch_memit", k_ch_memit, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-               (const uint32_t *)eoff, (const uint32_t *)ulist, (const uint32_t *)uoff, urec, u, s, (const uint32_t *)moff, mm, ml, mn);
+               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, (const uint32_t *)moff, mm, ml, mn);
     ctx->stat("cfk.hot_keys", nh);
     ctx->stat("cfk.hot_items", NI);
     ho.nh = nh; ho.ne = ne; ho.nm = nm;
@@ -1490,12 +1553,18 @@ __global__ __launch_bounds__(BLOCK) void k_cb_first(uint64_t NE, const uint64_t 
     b.ko[t] = qpos[e];
     if (t + 1 == n) b.ko[n] = (uint32_t)NE;
 }
-// owner key of every entry (a lane per key)
-__global__ __launch_bounds__(BLOCK) void k_cb_owner(uint32_t nk, const uint32_t *__restrict__ ent_off, uint32_t *__restrict__ owner)
+// owner key of every entry (the last key whose entries start at or before it)
+__global__ __launch_bounds__(BLOCK) void k_cb_owner(uint64_t NE, uint32_t nk, const uint32_t *__restrict__ ent_off,
+                                                    uint32_t *__restrict__ owner)
 {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nk) return;
-    for (uint32_t e = ent_off[k], e1 = ent_off[k + 1]; e < e1; ++e) owner[e] = k;
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= NE) return;
+    uint32_t lo = 0, hi = nk;   // first k with ent_off[k + 1] > e
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ent_off[mid + 1] > e) hi = mid; else lo = mid + 1;
+    }
+    owner[e] = lo;
 }
 // per entry, in entry order (its columns read contiguously): its key code and missing count at its sorted position,
 // and the check that it carries its TxnId's executeAt and InternalStatus (a TxnId twice on one key is already refused
@@ -1513,31 +1582,62 @@ __global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, const uint32_t *_
     if (s.st[e] != c.st || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ c.xm, c.xl, c.xn }) != 0)
         atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
 }
-// each pair's missing[] TxnIds as batch indices (binary search over the batch's TxnIds)
+// each pair's missing[] TxnIds as batch indices (binary search over the batch's TxnIds), each result checked against the
+// one before it (sorted unique). A pair with a short missing[] is its lane's; the long ones (a hot key's entries carry
+// thousands) are taken by the whole wave one after another, its lanes splitting the searches
+constexpr uint32_t CB_LONG = 32;
+__device__ __forceinline__ uint32_t cb_find(const BatchOut &b, uint32_t n, const Ts &k, uint64_t &bad)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cmp(Ts{ b.tm[mid], b.tl[mid], b.tn[mid] }, k) < 0) lo = mid + 1; else hi = mid;
+    }
+    if (lo == n || cmp(Ts{ b.tm[lo], b.tl[lo], b.tn[lo] }, k) != 0) {
+        bad |= E_STATE;
+        lo = 0;
+    }
+    return lo;
+}
 __global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
                                                    const uint64_t *__restrict__ ntxn, BatchOut b,
                                                    const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
                                                    uint64_t *__restrict__ err)
 {
     const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= NE) return;
-    const uint32_t e = perm[i], n = (uint32_t)*ntxn;
-    const uint32_t m0 = s.miss_off[e], m1 = s.miss_off[e + 1];
-    uint32_t w = mo[i];
-    for (uint32_t j = m0; j < m1; ++j) {
-        const Ts k{ s.mm[j], s.ml[j], s.mn[j] };
-        uint32_t lo = 0, hi = n;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (cmp(Ts{ b.tm[mid], b.tl[mid], b.tn[mid] }, k) < 0) lo = mid + 1; else hi = mid;
-        }
-        if (lo == n || cmp(Ts{ b.tm[lo], b.tl[lo], b.tn[lo] }, k) != 0) {
-            atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
-            lo = 0;
-        }
-        if (j > m0 && lo <= mt[w - 1]) atomicOr((unsigned long long *)err, (unsigned long long)E_ARG_SORT);
-        mt[w++] = lo;
+    const uint32_t lane = lane_id(), n = (uint32_t)*ntxn;
+    uint64_t bad = 0;
+    uint32_t m0 = 0, m1 = 0, w0 = 0;
+    if (i < NE) {
+        const uint32_t e = perm[i];
+        m0 = s.miss_off[e]; m1 = s.miss_off[e + 1]; w0 = mo[i];
     }
+    const bool lng = m1 - m0 >= CB_LONG;
+    if (!lng) {
+        uint32_t prev = 0;
+        for (uint32_t j = m0; j < m1; ++j) {
+            const uint32_t lo = cb_find(b, n, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad);
+            if (j > m0 && lo <= prev) bad |= E_ARG_SORT;
+            mt[w0 + (j - m0)] = lo;
+            prev = lo;
+        }
+    }
+    for (uint64_t todo = __ballot(lng); todo; todo &= todo - 1) {
+        const int src = __builtin_ctzll(todo);
+        const uint32_t a = __shfl(m0, src, 64), z = __shfl(m1, src, 64), w = __shfl(w0, src, 64);
+        uint32_t carry = 0;
+        for (uint32_t base = a; base < z; base += 64) {
+            const uint32_t j = base + lane;
+            const bool valid = j < z;
+            const uint32_t lo = valid ? cb_find(b, n, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad) : 0u;
+            uint32_t prev = __shfl_up(lo, 1, 64);
+            if (lane == 0) prev = carry;
+            if (valid && j > a && lo <= prev) bad |= E_ARG_SORT;
+            if (valid) mt[w + (j - a)] = lo;
+            carry = __shfl(lo, 63, 64);
+        }
+    }
+    if (bad) atomicOr((unsigned long long *)err, (unsigned long long)bad);
 }
 
 }  // namespace cd
@@ -1585,7 +1685,8 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
     } else {
         if (!trusted) {   // (acc_cfk_apply_deps hands over acc_cfk_apply's own output: already in this form)
             Upd none{};
-            launch(ctx, "cb_check", k_cd_check, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, s, none, (uint32_t *)nullptr, errs,
+            launch(ctx, "cb_check", k_cd_check, dim3(grid_for(std::max<uint64_t>(nk, NE), BLOCK)), dim3(BLOCK), 0, s, none,
+                   (uint32_t *)nullptr, errs,
                    (uint64_t *)nullptr);
             ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
             ctx->sync();
@@ -1614,7 +1715,7 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         launch(ctx, "cb_first", k_cb_first, g, dim3(BLOCK), 0, NE, (const uint64_t *)dr.count_dev, (const uint32_t *)dr.first,
                (const uint32_t *)qpos, s, b, chk);
         uint32_t *owner = ctx->get<uint32_t>("cb_owner", NE);
-        launch(ctx, "cb_owner", k_cb_owner, dim3(grid_for(nk, BLOCK)), dim3(BLOCK), 0, nk, s.ent_off, owner);
+        launch(ctx, "cb_owner", k_cb_owner, g, dim3(BLOCK), 0, NE, nk, s.ent_off, owner);
         launch(ctx, "cb_ent", k_cb_ent, g, dim3(BLOCK), 0, NE, (const uint32_t *)owner, (const uint32_t *)dr.rank, (const uint32_t *)qpos, s, (const TxnChk *)chk, b, errs);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, b.mcnt, mo, NE, true, mo + NE);
         if (NM)
@@ -1687,7 +1788,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     u.owner = owner;
     uint64_t *errs = ctx->get<uint64_t>("cd_errs", 1);
     ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
-    const uint64_t gmax = std::max<uint64_t>({ (uint64_t)nk, (uint64_t)nu, NP, 1 });
+    const uint64_t gmax = std::max<uint64_t>({ (uint64_t)nk, (uint64_t)nu, NP, NE, 1 });
     uint64_t *krng = ctx->get<uint64_t>("cd_krng", 2);
     ACC_HIP(hipMemsetAsync(krng, 0xFF, 8, st));
     ACC_HIP(hipMemsetAsync(krng + 1, 0, 8, st));
@@ -1867,7 +1968,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
                (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
                (const uint8_t *)hot);
         if (ho.nm)
-            launch(ctx, "ch_out4", k_ch_out4, dim3(grid_for(ho.ne, BLOCK)), dim3(BLOCK), 0, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
+            launch(ctx, "ch_out4", k_ch_out4, dim3(grid_for(ho.nm, BLOCK)), dim3(BLOCK), 0, ho.nm, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
                    (const uint32_t *)kpos, ho.moff, ho.mm, ho.ml, ho.mn, o);
     }
     ctx->sync();

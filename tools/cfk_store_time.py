@@ -16,7 +16,8 @@ from accord_amd import _lib as L  # noqa: E402
 from accord_amd import workload as W  # noqa: E402
 from accord_amd.deps import Context  # noqa: E402
 
-u = W.cfk_update_stream(1_000_000)
+DIST = os.environ.get("CFK_DIST", "uniform")   # "zipf": the config-2-shaped zipf(0.99) stream (hot keys)
+u = W.cfk_update_stream(1_000_000, dist=DIST)
 dev = torch.device("cuda", 0)
 d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in u.items()}
 ptr = lambda k: d[k].data_ptr()  # noqa: E731
@@ -43,7 +44,7 @@ with Context(0) as c:
         torch.cuda.synchronize()
         res.setdefault("keydeps_on_store_ms", []).append(round((time.perf_counter() - t0) * 1e3, 2))
         c._lib.acc_cfk_destroy(h)
-    print({"updates": len(u["msb"]), "pairs": len(u["key"]), "deps": len(u["dmsb"]), "store_txns": int(v.n_txn),
+    print({"dist": DIST, "updates": len(u["msb"]), "pairs": len(u["key"]), "deps": len(u["dmsb"]), "store_txns": int(v.n_txn),
            "store_pairs": int(v.n_pairs), **res})
 with Context(0, timing=True) as c:   # one more store update with every kernel timed: where its time goes
     h = C.c_void_p()
@@ -58,5 +59,5 @@ with Context(0, timing=True) as c:   # one more store update with every kernel t
     t = c.timing()
     top = sorted(t.items(), key=lambda kv: -kv[1][0])[:14]
     print("store update kernels (ms):", {k: round(v[0], 3) for k, v in top}, "sum", round(sum(v[0] for v in t.values()), 3))
-    print("paths:", {k: v for k, v in c.stats().items() if k.startswith("cfk.apply")})
+    print("paths:", {k: v for k, v in c.stats().items() if k.startswith("cfk.")})
     c._lib.acc_cfk_destroy(h)
