@@ -1300,22 +1300,78 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
     }
     return n;
 }
-__global__ __launch_bounds__(BLOCK) void k_ch_mcount(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                                     const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
-                                                     const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
-                                                     Snap s, uint32_t *__restrict__ mcnt)
+// count (EMIT false) or write the missing[] of every entry. An entry computed in this batch whose uncommitted range is
+// long (a hot key's late entries: thousands) is walked by the whole wave, lanes side by side over the range (a ballot
+// compacts the kept TxnIds, deps looked up by search); the others by their own lane
+constexpr uint32_t CH_LONG = 32;
+template <bool EMIT>
+__global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
+                                                   const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
+                                                   const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
+                                                   Snap s, uint32_t *__restrict__ mcnt, const uint32_t *__restrict__ moff,
+                                                   uint64_t *__restrict__ mm, uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
 {
-    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e < ne) mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, nullptr, nullptr, nullptr);
-}
-__global__ __launch_bounds__(BLOCK) void k_ch_memit(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                                    const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
-                                                    const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
-                                                    Snap s, const uint32_t *__restrict__ moff, uint64_t *__restrict__ mm,
-                                                    uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
-{
-    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e < ne) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, mm + moff[e], ml + moff[e], mn + moff[e]);
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x, lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    bool lng = false;
+    uint32_t u0 = 0, ub = 0, da = 0, db = 0, wm = 0, out = 0;
+    Ts id{ 0, 0, 0 };
+    if (e < ne) {
+        const HG X = G[eg[e]];
+        if (has_info(X.st) && X.info_q != NONE) {
+            id = hg_id(X);
+            const Ts bound = hg_bound(X);
+            u0 = uoff[X.h];
+            uint32_t lo = u0, hi = uoff[X.h + 1];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (cmp(Ts{ ulist[mid].m, ulist[mid].l, ulist[mid].n }, bound) < 0) lo = mid + 1; else hi = mid;
+            }
+            ub = lo;
+            lng = ub - u0 >= CH_LONG;
+            const UpdRec r = urec[X.info_q];
+            da = r.da; db = r.db;
+            wm = witnesses_mask(kind(id));
+            if (EMIT) out = moff[e];
+        }
+        if (!lng) {
+            if (EMIT) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, mm + moff[e], ml + moff[e], mn + moff[e]);
+            else mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, nullptr, nullptr, nullptr);
+        }
+    }
+    for (uint64_t todo = __ballot(lng); todo; todo &= todo - 1) {
+        const int src = __builtin_ctzll(todo);
+        const uint32_t a = __shfl(u0, src, 64), z = __shfl(ub, src, 64), d0 = __shfl(da, src, 64), d1 = __shfl(db, src, 64);
+        const uint32_t w = __shfl(wm, src, 64), o0 = __shfl(out, src, 64);
+        const Ts x{ (uint64_t)__shfl((unsigned long long)id.m, src, 64), (uint64_t)__shfl((unsigned long long)id.l, src, 64),
+                    __shfl(id.n, src, 64) };
+        uint32_t n = 0;
+        for (uint32_t base = a; base < z; base += 64) {
+            const uint32_t k = base + lane;
+            bool keep = false;
+            UR t{};
+            if (k < z) {
+                t = ulist[k];
+                const Ts tid{ t.m, t.l, t.n };
+                keep = cmp(tid, x) != 0 && ((w >> kind(tid)) & 1u);
+                if (keep) {   // not among the deps (sorted)
+                    uint32_t lo = d0, hi = d1;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (cmp(Ts{ u.dm[mid], u.dl[mid], u.dn[mid] }, tid) < 0) lo = mid + 1; else hi = mid;
+                    }
+                    if (lo < d1 && cmp(Ts{ u.dm[lo], u.dl[lo], u.dn[lo] }, tid) == 0) keep = false;
+                }
+            }
+            const uint64_t kb = __ballot(keep);
+            if (EMIT && keep) {
+                const uint32_t q = o0 + n + (uint32_t)__popcll(kb & lt);
+                mm[q] = t.m; ml[q] = t.l; mn[q] = t.n;
+            }
+            n += (uint32_t)__popcll(kb);
+        }
+        if (!EMIT && lane == (uint32_t)src) mcnt[e] = n;
+    }
 }
 // the hot keys' final entry counts (the lane path's fin_n), and the irregular ones back to the lane path
 __global__ __launch_bounds__(BLOCK) void k_ch_fin(uint32_t nh, const uint32_t *__restrict__ hk, const uint32_t *__restrict__ eoff,
@@ -1494,15 +1550,17 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nu,
            (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, (const uint32_t *)eg, (const HG *)G, ulist, uoff);
     uint32_t *mcnt = ctx->get<uint32_t>("ch_mcnt", std::max<uint32_t>(ne, 1)), *moff = ctx->get<uint32_t>("ch_moff", (size_t)ne + 1);
-    launch(ctx, "ch_mcount", k_ch_mcount, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt);
+    launch(ctx, "ch_mcount", k_ch_miss<false>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
+           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt, (const uint32_t *)nullptr,
+           (uint64_t *)nullptr, (uint64_t *)nullptr, (int32_t *)nullptr);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, mcnt, moff, ne, true, moff + ne);
     const uint64_t nm = read32(moff + ne);
     uint64_t *mm = ctx->get<uint64_t>("ch_mm", nm), *ml = ctx->get<uint64_t>("ch_ml", nm);
     int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
     if (nm)
-        launch(ctx, "ch_memit", k_ch_memit, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, (const uint32_t *)moff, mm, ml, mn);
+        launch(ctx, "ch_memit", k_ch_miss<true>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
+               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, (uint32_t *)nullptr,
+               (const uint32_t *)moff, mm, ml, mn);
     ctx->stat("cfk.hot_keys", nh);
     ctx->stat("cfk.hot_items", NI);
     ho.nh = nh; ho.ne = ne; ho.nm = nm;
