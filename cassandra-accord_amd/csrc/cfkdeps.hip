@@ -18,6 +18,8 @@
 //      not the quadratic bound; from the third round on a flagged key takes the bound at once, so a batch replays at
 //      most four times (every key replays: the pool's layout moves when the flagged keys grow);
 //   4. final sizes, two scans, and a compaction into the key-major output (keys without entries dropped).
+// Keys with more than ACC_CFK_HOT (64) sorted elements skip step 3: their final state is the replay's closed form,
+// computed data-parallel over the key's updates (the hot-key section below).
 // Errors: a status going back (IllegalStateException "stale status", ACC_E_STATE), an addition equal to an existing
 // TxnId or depsKnownBefore equal to a TxnId (the reference's checkState, ACC_E_STATE), malformed input (ACC_E_ARG).
 #include "dict.hpp"
