@@ -563,9 +563,17 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
     if (i < u.NP) {
         const uint32_t a = u.dep_off[i], b = u.dep_off[i + 1];
         if (b < a || b > u.ND || (i == 0 && a != 0) || (i + 1 == u.NP && b != u.ND)) e |= E_ARG_OFF;
-        else
-            for (uint32_t j = a + 1; j < b; ++j)
-                if (cmp(Ts{ u.dm[j - 1], u.dl[j - 1], u.dn[j - 1] }, Ts{ u.dm[j], u.dl[j], u.dn[j] }) >= 0) { e |= E_ARG_SORT; break; }
+        else if (b > a) {   // strictly ascending; the lsb / node words read only where two msb words tie
+            uint64_t pm = u.dm[a];
+            for (uint32_t j = a + 1; j < b; ++j) {
+                const uint64_t m = u.dm[j];
+                if (m < pm || (m == pm && cmp(Ts{ pm, u.dl[j - 1], u.dn[j - 1] }, Ts{ m, u.dl[j], u.dn[j] }) >= 0)) {
+                    e |= E_ARG_SORT;
+                    break;
+                }
+                pm = m;
+            }
+        }
     }
     if (i < s.n_keys) {
         if (i > 0 && s.key[i - 1] >= s.key[i]) e |= E_ARG_SORT;
@@ -791,10 +799,11 @@ uint32_t nkeys, const uint32_t *__restrict__ kstart,
     A.n = 0; A.mtop = 0;
     Ctx::Sum sm{};
     bool sum_ok = false;
-    const uint32_t q0 = kstart[k], q1 = kstart[k + 1];
-    for (uint32_t q = q0; q < q1 && !c.err; ++q) {
-        const uint32_t v = src[q];
-        if (v < nk) {   // the snapshot of this key
+    uint32_t q0 = kstart[k];
+    const uint32_t q1 = kstart[k + 1];
+    if (const uint32_t v = src[q0]; v < nk) {   // the snapshot of this key: the first element of its run
+        ++q0;
+        {
             for (uint32_t x = s.ent_off[v]; x < s.ent_off[v + 1]; ++x) {
                 Info y;
                 y.id = Ts{ s.em[x], s.el[x], s.en[x] };
@@ -812,8 +821,9 @@ uint32_t nkeys, const uint32_t *__restrict__ kstart,
                 A.mtop += y.mn;
                 c.put_e(A, y);
             }
-            continue;
         }
+    }
+    for (uint32_t q = q0; q < q1 && !c.err; ++q) {   // then its updates (one record each)
         const UpdRec ur = urec[q];
         const uint32_t st = ur.st_fl & 0xFFu, fl = ur.st_fl >> 8;
         if (st == 0xFF) continue;   // InternalStatus.from(saveStatus) == null: unchanged
