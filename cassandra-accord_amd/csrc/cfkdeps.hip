@@ -702,6 +702,12 @@ __device__ __forceinline__ void key_bufs(const Pool &p, uint32_t k, Work &w)
     w.b.m = w.a.m + (long)mc;
 }
 
+// slots in descending capacity: the waves with the longest replays start first (the short ones fill in behind them)
+__global__ __launch_bounds__(BLOCK) void k_cd_rev(uint32_t nkeys, const uint32_t *__restrict__ in, uint32_t *__restrict__ out)
+{
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k < nkeys) out[k] = in[nkeys - 1 - k];
+}
 // per wave of 64 keys: the largest capacities of its keys and the wave's per-lane region sizes
 __global__ __launch_bounds__(BLOCK) void k_cd_wcap(uint32_t nkeys, const uint32_t *__restrict__ perm, uint32_t *__restrict__ kslot,
                                                    const uint64_t *__restrict__ ecap,
@@ -1949,7 +1955,15 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, nhot, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
         const uint32_t nh = (uint32_t)ctx->pinned[1];
-        perm = radix_sort(ctx, "cd_rs_cap", ecap, nullptr, nkeys, std::max(1, bits_for(ctx->pinned[0]))).vals;
+        {
+            const uint32_t *asc = radix_sort(ctx, "cd_rs_cap", ecap, nullptr, nkeys, std::max(1, bits_for(ctx->pinned[0]))).vals;
+            uint32_t *desc = ctx->get<uint32_t>("cd_perm_desc", nkeys);
+            if (getenv("ACC_CD_ASC")) perm = asc;   // tuning switch: ascending capacity
+            else {
+                launch(ctx, "cd_rev", k_cd_rev, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, asc, desc);
+                perm = desc;
+            }
+        }
         wave_layout();
         // the hot keys' final states; keys found irregular go back to the lane path (layout again)
         if (!nh || hot_keys(ctx, nkeys, hot, kstart, so.vals, nk, s, u, urec, fin_n, errs, ho)) break;
