@@ -25,6 +25,9 @@ struct acc_cfk {
         uint8_t *status = nullptr;
         uint32_t *key_off = nullptr;
         size_t cap_n = 0, cap_p = 0;
+        // byte sizes of the arrays above in declaration order (tm tl em el key_code tn en status key_off): they differ
+        // once acc_cfk_apply_deps has adopted a call's result arrays
+        size_t bytes[9] = {};
     } set[2];
     int cur = 0;
     // acc_cfk_apply_deps: the same store with every TxnInfo's missing[] — the key-major CommandsForKey state (what
@@ -39,11 +42,12 @@ struct acc_cfk {
         int32_t *en = nullptr, *xn = nullptr, *mn = nullptr;
         uint8_t *st = nullptr;
         uint32_t *ent_off = nullptr, *miss_off = nullptr;
-        size_t cap_k = 0, cap_e = 0, cap_m = 0;
+        // byte sizes (key ent_off em el en xm xl xn st miss_off mm ml mn): adopted result arrays (acc_cfk_apply_deps)
+        size_t bytes[13] = {};
     } km;
     uint32_t *bmiss_off = nullptr, *bmiss_txn = nullptr;   // [P + 1], [bnm]
     uint64_t bnm = 0;
-    size_t cap_bmo = 0, cap_bmt = 0;
+    size_t bytes_bmo = 0, bytes_bmt = 0;
 };
 
 namespace acc {
@@ -263,11 +267,15 @@ void reserve(acc_cfk::Set &s, size_t n, size_t P)
         realloc_dev(s.tm, c); realloc_dev(s.tl, c); realloc_dev(s.em, c); realloc_dev(s.el, c);
         realloc_dev(s.tn, c); realloc_dev(s.en, c); realloc_dev(s.status, c); realloc_dev(s.key_off, c);
         s.cap_n = c;
+        s.bytes[0] = s.bytes[1] = s.bytes[2] = s.bytes[3] = c * 8;
+        s.bytes[5] = s.bytes[6] = s.bytes[8] = c * 4;
+        s.bytes[7] = c;
     }
     if (P + 1 > s.cap_p) {
         const size_t c = P + P / 4 + 64;
         realloc_dev(s.key_code, c);
         s.cap_p = c;
+        s.bytes[4] = c * 8;
     }
 }
 
@@ -391,21 +399,6 @@ void cfk_view(acc_cfk *cfk, acc_batch_in *out);
 
 namespace {
 
-template <class T>
-void grow_dev(T *&p, size_t &cap, size_t count)   // capacity for count elements (at least 1); contents not kept
-{
-    if (count + 1 <= cap && p) return;
-    const size_t c = count + count / 4 + 64;
-    realloc_dev(p, c);
-    cap = c;
-}
-
-template <class T>
-void copy_dev(acc_ctx *ctx, T *dst, const T *src, size_t count)
-{
-    if (count) ACC_HIP(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
-}
-
 acc_cfk_snap km_snap(acc_cfk *cfk)
 {
     const acc_cfk::KeyMajor &k = cfk->km;
@@ -426,9 +419,10 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     if (!cfk->deps && cfk->n)
         fail(ACC_E_STATE, "the store holds status-only state (acc_cfk_update): missing[] is maintained from an empty store");
     acc_cfk::KeyMajor &k = cfk->km;
-    if (!k.ent_off) {   // empty state: offsets [0] (the grown arrays are reallocated below, ent_off / miss_off first)
+    if (!k.ent_off) {   // empty state: offsets [0]
         realloc_dev(k.ent_off, 1);
         realloc_dev(k.miss_off, 1);
+        k.bytes[1] = k.bytes[9] = 4;
         ACC_HIP(hipMemsetAsync(k.ent_off, 0, 4, ctx->stream));
         ACC_HIP(hipMemsetAsync(k.miss_off, 0, 4, ctx->stream));
     }
@@ -439,49 +433,37 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
                              v.status, v.miss_off, v.missing };
     acc_cfk_batch_view bv{};
     cfk_snap_to_batch(ctx, &next, &bv, true);
-    // ---- both results in the store
+    // ---- both results become the store's arrays: the context's result buffers and the store's previous arrays trade
+    // places (no copies; the context writes its next results into the old arrays)
+    auto adopt = [&](const char *name, auto *&p, size_t &bytes) {
+        void *v = p;
+        ctx->swap_buf(name, v, bytes);
+        p = static_cast<std::remove_reference_t<decltype(p)>>(v);
+    };
     const uint32_t nk = v.n_keys;
     const uint64_t ne = v.n_entries, nm = v.n_missing;
-    auto cap_for = [](size_t need) { return need + need / 4 + 64; };
-    if (nk + 1 > k.cap_k || !k.key) {
-        const size_t c = cap_for((size_t)nk + 1);
-        realloc_dev(k.key, c); realloc_dev(k.ent_off, c);
-        k.cap_k = c;
-    }
-    if (ne + 1 > k.cap_e || !k.em) {
-        const size_t c = cap_for(ne + 1);
-        realloc_dev(k.em, c); realloc_dev(k.el, c); realloc_dev(k.en, c); realloc_dev(k.xm, c); realloc_dev(k.xl, c);
-        realloc_dev(k.xn, c); realloc_dev(k.st, c); realloc_dev(k.miss_off, c);
-        k.cap_e = c;
-    }
-    if (nm + 1 > k.cap_m || !k.mm) {
-        const size_t c = cap_for(nm + 1);
-        realloc_dev(k.mm, c); realloc_dev(k.ml, c); realloc_dev(k.mn, c);
-        k.cap_m = c;
-    }
-    copy_dev(ctx, k.key, v.key, nk);
-    copy_dev(ctx, k.ent_off, v.ent_off, (size_t)nk + 1);
-    copy_dev(ctx, k.em, v.txn_id.msb, ne); copy_dev(ctx, k.el, v.txn_id.lsb, ne); copy_dev(ctx, k.en, v.txn_id.node, ne);
-    copy_dev(ctx, k.xm, v.execute_at.msb, ne); copy_dev(ctx, k.xl, v.execute_at.lsb, ne);
-    copy_dev(ctx, k.xn, v.execute_at.node, ne);
-    copy_dev(ctx, k.st, v.status, ne);
-    copy_dev(ctx, k.miss_off, v.miss_off, ne + 1);
-    copy_dev(ctx, k.mm, v.missing.msb, nm); copy_dev(ctx, k.ml, v.missing.lsb, nm); copy_dev(ctx, k.mn, v.missing.node, nm);
+    size_t *kb = k.bytes;
+    adopt("cd_okey", k.key, kb[0]); adopt("cd_oent_off", k.ent_off, kb[1]);
+    adopt("cd_oem", k.em, kb[2]); adopt("cd_oel", k.el, kb[3]); adopt("cd_oen", k.en, kb[4]);
+    adopt("cd_oxm", k.xm, kb[5]); adopt("cd_oxl", k.xl, kb[6]); adopt("cd_oxn", k.xn, kb[7]);
+    adopt("cd_ost", k.st, kb[8]); adopt("cd_omoff", k.miss_off, kb[9]);
+    adopt("cd_omm", k.mm, kb[10]); adopt("cd_oml", k.ml, kb[11]); adopt("cd_omn", k.mn, kb[12]);
+    if (k.key != v.key || k.em != v.txn_id.msb || k.mm != v.missing.msb || k.miss_off != v.miss_off)
+        fail(ACC_E_STATE, "internal: CommandsForKey result buffers moved");
     k.nk = nk; k.ne = ne; k.nm = nm;
     const acc_batch_in &b = bv.batch;
     const uint32_t n = b.n_txn;
     const uint64_t P = b.n_pairs;
     acc_cfk::Set &S = cfk->set[cfk->cur];
-    reserve(S, n, P);
-    copy_dev(ctx, S.tm, b.txn_id.msb, n); copy_dev(ctx, S.tl, b.txn_id.lsb, n); copy_dev(ctx, S.tn, b.txn_id.node, n);
-    copy_dev(ctx, S.em, b.execute_at.msb, n); copy_dev(ctx, S.el, b.execute_at.lsb, n); copy_dev(ctx, S.en, b.execute_at.node, n);
-    copy_dev(ctx, S.status, b.status, n);
-    copy_dev(ctx, S.key_off, b.key_off, (size_t)n + 1);
-    copy_dev(ctx, S.key_code, b.key_code, P);
-    grow_dev(cfk->bmiss_off, cfk->cap_bmo, P + 1);
-    grow_dev(cfk->bmiss_txn, cfk->cap_bmt, bv.n_missing + 1);
-    copy_dev(ctx, cfk->bmiss_off, bv.missing_off, P + 1);
-    copy_dev(ctx, cfk->bmiss_txn, bv.missing_txn, bv.n_missing);
+    size_t *sb = S.bytes;
+    adopt("cb_tm", S.tm, sb[0]); adopt("cb_tl", S.tl, sb[1]); adopt("cb_xm", S.em, sb[2]); adopt("cb_xl", S.el, sb[3]);
+    adopt("cb_kc", S.key_code, sb[4]); adopt("cb_tn", S.tn, sb[5]); adopt("cb_xn", S.en, sb[6]);
+    adopt("cb_st", S.status, sb[7]); adopt("cb_ko", S.key_off, sb[8]);
+    S.cap_n = S.cap_p = 0;   // (sizes now per array: a status-only reserve would reallocate; deps mode refuses it)
+    adopt("cb_mo", cfk->bmiss_off, cfk->bytes_bmo);
+    adopt("cb_mt", cfk->bmiss_txn, cfk->bytes_bmt);
+    if (S.tm != b.txn_id.msb || S.key_off != b.key_off || cfk->bmiss_off != bv.missing_off)
+        fail(ACC_E_STATE, "internal: CommandsForKey view buffers moved");
     cfk->bnm = bv.n_missing;
     ctx->sync();
     cfk->n = n;

@@ -864,15 +864,17 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out1(uint32_t nkeys, const uint32_
     if (k < nkeys) keep[k] = fin_n[k] ? 1u : 0u;
 }
 
+// the kept keys' codes and entry offsets (eall: exclusive scan of the entry counts over every key)
 __global__ __launch_bounds__(BLOCK) void k_cd_out2(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
                                                    const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ sk,
-                                                   uint64_t kbase, const uint32_t *__restrict__ fin_n, uint64_t *__restrict__ okey,
-                                                   uint32_t *__restrict__ ocnt)
+                                                   uint64_t kbase, const uint32_t *__restrict__ eall, uint64_t *__restrict__ okey,
+                                                   uint32_t *__restrict__ ent_off, uint32_t nko, uint32_t ne)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k == 0) ent_off[nko] = ne;
     if (k >= nkeys || !keep[k]) return;
     okey[kpos[k]] = sk[kstart[k]] + kbase;
-    ocnt[kpos[k]] = fin_n[k];
+    ent_off[kpos[k]] = eall[k];
 }
 
 struct Out {
@@ -1973,6 +1975,11 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     // ---- 3. replay, again with grown missing areas while some key outgrows its guess
     Pool p{};
     uint32_t regrow = 0;
+    // the kept keys and the output entry offsets, scanned right after each replay (one host sync for both)
+    uint32_t *keep = ctx->get<uint32_t>("cd_keep", nkeys), *kpos = ctx->get<uint32_t>("cd_kpos", (size_t)nkeys + 1);
+    uint32_t *eall = ctx->get<uint32_t>("cd_eall", (size_t)nkeys + 1);
+    uint32_t nko = 0;
+    uint64_t NEo = 0, NMo = 0;
     for (;; ++regrow) {
         const uint64_t pool_bytes = (uint64_t)CD_W * (Ew * sizeof(InfoP) + Tw * sizeof(Ts));
         if (pool_bytes > (64ull << 30)) fail(ACC_E_CAP, "CommandsForKey working space beyond 64 GiB for this batch");
@@ -1984,13 +1991,24 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         launch(ctx, "cd_apply", k_cd_apply, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
                (const uint32_t *)so.vals, (const uint64_t *)ecap, (const uint64_t *)mcap, nk, s, u, p, final_b, fin_n, fin_m,
                ovf, errs, paths, (const UpdRec *)urec, (const uint8_t *)hot);
+        launch(ctx, "cd_out1", k_cd_out1, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)fin_n, keep);
+        {
+            const uint32_t *si[2] = { keep, fin_n };
+            uint32_t *so2[2] = { kpos, eall }, *stot[2] = { kpos + nkeys, eall + nkeys };
+            const size_t sn[2] = { nkeys, nkeys };
+            scan_multi<uint32_t, OpAdd<uint32_t>>(ctx, 2, si, so2, sn, true, stot);
+        }
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, paths, 16, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, kpos + nkeys, 4, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + 4, eall + nkeys, 4, hipMemcpyDeviceToHost, st));
         ctx->sync();
         ctx->stat("cfk.apply_in_place", ctx->pinned[1]);
         ctx->stat("cfk.apply_rebuilt", ctx->pinned[2]);
         const uint64_t e = ctx->pinned[0];
         check(e & ~E_MCAP);
+        nko = (uint32_t)ctx->pinned[3];
+        NEo = (uint32_t)ctx->pinned[4];
         if (!(e & E_MCAP)) break;
         ACC_HIP(hipMemsetAsync(errs, 0, 8, st));
         launch(ctx, "cd_grow", k_cd_grow, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, ovf, mcap,
@@ -2002,27 +2020,13 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     }
     ctx->stat("cfk.apply_regrow", regrow);
     // ---- 4. key-major output
-    uint32_t *keep = ctx->get<uint32_t>("cd_keep", nkeys), *kpos = ctx->get<uint32_t>("cd_kpos", (size_t)nkeys + 1);
-    uint32_t nko = 0;
-    if (nkeys) {
-        launch(ctx, "cd_out1", k_cd_out1, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)fin_n, keep);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, keep, kpos, nkeys, true, kpos + nkeys);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, kpos + nkeys, 4, hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        nko = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
-    }
     uint64_t *okey = ctx->get<uint64_t>("cd_okey", nko);
-    uint32_t *ocnt = ctx->get<uint32_t>("cd_ocnt", nko);
     Out o{};
     o.ent_off = ctx->get<uint32_t>("cd_oent_off", (size_t)nko + 1);
-    uint64_t NEo = 0, NMo = 0;
     if (nko) {
         launch(ctx, "cd_out2", k_cd_out2, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-               (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, kbase, (const uint32_t *)fin_n, okey, ocnt);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, ocnt, o.ent_off, nko, true, o.ent_off + nko);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, o.ent_off + nko, 4, hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        NEo = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+               (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, kbase, (const uint32_t *)eall, okey,
+               o.ent_off, nko, (uint32_t)NEo);
     } else {
         ACC_HIP(hipMemsetAsync(o.ent_off, 0, 4, st));
     }

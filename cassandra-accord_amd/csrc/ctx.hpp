@@ -141,6 +141,16 @@ struct acc_ctx {
         return static_cast<T *>(b.ptr);
     }
 
+    // Exchange the named buffer with (ptr, bytes): the caller takes the buffer (and its contents), the context keeps the
+    // caller's allocation under that name (grown by a later get as usual). Lets a store adopt a call's result arrays
+    // instead of copying them.
+    void swap_buf(const char *name, void *&ptr, size_t &bytes)
+    {
+        acc::Buf &b = bufs[ns.empty() ? std::string(name) : ns + name];
+        std::swap(b.ptr, ptr);
+        std::swap(b.bytes, bytes);
+    }
+
     hipEvent_t take_event()
     {
         if (!event_pool.empty()) {

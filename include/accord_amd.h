@@ -814,7 +814,10 @@ int  acc_cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *snap, acc_cfk_batch
  * acc_cfk_state (the key-major state in the acc_cfk_apply layout, DEVICE memory) read one state in place, valid until
  * the next update of the store. A rejected batch (ACC_E_STATE / ACC_E_ARG) leaves the store unchanged. A store keeps
  * missing[] from its first acc_cfk_apply_deps on; acc_cfk_update (status-only, no missing[]) is then ACC_E_STATE, and
- * acc_cfk_apply_deps on a store holding acc_cfk_update state is ACC_E_STATE. */
+ * acc_cfk_apply_deps on a store holding acc_cfk_update state is ACC_E_STATE. The store adopts the call's result
+ * arrays from the context (no copies) and hands its previous arrays to the context for its next results. Keys with
+ * many updates in one batch (more than ACC_CFK_HOT, default 64, snapshot + update elements) are computed by the
+ * data-parallel closed form of the replay (acc_cfk_apply too); results are the same. */
 int  acc_cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *updates);
 int  acc_cfk_state(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_snap *out);
 int  acc_cfk_missing(acc_ctx *ctx, acc_cfk *cfk, acc_cfk_batch_view *out);
