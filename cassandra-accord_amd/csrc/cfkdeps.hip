@@ -563,17 +563,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
     if (i < u.NP) {
         const uint32_t a = u.dep_off[i], b = u.dep_off[i + 1];
         if (b < a || b > u.ND || (i == 0 && a != 0) || (i + 1 == u.NP && b != u.ND)) e |= E_ARG_OFF;
-        else if (b > a) {   // strictly ascending; the lsb / node words read only where two msb words tie
-            uint64_t pm = u.dm[a];
-            for (uint32_t j = a + 1; j < b; ++j) {
-                const uint64_t m = u.dm[j];
-                if (m < pm || (m == pm && cmp(Ts{ pm, u.dl[j - 1], u.dn[j - 1] }, Ts{ m, u.dl[j], u.dn[j] }) >= 0)) {
-                    e |= E_ARG_SORT;
-                    break;
-                }
-                pm = m;
-            }
-        }
+        // (each pair's deps strictly ascending: k_cd_depchk)
     }
     if (i < s.n_keys) {
         if (i > 0 && s.key[i - 1] >= s.key[i]) e |= E_ARG_SORT;
@@ -592,6 +582,38 @@ __global__ __launch_bounds__(BLOCK) void k_cd_check(Snap s, Upd u, uint32_t *__r
         if (m1 < m0 || m1 > s.n_miss) e |= E_ARG_OFF;
     }
     if (e) atomicOr((unsigned long long *)err, (unsigned long long)e);
+}
+
+// each pair's deps strictly ascending. A wave takes 64 consecutive pairs and walks their deps (one contiguous range)
+// side by side, so the loads coalesce; a dep is compared with the one before it unless it starts its pair's range (a
+// search of the 64 starts held one per lane). The lsb / node words are read only where two msb words tie. Ranges are
+// clamped to [0, n_deps): malformed offsets (k_cd_check reports them) never read out of bounds.
+__global__ __launch_bounds__(BLOCK) void k_cd_depchk(Upd u, uint64_t *__restrict__ err)
+{
+    const uint64_t p0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) & ~(uint64_t)63;
+    if (p0 >= u.NP) return;   // (whole waves: p0 is the wave's first pair)
+    const uint32_t lane = lane_id();
+    const uint64_t pl = p0 + lane < u.NP ? p0 + lane : u.NP;   // lanes past the end hold the end offset
+    const uint32_t st = (uint32_t)std::min<uint64_t>(u.dep_off[pl], u.ND);
+    const uint32_t lo = __shfl(st, 0, 64);
+    const uint64_t pe = p0 + 64 < u.NP ? p0 + 64 : u.NP;
+    const uint32_t hi = (uint32_t)std::min<uint64_t>(u.dep_off[pe], u.ND);
+    bool bad = false;
+    for (uint32_t base = lo; base < hi; base += 64) {   // (uniform over the wave: every lane takes part in the shuffles)
+        const uint32_t j = base + lane;
+        // a pair's start: some lane's st == j (st non-decreasing over lanes when the offsets are valid); branchless
+        // lower bound over the 64 starts
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (__shfl(st, (int)(pos + step - 1), 64) < j) pos += step;
+        const bool start = __shfl(st, (int)pos, 64) == j;
+        if (j < hi && j > 0 && !start) {
+            const uint64_t pm = u.dm[j - 1], m = u.dm[j];
+            if (m < pm || (m == pm && cmp(Ts{ pm, u.dl[j - 1], u.dn[j - 1] }, Ts{ m, u.dl[j], u.dn[j] }) >= 0)) bad = true;
+        }
+    }
+    if (__ballot(bad) && lane == 0) atomicOr((unsigned long long *)err, (unsigned long long)E_ARG_SORT);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_cd_keys(uint32_t nk, uint64_t NP, const uint64_t *__restrict__ skey,
@@ -1871,6 +1893,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     ACC_HIP(hipMemsetAsync(krng, 0xFF, 8, st));
     ACC_HIP(hipMemsetAsync(krng + 1, 0, 8, st));
     launch(ctx, "cd_check", k_cd_check, dim3(grid_for(gmax, BLOCK)), dim3(BLOCK), 0, s, u, owner, errs, krng);
+    if (NP) launch(ctx, "cd_depchk", k_cd_depchk, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, u, errs);
     ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
     ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, krng, 16, hipMemcpyDeviceToHost, st));
     ctx->sync();

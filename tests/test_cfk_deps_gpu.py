@@ -460,3 +460,31 @@ def test_cfk_store_modes(ctx):
         same(st.state(), oracle.cfk_apply(CC.empty_snapshot(), upd), "store from empty")
     finally:
         st.close()
+
+
+def test_cfk_deps_order_checked(ctx):
+    """Each (update, key) pair's deps must be strictly ascending (KeyDeps.txnIds(key) is a SortedList): a swapped or
+    repeated dep inside one pair's range is IllegalArgumentException; a larger dep ending one pair before a smaller
+    dep starting the next is legal (the check sees range boundaries)."""
+    from accord_amd import workload as W
+    from accord_amd.deps import IllegalArgumentException, cfk_apply
+    upd = W.cfk_update_stream(3_000, 4, 400)
+    off = upd["dep_off"].astype(np.int64)
+    cnt = np.diff(off)
+    p = int(np.nonzero(cnt >= 3)[0][5])
+    a = int(off[p])
+    for mode in ("swap", "repeat"):
+        bad = {k: v.copy() for k, v in upd.items()}
+        for col in ("dmsb", "dlsb", "dnode"):
+            if mode == "swap":
+                bad[col][a], bad[col][a + 1] = upd[col][a + 1], upd[col][a]
+            else:
+                bad[col][a + 1] = upd[col][a]
+        with pytest.raises(IllegalArgumentException):
+            cfk_apply(ctx, CC.empty_snapshot(), bad)
+    # pair boundaries: consecutive pairs' ranges abut, the next range may start below the previous one's end
+    q = int(np.nonzero((cnt[:-1] >= 2) & (cnt[1:] >= 2))[0][3])
+    b = int(off[q + 1])
+    assert (upd["dmsb"][b - 1], upd["dlsb"][b - 1]) != (upd["dmsb"][b], upd["dlsb"][b])
+    g = cfk_apply(ctx, CC.empty_snapshot(), upd)
+    same(g, oracle.cfk_apply(CC.empty_snapshot(), upd), "ordered deps")
