@@ -638,10 +638,10 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kstart(uint64_t T, const uint32_t 
     if (i < T && f[i]) kstart[fi[i] - 1] = (uint32_t)i;
     if (i == 0) kstart[nkeys] = (uint32_t)T;
 }
-// per distinct key (a lane per key, so a wave's lanes walk adjacent runs): its working-space bounds. snd: each update
-// element's deps count (k_cd_urec)
+// per distinct key (a lane per key, so a wave's lanes walk adjacent runs): its working-space bounds. rec: each update
+// element's record (k_cd_urec: its deps range)
 __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart,
-                                                     const uint32_t *__restrict__ src, const uint32_t *__restrict__ snd,
+                                                     const uint32_t *__restrict__ src, const uint2 *__restrict__ rda,
                                                      uint32_t nk, Snap s, uint64_t *__restrict__ ecap,
                                                      uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
                                                      uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf,
@@ -665,7 +665,8 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint3
             e += s.ent_off[v + 1] - s.ent_off[v];
             m += s.miss_off[s.ent_off[v + 1]] - s.miss_off[s.ent_off[v]];
         } else {
-            const uint64_t nd = snd[q];
+            const uint2 r = rda[q * 8 + 7];   // the record's (da, db) words (UpdRec bytes 56..63)
+            const uint64_t nd = r.y - r.x;
             e += 1 + nd;
             d = d > nd ? d : nd;
             grow += nd + 2;
@@ -763,8 +764,8 @@ struct UpdRec {
     uint64_t im, il, xm, xl;
     int32_t in, xn;
     uint32_t st_fl;   // status | flags << 8
-    uint32_t da, db;  // deps range
     uint32_t pad[3];
+    uint32_t da, db;  // deps range (the record's last 8 bytes: k_cd_bounds reads them alone)
 };
 static_assert(sizeof(UpdRec) == 64, "64-B update record");
 // the sorted position of every (update, key) pair
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_inv(uint64_t T, const uint32_t *__
 }
 // thread per pair, in pair order (the update columns read nearly contiguously), record written at its sorted position
 __global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *__restrict__ qpos, Upd u,
-                                                   UpdRec *__restrict__ rec, uint32_t *__restrict__ snd)
+                                                   UpdRec *__restrict__ rec)
 {
     const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (j >= NP) return;
@@ -789,9 +790,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_urec(uint64_t NP, const uint32_t *
     r.st_fl = (uint32_t)u.st[i] | ((uint32_t)u.fl[i] << 8);
     r.da = u.dep_off[j]; r.db = u.dep_off[j + 1];
     r.pad[0] = r.pad[1] = r.pad[2] = 0;
-    const uint32_t q = qpos[j];
-    rec[q] = r;
-    snd[q] = r.db - r.da;
+    rec[qpos[j]] = r;
 }
 
 // one lane per key: load the snapshot, replay its updates, record the final buffer and sizes
@@ -1948,13 +1947,12 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         ctx->sync();
         Ew = ctx->pinned[0]; Tw = ctx->pinned[1];
     };
-    // each (update, key) pair's update record at its sorted position, and its deps count
+    // each (update, key) pair's update record at its sorted position
     UpdRec *urec = ctx->get<UpdRec>("cd_urec", std::max<uint64_t>(T, 1));
-    uint32_t *snd = ctx->get<uint32_t>("cd_snd", std::max<uint64_t>(T, 1));
     if (NP) {
         uint32_t *qpos = ctx->get<uint32_t>("cd_qpos", NP);
         launch(ctx, "cd_inv", k_cd_inv, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)so.vals, nk, qpos);
-        launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec, snd);
+        launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec);
     }
     uint8_t *hot = ctx->get<uint8_t>("cd_hot", nkeys);
     uint32_t hot_thr = CH_DEFAULT_HOT;
@@ -1970,7 +1968,8 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     for (int keep_hot = 0; nkeys; keep_hot = 1) {
         ACC_HIP(hipMemsetAsync(nhot, 0, 4, st));
         launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
-               (const uint32_t *)so.vals, (const uint32_t *)snd, nk, s, ecap, mcap, mmax, dcap, ovf, hot_thr, keep_hot, hot,
+               (const uint32_t *)so.vals, reinterpret_cast<const uint2 *>(urec), nk, s, ecap, mcap, mmax, dcap, ovf, hot_thr,
+               keep_hot, hot,
                nhot);
         // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size
         uint64_t *cmax = ctx->get<uint64_t>("cd_cmax", 1);
