@@ -28,6 +28,7 @@ namespace acc {
 namespace cd {
 
 constexpr uint64_t IDENTITY_LSB = 0xFFFFFFFFFFFF001EULL;
+constexpr uint32_t NONE_K = 0xFFFFFFFFu;
 enum : uint32_t { TK = 0, PRE = 2, ACC = 3, COMMITTED = 4, APPLIED = 6, INVALID = 7 };
 enum : uint64_t { E_ARG_STATUS = 1, E_ARG_SORT = 2, E_ARG_OFF = 4, E_STALE = 8, E_STATE = 16, E_CAP = 32, E_MCAP = 64 };
 
@@ -640,9 +641,50 @@ __global__ __launch_bounds__(BLOCK) void k_cd_kstart(uint64_t T, const uint32_t 
 }
 // per distinct key (a lane per key, so a wave's lanes walk adjacent runs): its working-space bounds. rec: each update
 // element's record (k_cd_urec: its deps range)
-__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart,
-                                                     const uint32_t *__restrict__ src, const uint2 *__restrict__ rda,
-                                                     uint32_t nk, Snap s, uint64_t *__restrict__ ecap,
+// per sorted element (in order, so the loads coalesce), its share of its key's bounds: entries, snapshot missing,
+// regrowth (deps + 2 per update) and the largest deps count, summed per key by a segmented scan over the wave (a key's
+// elements are adjacent) and one atomic per key and wave into zeroed accumulators
+struct BSum {
+    uint64_t *e, *m, *g;
+    uint32_t *d;
+};
+__global__ __launch_bounds__(BLOCK) void k_cd_bsum(uint64_t T, const uint32_t *__restrict__ kinc, const uint32_t *__restrict__ src,
+                                                   const uint2 *__restrict__ rda, uint32_t nk, Snap s, BSum b)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t lane = lane_id();
+    uint32_t k = NONE_K, d = 0;
+    uint64_t e = 0, m = 0, g = 0;
+    if (q < T) {
+        k = kinc[q] - 1;
+        const uint32_t v = src[q];
+        if (v < nk) {
+            e = s.ent_off[v + 1] - s.ent_off[v];
+            m = s.miss_off[s.ent_off[v + 1]] - s.miss_off[s.ent_off[v]];
+        } else {
+            const uint2 r = rda[q * 8 + 7];   // the record's (da, db) words (UpdRec bytes 56..63)
+            d = r.y - r.x;
+            e = 1 + (uint64_t)d;
+            g = (uint64_t)d + 2;
+        }
+    }
+#pragma unroll
+    for (int w = 1; w < 64; w <<= 1) {
+        const uint32_t ok = __shfl_up(k, w, 64), od = __shfl_up(d, w, 64);
+        const uint64_t oe = __shfl_up((unsigned long long)e, w, 64), om = __shfl_up((unsigned long long)m, w, 64);
+        const uint64_t og = __shfl_up((unsigned long long)g, w, 64);
+        if ((int)lane >= w && ok == k) { e += oe; m += om; g += og; d = od > d ? od : d; }
+    }
+    const uint32_t nxt = __shfl_down(k, 1, 64);
+    if (k != NONE_K && (lane == 63 || nxt != k)) {
+        atomicAdd((unsigned long long *)&b.e[k], (unsigned long long)e);
+        if (m) atomicAdd((unsigned long long *)&b.m[k], (unsigned long long)m);
+        if (g) atomicAdd((unsigned long long *)&b.g[k], (unsigned long long)g);
+        if (d) atomicMax(&b.d[k], d);
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart, BSum b,
+                                                     uint64_t *__restrict__ ecap,
                                                      uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
                                                      uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf,
                                                      uint32_t hot_thr, int keep_hot, uint8_t *__restrict__ hot,
@@ -658,20 +700,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint3
         atomicAdd(nhot, 1u);
         return;
     }
-    uint64_t e = 0, m = 0, d = 0, grow = 0;
-    for (uint32_t q = kstart[k], q1 = kstart[k + 1]; q < q1; ++q) {
-        const uint32_t v = src[q];
-        if (v < nk) {
-            e += s.ent_off[v + 1] - s.ent_off[v];
-            m += s.miss_off[s.ent_off[v + 1]] - s.miss_off[s.ent_off[v]];
-        } else {
-            const uint2 r = rda[q * 8 + 7];   // the record's (da, db) words (UpdRec bytes 56..63)
-            const uint64_t nd = r.y - r.x;
-            e += 1 + nd;
-            d = d > nd ? d : nd;
-            grow += nd + 2;
-        }
-    }
+    const uint64_t e = b.e[k], m = b.m[k], d = b.d[k], grow = b.g[k];
     ecap[k] = e;
     // every missing[] entry is an uncommitted TxnId of the key held by an entry with info: at most e per entry, and an
     // update adds at most its deps + 2 to each entry
@@ -967,6 +996,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 // to the txn, depsKnownBefore equal to an entry, two encodings of one TxnId -- mark the key irregular: it is replayed by
 // the lane path instead (which also reports the reference's errors exactly).
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+static_assert(NONE == NONE_K, "one sentinel");
 constexpr uint32_t CH_DEFAULT_HOT = 64;
 enum : uint8_t { HI_SNAP = 0, HI_PAIR = 1, HI_TK = 2 };
 enum : uint8_t { HF_CROSSED = 1, HF_NEW = 2 };
@@ -1963,13 +1993,22 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         launch(ctx, "cd_kstart", k_cd_kstart, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kflag,
                (const uint32_t *)kinc, nkeys, kstart);
     uint32_t *nhot = ctx->get<uint32_t>("cd_nhot", 1);
+    BSum bs{ ctx->get<uint64_t>("cd_bs_e", nkeys), ctx->get<uint64_t>("cd_bs_m", nkeys), ctx->get<uint64_t>("cd_bs_g", nkeys),
+             ctx->get<uint32_t>("cd_bs_d", nkeys) };
+    if (nkeys) {
+        ACC_HIP(hipMemsetAsync(bs.e, 0, (size_t)nkeys * 8, st));
+        ACC_HIP(hipMemsetAsync(bs.m, 0, (size_t)nkeys * 8, st));
+        ACC_HIP(hipMemsetAsync(bs.g, 0, (size_t)nkeys * 8, st));
+        ACC_HIP(hipMemsetAsync(bs.d, 0, (size_t)nkeys * 4, st));
+        launch(ctx, "cd_bsum", k_cd_bsum, dim3(grid_for(T, BLOCK)), dim3(BLOCK), 0, T, (const uint32_t *)kinc, (const uint32_t *)so.vals,
+               reinterpret_cast<const uint2 *>(urec), nk, s, bs);
+    }
     ctx->stat("cfk.hot_keys", 0);
     ctx->stat("cfk.hot_irregular", 0);
     for (int keep_hot = 0; nkeys; keep_hot = 1) {
         ACC_HIP(hipMemsetAsync(nhot, 0, 4, st));
-        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
-               (const uint32_t *)so.vals, reinterpret_cast<const uint2 *>(urec), nk, s, ecap, mcap, mmax, dcap, ovf, hot_thr,
-               keep_hot, hot,
+        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart, bs,
+               ecap, mcap, mmax, dcap, ovf, hot_thr, keep_hot, hot,
                nhot);
         // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size
         uint64_t *cmax = ctx->get<uint64_t>("cd_cmax", 1);
