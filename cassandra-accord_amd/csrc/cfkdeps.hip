@@ -918,13 +918,15 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out1(uint32_t nkeys, const uint32_
 __global__ __launch_bounds__(BLOCK) void k_cd_out2(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
                                                    const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ sk,
                                                    uint64_t kbase, const uint32_t *__restrict__ eall, uint64_t *__restrict__ okey,
-                                                   uint32_t *__restrict__ ent_off, uint32_t nko, uint32_t ne)
+                                                   uint32_t *__restrict__ ent_off, uint32_t nko, uint32_t ne,
+                                                   uint32_t *__restrict__ kkey)
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k == 0) ent_off[nko] = ne;
     if (k >= nkeys || !keep[k]) return;
     okey[kpos[k]] = sk[kstart[k]] + kbase;
     ent_off[kpos[k]] = eall[k];
+    kkey[kpos[k]] = k;
 }
 
 struct Out {
@@ -952,6 +954,28 @@ __global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_
         o.st[base + i] = (uint8_t)x.st;
         o.mcnt[base + i] = x.mn;
     }
+}
+
+// the same, a thread per output entry (its key by a search of the kept keys' offsets): the column writes coalesce
+__global__ __launch_bounds__(BLOCK) void k_cd_out3e(uint32_t ne, uint32_t nko, const uint32_t *__restrict__ kkey, Pool p,
+                                                    const uint8_t *__restrict__ final_b, Out o, const uint8_t *__restrict__ hot)
+{
+    const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= ne) return;
+    uint32_t lo = 0, hi = nko;   // last kept key whose entries start at or before e
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (o.ent_off[mid] <= e) lo = mid; else hi = mid;
+    }
+    const uint32_t k = kkey[lo];
+    if (hot[k]) return;   // (k_ch_out3)
+    Work w;
+    key_bufs(p, p.kslot[k], w);
+    const Info x = (final_b[k] ? w.b.e : w.a.e).get(e - o.ent_off[lo]);
+    o.em[e] = x.id.m; o.el[e] = x.id.l; o.en[e] = x.id.n;
+    o.xm[e] = x.ex.m; o.xl[e] = x.ex.l; o.xn[e] = x.ex.n;
+    o.st[e] = (uint8_t)x.st;
+    o.mcnt[e] = x.mn;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_cd_out4(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
@@ -2082,12 +2106,13 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     ctx->stat("cfk.apply_regrow", regrow);
     // ---- 4. key-major output
     uint64_t *okey = ctx->get<uint64_t>("cd_okey", nko);
+    uint32_t *kkey = ctx->get<uint32_t>("cd_kkey", std::max<uint32_t>(nko, 1));
     Out o{};
     o.ent_off = ctx->get<uint32_t>("cd_oent_off", (size_t)nko + 1);
     if (nko) {
         launch(ctx, "cd_out2", k_cd_out2, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
                (const uint32_t *)kpos, (const uint32_t *)kstart, (const uint64_t *)so.keys, kbase, (const uint32_t *)eall, okey,
-               o.ent_off, nko, (uint32_t)NEo);
+               o.ent_off, nko, (uint32_t)NEo, kkey);
     } else {
         ACC_HIP(hipMemsetAsync(o.ent_off, 0, 4, st));
     }
@@ -2097,9 +2122,13 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     o.mcnt = ctx->get<uint32_t>("cd_omcnt", NEo);
     o.miss_off = ctx->get<uint32_t>("cd_omoff", NEo + 1);
     if (NEo) {
-        launch(ctx, "cd_out3", k_cd_out3, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-               (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
-               (const uint8_t *)hot);
+        if (getenv("ACC_CD_OUT3_KEY"))   // tuning switch: a lane per key
+            launch(ctx, "cd_out3", k_cd_out3, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
+                   (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
+                   (const uint8_t *)hot);
+        else
+            launch(ctx, "cd_out3", k_cd_out3e, dim3(grid_for(NEo, BLOCK)), dim3(BLOCK), 0, (uint32_t)NEo, nko, (const uint32_t *)kkey,
+                   p, (const uint8_t *)final_b, o, (const uint8_t *)hot);
         if (ho.ne)
             launch(ctx, "ch_out3", k_ch_out3, dim3(grid_for(ho.ne, BLOCK)), dim3(BLOCK), 0, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
                    (const uint32_t *)kpos, ho.mcnt, o);
