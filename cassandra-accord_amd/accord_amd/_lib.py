@@ -16,6 +16,10 @@ ACC_OK, ACC_E_ARG, ACC_E_STATE, ACC_E_NOMEM, ACC_E_DEVICE, ACC_E_CAP = 0, -1, -2
 ACC_MEM_HOST, ACC_MEM_DEVICE = 0, 1
 ACC_OPT_TIMING = 1
 ACC_OPT_FORCE_REPLAY = 2
+ACC_OPT_NO_WINDOW_TIER = 4
+ACC_OPT_RD_WIDE_SORT = 8
+ACC_OPT_PD_SERIAL = 16
+ACC_LV_AUTO, ACC_LV_LDS_WALK, ACC_LV_WINDOWED, ACC_LV_WAVES = 0, 1, 2, 3
 # SafeCommandStore.TestStartedAt / TestDep / TestStatus ordinals (local/SafeCommandStore.java:63-70)
 ACC_STARTED_BEFORE, ACC_STARTED_AFTER, ACC_STARTED_ANY = 0, 1, 2
 ACC_DEP_WITH, ACC_DEP_WITHOUT, ACC_DEP_ANY = 0, 1, 2
@@ -49,11 +53,12 @@ EXPORTS = ["acc_create", "acc_destroy", "acc_last_error", "acc_sync", "acc_strea
            "acc_maxconflicts_size",
            "acc_ranges_of", "acc_ranges_with", "acc_ranges_subtract", "acc_ranges_merge_touching", "acc_ranges_select",
            "acc_ranges_index_of", "acc_ranges_contains_all_keys", "acc_ranges_contains_all", "acc_rangedeps_is_covered_by",
-           "acc_partial_deps_covering"]
+           "acc_partial_deps_covering", "acc_rmm_without", "acc_recovery_deps_reduce"]
 
 
 class Opts(C.Structure):
-    _fields_ = [("flags", C.c_uint32), ("reserved", C.c_uint32)]
+    _fields_ = [("flags", C.c_uint32), ("reserved", C.c_uint32), ("cfk_hot", C.c_uint32), ("lv_tier", C.c_uint32),
+                ("lv_chunk", C.c_uint32), ("reserved2", C.c_uint32)]
 
 
 class TsCols(C.Structure):
@@ -210,6 +215,23 @@ class SliceView(C.Structure):
                 ("val_idx", C.c_void_p), ("k2v_off", C.c_void_p), ("k2v", C.c_void_p)]
 
 
+ACC_WITHOUT_FROM, ACC_WITHOUT_NONE, ACC_WITHOUT_NEW = 0, 1, 2
+
+
+class TxnSets(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("txn", TsCols)]
+
+
+class WithoutView(C.Structure):
+    _fields_ = [("sl", SliceView), ("kind", C.c_void_p), ("n_from", C.c_uint64), ("n_none", C.c_uint64),
+                ("n_new", C.c_uint64)]
+
+
+class RecoveryDepsView(C.Structure):
+    _fields_ = [("committed", DepsMergeView), ("accepted_merged", DepsMergeView), ("accepted_key", WithoutView),
+                ("accepted_range", WithoutView)]
+
+
 class StabIn(C.Structure):
     _fields_ = [("mem", C.c_uint32), ("n_queries", C.c_uint32), ("grp", C.c_void_p), ("q_start", C.c_void_p),
                 ("q_end", C.c_void_p), ("end_inclusive", C.c_uint32), ("want_txns", C.c_uint32)]
@@ -333,7 +355,13 @@ class _Tolerant:
     points: their signatures are skipped, and calling one fails with the library's own AttributeError."""
 
     class _Skip:
-        pass
+        """A missing acc_* symbol: signature assignments land here harmlessly; a call raises AttributeError."""
+
+        def __init__(self, name):
+            object.__setattr__(self, "_name", name)
+
+        def __call__(self, *args, **kwargs):
+            raise AttributeError(f"{self._name} not exported by {LIB_PATH}")
 
     def __init__(self, lib):
         object.__setattr__(self, "_l", lib)
@@ -343,7 +371,7 @@ class _Tolerant:
             return getattr(self._l, name)
         except AttributeError:
             if name.startswith("acc_"):
-                return _Tolerant._Skip()
+                return _Tolerant._Skip(name)
             raise
 
 
@@ -406,6 +434,12 @@ def load():
     L.acc_rmm_invert.restype = C.c_int
     L.acc_rmm_slice.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(RangesIn), C.POINTER(SliceView)]
     L.acc_rmm_slice.restype = C.c_int
+    L.acc_rmm_without.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(TsCols), C.POINTER(TxnSets),
+                                  C.POINTER(TxnSets), C.POINTER(WithoutView)]
+    L.acc_rmm_without.restype = C.c_int
+    L.acc_recovery_deps_reduce.argtypes = [C.c_void_p, C.POINTER(DepsMergeIn), C.POINTER(DepsMergeIn),
+                                           C.POINTER(RecoveryDepsView)]
+    L.acc_recovery_deps_reduce.restype = C.c_int
     L.acc_rangedeps_stab.argtypes = [C.c_void_p, C.POINTER(RmmBatch), C.POINTER(StabIn), C.POINTER(StabView)]
     L.acc_rangedeps_stab.restype = C.c_int
     L.acc_comm_unique_id.argtypes = [C.c_void_p]

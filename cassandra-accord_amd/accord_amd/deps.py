@@ -46,12 +46,23 @@ def _ptr(a: np.ndarray):
 class Context:
     """One acc_ctx: a HIP stream plus device scratch (one per host thread / CommandStore)."""
 
-    def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False):
+    LV_TIERS = {"auto": 0, "lds": 1, "windowed": 2, "waves": 3}
+
+    def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False, *, cfk_hot: int = 0,
+                 lv_tier: str = "auto", lv_chunk: int = 0, no_window_tier: bool = False, rd_wide_sort: bool = False,
+                 pd_serial: bool = False):
+        """acc_opts, fixed for the context's life (the library reads no environment): timing = per-kernel HIP events;
+        the rest force code paths for tests (force_replay: the exact replay scan; cfk_hot: the closed-form threshold of
+        acc_cfk_apply; lv_tier / lv_chunk: the levelise walk; no_window_tier: the KeyDeps sorting tiers; rd_wide_sort:
+        RangeDeps 64-bit sort keys) or trade speed for memory (pd_serial: acc_partial_deps_batch on one buffer set)."""
         self.timing_enabled = timing
         self.device = device
         self._lib = L.load()
         h = C.c_void_p()
-        opts = L.Opts((L.ACC_OPT_TIMING if timing else 0) | (L.ACC_OPT_FORCE_REPLAY if force_replay else 0), 0)
+        flags = ((L.ACC_OPT_TIMING if timing else 0) | (L.ACC_OPT_FORCE_REPLAY if force_replay else 0) |
+                 (L.ACC_OPT_NO_WINDOW_TIER if no_window_tier else 0) | (L.ACC_OPT_RD_WIDE_SORT if rd_wide_sort else 0) |
+                 (L.ACC_OPT_PD_SERIAL if pd_serial else 0))
+        opts = L.Opts(flags, 0, int(cfk_hot), self.LV_TIERS[lv_tier], int(lv_chunk), 0)
         rc = self._lib.acc_create(device, C.byref(opts), C.byref(h))
         if rc != L.ACC_OK:
             raise _ERRORS.get(rc, AccordError)(f"acc_create failed ({rc})")
@@ -613,6 +624,71 @@ def rmm_slice(ctx: Context, m: dict, sel_off, sel_start, sel_end, end_inclusive:
     return dict(key_off=device_array(ctx, v.key_off, g, np.uint64), key_idx=device_array(ctx, v.key_idx, v.total_keys, np.uint32),
                 val_off=device_array(ctx, v.val_off, g, np.uint64), val_idx=device_array(ctx, v.val_idx, v.total_vals, np.uint32),
                 k2v_off=device_array(ctx, v.k2v_off, g, np.uint64), k2v=device_array(ctx, v.k2v, v.total_k2v, np.int32))
+
+
+def _slice_copy(ctx: Context, v) -> dict:
+    g = v.n_groups + 1
+    return dict(key_off=device_array(ctx, v.key_off, g, np.uint64), key_idx=device_array(ctx, v.key_idx, v.total_keys, np.uint32),
+                val_off=device_array(ctx, v.val_off, g, np.uint64), val_idx=device_array(ctx, v.val_idx, v.total_vals, np.uint32),
+                k2v_off=device_array(ctx, v.k2v_off, g, np.uint64), k2v=device_array(ctx, v.k2v, v.total_k2v, np.int32))
+
+
+def _without_copy(ctx: Context, w) -> dict:
+    out = _slice_copy(ctx, w.sl)
+    out["kind"] = device_array(ctx, w.kind, w.sl.n_groups, np.uint8)
+    out["counts"] = (int(w.n_from), int(w.n_none), int(w.n_new))
+    return out
+
+
+def _txn_sets(x, keep: list) -> "L.TxnSets | None":
+    if x is None:
+        return None
+    a = {k: np.ascontiguousarray(x[k], dtype=dt) for k, dt in
+         (("off", np.uint64), ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32))}
+    keep.append(a)
+    return L.TxnSets(a["off"].ctypes.data, L.TsCols(a["msb"].ctypes.data, a["lsb"].ctypes.data, a["node"].ctypes.data))
+
+
+def rmm_without(ctx: Context, m: dict, set_a=None, set_b=None) -> dict:
+    """KeyDeps.without / RangeDeps.without (RelationMultiMap.remove, utils/RelationMultiMap.java:843-905) of every group
+    with remove = membership in the group's sorted TxnId set(s) (Deps::contains). `m`: one deps half per group (the
+    acc_rmm_batch dict + its TxnIds msb/lsb/node); sets: dict(off, msb, lsb, node) or None. Returns the slice-shaped
+    result (kept key / TxnId indices, the new int[]) with kind[g] = ACC_WITHOUT_FROM / _NONE / _NEW."""
+    keep = []
+    b = _rmm_batch(m, keep)
+    t = {k: np.ascontiguousarray(m[k], dtype=dt) for k, dt in (("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32))}
+    keep.append(t)
+    txn = L.TsCols(t["msb"].ctypes.data, t["lsb"].ctypes.data, t["node"].ctypes.data)
+    sa, sb = _txn_sets(set_a, keep), _txn_sets(set_b, keep)
+    v = L.WithoutView()
+    ctx.check(ctx._lib.acc_rmm_without(ctx.handle, C.byref(b), C.byref(txn), C.byref(sa) if sa is not None else None,
+                                       C.byref(sb) if sb is not None else None, C.byref(v)))
+    return _without_copy(ctx, v)
+
+
+def recovery_deps_reduce(ctx: Context, committed: dict, accepted: dict) -> dict:
+    """The recovery coordinator's reduce of the replies' recovery deps (coordinate/Recover.java:320-322,
+    messages/BeginRecovery.java:180-183; acc_recovery_deps_reduce): earlierCommittedWitness = Deps.merge(...),
+    earlierAcceptedNoWitness = Deps.merge(...).without(earlierCommittedWitness::contains). Inputs as deps_merge's `m`
+    (same grp_off). Returns dict(committed=merged halves, accepted_merged=merged halves, accepted_key / accepted_range =
+    the without results over accepted_merged's halves)."""
+    keep = []
+
+    def dmi(m):
+        grp_off = np.ascontiguousarray(m["grp_off"], dtype=np.uint64)
+        keep.append(grp_off)
+        ng = len(grp_off) - 1
+        return L.DepsMergeIn(L.ACC_MEM_HOST, ng, int(grp_off[-1]) if ng >= 0 else 0, grp_off.ctypes.data,
+                             _rmm_in(m.get("key"), keep), _rmm_in(m.get("range"), keep)), ng
+    ci, ng = dmi(committed)
+    ai, ng2 = dmi(accepted)
+    v = L.RecoveryDepsView()
+    ctx.check(ctx._lib.acc_recovery_deps_reduce(ctx.handle, C.byref(ci), C.byref(ai), C.byref(v)))
+    return dict(committed=dict(key=rmm_copy_out(ctx, ng, v.committed.key_deps, False),
+                               range=rmm_copy_out(ctx, ng, v.committed.range_deps, True)),
+                accepted_merged=dict(key=rmm_copy_out(ctx, ng, v.accepted_merged.key_deps, False),
+                                     range=rmm_copy_out(ctx, ng, v.accepted_merged.range_deps, True)),
+                accepted_key=_without_copy(ctx, v.accepted_key), accepted_range=_without_copy(ctx, v.accepted_range))
 
 
 def rangedeps_stab(ctx: Context, m: dict, grp, q_start, q_end=None, end_inclusive: bool = True, want_txns: bool = True):

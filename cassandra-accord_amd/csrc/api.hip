@@ -16,6 +16,9 @@ void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *
 void rmm_invert(acc_ctx *ctx, const acc_rmm_batch *in, acc_csr_view *out);
 void rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out);
 void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q, acc_stab_view *out);
+void rmm_without(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ts_cols *txn, const acc_txn_sets *set_a,
+                 const acc_txn_sets *set_b, acc_without_view *out);
+void recovery_deps_reduce(acc_ctx *ctx, const acc_deps_merge_in *cw, const acc_deps_merge_in *anw, acc_recovery_deps_view *view);
 void map_reduce_full(acc_ctx *ctx, const acc_batch_in *in, const acc_recovery_in *q, acc_keydeps_view *view);
 void map_reduce_full_ranges(acc_ctx *ctx, const acc_range_cmds_in *c, const acc_recovery_ranges_in *q, acc_rangedeps_view *view);
 void latest_deps_merge(acc_ctx *ctx, const acc_latest_in *in, acc_latest_view *view);
@@ -70,7 +73,8 @@ int ctx_create(int device, const acc_opts *opts, acc_ctx **out_ctx)
         if (device < 0 || device >= count) acc::fail(ACC_E_ARG, "no such HIP device");
         ACC_HIP(hipSetDevice(device));
         ctx->device = device;
-        ctx->flags = opts ? opts->flags : 0;
+        if (opts) ctx->opts = *opts;
+        ctx->flags = ctx->opts.flags;
         ACC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ACC_HIP(hipHostMalloc((void **)&ctx->pinned, acc_ctx::PINNED_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     });
@@ -171,13 +175,13 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         if (!key_view || !range_view) acc::fail(ACC_E_ARG, "null argument");
-        if (!ctx->child && !getenv("ACC_PD_SERIAL")) {   // tuning switch: both halves in order on this context
-            acc_opts o{};
-            o.flags = ctx->flags;
+        const bool serial = (ctx->flags & ACC_OPT_PD_SERIAL) != 0;   // both halves in order on this context
+        if (!ctx->child && !serial) {
+            const acc_opts o = ctx->opts;
             const int rc = ctx_create(ctx->device, &o, &ctx->child);
             if (rc != ACC_OK) acc::fail(rc, "cannot create the RangeDeps half's context");
         }
-        acc_ctx *const child = getenv("ACC_PD_SERIAL") ? nullptr : ctx->child;
+        acc_ctx *const child = serial ? nullptr : ctx->child;
         // the RangeDeps half starts on the child context (own stream, own host thread) as soon as the KeyDeps half's
         // dictionary is enqueued: its stream waits for that point of this context's stream, and it reads the
         // dictionary in place (not written again by the KeyDeps half)
@@ -191,7 +195,8 @@ int acc_partial_deps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_keyde
             ~Join() { if (t.joinable()) t.join(); if (e) (void)hipEventDestroy(e); }
         } join{ th, ev };
         if (child) {
-            child->flags = ctx->flags;            // acc_opts holds only flags; the timing filter too
+            child->opts = ctx->opts;              // the options and the timing filter as the parent's
+            child->flags = ctx->flags;
             child->time_only = ctx->time_only;
             sd.ready = [&](const acc::SharedDict &d) {
                 ACC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -478,6 +483,26 @@ int acc_rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *se
     return acc_guard(ctx, [&] {
         ACC_HIP(hipSetDevice(ctx->device));
         acc::rmm_slice(ctx, in, select, out_view);
+    });
+}
+
+int acc_rmm_without(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ts_cols *txn, const acc_txn_sets *set_a,
+                    const acc_txn_sets *set_b, acc_without_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::rmm_without(ctx, in, txn, set_a, set_b, out_view);
+    });
+}
+
+int acc_recovery_deps_reduce(acc_ctx *ctx, const acc_deps_merge_in *committed_witness,
+                             const acc_deps_merge_in *accepted_no_witness, acc_recovery_deps_view *out_view)
+{
+    if (!ctx) return ACC_E_ARG;
+    return acc_guard(ctx, [&] {
+        ACC_HIP(hipSetDevice(ctx->device));
+        acc::recovery_deps_reduce(ctx, committed_witness, accepted_no_witness, out_view);
     });
 }
 

@@ -440,6 +440,14 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
         ctx->swap_buf(name, v, bytes);
         p = static_cast<std::remove_reference_t<decltype(p)>>(v);
     };
+    const acc_batch_in &b = bv.batch;
+    // the results must sit in the context's named buffers before any array is adopted: a rejected call leaves the
+    // store holding its previous arrays, none of the new ones
+    if (ctx->buf_ptr("cd_okey") != v.key || ctx->buf_ptr("cd_oem") != v.txn_id.msb || ctx->buf_ptr("cd_omm") != v.missing.msb ||
+        ctx->buf_ptr("cd_omoff") != v.miss_off)
+        fail(ACC_E_STATE, "internal: CommandsForKey result buffers moved");
+    if (ctx->buf_ptr("cb_tm") != b.txn_id.msb || ctx->buf_ptr("cb_ko") != b.key_off || ctx->buf_ptr("cb_mo") != bv.missing_off)
+        fail(ACC_E_STATE, "internal: CommandsForKey view buffers moved");
     const uint32_t nk = v.n_keys;
     const uint64_t ne = v.n_entries, nm = v.n_missing;
     size_t *kb = k.bytes;
@@ -448,10 +456,7 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     adopt("cd_oxm", k.xm, kb[5]); adopt("cd_oxl", k.xl, kb[6]); adopt("cd_oxn", k.xn, kb[7]);
     adopt("cd_ost", k.st, kb[8]); adopt("cd_omoff", k.miss_off, kb[9]);
     adopt("cd_omm", k.mm, kb[10]); adopt("cd_oml", k.ml, kb[11]); adopt("cd_omn", k.mn, kb[12]);
-    if (k.key != v.key || k.em != v.txn_id.msb || k.mm != v.missing.msb || k.miss_off != v.miss_off)
-        fail(ACC_E_STATE, "internal: CommandsForKey result buffers moved");
     k.nk = nk; k.ne = ne; k.nm = nm;
-    const acc_batch_in &b = bv.batch;
     const uint32_t n = b.n_txn;
     const uint64_t P = b.n_pairs;
     acc_cfk::Set &S = cfk->set[cfk->cur];
@@ -462,8 +467,6 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     S.cap_n = S.cap_p = 0;   // (sizes now per array: a status-only reserve would reallocate; deps mode refuses it)
     adopt("cb_mo", cfk->bmiss_off, cfk->bytes_bmo);
     adopt("cb_mt", cfk->bmiss_txn, cfk->bytes_bmt);
-    if (S.tm != b.txn_id.msb || S.key_off != b.key_off || cfk->bmiss_off != bv.missing_off)
-        fail(ACC_E_STATE, "internal: CommandsForKey view buffers moved");
     cfk->bnm = bv.n_missing;
     ctx->sync();
     cfk->n = n;

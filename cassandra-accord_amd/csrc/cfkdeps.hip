@@ -18,7 +18,7 @@
 //      not the quadratic bound; from the third round on a flagged key takes the bound at once, so a batch replays at
 //      most four times (every key replays: the pool's layout moves when the flagged keys grow);
 //   4. final sizes, two scans, and a compaction into the key-major output (keys without entries dropped).
-// Keys with more than ACC_CFK_HOT (64) sorted elements skip step 3: their final state is the replay's closed form,
+// Keys with more than acc_opts.cfk_hot (64) sorted elements skip step 3: their final state is the replay's closed form,
 // computed data-parallel over the key's updates (the hot-key section below).
 // Errors: a status going back (IllegalStateException "stale status", ACC_E_STATE), an addition equal to an existing
 // TxnId or depsKnownBefore equal to a TxnId (the reference's checkState, ACC_E_STATE), malformed input (ACC_E_ARG).
@@ -936,27 +936,8 @@ struct Out {
     uint32_t *ent_off, *mcnt, *miss_off;
 };
 
-// entries of every kept key (one lane per key), and each entry's missing count
-__global__ __launch_bounds__(BLOCK) void k_cd_out3(uint32_t nkeys, const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kpos,
-                                                   const uint64_t *__restrict__ ecap, const uint64_t *__restrict__ mcap, Pool p,
-                                                   const uint8_t *__restrict__ final_b, Out o, const uint8_t *__restrict__ hot)
-{
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;   // key order: a wave's lanes write adjacent output runs
-    if (k >= nkeys || !keep[k] || hot[k]) return;
-    Work w;
-    key_bufs(p, p.kslot[k], w);
-    const EP E = final_b[k] ? w.b.e : w.a.e;
-    const uint32_t base = o.ent_off[kpos[k]], n = o.ent_off[kpos[k] + 1] - base;
-    for (uint32_t i = 0; i < n; ++i) {
-        const Info x = E.get(i);
-        o.em[base + i] = x.id.m; o.el[base + i] = x.id.l; o.en[base + i] = x.id.n;
-        o.xm[base + i] = x.ex.m; o.xl[base + i] = x.ex.l; o.xn[base + i] = x.ex.n;
-        o.st[base + i] = (uint8_t)x.st;
-        o.mcnt[base + i] = x.mn;
-    }
-}
-
-// the same, a thread per output entry (its key by a search of the kept keys' offsets): the column writes coalesce
+// entries of every kept key and each entry's missing count, a thread per output entry (its key by a search of the kept
+// keys' offsets): the column writes coalesce
 __global__ __launch_bounds__(BLOCK) void k_cd_out3e(uint32_t ne, uint32_t nko, const uint32_t *__restrict__ kkey, Pool p,
                                                     const uint8_t *__restrict__ final_b, Out o, const uint8_t *__restrict__ hot)
 {
@@ -1005,7 +986,7 @@ __global__ __launch_bounds__(BLOCK) void k_cd_widen(uint32_t n, const uint32_t *
 }
 
 // ---- hot keys: the replay's closed form, data-parallel over a key's updates
-// A key with more than ACC_CFK_HOT (default 64) updates in the batch is not replayed by one lane: its final state is
+// A key with more than acc_opts.cfk_hot (default 64) updates in the batch is not replayed by one lane: its final state is
 // computed from the update stream directly. Its TxnInfos are every TxnId its snapshot, its updates or their deps name
 // (a dep the key lacks becomes a TRANSITIVELY_KNOWN entry, updateOrInsertWithAdditions :772-863); each takes the status /
 // executeAt of its last update that changed it (update :657-706: stale checks, unchanged returns). The missing[] of an
@@ -1648,8 +1629,13 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     launch(ctx, "ch_mcount", k_ch_miss<false>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
            (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt, (const uint32_t *)nullptr,
            (uint64_t *)nullptr, (uint64_t *)nullptr, (int32_t *)nullptr);
+    uint64_t *nm64 = ctx->get<uint64_t>("ch_nm64", 1);
+    sum_u32(ctx, mcnt, ne, nm64);   // the u32 offsets below must not wrap
     scan<uint32_t, OpAdd<uint32_t>>(ctx, mcnt, moff, ne, true, moff + ne);
-    const uint64_t nm = read32(moff + ne);
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, nm64, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t nm = ctx->pinned[0];
+    if (nm >= 0xFFFFFFFFull) fail(ACC_E_CAP, "CommandsForKey update: more than 2^32-2 missing[] TxnIds over the hot keys");
     uint64_t *mm = ctx->get<uint64_t>("ch_mm", nm), *ml = ctx->get<uint64_t>("ch_ml", nm);
     int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
     if (nm)
@@ -2009,8 +1995,7 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         launch(ctx, "cd_urec", k_cd_urec, dim3(grid_for(NP, BLOCK)), dim3(BLOCK), 0, NP, (const uint32_t *)qpos, u, urec);
     }
     uint8_t *hot = ctx->get<uint8_t>("cd_hot", nkeys);
-    uint32_t hot_thr = CH_DEFAULT_HOT;
-    if (const char *e = getenv("ACC_CFK_HOT")) hot_thr = (uint32_t)std::max(1L, strtol(e, nullptr, 10));
+    const uint32_t hot_thr = ctx->opts.cfk_hot ? ctx->opts.cfk_hot : CH_DEFAULT_HOT;   // acc_opts.cfk_hot
     uint32_t *fin_n = ctx->get<uint32_t>("cd_fin_n", nkeys);
     HotOut ho;
     if (nkeys)
@@ -2045,11 +2030,8 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
         {
             const uint32_t *asc = radix_sort(ctx, "cd_rs_cap", ecap, nullptr, nkeys, std::max(1, bits_for(ctx->pinned[0]))).vals;
             uint32_t *desc = ctx->get<uint32_t>("cd_perm_desc", nkeys);
-            if (getenv("ACC_CD_ASC")) perm = asc;   // tuning switch: ascending capacity
-            else {
-                launch(ctx, "cd_rev", k_cd_rev, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, asc, desc);
-                perm = desc;
-            }
+            launch(ctx, "cd_rev", k_cd_rev, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, asc, desc);
+            perm = desc;
         }
         wave_layout();
         // the hot keys' final states; keys found irregular go back to the lane path (layout again)
@@ -2122,20 +2104,18 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     o.mcnt = ctx->get<uint32_t>("cd_omcnt", NEo);
     o.miss_off = ctx->get<uint32_t>("cd_omoff", NEo + 1);
     if (NEo) {
-        if (getenv("ACC_CD_OUT3_KEY"))   // tuning switch: a lane per key
-            launch(ctx, "cd_out3", k_cd_out3, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)keep,
-                   (const uint32_t *)kpos, (const uint64_t *)ecap, (const uint64_t *)mcap, p, (const uint8_t *)final_b, o,
-                   (const uint8_t *)hot);
-        else
-            launch(ctx, "cd_out3", k_cd_out3e, dim3(grid_for(NEo, BLOCK)), dim3(BLOCK), 0, (uint32_t)NEo, nko, (const uint32_t *)kkey,
-                   p, (const uint8_t *)final_b, o, (const uint8_t *)hot);
+        launch(ctx, "cd_out3", k_cd_out3e, dim3(grid_for(NEo, BLOCK)), dim3(BLOCK), 0, (uint32_t)NEo, nko, (const uint32_t *)kkey,
+               p, (const uint8_t *)final_b, o, (const uint8_t *)hot);
         if (ho.ne)
             launch(ctx, "ch_out3", k_ch_out3, dim3(grid_for(ho.ne, BLOCK)), dim3(BLOCK), 0, ho.ne, ho.eg, ho.G, ho.eoff, ho.hk,
                    (const uint32_t *)kpos, ho.mcnt, o);
+        uint64_t *nm64 = ctx->get<uint64_t>("cd_onm64", 1);
+        sum_u32(ctx, o.mcnt, NEo, nm64);   // the u32 miss_off of the result must not wrap
         scan<uint32_t, OpAdd<uint32_t>>(ctx, o.mcnt, o.miss_off, NEo, true, o.miss_off + NEo);
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, o.miss_off + NEo, 4, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipMemcpyAsync(ctx->pinned, nm64, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
-        NMo = reinterpret_cast<uint32_t *>(ctx->pinned)[0];
+        if (ctx->pinned[0] >= 0xFFFFFFFFull) fail(ACC_E_CAP, "CommandsForKey update: more than 2^32-2 missing[] TxnIds in the result");
+        NMo = (uint32_t)ctx->pinned[0];
     } else {
         ACC_HIP(hipMemsetAsync(o.miss_off, 0, 4, st));
     }

@@ -267,6 +267,9 @@ void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in
 {
     if (!c || !in || !key_view || !range_view || (covering && !covering_view)) fail(ACC_E_ARG, "null argument");
     if (c->ctx != ctx) fail(ACC_E_ARG, "communicator belongs to another context");
+    // without a placement the batch index is the global index: one check for every call form (with or without a
+    // covering), so the key / range results never depend on whether a covering is passed
+    if (!txn_global && n_global < in->n_txn) fail(ACC_E_ARG, "n_global must be >= n_txn when txn_global is null");
     const acc_batch_in kin{ in->n_txn, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
     Streams S;
     add_key_streams(ctx, &kin, txn_global, c->world, S);
@@ -284,7 +287,6 @@ void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in
             uint32_t *io = ctx->get<uint32_t>("cov_iota", std::max<uint32_t>(n, 1));
             if (n) launch(ctx, "iota", k_iota, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, io, (size_t)n);
             gidx = io;
-            n_global = std::max(n_global, n);
         }
         void *cs[2];
         std::vector<uint64_t> co[2];

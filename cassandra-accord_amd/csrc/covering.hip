@@ -126,6 +126,9 @@ void partial_deps_covering(acc_ctx *ctx, const acc_rlist *covering, uint32_t end
     if (!ctx->kd_valid || !ctx->rd_valid) fail(ACC_E_STATE, "no acc_partial_deps_batch result on this context");
     const rg::V c = rg::check_sorted_deoverlapped(rg::load(covering));
     hipStream_t st = ctx->stream;
+    const acc_keydeps_view &kv = ctx->kd_view;
+    const acc_rangedeps_view &rv = ctx->rd_view;
+    if (kv.n_txn != rv.n_txn) fail(ACC_E_STATE, "internal: PartialDeps halves of different batches");
     const size_t nc = c.size();
     std::vector<uint64_t> h(2 + 2 * nc);
     h[0] = 0; h[1] = nc;
@@ -134,9 +137,6 @@ void partial_deps_covering(acc_ctx *ctx, const acc_rlist *covering, uint32_t end
     ACC_HIP(hipMemcpyAsync(d, h.data(), h.size() * 8, hipMemcpyHostToDevice, st));
     uint64_t *err = ctx->get<uint64_t>("cov_err", 1);
     ACC_HIP(hipMemsetAsync(err, 0, 8, st));
-    const acc_keydeps_view &kv = ctx->kd_view;
-    const acc_rangedeps_view &rv = ctx->rd_view;
-    if (kv.n_txn != rv.n_txn) fail(ACC_E_STATE, "internal: PartialDeps halves of different batches");
     Groups g{ kv.n_txn, kv.kd_key ? kv.kd_off : nullptr, kv.kd_key, rv.rd_off, rv.rng_start, rv.rng_end, rv.range_id, nullptr };
     const Table t{ d, d + 2, d + 2 + nc, (int)end_inclusive };
     if (g.n) launch(ctx, "cov_check", k_cov_check, dim3(grid_for(g.n, BLOCK)), dim3(BLOCK), 0, g, t, err);
@@ -181,6 +181,7 @@ void covering_pack(acc_ctx *ctx, const acc_rlist *covering, const uint32_t *txn_
     send[1] = cs;
     off[1].assign(world + 1, 0);
     for (uint32_t d = 0; d < world; ++d) off[1][d + 1] = off[1][d] + nc;
+    ctx->sync();   // cur and hs are pageable host vectors: their copies complete before they go out of scope
 }
 
 // Home side: the store mask of every home txn, the distinct masks' coverings folded on the host in store order
@@ -193,6 +194,8 @@ void covering_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_glob
     using namespace cov;
     hipStream_t st = ctx->stream;
     const uint32_t ng = n_global > rank ? (n_global - rank + world - 1) / world : 0;
+    // checked before any copy from a host vector is queued (a throw would free them under a pending copy)
+    if (kv->n_groups != ng || rv->n_groups != ng) fail(ACC_E_STATE, "internal: reduced halves of different home sets");
     // the stores' coverings (a few ranges each)
     uint64_t ncov_all = 0;
     for (uint32_t s = 0; s < world; ++s) ncov_all += n_cov[s];
@@ -250,7 +253,6 @@ void covering_merge(acc_ctx *ctx, uint32_t world, uint32_t rank, uint32_t n_glob
     // invariants of the reduced PartialDeps (the constructor's checks on the final fold)
     uint64_t *err = ctx->get<uint64_t>("cov_err", 1);
     ACC_HIP(hipMemsetAsync(err, 0, 8, st));
-    if (kv->n_groups != ng || rv->n_groups != ng) fail(ACC_E_STATE, "internal: reduced halves of different home sets");
     Groups g{ ng, kv->key_off, kv->key_code, rv->range_deps.key_off, rv->range_deps.key_a, rv->range_deps.key_b, nullptr, dcid };
     const Table t{ doff, dts, dte, (int)end_inclusive };
     if (ng) launch(ctx, "cov_check", k_cov_check, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, g, t, err);

@@ -68,6 +68,7 @@ struct acc_ctx {
     };
     std::unordered_map<std::string, OsState> os_state;
     uint32_t flags = 0;
+    acc_opts opts{};   // as given to acc_create (flags == opts.flags)
     std::string last_error;
     // a second context on the same device (own stream, buffers, pinned staging), created on first use: the RangeDeps
     // half of acc_partial_deps_batch runs on it from a second host thread, concurrently with the KeyDeps half
@@ -107,7 +108,6 @@ struct acc_ctx {
     acc_deps_merge_view dm_view{};
     bool dm_valid = false;
     uint64_t rd_ent_hint = 0;   // RangeDeps raw pairs of the last batch (output capacity of the stabbing pass)
-    uint64_t kd_e_hint = 0;     // KeyDeps: capacity for the next batch's E (entries) from the batches seen (optimistic build)
     bool rd_valid = false;
     bool kd_valid = false;
     bool merge_valid = false;
@@ -149,6 +149,13 @@ struct acc_ctx {
         acc::Buf &b = bufs[ns.empty() ? std::string(name) : ns + name];
         std::swap(b.ptr, ptr);
         std::swap(b.bytes, bytes);
+    }
+
+    // the named buffer's current allocation (nullptr if none)
+    const void *buf_ptr(const char *name) const
+    {
+        auto it = bufs.find(ns.empty() ? std::string(name) : ns + name);
+        return it == bufs.end() ? nullptr : it->second.ptr;
     }
 
     hipEvent_t take_event()

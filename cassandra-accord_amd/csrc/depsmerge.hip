@@ -467,4 +467,42 @@ void deps_merge(acc_ctx *ctx, const acc_deps_merge_in *in, acc_deps_merge_view *
     ctx->dm_valid = true;
 }
 
+void rmm_without_dev(acc_ctx *ctx, uint32_t ng, const acc_rmm_in &h, uint64_t NK, uint64_t NV, uint64_t NO,
+                     const acc_txn_sets *sa, const acc_txn_sets *sb, acc_without_view *out);   // rmm.hip
+
+// The recovery coordinator's fold of the replies' recovery deps (coordinate/Recover.java:320-322; pairwise,
+// BeginRecovery.RecoverOk.reduce, messages/BeginRecovery.java:180-183): earlierCommittedWitness = Deps.merge of the
+// replies'; earlierAcceptedNoWitness = Deps.merge of the replies', then .without(earlierCommittedWitness::contains) on
+// both halves (Deps.without, primitives/Deps.java:122-124) with the merged committed key and range TxnIds as the sets
+// (Deps.contains = KeyDeps.contains || RangeDeps.contains). Everything stays on the device between the steps.
+void recovery_deps_reduce(acc_ctx *ctx, const acc_deps_merge_in *cw, const acc_deps_merge_in *anw, acc_recovery_deps_view *view)
+{
+    if (!cw || !anw || !view) fail(ACC_E_ARG, "null argument");
+    if (cw->n_groups != anw->n_groups) fail(ACC_E_ARG, "committed and accepted deps must cover the same recovered txns");
+    acc_recovery_deps_view v{};
+    {
+        NsScope s(ctx, "rcw.");
+        deps_merge(ctx, cw, &v.committed);
+    }
+    {
+        NsScope s(ctx, "ran.");
+        deps_merge(ctx, anw, &v.accepted_merged);
+    }
+    const uint32_t ng = anw->n_groups;
+    const acc_rmm_view &ck = v.committed.key_deps, &cr = v.committed.range_deps;
+    const acc_txn_sets sa{ ck.val_off, acc_ts_cols{ ck.txn_msb, ck.txn_lsb, ck.txn_node } };
+    const acc_txn_sets sb{ cr.val_off, acc_ts_cols{ cr.txn_msb, cr.txn_lsb, cr.txn_node } };
+    for (int half = 0; half < 2; ++half) {
+        const acc_rmm_view &m = half ? v.accepted_merged.range_deps : v.accepted_merged.key_deps;
+        acc_rmm_in h{};
+        h.key_off = m.key_off; h.key_a = m.key_a; h.key_b = m.key_b; h.val_off = m.val_off;
+        h.txn = acc_ts_cols{ m.txn_msb, m.txn_lsb, m.txn_node };
+        h.k2v_off = m.k2v_off; h.k2v = m.k2v;
+        NsScope s(ctx, half ? "rwr." : "rwk.");
+        rmm_without_dev(ctx, ng, h, m.total_keys, m.total_vals, m.total_k2v, &sa, &sb,
+                        half ? &v.accepted_range : &v.accepted_key);
+    }
+    *view = v;
+}
+
 }  // namespace acc

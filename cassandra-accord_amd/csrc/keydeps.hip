@@ -809,18 +809,11 @@ __global__ __launch_bounds__(BLOCK) void k_cfk_gather4(size_t P, uint32_t *__res
                                                        uint32_t *__restrict__ seg_flag, uint32_t *__restrict__ s_rank,
                                                        uint32_t *__restrict__ s_exec, uint8_t *__restrict__ s_info,
                                                        uint32_t *__restrict__ pair_pos, uint32_t *__restrict__ tile_sums,
-                                                       uint32_t ntiles, uint32_t *__restrict__ ev1, uint32_t *__restrict__ ev2,
-                                                       uint32_t *__restrict__ bq_cnt)
+                                                       uint32_t ntiles)
 {
     __shared__ uint32_t lds[WAVES];
     const size_t base = (size_t)blockIdx.x * V2_TILE + (size_t)threadIdx.x * V2_ITEMS;
     uint32_t c[NCNT] = {};
-    if (blockIdx.x == 0 && threadIdx.x == 0 && bq_cnt) *bq_cnt = 0;
-    if (base < P && ev1) {   // the O(1) query columns' event counts ([P + 1], padded to whole 16-B stores)
-        *reinterpret_cast<uint4 *>(ev1 + base) = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4 *>(ev2 + base) = make_uint4(0u, 0u, 0u, 0u);
-        if (base + V2_ITEMS >= P) { ev1[P] = 0; ev2[P] = 0; }
-    }
     if (base < P) {
         uint32_t j[V2_ITEMS], fl[V2_ITEMS];
         uint4 ti[V2_ITEMS];
@@ -913,11 +906,9 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
                                                     const uint64_t *__restrict__ sp, Runs krun, uint64_t rk_mask,
                                                     uint32_t *__restrict__ bases, uint64_t *__restrict__ z0, uint32_t nz0,
                                                     uint64_t *__restrict__ z1, uint32_t nz1, const uint64_t *__restrict__ g,
-                                                    uint64_t *__restrict__ stage, uint32_t *__restrict__ bq_list,
-                                                    uint32_t *__restrict__ bq_cnt)
+                                                    uint64_t *__restrict__ stage)
 {
     __shared__ uint32_t lds[WAVES];
-    __shared__ uint32_t s_bq;
     if (blockIdx.x == 0) {
         // the list bases for the count pass (list l at [bases[l], bases[l] + totals[l]) of the class-list arrays), the
         // count / mark passes' accumulators zeroed, the dictionary's error / tie words staged beside the totals
@@ -982,16 +973,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_apply(size_t P, const uint32_t *__
         uint32_t pre = tile_pref[(size_t)q * ntiles + blockIdx.x];
         if (!cnt_is_max(q)) run[q] = pre + block_exclusive(c[q], OpAdd<uint32_t>(), lds, total);
         else { uint32_t e = block_exclusive(c[q], OpMax<uint32_t>(), lds, total); run[q] = e > pre ? e : pre; }
-    }
-    if (bq_list) {   // the bumped queries (k_v2_bq), unordered: one counter add per workgroup
-        uint32_t tot;
-        const uint32_t pre = block_exclusive((uint32_t)__popc(bqm), OpAdd<uint32_t>(), lds, tot);
-        if (threadIdx.x == 0) s_bq = tot ? atomicAdd(bq_cnt, tot) : 0u;
-        __syncthreads();
-        uint32_t k = s_bq + pre;
-#pragma unroll
-        for (int i = 0; i < V2_ITEMS; ++i)
-            if ((bqm >> i) & 1u) bq_list[k++] = (uint32_t)(base + i);
     }
     // rank directory: the chunk's running values from its first thread (RD_W / V2_ITEMS = 8 threads per chunk), the bit
     // planes OR-reduced over those 8 threads (threads past P contribute nothing)
@@ -1093,54 +1074,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_bcs_cols(uint32_t nbc, const uint6
 
 __device__ __forceinline__ uint32_t rd_cbc(const uint4 *rdir, uint32_t p);   // the rank directory, below
 
-// The O(1) query columns, part 1, a thread per bumped committed entry i (both orders at once):
-//   sorted entry i (segment, executeAt): ins[i] = first position of its segment with TxnId > executeAt, one event at
-//     ins[i] in ev1 (the inclusive prefix of ev1 over positions is g1: the sorted index after every entry whose
-//     executeAt is below TxnId(q), b0 included, since earlier segments' events all lie at or before q's segment start);
-//     for a Write, bsw[i] = lower_bound of executeAt + 1 over the segment's running maxima (position order);
-//   position-order entry i: one event in ev2 at the first position with TxnId > its running executeAt maximum (g2).
-__global__ __launch_bounds__(BLOCK) void k_v2_ins(uint32_t nbc, const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ svals,
-                                                  int rbits, const uint8_t *__restrict__ bc_kind, const uint64_t *__restrict__ bc_pm,
-                                                  const uint32_t *__restrict__ seg_start, const uint32_t *__restrict__ s_rank,
-                                                  const uint4 *__restrict__ rdir, uint32_t *__restrict__ ins,
-                                                  uint32_t *__restrict__ bsw, uint32_t *__restrict__ ev1, uint32_t *__restrict__ ev2)
-{
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= nbc) return;
-    const uint64_t key = skeys[i];
-    const uint32_t kind = bc_kind[svals[i]];
-    const uint64_t pm = bc_pm[i];
-    const uint32_t seg = (uint32_t)(key >> rbits), ex = (uint32_t)(key & ((1ull << rbits) - 1));
-    const uint32_t pseg = (uint32_t)(pm >> 32), mx = (uint32_t)pm - 1u;
-    const uint32_t s0 = seg_start[seg], s1 = seg_start[seg + 1];
-    const uint32_t ps0 = seg_start[pseg], ps1 = seg_start[pseg + 1];
-    const uint32_t a = lower_bound_u32(s_rank, s0, s1, ex);
-    const uint32_t b = lower_bound_u32(s_rank, ps0, ps1, mx);
-    ins[i] = a;
-    atomicAdd(&ev1[a], 1u);
-    atomicAdd(&ev2[b], 1u);
-    if (kind == 1) bsw[i] = lower_bound_lo32(bc_pm, rd_cbc(rdir, s0), rd_cbc(rdir, s1), ex + 1);
-}
-
-// Part 2, a thread per bumped query (pair whose executeAt differs from its TxnId, listed by k_v2_apply): its insert
-// position (first position after it with TxnId >= executeAt) and the predecessor index of its executeAt among the
-// segment's sorted bumped committed entries, so the count pass's lanes all take the same O(1) query.
-__global__ __launch_bounds__(BLOCK) void k_v2_bq(uint32_t nbq, const uint32_t *__restrict__ bq_list, const uint32_t *__restrict__ s_rank,
-                                                 const uint32_t *__restrict__ s_exec, const uint32_t *__restrict__ seg_incl,
-                                                 const uint32_t *__restrict__ seg_start, const uint4 *__restrict__ rdir,
-                                                 const uint32_t *__restrict__ bcs_exec, uint32_t *__restrict__ bq_pos,
-                                                 uint32_t *__restrict__ bq_i)
-{
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nbq) return;
-    const uint32_t p = bq_list[k];
-    const uint32_t S = s_exec[p], seg = seg_incl[p] - 1;
-    const uint32_t s0 = seg_start[seg], s1 = seg_start[seg + 1];
-    const uint32_t b0 = rd_cbc(rdir, s0), b1 = rd_cbc(rdir, s1);
-    bq_pos[p] = lower_bound_u32(s_rank, p + 1, s1, S);
-    bq_i[p] = lower_bound_u32(bcs_exec, b0, b1, S);
-}
-
 // The eight per-tile column scans of the multi-scan (7 counts: exclusive sums; the last-unbumped-committed-Write
 // column: exclusive max) in ONE launch, one workgroup per column, carrying the running value across chunks.
 constexpr int V2TS_ITEMS = 32;
@@ -1189,13 +1122,6 @@ struct V2View {
     const uint4 *tinfo;   // per txn: rank, executeAt rank, status | kind << 3
     const uint32_t *irec32;  // the count pass's inline records as u32 (IREC_W words per pair; word 7 = E | flag)
     const uint4 *rec;        // the count pass's 64-B records (runs; inline entries beyond IREC_N)
-    // O(1) query columns (k_v2_ins / k_v2_bq; null: the binary-search query v2_query):
-    const uint32_t *g1;      // [P + 1] per position q: b0 + #{bumped committed of q's segment with executeAt < TxnId(q)}
-    const uint32_t *g2;      // [P + 1] per position q: b0 + #{position-order bumped committed j of the segment whose
-                             //          running executeAt maximum is < TxnId(q)}
-    const uint32_t *ins;     // [nbc] per (segment, executeAt)-sorted entry: first position with TxnId > its executeAt
-    const uint32_t *bsw;     // [nbc] per sorted Write entry: first position-order index whose running max >= its executeAt
-    const uint32_t *bq_pos, *bq_i;   // [P] bumped queries (executeAt != TxnId): insert position, sorted predecessor index
 };
 
 struct Row { uint32_t c[8]; };
@@ -1276,49 +1202,6 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     return q;
 }
 
-// The same query from the precomputed columns: no binary search, five rounds of dependent loads (the search query walks
-// ~17 levels twice for a pair of a hot segment, whose bumped committed list is long: 73% of the count pass's cycles).
-//   i     = predecessor index of S among the segment's bumped committed by executeAt (g1[p], or bq_i[p] when S != TxnId);
-//   w     = the nearest Write at or below it (bcs_lastw), M_b = its executeAt, posM = ins[w] (first position with
-//           TxnId > M_b: TxnId >= M_b, as no TxnId equals another txn's executeAt on this path), bstart = bsw[w];
-//   M_u   = the last unbumped committed Write before pos (rank directory), posM = its position, bstart = g2[posM].
-__device__ __forceinline__ V2Query v2_query_fast(const V2View &v, uint32_t p)
-{
-    V2Query q;
-    const Row rpp = ld_row(v, p);
-    const uint32_t seg = v.seg_incl[p] - 1;
-    q.trank = v.s_rank[p];
-    const uint32_t S = v.s_exec[p];
-    q.info = v.s_info[p];
-    const uint32_t gi = v.g1[p];
-    q.s0 = v.seg_start[seg];
-    q.wk = witnesses(q.info >> 3);
-    q.wc = wk_classes(q.wk);
-    q.bq = S != q.trank;
-    uint32_t i = gi;
-    if (q.bq) { q.pos = v.bq_pos[p]; i = v.bq_i[p]; q.rp = ld_row(v, q.pos); }
-    else { q.pos = p; q.rp = rpp; }
-    // the candidates' loads before the segment's row is known (validity is checked against b0 below)
-    const uint32_t lu = q.rp.c[RW_LUCW];
-    const uint32_t w = i > 0 ? (uint32_t)v.bcs_lastw[i - 1] : 0u;
-    q.r0 = ld_row(v, q.s0);
-    const bool has_mu = lu > q.s0;
-    const uint32_t mu = has_mu ? v.s_rank[lu - 1] : 0u;
-    const uint32_t b0 = q.r0.c[RW_CBC];
-    const bool has_mb = w > b0;
-    uint32_t mb = 0, insw = 0, bsw = 0;
-    if (has_mb) { mb = v.bcs_exec[w - 1]; insw = v.ins[w - 1]; bsw = v.bsw[w - 1]; }
-    const uint32_t g2u = has_mu ? v.g2[lu - 1] : 0u;
-    q.has_m = has_mu || has_mb;
-    const bool from_b = has_mb && (!has_mu || mb > mu);
-    q.m = from_b ? mb : mu;
-    q.posm = !q.has_m ? q.s0 : from_b ? insw : lu - 1;
-    q.rm = q.posm == q.s0 ? q.r0 : ld_row(v, q.posm);
-    q.bend = q.rm.c[RW_CBC];
-    q.bstart = q.has_m ? min(from_b ? bsw : g2u, q.bend) : q.bend;
-    return q;
-}
-
 // per-pair results for the write pass, stored by pair index j (the write pass reads a txn's pairs contiguously):
 //   irec[j] (32 B, every pair): word 7 = E, | REC_INLINE_FLAG for an inline record (the mark pass reads this word;
 //           a separate 4-B E word per pair measured slower: the count pass's extra scattered store costs more than
@@ -1365,7 +1248,6 @@ __device__ unsigned long long *g_ct_prof;
 #define CT_PH(i) ((void)0)
 #endif
 
-template <bool FAST>
 __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
                                                   const RecOut &ro, uint32_t *__restrict__ bigflag)
 {
@@ -1374,7 +1256,7 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
 #endif
     CT_PH(0);
     const uint32_t j = v.perm[p];   // independent of the query chain: issued first
-    V2Query q = FAST ? v2_query_fast(v, p) : v2_query(v, p);
+    V2Query q = v2_query(v, p);
     CT_PH(1);
     uint32_t a[6] = {}, l[6] = {};
     uint64_t e = 0;
@@ -1483,7 +1365,6 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
 
 // Also: bigflag[T] = 1 for txns with a run record (they take the v2 tiers, the rest the stream pass) and per-block
 // entry totals (blk_e) for the batch's E.
-template <bool FAST>
 __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, const uint32_t *__restrict__ owner,
                                                     RecOut ro, uint32_t *__restrict__ bigflag,
                                                     uint64_t *__restrict__ blk_e)
@@ -1491,7 +1372,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, const ui
     __shared__ uint64_t lds[WAVES];
     size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t e = 0;
-    if (p < P) e = v2_count_one<FAST>(v, (uint32_t)p, owner, ro, bigflag);
+    if (p < P) e = v2_count_one(v, (uint32_t)p, owner, ro, bigflag);
     uint64_t total;
     block_exclusive(e, OpAdd<uint64_t>(), lds, total);
     if (threadIdx.x == 0) blk_e[blockIdx.x] = total;
@@ -1523,12 +1404,8 @@ struct V2Out {
     uint32_t *med_list, *big_list, *fb_list, *huge_list;
     uint64_t *gstat;         // [0] medium, [1] big, [2] count mismatches, [3] fallback txns, [4] fallback entries,
                              // [5] small, [6] huge (second big launch), [7] / [8] window tier (<= 8 / <= 16 keys)
-    const uint64_t *e_tot;   // the batch's E (device) and the capacity the E-sized buffers were allocated with:
-    uint64_t e_cap;          // a launch made before E reached the host does nothing when E exceeds it (redone exactly)
 };
 constexpr int GSTAT_N = 12;
-// E beyond the optimistic capacity of this call's E-sized buffers (a block-uniform test; null e_tot: E was exact)
-__device__ __forceinline__ bool e_over(const uint64_t *e_tot, uint64_t e_cap) { return e_tot && *e_tot > e_cap; }
 
 template <int MAXK>
 struct RunsT {
@@ -1745,7 +1622,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_medium(const uint64_t *__res
 {
     __shared__ uint64_t sbuf[WAVES][MED_E];
     __shared__ RunsT<MED_K> sruns[WAVES];
-    if (e_over(o.e_tot, o.e_cap)) return;
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint32_t cnt_list = (uint32_t)*cnt_dev;
     RunsT<MED_K> &R = sruns[wave];
@@ -2073,7 +1949,6 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(const uint32_t *__restrict_
                                                      const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ BigLds<CAP, NT> L;
-    if (e_over(o.e_tot, o.e_cap)) return;
     const uint32_t cnt_list = (uint32_t)o.gstat[CAP > BIG_E ? 6 : CAP == MED_CAP ? 0 : 1];
     for (uint32_t b = blockIdx.x; b < cnt_list; b += gridDim.x) {
         big_one<CAP, NT>(L, list[b], v, cnt, o);
@@ -2110,7 +1985,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
                                                        V2View v, const uint64_t *__restrict__ cnt, V2Out o)
 {
     __shared__ WinLds<WK> L;
-    if (e_over(o.e_tot, o.e_cap)) return;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const uint32_t n_list = (uint32_t)*cnt_dev;
     RunsT<WK> &R = L.R;
@@ -2505,17 +2379,13 @@ __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t
 // tier routing of the big txns (thread per list entry, one atomic per list per block). With ranks within 25 bits: the
 // window tier (<= 8 or <= 16 keys; gstat[7] / gstat[8]), else medium (E <= MED_E, <= MED_K keys) or the u32-record
 // block tier; with wider ranks: the u64 wave tier (E <= MED_E, <= MED_K keys) or the global path.
-// nbig_dev (non-null): the count on the device (the grid covers an upper bound; blocks past the count leave at once)
-__global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_t *__restrict__ nbig_dev,
-                                                    const uint32_t *__restrict__ blist,
+__global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_t *__restrict__ blist,
                                                     const uint32_t *__restrict__ key_off, const uint64_t *__restrict__ eb,
                                                     int big_ok, int win_ok, uint32_t *__restrict__ med_list,
                                                     uint32_t *__restrict__ big_list, uint32_t *__restrict__ fb_list,
                                                     uint32_t *__restrict__ w8_list, uint32_t *__restrict__ w16_list,
                                                     uint64_t *__restrict__ gstat)
 {
-    if (nbig_dev) nbig = *nbig_dev;
-    if (blockIdx.x * BLOCK >= nbig) return;   // block-uniform: before the block's reductions
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     bool med = false, bg = false, fb = false, w8 = false, w16 = false;
     uint32_t t = 0;
@@ -2556,9 +2426,6 @@ __global__ __launch_bounds__(BLOCK) void k_v3_route(uint32_t nbig, const uint32_
 }
 
 struct V3Big {
-    const uint32_t *nbig_dev;                 // the big-txn count on the device (persistent grid)
-    const uint64_t *e_tot;                    // E and the E-sized buffers' capacity (e_over)
-    uint64_t e_cap;
     const uint32_t *blist, *key_off;
     const uint32_t *psz;                      // per pair of a big txn: its entry count (k_v3_mark)
     const uint64_t *dB;                       // per txn: exclusive prefix of the big txns' E (TxnId scratch bases)
@@ -2574,8 +2441,6 @@ struct V3Big {
 // final arena / key_idx (the tiers then write the entries at arena_off[t] too: no copy into place afterwards)
 __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
 {
-    if (e_over(b.e_tot, b.e_cap)) return;
-    if (b.nbig_dev) nbig = *b.nbig_dev;
     const uint32_t lane = lane_id();
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6); i < nbig; i += gridDim.x * WAVES) {
@@ -2621,8 +2486,6 @@ struct V3Stream {
     uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's slot t * ST_N2, compacted by k_v3_ucompact
     uint64_t *err;                            // gather count mismatches
     uint32_t n, ntiles;
-    const uint64_t *e_tot;                    // E and the E-sized buffers' capacity (e_over)
-    uint64_t e_cap;
 };
 
 // inclusive prefix over the ST_G lanes of a group
@@ -2703,7 +2566,6 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     uint64_t ph[8];
 #endif
     ST_PH(0);
-    if (e_over(s.e_tot, s.e_cap)) return;
     __shared__ EntT ent[TT][ST_N2];
     __shared__ uint32_t kc[TT][ST_K];
     __shared__ uint32_t kbase[TT][ST_K];
@@ -2961,8 +2823,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
                                                        const uint32_t *__restrict__ dep_big,
                                                        const uint32_t *__restrict__ tmap, const uint32_t *__restrict__ n_dev,
                                                        uint32_t *__restrict__ dep_txn, const uint64_t *__restrict__ u_all,
-                                                       uint64_t *__restrict__ totals, const uint64_t *__restrict__ tot3,
-                                                       uint64_t e_cap)
+                                                       uint64_t *__restrict__ totals)
 {
     __shared__ uint64_t uo[BLOCK + 1];
     __shared__ uint64_t src[BLOCK];
@@ -2970,9 +2831,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
     const uint32_t tid = threadIdx.x;
     if (tid == 0 && blockIdx.x == gridDim.x - 1) {   // the batch totals beside the status words: one host copy
         totals[0] = arena_off[n]; totals[1] = kd_off[n]; totals[2] = u_all[n];
-        totals[3] = tot3[0]; totals[4] = tot3[1]; totals[5] = tot3[2];   // E, big txns, a 9-16-key big txn (mark)
     }
-    if (tot3[0] > e_cap) return;   // E beyond the optimistic capacity: redone once E is on the host
     if (tmap) n = *n_dev;
     const uint64_t total = u_off[n];
     const uint64_t c0 = (uint64_t)blockIdx.x * UC_CHUNK;
@@ -3407,12 +3266,12 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     bool flags_done = false;
     const uint64_t *sp_m4 = nullptr;   // mode 4: the sorted packed keys, unpacked by the CFK gather
     pp.sb = std::max(1, bits_for(hg[6]));   // bounds the key slot within a txn (hg[6] = OR of the key counts)
-    if (batch_sorted && pp.rk.bits <= 32 && !getenv("ACC_PAIR_UNPACKED")) {
+    if (batch_sorted && pp.rk.bits <= 32) {
         // pair index order is already TxnId order within every key: a stable keys-only sort of (key << 32 | pair index),
         // 8 B per element; the segment flags pass unpacks the permutation. Mode 4 packs (owner, slot) instead of the
         // pair index and the CFK gather unpacks it (one random read of the owner's record per pair, which carries
         // key_off[owner] for the pair index)
-        const bool m4 = bits_for((uint64_t)n - 1) + pp.sb <= 32 && !getenv("ACC_PAIR_NO_OWNER");
+        const bool m4 = bits_for((uint64_t)n - 1) + pp.sb <= 32;
         pp.mode = m4 ? 4 : 3;
         TxnInfoArgs ti;   // the txn records (k_txn_info) by the same launch: the ranks are final unless ties turn up
         ti.n = n; ti.status = status; ti.tl = tl; ti.tinfo = tinfo; ti.bigflag = bigflag;
@@ -3484,14 +3343,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N + 6);   // + the batch totals and E / big counts (k_v3_ucompact)
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
-    // the O(1) query columns' event counts (zeroed by the CFK gather) and the bumped-query list (k_v2_apply)
-    // tuning switch: the O(1) query columns (k_v2_ins / k_v2_bq and two more scanned columns) instead of the search
-    // query. Measured slower overall (config 2: 2.74 vs 2.58 ms, config 3: 24.3 vs 22.8): the count pass gains 0.1 / 1.2 ms,
-    // the extra column kernels cost 0.26 / 2.6 ms
-    const bool fastq = getenv("ACC_V2_FASTQ") != nullptr;
-    uint32_t *ev1 = ctx->get<uint32_t>("v2_ev1", P + V2_ITEMS + 1), *ev2 = ctx->get<uint32_t>("v2_ev2", P + V2_ITEMS + 1);
-    uint32_t *bq_list = ctx->get<uint32_t>("v2_bq_list", P);
-    uint32_t *bq_cnt = totals + 14;   // beside the totals and the staged error words: the same host copy
     auto build_columns = [&]() {
         if (!tinfo_done)
             launch(ctx, "txn_info", k_txn_info, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)rank, status,
@@ -3500,14 +3351,12 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         if (!sp_m4)
             launch(ctx, "pair_tinfo", k_pair_tinfo, dim3(gP), dim3(BLOCK), 0, P, (const uint32_t *)owner, (const uint4 *)tinfo, ptinfo);
         launch(ctx, "cfk_gather", k_cfk_gather4, dim3(nt), dim3(BLOCK), 0, P, ps.vals, (const uint4 *)ptinfo, sp_m4, pp.sb,
-               (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt,
-               fastq ? ev1 : (uint32_t *)nullptr, ev2, bq_cnt);
+               (const uint4 *)tinfo, seg_flag, s_rank, s_exec, s_info, ks ? pair_pos : (uint32_t *)nullptr, tile_sums, nt);
         launch(ctx, "v2_tile_scans", k_v2_tile_scans, dim3(NCNT), dim3(BLOCK), 0, (const uint32_t *)tile_sums, tile_pref, nt, totals);
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
                (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)totals, nt,
                rbits, cols, seg_incl, seg_start, (const uint32_t *)ps.vals, key_code, seg_key_buf, sp_m4, pp.rk, rk_mask,
-               bases, tot, 3u, gstat, (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4,
-               fastq ? bq_list : (uint32_t *)nullptr, bq_cnt);
+               bases, tot, 3u, gstat, (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
     };
     build_columns();
     // totals, g[4..6] staged by k_v2_apply, the bumped-query count
@@ -3565,30 +3414,6 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     vv.s_rank = s_rank; vv.s_exec = s_exec; vv.s_info = s_info; vv.rdir = cols.rdir; vv.tinfo = tinfo;
     vv.list_rank = cols.list_rank; vv.bases = bases; vv.bc_rank = cols.bc_rank; vv.bc_exec = cols.bc_exec; vv.bc_pm = bc_pm64;
     vv.bc_kind = cols.bc_kind; vv.bcs_exec = bcs_exec; vv.bcs_lastw = bcs_lw64;
-    if (fastq) {
-        // ---- the O(1) query columns: two binary searches per bumped committed entry and per bumped query (about a
-        // tenth of the pairs each, in dense waves) instead of two per pair in the count pass
-        const uint32_t nbq = htot[14];
-        uint32_t *ins = ctx->get<uint32_t>("v2_ins", nbc), *bsw = ctx->get<uint32_t>("v2_bsw", nbc);
-        if (nbc)
-            launch(ctx, "v2_ins", k_v2_ins, dim3(grid_for(nbc, BLOCK)), dim3(BLOCK), 0, nbc, (const uint64_t *)bcs.keys,
-                   (const uint32_t *)bcs.vals, rbits, (const uint8_t *)cols.bc_kind, (const uint64_t *)bc_pm64,
-                   (const uint32_t *)seg_start, (const uint32_t *)s_rank, (const uint4 *)cols.rdir, ins, bsw, ev1, ev2);
-        {   // g1 / g2: inclusive prefix sums of the events over positions 0..P, in place
-            const uint32_t *si[2] = { ev1, ev2 };
-            uint32_t *so[2] = { ev1, ev2 };
-            const size_t sn[2] = { P + 1, P + 1 };
-            scan_multi<uint32_t, OpAdd<uint32_t>>(ctx, 2, si, so, sn, false, (uint32_t *const *)nullptr);
-        }
-        uint32_t *bq_pos = ctx->get<uint32_t>("v2_bq_pos", P), *bq_i = ctx->get<uint32_t>("v2_bq_i", P);
-        if (nbq)
-            launch(ctx, "v2_bq", k_v2_bq, dim3(grid_for(nbq, BLOCK)), dim3(BLOCK), 0, nbq, (const uint32_t *)bq_list,
-                   (const uint32_t *)s_rank, (const uint32_t *)s_exec, (const uint32_t *)seg_incl, (const uint32_t *)seg_start,
-                   (const uint4 *)cols.rdir, (const uint32_t *)bcs_exec, bq_pos, bq_i);
-        vv.g1 = ev1; vv.g2 = ev2; vv.ins = ins; vv.bsw = bsw; vv.bq_pos = bq_pos; vv.bq_i = bq_i;
-        ctx->stat("keydeps.bumped_queries", nbq);
-    }
-
     // ---- count pass: per-pair records, big-txn flags, E
     if (P >= 0x80000000ull) fail(ACC_E_CAP, "n_pairs must be < 2^31 (count-pass record format)");
     RecOut ro;
@@ -3607,8 +3432,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ACC_HIP(hipMemsetAsync(ct_buf, 0, 8 * ct_rows * sizeof(unsigned long long), st));
     ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ct_prof), &ct_buf, sizeof ct_buf, 0, hipMemcpyHostToDevice, st));
 #endif
-    if (fastq) launch(ctx, "v2_count", k_v2_count<true>, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
-    else launch(ctx, "v2_count", k_v2_count<false>, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
 #ifdef ACC_PHASE_PROF
     {
         std::vector<unsigned long long> h(8 * ct_rows);
@@ -3630,10 +3454,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                 sum[7] / P);
     }
 #endif
-    const char *rc_env = getenv("ACC_ST_RAW");
-    const uint32_t raw_cap = rc_env ? (uint32_t)atoi(rc_env) : ST_RAW;
-    const char *ec_env = getenv("ACC_ST_ECAP");
-    const uint32_t e_cap = ec_env ? std::min<uint32_t>((uint32_t)atoi(ec_env), ST_N2) : ST_N2;
+    const uint32_t raw_cap = ST_RAW, e_cap = ST_N2;
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
@@ -3649,33 +3470,17 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     }
     // the big-txn list in txn order (k_v3_bigfill's per-txn ranges abut: a big txn writes its end where the next
     // txn's first pair starts, equal values when the next txn is big too)
-    uint32_t *nbig_dev = reinterpret_cast<uint32_t *>(tot + 1);
-    scan<uint32_t, OpAdd<uint32_t>>(ctx, bigflag, bpos, n, true, nbig_dev);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, bigflag, bpos, n, true, reinterpret_cast<uint32_t *>(tot + 1));
     uint32_t *blist = ctx->get<uint32_t>("v3_blist", n);
     launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bigflag,
            (const uint32_t *)bpos, blist);
-    // ---- E (dependency entries), the big-txn count and the 9-16-key flag reach the host here -- or, on a context that
-    // has seen a batch's E before (kd_e_hint), the build below is enqueued at once over E-sized buffers of that capacity,
-    // its grids persistent over the device-side counts, and the final sync checks E: a batch beyond the capacity (its
-    // launches did nothing) is built once more with the exact sizes. One host sync fewer per call in the steady state.
-    uint64_t E = 0;
-    uint32_t nbig = 0;
-    bool any16 = false;
-    // tuning switch ACC_KD_OPT: the optimistic build (one host sync fewer; measured no faster: config 2 2.74 vs 2.69 ms,
-    // the persistent grids sized for every txn cost what the sync saved)
-    bool exact = ctx->kd_e_hint == 0 || getenv("ACC_KD_OPT") == nullptr;
-    auto fetch_sizes = [&]() {
-        ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        ctx->sync();
-        E = ctx->pinned[0];
-        nbig = (uint32_t)ctx->pinned[1];
-        any16 = ctx->pinned[2] != 0;
-    };
-    if (exact) fetch_sizes();
-    else { E = ctx->kd_e_hint; nbig = n; any16 = true; }
+    // ---- E (dependency entries), the big-txn count and the 9-16-key flag reach the host here
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t E = ctx->pinned[0];
+    const uint32_t nbig = (uint32_t)ctx->pinned[1];
+    const bool any16 = ctx->pinned[2] != 0;
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
-    int32_t *arena = nullptr;
-    uint32_t *key_idx = nullptr, *dep_txn = nullptr;
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
     uint64_t *vdep_off = nullptr;
@@ -3683,7 +3488,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t nfb = 0, efb = 0, nmed = 0, nbig2 = 0;
     ctx->stat("keydeps.huge_txns", 0);
     V2Out wo{};
-    bool win_ok = false, side = false;
+    bool win_ok = false;
     uint64_t *vcnt = nullptr;
     uint32_t *med_list = nullptr, *big_list = nullptr, *fb_list = nullptr;
     // the sorting tiers: medium (<= MED_CAP raw entries), block (<= BIG_E), huge (<= HUGE_E, fed by the block tier)
@@ -3691,14 +3496,15 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         if (with_med)
             launch(ctx, "v2_write_med", k_v2_write_big<MED_CAP, BLOCK>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
                    (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
-        const char *bg_env = getenv("ACC_BIG_GRID");   // tuning: persistent grid of the BIG_E tier
-        const unsigned big_grid = bg_env ? (unsigned)std::max(1, atoi(bg_env)) : 1024u;
-        launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, 512>, dim3(std::min<unsigned>(nbig, big_grid)), dim3(512), 0,
+        launch(ctx, "v2_write_big", k_v2_write_big<BIG_E, 512>, dim3(std::min<unsigned>(nbig, 1024)), dim3(512), 0,
                (const uint32_t *)big_list, vv, (const uint64_t *)vcnt, wo);
         launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
                (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
     };
     uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);   // stream txns' TxnIds, slot t * ST_N2
+    int32_t *const arena = ctx->get<int32_t>("arena", P + E);
+    uint32_t *const key_idx = ctx->get<uint32_t>("key_idx", P);
+    uint32_t *const dep_txn = ctx->get<uint32_t>("dep_txn", std::max<uint64_t>(E, 1));
     // ---- big txns' arena / keys into place, TxnId offsets and compaction. With global-path txns (known only after
     // the tiers ran) this is redone once they are written, so the common case pays one host sync here.
     auto finish = [&]() {
@@ -3718,71 +3524,61 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v3_ucompact", k_v3_ucompact, dim3((unsigned)((E + UC_CHUNK - 1) / UC_CHUNK) + 1), dim3(BLOCK), 0, n,
                uo, (const uint64_t *)arena_off, (const uint64_t *)kd_off, (const uint32_t *)bigflag, key_off,
                (const uint64_t *)vdep_off, (const uint32_t *)dep_st, (const uint32_t *)dep_scr,
-               tmap, ne_cnt, dep_txn, (const uint64_t *)u_off, gstat + GSTAT_N, (const uint64_t *)tot, E);
+               tmap, ne_cnt, dep_txn, (const uint64_t *)u_off, gstat + GSTAT_N);
         ACC_HIP(hipMemcpyAsync(ctx->pinned, gstat, (GSTAT_N + 6) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         ctx->sync();
     };
-    while (true) {
-        arena = ctx->get<int32_t>("arena", P + E);
-        key_idx = ctx->get<uint32_t>("key_idx", P);
-        dep_txn = ctx->get<uint32_t>("dep_txn", std::max<uint64_t>(E, 1));
-        // ---- big txns: v2 tiers, headers / key indices / entries into the final arrays, TxnIds into scratch
-        if (nbig) {
-            const unsigned gB = (nbig + WAVES - 1) / WAVES;   // (an upper bound when !exact: the grids below persist)
-            vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
-            vcnt = ctx->get<uint64_t>("cnt", P);
-            uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
-            dep_scr = ctx->get<uint32_t>("v2_dep_scratch", std::max<uint64_t>(E, 1));
-            med_list = ctx->get<uint32_t>("v2_med_list", nbig);
-            big_list = ctx->get<uint32_t>("v2_big_list", nbig);
-            fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
-            V3Big bg;
-            bg.nbig_dev = exact ? nullptr : nbig_dev; bg.e_tot = exact ? nullptr : tot; bg.e_cap = E;
-            bg.blist = blist; bg.key_off = key_off; bg.psz = psz; bg.dB = dB; bg.arena_off = arena_off; bg.kd_off = kd_off;
-            bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.u_cnt = u_cnt; bg.arena = arena; bg.key_idx = key_idx;
-            const bool big_ok = rbits + 6 <= 31;
-            win_ok = big_ok && !getenv("ACC_NO_WIN");   // tuning switch: the sorting tiers instead of the window tier
-            launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig,
-                   exact ? (const uint32_t *)nullptr : nbig_dev, (const uint32_t *)blist,
-                   key_off, (const uint64_t *)eb, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
-                   ctx->get<uint32_t>("v2_w8_list", nbig), ctx->get<uint32_t>("v2_w16_list", nbig), gstat);
-            launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(exact ? gB : std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0, nbig, bg);
-            wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = arena_off; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
-            wo.arena = arena; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
-            wo.rec = rec; wo.irec32 = vv.irec32; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
-            wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
-            wo.e_tot = exact ? nullptr : tot; wo.e_cap = E;
-            // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run
-            // on a side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
-            side = !getenv("ACC_KD_SERIAL");   // tuning switch: the tiers in order on the main stream
-            if (side) {
-                ctx->fork(1);
-                ctx->launch_stream = ctx->aux[0];
-            }
-            if (win_ok) {
-                // the window tier takes every big txn of <= 16 keys; the sorting tiers run after the next host sync, only
-                // when it passed txns on or some txn has more keys (no launch without work)
-                launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
-                       (const uint32_t *)ctx->get<uint32_t>("v2_w8_list", nbig), (const uint64_t *)(gstat + 7), vv,
+    // ---- big txns: v2 tiers, headers / key indices / entries into the final arrays, TxnIds into scratch
+    if (nbig) {
+        const unsigned gB = (nbig + WAVES - 1) / WAVES;
+        vdep_off = ctx->get<uint64_t>("dep_off", P + 1);
+        vcnt = ctx->get<uint64_t>("cnt", P);
+        uint32_t *vcnz = ctx->get<uint32_t>("cnz", P + 1);
+        dep_scr = ctx->get<uint32_t>("v2_dep_scratch", std::max<uint64_t>(E, 1));
+        med_list = ctx->get<uint32_t>("v2_med_list", nbig);
+        big_list = ctx->get<uint32_t>("v2_big_list", nbig);
+        fb_list = ctx->get<uint32_t>("v2_fb_list", nbig);
+        V3Big bg;
+        bg.blist = blist; bg.key_off = key_off; bg.psz = psz; bg.dB = dB; bg.arena_off = arena_off; bg.kd_off = kd_off;
+        bg.vdep_off = vdep_off; bg.vcnt = vcnt; bg.vcnz = vcnz; bg.u_cnt = u_cnt; bg.arena = arena; bg.key_idx = key_idx;
+        const bool big_ok = rbits + 6 <= 31;
+        win_ok = big_ok && !(ctx->flags & ACC_OPT_NO_WINDOW_TIER);   // (testing: the sorting tiers instead)
+        launch(ctx, "v3_route", k_v3_route, dim3(grid_for(nbig, BLOCK)), dim3(BLOCK), 0, nbig, (const uint32_t *)blist,
+               key_off, (const uint64_t *)eb, (int)big_ok, (int)win_ok, med_list, big_list, fb_list,
+               ctx->get<uint32_t>("v2_w8_list", nbig), ctx->get<uint32_t>("v2_w16_list", nbig), gstat);
+        launch(ctx, "v3_bigfill", k_v3_bigfill, dim3(gB), dim3(BLOCK), 0, nbig, bg);
+        wo.key_off = key_off; wo.dep_off = vdep_off; wo.arena_off = arena_off; wo.cnz = vcnz; wo.txn_of_rank = txn_of_rank;
+        wo.arena = arena; wo.dep_scratch = dep_scr; wo.u_cnt = u_cnt; wo.gstat = gstat;
+        wo.rec = rec; wo.irec32 = vv.irec32; wo.med_list = med_list; wo.big_list = big_list; wo.fb_list = fb_list;
+        wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
+        // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run on a
+        // side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
+        ctx->fork(1);
+        ctx->launch_stream = ctx->aux[0];
+        if (win_ok) {
+            // the window tier takes every big txn of <= 16 keys; the sorting tiers run after the next host sync, only
+            // when it passed txns on or some txn has more keys (no launch without work)
+            launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
+                   (const uint32_t *)ctx->get<uint32_t>("v2_w8_list", nbig), (const uint64_t *)(gstat + 7), vv,
+                   (const uint64_t *)vcnt, wo);
+            // (> 8 keys is rare: a small persistent grid, launched only when the mark pass saw a big txn of 9-16 keys)
+            if (any16)
+                launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 256)), dim3(BLOCK), 0,
+                       (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
                        (const uint64_t *)vcnt, wo);
-                // (> 8 keys is rare: a small persistent grid, launched only when the mark pass saw a big txn of 9-16 keys)
-                if (any16)
-                    launch(ctx, "v2_write_win16", k_v2_write_win<16>, dim3(std::min<unsigned>(nbig, 256)), dim3(BLOCK), 0,
-                           (const uint32_t *)ctx->get<uint32_t>("v2_w16_list", nbig), (const uint64_t *)(gstat + 8), vv,
-                           (const uint64_t *)vcnt, wo);
-            } else if (big_ok) {
-                sort_tiers(true);
-            } else {
-                // ranks beyond 25 bits: u64 records in the wave tier (k_v3_route sends everything else to the global path)
-                launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
-                       (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
-            }
-            ctx->launch_stream = nullptr;
+        } else if (big_ok) {
+            sort_tiers(true);
+        } else {
+            // ranks beyond 25 bits: u64 records in the wave tier (k_v3_route sends everything else to the global path)
+            launch(ctx, "v2_write_medium", k_v2_write_medium, dim3(std::min<unsigned>(gB, 2048)), dim3(BLOCK), 0,
+                   (const uint64_t *)gstat, (const uint32_t *)med_list, vv, (const uint64_t *)vcnt, wo);
         }
-        // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch)
-        const char *nt_env = getenv("ACC_ST_NT");
-        int st_nt = nt_env ? atoi(nt_env) : 256;   // 256: co-schedules best with the 512-thread block tier (A/B)
-        if (rbits > 28 && st_nt > 512) st_nt = 512;
+        ctx->launch_stream = nullptr;
+    }
+    {
+        // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch); 256-thread
+        // workgroups co-schedule best with the 512-thread block tier (A/B)
+        constexpr int st_nt = 256;
         const uint32_t tt = (uint32_t)st_nt / ST_G;
         const uint32_t nblocks = (n + tt - 1) / tt;
         const uint32_t ntiles = nblocks * (uint32_t)(st_nt / 64);   // waves (phase-profile rows)
@@ -3791,23 +3587,14 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.irec = ro.irec;
         sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
         sp.dep_scr = dep_st; sp.n = n; sp.ntiles = ntiles;
-        sp.e_tot = exact ? nullptr : tot; sp.e_cap = E;
-        auto stream = [&](auto ent_tag) {
-            using EntT = decltype(ent_tag);
-            if constexpr (sizeof(EntT) == 4) {
-                if (st_nt == 1024) { launch(ctx, "v3_stream", k_v3_stream<EntT, 1024>, dim3(nblocks), dim3(1024), 0, sp); return; }
-            }
-            if (st_nt == 512) launch(ctx, "v3_stream", k_v3_stream<EntT, 512>, dim3(nblocks), dim3(512), 0, sp);
-            else launch(ctx, "v3_stream", k_v3_stream<EntT, 256>, dim3(nblocks), dim3(256), 0, sp);
-        };
 #ifdef ACC_PHASE_PROF
         const size_t prof_rows = (size_t)ntiles;
         unsigned long long *prof_buf = ctx->get<unsigned long long>("v3_prof", 8 * prof_rows);
         ACC_HIP(hipMemsetAsync(prof_buf, 0, 8 * prof_rows * sizeof(unsigned long long), st));
         ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_st_prof), &prof_buf, sizeof prof_buf, 0, hipMemcpyHostToDevice, st));
 #endif
-        if (rbits <= 28) stream(uint32_t{});
-        else stream(uint64_t{});
+        if (rbits <= 28) launch(ctx, "v3_stream", k_v3_stream<uint32_t, st_nt>, dim3(nblocks), dim3(st_nt), 0, sp);
+        else launch(ctx, "v3_stream", k_v3_stream<uint64_t, st_nt>, dim3(nblocks), dim3(st_nt), 0, sp);
 #ifdef ACC_PHASE_PROF
         {
             std::vector<unsigned long long> h(8 * prof_rows);
@@ -3825,22 +3612,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                     w, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
         }
 #endif
-        if (nbig && !getenv("ACC_KD_SERIAL")) ctx->join(1);
-        finish();
-        if (exact) break;
-        // the optimistic build: the real sizes came with the final copy (k_v3_ucompact's last block)
-        const uint64_t e_real = ctx->pinned[GSTAT_N + 3];
-        const uint32_t nbig_real = (uint32_t)ctx->pinned[GSTAT_N + 4];
-        const bool any16_real = ctx->pinned[GSTAT_N + 5] != 0;
-        if (e_real >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
-        exact = true;
-        if (e_real <= E) { E = e_real; nbig = nbig_real; any16 = any16_real; break; }
-        // beyond the capacity: every E-sized write was skipped; once more with the exact sizes
-        E = e_real; nbig = nbig_real; any16 = any16_real;
-        ACC_HIP(hipMemsetAsync(gstat, 0, GSTAT_N * sizeof(uint64_t), st));   // the skipped attempt's list counters
-        ctx->stat("keydeps.capacity_retry", 1);
     }
-    ctx->kd_e_hint = std::max(ctx->kd_e_hint, E + E / 16 + 1024);
+    if (nbig) ctx->join(1);
+    finish();
     if (ctx->pinned[5]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
     if (nbig && win_ok && (ctx->pinned[0] || ctx->pinned[1])) {
@@ -4675,7 +4449,7 @@ void keydeps_mixed(acc_ctx *ctx, const acc_range_batch_in *in, acc_keydeps_view 
     uint4 *prec = ctx->get<uint4>("mx_prec", 2 * NP + 2);
     if (NP) {
         const uint32_t pack = ks.rbits <= 31;
-        const bool defer = NP * 32 < 0xFFFFFFFFull && !getenv("ACC_MX_NO_DEFER");   // tuning switch: every query in place
+        const bool defer = NP * 32 < 0xFFFFFFFFull;
         if (!ks.v1) {
             // with deferral and packed single results the exact-replay scan only ever runs on segments of two or more
             // entries (pcount / pdefer; pemit replays only lanes of two or more entries)

@@ -416,8 +416,7 @@ __global__ __launch_bounds__(BLOCK) void k_lw_write(uint32_t n, const uint32_t *
                                                     const uint64_t *__restrict__ foff, const uint64_t *__restrict__ poff,
                                                     const uint64_t *__restrict__ coff, uint32_t *__restrict__ far,
                                                     uint32_t *__restrict__ prev, uint16_t *__restrict__ cur,
-                                                    const uint32_t *__restrict__ err, uint16_t *__restrict__ prev16,
-                                                    uint16_t *__restrict__ far16)
+                                                    const uint32_t *__restrict__ err)
 {
     const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
     if (i >= n || *err) return;   // an invalid graph (k_lw_count): its counts may exceed the lists, write nothing
@@ -435,26 +434,18 @@ __global__ __launch_bounds__(BLOCK) void k_lw_write(uint32_t n, const uint32_t *
         }
         const bool kc = keep && wd == wi, kp = keep && wd + 1 == wi, kf = keep && !kc && !kp;
         const uint64_t bf = __ballot(kf), bp = __ballot(kp), bc = __ballot(kc);
-        if (kf) {   // far16 (the LDS windowed walk, n <= 65535): u16 positions
-            if (far16) far16[wf + (uint64_t)__popcll(bf & lt)] = (uint16_t)p;
-            else far[wf + (uint64_t)__popcll(bf & lt)] = p;
-        }
-        if (kp) {   // prev16 (the LDS windowed walk): the offset in the previous window; else the position
-            if (prev16) prev16[wp + (uint64_t)__popcll(bp & lt)] = (uint16_t)(p - (wi - 1) * LW);
-            else prev[wp + (uint64_t)__popcll(bp & lt)] = p;
-        }
+        if (kf) far[wf + (uint64_t)__popcll(bf & lt)] = p;
+        if (kp) prev[wp + (uint64_t)__popcll(bp & lt)] = p;
         if (kc) cur[wc + (uint64_t)__popcll(bc & lt)] = (uint16_t)(p - wi * LW);
         wf += (uint64_t)__popcll(bf); wp += (uint64_t)__popcll(bp); wc += (uint64_t)__popcll(bc);
     }
 }
 
-__device__ __forceinline__ uint32_t lw_lds_ld(const uint32_t *p) { return *(const volatile uint32_t *)p; }
 
 struct LwLists {
     const uint64_t *foff, *poff, *coff;
     const uint32_t *far, *prev;
     const uint16_t *cur;
-    const uint16_t *prev16;   // the LDS windowed walk's prev lists (offsets in the previous window)
 };
 
 // The in-window walk with a pending set (both windowed walks, many deps per position): a lane scans its cur list 8
@@ -511,9 +502,8 @@ __device__ __forceinline__ void lw_walk_pend(bool valid, uint64_t ca, uint64_t c
     }
 }
 
-// one window step (launch w): block 0 walks window w, blocks 1.. gather the far maxima of window w + 1.
-// POLL = 1: the batch walk for long chains (a blocked lane re-reads one entry per round); else the sliding walk
-template <int POLL>
+// one window step (launch w): block 0 walks window w (the pending-set walk), blocks 1.. gather the far maxima of
+// window w + 1
 __global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists g, uint32_t *__restrict__ base,
                                                 uint32_t *__restrict__ lvlp, const uint32_t *__restrict__ order_exec,
                                                 uint32_t *__restrict__ level, uint32_t *__restrict__ max_level,
@@ -571,62 +561,8 @@ __global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists 
     uint64_t ca = 0, cb = 0;
     if (valid) { ca = g.coff[i] - cbase; cb = g.coff[i + 1] - cbase; }
     auto cur_at = [&](uint64_t e) -> uint32_t { return e < cin ? (uint32_t)CL[e] : (uint32_t)g.cur[cbase + e]; };
-    constexpr int LW_B = 8;
-    bool done = !valid;
-    uint32_t my = 0;
-    if (POLL != 1) {   // graphs with many in-window deps per position: the pending-set walk
-        lw_walk_pend(valid, ca, cb, m, L, tid, cur_at);
-        my = m;
-        done = true;
-    } else {
-        // few deps per position (long chains): batches of LW_B entries held in registers (read from LDS once per
-        // batch); a "full" round loads the levels of every entry left in the batch and consumes up to the first
-        // unpublished one, then the blocked lane polls that one entry only (one LDS load per round, so the waves
-        // spinning behind the chain leave the LDS to the wave advancing it) and goes back to a full round once it is
-        // published: a hop costs about two short rounds
-        uint64_t e = ca;             // first entry of the batch
-        uint32_t p[LW_B];
-        uint32_t np = 0, k = 0;      // batch size, entries consumed
-        bool full = true;
-        while (true) {
-            if (!done) {
-                if (k == np) {
-                    e += np;
-                    np = (uint32_t)min<uint64_t>(LW_B, cb - e);
-#pragma unroll
-                    for (int u = 0; u < LW_B; ++u) p[u] = (uint32_t)u < np ? cur_at(e + u) : 0u;
-                    k = 0;
-                    full = true;
-                }
-                if (full) {
-                    uint32_t v[LW_B];
-#pragma unroll
-                    for (int u = 0; u < LW_B; ++u) v[u] = ((uint32_t)u >= k && (uint32_t)u < np) ? lw_lds_ld(&L[p[u]]) : 1u;
-                    bool blocked = false;
-#pragma unroll
-                    for (int u = 0; u < LW_B; ++u) {
-                        if (blocked || (uint32_t)u < k || (uint32_t)u >= np) continue;
-                        if (!v[u]) { blocked = true; continue; }
-                        m = max(m, v[u]);
-                        ++k;
-                    }
-                    full = !blocked;
-                } else {
-                    uint32_t pk = p[0];
-#pragma unroll
-                    for (int u = 1; u < LW_B; ++u) if ((uint32_t)u == k) pk = p[u];
-                    const uint32_t v = lw_lds_ld(&L[pk]);
-                    if (v) { m = max(m, v); ++k; full = true; }
-                }
-                if (k == np && e + np >= cb) {
-                    *(volatile uint32_t *)&L[tid] = m + 1;
-                    my = m;
-                    done = true;
-                }
-            }
-            if (__all(done)) break;
-        }
-    }
+    lw_walk_pend(valid, ca, cb, m, L, tid, cur_at);
+    uint32_t my = m;
 #ifdef ACC_LV_PROF
     const unsigned long long t_2 = clock64();
 #endif
@@ -643,190 +579,6 @@ __global__ __launch_bounds__(LW) void k_lw_step(uint32_t n, uint32_t w, LwLists 
         g_lv_prof[3 * w] = t_1 - t_0; g_lv_prof[3 * w + 1] = t_2 - t_1; g_lv_prof[3 * w + 2] = ctot;
     }
 #endif
-    if (tid == 0) {
-        uint32_t mx = 0;
-        for (uint32_t q = 0; q < LW / 64; ++q) mx = max(mx, red[q]);
-        if (mx) atomicMax(max_level, mx);
-    }
-}
-
-// ---- LDS windowed walk (tier 3, n <= LV_W1_MAX_N; tuning tier, ACC_LV_W1): the windowed tier's split inside ONE
-// workgroup, every level in LDS (u16, level + 1, 0 = unpublished). Window u (LW positions, a lane per position):
-//   1. fold: each lane folds its position's deps in earlier windows (far: absolute u16 positions, prev: offsets in window
-//      u - 1), all published, reading its lists as aligned 16-B pieces, eight in flight;
-//   2. the window's in-window (cur) edges transposed in LDS (successor lists by counting sort: LDS atomics);
-//   3. push walk: a lane waits for its own pending-dependency counter to reach zero (one LDS word polled), then publishes
-//      its level and pushes level + 1 to its successors (atomic max) and decrements their counters. A hop costs one
-//      LDS atomic and one poll, however many deps a position has; a window whose cur edges exceed the successor buffer
-//      takes the pending-set walk instead.
-// Termination: the cur edges of a window form a DAG (earlier positions only), so some pending lane always has a zero
-// counter. Measured (config 5): the single-CU fold costs ~60K cycles per window, so this tier stays behind the
-// whole-graph LDS walk there (§7); kept as a tuning tier.
-constexpr uint32_t LV_W1_MAX_N = 32768;
-constexpr uint32_t LV_W1_SU = 36864;   // successor-list entries of a window in LDS (u16)
-constexpr uint32_t LV_W1_MIN = 0xFFFFFFFFu;   // not a default tier (see above)
-
-// max over list entries [a, b) of LV[base + entry] (level + 1, all published), the list read as aligned uint4 pieces
-// (the list buffers are padded by a piece), eight pieces per round
-__device__ __forceinline__ uint32_t lv_fold16(const uint16_t *__restrict__ list, uint64_t a, uint64_t b, const uint16_t *LV,
-                                              uint32_t base)
-{
-    uint32_t m = 0;
-    const uint4 *l4 = reinterpret_cast<const uint4 *>(list);
-    for (uint64_t c = a & ~7ull; c < b; c += 64) {
-        uint4 v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = c + 8u * q < b ? l4[(c >> 3) + q] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t w[4] = { v[q].x, v[q].y, v[q].z, v[q].w };
-#pragma unroll
-            for (int h = 0; h < 8; ++h) {
-                const uint64_t e = c + 8u * q + h;
-                if (e >= a && e < b) m = max(m, (uint32_t)LV[base + ((w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu)]);
-            }
-        }
-    }
-    return m;
-}
-
-__global__ __launch_bounds__(LW) void k_lv_win1(uint32_t n, LwLists g, const uint16_t *__restrict__ far16,
-                                                const uint32_t *__restrict__ order_exec, uint32_t *__restrict__ level,
-                                                uint32_t *__restrict__ max_level, const uint32_t *__restrict__ err)
-{
-    if (*err) return;   // invalid graph: the lists were not written (the host fails after the walk)
-    __shared__ __attribute__((aligned(16))) uint16_t LV[LV_W1_MAX_N];
-    __shared__ uint16_t SU[LV_W1_SU];
-    __shared__ uint32_t Mw[LW], dg[LW], so[LW + 1], fc[LW];
-    __shared__ uint32_t red[LW / 64];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    for (uint32_t i = tid; i < n; i += LW) LV[i] = 0;
-    const uint32_t nw = (n + LW - 1) / LW;
-    uint32_t my = 0;
-    __syncthreads();
-    for (uint32_t u = 0; u < nw; ++u) {
-        const uint32_t w0 = u * LW, wend = min(n, w0 + LW), i = w0 + tid;
-        const bool valid = i < wend;
-        const uint64_t cbase = g.coff[w0], ctot = g.coff[wend] - cbase;
-#ifdef ACC_LV_PROF
-        const unsigned long long t_0 = clock64();
-#endif
-        uint32_t m = 0;
-        if (valid && u >= 1) {
-            m = lv_fold16(far16, u >= 2 ? g.foff[i] : 0, u >= 2 ? g.foff[i + 1] : 0, LV, 0u);
-            m = max(m, lv_fold16(g.prev16, g.poff[i], g.poff[i + 1], LV, (u - 1) * LW));
-        }
-        uint64_t ca = 0, cb = 0;
-        if (valid) { ca = g.coff[i] - cbase; cb = g.coff[i + 1] - cbase; }
-        uint16_t *Lw = LV + w0;
-        const bool push = ctot <= LV_W1_SU;   // block-uniform
-        if (push) {
-            Mw[tid] = m;
-            dg[tid] = (uint32_t)(cb - ca);
-            fc[tid] = 0;
-            __syncthreads();
-            for (uint64_t e = ca; e < cb; e += 8) {   // eight list loads in flight, then their counter adds
-                uint32_t d[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) d[q] = e + q < cb ? (uint32_t)g.cur[cbase + e + q] : 0xFFFFFFFFu;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) if (d[q] != 0xFFFFFFFFu) atomicAdd(&fc[d[q]], 1u);
-            }
-            __syncthreads();
-            {   // exclusive scan of the successor counts -> so (and the fill cursors)
-                const uint32_t c = fc[tid];
-                uint32_t x = c;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-                    if (lane >= (uint32_t)d) x += y;
-                }
-                if (lane == 63) red[wave] = x;
-                __syncthreads();
-                uint32_t pre = 0;
-                for (uint32_t q = 0; q < wave; ++q) pre += red[q];
-                so[tid] = pre + x - c;
-                if (tid == LW - 1) so[LW] = pre + x;
-                __syncthreads();
-                fc[tid] = so[tid];
-            }
-            __syncthreads();
-            for (uint64_t e = ca; e < cb; e += 8) {
-                uint32_t d[8], slot[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) d[q] = e + q < cb ? (uint32_t)g.cur[cbase + e + q] : 0xFFFFFFFFu;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) slot[q] = d[q] != 0xFFFFFFFFu ? atomicAdd(&fc[d[q]], 1u) : 0u;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) if (d[q] != 0xFFFFFFFFu) SU[slot[q]] = (uint16_t)tid;
-            }
-            __syncthreads();
-        } else {
-            __syncthreads();
-        }
-#ifdef ACC_LV_PROF
-        const unsigned long long t_1 = clock64();
-#endif
-#ifdef ACC_LV_PROF
-        uint32_t rounds = 0;
-#endif
-        if (push) {
-            bool done = !valid;
-            while (true) {
-#ifdef ACC_LV_PROF
-                ++rounds;
-#endif
-                if (!done && *(volatile uint32_t *)&dg[tid] == 0) {
-                    const uint32_t lv = *(volatile uint32_t *)&Mw[tid];
-                    *(volatile uint16_t *)&Lw[tid] = (uint16_t)(lv + 1);
-                    m = lv;
-                    // the successor ids eight at a time, then their updates back to back (no-return LDS atomics,
-                    // executed in order per lane: a successor's max lands before its counter reaches zero)
-                    const uint32_t k1 = so[tid + 1];
-                    for (uint32_t k = so[tid]; k < k1; k += 8) {
-                        uint32_t sc[8];
-#pragma unroll
-                        for (int q = 0; q < 8; ++q) sc[q] = k + q < k1 ? (uint32_t)SU[k + q] : 0xFFFFFFFFu;
-#pragma unroll
-                        for (int q = 0; q < 8; ++q)
-                            if (sc[q] != 0xFFFFFFFFu) { atomicMax(&Mw[sc[q]], lv + 1); atomicSub(&dg[sc[q]], 1u); }
-                    }
-                    done = true;
-                }
-                if (__all(done)) break;
-            }
-        } else {
-            auto cur_at = [&](uint64_t e) -> uint32_t { return (uint32_t)g.cur[cbase + e]; };
-            lw_walk_pend(valid, ca, cb, m, Lw, tid, cur_at);
-        }
-        if (valid) {
-            level[order_exec[i]] = m;
-            my = max(my, m);
-        }
-        __syncthreads();   // window u published before window u + 1 folds it
-#ifdef ACC_LV_PROF
-        {   // rounds of the slowest wave and the window's level span
-            uint32_t lo = valid ? m : 0xFFFFFFFFu, hi = valid ? m : 0u, r = rounds;
-            for (int d = 32; d >= 1; d >>= 1) {
-                lo = min(lo, (uint32_t)__shfl_xor(lo, d, 64)); hi = max(hi, (uint32_t)__shfl_xor(hi, d, 64));
-                r = max(r, (uint32_t)__shfl_xor(r, d, 64));
-            }
-            if (lane == 0) { Mw[wave] = lo; dg[wave] = hi; fc[wave] = r; }
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t a = 0xFFFFFFFFu, b = 0, rr = 0;
-                for (uint32_t q = 0; q < LW / 64; ++q) { a = min(a, Mw[q]); b = max(b, dg[q]); rr = max(rr, fc[q]); }
-                g_lv_prof[3 * u] = t_1 - t_0; g_lv_prof[3 * u + 1] = clock64() - t_1;
-                g_lv_prof[3 * u + 2] = ((unsigned long long)rr << 32) | (b - a);
-            }
-            __syncthreads();
-        }
-#endif
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) my = max(my, (uint32_t)__shfl_xor(my, d, 64));
-    if (lane == 0) red[tid >> 6] = my;
-    __syncthreads();
     if (tid == 0) {
         uint32_t mx = 0;
         for (uint32_t q = 0; q < LW / 64; ++q) mx = max(mx, red[q]);
@@ -871,21 +623,18 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     uint32_t *err = ctx->get<uint32_t>("lv_err", 4);
     ACC_HIP(hipMemsetAsync(err, 0, 16, st));
     // tier: the whole graph's levels in one workgroup's LDS when they fit (chunk size CH: a power of two, three
-    // chunk slots beside the levels; ACC_LV_CH caps it, ACC_LV_WAVES forces the persistent-wave walk)
+    // chunk slots beside the levels; acc_opts.lv_chunk caps it)
     const uint32_t npad = (n + 7u) & ~7u;
     uint32_t ch = 0;
     // tiers: the whole-graph LDS walk (n <= 65535: config 5 0.89 ms, the windowed walk 1.07), the windowed walk beyond
-    // (ACC_LV_WIN forces it; the 1M-txn chain graph: 0.54 us per level, the persistent-wave walk 0.75); ACC_LV_WAVES:
-    // the persistent-wave walk
-    // tier 3 (tuning, ACC_LV_W1, n <= LV_W1_MAX_N): the LDS windowed walk in one workgroup; ACC_LV_LDS / ACC_LV_WIN /
-    // ACC_LV_WAVES select the other tiers
-    const bool w1 = n <= LV_W1_MAX_N && (n >= LV_W1_MIN || getenv("ACC_LV_W1")) && !getenv("ACC_LV_LDS") &&
-                    !getenv("ACC_LV_WIN") && !getenv("ACC_LV_WAVES");
-    const bool windowed = (n > LV_LDS_MAX_N || getenv("ACC_LV_WIN") || w1) && !getenv("ACC_LV_LDS") && !getenv("ACC_LV_WAVES");
-    if (!windowed && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && !getenv("ACC_LV_WAVES")) {
+    // (the 1M-txn chain graph: 0.264 us per level); acc_opts.lv_tier forces one (ACC_LV_WAVES: the persistent-wave walk)
+    const uint32_t tier = ctx->opts.lv_tier;
+    if (tier > ACC_LV_WAVES) fail(ACC_E_ARG, "acc_opts.lv_tier: unknown levelise tier");
+    const bool windowed = tier == ACC_LV_WINDOWED || (tier == ACC_LV_AUTO && n > LV_LDS_MAX_N);
+    if (!windowed && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && tier != ACC_LV_WAVES) {
         const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
         uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
-        if (const char *ce = getenv("ACC_LV_CH")) cap = std::min<uint32_t>(cap, (uint32_t)std::max(1, atoi(ce)));
+        if (ctx->opts.lv_chunk) cap = std::min<uint32_t>(cap, ctx->opts.lv_chunk);
         ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
     }
     if (!ch && !windowed) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
@@ -919,13 +668,12 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
         // An invalid graph (flagged by the count pass: decreasing offsets, a dep >= n) writes and walks nothing (the
         // later kernels read the flag first) and fails at the end
         const uint64_t cap = std::max<uint64_t>(E, 1);
-        uint32_t *far = w1 ? nullptr : ctx->get<uint32_t>("lw_far", cap), *prev = w1 ? nullptr : ctx->get<uint32_t>("lw_prev", cap);
-        uint16_t *cur = ctx->get<uint16_t>("lw_cur", cap), *prev16 = w1 ? ctx->get<uint16_t>("lw_prev16", cap + 8) : nullptr;
-        uint16_t *far16 = w1 ? ctx->get<uint16_t>("lw_far16", cap + 8) : nullptr;   // + a 16-B piece (k_lv_win1 reads)
+        uint32_t *far = ctx->get<uint32_t>("lw_far", cap), *prev = ctx->get<uint32_t>("lw_prev", cap);
+        uint16_t *cur = ctx->get<uint16_t>("lw_cur", cap);
         launch(ctx, "lv_fwrite", k_lw_write, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
                (const uint32_t *)pos, (const uint64_t *)foff, (const uint64_t *)poff, (const uint64_t *)coff, far, prev, cur,
-               (const uint32_t *)err, prev16, far16);
-        ls.foff = foff; ls.poff = poff; ls.coff = coff; ls.far = far; ls.prev = prev; ls.cur = cur; ls.prev16 = prev16;
+               (const uint32_t *)err);
+        ls.foff = foff; ls.poff = poff; ls.coff = coff; ls.far = far; ls.prev = prev; ls.cur = cur;
         uint32_t *base = ctx->get<uint32_t>("lw_base", n), *lvlp = ctx->get<uint32_t>("lw_lvlp", n);
         const uint32_t nw = (n + LW - 1) / LW;
 #ifdef ACC_LV_PROF
@@ -934,25 +682,14 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
             ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lv_prof), &pb, sizeof pb, 0, hipMemcpyHostToDevice, st));
         }
 #endif
-        // the pending-set walk (the 1M-txn test graph: 0.264 us per level; the batch walk, ACC_LV_POLL=1: 0.543)
-        int poll = 8;
-        if (const char *pe = getenv("ACC_LV_POLL")) poll = atoi(pe) == 1 ? 1 : 8;   // tuning switch
-        ctx->stat("levelise.poll", (uint64_t)poll);
-        if (w1)
-            launch(ctx, "lv_walk_w1", k_lv_win1, dim3(1), dim3(LW), 0, n, ls, (const uint16_t *)far16,
-                   (const uint32_t *)order_exec, level, maxl, (const uint32_t *)err);
-        for (uint32_t w = 0; !w1 && w < nw; ++w) {
+        for (uint32_t w = 0; w < nw; ++w) {
             // gatherers only when window w + 1 exists and has far deps (w + 1 >= 2)
             const uint32_t nxt = (w + 2 <= nw && w + 1 >= 2) ? std::min<uint32_t>(LW, n - (w + 1) * LW) : 0u;
             const unsigned gb = 1 + (nxt + LW_GW - 1) / LW_GW;
-            if (poll == 1)
-                launch(ctx, "lv_walk_win", k_lw_step<1>, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec,
-                       level, maxl, (const uint32_t *)err);
-            else
-                launch(ctx, "lv_walk_win", k_lw_step<8>, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec,
-                       level, maxl, (const uint32_t *)err);
+            launch(ctx, "lv_walk_win", k_lw_step, dim3(gb), dim3(LW), 0, n, w, ls, base, lvlp, (const uint32_t *)order_exec,
+                   level, maxl, (const uint32_t *)err);
         }
-        ctx->stat("levelise.lds_tier", w1 ? 3 : 2);
+        ctx->stat("levelise.lds_tier", 2);
 #ifdef ACC_LV_PROF
         {
             std::vector<unsigned long long> h(3 * (size_t)nw);
@@ -960,13 +697,8 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
             ACC_HIP(hipMemcpyAsync(h.data(), pb, h.size() * 8, hipMemcpyDeviceToHost, st));
             ACC_HIP(hipStreamSynchronize(st));
             double a = 0, b = 0, c = 0;
-            for (uint32_t q = 0; q < nw; ++q) { a += h[3 * q]; b += h[3 * q + 1]; c += w1 ? (h[3 * q + 2] & 0xFFFFFFFFu) : h[3 * q + 2]; }
-            if (w1) {
-                double r = 0;
-                for (uint32_t q = 0; q < nw; ++q) r += (double)(h[3 * q + 2] >> 32);
-                fprintf(stderr, "[lw_prof] w1: avg rounds of the slowest wave per window %.0f (level span in cur-entries slot)\n", r / nw);
-            }
-            fprintf(stderr, "[lw_prof] %s windows=%u avg cycles per window: lists+fold %.0f walk %.0f | cur entries %.0f\n", w1 ? "w1" : "step", nw,
+            for (uint32_t q = 0; q < nw; ++q) { a += h[3 * q]; b += h[3 * q + 1]; c += h[3 * q + 2]; }
+            fprintf(stderr, "[lw_prof] step windows=%u avg cycles per window: lists+fold %.0f walk %.0f | cur entries %.0f\n", nw,
                     a / nw, b / nw, c / nw);
         }
 #endif

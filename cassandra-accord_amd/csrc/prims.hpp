@@ -325,6 +325,25 @@ void scan(acc_ctx *ctx, const T *in, T *out, size_t n, bool exclusive, T *total_
     scan_multi<T, Op>(ctx, 1, &in, &out, &n, exclusive, tot);
 }
 
+// u64 total of a u32 array (one atomic per block): the guard beside a u32 scan whose total may pass 2^32 - 1
+static __global__ __launch_bounds__(BLOCK) void k_sum_u32(const uint32_t *__restrict__ in, size_t n, uint64_t *__restrict__ out)
+{
+    __shared__ uint64_t lds[WAVES];
+    uint64_t x = 0;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) x += in[i];
+    uint64_t total;
+    block_exclusive(x, OpAdd<uint64_t>(), lds, total);
+    if (threadIdx.x == 0 && total) atomicAdd((unsigned long long *)out, (unsigned long long)total);
+}
+
+// enqueues the u64 total of in[0, n) into *out (zeroed first); the caller reads it at its next sync
+inline void sum_u32(acc_ctx *ctx, const uint32_t *in, size_t n, uint64_t *out)
+{
+    ACC_HIP(hipMemsetAsync(out, 0, 8, ctx->stream));
+    if (n) launch(ctx, "sum_u32", k_sum_u32, dim3((unsigned)std::min<size_t>(1024, (n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                  in, n, out);
+}
+
 // ---------------------------------------------------------------- bit compaction plan
 
 // pext(w, mask) as a list of contiguous runs; masks with more than MAX_RUNS runs fall back to the
@@ -381,11 +400,7 @@ constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = BLOCK * RS_ITEMS;
 constexpr int RS_ITEMS_S = 4;                      // one-sweep tiles of mid-size sorts
 constexpr int RS_TILE_S = BLOCK * RS_ITEMS_S;
-inline size_t rs_small_n()                         // ACC_RS_SMALL_N: tuning switch (0: never)
-{
-    static const size_t v = getenv("ACC_RS_SMALL_N") ? (size_t)atoll(getenv("ACC_RS_SMALL_N")) : (size_t)256 << 10;
-    return v;
-}
+constexpr size_t rs_small_n() { return (size_t)256 << 10; }   // below: the one-sweep sort's 1,024-element tiles
 
 static __global__ __launch_bounds__(BLOCK) void k_rs_hist(const uint64_t *__restrict__ keys, size_t n, int shift,
                                                    uint32_t *__restrict__ hist, uint32_t ntiles)
@@ -755,8 +770,7 @@ static inline Sorted radix_sort(acc_ctx *ctx, const char *tag, const uint64_t *k
         else launch(ctx, "iota", k_iota, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, v[0], n);
         return { k[0], v[0] };
     }
-    static const bool legacy = getenv("ACC_RS_LEGACY") != nullptr;   // tuning switch: three launches per pass
-    if (n < (size_t)OS_VAL && passes <= OS_MAXP && !legacy) {
+    if (n < (size_t)OS_VAL && passes <= OS_MAXP) {   // else (very large sorts): three launches per pass below
         const bool small = n < rs_small_n();
         const uint32_t ntiles = (uint32_t)((n + (small ? RS_TILE_S : RS_TILE) - 1) / (small ? RS_TILE_S : RS_TILE));
         const size_t words = (size_t)passes * 256 + passes + (size_t)passes * ntiles * 256;

@@ -1290,7 +1290,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     o.s_dep = ctx->get<uint32_t>("rd_s_dep", E);
     const uint32_t *tl_sorted = ts.vals;
     // 32-bit sort keys in the lane-group tiers: range ids (< NE) and TxnId positions (< n) within 26 bits
-    const bool narrow = NE < (1u << 26) && n < (1u << 26) && !getenv("ACC_RD_WIDE");   // tuning switch: 64-bit sorts
+    const bool narrow = NE < (1u << 26) && n < (1u << 26) && !(ctx->flags & ACC_OPT_RD_WIDE_SORT);   // (testing: 64-bit sorts throughout)
     ctx->stat("rangedeps.narrow_sorts", narrow ? 1 : 0);
     // tiers own disjoint txns (disjoint scratch): LDS workgroup tiers on side stream 1, 16-lane groups on side
     // stream 0, waves on the main stream, all concurrently

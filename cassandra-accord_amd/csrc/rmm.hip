@@ -587,4 +587,263 @@ void rangedeps_stab(acc_ctx *ctx, const acc_rmm_batch *rd, const acc_stab_in *q,
     *out = v;
 }
 
+// ---------------------------------------------------------------- without (RelationMultiMap.remove)
+// RelationMultiMap.remove (utils/RelationMultiMap.java:843-905) of every group: a value is removed when its TxnId is in
+// the group's set a or set b (Deps::contains = KeyDeps.contains || RangeDeps.contains, primitives/Deps.java:107-110, each
+// Arrays.binarySearch: Timestamp.compareTo == 0). The Java builds remapValue by counting the kept values in order
+// (:855-860), then walks keysToValues once (:877-891); here both are exclusive scans of keep flags: over the values
+// (the remap) and over the int positions (the new end offsets and entry slots), so every output is one thread's write.
+
+namespace {
+
+struct WoSet {
+    const uint64_t *off, *m, *l;
+    const int32_t *n;
+};
+
+struct Wo {
+    uint32_t ng;
+    const uint64_t *key_off, *val_off, *k2v_off;
+    const int32_t *k2v;
+    uint64_t NK, NV, NO;
+    const uint64_t *tm, *tl;   // the half's TxnIds [NV]
+    const int32_t *tn;
+    WoSet a, b;
+    uint32_t *keep, *ekeep;           // [NV + 1], [NO + 1]
+    const uint32_t *keep_x, *ekeep_x; // their exclusive scans
+    uint8_t *kind;
+    uint64_t *c_keys, *c_vals, *c_k2v, *cnt;
+    const uint64_t *key_out, *val_out, *k2v_out;
+    uint32_t *key_idx, *val_idx;
+    int32_t *out;
+};
+
+// Timestamp.compareTo (primitives/Timestamp.java:208-217): msb, then lsb & IDENTITY_LSB (lowHlc, identity flags), node
+__device__ __forceinline__ int wo_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn)
+{
+    if (am != bm) return am < bm ? -1 : 1;
+    const uint64_t a1 = al & 0xFFFFFFFFFFFF001EULL, b1 = bl & 0xFFFFFFFFFFFF001EULL;
+    if (a1 != b1) return a1 < b1 ? -1 : 1;
+    if (an != bn) return an < bn ? -1 : 1;
+    return 0;
+}
+
+__device__ __forceinline__ bool wo_contains(const WoSet &s, uint64_t g, uint64_t m, uint64_t l, int32_t n)
+{
+    if (!s.off) return false;
+    uint64_t lo = s.off[g], hi = s.off[g + 1];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const int c = wo_cmp(s.m[mid], s.l[mid], s.n[mid], m, l, n);
+        if (c == 0) return true;
+        if (c < 0) lo = mid + 1; else hi = mid;
+    }
+    return false;
+}
+
+// a set's offsets monotone and its TxnIds strictly ascending within each group (err bit 4)
+__global__ __launch_bounds__(BLOCK) void k_wo_set_check(uint32_t ng, WoSet s, uint64_t ns, uint64_t *__restrict__ err)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    bool bad = false;
+    if (q < ng && s.off[q + 1] < s.off[q]) bad = true;
+    if (q < ns) {
+        const uint64_t g = ub64(s.off, 0, (uint64_t)ng + 1, q) - 1;
+        if (q > s.off[g] && wo_cmp(s.m[q - 1], s.l[q - 1], s.n[q - 1], s.m[q], s.l[q], s.n[q]) >= 0) bad = true;
+    }
+    if (__ballot(bad) && bad) atomicOr((unsigned long long *)err, 4ull);
+}
+
+// per value: kept unless in set a or b (the remove predicate, :855-860)
+__global__ __launch_bounds__(BLOCK) void k_wo_keep(Wo w)
+{
+    const uint64_t s = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (s > w.NV) return;
+    if (s == w.NV) { w.keep[s] = 0; return; }
+    const uint64_t g = ub64(w.val_off, 0, (uint64_t)w.ng + 1, s) - 1;
+    const uint64_t m = w.tm[s], l = w.tl[s];
+    const int32_t n = w.tn[s];
+    w.keep[s] = (wo_contains(w.a, g, m, l, n) || wo_contains(w.b, g, m, l, n)) ? 0u : 1u;
+}
+
+// per int position: 1 for an entry whose TxnId is kept (header slots 0)
+__global__ __launch_bounds__(BLOCK) void k_wo_ekeep(Wo w)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (q > w.NO) return;
+    if (q == w.NO) { w.ekeep[q] = 0; return; }
+    const uint64_t g = ub64(w.k2v_off, 0, (uint64_t)w.ng + 1, q) - 1;
+    const uint64_t nk = w.key_off[g + 1] - w.key_off[g], local = q - w.k2v_off[g];
+    w.ekeep[q] = local >= nk ? w.keep[w.val_off[g] + (uint32_t)w.k2v[q]] : 0u;
+}
+
+// per group: the Java's three returns (:844-845 isEmpty -> from; :862-863 nothing removed -> from; :865-866 all removed
+// -> none) and the output sizes
+__global__ __launch_bounds__(BLOCK) void k_wo_group(Wo w)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t kd = 3;
+    if (g < w.ng) {
+        const uint64_t nk = w.key_off[g + 1] - w.key_off[g], nv = w.val_off[g + 1] - w.val_off[g];
+        const uint64_t no = w.k2v_off[g + 1] - w.k2v_off[g];
+        const uint64_t kept = w.keep_x[w.val_off[g + 1]] - w.keep_x[w.val_off[g]];
+        const uint64_t kept_e = w.ekeep_x[w.k2v_off[g + 1]] - w.ekeep_x[w.k2v_off[g]];
+        kd = (no == nk || kept == nv) ? ACC_WITHOUT_FROM : kept == 0 ? ACC_WITHOUT_NONE : ACC_WITHOUT_NEW;
+        w.kind[g] = (uint8_t)kd;
+        w.c_keys[g] = kd == ACC_WITHOUT_NONE ? 0 : nk;
+        w.c_vals[g] = kd == ACC_WITHOUT_FROM ? nv : kd == ACC_WITHOUT_NONE ? 0 : kept;
+        w.c_k2v[g] = kd == ACC_WITHOUT_FROM ? no : kd == ACC_WITHOUT_NONE ? 0 : nk + kept_e;
+    }
+    for (uint32_t k = 0; k < 3; ++k) {
+        const uint64_t b = __ballot(kd == k);
+        if (lane_id() == 0 && b) atomicAdd((unsigned long long *)&w.cnt[k], (unsigned long long)__popcll(b));
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_wo_keys(Wo w)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= w.NK) return;
+    const uint64_t g = ub64(w.key_off, 0, (uint64_t)w.ng + 1, i) - 1;
+    if (w.kind[g] != ACC_WITHOUT_NONE) w.key_idx[w.key_out[g] + (i - w.key_off[g])] = (uint32_t)(i - w.key_off[g]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_wo_vals(Wo w)
+{
+    const uint64_t s = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= w.NV) return;
+    const uint64_t g = ub64(w.val_off, 0, (uint64_t)w.ng + 1, s) - 1;
+    const uint32_t local = (uint32_t)(s - w.val_off[g]);
+    const uint8_t kd = w.kind[g];
+    if (kd == ACC_WITHOUT_FROM) w.val_idx[w.val_out[g] + local] = local;
+    else if (kd == ACC_WITHOUT_NEW && w.keep[s]) w.val_idx[w.val_out[g] + (w.keep_x[s] - w.keep_x[w.val_off[g]])] = local;
+}
+
+// the new keysToValues (:874-894): end offset of key k = nk + kept entries before its old end; entry = remapValue
+__global__ __launch_bounds__(BLOCK) void k_wo_ints(Wo w)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= w.NO) return;
+    const uint64_t g = ub64(w.k2v_off, 0, (uint64_t)w.ng + 1, q) - 1;
+    const uint8_t kd = w.kind[g];
+    if (kd == ACC_WITHOUT_NONE) return;
+    const uint64_t o0 = w.k2v_off[g], local = q - o0, base = w.k2v_out[g];
+    const int32_t x = w.k2v[q];
+    if (kd == ACC_WITHOUT_FROM) { w.out[base + local] = x; return; }
+    const uint64_t nk = w.key_off[g + 1] - w.key_off[g];
+    if (local < nk) {
+        w.out[base + local] = (int32_t)(nk + (w.ekeep_x[o0 + (uint32_t)x] - w.ekeep_x[o0]));
+    } else if (w.ekeep[q]) {
+        const uint64_t v0 = w.val_off[g];
+        w.out[base + nk + (w.ekeep_x[q] - w.ekeep_x[o0])] = (int32_t)(w.keep_x[v0 + (uint32_t)x] - w.keep_x[v0]);
+    }
+}
+
+}  // namespace
+
+// the without of one half held in device memory (layout already valid; sets sorted); results in the context's "wo_*"
+// buffers under the caller's namespace
+void rmm_without_dev(acc_ctx *ctx, uint32_t ng, const acc_rmm_in &h, uint64_t NK, uint64_t NV, uint64_t NO,
+                     const acc_txn_sets *sa, const acc_txn_sets *sb, acc_without_view *out)
+{
+    hipStream_t st = ctx->stream;
+    if (NK >= 0xFFFFFFFFull || NV >= 0xFFFFFFFFull || NO >= 0xFFFFFFFFull) fail(ACC_E_CAP, "deps batch too large");
+    Wo w{};
+    w.ng = ng; w.key_off = h.key_off; w.val_off = h.val_off; w.k2v_off = h.k2v_off; w.k2v = h.k2v;
+    w.NK = NK; w.NV = NV; w.NO = NO;
+    w.tm = h.txn.msb; w.tl = h.txn.lsb; w.tn = h.txn.node;
+    w.a = WoSet{ sa ? sa->off : nullptr, sa ? sa->txn.msb : nullptr, sa ? sa->txn.lsb : nullptr, sa ? sa->txn.node : nullptr };
+    w.b = WoSet{ sb ? sb->off : nullptr, sb ? sb->txn.msb : nullptr, sb ? sb->txn.lsb : nullptr, sb ? sb->txn.node : nullptr };
+    w.keep = ctx->get<uint32_t>("wo_keep", NV + 1);
+    w.ekeep = ctx->get<uint32_t>("wo_ekeep", NO + 1);
+    uint32_t *keep_x = ctx->get<uint32_t>("wo_keep_x", NV + 1), *ekeep_x = ctx->get<uint32_t>("wo_ekeep_x", NO + 1);
+    w.keep_x = keep_x; w.ekeep_x = ekeep_x;
+    w.kind = ctx->get<uint8_t>("wo_kind", (size_t)ng + 1);
+    w.c_keys = ctx->get<uint64_t>("wo_c_keys", (size_t)ng + 1);
+    w.c_vals = ctx->get<uint64_t>("wo_c_vals", (size_t)ng + 1);
+    w.c_k2v = ctx->get<uint64_t>("wo_c_k2v", (size_t)ng + 1);
+    w.cnt = ctx->get<uint64_t>("wo_cnt", 4);
+    ACC_HIP(hipMemsetAsync(w.cnt, 0, 32, st));
+    launch(ctx, "wo_keep", k_wo_keep, dim3(grid_for(NV + 1, BLOCK)), dim3(BLOCK), 0, w);
+    launch(ctx, "wo_ekeep", k_wo_ekeep, dim3(grid_for(NO + 1, BLOCK)), dim3(BLOCK), 0, w);
+    {
+        const uint32_t *si[2] = { w.keep, w.ekeep };
+        uint32_t *so[2] = { keep_x, ekeep_x };
+        const size_t sn[2] = { NV + 1, NO + 1 };
+        scan_multi<uint32_t, OpAdd<uint32_t>>(ctx, 2, si, so, sn, true, (uint32_t *const *)nullptr);
+    }
+    if (ng) launch(ctx, "wo_group", k_wo_group, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, w);
+    uint64_t *key_out = ctx->get<uint64_t>("wo_key_out", (size_t)ng + 1);
+    uint64_t *val_out = ctx->get<uint64_t>("wo_val_out", (size_t)ng + 1);
+    uint64_t *k2v_out = ctx->get<uint64_t>("wo_k2v_out", (size_t)ng + 1);
+    {
+        const uint64_t *si[3] = { w.c_keys, w.c_vals, w.c_k2v };
+        uint64_t *so[3] = { key_out, val_out, k2v_out }, *tot[3] = { key_out + ng, val_out + ng, k2v_out + ng };
+        const size_t sn[3] = { ng, ng, ng };
+        scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 3, si, so, sn, true, tot);
+    }
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, key_out + ng, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, val_out + ng, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 2, k2v_out + ng, 8, hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned + 3, w.cnt, 24, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    const uint64_t TK = ctx->pinned[0], TV = ctx->pinned[1], TO = ctx->pinned[2];
+    const uint64_t nf = ctx->pinned[3], nn = ctx->pinned[4], nw = ctx->pinned[5];
+    w.key_out = key_out; w.val_out = val_out; w.k2v_out = k2v_out;
+    w.key_idx = ctx->get<uint32_t>("wo_key_idx", TK + 1);
+    w.val_idx = ctx->get<uint32_t>("wo_val_idx", TV + 1);
+    w.out = ctx->get<int32_t>("wo_k2v", TO + 1);
+    if (NK) launch(ctx, "wo_keys", k_wo_keys, dim3(grid_for(NK, BLOCK)), dim3(BLOCK), 0, w);
+    if (NV) launch(ctx, "wo_vals", k_wo_vals, dim3(grid_for(NV, BLOCK)), dim3(BLOCK), 0, w);
+    if (NO) launch(ctx, "wo_ints", k_wo_ints, dim3(grid_for(NO, BLOCK)), dim3(BLOCK), 0, w);
+    ctx->sync();
+    ctx->stat("without.from", nf);
+    ctx->stat("without.none", nn);
+    ctx->stat("without.new", nw);
+    *out = acc_without_view{ acc_slice_view{ ng, TK, TV, TO, key_out, w.key_idx, val_out, w.val_idx, k2v_out, w.out },
+                             w.kind, nf, nn, nw };
+}
+
+// The ABI form: one deps half per group from caller memory, validated (layout as acc_rmm_slice; sets sorted unique).
+void rmm_without(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ts_cols *txn, const acc_txn_sets *set_a,
+                 const acc_txn_sets *set_b, acc_without_view *out)
+{
+    if (!out || !txn) fail(ACC_E_ARG, "null argument");
+    Batch b = stage_batch(ctx, in, false);
+    hipStream_t st = ctx->stream;
+    acc_rmm_in h{};
+    h.key_off = b.key_off; h.val_off = b.val_off; h.k2v_off = b.k2v_off; h.k2v = b.k2v;
+    h.txn.msb = stage_in(ctx, "wo_tm", txn->msb, b.NV, in->mem);
+    h.txn.lsb = stage_in(ctx, "wo_tl", txn->lsb, b.NV, in->mem);
+    h.txn.node = stage_in(ctx, "wo_tn", txn->node, b.NV, in->mem);
+    acc_txn_sets sets[2];
+    const acc_txn_sets *src[2] = { set_a, set_b };
+    uint64_t ns[2] = { 0, 0 };
+    const char *nm[2][4] = { { "wo_a_off", "wo_a_m", "wo_a_l", "wo_a_n" }, { "wo_b_off", "wo_b_m", "wo_b_l", "wo_b_n" } };
+    for (int k = 0; k < 2; ++k) {
+        sets[k] = acc_txn_sets{};
+        if (!src[k] || !src[k]->off) continue;
+        sets[k].off = stage_in(ctx, nm[k][0], src[k]->off, (size_t)b.ng + 1, in->mem);
+        ACC_HIP(hipMemcpyAsync(ctx->pinned + k, sets[k].off + b.ng, 8, hipMemcpyDeviceToHost, st));
+    }
+    ctx->sync();
+    for (int k = 0; k < 2; ++k) if (sets[k].off) ns[k] = ctx->pinned[k];
+    uint64_t *err = ctx->get<uint64_t>("wo_err", 1);
+    ACC_HIP(hipMemsetAsync(err, 0, 8, st));
+    for (int k = 0; k < 2; ++k) {
+        if (!sets[k].off) continue;
+        if (ns[k] >= 0xFFFFFFFFull) fail(ACC_E_CAP, "TxnId sets too large");
+        sets[k].txn.msb = stage_in(ctx, nm[k][1], src[k]->txn.msb, ns[k], in->mem);
+        sets[k].txn.lsb = stage_in(ctx, nm[k][2], src[k]->txn.lsb, ns[k], in->mem);
+        sets[k].txn.node = stage_in(ctx, nm[k][3], src[k]->txn.node, ns[k], in->mem);
+        const WoSet ws{ sets[k].off, sets[k].txn.msb, sets[k].txn.lsb, sets[k].txn.node };
+        launch(ctx, "wo_set_check", k_wo_set_check, dim3(grid_for(std::max<uint64_t>(ns[k], b.ng), BLOCK)), dim3(BLOCK), 0,
+               b.ng, ws, ns[k], err);
+    }
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, err, 8, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    if (ctx->pinned[0] & 4) fail(ACC_E_ARG, "without: a TxnId set is not sorted unique (Arrays.binarySearch needs sorted input)");
+    rmm_without_dev(ctx, b.ng, h, b.NK, b.NV, b.NO, sets[0].off ? &sets[0] : nullptr, sets[1].off ? &sets[1] : nullptr, out);
+}
+
 }  // namespace acc

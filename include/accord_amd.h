@@ -106,12 +106,29 @@ typedef struct acc_rlist {
 /* ---- context options ---- */
 #define ACC_OPT_TIMING 0x1u   /* record per-kernel HIP events (bench / profiling) */
 #define ACC_OPT_FORCE_REPLAY 0x2u  /* always take the exact FAST-bisection replay path (testing) */
+#define ACC_OPT_NO_WINDOW_TIER 0x4u  /* KeyDeps: the sorting build tiers instead of the window tier (testing) */
+#define ACC_OPT_RD_WIDE_SORT 0x8u    /* RangeDeps: 64-bit sort keys in the lane-group build tiers (testing) */
+#define ACC_OPT_PD_SERIAL 0x10u      /* acc_partial_deps_batch: both halves in order on this context (one buffer set:
+                                        less device memory, no overlap) */
+
+/* levelise walk (acc_opts.lv_tier); AUTO picks the whole-graph LDS walk up to 65,535 txns, the windowed walk beyond */
+#define ACC_LV_AUTO     0u
+#define ACC_LV_LDS_WALK 1u
+#define ACC_LV_WINDOWED 2u
+#define ACC_LV_WAVES    3u
 
 typedef struct acc_ctx acc_ctx;
 
+/* Context options, fixed at acc_create (the library reads no environment): flags plus the knobs the tests use to force
+ * a code path; zero everywhere = the defaults. */
 typedef struct acc_opts {
     uint32_t flags;           /* ACC_OPT_* */
     uint32_t reserved;
+    uint32_t cfk_hot;         /* acc_cfk_apply: keys with more than this many sorted elements take the closed form
+                                 of the replay (0: 64) */
+    uint32_t lv_tier;         /* ACC_LV_* */
+    uint32_t lv_chunk;        /* the LDS walk's dependency chunk cap in entries (0: as large as the LDS allows) */
+    uint32_t reserved2;
 } acc_opts;
 
 /* Timestamp / TxnId as three SoA columns: Timestamp.msb, Timestamp.lsb, Node.Id.id
@@ -406,6 +423,57 @@ typedef struct acc_slice_view {
  * (utils/RelationMultiMap.java:491-532), each group against its own select Ranges; the reference's short cuts are kept
  * (empty input, nothing selected, everything selected = `return this` without trimming). */
 int acc_rmm_slice(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ranges_in *select, acc_slice_view *out_view);
+
+/* RelationMultiMap.remove (utils/RelationMultiMap.java:843-905) = KeyDeps.without (primitives/KeyDeps.java:255-259) /
+ * RangeDeps.without (primitives/RangeDeps.java:584-588) of every group, with the predicate of the recovery callers
+ * (`without(earlierCommittedWitness::contains)`, messages/BeginRecovery.java:180-183, coordinate/Recover.java:322):
+ * remove(t) = Deps.contains(t) = KeyDeps.contains || RangeDeps.contains (primitives/Deps.java:107-110), each an
+ * Arrays.binarySearch over that deps object's sorted TxnIds (Timestamp.compareTo == 0). The group's TxnId set(s) to
+ * test against: set_a and set_b (either may be absent: off null), each sorted ascending by Timestamp.compareTo
+ * without duplicates per group (ACC_E_ARG otherwise). The input half's TxnIds are `txn` ([val_off[n_groups]] raw).
+ * Result per group, exactly as the Java returns:
+ *   ACC_WITHOUT_FROM — `return from` (isEmpty(): no entries; or nothing removed): the input object itself;
+ *   ACC_WITHOUT_NONE — `return none` (every TxnId removed): KeyDeps.NONE / RangeDeps.NONE, no keys;
+ *   ACC_WITHOUT_NEW  — rebuilt: every key kept (keys whose lists emptied stay, :877-891), the kept TxnIds in order,
+ *                      the new keysToTxnIds int[].
+ * The view is an acc_slice_view over the input (key_idx: kept key indices, val_idx: kept TxnId indices, k2v: the
+ * group's int[]; FROM groups list everything with the input int[] verbatim) plus the kind per group. */
+#define ACC_WITHOUT_FROM 0
+#define ACC_WITHOUT_NONE 1
+#define ACC_WITHOUT_NEW  2
+
+typedef struct acc_txn_sets {
+    const uint64_t *off;       /* [n_groups+1]; null: every set is empty */
+    acc_ts_cols     txn;       /* sorted unique TxnIds of every group's set */
+} acc_txn_sets;
+
+typedef struct acc_without_view {
+    acc_slice_view sl;
+    const uint8_t *kind;       /* [n_groups] ACC_WITHOUT_* */
+    uint64_t n_from, n_none, n_new;
+} acc_without_view;
+
+int acc_rmm_without(acc_ctx *ctx, const acc_rmm_batch *in, const acc_ts_cols *txn, const acc_txn_sets *set_a,
+                    const acc_txn_sets *set_b, acc_without_view *out_view);
+
+/* The recovery reply reduce of the deps the recovery coordinator folds (coordinate/Recover.java:320-322; pairwise as
+ * BeginRecovery.RecoverOk.reduce, messages/BeginRecovery.java:180-183): per recovered txn (group),
+ *   earlierCommittedWitness  = Deps.merge(replies' earlierCommittedWitness)           -> committed_view,
+ *   earlierAcceptedNoWitness = Deps.merge(replies' earlierAcceptedNoWitness)
+ *                                .without(earlierCommittedWitness::contains)            -> accepted_merged + accepted_*.
+ * Both merges as acc_deps_merge (same input layout; the replies in the order the Java folds them); the without runs on
+ * the merged accepted halves with each group's merged committed key and range TxnIds as the two sets. accepted_key /
+ * accepted_range index into accepted_merged's halves (val_idx into its TxnIds, key_idx into its keys / ranges).
+ * Views are device pointers owned by the context, valid until its next compute call. */
+typedef struct acc_recovery_deps_view {
+    acc_deps_merge_view committed;        /* earlierCommittedWitness per group */
+    acc_deps_merge_view accepted_merged;  /* Deps.merge of earlierAcceptedNoWitness per group (before the without) */
+    acc_without_view accepted_key;        /* KeyDeps.without over accepted_merged.key_deps */
+    acc_without_view accepted_range;      /* RangeDeps.without over accepted_merged.range_deps */
+} acc_recovery_deps_view;
+
+int acc_recovery_deps_reduce(acc_ctx *ctx, const acc_deps_merge_in *committed_witness,
+                             const acc_deps_merge_in *accepted_no_witness, acc_recovery_deps_view *out_view);
 
 /* Stabbing queries over built RangeDeps (SearchableRangeList.forEach, utils/SearchableRangeList.java:89-116;
  * RangeDeps.forEach / computeTxnIds, primitives/RangeDeps.java:152-412, 629-643): query q against group grp[q]:

@@ -186,6 +186,15 @@ orc_slice_result *orc_rmm_slice(uint32_t n_groups, int is_range, int end_inclusi
                                 const uint64_t *sel_off, const uint64_t *sel_s, const uint64_t *sel_e);
 void orc_slice_free(orc_slice_result *r);
 
+/* RelationMultiMap.remove = KeyDeps/RangeDeps.without per group, remove = membership in the group's set a or b
+ * (Deps::contains); kind[g]: 0 from, 1 none, 2 rebuilt. Free with orc_slice_free. */
+orc_slice_result *orc_rmm_without(uint32_t n_groups, const uint64_t *key_off, const uint64_t *val_off,
+                                  const uint64_t *k2v_off, const int32_t *k2v,
+                                  const uint64_t *vm, const uint64_t *vl, const int32_t *vn,
+                                  const uint64_t *a_off, const uint64_t *am, const uint64_t *al, const int32_t *an,
+                                  const uint64_t *b_off, const uint64_t *bm, const uint64_t *bl, const int32_t *bn,
+                                  uint8_t *kind);
+
 /* Stabbing queries over built RangeDeps: per query the ascending indices of group grp[q]'s ranges containing the
  * key qs[q] (is_key_query) or intersecting [qs[q], qe[q]). */
 typedef struct orc_stab_result { uint64_t *off; uint32_t *idx; } orc_stab_result;

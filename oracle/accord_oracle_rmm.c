@@ -521,6 +521,96 @@ orc_slice_result *orc_rmm_slice(uint32_t n_groups, int is_range, int end_inclusi
     return R;
 }
 
+/* ------------------------------------------------------------------ without (RelationMultiMap.remove) */
+
+/* Arrays.binarySearch(txnIds, t) >= 0 over a sorted TxnId[] (java.util.Arrays: lo/hi bisection, compareTo) */
+static int bsearch_contains(const uint64_t *m, const uint64_t *l, const int32_t *n, uint64_t lo, uint64_t hi, const rts *t)
+{
+    if (!m) return 0;
+    int64_t low = (int64_t)lo, high = (int64_t)hi - 1;
+    while (low <= high) {
+        int64_t mid = (low + high) >> 1;
+        rts x = { m[mid], l[mid], n[mid] };
+        int c = rts_cmp(&x, t);
+        if (c < 0) low = mid + 1;
+        else if (c > 0) high = mid - 1;
+        else return 1;
+    }
+    return 0;
+}
+
+/* RelationMultiMap.remove (utils/RelationMultiMap.java:843-905) per group = KeyDeps.without (primitives/KeyDeps.java:
+ * 255-259) / RangeDeps.without (primitives/RangeDeps.java:584-588) with remove = Deps::contains over the group's two
+ * sets (primitives/Deps.java:107-110: keyDeps.contains || rangeDeps.contains). kind[g]: 0 `return from`, 1 `return
+ * none`, 2 the rebuilt object (keys passed through: emptied keys stay). Output as orc_rmm_slice's. */
+orc_slice_result *orc_rmm_without(uint32_t n_groups, const uint64_t *key_off, const uint64_t *val_off,
+                                  const uint64_t *k2v_off, const int32_t *k2v,
+                                  const uint64_t *vm, const uint64_t *vl, const int32_t *vn,
+                                  const uint64_t *a_off, const uint64_t *am, const uint64_t *al, const int32_t *an,
+                                  const uint64_t *b_off, const uint64_t *bm, const uint64_t *bl, const int32_t *bn,
+                                  uint8_t *kind)
+{
+    orc_slice_result *R = calloc(1, sizeof *R);
+    R->n_groups = n_groups;
+    R->key_off = calloc(n_groups + 1, 8); R->val_off = calloc(n_groups + 1, 8); R->k2v_off = calloc(n_groups + 1, 8);
+    rivec ks = { 0 }, vs = { 0 }, oo = { 0 };
+    for (uint32_t g = 0; g < n_groups; ++g) {
+        R->key_off[g] = ks.n; R->val_off[g] = vs.n; R->k2v_off[g] = oo.n;
+        size_t nk = key_off[g + 1] - key_off[g], nv = val_off[g + 1] - val_off[g], no = k2v_off[g + 1] - k2v_off[g];
+        const int32_t *old = k2v + k2v_off[g];
+        /* :844-845 if (isEmpty(keys, oldKeysToValues)) return from; */
+        int from = no == nk;
+        int32_t *remapValue = malloc((nv + 1) * sizeof *remapValue);
+        int count = 0;
+        if (!from) {
+            /* :853-858 remapValue[i] = remove.test(oldValues[i]) ? -1 : count++ */
+            for (size_t i = 0; i < nv; ++i) {
+                size_t v = val_off[g] + i;
+                rts t = { vm[v], vl[v], vn[v] };
+                int rm = (a_off && bsearch_contains(am, al, an, a_off[g], a_off[g + 1], &t)) ||
+                         (b_off && bsearch_contains(bm, bl, bn, b_off[g], b_off[g + 1], &t));
+                remapValue[i] = rm ? -1 : count++;
+            }
+            /* :862-863 if (count == oldValues.length) return from; */
+            if ((size_t)count == nv) from = 1;
+        }
+        if (from) {
+            kind[g] = 0;
+            for (size_t k = 0; k < nk; ++k) rpush(&ks, (int64_t)k);
+            for (size_t v = 0; v < nv; ++v) rpush(&vs, (int64_t)v);
+            for (size_t q = 0; q < no; ++q) rpush(&oo, old[q]);
+            free(remapValue);
+            continue;
+        }
+        /* :865-866 if (count == 0) return none; */
+        if (count == 0) { kind[g] = 1; free(remapValue); continue; }
+        kind[g] = 2;
+        /* :868-873 newValues[remapValue[i]] = oldValues[i] */
+        for (size_t i = 0; i < nv; ++i) if (remapValue[i] >= 0) rpush(&vs, (int64_t)i);
+        /* :875-894 the keysToValues walk, literally */
+        int32_t *nkv = malloc((no + 1) * sizeof *nkv);
+        size_t k = 0, i = nk, o = nk;
+        while (i < no) {
+            while (old[k] == (int32_t)i) nkv[k++] = (int32_t)o;
+            int32_t remapped = remapValue[old[i]];
+            if (remapped >= 0) nkv[o++] = remapped;
+            ++i;
+        }
+        while (k < nk) nkv[k++] = (int32_t)o;
+        /* passthrough keys (:904 constructor.construct(passthroughKeys, ...)) */
+        for (size_t kk = 0; kk < nk; ++kk) rpush(&ks, (int64_t)kk);
+        for (size_t q = 0; q < o; ++q) rpush(&oo, nkv[q]);
+        free(nkv); free(remapValue);
+    }
+    R->key_off[n_groups] = ks.n; R->val_off[n_groups] = vs.n; R->k2v_off[n_groups] = oo.n;
+    R->key_idx = malloc((ks.n + 1) * 4); R->val_idx = malloc((vs.n + 1) * 4); R->k2v = malloc((oo.n + 1) * 4);
+    for (size_t q = 0; q < ks.n; ++q) R->key_idx[q] = (uint32_t)ks.v[q];
+    for (size_t q = 0; q < vs.n; ++q) R->val_idx[q] = (uint32_t)vs.v[q];
+    for (size_t q = 0; q < oo.n; ++q) R->k2v[q] = (int32_t)oo.v[q];
+    free(ks.v); free(vs.v); free(oo.v);
+    return R;
+}
+
 void orc_slice_free(orc_slice_result *r)
 {
     if (!r) return;

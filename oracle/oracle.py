@@ -111,6 +111,9 @@ def lib():
         L.orc_rmm_slice.restype = C.POINTER(SliceResult)
         L.orc_rmm_slice.argtypes = [C.c_uint32, C.c_int, C.c_int, u64p, u64p, u64p, u64p, u64p, i32p, u64p, u64p, u64p]
         L.orc_slice_free.argtypes = [C.POINTER(SliceResult)]
+        L.orc_rmm_without.restype = C.POINTER(SliceResult)
+        L.orc_rmm_without.argtypes = [C.c_uint32, u64p, u64p, u64p, i32p, u64p, u64p, i32p,
+                                      u64p, u64p, u64p, i32p, u64p, u64p, u64p, i32p, u8p]
         L.orc_rmm_stab.restype = C.POINTER(StabResult)
         L.orc_rmm_stab.argtypes = [C.c_uint32, u32p, u64p, u64p, C.c_int, C.c_int, u64p, u64p, u64p]
         L.orc_stab_free.argtypes = [C.POINTER(StabResult)]
@@ -572,6 +575,38 @@ def rmm_slice(m: dict, sel_off, sel_s, sel_e, is_range: bool, end_inclusive: boo
                    val_idx=_arr(R.val_idx, vo[-1], np.uint32), k2v=_arr(R.k2v, oo[-1], np.int32))
     finally:
         L.orc_slice_free(r)
+    return out
+
+
+def rmm_without(m: dict, set_a=None, set_b=None) -> dict:
+    """RelationMultiMap.remove = KeyDeps/RangeDeps.without per group (accord_oracle_rmm.c orc_rmm_without). m: one deps
+    half per group (key_off, val_off, k2v_off, k2v, msb, lsb, node); set_a / set_b: dict(off, msb, lsb, node) or None.
+    Returns the slice-shaped result plus kind[g] (0 from, 1 none, 2 rebuilt)."""
+    L = lib()
+    a = {k: np.ascontiguousarray(m[k], dtype=dt) for k, dt in
+         (("key_off", np.uint64), ("val_off", np.uint64), ("k2v_off", np.uint64), ("k2v", np.int32),
+          ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32))}
+    g = len(a["key_off"]) - 1
+
+    def sp(x):
+        if x is None:
+            return (None,) * 4, None
+        y = {k: np.ascontiguousarray(x[k], dtype=dt) for k, dt in
+             (("off", np.uint64), ("msb", np.uint64), ("lsb", np.uint64), ("node", np.int32))}
+        return (_p(y["off"], u64p), _p(y["msb"], u64p), _p(y["lsb"], u64p), _p(y["node"], i32p)), y
+    pa, ka = sp(set_a)
+    pb, kb = sp(set_b)
+    kind = np.zeros(max(g, 1), np.uint8)
+    r = L.orc_rmm_without(g, _p(a["key_off"], u64p), _p(a["val_off"], u64p), _p(a["k2v_off"], u64p), _p(a["k2v"], i32p),
+                          _p(a["msb"], u64p), _p(a["lsb"], u64p), _p(a["node"], i32p), *pa, *pb, _p(kind, u8p))
+    try:
+        R = r.contents
+        ko, vo, oo = (_arr(x, g + 1, np.uint64) for x in (R.key_off, R.val_off, R.k2v_off))
+        out = dict(key_off=ko, val_off=vo, k2v_off=oo, key_idx=_arr(R.key_idx, ko[-1], np.uint32),
+                   val_idx=_arr(R.val_idx, vo[-1], np.uint32), k2v=_arr(R.k2v, oo[-1], np.int32), kind=kind[:g].copy())
+    finally:
+        L.orc_slice_free(r)
+    del ka, kb
     return out
 
 

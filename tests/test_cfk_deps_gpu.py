@@ -20,6 +20,15 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(scope="module")
+def lane_ctx():
+    """Every key through the one-lane replay (acc_opts.cfk_hot above any key's size)."""
+    from accord_amd.deps import Context
+    c = Context(0, cfk_hot=1_000_000)
+    yield c
+    c.close()
+
+
 def same(g, o, label):
     for k in o:
         np.testing.assert_array_equal(np.asarray(g[k]), np.asarray(o[k]), err_msg=f"{label}: {k}")
@@ -80,12 +89,12 @@ def hot_key_case(request):
 
 @pytest.mark.parametrize("path", ["hot", "lane"])
 @pytest.mark.parametrize("frac", [0.3, 0.6, 1.0])
-def test_cfk_deps_hot_key(ctx, hot_key_case, frac, path, monkeypatch):
-    """The hot key through the hot-key closed form (its ~2,700 updates are above ACC_CFK_HOT's default) and through
-    the one-lane replay (threshold raised)."""
+def test_cfk_deps_hot_key(ctx, lane_ctx, hot_key_case, frac, path):
+    """The hot key through the hot-key closed form (its ~2,700 updates are above acc_opts.cfk_hot's default) and
+    through the one-lane replay (threshold raised)."""
     from accord_amd.deps import cfk_apply
     if path == "lane":
-        monkeypatch.setenv("ACC_CFK_HOT", "1000000")
+        ctx = lane_ctx
     p_dep, upd = hot_key_case
     part, _ = CC.split_updates(upd, int(len(upd["msb"]) * frac))
     g = cfk_apply(ctx, CC.empty_snapshot(), part)
@@ -100,14 +109,18 @@ def test_cfk_deps_hot_key(ctx, hot_key_case, frac, path, monkeypatch):
             assert st["cfk.apply_regrow"] > 0
 
 
-@pytest.fixture(params=["1", "3"], ids=["hot_gt1", "hot_gt3"])
-def hot_all(request, monkeypatch):
-    """Every key with more than 1 (3) sorted elements (its snapshot + its updates) through the hot-key closed form."""
-    monkeypatch.setenv("ACC_CFK_HOT", request.param)
-    return int(request.param)
+@pytest.fixture(scope="module", params=[1, 3], ids=["hot_gt1", "hot_gt3"])
+def hot_all(request):
+    """A context whose acc_opts.cfk_hot sends every key with more than 1 (3) sorted elements (its snapshot + its
+    updates) through the hot-key closed form."""
+    from accord_amd.deps import Context
+    c = Context(0, cfk_hot=request.param)
+    yield c
+    c.close()
 
 
-def test_cfk_hot_path_handmade(ctx, hot_all):
+def test_cfk_hot_path_handmade(hot_all):
+    ctx = hot_all
     from accord_amd.deps import cfk_apply
     upd, expect = CC.handmade()
     for n, want in expect:
@@ -118,9 +131,10 @@ def test_cfk_hot_path_handmade(ctx, hot_all):
 
 
 @pytest.mark.parametrize("seed,n_txn,n_keys", [(0, 200, 12), (1, 400, 30), (2, 120, 3), (3, 1500, 200)])
-def test_cfk_hot_path_random(ctx, hot_all, seed, n_txn, n_keys):
+def test_cfk_hot_path_random(hot_all, seed, n_txn, n_keys):
     """Generated lifecycles (TRANSITIVELY_KNOWN additions, re-accepted ballots, bumped executeAts, invalidations):
     the closed form equals the serial restatement bit for bit."""
+    ctx = hot_all
     from accord_amd.deps import cfk_apply
     upd = CC.cfk_case(seed, n_txn=n_txn, n_keys=n_keys)
     hot = 0
@@ -132,9 +146,10 @@ def test_cfk_hot_path_random(ctx, hot_all, seed, n_txn, n_keys):
     assert hot > 0
 
 
-def test_cfk_hot_path_chained(ctx, hot_all):
+def test_cfk_hot_path_chained(hot_all):
     """Batches applied to the previous result: the snapshot's missing[] carried (less the TxnIds committed since), new
     uncommitted TxnIds added."""
+    ctx = hot_all
     from accord_amd.deps import cfk_apply
     upd = CC.cfk_case(7, n_txn=600, n_keys=40)
     n = len(upd["msb"])
@@ -150,7 +165,8 @@ def test_cfk_hot_path_chained(ctx, hot_all):
         same(snap, oracle.cfk_apply(CC.empty_snapshot(), head), f"after {c} updates")
 
 
-def test_cfk_hot_path_stream_and_errors(ctx, hot_all):
+def test_cfk_hot_path_stream_and_errors(hot_all):
+    ctx = hot_all
     from accord_amd import workload as W
     from accord_amd.deps import IllegalStateException, cfk_apply
     upd = W.cfk_update_stream(5_000, 4, 800)

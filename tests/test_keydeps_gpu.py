@@ -112,24 +112,6 @@ def test_zipf_hot_keys(ctx):
     assert_same(g, o, b.n_txn, "zipf")
 
 
-@pytest.mark.parametrize("switch", ["ACC_V2_FASTQ", "ACC_KD_OPT"])
-def test_tuning_switches_parity(monkeypatch, switch):
-    """The KeyDeps tuning switches kept off by default stay bit-exact: the O(1) query columns
-    (ACC_V2_FASTQ) and the optimistic build without the E host sync (ACC_KD_OPT: from a context's second batch on; a
-    larger third batch exceeds the capacity the first two left and takes the exact rebuild)."""
-    import oracle
-    from accord_amd.deps import Context
-    monkeypatch.setenv(switch, "1")
-    c = Context(0)
-    try:
-        for n, seed in ((6000, 0x51), (6000, 0x52), (12000, 0x53)):
-            b = W.keydeps_batch(n, 8, 1500, seed, "zipf", 0.99, status_model="model", window=1200)
-            g = c.calculate_partial_deps(b)
-            assert_same(g, oracle.keydeps_batch(b), b.n_txn, f"{switch} n={n}")
-    finally:
-        c.close()
-
-
 def test_mixed_kinds_and_accept_style(ctx):
     """SyncPoint kinds, random executeAt bumps on uncommitted txns (Accept-style queries with p1)."""
     import oracle
@@ -215,8 +197,7 @@ def test_tiers_medium_big_fallback(ctx, hot_every, tail):
 def test_window_tier(nk):
     """The uncommitted window's txns on hot keys (E up to thousands) through the per-key bitmap tier (<= 8 and
     <= 16 keys: k_v2_write_win) or, beyond 16 keys, the sorting tiers run after the host sync: bit-exact with the
-    oracle on the window's txns and, on every txn, with the sorting tiers alone (ACC_NO_WIN)."""
-    import os
+    oracle on the window's txns and, on every txn, with the sorting tiers alone (acc_opts ACC_OPT_NO_WINDOW_TIER)."""
     import oracle
     from accord_amd.deps import Context
     b = W.keydeps_batch(40_000, nk, 12_000, 0xB17 + nk, "zipf", 0.99, status_model="model", window=2500)
@@ -227,12 +208,8 @@ def test_window_tier(nk):
         assert st["keydeps.window_txns"] > 0
     else:
         assert st["keydeps.window_txns"] == 0 and st["keydeps.medium_txns"] + st["keydeps.big_txns"] > 0
-    os.environ["ACC_NO_WIN"] = "1"
-    try:
-        with Context(0) as c:
-            s = c.calculate_partial_deps(b)
-    finally:
-        del os.environ["ACC_NO_WIN"]
+    with Context(0, no_window_tier=True) as c:
+        s = c.calculate_partial_deps(b)
     assert_same(g, s, b.n_txn, f"window vs sorting tiers, {nk} keys")
     n = b.n_txn
     o = oracle.keydeps_batch(b, query_lo=n - 400, query_hi=n)

@@ -1,4 +1,6 @@
 """GPU parity: acc_levelise vs the C restatement and the canonical model."""
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -66,13 +68,30 @@ def test_levelise_rejects_bad_dep(ctx):
         levelise(ctx, np.array([0, 1], np.uint64), np.array([7], np.uint32), np.array([0], np.uint32))
 
 
-@pytest.mark.parametrize("n,env", [(1000, None), (70000, None), (1000, "ACC_LV_WIN"), (1000, "ACC_LV_WAVES")])
-def test_levelise_rejects_decreasing_offsets(ctx, monkeypatch, n, env):
+@contextlib.contextmanager
+def tier_ctx(ctx, tier="auto", chunk=0):
+    """The module context for the default walk, else a context whose acc_opts force the tier / chunk cap."""
+    from accord_amd.deps import Context
+    if tier == "auto" and not chunk:
+        yield ctx
+        return
+    c = Context(0, lv_tier=tier, lv_chunk=chunk)
+    try:
+        yield c
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("n,tier", [(1000, "auto"), (70000, "auto"), (1000, "windowed"), (1000, "waves")])
+def test_levelise_rejects_decreasing_offsets(ctx, n, tier):
     """Non-monotone offsets with off[n] == E (every range in bounds on its own, but ranges overlap, so the filtered
     counts sum past E): each tier must fail with IllegalArgumentException before writing its lists."""
+    with tier_ctx(ctx, tier) as c:
+        check_rejects_decreasing(c, n)
+
+
+def check_rejects_decreasing(ctx, n):
     from accord_amd.deps import IllegalArgumentException, levelise
-    if env:
-        monkeypatch.setenv(env, "1")
     E = 10
     off = np.full(n + 1, E, np.uint64)
     off[0] = 0
@@ -153,60 +172,39 @@ def test_levelise_one_million(ctx):
     assert nl == nl2 and nl > 1000
 
 
-@pytest.mark.parametrize("env,n,max_deps,tier", [
-    ({}, 2000, 300, 1),                                      # LDS walk (default below 4,096 txns), default chunks
-    ({"ACC_LV_CH": "64"}, 2000, 300, 1),                     # LDS walk, 64-entry chunks: long lists read from HBM
-    ({"ACC_LV_LDS": "1", "ACC_LV_CH": "256"}, 20000, 12, 1), # many rounds, rounds of > 2048 positions
-    ({"ACC_LV_LDS": "1"}, 65535, 6, 1),                      # largest LDS-walk graph (u16 levels and positions)
-    ({}, 20000, 12, 1),                                      # the LDS walk up to 65,535 txns
-    ({"ACC_LV_W1": "1"}, 32768, 6, 3),                       # the LDS windowed walk: its largest graph
-    ({"ACC_LV_W1": "1"}, 20000, 12, 3),
-    ({"ACC_LV_W1": "1"}, 1024, 40, 3),                       # exactly one window
-    ({"ACC_LV_W1": "1"}, 3073, 900, 3),                      # a partial last window; windows beyond the successor buffer
-    ({"ACC_LV_W1": "1"}, 1025, 1100, 3),                     # two windows, the first beyond the successor buffer
-    ({"ACC_LV_W1": "1"}, 5000, 30, 3),                       # far deps for windows 2..4
-    ({}, 65536, 6, 2),                                       # beyond the LDS tiers: one launch per window
-    ({"ACC_LV_POLL": "1"}, 65536, 6, 2),                     # the same, batch polling
-    ({"ACC_LV_WIN": "1"}, 2000, 300, 2),                     # windowed walk, pending-set walk: two windows
-    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 2000, 300, 2), # windowed walk, batch polling
-    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 5000, 30, 2),  # far deps gathered for windows 2..4 (batch polling)
-    ({"ACC_LV_WIN": "1"}, 5000, 30, 2),                      # the same, pending-set walk
-    ({"ACC_LV_WIN": "1"}, 1024, 40, 2),                      # exactly one window
-    ({"ACC_LV_WIN": "1"}, 3073, 900, 2),                     # a partial last window, long lists
-    ({"ACC_LV_WIN": "1", "ACC_LV_POLL": "1"}, 3073, 900, 2), # the same, batch polling
-    ({"ACC_LV_WAVES": "1"}, 5000, 30, 0),                    # the persistent-wave walk at a size the LDS tier takes
-    ({"ACC_LV_WAVES": "1"}, 65536, 6, 0),                    # the persistent-wave walk beyond it
+@pytest.mark.parametrize("tier,chunk,n,max_deps,stat", [
+    ("auto", 0, 2000, 300, 1),             # LDS walk (default below 4,096 txns), default chunks
+    ("auto", 64, 2000, 300, 1),            # LDS walk, 64-entry chunks: long lists read from HBM
+    ("lds", 256, 20000, 12, 1),            # many rounds, rounds of > 2048 positions
+    ("lds", 0, 65535, 6, 1),               # largest LDS-walk graph (u16 levels and positions)
+    ("auto", 0, 20000, 12, 1),             # the LDS walk up to 65,535 txns
+    ("auto", 0, 65536, 6, 2),              # beyond the LDS tiers: one launch per window
+    ("windowed", 0, 2000, 300, 2),         # windowed walk, pending-set walk: two windows
+    ("windowed", 0, 5000, 30, 2),          # far deps gathered for windows 2..4
+    ("windowed", 0, 1024, 40, 2),          # exactly one window
+    ("windowed", 0, 3073, 900, 2),         # a partial last window, long lists
+    ("waves", 0, 5000, 30, 0),             # the persistent-wave walk at a size the LDS tier takes
+    ("waves", 0, 65536, 6, 0),             # the persistent-wave walk beyond it
 ])
-def test_levelise_tiers(ctx, monkeypatch, env, n, max_deps, tier):
+def test_levelise_tiers(ctx, tier, chunk, n, max_deps, stat):
     import oracle
     from accord_amd.deps import levelise
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     off, dep, er = random_graph(np.random.RandomState(n + max_deps), n, max_deps)
-    lv, order, nl = levelise(ctx, off, dep, er)
-    assert ctx.stats().get("levelise.lds_tier") == tier
+    with tier_ctx(ctx, tier, chunk) as c:
+        lv, order, nl = levelise(c, off, dep, er)
+        assert c.stats().get("levelise.lds_tier") == stat
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)
     assert nl == nl2
 
 
-@pytest.mark.parametrize("walk", ["w1", "windowed", "windowed_poll1", "lds", "waves"])
-def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
+@pytest.mark.parametrize("walk", ["windowed", "lds", "waves"])
+def test_levelise_config5_graph_both_tiers(ctx, walk):
     """A config-5-shaped merged graph (16,384 txns, deps on recent txns, hundreds of levels) through the windowed walk,
     the LDS walk and the persistent-wave walk: identical levels and order, equal to the oracle."""
     import oracle
     from accord_amd.deps import levelise
-    if walk == "waves":
-        monkeypatch.setenv("ACC_LV_WAVES", "1")
-    if walk.startswith("windowed"):
-        monkeypatch.setenv("ACC_LV_WIN", "1")
-    if walk.endswith("_poll1"):
-        monkeypatch.setenv("ACC_LV_POLL", "1")
-    if walk == "lds":
-        monkeypatch.setenv("ACC_LV_LDS", "1")
-    if walk == "w1":
-        monkeypatch.setenv("ACC_LV_W1", "1")
     rng = np.random.RandomState(55)
     n = 16384
     er = rng.permutation(n).astype(np.uint32)
@@ -220,9 +218,9 @@ def test_levelise_config5_graph_both_tiers(ctx, monkeypatch, walk):
                     np.zeros(0, np.int64))
     off = np.concatenate([[0], np.cumsum([len(d) for d in deps])]).astype(np.uint64)
     dep = np.concatenate(deps).astype(np.uint32)
-    lv, order, nl = levelise(ctx, off, dep, er)
-    assert ctx.stats().get("levelise.lds_tier") == {"w1": 3, "windowed": 2, "windowed_poll1": 2,
-                                                    "lds": 1, "waves": 0}[walk]
+    with tier_ctx(ctx, walk) as c:
+        lv, order, nl = levelise(c, off, dep, er)
+        assert c.stats().get("levelise.lds_tier") == {"windowed": 2, "lds": 1, "waves": 0}[walk]
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)

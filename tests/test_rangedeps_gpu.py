@@ -63,16 +63,20 @@ def test_block_and_global_tiers(ctx):
 
 
 @pytest.mark.parametrize("wide", [False, True])
-def test_identical_ranges(ctx, monkeypatch, wide):
+def test_identical_ranges(ctx, wide):
     """Range commands sharing one stored range (64 keys, widths <= 8: ~500 distinct ranges for ~1,500 range txns), so
     the lane-group tiers see range ids held by several TxnIds: the 32-bit (range id, lane) sort falls back to the 64-bit
-    one for those waves (ACC_RD_WIDE: the 64-bit sorts throughout)."""
+    one for those waves (acc_opts ACC_OPT_RD_WIDE_SORT: the 64-bit sorts throughout)."""
     import oracle
-    if wide:
-        monkeypatch.setenv("ACC_RD_WIDE", "1")
+    from accord_amd.deps import Context
     rb = rd_cases.dense(11, n=3000, key_bits=6, max_width_log2=3, ranges_per_txn=1)
-    g = ctx.calculate_partial_range_deps(rb)
-    st = ctx.stats()
+    c = Context(0, rd_wide_sort=True) if wide else ctx
+    try:
+        g = c.calculate_partial_range_deps(rb)
+        st = c.stats()
+    finally:
+        if wide:
+            c.close()
     assert st["rangedeps.narrow_sorts"] == (0 if wide else 1)
     assert st["rangedeps.s16_txns"] > 0 and st["rangedeps.s32_txns"] + st["rangedeps.s64_txns"] > 0
     assert st["rangedeps.stored_ranges"] < st["rangedeps.entries"] // 2

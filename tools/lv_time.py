@@ -1,5 +1,5 @@
 """Time acc_levelise on the 1M-txn test graph (tests/test_levelise_gpu.py::test_levelise_one_million) per tier:
-python tools/lv_time.py  (ACC_LV_WAVES=1 / ACC_LV_LDS=1 select the other tiers)."""
+python tools/lv_time.py [auto|lds|windowed|waves]  (the walk, as acc_opts.lv_tier)."""
 import os
 import sys
 import time
@@ -31,7 +31,7 @@ allsrc, alld = allsrc[keep], alld[keep]
 off = np.zeros(n + 1, np.uint64)
 np.cumsum(np.bincount(allsrc, minlength=n), out=off[1:])
 alld = alld.astype(np.uint32)
-with Context(0) as ctx:
+with Context(0, lv_tier=sys.argv[1] if len(sys.argv) > 1 else "auto") as ctx:
     levelise(ctx, off, alld, er)
     t = time.perf_counter()
     lv, order, nl = levelise(ctx, off, alld, er)
