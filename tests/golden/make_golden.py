@@ -111,6 +111,75 @@ def config2():
     print(path, os.path.getsize(path), "bytes;", len(txn), "txns")
 
 
+_K1, _K2, _K3 = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix(x):
+    """splitmix64's finalizer over a uint64 array (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * _K1
+        x = (x ^ (x >> np.uint64(27))) * _K2
+        return x ^ (x >> np.uint64(31))
+
+
+def _seg_hash(off, vals, lo, hi, salt):
+    """Per segment t in [lo, hi) of the CSR (off, vals): sum over its elements of mix(value, position, salt)."""
+    o = np.asarray(off[lo:hi + 1], np.int64)
+    a, b = int(o[0]), int(o[-1])
+    v = np.asarray(vals[a:b]).astype(np.int64).astype(np.uint64)
+    cnt = np.diff(o)
+    pos = np.arange(b - a, dtype=np.int64) - np.repeat(o[:-1] - a, cnt)
+    with np.errstate(over="ignore"):
+        h = _mix(v * _K3 + pos.astype(np.uint64) * _K1 + np.uint64(salt))
+        c = np.concatenate([[np.uint64(0)], np.cumsum(h, dtype=np.uint64)])
+        return c[o[1:] - a] - c[o[:-1] - a], cnt.astype(np.uint64)
+
+
+def txn_hashes(out, lo, hi) -> np.ndarray:
+    """32-bit hash of each txn t in [lo, hi) of a KeyDeps batch result (acc_keydeps_view / oracle layout): its
+    keysToTxnIds ints, key indices and dependency batch indices, every element mixed with its position and every array
+    with its length, so a changed, missing, extra or reordered element changes the txn's hash. Vectorised (numpy), so
+    all 1M config-2 txns hash in seconds."""
+    ha, na = _seg_hash(out.arena_off, out.arena, lo, hi, 1)
+    hk, nk = _seg_hash(out.kd_off, out.key_idx, lo, hi, 2)
+    hd, nd = _seg_hash(out.u_off, out.dep_txn, lo, hi, 3)
+    with np.errstate(over="ignore"):
+        h = _mix(ha ^ _mix(na + _K1)) + _mix(hk ^ _mix(nk + _K2)) * _K3 + _mix(hd ^ _mix(nd + _K3))
+    return (h >> np.uint64(32)).astype(np.uint32)
+
+
+def _c2_chunk(args):
+    lo, hi = args
+    b = W.config("2")
+    o = oracle.keydeps_batch(b, query_lo=lo, query_hi=hi)
+    sz = np.stack([np.diff(o.kd_off[lo:hi + 1].astype(np.int64)), np.diff(o.u_off[lo:hi + 1].astype(np.int64)),
+                   np.diff(o.arena_off[lo:hi + 1].astype(np.int64))], axis=1).astype(np.uint32)
+    return lo, hi, txn_hashes(o, lo, hi), sz
+
+
+def config2_all(workers=8):
+    """Every one of config 2's 1M txns from the C restatement (8 processes over txn ranges, a few minutes): per txn
+    a 32-bit hash of its KeyDeps arrays (txn_hashes) and its sizes, plus the input's sha256. The GPU test compares
+    every txn (tests/test_keydeps_gpu.py::test_config2_sample_and_properties)."""
+    from multiprocessing import Pool
+    b = W.config("2")
+    n = b.n_txn
+    # the O(prefix) scan's cost grows with a txn's position in its segments: chunks by sqrt spacing
+    cuts = sorted({int(round(n * (i / 96) ** 0.5)) for i in range(97)})
+    jobs = list(zip(cuts[:-1], cuts[1:]))
+    h = np.zeros(n, np.uint32)
+    sizes = np.zeros((n, 3), np.uint32)
+    with Pool(workers) as pool:
+        for lo, hi, hh, sz in pool.imap_unordered(_c2_chunk, jobs):
+            h[lo:hi] = hh
+            sizes[lo:hi] = sz
+            print("chunk", lo, hi, flush=True)
+    path = os.path.join(HERE, "config2_all.npz")
+    np.savez_compressed(path, input_sha256=np.frombuffer(bytes.fromhex(batch_digest(b)), np.uint8), hash32=h,
+                        sizes=sizes)
+    print(path, os.path.getsize(path), "bytes")
+
+
 def sub_batch(b, keyset):
     """Every txn of b, keys restricted to `keyset` (sorted unique codes)."""
     keep = np.isin(b.key_code, keyset)
@@ -224,5 +293,7 @@ if __name__ == "__main__":
         config4s()
     if which in ("2", "all"):
         config2()
+    if which in ("2all", "all"):
+        config2_all()
     if which in ("3", "all"):
         config3()

@@ -286,16 +286,25 @@ def test_errors(ctx):
 
 
 def test_config2_sample_and_properties(ctx):
-    """BASELINE config 2 (1M txns x 8 keys, zipf 0.99 over 1M keys) on the GPU; bit-exact against the committed
-    oracle fixture of 20,000 query txns (the O(prefix) restatement takes ~2 min for them, too slow for all 1M), plus
-    size-independent layout properties over every txn."""
+    """BASELINE config 2 (1M txns x 8 keys, zipf 0.99 over 1M keys) on the GPU, bit-exact against the oracle on EVERY
+    txn: the committed per-txn sizes and 32-bit hashes of all 1M txns' KeyDeps arrays (tests/golden/config2_all.npz,
+    the C restatement run over the whole batch on 8 cores by make_golden.py config2_all), the 20,000-txn fixture's
+    16-byte digests and full arrays, and size-independent layout properties over every txn."""
     sys.path.insert(0, os.path.join(HERE, "golden"))
-    from make_golden import batch_digest, txn_digest
+    from make_golden import batch_digest, txn_digest, txn_hashes
     b = W.config("2")
     fx = dict(np.load(os.path.join(HERE, "golden", "config2_sample.npz")))   # decompress each array once
     assert batch_digest(b).encode() == bytes(fx["input_sha256"]).hex().encode(), "config-2 generator changed"
     g = ctx.calculate_partial_deps(b)
     n = b.n_txn
+    fa = dict(np.load(os.path.join(HERE, "golden", "config2_all.npz")))
+    assert bytes(fa["input_sha256"]) == bytes(fx["input_sha256"])
+    sz = np.stack([np.diff(g.kd_off.astype(np.int64)), np.diff(g.u_off.astype(np.int64)),
+                   np.diff(g.arena_off.astype(np.int64))], axis=1)
+    bad = np.flatnonzero((sz != fa["sizes"].astype(np.int64)).any(axis=1))
+    assert len(bad) == 0, f"{len(bad)} txns differ in size from the oracle, first {bad[:5].tolist()}"
+    bad = np.flatnonzero(txn_hashes(g, 0, n) != fa["hash32"])
+    assert len(bad) == 0, f"{len(bad)} txns differ from the oracle, first {bad[:5].tolist()}"
     # the committed oracle sample (tests/golden/make_golden.py config2): 20,000 query txns, the hottest 2,000 among
     # them; per-txn sizes + digests for all, full arrays for the spread windows
     for t, sz, dg in zip(fx["txn"].tolist(), fx["sizes"], fx["digest"]):

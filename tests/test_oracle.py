@@ -185,3 +185,19 @@ def test_config2_fixture_reproduces():
     for t in range(lo, lo + 200):
         k, d, a = o.txn(t)
         assert txn_digest(k, d, a) == bytes(fx["digest"][pos[t]]), t
+
+
+def test_config2_all_fixture_reproduces():
+    """tests/golden/config2_all.npz (every config-2 txn's 32-bit KeyDeps hash, made by make_golden.py config2_all on 8
+    processes) matches the C restatement re-run here on the first 3,000 txns and on 300 of the hot uncommitted window."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden import batch_digest, txn_hashes
+    b = W.config("2")
+    fa = np.load(os.path.join(HERE, "golden", "config2_all.npz"))
+    assert batch_digest(b) == bytes(fa["input_sha256"]).hex()
+    assert fa["hash32"].shape == (b.n_txn,) and fa["sizes"].shape == (b.n_txn, 3)
+    for lo, hi in ((0, 3000), (998_000, 998_300)):
+        o = oracle.keydeps_batch(b, query_lo=lo, query_hi=hi)
+        np.testing.assert_array_equal(txn_hashes(o, lo, hi), fa["hash32"][lo:hi])
+        np.testing.assert_array_equal(np.diff(o.u_off[lo:hi + 1].astype(np.int64)), fa["sizes"][lo:hi, 1].astype(np.int64))
