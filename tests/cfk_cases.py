@@ -279,3 +279,57 @@ def recovery_queries(b, seed, n_query=80):
         qo.append(len(qk))
     return dict(msb=np.array(qm, np.uint64), lsb=np.array(ql, np.uint64), node=np.array(qn, np.int32),
                 key_off=np.array(qo, np.uint32), key_code=np.array(qk, np.uint64))
+
+
+def restrict(upd, keyset):
+    """The update stream restricted to the keys in `keyset` (CommandsForKey states are per key, so a key's state after
+    the restricted stream equals its state after the whole one); updates left without keys are dropped."""
+    ko = upd["key_off"].astype(np.int64)
+    do = upd["dep_off"].astype(np.int64)
+    keep = np.isin(upd["key"], keyset)
+    csum = np.concatenate([[0], np.cumsum(keep.astype(np.int64))])
+    per = csum[ko[1:]] - csum[ko[:-1]]
+    ukeep = per > 0
+    out = {k: upd[k][ukeep] for k in ("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags")}
+    out["key_off"] = np.concatenate([[0], np.cumsum(per[ukeep])]).astype(np.uint32)
+    out["key"] = upd["key"][keep]
+    out["dep_off"] = np.concatenate([[0], np.cumsum(np.diff(do)[keep])]).astype(np.uint32)
+    dsel = np.repeat(keep, np.diff(do))
+    for f in ("dmsb", "dlsb", "dnode"):
+        out[f] = upd[f][dsel]
+    return out
+
+
+def key_hashes(snap, keys):
+    """Per key of `keys` (each present in the key-major snapshot `snap`): a 64-bit hash of its CommandsForKey state --
+    every TxnInfo (TxnId, executeAt, status) in order and each one's missing[] TxnIds in order -- plus (entries, missing)
+    counts. Vectorised over the selected keys."""
+    def mix(x):
+        with np.errstate(over="ignore"):
+            x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            return x ^ (x >> np.uint64(31))
+    k = np.searchsorted(snap["key"], keys)
+    assert np.array_equal(snap["key"][k], keys), "a sampled key is missing from the state"
+    eo = snap["ent_off"].astype(np.int64)
+    mo = snap["miss_off"].astype(np.int64)
+    e0, e1 = eo[k], eo[k + 1]
+    m0, m1 = mo[e0], mo[e1]
+
+    def seg(cols, a, b, salt):
+        n = b - a
+        idx = np.repeat(a, n) + (np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n))
+        pos = (idx - np.repeat(a, n)).astype(np.uint64)
+        with np.errstate(over="ignore"):
+            h = np.full(len(idx), np.uint64(salt))
+            for c in cols:
+                h = mix(h ^ (np.asarray(c)[idx].astype(np.int64).astype(np.uint64) + pos * np.uint64(0x9E3779B97F4A7C15)))
+            cs = np.concatenate([[np.uint64(0)], np.cumsum(h, dtype=np.uint64)])
+            ends = np.cumsum(n)
+            return cs[ends] - cs[ends - n]
+    he = seg([snap["emsb"], snap["elsb"], snap["enode"], snap["xmsb"], snap["xlsb"], snap["xnode"], snap["status"],
+              np.diff(mo)], e0, e1, 11)
+    hm = seg([snap["mmsb"], snap["mlsb"], snap["mnode"]], m0, m1, 13)
+    with np.errstate(over="ignore"):
+        h = mix(he + np.uint64(0x632BE59BD9B4E019)) ^ mix(hm + (e1 - e0).astype(np.uint64))
+    return h, (e1 - e0).astype(np.int64), (m1 - m0).astype(np.int64)

@@ -180,6 +180,41 @@ def config2_all(workers=8):
     print(path, os.path.getsize(path), "bytes")
 
 
+def cfk_zipf_keys(upd, seed=0xC4F):
+    """The sampled keys of the bench's zipf CommandsForKey update stream: hot keys near 50K, 20K, 10K, 5K, 2K and 1K
+    (update, key) pairs (1, 2, 4, 8, 16 and 16 of them) plus 3,000 keys drawn uniformly from the rest."""
+    keys, cnt = np.unique(upd["key"], return_counts=True)
+    rng = np.random.default_rng(seed)
+    pick = []
+    for target, m in ((50_000, 1), (20_000, 2), (10_000, 4), (5_000, 8), (2_000, 16), (1_000, 16)):
+        pick.extend(np.argsort(np.abs(cnt - target))[:m].tolist())
+    rest = np.setdiff1d(np.arange(len(keys)), pick)
+    pick.extend(rng.choice(rest, size=3_000, replace=False).tolist())
+    return np.sort(keys[np.unique(pick)])
+
+
+def cfk_zipf():
+    """N4 at bench size: workload.cfk_update_stream(1M txns x 8 keys over 1M keys, zipf 0.99) -- the bench's cfk_apply_zipf
+    leg -- restricted to a key sample (cfk_zipf_keys: hot keys up to ~50K updates and 3,000 others; keys are independent)
+    and applied to an empty store by the C restatement: per key a 64-bit hash of its final CommandsForKey state and its
+    entry / missing[] counts, plus the stream's sha256."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cfk_cases as CC
+    upd = W.cfk_update_stream(1_000_000, 8, 1_000_000, dist="zipf")
+    h = hashlib.sha256()
+    for k in sorted(upd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(upd[k]).tobytes())
+    keys = cfk_zipf_keys(upd)
+    o = oracle.cfk_apply(CC.empty_snapshot(), CC.restrict(upd, keys))
+    kh, ne, nm = CC.key_hashes(o, keys)
+    path = os.path.join(HERE, "cfk_zipf_sample.npz")
+    np.savez_compressed(path, stream_sha256=np.frombuffer(h.digest(), np.uint8), keys=keys, hash64=kh,
+                        entries=ne.astype(np.uint32), missing=nm.astype(np.uint32))
+    print(path, os.path.getsize(path), "bytes;", len(keys), "keys,", int(ne.sum()), "entries,", int(nm.sum()), "missing")
+
+
 def sub_batch(b, keyset):
     """Every txn of b, keys restricted to `keyset` (sorted unique codes)."""
     keep = np.isin(b.key_code, keyset)
@@ -295,5 +330,7 @@ if __name__ == "__main__":
         config2()
     if which in ("2all", "all"):
         config2_all()
+    if which in ("cfkz", "all"):
+        cfk_zipf()
     if which in ("3", "all"):
         config3()

@@ -194,6 +194,33 @@ def test_cfk_zipf_update_stream(ctx):
     assert st["cfk.hot_keys"] > 0 and st["cfk.hot_irregular"] == 0
 
 
+def test_cfk_zipf_bench_stream_key_sample(ctx):
+    """N4 at bench size: the bench's zipf(0.99) update stream (1M txns x 8 keys over 1M keys: 2M updates, 15.9M
+    (update, key) pairs, 190M deps; the hottest key holds 835K pairs) applied to an empty store on the GPU, and the final
+    CommandsForKey state of 3,047 sampled keys -- hot keys up to ~54K updates among them -- compared with the C
+    restatement run on the stream restricted to those keys (tests/golden/cfk_zipf_sample.npz; keys are independent)."""
+    import hashlib
+    import os
+    from accord_amd import workload as W
+    from accord_amd.deps import cfk_apply
+    here = os.path.dirname(os.path.abspath(__file__))
+    fx = np.load(os.path.join(here, "golden", "cfk_zipf_sample.npz"))
+    upd = W.cfk_update_stream(1_000_000, 8, 1_000_000, dist="zipf")
+    h = hashlib.sha256()
+    for k in sorted(upd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(upd[k]).tobytes())
+    assert h.digest() == bytes(fx["stream_sha256"]), "update-stream generator changed"
+    g = cfk_apply(ctx, CC.empty_snapshot(), upd)
+    st = ctx.stats()
+    assert st["cfk.hot_keys"] > 10_000 and st["cfk.hot_irregular"] == 0
+    kh, ne, nm = CC.key_hashes(g, fx["keys"])
+    np.testing.assert_array_equal(ne, fx["entries"].astype(np.int64))
+    np.testing.assert_array_equal(nm, fx["missing"].astype(np.int64))
+    bad = np.flatnonzero(kh != fx["hash64"])
+    assert len(bad) == 0, f"{len(bad)} keys differ, first {fx['keys'][bad[:5]].tolist()}"
+
+
 def test_cfk_update_stream(ctx):
     """The bench leg's update stream (workload.cfk_update_stream: Accept with deps, then commit / stable / apply /
     invalidate with deps, interleaved) at 20,000 txns x 4 keys, applied in one call and in two chained halves."""
