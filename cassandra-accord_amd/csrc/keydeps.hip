@@ -1157,31 +1157,52 @@ struct V2Query {
 };
 
 // The query of the pair at CFK position p (pair order (key, TxnId)): every per-txn input comes from the
-// position-ordered columns, so neighbouring lanes read neighbouring rows.
+// position-ordered columns, so neighbouring lanes read neighbouring rows. The loads are ordered for a short dependency
+// chain: the pair's own row and columns; then its segment's bounds; then, together, the segment start's row, the
+// bumped-committed count at the segment end, and -- speculatively, assuming M is the last unbumped committed Write
+// before the pair (it is unless the segment holds bumped committed entries or the query's executeAt is bumped, ~1.5% of
+// pairs, recomputed below) -- that Write's TxnId and its row.
 __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
 {
     V2Query q;
-    const Row rpp = ld_row(v, p);   // the insert position's row for the ~90% of pairs with executeAt == TxnId, issued
-                                    // with the pair's own columns instead of after the segment lookup
-    uint32_t seg = v.seg_incl[p] - 1;
+    const Row rpp = ld_row(v, p);
+    const uint32_t seg = v.seg_incl[p] - 1;
     q.trank = v.s_rank[p];
-    uint32_t S = v.s_exec[p];
+    const uint32_t S = v.s_exec[p];
     q.info = v.s_info[p];
     q.s0 = v.seg_start[seg];
-    uint32_t s1 = v.seg_start[seg + 1];
+    const uint32_t s1 = v.seg_start[seg + 1];
     q.wk = witnesses(q.info >> 3);
     q.wc = wk_classes(q.wk);
     q.bq = S != q.trank;
+    // level 3: issued together
+    const uint32_t lu0 = rpp.c[RW_LUCW];
+    const bool spec = !q.bq && lu0 > q.s0;   // the last unbumped committed Write before p lies in p's segment
+    q.r0 = ld_row(v, q.s0);
+    const uint32_t b1 = ld_cbc(v, s1);
+    uint32_t mu = 0;
+    Row rms = q.r0;
+    if (spec) { mu = v.s_rank[lu0 - 1]; rms = ld_row(v, lu0 - 1); }
+    const uint32_t b0 = q.r0.c[RW_CBC];
+    if (!q.bq && b1 == b0) {
+        // common path: no bumped committed entry in the segment, executeAt == TxnId
+        q.pos = p;
+        q.rp = rpp;
+        q.has_m = spec;
+        q.m = mu;
+        q.posm = spec ? lu0 - 1 : q.s0;
+        q.rm = rms;
+        q.bend = q.rm.c[RW_CBC];
+        q.bstart = q.bend;   // no bumped committed entry before posM in this segment (b1 == b0)
+        return q;
+    }
     q.pos = q.bq ? lower_bound_u32(v.s_rank, p + 1, s1, S) : p;
     q.rp = q.bq ? ld_row(v, q.pos) : rpp;
-    q.r0 = ld_row(v, q.s0);
     // M from the last unbumped committed Write before pos
-    uint32_t lu = q.rp.c[RW_LUCW];
-    bool has_mu = lu > q.s0;
-    uint32_t mu = has_mu ? v.s_rank[lu - 1] : 0;
+    const uint32_t lu = q.rp.c[RW_LUCW];
+    const bool has_mu = lu > q.s0;
+    if (q.bq) mu = has_mu ? v.s_rank[lu - 1] : 0;
     // M from bumped committed Writes of this segment: predecessor of S by executeAt, then nearest Write
-    uint32_t b0 = q.r0.c[RW_CBC];
-    uint32_t b1 = ld_cbc(v, s1);
     bool has_mb = false;
     uint32_t mb = 0;
     if (b1 > b0) {
@@ -1196,7 +1217,7 @@ __device__ __forceinline__ V2Query v2_query(const V2View &v, uint32_t p)
     if (!q.has_m) q.posm = q.s0;
     else if (has_mu && q.m == mu) q.posm = lu - 1;
     else q.posm = lower_bound_u32(v.s_rank, q.s0, q.pos, q.m);
-    q.rm = q.posm == q.s0 ? q.r0 : ld_row(v, q.posm);
+    q.rm = q.posm == q.s0 ? q.r0 : (spec && q.posm == lu0 - 1) ? rms : ld_row(v, q.posm);
     q.bend = q.rm.c[RW_CBC];
     q.bstart = q.has_m ? lower_bound_lo32(v.bc_pm, b0, q.bend, q.m + 1) : q.bend;
     return q;
@@ -1248,6 +1269,9 @@ __device__ unsigned long long *g_ct_prof;
 #define CT_PH(i) ((void)0)
 #endif
 
+#ifndef ACC_R3U
+#define ACC_R3U 4   // R3 candidates loaded per round of the count pass's loops
+#endif
 __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
                                                   const RecOut &ro, uint32_t *__restrict__ bigflag)
 {
@@ -1269,15 +1293,30 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         l[2 * c + 1] = q.rp.c[3 + c] - q.rm.c[3 + c];
         e += l[2 * c] + l[2 * c + 1];
     }
-    for (uint32_t i = q.bstart; i < q.bend; i += 4) {   // R3 candidates, four loads in flight
-        uint32_t ex[4], kd[4];
+    // the class runs' entries of a record that may be inline (L6 <= 16: e <= 15 needs it) are loaded before the R3
+    // candidates are counted, so both sets of loads are in flight together (static slots, predicated)
+    uint32_t pre[6], L6 = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
+    for (int q2 = 0; q2 < 6; ++q2) { pre[q2] = L6; L6 += l[q2]; }
+    uint32_t xs[REC_INLINE + 1];
+    const bool may_inline = L6 <= REC_INLINE + 1;
+#pragma unroll
+    for (uint32_t s = 0; s <= REC_INLINE; ++s) {
+        uint32_t idx = a[0] + s;
+#pragma unroll
+        for (int q2 = 1; q2 < 6; ++q2)
+            if (s >= pre[q2]) idx = a[q2] + (s - pre[q2]);   // empty runs are overridden by the next one
+        xs[s] = (may_inline && s < L6) ? v.list_rank[idx] : 0u;
+    }
+    for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {   // R3 candidates, ACC_R3U loads in flight
+        uint32_t ex[ACC_R3U], kd[ACC_R3U];
+#pragma unroll
+        for (uint32_t u = 0; u < ACC_R3U; ++u) {
             ex[u] = i + u < q.bend ? v.bc_exec[i + u] : 0u;
             kd[u] = i + u < q.bend ? (uint32_t)v.bc_kind[i + u] : 0u;
         }
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) e += (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u)) ? 1u : 0u;
+        for (uint32_t u = 0; u < ACC_R3U; ++u) e += (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u)) ? 1u : 0u;
     }
     if (q.bq) {
         uint32_t st = q.info & 7u, kind = q.info >> 3;
@@ -1285,20 +1324,7 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
     }
     CT_PH(2);
     if (e <= REC_INLINE) {
-        // the six class runs hold L6 <= e + 1 <= 8 elements (T itself is dropped at most once): all their loads are
-        // issued together (static slots, predicated), not one dependent load per element
-        uint32_t pre[6], L6 = 0;
-#pragma unroll
-        for (int q2 = 0; q2 < 6; ++q2) { pre[q2] = L6; L6 += l[q2]; }
-        uint32_t xs[REC_INLINE + 1];
-#pragma unroll
-        for (uint32_t s = 0; s <= REC_INLINE; ++s) {
-            uint32_t idx = a[0] + s;
-#pragma unroll
-            for (int q2 = 1; q2 < 6; ++q2)
-                if (s >= pre[q2]) idx = a[q2] + (s - pre[q2]);   // empty runs are overridden by the next one
-            xs[s] = s < L6 ? v.list_rank[idx] : 0u;
-        }
+        // (L6 <= e + 1 <= 16: T itself is dropped at most once, so xs holds every class entry)
         uint32_t d = L6;   // position of T among them (at most one)
 #pragma unroll
         for (uint32_t s = 0; s <= REC_INLINE; ++s)
@@ -1308,17 +1334,17 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
         for (uint32_t s = 0; s < REC_INLINE; ++s) buf[s] = s < d ? xs[s] : xs[s + 1];
         uint32_t n = L6 - (d < L6 ? 1u : 0u);
         if (q.has_m)
-            for (uint32_t i = q.bstart; i < q.bend; i += 4) {   // R3 candidates, four at a time
-                uint32_t ex[4], kd[4], xr[4];
+            for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {   // R3 candidates, ACC_R3U at a time
+                uint32_t ex[ACC_R3U], kd[ACC_R3U], xr[ACC_R3U];
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
+                for (uint32_t u = 0; u < ACC_R3U; ++u) {
                     const bool in = i + u < q.bend;
                     ex[u] = in ? v.bc_exec[i + u] : 0u;
                     kd[u] = in ? (uint32_t)v.bc_kind[i + u] : 0u;
                     xr[u] = in ? v.bc_rank[i + u] : 0u;
                 }
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u)
+                for (uint32_t u = 0; u < ACC_R3U; ++u)
                     if (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u) && !(q.bq && xr[u] == q.trank))
                         inl_put(buf, n, xr[u]);
             }
@@ -2304,8 +2330,8 @@ __global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t
 
 // ---------------------------------------------------------------- v3: streaming write pass
 //
-// A txn with at most ST_K keys, at most ST_N2 dependency entries and at most ST_RAW raw run elements (config 2: ~99%
-// of txns) is finished by one kernel, k_v3_stream: a tile of ST_T txns per block, ST_G lanes per txn, takes the
+// A txn with at most ST_G keys, at most ST_N2 dependency entries and at most ST_RAW raw run elements (config 2: ~99% of
+// txns) is finished by one kernel, k_v3_stream: a tile of txns per block, one lane per key, takes the
 // inline entries of its count-pass records and gathers the entries of its run records, sorts the (rank, key) entries
 // in LDS, counts the distinct TxnIds, takes the tile's output offsets (arena, keys, TxnIds) from a decoupled look-back
 // over the previous tiles' sizes and writes the final KeyDeps arrays (arena_off / kd_off / u_off, arena, key_idx,
@@ -2314,29 +2340,34 @@ __global__ __launch_bounds__(BLOCK) void k_fb_sizes(uint32_t nfb, const uint32_t
 // order (k_v3_bigfill gives them per-pair offsets, so the tiers' indexing is unchanged), report their sizes to the
 // stream pass; their KeyDeps headers, key indices and entries go straight to the final arrays.
 
-constexpr int ST_G = 16;                      // lanes per txn
-constexpr int ST_K = 16;                      // keys of a stream txn
-constexpr int ST_N2 = 128;                    // dependency entries of a stream txn (LDS sort buffer, power of two)
+constexpr int ST_G = 16;                      // lanes per txn of the stream pass (one key per lane)
+constexpr int ST_N2 = 128;                    // its dependency entries (LDS sort buffer, power of two)
+constexpr int ST_SLOT = ST_N2;                // TxnId scratch slot per stream txn (t * ST_SLOT)
 constexpr uint32_t ST_RAW = 1024;             // raw run elements of a stream txn
+constexpr int MK_G = 8;                       // lanes per txn of the mark pass
 
-// Per txn, ST_G lanes: its KeyDeps sizes A = Kd + E (arena ints) and K = Kd (keys with >= 1 dependency) from the
-// count-pass records' word 15 (the exclusive scans of A and K are the txns' arena / key offsets, so the stream pass needs
-// no look-back), and the big-txn classification: more than ST_K keys, or (txns with a run record: bigflag = 1 from the
-// count pass) more than ST_N2 entries or ST_RAW raw run elements. bigflag becomes the 0/1 big flag.
+// Per txn, MK_G lanes: its KeyDeps sizes A = Kd + E (arena ints) and K = Kd (keys with >= 1 dependency) from the
+// count-pass records' word 7 (the exclusive scans of A and K are the txns' arena / key offsets, so the stream pass needs
+// no look-back), and the classification: a stream txn has <= ST_G keys and <= ST_N2 entries (and, with run records:
+// bigflag = 1 from the count pass, <= ST_RAW raw run elements), else it is big (bigflag = 1: the v2 tiers). (8 lanes per
+// txn measured faster than 16 for the 8-key txns of configs 2 / 3; a 16-lane stream pass with 8 lanes per txn lost:
+// its sort and gather sizes are wave-uniform maxima over twice the txns.)
 __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *__restrict__ key_off,
                                                    const uint32_t *__restrict__ irec32, const uint4 *__restrict__ rec,
-                                                   uint32_t *__restrict__ psz, uint32_t raw_cap, uint32_t e_cap,
+                                                   uint32_t *__restrict__ psz, uint32_t raw_cap,
                                                    uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
                                                    uint64_t *__restrict__ szK, uint64_t *__restrict__ any16,
                                                    uint64_t *__restrict__ eb)
 {
-    const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / ST_G, sub = threadIdx.x & (ST_G - 1);
+    const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / MK_G, sub = threadIdx.x & (MK_G - 1);
     if (t >= n) return;   // group-uniform: shuffles stay inside the group
     const uint32_t j0 = key_off[t], nk = key_off[t + 1] - j0;
     const bool run_rec = bigflag[t] != 0;
-    const bool maybe_big = run_rec || nk > (uint32_t)ST_K;
+    // could be big: a run record, more than ST_G keys, or more than 8 keys (8 inline records hold at most 8 * 15 <= ST_N2
+    // entries; more may sum past ST_N2)
+    const bool maybe_big = run_rec || nk > 8u;
     uint32_t e = 0, kd = 0, raw = 0;
-    for (uint32_t c0 = 0; c0 < nk; c0 += ST_G) {
+    for (uint32_t c0 = 0; c0 < nk; c0 += MK_G) {
         if (c0 + sub < nk) {
             const uint32_t w = irec32[IREC_W * (size_t)(j0 + c0 + sub) + 7];
             const uint32_t ej = w & ~REC_INLINE_FLAG;
@@ -2351,12 +2382,13 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
         }
     }
 #pragma unroll
-    for (int d = 1; d < ST_G; d <<= 1) {
+    for (int d = 1; d < MK_G; d <<= 1) {
         e += __shfl_xor(e, d, 64);
         kd += __shfl_xor(kd, d, 64);
         raw += __shfl_xor(raw, d, 64);
     }
-    const bool big = nk > (uint32_t)ST_K || (run_rec && (e > e_cap || raw > raw_cap));
+    // (an all-inline txn of 9-16 keys can hold up to 240 entries: beyond ST_N2 it is big)
+    const bool big = nk > (uint32_t)ST_G || e > (uint32_t)ST_N2 || (run_rec && raw > raw_cap);
     if (sub == 0) {
         bigflag[t] = big ? 1u : 0u;
         szA[t] = (uint64_t)kd + e;
@@ -2375,7 +2407,6 @@ __global__ __launch_bounds__(BLOCK) void k_v3_compact(uint32_t n, const uint32_t
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     if (t < n && bigflag[t]) blist[bpos[t]] = t;
 }
-
 // tier routing of the big txns (thread per list entry, one atomic per list per block). With ranks within 25 bits: the
 // window tier (<= 8 or <= 16 keys; gstat[7] / gstat[8]), else medium (E <= MED_E, <= MED_K keys) or the u32-record
 // block tier; with wider ranks: the u64 wave tier (E <= MED_E, <= MED_K keys) or the global path.
@@ -2479,20 +2510,22 @@ __global__ __launch_bounds__(BLOCK) void k_v3_bigfill(uint32_t nbig, V3Big b)
 struct V3Stream {
     V2View v;
     const uint32_t *key_off, *bigflag, *txn_of_rank;
+    const uint32_t *list;                     // LIST: the txns of the pass (else every txn, the stream ones taken)
     const uint4 *rec, *irec;
     const uint64_t *arena_off, *kd_off;       // from the size scans
     uint64_t *u_cnt_out;
     int32_t *arena;
-    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's slot t * ST_N2, compacted by k_v3_ucompact
+    uint32_t *key_idx, *dep_scr;              // dep_scr: TxnIds at the txn's slot t * ST_SLOT, compacted by k_v3_ucompact
     uint64_t *err;                            // gather count mismatches
     uint32_t n, ntiles;
 };
 
-// inclusive prefix over the ST_G lanes of a group
+// inclusive prefix over the G lanes of a group
+template <int G>
 __device__ __forceinline__ uint32_t group_inclusive(uint32_t x, uint32_t sub)
 {
 #pragma unroll
-    for (uint32_t d = 1; d < (uint32_t)ST_G; d <<= 1) {
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
         const uint32_t u = __shfl_up(x, d, 64);
         if (sub >= d) x += u;
     }
@@ -2505,28 +2538,28 @@ __device__ __forceinline__ T gshfl_xor(T v, int m)
     if constexpr (sizeof(T) == 8) return shfl_xor64(v, m);
     else return (T)__shfl_xor(v, m, 64);
 }
-// Sorts buf[0, 16 * R) of a ST_G-lane group ascending (positions >= n_valid read as all-ones pads) with R entries per
-// lane in registers, element i = r * 16 + sub: partners at distance < 16 are lanes of the group (shuffles), the others
-// registers of the same lane. Writes the sorted entries back.
-template <class EntT, int R>
+// Sorts buf[0, G * R) of a G-lane group ascending (positions >= n_valid read as all-ones pads) with R entries per lane
+// in registers, element i = r * G + sub: partners at distance < G are lanes of the group (shuffles), the others registers
+// of the same lane. Writes the sorted entries back.
+template <class EntT, int G, int R>
 __device__ __forceinline__ void group_reg_sort(EntT *buf, uint32_t sub, uint32_t n_valid)
 {
     EntT v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t i = r * ST_G + sub;
+        const uint32_t i = r * G + sub;
         v[r] = i < n_valid ? buf[i] : ~(EntT)0;
     }
 #pragma unroll
-    for (uint32_t k = 2; k <= (uint32_t)(ST_G * R); k <<= 1) {
+    for (uint32_t k = 2; k <= (uint32_t)(G * R); k <<= 1) {
 #pragma unroll
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            if (jj >= (uint32_t)ST_G) {
+            if (jj >= (uint32_t)G) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const int r2 = r ^ (int)(jj / ST_G);
+                    const int r2 = r ^ (int)(jj / G);
                     if (r2 > r) {
-                        const bool up = (((uint32_t)r * ST_G + sub) & k) == 0;
+                        const bool up = (((uint32_t)r * G + sub) & k) == 0;
                         const EntT a = v[r], b = v[r2];
                         if ((a > b) == up) { v[r] = b; v[r2] = a; }
                     }
@@ -2535,7 +2568,7 @@ __device__ __forceinline__ void group_reg_sort(EntT *buf, uint32_t sub, uint32_t
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const EntT y = gshfl_xor(v[r], (int)jj);
-                    const bool up = (((uint32_t)r * ST_G + sub) & k) == 0, lower = (sub & jj) == 0;
+                    const bool up = (((uint32_t)r * G + sub) & k) == 0, lower = (sub & jj) == 0;
                     const EntT lo = v[r] < y ? v[r] : y, hi = v[r] < y ? y : v[r];
                     v[r] = (lower == up) ? lo : hi;
                 }
@@ -2543,7 +2576,7 @@ __device__ __forceinline__ void group_reg_sort(EntT *buf, uint32_t sub, uint32_t
         }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) buf[r * ST_G + sub] = v[r];
+    for (int r = 0; r < R; ++r) buf[r * G + sub] = v[r];
 }
 
 #ifdef ACC_PHASE_PROF
@@ -2558,25 +2591,30 @@ __device__ unsigned long long *g_st_prof;
 #ifndef ACC_ST_WAVES
 #define ACC_ST_WAVES 24   // resident waves per CU the stream pass is compiled for (32: a 64-VGPR budget that spills)
 #endif
-template <class EntT, int NT>
+// G lanes per txn (one key each), N2 entries per txn at most. LIST = false: every txn (the stream ones taken); true: the
+// txns of s.list[0, s.n).
+template <class EntT, int NT, int G, int N2, bool LIST>
 __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stream s)
 {
-    constexpr int TT = NT / ST_G;   // txns per tile
+    constexpr int TT = NT / G;   // txns per tile
+    constexpr uint32_t KB = G <= 8 ? 3 : 4;   // key bits under the rank in an entry
+    static_assert(G <= 16, "entries keep the key index in 4 bits");
 #ifdef ACC_PHASE_PROF
     uint64_t ph[8];
 #endif
     ST_PH(0);
-    __shared__ EntT ent[TT][ST_N2];
-    __shared__ uint32_t kc[TT][ST_K];
-    __shared__ uint32_t kbase[TT][ST_K];
-    __shared__ uint16_t stA[TT][ST_K + ST_N2];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (ST_G - 1), grp = tid / ST_G, g0 = lane & (64 - ST_G);
-    const uint64_t gmask = ((1ull << ST_G) - 1) << g0;
+    __shared__ EntT ent[TT][N2];
+    __shared__ uint32_t kc[TT][G];
+    __shared__ uint32_t kbase[TT][G];
+    __shared__ uint16_t stA[TT][G + N2];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), sub = lane & (G - 1), grp = tid / G, g0 = lane & (64 - G);
+    const uint64_t gmask = ((1ull << G) - 1) << g0;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     // no block barriers: every wave is independent (its txns' arena / key offsets come from the size scans)
-    const uint32_t tile = blockIdx.x * (NT / 64) + (tid >> 6);   // wave tile: 64 / ST_G txns
-    const uint32_t t = tile * (64 / ST_G) + (lane >> 4);
-    const bool valid = t < s.n;
+    const uint32_t tile = blockIdx.x * (NT / 64) + (tid >> 6);   // wave tile: 64 / G txns
+    const uint32_t slot = tile * (64 / G) + lane / G;
+    const bool valid = slot < s.n;
+    const uint32_t t = LIST ? (valid ? s.list[slot] : 0u) : slot;
     TxnCtx c{};
     bool big = false;
     uint64_t aoff = 0, koff = 0;
@@ -2619,9 +2657,9 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         }
     }
     const uint32_t ein = run ? 0u : e;
-    const uint32_t e_incl = group_inclusive(e, sub), in_incl = group_inclusive(ein, sub);
-    const uint32_t E = __shfl(e_incl, (int)(g0 + ST_G - 1), 64);
-    const uint32_t E_in = __shfl(in_incl, (int)(g0 + ST_G - 1), 64);
+    const uint32_t e_incl = group_inclusive<G>(e, sub), in_incl = group_inclusive<G>(ein, sub);
+    const uint32_t E = __shfl(e_incl, (int)(g0 + G - 1), 64);
+    const uint32_t E_in = __shfl(in_incl, (int)(g0 + G - 1), 64);
     const uint64_t nzb = __ballot(e != 0) & gmask;
     const uint32_t Kd = (uint32_t)__popcll(nzb);
     const uint64_t A = sm ? (uint64_t)Kd + E : 0;
@@ -2632,7 +2670,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         const uint32_t b0 = in_incl - ein;
 #pragma unroll
         for (uint32_t q = 0; q < REC_INLINE; ++q)
-            if (q < e) buf[b0 + q] = ((EntT)w[q] << 4) | (EntT)sub;
+            if (q < e) buf[b0 + q] = ((EntT)w[q] << KB) | (EntT)sub;
     }
     ST_PH(2);
     // ---- run records, one key at a time (its runs broadcast from the owning lane): the group gathers the flattened
@@ -2642,7 +2680,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     const uint32_t nrun = (uint32_t)__popcll(runmask);
     uint32_t wnrun = nrun;
 #pragma unroll
-    for (int d = ST_G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
+    for (int d = G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
     uint32_t cursor = E_in;
     uint64_t rem = runmask;
     for (uint32_t ri = 0; ri < wnrun; ++ri) {
@@ -2661,8 +2699,8 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         const uint32_t kj = (uint32_t)(src - (int)g0);
         uint32_t wr = raw;
 #pragma unroll
-        for (int d = ST_G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
-        for (uint32_t c0 = 0; c0 < wr; c0 += ST_G) {
+        for (int d = G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
+        for (uint32_t c0 = 0; c0 < wr; c0 += G) {
             const uint32_t off = c0 + sub;
             bool keep = false;
             uint32_t x = 0;
@@ -2685,8 +2723,8 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
             }
             const uint64_t bal = __ballot(keep) & gmask;
             if (keep) {
-                const uint32_t slot = cursor + (uint32_t)__popcll(bal & lt);
-                if (slot < (uint32_t)ST_N2) buf[slot] = ((EntT)x << 4) | (EntT)kj;
+                const uint32_t at = cursor + (uint32_t)__popcll(bal & lt);
+                if (at < (uint32_t)N2) buf[at] = ((EntT)x << KB) | (EntT)kj;
             }
             cursor += (uint32_t)__popcll(bal);
         }
@@ -2699,27 +2737,27 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     }
     uint32_t wE = ok ? E : 0;
 #pragma unroll
-    for (int d = ST_G; d < 64; d <<= 1) wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
+    for (int d = G; d < 64; d <<= 1) wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // ---- sort each group's entries: registers + shuffles up to 64 entries (wave-uniform choice), LDS bitonic beyond
-    if (wE <= 16) group_reg_sort<EntT, 1>(buf, sub, ok ? E : 0);
-    else if (wE <= 32) group_reg_sort<EntT, 2>(buf, sub, ok ? E : 0);
-    else if (wE <= 64) group_reg_sort<EntT, 4>(buf, sub, ok ? E : 0);
+    // ---- sort each group's entries: registers + shuffles up to 4 per lane (wave-uniform choice), LDS bitonic beyond
+    if (wE <= (uint32_t)G) group_reg_sort<EntT, G, 1>(buf, sub, ok ? E : 0);
+    else if (wE <= 2u * G) group_reg_sort<EntT, G, 2>(buf, sub, ok ? E : 0);
+    else if (wE <= 4u * G) group_reg_sort<EntT, G, 4>(buf, sub, ok ? E : 0);
     else {
-        uint32_t n2 = 16;
+        uint32_t n2 = G;
         while (n2 < E) n2 <<= 1;
         if (!ok) n2 = 0;
-        for (uint32_t q = E + sub; q < n2; q += ST_G) buf[q] = ~(EntT)0;
+        for (uint32_t q = E + sub; q < n2; q += G) buf[q] = ~(EntT)0;
         uint32_t wn2 = n2;
 #pragma unroll
-        for (int d = ST_G; d < 64; d <<= 1) wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
+        for (int d = G; d < 64; d <<= 1) wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         for (uint32_t k = 2; k <= wn2; k <<= 1) {
             for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
                 if (k <= n2) {
-                    for (uint32_t pi = sub; pi < (n2 >> 1); pi += ST_G) {
+                    for (uint32_t pi = sub; pi < (n2 >> 1); pi += G) {
                         const uint32_t i = ((pi & ~(jj - 1)) << 1) | (pi & (jj - 1));
                         const uint32_t l = i | jj;
                         const EntT xa = buf[i], ya = buf[l];
@@ -2736,28 +2774,28 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     ST_PH(4);
     // ---- KeyDeps in LDS: the arena (header ints and per-key TxnId indices) staged as u16; the distinct TxnIds go
-    // straight to the txn's fixed scratch slot t * ST_N2
+    // straight to the txn's fixed scratch slot t * ST_SLOT
     uint32_t distinct = 0;
     if (ok && e != 0) stA[grp][(uint32_t)__popcll(nzb & lt)] = (uint16_t)(Kd + e_incl);
-    for (uint32_t q0 = 0; q0 < wE; q0 += ST_G) {
+    for (uint32_t q0 = 0; q0 < wE; q0 += G) {
         const uint32_t q = q0 + sub;
         const bool in = ok && q < E;
         const EntT x = in ? buf[q] : (EntT)0;
         const EntT pv = (in && q > 0) ? buf[q - 1] : (EntT)0;
-        const uint32_t kj = (uint32_t)(x & 15u);
-        const bool nw = in && (q == 0 || (x >> 4) != (pv >> 4));
+        const uint32_t kj = (uint32_t)(x & ((1u << KB) - 1u));
+        const bool nw = in && (q == 0 || (x >> KB) != (pv >> KB));
         const uint64_t bal = __ballot(nw) & gmask;
         const uint32_t idx = distinct + (uint32_t)__popcll(bal & lt) + (nw ? 1u : 0u) - 1u;
         uint64_t peers = __ballot(in) & gmask;
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
+        for (uint32_t bb = 0; bb < KB; ++bb) {
             const uint64_t m = __ballot((kj >> bb) & 1u);
             peers &= ((kj >> bb) & 1u) ? m : ~m;
         }
         const uint32_t before = (uint32_t)__popcll(peers & lt);
         if (in) {
             stA[grp][Kd + kbase[grp][kj] + kc[grp][kj] + before] = (uint16_t)idx;
-            if (nw) s.dep_scr[(size_t)t * ST_N2 + idx] = s.txn_of_rank[(uint32_t)(x >> 4)];
+            if (nw) s.dep_scr[(size_t)t * ST_SLOT + idx] = s.txn_of_rank[(uint32_t)(x >> KB)];
         }
         __builtin_amdgcn_wave_barrier();
         if (in && before == 0) kc[grp][kj] += (uint32_t)__popcll(peers);
@@ -2770,7 +2808,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     // ---- the staged arena and key indices to their places
     if (!valid) return;
     if (ok) {
-        for (uint32_t q = sub; q < (uint32_t)A; q += ST_G) s.arena[aoff + q] = (int32_t)stA[grp][q];
+        for (uint32_t q = sub; q < (uint32_t)A; q += G) s.arena[aoff + q] = (int32_t)stA[grp][q];
         if (e != 0) s.key_idx[koff + (uint32_t)__popcll(nzb & lt)] = sub;
     }
 #ifdef ACC_PHASE_PROF
@@ -2800,7 +2838,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_nelist(uint32_t n, const uint32_t 
     if (t == 0) ne_uoff[*cnt] = u_off[n];
 }
 
-// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: at its slot t * ST_N2 of dep_scr; big
+// KeyDeps.txnIds: each txn's distinct TxnIds from its scratch (stream txns: at its slot t * ST_SLOT of dep_scr; big
 // txns: at vdep_off of its first pair in dep_big) to dep_txn[u_off[t] ...). A block takes a fixed chunk
 // of UC_CHUNK outputs (the uncommitted window's txns are consecutive and hold most TxnIds: partitioning by txns left a
 // few blocks with most of the work), finds the txns spanning it by binary search over u_off, and strides over the
@@ -2842,7 +2880,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_ucompact(uint32_t n, const uint64_
     const uint32_t tlo = s_t[0], thi = s_t[1];
     auto source = [&](uint32_t j) {
         const uint32_t t = tmap ? tmap[j] : j;
-        return bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_N2;
+        return bigflag[t] ? (vdep_off[key_off[t]] | (1ull << 63)) : (uint64_t)t * ST_SLOT;
     };
     if (thi - tlo >= 8 * BLOCK) {
         // sparse chunk (long runs of txns without TxnIds, e.g. the range txns of a mixed batch): every output finds its
@@ -3340,7 +3378,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
     // the count / mark passes' accumulators, zeroed by the column kernels (txn records, k_v2_apply); bigflag above
-    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);
+    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);   // E, big txns, a 9-16-key big txn
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N + 6);   // + the batch totals and E / big counts (k_v3_ucompact)
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
@@ -3454,13 +3492,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
                 sum[7] / P);
     }
 #endif
-    const uint32_t raw_cap = ST_RAW, e_cap = ST_N2;
+    const uint32_t raw_cap = ST_RAW;
     uint64_t *kd_off = ctx->get<uint64_t>("kd_off", (size_t)n + 1);
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
     uint64_t *eb = ctx->get<uint64_t>("v3_eb", n), *dB = ctx->get<uint64_t>("v3_dB", (size_t)n + 1);
-    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * ST_G, BLOCK)), dim3(BLOCK), 0, n, key_off, (const uint32_t *)ro.irec, (const uint4 *)rec, psz,
-           raw_cap, e_cap, bigflag, szA, szK, tot + 2, eb);
+    launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * MK_G, BLOCK)), dim3(BLOCK), 0, n, key_off,
+           (const uint32_t *)ro.irec, (const uint4 *)rec, psz, raw_cap, bigflag, szA, szK, tot + 2, eb);
     uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
     {   // arena / key offsets, the count pass's per-block entry totals, the big txns' TxnId scratch bases: one launch
         const uint64_t *si[4] = { szA, szK, blk_e, eb };
@@ -3501,7 +3539,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v2_write_huge", k_v2_write_big<HUGE_E, 1024>, dim3(std::min<unsigned>(nbig, 64)), dim3(1024), 0,
                (const uint32_t *)wo.huge_list, vv, (const uint64_t *)vcnt, wo);
     };
-    uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_N2);   // stream txns' TxnIds, slot t * ST_N2
+    uint32_t *dep_st = ctx->get<uint32_t>("v3_dep_stream", (size_t)n * ST_SLOT);   // stream txns' TxnIds, slot t * ST_SLOT
     int32_t *const arena = ctx->get<int32_t>("arena", P + E);
     uint32_t *const key_idx = ctx->get<uint32_t>("key_idx", P);
     uint32_t *const dep_txn = ctx->get<uint32_t>("dep_txn", std::max<uint64_t>(E, 1));
@@ -3576,15 +3614,16 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ctx->launch_stream = nullptr;
     }
     {
-        // ---- stream pass: every txn's arena / key offsets; stream txns' KeyDeps (TxnIds to scratch); 256-thread
-        // workgroups co-schedule best with the 512-thread block tier (A/B)
+        // ---- stream pass: the stream txns' KeyDeps (a grid over every txn, 16 lanes per txn), TxnIds to scratch;
+        // 256-thread workgroups co-schedule best with the 512-thread block tier
         constexpr int st_nt = 256;
         const uint32_t tt = (uint32_t)st_nt / ST_G;
         const uint32_t nblocks = (n + tt - 1) / tt;
         const uint32_t ntiles = nblocks * (uint32_t)(st_nt / 64);   // waves (phase-profile rows)
         V3Stream sp;
         sp.v = vv; sp.err = gstat + 5;
-        sp.key_off = key_off; sp.bigflag = bigflag; sp.txn_of_rank = txn_of_rank; sp.rec = rec; sp.irec = ro.irec;
+        sp.key_off = key_off; sp.bigflag = bigflag; sp.list = nullptr; sp.txn_of_rank = txn_of_rank;
+        sp.rec = rec; sp.irec = ro.irec;
         sp.arena_off = arena_off; sp.kd_off = kd_off; sp.u_cnt_out = u_cnt; sp.arena = arena; sp.key_idx = key_idx;
         sp.dep_scr = dep_st; sp.n = n; sp.ntiles = ntiles;
 #ifdef ACC_PHASE_PROF
@@ -3593,8 +3632,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ACC_HIP(hipMemsetAsync(prof_buf, 0, 8 * prof_rows * sizeof(unsigned long long), st));
         ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_st_prof), &prof_buf, sizeof prof_buf, 0, hipMemcpyHostToDevice, st));
 #endif
-        if (rbits <= 28) launch(ctx, "v3_stream", k_v3_stream<uint32_t, st_nt>, dim3(nblocks), dim3(st_nt), 0, sp);
-        else launch(ctx, "v3_stream", k_v3_stream<uint64_t, st_nt>, dim3(nblocks), dim3(st_nt), 0, sp);
+        if (rbits <= 28) launch(ctx, "v3_stream", k_v3_stream<uint32_t, st_nt, ST_G, ST_N2, false>, dim3(nblocks), dim3(st_nt), 0, sp);
+        else launch(ctx, "v3_stream", k_v3_stream<uint64_t, st_nt, ST_G, ST_N2, false>, dim3(nblocks), dim3(st_nt), 0, sp);
 #ifdef ACC_PHASE_PROF
         {
             std::vector<unsigned long long> h(8 * prof_rows);

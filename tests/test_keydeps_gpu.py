@@ -112,6 +112,20 @@ def test_zipf_hot_keys(ctx):
     assert_same(g, o, b.n_txn, "zipf")
 
 
+@pytest.mark.parametrize("n,k,nkeys,window", [(4000, 16, 3000, 2000), (6000, 16, 4000, 3000)])
+def test_inline_txns_beyond_stream_cap(ctx, n, k, nkeys, window):
+    """16-key txns whose every pair keeps its entries inline (<= 15 each) yet sum past the stream pass's 128-entry
+    buffer (E up to ~265; 161 / 192 such txns here): the mark pass routes them to the block tiers, every txn equals the
+    oracle."""
+    import oracle
+    b = W.keydeps_batch(n, k, nkeys, 0x5EED, "uniform", status_model="model", window=window)
+    g = ctx.calculate_partial_deps(b)
+    o = oracle.keydeps_batch(b)
+    E = np.diff(o.arena_off.astype(np.int64)) - np.diff(o.kd_off.astype(np.int64))
+    assert E.max() > 200
+    assert_same(g, o, b.n_txn, f"{k}-key inline txns past the stream cap")
+
+
 def test_mixed_kinds_and_accept_style(ctx):
     """SyncPoint kinds, random executeAt bumps on uncommitted txns (Accept-style queries with p1)."""
     import oracle
