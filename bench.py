@@ -369,7 +369,115 @@ def run_config2(args, world, rank, local, dev):
         # the same stream shape over zipf(0.99) keys (the hottest key ~835K pairs): the hot keys take acc_cfk_apply's
         # closed form (csrc/cfkdeps.hip, hot keys)
         result["cfk_apply_zipf"] = cfk_apply_leg(local, calls=2, dist="zipf")
+        # a replica in steady state: 100K-txn PreAccept batches against a resident 1M-txn store
+        result["cfk_steady"] = cfk_steady_leg(local)
+        result["cfk_steady_zipf"] = cfk_steady_leg(local, dist="zipf")
     return ctx, timing, elapsed, result
+
+
+def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_batches=5):
+    """N4 in steady state (messages/PreAccept.java:107-138, local/CommandStore.java:280-345,
+    local/CommandsForKey.java:652-706): a device store built from the first n_init txns of workload.cfk_update_stream
+    (8 keys per txn over 1M keys), then n_batches batches of `batch` new txns (plus the final statuses that fall due,
+    workload.cfk_stream_cuts). Each batch: MaxConflicts proposes every new txn's executeAt (acc_maxconflicts_get), the
+    batch's executeAts merge into it (acc_maxconflicts_update), CommandsForKey.update with deps on the resident store
+    (acc_cfk_apply_deps: key-major update + the txn-major view / missing[] indices), and the KeyDeps scan of the whole
+    store in place (acc_cfk_view -> acc_keydeps_batch). Inputs resident in HBM. Pass 1 times each phase (wall clock,
+    synchronised); pass 2 replays it on a fresh store with every kernel timed for the breakdown."""
+    import torch
+    from accord_amd import _lib as L
+    from accord_amd import workload as W
+    from accord_amd.deps import Context
+    t0 = time.perf_counter()
+    u = W.cfk_update_stream(n_init + batch * n_batches, 8, 1_000_000, dist=dist)
+    cuts = W.cfk_stream_cuts(u, n_init, batch, n_batches)
+    parts = [W.cfk_slice(u, 0, cuts[0])] + [W.cfk_slice(u, cuts[b], cuts[b + 1]) for b in range(n_batches)]
+    qs = [W.preaccept_queries(p) for p in parts]
+    t_gen = time.perf_counter() - t0
+    dev = torch.device("cuda", local)
+    keep = []
+
+    def up(a):
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        keep.append(t)
+        return t.data_ptr()
+
+    ins = []
+    for p, q in zip(parts, qs):
+        P = {k: up(v) for k, v in p.items()}
+        U = len(p["msb"])
+        ui = L.CfkUpdates(L.ACC_MEM_DEVICE, U, len(p["key"]), len(p["dmsb"]), L.TsCols(P["msb"], P["lsb"], P["node"]),
+                          L.TsCols(P["xmsb"], P["xlsb"], P["xnode"]), P["status"], P["flags"], P["key_off"], P["key"],
+                          P["dep_off"], L.TsCols(P["dmsb"], P["dlsb"], P["dnode"]))
+        z = up(np.zeros(U + 1, np.uint32))
+        ci = L.ConflictsIn(L.ACC_MEM_DEVICE, U, 1, len(p["key"]), 0, L.TsCols(P["xmsb"], P["xlsb"], P["xnode"]),
+                           P["key_off"], P["key"], z, z, z)
+        Q = {k: up(v) for k, v in q.items()}
+        nq = len(q["msb"])
+        qi = L.PreacceptIn(L.ACC_MEM_DEVICE, nq, len(q["part_start"]), L.TsCols(Q["msb"], Q["lsb"], Q["node"]),
+                           Q["is_range"], Q["part_off"], Q["part_start"], Q["part_end"])
+        qo = L.PreacceptOut(L.ACC_MEM_DEVICE, up(np.zeros(nq, np.uint64)), up(np.zeros(nq, np.uint64)),
+                            up(np.zeros(nq, np.int32)), up(np.zeros(nq, np.uint8)))
+        ins.append((ui, ci, qi, qo))
+    torch.cuda.synchronize()
+
+    def run(timing):
+        rows, tm = [], {}
+        with Context(local, timing=timing) as c:
+            lib = c._lib
+            h, m = C.c_void_p(), C.c_void_p()
+            c.check(lib.acc_cfk_create(c.handle, C.byref(h)))
+            c.check(lib.acc_maxconflicts_create(c.handle, 1, C.byref(m)))
+            try:
+                ui, ci, _, _ = ins[0]
+                c.check(lib.acc_maxconflicts_update(c.handle, m, C.byref(ci)))
+                c.check(lib.acc_cfk_apply_deps(c.handle, h, C.byref(ui)))
+                v, kv = L.BatchIn(), L.KeydepsView()
+                c.check(lib.acc_cfk_view(c.handle, h, C.byref(v)))
+                c.check(lib.acc_keydeps_batch(c.handle, C.byref(v), C.byref(kv)))   # warm the scan's buffers
+                torch.cuda.synchronize()
+                c.timing_reset()
+                for ui, ci, qi, qo in ins[1:]:
+                    t = [time.perf_counter()]
+                    c.check(lib.acc_maxconflicts_get(c.handle, m, C.byref(qi), C.byref(qo)))
+                    torch.cuda.synchronize(); t.append(time.perf_counter())
+                    c.check(lib.acc_maxconflicts_update(c.handle, m, C.byref(ci)))
+                    torch.cuda.synchronize(); t.append(time.perf_counter())
+                    c.check(lib.acc_cfk_apply_deps(c.handle, h, C.byref(ui)))
+                    torch.cuda.synchronize(); t.append(time.perf_counter())
+                    st = c.stats()
+                    c.check(lib.acc_cfk_view(c.handle, h, C.byref(v)))
+                    c.check(lib.acc_keydeps_batch(c.handle, C.byref(v), C.byref(kv)))
+                    torch.cuda.synchronize(); t.append(time.perf_counter())
+                    d = [(t[i + 1] - t[i]) * 1e3 for i in range(4)]
+                    rows.append(dict(propose_ms=d[0], maxconflicts_update_ms=d[1], cfk_update_ms=d[2],
+                                     cfk_apply_ms=st.get("cfk.apply_us", 0) / 1e3, view_ms=st.get("cfk.view_us", 0) / 1e3,
+                                     keydeps_scan_ms=d[3], total_ms=sum(d), store_txns=int(v.n_txn),
+                                     store_pairs=int(v.n_pairs), dep_edges=int(kv.total_edges)))
+                if timing:
+                    tm = c.timing()
+            finally:
+                lib.acc_maxconflicts_destroy(m)
+                lib.acc_cfk_destroy(h)
+        return rows, tm
+
+    rows, _ = run(False)
+    _, tm = run(True)
+    nb = len(rows)
+    mean = {k: round(sum(r[k] for r in rows) / nb, 3) for k in rows[0] if k.endswith("_ms")}
+    top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:10]
+    return {"workload": f"workload.cfk_update_stream({(n_init + batch * n_batches) // 1000}K txns x 8 {dist} keys over "
+                        f"1M keys): a {n_init // 1000}K-txn device store, then {n_batches} PreAccept batches of "
+                        f"{batch // 1000}K new txns (MaxConflicts propose + merge, CommandsForKey.update with deps, "
+                        "KeyDeps scan of the whole store in place)",
+            "ms_per_batch": mean["total_ms"], **{k: v for k, v in mean.items() if k != "total_ms"},
+            "batch_updates": [int(cuts[b + 1] - cuts[b]) for b in range(n_batches)],
+            "final_store_txns": rows[-1]["store_txns"], "final_store_pairs": rows[-1]["store_pairs"],
+            "final_dep_edges": rows[-1]["dep_edges"],
+            "per_batch_total_ms": [round(r["total_ms"], 3) for r in rows],
+            "per_batch_view_ms": [round(r["view_ms"], 3) for r in rows],
+            "setup_gen_s": round(t_gen, 2),
+            "top_kernels_ms_per_batch": {k: round(x[0] / nb, 3) for k, x in top}}
 
 
 def cfk_apply_leg(local, calls=3, dist="uniform"):

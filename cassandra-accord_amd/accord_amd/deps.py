@@ -1064,3 +1064,36 @@ class CfkStore:
         bv = L.CfkBatchView()
         self.ctx.check(self.ctx._lib.acc_cfk_missing(self.ctx.handle, self._h, C.byref(bv)))
         return bv
+
+
+class ReplicaStore:
+    """A replica CommandStore's PreAccept path on device-resident state (SURVEY.md §8(f) N4 in steady state): per batch
+    of commands, the store's MaxConflicts proposes each new txn's executeAt (CommandStore.preaccept,
+    local/CommandStore.java:320-345), the batch's executeAts merge into it (updateMaxConflicts, :280-290), every key's
+    CommandsForKey takes the updates with deps (CommandsForKey.update, local/CommandsForKey.java:652-706, through
+    acc_cfk_apply_deps: the key-major state and the txn-major view with missing[] indices stay in HBM), and the KeyDeps
+    scan reads the updated store in place (PreAccept.calculatePartialDeps, messages/PreAccept.java:107-138). A batch's
+    commands are concurrent: its proposals see MaxConflicts as of the previous batch."""
+
+    def __init__(self, ctx: Context, end_inclusive: int = 1):
+        self.ctx = ctx
+        self.end_inclusive = int(end_inclusive)
+        self.cfk = CfkStore(ctx)
+        self.mc = MaxConflictsMap(ctx, end_inclusive)
+
+    def preaccept_batch(self, part: dict, queries: dict | None = None, scan: bool = True) -> dict:
+        """part: the batch's updates (cfk_update_stream layout); queries: its PreAccept queries (default: one per
+        command first seen in part). Returns dict(propose = MaxConflicts.get + fast path per query, keydeps = the
+        KeyDeps of every txn of the store after the batch, when scan)."""
+        from . import workload as W
+        q = W.preaccept_queries(part) if queries is None else queries
+        out = dict(propose=self.mc.get(q))
+        self.mc.update(W.conflicts_updates(part, self.end_inclusive))
+        self.cfk.apply_deps(part)
+        if scan:
+            out["keydeps"] = self.cfk.calculate_partial_deps()
+        return out
+
+    def close(self):
+        self.cfk.close()
+        self.mc.close()

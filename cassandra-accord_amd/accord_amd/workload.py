@@ -484,7 +484,7 @@ def config4(scale: float = 1.0, **kw) -> RangeBatch:
 
 
 def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = None, seed: int = CONFIG_SEEDS["2"] + 7,
-                      max_deps: int = 16, lag: int = 64, dist: str = "uniform") -> dict:
+                      max_deps: int = 16, lag: int = 64, dist: str = "uniform", window: int = 10_000) -> dict:
     """A CommandsForKey update stream of config-2 size (acc_cfk_apply's CFK_UPD layout), for the N4 bench leg: the txns
     of keydeps_batch(n_txn, keys_per_txn, n_keys, uniform keys, status model) as SafeCommandStore.updateCommandsForKey
     sees them (local/SafeCommandStore.java:217-240): an Accept (ACCEPTED, executeAt = TxnId) at time i, then the final
@@ -493,9 +493,10 @@ def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = No
     a key (its keyDeps.txnIds(key)) are the latest max_deps txns below it on that key, every one already known to the
     key's CFK. Uniform keys: a zipf hot key's CFK grows with its whole history (CommandsForKey.update copies the key's
     arrays, linear per update), which the reference bounds by pruning, outside the §8 path. dist="zipf": zipf(0.99) keys
-    as config 2 (a hot key's updates take acc_cfk_apply's hot-key closed form)."""
+    as config 2 (a hot key's updates take acc_cfk_apply's hot-key closed form). window: the status model's
+    uncommitted tail (the last `window` txns never reach a final status)."""
     n_keys = n_keys or n_txn
-    b = keydeps_batch(n_txn, keys_per_txn, n_keys, seed, dist, status_model="model")
+    b = keydeps_batch(n_txn, keys_per_txn, n_keys, seed, dist, status_model="model", window=window)
     st = b.status.astype(np.int64)
     K = keys_per_txn
     # deps per (txn, key) pair: the latest max_deps txns below it on the key (pairs sorted by (key, txn))
@@ -539,4 +540,52 @@ def cfk_update_stream(n_txn: int, keys_per_txn: int = 8, n_keys: int | None = No
     return dict(msb=b.txn_msb[ev_txn], lsb=b.txn_lsb[ev_txn], node=b.txn_node[ev_txn], xmsb=xmsb, xlsb=xlsb, xnode=xnode,
                 status=ust, flags=np.ones(U, np.uint8), key_off=(np.arange(U + 1, dtype=np.int64) * K).astype(np.uint32),
                 key=b.key_code[up_pair], dep_off=dep_off.astype(np.uint32), dmsb=b.txn_msb[dtx], dlsb=b.txn_lsb[dtx],
-                dnode=b.txn_node[dtx])
+                dnode=b.txn_node[dtx], time=ev_time[o])
+
+
+UPD_FIELDS = ("msb", "lsb", "node", "xmsb", "xlsb", "xnode", "status", "flags")
+
+
+def cfk_slice(u: dict, a: int, b: int) -> dict:
+    """Updates [a, b) of a CFK_UPD update list (cfk_update_stream layout), offsets rebased."""
+    ko, do = u["key_off"].astype(np.int64), u["dep_off"].astype(np.int64)
+    out = {k: u[k][a:b] for k in UPD_FIELDS}
+    out["key_off"] = (ko[a:b + 1] - ko[a]).astype(np.uint32)
+    out["key"] = u["key"][ko[a]:ko[b]]
+    out["dep_off"] = (do[ko[a]:ko[b] + 1] - do[ko[a]]).astype(np.uint32)
+    for f in ("dmsb", "dlsb", "dnode"):
+        out[f] = u[f][do[ko[a]]:do[ko[b]]]
+    return out
+
+
+def cfk_stream_cuts(u: dict, n_initial: int, batch_txns: int, n_batches: int) -> list:
+    """Update-index cuts of a cfk_update_stream for a replica's steady state: [0, cuts[0]) builds the initial store
+    (the first n_initial txns' PreAccept / Accept and every final status due by then), then batch b = [cuts[b],
+    cuts[b + 1]) brings batch_txns new txns and the final statuses of older ones (time order: txn i's first update at
+    2i, its final status at 2(i + lag) + 1)."""
+    t = u["time"]
+    return [int(np.searchsorted(t, 2 * (n_initial + b * batch_txns))) for b in range(n_batches + 1)]
+
+
+def preaccept_queries(part: dict) -> dict:
+    """The PreAccept queries of an update slice (acc_preaccept_in host layout: TxnId + its keys): one per command
+    first seen in it (a cfk_update_stream txn's first update is its only PreAccept / Accept)."""
+    sel = np.nonzero((part["status"] == PREACCEPTED) | (part["status"] == ACCEPTED))[0]
+    ko = part["key_off"].astype(np.int64)
+    cnt = ko[sel + 1] - ko[sel]
+    off = np.zeros(len(sel) + 1, np.int64)
+    np.cumsum(cnt, out=off[1:])
+    src = np.repeat(ko[sel], cnt) + (np.arange(int(off[-1])) - np.repeat(off[:-1], cnt))
+    keys = part["key"][src]
+    return dict(msb=part["msb"][sel], lsb=part["lsb"][sel], node=part["node"][sel],
+                is_range=np.zeros(len(sel), np.uint8), part_off=off.astype(np.uint32), part_start=keys,
+                part_end=np.zeros(len(keys), np.uint64))
+
+
+def conflicts_updates(part: dict, end_inclusive: int = 1) -> dict:
+    """An update slice as MaxConflicts updates (CommandStore.updateMaxConflicts: each command's keys with its
+    executeAt; acc_conflicts_in host layout)."""
+    U = len(part["msb"])
+    return dict(end_inclusive=end_inclusive, xmsb=part["xmsb"], xlsb=part["xlsb"], xnode=part["xnode"],
+                key_off=part["key_off"], key=part["key"], rng_off=np.zeros(U + 1, np.uint32),
+                rng_start=np.zeros(0, np.uint64), rng_end=np.zeros(0, np.uint64))

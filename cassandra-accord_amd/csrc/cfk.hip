@@ -428,11 +428,20 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     }
     const acc_cfk_snap prev = km_snap(cfk);
     acc_cfk_snap_view v{};
+    // stream time of the two halves (stats cfk.apply_us / cfk.view_us: the steady-state bench's view step)
+    hipEvent_t ev[3] = { ctx->take_event(), ctx->take_event(), ctx->take_event() };
+    struct Give {
+        acc_ctx *c; hipEvent_t *e;
+        ~Give() { for (int i = 0; i < 3; ++i) c->event_pool.push_back(e[i]); }
+    } give{ ctx, ev };
+    ACC_HIP(hipEventRecord(ev[0], ctx->stream));
     cfk_apply(ctx, &prev, up, &v);
+    ACC_HIP(hipEventRecord(ev[1], ctx->stream));
     const acc_cfk_snap next{ ACC_MEM_DEVICE, v.n_keys, v.n_entries, v.n_missing, v.key, v.ent_off, v.txn_id, v.execute_at,
                              v.status, v.miss_off, v.missing };
     acc_cfk_batch_view bv{};
     cfk_snap_to_batch(ctx, &next, &bv, true);
+    ACC_HIP(hipEventRecord(ev[2], ctx->stream));
     // ---- both results become the store's arrays: the context's result buffers and the store's previous arrays trade
     // places (no copies; the context writes its next results into the old arrays)
     auto adopt = [&](const char *name, auto *&p, size_t &bytes) {
@@ -469,6 +478,11 @@ void cfk_apply_deps(acc_ctx *ctx, acc_cfk *cfk, const acc_cfk_updates *up)
     adopt("cb_mt", cfk->bmiss_txn, cfk->bytes_bmt);
     cfk->bnm = bv.n_missing;
     ctx->sync();
+    float ms_a = 0, ms_v = 0;
+    ACC_HIP(hipEventElapsedTime(&ms_a, ev[0], ev[1]));
+    ACC_HIP(hipEventElapsedTime(&ms_v, ev[1], ev[2]));
+    ctx->stat("cfk.apply_us", (uint64_t)(ms_a * 1000.0f));
+    ctx->stat("cfk.view_us", (uint64_t)(ms_v * 1000.0f));
     cfk->n = n;
     cfk->P = P;
     cfk->deps = true;

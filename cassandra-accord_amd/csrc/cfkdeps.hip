@@ -683,7 +683,9 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bsum(uint64_t T, const uint32_t *_
         if (d) atomicMax(&b.d[k], d);
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart, BSum b,
+__global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint32_t *__restrict__ kstart,
+                                                     const uint32_t *__restrict__ src, uint32_t nk,
+                                                     const uint32_t *__restrict__ snap_ent_off, BSum b,
                                                      uint64_t *__restrict__ ecap,
                                                      uint64_t *__restrict__ mcap, uint64_t *__restrict__ mmax,
                                                      uint64_t *__restrict__ dcap, uint32_t *__restrict__ ovf,
@@ -692,9 +694,15 @@ __global__ __launch_bounds__(BLOCK) void k_cd_bounds(uint32_t nkeys, const uint3
 {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys) return;
-    // a key with more than hot_thr elements takes the hot-key path (no lane working space); keep_hot: flags as left by
-    // the hot-key path (its irregular keys cleared)
-    if (!keep_hot) hot[k] = kstart[k + 1] - kstart[k] > hot_thr ? 1 : 0;
+    // a key with more than hot_thr items (snapshot entries + update pairs) takes the hot-key path (no lane working
+    // space: a lane would copy a large snapshot alone); keep_hot: flags as left by the hot-key path (its irregular keys
+    // cleared)
+    if (!keep_hot) {
+        const uint32_t q0 = kstart[k], v = src[q0];
+        const uint64_t items = (uint64_t)(kstart[k + 1] - q0) - (v < nk ? 1u : 0u) +
+                               (v < nk ? snap_ent_off[v + 1] - snap_ent_off[v] : 0u);
+        hot[k] = items > hot_thr ? 1 : 0;
+    }
     if (hot[k]) {
         ecap[k] = 0; mcap[k] = 0; mmax[k] = 0; dcap[k] = 1; ovf[k] = 0;
         atomicAdd(nhot, 1u);
@@ -1721,9 +1729,9 @@ __global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, const uint32_t *_
     if (s.st[e] != c.st || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ c.xm, c.xl, c.xn }) != 0)
         atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
 }
-// each pair's missing[] TxnIds as batch indices (binary search over the batch's TxnIds), each result checked against the
-// one before it (sorted unique). A pair with a short missing[] is its lane's; the long ones (a hot key's entries carry
-// thousands) are taken by the whole wave one after another, its lanes splitting the searches
+// each pair's missing[] TxnIds as batch indices, each result checked against the one before it (sorted unique). A pair
+// with a short missing[] is its lane's; the long ones (a hot key's entries carry thousands) are taken by the whole wave
+// one after another, its lanes splitting the searches. cb_find: the binary search over the batch's TxnIds.
 constexpr uint32_t CB_LONG = 32;
 __device__ __forceinline__ uint32_t cb_find(const BatchOut &b, uint32_t n, const Ts &k, uint64_t &bad)
 {
@@ -1738,24 +1746,60 @@ __device__ __forceinline__ uint32_t cb_find(const BatchOut &b, uint32_t n, const
     }
     return lo;
 }
-__global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *__restrict__ perm, Snap s,
-                                                   const uint64_t *__restrict__ ntxn, BatchOut b,
-                                                   const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
-                                                   uint64_t *__restrict__ err)
+// Per entry in key-major order (its missing[] read contiguously): each missing TxnId's batch index from an
+// open-addressing hash table of the batch's TxnIds (built once per call: one probe of a 32-B slot per lookup, where a
+// binary search over the batch's TxnIds costs ~20 dependent loads of 20 B). Long lists (a hot key's entries carry
+// thousands) are taken by the whole wave, its lanes splitting the list.
+struct TxnHash {
+    ulonglong4 *slot;   // (msb, lsb & IDENTITY_LSB, node << 32 | index, used)
+    uint32_t mask;
+};
+constexpr uint64_t TH_EMPTY = 0;
+__device__ __forceinline__ uint32_t th_hash(uint64_t m, uint64_t l, int32_t n)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t lane = lane_id(), n = (uint32_t)*ntxn;
+    uint64_t x = m * 0x9E3779B97F4A7C15ull ^ (l & IDENTITY_LSB) ^ ((uint64_t)(uint32_t)n << 40);
+    x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29; x *= 0x94D049BB133111EBull; x ^= x >> 32;
+    return (uint32_t)x;
+}
+__global__ __launch_bounds__(BLOCK) void k_cb_hash_build(const uint64_t *__restrict__ ntxn, BatchOut b,
+                                                         TxnHash h)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= *ntxn) return;
+    const uint64_t m = b.tm[t], l = b.tl[t] & IDENTITY_LSB;
+    const int32_t n = b.tn[t];
+    for (uint32_t i = th_hash(m, l, n) & h.mask;; i = (i + 1) & h.mask)
+        if (atomicCAS((unsigned long long *)&h.slot[i].w, (unsigned long long)TH_EMPTY, 1ull) == TH_EMPTY) {
+            h.slot[i].x = m; h.slot[i].y = l; h.slot[i].z = ((uint64_t)(uint32_t)n << 32) | (uint32_t)t;
+            return;
+        }
+}
+__device__ __forceinline__ uint32_t th_find(const TxnHash &h, const Ts &k, uint64_t &bad)
+{
+    const uint64_t l = k.l & IDENTITY_LSB;
+    for (uint32_t i = th_hash(k.m, l, k.n) & h.mask;; i = (i + 1) & h.mask) {
+        const ulonglong4 e = h.slot[i];
+        if (e.w == TH_EMPTY) { bad |= E_STATE; return 0; }   // a TxnId that is no entry of the batch
+        if (e.x == k.m && e.y == l && (int32_t)(e.z >> 32) == k.n) return (uint32_t)e.z;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_cb_miss_hash(uint64_t NE, const uint32_t *__restrict__ qpos, Snap s, TxnHash h,
+                                                        const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
+                                                        uint64_t *__restrict__ err)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t lane = lane_id();
     uint64_t bad = 0;
     uint32_t m0 = 0, m1 = 0, w0 = 0;
-    if (i < NE) {
-        const uint32_t e = perm[i];
-        m0 = s.miss_off[e]; m1 = s.miss_off[e + 1]; w0 = mo[i];
+    if (e < NE) {
+        m0 = s.miss_off[e]; m1 = s.miss_off[e + 1];
+        if (m1 > m0) w0 = mo[qpos[e]];
     }
     const bool lng = m1 - m0 >= CB_LONG;
     if (!lng) {
         uint32_t prev = 0;
         for (uint32_t j = m0; j < m1; ++j) {
-            const uint32_t lo = cb_find(b, n, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad);
+            const uint32_t lo = th_find(h, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad);
             if (j > m0 && lo <= prev) bad |= E_ARG_SORT;
             mt[w0 + (j - m0)] = lo;
             prev = lo;
@@ -1768,7 +1812,7 @@ __global__ __launch_bounds__(BLOCK) void k_cb_miss(uint64_t NE, const uint32_t *
         for (uint32_t base = a; base < z; base += 64) {
             const uint32_t j = base + lane;
             const bool valid = j < z;
-            const uint32_t lo = valid ? cb_find(b, n, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad) : 0u;
+            const uint32_t lo = valid ? th_find(h, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad) : 0u;
             uint32_t prev = __shfl_up(lo, 1, 64);
             if (lane == 0) prev = carry;
             if (valid && j > a && lo <= prev) bad |= E_ARG_SORT;
@@ -1857,8 +1901,19 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
         launch(ctx, "cb_owner", k_cb_owner, g, dim3(BLOCK), 0, NE, nk, s.ent_off, owner);
         launch(ctx, "cb_ent", k_cb_ent, g, dim3(BLOCK), 0, NE, (const uint32_t *)owner, (const uint32_t *)dr.rank, (const uint32_t *)qpos, s, (const TxnChk *)chk, b, errs);
         scan<uint32_t, OpAdd<uint32_t>>(ctx, b.mcnt, mo, NE, true, mo + NE);
-        if (NM)
-            launch(ctx, "cb_miss", k_cb_miss, g, dim3(BLOCK), 0, NE, perm, s, (const uint64_t *)dr.count_dev, b, (const uint32_t *)mo, mt, errs);
+        if (NM) {
+            // the batch's TxnIds in a hash table of >= 2x their count (one read-back of the count)
+            ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, dr.count_dev, 8, hipMemcpyDeviceToHost, st));
+            ctx->sync();
+            const uint64_t nt = ctx->pinned[1] & 0xFFFFFFFFu;
+            uint32_t cap = 1024;
+            while (cap < 2 * nt && cap < (1u << 31)) cap <<= 1;
+            TxnHash th{ ctx->get<ulonglong4>("cb_hash", cap), cap - 1 };
+            ACC_HIP(hipMemsetAsync(th.slot, 0, (size_t)cap * sizeof(ulonglong4), st));
+            launch(ctx, "cb_hash", k_cb_hash_build, dim3(grid_for(nt, BLOCK)), dim3(BLOCK), 0, (const uint64_t *)dr.count_dev, b, th);
+            launch(ctx, "cb_miss", k_cb_miss_hash, g, dim3(BLOCK), 0, NE, (const uint32_t *)qpos, s, th, (const uint32_t *)mo,
+                   mt, errs);
+        }
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, dr.count_dev, 8, hipMemcpyDeviceToHost, st));
         ctx->sync();
@@ -2016,7 +2071,8 @@ void cfk_apply(acc_ctx *ctx, const acc_cfk_snap *in, const acc_cfk_updates *up, 
     ctx->stat("cfk.hot_irregular", 0);
     for (int keep_hot = 0; nkeys; keep_hot = 1) {
         ACC_HIP(hipMemsetAsync(nhot, 0, 4, st));
-        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart, bs,
+        launch(ctx, "cd_bounds", k_cd_bounds, dim3(grid_for(nkeys, BLOCK)), dim3(BLOCK), 0, nkeys, (const uint32_t *)kstart,
+               (const uint32_t *)so.vals, nk, s.ent_off, bs,
                ecap, mcap, mmax, dcap, ovf, hot_thr, keep_hot, hot,
                nhot);
         // keys by entry capacity (bits up to the largest), so interleaved waves hold keys of similar size

@@ -17,6 +17,11 @@
 namespace acc {
 void shard_pack(acc_ctx *ctx, const acc_batch_in *in, acc_frag_streams *out, bool ctx_alloc);
 void shard_merge(acc_ctx *ctx, const acc_frag_recv *in, acc_merge_view *view);
+uint8_t *frag_encode(acc_ctx *ctx, uint32_t W, const uint64_t *fo, const uint64_t *ko_h, const uint64_t *vo_h,
+                     const uint64_t *oo_h, const uint32_t *hdr, const uint64_t *keys, const uint32_t *vals,
+                     const int32_t *k2v, uint32_t G, std::vector<uint64_t> &boff);
+void frag_decode(acc_ctx *ctx, uint32_t W, uint32_t rank, uint32_t n_global, const uint8_t *recv,
+                 const std::vector<uint64_t> &nb, acc_frag_recv &fr, std::vector<uint64_t> cnt[4]);
 void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in, const uint32_t *txn_global,
                          uint32_t n_global, const acc_rlist *covering, acc_merge_view *key_view,
                          acc_deps_merge_view *range_view, acc_covering_view *covering_view);
@@ -213,26 +218,30 @@ static void exchange_streams(acc_comm *c, Streams &S)
     ctx->sync();
 }
 
-// the KeyDeps fragments of the last KeyDeps result on ctx, packed into the four streams of S (slots 0..3)
-static void add_key_streams(acc_ctx *ctx, const acc_batch_in *in, const uint32_t *txn_global, uint32_t W, Streams &S)
+// the KeyDeps fragments of the last KeyDeps result on ctx (acc_shard_pack's four streams, on the device) in their
+// compact wire form (fragwire.hip): one byte stream, slot 0 of S
+static void add_key_streams(acc_ctx *ctx, const acc_batch_in *in, const uint32_t *txn_global, uint32_t W, uint32_t n_global,
+                            Streams &S)
 {
-    for (int q = 0; q < 4; ++q) S.off[q].assign(W + 1, 0);
+    std::vector<uint64_t> fo(W + 1), ko(W + 1), vo(W + 1), oo(W + 1);
     acc_frag_streams fs{};
     fs.world = W;
     fs.mem = ACC_MEM_DEVICE;
-    fs.frag_off = S.off[0].data(); fs.key_off = S.off[1].data(); fs.val_off = S.off[2].data(); fs.k2v_off = S.off[3].data();
+    fs.frag_off = fo.data(); fs.key_off = ko.data(); fs.val_off = vo.data(); fs.k2v_off = oo.data();
     fs.txn_global = txn_global;
     shard_pack(ctx, in, &fs, true);
-    S.send[0] = fs.hdr; S.send[1] = fs.keys; S.send[2] = fs.vals; S.send[3] = fs.k2v;
-    S.esz[0] = 16; S.esz[1] = 8; S.esz[2] = 4; S.esz[3] = 4;   // header (4 x u32), key code, TxnId index, int
-    S.ns = 4;
+    const uint32_t G = (std::max(n_global, 1u) + W - 1) / W;
+    S.off[0].clear();
+    S.send[0] = frag_encode(ctx, W, fo.data(), ko.data(), vo.data(), oo.data(), fs.hdr, fs.keys, fs.vals, fs.k2v, G, S.off[0]);
+    S.esz[0] = 1;
+    S.ns = 1;
 }
 
 static void merge_key_streams(acc_ctx *ctx, acc_comm *c, uint32_t n_global, const Streams &S, acc_merge_view *view)
 {
-    acc_frag_recv fr{ ACC_MEM_DEVICE, c->world, c->rank, n_global, S.n_src[0].data(), S.n_src[1].data(), S.n_src[2].data(),
-                      S.n_src[3].data(), static_cast<const uint32_t *>(S.recv[0]), static_cast<const uint64_t *>(S.recv[1]),
-                      static_cast<const uint32_t *>(S.recv[2]), static_cast<const int32_t *>(S.recv[3]) };
+    acc_frag_recv fr{};
+    std::vector<uint64_t> cnt[4];
+    frag_decode(ctx, c->world, c->rank, n_global, static_cast<const uint8_t *>(S.recv[0]), S.n_src[0], fr, cnt);
     shard_merge(ctx, &fr, view);
 }
 
@@ -241,8 +250,9 @@ void shard_reduce(acc_ctx *ctx, acc_comm *c, const acc_batch_in *in, const uint3
 {
     if (!c || !in || !view) fail(ACC_E_ARG, "null argument");
     if (c->ctx != ctx) fail(ACC_E_ARG, "communicator belongs to another context");
+    if (!txn_global && n_global < in->n_txn) fail(ACC_E_ARG, "n_global must be >= n_txn when txn_global is null");
     Streams S;
-    add_key_streams(ctx, in, txn_global, c->world, S);
+    add_key_streams(ctx, in, txn_global, c->world, n_global, S);
     exchange_streams(c, S);
     // KeyDeps.with fold of every home txn (stream order makes the merge wait for the receives)
     merge_key_streams(ctx, c, n_global, S, view);
@@ -272,13 +282,13 @@ void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in
     if (!txn_global && n_global < in->n_txn) fail(ACC_E_ARG, "n_global must be >= n_txn when txn_global is null");
     const acc_batch_in kin{ in->n_txn, in->mem, in->n_pairs, in->txn_id, in->execute_at, in->status, in->key_off, in->key_code };
     Streams S;
-    add_key_streams(ctx, &kin, txn_global, c->world, S);
+    add_key_streams(ctx, &kin, txn_global, c->world, n_global, S);
     void *rs[4];
     std::vector<uint64_t> ro[4];
     range_pack(ctx, in, txn_global, c->world, n_global, rs, ro);
     const uint64_t resz[4] = { 16, 16, 24, 4 };   // header (4 x u32), Range (start, end), raw TxnId (msb, lsb, node), int
-    for (int q = 0; q < 4; ++q) { S.send[4 + q] = rs[q]; S.off[4 + q] = ro[q]; S.esz[4 + q] = resz[q]; }
-    S.ns = 8;
+    for (int q = 0; q < 4; ++q) { S.send[1 + q] = rs[q]; S.off[1 + q] = ro[q]; S.esz[1 + q] = resz[q]; }
+    S.ns = 5;
     if (covering) {   // the store's txns (u32 global indices) by home rank and its covering ((start, end) pairs)
         const uint32_t n = in->n_txn;
         const uint32_t *gidx = nullptr;
@@ -291,18 +301,18 @@ void partial_deps_reduce(acc_ctx *ctx, acc_comm *c, const acc_range_batch_in *in
         void *cs[2];
         std::vector<uint64_t> co[2];
         covering_pack(ctx, covering, gidx, n, c->world, cs, co);
-        S.send[8] = cs[0]; S.off[8] = co[0]; S.esz[8] = 4;
-        S.send[9] = cs[1]; S.off[9] = co[1]; S.esz[9] = 16;
-        S.ns = 10;
+        S.send[5] = cs[0]; S.off[5] = co[0]; S.esz[5] = 4;
+        S.send[6] = cs[1]; S.off[6] = co[1]; S.esz[6] = 16;
+        S.ns = 7;
     }
     exchange_streams(c, S);
     merge_key_streams(ctx, c, n_global, S, key_view);
     std::vector<uint64_t> rn[4];
     void *rr[4];
-    for (int q = 0; q < 4; ++q) { rn[q] = S.n_src[4 + q]; rr[q] = S.recv[4 + q]; }
+    for (int q = 0; q < 4; ++q) { rn[q] = S.n_src[1 + q]; rr[q] = S.recv[1 + q]; }
     range_merge(ctx, c->world, c->rank, n_global, rn, rr, range_view);
     if (covering)
-        covering_merge(ctx, c->world, c->rank, n_global, in->end_inclusive, S.n_src[8], S.recv[8], S.n_src[9], S.recv[9],
+        covering_merge(ctx, c->world, c->rank, n_global, in->end_inclusive, S.n_src[5], S.recv[5], S.n_src[6], S.recv[6],
                        key_view, range_view, covering_view);
 }
 

@@ -1270,7 +1270,10 @@ __device__ unsigned long long *g_ct_prof;
 #endif
 
 #ifndef ACC_R3U
-#define ACC_R3U 4   // R3 candidates loaded per round of the count pass's loops
+#define ACC_R3U 4   // R3 candidates loaded per round of the count pass's per-lane loops
+#endif
+#ifndef ACC_R3_COOP
+#define ACC_R3_COOP 8   // a wave walks the R3 candidates cooperatively when one of its lanes has more
 #endif
 __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, const uint32_t *__restrict__ owner,
                                                   const RecOut &ro, uint32_t *__restrict__ bigflag)
@@ -1308,46 +1311,94 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
             if (s >= pre[q2]) idx = a[q2] + (s - pre[q2]);   // empty runs are overridden by the next one
         xs[s] = (may_inline && s < L6) ? v.list_rank[idx] : 0u;
     }
-    for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {   // R3 candidates, ACC_R3U loads in flight
-        uint32_t ex[ACC_R3U], kd[ACC_R3U];
+    // R3 candidates [bstart, bend): one lane walks its own (ACC_R3U loads in flight), or, when some lane of the wave has
+    // more than ACC_R3_COOP (the lanes of a hot segment share nearly the same range), the wave loads the union of the
+    // ranges 64 candidates at a time (coalesced) and every lane tests each candidate broadcast from its lane
+    // (v_readlane): one memory round trip per 64 candidates instead of one per ACC_R3U
+    const uint32_t nc = q.bend > q.bstart ? q.bend - q.bstart : 0u;
+    uint32_t wmax = nc, clo = nc ? q.bstart : 0xFFFFFFFFu, chi = nc ? q.bend : 0u;
 #pragma unroll
-        for (uint32_t u = 0; u < ACC_R3U; ++u) {
-            ex[u] = i + u < q.bend ? v.bc_exec[i + u] : 0u;
-            kd[u] = i + u < q.bend ? (uint32_t)v.bc_kind[i + u] : 0u;
+    for (int d = 1; d < 64; d <<= 1) {
+        wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, d, 64));
+        clo = min(clo, (uint32_t)__shfl_xor((int)clo, d, 64));
+        chi = max(chi, (uint32_t)__shfl_xor((int)chi, d, 64));
+    }
+    const bool coop = wmax > (uint32_t)ACC_R3_COOP && chi - clo <= 64u * 64u;   // wave-uniform
+    if (coop) {
+        for (uint32_t c = clo; c < chi; c += 64) {
+            const uint32_t i = c + lane_id();
+            const uint32_t exl = i < chi ? v.bc_exec[i] : 0u, kdl = i < chi ? (uint32_t)v.bc_kind[i] : 0u;
+            const uint32_t cnt = min(64u, chi - c);
+            for (uint32_t u = 0; u < cnt; ++u) {
+                const uint32_t exu = (uint32_t)__builtin_amdgcn_readlane((int)exl, (int)u);
+                const uint32_t kdu = (uint32_t)__builtin_amdgcn_readlane((int)kdl, (int)u);
+                const uint32_t iu = c + u;
+                e += (iu >= q.bstart && iu < q.bend && exu >= q.m && ((q.wk >> kdu) & 1u)) ? 1u : 0u;
+            }
         }
+    } else {
+        for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {
+            uint32_t ex[ACC_R3U], kd[ACC_R3U];
 #pragma unroll
-        for (uint32_t u = 0; u < ACC_R3U; ++u) e += (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u)) ? 1u : 0u;
+            for (uint32_t u = 0; u < ACC_R3U; ++u) {
+                ex[u] = i + u < q.bend ? v.bc_exec[i + u] : 0u;
+                kd[u] = i + u < q.bend ? (uint32_t)v.bc_kind[i + u] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < ACC_R3U; ++u) e += (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u)) ? 1u : 0u;
+        }
     }
     if (q.bq) {
         uint32_t st = q.info & 7u, kind = q.info >> 3;
         if (((q.wk >> kind) & 1u) && st != 0 && st != 7) --e;
     }
     CT_PH(2);
-    if (e <= REC_INLINE) {
-        // (L6 <= e + 1 <= 16: T itself is dropped at most once, so xs holds every class entry)
-        uint32_t d = L6;   // position of T among them (at most one)
+    const bool inl = e <= REC_INLINE;
+    // an inline record: the class entries without T (L6 <= e + 1 <= 16: T itself is dropped at most once, so xs holds
+    // every class entry), then the kept R3 entries
+    uint32_t d = L6;   // position of T among them (at most one)
 #pragma unroll
-        for (uint32_t s = 0; s <= REC_INLINE; ++s)
-            if (q.bq && s < L6 && xs[s] == q.trank) d = s;
-        uint32_t buf[16] = {};
+    for (uint32_t s = 0; s <= REC_INLINE; ++s)
+        if (q.bq && s < L6 && xs[s] == q.trank) d = s;
+    uint32_t buf[16] = {};
 #pragma unroll
-        for (uint32_t s = 0; s < REC_INLINE; ++s) buf[s] = s < d ? xs[s] : xs[s + 1];
-        uint32_t n = L6 - (d < L6 ? 1u : 0u);
-        if (q.has_m)
-            for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {   // R3 candidates, ACC_R3U at a time
-                uint32_t ex[ACC_R3U], kd[ACC_R3U], xr[ACC_R3U];
-#pragma unroll
-                for (uint32_t u = 0; u < ACC_R3U; ++u) {
-                    const bool in = i + u < q.bend;
-                    ex[u] = in ? v.bc_exec[i + u] : 0u;
-                    kd[u] = in ? (uint32_t)v.bc_kind[i + u] : 0u;
-                    xr[u] = in ? v.bc_rank[i + u] : 0u;
+    for (uint32_t s = 0; s < REC_INLINE; ++s) buf[s] = s < d ? xs[s] : xs[s + 1];
+    uint32_t n = L6 - (d < L6 ? 1u : 0u);
+    if (coop) {
+        const bool want = inl && q.has_m && nc;
+        if (__ballot(want))
+            for (uint32_t c = clo; c < chi; c += 64) {
+                const uint32_t i = c + lane_id();
+                const uint32_t exl = i < chi ? v.bc_exec[i] : 0u, kdl = i < chi ? (uint32_t)v.bc_kind[i] : 0u;
+                const uint32_t xrl = i < chi ? v.bc_rank[i] : 0u;
+                const uint32_t cnt = min(64u, chi - c);
+                for (uint32_t u = 0; u < cnt; ++u) {
+                    const uint32_t exu = (uint32_t)__builtin_amdgcn_readlane((int)exl, (int)u);
+                    const uint32_t kdu = (uint32_t)__builtin_amdgcn_readlane((int)kdl, (int)u);
+                    const uint32_t xru = (uint32_t)__builtin_amdgcn_readlane((int)xrl, (int)u);
+                    const uint32_t iu = c + u;
+                    if (want && iu >= q.bstart && iu < q.bend && exu >= q.m && ((q.wk >> kdu) & 1u) &&
+                        !(q.bq && xru == q.trank))
+                        inl_put(buf, n, xru);
                 }
-#pragma unroll
-                for (uint32_t u = 0; u < ACC_R3U; ++u)
-                    if (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u) && !(q.bq && xr[u] == q.trank))
-                        inl_put(buf, n, xr[u]);
             }
+    } else if (inl && q.has_m) {
+        for (uint32_t i = q.bstart; i < q.bend; i += ACC_R3U) {   // R3 candidates, ACC_R3U at a time
+            uint32_t ex[ACC_R3U], kd[ACC_R3U], xr[ACC_R3U];
+#pragma unroll
+            for (uint32_t u = 0; u < ACC_R3U; ++u) {
+                const bool in = i + u < q.bend;
+                ex[u] = in ? v.bc_exec[i + u] : 0u;
+                kd[u] = in ? (uint32_t)v.bc_kind[i + u] : 0u;
+                xr[u] = in ? v.bc_rank[i + u] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < ACC_R3U; ++u)
+                if (i + u < q.bend && ex[u] >= q.m && ((q.wk >> kd[u]) & 1u) && !(q.bq && xr[u] == q.trank))
+                    inl_put(buf, n, xr[u]);
+        }
+    }
+    if (inl) {
         uint4 *r = ro.irec + 2 * (size_t)j;
         r[0] = make_uint4(buf[0], buf[1], buf[2], buf[3]);
         r[1] = make_uint4(buf[4], buf[5], buf[6], REC_INLINE_FLAG | (uint32_t)e);
