@@ -58,8 +58,8 @@ TAG_KERNEL = {
     # the levelise walk tiers (levelise.hip: one tag per tier)
     "lv_walk_lds": "k_lv_lds",
     "lv_walk_win": "k_lw_step<",
-    "lv_walk_w1": "k_lv_win1<",
     "lv_walk_waves": "k_lv_waves",
+    "lv_walk_blocks": "k_lv_blk",
 }
 
 
@@ -375,7 +375,7 @@ def run_config2(args, world, rank, local, dev):
     return ctx, timing, elapsed, result
 
 
-def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_batches=5):
+def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_batches=5, top_n=10):
     """N4 in steady state (messages/PreAccept.java:107-138, local/CommandStore.java:280-345,
     local/CommandsForKey.java:652-706): a device store built from the first n_init txns of workload.cfk_update_stream
     (8 keys per txn over 1M keys), then n_batches batches of `batch` new txns (plus the final statuses that fall due,
@@ -421,7 +421,10 @@ def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_bat
         ins.append((ui, ci, qi, qo))
     torch.cuda.synchronize()
 
+    scan_stats = {}
+
     def run(timing):
+        nonlocal scan_stats
         rows, tm = [], {}
         with Context(local, timing=timing) as c:
             lib = c._lib
@@ -450,6 +453,7 @@ def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_bat
                     c.check(lib.acc_keydeps_batch(c.handle, C.byref(v), C.byref(kv)))
                     torch.cuda.synchronize(); t.append(time.perf_counter())
                     d = [(t[i + 1] - t[i]) * 1e3 for i in range(4)]
+                    scan_stats = {k: v for k, v in c.stats().items() if k.startswith("keydeps.")}
                     rows.append(dict(propose_ms=d[0], maxconflicts_update_ms=d[1], cfk_update_ms=d[2],
                                      cfk_apply_ms=st.get("cfk.apply_us", 0) / 1e3, view_ms=st.get("cfk.view_us", 0) / 1e3,
                                      keydeps_scan_ms=d[3], total_ms=sum(d), store_txns=int(v.n_txn),
@@ -465,7 +469,7 @@ def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_bat
     _, tm = run(True)
     nb = len(rows)
     mean = {k: round(sum(r[k] for r in rows) / nb, 3) for k in rows[0] if k.endswith("_ms")}
-    top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:10]
+    top = sorted(tm.items(), key=lambda kv: -kv[1][0])[:top_n]
     return {"workload": f"workload.cfk_update_stream({(n_init + batch * n_batches) // 1000}K txns x 8 {dist} keys over "
                         f"1M keys): a {n_init // 1000}K-txn device store, then {n_batches} PreAccept batches of "
                         f"{batch // 1000}K new txns (MaxConflicts propose + merge, CommandsForKey.update with deps, "
@@ -476,7 +480,7 @@ def cfk_steady_leg(local, dist="uniform", n_init=1_000_000, batch=100_000, n_bat
             "final_dep_edges": rows[-1]["dep_edges"],
             "per_batch_total_ms": [round(r["total_ms"], 3) for r in rows],
             "per_batch_view_ms": [round(r["view_ms"], 3) for r in rows],
-            "setup_gen_s": round(t_gen, 2),
+            "setup_gen_s": round(t_gen, 2), "last_scan_stats": scan_stats,
             "top_kernels_ms_per_batch": {k: round(x[0] / nb, 3) for k, x in top}}
 
 

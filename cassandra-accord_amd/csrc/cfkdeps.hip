@@ -1729,27 +1729,8 @@ __global__ __launch_bounds__(BLOCK) void k_cb_ent(uint64_t NE, const uint32_t *_
     if (s.st[e] != c.st || cmp(Ts{ s.xm[e], s.xl[e], s.xn[e] }, Ts{ c.xm, c.xl, c.xn }) != 0)
         atomicOr((unsigned long long *)err, (unsigned long long)E_STATE);
 }
-// each pair's missing[] TxnIds as batch indices, each result checked against the one before it (sorted unique). A pair
-// with a short missing[] is its lane's; the long ones (a hot key's entries carry thousands) are taken by the whole wave
-// one after another, its lanes splitting the searches. cb_find: the binary search over the batch's TxnIds.
-constexpr uint32_t CB_LONG = 32;
-__device__ __forceinline__ uint32_t cb_find(const BatchOut &b, uint32_t n, const Ts &k, uint64_t &bad)
-{
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (cmp(Ts{ b.tm[mid], b.tl[mid], b.tn[mid] }, k) < 0) lo = mid + 1; else hi = mid;
-    }
-    if (lo == n || cmp(Ts{ b.tm[lo], b.tl[lo], b.tn[lo] }, k) != 0) {
-        bad |= E_STATE;
-        lo = 0;
-    }
-    return lo;
-}
-// Per entry in key-major order (its missing[] read contiguously): each missing TxnId's batch index from an
-// open-addressing hash table of the batch's TxnIds (built once per call: one probe of a 32-B slot per lookup, where a
-// binary search over the batch's TxnIds costs ~20 dependent loads of 20 B). Long lists (a hot key's entries carry
-// thousands) are taken by the whole wave, its lanes splitting the list.
+// Each missing TxnId's batch index from an open-addressing hash table of the batch's TxnIds (built once per call: one
+// probe of a 32-B slot per lookup, where a binary search over the batch's TxnIds costs ~20 dependent loads of 20 B).
 struct TxnHash {
     ulonglong4 *slot;   // (msb, lsb & IDENTITY_LSB, node << 32 | index, used)
     uint32_t mask;
@@ -1783,43 +1764,28 @@ __device__ __forceinline__ uint32_t th_find(const TxnHash &h, const Ts &k, uint6
         if (e.x == k.m && e.y == l && (int32_t)(e.z >> 32) == k.n) return (uint32_t)e.z;
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_cb_miss_hash(uint64_t NE, const uint32_t *__restrict__ qpos, Snap s, TxnHash h,
+// missing[] elements in parallel (a thread each, their TxnIds read contiguously): the owning entry of element j from
+// a max-scan of the entries' first-element marks; the element's batch index by one hash probe, written at its pair's
+// place in the txn-major layout; each element's TxnId must exceed the one before it in its list (sorted unique)
+__global__ __launch_bounds__(BLOCK) void k_cb_mhead(uint64_t NE, Snap s, uint32_t *__restrict__ head)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e < NE && s.miss_off[e + 1] > s.miss_off[e]) head[s.miss_off[e]] = (uint32_t)e;
+}
+__global__ __launch_bounds__(BLOCK) void k_cb_miss_elem(uint64_t NM, const uint32_t *__restrict__ owner,
+                                                        const uint32_t *__restrict__ qpos, Snap s, TxnHash h,
                                                         const uint32_t *__restrict__ mo, uint32_t *__restrict__ mt,
                                                         uint64_t *__restrict__ err)
 {
-    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t lane = lane_id();
+    const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= NM) return;
     uint64_t bad = 0;
-    uint32_t m0 = 0, m1 = 0, w0 = 0;
-    if (e < NE) {
-        m0 = s.miss_off[e]; m1 = s.miss_off[e + 1];
-        if (m1 > m0) w0 = mo[qpos[e]];
-    }
-    const bool lng = m1 - m0 >= CB_LONG;
-    if (!lng) {
-        uint32_t prev = 0;
-        for (uint32_t j = m0; j < m1; ++j) {
-            const uint32_t lo = th_find(h, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad);
-            if (j > m0 && lo <= prev) bad |= E_ARG_SORT;
-            mt[w0 + (j - m0)] = lo;
-            prev = lo;
-        }
-    }
-    for (uint64_t todo = __ballot(lng); todo; todo &= todo - 1) {
-        const int src = __builtin_ctzll(todo);
-        const uint32_t a = __shfl(m0, src, 64), z = __shfl(m1, src, 64), w = __shfl(w0, src, 64);
-        uint32_t carry = 0;
-        for (uint32_t base = a; base < z; base += 64) {
-            const uint32_t j = base + lane;
-            const bool valid = j < z;
-            const uint32_t lo = valid ? th_find(h, Ts{ s.mm[j], s.ml[j], s.mn[j] }, bad) : 0u;
-            uint32_t prev = __shfl_up(lo, 1, 64);
-            if (lane == 0) prev = carry;
-            if (valid && j > a && lo <= prev) bad |= E_ARG_SORT;
-            if (valid) mt[w + (j - a)] = lo;
-            carry = __shfl(lo, 63, 64);
-        }
-    }
+    const uint32_t e = owner[j];
+    const uint32_t m0 = s.miss_off[e];
+    const Ts x{ s.mm[j], s.ml[j], s.mn[j] };
+    if (j > m0 && cmp(Ts{ s.mm[j - 1], s.ml[j - 1], s.mn[j - 1] }, x) >= 0) bad |= E_ARG_SORT;
+    const uint32_t lo = th_find(h, x, bad);
+    mt[mo[qpos[e]] + (j - m0)] = lo;
     if (bad) atomicOr((unsigned long long *)err, (unsigned long long)bad);
 }
 
@@ -1911,8 +1877,12 @@ void cfk_snap_to_batch(acc_ctx *ctx, const acc_cfk_snap *in, acc_cfk_batch_view 
             TxnHash th{ ctx->get<ulonglong4>("cb_hash", cap), cap - 1 };
             ACC_HIP(hipMemsetAsync(th.slot, 0, (size_t)cap * sizeof(ulonglong4), st));
             launch(ctx, "cb_hash", k_cb_hash_build, dim3(grid_for(nt, BLOCK)), dim3(BLOCK), 0, (const uint64_t *)dr.count_dev, b, th);
-            launch(ctx, "cb_miss", k_cb_miss_hash, g, dim3(BLOCK), 0, NE, (const uint32_t *)qpos, s, th, (const uint32_t *)mo,
-                   mt, errs);
+            uint32_t *head = ctx->get<uint32_t>("cb_mhead", NM), *owner_m = ctx->get<uint32_t>("cb_mowner", NM);
+            ACC_HIP(hipMemsetAsync(head, 0, NM * 4, st));
+            launch(ctx, "cb_mhead", k_cb_mhead, g, dim3(BLOCK), 0, NE, s, head);
+            scan<uint32_t, OpMax<uint32_t>>(ctx, head, owner_m, NM, false, (uint32_t *)nullptr);
+            launch(ctx, "cb_miss", k_cb_miss_elem, dim3(grid_for(NM, BLOCK)), dim3(BLOCK), 0, NM, (const uint32_t *)owner_m,
+                   (const uint32_t *)qpos, s, th, (const uint32_t *)mo, mt, errs);
         }
         ACC_HIP(hipMemcpyAsync(ctx->pinned, errs, 8, hipMemcpyDeviceToHost, st));
         ACC_HIP(hipMemcpyAsync(ctx->pinned + 1, dr.count_dev, 8, hipMemcpyDeviceToHost, st));

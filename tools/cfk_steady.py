@@ -9,4 +9,5 @@ import bench  # noqa: E402
 
 dist = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-print(json.dumps({dist: bench.cfk_steady_leg(0, dist=dist, n_batches=nb)}), flush=True)
+top = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+print(json.dumps({dist: bench.cfk_steady_leg(0, dist=dist, n_batches=nb, top_n=top)}), flush=True)
