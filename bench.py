@@ -59,7 +59,6 @@ TAG_KERNEL = {
     "lv_walk_lds": "k_lv_lds",
     "lv_walk_win": "k_lw_step<",
     "lv_walk_waves": "k_lv_waves",
-    "lv_walk_blocks": "k_lv_blk",
 }
 
 

@@ -19,7 +19,7 @@ ACC_OPT_FORCE_REPLAY = 2
 ACC_OPT_NO_WINDOW_TIER = 4
 ACC_OPT_RD_WIDE_SORT = 8
 ACC_OPT_PD_SERIAL = 16
-ACC_LV_AUTO, ACC_LV_LDS_WALK, ACC_LV_WINDOWED, ACC_LV_WAVES, ACC_LV_BLOCKS = 0, 1, 2, 3, 4
+ACC_LV_AUTO, ACC_LV_LDS_WALK, ACC_LV_WINDOWED, ACC_LV_WAVES = 0, 1, 2, 3
 # SafeCommandStore.TestStartedAt / TestDep / TestStatus ordinals (local/SafeCommandStore.java:63-70)
 ACC_STARTED_BEFORE, ACC_STARTED_AFTER, ACC_STARTED_ANY = 0, 1, 2
 ACC_DEP_WITH, ACC_DEP_WITHOUT, ACC_DEP_ANY = 0, 1, 2

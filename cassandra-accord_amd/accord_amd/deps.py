@@ -46,7 +46,7 @@ def _ptr(a: np.ndarray):
 class Context:
     """One acc_ctx: a HIP stream plus device scratch (one per host thread / CommandStore)."""
 
-    LV_TIERS = {"auto": 0, "lds": 1, "windowed": 2, "waves": 3, "blocks": 4}
+    LV_TIERS = {"auto": 0, "lds": 1, "windowed": 2, "waves": 3}
 
     def __init__(self, device: int = 0, timing: bool = False, force_replay: bool = False, *, cfk_hot: int = 0,
                  lv_tier: str = "auto", lv_chunk: int = 0, no_window_tier: bool = False, rd_wide_sort: bool = False,

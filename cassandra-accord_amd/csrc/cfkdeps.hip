@@ -1220,18 +1220,6 @@ __global__ __launch_bounds__(BLOCK) void k_ch_ulist(uint32_t ne, uint32_t nh, ui
     if (e <= nh) uoff[e] = e == nh ? nu : (eoff[e] < ne ? uexcl[eoff[e]] : nu);
 }
 
-// the entry of hot key h with TxnId t (NONE when absent)
-__device__ __forceinline__ uint32_t ch_find(const uint32_t *__restrict__ eg, const HG *__restrict__ G, uint32_t e0, uint32_t e1,
-                                            const Ts &t)
-{
-    uint32_t lo = e0, hi = e1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const HG &x = G[eg[mid]];
-        if (cmp(hg_id(x), t) < 0) lo = mid + 1; else hi = mid;
-    }
-    return lo < e1 && cmp(hg_id(G[eg[lo]]), t) == 0 ? lo : NONE;
-}
 // the first entry >= t in [lo, e1): galloping from lo (a sorted run of TxnIds looked up in order moves a few steps)
 __device__ __forceinline__ uint32_t ch_lower(const uint32_t *__restrict__ eg, const HG *__restrict__ G, uint32_t lo, uint32_t e1,
                                              const Ts &t)
@@ -1309,10 +1297,53 @@ __global__ __launch_bounds__(BLOCK) void k_ch_mention(uint64_t NI, const uint8_t
 }
 
 // the closed-form missing[] of entry e (count only when out is null)
+// The (hot key, TxnId) groups that crossed to committed in this batch, as an open-addressing hash set (32-B slots): a
+// snapshot missing[] TxnId is dropped when its group crossed (removeMissing, CommandsForKey.java:946-972), one probe per
+// element instead of a binary search over the key's entries (a hot key holds ~10^6: ~40 dependent loads)
+struct XSet {
+    ulonglong4 *slot;   // (msb, lsb & IDENTITY_LSB, node << 32 | hot key, used)
+    uint32_t mask;      // 0: the set is empty (no lookups)
+};
+__device__ __forceinline__ uint32_t xs_hash(uint32_t h, uint64_t m, uint64_t l, int32_t n)
+{
+    uint64_t x = m * 0x9E3779B97F4A7C15ull ^ (l & IDENTITY_LSB) ^ ((uint64_t)(uint32_t)n << 40) ^ ((uint64_t)h << 20);
+    x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29; x *= 0x94D049BB133111EBull; x ^= x >> 32;
+    return (uint32_t)x;
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_xcount(uint32_t ng, const HG *__restrict__ G, uint32_t *__restrict__ cnt)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    const bool x = g < ng && (G[g].flags & HF_CROSSED);
+    const uint64_t b = __ballot(x);
+    if (lane_id() == 0 && b) atomicAdd(cnt, (uint32_t)__popcll(b));
+}
+__global__ __launch_bounds__(BLOCK) void k_ch_xbuild(uint32_t ng, const HG *__restrict__ G, XSet xs)
+{
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= ng || !(G[g].flags & HF_CROSSED)) return;
+    const HG &X = G[g];
+    const uint64_t l = X.il & IDENTITY_LSB;
+    for (uint32_t i = xs_hash(X.h, X.im, l, X.in) & xs.mask;; i = (i + 1) & xs.mask)
+        if (atomicCAS((unsigned long long *)&xs.slot[i].w, 0ull, 1ull) == 0ull) {
+            xs.slot[i].x = X.im; xs.slot[i].y = l; xs.slot[i].z = ((uint64_t)(uint32_t)X.in << 32) | X.h;
+            return;
+        }
+}
+__device__ __forceinline__ bool xs_has(const XSet &xs, uint32_t h, const Ts &t)
+{
+    if (!xs.mask) return false;
+    const uint64_t l = t.l & IDENTITY_LSB, z = ((uint64_t)(uint32_t)t.n << 32) | h;
+    for (uint32_t i = xs_hash(h, t.m, l, t.n) & xs.mask;; i = (i + 1) & xs.mask) {
+        const ulonglong4 e = xs.slot[i];
+        if (e.w == 0) return false;
+        if (e.x == t.m && e.y == l && e.z == z) return true;
+    }
+}
+
 __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
                                                const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u, Snap s,
-                                               uint64_t *om, uint64_t *ol, int32_t *on)
+                                               const XSet &xs, uint64_t *om, uint64_t *ol, int32_t *on)
 {
     const HG X = G[eg[e]];
     if (!has_info(X.st)) return 0;
@@ -1346,7 +1377,6 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
     if (X.snap_x == NONE) return 0;
     // the snapshot's missing[] (less the TxnIds committed in this batch) merged with the new uncommitted entries
     const uint32_t m0 = s.miss_off[X.snap_x], m1 = s.miss_off[X.snap_x + 1];
-    const uint32_t e0 = eoff[h], e1 = eoff[h + 1];
     uint32_t a = m0, k = u0;
     auto next_new = [&]() {
         while (k < ub) {
@@ -1356,12 +1386,8 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
             ++k;
         }
     };
-    auto next_snap = [&]() {
-        while (a < m1) {
-            const uint32_t f = ch_find(eg, G, e0, e1, Ts{ s.mm[a], s.ml[a], s.mn[a] });
-            if (f == NONE || !(G[eg[f]].flags & HF_CROSSED)) return;
-            ++a;
-        }
+    auto next_snap = [&]() {   // (skips the snapshot TxnIds whose group on this key crossed to committed)
+        while (a < m1 && xs_has(xs, h, Ts{ s.mm[a], s.ml[a], s.mn[a] })) ++a;
     };
     next_new();
     next_snap();
@@ -1392,7 +1418,7 @@ template <bool EMIT>
 __global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
                                                    const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                    const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
-                                                   Snap s, uint32_t *__restrict__ mcnt, const uint32_t *__restrict__ moff,
+                                                   Snap s, XSet xs, uint32_t *__restrict__ mcnt, const uint32_t *__restrict__ moff,
                                                    uint64_t *__restrict__ mm, uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
 {
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x, lane = lane_id();
@@ -1419,8 +1445,8 @@ __global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *
             if (EMIT) out = moff[e];
         }
         if (!lng) {
-            if (EMIT) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, mm + moff[e], ml + moff[e], mn + moff[e]);
-            else mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, nullptr, nullptr, nullptr);
+            if (EMIT) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, mm + moff[e], ml + moff[e], mn + moff[e]);
+            else mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, nullptr, nullptr, nullptr);
         }
     }
     for (uint64_t todo = __ballot(lng); todo; todo &= todo - 1) {
@@ -1633,9 +1659,25 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     uint32_t *uoff = ctx->get<uint32_t>("ch_uoff", (size_t)nh + 1);
     launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nu,
            (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, (const uint32_t *)eg, (const HG *)G, ulist, uoff);
+    // the groups that crossed to committed in this batch, as a hash set
+    XSet xs{ nullptr, 0 };
+    {
+        uint32_t *xc = ctx->get<uint32_t>("ch_xcnt", 1);
+        ACC_HIP(hipMemsetAsync(xc, 0, 4, st));
+        launch(ctx, "ch_xcount", k_ch_xcount, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, (const HG *)G, xc);
+        const uint32_t nxc = read32(xc);
+        if (nxc) {
+            uint32_t cap = 1024;
+            while (cap < 2 * nxc && cap < (1u << 31)) cap <<= 1;
+            xs.slot = ctx->get<ulonglong4>("ch_xset", cap);
+            xs.mask = cap - 1;
+            ACC_HIP(hipMemsetAsync(xs.slot, 0, (size_t)cap * sizeof(ulonglong4), st));
+            launch(ctx, "ch_xbuild", k_ch_xbuild, dim3(grid_for(ng, BLOCK)), dim3(BLOCK), 0, ng, (const HG *)G, xs);
+        }
+    }
     uint32_t *mcnt = ctx->get<uint32_t>("ch_mcnt", std::max<uint32_t>(ne, 1)), *moff = ctx->get<uint32_t>("ch_moff", (size_t)ne + 1);
     launch(ctx, "ch_mcount", k_ch_miss<false>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, mcnt, (const uint32_t *)nullptr,
+           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, mcnt, (const uint32_t *)nullptr,
            (uint64_t *)nullptr, (uint64_t *)nullptr, (int32_t *)nullptr);
     uint64_t *nm64 = ctx->get<uint64_t>("ch_nm64", 1);
     sum_u32(ctx, mcnt, ne, nm64);   // the u32 offsets below must not wrap
@@ -1648,7 +1690,7 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
     if (nm)
         launch(ctx, "ch_memit", k_ch_miss<true>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, (uint32_t *)nullptr,
+               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, (uint32_t *)nullptr,
                (const uint32_t *)moff, mm, ml, mn);
     ctx->stat("cfk.hot_keys", nh);
     ctx->stat("cfk.hot_items", NI);

@@ -2084,11 +2084,17 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
 #pragma unroll
                 for (int q = 0; q < 6; ++q)
                     if (R.pre[k][q + 1] > R.pre[k][q]) mn = min(mn, v.list_rank[R.start[k][q]]);
-                const uint32_t l3 = R.pre[k][7] - R.pre[k][6];
-                if (l3 > 256) mn = 0u;
-                else for (uint32_t j = 0; j < l3; ++j) mn = min(mn, v.bc_rank[R.start[k][6] + j]);
+                if (R.pre[k][7] - R.pre[k][6] > 256) mn = 0u;   // (a long R3 run: from 0; a short one: below)
             }
             atomicMin(&L.minr, mn);
+        }
+        // the short R3 runs' smallest ranks, the block's threads side by side (one thread walking a run serially waits on
+        // one load at a time)
+        for (uint32_t k = 0; k < c.nk; ++k) {
+            if (R.m[k] == INLINE_M) continue;
+            const uint32_t l3 = R.pre[k][7] - R.pre[k][6];
+            if (l3 > 256 || tid >= l3) continue;
+            atomicMin(&L.minr, v.bc_rank[R.start[k][6] + tid]);
         }
         __syncthreads();
         const uint32_t lo_span = S > WIN_W * 32 ? S - WIN_W * 32 : 0u;
@@ -2408,7 +2414,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
                                                    uint32_t *__restrict__ psz, uint32_t raw_cap,
                                                    uint32_t *__restrict__ bigflag, uint64_t *__restrict__ szA,
                                                    uint64_t *__restrict__ szK, uint64_t *__restrict__ any16,
-                                                   uint64_t *__restrict__ eb)
+                                                   uint64_t *__restrict__ eb, uint32_t *__restrict__ runflag)
 {
     const uint32_t t = (blockIdx.x * BLOCK + threadIdx.x) / MK_G, sub = threadIdx.x & (MK_G - 1);
     if (t >= n) return;   // group-uniform: shuffles stay inside the group
@@ -2442,6 +2448,7 @@ __global__ __launch_bounds__(BLOCK) void k_v3_mark(uint32_t n, const uint32_t *_
     const bool big = nk > (uint32_t)ST_G || e > (uint32_t)ST_N2 || (run_rec && raw > raw_cap);
     if (sub == 0) {
         bigflag[t] = big ? 1u : 0u;
+        runflag[t] = run_rec && !big ? 1u : 0u;   // a stream txn with a run record: the RUNS stream pass
         szA[t] = (uint64_t)kd + e;
         szK[t] = kd;
         eb[t] = big ? e : 0u;   // the big txns' entries: their TxnId scratch bases by the same multi-scan
@@ -2644,7 +2651,7 @@ __device__ unsigned long long *g_st_prof;
 #endif
 // G lanes per txn (one key each), N2 entries per txn at most. LIST = false: every txn (the stream ones taken); true: the
 // txns of s.list[0, s.n).
-template <class EntT, int NT, int G, int N2, bool LIST>
+template <class EntT, int NT, int G, int N2, bool LIST, bool RUNS>
 __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stream s)
 {
     constexpr int TT = NT / G;   // txns per tile
@@ -2685,7 +2692,8 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     const bool sm = valid && !big;
     EntT *buf = ent[grp];
     ST_PH(1);
-    // ---- records: inline entries straight to LDS; a run record's runs stay in its lane's registers
+    // ---- records: inline entries straight to LDS; a run record's runs stay in its lane's registers (RUNS only: the
+    // lean pass leaves a txn with a run record to the RUNS pass, which the mark pass listed it for)
     uint32_t e = 0, rawk = 0;
     bool run = false;
     uint4 r0 = {}, r1 = {}, r2 = {}, r3 = {};
@@ -2700,11 +2708,13 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
                 r2 = r[0]; r3 = r[1];
             }
         } else {
-            const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
-            r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
             run = true;
             e = w;
-            rawk = r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
+            if constexpr (RUNS) {
+                const uint4 *r = s.rec + 4 * (size_t)(c.j0 + sub);
+                r0 = r[0]; r1 = r[1]; r2 = r[2]; r3 = r[3];
+                rawk = r1.z + r1.w + r2.x + r2.y + r2.z + r2.w + r3.y;
+            }
         }
     }
     const uint32_t ein = run ? 0u : e;
@@ -2728,8 +2738,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     // runs R1/R2 per class and R3, dropping T itself and R3 entries below M or of unwitnessed kinds, after the inline
     // entries
     const uint64_t runmask = __ballot(sm && run) & gmask;
-    const uint32_t nrun = (uint32_t)__popcll(runmask);
-    uint32_t wnrun = nrun;
+    uint32_t wnrun = RUNS ? (uint32_t)__popcll(runmask) : 0u;
 #pragma unroll
     for (int d = G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
     uint32_t cursor = E_in;
@@ -2781,8 +2790,8 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         }
     }
     ST_PH(3);
-    bool ok = sm;
-    if (sm && cursor != E) {
+    bool ok = sm && (RUNS || !runmask);   // (the lean pass skips a txn with a run record: the RUNS pass takes it)
+    if (ok && cursor != E) {
         if (sub == 0) atomicAdd((unsigned long long *)s.err, 1ull);
         ok = false;
     }
@@ -2864,7 +2873,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     }
 #ifdef ACC_PHASE_PROF
     ST_PH(6);
-    if (lane == 0) {
+    if (lane == 0 && !LIST) {
         unsigned long long *row = g_st_prof + 8 * (size_t)tile;
         for (int i = 0; i < 6; ++i) row[i] = ph[i + 1] - ph[i];
         row[7] = 1;
@@ -3429,7 +3438,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     cols.bc_pm_in = ctx->get<uint64_t>("v2_bc_pm_in", P);
     cols.bc_key = ctx->get<uint64_t>("v2_bc_key", P);
     // the count / mark passes' accumulators, zeroed by the column kernels (txn records, k_v2_apply); bigflag above
-    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 3);   // E, big txns, a 9-16-key big txn
+    uint64_t *tot = ctx->get<uint64_t>("v3_tot", 4);   // E, big txns, a 9-16-key big txn, stream txns with a run record
     uint64_t *gstat = ctx->get<uint64_t>("v2_gstat", GSTAT_N + 6);   // + the batch totals and E / big counts (k_v3_ucompact)
     // the rank-dependent columns (run again when the deferred tie check finds the sorted-batch ranks invalid)
     auto build_columns = [&]() {
@@ -3445,7 +3454,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         launch(ctx, "v2_apply", k_v2_apply, dim3(nt), dim3(BLOCK), 0, P, (const uint32_t *)s_rank, (const uint32_t *)s_exec,
                (const uint8_t *)s_info, (const uint32_t *)seg_flag, (const uint32_t *)tile_pref, (const uint32_t *)totals, nt,
                rbits, cols, seg_incl, seg_start, (const uint32_t *)ps.vals, key_code, seg_key_buf, sp_m4, pp.rk, rk_mask,
-               bases, tot, 3u, gstat, (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
+               bases, tot, 4u, gstat, (uint32_t)GSTAT_N, (const uint64_t *)g, reinterpret_cast<uint64_t *>(totals) + 4);
     };
     build_columns();
     // totals, g[4..6] staged by k_v2_apply, the bumped-query count
@@ -3548,8 +3557,9 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint64_t *arena_off = ctx->get<uint64_t>("arena_off", (size_t)n + 1);
     uint64_t *szA = ctx->get<uint64_t>("v3_szA", n), *szK = ctx->get<uint64_t>("v3_szK", n);
     uint64_t *eb = ctx->get<uint64_t>("v3_eb", n), *dB = ctx->get<uint64_t>("v3_dB", (size_t)n + 1);
+    uint32_t *runflag = ctx->get<uint32_t>("v3_runflag", n);
     launch(ctx, "v3_mark", k_v3_mark, dim3(grid_for((size_t)n * MK_G, BLOCK)), dim3(BLOCK), 0, n, key_off,
-           (const uint32_t *)ro.irec, (const uint4 *)rec, psz, raw_cap, bigflag, szA, szK, tot + 2, eb);
+           (const uint32_t *)ro.irec, (const uint4 *)rec, psz, raw_cap, bigflag, szA, szK, tot + 2, eb, runflag);
     uint64_t *blk_pre = ctx->get<uint64_t>("v3_blk_pre", gP);
     {   // arena / key offsets, the count pass's per-block entry totals, the big txns' TxnId scratch bases: one launch
         const uint64_t *si[4] = { szA, szK, blk_e, eb };
@@ -3563,12 +3573,18 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     uint32_t *blist = ctx->get<uint32_t>("v3_blist", n);
     launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)bigflag,
            (const uint32_t *)bpos, blist);
+    // the stream txns with a run record, for the RUNS stream pass
+    uint32_t *rpos = ctx->get<uint32_t>("v3_rpos", n), *rlist = ctx->get<uint32_t>("v3_rlist", n);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, runflag, rpos, n, true, reinterpret_cast<uint32_t *>(tot + 3));
+    launch(ctx, "v3_compact", k_v3_compact, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, (const uint32_t *)runflag,
+           (const uint32_t *)rpos, rlist);
     // ---- E (dependency entries), the big-txn count and the 9-16-key flag reach the host here
-    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ACC_HIP(hipMemcpyAsync(ctx->pinned, tot, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     ctx->sync();
     const uint64_t E = ctx->pinned[0];
     const uint32_t nbig = (uint32_t)ctx->pinned[1];
     const bool any16 = ctx->pinned[2] != 0;
+    const uint32_t nrun = (uint32_t)ctx->pinned[3];
     if (E >= 0xFFFFFFFFull) fail(ACC_E_CAP, "more than 2^32-1 dependency entries in one batch");
     uint64_t *u_off = ctx->get<uint64_t>("u_off", (size_t)n + 1);
     uint64_t *u_cnt = ctx->get<uint64_t>("u_cnt", n);
@@ -3642,7 +3658,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         wo.huge_list = ctx->get<uint32_t>("v2_huge_list", nbig);
         // persistent grids over device-side list counts (routing happened after the last host sync); the tiers run on a
         // side stream, concurrently with the stream pass (it needs only the big txns' sizes, set by bigfill)
-        ctx->fork(1);
+        ctx->fork(nrun ? 2 : 1);
         ctx->launch_stream = ctx->aux[0];
         if (win_ok) {
             // the window tier takes every big txn of <= 16 keys; the sorting tiers run after the next host sync, only
@@ -3683,8 +3699,20 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ACC_HIP(hipMemsetAsync(prof_buf, 0, 8 * prof_rows * sizeof(unsigned long long), st));
         ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_st_prof), &prof_buf, sizeof prof_buf, 0, hipMemcpyHostToDevice, st));
 #endif
-        if (rbits <= 28) launch(ctx, "v3_stream", k_v3_stream<uint32_t, st_nt, ST_G, ST_N2, false>, dim3(nblocks), dim3(st_nt), 0, sp);
-        else launch(ctx, "v3_stream", k_v3_stream<uint64_t, st_nt, ST_G, ST_N2, false>, dim3(nblocks), dim3(st_nt), 0, sp);
+        if (nrun) {
+            // the stream txns with a run record on side stream 1, concurrently with the lean pass below (their gathers
+            // kept out of the lean pass: registers and a wave-uniform loop in every wave for ~0.5% of the txns)
+            if (!nbig) ctx->fork(2);
+            V3Stream sr = sp;
+            sr.list = rlist; sr.n = nrun;
+            const uint32_t rblocks = (nrun + tt - 1) / tt;
+            ctx->launch_stream = ctx->aux[1];
+            if (rbits <= 28) launch(ctx, "v3_stream_runs", k_v3_stream<uint32_t, st_nt, ST_G, ST_N2, true, true>, dim3(rblocks), dim3(st_nt), 0, sr);
+            else launch(ctx, "v3_stream_runs", k_v3_stream<uint64_t, st_nt, ST_G, ST_N2, true, true>, dim3(rblocks), dim3(st_nt), 0, sr);
+            ctx->launch_stream = nullptr;
+        }
+        if (rbits <= 28) launch(ctx, "v3_stream", k_v3_stream<uint32_t, st_nt, ST_G, ST_N2, false, false>, dim3(nblocks), dim3(st_nt), 0, sp);
+        else launch(ctx, "v3_stream", k_v3_stream<uint64_t, st_nt, ST_G, ST_N2, false, false>, dim3(nblocks), dim3(st_nt), 0, sp);
 #ifdef ACC_PHASE_PROF
         {
             std::vector<unsigned long long> h(8 * prof_rows);
@@ -3703,7 +3731,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         }
 #endif
     }
-    if (nbig) ctx->join(1);
+    if (nbig || nrun) ctx->join(nrun ? 2 : 1);
     finish();
     if (ctx->pinned[5]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
@@ -3761,6 +3789,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         finish();
     }
     ctx->stat("keydeps.stream_txns", n - nbig);
+    ctx->stat("keydeps.stream_run_txns", nrun);
     ctx->stat("keydeps.big_path_txns", nbig);
     ctx->stat("keydeps.medium_txns", nmed);
     ctx->stat("keydeps.big_txns", nbig2);

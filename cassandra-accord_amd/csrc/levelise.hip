@@ -368,179 +368,6 @@ __global__ __launch_bounds__(LV_NT) void k_lv_lds(uint32_t n, uint32_t npad, int
     if (lane == 0 && my_max) atomicMax(max_level, my_max);
 }
 
-// ---- block walk (n <= LV_LDS_MAX_N): the exec order cut into blocks of 64 positions, one lane per position, every
-// level in one workgroup's LDS.
-// 1. k_lv_bcount / k_lv_bwrite (whole GPU, wave per position i): i's waiting deps (exec rank below its own,
-//    Commands.java:804-810) in blocks blk(i) - d for d < LB_D become bits of LB_D 64-bit masks per position
-//    (d = 0: earlier lanes of its own block); deps further back go to a residual u16 list (none when deps are recent).
-// 2. k_lv_blk (one workgroup, LB_W waves taking the blocks round robin): a wave loads its block's masks, folds the
-//    residual deps (their blocks published long ago), then, oldest first, as each of blocks b - LB_D + 1 .. b - 1 is
-//    published broadcasts its levels lane by lane (v_readlane) into the masked maxima, and resolves the near chain in
-//    lane order (lane k's level is final when step k comes). A dependency hop costs a few VALU instructions; the
-//    critical path per block is the last two 64-step mask loops.
-constexpr int LB_D = 8;                 // blocks of deps held as masks (the own block + 7 back)
-constexpr int LB_W = 4;                 // waves (blocks in flight)
-constexpr int LB_NT = 64 * LB_W;
-
-// per position: residual count (deps more than LB_D - 1 blocks back); also the graph validation (err |= 1 decreasing
-// offsets, 2 a dep >= n)
-__global__ __launch_bounds__(BLOCK) void k_lv_bcount(uint32_t n, const uint32_t *__restrict__ order_exec,
-                                                     const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
-                                                     const uint32_t *__restrict__ exec_rank, const uint32_t *__restrict__ pos,
-                                                     uint32_t *__restrict__ cnt, uint32_t *__restrict__ err)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= n) return;
-    const uint32_t t = order_exec[i], er = exec_rank[t], bi = i >> 6;
-    const uint64_t a = off[t], b = off[t + 1];
-    if (b < a && lane == 0) atomicOr(err, 1u);
-    uint32_t c = 0;
-    for (uint64_t e = a + lane; e < b; e += 64) {
-        const uint32_t d = dep[e];
-        if (d >= n) { atomicOr(err, 2u); continue; }
-        c += exec_rank[d] < er && bi - (pos[d] >> 6) >= (uint32_t)LB_D;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-    if (lane == 0) cnt[i] = c;
-}
-
-__global__ __launch_bounds__(BLOCK) void k_lv_bwrite(uint32_t n, const uint32_t *__restrict__ order_exec,
-                                                     const uint64_t *__restrict__ off, const uint32_t *__restrict__ dep,
-                                                     const uint32_t *__restrict__ exec_rank, const uint32_t *__restrict__ pos,
-                                                     const uint32_t *__restrict__ roff, uint16_t *__restrict__ rdep,
-                                                     uint64_t *__restrict__ mask, const uint32_t *__restrict__ err)
-{
-    const uint32_t i = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = lane_id();
-    if (i >= n || *err) return;   // an invalid graph (k_lv_bcount): write nothing
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t t = order_exec[i], er = exec_rank[t], bi = i >> 6;
-    const uint64_t a = off[t], b = off[t + 1];
-    uint64_t m[LB_D];
-#pragma unroll
-    for (int d = 0; d < LB_D; ++d) m[d] = 0;
-    uint32_t w = roff[i];
-    for (uint64_t c0 = a; c0 < b; c0 += 64) {
-        const uint64_t e = c0 + lane;
-        uint32_t q = 0, dd = 0;
-        bool keep = false;
-        if (e < b) {
-            const uint32_t d = dep[e];
-            keep = d < n && exec_rank[d] < er;
-            if (keep) { q = pos[d]; dd = bi - (q >> 6); }
-        }
-        const bool res = keep && dd >= (uint32_t)LB_D;
-#pragma unroll
-        for (int d = 0; d < LB_D; ++d) if (keep && dd == (uint32_t)d) m[d] |= 1ull << (q & 63);
-        const uint64_t bal = __ballot(res);
-        if (res) rdep[w + (uint32_t)__popcll(bal & lt)] = (uint16_t)q;
-        w += (uint32_t)__popcll(bal);
-    }
-#pragma unroll
-    for (int d = 0; d < LB_D; ++d) {
-#pragma unroll
-        for (int x = 1; x < 64; x <<= 1) m[d] |= __shfl_xor(m[d], x, 64);
-    }
-    if (lane < (uint32_t)LB_D) {
-        uint64_t v = 0;
-#pragma unroll
-        for (int d = 0; d < LB_D; ++d) if (lane == (uint32_t)d) v = m[d];
-        mask[(size_t)i * LB_D + lane] = v;
-    }
-}
-
-__global__ __launch_bounds__(LB_NT) void k_lv_blk(uint32_t n, const uint64_t *__restrict__ mask,
-                                                  const uint32_t *__restrict__ roff, const uint16_t *__restrict__ rdep,
-                                                  const uint32_t *__restrict__ order_exec, uint32_t *__restrict__ level,
-                                                  uint32_t *__restrict__ max_level, const uint32_t *__restrict__ err)
-{
-    if (*err) return;   // invalid graph: nothing was written (the host fails after the walk)
-    extern __shared__ __attribute__((aligned(16))) uint16_t lvl[];   // [npad]: level + 1 once published
-    __shared__ uint32_t done;                                        // blocks published (in order)
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const uint32_t nb = (n + 63) / 64;
-    if (tid == 0) done = 0;
-    __syncthreads();
-    uint32_t my_max = 0;
-#ifdef ACC_LV_PROF
-    unsigned long long pr[6] = {};   // masks+residual, fold waits, fold loops, near loop, publish wait, blocks
-    unsigned long long tq = clock64();
-#define LB_T(k) do { const unsigned long long t_ = clock64(); pr[k] += t_ - tq; tq = t_; } while (0)
-#else
-#define LB_T(k) ((void)0)
-#endif
-    for (uint32_t b = wave; b < nb; b += LB_W) {
-        const uint32_t i = b * 64 + lane;
-        const bool valid = i < n;
-        uint64_t mk[LB_D];
-#pragma unroll
-        for (int d = 0; d < LB_D; ++d) mk[d] = valid ? mask[(size_t)i * LB_D + d] : 0ull;
-        uint32_t m = 0;
-        // residual deps: more than LB_D - 1 blocks back, published before this wave's previous block (b - LB_W) was
-        if (valid) {
-            static_assert(LB_W <= LB_D, "residual deps must lie in blocks this wave has seen published");
-            const uint32_t r0 = roff[i], r1 = roff[i + 1];
-            for (uint32_t e = r0; e < r1; ++e) m = max(m, (uint32_t)lvl[rdep[e]]);
-        }
-        LB_T(0);
-        // blocks b - LB_D + 1 .. b - 1, oldest first, each once it is published
-#pragma unroll
-        for (int d = LB_D - 1; d >= 1; --d) {
-            if (b < (uint32_t)d) continue;
-            uint64_t mu = mk[d];
-#pragma unroll
-            for (int x = 1; x < 64; x <<= 1) mu |= __shfl_xor(mu, x, 64);
-            if (!mu) continue;
-            const uint32_t pb = b - (uint32_t)d;
-            if (pb + LB_W > b)   // (blocks <= b - LB_W were published before this wave's previous block was)
-                while (*(volatile uint32_t *)&done <= pb) __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            LB_T(1);
-            const uint32_t pl = (uint32_t)*(volatile uint16_t *)&lvl[pb * 64 + lane];
-            for (uint64_t r = mu; r; r &= r - 1) {   // wave-uniform
-                const int k = __builtin_ctzll(r);
-                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pl, k);
-                if ((mk[d] >> k) & 1ull) m = max(m, v);
-            }
-            LB_T(2);
-        }
-        // the near chain, in lane order (every dep is an earlier lane)
-        uint64_t nu = mk[0];
-#pragma unroll
-        for (int x = 1; x < 64; x <<= 1) nu |= __shfl_xor(nu, x, 64);
-        for (uint64_t r = nu; r; r &= r - 1) {       // wave-uniform; lane k is final when step k comes
-            const int k = __builtin_ctzll(r);
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)m, k) + 1u;
-            if ((mk[0] >> k) & 1ull) m = max(m, v);
-        }
-        LB_T(3);
-        // m = level (max over deps of level + 1, 0 without deps); publish level + 1, then the block count
-        if (valid) {
-            lvl[i] = (uint16_t)(m + 1);
-            my_max = max(my_max, m);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        if (b > 0)   // blocks publish in order: wait for b - 1's count before moving it to b + 1
-            while (*(volatile uint32_t *)&done < b) __builtin_amdgcn_s_sleep(1);
-        if (lane == 0) *(volatile uint32_t *)&done = b + 1;
-        LB_T(4);
-#ifdef ACC_LV_PROF
-        ++pr[5];
-#endif
-    }
-#ifdef ACC_LV_PROF
-    if (lane == 0)
-        for (int k = 0; k < 6; ++k) g_lv_prof[6 * wave + k] = pr[k];
-#endif
-#undef LB_T
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += LB_NT) level[order_exec[i]] = (uint32_t)lvl[i] - 1u;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor(my_max, d, 64));
-    if (lane == 0 && my_max) atomicMax(max_level, my_max);
-}
-
 // ---- windowed tier (default): the exec order cut into windows of LW positions. A dep of position i is "far" when it
 // lies two or more windows back, "prev" when it lies in the window before i's, "cur" in i's own window. One launch per
 // window w: block 0 walks window w with one lane per position, the window's levels and its cur lists (u16 window
@@ -799,20 +626,18 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     // chunk slots beside the levels; acc_opts.lv_chunk caps it)
     const uint32_t npad = (n + 7u) & ~7u;
     uint32_t ch = 0;
-    // tiers: the whole-graph LDS walk (n <= 65535: config 5 0.89 ms), the windowed walk beyond (the 1M-txn chain
-    // graph: 0.264 us per level); acc_opts.lv_tier forces one (ACC_LV_BLOCKS: the block walk; ACC_LV_WAVES: the
-    // persistent-wave walk)
+    // tiers: the whole-graph LDS walk (n <= 65535: config 5 0.89 ms, the windowed walk 1.07), the windowed walk beyond
+    // (the 1M-txn chain graph: 0.264 us per level); acc_opts.lv_tier forces one (ACC_LV_WAVES: the persistent-wave walk)
     const uint32_t tier = ctx->opts.lv_tier;
-    if (tier > ACC_LV_BLOCKS) fail(ACC_E_ARG, "acc_opts.lv_tier: unknown levelise tier");
-    const bool blocks = n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && tier == ACC_LV_BLOCKS;
+    if (tier > ACC_LV_WAVES) fail(ACC_E_ARG, "acc_opts.lv_tier: unknown levelise tier");
     const bool windowed = tier == ACC_LV_WINDOWED || (tier == ACC_LV_AUTO && n > LV_LDS_MAX_N);
-    if (!windowed && !blocks && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && tier != ACC_LV_WAVES) {
+    if (!windowed && n <= LV_LDS_MAX_N && E < 0xFFFFFFFFull && tier != ACC_LV_WAVES) {
         const uint32_t room = ((uint32_t)LV_LDS - npad) / 3u;
         uint32_t cap = std::min<uint32_t>(room, LV_CH_MAX);
         if (ctx->opts.lv_chunk) cap = std::min<uint32_t>(cap, ctx->opts.lv_chunk);
         ch = cap >= 64 ? 1u << (31 - __builtin_clz(cap)) : 0u;   // largest power of two <= cap
     }
-    if (!ch && !windowed && !blocks) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
+    if (!ch && !windowed) launch(ctx, "lv_check", k_lv_check, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, off, dep, err);
     uint64_t *key = ctx->get<uint64_t>("lv_key", n);
     launch(ctx, "lv_keys", k_lv_keys, dim3(grid_for(n, BLOCK)), dim3(BLOCK), 0, n, exec_rank, key);
     Sorted se = radix_sort(ctx, "lv_rs_exec", key, nullptr, n, 32);
@@ -827,40 +652,7 @@ void levelise(acc_ctx *ctx, const acc_graph_in *in, uint32_t *level_out, uint32_
     uint32_t *level = ctx->get<uint32_t>("lv_level", n);
     uint32_t *maxl = ctx->get<uint32_t>("lv_max", 4);   // [0] max level, [1] ticket counter
     ACC_HIP(hipMemsetAsync(maxl, 0, 16, st));
-    if (blocks) {
-        uint32_t *rcnt = ctx->get<uint32_t>("lv_rcnt", n);
-        uint32_t *roff = ctx->get<uint32_t>("lv_roff", (size_t)n + 1);
-        const unsigned gw = (n + WAVES - 1) / WAVES;
-        launch(ctx, "lv_fcount", k_lv_bcount, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
-               (const uint32_t *)pos, rcnt, err);
-        scan<uint32_t, OpAdd<uint32_t>>(ctx, rcnt, roff, n, true, roff + n);
-        // (residual lists sized by the unfiltered E: their sum stays on the device)
-        uint16_t *rdep = ctx->get<uint16_t>("lv_rdep", std::max<uint64_t>(E, 1));
-        uint64_t *mask = ctx->get<uint64_t>("lv_mask", (size_t)n * LB_D);
-        launch(ctx, "lv_fwrite", k_lv_bwrite, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,
-               (const uint32_t *)pos, (const uint32_t *)roff, rdep, mask, (const uint32_t *)err);
-#ifdef ACC_LV_PROF
-        unsigned long long *pbk = ctx->get<unsigned long long>("lv_prof", 6 * LB_W);
-        ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lv_prof), &pbk, sizeof pbk, 0, hipMemcpyHostToDevice, st));
-#endif
-        // (levels up to 128 KiB of LDS: above the default dynamic limit)
-        ACC_HIP(hipFuncSetAttribute((const void *)k_lv_blk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(npad * 2)));
-        launch(ctx, "lv_walk_blocks", k_lv_blk, dim3(1), dim3(LB_NT), (size_t)npad * 2, n, (const uint64_t *)mask,
-               (const uint32_t *)roff, (const uint16_t *)rdep, (const uint32_t *)order_exec, level, maxl, (const uint32_t *)err);
-#ifdef ACC_LV_PROF
-        {
-            std::vector<unsigned long long> h(6 * LB_W);
-            ACC_HIP(hipMemcpyAsync(h.data(), pbk, h.size() * 8, hipMemcpyDeviceToHost, st));
-            ACC_HIP(hipStreamSynchronize(st));
-            double a[6] = {};
-            for (int w = 0; w < LB_W; ++w) for (int k = 0; k < 6; ++k) a[k] += (double)h[6 * w + k];
-            const double nbk = a[5] > 0 ? a[5] : 1;
-            fprintf(stderr, "[lb_prof] per block cycles: masks+residual %.0f fold-wait %.0f fold-loops %.0f near %.0f publish-wait %.0f (blocks %.0f)\n",
-                    a[0] / nbk, a[1] / nbk, a[2] / nbk, a[3] / nbk, a[4] / nbk, a[5]);
-        }
-#endif
-        ctx->stat("levelise.lds_tier", 3);
-    } else if (windowed) {
+    if (windowed) {
         uint64_t *cf = ctx->get<uint64_t>("lw_cf", n), *cp = ctx->get<uint64_t>("lw_cp", n), *cc = ctx->get<uint64_t>("lw_cc", n);
         const unsigned gw = (n + WAVES - 1) / WAVES;
         launch(ctx, "lv_fcount", k_lw_count, dim3(gw), dim3(BLOCK), 0, n, (const uint32_t *)order_exec, off, dep, exec_rank,

@@ -116,7 +116,6 @@ typedef struct acc_rlist {
 #define ACC_LV_LDS_WALK 1u
 #define ACC_LV_WINDOWED 2u
 #define ACC_LV_WAVES    3u
-#define ACC_LV_BLOCKS   4u
 
 typedef struct acc_ctx acc_ctx;
 

@@ -173,16 +173,11 @@ def test_levelise_one_million(ctx):
 
 
 @pytest.mark.parametrize("tier,chunk,n,max_deps,stat", [
-    ("auto", 0, 2000, 300, 1),             # LDS walk (the default up to 65,535 txns)
-    ("blocks", 0, 2000, 300, 3),           # block walk
-    ("blocks", 0, 63, 40, 3),              # one partial block
-    ("blocks", 0, 130, 200, 3),            # three blocks, long lists (every class)
-    ("blocks", 0, 20000, 12, 3),           # the block walk, many waves' rounds
-    ("blocks", 0, 65535, 6, 3),            # largest block-walk graph (u16 levels and positions, 128 KiB of LDS)
-    ("lds", 0, 2000, 300, 1),              # LDS walk, default chunks
-    ("lds", 64, 2000, 300, 1),             # LDS walk, 64-entry chunks: long lists read from HBM
+    ("auto", 0, 2000, 300, 1),             # LDS walk (default below 4,096 txns), default chunks
+    ("auto", 64, 2000, 300, 1),            # LDS walk, 64-entry chunks: long lists read from HBM
     ("lds", 256, 20000, 12, 1),            # many rounds, rounds of > 2048 positions
     ("lds", 0, 65535, 6, 1),               # largest LDS-walk graph (u16 levels and positions)
+    ("auto", 0, 20000, 12, 1),             # the LDS walk up to 65,535 txns
     ("auto", 0, 65536, 6, 2),              # beyond the LDS tiers: one launch per window
     ("windowed", 0, 2000, 300, 2),         # windowed walk, pending-set walk: two windows
     ("windowed", 0, 5000, 30, 2),          # far deps gathered for windows 2..4
@@ -204,10 +199,10 @@ def test_levelise_tiers(ctx, tier, chunk, n, max_deps, stat):
     assert nl == nl2
 
 
-@pytest.mark.parametrize("walk", ["windowed", "lds", "waves", "blocks"])
+@pytest.mark.parametrize("walk", ["windowed", "lds", "waves"])
 def test_levelise_config5_graph_both_tiers(ctx, walk):
     """A config-5-shaped merged graph (16,384 txns, deps on recent txns, hundreds of levels) through the windowed walk,
-    the LDS walk, the persistent-wave walk and the block walk: identical levels and order, equal to the oracle."""
+    the LDS walk and the persistent-wave walk: identical levels and order, equal to the oracle."""
     import oracle
     from accord_amd.deps import levelise
     rng = np.random.RandomState(55)
@@ -225,7 +220,7 @@ def test_levelise_config5_graph_both_tiers(ctx, walk):
     dep = np.concatenate(deps).astype(np.uint32)
     with tier_ctx(ctx, walk) as c:
         lv, order, nl = levelise(c, off, dep, er)
-        assert c.stats().get("levelise.lds_tier") == {"windowed": 2, "lds": 1, "waves": 0, "blocks": 3}[walk]
+        assert c.stats().get("levelise.lds_tier") == {"windowed": 2, "lds": 1, "waves": 0}[walk]
     l2, o2, nl2 = oracle.levelise(off, dep, er)
     np.testing.assert_array_equal(lv, l2)
     np.testing.assert_array_equal(order, o2)

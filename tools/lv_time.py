@@ -1,5 +1,5 @@
 """Time acc_levelise on the 1M-txn test graph (tests/test_levelise_gpu.py::test_levelise_one_million) per tier:
-python tools/lv_time.py [auto|lds|windowed|waves|blocks]  (the walk, as acc_opts.lv_tier)."""
+python tools/lv_time.py [auto|lds|windowed|waves]  (the walk, as acc_opts.lv_tier)."""
 import os
 import sys
 import time
