@@ -1196,11 +1196,14 @@ __global__ __launch_bounds__(BLOCK) void k_ch_entries(uint32_t ng, uint32_t nh, 
     if (g <= nh) eoff[g] = g == nh ? ne : pexcl[gofs[g]];
 }
 // entries still uncommitted (missing[] candidates), and each hot key's first one
+// newonly: only the entries new in this batch (the TxnIds a snapshot entry's missing[] may gain)
 __global__ __launch_bounds__(BLOCK) void k_ch_uflag(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
-                                                    uint32_t *__restrict__ uflag)
+                                                    int newonly, uint32_t *__restrict__ uflag)
 {
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e < ne) uflag[e] = G[eg[e]].st < COMMITTED ? 1u : 0u;
+    if (e >= ne) return;
+    const HG &g = G[eg[e]];
+    uflag[e] = g.st < COMMITTED && (!newonly || (g.flags & HF_NEW)) ? 1u : 0u;
 }
 struct UR {   // an uncommitted entry, as the missing[] walks read it
     uint64_t m, l;
@@ -1340,28 +1343,35 @@ __device__ __forceinline__ bool xs_has(const XSet &xs, uint32_t h, const Ts &t)
     }
 }
 
+struct NewList {   // per hot key, its uncommitted entries new in this batch
+    const UR *list;
+    const uint32_t *off;
+};
+__device__ __forceinline__ uint32_t ur_lower(const UR *__restrict__ l, uint32_t lo, uint32_t hi, const Ts &t)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cmp(Ts{ l[mid].m, l[mid].l, l[mid].n }, t) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
 __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
                                                const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u, Snap s,
-                                               const XSet &xs, uint64_t *om, uint64_t *ol, int32_t *on)
+                                               const XSet &xs, const NewList &nl, uint64_t *om, uint64_t *ol, int32_t *on)
 {
     const HG X = G[eg[e]];
     if (!has_info(X.st)) return 0;
     const Ts id = hg_id(X), bound = hg_bound(X);
     const uint32_t wm = witnesses_mask(kind(id));
-    const uint32_t h = X.h, u0 = uoff[h], u1 = uoff[h + 1];
-    uint32_t lo = u0, hi = u1;   // uncommitted entries below the bound: [u0, ub)
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (cmp(Ts{ ulist[mid].m, ulist[mid].l, ulist[mid].n }, bound) < 0) lo = mid + 1; else hi = mid;
-    }
-    const uint32_t ub = lo;
+    const uint32_t h = X.h;
     uint32_t n = 0;
     auto put = [&](const UR &t) {
         if (om) { om[n] = t.m; ol[n] = t.l; on[n] = t.n; }
         ++n;
     };
     if (X.info_q != NONE) {   // computed in this batch: the uncommitted entries below the bound, less its deps
+        const uint32_t u0 = uoff[h], ub = ur_lower(ulist, u0, uoff[h + 1], bound);
         const UpdRec r = urec[X.info_q];
         uint32_t d = r.da;
         for (uint32_t k = u0; k < ub; ++k) {
@@ -1375,14 +1385,18 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
         return n;
     }
     if (X.snap_x == NONE) return 0;
-    // the snapshot's missing[] (less the TxnIds committed in this batch) merged with the new uncommitted entries
+    // the snapshot's missing[] (less the TxnIds committed in this batch) merged with the new uncommitted entries below
+    // the bound (a list of the new ones only: walking every uncommitted entry of a hot key per snapshot entry was the
+    // cost)
     const uint32_t m0 = s.miss_off[X.snap_x], m1 = s.miss_off[X.snap_x + 1];
-    uint32_t a = m0, k = u0;
+    const uint32_t ub = ur_lower(nl.list, nl.off[h], nl.off[h + 1], bound);
+    uint32_t a = m0, k = nl.off[h];
+    const UR *ulist_n = nl.list;
     auto next_new = [&]() {
         while (k < ub) {
-            const UR &t = ulist[k];
+            const UR &t = ulist_n[k];
             const Ts tid{ t.m, t.l, t.n };
-            if ((t.flags & HF_NEW) && cmp(tid, id) != 0 && ((wm >> kind(tid)) & 1u)) return;
+            if (cmp(tid, id) != 0 && ((wm >> kind(tid)) & 1u)) return;
             ++k;
         }
     };
@@ -1395,14 +1409,14 @@ __device__ __forceinline__ uint32_t ch_missing(uint32_t e, const uint32_t *__res
         int c;
         if (a == m1) c = 1;
         else if (k == ub) c = -1;
-        else c = cmp(Ts{ s.mm[a], s.ml[a], s.mn[a] }, Ts{ ulist[k].m, ulist[k].l, ulist[k].n });
+        else c = cmp(Ts{ s.mm[a], s.ml[a], s.mn[a] }, Ts{ ulist_n[k].m, ulist_n[k].l, ulist_n[k].n });
         if (c <= 0) {
             if (om) { om[n] = s.mm[a]; ol[n] = s.ml[a]; on[n] = s.mn[a]; }
             ++n;
             ++a;
             if (c == 0) ++k;
         } else {
-            put(ulist[k]);
+            put(ulist_n[k]);
             ++k;
         }
         next_new();
@@ -1418,13 +1432,14 @@ template <bool EMIT>
 __global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *__restrict__ eg, const HG *__restrict__ G,
                                                    const uint32_t *__restrict__ eoff, const UR *__restrict__ ulist,
                                                    const uint32_t *__restrict__ uoff, const UpdRec *__restrict__ urec, Upd u,
-                                                   Snap s, XSet xs, uint32_t *__restrict__ mcnt, const uint32_t *__restrict__ moff,
-                                                   uint64_t *__restrict__ mm, uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
+                                                   Snap s, XSet xs, NewList nl, uint32_t *__restrict__ mcnt,
+                                                   const uint32_t *__restrict__ moff, uint64_t *__restrict__ mm,
+                                                   uint64_t *__restrict__ ml, int32_t *__restrict__ mn)
 {
     const uint32_t e = blockIdx.x * BLOCK + threadIdx.x, lane = lane_id();
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    bool lng = false;
-    uint32_t u0 = 0, ub = 0, da = 0, db = 0, wm = 0, out = 0;
+    bool lng = false, lsn = false;
+    uint32_t u0 = 0, ub = 0, da = 0, db = 0, wm = 0, out = 0, h = 0;
     Ts id{ 0, 0, 0 };
     if (e < ne) {
         const HG X = G[eg[e]];
@@ -1432,21 +1447,26 @@ __global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *
             id = hg_id(X);
             const Ts bound = hg_bound(X);
             u0 = uoff[X.h];
-            uint32_t lo = u0, hi = uoff[X.h + 1];
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (cmp(Ts{ ulist[mid].m, ulist[mid].l, ulist[mid].n }, bound) < 0) lo = mid + 1; else hi = mid;
-            }
-            ub = lo;
+            ub = ur_lower(ulist, u0, uoff[X.h + 1], bound);
             lng = ub - u0 >= CH_LONG;
             const UpdRec r = urec[X.info_q];
             da = r.da; db = r.db;
             wm = witnesses_mask(kind(id));
             if (EMIT) out = moff[e];
+        } else if (has_info(X.st) && X.snap_x != NONE) {
+            // a snapshot entry with a long missing[] and no new uncommitted TxnId below its bound (an old entry of a hot
+            // key): its list less the crossed TxnIds, filtered by the whole wave
+            const uint32_t m0 = s.miss_off[X.snap_x], m1 = s.miss_off[X.snap_x + 1];
+            const uint32_t n0 = nl.off[X.h];
+            if (m1 - m0 >= CH_LONG && ur_lower(nl.list, n0, nl.off[X.h + 1], hg_bound(X)) == n0) {
+                lsn = true;
+                u0 = m0; ub = m1; h = X.h;
+                if (EMIT) out = moff[e];
+            }
         }
-        if (!lng) {
-            if (EMIT) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, mm + moff[e], ml + moff[e], mn + moff[e]);
-            else mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, nullptr, nullptr, nullptr);
+        if (!lng && !lsn) {
+            if (EMIT) ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, nl, mm + moff[e], ml + moff[e], mn + moff[e]);
+            else mcnt[e] = ch_missing(e, eg, G, eoff, ulist, uoff, urec, u, s, xs, nl, nullptr, nullptr, nullptr);
         }
     }
     for (uint64_t todo = __ballot(lng); todo; todo &= todo - 1) {
@@ -1472,6 +1492,27 @@ __global__ __launch_bounds__(BLOCK) void k_ch_miss(uint32_t ne, const uint32_t *
                     }
                     if (lo < d1 && cmp(Ts{ u.dm[lo], u.dl[lo], u.dn[lo] }, tid) == 0) keep = false;
                 }
+            }
+            const uint64_t kb = __ballot(keep);
+            if (EMIT && keep) {
+                const uint32_t q = o0 + n + (uint32_t)__popcll(kb & lt);
+                mm[q] = t.m; ml[q] = t.l; mn[q] = t.n;
+            }
+            n += (uint32_t)__popcll(kb);
+        }
+        if (!EMIT && lane == (uint32_t)src) mcnt[e] = n;
+    }
+    for (uint64_t todo = __ballot(lsn); todo; todo &= todo - 1) {
+        const int src = __builtin_ctzll(todo);
+        const uint32_t a = __shfl(u0, src, 64), z = __shfl(ub, src, 64), hk = __shfl(h, src, 64), o0 = __shfl(out, src, 64);
+        uint32_t n = 0;
+        for (uint32_t base = a; base < z; base += 64) {
+            const uint32_t j = base + lane;
+            bool keep = false;
+            Ts t{ 0, 0, 0 };
+            if (j < z) {
+                t = Ts{ s.mm[j], s.ml[j], s.mn[j] };
+                keep = !xs_has(xs, hk, t);
             }
             const uint64_t kb = __ballot(keep);
             if (EMIT && keep) {
@@ -1652,13 +1693,22 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     if (ni) return false;
     // the uncommitted entries per hot key, then every entry's missing[]
     uint32_t *uf = ctx->get<uint32_t>("ch_uf", std::max<uint32_t>(ne, 1)), *ux = ctx->get<uint32_t>("ch_ux", (size_t)ne + 1);
-    launch(ctx, "ch_uflag", k_ch_uflag, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G, uf);
+    launch(ctx, "ch_uflag", k_ch_uflag, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G, 0, uf);
     scan<uint32_t, OpAdd<uint32_t>>(ctx, uf, ux, ne, true, ux + ne);
     const uint32_t nu = read32(ux + ne);
     UR *ulist = ctx->get<UR>("ch_ulist", std::max<uint32_t>(nu, 1));
     uint32_t *uoff = ctx->get<uint32_t>("ch_uoff", (size_t)nh + 1);
     launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nu,
            (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, (const uint32_t *)eg, (const HG *)G, ulist, uoff);
+    // the same for the uncommitted entries new in this batch
+    launch(ctx, "ch_uflag", k_ch_uflag, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G, 1, uf);
+    scan<uint32_t, OpAdd<uint32_t>>(ctx, uf, ux, ne, true, ux + ne);
+    const uint32_t nun = read32(ux + ne);
+    UR *ulist_n = ctx->get<UR>("ch_ulist_n", std::max<uint32_t>(nun, 1));
+    uint32_t *uoff_n = ctx->get<uint32_t>("ch_uoff_n", (size_t)nh + 1);
+    launch(ctx, "ch_ulist", k_ch_ulist, dim3(grid_for(std::max<uint64_t>(ne, (uint64_t)nh + 1), BLOCK)), dim3(BLOCK), 0, ne, nh, nun,
+           (const uint32_t *)uf, (const uint32_t *)ux, (const uint32_t *)eoff, (const uint32_t *)eg, (const HG *)G, ulist_n, uoff_n);
+    const NewList nl{ ulist_n, uoff_n };
     // the groups that crossed to committed in this batch, as a hash set
     XSet xs{ nullptr, 0 };
     {
@@ -1677,7 +1727,7 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     }
     uint32_t *mcnt = ctx->get<uint32_t>("ch_mcnt", std::max<uint32_t>(ne, 1)), *moff = ctx->get<uint32_t>("ch_moff", (size_t)ne + 1);
     launch(ctx, "ch_mcount", k_ch_miss<false>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, mcnt, (const uint32_t *)nullptr,
+           (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, nl, mcnt, (const uint32_t *)nullptr,
            (uint64_t *)nullptr, (uint64_t *)nullptr, (int32_t *)nullptr);
     uint64_t *nm64 = ctx->get<uint64_t>("ch_nm64", 1);
     sum_u32(ctx, mcnt, ne, nm64);   // the u32 offsets below must not wrap
@@ -1690,7 +1740,7 @@ static bool hot_keys(acc_ctx *ctx, uint32_t nkeys, uint8_t *hot, const uint32_t 
     int32_t *mn = ctx->get<int32_t>("ch_mn", nm);
     if (nm)
         launch(ctx, "ch_memit", k_ch_miss<true>, dim3(grid_for(ne, BLOCK)), dim3(BLOCK), 0, ne, (const uint32_t *)eg, (const HG *)G,
-               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, (uint32_t *)nullptr,
+               (const uint32_t *)eoff, (const UR *)ulist, (const uint32_t *)uoff, urec, u, s, xs, nl, (uint32_t *)nullptr,
                (const uint32_t *)moff, mm, ml, mn);
     ctx->stat("cfk.hot_keys", nh);
     ctx->stat("cfk.hot_items", NI);

@@ -2043,6 +2043,50 @@ __global__ __launch_bounds__(NT) void k_v2_write_big(const uint32_t *__restrict_
 // the union: O(E + keys * span / 32) work instead of a merge sort. Entries below base (a cold key's last committed
 // Write far back) go to a short sorted list that precedes the bitmap span. A txn whose list overflows is passed on to
 // the sorting tier (k_v2_write_big<BIG_E>).
+// One wave sorts buf[0, 64 R) ascending with R entries per lane in registers (element r * 64 + lane; positions >=
+// n_valid read as all-ones pads): partners closer than 64 are lanes (shuffles), the others registers of the same lane.
+template <int R>
+__device__ __forceinline__ void wave_reg_sort_u32(uint32_t *buf, uint32_t n_valid)
+{
+    const uint32_t lane = lane_id();
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = (uint32_t)r * 64 + lane;
+        v[r] = i < n_valid ? buf[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t k = 2; k <= 64u * R; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            if (jj >= 64) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int r2 = r ^ (int)(jj / 64);
+                    if (r2 > r) {
+                        const bool up = (((uint32_t)r * 64 + lane) & k) == 0;
+                        const uint32_t a = v[r], b = v[r2];
+                        if ((a > b) == up) { v[r] = b; v[r2] = a; }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t y = (uint32_t)__shfl_xor((int)v[r], (int)jj, 64);
+                    const bool up = (((uint32_t)r * 64 + lane) & k) == 0, lower = (lane & jj) == 0;
+                    const uint32_t lo = min(v[r], y), hi = max(v[r], y);
+                    v[r] = (lower == up) ? lo : hi;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = (uint32_t)r * 64 + lane;
+        if (i < n_valid) buf[i] = v[r];
+    }
+}
+
 constexpr uint32_t WIN_W = 512;      // bitmap words per key: 16384 ranks below S
 constexpr uint32_t WIN_OUT = 1024;   // entries below the span
 
@@ -2057,6 +2101,14 @@ struct WinLds {
     uint32_t n_out, kept, d_out, bad, minr;
 };
 
+#ifdef ACC_PHASE_PROF
+// tuning build only: per workgroup of the window tier, summed over its txns: cycles in runs + span low end, bitmap gather,
+// below-span sort, prefix popcounts, the span's writes, rank -> TxnId; then txns, entries, span words, entries below
+__device__ unsigned long long *g_win_prof;
+#define WN_PH(k) do { if (tid == 0) { const unsigned long long t_ = clock64(); wp[k] += t_ - wq; wq = t_; } } while (0)
+#else
+#define WN_PH(k) ((void)0)
+#endif
 template <int WK>
 __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restrict__ list, const uint64_t *__restrict__ cnt_dev,
                                                        V2View v, const uint64_t *__restrict__ cnt, V2Out o)
@@ -2065,7 +2117,11 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
     const uint32_t n_list = (uint32_t)*cnt_dev;
     RunsT<WK> &R = L.R;
+#ifdef ACC_PHASE_PROF
+    unsigned long long wp[10] = {}, wq = clock64();
+#endif
     for (uint32_t b = blockIdx.x; b < n_list; b += gridDim.x) {
+        WN_PH(9);
         const uint32_t t = list[b];
         const TxnCtx c = txn_ctx(v, o, t);
         const uint32_t S = v.tinfo[t].y;
@@ -2098,8 +2154,12 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
         }
         __syncthreads();
         const uint32_t lo_span = S > WIN_W * 32 ? S - WIN_W * 32 : 0u;
-        const uint32_t base = max(lo_span, min(L.minr, S));
-        const uint32_t nw = (S - base + 31) / 32;
+        uint32_t base = max(lo_span, min(L.minr, S));
+        uint32_t nw = (S - base + 31) / 32;
+        // a sparse span (fewer than one entry per 16 ranks: deps on old commands far below S) is all overhead, the
+        // (nk + 1) bitmaps zeroed, scanned and walked word by word: every entry goes to the sorted list instead
+        if (c.E <= WIN_OUT && (uint64_t)nw * 32 > 16ull * c.E) { base = S; nw = 0; }
+        WN_PH(0);
         for (uint32_t i = tid; i < c.nk * nw; i += BLOCK) L.bm[i / nw][i % nw] = 0;
         __syncthreads();
         const uint32_t total = R.total;
@@ -2144,6 +2204,10 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             continue;
         }
         const uint32_t n_out = L.n_out;
+        WN_PH(1);
+#ifdef ACC_PHASE_PROF
+        if (tid == 0) { wp[6] += 1; wp[7] += c.E; wp[8] += (uint64_t)nw << 32 | min(n_out, 0xFFFFFFFFu); }
+#endif
         if (n_out > WIN_OUT) {   // too many entries below the span: the sorting tier
             if (tid == 0) {
                 const uint32_t f = (uint32_t)atomicAdd((unsigned long long *)&o.gstat[1], 1ull);
@@ -2158,15 +2222,21 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             for (uint32_t k = 0; k < c.nk; ++k) u |= L.bm[k][w];
             L.un[w] = u;
         }
-        // ---- the entries below the span, sorted (rank, key)
+        // ---- the entries below the span, sorted (rank, key): one wave in registers up to 512 (no block barriers), the
+        // block's LDS bitonic beyond
         if (n_out > 1) {
-            uint32_t n2 = 64;
-            while (n2 < n_out) n2 <<= 1;
-            for (uint32_t q = n_out + tid; q < n2; q += BLOCK) L.out[q] = 0xFFFFFFFFu;
-            __syncthreads();
-            block_bitonic<uint32_t, BLOCK>(L.out, n2);
+            if (n_out <= 128) { if (wave == 0) wave_reg_sort_u32<2>(L.out, n_out); }
+            else if (n_out <= 512) { if (wave == 0) wave_reg_sort_u32<8>(L.out, n_out); }
+            else {
+                uint32_t n2 = 64;
+                while (n2 < n_out) n2 <<= 1;
+                for (uint32_t q = n_out + tid; q < n2; q += BLOCK) L.out[q] = 0xFFFFFFFFu;
+                __syncthreads();
+                block_bitonic<uint32_t, BLOCK>(L.out, n2);
+            }
         }
         __syncthreads();
+        WN_PH(2);
         // ---- exclusive prefix popcounts of every series (keys 0..nk-1, union = nk): a wave per series, 8 words a lane
         for (uint32_t s = wave; s <= c.nk; s += WAVES) {
             const uint32_t *words = s < c.nk ? L.bm[s] : L.un;
@@ -2184,6 +2254,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             }
             if (lane == 0) L.ser_tot[s] = run;
         }
+        WN_PH(3);
         const uint64_t abase = o.arena_off[t] + (o.cnz[c.j1] - o.cnz[c.j0]);
         uint32_t *dsc = o.dep_scratch + c.e0;
         // ---- the sorted entries below the span (one wave): distinct TxnIds first in the union, each key's first slots
@@ -2249,6 +2320,7 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
             }
         }
         __syncthreads();   // the block's rank writes are visible to the block
+        WN_PH(4);
         for (uint32_t i0 = d_out + tid; i0 < d_out + nu; i0 += 4 * BLOCK) {
             uint32_t r[4];
 #pragma unroll
@@ -2260,8 +2332,14 @@ __global__ __launch_bounds__(BLOCK) void k_v2_write_win(const uint32_t *__restri
         }
         if (tid == 0) o.u_cnt[t] = d_out + nu;
         __syncthreads();
+        WN_PH(5);
     }
+#ifdef ACC_PHASE_PROF
+    if (tid == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_win_prof[k], wp[k]);
+#endif
 }
+#undef WN_PH
 
 // ---- global path for txns beyond the wave path: gather to global, two radix sorts
 
@@ -3661,6 +3739,13 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
         ctx->fork(nrun ? 2 : 1);
         ctx->launch_stream = ctx->aux[0];
         if (win_ok) {
+#ifdef ACC_PHASE_PROF
+            {
+                unsigned long long *wpb = ctx->get<unsigned long long>("v2_win_prof", 10);
+                ACC_HIP(hipMemsetAsync(wpb, 0, 80, ctx->aux[0]));
+                ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_win_prof), &wpb, sizeof wpb, 0, hipMemcpyHostToDevice, ctx->aux[0]));
+            }
+#endif
             // the window tier takes every big txn of <= 16 keys; the sorting tiers run after the next host sync, only
             // when it passed txns on or some txn has more keys (no launch without work)
             launch(ctx, "v2_write_win", k_v2_write_win<8>, dim3(std::min<unsigned>(nbig, 2048)), dim3(BLOCK), 0,
@@ -3732,6 +3817,18 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
 #endif
     }
     if (nbig || nrun) ctx->join(nrun ? 2 : 1);
+#ifdef ACC_PHASE_PROF
+    if (nbig && win_ok) {
+        std::vector<unsigned long long> h(10);
+        ACC_HIP(hipMemcpyAsync(h.data(), ctx->get<unsigned long long>("v2_win_prof", 10), 80, hipMemcpyDeviceToHost, st));
+        ACC_HIP(hipStreamSynchronize(st));
+        const double nt = h[6] ? (double)h[6] : 1.0;
+        fprintf(stderr, "[win_phase] txns=%llu avg cycles per txn (thread 0 of each block): runs+lowend %.0f gather %.0f "
+                "below-sort %.0f prefix %.0f span-writes %.0f rank-map %.0f list-wait %.0f | avg E %.1f span words %.1f below %.1f\n",
+                h[6], h[0] / nt, h[1] / nt, h[2] / nt, h[3] / nt, h[4] / nt, h[5] / nt, h[9] / nt, h[7] / nt,
+                (double)(h[8] >> 32) / nt, (double)(h[8] & 0xFFFFFFFFull) / nt);
+    }
+#endif
     finish();
     if (ctx->pinned[5]) fail(ACC_E_STATE, "internal: stream gather count differs from the count pass");
     if (ctx->pinned[2]) fail(ACC_E_STATE, "internal: v2 gather count differs from the count pass");
