@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 
 # KeyDeps tiers launched on a side stream, concurrently with the stream pass (csrc/keydeps.hip keydeps_core)
 SIDE_STREAM_TAGS = {"v2_write_med", "v2_write_big", "v2_write_huge", "v2_write_medium", "v2_write_win", "v2_write_win16",
+                    "v3_stream_runs",
                     # RangeDeps build tiers on side streams beside the wave tier (csrc/rangedeps.hip rangedeps_batch)
                     "rd_build_s16", "rd_build_s32", "rd_build_block"}
 
@@ -51,6 +52,9 @@ TAG_KERNEL = {
     "v2_write_huge": "k_v2_write_big<16384,1024>",
     "v2_write_win": "k_v2_write_win<8>",
     "v2_write_win16": "k_v2_write_win<16>",
+    # the stream pass: k_v3_stream<EntT, NT, G, N2, LIST, RUNS> (lean pass / RUNS pass on a side stream; either EntT)
+    "v3_stream": ("k_v3_stream<", "false,false>"),
+    "v3_stream_runs": ("k_v3_stream<", "true,true>"),
     # the RangeDeps lane-group tiers: k_rd_build_seg<S, NARROW> (prefix: either sort width)
     "rd_build_s16": "k_rd_build_seg<16,",
     "rd_build_s32": "k_rd_build_seg<32,",
@@ -119,7 +123,9 @@ def roofline(step_bytes, step, steps, ms_per_step, config, variant="", profiled=
         # variants map to their instance, the others match on the base name
         kernels = prof.get("kernels", {})
         exact = TAG_KERNEL.get(dom_name)
-        if exact and exact in kernels:
+        if isinstance(exact, tuple):   # (prefix, suffix): one template instance whatever its leading arguments
+            ks = [v for name, v in kernels.items() if name.startswith(exact[0]) and name.endswith(exact[1])]
+        elif exact and exact in kernels:
             ks = [kernels[exact]]
         elif exact and exact.endswith((",", "<")):
             ks = [v for name, v in kernels.items() if name.startswith(exact)]
