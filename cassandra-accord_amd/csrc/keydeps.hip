@@ -1442,20 +1442,14 @@ __device__ __forceinline__ uint64_t v2_count_one(const V2View &v, uint32_t p, co
 
 // Also: bigflag[T] = 1 for txns with a run record (they take the v2 tiers, the rest the stream pass) and per-block
 // entry totals (blk_e) for the batch's E.
-#ifndef ACC_CT_PAIRS
-#define ACC_CT_PAIRS 1
-#endif
 __global__ __launch_bounds__(BLOCK) void k_v2_count(size_t P, V2View v, const uint32_t *__restrict__ owner,
                                                     RecOut ro, uint32_t *__restrict__ bigflag,
                                                     uint64_t *__restrict__ blk_e)
 {
     __shared__ uint64_t lds[WAVES];
+    const size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t e = 0;
-#pragma unroll
-    for (int u = 0; u < ACC_CT_PAIRS; ++u) {   // (pairs per thread: independent query chains in flight)
-        const size_t p = ((size_t)blockIdx.x * ACC_CT_PAIRS + (size_t)u) * BLOCK + threadIdx.x;
-        if (p < P) e += v2_count_one(v, (uint32_t)p, owner, ro, bigflag);
-    }
+    if (p < P) e = v2_count_one(v, (uint32_t)p, owner, ro, bigflag);
     uint64_t total;
     block_exclusive(e, OpAdd<uint64_t>(), lds, total);
     if (threadIdx.x == 0) blk_e[blockIdx.x] = total;
@@ -3614,8 +3608,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     ACC_HIP(hipMemsetAsync(ct_buf, 0, 8 * ct_rows * sizeof(unsigned long long), st));
     ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ct_prof), &ct_buf, sizeof ct_buf, 0, hipMemcpyHostToDevice, st));
 #endif
-    const unsigned gC = grid_for(P, (size_t)BLOCK * ACC_CT_PAIRS);   // count-pass workgroups (blk_e entries)
-    launch(ctx, "v2_count", k_v2_count, dim3(gC), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
+    launch(ctx, "v2_count", k_v2_count, dim3(gP), dim3(BLOCK), 0, P, vv, (const uint32_t *)owner, ro, bigflag, blk_e);
 #ifdef ACC_PHASE_PROF
     {
         std::vector<unsigned long long> h(8 * ct_rows);
@@ -3649,7 +3642,7 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
     {   // arena / key offsets, the count pass's per-block entry totals, the big txns' TxnId scratch bases: one launch
         const uint64_t *si[4] = { szA, szK, blk_e, eb };
         uint64_t *so[4] = { arena_off, kd_off, blk_pre, dB }, *stot[4] = { arena_off + n, kd_off + n, tot, dB + n };
-        const size_t sn[4] = { n, n, gC, n };
+        const size_t sn[4] = { n, n, gP, n };
         scan_multi<uint64_t, OpAdd<uint64_t>>(ctx, 4, si, so, sn, true, stot);
     }
     // the big-txn list in txn order (k_v3_bigfill's per-txn ranges abut: a big txn writes its end where the next
