@@ -3786,7 +3786,8 @@ static void keydeps_core(acc_ctx *ctx, const acc_batch_in *in, acc_keydeps_view 
 #endif
         if (nrun) {
             // the stream txns with a run record on side stream 1, concurrently with the lean pass below (their gathers
-            // kept out of the lean pass: registers and a wave-uniform loop in every wave for ~0.5% of the txns)
+            // kept out of the lean pass: registers and a wave-uniform loop in every wave that holds one; config 2: 25%
+            // of the txns)
             if (!nbig) ctx->fork(2);
             V3Stream sr = sp;
             sr.list = rlist; sr.n = nrun;
