@@ -2072,7 +2072,7 @@ __device__ __forceinline__ void wave_reg_sort_u32(uint32_t *buf, uint32_t n_vali
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const uint32_t y = (uint32_t)__shfl_xor((int)v[r], (int)jj, 64);
+                    const uint32_t y = xor_lanes(v[r], (int)jj);
                     const bool up = (((uint32_t)r * 64 + lane) & k) == 0, lower = (lane & jj) == 0;
                     const uint32_t lo = min(v[r], y), hi = max(v[r], y);
                     v[r] = (lower == up) ? lo : hi;
@@ -2671,8 +2671,7 @@ __device__ __forceinline__ uint32_t group_inclusive(uint32_t x, uint32_t sub)
 template <class T>
 __device__ __forceinline__ T gshfl_xor(T v, int m)
 {
-    if constexpr (sizeof(T) == 8) return shfl_xor64(v, m);
-    else return (T)__shfl_xor(v, m, 64);
+    return xor_lanes(v, m);   // (group_reg_sort runs in the whole wave: no lane of k_v3_stream returns early)
 }
 // Sorts buf[0, G * R) of a G-lane group ascending (positions >= n_valid read as all-ones pads) with R entries per lane
 // in registers, element i = r * G + sub: partners at distance < G are lanes of the group (shuffles), the others registers
@@ -2818,7 +2817,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     const uint64_t runmask = __ballot(sm && run) & gmask;
     uint32_t wnrun = RUNS ? (uint32_t)__popcll(runmask) : 0u;
 #pragma unroll
-    for (int d = G; d < 64; d <<= 1) wnrun = max(wnrun, (uint32_t)__shfl_xor(wnrun, d, 64));
+    for (int d = G; d < 64; d <<= 1) wnrun = max(wnrun, xor_lanes(wnrun, d));
     uint32_t cursor = E_in;
     uint64_t rem = runmask;
     for (uint32_t ri = 0; ri < wnrun; ++ri) {
@@ -2837,7 +2836,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         const uint32_t kj = (uint32_t)(src - (int)g0);
         uint32_t wr = raw;
 #pragma unroll
-        for (int d = G; d < 64; d <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, d, 64));
+        for (int d = G; d < 64; d <<= 1) wr = max(wr, xor_lanes(wr, d));
         for (uint32_t c0 = 0; c0 < wr; c0 += G) {
             const uint32_t off = c0 + sub;
             bool keep = false;
@@ -2875,7 +2874,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
     }
     uint32_t wE = ok ? E : 0;
 #pragma unroll
-    for (int d = G; d < 64; d <<= 1) wE = max(wE, (uint32_t)__shfl_xor(wE, d, 64));
+    for (int d = G; d < 64; d <<= 1) wE = max(wE, xor_lanes(wE, d));
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // ---- sort each group's entries: registers + shuffles up to 4 per lane (wave-uniform choice), LDS bitonic beyond
@@ -2889,7 +2888,7 @@ __global__ __launch_bounds__(NT, ACC_ST_WAVES * 64 / NT) void k_v3_stream(V3Stre
         for (uint32_t q = E + sub; q < n2; q += G) buf[q] = ~(EntT)0;
         uint32_t wn2 = n2;
 #pragma unroll
-        for (int d = G; d < 64; d <<= 1) wn2 = max(wn2, (uint32_t)__shfl_xor(wn2, d, 64));
+        for (int d = G; d < 64; d <<= 1) wn2 = max(wn2, xor_lanes(wn2, d));
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         for (uint32_t k = 2; k <= wn2; k <<= 1) {
@@ -4269,7 +4268,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_union_seg(const uint32_t *__restri
     for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
 #pragma unroll
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint64_t y = shfl_xor(x, (int)jj);
+            const uint64_t y = xor_lanes(x, (int)jj);
             const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;   // ascending per group
             const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
             x = (lower == up) ? mn : mx;
@@ -4311,7 +4310,7 @@ __device__ __forceinline__ void wave_reg_sort(uint64_t (&v)[R])
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const uint64_t y = shfl_xor(v[r], (int)jj);
+                    const uint64_t y = xor_lanes(v[r], (int)jj);
                     const bool up = ((((uint32_t)r << 6) | lane) & k) == 0, lower = (lane & jj) == 0;
                     const uint64_t mn = v[r] < y ? v[r] : y, mx = v[r] < y ? y : v[r];
                     v[r] = (lower == up) ? mn : mx;

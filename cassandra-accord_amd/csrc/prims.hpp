@@ -52,6 +52,47 @@ __device__ __forceinline__ T shfl_xor(T v, int m)
     }
 }
 
+// The value of lane (lane ^ m), m a power of two below 64 known at compile time (unrolled loops), without the LDS
+// round trip of ds_bpermute: xor 1 / 2 are quad permutes, xor 4 / 8 a row (half-)mirror followed by a quad or
+// half-mirror permute (i ^ 7 ^ 3 = i ^ 4, i ^ 15 ^ 7 = i ^ 8), xor 16 / 32 gfx950's v_permlane16/32_swap (each lane
+// takes the half the swap moved across). Every lane of the wave must be active: a DPP read of a disabled lane leaves
+// the `old` operand (0) instead of the value.
+__device__ __forceinline__ uint32_t xor_lanes_u32(uint32_t x, int m)
+{
+    switch (m) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    case 4: {
+        const int y = __builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);           // row_half_mirror
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, y, 0x1B, 0xF, 0xF, false);              // quad_perm [3,2,1,0]
+    }
+    case 8: {
+        const int y = __builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);           // row_mirror
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, y, 0x141, 0xF, 0xF, false);             // row_half_mirror
+    }
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (threadIdx.x & 16u) ? r[0] : r[1];
+    }
+    default: {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (threadIdx.x & 32u) ? r[0] : r[1];
+    }
+    }
+}
+
+template <class T>
+__device__ __forceinline__ T xor_lanes(T v, int m)
+{
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = xor_lanes_u32((uint32_t)u, m), hi = xor_lanes_u32((uint32_t)(u >> 32), m);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)xor_lanes_u32((uint32_t)v, m);
+    }
+}
+
 template <class T>
 struct OpAdd {
     __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
@@ -112,7 +153,7 @@ __device__ __forceinline__ T bitonic_reg(T x)
     for (uint32_t k = 2; k <= 64; k <<= 1) {
 #pragma unroll
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const T y = shfl_xor(x, (int)jj);
+            const T y = xor_lanes(x, (int)jj);   // (callers run the whole wave)
             const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
             const T mn = x < y ? x : y, mx = x < y ? y : x;
             x = (lower == up) ? mn : mx;

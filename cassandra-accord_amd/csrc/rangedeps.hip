@@ -737,7 +737,8 @@ __global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t 
 }
 
 
-// bitonic sort within lane groups of S (lane-aligned: the xor partners stay inside), ascending
+// bitonic sort within lane groups of S (lane-aligned: the xor partners stay inside), ascending; partners through DPP /
+// permlane swaps (xor_lanes: the whole wave active, as at every call below)
 template <int S, class T>
 __device__ __forceinline__ T group_sort(T x, uint32_t lane)
 {
@@ -745,7 +746,7 @@ __device__ __forceinline__ T group_sort(T x, uint32_t lane)
     for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
 #pragma unroll
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const T y = shfl_xor(x, (int)jj);
+            const T y = xor_lanes(x, (int)jj);
             const bool up = k == (uint32_t)S || (lane & k) == 0, lower = (lane & jj) == 0;
             const T mn = x < y ? x : y, mx = x < y ? y : x;
             x = (lower == up) ? mn : mx;
@@ -760,9 +761,22 @@ __device__ __forceinline__ T group_sort(T x, uint32_t lane)
 // 64-bit network. The first sorts (range id << 6 | lane) and each lane then takes its key's entry; when some range id is
 // held by entries of different TxnIds (commands with identical ranges: rare) the (range id, lane) order may separate
 // duplicates or misorder TxnIds, so that wave sorts the 64-bit entries instead.
+#ifdef ACC_PHASE_PROF
+// tuning build only (tools/build_prof.sh): per-wave phase cycles of k_rd_build_seg, one row of 8 per wave, each phase
+// closed by a full s_waitcnt so a phase owns its loads' latency
+__device__ unsigned long long *g_rd_prof;
+#define RD_PH(i) do { __builtin_amdgcn_s_waitcnt(0); ph[i] = clock64(); } while (0)
+#else
+#define RD_PH(i) ((void)0)
+#endif
+
 template <int S, bool NARROW>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
 {
+#ifdef ACC_PHASE_PROF
+    uint64_t ph[6];
+#endif
+    RD_PH(0);
     __shared__ uint32_t slot[WAVES][64];
     constexpr int G = 64 / S;
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
@@ -774,6 +788,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint64_t m = 0, x = ~0ull;
+    RD_PH(1);
     if (live) {
         // the txn's queries S at a time: one load round for their counts and offsets, a shuffle search for the
         // query holding entry `sub`, one load round for the entry (not two dependent loads per query)
@@ -805,6 +820,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
             m += total;
         }
     }
+    RD_PH(2);
     if (NARROW) {
         uint32_t k1 = (live && sub < m) ? ((uint32_t)(x >> 32) << 6) | sub : 0xFFFFFFFFu;
         k1 = group_sort<S>(k1, lane);
@@ -841,24 +857,37 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint64_t rb = __ballot(rnew) & gmask;
     const uint32_t Rd = (uint32_t)__popcll(rb);
     const uint32_t g0 = grp * S;
+    RD_PH(3);
     if (yin) slot[wave][g0 + ypos] = uidx;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (!live || m == 0) return;
-    uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
-    if (ynew) sd[uidx] = dep_of(o, ytp);
-    const uint32_t g = (uint32_t)__popcll(rb & lt);
-    if (valid) {
-        sa[Rd + pos] = slot[wave][g0 + pos];
-        if (rnew) {
-            sr[g] = rid;
-            if (g > 0) sa[g - 1] = Rd + pos;
+#ifdef ACC_PHASE_PROF
+    const bool wlive = __ballot(live && m != 0) != 0;
+#endif
+    if (live && m != 0) {
+        uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
+        if (ynew) sd[uidx] = dep_of(o, ytp);
+        const uint32_t g = (uint32_t)__popcll(rb & lt);
+        if (valid) {
+            sa[Rd + pos] = slot[wave][g0 + pos];
+            if (rnew) {
+                sr[g] = rid;
+                if (g > 0) sa[g - 1] = Rd + pos;
+            }
+        }
+        if (sub == 0) {
+            sa[Rd - 1] = Rd + M;
+            o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M;
         }
     }
-    if (sub == 0) {
-        sa[Rd - 1] = Rd + M;
-        o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M;
+#ifdef ACC_PHASE_PROF
+    RD_PH(4);
+    if (lane == 0 && wlive) {
+        unsigned long long *row = g_rd_prof + 8 * ((size_t)blockIdx.x * WAVES + wave);
+        for (int i = 0; i < 4; ++i) row[i] = ph[i + 1] - ph[i];
+        row[7] = 1;
     }
+#endif
 }
 
 // One workgroup per txn over buffers A, B of n2 >= m elements (LDS sized to the tier, or global scratch)
@@ -1040,6 +1069,35 @@ __global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
 }  // namespace rd
 
 using namespace rd;
+
+#ifdef ACC_PHASE_PROF
+// tuning build: rows for one k_rd_build_seg launch of `blocks` workgroups; rd_prof_print after it (serialises the tier)
+static unsigned long long *rd_prof_arm(acc_ctx *ctx, uint32_t blocks)
+{
+    const size_t rows = (size_t)blocks * WAVES;
+    unsigned long long *buf = ctx->get<unsigned long long>("rd_prof", 8 * rows);
+    ACC_HIP(hipMemsetAsync(buf, 0, 8 * rows * sizeof(unsigned long long), ctx->stream));
+    ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_rd_prof), &buf, sizeof buf, 0, hipMemcpyHostToDevice, ctx->stream));
+    return buf;
+}
+static void rd_prof_print(acc_ctx *ctx, const char *tier, unsigned long long *buf, uint32_t blocks)
+{
+    const size_t rows = (size_t)blocks * WAVES;
+    std::vector<unsigned long long> h(8 * rows);
+    ACC_HIP(hipMemcpyAsync(h.data(), buf, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    ACC_HIP(hipStreamSynchronize(ctx->stream));
+    double sum[4] = {};
+    size_t w = 0;
+    for (size_t r = 0; r < rows; ++r) {
+        if (!h[8 * r + 7]) continue;
+        ++w;
+        for (int i = 0; i < 4; ++i) sum[i] += (double)h[8 * r + i];
+    }
+    const double d = w ? (double)w : 1.0;
+    fprintf(stderr, "[rd_phase] %s waves=%zu avg cycles: head %.0f gather %.0f sort %.0f write %.0f\n", tier, w, sum[0] / d,
+            sum[1] / d, sum[2] / d, sum[3] / d);
+}
+#endif
 
 static void rd_check_errors(uint64_t errs)
 {
@@ -1298,18 +1356,34 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     if (hh[1]) {
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[1];
+#ifdef ACC_PHASE_PROF
+        const uint32_t pb16 = (hh[1] + 4 * WAVES - 1) / (4 * WAVES);
+        ctx->launch_stream = nullptr;
+        unsigned long long *pf16 = rd_prof_arm(ctx, pb16);
+#endif
         if (narrow)
             launch(ctx, "rd_build_s16", k_rd_build_seg<16, true>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
         else
             launch(ctx, "rd_build_s16", k_rd_build_seg<16, false>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+#ifdef ACC_PHASE_PROF
+        rd_prof_print(ctx, "s16", pf16, pb16);
+#endif
     }
     if (hh[11]) {
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[11];
+#ifdef ACC_PHASE_PROF
+        const uint32_t pb32 = (hh[11] + 2 * WAVES - 1) / (2 * WAVES);
+        ctx->launch_stream = nullptr;
+        unsigned long long *pf32 = rd_prof_arm(ctx, pb32);
+#endif
         if (narrow)
             launch(ctx, "rd_build_s32", k_rd_build_seg<32, true>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
         else
             launch(ctx, "rd_build_s32", k_rd_build_seg<32, false>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
+#ifdef ACC_PHASE_PROF
+        rd_prof_print(ctx, "s32", pf32, pb32);
+#endif
     }
     uint64_t nblk = 0;
     ctx->launch_stream = ctx->aux[1];
@@ -1326,10 +1400,18 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     ctx->launch_stream = nullptr;
     if (hh[2]) {
         o.list = tl_sorted + toff[2];
+#ifdef ACC_PHASE_PROF
+        const uint32_t pb64 = (hh[2] + WAVES - 1) / WAVES;
+        ctx->launch_stream = nullptr;
+        unsigned long long *pf64 = rd_prof_arm(ctx, pb64);
+#endif
         if (narrow)
             launch(ctx, "rd_build_s64", k_rd_build_seg<64, true>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
         else
             launch(ctx, "rd_build_s64", k_rd_build_seg<64, false>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+#ifdef ACC_PHASE_PROF
+        rd_prof_print(ctx, "s64", pf64, pb64);
+#endif
     }
     ctx->join(2);
     const uint32_t nglb = hh[10];
