@@ -364,8 +364,7 @@ struct View {
     uint64_t *cursor;             // global output cursor
     uint64_t cap;                 // capacity of ent
     uint64_t *ent;                // (range id << 32 | TxnId position) per emitted pair
-    uint64_t *q_off;              // per query (original index): first entry
-    uint32_t *q_cnt;              // per query: entries
+    ulonglong2 *q_out;            // per query (original index): (first entry, entries), one 16-B store per query
 };
 
 __device__ __forceinline__ uint32_t lower_bound_s(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v)
@@ -628,7 +627,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
     pool.cur[tid] = mine;
     __syncthreads();
     const uint64_t base = T.base;
-    if (valid) { v.q_off[r.q] = base + mine; v.q_cnt[r.q] = count; }
+    if (valid) v.q_out[r.q] = make_ulonglong2(base + mine, count);
     if (base + total > v.cap) return;   // uniform: the host re-runs with a larger capacity
     if (flat && total <= POOL) {
         // each pooled hit's place in its query's run (per-query cursors), the pool permuted in place through
@@ -659,8 +658,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
 struct Out {
     uint32_t n, P;
     const uint32_t *key_off, *rng_off;
-    const uint64_t *q_off;
-    const uint32_t *q_cnt;
+    const ulonglong2 *q_out;      // (first entry, entries) per query
     const uint64_t *ent;
     const uint32_t *txn_of_tpos;  // null: batch in TxnId order (tpos = batch index)
     const uint64_t *raw_off;      // [n + 1] raw entries per txn (scratch placement)
@@ -706,7 +704,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_tsize(uint32_t n, Out o, uint64_t 
             for (uint32_t qb = q0; qb < q1; qb += 8) {   // eight count loads in flight, not one dependent add per load
                 uint32_t c[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) c[u] = qb + u < q1 ? o.q_cnt[qb + u] : 0u;
+                for (int u = 0; u < 8; ++u) c[u] = qb + u < q1 ? (uint32_t)o.q_out[qb + u].y : 0u;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) m += c[u];
             }
@@ -755,8 +753,39 @@ __device__ __forceinline__ T group_sort(T x, uint32_t lane)
     return x;
 }
 
-// Groups of S lanes (S = 16, 32 or 64), one txn each: load, sort (range id, TxnId position), dedupe, TxnId union and
-// index, range groups; results to the scratch regions of the txn.
+// One chunk of S queries [qc, min(qc + S, q1)) of a txn whose (first entry, entries) records the group's lanes hold
+// in qv: an inclusive count scan, a shuffle search for the query holding entry `sub` of the txn (after the m entries
+// of earlier chunks), and that entry's load (issued here, waited for by the first use).
+template <int S>
+__device__ __forceinline__ void seg_chunk(const Out &o, ulonglong2 qv, uint32_t sub, int gb, uint64_t &m, uint64_t &x)
+{
+    const uint32_t c = (uint32_t)qv.y;
+    const uint64_t qo = qv.x;
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < S; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (sub >= (uint32_t)d) incl += u;
+    }
+    const uint32_t total = __shfl(incl, gb + S - 1, 64);
+    uint32_t j = 0;   // lanes whose queries end at or before entry sub
+#pragma unroll
+    for (int step = S / 2; step >= 1; step >>= 1) {
+        const uint32_t end = (uint32_t)m + __shfl(incl, gb + (int)j + step - 1, 64);
+        if (end <= sub) j += step;
+    }
+    j = min(j, (uint32_t)S - 1);
+    const uint64_t qoj = shfl_idx(qo, gb + (int)j);
+    const uint32_t startj = (uint32_t)m + __shfl(incl - c, gb + (int)j, 64);
+    if (sub >= m && sub < m + total) x = o.ent[qoj + (sub - startj)];
+    m += total;
+}
+
+// Groups of S lanes (S = 16, 32 or 64), K txns each in turn: load, sort (range id, TxnId position), dedupe, TxnId
+// union and index, range groups; results to the scratch regions of the txn.
+// The K txns' loads are issued together — list entries, then their offsets, then their first S query records, then
+// their entries — so a group waits for four dependent memory latencies per K txns, not per txn (the tier is
+// latency-bound: each of those loads costs ~2.5K cycles under the build's load, the sorts ~1K).
 // NARROW (range ids and TxnId positions below 2^26): both sorts on 32-bit keys, half the cross-lane traffic of the
 // 64-bit network. The first sorts (range id << 6 | lane) and each lane then takes its key's entry; when some range id is
 // held by entries of different TxnIds (commands with identical ranges: rare) the (range id, lane) order may separate
@@ -769,8 +798,12 @@ __device__ unsigned long long *g_rd_prof;
 #else
 #define RD_PH(i) ((void)0)
 #endif
+#ifndef ACC_RD_SEGK
+#define ACC_RD_SEGK 4
+#endif
+constexpr int RD_SEGK = ACC_RD_SEGK;   // txns per lane group
 
-template <int S, bool NARROW>
+template <int S, bool NARROW, int K>
 __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
 {
 #ifdef ACC_PHASE_PROF
@@ -781,110 +814,130 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     constexpr int G = 64 / S;
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint32_t grp = lane / S, sub = lane & (S - 1);
-    const uint32_t li = (blockIdx.x * WAVES + wave) * G + grp;
-    const bool live = li < cnt;
-    const uint32_t t = live ? o.list[li] : 0;
-    const uint64_t ra = live ? o.raw_off[t] : 0;   // issued now: its latency hides under the gather and the sorts
+    const uint32_t li0 = ((blockIdx.x * WAVES + wave) * G + grp) * K;
     const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint64_t m = 0, x = ~0ull;
+    const int gb = (int)(grp * S);
+    const uint32_t g0 = grp * S;
+    uint32_t t[K], q0[K], q1[K];
+    uint64_t ra[K], m[K], x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = li0 + k < cnt ? o.list[li0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        // both the key and the range bounds (txn_queries' choice made after the loads, not between them)
+        q0[k] = q1[k] = 0; ra[k] = 0;
+        if (li0 + k < cnt) {
+            const uint32_t k0 = o.key_off[t[k]], k1 = o.key_off[t[k] + 1];
+            const uint32_t r0 = o.rng_off[t[k]], r1 = o.rng_off[t[k] + 1];
+            ra[k] = o.raw_off[t[k]];
+            if (k1 > k0) { q0[k] = k0; q1[k] = k1; } else { q0[k] = o.P + r0; q1[k] = o.P + r1; }
+        }
+    }
     RD_PH(1);
-    if (live) {
-        // the txn's queries S at a time: one load round for their counts and offsets, a shuffle search for the
-        // query holding entry `sub`, one load round for the entry (not two dependent loads per query)
-        uint32_t q0, q1;
-        txn_queries(o, t, q0, q1);
-        const int gb = (int)(grp * S);
-        for (uint32_t qc = q0; qc < q1; qc += S) {   // group-uniform
+    ulonglong2 qv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t q = q0[k] + sub;
+        qv[k] = make_ulonglong2(0, 0);
+        if (q < q1[k]) qv[k] = o.q_out[q];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        m[k] = 0; x[k] = ~0ull;
+        seg_chunk<S>(o, qv[k], sub, gb, m[k], x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        for (uint32_t qc = q0[k] + S; qc < q1[k]; qc += S) {   // group-uniform: txns of more than S queries
             const uint32_t q = qc + sub;
-            uint32_t c = 0;
-            uint64_t qo = 0;
-            if (q < q1) { c = o.q_cnt[q]; qo = o.q_off[q]; }
-            uint32_t incl = c;
-#pragma unroll
-            for (int d = 1; d < S; d <<= 1) {
-                const uint32_t u = __shfl_up(incl, d, 64);
-                if (sub >= (uint32_t)d) incl += u;
-            }
-            const uint32_t total = __shfl(incl, gb + S - 1, 64);
-            uint32_t j = 0;   // lanes whose queries end at or before entry sub
-#pragma unroll
-            for (int step = S / 2; step >= 1; step >>= 1) {
-                const uint32_t end = (uint32_t)m + __shfl(incl, gb + (int)j + step - 1, 64);
-                if (end <= sub) j += step;
-            }
-            j = min(j, (uint32_t)S - 1);
-            const uint64_t qoj = shfl_idx(qo, gb + (int)j);
-            const uint32_t startj = (uint32_t)m + __shfl(incl - c, gb + (int)j, 64);
-            if (sub >= m && sub < m + total) x = o.ent[qoj + (sub - startj)];
-            m += total;
+            ulonglong2 v = make_ulonglong2(0, 0);
+            if (q < q1[k]) v = o.q_out[q];
+            seg_chunk<S>(o, v, sub, gb, m[k], x[k]);
         }
     }
     RD_PH(2);
-    if (NARROW) {
-        uint32_t k1 = (live && sub < m) ? ((uint32_t)(x >> 32) << 6) | sub : 0xFFFFFFFFu;
-        k1 = group_sort<S>(k1, lane);
-        const uint64_t xs = shfl_idx(x, (int)(grp * S + (k1 & 63u)));
-        x = k1 == 0xFFFFFFFFu ? ~0ull : xs;
-        const uint64_t pv = shfl_up(x, 1);
-        const bool mixed = live && sub > 0 && sub < m && (uint32_t)(pv >> 32) == (uint32_t)(x >> 32) && (uint32_t)pv != (uint32_t)x;
-        if (__ballot(mixed)) x = group_sort<S>(x, lane);   // wave-uniform; sorted groups stay as they are
-    } else {
-        x = group_sort<S>(x, lane);
-    }
-    const uint64_t prev = shfl_up(x, 1);
-    const bool valid = live && sub < m && (sub == 0 || x != prev);       // dedupe identical (range, txn)
-    const uint64_t vb = __ballot(valid) & gmask;
-    const uint32_t M = (uint32_t)__popcll(vb);
-    const uint32_t pos = (uint32_t)__popcll(vb & lt);
-    const uint32_t rid = (uint32_t)(x >> 32), tp = (uint32_t)x;
-    // (TxnId position, entry) sorted: the TxnId union and each entry's index
-    uint32_t ytp, ypos;
-    if (NARROW) {
-        const uint32_t y = group_sort<S>(valid ? (tp << 6) | pos : 0xFFFFFFFFu, lane);
-        ytp = y >> 6; ypos = y & 63u;
-    } else {
-        const uint64_t y = group_sort<S>(valid ? (((uint64_t)tp << 8) | pos) : ~0ull, lane);
-        ytp = (uint32_t)(y >> 8); ypos = (uint32_t)y & 0xFFu;
-    }
-    const uint32_t yprev = __shfl_up(ytp, 1, 64);
-    const bool ynew = live && sub < M && (sub == 0 || ytp != yprev);
-    const uint64_t nb = __ballot(ynew) & gmask;
-    const uint32_t U = (uint32_t)__popcll(nb);
-    const bool yin = live && sub < M;
-    const uint32_t uidx = (uint32_t)__popcll(nb & lt) + (ynew ? 1u : 0u) - 1u;   // index of this entry's TxnId
-    const bool rnew = valid && (sub == 0 || (uint32_t)(prev >> 32) != rid);
-    const uint64_t rb = __ballot(rnew) & gmask;
-    const uint32_t Rd = (uint32_t)__popcll(rb);
-    const uint32_t g0 = grp * S;
-    RD_PH(3);
-    if (yin) slot[wave][g0 + ypos] = uidx;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #ifdef ACC_PHASE_PROF
-    const bool wlive = __ballot(live && m != 0) != 0;
+    uint64_t sort_cy = 0, write_cy = 0;
+    bool wlive = false;
 #endif
-    if (live && m != 0) {
-        uint32_t *sa = o.s_arena + 2 * ra, *sr = o.s_rid + ra, *sd = o.s_dep + ra;
-        if (ynew) sd[uidx] = dep_of(o, ytp);
-        const uint32_t g = (uint32_t)__popcll(rb & lt);
-        if (valid) {
-            sa[Rd + pos] = slot[wave][g0 + pos];
-            if (rnew) {
-                sr[g] = rid;
-                if (g > 0) sa[g - 1] = Rd + pos;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#ifdef ACC_PHASE_PROF
+        RD_PH(3);
+#endif
+        const bool live = li0 + k < cnt;
+        uint64_t xk = x[k];
+        const uint64_t mk = m[k];
+        if (NARROW) {
+            uint32_t k1 = (live && sub < mk) ? ((uint32_t)(xk >> 32) << 6) | sub : 0xFFFFFFFFu;
+            k1 = group_sort<S>(k1, lane);
+            const uint64_t xs = shfl_idx(xk, (int)(grp * S + (k1 & 63u)));
+            xk = k1 == 0xFFFFFFFFu ? ~0ull : xs;
+            const uint64_t pv = shfl_up(xk, 1);
+            const bool mixed = live && sub > 0 && sub < mk && (uint32_t)(pv >> 32) == (uint32_t)(xk >> 32) && (uint32_t)pv != (uint32_t)xk;
+            if (__ballot(mixed)) xk = group_sort<S>(xk, lane);   // wave-uniform; sorted groups stay as they are
+        } else {
+            xk = group_sort<S>(xk, lane);
+        }
+        const uint64_t prev = shfl_up(xk, 1);
+        const bool valid = live && sub < mk && (sub == 0 || xk != prev);       // dedupe identical (range, txn)
+        const uint64_t vb = __ballot(valid) & gmask;
+        const uint32_t M = (uint32_t)__popcll(vb);
+        const uint32_t pos = (uint32_t)__popcll(vb & lt);
+        const uint32_t rid = (uint32_t)(xk >> 32), tp = (uint32_t)xk;
+        // (TxnId position, entry) sorted: the TxnId union and each entry's index
+        uint32_t ytp, ypos;
+        if (NARROW) {
+            const uint32_t y = group_sort<S>(valid ? (tp << 6) | pos : 0xFFFFFFFFu, lane);
+            ytp = y >> 6; ypos = y & 63u;
+        } else {
+            const uint64_t y = group_sort<S>(valid ? (((uint64_t)tp << 8) | pos) : ~0ull, lane);
+            ytp = (uint32_t)(y >> 8); ypos = (uint32_t)y & 0xFFu;
+        }
+        const uint32_t yprev = __shfl_up(ytp, 1, 64);
+        const bool ynew = live && sub < M && (sub == 0 || ytp != yprev);
+        const uint64_t nb = __ballot(ynew) & gmask;
+        const uint32_t U = (uint32_t)__popcll(nb);
+        const bool yin = live && sub < M;
+        const uint32_t uidx = (uint32_t)__popcll(nb & lt) + (ynew ? 1u : 0u) - 1u;   // index of this entry's TxnId
+        const bool rnew = valid && (sub == 0 || (uint32_t)(prev >> 32) != rid);
+        const uint64_t rb = __ballot(rnew) & gmask;
+        const uint32_t Rd = (uint32_t)__popcll(rb);
+#ifdef ACC_PHASE_PROF
+        RD_PH(4);
+        sort_cy += ph[4] - ph[3];
+        wlive = wlive || __ballot(live && mk != 0) != 0;
+#endif
+        __builtin_amdgcn_wave_barrier();   // the previous txn's reads of slot are done
+        if (yin) slot[wave][g0 + ypos] = uidx;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (live && mk != 0) {
+            uint32_t *sa = o.s_arena + 2 * ra[k], *sr = o.s_rid + ra[k], *sd = o.s_dep + ra[k];
+            if (ynew) sd[uidx] = dep_of(o, ytp);
+            const uint32_t g = (uint32_t)__popcll(rb & lt);
+            if (valid) {
+                sa[Rd + pos] = slot[wave][g0 + pos];
+                if (rnew) {
+                    sr[g] = rid;
+                    if (g > 0) sa[g - 1] = Rd + pos;
+                }
+            }
+            if (sub == 0) {
+                sa[Rd - 1] = Rd + M;
+                o.rd_cnt[t[k]] = Rd; o.u_cnt[t[k]] = U; o.a_cnt[t[k]] = (uint64_t)Rd + M;
             }
         }
-        if (sub == 0) {
-            sa[Rd - 1] = Rd + M;
-            o.rd_cnt[t] = Rd; o.u_cnt[t] = U; o.a_cnt[t] = (uint64_t)Rd + M;
-        }
+#ifdef ACC_PHASE_PROF
+        RD_PH(5);
+        write_cy += ph[5] - ph[4];
+#endif
     }
 #ifdef ACC_PHASE_PROF
-    RD_PH(4);
     if (lane == 0 && wlive) {
         unsigned long long *row = g_rd_prof + 8 * ((size_t)blockIdx.x * WAVES + wave);
-        for (int i = 0; i < 4; ++i) row[i] = ph[i + 1] - ph[i];
+        row[0] = ph[1] - ph[0]; row[1] = ph[2] - ph[1]; row[2] = sort_cy; row[3] = write_cy;
         row[7] = 1;
     }
 #endif
@@ -903,7 +956,7 @@ __device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, 
         // every query's count and offset in one load round, then the raw entries four loads per thread at a time
         uint32_t c = 0;
         uint64_t off = 0;
-        if (tid < nq) { c = o.q_cnt[q0 + tid]; off = o.q_off[q0 + tid]; }
+        if (tid < nq) { const ulonglong2 qv = o.q_out[q0 + tid]; c = (uint32_t)qv.y; off = qv.x; }
         const uint32_t st = block_exclusive(c, OpAdd<uint32_t>(), red, m);
         if (tid < nq) { qs[tid] = st; qo[tid] = off; }
         __syncthreads();
@@ -924,8 +977,9 @@ __device__ void build_block(const Out &o, uint32_t t, uint64_t *A, uint64_t *B, 
         }
     } else {
         for (uint32_t q = q0; q < q1; ++q) {
-            const uint32_t c = o.q_cnt[q];
-            const uint64_t off = o.q_off[q];
+            const ulonglong2 qv = o.q_out[q];
+            const uint32_t c = (uint32_t)qv.y;
+            const uint64_t off = qv.x;
             for (uint32_t k = tid; k < c; k += BLOCK) A[m + k] = o.ent[off + k];
             m += c;
         }
@@ -1289,8 +1343,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     View v{};
     v.Q = Qp; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
     v.cs_s = cs_s; v.cs_e = cs_e; v.cs_info = cs_info; v.cs_kind = cs_kind; v.class_off = class_off;
-    v.q_off = ctx->get<uint64_t>("rd_q_off", Q);
-    v.q_cnt = ctx->get<uint32_t>("rd_q_cnt", Q);
+    v.q_out = ctx->get<ulonglong2>("rd_q_out", Q);
     v.cursor = ctx->get<uint64_t>("rd_cursor", 1);
     uint32_t *win = ctx->get<uint32_t>("rd_win", (size_t)nsb * 2 * NCLS);
     v.win = win;
@@ -1318,7 +1371,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
 
     // ---- 4. per-txn RangeDeps: raw sizes and tiers, build into scratch, offsets, compaction
     Out o{};
-    o.n = n; o.P = (uint32_t)P; o.key_off = key_off; o.rng_off = rng_off; o.q_off = v.q_off; o.q_cnt = v.q_cnt;
+    o.n = n; o.P = (uint32_t)P; o.key_off = key_off; o.rng_off = rng_off; o.q_out = v.q_out;
     o.ent = v.ent;
     o.txn_of_tpos = dict.batch_sorted ? nullptr : txn_of_tpos;
     o.rd_cnt = ctx->get<uint32_t>("rd_rd_cnt", n);
@@ -1357,14 +1410,14 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[1];
 #ifdef ACC_PHASE_PROF
-        const uint32_t pb16 = (hh[1] + 4 * WAVES - 1) / (4 * WAVES);
+        const uint32_t pb16 = (hh[1] + RD_SEGK * 4 * WAVES - 1) / (RD_SEGK * 4 * WAVES);
         ctx->launch_stream = nullptr;
         unsigned long long *pf16 = rd_prof_arm(ctx, pb16);
 #endif
         if (narrow)
-            launch(ctx, "rd_build_s16", k_rd_build_seg<16, true>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+            launch(ctx, "rd_build_s16", k_rd_build_seg<16, true, RD_SEGK>, dim3((hh[1] + RD_SEGK * 4 * WAVES - 1) / (RD_SEGK * 4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
         else
-            launch(ctx, "rd_build_s16", k_rd_build_seg<16, false>, dim3((hh[1] + 4 * WAVES - 1) / (4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
+            launch(ctx, "rd_build_s16", k_rd_build_seg<16, false, RD_SEGK>, dim3((hh[1] + RD_SEGK * 4 * WAVES - 1) / (RD_SEGK * 4 * WAVES)), dim3(BLOCK), 0, hh[1], o);
 #ifdef ACC_PHASE_PROF
         rd_prof_print(ctx, "s16", pf16, pb16);
 #endif
@@ -1373,14 +1426,14 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
         ctx->launch_stream = ctx->aux[0];
         o.list = tl_sorted + toff[11];
 #ifdef ACC_PHASE_PROF
-        const uint32_t pb32 = (hh[11] + 2 * WAVES - 1) / (2 * WAVES);
+        const uint32_t pb32 = (hh[11] + RD_SEGK * 2 * WAVES - 1) / (RD_SEGK * 2 * WAVES);
         ctx->launch_stream = nullptr;
         unsigned long long *pf32 = rd_prof_arm(ctx, pb32);
 #endif
         if (narrow)
-            launch(ctx, "rd_build_s32", k_rd_build_seg<32, true>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
+            launch(ctx, "rd_build_s32", k_rd_build_seg<32, true, RD_SEGK>, dim3((hh[11] + RD_SEGK * 2 * WAVES - 1) / (RD_SEGK * 2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
         else
-            launch(ctx, "rd_build_s32", k_rd_build_seg<32, false>, dim3((hh[11] + 2 * WAVES - 1) / (2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
+            launch(ctx, "rd_build_s32", k_rd_build_seg<32, false, RD_SEGK>, dim3((hh[11] + RD_SEGK * 2 * WAVES - 1) / (RD_SEGK * 2 * WAVES)), dim3(BLOCK), 0, hh[11], o);
 #ifdef ACC_PHASE_PROF
         rd_prof_print(ctx, "s32", pf32, pb32);
 #endif
@@ -1401,14 +1454,14 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     if (hh[2]) {
         o.list = tl_sorted + toff[2];
 #ifdef ACC_PHASE_PROF
-        const uint32_t pb64 = (hh[2] + WAVES - 1) / WAVES;
+        const uint32_t pb64 = (hh[2] + RD_SEGK * WAVES - 1) / (RD_SEGK * WAVES);
         ctx->launch_stream = nullptr;
         unsigned long long *pf64 = rd_prof_arm(ctx, pb64);
 #endif
         if (narrow)
-            launch(ctx, "rd_build_s64", k_rd_build_seg<64, true>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+            launch(ctx, "rd_build_s64", k_rd_build_seg<64, true, RD_SEGK>, dim3((hh[2] + RD_SEGK * WAVES - 1) / (RD_SEGK * WAVES)), dim3(BLOCK), 0, hh[2], o);
         else
-            launch(ctx, "rd_build_s64", k_rd_build_seg<64, false>, dim3((hh[2] + WAVES - 1) / WAVES), dim3(BLOCK), 0, hh[2], o);
+            launch(ctx, "rd_build_s64", k_rd_build_seg<64, false, RD_SEGK>, dim3((hh[2] + RD_SEGK * WAVES - 1) / (RD_SEGK * WAVES)), dim3(BLOCK), 0, hh[2], o);
 #ifdef ACC_PHASE_PROF
         rd_prof_print(ctx, "s64", pf64, pb64);
 #endif
