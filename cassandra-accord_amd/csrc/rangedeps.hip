@@ -34,9 +34,6 @@ constexpr int NCLS = 33;          // width classes 0..32 (4^32 = 2^64 covers eve
 #ifndef ACC_RD_TILE
 #define ACC_RD_TILE 256
 #endif
-#ifndef ACC_RD_POOL
-#define ACC_RD_POOL 1024
-#endif
 constexpr int TILE = ACC_RD_TILE;   // entries per LDS tile in the stabbing pass (LDS per block sets the occupancy)
 constexpr uint32_t BLOCK_E = 8192;  // workgroup tier (LDS)
 
@@ -291,7 +288,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
                                                    const uint32_t *__restrict__ owner, const uint64_t *__restrict__ rs,
                                                    const uint64_t *__restrict__ re, const uint32_t *__restrict__ rowner,
                                                    const uint4 *__restrict__ tinfo, Runs plan, QRec *__restrict__ rec,
-                                                   uint64_t *__restrict__ qkey, uint32_t rbit, int ibits)
+                                                   uint64_t *__restrict__ qkey, uint32_t rbit, int ibits, int qdrop)
 {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
     if (q >= P + R) return;
@@ -306,7 +303,8 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
     // wave would leave the key lanes idle behind it
     // ibits > 0: the query index packed under the key (a keys-only sort, 8 B per element moved instead of 12)
     const uint64_t k = pext_runs(r.lo, plan) | (q >= P && rbit < 64 ? 1ull << rbit : 0ull);
-    qkey[q] = ibits ? (k << ibits) | q : k;
+    // qdrop: the low key bits the sort leaves out (the stabbing blocks need neighbouring queries, not an exact order)
+    qkey[q] = ibits ? ((k >> qdrop) << ibits) | q : k >> qdrop;
 }
 
 // sorted records, and per block of BLOCK sorted queries (the stabbing blocks) the largest high bound
@@ -525,26 +523,17 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const uint6
 }
 
 // Every class's window of the block in one tile (when they fit TILE together): one load round for the block.
-// Count pass (pool != null): each hit is also appended to the block's LDS pool (wave-aggregated slot claims) with its
-// thread, so a block whose hits fit the pool needs no second scan. Emit pass: hits to ent at out.
-constexpr uint32_t POOL = ACC_RD_POOL;
-struct StabPool {
-    uint64_t x[POOL];
-    uint8_t q[POOL];
-    uint32_t n;
-    uint32_t cur[BLOCK];
-};
+// Count pass (hv != null): the query's first STAB_RH hits are kept in registers. Emit pass: hits to ent at out.
+constexpr int STAB_RH = 16;   // hits a query keeps in registers through the count pass (flat blocks)
 
 template <bool EMIT>
 __device__ __forceinline__ uint32_t stab_flat(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
-                                              StabPool *pool)
+                                              uint64_t (*hv)[STAB_RH])
 {
     uint32_t count = 0;
     if (!valid) return 0;
     const bool isr = (r.flags >> 8) & 1u;
     const uint32_t wm = r.flags & 0xFFu;
-    const uint32_t lane = lane_id();
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
         const uint32_t p0 = T.pre[c], p1 = T.pre[c + 1];
         if (p0 == p1) continue;
@@ -564,16 +553,10 @@ __device__ __forceinline__ uint32_t stab_flat(const View &v, StabTile &T, bool v
             const uint64_t x = ((uint64_t)info.x << 32) | info.y;
             if (EMIT) {
                 if (hit) v.ent[out + count] = x;
-            } else if (pool) {
-                const uint64_t bm = __ballot(hit);
-                if (bm) {
-                    const uint32_t leader = (uint32_t)__builtin_ctzll(bm);
-                    uint32_t b = 0;
-                    if (lane == leader) b = atomicAdd(&pool->n, (uint32_t)__popcll(bm));
-                    b = __shfl(b, (int)leader, 64);
-                    const uint32_t slot = b + (uint32_t)__popcll(bm & lt);
-                    if (hit && slot < POOL) { pool->x[slot] = x; pool->q[slot] = (uint8_t)threadIdx.x; }
-                }
+            } else if (hv) {
+#pragma unroll
+                for (int u = 0; u < STAB_RH; ++u)
+                    if (hit && (uint32_t)u == count) (*hv)[u] = x;
             }
             count += hit ? 1u : 0u;
         }
@@ -581,14 +564,27 @@ __device__ __forceinline__ uint32_t stab_flat(const View &v, StabTile &T, bool v
     return count;
 }
 
+#ifdef ACC_PHASE_PROF
+// tuning build only: per-block phase cycles of k_rd_stab (thread 0, each phase closed by a barrier and a full waitcnt)
+__device__ unsigned long long *g_stab_prof;
+#define SB_PH(i) do { __syncthreads(); __builtin_amdgcn_s_waitcnt(0); ph[i] = clock64(); } while (0)
+#else
+#define SB_PH(i) ((void)0)
+#endif
+
 // A workgroup of BLOCK consecutive (sorted) queries over its precomputed windows: count every query's pairs, take the
-// block's output slice with one atomic, write them. When the windows fit one tile they are loaded once, and when the
-// block's hits fit the LDS pool the count pass has already gathered them: they are placed into each query's run of the
-// slice (a per-query cursor) with no second scan. Otherwise the (class, tile) sequence is scanned again to emit.
+// block's output slice with one atomic, write them. When the windows fit one tile they are loaded once and each query
+// keeps its first STAB_RH hits in registers through the count pass: a query with no more than that writes them from
+// there, a query with more scans the tile again. Otherwise the (class, tile) sequence is scanned again to emit.
+// (A config-4 key block holds ~1,400 hits: an LDS pool of them would cost the occupancy, a per-hit slot claim the
+// count pass's time.)
 __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
 {
+#ifdef ACC_PHASE_PROF
+    uint64_t ph[6];
+#endif
+    SB_PH(0);
     __shared__ StabTile T;
-    __shared__ StabPool pool;
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * BLOCK + tid;
     QRec r{};
@@ -598,7 +594,6 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
         T.b0[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + tid];
         T.b1[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + NCLS + tid];
     }
-    if (tid == 0) pool.n = 0;
     __syncthreads();
     if (tid == 0) {
         uint32_t a = 0;
@@ -606,9 +601,11 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
         T.pre[NCLS] = a;
     }
     __syncthreads();
+    SB_PH(1);
     const uint32_t wtot = T.pre[NCLS];
     const bool flat = wtot <= (uint32_t)TILE;
     uint32_t count;
+    uint64_t hv[STAB_RH];
     if (flat) {
         for (uint32_t k = tid; k < wtot; k += BLOCK) {
             uint32_t lo = 0, hi = NCLS;   // the class holding flat position k: last c with pre[c] <= k
@@ -617,40 +614,40 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
             T.s[k] = v.cs_s[src]; T.e[k] = v.cs_e[src]; T.info[k] = v.cs_info[src]; T.kind[k] = v.cs_kind[src];
         }
         __syncthreads();
-        count = stab_flat<false>(v, T, valid, r, 0, &pool);
+        SB_PH(2);
+        count = stab_flat<false>(v, T, valid, r, 0, &hv);
     } else {
+        SB_PH(2);
         count = stab_pass<false>(v, T, valid, r, 0, nullptr);
     }
+    SB_PH(3);
     uint32_t total;
     const uint32_t mine = block_exclusive(count, OpAdd<uint32_t>(), T.red, total);
     if (tid == 0) T.base = atomicAdd((unsigned long long *)v.cursor, (unsigned long long)total);
-    pool.cur[tid] = mine;
     __syncthreads();
+    SB_PH(4);
     const uint64_t base = T.base;
     if (valid) v.q_out[r.q] = make_ulonglong2(base + mine, count);
     if (base + total > v.cap) return;   // uniform: the host re-runs with a larger capacity
-    if (flat && total <= POOL) {
-        // each pooled hit's place in its query's run (per-query cursors), the pool permuted in place through
-        // registers, then the slice written in whole lines
-        constexpr int PT = (POOL + BLOCK - 1) / BLOCK;
-        uint64_t xv[PT];
-        uint32_t pv[PT];
+    if (flat && count <= (uint32_t)STAB_RH) {
 #pragma unroll
-        for (int u = 0; u < PT; ++u) {
-            const uint32_t k = tid + (uint32_t)u * BLOCK;
-            if (k < total) { pv[u] = atomicAdd(&pool.cur[pool.q[k]], 1u); xv[u] = pool.x[k]; }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < PT; ++u)
-            if (tid + (uint32_t)u * BLOCK < total) pool.x[pv[u]] = xv[u];
-        __syncthreads();
-        for (uint32_t k = tid; k < total; k += BLOCK) v.ent[base + k] = pool.x[k];
+        for (int u = 0; u < STAB_RH; ++u)
+            if ((uint32_t)u < count) v.ent[base + mine + u] = hv[u];
     } else if (flat) {
         stab_flat<true>(v, T, valid, r, base + mine, nullptr);
     } else {
         stab_pass<true>(v, T, valid, r, base + mine, nullptr);
     }
+#ifdef ACC_PHASE_PROF
+    SB_PH(5);
+    if (tid == 0) {
+        unsigned long long *row = g_stab_prof + 8 * (size_t)blockIdx.x;
+        for (int k = 0; k < 5; ++k) row[k] = ph[k + 1] - ph[k];
+        row[6] = flat ? 1 : 2;
+        row[5] = total;
+        row[7] = 1;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- per-txn build
@@ -1324,11 +1321,18 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     const Runs q_plan = make_runs(hm[2]);
     QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = nullptr;
     uint64_t *qkey = ctx->get<uint64_t>("rd_qkey", Q);
-    const int qbits = q_plan.bits < 64 ? q_plan.bits + 1 : 64;
+    const int qbits_full = q_plan.bits < 64 ? q_plan.bits + 1 : 64;
+    // Only the high bits of the low bound are sorted: a stabbing block needs BLOCK queries with neighbouring low bounds
+    // (its windows span their lowest to highest bound), and each query's scan is independent of its place in the block.
+    // 2^(bits_for(Q) - 2) buckets hold ~4 queries each on spread keys, so a block spans ~64 buckets — about the span of
+    // an exact sort — in whole 8-bit passes (config 4: 3 passes instead of 5).
+    const int qsort_bits = std::min(qbits_full, std::max(8, (bits_for(Q) - 2 + 7) / 8 * 8));
+    const int qdrop = qbits_full - qsort_bits;
+    const int qbits = qsort_bits;
     const int ibits = qbits + bits_for(Q) <= 64 && Q < OS_VAL ? std::max(1, bits_for(Q)) : 0;
     launch(ctx, "rd_qrec", k_rd_qrec, dim3(grid_for(Q, BLOCK)), dim3(BLOCK), 0, (uint32_t)P, (uint32_t)R, key_code,
            (const uint32_t *)owner, rs, re, (const uint32_t *)rowner, (const uint4 *)tinfo, q_plan, rec, qkey,
-           (uint32_t)q_plan.bits, ibits);
+           (uint32_t)q_plan.bits, ibits, qdrop);
     Sorted qs{ nullptr, nullptr };
     const uint64_t *qpk = nullptr;
     if (ibits) qpk = radix_sort_keys(ctx, "rs_rd_q", qkey, Q, ibits, qbits);
@@ -1357,7 +1361,31 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
             v.ent = ctx->get<uint64_t>("rd_ent", want);
             v.cap = ctx->bufs["rd_ent"].bytes / sizeof(uint64_t);
             ACC_HIP(hipMemsetAsync(v.cursor, 0, 8, st));
+#ifdef ACC_PHASE_PROF
+            unsigned long long *sbp = ctx->get<unsigned long long>("stab_prof", 8 * (size_t)nsb);
+            ACC_HIP(hipMemsetAsync(sbp, 0, 8 * (size_t)nsb * sizeof(unsigned long long), st));
+            ACC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stab_prof), &sbp, sizeof sbp, 0, hipMemcpyHostToDevice, st));
+#endif
             launch(ctx, "rd_stab", k_rd_stab, dim3(nsb), dim3(BLOCK), 0, v);
+#ifdef ACC_PHASE_PROF
+            {
+                std::vector<unsigned long long> h(8 * (size_t)nsb);
+                ACC_HIP(hipMemcpyAsync(h.data(), sbp, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+                ACC_HIP(hipStreamSynchronize(st));
+                for (int f = 1; f <= 2; ++f) {
+                    double sum[6] = {};
+                    size_t nb = 0;
+                    for (size_t b = 0; b < nsb; ++b) {
+                        if (!h[8 * b + 7] || h[8 * b + 6] != (unsigned long long)f) continue;
+                        ++nb;
+                        for (int k = 0; k < 6; ++k) sum[k] += (double)h[8 * b + k];
+                    }
+                    const double d = nb ? (double)nb : 1.0;
+                    fprintf(stderr, "[stab_phase] %s blocks=%zu avg cycles: head %.0f tile %.0f count %.0f scan+claim %.0f write %.0f | hits %.0f\n",
+                            f == 1 ? "flat" : "tiled", nb, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d);
+                }
+            }
+#endif
             ACC_HIP(hipMemcpyAsync(ctx->pinned, v.cursor, 8, hipMemcpyDeviceToHost, st));
             ctx->sync();
             E = ctx->pinned[0];
