@@ -73,12 +73,6 @@ __global__ __launch_bounds__(BLOCK) void k_permute_u64(size_t n, const uint32_t 
     if (p < n) out[p] = in[perm[p]];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_pext_u64(size_t n, const uint64_t *__restrict__ in, Runs plan, uint64_t *__restrict__ out)
-{
-    const size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (p < n) out[p] = pext_runs(in[p], plan);
-}
-
 __global__ __launch_bounds__(BLOCK) void k_widen_u32(size_t n, const uint32_t *__restrict__ in, uint64_t *__restrict__ out)
 {
     const size_t p = (size_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -155,15 +149,13 @@ __global__ __launch_bounds__(BLOCK) void k_rd_entries(uint32_t R, uint32_t n, co
                                                       const uint32_t *__restrict__ eidx, const uint32_t *__restrict__ rowner,
                                                       const uint64_t *__restrict__ rs, const uint64_t *__restrict__ re,
                                                       const uint4 *__restrict__ tinfo, const uint64_t *__restrict__ tl,
-                                                      Runs rs_plan, Runs re_plan, int e_bits, int split,
-                                                      uint64_t *__restrict__ e_s, uint4 *__restrict__ erec,
+                                                      Runs rs_plan, Runs re_plan, int e_bits, int split, uint4 *__restrict__ erec,
                                                       uint64_t *__restrict__ dkey, uint64_t *__restrict__ ekey)
 {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= R || !eflag[j]) return;
     const uint32_t i = eidx[j], t = rowner[j];
     const uint64_t s = rs[j], e = re[j];
-    e_s[i] = s;
     // the entry's 32-B record: start, end | TxnId position, kind, range id (k_rd_dict_write) — the permuted reads of
     // the dictionary and class passes take one record per entry instead of a line per column
     erec[2 * (size_t)i] = make_uint4((uint32_t)s, (uint32_t)(s >> 32), (uint32_t)e, (uint32_t)(e >> 32));
@@ -190,8 +182,8 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_flags(uint32_t ne, const uint
 __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint32_t *__restrict__ perm,
                                                          const uint32_t *__restrict__ flag, const uint32_t *__restrict__ incl,
                                                          uint4 *__restrict__ erec, uint64_t *__restrict__ dict_s,
-                                                         uint64_t *__restrict__ dict_e, Runs rs_plan, int s_bits, int cls_only,
-                                                         uint64_t *__restrict__ ckey, uint32_t *__restrict__ cls_hist)
+                                                         uint64_t *__restrict__ dict_e, uint64_t *__restrict__ ckey,
+                                                         uint32_t *__restrict__ cls_hist)
 {
     __shared__ uint32_t h[NCLS];
     if (threadIdx.x < NCLS) h[threadIdx.x] = 0;
@@ -207,7 +199,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_dict_write(uint32_t ne, const uint
         reinterpret_cast<uint32_t *>(erec + 2 * (size_t)i + 1)[2] = rid;   // the entry's range id
         if (flag[p]) { dict_s[rid] = es; dict_e[rid] = ee; }
         c = width_class(es, ee);
-        ckey[i] = cls_only ? (uint64_t)c : (((uint64_t)c << s_bits) | pext_runs(es, rs_plan));
+        ckey[p] = c;   // in (start, end) order: one stable pass by class gives the (class, start) order
     }
     // LDS histogram, one add per distinct class of a wave (per-thread atomics on a few hot words serialise); one global
     // atomic per class and block
@@ -359,6 +351,7 @@ struct View {
     const uint8_t *cs_kind;
     const uint32_t *class_off;    // [NCLS + 1]
     const uint32_t *win;          // per block: b0[NCLS], b1[NCLS] (k_rd_stab_win)
+    const uint64_t *blo, *bhi;    // per block: lowest low bound, highest high bound of its queries
     uint64_t *cursor;             // global output cursor
     uint64_t cap;                 // capacity of ent
     uint64_t *ent;                // (range id << 32 | TxnId position) per emitted pair
@@ -373,6 +366,15 @@ __device__ __forceinline__ uint32_t lower_bound_s(const uint64_t *a, uint32_t lo
     }
     return lo;
 }
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *a, uint32_t lo, uint32_t hi, uint32_t v)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
 __device__ __forceinline__ uint32_t upper_bound_s(const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t v)
 {
     while (lo < hi) {
@@ -404,10 +406,11 @@ __device__ __forceinline__ uint32_t wave_search(const uint64_t *a, uint32_t lo, 
 
 struct StabTile {
     uint64_t s[TILE], e[TILE];
+    uint32_t s32[TILE], e32[TILE];  // flat tile, rel: bounds - rbase (ends clamped to 2^32 - 1)
     uint2 info[TILE];
     uint8_t kind[TILE];
-    uint64_t hi[WAVES];
-    uint64_t lo;
+    uint64_t rbase;
+    uint32_t rel;                  // flat tile: the block's window spans less than 2^32 - 1 above rbase
     uint32_t b0[NCLS], b1[NCLS];   // the block's window per width class
     uint32_t pre[NCLS + 1];        // flat tile: class c at [pre[c], pre[c + 1])
     uint32_t red[WAVES];
@@ -449,13 +452,16 @@ __device__ __forceinline__ void stab_next(const StabTile &T, uint32_t &c, uint32
         if (T.b0[c] < T.b1[c]) { base = T.b0[c]; return; }
 }
 
-template <bool EMIT>
+// REL: the probes on 32-bit offsets above the block's rbase (as stab_flat_rel)
+template <bool EMIT, bool REL>
 __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
                                               uint64_t *stage)
 {
     const uint32_t tid = threadIdx.x;
     const bool isr = (r.flags >> 8) & 1u;
     const uint32_t wm = r.flags & 0xFFu;
+    const uint64_t rb = REL ? T.rbase : 0;
+    const uint32_t qlo = (uint32_t)(r.lo - rb), qhi = (uint32_t)(r.hi - rb);   // (REL)
     uint32_t count = 0;
     uint32_t c = 0, base = 0;
     while (c < (uint32_t)NCLS && T.b0[c] >= T.b1[c]) ++c;
@@ -467,7 +473,15 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
 #pragma unroll
         for (int u = 0; u < ST_PT; ++u) {
             const uint32_t k = tid + (uint32_t)u * BLOCK;
-            if (k < len) { T.s[k] = g.s[u]; T.e[k] = g.e[u]; T.info[k] = g.info[u]; T.kind[k] = (uint8_t)g.kind[u]; }
+            if (k < len) {
+                if (REL) {
+                    T.s32[k] = (uint32_t)(g.s[u] - rb);
+                    T.e32[k] = g.e[u] - rb < 0xFFFFFFFFull ? (uint32_t)(g.e[u] - rb) : 0xFFFFFFFFu;
+                } else {
+                    T.s[k] = g.s[u]; T.e[k] = g.e[u];
+                }
+                T.info[k] = g.info[u]; T.kind[k] = (uint8_t)g.kind[u];
+            }
         }
         __syncthreads();
         uint32_t c2 = c, base2 = base;
@@ -475,16 +489,27 @@ __device__ __forceinline__ uint32_t stab_pass(const View &v, StabTile &T, bool v
         if (c2 < (uint32_t)NCLS) stab_load(v, g, base2, min((uint32_t)TILE, T.b1[c2] - base2));
         if (valid) {
             const uint64_t W = class_width(c);
-            const uint64_t qwlo = r.lo > W ? r.lo - W : 0;
             // this query's own window inside the tile: starts in [lo - W, hi]
-            for (uint32_t k = lower_bound_s(T.s, 0, len, qwlo); k < len; ++k) {
-                const uint64_t s = T.s[k];
-                if (s > r.hi) break;
-                const uint64_t e = T.e[k];
+            uint32_t k;
+            if (REL) k = lower_bound_u32(T.s32, 0, len, (uint64_t)qlo > W ? qlo - (uint32_t)W : 0u);
+            else k = lower_bound_s(T.s, 0, len, r.lo > W ? r.lo - W : 0);
+            for (; k < len; ++k) {
                 bool hit;
-                if (isr) hit = s < r.hi && e > r.lo;                           // Range.compareIntersecting == 0
-                else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;         // EndInclusive.contains (s, e]
-                else hit = s <= r.lo && r.lo < e;                              // StartInclusive.contains [s, e)
+                if (REL) {
+                    const uint32_t s = T.s32[k];
+                    if (s > qhi) break;
+                    const uint32_t e = T.e32[k];
+                    if (isr) hit = s < qhi && e > qlo;                         // Range.compareIntersecting == 0
+                    else if (v.end_inclusive) hit = s < qlo && qlo <= e;       // EndInclusive.contains (s, e]
+                    else hit = s <= qlo && qlo < e;                            // StartInclusive.contains [s, e)
+                } else {
+                    const uint64_t s = T.s[k];
+                    if (s > r.hi) break;
+                    const uint64_t e = T.e[k];
+                    if (isr) hit = s < r.hi && e > r.lo;
+                    else if (v.end_inclusive) hit = s < r.lo && r.lo <= e;
+                    else hit = s <= r.lo && r.lo < e;
+                }
                 if (!hit) continue;
                 const uint2 info = T.info[k];
                 if (info.y >= r.lim || info.y == r.tpos) continue;            // STARTED_BEFORE; p1
@@ -524,7 +549,52 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab_win(uint32_t nsb, const uint6
 
 // Every class's window of the block in one tile (when they fit TILE together): one load round for the block.
 // Count pass (hv != null): the query's first STAB_RH hits are kept in registers. Emit pass: hits to ent at out.
+// REL: bounds as 32-bit offsets above the block's rbase (half the LDS bytes per probe and per candidate: the pass is
+// bound by LDS reads); a candidate's TxnId position and kind are read only when its bounds hit.
 constexpr int STAB_RH = 16;   // hits a query keeps in registers through the count pass (flat blocks)
+
+template <bool EMIT>
+__device__ __forceinline__ uint32_t stab_flat_rel(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
+                                                  uint64_t (*hv)[STAB_RH])
+{
+    uint32_t count = 0;
+    if (!valid) return 0;
+    const bool isr = (r.flags >> 8) & 1u;
+    const uint32_t wm = r.flags & 0xFFu;
+    const uint32_t qlo = (uint32_t)(r.lo - T.rbase), qhi = (uint32_t)(r.hi - T.rbase);
+    for (uint32_t c = 0; c < (uint32_t)NCLS; ++c) {
+        const uint32_t p0 = T.pre[c], p1 = T.pre[c + 1];
+        if (p0 == p1) continue;
+        const uint64_t W = class_width(c);
+        const uint32_t qwlo = (uint64_t)qlo > W ? qlo - (uint32_t)W : 0u;
+        for (uint32_t k = lower_bound_u32(T.s32, p0, p1, qwlo); k < p1; ++k) {
+            const uint32_t s = T.s32[k];
+            if (s > qhi) break;
+            const uint32_t e = T.e32[k];
+            bool hit;
+            if (isr) hit = s < qhi && e > qlo;                             // Range.compareIntersecting == 0
+            else if (v.end_inclusive) hit = s < qlo && qlo <= e;           // EndInclusive.contains (s, e]
+            else hit = s <= qlo && qlo < e;                                // StartInclusive.contains [s, e)
+            if (hit) {
+                const uint2 info = T.info[k];
+                hit = info.y < r.lim && info.y != r.tpos                   // STARTED_BEFORE; p1
+                      && ((wm >> T.kind[k]) & 1u);                         // testKind
+                if (hit) {
+                    const uint64_t x = ((uint64_t)info.x << 32) | info.y;
+                    if (EMIT) {
+                        v.ent[out + count] = x;
+                    } else if (hv) {
+#pragma unroll
+                        for (int u = 0; u < STAB_RH; ++u)
+                            if ((uint32_t)u == count) (*hv)[u] = x;
+                    }
+                    ++count;
+                }
+            }
+        }
+    }
+    return count;
+}
 
 template <bool EMIT>
 __device__ __forceinline__ uint32_t stab_flat(const View &v, StabTile &T, bool valid, const QRec &r, uint64_t out,
@@ -596,9 +666,17 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
     }
     __syncthreads();
     if (tid == 0) {
-        uint32_t a = 0;
-        for (int c = 0; c < NCLS; ++c) { T.pre[c] = a; a += T.b1[c] - T.b0[c]; }
+        uint32_t a = 0, cmax = 0;
+        for (int c = 0; c < NCLS; ++c) {
+            T.pre[c] = a;
+            a += T.b1[c] - T.b0[c];
+            if (T.b1[c] > T.b0[c]) cmax = (uint32_t)c;
+        }
         T.pre[NCLS] = a;
+        // every windowed start is at least the block's lowest bound less its widest class; the highest probe bound is bhi
+        const uint64_t W = class_width(cmax), lo = v.blo[blockIdx.x], hi = v.bhi[blockIdx.x];
+        T.rbase = lo > W ? lo - W : 0;
+        T.rel = hi >= T.rbase && hi - T.rbase < 0xFFFFFFFFull;
     }
     __syncthreads();
     SB_PH(1);
@@ -611,14 +689,17 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
             uint32_t lo = 0, hi = NCLS;   // the class holding flat position k: last c with pre[c] <= k
             while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (T.pre[md] <= k) lo = md; else hi = md; }
             const uint32_t src = T.b0[lo] + (k - T.pre[lo]);
-            T.s[k] = v.cs_s[src]; T.e[k] = v.cs_e[src]; T.info[k] = v.cs_info[src]; T.kind[k] = v.cs_kind[src];
+            const uint64_t cs = v.cs_s[src], ce = v.cs_e[src];
+            T.s[k] = cs; T.e[k] = ce; T.info[k] = v.cs_info[src]; T.kind[k] = v.cs_kind[src];
+            T.s32[k] = (uint32_t)(cs - T.rbase);
+            T.e32[k] = ce - T.rbase < 0xFFFFFFFFull ? (uint32_t)(ce - T.rbase) : 0xFFFFFFFFu;
         }
         __syncthreads();
         SB_PH(2);
-        count = stab_flat<false>(v, T, valid, r, 0, &hv);
+        count = T.rel ? stab_flat_rel<false>(v, T, valid, r, 0, &hv) : stab_flat<false>(v, T, valid, r, 0, &hv);
     } else {
         SB_PH(2);
-        count = stab_pass<false>(v, T, valid, r, 0, nullptr);
+        count = T.rel ? stab_pass<false, true>(v, T, valid, r, 0, nullptr) : stab_pass<false, false>(v, T, valid, r, 0, nullptr);
     }
     SB_PH(3);
     uint32_t total;
@@ -634,9 +715,11 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
         for (int u = 0; u < STAB_RH; ++u)
             if ((uint32_t)u < count) v.ent[base + mine + u] = hv[u];
     } else if (flat) {
-        stab_flat<true>(v, T, valid, r, base + mine, nullptr);
+        if (T.rel) stab_flat_rel<true>(v, T, valid, r, base + mine, nullptr);
+        else stab_flat<true>(v, T, valid, r, base + mine, nullptr);
     } else {
-        stab_pass<true>(v, T, valid, r, base + mine, nullptr);
+        if (T.rel) stab_pass<true, true>(v, T, valid, r, base + mine, nullptr);
+        else stab_pass<true, false>(v, T, valid, r, base + mine, nullptr);
     }
 #ifdef ACC_PHASE_PROF
     SB_PH(5);
@@ -812,7 +895,7 @@ __global__ __launch_bounds__(BLOCK) void k_rd_build_seg(uint32_t cnt, Out o)
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint32_t grp = lane / S, sub = lane & (S - 1);
     const uint32_t li0 = ((blockIdx.x * WAVES + wave) * G + grp) * K;
-    const uint64_t gmask = S == 64 ? ~0ull : (((1ull << S) - 1) << (grp * S));
+    const uint64_t gmask = S == 64 ? ~0ull : (((1ull << (S & 63)) - 1) << (grp * S));
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int gb = (int)(grp * S);
     const uint32_t g0 = grp * S;
@@ -1265,13 +1348,12 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
 
     // ---- 2. range-command entries, stored-range dictionary, class order
     const Runs rs_plan = make_runs(hm[0]), re_plan = make_runs(hm[1]);
-    uint64_t *e_s = ctx->get<uint64_t>("rd_e_s", NE);
     uint4 *erec = ctx->get<uint4>("rd_erec", 2 * (size_t)NE);
     uint64_t *dkey = ctx->get<uint64_t>("rd_dkey", NE), *ekey = ctx->get<uint64_t>("rd_ekey", NE);
     const bool split = rs_plan.bits + re_plan.bits > 64;
     launch(ctx, "rd_entries", k_rd_entries, dim3(grid_for(R, BLOCK)), dim3(BLOCK), 0, (uint32_t)R, n, (const uint32_t *)eflag,
            (const uint32_t *)eidx, (const uint32_t *)rowner, rs, re, (const uint4 *)tinfo, tl, rs_plan, re_plan, re_plan.bits,
-           split ? 1 : 0, e_s, erec, dkey, ekey);
+           split ? 1 : 0, erec, dkey, ekey);
     Sorted ds;
     if (!split) {
         ds = radix_sort(ctx, "rs_rd_dict", dkey, nullptr, NE, rs_plan.bits + re_plan.bits);
@@ -1292,25 +1374,11 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     uint32_t *cls = ctx->get<uint32_t>("rd_cls", 2 * (NCLS + 1));
     uint32_t *cls_hist = cls, *class_off = cls + (NCLS + 1);
     ACC_HIP(hipMemsetAsync(cls_hist, 0, (NCLS + 1) * sizeof(uint32_t), st));
-    const bool csplit = rs_plan.bits + 6 > 64;
     launch(ctx, "rd_dict_write", k_rd_dict_write, dim3(grid_for(NE, (size_t)BLOCK * RD_TS)), dim3(BLOCK), 0, NE, (const uint32_t *)ds.vals,
-           (const uint32_t *)dflag, (const uint32_t *)dincl, erec, dict_s,
-           dict_e, rs_plan, rs_plan.bits, csplit ? 1 : 0, ckey, cls_hist);
+           (const uint32_t *)dflag, (const uint32_t *)dincl, erec, dict_s, dict_e, ckey, cls_hist);
     launch(ctx, "rd_class_off", k_rd_class_off, dim3(1), dim3(64), 0, (const uint32_t *)cls_hist, class_off);
-    Sorted cs;
-    if (!csplit) {
-        cs = radix_sort(ctx, "rs_rd_cls", ckey, nullptr, NE, rs_plan.bits + 6);
-    } else {
-        // > 58 start bits: stable sort by start, then by class (the class key alone is in ckey's low bits)
-        uint64_t *sk = ctx->get<uint64_t>("rd_skey", NE);
-        launch(ctx, "rd_skey", k_pext_u64, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, (size_t)NE, (const uint64_t *)e_s,
-               rs_plan, sk);
-        Sorted by_s = radix_sort(ctx, "rs_rd_s", sk, nullptr, NE, rs_plan.bits);
-        uint64_t *ck2 = ctx->get<uint64_t>("rd_ckey2", NE);
-        launch(ctx, "rd_permute", k_permute_u64, dim3(grid_for(NE, BLOCK)), dim3(BLOCK), 0, (size_t)NE,
-               (const uint32_t *)by_s.vals, (const uint64_t *)ckey, ck2);
-        cs = radix_sort(ctx, "rs_rd_cls", ck2, by_s.vals, NE, 6);
-    }
+    // (class, start) order: the (start, end)-sorted entries partitioned stably by class, one 8-bit pass
+    const Sorted cs = radix_sort(ctx, "rs_rd_cls", ckey, ds.vals, NE, 6);
     uint64_t *cs_s = ctx->get<uint64_t>("rd_cs_s", NE), *cs_e = ctx->get<uint64_t>("rd_cs_e", NE);
     uint2 *cs_info = ctx->get<uint2>("rd_cs_info", NE);
     uint8_t *cs_kind = ctx->get<uint8_t>("rd_cs_kind", NE);
@@ -1351,6 +1419,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     v.cursor = ctx->get<uint64_t>("rd_cursor", 1);
     uint32_t *win = ctx->get<uint32_t>("rd_win", (size_t)nsb * 2 * NCLS);
     v.win = win;
+    v.blo = blo; v.bhi = bhi;
     uint64_t E = 0;
     if (Q) {
         launch(ctx, "rd_stab_win", k_rd_stab_win, dim3(grid_for((uint64_t)nsb * NCLS, BLOCK)), dim3(BLOCK), 0, nsb,
