@@ -294,17 +294,49 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qrec(uint32_t P, uint32_t R, const
     // range queries after the key queries (rbit < 64): a range query scans its whole span, so mixing the two in one
     // wave would leave the key lanes idle behind it
     // ibits > 0: the query index packed under the key (a keys-only sort, 8 B per element moved instead of 12)
-    const uint64_t k = pext_runs(r.lo, plan) | (q >= P && rbit < 64 ? 1ull << rbit : 0ull);
+    // rbit < 62: range queries also grouped by width (2 bits under the range bit: widths below 2^4, 2^8, 2^12, beyond),
+    // so a block's lanes scan spans of similar length — a wave waits for its widest lane
+    uint64_t k = pext_runs(r.lo, plan);
+    if (q >= P && rbit < 64) {
+        if (rbit < 62) {
+            const uint64_t w = r.hi - r.lo;
+            const uint32_t g = min(3u, (63u - (uint32_t)__builtin_clzll(w | 1)) / 4u);
+            k |= (4ull | g) << rbit;
+        } else {
+            k |= 1ull << rbit;
+        }
+    }
     // qdrop: the low key bits the sort leaves out (the stabbing blocks need neighbouring queries, not an exact order)
     qkey[q] = ibits ? ((k >> qdrop) << ibits) | q : k >> qdrop;
 }
 
+// The sorted runs' bounds bnd[0..4]: key queries [0, bnd[0] = P), range queries of width group g at [bnd[g], bnd[g + 1])
+// (the group in the top 3 sorted key bits: 4 | g). One thread per group boundary, a binary search over the sorted keys.
+__global__ void k_rd_qgroups(const uint64_t *__restrict__ keys, uint32_t P, uint32_t Q, int top_shift, int groups,
+                             uint32_t *__restrict__ bnd)
+{
+    const uint32_t g = threadIdx.x;
+    if (g > 4) return;
+    uint32_t b = g == 0 ? P : Q;
+    if (groups && g >= 1 && g <= 3) {
+        uint32_t lo = P, hi = Q;   // first sorted position whose group field is >= 4 | g
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            if ((keys[mid] >> top_shift) < (4u | g)) lo = mid + 1; else hi = mid;
+        }
+        b = lo;
+    }
+    bnd[g] = b;
+}
+
 // sorted records, and per block of BLOCK sorted queries (the stabbing blocks) the largest high bound
-// Sorted position j of a range query lands at j + (Pp - P) (Pp = P rounded up to a block): no block mixes key and
-// range queries, so no block's window spans both sorted runs. The gap holds PAD records.
+// Each sorted run (the key queries, then each width group of range queries) starts at a block boundary: no block mixes
+// two runs, so no block's window spans the key space between them. Run g of c_g queries at padded position base_g
+// (base_0 = Pp = P rounded up to a block, base_{g+1} = base_g + c_g rounded up); the gaps hold PAD records.
 constexpr uint32_t QPAD = 1u << 31;
 // perm: the sorted query indices, or (perm null) the low bits (imask) of the sorted packed keys pk
-__global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uint32_t Pp, const uint32_t *__restrict__ perm,
+__global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uint32_t Pp, const uint32_t *__restrict__ bnd,
+                                                    const uint32_t *__restrict__ perm,
                                                     const uint64_t *__restrict__ pk, uint64_t imask,
                                                     const QRec *__restrict__ rec, QRec *__restrict__ srec,
                                                     uint64_t *__restrict__ blo, uint64_t *__restrict__ bhi)
@@ -313,12 +345,23 @@ __global__ __launch_bounds__(BLOCK) void k_rd_qsort(uint32_t Qp, uint32_t P, uin
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     uint64_t h = 0, l = ~0ull;
     if (i < Qp) {
-        if (i >= P && i < Pp) {
+        uint32_t j = 0xFFFFFFFFu;   // sorted position of padded position i (none: PAD)
+        if (i < P) {
+            j = i;
+        } else {
+            uint32_t base = Pp;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint32_t c = bnd[g + 1] - bnd[g];
+                if (i >= base && i < base + c) j = bnd[g] + (i - base);
+                base += (c + BLOCK - 1) / BLOCK * BLOCK;
+            }
+        }
+        if (j == 0xFFFFFFFFu) {
             QRec r{};
             r.flags = QPAD;
             srec[i] = r;
         } else {
-            const uint32_t j = i < P ? i : i - (Pp - P);
             const QRec r = rec[perm ? perm[j] : (uint32_t)(pk[j] & imask)];
             srec[i] = r; h = r.hi; l = r.lo;
         }
@@ -1389,7 +1432,7 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     const Runs q_plan = make_runs(hm[2]);
     QRec *rec = ctx->get<QRec>("rd_qrec", Q), *srec = nullptr;
     uint64_t *qkey = ctx->get<uint64_t>("rd_qkey", Q);
-    const int qbits_full = q_plan.bits < 64 ? q_plan.bits + 1 : 64;
+    const int qbits_full = q_plan.bits < 62 ? q_plan.bits + 3 : q_plan.bits < 64 ? q_plan.bits + 1 : 64;
     // Only the high bits of the low bound are sorted: a stabbing block needs BLOCK queries with neighbouring low bounds
     // (its windows span their lowest to highest bound), and each query's scan is independent of its place in the block.
     // 2^(bits_for(Q) - 2) buckets hold ~4 queries each on spread keys, so a block spans ~64 buckets — about the span of
@@ -1406,11 +1449,18 @@ void rangedeps_batch(acc_ctx *ctx, const acc_range_batch_in *in, acc_rangedeps_v
     if (ibits) qpk = radix_sort_keys(ctx, "rs_rd_q", qkey, Q, ibits, qbits);
     else qs = radix_sort(ctx, "rs_rd_q", qkey, nullptr, Q, qbits);
     const uint32_t Pp = q_plan.bits < 64 && P && R ? (uint32_t)((P + BLOCK - 1) / BLOCK * BLOCK) : (uint32_t)P;
-    const uint32_t Qp = Q + (Pp - (uint32_t)P);
+    // the range queries' width groups (q_plan.bits < 62) each from a block boundary: their sizes stay on the device, so
+    // the padded length is bounded (three more gaps of under a block)
+    const int wgroups = q_plan.bits < 62 && R ? 1 : 0;
+    const uint32_t Qp = Q + (Pp - (uint32_t)P) + (wgroups ? 3u * BLOCK : 0u);
+    uint32_t *qbnd = ctx->get<uint32_t>("rd_qbnd", 8);
+    launch(ctx, "rd_qgroups", k_rd_qgroups, dim3(1), dim3(64), 0, ibits ? qpk : (const uint64_t *)qs.keys, (uint32_t)P, Q,
+           ibits + qbits - 3, wgroups, qbnd);
     const uint32_t nsb = (uint32_t)grid_for(Qp, BLOCK);
     uint64_t *bhi = ctx->get<uint64_t>("rd_bhi", nsb), *blo = ctx->get<uint64_t>("rd_blo", nsb);
     srec = ctx->get<QRec>("rd_qrec_sorted", Qp);
-    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Qp, (uint32_t)P, Pp, (const uint32_t *)qs.vals, qpk,
+    launch(ctx, "rd_qsort", k_rd_qsort, dim3(nsb), dim3(BLOCK), 0, Qp, (uint32_t)P, Pp, (const uint32_t *)qbnd,
+           (const uint32_t *)qs.vals, qpk,
            ibits ? (1ull << ibits) - 1 : 0ull, (const QRec *)rec, srec, blo, bhi);
     View v{};
     v.Q = Qp; v.end_inclusive = (int)in->end_inclusive; v.srec = srec;
