@@ -1197,38 +1197,60 @@ __global__ __launch_bounds__(BLOCK) void k_rd_glb_sizes(uint32_t ng, Out o, uint
 }
 
 // scratch -> Java-layout CSR. A workgroup owns BLOCK consecutive txns, whose output runs are one contiguous range of
-// each output array: a thread per output element finds its txn among the block's offsets in LDS and copies from that
-// txn's scratch, so every write (and most reads) is a whole-line access.
+// each output array, copied in chunks of CP_CHUNK elements: each txn whose run starts inside the chunk marks its start
+// in an LDS owner map (LDS max: of the txns starting at one position the last, the only non-empty one, wins), a block
+// max-scan spreads the owners over the chunk (CP_PT consecutive positions per thread, written back to the map), and the
+// block copies the chunk element-interleaved from the txns' scratch: every store instruction writes whole lines and no
+// element searches for its txn.
+constexpr int CP_PT = 8;
+constexpr int CP_CHUNK = CP_PT * BLOCK;
+
 __device__ __forceinline__ void compact_array(uint32_t nt, const uint64_t *off, const uint64_t *src_base,
-                                              const uint32_t *__restrict__ src, uint32_t *__restrict__ dst)
+                                              const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                              uint32_t *own, uint32_t *red)
 {
-    // U outputs per thread per round: their LDS searches and source loads are independent, so they overlap instead of
-    // one dependent chain (8 LDS round trips, then the gather) per output
-    constexpr int U = 4;
+    const uint32_t tid = threadIdx.x;
     const uint64_t j1 = off[nt];
-    for (uint64_t j0 = off[0] + threadIdx.x; j0 < j1; j0 += (uint64_t)U * BLOCK) {
-        uint32_t x[U];
+    uint32_t carry = 0;   // the owner of the chunk's first element (the txn whose run crosses into the chunk)
+    for (uint64_t c0 = off[0]; c0 < j1; c0 += CP_CHUNK) {
+        for (uint32_t p = tid; p < (uint32_t)CP_CHUNK; p += BLOCK) own[p] = 0;
+        __syncthreads();
+        if (tid == 0) own[0] = carry;
+        if (tid < nt && off[tid] < off[tid + 1] && off[tid] >= c0 && off[tid] < c0 + CP_CHUNK)
+            atomicMax(&own[off[tid] - c0], tid);
+        __syncthreads();
+        // inclusive max-scan: CP_PT consecutive positions per thread, then across threads
+        uint32_t v[CP_PT], m = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
-            x[u] = 0;
-            if (j < j1) {
-                uint32_t lo = 0, hi = nt;   // last txn k with off[k] <= j
-                while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (off[md] <= j) lo = md; else hi = md; }
-                x[u] = src[src_base[lo] + (j - off[lo])];
-            }
+        for (int u = 0; u < CP_PT; ++u) { m = max(m, own[tid * CP_PT + u]); v[u] = m; }
+        uint32_t tot;
+        const uint32_t pre = block_exclusive(m, OpMax<uint32_t>(), red, tot);
+#pragma unroll
+        for (int u = 0; u < CP_PT; ++u) own[tid * CP_PT + u] = max(pre, v[u]);
+        __syncthreads();
+        // copies interleaved across the block (element u * BLOCK + tid): each store instruction writes whole lines
+        uint32_t x[CP_PT];
+#pragma unroll
+        for (int u = 0; u < CP_PT; ++u) {
+            const uint32_t p = (uint32_t)u * BLOCK + tid;
+            const uint64_t j = c0 + p;
+            const uint32_t k = own[p];
+            x[u] = j < j1 ? src[src_base[k] + (j - off[k])] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+        for (int u = 0; u < CP_PT; ++u) {
+            const uint64_t j = c0 + (uint64_t)u * BLOCK + tid;
             if (j < j1) dst[j] = x[u];
         }
+        carry = tot;
+        __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
 {
     __shared__ uint64_t ao[BLOCK + 1], ro[BLOCK + 1], uo[BLOCK + 1], sa[BLOCK], sr[BLOCK];
+    __shared__ uint32_t own[CP_CHUNK], red[WAVES];
     const uint32_t t0 = blockIdx.x * BLOCK, nt = min((uint32_t)BLOCK, n - t0), tid = threadIdx.x;
     if (tid < nt) {
         const uint32_t t = t0 + tid;
@@ -1238,9 +1260,9 @@ __global__ __launch_bounds__(BLOCK) void k_rd_compact(uint32_t n, Out o)
     }
     if (tid == 0) { ao[nt] = o.arena_off[t0 + nt]; ro[nt] = o.rd_off[t0 + nt]; uo[nt] = o.u_off[t0 + nt]; }   // the block's ends
     __syncthreads();
-    compact_array(nt, ao, sa, o.s_arena, reinterpret_cast<uint32_t *>(o.arena));
-    compact_array(nt, ro, sr, o.s_rid, o.range_id);
-    compact_array(nt, uo, sr, o.s_dep, o.dep_txn);
+    compact_array(nt, ao, sa, o.s_arena, reinterpret_cast<uint32_t *>(o.arena), own, red);
+    compact_array(nt, ro, sr, o.s_rid, o.range_id, own, red);
+    compact_array(nt, uo, sr, o.s_dep, o.dep_txn, own, red);
 }
 
 }  // namespace rd
