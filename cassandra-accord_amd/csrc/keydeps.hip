@@ -4467,7 +4467,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_sizes(uint32_t n, MxKv kv, const u
 }
 
 // the combined layout. A workgroup owns BLOCK consecutive txns, whose output runs are one contiguous range of each
-// output array: a thread per output element finds its txn among the block's offsets in LDS and reads from that txn's
+// output array: each output element takes its txn from a chunk owner map (chunk_owners) and reads from that txn's
 // source (key txns: keydeps_core's result, with key codes; range txns: their key records, per-entry union indices and
 // union TxnIds), so every write is a whole-line access.
 __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const uint64_t *__restrict__ etoff,
@@ -4479,6 +4479,7 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
     __shared__ uint64_t ao[BLOCK + 1], ko[BLOCK + 1], uo[BLOCK + 1];   // output offsets
     __shared__ uint64_t sa[BLOCK], sk[BLOCK], su[BLOCK];                // source bases: arena / keys / TxnIds
     __shared__ uint32_t kdn[BLOCK], kofs[BLOCK];                        // range txn: key records; key txn: key_off
+    __shared__ uint32_t own[8 * BLOCK], red[WAVES];                     // chunk owner map (chunk_owners)
     const uint32_t t0 = blockIdx.x * BLOCK, nt = min((uint32_t)BLOCK, n - t0), tid = threadIdx.x;
     if (tid < nt) {
         const uint32_t t = t0 + tid;
@@ -4496,17 +4497,20 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
     }
     if (tid == 0) { ao[nt] = o.arena_off[t0 + nt]; ko[nt] = o.kd_off[t0 + nt]; uo[nt] = o.u_off[t0 + nt]; }
     __syncthreads();
-    // U outputs per thread per round: independent LDS searches and source loads overlap (one dependent chain of ~8 LDS
-    // round trips + a gather per output otherwise)
-    constexpr int U = 4;
-    for (uint64_t j0 = ao[0] + tid; j0 < ao[nt]; j0 += (uint64_t)U * BLOCK) {
+    // per array, chunks of U * BLOCK outputs: the owner map of the chunk (chunk_owners), then U outputs per thread,
+    // interleaved across the block (whole-line stores), each reading its txn from the map
+    constexpr int U = 8;
+    uint32_t carry = 0;
+    for (uint64_t c0 = ao[0]; c0 < ao[nt]; c0 += (uint64_t)U * BLOCK) {
+        chunk_owners<U>(nt, ao, c0, own, red, carry);
         int32_t v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint32_t p = (uint32_t)u * BLOCK + tid;
+            const uint64_t j = c0 + p;
             v[u] = 0;
             if (j < ao[nt]) {
-                const uint32_t a = last_le(ao, nt, j);
+                const uint32_t a = own[p];
                 const uint64_t i = j - ao[a];
                 const uint32_t kd = kdn[a];
                 if (kd == 0xFFFFFFFFu) v[u] = kv.arena[sa[a] + i];
@@ -4516,19 +4520,22 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint64_t j = c0 + (uint64_t)u * BLOCK + tid;
             if (j < ao[nt]) o.arena[j] = v[u];
         }
     }
-    for (uint64_t j0 = ko[0] + tid; j0 < ko[nt]; j0 += (uint64_t)U * BLOCK) {
+    carry = 0;
+    for (uint64_t c0 = ko[0]; c0 < ko[nt]; c0 += (uint64_t)U * BLOCK) {
+        chunk_owners<U>(nt, ko, c0, own, red, carry);
         uint32_t ki[U];
         uint64_t kc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint32_t p = (uint32_t)u * BLOCK + tid;
+            const uint64_t j = c0 + p;
             ki[u] = 0; kc[u] = 0;
             if (j < ko[nt]) {
-                const uint32_t a = last_le(ko, nt, j);
+                const uint32_t a = own[p];
                 const uint64_t i = j - ko[a];
                 if (kdn[a] == 0xFFFFFFFFu) {
                     ki[u] = kv.key_idx[sk[a] + i];
@@ -4541,25 +4548,28 @@ __global__ __launch_bounds__(BLOCK) void k_mx_write(uint32_t n, MxKv kv, const u
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint64_t j = c0 + (uint64_t)u * BLOCK + tid;
             if (j < ko[nt]) { o.key_idx[j] = ki[u]; o.kd_key[j] = kc[u]; }
         }
     }
-    for (uint64_t j0 = uo[0] + tid; j0 < uo[nt]; j0 += (uint64_t)U * BLOCK) {
+    carry = 0;
+    for (uint64_t c0 = uo[0]; c0 < uo[nt]; c0 += (uint64_t)U * BLOCK) {
+        chunk_owners<U>(nt, uo, c0, own, red, carry);
         uint32_t d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint32_t p = (uint32_t)u * BLOCK + tid;
+            const uint64_t j = c0 + p;
             d[u] = 0;
             if (j < uo[nt]) {
-                const uint32_t a = last_le(uo, nt, j);
+                const uint32_t a = own[p];
                 const uint64_t i = j - uo[a];
                 d[u] = kdn[a] == 0xFFFFFFFFu ? kv.dep_txn[su[a] + i] : dep_scr[su[a] + i];
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * BLOCK;
+            const uint64_t j = c0 + (uint64_t)u * BLOCK + tid;
             if (j < uo[nt]) o.dep_txn[j] = d[u];
         }
     }

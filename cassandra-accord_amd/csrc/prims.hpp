@@ -142,6 +142,34 @@ __device__ __forceinline__ T block_exclusive(T v, Op op, T *lds, T &total)
     return op(wave_prefix, excl);
 }
 
+// Owner map of one chunk of a workgroup's output range: own[p] = the index k < nt of the run [off[k], off[k + 1]) holding
+// position c0 + p, for p < PT * BLOCK (off ascending, in LDS or registers' reach; carry = the owner of position c0,
+// updated to the owner of the chunk's last position). Each run starting in the chunk marks its start (LDS max: of the
+// runs starting at one position the last, the only non-empty one, wins), then a block max-scan spreads the marks:
+// copies that follow read their run from own[] instead of searching the offsets per element. Whole block, uniform.
+template <int PT>
+__device__ __forceinline__ void chunk_owners(uint32_t nt, const uint64_t *off, uint64_t c0, uint32_t *own, uint32_t *red,
+                                             uint32_t &carry)
+{
+    constexpr uint32_t CH = (uint32_t)PT * BLOCK;
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();   // the previous chunk's reads of own[] are done
+    for (uint32_t p = tid; p < CH; p += BLOCK) own[p] = 0;
+    __syncthreads();
+    if (tid == 0) own[0] = carry;
+    if (tid < nt && off[tid] < off[tid + 1] && off[tid] >= c0 && off[tid] < c0 + CH) atomicMax(&own[off[tid] - c0], tid);
+    __syncthreads();
+    uint32_t v[PT], m = 0;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) { m = max(m, own[tid * PT + u]); v[u] = m; }
+    uint32_t tot;
+    const uint32_t pre = block_exclusive(m, OpMax<uint32_t>(), red, tot);
+#pragma unroll
+    for (int u = 0; u < PT; ++u) own[tid * PT + u] = max(pre, v[u]);
+    __syncthreads();
+    carry = tot;
+}
+
 // ---------------------------------------------------------------- sorting networks
 
 // ascending bitonic sort of one value per lane across the 64 lanes of a wave

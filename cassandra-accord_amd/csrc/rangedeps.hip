@@ -1211,23 +1211,9 @@ __device__ __forceinline__ void compact_array(uint32_t nt, const uint64_t *off, 
 {
     const uint32_t tid = threadIdx.x;
     const uint64_t j1 = off[nt];
-    uint32_t carry = 0;   // the owner of the chunk's first element (the txn whose run crosses into the chunk)
+    uint32_t carry = 0;
     for (uint64_t c0 = off[0]; c0 < j1; c0 += CP_CHUNK) {
-        for (uint32_t p = tid; p < (uint32_t)CP_CHUNK; p += BLOCK) own[p] = 0;
-        __syncthreads();
-        if (tid == 0) own[0] = carry;
-        if (tid < nt && off[tid] < off[tid + 1] && off[tid] >= c0 && off[tid] < c0 + CP_CHUNK)
-            atomicMax(&own[off[tid] - c0], tid);
-        __syncthreads();
-        // inclusive max-scan: CP_PT consecutive positions per thread, then across threads
-        uint32_t v[CP_PT], m = 0;
-#pragma unroll
-        for (int u = 0; u < CP_PT; ++u) { m = max(m, own[tid * CP_PT + u]); v[u] = m; }
-        uint32_t tot;
-        const uint32_t pre = block_exclusive(m, OpMax<uint32_t>(), red, tot);
-#pragma unroll
-        for (int u = 0; u < CP_PT; ++u) own[tid * CP_PT + u] = max(pre, v[u]);
-        __syncthreads();
+        chunk_owners<CP_PT>(nt, off, c0, own, red, carry);
         // copies interleaved across the block (element u * BLOCK + tid): each store instruction writes whole lines
         uint32_t x[CP_PT];
 #pragma unroll
@@ -1242,8 +1228,6 @@ __device__ __forceinline__ void compact_array(uint32_t nt, const uint64_t *off, 
             const uint64_t j = c0 + (uint64_t)u * BLOCK + tid;
             if (j < j1) dst[j] = x[u];
         }
-        carry = tot;
-        __syncthreads();
     }
 }
 
