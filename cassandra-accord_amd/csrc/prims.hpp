@@ -155,8 +155,8 @@ __device__ __forceinline__ void chunk_owners(uint32_t nt, const uint64_t *off, u
     const uint32_t tid = threadIdx.x;
     __syncthreads();   // the previous chunk's reads of own[] are done
     for (uint32_t p = tid; p < CH; p += BLOCK) own[p] = 0;
+    if (tid == 0) own[0] = carry;   // (thread 0 zeroed own[0]; before the barrier: no race with a run starting at c0)
     __syncthreads();
-    if (tid == 0) own[0] = carry;
     if (tid < nt && off[tid] < off[tid + 1] && off[tid] >= c0 && off[tid] < c0 + CH) atomicMax(&own[off[tid] - c0], tid);
     __syncthreads();
     uint32_t v[PT], m = 0;
