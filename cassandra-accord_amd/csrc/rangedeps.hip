@@ -708,18 +708,20 @@ __global__ __launch_bounds__(BLOCK) void k_rd_stab(View v)
         T.b1[tid] = v.win[(size_t)blockIdx.x * 2 * NCLS + NCLS + tid];
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t a = 0, cmax = 0;
-        for (int c = 0; c < NCLS; ++c) {
-            T.pre[c] = a;
-            a += T.b1[c] - T.b0[c];
-            if (T.b1[c] > T.b0[c]) cmax = (uint32_t)c;
+    if (tid < 64) {   // wave 0: the classes' tile offsets by one wave scan (a serial loop over 33 classes cost ~3K cycles)
+        const uint32_t len = tid < (uint32_t)NCLS ? T.b1[tid] - T.b0[tid] : 0u;
+        const uint32_t incl = wave_inclusive(len, OpAdd<uint32_t>());
+        if (tid < (uint32_t)NCLS) T.pre[tid] = incl - len;
+        if (tid == (uint32_t)NCLS - 1) T.pre[NCLS] = incl;
+        const uint64_t ne = __ballot(len != 0);
+        if (tid == 0) {
+            const uint32_t cmax = ne ? 63u - (uint32_t)__builtin_clzll(ne) : 0u;
+            // every windowed start is at least the block's lowest bound less its widest class; the highest probe
+            // bound is bhi
+            const uint64_t W = class_width(cmax), lo = v.blo[blockIdx.x], hi = v.bhi[blockIdx.x];
+            T.rbase = lo > W ? lo - W : 0;
+            T.rel = hi >= T.rbase && hi - T.rbase < 0xFFFFFFFFull;
         }
-        T.pre[NCLS] = a;
-        // every windowed start is at least the block's lowest bound less its widest class; the highest probe bound is bhi
-        const uint64_t W = class_width(cmax), lo = v.blo[blockIdx.x], hi = v.bhi[blockIdx.x];
-        T.rbase = lo > W ? lo - W : 0;
-        T.rel = hi >= T.rbase && hi - T.rbase < 0xFFFFFFFFull;
     }
     __syncthreads();
     SB_PH(1);
